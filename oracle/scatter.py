@@ -1,0 +1,44 @@
+"""torch_scatter.scatter semantics on CPU (TEST INFRASTRUCTURE; see oracle/__init__.py).
+
+Follows the call sites models/layers/egnn_layer.py:77,79, models/layers/tfn_layer.py:87,
+models/layers/gvp_layer.py:415 and PyG's default aggregate / global pools:
+  out[index[e]] (+)= src[e]; rows = dim_size or index.max()+1; empty rows are 0;
+  mean = sum / count.clamp(min=1); max: empty rows 0.
+"""
+import torch
+
+
+def _rows(index, dim_size):
+    if dim_size is not None:
+        return int(dim_size)
+    return int(index.max()) + 1 if index.numel() else 0
+
+
+def scatter(src, index, dim=0, dim_size=None, reduce="sum"):
+    dim = dim % src.dim()
+    n = _rows(index, dim_size)
+    x = src.movedim(dim, 0)
+    shape = (n,) + tuple(x.shape[1:])
+    if reduce in ("sum", "add", "mean"):
+        out = torch.zeros(shape, dtype=src.dtype)
+        out.index_add_(0, index, x)
+        if reduce == "mean":
+            cnt = torch.zeros(n, dtype=src.dtype)
+            cnt.index_add_(0, index, torch.ones(index.shape[0], dtype=src.dtype))
+            out = out / cnt.clamp(min=1).view((n,) + (1,) * (out.dim() - 1))
+    elif reduce == "max":
+        out = torch.full(shape, float("-inf"), dtype=src.dtype)
+        idx = index.view((-1,) + (1,) * (x.dim() - 1)).expand_as(x)
+        out = out.scatter_reduce(0, idx, x, reduce="amax", include_self=True)
+        out = torch.where(torch.isinf(out) & (out < 0), torch.zeros_like(out), out)
+    else:
+        raise ValueError(reduce)
+    return out.movedim(0, dim)
+
+
+def global_add_pool(x, batch, size=None):
+    return scatter(x, batch, 0, size if size is not None else int(batch.max()) + 1, "sum")
+
+
+def global_mean_pool(x, batch, size=None):
+    return scatter(x, batch, 0, size if size is not None else int(batch.max()) + 1, "mean")
