@@ -1,0 +1,813 @@
+// K4: EGNN fused edge message + segmented aggregation (forward and backward), gfx950.
+//
+// Reference: models/layers/egnn_layer.py:62-80 (message / aggregate) with the MLPs of :28-39.
+// Design:
+//  * edges are receiver-sorted (CSR); every wave owns a node-aligned, edge-balanced range and
+//    walks it in 16-edge chunks, so each receiver's sum is formed inside one wave in a fixed
+//    order (deterministic, no atomics);
+//  * lane l holds edge e = l & 15 and feature group g = l >> 4: features 16p + 4g + c
+//    (p < d/16, c < 4) — exactly the register order that v_mfma_f32_16x16x4_f32 uses for its B
+//    operand AND produces as its C/D accumulator when computing out^T = W . x^T, so the chain
+//    Linear -> LN -> act -> Linear -> LN -> act -> Linear -> LN -> act -> dot stays in
+//    registers with no LDS transpose (exact fp32: the f32 MFMA is a k-ordered fmaf chain);
+//  * W2 / W3 (d x d, row-major) live in LDS with row stride d+4 floats; W.x reads W rows with
+//    ds_read_b128, W^T.g reads W columns with conflict-free ds_read_b32;
+//  * the first Linear(2d+1 -> d) is split into per-node projections AB = [h W1a^T | h W1b^T]
+//    (a node-level GEMM done once per node by the caller) plus a rank-1 distance term.
+#include "gmp_common.h"
+
+namespace gmp {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 512;  // 8 waves per workgroup, 1 workgroup per CU (LDS-bound)
+constexpr int kWavesPerBlock = kThreads / 64;
+
+template <int D>
+struct Cfg {
+  static constexpr int T = D / 16;   // f32x4 groups per lane = 16-feature MFMA tiles
+  static constexpr int N = D / 4;    // feature slots per lane
+  static constexpr int LDW = D + 4;  // LDS row stride of W (floats)
+};
+
+// feature held by lane group g in slot s = 4p + c
+__device__ __forceinline__ constexpr int featq(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
+
+enum VecId { V_W1D = 0, V_B1, V_LN1W, V_LN1B, V_B2, V_LN2W, V_LN2B, V_B3, V_LN3W, V_LN3B, V_W4, NV };
+
+template <int D>
+constexpr int carry_stride() { return D / 4 + 4; }
+
+// LDS: W2 | W3 | NV vectors | per-wave carries [wave][g][d/4 + 4]
+template <int D>
+constexpr size_t smem_params_floats() { return (size_t)2 * D * Cfg<D>::LDW + NV * D; }
+template <int D>
+constexpr size_t smem_total() {
+  return (smem_params_floats<D>() + (size_t)kWavesPerBlock * 4 * carry_stride<D>()) * sizeof(float);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float z) {
+  if (ACT == GMP_ACT_RELU) return z > 0.f ? z : 0.f;
+  const float sg = 1.f / (1.f + __expf(-z));
+  return z * sg;
+}
+template <int ACT>
+__device__ __forceinline__ float act_df(float z) {
+  if (ACT == GMP_ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  const float sg = 1.f / (1.f + __expf(-z));
+  return sg * (1.f + z * (1.f - sg));
+}
+
+// ---------------------------------------------------------------------------------- LDS setup
+template <int D>
+__device__ void load_params_to_lds(float* smem, const gmp_egnn_params& P) {
+  constexpr int LDW = Cfg<D>::LDW;
+  float* sW2 = smem;
+  float* sW3 = smem + D * LDW;
+  float* sV = smem + 2 * D * LDW;
+  for (int i = threadIdx.x; i < D * D / 4; i += blockDim.x) {
+    const int o = (4 * i) / D, k = (4 * i) % D;
+    const float4 a = reinterpret_cast<const float4*>(P.W2)[i];
+    const float4 b = reinterpret_cast<const float4*>(P.W3)[i];
+    *reinterpret_cast<float4*>(sW2 + o * LDW + k) = a;
+    *reinterpret_cast<float4*>(sW3 + o * LDW + k) = b;
+  }
+  const float* vsrc[NV] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
+                           P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
+  for (int i = threadIdx.x; i < NV * D; i += blockDim.x) sV[i] = vsrc[i / D][i % D];
+}
+
+// this lane's 4 consecutive slots (4p..4p+3) of LDS vector v
+template <int D>
+__device__ __forceinline__ f32x4 vec4(const float* sV, int v, int p, int g) {
+  return *reinterpret_cast<const f32x4*>(sV + v * D + 16 * p + 4 * g);
+}
+
+template <int D>
+__device__ __forceinline__ void load_vec(f32x4 (&x)[D / 16], const float* sV, int v, int g) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) x[p] = vec4<D>(sV, v, p, g);
+}
+
+// row of a (rows, d) global tensor: this lane's slots
+template <int D>
+__device__ __forceinline__ void load_row(f32x4 (&x)[D / 16], const float* __restrict__ row, int g) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) x[p] = *reinterpret_cast<const f32x4*>(row + 16 * p + 4 * g);
+}
+template <int D>
+__device__ __forceinline__ void store_row(float* __restrict__ row, const f32x4 (&x)[D / 16], int g) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) *reinterpret_cast<f32x4*>(row + 16 * p + 4 * g) = x[p];
+}
+
+// ---------------------------------------------------------------------------------- MFMA GEMMs
+// GMP_GEMM_FENCE bounds how far the scheduler may hoist LDS operand reads (register pressure).
+#ifndef GMP_GEMM_FENCE
+#define GMP_GEMM_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+// y[slot(o)] += sum_k W[o][k] x[slot(k)]   (W row-major [o][k] in LDS; lane i = edge = l & 15)
+template <int D>
+__device__ __forceinline__ void gemm_wx(const float* __restrict__ sW, const f32x4 (&x)[D / 16],
+                                        f32x4 (&y)[D / 16], int i, int g) {
+  constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
+#pragma unroll
+  for (int p = 0; p < T; ++p) {  // contraction block: features 16p + 4g' + c
+    f32x4 a[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) a[t] = *reinterpret_cast<const f32x4*>(sW + (16 * t + i) * LDW + 16 * p + 4 * g);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][c], x[p][c], y[t], 0, 0, 0);
+    GMP_GEMM_FENCE();
+  }
+}
+
+// y[slot(k)] += sum_o W[o][k] gin[slot(o)]   (transposed product for the backward)
+template <int D>
+__device__ __forceinline__ void gemm_wtx(const float* __restrict__ sW, const f32x4 (&gin)[D / 16],
+                                         f32x4 (&y)[D / 16], int i, int g) {
+  constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float* wrow = sW + (16 * p + 4 * g + c) * LDW + i;
+      float a[T];
+#pragma unroll
+      for (int t = 0; t < T; ++t) a[t] = wrow[16 * t];
+#pragma unroll
+      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], gin[p][c], y[t], 0, 0, 0);
+      GMP_GEMM_FENCE();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- LayerNorm
+__device__ __forceinline__ float sum_groups(float v) {  // sum over the 4 lane groups of an edge
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+// in place: x <- (x - mean) * rstd  (x_hat); returns rstd.  Two-pass statistics.
+template <int D>
+__device__ __forceinline__ float ln_normalize(f32x4 (&x)[D / 16], float eps) {
+  constexpr int T = D / 16;
+  float s = 0.f;
+#pragma unroll
+  for (int p = 0; p < T; ++p) s += (x[p][0] + x[p][1]) + (x[p][2] + x[p][3]);
+  const float mean = sum_groups(s) * (1.f / D);
+  float v = 0.f;
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+    x[p] -= mean;
+    v += x[p][0] * x[p][0] + x[p][1] * x[p][1] + x[p][2] * x[p][2] + x[p][3] * x[p][3];
+  }
+  const float rstd = 1.f / sqrtf(sum_groups(v) * (1.f / D) + eps);
+#pragma unroll
+  for (int p = 0; p < T; ++p) x[p] *= rstd;
+  return rstd;
+}
+
+// dpre = rstd * (gr - mean(gr) - xhat * mean(gr * xhat)), gr = dL/dxhat ; in place on gr
+template <int D>
+__device__ __forceinline__ void ln_backward(f32x4 (&gr)[D / 16], const f32x4 (&xhat)[D / 16],
+                                            float rstd) {
+  constexpr int T = D / 16;
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int p = 0; p < T; ++p)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      a += gr[p][c];
+      b += gr[p][c] * xhat[p][c];
+    }
+  a = sum_groups(a) * (1.f / D);
+  b = sum_groups(b) * (1.f / D);
+#pragma unroll
+  for (int p = 0; p < T; ++p) gr[p] = rstd * (gr[p] - a - xhat[p] * b);
+}
+
+// x <- act(x * w + b) with LDS vectors w, b
+template <int D, int ACT>
+__device__ __forceinline__ void affine_act(f32x4 (&x)[D / 16], const float* sV, int vw, int vb, int g) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) {
+    const f32x4 w = vec4<D>(sV, vw, p, g), b = vec4<D>(sV, vb, p, g);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[p][c] = act_f<ACT>(x[p][c] * w[c] + b[c]);
+  }
+}
+
+// ---------------------------------------------------------------------------------- segments
+// inclusive segmented scan over the 16 edge lanes of each group; `head` = first lane of this
+// lane's segment inside the chunk.
+template <int T>
+__device__ __forceinline__ void seg_scan(f32x4 (&x)[T], int i, int head) {
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const bool take = (i - off) >= head;
+#pragma unroll
+    for (int p = 0; p < T; ++p)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float u = __shfl_up(x[p][c], off, 16);
+        if (take) x[p][c] += u;
+      }
+  }
+}
+
+// Reduce-scatter over the 16 edge lanes (levels xor M = 8, 4, 2, 1).
+template <int N, int M, int N0>
+struct RS {
+  __device__ __forceinline__ static void run(float (&x)[N0], int i) {
+    if constexpr (M == 0) {
+      return;
+    } else if constexpr (N >= 2) {
+      constexpr int H = N / 2;
+      const bool up = (i & M) != 0;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const float lo = x[k], hi = x[k + H];
+        x[k] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, M, 16);
+      }
+      RS<H, M / 2, N0>::run(x, i);
+    } else {
+      x[0] += __shfl_xor(x[0], M, 16);
+      RS<1, M / 2, N0>::run(x, i);
+    }
+  }
+};
+
+template <int D>
+struct VecAcc {
+  static constexpr int N = D / 4;
+  static constexpr int K = (N >= 16) ? N / 16 : 1;  // accumulated values per lane per vector
+};
+// slot of accumulator k of lane i, and whether lane i owns it (counted once)
+template <int D>
+__device__ __forceinline__ int acc_slot(int i, int k) {
+  constexpr int N = D / 4;
+  if constexpr (N >= 16) return (N / 16) * i + k;
+  else return i / (16 / N);
+}
+template <int D>
+__device__ __forceinline__ bool acc_owner(int i) {
+  constexpr int N = D / 4;
+  if constexpr (N >= 16) return true;
+  else return (i % (16 / N)) == 0;
+}
+
+// acc += reduce-scatter over the 16 edge lanes of f(slot); the first level is formed on the fly
+// so only N/2 temporaries are live.
+template <int D, class F>
+__device__ __forceinline__ void accumulate_vec(F f, float (&acc)[VecAcc<D>::K], int i) {
+  constexpr int N = D / 4, H = N / 2;
+  float t[H];
+  const bool up = (i & 8) != 0;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const float lo = f(k), hi = f(k + H);
+    t[k] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 8, 16);
+  }
+  RS<H, 4, H>::run(t, i);
+#pragma unroll
+  for (int k = 0; k < VecAcc<D>::K; ++k) acc[k] += t[k];
+}
+
+// Node-aligned, edge-balanced wave partition: wave w owns nodes [nb(w), nb(w+1)).
+__device__ __forceinline__ int64_t node_begin(const int64_t* __restrict__ rowptr, int64_t n_nodes,
+                                              int64_t n_edges, int64_t w, int64_t n_waves) {
+  if (w >= n_waves) return n_nodes;
+  if (w <= 0) return 0;
+  const int64_t target = (n_edges * w) / n_waves;
+  int64_t lo = 0, hi = n_nodes;  // first n in [0, n_nodes] with rowptr[n] >= target
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// carry of the open segment: lane 15 of each group stores, lane 0 of the next chunk adds.
+template <int D>
+__device__ __forceinline__ void carry_store(float* cbuf, const f32x4 (&x)[D / 16], const float (&p3)[3]) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) *reinterpret_cast<f32x4*>(cbuf + 4 * p) = x[p];
+  cbuf[D / 4 + 0] = p3[0];
+  cbuf[D / 4 + 1] = p3[1];
+  cbuf[D / 4 + 2] = p3[2];
+}
+template <int D>
+__device__ __forceinline__ void carry_apply(const float* cbuf, f32x4 (&x)[D / 16], float (&p3)[3],
+                                            bool valid, bool take) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) {
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+    if (take) c = *reinterpret_cast<const f32x4*>(cbuf + 4 * p);
+    x[p] = valid ? x[p] + c : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) p3[c] = valid ? p3[c] + (take ? cbuf[D / 4 + c] : 0.f) : 0.f;
+}
+
+// first pre-activation AB[i,:d] + AB[j,d:] + w1d*dist + b1
+template <int D>
+__device__ __forceinline__ void load_pre1(f32x4 (&x)[D / 16], const float* arow, const float* brow,
+                                          const float* sV, float dist, int g) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(arow + 16 * p + 4 * g);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 16 * p + 4 * g);
+    x[p] = (a + b) + (vec4<D>(sV, V_W1D, p, g) * dist + vec4<D>(sV, V_B1, p, g));
+  }
+}
+
+struct EdgeCtx {
+  int e, i, j, seg0, seg1;  // 32-bit (n_nodes, n_edges < 2^31 checked at the C ABI)
+  bool valid;
+  float rx, ry, rz, dist;
+};
+
+__device__ __forceinline__ EdgeCtx edge_ctx(int base, int lane_e, int e_hi, int n_nodes,
+                                            const int64_t* __restrict__ recv,
+                                            const int64_t* __restrict__ send,
+                                            const int64_t* __restrict__ rowptr,
+                                            const float* __restrict__ pos) {
+  EdgeCtx c;
+  c.e = base + lane_e;
+  c.valid = c.e < e_hi;
+  c.i = c.valid ? (int)recv[c.e] : 0;
+  c.j = c.valid ? (int)send[c.e] : 0;
+  if ((unsigned)c.j >= (unsigned)n_nodes) c.j = c.i;  // out-of-range sender (flagged by the CSR
+                                                       // build): never read outside the tables
+  c.seg0 = c.valid ? (int)rowptr[c.i] : c.e;
+  c.seg1 = c.valid ? (int)rowptr[c.i + 1] : c.e + 1;
+  c.rx = pos[3 * c.i + 0] - pos[3 * c.j + 0];  // pos_i - pos_j  (egnn_layer.py:64)
+  c.ry = pos[3 * c.i + 1] - pos[3 * c.j + 1];
+  c.rz = pos[3 * c.i + 2] - pos[3 * c.j + 2];
+  c.dist = sqrtf(c.rx * c.rx + c.ry * c.ry + c.rz * c.rz);
+  return c;
+}
+
+// row r of a (rows, ld) fp32 tensor (64-bit offset)
+__device__ __forceinline__ const float* rowp(const float* base, int r, int ld) {
+  return base + (size_t)(unsigned)r * (size_t)ld;
+}
+__device__ __forceinline__ float* rowp(float* base, int r, int ld) {
+  return base + (size_t)(unsigned)r * (size_t)ld;
+}
+
+// wave-uniform range of this wave (scalar registers)
+struct WaveRange {
+  int e_lo, e_hi;
+};
+__device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowptr, int64_t n_nodes,
+                                                int64_t n_edges, int64_t n_waves, int wid) {
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t nb = node_begin(rowptr, n_nodes, n_edges, wave, n_waves);
+  const int64_t ne = node_begin(rowptr, n_nodes, n_edges, wave + 1, n_waves);
+  WaveRange r;
+  r.e_lo = (nb < ne) ? (int)rowptr[nb] : 0;
+  r.e_hi = (nb < ne) ? (int)rowptr[ne] : 0;
+  r.e_lo = __builtin_amdgcn_readfirstlane(r.e_lo);
+  r.e_hi = __builtin_amdgcn_readfirstlane(r.e_hi);
+  return r;
+}
+
+// ================================================================================== forward
+template <int D, int ACT, bool MSG_MEAN>
+__global__ __launch_bounds__(kThreads, 2) void egnn_fwd_kernel(
+    int64_t n_nodes, int64_t n_edges, const float* __restrict__ AB, const float* __restrict__ pos,
+    const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
+    const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
+    float* __restrict__ m_aggr, float* __restrict__ pos_aggr) {
+  constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const float* sW2 = smem;
+  const float* sW3 = smem + D * LDW;
+  const float* sV = smem + 2 * D * LDW;
+  load_params_to_lds<D>(smem, P);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* cbuf = smem + smem_params_floats<D>() + (wid * 4 + g) * carry_stride<D>();
+  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid);
+  const float b4 = P.b4[0];
+  int carry_node = -1;
+
+  for (int base = wr.e_lo; base < wr.e_hi; base += 16) {
+    asm volatile("" ::: "memory");  // keep LDS parameter reads inside the loop
+    const EdgeCtx c = edge_ctx(base, li, wr.e_hi, (int)n_nodes, recv, send, rowptr, pos);
+
+    f32x4 x[T];  // y1 = act(LN1(pre1))
+    load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c.dist, g);
+    ln_normalize<D>(x, eps);
+    affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
+
+    f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
+    load_vec<D>(m, sV, V_B2, g);
+    gemm_wx<D>(sW2, x, m, li, g);
+    ln_normalize<D>(m, eps);
+    affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);
+
+    // y3 = act(LN3(W3 m + b3)); s = w4 . y3 + b4   (x reused)
+    load_vec<D>(x, sV, V_B3, g);
+    gemm_wx<D>(sW3, m, x, li, g);
+    ln_normalize<D>(x, eps);
+    affine_act<D, ACT>(x, sV, V_LN3W, V_LN3B, g);
+    float sp = 0.f;
+#pragma unroll
+    for (int p = 0; p < T; ++p) {
+      const f32x4 w = vec4<D>(sV, V_W4, p, g);
+      sp += w[0] * x[p][0] + w[1] * x[p][1] + w[2] * x[p][2] + w[3] * x[p][3];
+    }
+    const float s_e = sum_groups(sp) + b4;
+
+    // segmented sums over receivers: m -> m_aggr (sum / mean), rel*s -> pos_aggr (mean)
+    const int head = c.valid ? (int)((c.seg0 > base) ? (c.seg0 - base) : 0) : li;
+    const bool is_end = c.valid && (c.e == c.seg1 - 1);
+    const bool take = (li == 0) && c.valid && (c.i == carry_node);
+    float pv[3] = {c.rx * s_e, c.ry * s_e, c.rz * s_e};
+    carry_apply<D>(cbuf, m, pv, c.valid, take);
+    seg_scan<T>(m, li, head);
+    {
+      f32x4 pw[1] = {{pv[0], pv[1], pv[2], 0.f}};
+      seg_scan<1>(pw, li, head);
+      pv[0] = pw[0][0]; pv[1] = pw[0][1]; pv[2] = pw[0][2];
+    }
+    if (is_end) {
+      const float deg = (float)(c.seg1 - c.seg0);
+      if (MSG_MEAN) {
+#pragma unroll
+        for (int p = 0; p < T; ++p) m[p] *= 1.f / deg;
+      }
+      store_row<D>(rowp(m_aggr, c.i, D), m, g);
+      if (g == 0) {
+        pos_aggr[3 * c.i + 0] = pv[0] / deg;
+        pos_aggr[3 * c.i + 1] = pv[1] / deg;
+        pos_aggr[3 * c.i + 2] = pv[2] / deg;
+      }
+    }
+    if (li == 15) carry_store<D>(cbuf, m, pv);
+    carry_node = __builtin_amdgcn_readlane(c.i, 15);
+  }
+}
+
+// ================================================================================== backward
+constexpr int NVG = 8;  // vector-gradient outputs: ln1w ln1b ln2w ln2b ln3w ln3b w4 w1d
+enum GradVec { G_LN1W = 0, G_LN1B, G_LN2W, G_LN2B, G_LN3W, G_LN3B, G_W4, G_W1D };
+
+template <int D>
+__device__ __forceinline__ float slot(const f32x4 (&x)[D / 16], int s) { return x[s >> 2][s & 3]; }
+template <int D>
+__device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
+  return sV[v * D + featq(s, g)];
+}
+
+template <int D, int ACT, bool MSG_MEAN>
+__global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
+    int64_t n_nodes, int64_t n_edges, const float* __restrict__ AB, const float* __restrict__ pos,
+    const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
+    const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
+    const float* __restrict__ g_maggr, const float* __restrict__ g_paggr, float* __restrict__ dA,
+    float* __restrict__ dpos_recv, float* __restrict__ dpre1_out, float* __restrict__ gdiff_out,
+    float* __restrict__ y1_out, float* __restrict__ m_out, float* __restrict__ dpre2_out,
+    float* __restrict__ dpre3_out, float* __restrict__ partials) {
+  constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW, K = VecAcc<D>::K;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const float* sW2 = smem;
+  const float* sW3 = smem + D * LDW;
+  const float* sV = smem + 2 * D * LDW;
+  load_params_to_lds<D>(smem, P);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* cbuf = smem + smem_params_floats<D>() + (wid * 4 + g) * carry_stride<D>();
+  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid);
+  const float b4 = P.b4[0];
+
+  float vacc[NVG][K];
+#pragma unroll
+  for (int v = 0; v < NVG; ++v)
+#pragma unroll
+    for (int k = 0; k < K; ++k) vacc[v][k] = 0.f;
+  float db4 = 0.f;
+  int carry_node = -1;
+
+  for (int base = wr.e_lo; base < wr.e_hi; base += 16) {
+    asm volatile("" ::: "memory");
+    const EdgeCtx c = edge_ctx(base, li, wr.e_hi, (int)n_nodes, recv, send, rowptr, pos);
+    const float* arow = rowp(AB, c.i, 2 * D);
+    const float* brow = rowp(AB, c.j, 2 * D) + D;
+
+    // ---------------- recompute y1 (x), xhat2 (xh2), m (x), xhat3 (z)
+    f32x4 x[T];
+    load_pre1<D>(x, arow, brow, sV, c.dist, g);
+    const float rstd1 = ln_normalize<D>(x, eps);
+    affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
+    if (c.valid) store_row<D>(rowp(y1_out, c.e, D), x, g);
+
+    f32x4 xh2[T];
+    load_vec<D>(xh2, sV, V_B2, g);
+    gemm_wx<D>(sW2, x, xh2, li, g);
+    const float rstd2 = ln_normalize<D>(xh2, eps);
+#pragma unroll
+    for (int p = 0; p < T; ++p) {
+      const f32x4 w = vec4<D>(sV, V_LN2W, p, g), b = vec4<D>(sV, V_LN2B, p, g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[p][q] = act_f<ACT>(xh2[p][q] * w[q] + b[q]);
+    }
+    if (c.valid) store_row<D>(rowp(m_out, c.e, D), x, g);
+
+    f32x4 z[T];
+    load_vec<D>(z, sV, V_B3, g);
+    gemm_wx<D>(sW3, x, z, li, g);
+    const float rstd3 = ln_normalize<D>(z, eps);  // z = xhat3
+
+    // ---------------- pos-branch backward
+    const float inv_deg = c.valid ? 1.f / (float)(c.seg1 - c.seg0) : 0.f;
+    const float gpx = c.valid ? g_paggr[3 * c.i + 0] * inv_deg : 0.f;
+    const float gpy = c.valid ? g_paggr[3 * c.i + 1] * inv_deg : 0.f;
+    const float gpz = c.valid ? g_paggr[3 * c.i + 2] * inv_deg : 0.f;
+    const float ds = gpx * c.rx + gpy * c.ry + gpz * c.rz;  // dL/ds_e
+    if (g == 0) db4 += ds;
+
+    float sp = 0.f;
+#pragma unroll
+    for (int p = 0; p < T; ++p) {
+      const f32x4 w3 = vec4<D>(sV, V_LN3W, p, g), b3 = vec4<D>(sV, V_LN3B, p, g);
+      const f32x4 w4 = vec4<D>(sV, V_W4, p, g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float zz = z[p][q] * w3[q] + b3[q];
+        sp += w4[q] * act_f<ACT>(zz);
+        x[p][q] = ds * w4[q] * act_df<ACT>(zz);  // dz3 (m already stored)
+      }
+    }
+    const float s_e = sum_groups(sp) + b4;
+    accumulate_vec<D>([&](int s) {
+      return ds * act_f<ACT>(slot<D>(z, s) * vslot<D>(sV, V_LN3W, s, g) + vslot<D>(sV, V_LN3B, s, g));
+    }, vacc[G_W4], li);
+    accumulate_vec<D>([&](int s) { return slot<D>(x, s) * slot<D>(z, s); }, vacc[G_LN3W], li);
+    accumulate_vec<D>([&](int s) { return slot<D>(x, s); }, vacc[G_LN3B], li);
+#pragma unroll
+    for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN3W, p, g);
+    ln_backward<D>(x, z, rstd3);  // x = dpre3
+    if (c.valid) store_row<D>(rowp(dpre3_out, c.e, D), x, g);
+
+    // ---------------- dm = g_m_aggr[i] (/deg) + W3^T dpre3   (z)
+    if (c.valid) {
+      load_row<D>(z, rowp(g_maggr, c.i, D), g);
+      if (MSG_MEAN) {
+#pragma unroll
+        for (int p = 0; p < T; ++p) z[p] *= inv_deg;
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < T; ++p) z[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    gemm_wtx<D>(sW3, x, z, li, g);
+#pragma unroll
+    for (int p = 0; p < T; ++p) {
+      const f32x4 w = vec4<D>(sV, V_LN2W, p, g), b = vec4<D>(sV, V_LN2B, p, g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) z[p][q] *= act_df<ACT>(xh2[p][q] * w[q] + b[q]);  // dz2
+    }
+    accumulate_vec<D>([&](int s) { return slot<D>(z, s) * slot<D>(xh2, s); }, vacc[G_LN2W], li);
+    accumulate_vec<D>([&](int s) { return slot<D>(z, s); }, vacc[G_LN2B], li);
+#pragma unroll
+    for (int p = 0; p < T; ++p) z[p] *= vec4<D>(sV, V_LN2W, p, g);
+    ln_backward<D>(z, xh2, rstd2);  // z = dpre2
+    if (c.valid) store_row<D>(rowp(dpre2_out, c.e, D), z, g);
+
+    // ---------------- dy1 = W2^T dpre2 (x); xhat1 recomputed into xh2
+#pragma unroll
+    for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_wtx<D>(sW2, z, x, li, g);
+    load_pre1<D>(xh2, arow, brow, sV, c.dist, g);
+    ln_normalize<D>(xh2, eps);
+#pragma unroll
+    for (int p = 0; p < T; ++p) {
+      const f32x4 w = vec4<D>(sV, V_LN1W, p, g), b = vec4<D>(sV, V_LN1B, p, g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[p][q] *= act_df<ACT>(xh2[p][q] * w[q] + b[q]);  // dz1
+    }
+    accumulate_vec<D>([&](int s) { return slot<D>(x, s) * slot<D>(xh2, s); }, vacc[G_LN1W], li);
+    accumulate_vec<D>([&](int s) { return slot<D>(x, s); }, vacc[G_LN1B], li);
+#pragma unroll
+    for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN1W, p, g);
+    ln_backward<D>(x, xh2, rstd1);  // x = dpre1
+    if (c.valid) store_row<D>(rowp(dpre1_out, c.e, D), x, g);
+
+    // dw1d += dpre1 * dist ; d(dist) = w1d . dpre1
+    float dd = 0.f;
+#pragma unroll
+    for (int p = 0; p < T; ++p) {
+      const f32x4 w = vec4<D>(sV, V_W1D, p, g);
+      dd += w[0] * x[p][0] + w[1] * x[p][1] + w[2] * x[p][2] + w[3] * x[p][3];
+    }
+    dd = sum_groups(dd);
+    const float dist = c.dist;
+    accumulate_vec<D>([&](int s) { return slot<D>(x, s) * dist; }, vacc[G_W1D], li);
+
+    const float rinv = (c.dist > 0.f) ? dd / c.dist : 0.f;
+    float gd[3] = {gpx * s_e + rinv * c.rx, gpy * s_e + rinv * c.ry, gpz * s_e + rinv * c.rz};
+    if (c.valid && g == 0) {
+      gdiff_out[3 * c.e + 0] = gd[0];
+      gdiff_out[3 * c.e + 1] = gd[1];
+      gdiff_out[3 * c.e + 2] = gd[2];
+    }
+
+    // ---------------- receiver-side segmented sums: dA (dpre1), dpos_recv (gdiff)
+    const int head = c.valid ? (int)((c.seg0 > base) ? (c.seg0 - base) : 0) : li;
+    const bool is_end = c.valid && (c.e == c.seg1 - 1);
+    const bool take = (li == 0) && c.valid && (c.i == carry_node);
+    carry_apply<D>(cbuf, x, gd, c.valid, take);
+    seg_scan<T>(x, li, head);
+    {
+      f32x4 pw[1] = {{gd[0], gd[1], gd[2], 0.f}};
+      seg_scan<1>(pw, li, head);
+      gd[0] = pw[0][0]; gd[1] = pw[0][1]; gd[2] = pw[0][2];
+    }
+    if (is_end) {
+      store_row<D>(rowp(dA, c.i, D), x, g);
+      if (g == 0) {
+        dpos_recv[3 * c.i + 0] = gd[0];
+        dpos_recv[3 * c.i + 1] = gd[1];
+        dpos_recv[3 * c.i + 2] = gd[2];
+      }
+    }
+    if (li == 15) carry_store<D>(cbuf, x, gd);
+    carry_node = __builtin_amdgcn_readlane(c.i, 15);
+  }
+
+  // ---------------- workgroup reduction of the vector grads -> partials[blockIdx]
+  __syncthreads();  // every wave is done with W2/W3: reuse that LDS as scratch
+  float* red = smem;  // [wave][NVG*D + 1]
+  constexpr int RW = NVG * D + 1;
+  for (int t = lane; t < RW; t += 64) red[wid * RW + t] = 0.f;
+  __syncthreads();
+  if (acc_owner<D>(li)) {
+#pragma unroll
+    for (int v = 0; v < NVG; ++v)
+#pragma unroll
+      for (int k = 0; k < K; ++k) red[wid * RW + v * D + featq(acc_slot<D>(li, k), g)] = vacc[v][k];
+  }
+  float t4 = db4;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) t4 += __shfl_xor(t4, off);
+  if (lane == 0) red[wid * RW + NVG * D] = t4;
+  __syncthreads();
+  for (int t = threadIdx.x; t < RW; t += blockDim.x) {
+    float sacc = 0.f;
+    for (int w = 0; w < kWavesPerBlock; ++w) sacc += red[w * RW + t];
+    partials[(int64_t)blockIdx.x * RW + t] = sacc;
+  }
+}
+
+int64_t n_waves_for(int64_t n_edges) {
+  int64_t w = ceil_div(n_edges, 128);  // >= 8 chunks per wave when the chip is full
+  const int64_t cap = (int64_t)device_cu_count() * kWavesPerBlock;
+  if (w > cap) w = cap;
+  if (w < 1) w = 1;
+  return ceil_div(w, kWavesPerBlock) * kWavesPerBlock;
+}
+
+template <class K>
+int prep_kernel(K k, size_t smem) {
+  return hip_check(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)smem));
+}
+
+template <int D, int ACT, bool MEAN>
+int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const int64_t* rowptr,
+               const int64_t* recv, const int64_t* send, const gmp_egnn_params& P, float eps,
+               float* m_aggr, float* pos_aggr, hipStream_t s) {
+  const int64_t W = n_waves_for(E);
+  const size_t smem = smem_total<D>();
+  auto k = egnn_fwd_kernel<D, ACT, MEAN>;
+  int rc = prep_kernel(k, smem);
+  if (rc) return rc;
+  k<<<(unsigned)(W / kWavesPerBlock), kThreads, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
+                                                           eps, W, m_aggr, pos_aggr);
+  return launch_status();
+}
+
+template <int D, int ACT, bool MEAN>
+int launch_bwd(int64_t N, int64_t E, const float* AB, const float* pos, const int64_t* rowptr,
+               const int64_t* recv, const int64_t* send, const gmp_egnn_params& P, float eps,
+               const float* gm, const float* gp, float* dA, float* dpos_recv, float* dpre1,
+               float* gdiff, float* y1, float* m, float* dpre2, float* dpre3, float* partials,
+               hipStream_t s) {
+  const int64_t W = n_waves_for(E);
+  const size_t smem = smem_total<D>();
+  auto k = egnn_bwd_kernel<D, ACT, MEAN>;
+  int rc = prep_kernel(k, smem);
+  if (rc) return rc;
+  k<<<(unsigned)(W / kWavesPerBlock), kThreads, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
+                                                           eps, W, gm, gp, dA, dpos_recv, dpre1,
+                                                           gdiff, y1, m, dpre2, dpre3, partials);
+  return launch_status();
+}
+
+bool params_ok(const gmp_egnn_params* P) {
+  return P && P->w1d && P->b1 && P->ln1_w && P->ln1_b && P->W2 && P->b2 && P->ln2_w &&
+         P->ln2_b && P->W3 && P->b3 && P->ln3_w && P->ln3_b && P->w4 && P->b4;
+}
+
+bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+}  // namespace
+}  // namespace gmp
+
+using namespace gmp;
+
+#define GMP_EGNN_DISPATCH(CALL)                                                                \
+  do {                                                                                         \
+    if (d == 128) {                                                                            \
+      if (act == 0) { if (msg_mean) CALL(128, 0, true); else CALL(128, 0, false); }            \
+      else          { if (msg_mean) CALL(128, 1, true); else CALL(128, 1, false); }            \
+    } else if (d == 64) {                                                                      \
+      if (act == 0) { if (msg_mean) CALL(64, 0, true); else CALL(64, 0, false); }              \
+      else          { if (msg_mean) CALL(64, 1, true); else CALL(64, 1, false); }              \
+    } else {                                                                                   \
+      if (act == 0) { if (msg_mean) CALL(32, 0, true); else CALL(32, 0, false); }              \
+      else          { if (msg_mean) CALL(32, 1, true); else CALL(32, 1, false); }              \
+    }                                                                                          \
+  } while (0)
+
+extern "C" {
+
+int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
+                          const float* pos, const int64_t* rowptr, const int64_t* recv,
+                          const int64_t* send, const gmp_egnn_params* params, int act,
+                          int msg_mean, float ln_eps, float* m_aggr, float* pos_aggr,
+                          void* stream) {
+  if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
+  GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
+  GMP_CHECK_ARG(params_ok(params) && m_aggr && pos_aggr && rowptr);
+  hipStream_t s = as_stream(stream);
+  if (n_nodes == 0) return GMP_OK;
+  int rc = hip_check(hipMemsetAsync(m_aggr, 0, n_nodes * d * sizeof(float), s));
+  if (!rc) rc = hip_check(hipMemsetAsync(pos_aggr, 0, n_nodes * 3 * sizeof(float), s));
+  if (rc || n_edges == 0) return rc;
+  GMP_CHECK_ARG(AB && pos && recv && send && aligned16(AB) && aligned16(m_aggr));
+  GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
+#define GMP_CALL_FWD(DD, AA, MM)                                                              \
+  rc = launch_fwd<DD, AA, MM>(n_nodes, n_edges, AB, pos, rowptr, recv, send, *params, ln_eps, \
+                              m_aggr, pos_aggr, s)
+  GMP_EGNN_DISPATCH(GMP_CALL_FWD);
+#undef GMP_CALL_FWD
+  return rc;
+}
+
+int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d) {
+  (void)d;
+  return n_waves_for(n_edges) / kWavesPerBlock;
+}
+
+int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
+                          const float* pos, const int64_t* rowptr, const int64_t* recv,
+                          const int64_t* send, const gmp_egnn_params* params, int act,
+                          int msg_mean, float ln_eps, const float* g_m_aggr,
+                          const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
+                          float* gdiff, float* y1, float* m, float* dpre2, float* dpre3,
+                          float* vec_partials, void* stream) {
+  if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
+  GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
+  GMP_CHECK_ARG(params_ok(params) && dA && dpos_recv && rowptr && vec_partials);
+  hipStream_t s = as_stream(stream);
+  int rc = GMP_OK;
+  if (n_nodes > 0) {
+    rc = hip_check(hipMemsetAsync(dA, 0, n_nodes * d * sizeof(float), s));
+    if (!rc) rc = hip_check(hipMemsetAsync(dpos_recv, 0, n_nodes * 3 * sizeof(float), s));
+  }
+  if (rc) return rc;
+  if (n_edges == 0 || n_nodes == 0) {
+    return hip_check(hipMemsetAsync(
+        vec_partials, 0,
+        gmp_egnn_edge_bwd_partials_rows(n_edges, d) * (8 * d + 1) * sizeof(float), s));
+  }
+  GMP_CHECK_ARG(AB && pos && recv && send && g_m_aggr && g_pos_aggr && dpre1 && gdiff && y1 &&
+                m && dpre2 && dpre3);
+  GMP_CHECK_ARG(aligned16(AB) && aligned16(dA) && aligned16(g_m_aggr) && aligned16(dpre1) &&
+                aligned16(y1) && aligned16(m) && aligned16(dpre2) && aligned16(dpre3));
+  GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
+#define GMP_CALL_BWD(DD, AA, MM)                                                              \
+  rc = launch_bwd<DD, AA, MM>(n_nodes, n_edges, AB, pos, rowptr, recv, send, *params, ln_eps, \
+                              g_m_aggr, g_pos_aggr, dA, dpos_recv, dpre1, gdiff, y1, m, dpre2,  \
+                              dpre3, vec_partials, s)
+  GMP_EGNN_DISPATCH(GMP_CALL_BWD);
+#undef GMP_CALL_BWD
+  return rc;
+}
+
+}  // extern "C"

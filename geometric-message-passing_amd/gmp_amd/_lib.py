@@ -1,0 +1,90 @@
+"""ctypes binding of libgmp.so (the C ABI declared in include/gmp.h).
+
+The product path has no CPU fallback: if the library is missing or a CUDA/HIP device is not
+available the ops raise.  Build with `python -c "import __graft_entry__ as g; g.build()"` or
+`make -C geometric-message-passing_amd/csrc`.
+"""
+import ctypes
+import os
+
+# Import torch first: its bundled libamdhip64.so (SONAME libamdhip64.so.7) must be the HIP
+# runtime that libgmp.so binds to, so both share one runtime, device context and streams.
+import torch  # noqa: F401
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GMP_LIB", os.path.join(_HERE, "libgmp.so"))
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_vp = ctypes.c_void_p
+c_f32 = ctypes.c_float
+c_size = ctypes.c_size_t
+
+GMP_OK, GMP_ERR_ARG, GMP_ERR_HIP, GMP_ERR_UNSUPPORTED, GMP_ERR_WORKSPACE = 0, -1, -2, -3, -4
+REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
+ACT = {"relu": 0, "swish": 1, "silu": 1}
+
+
+class GmpEgnnParams(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in (
+        "w1d", "b1", "ln1_w", "ln1_b", "W2", "b2", "ln2_w", "ln2_b", "W3", "b3", "ln3_w", "ln3_b",
+        "w4", "b4")]
+
+
+# name -> (restype, argtypes); must mirror include/gmp.h exactly
+SIGNATURES = {
+    "gmp_abi_version": (c_int, []),
+    "gmp_error_string": (ctypes.c_char_p, [c_int]),
+    "gmp_last_hip_error": (c_int, []),
+    "gmp_csr_workspace_size": (c_size, [c_i64, c_i64]),
+    "gmp_csr_build": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                              c_size, c_vp]),
+    "gmp_gather_rows_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "gmp_segment_reduce_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
+                                       c_vp]),
+    "gmp_segment_reduce_bwd_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp,
+                                           c_vp, c_vp]),
+    "gmp_egnn_edge_fwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
+                                      c_vp, c_vp]),
+    "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
+    "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp]),
+}
+
+_lib = None
+
+
+class GmpError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load libgmp.so and declare every C-ABI signature. Raises if anything is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise GmpError(f"libgmp.so not found at {p}: build it first "
+                       "(python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if the symbol is not exported
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gmp_abi_version() != 1:
+        raise GmpError("libgmp ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != GMP_OK:
+        lib = load()
+        msg = lib.gmp_error_string(rc).decode()
+        hip = lib.gmp_last_hip_error() if rc == GMP_ERR_HIP else 0
+        raise GmpError(f"{what} failed: {msg} (code {rc}, hip error {hip})")

@@ -1,0 +1,66 @@
+"""torch_scatter-compatible scatter on the MI355X (drop-in for the reference's call sites
+models/layers/egnn_layer.py:77,79, models/layers/tfn_layer.py:87, gvp_layer.py:415, PyG
+aggregate and pools).
+
+Semantics (torch_scatter 2.x): out rows along `dim` = dim_size or index.max()+1 (the latter
+costs one host sync, as in torch_scatter); empty rows are 0; mean = sum / count.clamp(1);
+max returns values only (empty rows 0).  Reductions are deterministic segmented sums over a
+stable receiver-sorted CSR (gmp_csr_build + gmp_segment_reduce_f32), not atomics.
+"""
+import torch
+
+from . import ops
+
+
+def _rows(index, dim_size):
+    if dim_size is not None:
+        return int(dim_size)
+    return int(index.max().item()) + 1 if index.numel() else 0
+
+
+def scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum"):
+    if reduce not in ("sum", "add", "mean", "max"):
+        raise ValueError(f"unsupported reduce {reduce!r}")
+    dim = dim % src.dim()
+    if index.dim() != 1:
+        # torch_scatter broadcasts index; the reference always passes a 1-D index along dim
+        raise NotImplementedError("gmp scatter supports 1-D index along `dim`")
+    n = _rows(index, dim_size)
+    x = src.movedim(dim, 0)
+    shp = x.shape
+    x2 = x.reshape(shp[0], -1)
+    csr = ops.get_csr(index, n)
+    red = "sum" if reduce == "add" else reduce
+    o = ops.SegmentReduceFn.apply(x2, csr, red).reshape((n,) + tuple(shp[1:])).movedim(0, dim)
+    if out is not None:
+        out.copy_(o)
+        return out
+    return o
+
+
+def scatter_sum(src, index, dim=-1, out=None, dim_size=None):
+    return scatter(src, index, dim, out, dim_size, "sum")
+
+
+scatter_add = scatter_sum
+
+
+def scatter_mean(src, index, dim=-1, out=None, dim_size=None):
+    return scatter(src, index, dim, out, dim_size, "mean")
+
+
+def scatter_max(src, index, dim=-1, out=None, dim_size=None):
+    return scatter(src, index, dim, out, dim_size, "max")
+
+
+def global_add_pool(x, batch, size=None):
+    """PyG global_add_pool: sum over nodes of each graph (batch vector)."""
+    if batch is None:
+        return x.sum(dim=-2, keepdim=x.dim() == 1)
+    return scatter(x, batch, dim=-2, dim_size=size, reduce="sum")
+
+
+def global_mean_pool(x, batch, size=None):
+    if batch is None:
+        return x.mean(dim=-2, keepdim=x.dim() == 1)
+    return scatter(x, batch, dim=-2, dim_size=size, reduce="mean")

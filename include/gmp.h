@@ -1,0 +1,150 @@
+/*
+ * gmp.h — C ABI of the MI355X (gfx950) geometric message-passing hot path.
+ *
+ * The reference (NW-JEFF/Geometric-Message-Passing) has no native code of its own: its hot path
+ * runs through PyG `MessagePassing.propagate`, `torch_scatter.scatter` (C++/CUDA custom ops
+ * `torch.ops.torch_scatter.scatter_sum/mean/max`) and e3nn modules.  Each
+ * entry point below replaces one of those call sites; the replaced interface is cited per
+ * function as reference file:line.
+ *
+ * Conventions (all functions):
+ *   - plain device pointers, int64 sizes, fp32 features, int64 indices (the reference dtypes);
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream); no function allocates,
+ *     frees or synchronises; all work is enqueued on `stream` (graph-capture safe);
+ *   - return GMP_OK (0) or a negative error code (gmp_error_string); argument checks are done
+ *     on the host before anything is enqueued; device-side index range errors are reported
+ *     through an optional int32 device flag (`err_flag`, set to 1; caller checks when it wants);
+ *   - outputs are fully written (zero rows included) unless documented as accumulating.
+ */
+#ifndef GMP_H_
+#define GMP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GMP_ABI_VERSION 1
+
+enum {
+  GMP_OK = 0,
+  GMP_ERR_ARG = -1,         /* bad pointer / size / unsupported combination */
+  GMP_ERR_HIP = -2,         /* a HIP runtime call failed (see gmp_last_hip_error) */
+  GMP_ERR_UNSUPPORTED = -3, /* shape not supported by this fused kernel */
+  GMP_ERR_WORKSPACE = -4    /* workspace too small */
+};
+
+enum { GMP_REDUCE_SUM = 0, GMP_REDUCE_MEAN = 1, GMP_REDUCE_MAX = 2 };
+enum { GMP_ACT_RELU = 0, GMP_ACT_SILU = 1 };
+
+int gmp_abi_version(void);
+const char* gmp_error_string(int code);
+int gmp_last_hip_error(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Index preprocessing: stable CSR of an index array (receiver-sorted edge lists).
+ * Replaces the implicit ordering work of torch_scatter's atomics (egnn_layer.py:77,79;
+ * tfn_layer.py:87; PyG aggregate): we sort once per graph and reduce deterministically.
+ *   perm[k]      = position of the k-th item in stable order of index (k = 0..n_items-1)
+ *   rowptr[s]    = first k with index[perm[k]] >= s   (s = 0..n_seg), rowptr[n_seg] = n_items
+ *   payload_out  = payload[perm] (optional, may be NULL)
+ * Workspace: gmp_csr_workspace_size(n_items, n_seg) bytes.
+ * ------------------------------------------------------------------------------------------ */
+size_t gmp_csr_workspace_size(int64_t n_items, int64_t n_seg);
+int gmp_csr_build(const int64_t* index, int64_t n_items, int64_t n_seg, const int64_t* payload,
+                  int64_t* perm, int64_t* rowptr, int64_t* index_sorted, int64_t* payload_out,
+                  int32_t* err_flag, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * K2 gather: out[e, :] = src[index[e], :]   (PyG `_collect` index_select of x_i / x_j,
+ * torch_geometric MessagePassing.propagate; tfn_layer.py:85 `node_attr[dst]`).
+ * Out-of-range index -> row of zeros and *err_flag = 1 (err_flag may be NULL).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_gather_rows_f32(const float* src, int64_t n_rows, int64_t F, const int64_t* index,
+                        int64_t n_index, float* out, int32_t* err_flag, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * K3 segmented reduce over a CSR (torch_scatter.scatter(src, index, dim=0, dim_size, reduce)
+ * with reduce in {sum/add, mean, max}; egnn_layer.py:77,79, tfn_layer.py:87, PyG aggregate,
+ * global_add_pool / global_mean_pool).
+ *   out[s, f] = reduce_{k in [rowptr[s], rowptr[s+1])} src[perm ? perm[k] : k, f]
+ *   empty segments -> 0; mean divides by max(count, 1); max also writes argmax[s, f]
+ *   (item index, n_items for empty segments; argmax may be NULL for sum/mean).
+ * Summation order is the CSR order (deterministic).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_segment_reduce_f32(const float* src, int64_t n_items, int64_t F, const int64_t* perm,
+                           const int64_t* rowptr, int64_t n_seg, int reduce, float* out,
+                           int64_t* argmax, void* stream);
+
+/* Backward of gmp_segment_reduce_f32 w.r.t. src (torch_scatter autograd):
+ *   sum : grad_src[e] = grad_out[index[e]]
+ *   mean: grad_src[e] = grad_out[index[e]] / max(count[index[e]], 1)   (count from rowptr)
+ *   max : grad_src[e, f] = (argmax[index[e], f] == e) ? grad_out[index[e], f] : 0            */
+int gmp_segment_reduce_bwd_f32(const float* grad_out, int64_t n_seg, int64_t F,
+                               const int64_t* index, int64_t n_items, const int64_t* rowptr,
+                               int reduce, const int64_t* argmax, float* grad_src, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * K4 EGNN fused edge message + aggregation (egnn_layer.py:62-80 message/aggregate; the node
+ * update :82-86 stays a node-level op).  Edges must be receiver-sorted (CSR from
+ * gmp_csr_build on edge_index[1]).  The first message Linear(2d+1 -> d) is split as
+ *   W1 [h_i | h_j | dist] = (h W1a^T)[i] + (h W1b^T)[j] + w1d * dist
+ * so the node projections AB = [h W1a^T | h W1b^T] (N x 2d) are computed once per node by the
+ * caller.  Per edge e = (j -> i), in registers:
+ *   rel = pos[i]-pos[j]; dist = |rel|; y1 = act(LN1(AB[i,:d] + AB[j,d:] + w1d*dist + b1))
+ *   m = act(LN2(W2 y1 + b2)); y3 = act(LN3(W3 m + b3)); s = w4.y3 + b4; shift = rel * s
+ * and per receiver i (segmented, deterministic, no atomics):
+ *   m_aggr[i] = sum_e m  (or mean if msg_mean), pos_aggr[i] = mean_e shift.
+ * d in {32, 64, 128}.  LayerNorm eps = ln_eps.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct gmp_egnn_params {
+  const float* w1d;  /* (d)  column 2d of mlp_msg.0.weight   */
+  const float* b1;   /* (d)  mlp_msg.0.bias                   */
+  const float* ln1_w;
+  const float* ln1_b;
+  const float* W2;   /* (d,d) mlp_msg.3.weight, row-major [out][in] */
+  const float* b2;
+  const float* ln2_w;
+  const float* ln2_b;
+  const float* W3;   /* (d,d) mlp_pos.0.weight */
+  const float* b3;
+  const float* ln3_w;
+  const float* ln3_b;
+  const float* w4;   /* (d)  mlp_pos.3.weight */
+  const float* b4;   /* (1)  mlp_pos.3.bias   */
+} gmp_egnn_params;
+
+int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
+                          const float* pos, const int64_t* rowptr, const int64_t* recv,
+                          const int64_t* send, const gmp_egnn_params* params, int act,
+                          int msg_mean, float ln_eps, float* m_aggr, float* pos_aggr,
+                          void* stream);
+
+/* Backward of gmp_egnn_edge_fwd_f32 (recomputes the forward chain per edge tile).
+ * Inputs g_m_aggr (N,d), g_pos_aggr (N,3).  Outputs:
+ *   dA        (N,d)  receiver part of d(AB)[:, :d]   (segment-summed in-kernel)
+ *   dpos_recv (N,3)  receiver part of d(pos)          (segment-summed in-kernel)
+ *   per edge, in receiver-sorted order (row e):
+ *     dpre1 (E,d)  grad of the first pre-activation   -> caller reduces by sender for
+ *                  d(AB)[:, d:], and takes db1 = sum_e dpre1
+ *     gdiff (E,3)  grad of rel                         -> caller: dpos[send] -= gdiff
+ *     y1, m, dpre2, dpre3 (E,d) each                   -> caller: dW2 = dpre2^T y1,
+ *                  dW3 = dpre3^T m, db2 = sum dpre2, db3 = sum dpre3 (GEMMs over edges)
+ *   vec_partials (n_blocks, 8*d+1): per-workgroup partial sums of
+ *     [dln1_w, dln1_b, dln2_w, dln2_b, dln3_w, dln3_b, dw4, dw1d, db4]   (caller sums rows;
+ *     n_blocks from gmp_egnn_edge_bwd_partials_rows). Deterministic. */
+int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d);
+int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
+                          const float* pos, const int64_t* rowptr, const int64_t* recv,
+                          const int64_t* send, const gmp_egnn_params* params, int act,
+                          int msg_mean, float ln_eps, const float* g_m_aggr,
+                          const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
+                          float* gdiff, float* y1, float* m, float* dpre2, float* dpre3,
+                          float* vec_partials, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMP_H_ */
