@@ -96,7 +96,98 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int64_t n_rows
   }
 }
 
-// One wave per segment; lanes cover the feature dim in VEC-wide pieces; items unrolled x4.
+// ------------------------------------------------------------------------------ K3 wave reduce
+// A wave reduces rows [k_beg, k_end) of the (perm-indexed) item list.  Lanes are split into
+// R = 64/LPR row slots x LPR column lanes (LPR = lanes per row, a power of two >= F/VEC, <= 64),
+// so a 128-float row uses 32 lanes and two rows are read per step; rows are unrolled x4.
+// Partials of the R row slots are combined in a fixed order (deterministic).
+struct RedVal {
+  float v;
+  int64_t arg;
+};
+
+template <int REDUCE>
+__device__ __forceinline__ void red_combine(float& acc, int64_t& arg, float x, int64_t xa) {
+  if (REDUCE == GMP_REDUCE_MAX) {
+    if (x > acc || (x == acc && xa < arg)) { acc = x; arg = xa; }
+  } else {
+    acc += x;
+  }
+}
+
+template <int VEC, int REDUCE>
+__device__ __forceinline__ void wave_reduce_rows(const float* __restrict__ src, int64_t F,
+                                                 const int64_t* __restrict__ perm, int64_t k_beg,
+                                                 int64_t k_end, int64_t n_items, int64_t c,
+                                                 int lpr, float (&acc)[VEC], int64_t (&arg)[VEC]) {
+  const int lane = threadIdx.x & 63;
+  const int R = 64 / lpr, sub = lane / lpr;
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    acc[v] = (REDUCE == GMP_REDUCE_MAX) ? -INFINITY : 0.f;
+    arg[v] = n_items;
+  }
+  const bool active = c < F / VEC;
+  int64_t k = k_beg + sub;
+  for (; k + 3 * R < k_end; k += 4 * R) {
+    int64_t it[4];
+    float x[4][VEC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) it[u] = perm ? perm[k + u * R] : (k + u * R);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* p = src + it[u] * F + c * VEC;
+      if (!active) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) x[u][v] = 0.f;
+      } else if constexpr (VEC == 4) {
+        float4 q = *reinterpret_cast<const float4*>(p);
+        x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
+      } else if constexpr (VEC == 2) {
+        float2 q = *reinterpret_cast<const float2*>(p);
+        x[u][0] = q.x; x[u][1] = q.y;
+      } else {
+        x[u][0] = p[0];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) red_combine<REDUCE>(acc[v], arg[v], x[u][v], it[u]);
+  }
+  for (; k < k_end; k += R) {
+    const int64_t i = perm ? perm[k] : k;
+    if (active) {
+      const float* p = src + i * F + c * VEC;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) red_combine<REDUCE>(acc[v], arg[v], p[v], i);
+    }
+  }
+  // combine the R row slots (lanes differing in the bits above log2(lpr))
+  for (int m = lpr; m < 64; m <<= 1) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const float ox = __shfl_xor(acc[v], m);
+      const int64_t oa = __shfl_xor(arg[v], m);
+      if (REDUCE == GMP_REDUCE_MAX) {
+        // keep the larger value; ties -> first occurrence (smallest item index)
+        if (ox > acc[v] || (ox == acc[v] && oa < arg[v])) { acc[v] = ox; arg[v] = oa; }
+      } else {
+        // fixed order: lower slot + upper slot
+        const bool upper = (lane & m) != 0;
+        acc[v] = upper ? ox + acc[v] : acc[v] + ox;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int lanes_per_row(int64_t cpr) {
+  int l = 1;
+  while (l < cpr && l < 64) l <<= 1;
+  return l;
+}
+
+// One wave per segment.
 template <int VEC, int REDUCE>
 __global__ __launch_bounds__(256) void segment_reduce_wave(
     const float* __restrict__ src, int64_t n_items, int64_t F, const int64_t* __restrict__ perm,
@@ -106,67 +197,76 @@ __global__ __launch_bounds__(256) void segment_reduce_wave(
   const int64_t seg = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
   if (seg >= n_seg) return;
   const int64_t k0 = rowptr[seg], k1 = rowptr[seg + 1];
-  const int64_t fv = F / VEC;
-  for (int64_t c = lane; c < fv; c += 64) {
+  const int64_t cpr = F / VEC;
+  const int lpr = lanes_per_row(cpr);
+  for (int64_t cb = 0; cb < cpr; cb += 64) {
+    const int64_t c = cb + lane % lpr;
     float acc[VEC];
     int64_t arg[VEC];
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) {
-      acc[v] = (REDUCE == GMP_REDUCE_MAX) ? -INFINITY : 0.f;
-      arg[v] = n_items;
-    }
-    int64_t k = k0;
-    for (; k + 4 <= k1; k += 4) {
-      int64_t it[4];
-      float x[4][VEC];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) it[u] = perm ? perm[k + u] : (k + u);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float* p = src + it[u] * F + c * VEC;
-        if constexpr (VEC == 4) {
-          float4 q = *reinterpret_cast<const float4*>(p);
-          x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
-        } else if constexpr (VEC == 2) {
-          float2 q = *reinterpret_cast<const float2*>(p);
-          x[u][0] = q.x; x[u][1] = q.y;
-        } else {
-          x[u][0] = p[0];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          if (REDUCE == GMP_REDUCE_MAX) {
-            if (x[u][v] > acc[v]) { acc[v] = x[u][v]; arg[v] = it[u]; }
-          } else {
-            acc[v] += x[u][v];
-          }
-        }
-    }
-    for (; k < k1; ++k) {
-      int64_t i = perm ? perm[k] : k;
-      const float* p = src + i * F + c * VEC;
+    wave_reduce_rows<VEC, REDUCE>(src, F, perm, k0, k1, n_items, c, lpr, acc, arg);
+    const int64_t cnt = k1 - k0;
+    if (lane < lpr && c < cpr) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
-        float xv = p[v];
-        if (REDUCE == GMP_REDUCE_MAX) {
-          if (xv > acc[v]) { acc[v] = xv; arg[v] = i; }
-        } else {
-          acc[v] += xv;
-        }
+        float r = acc[v];
+        if (REDUCE == GMP_REDUCE_MEAN) r = r / (float)(cnt > 0 ? cnt : 1);
+        if (REDUCE == GMP_REDUCE_MAX && cnt == 0) r = 0.f;
+        out[seg * F + c * VEC + v] = r;
+        if (REDUCE == GMP_REDUCE_MAX && argmax) argmax[seg * F + c * VEC + v] = arg[v];
       }
     }
-    const int64_t cnt = k1 - k0;
+  }
+}
+
+// Long segments (sum / mean): block (seg, part) reduces a contiguous slice of the segment with
+// its 4 waves; partial[seg][part][F] in a fixed order; finished by segment_split_finish.
+template <int VEC, int REDUCE>
+__global__ __launch_bounds__(256) void segment_reduce_split(
+    const float* __restrict__ src, int64_t n_items, int64_t F, const int64_t* __restrict__ perm,
+    const int64_t* __restrict__ rowptr, int64_t n_seg, int64_t S, float* __restrict__ partial) {
+  __shared__ float red[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t seg = blockIdx.x / S, part = blockIdx.x % S;
+  const int64_t k0 = rowptr[seg], k1 = rowptr[seg + 1], len = k1 - k0;
+  const int64_t pb = k0 + len * part / S, pe = k0 + len * (part + 1) / S;
+  const int64_t wb = pb + (pe - pb) * w / 4, we = pb + (pe - pb) * (w + 1) / 4;
+  const int64_t cpr = F / VEC;
+  const int lpr = lanes_per_row(cpr);
+  for (int64_t cb = 0; cb < cpr; cb += 64) {
+    const int64_t c = cb + lane % lpr;
+    float acc[VEC];
+    int64_t arg[VEC];
+    wave_reduce_rows<VEC, REDUCE>(src, F, perm, wb, we, n_items, c, lpr, acc, arg);
+    if (lane < lpr) {
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) {
-      float r = acc[v];
-      if (REDUCE == GMP_REDUCE_MEAN) r = r / (float)(cnt > 0 ? cnt : 1);
-      if (REDUCE == GMP_REDUCE_MAX && cnt == 0) r = 0.f;
-      out[seg * F + c * VEC + v] = r;
-      if (REDUCE == GMP_REDUCE_MAX && argmax) argmax[seg * F + c * VEC + v] = arg[v];
+      for (int v = 0; v < VEC; ++v) red[w][lane * VEC + v] = acc[v];
     }
+    __syncthreads();
+    if (w == 0 && lane < lpr && c < cpr) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const float t = ((red[0][lane * VEC + v] + red[1][lane * VEC + v]) + red[2][lane * VEC + v]) +
+                        red[3][lane * VEC + v];
+        partial[(seg * S + part) * F + c * VEC + v] = t;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int REDUCE>
+__global__ void segment_split_finish(const float* __restrict__ partial, const int64_t* __restrict__ rowptr,
+                                     int64_t n_seg, int64_t S, int64_t F, float* __restrict__ out) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n_seg * F;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t seg = t / F, f = t - seg * F;
+    float s = 0.f;
+    for (int64_t p = 0; p < S; ++p) s += partial[(seg * S + p) * F + f];
+    if (REDUCE == GMP_REDUCE_MEAN) {
+      const int64_t cnt = rowptr[seg + 1] - rowptr[seg];
+      s = s / (float)(cnt > 0 ? cnt : 1);
+    }
+    out[t] = s;
   }
 }
 
@@ -316,27 +416,61 @@ int gmp_gather_rows_f32(const float* src, int64_t n_rows, int64_t F, const int64
   return launch_status();
 }
 
+static int64_t split_parts(int64_t n_items, int64_t n_seg, int reduce) {
+  if (reduce == GMP_REDUCE_MAX || n_seg <= 0) return 1;
+  const int64_t avg = n_items / n_seg;
+  if (avg < 2048) return 1;
+  int64_t S = ceil_div(avg, 1024);
+  return S > 4096 ? 4096 : S;
+}
+
+size_t gmp_segment_reduce_workspace_size(int64_t n_items, int64_t n_seg, int64_t F, int reduce) {
+  const int64_t S = split_parts(n_items, n_seg, reduce);
+  return S > 1 ? (size_t)(n_seg * S * F) * sizeof(float) : 0;
+}
+
 int gmp_segment_reduce_f32(const float* src, int64_t n_items, int64_t F, const int64_t* perm,
                            const int64_t* rowptr, int64_t n_seg, int reduce, float* out,
-                           int64_t* argmax, void* stream) {
+                           int64_t* argmax, void* workspace, size_t workspace_bytes,
+                           void* stream) {
   GMP_CHECK_ARG(n_items >= 0 && F >= 0 && n_seg >= 0);
   GMP_CHECK_ARG(reduce == GMP_REDUCE_SUM || reduce == GMP_REDUCE_MEAN || reduce == GMP_REDUCE_MAX);
   if (n_seg == 0 || F == 0) return GMP_OK;
   GMP_CHECK_ARG(rowptr && out && (n_items == 0 || src));
   hipStream_t s = as_stream(stream);
-  const bool aligned = (reinterpret_cast<uintptr_t>(src) % 16 == 0);
+  const bool a16 = (reinterpret_cast<uintptr_t>(src) % 16 == 0);
+  const bool a8 = (reinterpret_cast<uintptr_t>(src) % 8 == 0);
+  const int vec = (F % 4 == 0 && a16) ? 4 : (F % 2 == 0 && a8) ? 2 : 1;
+  const int64_t S = split_parts(n_items, n_seg, reduce);
+  if (S > 1 && workspace && workspace_bytes >= gmp_segment_reduce_workspace_size(n_items, n_seg, F, reduce)) {
+    float* part = reinterpret_cast<float*>(workspace);
+    const unsigned g = (unsigned)(n_seg * S);
+#define GMP_SPLIT(V, RED) segment_reduce_split<V, RED><<<g, 256, 0, s>>>(src, n_items, F, perm, rowptr, n_seg, S, part)
+    if (reduce == GMP_REDUCE_SUM) {
+      if (vec == 4) GMP_SPLIT(4, GMP_REDUCE_SUM); else if (vec == 2) GMP_SPLIT(2, GMP_REDUCE_SUM); else GMP_SPLIT(1, GMP_REDUCE_SUM);
+    } else {
+      if (vec == 4) GMP_SPLIT(4, GMP_REDUCE_MEAN); else if (vec == 2) GMP_SPLIT(2, GMP_REDUCE_MEAN); else GMP_SPLIT(1, GMP_REDUCE_MEAN);
+    }
+#undef GMP_SPLIT
+    int rc = launch_status();
+    if (rc) return rc;
+    if (reduce == GMP_REDUCE_SUM)
+      segment_split_finish<GMP_REDUCE_SUM><<<grid_for(n_seg * F, 256), 256, 0, s>>>(part, rowptr, n_seg, S, F, out);
+    else
+      segment_split_finish<GMP_REDUCE_MEAN><<<grid_for(n_seg * F, 256), 256, 0, s>>>(part, rowptr, n_seg, S, F, out);
+    return launch_status();
+  }
 #define GMP_SEG_LAUNCH(VEC, RED)                                                            \
   segment_reduce_wave<VEC, RED><<<(unsigned)ceil_div(n_seg, 4), 256, 0, s>>>(              \
       src, n_items, F, perm, rowptr, n_seg, out, argmax)
 #define GMP_SEG_DISPATCH(RED)                                                               \
   do {                                                                                      \
-    if (F >= 16 && F % 4 == 0 && aligned) GMP_SEG_LAUNCH(4, RED);                           \
-    else if (F >= 16 && F % 2 == 0 && reinterpret_cast<uintptr_t>(src) % 8 == 0)           \
-      GMP_SEG_LAUNCH(2, RED);                                                               \
-    else if (F >= 16) GMP_SEG_LAUNCH(1, RED);                                               \
-    else                                                                                    \
+    if (F < 4 && n_items < 64 * n_seg)                                                      \
       segment_reduce_thread<RED><<<grid_for(n_seg * F, 256), 256, 0, s>>>(                 \
           src, n_items, F, perm, rowptr, n_seg, out, argmax);                               \
+    else if (vec == 4) GMP_SEG_LAUNCH(4, RED);                                              \
+    else if (vec == 2) GMP_SEG_LAUNCH(2, RED);                                              \
+    else GMP_SEG_LAUNCH(1, RED);                                                            \
   } while (0)
   if (reduce == GMP_REDUCE_SUM) GMP_SEG_DISPATCH(GMP_REDUCE_SUM);
   else if (reduce == GMP_REDUCE_MEAN) GMP_SEG_DISPATCH(GMP_REDUCE_MEAN);

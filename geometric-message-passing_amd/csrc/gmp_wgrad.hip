@@ -1,0 +1,173 @@
+// Edge-reduction GEMM for weight gradients: C = A^T B (+ colsum(A)) with A (K, M), B (K, N)
+// row-major and K = number of edges (~1M), M = N = d.  This is the dW of a per-edge Linear
+// (egnn_layer.py:28-39 mlp_msg / mlp_pos: dW = sum_e dpre_e (x) x_e, db = sum_e dpre_e).
+//
+// Split-K over workgroups (each a contiguous edge range), f32 MFMA 16x16x4 with the edge index
+// as the MFMA k dimension, partial slabs in a workspace and an ordered second pass (bitwise
+// deterministic; no atomics).  HBM-bound: reads A and B once.
+#include "gmp_common.h"
+
+namespace gmp {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kT = 256;      // threads (4 waves)
+constexpr int kKT = 32;      // edges per LDS tile
+constexpr int kLD = 128 + 16;  // LDS row stride (floats): lanes 0-15 / 16-31 on disjoint banks
+
+template <int D>
+struct WCfg {
+  static constexpr int TW = D / 32;  // 16x16 tiles per wave per dim (wave owns a D/2 x D/2 block)
+};
+
+// One workgroup: edges [k0, k1) -> partial[blockIdx] = A^T B (D x D) and colsum(A) (D).
+template <int D>
+__global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restrict__ A,
+                                                          const float* __restrict__ B, int64_t K,
+                                                          int64_t k_per_block,
+                                                          float* __restrict__ partial) {
+  constexpr int TW = WCfg<D>::TW;
+  constexpr int LD = D + 16;
+  __shared__ __attribute__((aligned(16))) float sA[2][kKT * LD];
+  __shared__ __attribute__((aligned(16))) float sB[2][kKT * LD];
+  __shared__ float sColsum[kT / (D / 4)][D];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, kk = lane >> 4;
+  const int m0 = (w >> 1) * (D / 2), n0 = (w & 1) * (D / 2);
+  const int64_t k0 = (int64_t)blockIdx.x * k_per_block;
+  const int64_t k1 = (k0 + k_per_block < K) ? k0 + k_per_block : K;
+
+  f32x4 acc[TW][TW];
+#pragma unroll
+  for (int a = 0; a < TW; ++a)
+#pragma unroll
+    for (int b = 0; b < TW; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // loader mapping: thread -> (row r0 + j*RS, column group c4) ; fixed column => colsum in regs
+  constexpr int CG = D / 4;            // float4 column groups per row
+  constexpr int RS = kT / CG;          // rows loaded per pass
+  const int c4 = tid % CG, r0 = tid / CG;
+  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+
+  auto load_tile = [&](int buf, int64_t kb) {
+#pragma unroll
+    for (int j = 0; j < kKT / RS; ++j) {
+      const int r = r0 + j * RS;
+      const int64_t k = kb + r;
+      f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+      if (k < k1) {
+        a = *reinterpret_cast<const f32x4*>(A + k * D + 4 * c4);
+        b = *reinterpret_cast<const f32x4*>(B + k * D + 4 * c4);
+      }
+      csum += a;
+      *reinterpret_cast<f32x4*>(&sA[buf][r * LD + 4 * c4]) = a;
+      *reinterpret_cast<f32x4*>(&sB[buf][r * LD + 4 * c4]) = b;
+    }
+  };
+
+  int buf = 0;
+  if (k0 < k1) load_tile(0, k0);
+  __syncthreads();
+  for (int64_t kb = k0; kb < k1; kb += kKT) {
+    if (kb + kKT < k1) load_tile(buf ^ 1, kb + kKT);
+    const float* a_s = sA[buf];
+    const float* b_s = sB[buf];
+#pragma unroll
+    for (int s = 0; s < kKT / 4; ++s) {
+      const int e = 4 * s + kk;
+      float af[TW], bf[TW];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        af[t] = a_s[e * LD + m0 + 16 * t + li];
+        bf[t] = b_s[e * LD + n0 + 16 * t + li];
+      }
+#pragma unroll
+      for (int a = 0; a < TW; ++a)
+#pragma unroll
+        for (int b = 0; b < TW; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // C/D map of 16x16x4: col = lane & 15, row = 4*(lane >> 4) + r
+  float* out = partial + (int64_t)blockIdx.x * (D * D + D);
+#pragma unroll
+  for (int a = 0; a < TW; ++a)
+#pragma unroll
+    for (int b = 0; b < TW; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(m0 + 16 * a + 4 * kk + r) * D + n0 + 16 * b + li] = acc[a][b][r];
+  // colsum(A): threads sharing a column group add in row-group order (deterministic)
+  *reinterpret_cast<f32x4*>(&sColsum[r0][4 * c4]) = csum;
+  __syncthreads();
+  for (int c = tid; c < D; c += kT) {
+    float sacc = 0.f;
+    for (int r = 0; r < RS; ++r) sacc += sColsum[r][c];
+    out[D * D + c] = sacc;
+  }
+}
+
+// out[x] = sum_g partial[g][x] in g order
+__global__ void sum_partials_kernel(const float* __restrict__ partial, int64_t G, int64_t X,
+                                    float* __restrict__ C, float* __restrict__ colsum, int64_t DD) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < X;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t g = 0; g < G; ++g) s += partial[g * X + x];
+    if (x < DD) C[x] = s;
+    else if (colsum) colsum[x - DD] = s;
+  }
+}
+
+int64_t blocks_for(int64_t K) {
+  int64_t g = (int64_t)device_cu_count() * 2;  // two resident workgroups per CU
+  const int64_t min_per = 4 * kKT;
+  if (g * min_per > K) g = ceil_div(K, min_per);
+  return g < 1 ? 1 : g;
+}
+
+}  // namespace
+}  // namespace gmp
+
+using namespace gmp;
+
+extern "C" {
+
+size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d) {
+  return (size_t)blocks_for(K) * (size_t)(d * d + d) * sizeof(float);
+}
+
+int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
+                           float* colsum_A, void* workspace, size_t workspace_bytes,
+                           void* stream) {
+  if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
+  GMP_CHECK_ARG(K >= 0 && C);
+  hipStream_t s = as_stream(stream);
+  if (K == 0) {
+    int rc = hip_check(hipMemsetAsync(C, 0, d * d * sizeof(float), s));
+    if (!rc && colsum_A) rc = hip_check(hipMemsetAsync(colsum_A, 0, d * sizeof(float), s));
+    return rc;
+  }
+  GMP_CHECK_ARG(A && B && workspace);
+  GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0);
+  if (workspace_bytes < gmp_edge_outer_sum_workspace_size(K, d)) return GMP_ERR_WORKSPACE;
+  const int64_t G = blocks_for(K);
+  const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
+  const int64_t Gr = ceil_div(K, per);
+  float* part = reinterpret_cast<float*>(workspace);
+  if (d == 128) outer_sum_kernel<128><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part);
+  else if (d == 64) outer_sum_kernel<64><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part);
+  else outer_sum_kernel<32><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part);
+  int rc = launch_status();
+  if (rc) return rc;
+  const int64_t X = d * d + d;
+  sum_partials_kernel<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(part, Gr, X, C, colsum_A, d * d);
+  return launch_status();
+}
+
+}  // extern "C"

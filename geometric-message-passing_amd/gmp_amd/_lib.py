@@ -40,14 +40,17 @@ SIGNATURES = {
     "gmp_csr_build": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_size, c_vp]),
     "gmp_gather_rows_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "gmp_segment_reduce_workspace_size": (c_size, [c_i64, c_i64, c_i64, c_int]),
     "gmp_segment_reduce_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
-                                       c_vp]),
+                                       c_vp, c_size, c_vp]),
     "gmp_segment_reduce_bwd_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp,
                                            c_vp, c_vp]),
     "gmp_egnn_edge_fwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
                                       c_vp, c_vp]),
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
+    "gmp_edge_outer_sum_workspace_size": (c_size, [c_i64, c_i64]),
+    "gmp_edge_outer_sum_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

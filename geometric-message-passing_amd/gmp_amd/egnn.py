@@ -103,7 +103,7 @@ class EGNNModel(nn.Module):
                                       nn.Linear(emb_dim, out_dim))
 
     def forward(self, batch):
-        h = self.emb_in(batch.atoms)
+        h = ops.gather(self.emb_in.weight, batch.atoms)  # == emb_in(atoms); bwd = segmented sum
         pos = batch.pos
         for conv in self.convs:
             h_update, pos = conv(h, pos, batch.edge_index)

@@ -153,11 +153,30 @@ def segment_reduce(src2d, csr, reduce="sum", use_perm=True):
     argmax = None
     if reduce == "max":
         argmax = torch.empty((csr.n_seg, F), dtype=torch.int64, device=src2d.device)
+    red = _lib.REDUCE[reduce]
+    ws_bytes = lib.gmp_segment_reduce_workspace_size(src2d.shape[0], csr.n_seg, F, red)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=src2d.device) if ws_bytes else None
     check(lib.gmp_segment_reduce_f32(_p(src2d), src2d.shape[0], F,
                                      _p(csr.perm) if use_perm else None, _p(csr.rowptr),
-                                     csr.n_seg, _lib.REDUCE[reduce], _p(out), _p(argmax),
+                                     csr.n_seg, red, _p(out), _p(argmax), _p(ws), ws_bytes,
                                      _stream()), "gmp_segment_reduce_f32")
     return out, argmax
+
+
+def edge_outer_sum(A, B, with_colsum=True):
+    """(A^T B, colsum(A)) over the edge dimension (gmp_edge_outer_sum_f32), deterministic."""
+    lib = _lib.load()
+    A, B = _f32c(A), _f32c(B)
+    _need_cuda(A, B)
+    K, d = A.shape
+    C = torch.empty((d, d), dtype=torch.float32, device=A.device)
+    cs = torch.empty(d, dtype=torch.float32, device=A.device) if with_colsum else None
+    ws_bytes = lib.gmp_edge_outer_sum_workspace_size(K, d)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
+    with _timed("edge_outer_sum"):
+        check(lib.gmp_edge_outer_sum_f32(K, d, _p(A), _p(B), _p(C), _p(cs), _p(ws), ws_bytes,
+                                         _stream()), "gmp_edge_outer_sum_f32")
+    return C, cs
 
 
 def segment_reduce_bwd(grad_out, csr, reduce, argmax, n_items):
@@ -319,10 +338,8 @@ class EgnnEdgeFn(torch.autograd.Function):
         dAB = torch.cat([dA, dB], dim=1)
         dpos = dpos_recv - dpos_send
         # weight gradients: GEMMs over edges (library GEMM) + reductions
-        dW2 = dpre2.t().mm(y1)
-        dW3 = dpre3.t().mm(m)
-        db2 = dpre2.sum(0)
-        db3 = dpre3.sum(0)
+        dW2, db2 = edge_outer_sum(dpre2, y1)
+        dW3, db3 = edge_outer_sum(dpre3, m)
         db1 = dA.sum(0)
         v = partials.sum(0)
         dln1w, dln1b, dln2w, dln2b, dln3w, dln3b, dw4, dw1d = v[:8 * d].view(8, d).unbind(0)

@@ -72,11 +72,15 @@ int gmp_gather_rows_f32(const float* src, int64_t n_rows, int64_t F, const int64
  *   out[s, f] = reduce_{k in [rowptr[s], rowptr[s+1])} src[perm ? perm[k] : k, f]
  *   empty segments -> 0; mean divides by max(count, 1); max also writes argmax[s, f]
  *   (item index, n_items for empty segments; argmax may be NULL for sum/mean).
- * Summation order is the CSR order (deterministic).
+ * Summation order is fixed by the CSR (deterministic).  Long segments (average length >= 2048,
+ * e.g. global pools) are split over workgroups when a workspace of
+ * gmp_segment_reduce_workspace_size(...) bytes is given (NULL / too small = single-wave path).
  * ------------------------------------------------------------------------------------------ */
+size_t gmp_segment_reduce_workspace_size(int64_t n_items, int64_t n_seg, int64_t F, int reduce);
 int gmp_segment_reduce_f32(const float* src, int64_t n_items, int64_t F, const int64_t* perm,
                            const int64_t* rowptr, int64_t n_seg, int reduce, float* out,
-                           int64_t* argmax, void* stream);
+                           int64_t* argmax, void* workspace, size_t workspace_bytes,
+                           void* stream);
 
 /* Backward of gmp_segment_reduce_f32 w.r.t. src (torch_scatter autograd):
  *   sum : grad_src[e] = grad_out[index[e]]
@@ -143,6 +147,19 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
                           const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
                           float* gdiff, float* y1, float* m, float* dpre2, float* dpre3,
                           float* vec_partials, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Edge-reduction GEMM for per-edge Linear weight gradients (egnn_layer.py:28-39 mlp_msg /
+ * mlp_pos backward; replaces torch's dW = dpre^T x over E rows):
+ *   C (d x d) = A^T B with A (K, d), B (K, d) row-major fp32, K = edges;
+ *   colsum_A (d) = sum_k A[k, :] (the bias gradient; may be NULL).
+ * Split-K over workgroups with f32 MFMA, partial slabs in `workspace` and an ordered second
+ * pass: bitwise deterministic.  d in {32, 64, 128}.
+ * ------------------------------------------------------------------------------------------ */
+size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d);
+int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
+                           float* colsum_A, void* workspace, size_t workspace_bytes,
+                           void* stream);
 
 #ifdef __cplusplus
 }
