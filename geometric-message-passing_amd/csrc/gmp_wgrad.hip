@@ -51,27 +51,39 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
   const int c4 = tid % CG, r0 = tid / CG;
   f32x4 csum = {0.f, 0.f, 0.f, 0.f};
 
-  auto load_tile = [&](int buf, int64_t kb) {
+  constexpr int NL = kKT / RS;  // float4 loads per thread per tile, per operand
+  f32x4 ra[NL], rb[NL];
+  auto fetch = [&](int64_t kb) {  // global -> registers
 #pragma unroll
-    for (int j = 0; j < kKT / RS; ++j) {
-      const int r = r0 + j * RS;
-      const int64_t k = kb + r;
-      f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NL; ++j) {
+      const int64_t k = kb + r0 + j * RS;
+      ra[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      rb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < k1) {
-        a = *reinterpret_cast<const f32x4*>(A + k * D + 4 * c4);
-        b = *reinterpret_cast<const f32x4*>(B + k * D + 4 * c4);
+        ra[j] = *reinterpret_cast<const f32x4*>(A + k * D + 4 * c4);
+        rb[j] = *reinterpret_cast<const f32x4*>(B + k * D + 4 * c4);
       }
-      csum += a;
-      *reinterpret_cast<f32x4*>(&sA[buf][r * LD + 4 * c4]) = a;
-      *reinterpret_cast<f32x4*>(&sB[buf][r * LD + 4 * c4]) = b;
+    }
+  };
+  auto stash = [&](int buf) {  // registers -> LDS (+ colsum of A)
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int r = r0 + j * RS;
+      csum += ra[j];
+      *reinterpret_cast<f32x4*>(&sA[buf][r * LD + 4 * c4]) = ra[j];
+      *reinterpret_cast<f32x4*>(&sB[buf][r * LD + 4 * c4]) = rb[j];
     }
   };
 
   int buf = 0;
-  if (k0 < k1) load_tile(0, k0);
+  if (k0 < k1) {
+    fetch(k0);
+    stash(0);
+  }
   __syncthreads();
   for (int64_t kb = k0; kb < k1; kb += kKT) {
-    if (kb + kKT < k1) load_tile(buf ^ 1, kb + kKT);
+    const bool more = kb + kKT < k1;
+    if (more) fetch(kb + kKT);  // in flight while this tile is computed
     const float* a_s = sA[buf];
     const float* b_s = sB[buf];
 #pragma unroll
@@ -89,6 +101,7 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
         for (int b = 0; b < TW; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf[b], acc[a][b], 0, 0, 0);
     }
+    if (more) stash(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
@@ -112,16 +125,31 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
   }
 }
 
-// out[x] = sum_g partial[g][x] in g order
-__global__ void sum_partials_kernel(const float* __restrict__ partial, int64_t G, int64_t X,
-                                    float* __restrict__ C, float* __restrict__ colsum, int64_t DD) {
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < X;
-       x += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int64_t g = 0; g < G; ++g) s += partial[g * X + x];
-    if (x < DD) C[x] = s;
-    else if (colsum) colsum[x - DD] = s;
-  }
+// Ordered two-level reduction of the G partial slabs: level 1 sums chunks of kGC slabs
+// (grid = X/256 x ceil(G/kGC)), level 2 sums the level-1 results in chunk order.
+constexpr int kGC = 16;
+__global__ void sum_partials_l1(const float* __restrict__ partial, int64_t G, int64_t X,
+                                float* __restrict__ l1) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  if (x >= X) return;
+  const int64_t g0 = c * kGC, g1 = (g0 + kGC < G) ? g0 + kGC : G;
+  float v[kGC];
+#pragma unroll
+  for (int u = 0; u < kGC; ++u) v[u] = (g0 + u < g1) ? partial[(g0 + u) * X + x] : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < kGC; ++u) s += v[u];
+  l1[c * X + x] = s;
+}
+__global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t X,
+                                float* __restrict__ out, float* __restrict__ colsum, int64_t DD) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= X) return;
+  float s = 0.f;
+  for (int64_t c = 0; c < C; ++c) s += l1[c * X + x];
+  if (x < DD) out[x] = s;
+  else if (colsum) colsum[x - DD] = s;
 }
 
 int64_t blocks_for(int64_t K) {
@@ -139,7 +167,8 @@ using namespace gmp;
 extern "C" {
 
 size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d) {
-  return (size_t)blocks_for(K) * (size_t)(d * d + d) * sizeof(float);
+  const int64_t G = blocks_for(K);
+  return (size_t)(G + ceil_div(G, kGC)) * (size_t)(d * d + d) * sizeof(float);
 }
 
 int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
@@ -166,7 +195,12 @@ int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B,
   int rc = launch_status();
   if (rc) return rc;
   const int64_t X = d * d + d;
-  sum_partials_kernel<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(part, Gr, X, C, colsum_A, d * d);
+  const int64_t NC = ceil_div(Gr, kGC);
+  float* l1 = part + Gr * X;
+  sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
+  rc = launch_status();
+  if (rc) return rc;
+  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, d * d);
   return launch_status();
 }
 

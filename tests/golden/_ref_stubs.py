@@ -223,3 +223,120 @@ def load_reference(ref_root):
         spec.loader.exec_module(mod)
         out[name] = mod
     return out
+
+
+# ----------------------------------------------------------------------------- e3nn-lite
+def install_e3nn_lite():
+    """Replace the def-time e3nn.o3 placeholders with a faithful-enough Irreps/Irrep algebra
+    and wigner_3j (restated in oracle/o3.py) so that the reference's own
+    models/mace_modules/cg.py and symmetric_contraction.py can run.  Parity of wigner_3j itself
+    is unpinned (see oracle/o3.py); everything cg.py / symmetric_contraction.py do on top of it
+    is the reference's code."""
+    import os
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    if root not in _sys.path:
+        _sys.path.insert(0, root)
+    from oracle import o3 as oo3
+
+    class Irrep(tuple):
+        def __new__(cls, l, p=None):
+            if isinstance(l, Irrep):
+                return l
+            if isinstance(l, str):
+                return super().__new__(cls, (int(l[:-1]), {"e": 1, "o": -1}[l[-1]]))
+            if isinstance(l, tuple):
+                l, p = l
+            return super().__new__(cls, (int(l), int(p)))
+
+        l = property(lambda self: self[0])
+        p = property(lambda self: self[1])
+        dim = property(lambda self: 2 * self[0] + 1)
+
+        def is_scalar(self):
+            return self == (0, 1)
+
+        def __mul__(self, other):
+            other = Irrep(other)
+            for l in range(abs(self.l - other.l), self.l + other.l + 1):
+                yield Irrep(l, self.p * other.p)
+
+        def __str__(self):
+            return f"{self.l}{'e' if self.p == 1 else 'o'}"
+
+        __repr__ = __str__
+
+    class _MulIr(tuple):
+        def __new__(cls, mul, ir):
+            return super().__new__(cls, (int(mul), Irrep(ir)))
+
+        mul = property(lambda self: self[0])
+        ir = property(lambda self: self[1])
+        dim = property(lambda self: self[0] * self[1].dim)
+
+        def __str__(self):
+            return f"{self.mul}x{self.ir}"
+
+    class Irreps(tuple):
+        def __new__(cls, spec=None):
+            if isinstance(spec, Irreps):
+                return spec
+            items = []
+            if spec is None:
+                pass
+            elif isinstance(spec, Irrep):
+                items = [_MulIr(1, spec)]
+            elif isinstance(spec, str):
+                for m, ir in oo3.Irreps(spec):
+                    items.append(_MulIr(m, ir))
+            else:
+                for x in spec:
+                    if isinstance(x, Irrep) or isinstance(x, str):
+                        items.append(_MulIr(1, Irrep(x)))
+                    else:
+                        m, ir = x
+                        items.append(_MulIr(m, ir))
+            return super().__new__(cls, items)
+
+        dim = property(lambda self: sum(mi.dim for mi in self))
+
+        def count(self, ir):
+            ir = Irrep(ir)
+            return sum(m for m, i in self if i == ir)
+
+        def __contains__(self, ir):
+            ir = Irrep(ir)
+            return any(i == ir for _, i in self)
+
+        def __str__(self):
+            return "+".join(str(mi) for mi in self)
+
+    o3 = sys.modules["e3nn.o3"]
+    o3.Irrep = Irrep
+    o3.Irreps = Irreps
+    o3.wigner_3j = lambda l1, l2, l3, dtype=None, device=None: oo3.wigner_3j(
+        l1, l2, l3, dtype or torch.get_default_dtype())
+
+
+def load_mace_contraction(ref_root):
+    """Load the reference's cg.py and symmetric_contraction.py on top of e3nn-lite."""
+    import importlib.util
+    import os
+
+    install()
+    install_e3nn_lite()
+    for name in ("models", "models.mace_modules"):
+        if name not in sys.modules:
+            m = types.ModuleType(name)
+            m.__path__ = [os.path.join(ref_root, name.replace(".", "/"))]
+            sys.modules[name] = m
+    out = {}
+    for name, rel in [("models.mace_modules.cg", "models/mace_modules/cg.py"),
+                      ("models.mace_modules.symmetric_contraction",
+                       "models/mace_modules/symmetric_contraction.py")]:
+        spec = importlib.util.spec_from_file_location(name, os.path.join(ref_root, rel))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+        out[name] = mod
+    return out

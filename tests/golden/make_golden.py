@@ -209,6 +209,26 @@ def main():
     torch.save(d, os.path.join(HERE, "gvp_model.pt"))
     out_files.append("gvp_model.pt")
 
+    # ---------------------------------------------------------------- MACE symmetric contraction
+    # (reference cg.py + symmetric_contraction.py on e3nn-lite; wigner_3j restated)
+    mm = _ref_stubs.load_mace_contraction(REF)
+    o3l = sys.modules["e3nn.o3"]
+    torch.manual_seed(16)
+    C = 16
+    irreps = o3l.Irreps(f"{C}x0e+{C}x1o+{C}x2e")
+    SC = mm["models.mace_modules.symmetric_contraction"].SymmetricContraction(
+        irreps_in=irreps, irreps_out=irreps, correlation=3, element_dependent=False,
+        num_elements=1)
+    x = torch.randn(37, C, 9, requires_grad=True)
+    y = SC(x, None)
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    d = {"x": x.detach(), "out": y.detach(), "g_out": gy, "grad_x": x.grad}
+    d.update({f"param.{k}": v.detach().clone() for k, v in SC.state_dict().items()})
+    d.update(grads_dict(SC))
+    torch.save(d, os.path.join(HERE, "mace_symmetric_contraction.pt"))
+    out_files.append("mace_symmetric_contraction.pt")
+
     for f in out_files:
         print(f, os.path.getsize(os.path.join(HERE, f)))
 

@@ -1,0 +1,157 @@
+"""Known-answer and equivariance tests for the e3nn restatement (oracle/o3.py) and the MACE /
+TFN oracle (oracle/mace.py).  e3nn itself is absent, so these pin conventions by closed forms
+(SURVEY.md §8(c) KATs) and by the reference's own cg.py / symmetric_contraction.py run on the
+restated wigner_3j (tests/golden/mace_symmetric_contraction.pt).  CPU only."""
+import math
+
+import pytest
+import torch
+
+from oracle import o3
+from oracle import mace as om
+
+
+def _D(l, a, b, c):
+    t = lambda v: torch.tensor(v, dtype=torch.float64)  # noqa: E731
+    return o3.wigner_D(l, t(a), t(b), t(c))
+
+
+ANG = (0.3, 1.1, -0.7)
+
+
+def test_sh_known_values():
+    s3, s5, s15 = math.sqrt(3), math.sqrt(5), math.sqrt(15)
+    e = torch.eye(3, dtype=torch.float64)
+    Y = o3.spherical_harmonics_l2(e)
+    # x-hat: l1 = sqrt3 (1,0,0); l2 = sqrt5 (0, 0, -1/2, 0, -sqrt3/2)
+    torch.testing.assert_close(Y[0], torch.tensor([1, s3, 0, 0, 0, 0, -s5 / 2, 0, -s15 / 2],
+                                                  dtype=torch.float64))
+    # y-hat (polar axis): l2 = sqrt5 (0, 0, 1, 0, 0)
+    torch.testing.assert_close(Y[1], torch.tensor([1, 0, s3, 0, 0, 0, s5, 0, 0],
+                                                  dtype=torch.float64))
+    torch.testing.assert_close(Y[2], torch.tensor([1, 0, 0, s3, 0, 0, -s5 / 2, 0, s15 / 2],
+                                                  dtype=torch.float64))
+    v = torch.randn(100, 3, dtype=torch.float64)
+    Yv = o3.spherical_harmonics_l2(v)
+    torch.testing.assert_close(Yv[:, 1:4].pow(2).sum(-1), torch.full((100,), 3.0, dtype=torch.float64))
+    torch.testing.assert_close(Yv[:, 4:9].pow(2).sum(-1), torch.full((100,), 5.0, dtype=torch.float64))
+    # normalize=True: scale invariant
+    torch.testing.assert_close(o3.spherical_harmonics_l2(3.7 * v), Yv)
+
+
+def test_cg_known_values():
+    for l in range(3):
+        C = o3.wigner_3j(0, l, l)[0]
+        torch.testing.assert_close(C, torch.eye(2 * l + 1, dtype=torch.float64) / math.sqrt(2 * l + 1))
+        C = o3.wigner_3j(l, l, 0)[:, :, 0]
+        torch.testing.assert_close(C, torch.eye(2 * l + 1, dtype=torch.float64) / math.sqrt(2 * l + 1))
+    eps = torch.zeros(3, 3, 3, dtype=torch.float64)
+    for i, j, k in [(0, 1, 2), (1, 2, 0), (2, 0, 1)]:
+        eps[i, j, k], eps[j, i, k] = 1.0, -1.0
+    torch.testing.assert_close(o3.wigner_3j(1, 1, 1), eps / math.sqrt(6))
+    for l1 in range(3):
+        for l2 in range(3):
+            for l3 in range(abs(l1 - l2), min(l1 + l2, 4) + 1):
+                assert abs(o3.wigner_3j(l1, l2, l3).norm().item() - 1.0) < 1e-12
+
+
+def test_sh_and_cg_equivariance():
+    D = [_D(l, *ANG) for l in range(5)]
+    R = D[1]
+    x = torch.randn(20, 3, dtype=torch.float64)
+    Y, YR = o3.spherical_harmonics_l2(x), o3.spherical_harmonics_l2(x @ R.T)
+    torch.testing.assert_close(YR, Y @ torch.block_diag(*D[:3]).T)
+    assert torch.allclose(R @ R.T, torch.eye(3, dtype=torch.float64)) and torch.det(R) > 0
+    for l1 in range(3):
+        for l2 in range(3):
+            for l3 in range(abs(l1 - l2), l1 + l2 + 1):
+                C = o3.wigner_3j(l1, l2, l3)
+                C2 = torch.einsum("il,jm,kn,lmn->ijk", D[l1], D[l2], D[l3], C)
+                torch.testing.assert_close(C2, C, atol=1e-12, rtol=0)
+
+
+def _rot_irreps(irreps, R_angles):
+    return torch.block_diag(*[_D(l, *R_angles) for m, (l, p) in o3.Irreps(irreps)
+                              for _ in range(m)])
+
+
+def test_fctp_equivariance_and_paths():
+    torch.manual_seed(0)
+    irr = o3.Irreps("4x0e+4x1o+4x2e")
+    sh = o3.spherical_harmonics_irreps(2)
+    tp = o3.FullyConnectedTensorProduct(irr, sh, irr)
+    assert len(tp.instructions) == 11 and tp.weight_numel == 11 * 16
+    x = torch.randn(5, irr.dim, dtype=torch.float64)
+    v = torch.randn(5, 3, dtype=torch.float64)
+    w = torch.randn(5, tp.weight_numel, dtype=torch.float64)
+    Dx = _rot_irreps(irr, ANG)
+    R = _D(1, *ANG)
+    out = tp(x, o3.spherical_harmonics_l2(v), w)
+    outR = tp(x @ Dx.T, o3.spherical_harmonics_l2(v @ R.T), w)
+    torch.testing.assert_close(outR, out @ Dx.T, atol=1e-10, rtol=1e-10)
+    # path normalisation alpha = (2 lo + 1) / (n_paths_to_o * mul1 * mul2)
+    pw = {(i["i1"], i["i2"], i["io"]): i["path_weight"] for i in tp.instructions}
+    assert abs(pw[(0, 0, 0)] - math.sqrt(1 / 12)) < 1e-12
+    assert abs(pw[(1, 1, 2)] - math.sqrt(5 / 16)) < 1e-12
+
+
+def test_symmetric_contraction_matches_reference_code(golden):
+    d = golden("mace_symmetric_contraction.pt")
+    sc = om.SymmetricContraction("16x0e+16x1o+16x2e", "16x0e+16x1o+16x2e", 3)
+    sd = {k[6:]: v for k, v in d.items() if k.startswith("param.")}
+    sc.load_state_dict(sd, strict=True)  # same keys, U buffers included
+    for k, v in sc.state_dict().items():
+        if "U_matrix" in k:
+            torch.testing.assert_close(v, sd[k], atol=1e-7, rtol=0)
+    x = d["x"].clone().requires_grad_(True)
+    y = sc(x)
+    torch.testing.assert_close(y, d["out"], atol=1e-5, rtol=1e-5)
+    (y * d["g_out"]).sum().backward()
+    torch.testing.assert_close(x.grad, d["grad_x"], atol=1e-5, rtol=1e-5)
+    for k, p in sc.named_parameters():
+        torch.testing.assert_close(p.grad, d[f"grad.{k}"], atol=1e-4, rtol=1e-5)
+
+
+def test_symmetric_contraction_equivariance():
+    torch.manual_seed(1)
+    sc = om.SymmetricContraction("8x0e+8x1o+8x2e", "8x0e+8x1o+8x2e", 3).double()
+    x = torch.randn(6, 8, 9, dtype=torch.float64)
+    D9 = torch.block_diag(*[_D(l, *ANG) for l in range(3)])
+    out = sc(x)
+    outR = sc(x @ D9.T)
+    Dout = _rot_irreps("8x0e+8x1o+8x2e", ANG)
+    # U buffers are stored in the default dtype (fp32, as in the reference): fp32-level error
+    torch.testing.assert_close(outR, out @ Dout.T, atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("model_cls,kw", [
+    (om.MACEModel, dict(num_layers=2, emb_dim=8, correlation=3)),
+    (om.TFNModel, dict(num_layers=2, emb_dim=8)),
+])
+def test_models_rotation_invariance(model_cls, kw):
+    from gmp_amd.graph import radius_graph
+    torch.manual_seed(2)
+    g = radius_graph(num_nodes=40, target_edges=300, r=2.5, seed=5, tol=0.3)
+    model = model_cls(**kw).double()
+    if hasattr(model, "convs"):
+        model.train()
+    R = _D(1, *ANG)
+    from gmp_amd.graph import Batch
+    b1 = Batch(g.atoms, g.pos.double(), g.edge_index)
+    b2 = Batch(g.atoms, g.pos.double() @ R.T + 1.5, g.edge_index)
+    torch.testing.assert_close(model(b1), model(b2), atol=1e-8, rtol=1e-8)
+
+
+def test_gate_constants_and_batchnorm():
+    c_silu, c_sig = o3.normalize2mom_const("silu"), o3.normalize2mom_const("sigmoid")
+    assert 1.6 < c_silu < 1.8 and 1.7 < c_sig < 1.9
+    bn = o3.BatchNorm("3x0e+2x1o")
+    x = torch.randn(50, 9) * 3 + 1
+    y = bn(x)
+    assert torch.allclose(y[:, :3].mean(0), torch.zeros(3), atol=1e-5)
+    v = y[:, 3:].reshape(50, 2, 3).pow(2).mean((0, 2))
+    assert torch.allclose(v, torch.ones(2), atol=1e-3)
+    s, g, gated = o3.irreps2gate(o3.Irreps("64x0e+64x1o+64x2e"))
+    assert str(s) == "64x0e" and str(g) == "128x0e" and str(gated) == "64x1o+64x2e"
+    gate = o3.Gate(s, g, gated)
+    assert str(gate.irreps_in) == "64x0e+128x0e+64x1o+64x2e"
