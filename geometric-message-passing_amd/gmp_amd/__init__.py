@@ -9,7 +9,12 @@ from .scatter import (scatter, scatter_sum, scatter_add, scatter_mean, scatter_m
 from .message_passing import MessagePassing  # noqa: F401
 from .egnn import EGNNLayer, EGNNModel  # noqa: F401
 from .graph import Batch, collate, radius_graph, create_kchains  # noqa: F401
+from .equivariant import (TensorProductConvLayer, MACEModel, TFNModel,  # noqa: F401
+                          RadialEmbeddingBlock, EquivariantProductBasisBlock,
+                          SymmetricContraction, first_node_pooling)
 
 __all__ = ["scatter", "scatter_sum", "scatter_add", "scatter_mean", "scatter_max",
            "global_add_pool", "global_mean_pool", "MessagePassing", "EGNNLayer", "EGNNModel",
-           "Batch", "collate", "radius_graph", "create_kchains"]
+           "Batch", "collate", "radius_graph", "create_kchains", "TensorProductConvLayer",
+           "MACEModel", "TFNModel", "RadialEmbeddingBlock", "EquivariantProductBasisBlock",
+           "SymmetricContraction", "first_node_pooling"]

@@ -31,6 +31,20 @@ class GmpEgnnParams(ctypes.Structure):
         "w4", "b4")]
 
 
+class TpPath(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("l1", "l2", "lo", "mul1", "mul_out", "x_off", "y_off", "io",
+                                       "out_off", "z_off", "cg_off", "pad")] + [
+        ("w_off", ctypes.c_longlong), ("alpha", c_f32), ("pad2", c_f32)]
+
+
+class TpDesc(ctypes.Structure):
+    _fields_ = [("n_paths", c_int), ("in_dim", c_int), ("out_dim", c_int), ("sh_dim", c_int),
+                ("weight_numel", ctypes.c_longlong), ("z_size", c_int), ("n_blocks", c_int),
+                ("blk_off", c_int * 4), ("blk_mul", c_int * 4), ("blk_l", c_int * 4)]
+
+
+assert ctypes.sizeof(TpPath) == 64 and ctypes.sizeof(TpDesc) == 80
+
 # name -> (restype, argtypes); must mirror include/gmp.h exactly
 SIGNATURES = {
     "gmp_abi_version": (c_int, []),
@@ -51,6 +65,14 @@ SIGNATURES = {
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
     "gmp_edge_outer_sum_workspace_size": (c_size, [c_i64, c_i64]),
     "gmp_edge_outer_sum_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "gmp_edge_featurize_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32, c_vp,
+                                       c_vp, c_vp, c_vp, c_vp]),
+    "gmp_edge_featurize_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32,
+                                           c_vp, c_vp, c_vp, c_vp]),
+    "gmp_tp_conv_fwd_f32": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "gmp_tp_conv_bwd_f32": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

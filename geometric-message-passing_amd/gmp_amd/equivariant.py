@@ -1,0 +1,638 @@
+"""TFN / MACE layers and models on the MI355X kernels — drop-ins for
+models/layers/tfn_layer.py:8-93 (TensorProductConvLayer), models/tfn.py:13-190 (TFNModel,
+first_node_pooling), models/mace.py:9-190 (MACEModel), models/mace_modules/blocks.py:84-135
+(RadialEmbeddingBlock, EquivariantProductBasisBlock), symmetric_contraction.py:20-188,
+irreps_tools.py:63-97 and the e3nn modules they use (SphericalHarmonics, o3.Linear,
+nn.BatchNorm, nn.Gate).
+
+Hot path on HIP: per-edge featurisation (K1: vectors, lengths, SH l<=2, Bessel x cutoff) and
+the tensor-product convolution (K7: radial-MLP weights x CG contraction x receiver sum), plus the
+gathers / segmented sums of the generic ops.  The radial MLP's wide second Linear
+(256 -> weight_numel, e.g. 180,224 for MACE-128) is evaluated chunk by chunk with the library
+GEMM so that the per-edge weights (721 KB per edge for MACE-128, 721 GB at 1M edges) never exist
+all at once; the HIP TP kernels stream each chunk once.  Node-level pieces (BatchNorm, Gate,
+o3.Linear, symmetric contraction) are PyTorch ops on N-row tensors.
+"""
+import ctypes
+import math
+import os
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from . import _lib, ops
+from . import o3
+from .ops import _p, _stream, check, _f32c, _need_cuda, _timed
+from .scatter import global_add_pool, global_mean_pool
+
+CHUNK_BYTES = int(os.environ.get("GMP_TP_CHUNK_BYTES", str(6 << 30)))
+
+
+# ===================================================================================== radial
+class BesselBasis(nn.Module):
+    """radial.py:12-52 (same buffers)."""
+
+    def __init__(self, r_max, num_basis=8, trainable=False):
+        super().__init__()
+        w = math.pi / r_max * torch.linspace(1.0, num_basis, num_basis)
+        if trainable:
+            self.bessel_weights = nn.Parameter(w)
+        else:
+            self.register_buffer("bessel_weights", w)
+        self.register_buffer("r_max", torch.tensor(float(r_max)))
+        self.register_buffer("prefactor", torch.tensor(math.sqrt(2.0 / r_max)))
+
+    def forward(self, x):
+        return self.prefactor * (torch.sin(self.bessel_weights * x) / x)
+
+
+class PolynomialCutoff(nn.Module):
+    """radial.py:55-81 (same buffers)."""
+
+    def __init__(self, r_max, p=6):
+        super().__init__()
+        self.register_buffer("p", torch.tensor(float(p)))
+        self.register_buffer("r_max", torch.tensor(float(r_max)))
+
+    def forward(self, x):
+        p, u = self.p, x / self.r_max
+        env = (1.0 - ((p + 1.0) * (p + 2.0) / 2.0) * torch.pow(u, p)
+               + p * (p + 2.0) * torch.pow(u, p + 1) - (p * (p + 1.0) / 2) * torch.pow(u, p + 2))
+        return env * (x < self.r_max)
+
+
+class RadialEmbeddingBlock(nn.Module):
+    """blocks.py:84-96."""
+
+    def __init__(self, r_max, num_bessel, num_polynomial_cutoff):
+        super().__init__()
+        self.bessel_fn = BesselBasis(r_max=r_max, num_basis=num_bessel)
+        self.cutoff_fn = PolynomialCutoff(r_max=r_max, p=num_polynomial_cutoff)
+        self.out_dim = num_bessel
+        # host copies of the constants for the fused featurisation kernel (no device sync)
+        self._host = (self.bessel_fn.bessel_weights.detach().cpu().numpy().astype("float32"),
+                      float(self.bessel_fn.prefactor), float(r_max), float(num_polynomial_cutoff))
+
+    def forward(self, edge_lengths):
+        return self.bessel_fn(edge_lengths) * self.cutoff_fn(edge_lengths)
+
+
+class EdgeFeaturizeFn(torch.autograd.Function):
+    """K1: (pos, edge_index) -> (edge_sh (E,9), edge_feats (E,nb)) in one pass over the edges."""
+
+    @staticmethod
+    def forward(ctx, pos, edge_index, host_consts, graph):
+        lib = _lib.load()
+        w, pref, r_max, p = host_consts
+        pos = _f32c(pos)
+        ei = edge_index.contiguous()
+        _need_cuda(pos, ei)
+        E = ei.shape[1]
+        nb = len(w)
+        sh = torch.empty((E, 9), dtype=torch.float32, device=pos.device)
+        rad = torch.empty((E, nb), dtype=torch.float32, device=pos.device)
+        wbuf = (ctypes.c_float * nb)(*w.tolist())
+        with _timed("edge_featurize"):
+            check(lib.gmp_edge_featurize_f32(_p(pos), _p(ei), E, nb, wbuf, pref, r_max, p, None,
+                                             None, _p(sh), _p(rad), _stream()),
+                  "gmp_edge_featurize_f32")
+        ctx.save_for_backward(pos, ei)
+        ctx.host, ctx.graph = host_consts, graph
+        return sh, rad
+
+    @staticmethod
+    def backward(ctx, g_sh, g_rad):
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        lib = _lib.load()
+        pos, ei = ctx.saved_tensors
+        w, pref, r_max, p = ctx.host
+        E, N = ei.shape[1], pos.shape[0]
+        g_vec = torch.empty((E, 3), dtype=torch.float32, device=pos.device)
+        wbuf = (ctypes.c_float * len(w))(*w.tolist())
+        check(lib.gmp_edge_featurize_bwd_f32(
+            _p(pos), _p(ei), E, len(w), wbuf, pref, r_max, p,
+            _p(_f32c(g_sh)) if g_sh is not None else None,
+            _p(_f32c(g_rad)) if g_rad is not None else None, _p(g_vec), _stream()),
+            "gmp_edge_featurize_bwd_f32")
+        g = ctx.graph  # vectors = pos[ei0] - pos[ei1]: + into receivers, - into senders
+        plus, _ = ops.segment_reduce(g_vec, g.recv_csr, "sum")
+        minus, _ = ops.segment_reduce(ops.gather_rows(g_vec, g.perm), g.src_csr, "sum")
+        return plus - minus, None, None, None
+
+
+def spherical_harmonics_l2(vec, normalize=True):
+    """e3nn SphericalHarmonics(lmax=2, normalize, 'component') on arbitrary vectors (GPU ops)."""
+    if normalize:
+        vec = F.normalize(vec, dim=-1)
+    x, y, z = vec[..., 0], vec[..., 1], vec[..., 2]
+    s3, s5, s15 = math.sqrt(3.0), math.sqrt(5.0), math.sqrt(15.0)
+    return torch.stack([torch.ones_like(x), s3 * x, s3 * y, s3 * z, s15 * x * z, s15 * x * y,
+                        s5 * (y * y - 0.5 * (x * x + z * z)), s15 * y * z,
+                        s15 / 2.0 * (z * z - x * x)], dim=-1)
+
+
+# ===================================================================================== e3nn-like
+class Linear(nn.Module):
+    """e3nn o3.Linear(irreps_in, irreps_out) with internal shared weights, no biases
+    (blocks.py:121-124): out_o[w, m] = sum_{i->o} sum_u W[u, w] x_i[u, m] / sqrt(fan_in_o)."""
+
+    def __init__(self, irreps_in, irreps_out):
+        super().__init__()
+        self.irreps_in, self.irreps_out = o3.parse_irreps(irreps_in), o3.parse_irreps(irreps_out)
+        self.instructions = [(i, j) for i, (_, a) in enumerate(self.irreps_in)
+                             for j, (_, b) in enumerate(self.irreps_out) if a == b]
+        n = sum(self.irreps_in[i][0] * self.irreps_out[j][0] for i, j in self.instructions)
+        self.weight = nn.Parameter(torch.randn(n))
+
+    def forward(self, x):
+        B = x.shape[0]
+        oi, oo = o3.irreps_offsets(self.irreps_in), o3.irreps_offsets(self.irreps_out)
+        outs = [None] * len(self.irreps_out)
+        off = 0
+        for i, j in self.instructions:
+            mi, (l, _) = self.irreps_in[i]
+            mo = self.irreps_out[j][0]
+            fan = sum(self.irreps_in[a][0] for a, b in self.instructions if b == j)
+            W = self.weight[off:off + mi * mo].view(mi, mo)
+            off += mi * mo
+            d = 2 * l + 1
+            xi = x[:, oi[i]:oi[i] + mi * d].reshape(B, mi, d)
+            r = torch.matmul(W.t() / math.sqrt(fan), xi).reshape(B, mo * d)
+            outs[j] = r if outs[j] is None else outs[j] + r
+        for j, (mo, (l, _)) in enumerate(self.irreps_out):
+            if outs[j] is None:
+                outs[j] = x.new_zeros(B, mo * (2 * l + 1))
+        return torch.cat(outs, dim=1)
+
+
+class BatchNorm(nn.Module):
+    """e3nn nn.BatchNorm(irreps) (eps 1e-5, momentum 0.1, affine, reduce mean, component)."""
+
+    def __init__(self, irreps, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.irreps = o3.parse_irreps(irreps)
+        self.eps, self.momentum = eps, momentum
+        ns = sum(m for m, ir in self.irreps if ir == (0, 1))
+        nf = sum(m for m, _ in self.irreps)
+        self.register_buffer("running_mean", torch.zeros(ns))
+        self.register_buffer("running_var", torch.ones(nf))
+        self.weight = nn.Parameter(torch.ones(nf))
+        self.bias = nn.Parameter(torch.zeros(ns))
+
+    def forward(self, x):
+        B = x.shape[0]
+        fields, new_means, new_vars = [], [], []
+        ix = irm = irv = iw = ib = 0
+        for mul, (l, p) in self.irreps:
+            d = 2 * l + 1
+            f = x[:, ix:ix + mul * d].reshape(B, mul, d)
+            ix += mul * d
+            scalar = (l == 0 and p == 1)
+            if scalar:
+                if self.training:
+                    mean = f.mean(dim=(0, 2))
+                    new_means.append((1 - self.momentum) * self.running_mean[irm:irm + mul]
+                                     + self.momentum * mean.detach())
+                else:
+                    mean = self.running_mean[irm:irm + mul]
+                irm += mul
+                f = f - mean.view(1, mul, 1)
+            if self.training:
+                norm = f.pow(2).mean(2).mean(0)
+                new_vars.append((1 - self.momentum) * self.running_var[irv:irv + mul]
+                                + self.momentum * norm.detach())
+            else:
+                norm = self.running_var[irv:irv + mul]
+            irv += mul
+            scale = (norm + self.eps).pow(-0.5) * self.weight[iw:iw + mul]
+            iw += mul
+            f = f * scale.view(1, mul, 1)
+            if scalar:
+                f = f + self.bias[ib:ib + mul].view(1, mul, 1)
+                ib += mul
+            fields.append(f.reshape(B, mul * d))
+        if self.training:
+            with torch.no_grad():
+                if new_means:
+                    self.running_mean.copy_(torch.cat(new_means))
+                self.running_var.copy_(torch.cat(new_vars))
+        return torch.cat(fields, dim=1)
+
+
+class Gate(nn.Module):
+    """e3nn nn.Gate(scalars, [silu], gates, [sigmoid], gated) (tfn_layer.py:45-63)."""
+
+    def __init__(self, irreps_scalars, irreps_gates, irreps_gated):
+        super().__init__()
+        self.irreps_scalars, self.irreps_gates = irreps_scalars, irreps_gates
+        self.irreps_gated = irreps_gated
+        self.irreps_in = tuple(irreps_scalars) + tuple(irreps_gates) + tuple(irreps_gated)
+        self.irreps_out = tuple(irreps_scalars) + tuple(irreps_gated)
+        self.c_act, self.c_gate = o3.normalize2mom("silu"), o3.normalize2mom("sigmoid")
+
+    def forward(self, x):
+        ns, ng = o3.irreps_dim(self.irreps_scalars), o3.irreps_dim(self.irreps_gates)
+        B = x.shape[0]
+        outs = [self.c_act * F.silu(x[:, :ns])]
+        g = self.c_gate * torch.sigmoid(x[:, ns:ns + ng])
+        v = x[:, ns + ng:]
+        gi = vi = 0
+        for mul, (l, _) in self.irreps_gated:
+            d = 2 * l + 1
+            outs.append((v[:, vi:vi + mul * d].reshape(B, mul, d)
+                         * g[:, gi:gi + mul].unsqueeze(-1)).reshape(B, mul * d))
+            vi += mul * d
+            gi += mul
+        return torch.cat(outs, dim=1)
+
+
+# ===================================================================================== TP conv
+class TPGraph:
+    """Receiver (edge_index[0])-sorted CSR for the TP convolution (scatter target ei0,
+    gather source ei1: tfn_layer.py:83-87), plus the CSR of the gather source over sorted
+    positions for the backward segmented sums."""
+
+    def __init__(self, edge_index, num_nodes):
+        ei = edge_index.contiguous()
+        self.num_nodes, self.num_edges = int(num_nodes), ei.shape[1]
+        self.recv_csr = ops.CSR(ei[0], self.num_nodes, payload=ei[1])
+        self.rowptr = self.recv_csr.rowptr
+        self.perm = self.recv_csr.perm
+        self.src_sorted = self.recv_csr.payload_sorted
+        self.src_csr = ops.CSR(self.src_sorted, self.num_nodes)
+
+
+_TP_GRAPHS = []
+
+
+def tp_graph(edge_index, num_nodes):
+    for t, ver, n, g in _TP_GRAPHS:
+        if t is edge_index and ver == edge_index._version and n == num_nodes:
+            return g
+    g = TPGraph(edge_index, num_nodes)
+    _TP_GRAPHS.insert(0, (edge_index, edge_index._version, num_nodes, g))
+    del _TP_GRAPHS[4:]
+    return g
+
+
+_LAYOUTS = {((0, 1), (1, -1), (2, 1)): 0, ((0, 1), (0, 1), (1, -1), (2, 1)): 1}
+
+
+class TPPlan:
+    """Instruction table + CG constants of one FullyConnectedTensorProduct, uploaded once."""
+
+    def __init__(self, irreps_in, irreps_sh, irreps_out):
+        self.irreps_in, self.irreps_sh, self.irreps_out = irreps_in, irreps_sh, irreps_out
+        self.instructions, self.weight_numel = o3.fctp_instructions(irreps_in, irreps_sh,
+                                                                    irreps_out)
+        key = tuple(ir for _, ir in irreps_out)
+        if key not in _LAYOUTS or any(m > 128 for m, _ in irreps_out) or \
+                any(m != 1 for m, _ in irreps_sh) or o3.irreps_dim(irreps_sh) != 9:
+            raise NotImplementedError(f"TP layout {o3.irreps_str(irreps_out)} not supported by K7")
+        self.layout = _LAYOUTS[key]
+        xo, yo, oo = (o3.irreps_offsets(irreps_in), o3.irreps_offsets(irreps_sh),
+                      o3.irreps_offsets(irreps_out))
+        paths = (_lib.TpPath * len(self.instructions))()
+        cg, z_off = [], 0
+        cg_off = 0
+        for k, ins in enumerate(self.instructions):
+            C = o3.wigner_3j(ins["l1"], ins["l2"], ins["lo"])
+            paths[k] = _lib.TpPath(ins["l1"], ins["l2"], ins["lo"], ins["mul1"], ins["mul_out"],
+                                   xo[ins["i1"]], yo[ins["i2"]], ins["io"], oo[ins["io"]], z_off,
+                                   cg_off, 0, ins["w_off"], ins["alpha"], 0.0)
+            cg.append(torch.from_numpy(C.reshape(-1).copy()))
+            cg_off += C.size
+            z_off += ins["mul1"] * (2 * ins["lo"] + 1)
+        self.paths_host = paths
+        self.cg_host = torch.cat(cg).float()
+        self.desc = _lib.TpDesc()
+        self.desc.n_paths = len(self.instructions)
+        self.desc.in_dim = o3.irreps_dim(irreps_in)
+        self.desc.out_dim = o3.irreps_dim(irreps_out)
+        self.desc.sh_dim = 9
+        self.desc.weight_numel = self.weight_numel
+        self.desc.z_size = z_off
+        self.desc.n_blocks = len(irreps_out)
+        for b, (m, (l, _)) in enumerate(irreps_out):
+            self.desc.blk_off[b], self.desc.blk_mul[b], self.desc.blk_l[b] = oo[b], m, l
+        self._dev = {}
+
+    def device_tables(self, device):
+        if device not in self._dev:
+            raw = torch.frombuffer(bytearray(bytes(self.paths_host)), dtype=torch.uint8)
+            self._dev[device] = (raw.to(device), self.cg_host.to(device))
+        return self._dev[device]
+
+    def chunk_edges(self):
+        e = CHUNK_BYTES // (4 * self.weight_numel)
+        return max(256, (e // 256) * 256)
+
+
+class TPConvFn(torch.autograd.Function):
+    """out = scatter_sum_{ei0}( FCTP(x[ei1], sh, fc(radial)) )   (tfn_layer.py:82-87).
+
+    Chunked over receiver-sorted edges: per chunk the radial MLP produces the per-edge weights
+    (library GEMM), then the HIP TP kernel contracts them with the CG-coupled features and sums
+    into the receiver rows.  Backward recomputes the chunk's weights."""
+
+    @staticmethod
+    def forward(ctx, x, sh, rad, W1, b1, W2, b2, plan, graph):
+        lib = _lib.load()
+        x, sh, rad = _f32c(x), _f32c(sh), _f32c(rad)
+        _need_cuda(x, sh, rad)
+        dev = x.device
+        paths_dev, cg_dev = plan.device_tables(dev)
+        N, E = graph.num_nodes, graph.num_edges
+        out = torch.zeros((N, plan.desc.out_dim), dtype=torch.float32, device=dev)
+        rad_s = ops.gather_rows(rad, graph.perm)  # radial features in receiver-sorted order
+        ce = plan.chunk_edges()
+        for c0 in range(0, E, ce):
+            c1 = min(E, c0 + ce)
+            a = torch.relu(torch.addmm(b1, rad_s[c0:c1], W1.t()))
+            Wc = torch.addmm(b2, a, W2.t())
+            with _timed("tp_conv_fwd"):
+                check(lib.gmp_tp_conv_fwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
+                                              _p(cg_dev), cg_dev.numel(), _p(x), _p(sh), _p(Wc),
+                                              _p(graph.rowptr), _p(graph.src_sorted),
+                                              _p(graph.perm), N, c0, c1, _p(out), _stream()),
+                      "gmp_tp_conv_fwd_f32")
+            del Wc, a
+        ctx.plan, ctx.graph = plan, graph
+        ctx.save_for_backward(x, sh, rad_s, W1, b1, W2, b2)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _lib.load()
+        x, sh, rad_s, W1, b1, W2, b2 = ctx.saved_tensors
+        plan, graph = ctx.plan, ctx.graph
+        paths_dev, cg_dev = plan.device_tables(x.device)
+        gout = _f32c(gout)
+        N, E = graph.num_nodes, graph.num_edges
+        f = dict(dtype=torch.float32, device=x.device)
+        dx_edge = torch.empty((E, plan.desc.in_dim), **f)
+        dY = torch.empty((E, 9), **f)
+        drad_s = torch.empty_like(rad_s)
+        dW2 = torch.zeros_like(W2)
+        db2 = torch.zeros_like(b2)
+        dW1 = torch.zeros_like(W1)
+        db1 = torch.zeros_like(b1)
+        ce = plan.chunk_edges()
+        for c0 in range(0, E, ce):
+            c1 = min(E, c0 + ce)
+            r = rad_s[c0:c1]
+            pre = torch.addmm(b1, r, W1.t())
+            a = torch.relu(pre)
+            Wc = torch.addmm(b2, a, W2.t())
+            dWc = torch.empty_like(Wc)
+            with _timed("tp_conv_bwd"):
+                check(lib.gmp_tp_conv_bwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
+                                              _p(cg_dev), cg_dev.numel(), _p(x), _p(sh), _p(Wc),
+                                              _p(graph.rowptr), _p(graph.src_sorted),
+                                              _p(graph.perm), N, c0, c1, _p(gout), _p(dWc),
+                                              _p(dx_edge), _p(dY), _stream()),
+                      "gmp_tp_conv_bwd_f32")
+            del Wc
+            dW2.addmm_(dWc.t(), a)
+            db2.add_(dWc.sum(0))
+            da = dWc.mm(W2)
+            del dWc
+            dpre = da * (pre > 0)
+            dW1.addmm_(dpre.t(), r)
+            db1.add_(dpre.sum(0))
+            drad_s[c0:c1] = dpre.mm(W1)
+        dx, _ = ops.segment_reduce(dx_edge, graph.src_csr, "sum")
+        dsh = torch.empty_like(sh).index_copy_(0, graph.perm, dY)
+        drad = torch.empty((E, rad_s.shape[1]), **f).index_copy_(0, graph.perm, drad_s)
+        return dx, dsh, drad, dW1, db1, dW2, db2, None, None
+
+
+class TensorProductConvLayer(nn.Module):
+    """tfn_layer.py:8-93 (same arguments; module tree fc.{0,2}, batch_norm, gate)."""
+
+    def __init__(self, in_irreps, out_irreps, sh_irreps, edge_feats_dim, mlp_dim, aggr="add",
+                 batch_norm=False, gate=False):
+        super().__init__()
+        self.in_irreps = o3.parse_irreps(in_irreps)
+        self.out_irreps = o3.parse_irreps(out_irreps)
+        self.sh_irreps = o3.parse_irreps(sh_irreps)
+        self.edge_feats_dim = edge_feats_dim
+        self.aggr = aggr
+        if gate:
+            s, g, v = o3.irreps2gate(self.out_irreps)
+            self.gate = Gate(s, g, v)
+            self.out_irreps = self.gate.irreps_in
+        else:
+            self.gate = None
+        self.plan = TPPlan(self.in_irreps, self.sh_irreps, self.out_irreps)
+        self.fc = nn.Sequential(nn.Linear(edge_feats_dim, mlp_dim), nn.ReLU(),
+                                nn.Linear(mlp_dim, self.plan.weight_numel))
+        self.batch_norm = BatchNorm(self.out_irreps) if batch_norm else None
+
+    def forward(self, node_attr, edge_index, edge_sh, edge_feat):
+        graph = tp_graph(edge_index, node_attr.shape[0])
+        out = TPConvFn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight, self.fc[0].bias,
+                             self.fc[2].weight, self.fc[2].bias, self.plan, graph)
+        if self.aggr == "mean":
+            out = out / graph.recv_csr.counts().clamp(min=1).unsqueeze(1).to(out.dtype)
+        elif self.aggr not in ("add", "sum"):
+            raise NotImplementedError(f"aggr={self.aggr}")
+        if self.gate is not None:
+            out = self.gate(out)
+        if self.batch_norm is not None:
+            out = self.batch_norm(out)
+        return out
+
+
+# ===================================================================================== MACE node
+def reshape_irreps(irreps, x):
+    """irreps_tools.py:63-79."""
+    B, out, ix = x.shape[0], [], 0
+    for mul, (l, _) in irreps:
+        d = 2 * l + 1
+        out.append(x[:, ix:ix + mul * d].reshape(B, mul, d))
+        ix += mul * d
+    return torch.cat(out, dim=-1)
+
+
+class Contraction(nn.Module):
+    """symmetric_contraction.py:88-188 (element_dependent=False): same buffers
+    U_matrix_{nu} and weights.{nu} (K_nu, C).  Evaluated as a per-channel polynomial in x with
+    coefficient tensors A_nu[c] = sum_k U_nu[..., k] W_nu[k, c] (identical algebra to the
+    reference's einsum chain, no (N, C, d, 9, 9) HBM intermediates held for backward)."""
+
+    node_chunk = 4096
+
+    def __init__(self, irreps_in, irrep_out, correlation):
+        super().__init__()
+        irreps_in = o3.parse_irreps(irreps_in)
+        self.num_features = sum(m for m, ir in irreps_in if ir == (0, 1))
+        coupling = tuple((1, ir) for _, ir in irreps_in)
+        self.correlation = correlation
+        for nu in range(1, correlation + 1):
+            U = torch.from_numpy(o3.u_matrix(coupling, irrep_out, nu).copy())
+            self.register_buffer(f"U_matrix_{nu}", U.to(torch.get_default_dtype()))
+        self.weights = nn.ParameterDict({
+            str(nu): nn.Parameter(torch.randn(self.U(nu).shape[-1], self.num_features)
+                                  / self.U(nu).shape[-1]) for nu in range(1, correlation + 1)})
+
+    def U(self, nu):
+        return self._buffers[f"U_matrix_{nu}"]
+
+    def _chunk(self, x, *A):
+        out = torch.einsum("c...i,bci->bc...", A[-1], x)
+        for nu in range(self.correlation - 1, 0, -1):
+            out = torch.einsum("bc...i,bci->bc...", A[nu - 1].unsqueeze(0) + out, x)
+        return out.reshape(out.shape[0], -1)
+
+    def forward(self, x):
+        A = [torch.einsum("...k,kc->c...", self.U(nu), self.weights[str(nu)])
+             for nu in range(1, self.correlation + 1)]
+        outs = []
+        for b0 in range(0, x.shape[0], self.node_chunk):
+            xb = x[b0:b0 + self.node_chunk]
+            if torch.is_grad_enabled():
+                outs.append(torch.utils.checkpoint.checkpoint(self._chunk, xb, *A,
+                                                              use_reentrant=False))
+            else:
+                outs.append(self._chunk(xb, *A))
+        return torch.cat(outs, dim=0)
+
+
+class SymmetricContraction(nn.Module):
+    def __init__(self, irreps_in, irreps_out, correlation):
+        super().__init__()
+        self.irreps_out = o3.parse_irreps(irreps_out)
+        self.contractions = nn.ModuleDict({
+            f"{m}x{l}{'e' if p == 1 else 'o'}": Contraction(irreps_in, (l, p), correlation)
+            for m, (l, p) in self.irreps_out})
+
+    def forward(self, x, y=None):
+        return torch.cat([c(x) for c in self.contractions.values()], dim=-1)
+
+
+class EquivariantProductBasisBlock(nn.Module):
+    """blocks.py:99-135 (element_dependent=False, batch_norm=False)."""
+
+    def __init__(self, node_feats_irreps, target_irreps, correlation, element_dependent=False,
+                 use_sc=True, batch_norm=False, num_elements=None):
+        super().__init__()
+        self.use_sc = use_sc
+        self.symmetric_contractions = SymmetricContraction(node_feats_irreps, target_irreps,
+                                                           correlation)
+        self.linear = Linear(target_irreps, target_irreps)
+        self.batch_norm = BatchNorm(target_irreps) if batch_norm else None
+
+    def forward(self, node_feats, sc, node_attrs=None):
+        out = self.linear(self.symmetric_contractions(node_feats, node_attrs))
+        if self.batch_norm is not None:
+            out = self.batch_norm(out)
+        return out + sc if self.use_sc else out
+
+
+# ===================================================================================== models
+def _edge_features(model, batch):
+    graph = tp_graph(batch.edge_index, batch.pos.shape[0])
+    return EdgeFeaturizeFn.apply(batch.pos, batch.edge_index, model.radial_embedding._host, graph)
+
+
+class MACEModel(nn.Module):
+    """models/mace.py:9-190 (same kwargs/defaults; max_ell = 2)."""
+
+    def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
+                 correlation=3, num_layers=5, emb_dim=64, hidden_irreps=None, mlp_dim=256,
+                 in_dim=1, out_dim=1, aggr="sum", pool="sum", batch_norm=True, residual=True,
+                 equivariant_pred=False):
+        super().__init__()
+        if max_ell != 2:
+            raise NotImplementedError("K1/K7 are specialised to l <= 2 (the configs' L_max)")
+        self.r_max, self.max_ell, self.num_layers = r_max, max_ell, num_layers
+        self.emb_dim, self.mlp_dim, self.residual = emb_dim, mlp_dim, residual
+        self.batch_norm, self.equivariant_pred = batch_norm, equivariant_pred
+        self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)
+        sh = o3.sh_irreps(max_ell)
+        self.emb_in = nn.Embedding(in_dim, emb_dim)
+        hidden = o3.parse_irreps(hidden_irreps) if hidden_irreps else o3.hidden_irreps(emb_dim,
+                                                                                       max_ell)
+        self.hidden_irreps = hidden
+        self.convs, self.prods = nn.ModuleList(), nn.ModuleList()
+        for k in range(num_layers):
+            inp = ((emb_dim, (0, 1)),) if k == 0 else hidden
+            self.convs.append(TensorProductConvLayer(inp, hidden, sh,
+                                                     self.radial_embedding.out_dim, mlp_dim, aggr,
+                                                     batch_norm=batch_norm, gate=False))
+            self.prods.append(EquivariantProductBasisBlock(hidden, hidden, correlation,
+                                                           element_dependent=False,
+                                                           use_sc=residual, num_elements=in_dim))
+        self.pool = {"mean": global_mean_pool, "sum": global_add_pool}[pool]
+        if equivariant_pred:
+            self.pred = nn.Linear(o3.irreps_dim(hidden), out_dim)
+        else:
+            self.pred = nn.Sequential(nn.Linear(emb_dim, emb_dim), nn.ReLU(),
+                                      nn.Linear(emb_dim, out_dim))
+
+    def forward(self, batch):
+        h = ops.gather(self.emb_in.weight, batch.atoms)
+        edge_sh, edge_feats = _edge_features(self, batch)
+        for conv, prod in zip(self.convs, self.prods):
+            hu = conv(h, batch.edge_index, edge_sh, edge_feats)
+            sc = F.pad(h, (0, hu.shape[-1] - h.shape[-1]))
+            h = prod(reshape_irreps(self.hidden_irreps, hu), sc, None)
+        out = self.pool(h, batch.batch, getattr(batch, "num_graphs", None))
+        if not self.equivariant_pred:
+            out = out[:, :self.emb_dim]
+        return self.pred(out)
+
+
+def first_node_pooling(x, batch, size=None):
+    """tfn.py:13-40: first node of each graph (batch vector sorted)."""
+    prev = torch.cat([batch[-1:], batch[:-1]])
+    prev[0] = -1
+    return x[(batch - prev) == 1]
+
+
+class TFNModel(nn.Module):
+    """models/tfn.py:42-190 (same kwargs/defaults; max_ell = 2)."""
+
+    def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
+                 num_layers=5, emb_dim=64, hidden_irreps=None, mlp_dim=256, in_dim=1, out_dim=1,
+                 aggr="sum", pool="first", gate=True, batch_norm=False, residual=True,
+                 equivariant_pred=False):
+        super().__init__()
+        if max_ell != 2:
+            raise NotImplementedError("K1/K7 are specialised to l <= 2 (the configs' L_max)")
+        self.emb_dim, self.residual, self.equivariant_pred = emb_dim, residual, equivariant_pred
+        self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)
+        sh = o3.sh_irreps(max_ell)
+        self.emb_in = nn.Embedding(in_dim, emb_dim)
+        hidden = o3.parse_irreps(hidden_irreps) if hidden_irreps else o3.hidden_irreps(emb_dim,
+                                                                                       max_ell)
+        self.convs = nn.ModuleList()
+        for k in range(num_layers):
+            inp = ((emb_dim, (0, 1)),) if k == 0 else hidden
+            self.convs.append(TensorProductConvLayer(inp, hidden, sh,
+                                                     self.radial_embedding.out_dim, mlp_dim, aggr,
+                                                     batch_norm=batch_norm, gate=gate))
+        self.pool = {"mean": global_mean_pool, "sum": global_add_pool,
+                     "first": first_node_pooling}[pool]
+        if equivariant_pred:
+            self.pred = nn.Linear(o3.irreps_dim(hidden), out_dim)
+        else:
+            self.pred = nn.Sequential(nn.Linear(emb_dim, emb_dim), nn.ReLU(),
+                                      nn.Linear(emb_dim, out_dim))
+
+    def forward(self, batch):
+        h = ops.gather(self.emb_in.weight, batch.atoms)
+        edge_sh, edge_feats = _edge_features(self, batch)
+        for conv in self.convs:
+            hu = conv(h, batch.edge_index, edge_sh, edge_feats)
+            h = hu + F.pad(h, (0, hu.shape[-1] - h.shape[-1])) if self.residual else hu
+        if self.pool is first_node_pooling:
+            out = first_node_pooling(h, batch.batch)
+        else:
+            out = self.pool(h, batch.batch, getattr(batch, "num_graphs", None))
+        if not self.equivariant_pred:
+            out = out[:, :self.emb_dim]
+        return self.pred(out)

@@ -161,6 +161,54 @@ int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B,
                            float* colsum_A, void* workspace, size_t workspace_bytes,
                            void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * K1 per-edge featurisation (models/mace.py:170-174, models/tfn.py:171-175,
+ * models/mace_modules/radial.py:44-46,71-78, blocks.py:91-96; e3nn SphericalHarmonics(l<=2,
+ * normalize=True, 'component')):
+ *   vec = pos[ei0] - pos[ei1] (E,3); len = |vec| (E); sh (E,9); radial = bessel * cutoff (E,nb)
+ * edge_index is (2, E) int64 (row 0 then row 1).  `bessel_weights` is a HOST array of nb floats
+ * (the module buffer, copied into the kernel arguments).  Any output pointer may be NULL.
+ * Backward: g_vec (E,3) from g_sh / g_radial (either may be NULL); the caller scatters g_vec to
+ * pos[ei0] (+) and pos[ei1] (-).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_edge_featurize_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                           int num_bessel, const float* bessel_weights, float prefactor,
+                           float r_max, float p_cutoff, float* vec_out, float* len_out,
+                           float* sh_out, float* radial_out, void* stream);
+int gmp_edge_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                               int num_bessel, const float* bessel_weights, float prefactor,
+                               float r_max, float p_cutoff, const float* g_sh,
+                               const float* g_radial, float* g_vec, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * K7 tensor-product convolution (models/layers/tfn_layer.py:82-87): e3nn
+ * FullyConnectedTensorProduct(in1, 1x0e+1x1o+1x2e, out, shared_weights=False) with per-edge
+ * weights W (chunk rows x weight_numel, produced by the radial MLP tfn_layer.py:73-77), summed
+ * into the receiver ei0 (scatter(tp, ei[0], dim=0, reduce='sum')).
+ * Edges are processed in receiver-sorted order over the chunk [c0, c1) of the CSR built on
+ * edge_index[0]: rowptr (N+1), src_sorted[k] = ei1 of sorted edge k, perm[k] = original edge id.
+ * x (N, in_dim) mul_ir; sh (E, 9) in ORIGINAL edge order; W row r = sorted edge c0 + r.
+ * `out` (N, out_dim) is ACCUMULATED (caller zeroes it once before the first chunk).
+ * desc_host: host pointer to the descriptor {int n_paths, in_dim, out_dim, sh_dim;
+ *   int64 weight_numel; int z_size, n_blocks; int blk_off[4], blk_mul[4], blk_l[4];}
+ * paths_dev: device array of 64-byte path records {int l1, l2, lo, mul1, mul_out, x_off, y_off,
+ *   io, out_off, z_off, cg_off, pad; int64 w_off; float alpha, pad}; cg_dev: concatenated
+ *   real CG tensors (cg_len floats).  layout: 0 = out blocks (0e,1o,2e), 1 = (0e,0e,1o,2e).
+ * Backward (per chunk): dW (chunk rows x weight_numel), dx_edge (E, in_dim) and dY_edge (E, 9)
+ * at SORTED positions, given gout = dL/dout (N, out_dim).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_tp_conv_fwd_f32(int layout, const void* desc_host, const void* paths_dev,
+                        const float* cg_dev, int cg_len, const float* x, const float* sh,
+                        const float* W, const int64_t* rowptr, const int64_t* src_sorted,
+                        const int64_t* perm, int64_t n_nodes, int64_t c0, int64_t c1, float* out,
+                        void* stream);
+int gmp_tp_conv_bwd_f32(int layout, const void* desc_host, const void* paths_dev,
+                        const float* cg_dev, int cg_len, const float* x, const float* sh,
+                        const float* W, const int64_t* rowptr, const int64_t* src_sorted,
+                        const int64_t* perm, int64_t n_nodes, int64_t c0, int64_t c1,
+                        const float* gout, float* dW, float* dx_edge, float* dY_edge,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif
