@@ -1,8 +1,11 @@
 """Benchmark: edges/s forward+backward (one training step) of the geometric message-passing hot
 path on MI355X (BASELINE.json metric).
 
-Workload at N=1: config C2 — EGNN 4 layers, emb_dim 128, one seeded random 3-D radius graph
-with 50,000 nodes and ~1M directed edges (r = 5, box tuned), synthetic data, random-init weights.
+Workload at N=1 (default, --workload egnn): config C2 — EGNN 4 layers, emb_dim 128, one seeded
+random 3-D radius graph with 50,000 nodes and ~1M directed edges (r = 5, box tuned), synthetic
+data, random-init weights.  --workload mace: config C4 (MACE L_max=2, correlation 3, 128
+channels, 5 layers, same graph); --workload tfn: config C5's per-GPU shard (TFN L_max=2, 64
+channels, 5 layers, gated, same graph).
 A step = the reference training step (experiments/utils/train_utils.py:128-139): forward,
 L1 loss, backward, Adam step.  Weak scaling: every rank owns its own ~1M-edge graph
 (seed = rank) and gradients are all-reduced by DDP (RCCL over xGMI).
@@ -37,13 +40,68 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--layers", type=int, default=4)
-    ap.add_argument("--emb", type=int, default=128)
+    ap.add_argument("--workload", choices=("egnn", "mace", "tfn"), default="egnn")
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--emb", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=50_000)
     ap.add_argument("--edges", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
+
+
+WORKLOADS = {  # name -> (config tag, layers, emb)
+    "egnn": ("C2 EGNN", 4, 128),
+    "mace": ("C4 MACE L=2 corr=3", 5, 128),
+    "tfn": ("C5 TFN L=2 gated (per-GPU shard)", 5, 64),
+}
+
+
+def build_model(mod, args, radius):
+    if args.workload == "egnn":
+        return mod.EGNNModel(num_layers=args.layers, emb_dim=args.emb, in_dim=1, out_dim=1)
+    if args.workload == "mace":
+        return mod.MACEModel(r_max=radius, num_layers=args.layers, emb_dim=args.emb,
+                             correlation=3, max_ell=2, in_dim=1, out_dim=1)
+    return mod.TFNModel(r_max=radius, num_layers=args.layers, emb_dim=args.emb, max_ell=2,
+                        in_dim=1, out_dim=1)
+
+
+def tp_bytes_per_edge(model):
+    """Algorithmic HBM bytes per edge per launch of the K7 TP kernels, summed over layers:
+    the per-edge weight row (4 * weight_numel) plus the sender row and SH (fwd; bwd also writes
+    dW and dx rows)."""
+    fwd = bwd = 0
+    for conv in model.convs:
+        pl = conv.plan
+        wn, din = pl.weight_numel, pl.desc.in_dim
+        fwd += 4 * (wn + din + 9) + 16
+        bwd += 4 * (2 * wn + 2 * din + 18) + 16
+    return fwd / len(model.convs), bwd / len(model.convs)
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_<workload>_kernels.json, scripts/prof_summary.py: FETCH_SIZE x2 +
+    WRITE_SIZE, separate passes), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_kernels.json")))
+    for path in reversed(files):
+        with open(path) as f:
+            rows = json.load(f)["kernels"]
+        for r in rows:
+            if r["kernel"].startswith(kernel) and r["hbm_read_bytes_per_launch"] is not None \
+                    and r["hbm_write_bytes_per_launch"] is not None:
+                return (r["hbm_read_bytes_per_launch"] + r["hbm_write_bytes_per_launch"],
+                        os.path.basename(path))
+    return None
+
+
+def egnn_bwd_bytes_per_edge(d):
+    """Minimum HBM bytes per edge of the fused EGNN edge backward: indices 16,
+    sender/receiver node rows of dA/AB 2 x 2d x 4 (gathered), pos 24, recomputed nothing else
+    read; per-edge activations written for the weight-gradient outer sums 5 x d x 4."""
+    return 16 + 2 * 2 * d * 4 + 24 + 5 * d * 4
 
 
 def egnn_flops_per_edge(d):
@@ -55,12 +113,20 @@ def egnn_flops_per_edge(d):
 def cpu_baseline(g, args):
     """Time the CPU oracle (fwd + L1 + bwd + Adam) on a spatial slab of the same graph."""
     from oracle import egnn as oegnn
+    from oracle import mace as omace
     from gmp_amd.graph import Batch
 
     threads = min(args.cpu_threads, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    frac = 0.25
-    keep = g.pos[:, 0] < g.box * frac
+    if args.workload == "egnn":
+        frac = 0.25  # slab x < box / 4
+        keep = g.pos[:, 0] < g.box * frac
+        shape = "spatial slab"
+    else:
+        # the oracle's TP materialises 4 * weight_numel bytes per edge: a small corner cube
+        frac = 0.003
+        keep = (g.pos < g.box * frac ** (1.0 / 3.0)).all(dim=1)
+        shape = "corner cube"
     idx = torch.nonzero(keep).view(-1)
     remap = torch.full((g.num_nodes,), -1, dtype=torch.long)
     remap[idx] = torch.arange(idx.numel())
@@ -69,7 +135,7 @@ def cpu_baseline(g, args):
     sub = Batch(torch.zeros(idx.numel(), dtype=torch.long), g.pos[idx], remap[ei[:, m]],
                 num_graphs=1)
     torch.manual_seed(0)
-    model = oegnn.EGNNModel(num_layers=args.layers, emb_dim=args.emb, in_dim=1, out_dim=1)
+    model = build_model(oegnn if args.workload == "egnn" else omace, args, g.radius)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     y = torch.zeros(1)
 
@@ -88,13 +154,16 @@ def cpu_baseline(g, args):
     ts.sort()
     med = ts[len(ts) // 2]
     return {"value": sub.num_edges / med, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/egnn.py EGNN {args.layers}x{args.emb} fwd+bwd+Adam on a "
-                      f"{frac:.0%} spatial slab of the C2 graph ({sub.num_nodes} nodes, "
+            "sample": f"oracle {args.workload} {args.layers}x{args.emb} fwd+bwd+Adam on a "
+                      f"{frac:.1%}-volume {shape} of the same graph ({sub.num_nodes} nodes, "
                       f"{sub.num_edges} edges), median of 3 steps"}
 
 
 def main():
     args = parse()
+    _, d_layers, d_emb = WORKLOADS[args.workload]
+    args.layers = args.layers or d_layers
+    args.emb = args.emb or d_emb
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -110,8 +179,8 @@ def main():
 
     g = radius_graph(num_nodes=args.nodes, target_edges=args.edges, seed=rank)
     torch.manual_seed(0)
-    model = gmp_amd.EGNNModel(num_layers=args.layers, emb_dim=args.emb, in_dim=1,
-                              out_dim=1).to(dev)
+    model = build_model(gmp_amd, args, g.radius).to(dev)
+    core = model
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local],
                                                           bucket_cap_mb=32)
@@ -149,13 +218,48 @@ def main():
         total_edges = e.item()
     else:
         total_edges = g.num_edges
-    ms_fwd = ops.kernel_time_ms("egnn_edge_fwd")
-    ms_bwd = ops.kernel_time_ms("egnn_edge_bwd")
+    timers = {k: ops.kernel_time_ms(k) for k in list(ops.KERNEL_TIMERS)}
+    totals = {k: timers[k] * len(v) for k, v in ops.KERNEL_TIMERS.items()}
     ops.KERNEL_TIMERS = None
 
+    def sum_ms(name):
+        return totals.get(name, 0.0)
+
     if rank == 0:
-        fl = egnn_flops_per_edge(args.emb)
-        achieved = fl["egnn_edge_bwd"] * g.num_edges / (ms_bwd * 1e-3) / 1e12
+        if args.workload == "egnn":
+            fl = egnn_flops_per_edge(args.emb)
+            ms_fwd, ms_bwd = timers["egnn_edge_fwd"], timers["egnn_edge_bwd"]
+            achieved = fl["egnn_edge_bwd"] * g.num_edges / (ms_bwd * 1e-3) / 1e12
+            roof = {"kernel": "egnn_edge_bwd", "bound": "mfma",
+                    "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                    "traffic": None, "ms_per_launch": ms_bwd,
+                    "flops_per_edge": fl["egnn_edge_bwd"],
+                    "bytes_per_edge_min": egnn_bwd_bytes_per_edge(args.emb),
+                    "fwd_kernel_ms": ms_fwd,
+                    "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
+                    / (ms_fwd * 1e-3) / 1e12}
+        else:
+            # K7 is timed per chunk launch; algorithmic bytes = bytes/edge x edges per launch
+            bf, bb = tp_bytes_per_edge(core)
+            n_f = len(core.convs) * (args.steps)
+            tot_f = sum_ms("tp_conv_fwd")
+            tot_b = sum_ms("tp_conv_bwd")
+            gbs_f = bf * g.num_edges * n_f / (tot_f * 1e-3) / 1e9
+            gbs_b = bb * g.num_edges * n_f / (tot_b * 1e-3) / 1e9
+            roof = {"kernel": "tp_conv_bwd", "bound": "hbm", "achieved": gbs_b,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs_b / HBM_PEAK_GBS,
+                    "traffic": None, "ms_per_launch": timers["tp_conv_bwd"],
+                    "bytes_per_edge": bb, "fwd_kernel_gbs": gbs_f,
+                    "fwd_kernel_ms_per_launch": timers["tp_conv_fwd"],
+                    "tp_fwd_ms_per_step": tot_f / args.steps,
+                    "tp_bwd_ms_per_step": tot_b / args.steps,
+                    "radial_gemm_ms_per_step": sum_ms("radial_gemm") / args.steps}
+        t = pmc_traffic(args.workload, roof["kernel_prefix"] if "kernel_prefix" in roof
+                        else {"egnn_edge_bwd": "egnn_bwd_kernel",
+                              "tp_conv_bwd": "tp_bwd_kernel"}[roof["kernel"]])
+        if t is not None:
+            roof["traffic"], roof["traffic_source"] = t[0], f"profiles/{t[1]}"
         rec = {
             "metric": "edges/sec forward+backward, EGNN & MACE L=2, 1M-edge radius graph, "
                       "1/2/4/8 GPU",
@@ -170,19 +274,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded random radius graph per rank, random-init weights)",
-            "config": {"workload": f"C2 EGNN {args.layers}L/{args.emb} radius graph "
+            "config": {"workload": f"{WORKLOADS[args.workload][0]} {args.layers}L/{args.emb} "
+                                   f"radius graph "
                                    f"{g.num_nodes} nodes / {g.num_edges} edges per GPU "
                                    f"(r={g.radius}, box={g.box:.3f}, seed=rank)",
                        "global_batch": world, "parallelism": f"dp{world}",
                        "step": "fwd + L1 loss + bwd + Adam"},
-            "roofline": {"kernel": "egnn_edge_bwd", "bound": "mfma",
-                         "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": None, "ms_per_launch": ms_bwd,
-                         "flops_per_edge": fl["egnn_edge_bwd"],
-                         "fwd_kernel_ms": ms_fwd,
-                         "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
-                         / (ms_fwd * 1e-3) / 1e12},
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -350,8 +350,9 @@ class TPConvFn(torch.autograd.Function):
         ce = plan.chunk_edges()
         for c0 in range(0, E, ce):
             c1 = min(E, c0 + ce)
-            a = torch.relu(torch.addmm(b1, rad_s[c0:c1], W1.t()))
-            Wc = torch.addmm(b2, a, W2.t())
+            with _timed("radial_gemm"):
+                a = torch.relu(torch.addmm(b1, rad_s[c0:c1], W1.t()))
+                Wc = torch.addmm(b2, a, W2.t())
             with _timed("tp_conv_fwd"):
                 check(lib.gmp_tp_conv_fwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
                                               _p(cg_dev), cg_dev.numel(), _p(x), _p(sh), _p(Wc),
@@ -383,9 +384,10 @@ class TPConvFn(torch.autograd.Function):
         for c0 in range(0, E, ce):
             c1 = min(E, c0 + ce)
             r = rad_s[c0:c1]
-            pre = torch.addmm(b1, r, W1.t())
-            a = torch.relu(pre)
-            Wc = torch.addmm(b2, a, W2.t())
+            with _timed("radial_gemm"):
+                pre = torch.addmm(b1, r, W1.t())
+                a = torch.relu(pre)
+                Wc = torch.addmm(b2, a, W2.t())
             dWc = torch.empty_like(Wc)
             with _timed("tp_conv_bwd"):
                 check(lib.gmp_tp_conv_bwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
@@ -395,14 +397,15 @@ class TPConvFn(torch.autograd.Function):
                                               _p(dx_edge), _p(dY), _stream()),
                       "gmp_tp_conv_bwd_f32")
             del Wc
-            dW2.addmm_(dWc.t(), a)
-            db2.add_(dWc.sum(0))
-            da = dWc.mm(W2)
-            del dWc
-            dpre = da * (pre > 0)
-            dW1.addmm_(dpre.t(), r)
-            db1.add_(dpre.sum(0))
-            drad_s[c0:c1] = dpre.mm(W1)
+            with _timed("radial_gemm"):
+                dW2.addmm_(dWc.t(), a)
+                db2.add_(dWc.sum(0))
+                da = dWc.mm(W2)
+                del dWc
+                dpre = da * (pre > 0)
+                dW1.addmm_(dpre.t(), r)
+                db1.add_(dpre.sum(0))
+                drad_s[c0:c1] = dpre.mm(W1)
         dx, _ = ops.segment_reduce(dx_edge, graph.src_csr, "sum")
         dsh = torch.empty_like(sh).index_copy_(0, graph.perm, dY)
         drad = torch.empty((E, rad_s.shape[1]), **f).index_copy_(0, graph.perm, drad_s)

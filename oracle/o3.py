@@ -220,7 +220,10 @@ class FullyConnectedTensorProduct(torch.nn.Module):
             b = x2[:, s2[ins["i2"]]].reshape(B, m2, 2 * l2 + 1)
             W = weight[:, ins["w_off"]:ins["w_off"] + m1 * m2 * mo].reshape(B, m1, m2, mo)
             C = wigner_3j(l1, l2, lo, x1.dtype)
-            r = torch.einsum("zuvw,ijk,zui,zvj->zwk", W, C, a, b) * ins["path_weight"]
+            # contraction order of e3nn's generated code: CG-couple the inputs first, then
+            # one batched matmul with the per-edge weights
+            zc = torch.einsum("ijk,zui,zvj->zuvk", C, a, b).reshape(B, m1 * m2, 2 * lo + 1)
+            r = torch.bmm(W.reshape(B, m1 * m2, mo).transpose(1, 2), zc) * ins["path_weight"]
             sl = so[ins["io"]]
             out[:, sl] = out[:, sl] + r.reshape(B, mo * (2 * lo + 1))
         return out
