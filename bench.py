@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("egnn", "mace", "tfn"), default="egnn")
+    ap.add_argument("--workload", choices=("egnn", "gvp", "mace", "tfn"), default="egnn")
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--emb", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=50_000)
@@ -54,17 +54,23 @@ WORKLOADS = {  # name -> (config tag, layers, emb)
     "egnn": ("C2 EGNN", 4, 128),
     "mace": ("C4 MACE L=2 corr=3", 5, 128),
     "tfn": ("C5 TFN L=2 gated (per-GPU shard)", 5, 64),
+    "gvp": ("C3 GVP-GNN s=128 v=16 edge=(32,1)", 4, 128),
 }
 
 
 def build_model(mod, args, radius):
     if args.workload == "egnn":
         return mod.EGNNModel(num_layers=args.layers, emb_dim=args.emb, in_dim=1, out_dim=1)
+    # r_max = 10 (model default) with radius-5 graphs keeps edges away from the cutoff's fp32
+    # cancellation near r_max
     if args.workload == "mace":
-        return mod.MACEModel(r_max=radius, num_layers=args.layers, emb_dim=args.emb,
-                             correlation=3, max_ell=2, in_dim=1, out_dim=1)
-    return mod.TFNModel(r_max=radius, num_layers=args.layers, emb_dim=args.emb, max_ell=2,
-                        in_dim=1, out_dim=1)
+        return mod.MACEModel(num_layers=args.layers, emb_dim=args.emb, correlation=3,
+                             max_ell=2, in_dim=1, out_dim=1)
+    if args.workload == "gvp":
+        return mod.GVPGNNModel(num_layers=args.layers, s_dim=args.emb, v_dim=16, s_dim_edge=32,
+                               v_dim_edge=1, in_dim=1, out_dim=1)
+    return mod.TFNModel(num_layers=args.layers, emb_dim=args.emb, max_ell=2, in_dim=1,
+                        out_dim=1)
 
 
 def tp_bytes_per_edge(model):
@@ -104,6 +110,15 @@ def egnn_bwd_bytes_per_edge(d):
     return 16 + 2 * 2 * d * 4 + 24 + 5 * d * 4
 
 
+def gvp_flops_per_edge(s, v, se, ve):
+    """Reference message-function FLOPs per edge per layer, forward (SURVEY §8(d):
+    ~186 kFLOP at s=128, v=16, edge (32, 1)): 3 GVPs of the message function."""
+    h0, si0, vi0 = max(2 * v + ve, v), 2 * s + se, 2 * v + ve
+    g0 = 3 * vi0 * h0 + (h0 + si0) * s + 3 * h0 * v + s * v
+    g1 = 3 * v * v + (v + s) * s + 3 * v * v + s * v
+    return 2 * (g0 + 2 * g1)
+
+
 def egnn_flops_per_edge(d):
     """Algorithmic fp32 FLOPs per edge of the two fused edge kernels."""
     gemm = 2 * d * d
@@ -118,8 +133,8 @@ def cpu_baseline(g, args):
 
     threads = min(args.cpu_threads, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    if args.workload == "egnn":
-        frac = 0.25  # slab x < box / 4
+    if args.workload in ("egnn", "gvp"):
+        frac = 0.25 if args.workload == "egnn" else 0.1  # slab x < frac * box
         keep = g.pos[:, 0] < g.box * frac
         shape = "spatial slab"
     else:
@@ -135,7 +150,8 @@ def cpu_baseline(g, args):
     sub = Batch(torch.zeros(idx.numel(), dtype=torch.long), g.pos[idx], remap[ei[:, m]],
                 num_graphs=1)
     torch.manual_seed(0)
-    model = build_model(oegnn if args.workload == "egnn" else omace, args, g.radius)
+    from oracle import gvp as ogvp
+    model = build_model({"egnn": oegnn, "gvp": ogvp}.get(args.workload, omace), args, g.radius)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     y = torch.zeros(1)
 
@@ -239,6 +255,14 @@ def main():
                     "fwd_kernel_ms": ms_fwd,
                     "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
                     / (ms_fwd * 1e-3) / 1e12}
+        elif args.workload == "gvp":
+            # no single dominant HIP kernel yet (torch GEMMs on gathered rows): whole step
+            fl = gvp_flops_per_edge(args.emb, 16, 32, 1) * 3 * args.layers
+            achieved = fl * g.num_edges / (elapsed / args.steps) / 1e12
+            roof = {"kernel": "whole step (fwd+bwd, all kernels)", "kernel_prefix": "-",
+                    "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                    "traffic": None, "flops_per_edge": fl}
         else:
             # K7 is timed per chunk launch; algorithmic bytes = bytes/edge x edges per launch
             bf, bb = tp_bytes_per_edge(core)

@@ -113,17 +113,27 @@ class CSR:
             raise IndexError("index out of range in gmp CSR build")
 
 
-_CSR_CACHE = []  # [(index_tensor, version, n_seg, has_payload, CSR)] small LRU; holds refs
+_CSR_CACHE = []  # [(key, index_tensor, payload_tensor, CSR)] small LRU; holds strong refs
+
+
+def _tkey(t):
+    """Content identity of a (possibly view) tensor while a strong ref is held: storage
+    address, geometry and the version counter shared with its base (in-place writes bump it).
+    Views such as edge_index[1] taken repeatedly map to the same key."""
+    if t is None:
+        return None
+    return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, t.device, t._version)
 
 
 def get_csr(index, n_seg, payload=None):
-    """Cached CSR for `index` (keyed on tensor identity + version; holds a strong ref)."""
-    for k, (t, ver, ns, pl, csr) in enumerate(_CSR_CACHE):
-        if t is index and ver == index._version and ns == n_seg and pl is payload:
+    """Cached CSR for `index` (keyed on storage/geometry/version; holds a strong ref)."""
+    key = (_tkey(index), int(n_seg), _tkey(payload))
+    for k, (kk, _, _, csr) in enumerate(_CSR_CACHE):
+        if kk == key:
             _CSR_CACHE.insert(0, _CSR_CACHE.pop(k))
             return csr
     csr = CSR(index, n_seg, payload)
-    _CSR_CACHE.insert(0, (index, index._version, n_seg, payload, csr))
+    _CSR_CACHE.insert(0, (key, index, payload, csr))
     del _CSR_CACHE[16:]
     return csr
 

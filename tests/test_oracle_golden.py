@@ -71,3 +71,35 @@ def test_radial_golden(golden):
     torch.testing.assert_close(e, d["emb"], atol=ATOL, rtol=1e-6)
     (e * d["g_emb"]).sum().backward()
     torch.testing.assert_close(r.grad, d["grad_lengths"], atol=1e-4, rtol=1e-5)
+
+
+def test_gvp_layer_golden(golden):
+    from oracle import gvp as ogvp
+    d = golden("gvp_layer.pt")
+    layer = ogvp.GVPConvLayer((32, 4), (8, 1), activations=(torch.nn.functional.relu, None),
+                              vector_gate=True)
+    _load_params(layer, d)
+    layer.eval()  # the fixture was made in eval mode (no dropout)
+    xs = [d[k].clone().requires_grad_(True) for k in ("s", "v", "es", "ev")]
+    so, vo = layer((xs[0], xs[1]), d["edge_index"], (xs[2], xs[3]))
+    torch.testing.assert_close(so, d["out_s"], atol=ATOL, rtol=1e-5)
+    torch.testing.assert_close(vo, d["out_v"], atol=ATOL, rtol=1e-5)
+    ((so * d["g_s"]).sum() + (vo * d["g_v"]).sum()).backward()
+    for t, k in zip(xs, ("grad_s", "grad_v", "grad_es", "grad_ev")):
+        torch.testing.assert_close(t.grad, d[k], atol=1e-4, rtol=1e-4)
+    _check_grads(layer, d, atol=1e-4)
+
+
+def test_gvp_model_golden(golden):
+    from oracle import gvp as ogvp
+    d = golden("gvp_model.pt")
+    model = ogvp.GVPGNNModel(num_layers=2, in_dim=2, out_dim=1, s_dim=32, v_dim=4, s_dim_edge=8,
+                             v_dim_edge=1)
+    _load_params(model, d)
+    model.eval()
+    p = d["pos"].clone().requires_grad_(True)
+    y = model(B(atoms=d["atoms"], pos=p, edge_index=d["edge_index"], batch=d["batch"]))
+    torch.testing.assert_close(y, d["out"], atol=ATOL, rtol=1e-5)
+    y.sum().backward()
+    torch.testing.assert_close(p.grad, d["grad_pos"], atol=1e-4, rtol=1e-4)
+    _check_grads(model, d, atol=1e-4)
