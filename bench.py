@@ -180,13 +180,8 @@ def main():
     _, d_layers, d_emb = WORKLOADS[args.workload]
     args.layers = args.layers or d_layers
     args.emb = args.emb or d_emb
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from gmp_amd import dist as gdist
+    rank, world, local = gdist.init("nccl")
     dev = torch.device("cuda", local)
 
     import gmp_amd
@@ -197,9 +192,7 @@ def main():
     torch.manual_seed(0)
     model = build_model(gmp_amd, args, g.radius).to(dev)
     core = model
-    if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local],
-                                                          bucket_cap_mb=32)
+    model = gdist.wrap_ddp(model, local, bucket_cap_mb=32)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     batch = g.to(dev)
     y = torch.randn(1, device=dev)
@@ -213,10 +206,7 @@ def main():
     for _ in range(args.warmup):
         step()
 
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
+    barrier = gdist.barrier
 
     ops.KERNEL_TIMERS = {}
     barrier()
@@ -225,15 +215,8 @@ def main():
         step()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
-        e = torch.tensor([g.num_edges], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(e)
-        total_edges = e.item()
-    else:
-        total_edges = g.num_edges
+    elapsed = gdist.max_over_ranks(elapsed, dev)
+    total_edges = gdist.sum_over_ranks(g.num_edges, dev)
     timers = {k: ops.kernel_time_ms(k) for k in list(ops.KERNEL_TIMERS)}
     totals = {k: timers[k] * len(v) for k, v in ops.KERNEL_TIMERS.items()}
     ops.KERNEL_TIMERS = None

@@ -13,10 +13,11 @@ from .equivariant import (TensorProductConvLayer, MACEModel, TFNModel,  # noqa: 
                           RadialEmbeddingBlock, EquivariantProductBasisBlock,
                           SymmetricContraction, first_node_pooling)
 from .gvp import GVP, GVPConv, GVPConvLayer, GVPGNNModel  # noqa: F401
+from .schnet import SchNetModel, CFConv, InteractionBlock  # noqa: F401
 
 __all__ = ["scatter", "scatter_sum", "scatter_add", "scatter_mean", "scatter_max",
            "global_add_pool", "global_mean_pool", "MessagePassing", "EGNNLayer", "EGNNModel",
            "Batch", "collate", "radius_graph", "create_kchains", "TensorProductConvLayer",
            "MACEModel", "TFNModel", "RadialEmbeddingBlock", "EquivariantProductBasisBlock",
            "SymmetricContraction", "first_node_pooling", "GVP", "GVPConv", "GVPConvLayer",
-           "GVPGNNModel"]
+           "GVPGNNModel", "SchNetModel", "CFConv", "InteractionBlock"]
