@@ -93,7 +93,10 @@ class SchNetModel(nn.Module):
         self.pool = {"mean": global_mean_pool, "sum": global_add_pool}[pool]
 
     def forward(self, batch):
-        h = ops.gather(self.embedding.weight, batch.atoms, 0)
+        w, pad = self.embedding.weight, self.embedding.padding_idx
+        if pad is not None:  # nn.Embedding(padding_idx): that row receives no gradient
+            w = torch.cat([w[:pad], w[pad:pad + 1].detach(), w[pad + 1:]], 0)
+        h = ops.gather(w, batch.atoms, 0)
         row, col = batch.edge_index
         edge_weight = (ops.gather(batch.pos, row, 0) - ops.gather(batch.pos, col, 0)).norm(dim=-1)
         edge_attr = self.distance_expansion(edge_weight)
