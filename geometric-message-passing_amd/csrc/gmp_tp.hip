@@ -1,28 +1,30 @@
-// K7: e3nn FullyConnectedTensorProduct(in1, sh, out, shared_weights=False) with per-edge weights
-// + scatter-sum to the receiver (models/layers/tfn_layer.py:82-87), forward and backward.
+// K7: e3nn FullyConnectedTensorProduct(in1, sh, out, shared_weights=False) with per-edge weights,
+// the message half of models/layers/tfn_layer.py:82-87, forward and backward.
 //
-//   out[n, o, w, k] = sum_{e: ei0[e] = n} sum_{p -> o} sum_u W_e[p, u, w] z_e[p, u, k]
-//   z_e[p, u, k]    = alpha_p sum_{i,j} C_p[i, j, k] x[ei1[e], b1(p), u, i] Y_e[b2(p), j]
+//   msg[e, o, w, k] = sum_{p -> o} sum_u W_e[p, u, w] z_e[p, u, k]
+//   z_e[p, u, k]    = alpha_p sum_i x[ei1[e], b1(p), u, i] t_e[p, i, k],
+//   t_e[p, i, k]    = sum_j C_p[i, j, k] Y_e[b2(p), j]
 //
-// Edges are processed in receiver (ei0)-sorted order; a workgroup owns a node-aligned range of
-// a chunk of edges, so each receiver row is summed in one workgroup in a fixed order (no
-// atomics; a receiver split across two chunks is read-modify-written by consecutive launches on
-// the same stream).  The per-edge weights W_e (E_chunk x weight_numel, from the radial MLP,
-// models/layers/tfn_layer.py:73-77) are produced chunk by chunk by the caller, so the kernels
-// stream them once (HBM-bound: 4 * weight_numel bytes per edge per pass).
+// The per-edge weight rows W_e (weight_numel floats: 721 kB per edge for MACE-128) are produced
+// chunk by chunk by the radial MLP (library GEMM) and streamed exactly once here, so both
+// kernels are HBM-bound on that stream (forward: read W; backward: read W, write dW).
 //
-// Register layout: thread t = output channel w; each thread keeps its (2l_o+1) accumulators of
-// every output block in registers.  The output-block structure is a template parameter
-// (MACE: 0e,1o,2e ; TFN gated: 0e,0e,1o,2e) so all register indices are compile-time.
+// Work decomposition: one wave per workgroup, each wave owns a contiguous range of
+// receiver-sorted edge positions of the chunk (no receiver alignment: messages are written per
+// edge and summed per receiver afterwards by the deterministic segmented reduce, so the result is
+// independent of chunking and grid size).  Per edge and path, z_p (mul1 x (2lo+1)) is built in
+// LDS, then the weight rows are streamed with 16-byte loads: lanes split a row's mul_out outputs
+// (4 per lane) and rows are interleaved across lane groups; the output-block accumulators stay in
+// registers (block structure = template parameters: MACE 0e,1o,2e; TFN gated 0e,0e,1o,2e).
 #include "gmp_common.h"
 
 namespace gmp {
 namespace {
 
-constexpr int kTP = 128;          // threads per workgroup (max channel multiplicity)
 constexpr int kMaxPaths = 16;
-constexpr int kMaxIn = 1152;      // max in1 row dim
-constexpr int kMaxZ = 5120;       // max sum_p mul1 * (2lo+1)
+constexpr int kMaxIn = 1152;     // max in1 row dim
+constexpr int kMaxMul = 128;     // max mul1 / mul_out of a path
+constexpr int kMaxOut = 2048;    // max out row dim
 
 struct Path {
   int l1, l2, lo, mul1, mul_out, x_off, y_off, io, out_off, z_off, cg_off, pad;
@@ -37,341 +39,377 @@ struct Desc {
   int blk_off[4], blk_mul[4], blk_l[4];
 };
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+
 template <int L>
 struct Dim {
   static constexpr int v = 2 * L + 1;
 };
 
-// Node-aligned partition of the chunk [c0, c1) of receiver-sorted edges over G workgroups.
-__device__ __forceinline__ int64_t lower_bound64(const int64_t* __restrict__ a, int64_t n, int64_t v) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-__device__ __forceinline__ int64_t chunk_node_begin(const int64_t* __restrict__ rowptr,
-                                                    int64_t n_nodes, int64_t c0, int64_t c1,
-                                                    int64_t b, int64_t G) {
-  if (b <= 0) {  // node containing edge c0
-    int64_t n = lower_bound64(rowptr, n_nodes + 1, c0 + 1) - 1;
-    return n < 0 ? 0 : n;
-  }
-  if (b >= G) return lower_bound64(rowptr, n_nodes + 1, c1);
-  return lower_bound64(rowptr, n_nodes + 1, c0 + (c1 - c0) * b / G);
+__device__ __forceinline__ int pow2_ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
 }
 
-// z for one edge: zs[z_off + u*(2lo+1) + k] = alpha sum_ij C x Y  (threads over (p, u) pairs)
-__device__ void compute_z(const Path* sp, int n_paths, const float* sCG, const float* sx,
-                          const float* sy, float* zs) {
-  for (int p = 0; p < n_paths; ++p) {
-    const Path P = sp[p];
-    const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1;
-    const float* C = sCG + P.cg_off;
-    for (int u = threadIdx.x; u < P.mul1; u += blockDim.x) {
-      const float* xu = sx + P.x_off + u * d1;
-      for (int k = 0; k < d3; ++k) {
-        float s = 0.f;
-        for (int i = 0; i < d1; ++i) {
-          float t = 0.f;
-          for (int j = 0; j < d2; ++j) t += C[(i * d2 + j) * d3 + k] * sy[P.y_off + j];
-          s += xu[i] * t;
-        }
-        zs[P.z_off + u * d3 + k] = P.alpha * s;
+// LDS layout of one wave (floats)
+struct Smem {
+  float* cg;   // cg_len
+  float* x;    // in_dim (sender row)
+  float* y;    // 16 (SH row)
+  float* t;    // 32 (t_p[i, k] of the current path)
+  float* z;    // kMaxMul * 5 (z_p, in place dz_p in the backward)
+  float* g;    // out_dim (backward: receiver gradient row)
+  float* dx;   // in_dim (backward: dx row accumulator)
+};
+
+__device__ __forceinline__ Smem carve(float* base, int cg_len, int in_dim, int out_dim) {
+  Smem s;
+  s.cg = base;
+  s.x = s.cg + ((cg_len + 3) & ~3);
+  s.y = s.x + ((in_dim + 3) & ~3);
+  s.t = s.y + 16;
+  s.z = s.t + 32;
+  s.g = s.z + kMaxMul * 5;
+  s.dx = s.g + ((out_dim + 3) & ~3);
+  return s;
+}
+
+// stage the sender row and the SH row of edge (sorted position) e
+__device__ __forceinline__ void stage_edge(const Desc& d, const float* __restrict__ x,
+                                           const float* __restrict__ sh, int64_t src, int64_t eo,
+                                           Smem& s, int lane) {
+  const float* xr = x + src * d.in_dim;
+  if ((d.in_dim & 3) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(xr);
+    float4* s4 = reinterpret_cast<float4*>(s.x);
+    for (int i = lane; i < (d.in_dim >> 2); i += kWave) s4[i] = x4[i];
+  } else {
+    for (int i = lane; i < d.in_dim; i += kWave) s.x[i] = xr[i];
+  }
+  if (lane < d.sh_dim) s.y[lane] = sh[eo * d.sh_dim + lane];
+}
+
+// t_p[i, k] = sum_j C[i, j, k] Y[y_off + j], then z_p[u, k] = alpha sum_i x[x_off + u d1 + i] t[i, k]
+__device__ __forceinline__ void build_z(const Path& P, Smem& s, int lane) {
+  const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1;
+  if (lane < d1 * d3) {
+    const int i = lane / d3, k = lane - i * d3;
+    const float* C = s.cg + P.cg_off;
+    float a = 0.f;
+    for (int j = 0; j < d2; ++j) a += C[(i * d2 + j) * d3 + k] * s.y[P.y_off + j];
+    s.t[lane] = a;
+  }
+  __syncthreads();
+  for (int u = lane; u < P.mul1; u += kWave) {
+    const float* xu = s.x + P.x_off + u * d1;
+    for (int k = 0; k < d3; ++k) {
+      float a = 0.f;
+      for (int i = 0; i < d1; ++i) a += xu[i] * s.t[i * d3 + k];
+      s.z[u * d3 + k] = P.alpha * a;
+    }
+  }
+  __syncthreads();
+}
+
+// -------------------------------------------------------------------------------- forward
+// lanes: Lr = pow2 >= mul_out/4 lanes per row (one float4 of outputs each), R = 64/Lr rows per
+// load instruction; acc[q][k] = partial msg[w = 4c + q, k] over the rows of lane group r.
+template <int D>
+__device__ __forceinline__ void fwd_path(const float* __restrict__ Wp, const float* zs, int m1,
+                                         int mo, int lane, float (&acc)[4][D]) {
+  const int f4 = mo >> 2;
+  const int Lr = pow2_ceil(f4), R = kWave / Lr;
+  const int r = lane / Lr, c = lane - r * Lr;
+  if (c >= f4) return;
+  const v4f* __restrict__ base = reinterpret_cast<const v4f*>(Wp) + c;
+  constexpr int U = 8;
+  int u = r;
+  for (; u + (U - 1) * R < m1; u += U * R) {
+    v4f w[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) w[q] = __builtin_nontemporal_load(base + (int64_t)(u + q * R) * f4);
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const float* zu = zs + (u + q * R) * D;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const float zk = zu[k];
+        acc[0][k] += w[q].x * zk;
+        acc[1][k] += w[q].y * zk;
+        acc[2][k] += w[q].z * zk;
+        acc[3][k] += w[q].w * zk;
       }
+    }
+  }
+  for (; u < m1; u += R) {
+    const v4f w = __builtin_nontemporal_load(base + (int64_t)u * f4);
+    const float* zu = zs + u * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const float zk = zu[k];
+      acc[0][k] += w.x * zk;
+      acc[1][k] += w.y * zk;
+      acc[2][k] += w.z * zk;
+      acc[3][k] += w.w * zk;
     }
   }
 }
 
 template <int D>
-__device__ __forceinline__ void tp_path_accumulate(const float* __restrict__ wrow, const float* zs,
-                                                   int mul1, int mul_out, int z_off, int t,
-                                                   float (&acc)[D]) {
-  if (t >= mul_out) return;
-  int u = 0;
-  for (; u + 4 <= mul1; u += 4) {
-    float wv[4];
+__device__ __forceinline__ void zero_acc(float (&a)[4][D]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wv[q] = wrow[(int64_t)(u + q) * mul_out + t];
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int k = 0; k < D; ++k) a[q][k] = 0.f;
+}
+
+// reduce the row groups and write block b of the message row: msg[blk_off + w*D + k]
+template <int D>
+__device__ __forceinline__ void fwd_store(float (&acc)[4][D], int mo, float* __restrict__ row,
+                                          int lane) {
+  const int f4 = mo >> 2;
+  const int Lr = pow2_ceil(f4);
+  for (int s = Lr; s < kWave; s <<= 1)
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] += wv[q] * zs[z_off + (u + q) * D + k];
-  }
-  for (; u < mul1; ++u) {
-    const float wv = wrow[(int64_t)u * mul_out + t];
+      for (int k = 0; k < D; ++k) acc[q][k] += __shfl_xor(acc[q][k], s);
+  if (lane < f4) {
+    float* o = row + 4 * lane * D;
 #pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] += wv * zs[z_off + u * D + k];
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < D; ++k) o[q * D + k] = acc[q][k];
   }
 }
 
 template <int NB, int L0, int L1, int L2, int L3>
-struct Acc {
-  float a0[Dim<L0>::v], a1[Dim<L1>::v], a2[Dim<L2>::v], a3[Dim<L3>::v];
-  __device__ void zero() {
-#pragma unroll
-    for (int k = 0; k < Dim<L0>::v; ++k) a0[k] = 0.f;
-#pragma unroll
-    for (int k = 0; k < Dim<L1>::v; ++k) a1[k] = 0.f;
-#pragma unroll
-    for (int k = 0; k < Dim<L2>::v; ++k) a2[k] = 0.f;
-#pragma unroll
-    for (int k = 0; k < Dim<L3>::v; ++k) a3[k] = 0.f;
-  }
-};
-
-template <int NB, int L0, int L1, int L2, int L3, int LB>
-__device__ __forceinline__ float* acc_block(Acc<NB, L0, L1, L2, L3>& A);
-
-// -------------------------------------------------------------------------------- forward
-template <int NB, int L0, int L1, int L2, int L3>
-__global__ __launch_bounds__(kTP) void tp_fwd_kernel(
-    Desc desc, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+__global__ __launch_bounds__(kWave) void tp_fwd_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
     const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ W,
-    const int64_t* __restrict__ rowptr, const int64_t* __restrict__ src_sorted,
-    const int64_t* __restrict__ perm, int64_t n_nodes, int64_t c0, int64_t c1,
-    float* __restrict__ out) {
+    const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t c0,
+    int64_t c1, float* __restrict__ msg) {
   __shared__ Path sp[kMaxPaths];
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sCG = smem;                 // cg_len
-  float* sx = sCG + cg_len;          // in_dim
-  float* sy = sx + desc.in_dim;      // 16
-  float* zs = sy + 16;               // z_size
-  const int t = threadIdx.x;
-  for (int i = t; i < desc.n_paths; i += blockDim.x) sp[i] = paths[i];
-  for (int i = t; i < cg_len; i += blockDim.x) sCG[i] = cg[i];
+  Smem s = carve(smem, cg_len, d.in_dim, d.out_dim);
+  const int lane = threadIdx.x;
+  for (int i = lane; i < d.n_paths; i += kWave) sp[i] = paths[i];
+  for (int i = lane; i < cg_len; i += kWave) s.cg[i] = cg[i];
   __syncthreads();
-
-  const int64_t G = gridDim.x;
-  const int64_t nb = chunk_node_begin(rowptr, n_nodes, c0, c1, blockIdx.x, G);
-  const int64_t ne = chunk_node_begin(rowptr, n_nodes, c0, c1, blockIdx.x + 1, G);
-  for (int64_t n = nb; n < ne; ++n) {
-    int64_t e0 = rowptr[n], e1 = rowptr[n + 1];
-    e0 = e0 < c0 ? c0 : e0;
-    e1 = e1 > c1 ? c1 : e1;
-    if (e0 >= e1) continue;
-    Acc<NB, L0, L1, L2, L3> A;
-    A.zero();
-    for (int64_t e = e0; e < e1; ++e) {
-      const int64_t s = src_sorted[e];      // node gathered from (ei1)
-      const int64_t eo = perm[e];           // original edge id (for sh)
-      for (int i = t; i < desc.in_dim; i += blockDim.x) sx[i] = x[s * desc.in_dim + i];
-      if (t < desc.sh_dim) sy[t] = sh[eo * desc.sh_dim + t];
-      __syncthreads();
-      compute_z(sp, desc.n_paths, sCG, sx, sy, zs);
-      __syncthreads();
-      const float* We = W + (e - c0) * desc.weight_numel;
-      for (int p = 0; p < desc.n_paths; ++p) {
-        const Path P = sp[p];
-        const float* wrow = We + P.w_off;
-        switch (P.io) {
-          case 0: tp_path_accumulate<Dim<L0>::v>(wrow, zs, P.mul1, P.mul_out, P.z_off, t, A.a0); break;
-          case 1: if (NB > 1) tp_path_accumulate<Dim<L1>::v>(wrow, zs, P.mul1, P.mul_out, P.z_off, t, A.a1); break;
-          case 2: if (NB > 2) tp_path_accumulate<Dim<L2>::v>(wrow, zs, P.mul1, P.mul_out, P.z_off, t, A.a2); break;
-          default: if (NB > 3) tp_path_accumulate<Dim<L3>::v>(wrow, zs, P.mul1, P.mul_out, P.z_off, t, A.a3); break;
-        }
+  const int64_t n = c1 - c0, G = gridDim.x, b = blockIdx.x;
+  const int64_t e_begin = c0 + n * b / G, e_end = c0 + n * (b + 1) / G;
+  for (int64_t e = e_begin; e < e_end; ++e) {
+    stage_edge(d, x, sh, src_sorted[e], perm[e], s, lane);
+    __syncthreads();
+    float a0[4][Dim<L0>::v], a1[4][Dim<L1>::v], a2[4][Dim<L2>::v], a3[4][Dim<L3>::v];
+    zero_acc(a0);
+    zero_acc(a1);
+    zero_acc(a2);
+    zero_acc(a3);
+    const float* We = W + (e - c0) * d.weight_numel;
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = sp[p];
+      build_z(P, s, lane);
+      const float* Wp = We + P.w_off;
+      switch (P.io) {
+        case 0: fwd_path(Wp, s.z, P.mul1, P.mul_out, lane, a0); break;
+        case 1: if (NB > 1) fwd_path(Wp, s.z, P.mul1, P.mul_out, lane, a1); break;
+        case 2: if (NB > 2) fwd_path(Wp, s.z, P.mul1, P.mul_out, lane, a2); break;
+        default: if (NB > 3) fwd_path(Wp, s.z, P.mul1, P.mul_out, lane, a3); break;
       }
-      __syncthreads();  // before the next edge overwrites sx / zs
+      __syncthreads();  // z is rebuilt for the next path
     }
-    float* orow = out + n * desc.out_dim;
-#define GMP_TP_STORE(B, ARR, L)                                                   \
-    if (NB > B && t < desc.blk_mul[B]) {                                          \
-      float* o = orow + desc.blk_off[B] + t * Dim<L>::v;                          \
-      _Pragma("unroll") for (int k = 0; k < Dim<L>::v; ++k) o[k] += A.ARR[k];     \
-    }
-    GMP_TP_STORE(0, a0, L0)
-    GMP_TP_STORE(1, a1, L1)
-    GMP_TP_STORE(2, a2, L2)
-    GMP_TP_STORE(3, a3, L3)
-#undef GMP_TP_STORE
+    float* row = msg + e * d.out_dim;
+    fwd_store(a0, d.blk_mul[0], row + d.blk_off[0], lane);
+    if (NB > 1) fwd_store(a1, d.blk_mul[1], row + d.blk_off[1], lane);
+    if (NB > 2) fwd_store(a2, d.blk_mul[2], row + d.blk_off[2], lane);
+    if (NB > 3) fwd_store(a3, d.blk_mul[3], row + d.blk_off[3], lane);
   }
 }
 
 // -------------------------------------------------------------------------------- backward
-// Per edge (grad of the receiver row g = dL/dout[n], same for all edges of n):
+// Per edge, with g = dL/dout[receiver] (the receiver row of the output gradient):
 //   dW_e[p,u,w] = sum_k z[p,u,k] g[o(p),w,k]
 //   dz[p,u,k]   = sum_w W_e[p,u,w] g[o(p),w,k]
-//   dx_e[b1,u,i] = sum_{p on b1} alpha_p sum_{j,k} C[i,j,k] Y[j] dz[p,u,k]
+//   dx_e[b1,u,i] = sum_{p on b1} alpha_p sum_k dz[p,u,k] t_p[i,k]
 //   dY_e[j]      = sum_p alpha_p sum_{u,i,k} C[i,j,k] x[u,i] dz[p,u,k]
-constexpr int kRows = 16;  // u rows per W tile (kTP / 8 threads per row)
-
+// Row streaming: Lr = min(8, pow2 >= mul_out/4) lanes per row, each lane nq = f4/Lr float4
+// columns (interleaved so that a load instruction covers whole 128-byte row segments); dz over a
+// row is a log2(Lr)-step shuffle reduction, written in place over z in LDS.
 template <int D>
-__device__ __forceinline__ void tp_bwd_path(const float* __restrict__ Wp, float* __restrict__ dWp,
-                                            const float* zs, const float* sg, float* dzs,
-                                            float* sWt, int mul1, int mul_out, int z_off,
-                                            int g_off, int t) {
-  // thread t's gradient row of this output block
-  float gt[D];
+__device__ __forceinline__ void bwd_path(const float* __restrict__ Wp, float* __restrict__ dWp,
+                                         float* zs, const float* gb, int m1, int mo, int lane) {
+  const int f4 = mo >> 2;
+  const int Lr = pow2_ceil(f4) < 8 ? pow2_ceil(f4) : 8;
+  const int nq = (f4 + Lr - 1) / Lr;   // <= 4 (mo <= 128)
+  const int R = kWave / Lr;
+  const int r = lane / Lr, c = lane - r * Lr;
+  float g[4][4][D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) gt[k] = (t < mul_out) ? sg[g_off + t * D + k] : 0.f;
-  const int row = t >> 3, part = t & 7;
-  const int cols = (mul_out + 7) / 8;
-  for (int u0 = 0; u0 < mul1; u0 += kRows) {
-    const int nrows = (mul1 - u0 < kRows) ? mul1 - u0 : kRows;
-    // coalesced W tile load (nrows x mul_out) into LDS; dW for the same tile
-    for (int r = 0; r < nrows; ++r) {
-      if (t < mul_out) {
-        const int u = u0 + r;
-        sWt[r * 129 + t] = Wp[(int64_t)u * mul_out + t];
-        float s = 0.f;
+  for (int t = 0; t < 4; ++t) {
+    const int q = c + Lr * t;
 #pragma unroll
-        for (int k = 0; k < D; ++k) s += zs[z_off + u * D + k] * gt[k];
-        dWp[(int64_t)u * mul_out + t] = s;
-      }
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < D; ++k) g[t][j][k] = (t < nq && q < f4) ? gb[(4 * q + j) * D + k] : 0.f;
+  }
+  const v4f* __restrict__ W4 = reinterpret_cast<const v4f*>(Wp);
+  v4f* __restrict__ dW4 = reinterpret_cast<v4f*>(dWp);
+  const int iters = (m1 + R - 1) / R;
+  for (int it = 0; it < iters; ++it) {
+    const int u = it * R + r;
+    const bool valid = u < m1;
+    float z[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) z[k] = valid ? zs[u * D + k] : 0.f;
+    v4f w[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int q = c + Lr * t;
+      w[t] = (valid && t < nq && q < f4) ? __builtin_nontemporal_load(W4 + (int64_t)u * f4 + q)
+                                         : v4f{0.f, 0.f, 0.f, 0.f};
     }
-    __syncthreads();
-    // dz: 8 threads per row, each a contiguous slice of the channels, shuffle-reduced
     float dz[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) dz[k] = 0.f;
-    if (row < nrows) {
-      for (int c = part * cols; c < (part + 1) * cols && c < mul_out; ++c) {
-        const float wv = sWt[row * 129 + c];
 #pragma unroll
-        for (int k = 0; k < D; ++k) dz[k] += wv * sg[g_off + c * D + k];
+    for (int t = 0; t < 4; ++t) {
+      const int q = c + Lr * t;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) a += z[k] * g[t][j][k];
+        o[j] = a;
+      }
+      if (valid && t < nq && q < f4)
+        __builtin_nontemporal_store(v4f{o[0], o[1], o[2], o[3]}, dW4 + (int64_t)u * f4 + q);
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        dz[k] += w[t].x * g[t][0][k] + w[t].y * g[t][1][k] + w[t].z * g[t][2][k] + w[t].w * g[t][3][k];
+    }
+    for (int s2 = 1; s2 < Lr; s2 <<= 1)
+#pragma unroll
+      for (int k = 0; k < D; ++k) dz[k] += __shfl_xor(dz[k], s2);
+    if (valid && c == 0) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) zs[u * D + k] = dz[k];  // in place: row u read above by this group
+    }
+  }
+}
+
+// dx / dY contributions of one path from dz_p (in s.z)
+__device__ __forceinline__ void bwd_inputs(const Path& P, Smem& s, int lane, float (&dyp)[9]) {
+  const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1;
+  const float* C = s.cg + P.cg_off;
+  for (int u = lane; u < P.mul1; u += kWave) {  // lane owns u (same for every path): no race
+    const float* dz = s.z + u * d3;
+    const float* xu = s.x + P.x_off + u * d1;
+    float* dxu = s.dx + P.x_off + u * d1;
+    for (int i = 0; i < d1; ++i) {
+      float a = 0.f;
+      for (int k = 0; k < d3; ++k) a += dz[k] * s.t[i * d3 + k];
+      dxu[i] += P.alpha * a;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {  // compile-time register index for dyp
+        const int j = jj - P.y_off;
+        if (j < 0 || j >= d2) continue;
+        float cz = 0.f;
+        for (int k = 0; k < d3; ++k) cz += C[(i * d2 + j) * d3 + k] * dz[k];
+        dyp[jj] += P.alpha * cz * xu[i];
       }
     }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1)
-#pragma unroll
-      for (int k = 0; k < D; ++k) dz[k] += __shfl_xor(dz[k], m);
-    if (row < nrows && part == 0) {
-#pragma unroll
-      for (int k = 0; k < D; ++k) dzs[z_off + (u0 + row) * D + k] = dz[k];
-    }
-    __syncthreads();
   }
 }
 
 template <int NB, int L0, int L1, int L2, int L3>
-__global__ __launch_bounds__(kTP) void tp_bwd_kernel(
-    Desc desc, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+__global__ __launch_bounds__(kWave) void tp_bwd_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
     const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ W,
-    const int64_t* __restrict__ rowptr, const int64_t* __restrict__ src_sorted,
-    const int64_t* __restrict__ perm, int64_t n_nodes, int64_t c0, int64_t c1,
-    const float* __restrict__ gout, float* __restrict__ dW, float* __restrict__ dx_edge,
-    float* __restrict__ dY_edge) {
+    const int64_t* __restrict__ recv_sorted, const int64_t* __restrict__ src_sorted,
+    const int64_t* __restrict__ perm, int64_t c0, int64_t c1, const float* __restrict__ gout,
+    float* __restrict__ dW, float* __restrict__ dx_edge, float* __restrict__ dY_edge) {
   __shared__ Path sp[kMaxPaths];
-  __shared__ float sred[kTP / 64][16];
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sCG = smem;
-  float* sx = sCG + cg_len;
-  float* sy = sx + desc.in_dim;
-  float* zs = sy + 16;
-  float* dzs = zs + desc.z_size;
-  float* sg = dzs + desc.z_size;            // out_dim
-  float* sWt = sg + desc.out_dim;           // kRows x 129
-  const int t = threadIdx.x;
-  for (int i = t; i < desc.n_paths; i += blockDim.x) sp[i] = paths[i];
-  for (int i = t; i < cg_len; i += blockDim.x) sCG[i] = cg[i];
+  Smem s = carve(smem, cg_len, d.in_dim, d.out_dim);
+  const int lane = threadIdx.x;
+  for (int i = lane; i < d.n_paths; i += kWave) sp[i] = paths[i];
+  for (int i = lane; i < cg_len; i += kWave) s.cg[i] = cg[i];
   __syncthreads();
-
-  const int64_t G = gridDim.x;
-  const int64_t nb = chunk_node_begin(rowptr, n_nodes, c0, c1, blockIdx.x, G);
-  const int64_t ne = chunk_node_begin(rowptr, n_nodes, c0, c1, blockIdx.x + 1, G);
-  for (int64_t n = nb; n < ne; ++n) {
-    int64_t e0 = rowptr[n], e1 = rowptr[n + 1];
-    e0 = e0 < c0 ? c0 : e0;
-    e1 = e1 > c1 ? c1 : e1;
-    if (e0 >= e1) continue;
-    for (int i = t; i < desc.out_dim; i += blockDim.x) sg[i] = gout[n * desc.out_dim + i];
-    for (int64_t e = e0; e < e1; ++e) {
-      const int64_t s = src_sorted[e];
-      const int64_t eo = perm[e];
-      for (int i = t; i < desc.in_dim; i += blockDim.x) sx[i] = x[s * desc.in_dim + i];
-      if (t < desc.sh_dim) sy[t] = sh[eo * desc.sh_dim + t];
-      __syncthreads();
-      compute_z(sp, desc.n_paths, sCG, sx, sy, zs);
-      __syncthreads();
-      const float* We = W + (e - c0) * desc.weight_numel;
-      float* dWe = dW + (e - c0) * desc.weight_numel;
-      for (int p = 0; p < desc.n_paths; ++p) {
-        const Path P = sp[p];
-        const int g_off = desc.blk_off[P.io];
-        switch (P.lo) {
-          case 0: tp_bwd_path<1>(We + P.w_off, dWe + P.w_off, zs, sg, dzs, sWt, P.mul1, P.mul_out, P.z_off, g_off, t); break;
-          case 1: tp_bwd_path<3>(We + P.w_off, dWe + P.w_off, zs, sg, dzs, sWt, P.mul1, P.mul_out, P.z_off, g_off, t); break;
-          default: tp_bwd_path<5>(We + P.w_off, dWe + P.w_off, zs, sg, dzs, sWt, P.mul1, P.mul_out, P.z_off, g_off, t); break;
-        }
-      }
-      // dx_e (threads over in-row entries) and dY_e partials (threads over (p, u))
-      float* dxe = dx_edge + e * desc.in_dim;
-      for (int i = t; i < desc.in_dim; i += blockDim.x) dxe[i] = 0.f;
-      __syncthreads();
-      float dyp[9];
-#pragma unroll
-      for (int j = 0; j < 9; ++j) dyp[j] = 0.f;
-      for (int p = 0; p < desc.n_paths; ++p) {
-        const Path P = sp[p];
-        const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1;
-        const float* C = sCG + P.cg_off;
-        for (int u = t; u < P.mul1; u += blockDim.x) {
-          const float* dz = dzs + P.z_off + u * d3;
-          const float* xu = sx + P.x_off + u * d1;
-          for (int i = 0; i < d1; ++i) {
-            float acc = 0.f;
-#pragma unroll
-            for (int jj = 0; jj < 9; ++jj) {  // compile-time register index for dyp
-              const int j = jj - P.y_off;
-              if (j < 0 || j >= d2) continue;
-              float cz = 0.f;
-              for (int k = 0; k < d3; ++k) cz += C[(i * d2 + j) * d3 + k] * dz[k];
-              acc += cz * sy[jj];
-              dyp[jj] += P.alpha * cz * xu[i];
-            }
-            // a thread owns row u of block b1 for every path on that block: no race
-            dxe[P.x_off + u * d1 + i] += P.alpha * acc;
-          }
-        }
-      }
-      // block reduction of dY partials
-#pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        float v = dyp[j];
-        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-        dyp[j] = v;
-      }
-      if ((t & 63) == 0) {
-#pragma unroll
-        for (int j = 0; j < 9; ++j) sred[t >> 6][j] = dyp[j];
-      }
-      __syncthreads();
-      if (t < desc.sh_dim) {
-        float v = 0.f;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += sred[w][t];
-        dY_edge[e * desc.sh_dim + t] = v;
-      }
-      __syncthreads();
+  const int64_t n = c1 - c0, G = gridDim.x, b = blockIdx.x;
+  const int64_t e_begin = c0 + n * b / G, e_end = c0 + n * (b + 1) / G;
+  int64_t cur = -1;
+  for (int64_t e = e_begin; e < e_end; ++e) {
+    const int64_t rcv = recv_sorted[e];
+    if (rcv != cur) {  // receiver gradient row (shared by the receiver's consecutive edges)
+      for (int i = lane; i < d.out_dim; i += kWave) s.g[i] = gout[rcv * d.out_dim + i];
+      cur = rcv;
     }
+    stage_edge(d, x, sh, src_sorted[e], perm[e], s, lane);
+    for (int i = lane; i < d.in_dim; i += kWave) s.dx[i] = 0.f;
+    __syncthreads();
+    float dyp[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) dyp[j] = 0.f;
+    const float* We = W + (e - c0) * d.weight_numel;
+    float* dWe = dW + (e - c0) * d.weight_numel;
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = sp[p];
+      build_z(P, s, lane);
+      const float* gb = s.g + d.blk_off[P.io];
+      switch (P.lo) {
+        case 0: bwd_path<1>(We + P.w_off, dWe + P.w_off, s.z, gb, P.mul1, P.mul_out, lane); break;
+        case 1: bwd_path<3>(We + P.w_off, dWe + P.w_off, s.z, gb, P.mul1, P.mul_out, lane); break;
+        default: bwd_path<5>(We + P.w_off, dWe + P.w_off, s.z, gb, P.mul1, P.mul_out, lane); break;
+      }
+      __syncthreads();
+      bwd_inputs(P, s, lane, dyp);
+      __syncthreads();  // z / t are rebuilt for the next path
+    }
+    float* dxr = dx_edge + e * d.in_dim;
+    for (int i = lane; i < d.in_dim; i += kWave) dxr[i] = s.dx[i];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      float v = dyp[j];
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+      dyp[j] = v;
+    }
+    if (lane < d.sh_dim) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) v = (lane == j) ? dyp[j] : v;
+      dY_edge[e * d.sh_dim + lane] = v;
+    }
+    __syncthreads();
   }
 }
 
 bool desc_ok(const Desc& d, int layout) {
   if (d.n_paths <= 0 || d.n_paths > kMaxPaths || d.in_dim <= 0 || d.in_dim > kMaxIn ||
-      d.z_size <= 0 || d.z_size > kMaxZ || d.sh_dim != 9 || d.weight_numel <= 0)
+      d.out_dim <= 0 || d.out_dim > kMaxOut || d.sh_dim != 9 || d.weight_numel <= 0 ||
+      (d.weight_numel & 3) != 0)
     return false;
   if (d.n_blocks != (layout == 0 ? 3 : 4)) return false;
   int dim = 0;
   for (int b = 0; b < d.n_blocks; ++b) {
-    if (d.blk_mul[b] <= 0 || d.blk_mul[b] > kTP || d.blk_off[b] != dim) return false;
-    dim += d.blk_mul[b] * (2 * d.blk_l[b] + 1);
+    const int m = d.blk_mul[b];
+    if (m <= 0 || m > kMaxMul || (m & 3) != 0 || d.blk_off[b] != dim) return false;
+    dim += m * (2 * d.blk_l[b] + 1);
   }
   return dim == d.out_dim;
 }
 
-size_t fwd_smem(const Desc& d, int cg_len) {
-  return (size_t)(cg_len + d.in_dim + 16 + d.z_size) * sizeof(float);
-}
-size_t bwd_smem(const Desc& d, int cg_len) {
-  return (size_t)(cg_len + d.in_dim + 16 + 2 * d.z_size + d.out_dim + kRows * 129) * sizeof(float);
+size_t smem_bytes(const Desc& d, int cg_len, bool bwd) {
+  size_t f = (size_t)((cg_len + 3) & ~3) + ((d.in_dim + 3) & ~3) + 16 + 32 + kMaxMul * 5;
+  if (bwd) f += (size_t)((d.out_dim + 3) & ~3) + d.in_dim;
+  return f * sizeof(float);
 }
 
 int64_t grid_for_chunk(int64_t edges) {
-  int64_t g = ceil_div(edges, 8);  // ~8 edges (a few receivers) per workgroup
-  const int64_t cap = (int64_t)device_cu_count() * 8;
-  if (g > cap) g = cap;
+  const int64_t cap = (int64_t)device_cu_count() * 8;  // ~8 resident waves per CU
+  int64_t g = edges < cap ? edges : cap;
   return g < 1 ? 1 : g;
 }
 
@@ -391,60 +429,55 @@ extern "C" {
 /* layout codes: 0 = out blocks (0e, 1o, 2e) [MACE]; 1 = (0e, 0e, 1o, 2e) [TFN gated] */
 int gmp_tp_conv_fwd_f32(int layout, const void* desc_host, const void* paths_dev,
                         const float* cg_dev, int cg_len, const float* x, const float* sh,
-                        const float* W, const int64_t* rowptr, const int64_t* src_sorted,
-                        const int64_t* perm, int64_t n_nodes, int64_t c0, int64_t c1, float* out,
-                        void* stream) {
-  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && W && rowptr && src_sorted && perm && out);
+                        const float* W, const int64_t* src_sorted, const int64_t* perm,
+                        int64_t c0, int64_t c1, float* msg, void* stream) {
+  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && W && src_sorted && perm && msg);
   const Desc d = *reinterpret_cast<const Desc*>(desc_host);
   GMP_CHECK_ARG(desc_ok(d, layout) && cg_len > 0 && cg_len <= 4096);
   GMP_CHECK_ARG(c0 >= 0 && c1 >= c0);
   if (c1 == c0) return GMP_OK;
   hipStream_t s = as_stream(stream);
-  const size_t smem = fwd_smem(d, cg_len);
-  GMP_CHECK_ARG(smem <= 160 * 1024);
+  const size_t smem = smem_bytes(d, cg_len, false);
+  GMP_CHECK_ARG(smem <= 64 * 1024);
   const unsigned G = (unsigned)grid_for_chunk(c1 - c0);
   int rc;
   if (layout == 0) {
     auto k = tp_fwd_kernel<3, 0, 1, 2, 0>;
     if ((rc = set_smem(k, smem))) return rc;
-    k<<<G, kTP, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, rowptr, src_sorted, perm, n_nodes, c0, c1, out);
-  } else if (layout == 1) {
+    k<<<G, kWave, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, src_sorted, perm, c0, c1, msg);
+  } else {
     auto k = tp_fwd_kernel<4, 0, 0, 1, 2>;
     if ((rc = set_smem(k, smem))) return rc;
-    k<<<G, kTP, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, rowptr, src_sorted, perm, n_nodes, c0, c1, out);
-  } else {
-    return GMP_ERR_UNSUPPORTED;
+    k<<<G, kWave, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, src_sorted, perm, c0, c1, msg);
   }
   return launch_status();
 }
 
 int gmp_tp_conv_bwd_f32(int layout, const void* desc_host, const void* paths_dev,
                         const float* cg_dev, int cg_len, const float* x, const float* sh,
-                        const float* W, const int64_t* rowptr, const int64_t* src_sorted,
-                        const int64_t* perm, int64_t n_nodes, int64_t c0, int64_t c1,
-                        const float* gout, float* dW, float* dx_edge, float* dY_edge,
-                        void* stream) {
-  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && W && rowptr && src_sorted && perm);
+                        const float* W, const int64_t* recv_sorted, const int64_t* src_sorted,
+                        const int64_t* perm, int64_t c0, int64_t c1, const float* gout,
+                        float* dW, float* dx_edge, float* dY_edge, void* stream) {
+  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && W && recv_sorted && src_sorted &&
+                perm);
   GMP_CHECK_ARG(gout && dW && dx_edge && dY_edge);
   const Desc d = *reinterpret_cast<const Desc*>(desc_host);
   GMP_CHECK_ARG(desc_ok(d, layout) && cg_len > 0 && cg_len <= 4096);
-  GMP_CHECK_ARG(c0 >= 0 && c1 >= c0 && d.sh_dim <= 9);
+  GMP_CHECK_ARG(c0 >= 0 && c1 >= c0);
   if (c1 == c0) return GMP_OK;
   hipStream_t s = as_stream(stream);
-  const size_t smem = bwd_smem(d, cg_len);
-  GMP_CHECK_ARG(smem <= 160 * 1024);
+  const size_t smem = smem_bytes(d, cg_len, true);
+  GMP_CHECK_ARG(smem <= 64 * 1024);
   const unsigned G = (unsigned)grid_for_chunk(c1 - c0);
   int rc;
   if (layout == 0) {
     auto k = tp_bwd_kernel<3, 0, 1, 2, 0>;
     if ((rc = set_smem(k, smem))) return rc;
-    k<<<G, kTP, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, rowptr, src_sorted, perm, n_nodes, c0, c1, gout, dW, dx_edge, dY_edge);
-  } else if (layout == 1) {
+    k<<<G, kWave, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, recv_sorted, src_sorted, perm, c0, c1, gout, dW, dx_edge, dY_edge);
+  } else {
     auto k = tp_bwd_kernel<4, 0, 0, 1, 2>;
     if ((rc = set_smem(k, smem))) return rc;
-    k<<<G, kTP, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, rowptr, src_sorted, perm, n_nodes, c0, c1, gout, dW, dx_edge, dY_edge);
-  } else {
-    return GMP_ERR_UNSUPPORTED;
+    k<<<G, kWave, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, recv_sorted, src_sorted, perm, c0, c1, gout, dW, dx_edge, dY_edge);
   }
   return launch_status();
 }

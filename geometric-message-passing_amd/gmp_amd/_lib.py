@@ -70,9 +70,9 @@ SIGNATURES = {
     "gmp_edge_featurize_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32,
                                            c_vp, c_vp, c_vp, c_vp]),
     "gmp_tp_conv_fwd_f32": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                    c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+                                    c_i64, c_i64, c_vp, c_vp]),
     "gmp_tp_conv_bwd_f32": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                    c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                    c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

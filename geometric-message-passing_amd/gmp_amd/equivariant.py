@@ -261,6 +261,7 @@ class TPGraph:
         self.rowptr = self.recv_csr.rowptr
         self.perm = self.recv_csr.perm
         self.src_sorted = self.recv_csr.payload_sorted
+        self.recv_sorted = self.recv_csr.sorted
         self.src_csr = ops.CSR(self.src_sorted, self.num_nodes)
 
 
@@ -288,7 +289,8 @@ class TPPlan:
         self.instructions, self.weight_numel = o3.fctp_instructions(irreps_in, irreps_sh,
                                                                     irreps_out)
         key = tuple(ir for _, ir in irreps_out)
-        if key not in _LAYOUTS or any(m > 128 for m, _ in irreps_out) or \
+        if key not in _LAYOUTS or any(m > 128 or m % 4 for m, _ in irreps_out) or \
+                any(m > 128 for m, _ in irreps_in) or \
                 any(m != 1 for m, _ in irreps_sh) or o3.irreps_dim(irreps_sh) != 9:
             raise NotImplementedError(f"TP layout {o3.irreps_str(irreps_out)} not supported by K7")
         self.layout = _LAYOUTS[key]
@@ -345,7 +347,7 @@ class TPConvFn(torch.autograd.Function):
         dev = x.device
         paths_dev, cg_dev = plan.device_tables(dev)
         N, E = graph.num_nodes, graph.num_edges
-        out = torch.zeros((N, plan.desc.out_dim), dtype=torch.float32, device=dev)
+        msg = torch.empty((E, plan.desc.out_dim), dtype=torch.float32, device=dev)
         rad_s = ops.gather_rows(rad, graph.perm)  # radial features in receiver-sorted order
         ce = plan.chunk_edges()
         for c0 in range(0, E, ce):
@@ -356,10 +358,13 @@ class TPConvFn(torch.autograd.Function):
             with _timed("tp_conv_fwd"):
                 check(lib.gmp_tp_conv_fwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
                                               _p(cg_dev), cg_dev.numel(), _p(x), _p(sh), _p(Wc),
-                                              _p(graph.rowptr), _p(graph.src_sorted),
-                                              _p(graph.perm), N, c0, c1, _p(out), _stream()),
+                                              _p(graph.src_sorted), _p(graph.perm), c0, c1,
+                                              _p(msg), _stream()),
                       "gmp_tp_conv_fwd_f32")
             del Wc, a
+        # receiver sums over the sorted messages (deterministic, chunk-independent)
+        out, _ = ops.segment_reduce(msg, graph.recv_csr, "sum", use_perm=False)
+        del msg
         ctx.plan, ctx.graph = plan, graph
         ctx.save_for_backward(x, sh, rad_s, W1, b1, W2, b2)
         return out
@@ -392,8 +397,8 @@ class TPConvFn(torch.autograd.Function):
             with _timed("tp_conv_bwd"):
                 check(lib.gmp_tp_conv_bwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
                                               _p(cg_dev), cg_dev.numel(), _p(x), _p(sh), _p(Wc),
-                                              _p(graph.rowptr), _p(graph.src_sorted),
-                                              _p(graph.perm), N, c0, c1, _p(gout), _p(dWc),
+                                              _p(graph.recv_sorted), _p(graph.src_sorted),
+                                              _p(graph.perm), c0, c1, _p(gout), _p(dWc),
                                               _p(dx_edge), _p(dY), _stream()),
                       "gmp_tp_conv_bwd_f32")
             del Wc

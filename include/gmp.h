@@ -181,33 +181,33 @@ int gmp_edge_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int6
                                const float* g_radial, float* g_vec, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * K7 tensor-product convolution (models/layers/tfn_layer.py:82-87): e3nn
- * FullyConnectedTensorProduct(in1, 1x0e+1x1o+1x2e, out, shared_weights=False) with per-edge
- * weights W (chunk rows x weight_numel, produced by the radial MLP tfn_layer.py:73-77), summed
- * into the receiver ei0 (scatter(tp, ei[0], dim=0, reduce='sum')).
- * Edges are processed in receiver-sorted order over the chunk [c0, c1) of the CSR built on
- * edge_index[0]: rowptr (N+1), src_sorted[k] = ei1 of sorted edge k, perm[k] = original edge id.
+ * K7 tensor-product convolution messages (models/layers/tfn_layer.py:82-86): e3nn
+ * FullyConnectedTensorProduct(in1, 1x0e+1x1o+1x2e, out, shared_weights=False) applied per edge
+ * with per-edge weights W (chunk rows x weight_numel, produced by the radial MLP
+ * tfn_layer.py:73-77).  The receiver sum of tfn_layer.py:87 (scatter(tp, ei[0], 'sum')) is the
+ * segmented reduce above over the same receiver-sorted order.
+ * Edges are addressed by their position k in the stable CSR of edge_index[0]:
+ *   src_sorted[k] = ei1 of sorted edge k, perm[k] = original edge id, recv_sorted[k] = ei0.
  * x (N, in_dim) mul_ir; sh (E, 9) in ORIGINAL edge order; W row r = sorted edge c0 + r.
- * `out` (N, out_dim) is ACCUMULATED (caller zeroes it once before the first chunk).
+ * Forward writes msg rows c0..c1-1 (E x out_dim, sorted positions).
  * desc_host: host pointer to the descriptor {int n_paths, in_dim, out_dim, sh_dim;
  *   int64 weight_numel; int z_size, n_blocks; int blk_off[4], blk_mul[4], blk_l[4];}
  * paths_dev: device array of 64-byte path records {int l1, l2, lo, mul1, mul_out, x_off, y_off,
  *   io, out_off, z_off, cg_off, pad; int64 w_off; float alpha, pad}; cg_dev: concatenated
  *   real CG tensors (cg_len floats).  layout: 0 = out blocks (0e,1o,2e), 1 = (0e,0e,1o,2e).
+ *   Multiplicities <= 128 and multiples of 4.
  * Backward (per chunk): dW (chunk rows x weight_numel), dx_edge (E, in_dim) and dY_edge (E, 9)
- * at SORTED positions, given gout = dL/dout (N, out_dim).
+ * at SORTED positions, given gout = dL/dout (N, out_dim) of the receiver sums.
  * ------------------------------------------------------------------------------------------ */
 int gmp_tp_conv_fwd_f32(int layout, const void* desc_host, const void* paths_dev,
                         const float* cg_dev, int cg_len, const float* x, const float* sh,
-                        const float* W, const int64_t* rowptr, const int64_t* src_sorted,
-                        const int64_t* perm, int64_t n_nodes, int64_t c0, int64_t c1, float* out,
-                        void* stream);
+                        const float* W, const int64_t* src_sorted, const int64_t* perm,
+                        int64_t c0, int64_t c1, float* msg, void* stream);
 int gmp_tp_conv_bwd_f32(int layout, const void* desc_host, const void* paths_dev,
                         const float* cg_dev, int cg_len, const float* x, const float* sh,
-                        const float* W, const int64_t* rowptr, const int64_t* src_sorted,
-                        const int64_t* perm, int64_t n_nodes, int64_t c0, int64_t c1,
-                        const float* gout, float* dW, float* dx_edge, float* dY_edge,
-                        void* stream);
+                        const float* W, const int64_t* recv_sorted, const int64_t* src_sorted,
+                        const int64_t* perm, int64_t c0, int64_t c1, const float* gout,
+                        float* dW, float* dx_edge, float* dY_edge, void* stream);
 
 #ifdef __cplusplus
 }
