@@ -159,7 +159,9 @@ class Linear(nn.Module):
             off += mi * mo
             d = 2 * l + 1
             xi = x[:, oi[i]:oi[i] + mi * d].reshape(B, mi, d)
-            r = torch.matmul(W.t() / math.sqrt(fan), xi).reshape(B, mo * d)
+            # one (B*d, mi) x (mi, mo) GEMM instead of B batched (mo, mi) x (mi, d) products
+            r = xi.transpose(1, 2).reshape(B * d, mi).matmul(W / math.sqrt(fan))
+            r = r.reshape(B, d, mo).transpose(1, 2).reshape(B, mo * d)
             outs[j] = r if outs[j] is None else outs[j] + r
         for j, (mo, (l, _)) in enumerate(self.irreps_out):
             if outs[j] is None:
@@ -509,15 +511,78 @@ class Contraction(nn.Module):
         return torch.cat(outs, dim=0)
 
 
+class SymmetricContractionFn(torch.autograd.Function):
+    """K8 (gmp_symmetric_contraction_{fwd,bwd}_f32): out (N, 9C) from x (N, C, 9) and the
+    stacked per-channel coefficients A_nu (C, 9, 9^nu)."""
+
+    @staticmethod
+    def forward(ctx, x, corr, *A):
+        lib = _lib.load()
+        x = _f32c(x)
+        A = [_f32c(a) for a in A]
+        _need_cuda(x, *A)
+        N, C = x.shape[0], x.shape[1]
+        out = torch.empty((N, 9 * C), dtype=torch.float32, device=x.device)
+        Ap = [_p(a) for a in A] + [None] * (3 - len(A))
+        with _timed("symmetric_contraction_fwd"):
+            check(lib.gmp_symmetric_contraction_fwd_f32(N, C, corr, _p(x), *Ap, _p(out),
+                                                        _stream()),
+                  "gmp_symmetric_contraction_fwd_f32")
+        ctx.corr = corr
+        ctx.save_for_backward(x, *A)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        x, *A = ctx.saved_tensors
+        g = _f32c(g)
+        N, C = x.shape[0], x.shape[1]
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        G = lib.gmp_sc_groups(N)
+        part = torch.empty((G, C, 9, 819), dtype=torch.float32, device=x.device)
+        Ap = [_p(a) for a in A] + [None] * (3 - len(A))
+        with _timed("symmetric_contraction_bwd"):
+            check(lib.gmp_symmetric_contraction_bwd_f32(N, C, ctx.corr, _p(x), *Ap, _p(g),
+                                                        _p(dx), _p(part), _stream()),
+                  "gmp_symmetric_contraction_bwd_f32")
+        dA = part.sum(0)  # fixed-order sum over node groups
+        grads = [dA[..., :9], dA[..., 9:90], dA[..., 90:]][:len(A)]
+        return (dx, None, *[gg.contiguous() for gg in grads])
+
+
 class SymmetricContraction(nn.Module):
     def __init__(self, irreps_in, irreps_out, correlation):
         super().__init__()
         self.irreps_out = o3.parse_irreps(irreps_out)
+        self.correlation = correlation
+        irreps_in = o3.parse_irreps(irreps_in)
+        C = irreps_in[0][0]
+        # K8 applies to C x (0e + 1o + 2e) -> the same irreps, correlation <= 3 (configs C4)
+        self._k8 = (tuple(ir for _, ir in irreps_in) == ((0, 1), (1, -1), (2, 1)) and
+                    all(m == C for m, _ in irreps_in) and
+                    tuple(self.irreps_out) == tuple(irreps_in) and 1 <= correlation <= 3)
         self.contractions = nn.ModuleDict({
             f"{m}x{l}{'e' if p == 1 else 'o'}": Contraction(irreps_in, (l, p), correlation)
             for m, (l, p) in self.irreps_out})
 
+    def coefficients(self):
+        """A_nu (C, 9, 9^nu): per-channel coefficient tensors, output rows [0e | 1o | 2e]."""
+        out = []
+        for nu in range(1, self.correlation + 1):
+            rows = []
+            for con in self.contractions.values():
+                U = con.U(nu)
+                if U.dim() == nu + 1:  # scalar output: the m axis was squeezed
+                    U = U.unsqueeze(0)
+                A = torch.einsum("m...k,kc->cm...", U, con.weights[str(nu)])
+                rows.append(A.reshape(A.shape[0], A.shape[1], -1))
+            out.append(torch.cat(rows, dim=1))
+        return out
+
     def forward(self, x, y=None):
+        if self._k8 and x.is_cuda:
+            return SymmetricContractionFn.apply(x, self.correlation, *self.coefficients())
         return torch.cat([c(x) for c in self.contractions.values()], dim=-1)
 
 

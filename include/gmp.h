@@ -209,6 +209,25 @@ int gmp_tp_conv_bwd_f32(int layout, const void* desc_host, const void* paths_dev
                         const int64_t* perm, int64_t c0, int64_t c1, const float* gout,
                         float* dW, float* dx_edge, float* dY_edge, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
+ * element_dependent=False, called per output irrep at :176-185), all three output irreps
+ * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)
+ * (irreps_tools.py:63-79).  A_nu (C, 9, 9^nu) = sum_k U_nu[m, ..., k] W_nu[k, c] stacked over
+ * the output rows m = [0e | 1o (3) | 2e (5)] (the host builds them from the module's
+ * U_matrix_nu buffers and weights).  out (N, 9C) in mul_ir order [0e: C | 1o: 3C | 2e: 5C].
+ * Backward: dx (N, C, 9) (may be NULL) and dA partials (gmp_sc_groups(N), C, 9, 819) with
+ * monomials q = [deg1 (9) | deg2 (81) | deg3 (729)] (may be NULL); the caller sums the groups.
+ * ------------------------------------------------------------------------------------------ */
+int gmp_sc_groups(int64_t n_nodes);
+int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int correlation,
+                                      const float* x, const float* A1, const float* A2,
+                                      const float* A3, float* out, void* stream);
+int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int correlation,
+                                      const float* x, const float* A1, const float* A2,
+                                      const float* A3, const float* gout, float* dx,
+                                      float* dA_partials, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

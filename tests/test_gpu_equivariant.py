@@ -188,3 +188,40 @@ def test_mace_rotation_invariance_gpu():
     y1 = model(Batch(g.atoms.to(DEV), g.pos.to(DEV), g.edge_index.to(DEV)))
     y2 = model(Batch(g.atoms.to(DEV), (g.pos @ R.T + 0.7).to(DEV), g.edge_index.to(DEV)))
     _close_scaled(y2, y1, 1e-4, "rotated")
+
+
+@pytest.mark.parametrize("C,corr", [(16, 3), (128, 3), (32, 2), (8, 1)])
+def test_symmetric_contraction_k8_vs_oracle(C, corr):
+    """K8 HIP symmetric contraction vs the oracle (the reference's nested einsum chain)."""
+    from gmp_amd import equivariant as eq
+    torch.manual_seed(C + corr)
+    irr = f"{C}x0e+{C}x1o+{C}x2e"
+    ref = om.SymmetricContraction(irr, irr, corr)
+    sc = eq.SymmetricContraction(irr, irr, corr)
+    sc.load_state_dict(ref.state_dict())
+    sc = sc.to(DEV)
+    assert sc._k8
+    x = torch.randn(700, C, 9)
+    xd = x.to(DEV).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y, yr = sc(xd), ref(xr)
+    torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-5, rtol=1e-5)
+    g = torch.randn_like(yr)
+    (y * g.to(DEV)).sum().backward()
+    (yr * g).sum().backward()
+    _close_scaled(xd.grad, xr.grad, 1e-5, "dx")
+    for (k, p), q in zip(sc.named_parameters(), ref.parameters()):
+        _close_scaled(p.grad, q.grad, 1e-5, k)
+
+
+def test_symmetric_contraction_k8_golden(golden):
+    from gmp_amd import equivariant as eq
+    d = golden("mace_symmetric_contraction.pt")
+    sc = eq.SymmetricContraction("16x0e+16x1o+16x2e", "16x0e+16x1o+16x2e", 3)
+    sc.load_state_dict({k[6:]: v for k, v in d.items() if k.startswith("param.")}, strict=True)
+    sc = sc.to(DEV)
+    x = d["x"].clone().to(DEV).requires_grad_(True)
+    y = sc(x)
+    torch.testing.assert_close(y.detach().cpu(), d["out"], atol=1e-5, rtol=1e-5)
+    (y * d["g_out"].to(DEV)).sum().backward()
+    torch.testing.assert_close(x.grad.cpu(), d["grad_x"], atol=1e-5, rtol=1e-5)
