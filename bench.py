@@ -103,6 +103,22 @@ def pmc_traffic(workload, kernel):
     return None
 
 
+def tp_node_flops(model, n_nodes, n_edges):
+    """Algorithmic FLOPs per training step of the receiver-factorised TP convolutions
+    (DESIGN.md §K7): per layer, S = sum_e z_e (x) a_e (2 E 257 z_size) and the path GEMMs
+    (2 N 257 sum_p (2lo+1) mul1 mul_out); forward 1 x both, backward 3 x S-shaped
+    (S recompute, dZ, dA) + 2 x GEMM-shaped (T, dW2)."""
+    total = 0
+    for conv in model.convs:
+        pl = conv.plan
+        J = conv.fc[0].out_features + 1
+        s_fl = 2 * n_edges * J * pl.desc.z_size
+        g_fl = 2 * n_nodes * J * sum((2 * i["lo"] + 1) * i["mul1"] * i["mul_out"]
+                                     for i in pl.instructions)
+        total += 4 * s_fl + 3 * g_fl
+    return total
+
+
 def egnn_bwd_bytes_per_edge(d):
     """Minimum HBM bytes per edge of the fused EGNN edge backward: indices 16,
     sender/receiver node rows of dA/AB 2 x 2d x 4 (gathered), pos 24, recomputed nothing else
@@ -247,21 +263,20 @@ def main():
                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                     "traffic": None, "flops_per_edge": fl}
         else:
-            # K7 is timed per chunk launch; algorithmic bytes = bytes/edge x edges per launch
-            bf, bb = tp_bytes_per_edge(core)
-            n_f = len(core.convs) * (args.steps)
-            tot_f = sum_ms("tp_conv_fwd")
-            tot_b = sum_ms("tp_conv_bwd")
-            gbs_f = bf * g.num_edges * n_f / (tot_f * 1e-3) / 1e9
-            gbs_b = bb * g.num_edges * n_f / (tot_b * 1e-3) / 1e9
-            roof = {"kernel": "tp_conv_bwd", "bound": "hbm", "achieved": gbs_b,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs_b / HBM_PEAK_GBS,
-                    "traffic": None, "ms_per_launch": timers["tp_conv_bwd"],
-                    "bytes_per_edge": bb, "fwd_kernel_gbs": gbs_f,
-                    "fwd_kernel_ms_per_launch": timers["tp_conv_fwd"],
-                    "tp_fwd_ms_per_step": tot_f / args.steps,
-                    "tp_bwd_ms_per_step": tot_b / args.steps,
-                    "radial_gemm_ms_per_step": sum_ms("radial_gemm") / args.steps}
+            # receiver-factorised K7: rocBLAS GEMMs over S / T (timed region "tp_node_gemm"
+            # includes the padded gathers) — MFMA-bound; algorithmic flops per step below
+            fl = tp_node_flops(core, g.num_nodes, g.num_edges)
+            t_gemm = sum_ms("tp_node_gemm") / args.steps
+            achieved = fl / (t_gemm * 1e-3) / 1e12
+            roof = {"kernel": "tp_node_gemm", "kernel_prefix": "-", "bound": "mfma",
+                    "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                    "flops_per_step": fl, "tp_node_gemm_ms_per_step": t_gemm,
+                    "tp_node_prep_ms_per_step": sum_ms("tp_node_prep") / args.steps,
+                    "tp_node_edge_bwd_ms_per_step": sum_ms("tp_node_edge_bwd") / args.steps,
+                    "symmetric_contraction_ms_per_step":
+                        (sum_ms("symmetric_contraction_fwd") +
+                         sum_ms("symmetric_contraction_bwd")) / args.steps}
         t = pmc_traffic(args.workload, roof["kernel_prefix"] if "kernel_prefix" in roof
                         else {"egnn_edge_bwd": "egnn_bwd_kernel",
                               "tp_conv_bwd": "tp_bwd_kernel"}[roof["kernel"]])

@@ -386,6 +386,129 @@ __global__ __launch_bounds__(kWave) void tp_bwd_kernel(
   }
 }
 
+// -------------------------------------------------------------------------------- node form
+// Receiver-factorised form (the radial MLP's second Linear commutes with the receiver sum):
+//   msg_n[w, k] = sum_{e -> n} sum_u (sum_j a_e[j] W2[(u,w), j]) z_e[u, k]
+//              = sum_{u, j} W2[(u,w), j] S_n[k, u, j],   S_n[k, u, j] = sum_{e -> n} z_e[u, k] a_e[j]
+// The host forms S with batched GEMMs over degree-padded receivers and contracts it with W2 in
+// one GEMM per path; these kernels produce z (per edge, per path, layout [p][e][k][u], alpha
+// folded in) and map dz back to dx_e / dY_e.  zbuf path p region: rows (n_e + 1) x (d3 * mul1)
+// starting at z_off_p * (n_e + 1); row n_e (padding) is left untouched (the host zeroes it).
+__global__ __launch_bounds__(kWave) void tp_edge_z_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+    const float* __restrict__ x, const float* __restrict__ sh,
+    const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
+    int64_t e1, float* __restrict__ zbuf) {
+  __shared__ Path sp[kMaxPaths];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  Smem s = carve(smem, cg_len, d.in_dim, d.out_dim);
+  const int lane = threadIdx.x;
+  for (int i = lane; i < d.n_paths; i += kWave) sp[i] = paths[i];
+  for (int i = lane; i < cg_len; i += kWave) s.cg[i] = cg[i];
+  __syncthreads();
+  const int64_t ne = e1 - e0, G = gridDim.x, b = blockIdx.x;
+  const int64_t eb = e0 + ne * b / G, ee = e0 + ne * (b + 1) / G;
+  for (int64_t e = eb; e < ee; ++e) {
+    stage_edge(d, x, sh, src_sorted[e], perm[e], s, lane);
+    __syncthreads();
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = sp[p];
+      const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1;
+      if (lane < d1 * d3) {
+        const int i = lane / d3, k = lane - i * d3;
+        const float* C = s.cg + P.cg_off;
+        float a = 0.f;
+        for (int j = 0; j < d2; ++j) a += C[(i * d2 + j) * d3 + k] * s.y[P.y_off + j];
+        s.t[lane] = a;
+      }
+      __syncthreads();
+      float* zr = zbuf + (int64_t)P.z_off * (ne + 1) + (e - e0) * (int64_t)(d3 * P.mul1);
+      for (int u = lane; u < P.mul1; u += kWave) {
+        const float* xu = s.x + P.x_off + u * d1;
+        for (int k = 0; k < d3; ++k) {
+          float a = 0.f;
+          for (int i = 0; i < d1; ++i) a += xu[i] * s.t[i * d3 + k];
+          zr[k * P.mul1 + u] = P.alpha * a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kWave) void tp_edge_z_bwd_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+    const float* __restrict__ x, const float* __restrict__ sh,
+    const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
+    int64_t e1, const float* __restrict__ dzbuf, float* __restrict__ dx_edge,
+    float* __restrict__ dY_edge) {
+  __shared__ Path sp[kMaxPaths];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  Smem s = carve(smem, cg_len, d.in_dim, d.out_dim);
+  const int lane = threadIdx.x;
+  for (int i = lane; i < d.n_paths; i += kWave) sp[i] = paths[i];
+  for (int i = lane; i < cg_len; i += kWave) s.cg[i] = cg[i];
+  __syncthreads();
+  const int64_t ne = e1 - e0, G = gridDim.x, b = blockIdx.x;
+  const int64_t eb = e0 + ne * b / G, ee = e0 + ne * (b + 1) / G;
+  for (int64_t e = eb; e < ee; ++e) {
+    stage_edge(d, x, sh, src_sorted[e], perm[e], s, lane);
+    for (int i = lane; i < d.in_dim; i += kWave) s.dx[i] = 0.f;
+    __syncthreads();
+    float dyp[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) dyp[j] = 0.f;
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = sp[p];
+      const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1;
+      const float* C = s.cg + P.cg_off;
+      if (lane < d1 * d3) {
+        const int i = lane / d3, k = lane - i * d3;
+        float a = 0.f;
+        for (int j = 0; j < d2; ++j) a += C[(i * d2 + j) * d3 + k] * s.y[P.y_off + j];
+        s.t[lane] = a;
+      }
+      __syncthreads();
+      const float* dzr = dzbuf + (int64_t)P.z_off * (ne + 1) + (e - e0) * (int64_t)(d3 * P.mul1);
+      for (int u = lane; u < P.mul1; u += kWave) {  // lane owns u for every path: no race on dx
+        float dz[5];
+        for (int k = 0; k < d3; ++k) dz[k] = dzr[k * P.mul1 + u];
+        const float* xu = s.x + P.x_off + u * d1;
+        float* dxu = s.dx + P.x_off + u * d1;
+        for (int i = 0; i < d1; ++i) {
+          float a = 0.f;
+          for (int k = 0; k < d3; ++k) a += dz[k] * s.t[i * d3 + k];
+          dxu[i] += P.alpha * a;
+#pragma unroll
+          for (int jj = 0; jj < 9; ++jj) {
+            const int j = jj - P.y_off;
+            if (j < 0 || j >= d2) continue;
+            float cz = 0.f;
+            for (int k = 0; k < d3; ++k) cz += C[(i * d2 + j) * d3 + k] * dz[k];
+            dyp[jj] += P.alpha * cz * xu[i];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    float* dxr = dx_edge + (e - e0) * d.in_dim;
+    for (int i = lane; i < d.in_dim; i += kWave) dxr[i] = s.dx[i];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      float v = dyp[j];
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+      dyp[j] = v;
+    }
+    if (lane < d.sh_dim) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) v = (lane == j) ? dyp[j] : v;
+      dY_edge[(e - e0) * d.sh_dim + lane] = v;
+    }
+    __syncthreads();
+  }
+}
+
 bool desc_ok(const Desc& d, int layout) {
   if (d.n_paths <= 0 || d.n_paths > kMaxPaths || d.in_dim <= 0 || d.in_dim > kMaxIn ||
       d.out_dim <= 0 || d.out_dim > kMaxOut || d.sh_dim != 9 || d.weight_numel <= 0 ||
@@ -479,6 +602,41 @@ int gmp_tp_conv_bwd_f32(int layout, const void* desc_host, const void* paths_dev
     if ((rc = set_smem(k, smem))) return rc;
     k<<<G, kWave, smem, s>>>(d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, W, recv_sorted, src_sorted, perm, c0, c1, gout, dW, dx_edge, dY_edge);
   }
+  return launch_status();
+}
+
+int gmp_tp_edge_z_f32(const void* desc_host, const void* paths_dev, const float* cg_dev,
+                      int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
+                      const int64_t* perm, int64_t e0, int64_t e1, float* zbuf, void* stream) {
+  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && zbuf);
+  const Desc d = *reinterpret_cast<const Desc*>(desc_host);
+  GMP_CHECK_ARG(desc_ok(d, d.n_blocks == 3 ? 0 : 1) && cg_len > 0 && cg_len <= 4096);
+  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
+  if (e1 == e0) return GMP_OK;
+  const size_t smem = smem_bytes(d, cg_len, false);
+  int rc;
+  if ((rc = set_smem(tp_edge_z_kernel, smem))) return rc;
+  tp_edge_z_kernel<<<(unsigned)grid_for_chunk(e1 - e0), kWave, smem, as_stream(stream)>>>(
+      d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
+  return launch_status();
+}
+
+int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const float* cg_dev,
+                          int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
+                          const int64_t* perm, int64_t e0, int64_t e1, const float* dzbuf,
+                          float* dx_edge, float* dY_edge, void* stream) {
+  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && dzbuf &&
+                dx_edge && dY_edge);
+  const Desc d = *reinterpret_cast<const Desc*>(desc_host);
+  GMP_CHECK_ARG(desc_ok(d, d.n_blocks == 3 ? 0 : 1) && cg_len > 0 && cg_len <= 4096);
+  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
+  if (e1 == e0) return GMP_OK;
+  const size_t smem = smem_bytes(d, cg_len, true);
+  int rc;
+  if ((rc = set_smem(tp_edge_z_bwd_kernel, smem))) return rc;
+  tp_edge_z_bwd_kernel<<<(unsigned)grid_for_chunk(e1 - e0), kWave, smem, as_stream(stream)>>>(
+      d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf, dx_edge,
+      dY_edge);
   return launch_status();
 }
 

@@ -265,6 +265,39 @@ class TPGraph:
         self.src_sorted = self.recv_csr.payload_sorted
         self.recv_sorted = self.recv_csr.sorted
         self.src_csr = ops.CSR(self.src_sorted, self.num_nodes)
+        self._node_form = None
+
+    def node_form(self):
+        """Host copy of rowptr (one sync per graph), max in-degree and per-edge slot."""
+        if self._node_form is None:
+            rp = self.rowptr.cpu()
+            deg = rp[1:] - rp[:-1]
+            dmax = int(deg.max()) if deg.numel() else 0
+            slot = torch.arange(self.num_edges, device=self.rowptr.device) - \
+                self.rowptr[self.recv_sorted]
+            self._node_form = (rp.tolist(), dmax, slot)
+        return self._node_form
+
+    def node_chunks(self, nodes_per_chunk):
+        rp, dmax, _ = self.node_form()
+        n = self.num_nodes
+        for n0 in range(0, n, nodes_per_chunk):
+            n1 = min(n, n0 + nodes_per_chunk)
+            yield n0, n1, rp[n0], rp[n1]
+
+    def chunk_pad(self, n0, n1, e0, e1):
+        """(c * dmax) gather index into the chunk's edge rows (padding -> n_e) and the (n_e,)
+        position of every chunk edge in the padded (c, dmax) grid."""
+        _, dmax, slot = self.node_form()
+        dev = self.rowptr.device
+        c, ne = n1 - n0, e1 - e0
+        s = torch.arange(dmax, device=dev)
+        rp = self.rowptr[n0:n1]
+        deg = self.rowptr[n0 + 1:n1 + 1] - rp
+        idx = torch.where(s[None, :] < deg[:, None], rp[:, None] - e0 + s[None, :],
+                          torch.full((), ne, device=dev, dtype=torch.int64))
+        pos = (self.recv_sorted[e0:e1] - n0) * dmax + slot[e0:e1]
+        return idx.reshape(-1), pos
 
 
 _TP_GRAPHS = []
@@ -321,6 +354,11 @@ class TPPlan:
         self.desc.n_blocks = len(irreps_out)
         for b, (m, (l, _)) in enumerate(irreps_out):
             self.desc.blk_off[b], self.desc.blk_mul[b], self.desc.blk_l[b] = oo[b], m, l
+        self.blocks = [(oo[b], m) for b, (m, _) in enumerate(irreps_out)]
+        # node form: path p's z rows (mul1 * (2lo+1) floats) at z_off_p * (n_e + 1)
+        self.z_regions = [(paths[k].z_off, ins["mul1"] * (2 * ins["lo"] + 1))
+                          for k, ins in enumerate(self.instructions)]
+        self.max_block_rows = max(w for _, w in self.z_regions)
         self._dev = {}
 
     def device_tables(self, device):
@@ -419,6 +457,148 @@ class TPConvFn(torch.autograd.Function):
         return dx, dsh, drad, dW1, db1, dW2, db2, None, None
 
 
+NODE_CHUNK_BYTES = int(os.environ.get("GMP_TP_NODE_CHUNK_BYTES", str(2 << 30)))
+TP_MODE = os.environ.get("GMP_TP_MODE", "node")  # "node" (receiver-factorised) | "edge"
+
+
+def _w2_ext(W2, b2, P):
+    """Path block of [W2 | b2] as (mul1 * 257, mul_out): row (u, j), column w."""
+    m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
+    blk = torch.cat([W2[off:off + m1 * mo].view(m1, mo, -1),
+                     b2[off:off + m1 * mo].view(m1, mo, 1)], dim=2)
+    return blk.permute(0, 2, 1).reshape(m1 * blk.shape[2], mo)
+
+
+class TPConvNodeFn(torch.autograd.Function):
+    """out = scatter_sum_{ei0}(FCTP(x[ei1], sh, fc(radial)))  (tfn_layer.py:82-87), evaluated in
+    receiver-factorised form: with a_e = [relu(W1 r_e + b1), 1] (257) the per-edge weights are
+    W_e = [W2 | b2] a_e, so for receiver n and path p
+        out_n[w, k] = sum_{u, j} [W2|b2][(u, w), j] S_n[k, u, j],   S_n = sum_{e -> n} z_e (x) a_e.
+    S is a batched GEMM over degree-padded receivers (K = max in-degree) and the contraction with
+    W2 one GEMM per path with K = mul1 * 257: E * 256 * weight_numel MACs become
+    N * 257 * sum_p mul1 mul_out (2lo+1) + E * 257 * z_size (N = E / 20 here).  Backward uses
+    T = G [W2|b2]^T (same shape as S) for dz and da, and dW2 = G^T S."""
+
+    @staticmethod
+    def forward(ctx, x, sh, rad, W1, b1, W2, b2, plan, graph):
+        lib = _lib.load()
+        x, sh, rad = _f32c(x), _f32c(sh), _f32c(rad)
+        _need_cuda(x, sh, rad)
+        dev = x.device
+        N, E = graph.num_nodes, graph.num_edges
+        out = torch.zeros((N, plan.desc.out_dim), dtype=torch.float32, device=dev)
+        rad_s = ops.gather_rows(rad, graph.perm)
+        W2x = [_w2_ext(W2, b2, P) for P in plan.instructions]
+        for n0, n1, e0, e1, idx, pos, Apad, zbuf, _ in _node_chunks(lib, plan, graph, x, sh,
+                                                                       rad_s, W1, b1):
+            c, ne = n1 - n0, e1 - e0
+            for P, W2p, (zoff, w) in zip(plan.instructions, W2x, plan.z_regions):
+                d3 = 2 * P["lo"] + 1
+                Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
+                with _timed("tp_node_gemm"):
+                    Zpad = ops.gather_rows(Zp, idx).view(c, -1, w)
+                    S = torch.bmm(Zpad.transpose(1, 2), Apad).view(c * d3, -1)
+                    op = S.mm(W2p).view(c, d3, P["mul_out"])
+                blk = plan.blocks[P["io"]]
+                out[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, blk[1], d3).add_(
+                    op.transpose(1, 2))
+        ctx.plan, ctx.graph = plan, graph
+        ctx.save_for_backward(x, sh, rad_s, W1, b1, W2, b2)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _lib.load()
+        x, sh, rad_s, W1, b1, W2, b2 = ctx.saved_tensors
+        plan, graph = ctx.plan, ctx.graph
+        paths_dev, cg_dev = plan.device_tables(x.device)
+        gout = _f32c(gout)
+        N, E = graph.num_nodes, graph.num_edges
+        f = dict(dtype=torch.float32, device=x.device)
+        dx_edge = torch.empty((E, plan.desc.in_dim), **f)
+        dY = torch.empty((E, 9), **f)
+        drad_s = torch.empty_like(rad_s)
+        dW1, db1 = torch.zeros_like(W1), torch.zeros_like(b1)
+        W2x = [_w2_ext(W2, b2, P) for P in plan.instructions]
+        dW2x = [torch.zeros_like(w) for w in W2x]
+        for n0, n1, e0, e1, idx, pos, Apad, zbuf, pre in _node_chunks(lib, plan, graph, x, sh,
+                                                                         rad_s, W1, b1):
+            c, ne = n1 - n0, e1 - e0
+            dzbuf = torch.empty_like(zbuf)
+            dApad = torch.zeros_like(Apad)
+            for P, W2p, dW2p, (zoff, w) in zip(plan.instructions, W2x, dW2x, plan.z_regions):
+                d3, mo = 2 * P["lo"] + 1, P["mul_out"]
+                blk = plan.blocks[P["io"]]
+                Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
+                with _timed("tp_node_gemm"):
+                    Zpad = ops.gather_rows(Zp, idx).view(c, -1, w)
+                    S = torch.bmm(Zpad.transpose(1, 2), Apad).view(c * d3, -1)
+                    G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
+                    G = G.reshape(c * d3, mo)
+                    dW2p.addmm_(S.t(), G)
+                    del S
+                    T = G.mm(W2p.t()).view(c, w, -1)
+                    dZpad = torch.bmm(Apad, T.transpose(1, 2)).view(c * Zpad.shape[1], w)
+                    dApad.baddbmm_(Zpad, T)
+                    del T
+                dZp = dzbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
+                dZp[:ne] = ops.gather_rows(dZpad, pos)
+            with _timed("tp_node_edge_bwd"):
+                check(lib.gmp_tp_edge_z_bwd_f32(ctypes.byref(plan.desc), _p(paths_dev),
+                                                _p(cg_dev), cg_dev.numel(), _p(x), _p(sh),
+                                                _p(graph.src_sorted), _p(graph.perm), e0, e1,
+                                                _p(dzbuf), _p(dx_edge[e0:e1]), _p(dY[e0:e1]),
+                                                _stream()),
+                      "gmp_tp_edge_z_bwd_f32")
+            da = ops.gather_rows(dApad.view(-1, dApad.shape[2]), pos)[:, :-1]
+            dpre = da * (pre > 0)
+            r = rad_s[e0:e1]
+            dW1.addmm_(dpre.t(), r)
+            db1.add_(dpre.sum(0))
+            drad_s[e0:e1] = dpre.mm(W1)
+        dW2, db2 = torch.empty_like(W2), torch.empty_like(b2)
+        for P, g in zip(plan.instructions, dW2x):
+            m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
+            g3 = g.view(m1, -1, mo).permute(0, 2, 1)  # (m1, mo, 257)
+            dW2[off:off + m1 * mo] = g3[:, :, :-1].reshape(m1 * mo, -1)
+            db2[off:off + m1 * mo] = g3[:, :, -1].reshape(-1)
+        dx, _ = ops.segment_reduce(dx_edge, graph.src_csr, "sum")
+        dsh = torch.empty_like(sh).index_copy_(0, graph.perm, dY)
+        drad = torch.empty((E, rad_s.shape[1]), **f).index_copy_(0, graph.perm, drad_s)
+        return dx, dsh, drad, dW1, db1, dW2, db2, None, None
+
+
+def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):
+    """Receiver chunks with their padded a rows and z rows (recomputed per pass)."""
+    paths_dev, cg_dev = plan.device_tables(x.device)
+    _, dmax, _ = graph.node_form()
+    if graph.num_edges == 0 or dmax == 0:
+        return
+    hidden = W1.shape[0]
+    per_node = max(plan.max_block_rows * (hidden + 1), dmax * plan.desc.z_size) * 4
+    npc = max(1, NODE_CHUNK_BYTES // per_node)
+    for n0, n1, e0, e1 in graph.node_chunks(npc):
+        if e1 == e0:
+            continue
+        c, ne = n1 - n0, e1 - e0
+        idx, pos = graph.chunk_pad(n0, n1, e0, e1)
+        with _timed("tp_node_prep"):
+            pre = torch.addmm(b1, rad_s[e0:e1], W1.t())
+            a = torch.ones((ne + 1, hidden + 1), dtype=torch.float32, device=x.device)
+            a[:ne, :hidden] = torch.relu(pre)
+            a[ne].zero_()
+            Apad = ops.gather_rows(a, idx).view(c, dmax, hidden + 1)
+            zbuf = torch.empty(((ne + 1) * plan.desc.z_size,), dtype=torch.float32,
+                               device=x.device)
+            for zoff, w in plan.z_regions:
+                zbuf[(zoff + w) * (ne + 1) - w:(zoff + w) * (ne + 1)].zero_()  # padding row
+            check(lib.gmp_tp_edge_z_f32(ctypes.byref(plan.desc), _p(paths_dev), _p(cg_dev),
+                                        cg_dev.numel(), _p(x), _p(sh), _p(graph.src_sorted),
+                                        _p(graph.perm), e0, e1, _p(zbuf), _stream()),
+                  "gmp_tp_edge_z_f32")
+        yield n0, n1, e0, e1, idx, pos, Apad, zbuf, pre
+
+
 class TensorProductConvLayer(nn.Module):
     """tfn_layer.py:8-93 (same arguments; module tree fc.{0,2}, batch_norm, gate)."""
 
@@ -443,8 +623,9 @@ class TensorProductConvLayer(nn.Module):
 
     def forward(self, node_attr, edge_index, edge_sh, edge_feat):
         graph = tp_graph(edge_index, node_attr.shape[0])
-        out = TPConvFn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight, self.fc[0].bias,
-                             self.fc[2].weight, self.fc[2].bias, self.plan, graph)
+        fn = TPConvNodeFn if TP_MODE == "node" else TPConvFn
+        out = fn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight, self.fc[0].bias,
+                       self.fc[2].weight, self.fc[2].bias, self.plan, graph)
         if self.aggr == "mean":
             out = out / graph.recv_csr.counts().clamp(min=1).unsqueeze(1).to(out.dtype)
         elif self.aggr not in ("add", "sum"):

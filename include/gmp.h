@@ -209,6 +209,19 @@ int gmp_tp_conv_bwd_f32(int layout, const void* desc_host, const void* paths_dev
                         const int64_t* perm, int64_t c0, int64_t c1, const float* gout,
                         float* dW, float* dx_edge, float* dY_edge, void* stream);
 
+/* K7 receiver-factorised form helpers: per-edge z rows (alpha_p sum_ij C x Y) for the edges
+ * [e0, e1) of a receiver chunk, in path-major layout: path p region starts at
+ * z_off_p * (n_e + 1) floats (n_e = e1 - e0) and holds (n_e + 1) rows of (2lo+1) * mul1 floats,
+ * k-major then u; row n_e is a padding row the kernels never write.  The backward maps dz (same
+ * layout) to dx_edge (n_e, in_dim) and dY_edge (n_e, 9) for those edges (sorted positions).  */
+int gmp_tp_edge_z_f32(const void* desc_host, const void* paths_dev, const float* cg_dev,
+                      int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
+                      const int64_t* perm, int64_t e0, int64_t e1, float* zbuf, void* stream);
+int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const float* cg_dev,
+                          int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
+                          const int64_t* perm, int64_t e0, int64_t e1, const float* dzbuf,
+                          float* dx_edge, float* dY_edge, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps

@@ -70,8 +70,10 @@ def test_featurize_vs_oracle():
     ("128x0e+128x1o+128x2e", "128x0e+128x1o+128x2e", False, True, "add", 64),
     ("64x0e+64x1o+64x2e", "64x0e+64x1o+64x2e", True, False, "add", 64),
 ])
-def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp):
+@pytest.mark.parametrize("mode", ["node", "edge"])
+def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp, mode, monkeypatch):
     from gmp_amd import equivariant as eq
+    monkeypatch.setattr(eq, "TP_MODE", mode)
     torch.manual_seed(len(inp) + mlp)
     n = 200 if "128x" in inp else 400
     g = _graph(n, 12 * n, seed=mlp)
@@ -99,12 +101,14 @@ def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp):
     _grads(lay, ref)
 
 
-def test_tp_conv_chunking_and_determinism(monkeypatch):
+@pytest.mark.parametrize("mode", ["node", "edge"])
+def test_tp_conv_chunking_and_determinism(monkeypatch, mode):
     """Edge chunks of the radial-weight materialisation must not change the result (the
     per-receiver summation order is chunk-independent; only the library GEMM producing the
     weights may pick a different kernel for a different chunk height, i.e. fp32 rounding) and
     repeated runs are bitwise equal."""
     from gmp_amd import equivariant as eq
+    monkeypatch.setattr(eq, "TP_MODE", mode)
     torch.manual_seed(0)
     g = _graph(300, 5000, seed=11)
     lay = eq.TensorProductConvLayer("32x0e+32x1o+32x2e", "32x0e+32x1o+32x2e", eq.o3.sh_irreps(2),
@@ -127,6 +131,7 @@ def test_tp_conv_chunking_and_determinism(monkeypatch):
         assert torch.equal(u, v)
     monkeypatch.setattr(eq, "CHUNK_BYTES", 4 * lay.plan.weight_numel * 700)
     assert lay.plan.chunk_edges() < g.num_edges
+    monkeypatch.setattr(eq, "NODE_CHUNK_BYTES", 60 * lay.plan.max_block_rows * 33 * 4)
     c = run()
     _close_scaled(c[0], a[0], 1e-5, "out (chunked)")
     _close_scaled(c[1], a[1], 1e-5, "dx (chunked)")
