@@ -152,6 +152,76 @@ __global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t
   else if (colsum) colsum[x - DD] = s;
 }
 
+// Rectangular variant for the other per-edge Linears (GVP message GVPs: 128 x 144, 128 x 80,
+// 16 x 128, 16 x 48, 16 x 16): C (M x N) = A^T B with M, N multiples of 16, T = (M/16)(N/16) <= 72
+// output tiles dealt round-robin to the 4 waves (<= 18 accumulator tiles each).  Same split-K /
+// ordered partial-sum scheme; A and B tiles of kKT edges staged through LDS.
+constexpr int kMaxTilesPerWave = 18;
+constexpr int kRectLD = 8;  // LDS row padding (floats)
+
+__global__ __launch_bounds__(kT, 2) void outer_sum_rect_kernel(
+    const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
+    int64_t k_per_block, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int LDA = M + kRectLD, LDB = N + kRectLD;
+  float* sA = sm;                      // kKT x LDA
+  float* sB = sA + kKT * LDA;          // kKT x LDB
+  float* sCol = sB + kKT * LDB;        // kT floats (colsum partials)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, kk = lane >> 4;
+  const int TN = N >> 4, T = (M >> 4) * TN;
+  const int64_t k0 = (int64_t)blockIdx.x * k_per_block;
+  const int64_t k1 = (k0 + k_per_block < K) ? k0 + k_per_block : K;
+  f32x4 acc[kMaxTilesPerWave];
+#pragma unroll
+  for (int q = 0; q < kMaxTilesPerWave; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float csum = 0.f;  // colsum(A) of column tid (tid < M), accumulated by its owner thread
+  const int CA = M >> 2, CB = N >> 2, CT = CA + CB;  // float4 chunks per edge row
+  for (int64_t kb = k0; kb < k1; kb += kKT) {
+    __syncthreads();
+    for (int c = tid; c < kKT * CT; c += kT) {
+      const int r = c / CT, q = c - r * CT;
+      const int64_t k = kb + r;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (q < CA) {
+        if (k < k1) v = *reinterpret_cast<const f32x4*>(A + k * M + 4 * q);
+        *reinterpret_cast<f32x4*>(&sA[r * LDA + 4 * q]) = v;
+      } else {
+        if (k < k1) v = *reinterpret_cast<const f32x4*>(B + k * N + 4 * (q - CA));
+        *reinterpret_cast<f32x4*>(&sB[r * LDB + 4 * (q - CA)]) = v;
+      }
+    }
+    __syncthreads();
+    if (tid < M)
+      for (int r = 0; r < kKT; ++r) csum += sA[r * LDA + tid];
+#pragma unroll
+    for (int s = 0; s < kKT / 4; ++s) {
+      const int e = 4 * s + kk;
+#pragma unroll
+      for (int q = 0; q < kMaxTilesPerWave; ++q) {
+        const int t = w + 4 * q;
+        if (t < T) {
+          const int tm = t / TN, tn = t - tm * TN;
+          const float af = sA[e * LDA + 16 * tm + li];
+          const float bf = sB[e * LDB + 16 * tn + li];
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, bf, acc[q], 0, 0, 0);
+        }
+      }
+    }
+  }
+  float* out = partial + (int64_t)blockIdx.x * ((int64_t)M * N + M);
+#pragma unroll
+  for (int q = 0; q < kMaxTilesPerWave; ++q) {
+    const int t = w + 4 * q;
+    if (t < T) {
+      const int tm = t / TN, tn = t - tm * TN;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(16 * tm + 4 * kk + r) * N + 16 * tn + li] = acc[q][r];
+    }
+  }
+  if (tid < M) out[(int64_t)M * N + tid] = csum;
+}
+
 int64_t blocks_for(int64_t K) {
   int64_t g = (int64_t)device_cu_count() * 2;  // two resident workgroups per CU
   const int64_t min_per = 4 * kKT;
@@ -201,6 +271,46 @@ int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B,
   rc = launch_status();
   if (rc) return rc;
   sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, d * d);
+  return launch_status();
+}
+
+size_t gmp_edge_outer_sum_rect_workspace_size(int64_t K, int64_t m, int64_t n) {
+  const int64_t G = blocks_for(K);
+  return (size_t)(G + ceil_div(G, kGC)) * (size_t)(m * n + m) * sizeof(float);
+}
+
+int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A, const float* B,
+                                float* C, float* colsum_A, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  GMP_CHECK_ARG(K >= 0 && C && m > 0 && n > 0 && m % 16 == 0 && n % 16 == 0 && m <= kT);
+  if ((m / 16) * (n / 16) > 4 * kMaxTilesPerWave) return GMP_ERR_UNSUPPORTED;
+  hipStream_t s = as_stream(stream);
+  if (K == 0) {
+    int rc = hip_check(hipMemsetAsync(C, 0, m * n * sizeof(float), s));
+    if (!rc && colsum_A) rc = hip_check(hipMemsetAsync(colsum_A, 0, m * sizeof(float), s));
+    return rc;
+  }
+  GMP_CHECK_ARG(A && B && workspace);
+  GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0);
+  if (workspace_bytes < gmp_edge_outer_sum_rect_workspace_size(K, m, n)) return GMP_ERR_WORKSPACE;
+  const int64_t G = blocks_for(K);
+  const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
+  const int64_t Gr = ceil_div(K, per);
+  float* part = reinterpret_cast<float*>(workspace);
+  const size_t smem = (size_t)(kKT * (m + kRectLD) + kKT * (n + kRectLD) + kT) * sizeof(float);
+  int rc = hip_check(hipFuncSetAttribute((const void*)outer_sum_rect_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  if (rc) return rc;
+  outer_sum_rect_kernel<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, per, part);
+  rc = launch_status();
+  if (rc) return rc;
+  const int64_t X = m * n + m;
+  const int64_t NC = ceil_div(Gr, kGC);
+  float* l1 = part + Gr * X;
+  sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
+  rc = launch_status();
+  if (rc) return rc;
+  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, m * n);
   return launch_status();
 }
 

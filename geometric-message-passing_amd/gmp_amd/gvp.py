@@ -76,9 +76,10 @@ class GVP(nn.Module):
         """Everything after s' = W_s[...] given the pre-activation s' and vh (B, 3, h)."""
         v = None
         if self.vo:
-            v = self.wv(vh).transpose(-1, -2)
+            v = ops.linear(vh, self.wv.weight).transpose(-1, -2)
             if self.vector_gate:
-                gate = self.wsv(self.vector_act(s) if self.vector_act else s)
+                gate = ops.linear(self.vector_act(s) if self.vector_act else s,
+                                  self.wsv.weight, self.wsv.bias)
                 v = v * torch.sigmoid(gate).unsqueeze(-1)
             elif self.vector_act:
                 v = v * self.vector_act(_norm_no_nan(v, axis=-1, keepdims=True))
@@ -89,8 +90,9 @@ class GVP(nn.Module):
     def forward(self, x):
         if self.vi:
             s, v = x
-            vh = self.wh(v.transpose(-1, -2))
-            s = self.ws(torch.cat([s, _norm_no_nan(vh, axis=-2)], -1))
+            vh = ops.linear(v.transpose(-1, -2), self.wh.weight)
+            s = ops.linear(torch.cat([s, _norm_no_nan(vh, axis=-2)], -1), self.ws.weight,
+                           self.ws.bias)
             return self._tail(s, vh)
         s = self.ws(x)
         v = torch.zeros(s.shape[0], self.vo, 3, device=s.device, dtype=s.dtype) if self.vo \
@@ -207,10 +209,12 @@ class GVPConv(MessagePassing):
         Qj = ops.gather(Q.view(n, 3, 2 * h)[:, :, :h].reshape(n, 3 * h), j, 0).view(-1, 3, h)
         Qi = ops.gather(Q.view(n, 3, 2 * h)[:, :, h:].reshape(n, 3 * h), i, 0).view(-1, 3, h)
         es, ev = edge_attr
-        vh = Qj + Qi + ev.transpose(-1, -2).matmul(Wh[:, vi:vi + ve].t())
+        evt = ev.transpose(-1, -2)                 # (E, 3, ve)
+        vh = Qj + Qi + ops.linear(evt, Wh[:, vi:vi + ve])
         vn = _norm_no_nan(vh, axis=-2)
-        s1 = torch.addmm(g0.ws.bias, es, Ws[:, si:si + se].t()) + Pj + Pi + \
-            vn.matmul(Ws[:, 2 * si + se:].t())
+        # edge part of W_s on [e_s | |vh|] as one per-edge Linear (dW by the edge outer sum)
+        We = torch.cat([Ws[:, si:si + se], Ws[:, 2 * si + se:]], 1)
+        s1 = ops.linear(torch.cat([es, vn], -1), We, g0.ws.bias) + Pj + Pi
         out = g0._tail(s1, vh)
         for mod in list(self.message_func)[1:]:
             out = mod(out)

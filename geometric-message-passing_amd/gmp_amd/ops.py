@@ -189,6 +189,72 @@ def edge_outer_sum(A, B, with_colsum=True):
     return C, cs
 
 
+def edge_outer_sum_rect(A, B):
+    """(A^T B, colsum(A)) over the rows (edges) for any widths: columns are zero-padded to
+    multiples of 16 for gmp_edge_outer_sum_rect_f32 (deterministic split-K).  Returns None when
+    the padded shape exceeds the kernel's tile budget."""
+    lib = _lib.load()
+    A, B = _f32c(A), _f32c(B)
+    _need_cuda(A, B)
+    K, m, n = A.shape[0], A.shape[1], B.shape[1]
+    mp, np_ = -(-m // 16) * 16, -(-n // 16) * 16
+    if mp > 256 or (mp // 16) * (np_ // 16) > 72:
+        return None
+    if mp != m:
+        A = torch.nn.functional.pad(A, (0, mp - m))
+    if np_ != n:
+        B = torch.nn.functional.pad(B, (0, np_ - n))
+    C = torch.empty((mp, np_), dtype=torch.float32, device=A.device)
+    cs = torch.empty(mp, dtype=torch.float32, device=A.device)
+    ws_bytes = lib.gmp_edge_outer_sum_rect_workspace_size(K, mp, np_)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=A.device)
+    with _timed("edge_outer_sum"):
+        check(lib.gmp_edge_outer_sum_rect_f32(K, mp, np_, _p(A), _p(B), _p(C), _p(cs), _p(ws),
+                                              ws_bytes, _stream()), "gmp_edge_outer_sum_rect_f32")
+    return C[:m, :n], cs[:m]
+
+
+class EdgeLinearFn(torch.autograd.Function):
+    """y = x W^T (+ b) over many rows (edges): forward and dx with the library GEMM (M = rows),
+    dW / db with the deterministic edge outer sum (K = rows), which the library's small-tile
+    K-reduction GEMMs run far below the HBM roofline."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return torch.addmm(b, x, W.t()) if b is not None else x.mm(W.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        g = g.contiguous()
+        dx = g.mm(W) if ctx.needs_input_grad[0] else None
+        dW = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+            r = edge_outer_sum_rect(g, x)
+            if r is None:
+                dW, db = g.t().mm(x), g.sum(0)
+            else:
+                dW, db = r
+        return dx, dW, (db if ctx.has_b else None)
+
+
+EDGE_LINEAR_MIN_ROWS = 1 << 16
+
+
+def linear(x, W, b=None):
+    """F.linear for (..., in) inputs; row counts >= EDGE_LINEAR_MIN_ROWS on the GPU take the
+    EdgeLinearFn path (deterministic outer-sum weight gradients)."""
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    if x2.is_cuda and x2.shape[0] >= EDGE_LINEAR_MIN_ROWS and x2.dtype == torch.float32:
+        y = EdgeLinearFn.apply(x2.contiguous(), W, b)
+    else:
+        y = torch.nn.functional.linear(x2, W, b)
+    return y.reshape(shp[:-1] + (W.shape[0],))
+
+
 def segment_reduce_bwd(grad_out, csr, reduce, argmax, n_items):
     lib = _lib.load()
     grad_out = _f32c(grad_out)

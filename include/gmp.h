@@ -161,6 +161,14 @@ int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B,
                            float* colsum_A, void* workspace, size_t workspace_bytes,
                            void* stream);
 
+/* Rectangular variant (GVP message GVPs, gvp_layer.py:101-170 applied per edge at :319-324):
+ * C (m x n) = A^T B, A (K, m), B (K, n) row-major, m, n multiples of 16, m <= 256,
+ * (m/16)(n/16) <= 72; colsum_A (m) optional.  Same deterministic split-K reduction. */
+size_t gmp_edge_outer_sum_rect_workspace_size(int64_t K, int64_t m, int64_t n);
+int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A, const float* B,
+                                float* C, float* colsum_A, void* workspace,
+                                size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * K1 per-edge featurisation (models/mace.py:170-174, models/tfn.py:171-175,
  * models/mace_modules/radial.py:44-46,71-78, blocks.py:91-96; e3nn SphericalHarmonics(l<=2,

@@ -59,9 +59,12 @@ def test_gvp_model_golden(golden):
     _scaled(p.grad, d["grad_pos"], 1e-4, "grad_pos")
 
 
-@pytest.mark.parametrize("fast", [True, False])
-def test_gvp_conv_layer_c3_widths_vs_oracle(fast):
+@pytest.mark.parametrize("fast,edge_linear", [(True, True), (True, False), (False, True)])
+def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, monkeypatch):
     import gmp_amd.gvp as g
+    from gmp_amd import ops
+    # small graphs: force the per-edge Linear path (outer-sum dW) on, or off
+    monkeypatch.setattr(ops, "EDGE_LINEAR_MIN_ROWS", 1 if edge_linear else 1 << 62)
     from gmp_amd.graph import radius_graph
     torch.manual_seed(5)
     gr = radius_graph(num_nodes=600, target_edges=9000, r=2.0, seed=4, tol=0.2, shuffle=True)
@@ -115,3 +118,18 @@ def test_gvp_model_c3_vs_oracle():
     y.sum().backward()
     yr.sum().backward()
     _scaled(pd.grad, pr.grad, 2e-4, "grad_pos")
+
+
+@pytest.mark.parametrize("m,n,K", [(128, 144, 7777), (128, 65, 3000), (16, 128, 5000),
+                                   (16, 33, 12345), (16, 16, 100), (48, 48, 0)])
+def test_edge_outer_sum_rect(m, n, K):
+    from gmp_amd import ops
+    torch.manual_seed(m + n)
+    A = torch.randn(K, m, dtype=torch.float64)
+    B = torch.randn(K, n, dtype=torch.float64)
+    C, cs = ops.edge_outer_sum_rect(A.float().to(DEV), B.float().to(DEV))
+    ref = A.t() @ B
+    assert (C.double().cpu() - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+    assert (cs.double().cpu() - A.sum(0)).abs().max().item() <= 1e-4
+    C2, _ = ops.edge_outer_sum_rect(A.float().to(DEV), B.float().to(DEV))
+    assert torch.equal(C, C2)  # deterministic
