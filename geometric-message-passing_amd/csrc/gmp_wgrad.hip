@@ -153,73 +153,127 @@ __global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t
 }
 
 // Rectangular variant for the other per-edge Linears (GVP message GVPs: 128 x 144, 128 x 80,
-// 16 x 128, 16 x 48, 16 x 16): C (M x N) = A^T B with M, N multiples of 16, T = (M/16)(N/16) <= 72
-// output tiles dealt round-robin to the 4 waves (<= 18 accumulator tiles each).  Same split-K /
-// ordered partial-sum scheme; A and B tiles of kKT edges staged through LDS.
-constexpr int kMaxTilesPerWave = 18;
-constexpr int kRectLD = 8;  // LDS row padding (floats)
+// 16 x 128, 16 x 48, 16 x 16): C (M x N) = A^T B with M, N multiples of 16.  Wave tiling: with
+// >= 4 row tiles a wave owns row tiles {w, w+4, ..} x all column tiles, otherwise all row tiles x
+// column tiles {w, w+4, ..}; operands are read from LDS once per tile row / column (register
+// reuse across the wave's tiles).  Register-staged double buffering of kKT-edge tiles; same
+// split-K / ordered partial-sum scheme as above.
+constexpr int kRectLD = 4;   // LDS row padding (floats)
+constexpr int kMaxL = 9;     // float4 loads per thread per tile (kKT * (M + N) / 4 / kT)
 
-__global__ __launch_bounds__(kT, 2) void outer_sum_rect_kernel(
+template <int MR, int MC>
+__global__ __launch_bounds__(kT, 1) void outer_sum_rect_kernel(
     const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
     int64_t k_per_block, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int LDA = M + kRectLD, LDB = N + kRectLD;
-  float* sA = sm;                      // kKT x LDA
-  float* sB = sA + kKT * LDA;          // kKT x LDB
-  float* sCol = sB + kKT * LDB;        // kT floats (colsum partials)
+  const int TILE = kKT * (LDA + LDB);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, kk = lane >> 4;
-  const int TN = N >> 4, T = (M >> 4) * TN;
+  const int TM = M >> 4, TN = N >> 4;
+  const bool rows_mode = TM >= 4;
+  const int RT = rows_mode ? (TM - w + 3) / 4 : TM;
+  const int CT = rows_mode ? TN : (TN - w + 3) / 4;
   const int64_t k0 = (int64_t)blockIdx.x * k_per_block;
   const int64_t k1 = (k0 + k_per_block < K) ? k0 + k_per_block : K;
-  f32x4 acc[kMaxTilesPerWave];
+  f32x4 acc[MR][MC];
 #pragma unroll
-  for (int q = 0; q < kMaxTilesPerWave; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float csum = 0.f;  // colsum(A) of column tid (tid < M), accumulated by its owner thread
-  const int CA = M >> 2, CB = N >> 2, CT = CA + CB;  // float4 chunks per edge row
-  for (int64_t kb = k0; kb < k1; kb += kKT) {
-    __syncthreads();
-    for (int c = tid; c < kKT * CT; c += kT) {
-      const int r = c / CT, q = c - r * CT;
-      const int64_t k = kb + r;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (q < CA) {
-        if (k < k1) v = *reinterpret_cast<const f32x4*>(A + k * M + 4 * q);
-        *reinterpret_cast<f32x4*>(&sA[r * LDA + 4 * q]) = v;
-      } else {
-        if (k < k1) v = *reinterpret_cast<const f32x4*>(B + k * N + 4 * (q - CA));
-        *reinterpret_cast<f32x4*>(&sB[r * LDB + 4 * (q - CA)]) = v;
+  for (int r = 0; r < MR; ++r)
+#pragma unroll
+    for (int c = 0; c < MC; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float csum = 0.f;
+  const int CA = M >> 2, CTOT = (M + N) >> 2;
+  const int NLD = kKT * CTOT;
+  f32x4 reg[kMaxL];
+  auto fetch = [&](int64_t kb) {
+#pragma unroll
+    for (int q = 0; q < kMaxL; ++q) {
+      const int c = tid + q * kT;
+      reg[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (c < NLD) {
+        const int r = c / CTOT, x = c - r * CTOT;
+        const int64_t k = kb + r;
+        if (k < k1)
+          reg[q] = (x < CA) ? *reinterpret_cast<const f32x4*>(A + k * M + 4 * x)
+                            : *reinterpret_cast<const f32x4*>(B + k * N + 4 * (x - CA));
       }
     }
-    __syncthreads();
+  };
+  auto stash = [&](float* buf) {
+#pragma unroll
+    for (int q = 0; q < kMaxL; ++q) {
+      const int c = tid + q * kT;
+      if (c < NLD) {
+        const int r = c / CTOT, x = c - r * CTOT;
+        float* dst = (x < CA) ? buf + r * LDA + 4 * x : buf + kKT * LDA + r * LDB + 4 * (x - CA);
+        *reinterpret_cast<f32x4*>(dst) = reg[q];
+      }
+    }
+  };
+  int cur = 0;
+  if (k0 < k1) {
+    fetch(k0);
+    stash(sm);
+  }
+  __syncthreads();
+  for (int64_t kb = k0; kb < k1; kb += kKT) {
+    const bool more = kb + kKT < k1;
+    if (more) fetch(kb + kKT);
+    const float* sA = sm + cur * TILE;
+    const float* sB = sA + kKT * LDA;
     if (tid < M)
       for (int r = 0; r < kKT; ++r) csum += sA[r * LDA + tid];
 #pragma unroll
-    for (int s = 0; s < kKT / 4; ++s) {
-      const int e = 4 * s + kk;
+    for (int st = 0; st < kKT / 4; ++st) {
+      const int e = 4 * st + kk;
+      float af[MR], bf[MC];
 #pragma unroll
-      for (int q = 0; q < kMaxTilesPerWave; ++q) {
-        const int t = w + 4 * q;
-        if (t < T) {
-          const int tm = t / TN, tn = t - tm * TN;
-          const float af = sA[e * LDA + 16 * tm + li];
-          const float bf = sB[e * LDB + 16 * tn + li];
-          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, bf, acc[q], 0, 0, 0);
-        }
+      for (int r = 0; r < MR; ++r) {
+        const int tm = rows_mode ? w + 4 * r : r;
+        af[r] = (r < RT) ? sA[e * LDA + 16 * tm + li] : 0.f;
       }
+#pragma unroll
+      for (int c = 0; c < MC; ++c) {
+        const int tn = rows_mode ? c : w + 4 * c;
+        bf[c] = (c < CT) ? sB[e * LDB + 16 * tn + li] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < MR; ++r)
+#pragma unroll
+        for (int c = 0; c < MC; ++c)
+          if (r < RT && c < CT)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[r], bf[c], acc[r][c], 0, 0, 0);
     }
+    if (more) stash(sm + (cur ^ 1) * TILE);
+    __syncthreads();
+    cur ^= 1;
   }
   float* out = partial + (int64_t)blockIdx.x * ((int64_t)M * N + M);
 #pragma unroll
-  for (int q = 0; q < kMaxTilesPerWave; ++q) {
-    const int t = w + 4 * q;
-    if (t < T) {
-      const int tm = t / TN, tn = t - tm * TN;
+  for (int r = 0; r < MR; ++r)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(16 * tm + 4 * kk + r) * N + 16 * tn + li] = acc[q][r];
-    }
-  }
+    for (int c = 0; c < MC; ++c)
+      if (r < RT && c < CT) {
+        const int tm = rows_mode ? w + 4 * r : r;
+        const int tn = rows_mode ? c : w + 4 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(16 * tm + 4 * kk + q) * N + 16 * tn + li] = acc[r][c][q];
+      }
   if (tid < M) out[(int64_t)M * N + tid] = csum;
+}
+
+// capacity bucket for (M, N): returns 0 if unsupported
+int rect_bucket(int64_t m, int64_t n) {
+  const int64_t TM = m / 16, TN = n / 16;
+  int64_t RT, CT;
+  if (TM >= 4) { RT = (TM + 3) / 4; CT = TN; }
+  else { RT = TM; CT = (TN + 3) / 4; }
+  if ((m + n) / 4 * kKT > (int64_t)kMaxL * kT) return 0;
+  if (RT <= 1 && CT <= 3) return 1;
+  if (RT <= 2 && CT <= 5) return 2;
+  if (RT <= 2 && CT <= 9) return 3;
+  if (RT <= 4 && CT <= 4) return 4;
+  return 0;
 }
 
 int64_t blocks_for(int64_t K) {
@@ -283,7 +337,8 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
                                 float* C, float* colsum_A, void* workspace,
                                 size_t workspace_bytes, void* stream) {
   GMP_CHECK_ARG(K >= 0 && C && m > 0 && n > 0 && m % 16 == 0 && n % 16 == 0 && m <= kT);
-  if ((m / 16) * (n / 16) > 4 * kMaxTilesPerWave) return GMP_ERR_UNSUPPORTED;
+  const int bucket = rect_bucket(m, n);
+  if (!bucket) return GMP_ERR_UNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if (K == 0) {
     int rc = hip_check(hipMemsetAsync(C, 0, m * n * sizeof(float), s));
@@ -297,11 +352,24 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-  const size_t smem = (size_t)(kKT * (m + kRectLD) + kKT * (n + kRectLD) + kT) * sizeof(float);
-  int rc = hip_check(hipFuncSetAttribute((const void*)outer_sum_rect_kernel,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-  if (rc) return rc;
-  outer_sum_rect_kernel<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, per, part);
+  const size_t smem = (size_t)2 * kKT * (m + kRectLD + n + kRectLD) * sizeof(float);
+  int rc;
+#define GMP_RECT(MR, MC)                                                                      \
+  {                                                                                           \
+    auto k = outer_sum_rect_kernel<MR, MC>;                                                   \
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                   \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                            (int)smem))))                                     \
+      return rc;                                                                              \
+    k<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, per, part);                     \
+  }
+  switch (bucket) {
+    case 1: GMP_RECT(1, 3) break;
+    case 2: GMP_RECT(2, 5) break;
+    case 3: GMP_RECT(2, 9) break;
+    default: GMP_RECT(4, 4) break;
+  }
+#undef GMP_RECT
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;

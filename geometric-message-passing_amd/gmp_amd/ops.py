@@ -209,8 +209,11 @@ def edge_outer_sum_rect(A, B):
     ws_bytes = lib.gmp_edge_outer_sum_rect_workspace_size(K, mp, np_)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=A.device)
     with _timed("edge_outer_sum"):
-        check(lib.gmp_edge_outer_sum_rect_f32(K, mp, np_, _p(A), _p(B), _p(C), _p(cs), _p(ws),
-                                              ws_bytes, _stream()), "gmp_edge_outer_sum_rect_f32")
+        rc = lib.gmp_edge_outer_sum_rect_f32(K, mp, np_, _p(A), _p(B), _p(C), _p(cs), _p(ws),
+                                             ws_bytes, _stream())
+    if rc == _lib.GMP_ERR_UNSUPPORTED:  # shape outside the kernel's tile buckets
+        return None
+    check(rc, "gmp_edge_outer_sum_rect_f32")
     return C[:m, :n], cs[:m]
 
 
