@@ -189,17 +189,10 @@ def edge_outer_sum(A, B, with_colsum=True):
     return C, cs
 
 
-def edge_outer_sum_rect(A, B):
-    """(A^T B, colsum(A)) over the rows (edges) for any widths: columns are zero-padded to
-    multiples of 16 for gmp_edge_outer_sum_rect_f32 (deterministic split-K).  Returns None when
-    the padded shape exceeds the kernel's tile budget."""
+def _outer_sum_rect_call(A, B):
     lib = _lib.load()
-    A, B = _f32c(A), _f32c(B)
-    _need_cuda(A, B)
     K, m, n = A.shape[0], A.shape[1], B.shape[1]
     mp, np_ = -(-m // 16) * 16, -(-n // 16) * 16
-    if mp > 256 or (mp // 16) * (np_ // 16) > 72:
-        return None
     if mp != m:
         A = torch.nn.functional.pad(A, (0, mp - m))
     if np_ != n:
@@ -215,6 +208,29 @@ def edge_outer_sum_rect(A, B):
         return None
     check(rc, "gmp_edge_outer_sum_rect_f32")
     return C[:m, :n], cs[:m]
+
+
+def edge_outer_sum_rect(A, B):
+    """(A^T B, colsum(A)) over the rows (edges / nodes) for any widths, deterministic: columns
+    zero-padded to multiples of 16 for gmp_edge_outer_sum_rect_f32, wide operands split into
+    <= 128 x 144 blocks.  None when a block shape is outside the kernel's buckets."""
+    A, B = _f32c(A), _f32c(B)
+    _need_cuda(A, B)
+    m, n = A.shape[1], B.shape[1]
+    if m <= 128 and n <= 144:
+        return _outer_sum_rect_call(A, B)
+    C = torch.empty((m, n), dtype=torch.float32, device=A.device)
+    cs = torch.empty(m, dtype=torch.float32, device=A.device)
+    for m0 in range(0, m, 128):
+        Am = A[:, m0:m0 + 128].contiguous()
+        for n0 in range(0, n, 128):
+            r = _outer_sum_rect_call(Am, B[:, n0:n0 + 128].contiguous())
+            if r is None:
+                return None
+            C[m0:m0 + 128, n0:n0 + 128] = r[0]
+            if n0 == 0:
+                cs[m0:m0 + 128] = r[1]
+    return C, cs
 
 
 class EdgeLinearFn(torch.autograd.Function):
@@ -243,7 +259,7 @@ class EdgeLinearFn(torch.autograd.Function):
         return dx, dW, (db if ctx.has_b else None)
 
 
-EDGE_LINEAR_MIN_ROWS = 1 << 16
+EDGE_LINEAR_MIN_ROWS = 1 << 15
 
 
 def linear(x, W, b=None):
