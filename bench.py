@@ -197,7 +197,12 @@ def main():
     args.layers = args.layers or d_layers
     args.emb = args.emb or d_emb
     from gmp_amd import dist as gdist
-    rank, world, local = gdist.init("nccl")
+    # GMP_DIST_BACKEND=gloo rehearses the multi-process path with several ranks on one GPU
+    backend = os.environ.get("GMP_DIST_BACKEND", "nccl")
+    rank, world, local = gdist.init(backend)
+    if backend != "nccl":
+        local = 0
+        torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
 
     import gmp_amd
@@ -208,7 +213,10 @@ def main():
     torch.manual_seed(0)
     model = build_model(gmp_amd, args, g.radius).to(dev)
     core = model
-    model = gdist.wrap_ddp(model, local, bucket_cap_mb=32)
+    # the fused EGNN path gives every parameter a gradient (checked in the gloo rehearsal), so
+    # DDP can skip the per-step unused-parameter traversal there
+    model = gdist.wrap_ddp(model, local if backend == "nccl" else None, bucket_cap_mb=32,
+                           find_unused_parameters=args.workload != "egnn")
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     batch = g.to(dev)
     y = torch.randn(1, device=dev)

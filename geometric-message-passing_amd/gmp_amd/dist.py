@@ -53,7 +53,7 @@ def barrier(cuda=True):
         torch.cuda.synchronize()
 
 
-def wrap_ddp(model, local=None, bucket_cap_mb=32):
+def wrap_ddp(model, local=None, bucket_cap_mb=32, find_unused_parameters=True):
     """DDP with buckets sized for xGMI ring all-reduce (few, large buckets).
     find_unused_parameters: the reference models leave parameters without gradient (EGNN's last
     position MLP, TFN/MACE readout slices), which a plain DDP reducer would wait for forever."""
@@ -62,4 +62,4 @@ def wrap_ddp(model, local=None, bucket_cap_mb=32):
     ids = [local] if local is not None else None
     return torch.nn.parallel.DistributedDataParallel(model, device_ids=ids,
                                                      bucket_cap_mb=bucket_cap_mb,
-                                                     find_unused_parameters=True)
+                                                     find_unused_parameters=find_unused_parameters)
