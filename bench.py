@@ -274,12 +274,16 @@ def main():
             # receiver-factorised K7: rocBLAS GEMMs over S / T (timed region "tp_node_gemm"
             # includes the padded gathers) — MFMA-bound; algorithmic flops per step below
             fl = tp_node_flops(core, g.num_nodes, g.num_edges)
-            t_gemm = sum_ms("tp_node_gemm") / args.steps
+            t_gemm = sum(sum_ms(k) for k in ("tp_node_S", "tp_node_W", "tp_node_dW",
+                                              "tp_node_dZA")) / args.steps
             achieved = fl / (t_gemm * 1e-3) / 1e12
             roof = {"kernel": "tp_node_gemm", "kernel_prefix": "-", "bound": "mfma",
                     "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
                     "flops_per_step": fl, "tp_node_gemm_ms_per_step": t_gemm,
+                    "split_ms_per_step": {k: sum_ms(k) / args.steps for k in
+                                          ("tp_node_S", "tp_node_W", "tp_node_dW",
+                                           "tp_node_dZA")},
                     "tp_node_prep_ms_per_step": sum_ms("tp_node_prep") / args.steps,
                     "tp_node_edge_bwd_ms_per_step": sum_ms("tp_node_edge_bwd") / args.steps,
                     "symmetric_contraction_ms_per_step":

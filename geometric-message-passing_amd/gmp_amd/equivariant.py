@@ -273,6 +273,7 @@ class TPGraph:
             rp = self.rowptr.cpu()
             deg = rp[1:] - rp[:-1]
             dmax = int(deg.max()) if deg.numel() else 0
+            dmax = -(-dmax // 8) * 8  # padded in-degree: 32-byte aligned batched-GEMM operands
             slot = torch.arange(self.num_edges, device=self.rowptr.device) - \
                 self.rowptr[self.recv_sorted]
             self._node_form = (rp.tolist(), dmax, slot)
@@ -461,12 +462,20 @@ NODE_CHUNK_BYTES = int(os.environ.get("GMP_TP_NODE_CHUNK_BYTES", str(2 << 30)))
 TP_MODE = os.environ.get("GMP_TP_MODE", "node")  # "node" (receiver-factorised) | "edge"
 
 
+def _jpad(hidden):
+    """a_e = [relu(.) (hidden) | 1 | 0 ...] padded to a multiple of 8 columns (aligned GEMMs)."""
+    return -(-(hidden + 1) // 8) * 8
+
+
 def _w2_ext(W2, b2, P):
-    """Path block of [W2 | b2] as (mul1 * 257, mul_out): row (u, j), column w."""
+    """Path block of [W2 | b2 | 0] as (mul1 * J, mul_out): row (u, j), column w."""
     m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
-    blk = torch.cat([W2[off:off + m1 * mo].view(m1, mo, -1),
-                     b2[off:off + m1 * mo].view(m1, mo, 1)], dim=2)
-    return blk.permute(0, 2, 1).reshape(m1 * blk.shape[2], mo)
+    H = W2.shape[1]
+    J = _jpad(H)
+    blk = torch.cat([W2[off:off + m1 * mo].view(m1, mo, H),
+                     b2[off:off + m1 * mo].view(m1, mo, 1),
+                     W2.new_zeros(m1, mo, J - H - 1)], dim=2)
+    return blk.permute(0, 2, 1).reshape(m1 * J, mo)
 
 
 class TPConvNodeFn(torch.autograd.Function):
@@ -495,9 +504,10 @@ class TPConvNodeFn(torch.autograd.Function):
             for P, W2p, (zoff, w) in zip(plan.instructions, W2x, plan.z_regions):
                 d3 = 2 * P["lo"] + 1
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                with _timed("tp_node_gemm"):
+                with _timed("tp_node_S"):
                     Zpad = ops.gather_rows(Zp, idx).view(c, -1, w)
                     S = torch.bmm(Zpad.transpose(1, 2), Apad).view(c * d3, -1)
+                with _timed("tp_node_W"):
                     op = S.mm(W2p).view(c, d3, P["mul_out"])
                 blk = plan.blocks[P["io"]]
                 out[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, blk[1], d3).add_(
@@ -530,17 +540,20 @@ class TPConvNodeFn(torch.autograd.Function):
                 d3, mo = 2 * P["lo"] + 1, P["mul_out"]
                 blk = plan.blocks[P["io"]]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                with _timed("tp_node_gemm"):
+                with _timed("tp_node_S"):
                     Zpad = ops.gather_rows(Zp, idx).view(c, -1, w)
                     S = torch.bmm(Zpad.transpose(1, 2), Apad).view(c * d3, -1)
-                    G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
-                    G = G.reshape(c * d3, mo)
+                G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
+                G = G.reshape(c * d3, mo)
+                with _timed("tp_node_dW"):
                     dW2p.addmm_(S.t(), G)
-                    del S
+                del S
+                with _timed("tp_node_W"):
                     T = G.mm(W2p.t()).view(c, w, -1)
+                with _timed("tp_node_dZA"):
                     dZpad = torch.bmm(Apad, T.transpose(1, 2)).view(c * Zpad.shape[1], w)
                     dApad.baddbmm_(Zpad, T)
-                    del T
+                del T
                 dZp = dzbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 dZp[:ne] = ops.gather_rows(dZpad, pos)
             with _timed("tp_node_edge_bwd"):
@@ -550,18 +563,19 @@ class TPConvNodeFn(torch.autograd.Function):
                                                 _p(dzbuf), _p(dx_edge[e0:e1]), _p(dY[e0:e1]),
                                                 _stream()),
                       "gmp_tp_edge_z_bwd_f32")
-            da = ops.gather_rows(dApad.view(-1, dApad.shape[2]), pos)[:, :-1]
+            da = ops.gather_rows(dApad.view(-1, dApad.shape[2]), pos)[:, :W1.shape[0]]
             dpre = da * (pre > 0)
             r = rad_s[e0:e1]
             dW1.addmm_(dpre.t(), r)
             db1.add_(dpre.sum(0))
             drad_s[e0:e1] = dpre.mm(W1)
         dW2, db2 = torch.empty_like(W2), torch.empty_like(b2)
+        H = W2.shape[1]
         for P, g in zip(plan.instructions, dW2x):
             m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
-            g3 = g.view(m1, -1, mo).permute(0, 2, 1)  # (m1, mo, 257)
-            dW2[off:off + m1 * mo] = g3[:, :, :-1].reshape(m1 * mo, -1)
-            db2[off:off + m1 * mo] = g3[:, :, -1].reshape(-1)
+            g3 = g.view(m1, -1, mo).permute(0, 2, 1)  # (m1, mo, J)
+            dW2[off:off + m1 * mo] = g3[:, :, :H].reshape(m1 * mo, H)
+            db2[off:off + m1 * mo] = g3[:, :, H].reshape(-1)
         dx, _ = ops.segment_reduce(dx_edge, graph.src_csr, "sum")
         dsh = torch.empty_like(sh).index_copy_(0, graph.perm, dY)
         drad = torch.empty((E, rad_s.shape[1]), **f).index_copy_(0, graph.perm, drad_s)
@@ -575,7 +589,8 @@ def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):
     if graph.num_edges == 0 or dmax == 0:
         return
     hidden = W1.shape[0]
-    per_node = max(plan.max_block_rows * (hidden + 1), dmax * plan.desc.z_size) * 4
+    J = _jpad(hidden)
+    per_node = max(plan.max_block_rows * J, dmax * plan.desc.z_size) * 4
     npc = max(1, NODE_CHUNK_BYTES // per_node)
     for n0, n1, e0, e1 in graph.node_chunks(npc):
         if e1 == e0:
@@ -584,10 +599,10 @@ def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):
         idx, pos = graph.chunk_pad(n0, n1, e0, e1)
         with _timed("tp_node_prep"):
             pre = torch.addmm(b1, rad_s[e0:e1], W1.t())
-            a = torch.ones((ne + 1, hidden + 1), dtype=torch.float32, device=x.device)
+            a = torch.zeros((ne + 1, J), dtype=torch.float32, device=x.device)
             a[:ne, :hidden] = torch.relu(pre)
-            a[ne].zero_()
-            Apad = ops.gather_rows(a, idx).view(c, dmax, hidden + 1)
+            a[:ne, hidden] = 1.0
+            Apad = ops.gather_rows(a, idx).view(c, dmax, J)
             zbuf = torch.empty(((ne + 1) * plan.desc.z_size,), dtype=torch.float32,
                                device=x.device)
             for zoff, w in plan.z_regions:
