@@ -80,6 +80,9 @@ SIGNATURES = {
     "gmp_edge_outer_sum_rect_workspace_size": (c_size, [c_i64, c_i64, c_i64]),
     "gmp_edge_outer_sum_rect_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_size, c_vp]),
+    "gmp_tp_node_outer_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_tp_node_apply_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp]),
     "gmp_sc_groups": (c_int, [c_i64]),
     "gmp_symmetric_contraction_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp]),

@@ -462,31 +462,30 @@ NODE_CHUNK_BYTES = int(os.environ.get("GMP_TP_NODE_CHUNK_BYTES", str(2 << 30)))
 TP_MODE = os.environ.get("GMP_TP_MODE", "node")  # "node" (receiver-factorised) | "edge"
 
 
-def _jpad(hidden):
-    """a_e = [relu(.) (hidden) | 1 | 0 ...] padded to a multiple of 8 columns (aligned GEMMs)."""
-    return -(-(hidden + 1) // 8) * 8
-
-
-def _w2_ext(W2, b2, P):
-    """Path block of [W2 | b2 | 0] as (mul1 * J, mul_out): row (u, j), column w."""
+def _w2_path(W2, b2, P):
+    """Path block of W2 as (mul1 * H, mul_out) [row (u, j), column w] and of b2 as
+    (mul1, mul_out)."""
     m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
     H = W2.shape[1]
-    J = _jpad(H)
-    blk = torch.cat([W2[off:off + m1 * mo].view(m1, mo, H),
-                     b2[off:off + m1 * mo].view(m1, mo, 1),
-                     W2.new_zeros(m1, mo, J - H - 1)], dim=2)
-    return blk.permute(0, 2, 1).reshape(m1 * J, mo)
+    return (W2[off:off + m1 * mo].view(m1, mo, H).permute(0, 2, 1).reshape(m1 * H, mo),
+            b2[off:off + m1 * mo].view(m1, mo))
+
+
+def node_form_ok(hidden):
+    return hidden % 16 == 0 and hidden <= 256
 
 
 class TPConvNodeFn(torch.autograd.Function):
     """out = scatter_sum_{ei0}(FCTP(x[ei1], sh, fc(radial)))  (tfn_layer.py:82-87), evaluated in
-    receiver-factorised form: with a_e = [relu(W1 r_e + b1), 1] (257) the per-edge weights are
-    W_e = [W2 | b2] a_e, so for receiver n and path p
-        out_n[w, k] = sum_{u, j} [W2|b2][(u, w), j] S_n[k, u, j],   S_n = sum_{e -> n} z_e (x) a_e.
-    S is a batched GEMM over degree-padded receivers (K = max in-degree) and the contraction with
-    W2 one GEMM per path with K = mul1 * 257: E * 256 * weight_numel MACs become
-    N * 257 * sum_p mul1 mul_out (2lo+1) + E * 257 * z_size (N = E / 20 here).  Backward uses
-    T = G [W2|b2]^T (same shape as S) for dz and da, and dW2 = G^T S."""
+    receiver-factorised form: with a_e = relu(W1 r_e + b1) (H) the per-edge weights are
+    W_e = W2 a_e + b2, so for receiver n and path p
+        out_n[w, k] = sum_{u, j} W2[(u, w), j] S_n[k, u, j] + sum_u b2[u, w] Sb_n[k, u],
+        S_n = sum_{e -> n} z_e (x) a_e,   Sb_n = sum_{e -> n} z_e.
+    S comes from the per-receiver MFMA kernel (gmp_tp_node_outer_f32, edge index as the MFMA k
+    dimension) and the contraction with W2 is one GEMM per path with K = mul1 * H:
+    E * H * weight_numel MACs become N * H * sum_p mul1 mul_out (2lo+1) + E * H * z_size
+    (N = E / 20 here).  Backward: T = G W2_p^T, Tb = G b2_p^T (GEMMs), then dz = a.T + Tb and
+    da = z.T per edge (gmp_tp_node_apply_f32); dW2 = G^T S, db2 = G^T Sb."""
 
     @staticmethod
     def forward(ctx, x, sh, rad, W1, b1, W2, b2, plan, graph):
@@ -495,23 +494,22 @@ class TPConvNodeFn(torch.autograd.Function):
         _need_cuda(x, sh, rad)
         dev = x.device
         N, E = graph.num_nodes, graph.num_edges
+        H = W1.shape[0]
         out = torch.zeros((N, plan.desc.out_dim), dtype=torch.float32, device=dev)
         rad_s = ops.gather_rows(rad, graph.perm)
-        W2x = [_w2_ext(W2, b2, P) for P in plan.instructions]
-        for n0, n1, e0, e1, idx, pos, Apad, zbuf, _ in _node_chunks(lib, plan, graph, x, sh,
-                                                                       rad_s, W1, b1):
+        W2x = [_w2_path(W2, b2, P) for P in plan.instructions]
+        for n0, n1, e0, e1, eoff, a, zbuf, _ in _node_chunks(lib, plan, graph, x, sh, rad_s,
+                                                             W1, b1):
             c, ne = n1 - n0, e1 - e0
-            for P, W2p, (zoff, w) in zip(plan.instructions, W2x, plan.z_regions):
+            for P, (W2p, b2p), (zoff, w) in zip(plan.instructions, W2x, plan.z_regions):
                 d3 = 2 * P["lo"] + 1
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                with _timed("tp_node_S"):
-                    Zpad = ops.gather_rows(Zp, idx).view(c, -1, w)
-                    S = torch.bmm(Zpad.transpose(1, 2), Apad).view(c * d3, -1)
+                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a)
                 with _timed("tp_node_W"):
-                    op = S.mm(W2p).view(c, d3, P["mul_out"])
+                    op = torch.addmm(Sb.view(c * d3, -1).mm(b2p), S.view(c * d3, -1), W2p)
                 blk = plan.blocks[P["io"]]
                 out[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, blk[1], d3).add_(
-                    op.transpose(1, 2))
+                    op.view(c, d3, -1).transpose(1, 2))
         ctx.plan, ctx.graph = plan, graph
         ctx.save_for_backward(x, sh, rad_s, W1, b1, W2, b2)
         return out
@@ -524,38 +522,40 @@ class TPConvNodeFn(torch.autograd.Function):
         paths_dev, cg_dev = plan.device_tables(x.device)
         gout = _f32c(gout)
         N, E = graph.num_nodes, graph.num_edges
+        H = W1.shape[0]
         f = dict(dtype=torch.float32, device=x.device)
         dx_edge = torch.empty((E, plan.desc.in_dim), **f)
         dY = torch.empty((E, 9), **f)
         drad_s = torch.empty_like(rad_s)
         dW1, db1 = torch.zeros_like(W1), torch.zeros_like(b1)
-        W2x = [_w2_ext(W2, b2, P) for P in plan.instructions]
-        dW2x = [torch.zeros_like(w) for w in W2x]
-        for n0, n1, e0, e1, idx, pos, Apad, zbuf, pre in _node_chunks(lib, plan, graph, x, sh,
-                                                                         rad_s, W1, b1):
+        W2x = [_w2_path(W2, b2, P) for P in plan.instructions]
+        dW2x = [(torch.zeros_like(wp), torch.zeros_like(bp)) for wp, bp in W2x]
+        for n0, n1, e0, e1, eoff, a, zbuf, pre in _node_chunks(lib, plan, graph, x, sh, rad_s,
+                                                               W1, b1):
             c, ne = n1 - n0, e1 - e0
             dzbuf = torch.empty_like(zbuf)
-            dApad = torch.zeros_like(Apad)
-            for P, W2p, dW2p, (zoff, w) in zip(plan.instructions, W2x, dW2x, plan.z_regions):
+            da = torch.zeros((ne, H), **f)
+            for P, (W2p, b2p), (dW2p, db2p), (zoff, w) in zip(plan.instructions, W2x, dW2x,
+                                                              plan.z_regions):
                 d3, mo = 2 * P["lo"] + 1, P["mul_out"]
                 blk = plan.blocks[P["io"]]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                with _timed("tp_node_S"):
-                    Zpad = ops.gather_rows(Zp, idx).view(c, -1, w)
-                    S = torch.bmm(Zpad.transpose(1, 2), Apad).view(c * d3, -1)
+                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a)
                 G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
                 G = G.reshape(c * d3, mo)
                 with _timed("tp_node_dW"):
-                    dW2p.addmm_(S.t(), G)
-                del S
+                    dW2p.addmm_(S.view(c * d3, -1).t(), G)
+                    db2p.addmm_(Sb.view(c * d3, -1).t(), G)
+                del S, Sb
                 with _timed("tp_node_W"):
-                    T = G.mm(W2p.t()).view(c, w, -1)
-                with _timed("tp_node_dZA"):
-                    dZpad = torch.bmm(Apad, T.transpose(1, 2)).view(c * Zpad.shape[1], w)
-                    dApad.baddbmm_(Zpad, T)
-                del T
+                    T = G.mm(W2p.t())
+                    Tb = G.mm(b2p.t())
                 dZp = dzbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                dZp[:ne] = ops.gather_rows(dZpad, pos)
+                with _timed("tp_node_dZA"):
+                    check(lib.gmp_tp_node_apply_f32(c, w, H, _p(eoff), _p(Zp), _p(a), _p(T),
+                                                    _p(Tb), _p(dZp), _p(da), _stream()),
+                          "gmp_tp_node_apply_f32")
+                del T, Tb
             with _timed("tp_node_edge_bwd"):
                 check(lib.gmp_tp_edge_z_bwd_f32(ctypes.byref(plan.desc), _p(paths_dev),
                                                 _p(cg_dev), cg_dev.numel(), _p(x), _p(sh),
@@ -563,55 +563,55 @@ class TPConvNodeFn(torch.autograd.Function):
                                                 _p(dzbuf), _p(dx_edge[e0:e1]), _p(dY[e0:e1]),
                                                 _stream()),
                       "gmp_tp_edge_z_bwd_f32")
-            da = ops.gather_rows(dApad.view(-1, dApad.shape[2]), pos)[:, :W1.shape[0]]
             dpre = da * (pre > 0)
             r = rad_s[e0:e1]
             dW1.addmm_(dpre.t(), r)
             db1.add_(dpre.sum(0))
             drad_s[e0:e1] = dpre.mm(W1)
         dW2, db2 = torch.empty_like(W2), torch.empty_like(b2)
-        H = W2.shape[1]
-        for P, g in zip(plan.instructions, dW2x):
+        for P, (gw, gb) in zip(plan.instructions, dW2x):
             m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
-            g3 = g.view(m1, -1, mo).permute(0, 2, 1)  # (m1, mo, J)
-            dW2[off:off + m1 * mo] = g3[:, :, :H].reshape(m1 * mo, H)
-            db2[off:off + m1 * mo] = g3[:, :, H].reshape(-1)
+            dW2[off:off + m1 * mo] = gw.view(m1, H, mo).permute(0, 2, 1).reshape(m1 * mo, H)
+            db2[off:off + m1 * mo] = gb.reshape(-1)
         dx, _ = ops.segment_reduce(dx_edge, graph.src_csr, "sum")
         dsh = torch.empty_like(sh).index_copy_(0, graph.perm, dY)
         drad = torch.empty((E, rad_s.shape[1]), **f).index_copy_(0, graph.perm, drad_s)
         return dx, dsh, drad, dW1, db1, dW2, db2, None, None
 
 
+def _node_outer(lib, c, w, H, eoff, Zp, a):
+    S = torch.empty((c, w, H), dtype=torch.float32, device=a.device)
+    Sb = torch.empty((c, w), dtype=torch.float32, device=a.device)
+    with _timed("tp_node_S"):
+        check(lib.gmp_tp_node_outer_f32(c, w, H, _p(eoff), _p(Zp), _p(a), _p(S), _p(Sb),
+                                        _stream()), "gmp_tp_node_outer_f32")
+    return S, Sb
+
+
 def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):
-    """Receiver chunks with their padded a rows and z rows (recomputed per pass)."""
+    """Receiver chunks with their chunk-local edge offsets, hidden radial rows a and z rows
+    (recomputed per pass)."""
     paths_dev, cg_dev = plan.device_tables(x.device)
-    _, dmax, _ = graph.node_form()
-    if graph.num_edges == 0 or dmax == 0:
+    if graph.num_edges == 0:
         return
-    hidden = W1.shape[0]
-    J = _jpad(hidden)
-    per_node = max(plan.max_block_rows * J, dmax * plan.desc.z_size) * 4
-    npc = max(1, NODE_CHUNK_BYTES // per_node)
+    H = W1.shape[0]
+    per_node = plan.max_block_rows * H * 4 * 2  # S (+ T) of the widest path
+    npc = max(1, min(65535, NODE_CHUNK_BYTES // per_node))
     for n0, n1, e0, e1 in graph.node_chunks(npc):
         if e1 == e0:
             continue
-        c, ne = n1 - n0, e1 - e0
-        idx, pos = graph.chunk_pad(n0, n1, e0, e1)
+        ne = e1 - e0
+        eoff = graph.rowptr[n0:n1 + 1] - e0
         with _timed("tp_node_prep"):
             pre = torch.addmm(b1, rad_s[e0:e1], W1.t())
-            a = torch.zeros((ne + 1, J), dtype=torch.float32, device=x.device)
-            a[:ne, :hidden] = torch.relu(pre)
-            a[:ne, hidden] = 1.0
-            Apad = ops.gather_rows(a, idx).view(c, dmax, J)
+            a = torch.relu(pre)
             zbuf = torch.empty(((ne + 1) * plan.desc.z_size,), dtype=torch.float32,
                                device=x.device)
-            for zoff, w in plan.z_regions:
-                zbuf[(zoff + w) * (ne + 1) - w:(zoff + w) * (ne + 1)].zero_()  # padding row
             check(lib.gmp_tp_edge_z_f32(ctypes.byref(plan.desc), _p(paths_dev), _p(cg_dev),
                                         cg_dev.numel(), _p(x), _p(sh), _p(graph.src_sorted),
                                         _p(graph.perm), e0, e1, _p(zbuf), _stream()),
                   "gmp_tp_edge_z_f32")
-        yield n0, n1, e0, e1, idx, pos, Apad, zbuf, pre
+        yield n0, n1, e0, e1, eoff, a, zbuf, pre
 
 
 class TensorProductConvLayer(nn.Module):
@@ -638,7 +638,8 @@ class TensorProductConvLayer(nn.Module):
 
     def forward(self, node_attr, edge_index, edge_sh, edge_feat):
         graph = tp_graph(edge_index, node_attr.shape[0])
-        fn = TPConvNodeFn if TP_MODE == "node" else TPConvFn
+        fn = TPConvNodeFn if (TP_MODE == "node" and node_form_ok(self.fc[0].out_features)) \
+            else TPConvFn
         out = fn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight, self.fc[0].bias,
                        self.fc[2].weight, self.fc[2].bias, self.plan, graph)
         if self.aggr == "mean":

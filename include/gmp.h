@@ -230,6 +230,18 @@ int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const fl
                           const int64_t* perm, int64_t e0, int64_t e1, const float* dzbuf,
                           float* dx_edge, float* dY_edge, void* stream);
 
+/* K7 receiver-factorised per-receiver kernels (tfn_layer.py:73-87 regrouped): for the
+ * receivers n of a chunk with chunk-local edge offsets eoff[n]..eoff[n+1] (receiver-sorted),
+ * Z (n_e, w) z rows of one path, A (n_e, H) radial hidden features (H % 16 == 0, <= 256):
+ *   outer: S[n, r, j] = sum_e Z[e, r] A[e, j] (n_recv, w, H), Sb[n, r] = sum_e Z[e, r]
+ *   apply: dZ[e, r] = sum_j T[n, r, j] A[e, j] + Tb[n, r];  dA[e, j] += sum_r Z[e, r] T[n, r, j]
+ * (T = G [W2_p]^T, Tb = G b2_p^T from the path GEMMs; dA is accumulated, dZ overwritten). */
+int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
+                          const float* Z, const float* A, float* S, float* Sb, void* stream);
+int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
+                          const float* Z, const float* A, const float* T, const float* Tb,
+                          float* dZ, float* dA, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps
