@@ -33,7 +33,9 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
   const int n = blockIdx.y, rb = blockIdx.x;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, i = lane & 15, kk = lane >> 4;
   const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
-  const int r = rb * kRowsPerBlock + wv * 16 + i;  // this lane's Z column (A operand row)
+  // D = S^T tile: D[j][r] = sum_e A[e, j] Z[e, r]  (A op = a columns, B op = Z columns), so a
+  // lane holds 4 consecutive j of one row r and stores them as one float4
+  const int r = rb * kRowsPerBlock + wv * 16 + i;  // this lane's output row (B operand column)
   const int TJ = H >> 4;
   f32x4 acc[kMaxH / 16];
 #pragma unroll
@@ -54,19 +56,14 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       const float zv = (e < deg && r < w) ? Z[(e0 + e) * w + r] : 0.f;
 #pragma unroll
       for (int t = 0; t < kMaxH / 16; ++t)
-        if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, sA[el * H + 16 * t + i], acc[t], 0, 0, 0);
+        if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * H + 16 * t + i], zv, acc[t], 0, 0, 0);
     }
   }
   float* Sn = S + (int64_t)n * w * H;
+  if (r < w) {
 #pragma unroll
-  for (int t = 0; t < kMaxH / 16; ++t) {
-    if (t < TJ) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = rb * kRowsPerBlock + wv * 16 + 4 * kk + q;
-        if (row < w) Sn[(int64_t)row * H + 16 * t + i] = acc[t][q];
-      }
-    }
+    for (int t = 0; t < kMaxH / 16; ++t)
+      if (t < TJ) *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
   }
   if (tid < kRowsPerBlock) {
     const int row = rb * kRowsPerBlock + tid;
@@ -133,11 +130,19 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
       __syncthreads();
       // dZ[e, r] = sum_j T[r, j] a[e, j]   (D[row][e]; A op = T rows, B op = a rows)
       if (16 * rt < nr && 16 * et < ng) {
-        f32x4 accZ = f32x4{0.f, 0.f, 0.f, 0.f};
+        // four independent accumulation chains over j (MFMA latency), summed in fixed order
+        f32x4 z4[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) z4[c] = f32x4{0.f, 0.f, 0.f, 0.f};
         const float* tr = sT + (16 * rt + i) * kLdT + kk;
         const float* ar = sA + (16 * et + i) * kLdT + kk;
-        for (int j0 = 0; j0 < H; j0 += 4)
-          accZ = __builtin_amdgcn_mfma_f32_16x16x4f32(tr[j0], ar[j0], accZ, 0, 0, 0);
+        for (int j0 = 0; j0 < H; j0 += 16) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            z4[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(tr[j0 + 4 * c], ar[j0 + 4 * c], z4[c],
+                                                         0, 0, 0);
+        }
+        const f32x4 accZ = (z4[0] + z4[1]) + (z4[2] + z4[3]);
         const int e = 16 * et + i;
         if (e < ng) {
 #pragma unroll
