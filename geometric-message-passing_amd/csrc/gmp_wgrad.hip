@@ -158,7 +158,9 @@ __global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t
 // column tiles {w, w+4, ..}; operands are read from LDS once per tile row / column (register
 // reuse across the wave's tiles).  Register-staged double buffering of kKT-edge tiles; same
 // split-K / ordered partial-sum scheme as above.
-constexpr int kRectLD = 4;   // LDS row padding (floats)
+// LDS row stride = 16 mod 64 floats: the 4 edge rows (kk) of an MFMA operand read fall on
+// disjoint 16-bank groups (conflict-free for all 64 lanes)
+__host__ __device__ __forceinline__ int rect_ld(int x) { return x + ((16 - x) % 64 + 64) % 64; }
 constexpr int kMaxL = 9;     // float4 loads per thread per tile (kKT * (M + N) / 4 / kT)
 
 template <int MR, int MC>
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(kT, 1) void outer_sum_rect_kernel(
     const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
     int64_t k_per_block, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int LDA = M + kRectLD, LDB = N + kRectLD;
+  const int LDA = rect_ld(M), LDB = rect_ld(N);
   const int TILE = kKT * (LDA + LDB);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, kk = lane >> 4;
@@ -352,7 +354,7 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-  const size_t smem = (size_t)2 * kKT * (m + kRectLD + n + kRectLD) * sizeof(float);
+  const size_t smem = (size_t)2 * kKT * (rect_ld((int)m) + rect_ld((int)n)) * sizeof(float);
   int rc;
 #define GMP_RECT(MR, MC)                                                                      \
   {                                                                                           \
