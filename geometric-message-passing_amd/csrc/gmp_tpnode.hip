@@ -29,8 +29,9 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
                                                             const float* __restrict__ A,
                                                             float* __restrict__ S,
                                                             float* __restrict__ Sb) {
-  __shared__ __attribute__((aligned(16))) float sA[kEdgeStage * kMaxH];
+  __shared__ __attribute__((aligned(16))) float sA[kEdgeStage * (kMaxH + 16)];
   const int n = blockIdx.y, rb = blockIdx.x;
+  const int LDA = H + 16;  // 16 mod 64 floats: the 4 edge rows of an MFMA read hit disjoint banks
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, i = lane & 15, kk = lane >> 4;
   const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
   // D = S^T tile: D[j][r] = sum_e A[e, j] Z[e, r]  (A op = a columns, B op = Z columns), so a
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       const int e = x / (H >> 2), q = x - e * (H >> 2);
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (eb + e < deg) v = *reinterpret_cast<const f32x4*>(A + (e0 + eb + e) * H + 4 * q);
-      *reinterpret_cast<f32x4*>(&sA[e * H + 4 * q]) = v;
+      *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
     }
     __syncthreads();
 #pragma unroll
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       const float zv = (e < deg && r < w) ? Z[(e0 + e) * w + r] : 0.f;
 #pragma unroll
       for (int t = 0; t < kMaxH / 16; ++t)
-        if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * H + 16 * t + i], zv, acc[t], 0, 0, 0);
+        if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zv, acc[t], 0, 0, 0);
     }
   }
   float* Sn = S + (int64_t)n * w * H;
@@ -96,6 +97,7 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
   __shared__ __attribute__((aligned(16))) float sT[kAR * kLdT];
   __shared__ __attribute__((aligned(16))) float sA[kAE * kLdT];
   __shared__ __attribute__((aligned(16))) float sZ[kAE * kLdZ];
+  __shared__ __attribute__((aligned(16))) float sDZ[kAE * kLdZ];  // dZ tile, written row-wise
   const int n = blockIdx.x;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, i = lane & 15, kk = lane >> 4;
   const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
@@ -143,15 +145,7 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
                                                          0, 0, 0);
         }
         const f32x4 accZ = (z4[0] + z4[1]) + (z4[2] + z4[3]);
-        const int e = 16 * et + i;
-        if (e < ng) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int rr = 16 * rt + 4 * kk + q;
-            if (rr < nr)
-              dZ[(e0 + g0 + e) * w + r0 + rr] = accZ[q] + Tb[(int64_t)n * w + r0 + rr];
-          }
-        }
+        *reinterpret_cast<f32x4*>(&sDZ[(16 * et + i) * kLdZ + 16 * rt + 4 * kk]) = accZ;
       }
       // dA[e, j] += sum_r Z[e, r] T[r, j]   (D[e][j]; A op = Z rows, B op = T columns)
 #pragma unroll
@@ -167,6 +161,12 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
             accA[a][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(z1, tv, accA[a][1], 0, 0, 0);
           }
         }
+      }
+      __syncthreads();  // sDZ complete: coalesced row-wise store (+ Tb)
+      for (int x = tid; x < kAE * kAR; x += kNT) {
+        const int e = x / kAR, rr = x - e * kAR;
+        if (e < ng && rr < nr)
+          dZ[(e0 + g0 + e) * w + r0 + rr] = sDZ[e * kLdZ + rr] + Tb[(int64_t)n * w + r0 + rr];
       }
     }
     // accumulate into dA (per-path launches on one stream: ordered RMW, deterministic)
