@@ -1,0 +1,677 @@
+// K5g: GVP-GNN message function (models/layers/gvp_layer.py:101-170 GVP applied per edge by
+// GVPConv.message :319-324, with the reference configuration activations = (relu, None),
+// vector_gate = True, s = 128 scalar / v = 16 vector channels, edge (32, 1)).
+//
+// Two fused kernels (forward and backward each), one wave per 16-edge chunk, lane l holding
+// edge i = l & 15 and feature group g = l >> 4 (features 16p + 4g + q: the register order the
+// v_mfma_f32_16x16x4_f32 B operand and C/D accumulator share, as in the EGNN kernels), so each
+// GVP's Linears, norms and gates run in registers; the xyz components of a vector channel sit in
+// the same lane (norms need no cross-lane traffic):
+//   * gvp_msg0: the first message GVP on [s_j, e_s, s_i] / [v_j, e_v, v_i].  Its scalar Linear is
+//     split into node projections P = [s W_a^T | s W_b^T] (gathered at j and i) plus the edge
+//     terms W_e e_s and W_n |vh|; its vector Linear W_h into node projections Q = [v W_ha^T |
+//     v W_hb^T] (33 channels padded to 48) plus the rank-1 e_v term;
+//   * gvp_layer: a GVP (128, 16) -> (128, 16) on per-edge rows (message GVPs 2 and 3).
+// Backward kernels recompute the forward in registers and write the input gradients plus the
+// per-edge factors of every weight gradient (reduced by the deterministic edge outer sum).
+#include "gmp_common.h"
+
+namespace gmp {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGT = 512;   // threads per workgroup (8 waves, 1 workgroup per CU: LDS-bound)
+constexpr int S = 128;     // scalar channels
+constexpr int V = 16;      // vector channels
+constexpr int SE = 32;     // edge scalar channels
+constexpr int H0 = 48;     // first GVP hidden vector channels (33 padded)
+
+// LDS row strides (floats): +4 keeps the 16 rows of an A-operand read on distinct banks
+constexpr int LDS_S = S + V + 4;   // Ws of a GVP layer: (128 x 144)
+constexpr int LD128 = S + 4;
+constexpr int LD16 = V + 4;
+constexpr int LD32 = SE + 4;
+constexpr int LD48 = H0 + 4;
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// y[tile t] += sum_k W[16t + i][k] x[k]  over K = 16 * TI features (x in slot layout)
+template <int TO, int TI>
+__device__ __forceinline__ void gemm_wx(const float* __restrict__ sW, int ldw, const f32x4 (&x)[TI],
+                                        f32x4 (&y)[TO], int i, int g) {
+#pragma unroll
+  for (int p = 0; p < TI; ++p) {
+    f32x4 a[TO];
+#pragma unroll
+    for (int t = 0; t < TO; ++t) a[t] = *reinterpret_cast<const f32x4*>(sW + (16 * t + i) * ldw + 16 * p + 4 * g);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < TO; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][c], x[p][c], y[t], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// y[tile t] += sum_o W[o][16t + i] gin[o]   (W is (16 * TIN) x ldw, output 16 * TO features)
+template <int TO, int TIN>
+__device__ __forceinline__ void gemm_wtx(const float* __restrict__ sW, int ldw,
+                                         const f32x4 (&gin)[TIN], f32x4 (&y)[TO], int i, int g) {
+#pragma unroll
+  for (int p = 0; p < TIN; ++p) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float* wrow = sW + (16 * p + 4 * g + c) * ldw + i;
+      float a[TO];
+#pragma unroll
+      for (int t = 0; t < TO; ++t) a[t] = wrow[16 * t];
+#pragma unroll
+      for (int t = 0; t < TO; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], gin[p][c], y[t], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void zero(f32x4 (&x)[T]) {
+#pragma unroll
+  for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// scalar row (D features) of a row-major tensor: this lane's slots
+template <int T>
+__device__ __forceinline__ void ld_row(f32x4 (&x)[T], const float* __restrict__ row, int g) {
+#pragma unroll
+  for (int p = 0; p < T; ++p) x[p] = *reinterpret_cast<const f32x4*>(row + 16 * p + 4 * g);
+}
+template <int T>
+__device__ __forceinline__ void st_row(float* __restrict__ row, const f32x4 (&x)[T], int g) {
+#pragma unroll
+  for (int p = 0; p < T; ++p) *reinterpret_cast<f32x4*>(row + 16 * p + 4 * g) = x[p];
+}
+template <int T>
+__device__ __forceinline__ void add_row(f32x4 (&x)[T], const float* __restrict__ row, int g) {
+#pragma unroll
+  for (int p = 0; p < T; ++p) x[p] += *reinterpret_cast<const f32x4*>(row + 16 * p + 4 * g);
+}
+// LDS vector slots
+template <int T>
+__device__ __forceinline__ void ld_vec(f32x4 (&x)[T], const float* v, int g) {
+#pragma unroll
+  for (int p = 0; p < T; ++p) x[p] = *reinterpret_cast<const f32x4*>(v + 16 * p + 4 * g);
+}
+
+// vector row in the reference's (channel, xyz) layout, C = 16 * T channels:
+// v[x][p][q] = row[(16p + 4g + q) * 3 + x]
+template <int T>
+__device__ __forceinline__ void ld_vrow(f32x4 (&v)[3][T], const float* __restrict__ row, int g) {
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+    const f32x4* r4 = reinterpret_cast<const f32x4*>(row + (16 * p + 4 * g) * 3);
+    const f32x4 a = r4[0], b = r4[1], c = r4[2];  // 12 floats: (q, x) q-major
+    v[0][p] = f32x4{a[0], a[3], b[2], c[1]};
+    v[1][p] = f32x4{a[1], b[0], b[3], c[2]};
+    v[2][p] = f32x4{a[2], b[1], c[0], c[3]};
+  }
+}
+template <int T>
+__device__ __forceinline__ void st_vrow(float* __restrict__ row, const f32x4 (&v)[3][T], int g) {
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+    f32x4* r4 = reinterpret_cast<f32x4*>(row + (16 * p + 4 * g) * 3);
+    r4[0] = f32x4{v[0][p][0], v[1][p][0], v[2][p][0], v[0][p][1]};
+    r4[1] = f32x4{v[1][p][1], v[2][p][1], v[0][p][2], v[1][p][2]};
+    r4[2] = f32x4{v[2][p][2], v[0][p][3], v[1][p][3], v[2][p][3]};
+  }
+}
+
+// norm over xyz with the reference's clamp (gvp_layer.py:66-73): sqrt(max(sum x^2, 1e-8))
+template <int T>
+__device__ __forceinline__ void vnorm(const f32x4 (&vh)[3][T], f32x4 (&vn)[T], f32x4 (&sq)[T]) {
+#pragma unroll
+  for (int p = 0; p < T; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float s2 = vh[0][p][q] * vh[0][p][q] + vh[1][p][q] * vh[1][p][q] + vh[2][p][q] * vh[2][p][q];
+      sq[p][q] = s2;
+      vn[p][q] = sqrtf(fmaxf(s2, 1e-8f));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Generic GVP (128, 16) -> (128, 16): LDS = Ws (128 x 144) | Wsv (16 x 128) | Wh | Wv | bs | bsv
+struct LayerW {
+  const float *Ws, *bs, *Wsv, *bsv, *Wh, *Wv;
+};
+constexpr int kLayerSmem = S * LDS_S + V * LD128 + 2 * V * LD16 + S + V;
+
+__device__ void layer_to_lds(float* sm, const LayerW& P) {
+  float* sWs = sm;
+  float* sWsv = sWs + S * LDS_S;
+  float* sWh = sWsv + V * LD128;
+  float* sWv = sWh + V * LD16;
+  float* sbs = sWv + V * LD16;
+  float* sbsv = sbs + S;
+  for (int x = threadIdx.x; x < S * (S + V); x += blockDim.x) sWs[(x / (S + V)) * LDS_S + x % (S + V)] = P.Ws[x];
+  for (int x = threadIdx.x; x < V * S; x += blockDim.x) sWsv[(x / S) * LD128 + x % S] = P.Wsv[x];
+  for (int x = threadIdx.x; x < V * V; x += blockDim.x) {
+    sWh[(x / V) * LD16 + x % V] = P.Wh[x];
+    sWv[(x / V) * LD16 + x % V] = P.Wv[x];
+  }
+  for (int x = threadIdx.x; x < S; x += blockDim.x) sbs[x] = P.bs[x];
+  for (int x = threadIdx.x; x < V; x += blockDim.x) sbsv[x] = P.bsv[x];
+}
+
+struct LayerFwd {
+  f32x4 vh[3][1], vn[1], sq[1], spre[S / 16], vpre[3][1], sg[1];
+};
+
+// forward of one GVP layer for this lane's edge; s is consumed
+__device__ __forceinline__ void layer_forward(const float* sm, f32x4 (&s)[S / 16], const f32x4 (&v)[3][1],
+                                              LayerFwd& F, int i, int g) {
+  const float* sWs = sm;
+  const float* sWsv = sWs + S * LDS_S;
+  const float* sWh = sWsv + V * LD128;
+  const float* sWv = sWh + V * LD16;
+  const float* sbs = sWv + V * LD16;
+  const float* sbsv = sbs + S;
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    zero(F.vh[x]);
+    gemm_wx<1, 1>(sWh, LD16, v[x], F.vh[x], i, g);
+  }
+  vnorm<1>(F.vh, F.vn, F.sq);
+  ld_vec<S / 16>(F.spre, sbs, g);
+  gemm_wx<S / 16, S / 16>(sWs, LDS_S, s, F.spre, i, g);
+  gemm_wx<S / 16, 1>(sWs + S, LDS_S, F.vn, F.spre, i, g);
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    zero(F.vpre[x]);
+    gemm_wx<1, 1>(sWv, LD16, F.vh[x], F.vpre[x], i, g);
+  }
+  f32x4 gate[1];
+  ld_vec<1>(gate, sbsv, g);
+  gemm_wx<1, S / 16>(sWsv, LD128, F.spre, gate, i, g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) F.sg[0][q] = sigm(gate[0][q]);
+}
+
+struct Chunk {
+  int64_t e;
+  bool valid;
+};
+__device__ __forceinline__ Chunk chunk_edge(int64_t c, int i, int64_t E) {
+  Chunk k;
+  k.e = 16 * c + i;
+  k.valid = k.e < E;
+  if (!k.valid) k.e = E - 1;  // clamp loads; stores are masked
+  return k;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kGT) void gvp_layer_fwd_kernel(int64_t E, const float* __restrict__ s_in,
+                                                            const float* __restrict__ v_in, LayerW P,
+                                                            float* __restrict__ s_out,
+                                                            float* __restrict__ v_out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  layer_to_lds(sm, P);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nchunks = (E + 15) / 16;
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const Chunk k = chunk_edge(c, i, E);
+    f32x4 s[S / 16], v[3][1];
+    ld_row<S / 16>(s, s_in + k.e * S, g);
+    ld_vrow<1>(v, v_in + k.e * (3 * V), g);
+    LayerFwd F;
+    layer_forward(sm, s, v, F, i, g);
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F.vpre[x][0][q] *= F.sg[0][q];
+    if (ACT) {
+#pragma unroll
+      for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F.spre[p][q] = fmaxf(F.spre[p][q], 0.f);
+    }
+    if (k.valid) {
+      st_row<S / 16>(s_out + k.e * S, F.spre, g);
+      st_vrow<1>(v_out + k.e * (3 * V), F.vpre, g);
+    }
+  }
+}
+
+// Backward: inputs s_in, v_in, ds_out, dv_out.  Outputs ds_in, dv_in and the weight-gradient
+// factors dspre (E,128), spre (E,128), dgate (E,16), vn (E,16), vh (E,48), dvpre (E,48),
+// dvh (E,48) (vector tensors in (channel, xyz) layout).
+struct LayerGrads {
+  float *ds_in, *dv_in, *dspre, *spre, *dgate, *vn, *vh, *dvpre, *dvh;
+};
+
+template <int ACT>
+__global__ __launch_bounds__(kGT) void gvp_layer_bwd_kernel(int64_t E, const float* __restrict__ s_in,
+                                                            const float* __restrict__ v_in, LayerW P,
+                                                            const float* __restrict__ ds_out,
+                                                            const float* __restrict__ dv_out,
+                                                            LayerGrads O) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  layer_to_lds(sm, P);
+  __syncthreads();
+  const float* sWs = sm;
+  const float* sWsv = sWs + S * LDS_S;
+  const float* sWh = sWsv + V * LD128;
+  const float* sWv = sWh + V * LD16;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nchunks = (E + 15) / 16;
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const Chunk k = chunk_edge(c, i, E);
+    f32x4 s[S / 16], v[3][1];
+    ld_row<S / 16>(s, s_in + k.e * S, g);
+    ld_vrow<1>(v, v_in + k.e * (3 * V), g);
+    LayerFwd F;
+    layer_forward(sm, s, v, F, i, g);
+    // ds (reuse s registers): dspre = ds_out * act'(spre)
+    ld_row<S / 16>(s, ds_out + k.e * S, g);
+    if (ACT) {
+#pragma unroll
+      for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[p][q] = F.spre[p][q] > 0.f ? s[p][q] : 0.f;
+    }
+    // gate: vout = vpre * sg
+    f32x4 dv[3][1];
+    ld_vrow<1>(dv, dv_out + k.e * (3 * V), g);
+    f32x4 dgate[1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float dsg = dv[0][0][q] * F.vpre[0][0][q] + dv[1][0][q] * F.vpre[1][0][q] + dv[2][0][q] * F.vpre[2][0][q];
+      dgate[0][q] = dsg * F.sg[0][q] * (1.f - F.sg[0][q]);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) dv[x][0][q] *= F.sg[0][q];  // dvpre
+    }
+    gemm_wtx<S / 16, 1>(sWsv, LD128, dgate, s, i, g);  // dspre += Wsv^T dgate
+    if (k.valid) {
+      st_row<S / 16>(O.dspre + k.e * S, s, g);
+      st_row<S / 16>(O.spre + k.e * S, F.spre, g);
+      st_row<1>(O.dgate + k.e * V, dgate, g);
+      st_row<1>(O.vn + k.e * V, F.vn, g);
+      st_vrow<1>(O.vh + k.e * (3 * V), F.vh, g);
+      st_vrow<1>(O.dvpre + k.e * (3 * V), dv, g);
+    }
+    // ds_in = Ws_s^T dspre ; dvn = Ws_v^T dspre
+    f32x4 dsin[S / 16], dvn[1];
+    zero(dsin);
+    zero(dvn);
+    gemm_wtx<S / 16, S / 16>(sWs, LDS_S, s, dsin, i, g);
+    gemm_wtx<1, S / 16>(sWs + S, LDS_S, s, dvn, i, g);
+    if (k.valid) st_row<S / 16>(O.ds_in + k.e * S, dsin, g);
+    // dvh = Wv^T dvpre + dvn * vh / vn (where sum vh^2 > eps)
+    f32x4 dvh[3][1];
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      zero(dvh[x]);
+      gemm_wtx<1, 1>(sWv, LD16, dv[x], dvh[x], i, g);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float f = F.sq[0][q] > 1e-8f ? dvn[0][q] / F.vn[0][q] : 0.f;
+#pragma unroll
+      for (int x = 0; x < 3; ++x) dvh[x][0][q] += f * F.vh[x][0][q];
+    }
+    if (k.valid) st_vrow<1>(O.dvh + k.e * (3 * V), dvh, g);
+    // dv_in = Wh^T dvh
+    f32x4 dvin[3][1];
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      zero(dvin[x]);
+      gemm_wtx<1, 1>(sWh, LD16, dvh[x], dvin[x], i, g);
+    }
+    if (k.valid) st_vrow<1>(O.dv_in + k.e * (3 * V), dvin, g);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// First message GVP: LDS = We (128 x 32) | Wn (128 x 48) | Wv0 (16 x 48) | Wsv0 (16 x 128) |
+// b0 (128) | bsv0 (16) | wev (48)
+struct Msg0W {
+  const float *We, *Wn, *b, *Wv, *Wsv, *bsv, *wev;  // Wn, Wv, wev zero-padded to 48 channels
+};
+constexpr int kMsg0Smem = S * LD32 + S * LD48 + V * LD48 + V * LD128 + S + V + H0;
+
+__device__ void msg0_to_lds(float* sm, const Msg0W& P) {
+  float* sWe = sm;
+  float* sWn = sWe + S * LD32;
+  float* sWv = sWn + S * LD48;
+  float* sWsv = sWv + V * LD48;
+  float* sb = sWsv + V * LD128;
+  float* sbsv = sb + S;
+  float* swev = sbsv + V;
+  for (int x = threadIdx.x; x < S * SE; x += blockDim.x) sWe[(x / SE) * LD32 + x % SE] = P.We[x];
+  for (int x = threadIdx.x; x < S * H0; x += blockDim.x) sWn[(x / H0) * LD48 + x % H0] = P.Wn[x];
+  for (int x = threadIdx.x; x < V * H0; x += blockDim.x) sWv[(x / H0) * LD48 + x % H0] = P.Wv[x];
+  for (int x = threadIdx.x; x < V * S; x += blockDim.x) sWsv[(x / S) * LD128 + x % S] = P.Wsv[x];
+  for (int x = threadIdx.x; x < S; x += blockDim.x) sb[x] = P.b[x];
+  for (int x = threadIdx.x; x < V; x += blockDim.x) sbsv[x] = P.bsv[x];
+  for (int x = threadIdx.x; x < H0; x += blockDim.x) swev[x] = P.wev[x];
+}
+
+struct Msg0Fwd {
+  f32x4 vh[3][3], vn[3], sq[3], spre[S / 16], vpre[3][1], sg[1];
+};
+
+// P row: [Pa (128) | Pb (128)]; Q row: [Qa (48 x 3) | Qb (48 x 3)] in (channel, xyz) layout
+__device__ __forceinline__ void msg0_forward(const float* sm, const float* __restrict__ Prow_j,
+                                             const float* __restrict__ Prow_i,
+                                             const float* __restrict__ Qrow_j,
+                                             const float* __restrict__ Qrow_i,
+                                             const float* __restrict__ es_row,
+                                             const float* __restrict__ ev_row, Msg0Fwd& F, int i,
+                                             int g) {
+  const float* sWe = sm;
+  const float* sWn = sWe + S * LD32;
+  const float* sWv = sWn + S * LD48;
+  const float* sWsv = sWv + V * LD48;
+  const float* sb = sWsv + V * LD128;
+  const float* sbsv = sb + S;
+  const float* swev = sbsv + V;
+  // vh = Qa[j] + Qb[i] + wev (x) ev
+  ld_vrow<3>(F.vh, Qrow_j, g);
+  f32x4 t[3][3];
+  ld_vrow<3>(t, Qrow_i + 3 * H0, g);
+  const float ev0 = ev_row[0], ev1 = ev_row[1], ev2 = ev_row[2];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const f32x4 w = *reinterpret_cast<const f32x4*>(swev + 16 * p + 4 * g);
+    F.vh[0][p] += t[0][p] + w * ev0;
+    F.vh[1][p] += t[1][p] + w * ev1;
+    F.vh[2][p] += t[2][p] + w * ev2;
+  }
+  vnorm<3>(F.vh, F.vn, F.sq);
+  // spre = b + Pa[j] + Pb[i] + We es + Wn vn
+  ld_vec<S / 16>(F.spre, sb, g);
+  add_row<S / 16>(F.spre, Prow_j, g);
+  add_row<S / 16>(F.spre, Prow_i + S, g);
+  f32x4 es[2];
+  ld_row<2>(es, es_row, g);
+  gemm_wx<S / 16, 2>(sWe, LD32, es, F.spre, i, g);
+  gemm_wx<S / 16, 3>(sWn, LD48, F.vn, F.spre, i, g);
+  // vpre = Wv vh ; gate = bsv + Wsv spre
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    zero(F.vpre[x]);
+    gemm_wx<1, 3>(sWv, LD48, F.vh[x], F.vpre[x], i, g);
+  }
+  f32x4 gate[1];
+  ld_vec<1>(gate, sbsv, g);
+  gemm_wx<1, S / 16>(sWsv, LD128, F.spre, gate, i, g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) F.sg[0][q] = sigm(gate[0][q]);
+}
+
+__global__ __launch_bounds__(kGT) void gvp_msg0_fwd_kernel(int64_t E, const int64_t* __restrict__ send,
+                                                           const int64_t* __restrict__ recv,
+                                                           const float* __restrict__ Pn,
+                                                           const float* __restrict__ Qn,
+                                                           const float* __restrict__ es,
+                                                           const float* __restrict__ ev, Msg0W W,
+                                                           float* __restrict__ s_out,
+                                                           float* __restrict__ v_out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  msg0_to_lds(sm, W);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nchunks = (E + 15) / 16;
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const Chunk k = chunk_edge(c, i, E);
+    const int64_t j = send[k.e], r = recv[k.e];
+    Msg0Fwd F;
+    msg0_forward(sm, Pn + j * 2 * S, Pn + r * 2 * S, Qn + j * 6 * H0, Qn + r * 6 * H0,
+                 es + k.e * SE, ev + k.e * 3, F, i, g);
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F.vpre[x][0][q] *= F.sg[0][q];
+#pragma unroll
+    for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F.spre[p][q] = fmaxf(F.spre[p][q], 0.f);
+    if (k.valid) {
+      st_row<S / 16>(s_out + k.e * S, F.spre, g);
+      st_vrow<1>(v_out + k.e * (3 * V), F.vpre, g);
+    }
+  }
+}
+
+// Backward of the first GVP.  Outputs: dspre (E,128) [= dPa rows at j, dPb rows at i, and the
+// dW_e / dW_n / db factor], spre (E,128), dgate (E,16), vn (E,48), vh (E,144), dvpre (E,48),
+// dvh (E,144) [= dQa rows at j, dQb rows at i], des (E,32), dev (E,3).
+struct Msg0Grads {
+  float *dspre, *spre, *dgate, *vn, *vh, *dvpre, *dvh, *des, *dev;
+};
+
+__global__ __launch_bounds__(kGT) void gvp_msg0_bwd_kernel(int64_t E, const int64_t* __restrict__ send,
+                                                           const int64_t* __restrict__ recv,
+                                                           const float* __restrict__ Pn,
+                                                           const float* __restrict__ Qn,
+                                                           const float* __restrict__ es,
+                                                           const float* __restrict__ ev, Msg0W W,
+                                                           const float* __restrict__ ds_out,
+                                                           const float* __restrict__ dv_out,
+                                                           Msg0Grads O) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  msg0_to_lds(sm, W);
+  __syncthreads();
+  const float* sWe = sm;
+  const float* sWn = sWe + S * LD32;
+  const float* sWv = sWn + S * LD48;
+  const float* sWsv = sWv + V * LD48;
+  const float* swev = sWsv + V * LD128 + S + V;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nchunks = (E + 15) / 16;
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const Chunk k = chunk_edge(c, i, E);
+    const int64_t j = send[k.e], r = recv[k.e];
+    Msg0Fwd F;
+    msg0_forward(sm, Pn + j * 2 * S, Pn + r * 2 * S, Qn + j * 6 * H0, Qn + r * 6 * H0,
+                 es + k.e * SE, ev + k.e * 3, F, i, g);
+    f32x4 ds[S / 16];
+    ld_row<S / 16>(ds, ds_out + k.e * S, g);
+#pragma unroll
+    for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ds[p][q] = F.spre[p][q] > 0.f ? ds[p][q] : 0.f;
+    f32x4 dv[3][1];
+    ld_vrow<1>(dv, dv_out + k.e * (3 * V), g);
+    f32x4 dgate[1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float dsg = dv[0][0][q] * F.vpre[0][0][q] + dv[1][0][q] * F.vpre[1][0][q] + dv[2][0][q] * F.vpre[2][0][q];
+      dgate[0][q] = dsg * F.sg[0][q] * (1.f - F.sg[0][q]);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) dv[x][0][q] *= F.sg[0][q];
+    }
+    gemm_wtx<S / 16, 1>(sWsv, LD128, dgate, ds, i, g);  // dspre total
+    if (k.valid) {
+      st_row<S / 16>(O.dspre + k.e * S, ds, g);
+      st_row<S / 16>(O.spre + k.e * S, F.spre, g);
+      st_row<1>(O.dgate + k.e * V, dgate, g);
+      st_row<3>(O.vn + k.e * H0, F.vn, g);
+      st_vrow<3>(O.vh + k.e * (3 * H0), F.vh, g);
+      st_vrow<1>(O.dvpre + k.e * (3 * V), dv, g);
+    }
+    // des = We^T dspre ; dvn = Wn^T dspre
+    f32x4 des[2], dvn[3];
+    zero(des);
+    zero(dvn);
+    gemm_wtx<2, S / 16>(sWe, LD32, ds, des, i, g);
+    gemm_wtx<3, S / 16>(sWn, LD48, ds, dvn, i, g);
+    if (k.valid) st_row<2>(O.des + k.e * SE, des, g);
+    // dvh = Wv^T dvpre + dvn * vh / vn
+    f32x4 dvh[3][3];
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      zero(dvh[x]);
+      gemm_wtx<3, 1>(sWv, LD48, dv[x], dvh[x], i, g);
+    }
+    float dev0 = 0.f, dev1 = 0.f, dev2 = 0.f;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(swev + 16 * p + 4 * g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float f = F.sq[p][q] > 1e-8f ? dvn[p][q] / F.vn[p][q] : 0.f;
+        dvh[0][p][q] += f * F.vh[0][p][q];
+        dvh[1][p][q] += f * F.vh[1][p][q];
+        dvh[2][p][q] += f * F.vh[2][p][q];
+        dev0 += w[q] * dvh[0][p][q];
+        dev1 += w[q] * dvh[1][p][q];
+        dev2 += w[q] * dvh[2][p][q];
+      }
+    }
+    // dev = sum over the 48 channels: reduce the 4 lane groups of this edge (fixed order)
+    dev0 += __shfl_xor(dev0, 16);
+    dev0 += __shfl_xor(dev0, 32);
+    dev1 += __shfl_xor(dev1, 16);
+    dev1 += __shfl_xor(dev1, 32);
+    dev2 += __shfl_xor(dev2, 16);
+    dev2 += __shfl_xor(dev2, 32);
+    if (k.valid) {
+      st_vrow<3>(O.dvh + k.e * (3 * H0), dvh, g);
+      if (g == 0) {
+        O.dev[k.e * 3 + 0] = dev0;
+        O.dev[k.e * 3 + 1] = dev1;
+        O.dev[k.e * 3 + 2] = dev2;
+      }
+    }
+  }
+}
+
+int64_t grid_for(int64_t E) {
+  const int64_t chunks = ceil_div(E, (int64_t)16);
+  int64_t b = ceil_div(chunks, (int64_t)(kGT / 64));
+  const int64_t cap = (int64_t)device_cu_count();
+  if (b > cap) b = cap;
+  return b < 1 ? 1 : b;
+}
+
+template <class K>
+int set_smem(K k, size_t bytes) {
+  return hip_check(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)bytes));
+}
+
+bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+}  // namespace
+}  // namespace gmp
+
+using namespace gmp;
+
+extern "C" {
+
+int gmp_gvp_layer_fwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
+                          const float* Ws, const float* bs, const float* Wsv, const float* bsv,
+                          const float* Wh, const float* Wv, float* s_out, float* v_out,
+                          void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(s_in && v_in && Ws && bs && Wsv && bsv && Wh && Wv && s_out && v_out);
+  GMP_CHECK_ARG(al16(s_in) && al16(v_in) && al16(s_out) && al16(v_out));
+  const LayerW P{Ws, bs, Wsv, bsv, Wh, Wv};
+  const size_t smem = kLayerSmem * sizeof(float);
+  const unsigned G = (unsigned)grid_for(n_edges);
+  hipStream_t s = as_stream(stream);
+  int rc;
+  if (relu) {
+    if ((rc = set_smem(gvp_layer_fwd_kernel<1>, smem))) return rc;
+    gvp_layer_fwd_kernel<1><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
+  } else {
+    if ((rc = set_smem(gvp_layer_fwd_kernel<0>, smem))) return rc;
+    gvp_layer_fwd_kernel<0><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
+  }
+  return launch_status();
+}
+
+int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
+                          const float* Ws, const float* bs, const float* Wsv, const float* bsv,
+                          const float* Wh, const float* Wv, const float* ds_out,
+                          const float* dv_out, float* ds_in, float* dv_in, float* dspre,
+                          float* spre, float* dgate, float* vn, float* vh, float* dvpre,
+                          float* dvh, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(s_in && v_in && Ws && bs && Wsv && bsv && Wh && Wv && ds_out && dv_out);
+  GMP_CHECK_ARG(ds_in && dv_in && dspre && spre && dgate && vn && vh && dvpre && dvh);
+  GMP_CHECK_ARG(al16(s_in) && al16(v_in) && al16(ds_out) && al16(dv_out) && al16(ds_in) &&
+                al16(dv_in) && al16(dspre) && al16(spre) && al16(dgate) && al16(vn) &&
+                al16(vh) && al16(dvpre) && al16(dvh));
+  const LayerW P{Ws, bs, Wsv, bsv, Wh, Wv};
+  const LayerGrads O{ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
+  const size_t smem = kLayerSmem * sizeof(float);
+  const unsigned G = (unsigned)grid_for(n_edges);
+  hipStream_t s = as_stream(stream);
+  int rc;
+  if (relu) {
+    if ((rc = set_smem(gvp_layer_bwd_kernel<1>, smem))) return rc;
+    gvp_layer_bwd_kernel<1><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
+  } else {
+    if ((rc = set_smem(gvp_layer_bwd_kernel<0>, smem))) return rc;
+    gvp_layer_bwd_kernel<0><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
+  }
+  return launch_status();
+}
+
+int gmp_gvp_msg0_fwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
+                         const float* P, const float* Q, const float* es, const float* ev,
+                         const float* We, const float* Wn, const float* b, const float* Wv,
+                         const float* Wsv, const float* bsv, const float* wev, float* s_out,
+                         float* v_out, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(send && recv && P && Q && es && ev && We && Wn && b && Wv && Wsv && bsv && wev &&
+                s_out && v_out);
+  GMP_CHECK_ARG(al16(P) && al16(Q) && al16(es) && al16(s_out) && al16(v_out));
+  const Msg0W W{We, Wn, b, Wv, Wsv, bsv, wev};
+  const size_t smem = kMsg0Smem * sizeof(float);
+  int rc;
+  if ((rc = set_smem(gvp_msg0_fwd_kernel, smem))) return rc;
+  gvp_msg0_fwd_kernel<<<(unsigned)grid_for(n_edges), kGT, smem, as_stream(stream)>>>(
+      n_edges, send, recv, P, Q, es, ev, W, s_out, v_out);
+  return launch_status();
+}
+
+int gmp_gvp_msg0_bwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
+                         const float* P, const float* Q, const float* es, const float* ev,
+                         const float* We, const float* Wn, const float* b, const float* Wv,
+                         const float* Wsv, const float* bsv, const float* wev,
+                         const float* ds_out, const float* dv_out, float* dspre, float* spre,
+                         float* dgate, float* vn, float* vh, float* dvpre, float* dvh,
+                         float* des, float* dev, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(send && recv && P && Q && es && ev && We && Wn && b && Wv && Wsv && bsv && wev &&
+                ds_out && dv_out);
+  GMP_CHECK_ARG(dspre && spre && dgate && vn && vh && dvpre && dvh && des && dev);
+  GMP_CHECK_ARG(al16(P) && al16(Q) && al16(es) && al16(ds_out) && al16(dv_out) && al16(dspre) &&
+                al16(spre) && al16(dgate) && al16(vn) && al16(vh) && al16(dvpre) && al16(dvh) &&
+                al16(des));
+  const Msg0W W{We, Wn, b, Wv, Wsv, bsv, wev};
+  const Msg0Grads O{dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev};
+  const size_t smem = kMsg0Smem * sizeof(float);
+  int rc;
+  if ((rc = set_smem(gvp_msg0_bwd_kernel, smem))) return rc;
+  gvp_msg0_bwd_kernel<<<(unsigned)grid_for(n_edges), kGT, smem, as_stream(stream)>>>(
+      n_edges, send, recv, P, Q, es, ev, W, ds_out, dv_out, O);
+  return launch_status();
+}
+
+}  // extern "C"

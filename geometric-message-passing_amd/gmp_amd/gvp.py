@@ -12,12 +12,14 @@ CSR (deterministic).  Subclasses with a custom message function or module_list f
 generic propagate path (gather -> message -> segmented reduce).
 """
 import functools
+import os
 
 import torch
 from torch import nn
 from torch.nn import functional as F
 
-from . import ops
+from . import _lib, ops
+from ._lib import check
 from .message_passing import MessagePassing
 from .scatter import global_add_pool, global_mean_pool
 
@@ -145,6 +147,127 @@ class LayerNorm(nn.Module):
         return self.scalar_norm(s), v / vn
 
 
+# ------------------------------------------------------------------------------------ K5g
+GVP_FUSED = os.environ.get("GMP_GVP_FUSED", "1") != "0"
+
+
+def _diag3(M, a, b):
+    """sum_x M[3o + x, 3c + x] for M (3a, 3b) -> (a, b): weight gradient of a per-xyz Linear
+    from the outer sum of (channel, xyz)-flattened rows."""
+    return M.reshape(a, 3, b, 3).diagonal(dim1=1, dim2=3).sum(-1)
+
+
+def _osum(A, B):
+    r = ops.edge_outer_sum_rect(A, B)
+    if r is None:
+        return A.t().mm(B), A.sum(0)
+    return r
+
+
+class GvpLayerFn(torch.autograd.Function):
+    """One GVP (128, 16) -> (128, 16) over edge rows (gmp_gvp_layer_{fwd,bwd}_f32)."""
+
+    @staticmethod
+    def forward(ctx, s, v, Ws, bs, Wsv, bsv, Wh, Wv, relu):
+        lib = _lib.load()
+        s, v = ops._f32c(s), ops._f32c(v)
+        ops._need_cuda(s, v)
+        E = s.shape[0]
+        W = [ops._f32c(t) for t in (Ws, bs, Wsv, bsv, Wh, Wv)]
+        s_out = torch.empty_like(s)
+        v_out = torch.empty_like(v)
+        with ops._timed("gvp_layer_fwd"):
+            check(lib.gmp_gvp_layer_fwd_f32(E, int(relu), ops._p(s), ops._p(v),
+                                            *[ops._p(t) for t in W], ops._p(s_out),
+                                            ops._p(v_out), ops._stream()), "gmp_gvp_layer_fwd_f32")
+        ctx.relu = relu
+        ctx.save_for_backward(s, v, *W)
+        return s_out, v_out
+
+    @staticmethod
+    def backward(ctx, ds, dv):
+        lib = _lib.load()
+        s, v, *W = ctx.saved_tensors
+        E = s.shape[0]
+        ds = ops._f32c(ds) if ds is not None else torch.zeros_like(s)
+        dv = ops._f32c(dv) if dv is not None else torch.zeros_like(v)
+        f = dict(dtype=torch.float32, device=s.device)
+        ds_in, dv_in = torch.empty_like(s), torch.empty_like(v)
+        dspre, spre = torch.empty((E, 128), **f), torch.empty((E, 128), **f)
+        dgate, vn = torch.empty((E, 16), **f), torch.empty((E, 16), **f)
+        vh, dvpre, dvh = (torch.empty((E, 48), **f) for _ in range(3))
+        with ops._timed("gvp_layer_bwd"):
+            check(lib.gmp_gvp_layer_bwd_f32(E, int(ctx.relu), ops._p(s), ops._p(v),
+                                            *[ops._p(t) for t in W], ops._p(ds), ops._p(dv),
+                                            ops._p(ds_in), ops._p(dv_in), ops._p(dspre),
+                                            ops._p(spre), ops._p(dgate), ops._p(vn), ops._p(vh),
+                                            ops._p(dvpre), ops._p(dvh), ops._stream()),
+                  "gmp_gvp_layer_bwd_f32")
+        dWs_s, dbs = _osum(dspre, s.view(E, 128))
+        dWs_v, _ = _osum(dspre, vn)
+        dWsv, dbsv = _osum(dgate, spre)
+        dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
+        dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
+        return (ds_in, dv_in, torch.cat([dWs_s, dWs_v], 1), dbs, dWsv, dbsv, dWh, dWv, None)
+
+
+class GvpMsg0Fn(torch.autograd.Function):
+    """First message GVP (gmp_gvp_msg0_{fwd,bwd}_f32) from node projections P, Q."""
+
+    @staticmethod
+    def forward(ctx, P, Q, es, ev, We, Wn, b, Wv, Wsv, bsv, wev, send_csr, recv_csr, ei):
+        lib = _lib.load()
+        P, Q, es, ev = (ops._f32c(t) for t in (P, Q, es, ev))
+        W = [ops._f32c(t) for t in (We, Wn, b, Wv, Wsv, bsv, wev)]
+        E = es.shape[0]
+        send, recv = ei[0].contiguous(), ei[1].contiguous()
+        s_out = torch.empty((E, 128), dtype=torch.float32, device=P.device)
+        v_out = torch.empty((E, 16, 3), dtype=torch.float32, device=P.device)
+        with ops._timed("gvp_msg0_fwd"):
+            check(lib.gmp_gvp_msg0_fwd_f32(E, ops._p(send), ops._p(recv), ops._p(P), ops._p(Q),
+                                           ops._p(es), ops._p(ev), *[ops._p(t) for t in W],
+                                           ops._p(s_out), ops._p(v_out), ops._stream()),
+                  "gmp_gvp_msg0_fwd_f32")
+        ctx.csrs = (send_csr, recv_csr)
+        ctx.save_for_backward(P, Q, es, ev, send, recv, *W)
+        return s_out, v_out
+
+    @staticmethod
+    def backward(ctx, ds, dv):
+        lib = _lib.load()
+        P, Q, es, ev, send, recv, *W = ctx.saved_tensors
+        send_csr, recv_csr = ctx.csrs
+        E = es.shape[0]
+        ds = ops._f32c(ds) if ds is not None else torch.zeros((E, 128), device=P.device)
+        dv = ops._f32c(dv) if dv is not None else torch.zeros((E, 16, 3), device=P.device)
+        f = dict(dtype=torch.float32, device=P.device)
+        dspre, spre = torch.empty((E, 128), **f), torch.empty((E, 128), **f)
+        dgate, vn = torch.empty((E, 16), **f), torch.empty((E, 48), **f)
+        vh, dvh = torch.empty((E, 144), **f), torch.empty((E, 144), **f)
+        dvpre = torch.empty((E, 48), **f)
+        des, dev = torch.empty((E, 32), **f), torch.empty((E, 3), **f)
+        with ops._timed("gvp_msg0_bwd"):
+            check(lib.gmp_gvp_msg0_bwd_f32(E, ops._p(send), ops._p(recv), ops._p(P), ops._p(Q),
+                                           ops._p(es), ops._p(ev), *[ops._p(t) for t in W],
+                                           ops._p(ds), ops._p(dv), ops._p(dspre), ops._p(spre),
+                                           ops._p(dgate), ops._p(vn), ops._p(vh), ops._p(dvpre),
+                                           ops._p(dvh), ops._p(des), ops._p(dev), ops._stream()),
+                  "gmp_gvp_msg0_bwd_f32")
+        # node-projection gradients: deterministic segmented sums at the senders / receivers
+        dPa, _ = ops.segment_reduce(dspre, send_csr, "sum")
+        dPb, _ = ops.segment_reduce(dspre, recv_csr, "sum")
+        dQa, _ = ops.segment_reduce(dvh, send_csr, "sum")
+        dQb, _ = ops.segment_reduce(dvh, recv_csr, "sum")
+        dWe, db = _osum(dspre, es)
+        dWn, _ = _osum(dspre, vn)
+        dWsv, dbsv = _osum(dgate, spre)
+        dWv = _diag3(_osum(dvpre, vh)[0], 16, 48)
+        M, _ = _osum(torch.nn.functional.pad(ev, (0, 13)), dvh)  # (16, 144): rows x = 0..2
+        dwev = M[:3].reshape(3, 48, 3).diagonal(dim1=0, dim2=2).sum(-1)
+        return (torch.cat([dPa, dPb], 1), torch.cat([dQa, dQb], 1).view(-1, 288), des, dev,
+                dWe, dWn, db, dWv, dWsv, dbsv, dwev, None, None, None)
+
+
 class GVPConv(MessagePassing):
     """gvp_layer.py:246-324."""
 
@@ -180,8 +303,44 @@ class GVPConv(MessagePassing):
         return (not self._custom and self.vi > 0 and g0.vi == 2 * self.vi + self.ve
                 and self.aggr in ("mean", "add", "sum") and x[0].is_cuda)
 
+    def _fused_ok(self, x, edge_attr):
+        mf = self.message_func
+        return (GVP_FUSED and len(mf) == 3 and (self.si, self.vi) == (128, 16) and
+                (self.so, self.vo) == (128, 16) and (self.se, self.ve) == (32, 1) and
+                all(m.vector_gate and m.vector_act is None for m in mf) and
+                mf[0].scalar_act is F.relu and mf[1].scalar_act is F.relu and
+                mf[2].scalar_act is None and mf[0].h_dim == 33 and
+                edge_attr[0].dtype == torch.float32)
+
+    def _fused_forward(self, s, v, edge_index, edge_attr):
+        """K5g path: message GVPs 1-3 as fused HIP kernels, mean at the receivers (K3)."""
+        n = s.shape[0]
+        g0, g1, g2 = self.message_func
+        Ws0, Wh0 = g0.ws.weight, g0.wh.weight
+        P = s.matmul(torch.cat([Ws0[:, :128], Ws0[:, 160:288]], 0).t())   # (N, 256)
+        Qa = torch.einsum("oc,ncx->nox", Wh0[:, :16], v)
+        Qb = torch.einsum("oc,ncx->nox", Wh0[:, 17:33], v)
+        Q = torch.cat([F.pad(Qa, (0, 0, 0, 15)), F.pad(Qb, (0, 0, 0, 15))], 1).reshape(n, 288)
+        es, ev = edge_attr
+        ei = edge_index
+        send_csr, recv_csr = ops.get_csr(ei[0], n), ops.get_csr(ei[1], n)
+        s1, v1 = GvpMsg0Fn.apply(P, Q, es, ev.reshape(-1, 3), Ws0[:, 128:160],
+                                 F.pad(Ws0[:, 288:321], (0, 15)), g0.ws.bias,
+                                 F.pad(g0.wv.weight, (0, 15)), g0.wsv.weight, g0.wsv.bias,
+                                 F.pad(Wh0[:, 16], (0, 15)), send_csr, recv_csr, ei)
+        s2, v2 = GvpLayerFn.apply(s1, v1, g1.ws.weight, g1.ws.bias, g1.wsv.weight, g1.wsv.bias,
+                                  g1.wh.weight, g1.wv.weight, True)
+        s3, v3 = GvpLayerFn.apply(s2, v2, g2.ws.weight, g2.ws.bias, g2.wsv.weight, g2.wsv.bias,
+                                  g2.wh.weight, g2.wv.weight, False)
+        msg = torch.cat([s3, v3.reshape(-1, 48)], 1)
+        reduce = "sum" if self.aggr == "add" else self.aggr
+        agg = ops.SegmentReduceFn.apply(msg, recv_csr, reduce)
+        return _split(agg, self.vo)
+
     def forward(self, x, edge_index, edge_attr):
         x_s, x_v = x
+        if self._fast_ok(x) and self._fused_ok(x, edge_attr):
+            return self._fused_forward(x_s, x_v, edge_index, edge_attr)
         if not self._fast_ok(x):
             msg = self.propagate(edge_index, s=x_s,
                                  v=x_v.contiguous().view(x_v.shape[0], x_v.shape[1] * 3),

@@ -243,6 +243,44 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
                           float* dZ, float* dA, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * K5g GVP-GNN message function (models/layers/gvp_layer.py:101-170 per edge via GVPConv.message
+ * :319-324; configuration of models/gvpgnn.py: activations (relu, None), vector_gate, s = 128,
+ * v = 16, edge (32, 1)).  Vector tensors in the reference's (channel, xyz) row layout.
+ *   gmp_gvp_layer_*: one GVP (128, 16) -> (128, 16) on E rows; Ws (128 x 144) = ws.weight on
+ *     [s | |vh|], Wsv (16 x 128), Wh, Wv (16 x 16); relu = scalar activation on/off.  Backward
+ *     writes ds_in, dv_in and the per-edge weight-gradient factors dspre, spre (E,128),
+ *     dgate, vn (E,16), vh, dvpre, dvh (E,48).
+ *   gmp_gvp_msg0_*: the first message GVP on [s_j, e_s, s_i] / [v_j, e_v, v_i] (j = send,
+ *     i = recv) from node projections P (N, 256) = [s W_a^T | s W_b^T] and Q (N, 288) =
+ *     [v W_ha^T | v W_hb^T] (33 channels zero-padded to 48, (channel, xyz)), es (E, 32),
+ *     ev (E, 3); We (128 x 32), Wn (128 x 48), Wv (16 x 48), wev (48) zero-padded.  Backward
+ *     writes dspre, spre (E,128), dgate (E,16), vn (E,48), vh, dvh (E,144), dvpre (E,48),
+ *     des (E,32), dev (E,3).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_gvp_layer_fwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
+                          const float* Ws, const float* bs, const float* Wsv, const float* bsv,
+                          const float* Wh, const float* Wv, float* s_out, float* v_out,
+                          void* stream);
+int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
+                          const float* Ws, const float* bs, const float* Wsv, const float* bsv,
+                          const float* Wh, const float* Wv, const float* ds_out,
+                          const float* dv_out, float* ds_in, float* dv_in, float* dspre,
+                          float* spre, float* dgate, float* vn, float* vh, float* dvpre,
+                          float* dvh, void* stream);
+int gmp_gvp_msg0_fwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
+                         const float* P, const float* Q, const float* es, const float* ev,
+                         const float* We, const float* Wn, const float* b, const float* Wv,
+                         const float* Wsv, const float* bsv, const float* wev, float* s_out,
+                         float* v_out, void* stream);
+int gmp_gvp_msg0_bwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
+                         const float* P, const float* Q, const float* es, const float* ev,
+                         const float* We, const float* Wn, const float* b, const float* Wv,
+                         const float* Wsv, const float* bsv, const float* wev,
+                         const float* ds_out, const float* dv_out, float* dspre, float* spre,
+                         float* dgate, float* vn, float* vh, float* dvpre, float* dvh,
+                         float* des, float* dev, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps
  * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)

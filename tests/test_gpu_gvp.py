@@ -59,10 +59,12 @@ def test_gvp_model_golden(golden):
     _scaled(p.grad, d["grad_pos"], 1e-4, "grad_pos")
 
 
-@pytest.mark.parametrize("fast,edge_linear", [(True, True), (True, False), (False, True)])
-def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, monkeypatch):
+@pytest.mark.parametrize("fast,edge_linear,fused", [(True, True, True), (True, True, False),
+                                                    (True, False, False), (False, True, False)])
+def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, fused, monkeypatch):
     import gmp_amd.gvp as g
     from gmp_amd import ops
+    monkeypatch.setattr(g, "GVP_FUSED", fused)
     # small graphs: force the per-edge Linear path (outer-sum dW) on, or off
     monkeypatch.setattr(ops, "EDGE_LINEAR_MIN_ROWS", 1 if edge_linear else 1 << 62)
     from gmp_amd.graph import radius_graph
@@ -83,6 +85,9 @@ def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, monkeypatch):
     es, ev = torch.randn(e, 32), torch.randn(e, 1, 3)
     xs = [t.clone().to(DEV).requires_grad_(True) for t in (s, v, es, ev)]
     xr = [t.clone().requires_grad_(True) for t in (s, v, es, ev)]
+    if fused:
+        assert lay.conv._fast_ok((xs[0], xs[1])) and lay.conv._fused_ok((xs[0], xs[1]),
+                                                                         (xs[2], xs[3]))
     so, vo = lay((xs[0], xs[1]), gr.edge_index.to(DEV), (xs[2], xs[3]))
     sr, vr = ref((xr[0], xr[1]), gr.edge_index, (xr[2], xr[3]))
     torch.testing.assert_close(so.detach().cpu(), sr.detach(), atol=1e-5, rtol=1e-5)
