@@ -163,8 +163,8 @@ __global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t
 __host__ __device__ __forceinline__ int rect_ld(int x) { return x + ((16 - x) % 64 + 64) % 64; }
 constexpr int kMaxL = 9;     // float4 loads per thread per tile (kKT * (M + N) / 4 / kT)
 
-template <int MR, int MC>
-__global__ __launch_bounds__(kT, 1) void outer_sum_rect_kernel(
+template <int MR, int MC, int NL, int OCC>
+__global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
     const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
     int64_t k_per_block, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -186,10 +186,10 @@ __global__ __launch_bounds__(kT, 1) void outer_sum_rect_kernel(
   float csum = 0.f;
   const int CA = M >> 2, CTOT = (M + N) >> 2;
   const int NLD = kKT * CTOT;
-  f32x4 reg[kMaxL];
+  f32x4 reg[NL];
   auto fetch = [&](int64_t kb) {
 #pragma unroll
-    for (int q = 0; q < kMaxL; ++q) {
+    for (int q = 0; q < NL; ++q) {
       const int c = tid + q * kT;
       reg[q] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (c < NLD) {
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kT, 1) void outer_sum_rect_kernel(
   };
   auto stash = [&](float* buf) {
 #pragma unroll
-    for (int q = 0; q < kMaxL; ++q) {
+    for (int q = 0; q < NL; ++q) {
       const int c = tid + q * kT;
       if (c < NLD) {
         const int r = c / CTOT, x = c - r * CTOT;
@@ -270,8 +270,9 @@ int rect_bucket(int64_t m, int64_t n) {
   int64_t RT, CT;
   if (TM >= 4) { RT = (TM + 3) / 4; CT = TN; }
   else { RT = TM; CT = (TN + 3) / 4; }
-  if ((m + n) / 4 * kKT > (int64_t)kMaxL * kT) return 0;
-  if (RT <= 1 && CT <= 3) return 1;
+  const int64_t loads = ceil_div((m + n) / 4 * kKT, kT);
+  if (loads > kMaxL) return 0;
+  if (RT <= 1 && CT <= 3 && loads <= 7) return 1;
   if (RT <= 2 && CT <= 5) return 2;
   if (RT <= 2 && CT <= 9) return 3;
   if (RT <= 4 && CT <= 4) return 4;
@@ -330,8 +331,15 @@ int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B,
   return launch_status();
 }
 
+int64_t rect_blocks_for(int64_t K) {
+  int64_t g = (int64_t)device_cu_count() * 2;
+  const int64_t min_per = 4 * kKT;
+  if (g * min_per > K) g = ceil_div(K, min_per);
+  return g < 1 ? 1 : g;
+}
+
 size_t gmp_edge_outer_sum_rect_workspace_size(int64_t K, int64_t m, int64_t n) {
-  const int64_t G = blocks_for(K);
+  const int64_t G = rect_blocks_for(K);
   return (size_t)(G + ceil_div(G, kGC)) * (size_t)(m * n + m) * sizeof(float);
 }
 
@@ -350,15 +358,15 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
   GMP_CHECK_ARG(A && B && workspace);
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0);
   if (workspace_bytes < gmp_edge_outer_sum_rect_workspace_size(K, m, n)) return GMP_ERR_WORKSPACE;
-  const int64_t G = blocks_for(K);
+  const int64_t G = rect_blocks_for(K);
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
   const size_t smem = (size_t)2 * kKT * (rect_ld((int)m) + rect_ld((int)n)) * sizeof(float);
   int rc;
-#define GMP_RECT(MR, MC)                                                                      \
+#define GMP_RECT(MR, MC, NL, OCC)                                                             \
   {                                                                                           \
-    auto k = outer_sum_rect_kernel<MR, MC>;                                                   \
+    auto k = outer_sum_rect_kernel<MR, MC, NL, OCC>;                                          \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                   \
                                             hipFuncAttributeMaxDynamicSharedMemorySize,      \
                                             (int)smem))))                                     \
@@ -366,10 +374,10 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
     k<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, per, part);                     \
   }
   switch (bucket) {
-    case 1: GMP_RECT(1, 3) break;
-    case 2: GMP_RECT(2, 5) break;
-    case 3: GMP_RECT(2, 9) break;
-    default: GMP_RECT(4, 4) break;
+    case 1: GMP_RECT(1, 3, 7, 2) break;
+    case 2: GMP_RECT(2, 5, 9, 1) break;
+    case 3: GMP_RECT(2, 9, 9, 1) break;
+    default: GMP_RECT(4, 4, 9, 1) break;
   }
 #undef GMP_RECT
   rc = launch_status();
