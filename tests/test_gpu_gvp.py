@@ -138,3 +138,27 @@ def test_edge_outer_sum_rect(m, n, K):
     assert (cs.double().cpu() - A.sum(0)).abs().max().item() <= 1e-4
     C2, _ = ops.edge_outer_sum_rect(A.float().to(DEV), B.float().to(DEV))
     assert torch.equal(C, C2)  # deterministic
+
+
+def test_gvp_fused_deterministic_and_model_c3():
+    """Fused GVP message kernels: bitwise-repeatable forward/backward on a C3-width model."""
+    import gmp_amd.gvp as g
+    from gmp_amd.graph import Batch, radius_graph
+    torch.manual_seed(11)
+    gr = radius_graph(num_nodes=800, target_edges=12000, r=2.0, seed=3, tol=0.2, shuffle=True)
+    model = g.GVPGNNModel(r_max=2.0, num_layers=2).to(DEV).eval()
+    b = Batch(gr.atoms.to(DEV), gr.pos.to(DEV).requires_grad_(True), gr.edge_index.to(DEV))
+    assert model.layers[0].conv._fused_ok((torch.zeros(1, 128, device=DEV),
+                                          torch.zeros(1, 16, 3, device=DEV)),
+                                         (torch.zeros(1, 32, device=DEV), None))
+
+    def run():
+        model.zero_grad()
+        b.pos.grad = None
+        y = model(b)
+        y.sum().backward()
+        return y.detach().clone(), b.pos.grad.clone(), model.layers[0].conv.message_func[1].ws.weight.grad.clone()
+
+    a1, a2 = run(), run()
+    for u, v in zip(a1, a2):
+        assert torch.equal(u, v)
