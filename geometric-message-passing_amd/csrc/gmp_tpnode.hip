@@ -116,20 +116,49 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
     f32x4 accA[4][2];
 #pragma unroll
     for (int a = 0; a < 4; ++a) accA[a][0] = accA[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // register-staged prefetch of the next row block (T rows and Z columns) so its HBM latency
+    // overlaps the current block's MFMAs
+    constexpr int kTL = kAR * (kMaxH / 4) / kNT;   // float4 T loads per thread (8)
+    constexpr int kZL = kAE * kAR / kNT;           // Z loads per thread (4)
+    f32x4 regT[kTL];
+    float regZ[kZL];
+    auto fetch = [&](int rb) {
+      const int nrb = (w - rb) < kAR ? (w - rb) : kAR;
+#pragma unroll
+      for (int q = 0; q < kTL; ++q) {
+        const int x = tid + kNT * q;
+        const int rr = x / H4, c4 = x - rr * H4;
+        regT[q] = (x < kAR * H4 && rr < nrb)
+                      ? *reinterpret_cast<const f32x4*>(Tn + (int64_t)(rb + rr) * H + 4 * c4)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < kZL; ++q) {
+        const int x = tid + kNT * q;
+        const int e = x / kAR, rr = x - e * kAR;
+        regZ[q] = (e < ng && rr < nrb) ? Z[(e0 + g0 + e) * w + rb + rr] : 0.f;
+      }
+    };
+    fetch(0);
     for (int r0 = 0; r0 < w; r0 += kAR) {
       const int nr = (w - r0) < kAR ? (w - r0) : kAR;
       __syncthreads();
-      for (int x = tid; x < kAR * H4; x += kNT) {
-        const int rr = x / H4, q = x - rr * H4;
-        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (rr < nr) v = *reinterpret_cast<const f32x4*>(Tn + (int64_t)(r0 + rr) * H + 4 * q);
-        *reinterpret_cast<f32x4*>(&sT[rr * kLdT + 4 * q]) = v;
+#pragma unroll
+      for (int q = 0; q < kTL; ++q) {
+        const int x = tid + kNT * q;
+        if (x < kAR * H4) {
+          const int rr = x / H4, c4 = x - rr * H4;
+          *reinterpret_cast<f32x4*>(&sT[rr * kLdT + 4 * c4]) = regT[q];
+        }
       }
-      for (int x = tid; x < kAE * kAR; x += kNT) {
+#pragma unroll
+      for (int q = 0; q < kZL; ++q) {
+        const int x = tid + kNT * q;
         const int e = x / kAR, rr = x - e * kAR;
-        sZ[e * kLdZ + rr] = (e < ng && rr < nr) ? Z[(e0 + g0 + e) * w + r0 + rr] : 0.f;
+        sZ[e * kLdZ + rr] = regZ[q];
       }
       __syncthreads();
+      if (r0 + kAR < w) fetch(r0 + kAR);
       // dZ[e, r] = sum_j T[r, j] a[e, j]   (D[row][e]; A op = T rows, B op = a rows)
       if (16 * rt < nr && 16 * et < ng) {
         // four independent accumulation chains over j (MFMA latency), summed in fixed order
