@@ -14,7 +14,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kT = 256;      // threads (4 waves)
 constexpr int kKT = 32;      // edges per LDS tile
-constexpr int kLD = 128 + 16;  // LDS row stride (floats): lanes 0-15 / 16-31 on disjoint banks
 
 template <int D>
 struct WCfg {

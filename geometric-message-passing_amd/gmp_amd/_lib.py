@@ -87,6 +87,11 @@ SIGNATURES = {
     "gmp_gvp_layer_bwd_f32": (c_int, [c_i64, c_int] + [c_vp] * 19 + [c_vp]),
     "gmp_gvp_msg0_fwd_f32": (c_int, [c_i64] + [c_vp] * 15 + [c_vp]),
     "gmp_gvp_msg0_bwd_f32": (c_int, [c_i64] + [c_vp] * 24 + [c_vp]),
+    "gmp_radius_cells_f32": (c_int, [c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp]),
+    "gmp_radius_count_f32": (c_int, [c_vp, c_vp, c_i64, c_f32, c_i64, c_vp, c_f32, c_vp, c_vp,
+                                     c_vp, c_vp, c_vp, c_vp]),
+    "gmp_radius_fill_f32": (c_int, [c_vp, c_vp, c_i64, c_f32, c_i64, c_vp, c_f32, c_vp, c_vp,
+                                    c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_sc_groups": (c_int, [c_i64]),
     "gmp_symmetric_contraction_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp]),

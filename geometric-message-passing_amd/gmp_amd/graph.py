@@ -119,3 +119,70 @@ def create_kchains(k=4):
         ei = ei[:, torch.argsort(ei[0] * (k + 2) + ei[1])]  # to_undirected sorts by (row, col)
         graphs.append(Batch(torch.zeros(k + 2, dtype=torch.long), pos, ei))
     return graphs
+
+
+def radius_graph_gpu(pos, r, batch=None, max_num_neighbors=32, num_graphs=None):
+    """Device radius graph (K9, gmp_radius_*), the builder PyG SchNet constructs
+    (models/schnet.py:47: torch_cluster.radius_graph(pos, r, batch, loop=False,
+    max_num_neighbors)).  Edge j -> i for j != i of the same graph with
+    ((dx*dx + dy*dy) + dz*dz) < r*r in fp32; per target the first max_num_neighbors + 1
+    candidates in ascending j (self included) are kept and self is dropped — torch_cluster's
+    GPU selection rule; max_num_neighbors=None or <= 0 keeps all.  Returns edge_index (2, E)
+    int64 [sources; targets] sorted by (target, source).  pos: (N, 3) fp32 on the GPU.
+    Host syncs: the bounding box, num_graphs (if not given) and the edge count."""
+    import ctypes
+    from . import _lib, ops
+    lib = _lib.load()
+    pos = ops._f32c(pos)
+    ops._need_cuda(pos)
+    if pos.dim() != 2 or pos.shape[1] != 3:
+        raise ValueError(f"pos must be (N, 3), got {tuple(pos.shape)}")
+    if not r > 0:
+        raise ValueError("r must be > 0")
+    N = pos.shape[0]
+    dev = pos.device
+    if N == 0:
+        return torch.empty((2, 0), dtype=torch.int64, device=dev)
+    if batch is not None:
+        batch = ops._i64c(batch)
+        ops._need_cuda(batch)
+        if num_graphs is None:
+            num_graphs = int(batch.max().item()) + 1
+    num_graphs = 1 if batch is None else int(num_graphs)
+    k = 0 if max_num_neighbors is None else max(int(max_num_neighbors), 0)
+    lo = pos.min(0).values.cpu().numpy().astype(np.float32)
+    hi = pos.max(0).values.cpu().numpy().astype(np.float32)
+    r32 = np.float32(r)
+    width = float(r32) * (1.0 + 1e-5)  # cell edge > r: rounding in the cell index stays safe
+    while True:  # bound the cell table at ~2 cells per node
+        inv = float(np.float32(1.0) / np.float32(width))
+        if inv > float(np.float32(1.0) / r32):
+            width *= 1.0 + 1e-5
+            continue
+        dims = [max(1, int(np.floor(float(hi[d] - lo[d]) * inv)) + 1) for d in range(3)]
+        n_cells = num_graphs * dims[0] * dims[1] * dims[2]
+        if n_cells <= 2 * N + 64:
+            break
+        width *= 1.25
+    lo_c = (ctypes.c_float * 3)(*lo.tolist())
+    dims_c = (ctypes.c_int * 3)(*dims)
+    s = ops._stream()
+    cells = torch.empty(N, dtype=torch.int64, device=dev)
+    ops.check(lib.gmp_radius_cells_f32(ops._p(pos), ops._p(batch), N, lo_c, inv, dims_c,
+                                       ops._p(cells), s), "gmp_radius_cells_f32")
+    csr = ops.CSR(cells, n_cells)
+    counts = torch.empty(N, dtype=torch.int64, device=dev)
+    ops.check(lib.gmp_radius_count_f32(ops._p(pos), ops._p(batch), N, float(r32), k, lo_c, inv,
+                                       dims_c, ops._p(cells), ops._p(csr.rowptr),
+                                       ops._p(csr.perm), ops._p(counts), s),
+              "gmp_radius_count_f32")
+    offs = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(counts, 0, out=offs[1:])
+    E = int(offs[-1].item())
+    src = torch.empty(E, dtype=torch.int64, device=dev)
+    ops.check(lib.gmp_radius_fill_f32(ops._p(pos), ops._p(batch), N, float(r32), k, lo_c, inv,
+                                      dims_c, ops._p(cells), ops._p(csr.rowptr),
+                                      ops._p(csr.perm), ops._p(offs), ops._p(src), s),
+              "gmp_radius_fill_f32")
+    dst = torch.repeat_interleave(torch.arange(N, device=dev), counts, output_size=E)
+    return torch.stack([src, dst])

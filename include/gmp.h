@@ -281,6 +281,32 @@ int gmp_gvp_msg0_bwd_f32(int64_t n_edges, const int64_t* send, const int64_t* re
                          float* des, float* dev, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * K9 radius graph.  Replaces torch_cluster.radius_graph(pos, r, batch,
+ * loop=False, max_num_neighbors) as PyG SchNet's RadiusInteractionGraph builds it
+ * (models/schnet.py:47; GPU-kernel selection rule): edge j -> i for j != i of the same graph with
+ * ((dx*dx + dy*dy) + dz*dz) < r*r in fp32 (dx = p_i - p_j, no contraction); per target the first
+ * max_num_neighbors + 1 candidates in ascending j (self included) are kept, then self is dropped
+ * (max_num_neighbors <= 0: no cap).  batch may be NULL (one graph).  Cells have edge
+ * 1/inv_cell >= r over the box [lo, lo + dims/inv_cell), keyed (graph, cell):
+ *   cells: cell id per node -> the caller buckets nodes with gmp_csr_build over
+ *          num_graphs*dims[0]*dims[1]*dims[2] segments (cell_rowptr, cell_perm);
+ *   count: number of sources per target;  fill: the sources of target i at
+ *          offsets[i]..offsets[i+1], ascending -> edge_index sorted by (target, source).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_radius_cells_f32(const float* pos, const int64_t* batch, int64_t n_nodes,
+                         const float* lo3, float inv_cell, const int* dims3, int64_t* cell_out,
+                         void* stream);
+int gmp_radius_count_f32(const float* pos, const int64_t* batch, int64_t n_nodes, float r,
+                         int64_t max_num_neighbors, const float* lo3, float inv_cell,
+                         const int* dims3, const int64_t* cell, const int64_t* cell_rowptr,
+                         const int64_t* cell_perm, int64_t* counts, void* stream);
+int gmp_radius_fill_f32(const float* pos, const int64_t* batch, int64_t n_nodes, float r,
+                        int64_t max_num_neighbors, const float* lo3, float inv_cell,
+                        const int* dims3, const int64_t* cell, const int64_t* cell_rowptr,
+                        const int64_t* cell_perm, const int64_t* offsets, int64_t* src_out,
+                        void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps
  * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)
