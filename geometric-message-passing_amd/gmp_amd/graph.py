@@ -180,6 +180,8 @@ def radius_graph_gpu(pos, r, batch=None, max_num_neighbors=32, num_graphs=None):
     torch.cumsum(counts, 0, out=offs[1:])
     E = int(offs[-1].item())
     src = torch.empty(E, dtype=torch.int64, device=dev)
+    if E == 0:
+        return torch.empty((2, 0), dtype=torch.int64, device=dev)
     ops.check(lib.gmp_radius_fill_f32(ops._p(pos), ops._p(batch), N, float(r32), k, lo_c, inv,
                                       dims_c, ops._p(cells), ops._p(csr.rowptr),
                                       ops._p(csr.perm), ops._p(offs), ops._p(src), s),

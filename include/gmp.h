@@ -307,6 +307,18 @@ int gmp_radius_fill_f32(const float* pos, const int64_t* batch, int64_t n_nodes,
                         void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * K10 batch collation (PyG Batch.from_data_list as the reference's loaders
+ * build it, experiments/utils/train_utils.py:28,132).  edge_index_local: (2, E) graph-local
+ * indices of B graphs packed back to back; node_ptr / edge_ptr: (B+1) prefix sums of the
+ * per-graph node / edge counts.  Writes edge_index_out = local + node_ptr[graph of edge] and
+ * batch_out[a] = graph of node a.  A local index outside [0, n_g) sets *err to 1 (err may be
+ * NULL).  Empty graphs are allowed.
+ * ------------------------------------------------------------------------------------------ */
+int gmp_batch_collate(const int64_t* edge_index_local, int64_t n_edges, const int64_t* node_ptr,
+                      const int64_t* edge_ptr, int64_t n_graphs, int64_t n_nodes,
+                      int64_t* edge_index_out, int64_t* batch_out, int* err, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps
  * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)
