@@ -47,12 +47,29 @@ __device__ __forceinline__ float dist2(const float* __restrict__ pos, int64_t i,
 
 // MODE 0: counts[i] = number of sources kept for target i; MODE 1: write them at offs[i],
 // ascending (bounded insert: the counts[i] smallest non-self candidates).
+// bounded sorted insert of j into arr[0, filled) with capacity cap (keeps the cap smallest)
+template <typename T>
+__device__ __forceinline__ void bounded_insert(T* arr, int64_t& filled, int64_t cap, int64_t j) {
+  if (filled == cap && !(j < (int64_t)arr[cap - 1])) return;
+  int64_t b = (filled < cap ? filled++ : cap - 1) - 1;
+  while (b >= 0 && (int64_t)arr[b] > j) {
+    arr[b + 1] = arr[b];
+    --b;
+  }
+  arr[b + 1] = (T)j;
+}
+
+constexpr int kRT = 256;   // threads per block
+constexpr int kLB = 48;    // per-thread LDS sort buffer (sources of one target)
+constexpr int kLS = kLB + 1;  // odd stride: lanes on distinct banks
+
 template <int MODE>
-__global__ void radius_kernel(const float* __restrict__ pos, const int64_t* __restrict__ batch,
+__global__ __launch_bounds__(kRT) void radius_kernel(const float* __restrict__ pos, const int64_t* __restrict__ batch,
                               int64_t N, float r2, int64_t max_nb, Grid G,
                               const int64_t* __restrict__ cell, const int64_t* __restrict__ crow,
                               const int64_t* __restrict__ cperm, int64_t* __restrict__ counts,
                               const int64_t* __restrict__ offs, int64_t* __restrict__ src) {
+  __shared__ int s_buf[MODE ? kRT * kLS : 1];
   const int64_t per_graph = (int64_t)G.n[0] * G.n[1] * G.n[2];
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -66,6 +83,8 @@ __global__ void radius_kernel(const float* __restrict__ pos, const int64_t* __re
     int64_t filled = 0;           // MODE 1
     const int64_t base = MODE ? offs[i] : 0;
     const int64_t cap = MODE ? offs[i + 1] - base : 0;
+    int* lbuf = s_buf + (MODE ? threadIdx.x * kLS : 0);
+    const bool in_lds = cap <= kLB;
     for (int z = cz - 1; z <= cz + 1; ++z) {
       if (z < 0 || z >= G.n[2]) continue;
       for (int y = cy - 1; y <= cy + 1; ++y) {
@@ -82,17 +101,15 @@ __global__ void radius_kernel(const float* __restrict__ pos, const int64_t* __re
               n_lt += (j < i);
               continue;
             }
-            if (j == i) continue;
-            if (filled == cap && !(j < src[base + cap - 1])) continue;
-            int64_t b = (filled < cap ? base + filled++ : base + cap - 1) - 1;
-            while (b >= base && src[b] > j) {
-              src[b + 1] = src[b];
-              --b;
-            }
-            src[b + 1] = j;
+            if (j == i || cap == 0) continue;
+            if (in_lds) bounded_insert(lbuf, filled, cap, j);
+            else bounded_insert(src + base, filled, cap, j);
           }
         }
       }
+    }
+    if (MODE && in_lds) {
+      for (int64_t a = 0; a < cap; ++a) src[base + a] = lbuf[a];
     }
     if (!MODE) {
       // torch_cluster keeps the first max_nb + 1 candidates (self included), then drops self
@@ -134,6 +151,7 @@ static int radius_launch(int mode, const float* pos, const int64_t* batch, int64
                          int64_t* src_out, void* stream) {
   GMP_CHECK_ARG(n_nodes >= 0 && lo3 && dims3 && r > 0.f);
   if (n_nodes == 0) return GMP_OK;
+  GMP_CHECK_ARG(n_nodes <= INT32_MAX);  // LDS sort buffer holds 32-bit node ids
   GMP_CHECK_ARG(pos && cell && cell_rowptr && cell_perm);
   GMP_CHECK_ARG(dims3[0] > 0 && dims3[1] > 0 && dims3[2] > 0);
   GMP_CHECK_ARG(inv_cell > 0.f && inv_cell <= 1.f / r);  // cell edge >= r: 27 cells suffice
@@ -141,12 +159,12 @@ static int radius_launch(int mode, const float* pos, const int64_t* batch, int64
   const float r2 = r * r;
   if (mode == 0) {
     GMP_CHECK_ARG(counts);
-    radius_kernel<0><<<grid1d(n_nodes), 256, 0, as_stream(stream)>>>(
+    radius_kernel<0><<<grid1d(n_nodes), kRT, 0, as_stream(stream)>>>(
         pos, batch, n_nodes, r2, max_nb, G, cell, cell_rowptr, cell_perm, counts, nullptr,
         nullptr);
   } else {
     GMP_CHECK_ARG(offsets && src_out);
-    radius_kernel<1><<<grid1d(n_nodes), 256, 0, as_stream(stream)>>>(
+    radius_kernel<1><<<grid1d(n_nodes), kRT, 0, as_stream(stream)>>>(
         pos, batch, n_nodes, r2, max_nb, G, cell, cell_rowptr, cell_perm, nullptr, offsets,
         src_out);
   }

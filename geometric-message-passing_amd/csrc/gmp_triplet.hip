@@ -1,0 +1,217 @@
+// K11: triplet enumeration + angle / torsion featurisation (the "angles"
+// of the north star's featurisation list).  Follows models/layers/spherenet_layer.py:496-564
+// (`xyz_to_dat`) and the DimeNet forward models/dimenet.py:77-90:
+//   edge e = (j -> i); its triplets are the in-edges kj = (k -> j) of j with k != i, in
+//   ascending k (the row-major order of torch_sparse's adj_t = SparseTensor(row=i, col=j));
+//   triplets of all edges are concatenated in edge order.
+//   angle (SphereNet, vertex j): atan2(|(p_i - p_j) x (p_k - p_j)|, (p_i - p_j).(p_k - p_j))
+//   angle (DimeNet,   vertex i): atan2(|(p_j - p_i) x (p_k - p_i)|, (p_j - p_i).(p_k - p_i))
+//   torsion (SphereNet): min over the in-neighbours k_n != i of j of atan2(b, a) mapped to
+//   (0, 2*pi], with plane1 = v_ji x v_jk, plane2 = v_ji x v_jkn, a = plane1.plane2,
+//   b = (plane1 x plane2).v_ji / |v_ji|.
+// The arithmetic reproduces the reference's torch CPU evaluation operation by operation:
+// torch.cross is a_i*b_j - a_j*b_i contracted to fma(a_i, b_j, -(a_j*b_i)); `(x*y).sum(-1)`
+// rounds each product then adds (((+0 + 0) + 1) + 2); `.norm(-1)` accumulates fma(x, x, acc);
+// `.pow(2).sum(-1).sqrt()` is products, ((0 + 1) + 2), sqrt.  This matters beyond the last ulp:
+// for k_n = k plane1 == plane2, and the sign of the contracted cross product's rounding
+// residual decides whether that candidate's torsion is ~1e-9 or 2*pi — the reference's
+// output depends on it, so the kernel follows it.
+#include "gmp_common.h"
+
+namespace gmp {
+namespace {
+
+constexpr float kTwoPi = 6.283185307179586f;
+
+struct V3 {
+  float x, y, z;
+};
+
+__device__ __forceinline__ V3 ld3(const float* __restrict__ p, int64_t a) {
+  return V3{p[3 * a], p[3 * a + 1], p[3 * a + 2]};
+}
+__device__ __forceinline__ V3 sub3(V3 a, V3 b) {
+  return V3{__fsub_rn(a.x, b.x), __fsub_rn(a.y, b.y), __fsub_rn(a.z, b.z)};
+}
+// torch.cross on CPU: fma(a_i, b_j, -(a_j * b_i))
+__device__ __forceinline__ V3 cross3(V3 a, V3 b) {
+  return V3{__fmaf_rn(a.y, b.z, -__fmul_rn(a.z, b.y)), __fmaf_rn(a.z, b.x, -__fmul_rn(a.x, b.z)),
+            __fmaf_rn(a.x, b.y, -__fmul_rn(a.y, b.x))};
+}
+// (a * b).sum(-1): the reduction starts from +0, so an all-(-0) sum is +0 (atan2(0, +0) = 0,
+// not pi, for a degenerate self-loop vector)
+__device__ __forceinline__ float dot3(V3 a, V3 b) {
+  return __fadd_rn(__fadd_rn(__fadd_rn(0.f, __fmul_rn(a.x, b.x)), __fmul_rn(a.y, b.y)),
+                   __fmul_rn(a.z, b.z));
+}
+// a.norm(dim=-1)
+__device__ __forceinline__ float norm3(V3 a) {
+  float acc = __fmul_rn(a.x, a.x);
+  acc = __fmaf_rn(a.y, a.y, acc);
+  acc = __fmaf_rn(a.z, a.z, acc);
+  return __fsqrt_rn(acc);
+}
+// a.pow(2).sum(-1).sqrt()
+__device__ __forceinline__ float len3(V3 a) { return __fsqrt_rn(dot3(a, a)); }
+
+// [p, q): entries of the (source-sorted) adjacency row [r0, r1) whose source equals s
+__device__ __forceinline__ void equal_range(const int64_t* __restrict__ asrc, int64_t r0,
+                                            int64_t r1, int64_t s, int64_t& p, int64_t& q) {
+  int64_t lo = r0, hi = r1;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (asrc[m] < s) lo = m + 1;
+    else hi = m;
+  }
+  p = lo;
+  hi = r1;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (asrc[m] <= s) lo = m + 1;
+    else hi = m;
+  }
+  q = lo;
+}
+
+__global__ void triplet_count_kernel(const float* __restrict__ pos,
+                                     const int64_t* __restrict__ ei, int64_t E,
+                                     const int64_t* __restrict__ arow,
+                                     const int64_t* __restrict__ asrc,
+                                     int64_t* __restrict__ counts, float* __restrict__ dist) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += stride) {
+    const int64_t j = ei[e], i = ei[E + e];
+    const int64_t r0 = arow[j], r1 = arow[j + 1];
+    int64_t p, q;
+    equal_range(asrc, r0, r1, i, p, q);
+    counts[e] = (r1 - r0) - (q - p);
+    if (dist) dist[e] = len3(sub3(ld3(pos, i), ld3(pos, j)));
+  }
+}
+
+// One workgroup per block of kFB consecutive edges.  Phase 1: a thread per edge puts the
+// edge's triplet offset, endpoints and adjacency window (row start, the [p, q) run of source i)
+// into LDS.  Phase 2: the block's triplets are spread over all threads; each finds its edge by
+// a binary search in LDS (no global-memory search per triplet).
+// mode 0: SphereNet angle at j (+ optional torsion); mode 1: DimeNet angle at i
+constexpr int kFB = 256;
+
+__global__ __launch_bounds__(kFB) void triplet_fill_kernel(
+    const float* __restrict__ pos, const int64_t* __restrict__ ei, int64_t E,
+    const int64_t* __restrict__ arow, const int64_t* __restrict__ asrc,
+    const int64_t* __restrict__ aeid, const int64_t* __restrict__ offs, int mode,
+    int64_t* __restrict__ idx_kj, int64_t* __restrict__ idx_ji, float* __restrict__ angle,
+    float* __restrict__ torsion) {
+  __shared__ int64_t s_off[kFB + 1];
+  __shared__ int64_t s_i[kFB], s_j[kFB], s_r0[kFB], s_r1[kFB], s_p[kFB], s_q[kFB];
+  const int64_t e0 = (int64_t)blockIdx.x * kFB;
+  const int nE = (int)(E - e0 < kFB ? E - e0 : kFB);
+  const int tid = threadIdx.x;
+  if (tid < nE) {
+    const int64_t e = e0 + tid;
+    const int64_t j = ei[e], i = ei[E + e];
+    const int64_t r0 = arow[j], r1 = arow[j + 1];
+    int64_t p, q;
+    equal_range(asrc, r0, r1, i, p, q);
+    s_off[tid] = offs[e];
+    s_i[tid] = i;
+    s_j[tid] = j;
+    s_r0[tid] = r0;
+    s_r1[tid] = r1;
+    s_p[tid] = p;
+    s_q[tid] = q;
+  }
+  if (tid == 0) s_off[nE] = offs[e0 + nE];
+  __syncthreads();
+  const int64_t t_begin = s_off[0], t_end = s_off[nE];
+  for (int64_t t = t_begin + tid; t < t_end; t += kFB) {
+    int lo = 0, hi = nE;  // largest local edge with s_off <= t
+    while (hi - lo > 1) {
+      const int m = (lo + hi) >> 1;
+      if (s_off[m] <= t) lo = m;
+      else hi = m;
+    }
+    const int64_t e = e0 + lo;
+    const int64_t i = s_i[lo], j = s_j[lo], r0 = s_r0[lo], r1 = s_r1[lo];
+    const int64_t p = s_p[lo], q = s_q[lo];
+    const int64_t local = t - s_off[lo];
+    const int64_t slot = r0 + local + (r0 + local >= p ? q - p : 0);
+    const int64_t k = asrc[slot];
+    idx_kj[t] = aeid[slot];
+    idx_ji[t] = e;
+    if (!angle && !torsion) continue;
+    const V3 pi = ld3(pos, i), pj = ld3(pos, j), pk = ld3(pos, k);
+    if (angle) {
+      V3 u, v;
+      if (mode == 0) {
+        u = sub3(pi, pj);
+        v = sub3(pk, pj);
+      } else {
+        u = sub3(pj, pi);
+        v = sub3(pk, pi);
+      }
+      angle[t] = atan2f(norm3(cross3(u, v)), dot3(u, v));
+    }
+    if (torsion) {
+      const V3 vji = sub3(pi, pj);
+      const V3 vj0 = sub3(pk, pj);
+      const float dji = len3(vji);
+      const V3 plane1 = cross3(vji, vj0);
+      float best = 3.402823466e38f;  // torch_scatter min: identity FLT_MAX, NaN never wins
+      for (int64_t m = r0; m < r1; ++m) {
+        const int64_t kn = asrc[m];
+        if (kn == i) continue;
+        const V3 vjk = sub3(ld3(pos, kn), pj);
+        const V3 plane2 = cross3(vji, vjk);
+        const float a = dot3(plane1, plane2);
+        const float b = __fdiv_rn(dot3(cross3(plane1, plane2), vji), dji);
+        float t1 = atan2f(b, a);
+        if (t1 <= 0.f) t1 = __fadd_rn(t1, kTwoPi);
+        if (t1 < best) best = t1;
+      }
+      torsion[t] = best == 3.402823466e38f ? 0.f : best;
+    }
+  }
+}
+
+int grid_for(int64_t n) {
+  int64_t g = ceil_div(n, 256);
+  const int64_t cap = (int64_t)device_cu_count() * 16;
+  return (int)(g > cap ? cap : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+}  // namespace gmp
+
+using namespace gmp;
+
+extern "C" {
+
+int gmp_triplet_count(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                      int64_t n_nodes, const int64_t* adj_rowptr, const int64_t* adj_src,
+                      int64_t* counts, float* dist, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(edge_index && adj_rowptr && adj_src && counts && (pos || !dist));
+  triplet_count_kernel<<<grid_for(n_edges), 256, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, adj_rowptr, adj_src, counts, dist);
+  return launch_status();
+}
+
+int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                         int64_t n_nodes, const int64_t* adj_rowptr, const int64_t* adj_src,
+                         const int64_t* adj_eid, const int64_t* offsets, int64_t n_triplets,
+                         int mode, int64_t* idx_kj, int64_t* idx_ji, float* angle,
+                         float* torsion, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && n_triplets >= 0 && (mode == 0 || mode == 1));
+  GMP_CHECK_ARG(mode == 0 || !torsion);
+  if (n_triplets == 0) return GMP_OK;
+  GMP_CHECK_ARG(n_edges > 0 && edge_index && adj_rowptr && adj_src && adj_eid && offsets &&
+                idx_kj && idx_ji && (pos || (!angle && !torsion)));
+  triplet_fill_kernel<<<(unsigned)ceil_div(n_edges, kFB), kFB, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, adj_rowptr, adj_src, adj_eid, offsets, mode, idx_kj, idx_ji,
+      angle, torsion);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -93,6 +93,9 @@ SIGNATURES = {
     "gmp_radius_fill_f32": (c_int, [c_vp, c_vp, c_i64, c_f32, c_i64, c_vp, c_f32, c_vp, c_vp,
                                     c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_batch_collate": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_triplet_count": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_triplet_fill_f32": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                     c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_sc_groups": (c_int, [c_i64]),
     "gmp_symmetric_contraction_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp]),

@@ -319,6 +319,28 @@ int gmp_batch_collate(const int64_t* edge_index_local, int64_t n_edges, const in
                       int64_t* edge_index_out, int64_t* batch_out, int* err, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * K11 triplets + angles / torsions.  Replaces `xyz_to_dat`
+ * (models/layers/spherenet_layer.py:496-564) and the triplet/angle block of the DimeNet forward
+ * (models/dimenet.py:79-90, PyG DimeNet.triplets).  edge_index (2, E): e = (j -> i).
+ * Adjacency by target, entries sorted by (target, source): adj_rowptr (N+1), adj_src (source
+ * of each entry), adj_eid (edge id of each entry).
+ *   count: counts[e] = in-degree(j) - #{in-edges of j with source i}; dist[e] = |p_i - p_j|
+ *          (dist may be NULL);
+ *   fill:  for t in [offsets[e], offsets[e+1]): idx_kj[t] = edge (k -> j) for the k != i in
+ *          ascending order, idx_ji[t] = e; angle[t] (mode 0: SphereNet, vertex j; mode 1:
+ *          DimeNet, vertex i; may be NULL); torsion[t] (mode 0 only, may be NULL).
+ * Arithmetic reproduces the reference's torch CPU evaluation op by op (see gmp_triplet.hip).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_triplet_count(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                      int64_t n_nodes, const int64_t* adj_rowptr, const int64_t* adj_src,
+                      int64_t* counts, float* dist, void* stream);
+int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                         int64_t n_nodes, const int64_t* adj_rowptr, const int64_t* adj_src,
+                         const int64_t* adj_eid, const int64_t* offsets, int64_t n_triplets,
+                         int mode, int64_t* idx_kj, int64_t* idx_ji, float* angle,
+                         float* torsion, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps
  * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)

@@ -1,4 +1,4 @@
-"""Time the device radius graph (K9) on the benchmark-size graph (50k nodes, ~1M edges) and on a
+"""Time the device radius graph (K9) and triplet featurisation (K11) on the benchmark-size graph (50k nodes, ~1M edges) and on a
 batch of QM9-sized molecules; the scipy cKDTree builder (host input synthesis) beside it."""
 import os
 import sys
@@ -37,3 +37,12 @@ mb = torch.from_numpy(np.repeat(np.arange(1024), sizes)).cuda()
 ms, ei = timeit(lambda: radius_graph_gpu(mpos, 10.0, mb, 32, num_graphs=1024))
 print(f"radius 1024 molecules / {mpos.shape[0]} atoms / {ei.shape[1]} edges, r=10, k=32: "
       f"gpu {ms:.3f} ms")
+
+from gmp_amd.triplets import xyz_to_dat  # noqa: E402
+
+ei = g.edge_index.cuda()
+for tors in (False, True):
+    ms, out = timeit(lambda: xyz_to_dat(pos, ei, pos.shape[0], use_torsion=tors), reps=10)
+    T = out[1].numel()
+    print(f"triplets 50k nodes / {ei.shape[1]} edges -> {T} triplets, torsion={tors}: "
+          f"gpu {ms:.3f} ms ({T / ms / 1e6:.2f} G triplets/s)")

@@ -70,12 +70,80 @@ def scatter_mean(src, index, dim=-1, out=None, dim_size=None):
     return out
 
 
+def scatter_min(src, index, dim=-1, out=None, dim_size=None):
+    """torch_scatter min (1-D use in spherenet_layer.py:561): rows = index.max()+1; each row
+    starts at the dtype's max and takes a value only if it compares smaller (so NaN never wins);
+    rows still at max become 0."""
+    assert src.dim() == 1 and out is None
+    n = dim_size if dim_size is not None else (int(index.max()) + 1 if index.numel() else 0)
+    big = torch.finfo(src.dtype).max
+    res = torch.full((n,), big, dtype=src.dtype).scatter_reduce(
+        0, index, torch.nan_to_num(src, nan=big), "amin", include_self=True)
+    res[res == big] = 0
+    return res
+
+
 def scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum"):
     if reduce in ("sum", "add"):
         return scatter_sum(src, index, dim, out, dim_size)
     if reduce == "mean":
         return scatter_mean(src, index, dim, out, dim_size)
+    if reduce == "min":
+        return scatter_min(src, index, dim, out, dim_size)
     raise ValueError(reduce)
+
+
+# ----------------------------------------------------------------------------- torch_sparse
+class _SparseStorage:
+    def __init__(self, row, col, value):
+        self._row, self._col, self._value = row, col, value
+
+    def row(self):
+        return self._row
+
+    def col(self):
+        return self._col
+
+    def value(self):
+        return self._value
+
+
+class SparseTensor:
+    """The slice of torch_sparse.SparseTensor that spherenet_layer.py:xyz_to_dat uses: COO
+    entries kept sorted row-major (by row * n_cols + col), row selection by an index vector
+    (the result's row r holds the entries of row index[r]), set_value(None) and sum(dim=1)
+    (entries per row)."""
+
+    def __init__(self, row, col, value=None, sparse_sizes=None, _sorted=False):
+        self.sizes = tuple(sparse_sizes) if sparse_sizes is not None else (
+            int(row.max()) + 1, int(col.max()) + 1)
+        if not _sorted:
+            perm = torch.argsort(row * self.sizes[1] + col, stable=True)
+            row, col = row[perm], col[perm]
+            value = value[perm] if value is not None else None
+        self.storage = _SparseStorage(row, col, value)
+
+    def set_value(self, value, layout=None):
+        s = self.storage
+        return SparseTensor(s.row(), s.col(), value, self.sizes, _sorted=True)
+
+    def sum(self, dim):
+        assert dim == 1
+        s = self.storage
+        v = s.value() if s.value() is not None else torch.ones(s.row().numel())
+        return torch.zeros(self.sizes[0], dtype=v.dtype).index_add_(0, s.row(), v)
+
+    def __getitem__(self, index):
+        s = self.storage
+        counts = torch.bincount(s.row(), minlength=self.sizes[0])
+        rowptr = torch.zeros(self.sizes[0] + 1, dtype=torch.long)
+        rowptr[1:] = torch.cumsum(counts, 0)
+        sel = [torch.arange(int(rowptr[r]), int(rowptr[r + 1])) for r in index.tolist()]
+        pos = torch.cat(sel) if sel else torch.zeros(0, dtype=torch.long)
+        new_row = torch.repeat_interleave(torch.arange(index.numel()), counts[index])
+        val = s.value()[pos] if s.value() is not None else None
+        return SparseTensor(new_row, s.col()[pos], val, (index.numel(), self.sizes[1]),
+                            _sorted=True)
 
 
 # ----------------------------------------------------------------------------- PyG
@@ -165,6 +233,12 @@ def install():
     ts.scatter_sum = scatter_sum
     ts.scatter_add = scatter_sum
     ts.scatter_mean = scatter_mean
+    ts.scatter_min = scatter_min
+    tsp = types.ModuleType("torch_sparse")
+    tsp.SparseTensor = SparseTensor
+    inits = types.ModuleType("torch_geometric.nn.inits")
+    inits.glorot_orthogonal = lambda *a, **k: None
+    tgnn.inits = inits
 
     e3 = types.ModuleType("e3nn")
     util = types.ModuleType("e3nn.util")
@@ -190,7 +264,8 @@ def install():
     for name, mod in {
         "torch_geometric": tg, "torch_geometric.nn": tgnn, "torch_scatter": ts, "e3nn": e3,
         "e3nn.util": util, "e3nn.util.jit": jit, "e3nn.util.codegen": codegen, "e3nn.o3": o3,
-        "e3nn.nn": enn, "opt_einsum": oe,
+        "e3nn.nn": enn, "opt_einsum": oe, "torch_sparse": tsp,
+        "torch_geometric.nn.inits": inits,
     }.items():
         sys.modules[name] = mod
 
@@ -216,6 +291,7 @@ def load_reference(ref_root):
         ("models.layers.gvp_layer", "models/layers/gvp_layer.py"),
         ("models.mace_modules.blocks", "models/mace_modules/blocks.py"),
         ("models.gvpgnn", "models/gvpgnn.py"),
+        ("models.layers.spherenet_layer", "models/layers/spherenet_layer.py"),
     ]:
         spec = importlib.util.spec_from_file_location(name, os.path.join(ref_root, rel))
         mod = importlib.util.module_from_spec(spec)

@@ -12,6 +12,7 @@ Modules exercised (all pure-torch arithmetic in the reference):
   models/mace_modules/blocks.py RadialEmbeddingBlock (84-96)
   models/layers/gvp_layer.py    GVP / GVPConv / GVPConvLayer (101-438)
   models/gvpgnn.py              GVPGNNModel (103-127)
+  models/layers/spherenet_layer.py xyz_to_dat (496-564)   [`python make_golden.py triplets`]
 """
 import os
 import sys
@@ -96,8 +97,45 @@ def create_kchains(k):
     return graphs
 
 
-def main():
+def make_triplets(mods):
+    """Reference xyz_to_dat (spherenet_layer.py:496-564) with and without torsion on seeded
+    random radius graphs (one with self loops), a batched pair and the k-chains."""
+    import warnings
+    sp = mods["models.layers.spherenet_layer"]
+    d = {}
+    cases = []
+    for seed, n, box, r in [(30, 40, 4.0, 1.6), (31, 64, 5.0, 1.8), (32, 25, 3.0, 1.5)]:
+        cases.append(make_graph(seed, n, box, r))
+    p, e, _ = batch_graphs([make_graph(33, 30, 4.0, 1.7), make_graph(34, 22, 3.5, 1.7)])
+    cases.append((p, e))
+    p, e, _ = batch_graphs(create_kchains(4))
+    cases.append((p.float(), e))
+    # self loops (dist 0: NaN torsion candidates, which torch_scatter's min never takes)
+    p, e = make_graph(35, 20, 3.0, 1.6)
+    loops = torch.arange(0, 20, 4)
+    cases.append((p, torch.cat([e, torch.stack([loops, loops])], 1)))
+    for c, (pos, ei) in enumerate(cases):
+        n = pos.shape[0]
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            full = sp.xyz_to_dat(pos, ei, n, use_torsion=True)
+            short = sp.xyz_to_dat(pos, ei, n, use_torsion=False)
+        d[f"{c}.pos"], d[f"{c}.edge_index"] = pos, ei
+        for name, v in zip(["dist", "angle", "torsion", "i", "j", "idx_kj", "idx_ji"], full):
+            d[f"{c}.{name}"] = v
+        for name, v in zip(["dist", "angle", "i", "j", "idx_kj", "idx_ji"], short):
+            assert torch.equal(v, d[f"{c}.{name}"])
+    d["n_cases"] = torch.tensor(len(cases))
+    torch.save(d, os.path.join(HERE, "triplets.pt"))
+    return "triplets.pt"
+
+
+def main(only=None):
     mods = _ref_stubs.load_reference(REF)
+    if only == "triplets":
+        f = make_triplets(mods)
+        print(f, os.path.getsize(os.path.join(HERE, f)))
+        return
     torch.set_default_dtype(torch.float32)
     out_files = []
 
@@ -234,4 +272,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

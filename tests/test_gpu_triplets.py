@@ -1,0 +1,113 @@
+"""GPU triplets + angles / torsions (K11) against the reference's own
+xyz_to_dat outputs (tests/golden/triplets.pt) and the oracle (oracle/triplets.py).
+Indices bit-exact; dist / angle / torsion within 1e-5 (atan2 / sqrt last-ulp differences)."""
+import math
+import os
+
+import pytest
+import torch
+
+from oracle.triplets import dimenet_angles as o_dimenet, xyz_to_dat as o_xyz
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "triplets.pt")
+TOL = 1e-5
+
+
+def _close(a, b, tol=TOL):
+    a, b = a.cpu(), b.cpu()
+    assert a.shape == b.shape
+    na, nb = torch.isnan(a), torch.isnan(b)
+    assert torch.equal(na, nb)
+    assert (a[~na] - b[~nb]).abs().max().item() <= tol if a.numel() else True
+
+
+def _check(out, ref, n_float):
+    for k, (a, b) in enumerate(zip(out, ref)):
+        if k < n_float:
+            _close(a, b)
+        else:
+            assert torch.equal(a.cpu(), b.cpu()), k
+
+
+def test_xyz_to_dat_golden():
+    from gmp_amd.triplets import xyz_to_dat
+    g = torch.load(GOLD, weights_only=True)
+    names = ["dist", "angle", "torsion", "i", "j", "idx_kj", "idx_ji"]
+    for c in range(int(g["n_cases"])):
+        pos, ei = g[f"{c}.pos"], g[f"{c}.edge_index"]
+        out = xyz_to_dat(pos.to(DEV), ei.to(DEV), pos.shape[0], use_torsion=True)
+        _check(out, [g[f"{c}.{n}"] for n in names], 3)
+        # the ~0 torsions (k_n = k candidate whose rounding residual is positive) are the same set
+        t_ref = g[f"{c}.torsion"]
+        assert torch.equal(out[2].cpu() < 1e-6, t_ref < 1e-6)
+
+
+def _graph(n, box, r, seed, shuffle=True):
+    g = torch.Generator().manual_seed(seed)
+    pos = torch.rand(n, 3, generator=g) * box
+    d = torch.cdist(pos.double(), pos.double())
+    ei = torch.nonzero((d < r) & (d > 0)).T.flip(0).contiguous()
+    if shuffle:
+        ei = ei[:, torch.randperm(ei.shape[1], generator=g)]
+    return pos, ei
+
+
+@pytest.mark.parametrize("n,box,r", [(300, 6.0, 1.5), (2000, 14.0, 1.8)])
+def test_xyz_to_dat_vs_oracle(n, box, r):
+    from gmp_amd.triplets import xyz_to_dat
+    pos, ei = _graph(n, box, r, n)
+    out = xyz_to_dat(pos.to(DEV), ei.to(DEV), n, use_torsion=True)
+    _check(out, o_xyz(pos, ei, n, use_torsion=True), 3)
+    out = xyz_to_dat(pos.to(DEV), ei.to(DEV), n, use_torsion=False)
+    _check(out, o_xyz(pos, ei, n, use_torsion=False), 2)
+
+
+def test_dimenet_vs_oracle():
+    from gmp_amd.triplets import dimenet_angles, dimenet_triplets
+    pos, ei = _graph(500, 7.0, 1.6, 5)
+    out = dimenet_angles(pos.to(DEV), ei.to(DEV), 500)
+    ref = o_dimenet(pos, ei, 500)
+    _check(out, ref, 2)
+    tri = dimenet_triplets(ei.to(DEV), 500)
+    for a, b in zip(tri, ref[2:]):
+        assert torch.equal(a.cpu(), b)
+
+
+def test_edge_cases():
+    from gmp_amd.triplets import xyz_to_dat
+    pos = torch.randn(4, 3)
+    # no edges
+    out = xyz_to_dat(pos.to(DEV), torch.zeros(2, 0, dtype=torch.long, device=DEV), 4, True)
+    assert out[1].numel() == 0 and out[2].numel() == 0
+    # one undirected edge: two directed edges, no triplets (k == i always)
+    ei = torch.tensor([[0, 1], [1, 0]])
+    out = xyz_to_dat(pos.to(DEV), ei.to(DEV), 4, True)
+    ref = o_xyz(pos, ei, 4, True)
+    _check(out, ref, 3)
+    assert out[1].numel() == 0
+    with pytest.raises(NotImplementedError):
+        xyz_to_dat(pos.to(DEV).requires_grad_(True), ei.to(DEV), 4)
+
+
+def test_benchmark_size_properties():
+    """50k nodes / ~1M edges: structural invariants + an fp64 spot check of angles."""
+    from gmp_amd.graph import radius_graph
+    from gmp_amd.triplets import xyz_to_dat
+    gr = radius_graph(num_nodes=50_000, target_edges=1_000_000)
+    pos, ei = gr.pos.to(DEV), gr.edge_index.to(DEV)
+    dist, angle, torsion, i, j, idx_kj, idx_ji = xyz_to_dat(pos, ei, 50_000, use_torsion=True)
+    deg = torch.bincount(ei[1], minlength=50_000)
+    assert idx_kj.numel() == int((deg[ei[0]] - 1).sum())  # symmetric simple graph
+    assert bool((idx_ji[1:] >= idx_ji[:-1]).all())
+    assert torch.equal(ei[1][idx_kj], ei[0][idx_ji])  # kj ends at j
+    assert not bool((ei[0][idx_kj] == ei[1][idx_ji]).any())  # k != i
+    assert float(angle.min()) >= 0 and float(angle.max()) <= math.pi + 1e-6
+    assert float(torsion.min()) >= 0 and float(torsion.max()) <= 2 * math.pi + 1e-6
+    sel = torch.randint(0, angle.numel(), (4096,), device=DEV)
+    p = pos.double()
+    u = p[ei[1][idx_ji[sel]]] - p[ei[0][idx_ji[sel]]]
+    v = p[ei[0][idx_kj[sel]]] - p[ei[0][idx_ji[sel]]]
+    a64 = torch.atan2(torch.linalg.cross(u, v).norm(dim=-1), (u * v).sum(-1))
+    assert (angle[sel].double() - a64).abs().max().item() < 1e-5
