@@ -146,12 +146,35 @@ __device__ __forceinline__ void gemm_wtx(const float* __restrict__ sW, const f32
   }
 }
 
-// ---------------------------------------------------------------------------------- LayerNorm
-__device__ __forceinline__ float sum_groups(float v) {  // sum over the 4 lane groups of an edge
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+// ---------------------------------------------------------------------------------- cross-lane
+// All in-wave exchanges are VALU (DPP, permlane swaps), never ds_bpermute: the LDS pipe stays
+// free for the W operand reads.
+// DPP within a 16-lane row; lanes without a source get 0
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+// the partner of lane i (within its 16-lane row) at reduce-scatter level M: i^8 (row_ror:8),
+// i^7 (row_half_mirror: flips bit 2 like i^4), i^2, i^1 (quad_perm)
+template <int M>
+__device__ __forceinline__ float rs_partner(float v) {
+  if constexpr (M == 8) return dpp<0x128>(v);
+  else if constexpr (M == 4) return dpp<0x141>(v);
+  else if constexpr (M == 2) return dpp<0x4E>(v);
+  else return dpp<0xB1>(v);
+}
+// sum over the 4 lane groups of an edge (lanes l, l^16, l^32, l^48): permlane16/32 swaps of
+// v with itself return {v, partner} in some order, so r[0] + r[1] = v + partner
+__device__ __forceinline__ float sum_groups(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// ---------------------------------------------------------------------------------- LayerNorm
 
 // in place: x <- (x - mean) * rstd  (x_hat); returns rstd.  Two-pass statistics.
 template <int D>
@@ -206,22 +229,26 @@ __device__ __forceinline__ void affine_act(f32x4 (&x)[D / 16], const float* sV, 
 // ---------------------------------------------------------------------------------- segments
 // inclusive segmented scan over the 16 edge lanes of each group; `head` = first lane of this
 // lane's segment inside the chunk.
+template <int OFF, int T>
+__device__ __forceinline__ void seg_scan_level(f32x4 (&x)[T], int i, int head) {
+  const bool take = (i - OFF) >= head;
+#pragma unroll
+  for (int p = 0; p < T; ++p)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float u = dpp<0x110 + OFF>(x[p][c]);  // row_shr:OFF = lane i - OFF
+      if (take) x[p][c] += u;
+    }
+}
 template <int T>
 __device__ __forceinline__ void seg_scan(f32x4 (&x)[T], int i, int head) {
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) {
-    const bool take = (i - off) >= head;
-#pragma unroll
-    for (int p = 0; p < T; ++p)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float u = __shfl_up(x[p][c], off, 16);
-        if (take) x[p][c] += u;
-      }
-  }
+  seg_scan_level<1>(x, i, head);
+  seg_scan_level<2>(x, i, head);
+  seg_scan_level<4>(x, i, head);
+  seg_scan_level<8>(x, i, head);
 }
 
-// Reduce-scatter over the 16 edge lanes (levels xor M = 8, 4, 2, 1).
+// Reduce-scatter over the 16 edge lanes (levels M = 8, 4, 2, 1; partners rs_partner<M>).
 template <int N, int M, int N0>
 struct RS {
   __device__ __forceinline__ static void run(float (&x)[N0], int i) {
@@ -233,11 +260,11 @@ struct RS {
 #pragma unroll
       for (int k = 0; k < H; ++k) {
         const float lo = x[k], hi = x[k + H];
-        x[k] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, M, 16);
+        x[k] = (up ? hi : lo) + rs_partner<M>(up ? lo : hi);
       }
       RS<H, M / 2, N0>::run(x, i);
     } else {
-      x[0] += __shfl_xor(x[0], M, 16);
+      x[0] += rs_partner<M>(x[0]);
       RS<1, M / 2, N0>::run(x, i);
     }
   }
@@ -272,7 +299,7 @@ __device__ __forceinline__ void accumulate_vec(F f, float (&acc)[VecAcc<D>::K], 
 #pragma unroll
   for (int k = 0; k < H; ++k) {
     const float lo = f(k), hi = f(k + H);
-    t[k] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 8, 16);
+    t[k] = (up ? hi : lo) + rs_partner<8>(up ? lo : hi);
   }
   RS<H, 4, H>::run(t, i);
 #pragma unroll
