@@ -119,11 +119,13 @@ def tp_node_flops(model, n_nodes, n_edges):
     return total
 
 
-def egnn_bwd_bytes_per_edge(d):
-    """Minimum HBM bytes per edge of the fused EGNN edge backward (DESIGN.md): indices 16,
-    sender/receiver node rows of dA/AB 2 x 2d x 4 (gathered), pos 24, recomputed nothing else
-    read; per-edge activations written for the weight-gradient outer sums 5 x d x 4."""
-    return 16 + 2 * 2 * d * 4 + 24 + 5 * d * 4
+def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges):
+    """Minimum HBM bytes per edge of the fused EGNN edge backward (DESIGN.md §K4): indices 16,
+    pos 24, the forward's saved x_hat1..3 (3 x d x 4) and rstd (12) read, dpre1..3 (3 x d x 4)
+    and gdiff (12) written; per-node rows (g_m_aggr + g_pos_aggr read, dA + dpos_recv
+    written) once per node, amortised over the edges."""
+    per_node = 2 * (d * 4 + 12)
+    return 16 + 24 + 3 * d * 4 + 12 + 3 * d * 4 + 12 + per_node * n_nodes / n_edges
 
 
 def gvp_flops_per_edge(s, v, se, ve):
@@ -138,7 +140,7 @@ def gvp_flops_per_edge(s, v, se, ve):
 def egnn_flops_per_edge(d):
     """Algorithmic fp32 FLOPs per edge of the two fused edge kernels."""
     gemm = 2 * d * d
-    return {"egnn_edge_fwd": 2 * gemm, "egnn_edge_bwd": 4 * gemm}
+    return {"egnn_edge_fwd": 2 * gemm, "egnn_edge_bwd": 2 * gemm}  # bwd: W3^T, W2^T
 
 
 def cpu_baseline(g, args):
@@ -252,13 +254,21 @@ def main():
         if args.workload == "egnn":
             fl = egnn_flops_per_edge(args.emb)
             ms_fwd, ms_bwd = timers["egnn_edge_fwd"], timers["egnn_edge_bwd"]
-            achieved = fl["egnn_edge_bwd"] * g.num_edges / (ms_bwd * 1e-3) / 1e12
-            roof = {"kernel": "egnn_edge_bwd", "bound": "mfma",
-                    "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+            tflops = fl["egnn_edge_bwd"] * g.num_edges / (ms_bwd * 1e-3) / 1e12
+            bpe = egnn_bwd_bytes_per_edge(args.emb, g.num_nodes, g.num_edges)
+            gbs = bpe * g.num_edges / (ms_bwd * 1e-3) / 1e9
+            f_mfma, f_hbm = tflops / FP32_MFMA_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
+            # both bounds are reported; the primary one is the closer of the two
+            if f_mfma >= f_hbm:
+                prim = {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": f_mfma}
+            else:
+                prim = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": f_hbm}
+            roof = {"kernel": "egnn_edge_bwd", **prim,
                     "traffic": None, "ms_per_launch": ms_bwd,
-                    "flops_per_edge": fl["egnn_edge_bwd"],
-                    "bytes_per_edge_min": egnn_bwd_bytes_per_edge(args.emb),
+                    "flops_per_edge": fl["egnn_edge_bwd"], "mfma_frac": f_mfma,
+                    "bytes_per_edge_min": bpe, "hbm_gbs": gbs, "hbm_frac": f_hbm,
                     "fwd_kernel_ms": ms_fwd,
                     "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
                     / (ms_fwd * 1e-3) / 1e12}

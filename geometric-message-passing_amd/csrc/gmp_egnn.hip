@@ -102,6 +102,13 @@ __device__ __forceinline__ void store_row(float* __restrict__ row, const f32x4 (
 #pragma unroll
   for (int p = 0; p < D / 16; ++p) *reinterpret_cast<f32x4*>(row + 16 * p + 4 * g) = x[p];
 }
+// streaming store (per-edge tensors consumed by later kernels: keep them out of L2)
+template <int D>
+__device__ __forceinline__ void stream_row(float* __restrict__ row, const f32x4 (&x)[D / 16], int g) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p)
+    __builtin_nontemporal_store(x[p], reinterpret_cast<f32x4*>(row + 16 * p + 4 * g));
+}
 
 // ---------------------------------------------------------------------------------- MFMA GEMMs
 // GMP_GEMM_FENCE bounds how far the scheduler may hoist LDS operand reads (register pressure).
@@ -408,12 +415,15 @@ __device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowp
 }
 
 // ================================================================================== forward
-template <int D, int ACT, bool MSG_MEAN>
+// SAVE (training): also write the three LayerNorm outputs x_hat1..3 (xsave, (3, E, d), rows in
+// receiver-sorted edge order) and their 1/std (rsave, (E, 3)) for the backward.
+template <int D, int ACT, bool MSG_MEAN, bool SAVE>
 __global__ __launch_bounds__(kThreads, 2) void egnn_fwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ AB, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
     const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
-    float* __restrict__ m_aggr, float* __restrict__ pos_aggr) {
+    float* __restrict__ m_aggr, float* __restrict__ pos_aggr, float* __restrict__ xsave,
+    float* __restrict__ rsave) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2 = smem;
@@ -433,21 +443,32 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_fwd_kernel(
     asm volatile("" ::: "memory");  // keep LDS parameter reads inside the loop
     const EdgeCtx c = edge_ctx(base, li, wr.e_hi, (int)n_nodes, recv, send, rowptr, pos);
 
+    const size_t ED = (size_t)n_edges * D;
     f32x4 x[T];  // y1 = act(LN1(pre1))
     load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c.dist, g);
-    ln_normalize<D>(x, eps);
+    const float r1 = ln_normalize<D>(x, eps);
+    if (SAVE && c.valid) stream_row<D>(rowp(xsave, c.e, D), x, g);
     affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
 
     f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
     load_vec<D>(m, sV, V_B2, g);
     gemm_wx<D>(sW2, x, m, li, g);
-    ln_normalize<D>(m, eps);
+    const float r2 = ln_normalize<D>(m, eps);
+    if (SAVE && c.valid) stream_row<D>(rowp(xsave + ED, c.e, D), m, g);
     affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);
 
     // y3 = act(LN3(W3 m + b3)); s = w4 . y3 + b4   (x reused)
     load_vec<D>(x, sV, V_B3, g);
     gemm_wx<D>(sW3, m, x, li, g);
-    ln_normalize<D>(x, eps);
+    const float r3 = ln_normalize<D>(x, eps);
+    if (SAVE && c.valid) {
+      stream_row<D>(rowp(xsave + 2 * ED, c.e, D), x, g);
+      if (g == 0) {
+        rsave[3 * (size_t)c.e + 0] = r1;
+        rsave[3 * (size_t)c.e + 1] = r2;
+        rsave[3 * (size_t)c.e + 2] = r3;
+      }
+    }
     affine_act<D, ACT>(x, sV, V_LN3W, V_LN3B, g);
     float sp = 0.f;
 #pragma unroll
@@ -498,15 +519,17 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
   return sV[v * D + featq(s, g)];
 }
 
+// Backward from the forward's saved x_hat1..3 / rstd (no forward recompute, no AB gathers):
+// two transposed GEMMs (W3^T, W2^T) per 16-edge chunk.
 template <int D, int ACT, bool MSG_MEAN>
 __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
-    int64_t n_nodes, int64_t n_edges, const float* __restrict__ AB, const float* __restrict__ pos,
+    int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
-    const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
+    const int64_t* __restrict__ send, gmp_egnn_params P, int64_t n_waves,
+    const float* __restrict__ xsave, const float* __restrict__ rsave,
     const float* __restrict__ g_maggr, const float* __restrict__ g_paggr, float* __restrict__ dA,
     float* __restrict__ dpos_recv, float* __restrict__ dpre1_out, float* __restrict__ gdiff_out,
-    float* __restrict__ y1_out, float* __restrict__ m_out, float* __restrict__ dpre2_out,
-    float* __restrict__ dpre3_out, float* __restrict__ partials) {
+    float* __restrict__ dpre2_out, float* __restrict__ dpre3_out, float* __restrict__ partials) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW, K = VecAcc<D>::K;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2 = smem;
@@ -520,6 +543,7 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
   float* cbuf = smem + smem_params_floats<D>() + (wid * 4 + g) * carry_stride<D>();
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid);
   const float b4 = P.b4[0];
+  const size_t ED = (size_t)n_edges * D;
 
   float vacc[NVG][K];
 #pragma unroll
@@ -532,34 +556,18 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
   for (int base = wr.e_lo; base < wr.e_hi; base += 16) {
     asm volatile("" ::: "memory");
     const EdgeCtx c = edge_ctx(base, li, wr.e_hi, (int)n_nodes, recv, send, rowptr, pos);
-    const float* arow = rowp(AB, c.i, 2 * D);
-    const float* brow = rowp(AB, c.j, 2 * D) + D;
-
-    // ---------------- recompute y1 (x), xhat2 (xh2), m (x), xhat3 (z)
-    f32x4 x[T];
-    load_pre1<D>(x, arow, brow, sV, c.dist, g);
-    const float rstd1 = ln_normalize<D>(x, eps);
-    affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
-    if (c.valid) store_row<D>(rowp(y1_out, c.e, D), x, g);
-
-    f32x4 xh2[T];
-    load_vec<D>(xh2, sV, V_B2, g);
-    gemm_wx<D>(sW2, x, xh2, li, g);
-    const float rstd2 = ln_normalize<D>(xh2, eps);
+    const float rstd1 = c.valid ? rsave[3 * (size_t)c.e + 0] : 0.f;
+    const float rstd2 = c.valid ? rsave[3 * (size_t)c.e + 1] : 0.f;
+    const float rstd3 = c.valid ? rsave[3 * (size_t)c.e + 2] : 0.f;
+    f32x4 x[T], xh2[T], z[T];
+    if (c.valid) {
+      load_row<D>(z, rowp(xsave + 2 * ED, c.e, D), g);  // z = xhat3
+    } else {
 #pragma unroll
-    for (int p = 0; p < T; ++p) {
-      const f32x4 w = vec4<D>(sV, V_LN2W, p, g), b = vec4<D>(sV, V_LN2B, p, g);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[p][q] = act_f<ACT>(xh2[p][q] * w[q] + b[q]);
+      for (int p = 0; p < T; ++p) z[p] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if (c.valid) store_row<D>(rowp(m_out, c.e, D), x, g);
 
-    f32x4 z[T];
-    load_vec<D>(z, sV, V_B3, g);
-    gemm_wx<D>(sW3, x, z, li, g);
-    const float rstd3 = ln_normalize<D>(z, eps);  // z = xhat3
-
-    // ---------------- pos-branch backward
+  // ---------------- pos-branch backward
     const float inv_deg = c.valid ? 1.f / (float)(c.seg1 - c.seg0) : 0.f;
     const float gpx = c.valid ? g_paggr[3 * c.i + 0] * inv_deg : 0.f;
     const float gpy = c.valid ? g_paggr[3 * c.i + 1] * inv_deg : 0.f;
@@ -588,7 +596,7 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN3W, p, g);
     ln_backward<D>(x, z, rstd3);  // x = dpre3
-    if (c.valid) store_row<D>(rowp(dpre3_out, c.e, D), x, g);
+    if (c.valid) stream_row<D>(rowp(dpre3_out, c.e, D), x, g);
 
     // ---------------- dm = g_m_aggr[i] (/deg) + W3^T dpre3   (z)
     if (c.valid) {
@@ -602,6 +610,12 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
       for (int p = 0; p < T; ++p) z[p] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     gemm_wtx<D>(sW3, x, z, li, g);
+    if (c.valid) {
+      load_row<D>(xh2, rowp(xsave + ED, c.e, D), g);
+    } else {
+#pragma unroll
+      for (int p = 0; p < T; ++p) xh2[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN2W, p, g), b = vec4<D>(sV, V_LN2B, p, g);
@@ -613,14 +627,18 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) z[p] *= vec4<D>(sV, V_LN2W, p, g);
     ln_backward<D>(z, xh2, rstd2);  // z = dpre2
-    if (c.valid) store_row<D>(rowp(dpre2_out, c.e, D), z, g);
+    if (c.valid) stream_row<D>(rowp(dpre2_out, c.e, D), z, g);
 
     // ---------------- dy1 = W2^T dpre2 (x); xhat1 recomputed into xh2
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
     gemm_wtx<D>(sW2, z, x, li, g);
-    load_pre1<D>(xh2, arow, brow, sV, c.dist, g);
-    ln_normalize<D>(xh2, eps);
+    if (c.valid) {  // xh2 <- xhat1
+      load_row<D>(xh2, rowp(xsave, c.e, D), g);
+    } else {
+#pragma unroll
+      for (int p = 0; p < T; ++p) xh2[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN1W, p, g), b = vec4<D>(sV, V_LN1B, p, g);
@@ -632,7 +650,7 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN1W, p, g);
     ln_backward<D>(x, xh2, rstd1);  // x = dpre1
-    if (c.valid) store_row<D>(rowp(dpre1_out, c.e, D), x, g);
+    if (c.valid) stream_row<D>(rowp(dpre1_out, c.e, D), x, g);
 
     // dw1d += dpre1 * dist ; d(dist) = w1d . dpre1
     float dd = 0.f;
@@ -717,31 +735,31 @@ int prep_kernel(K k, size_t smem) {
 template <int D, int ACT, bool MEAN>
 int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const int64_t* rowptr,
                const int64_t* recv, const int64_t* send, const gmp_egnn_params& P, float eps,
-               float* m_aggr, float* pos_aggr, hipStream_t s) {
+               float* m_aggr, float* pos_aggr, float* xsave, float* rsave, hipStream_t s) {
   const int64_t W = n_waves_for(E);
   const size_t smem = smem_total<D>();
-  auto k = egnn_fwd_kernel<D, ACT, MEAN>;
+  auto k = xsave ? egnn_fwd_kernel<D, ACT, MEAN, true> : egnn_fwd_kernel<D, ACT, MEAN, false>;
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / kWavesPerBlock), kThreads, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
-                                                           eps, W, m_aggr, pos_aggr);
+                                                           eps, W, m_aggr, pos_aggr, xsave, rsave);
   return launch_status();
 }
 
 template <int D, int ACT, bool MEAN>
-int launch_bwd(int64_t N, int64_t E, const float* AB, const float* pos, const int64_t* rowptr,
-               const int64_t* recv, const int64_t* send, const gmp_egnn_params& P, float eps,
-               const float* gm, const float* gp, float* dA, float* dpos_recv, float* dpre1,
-               float* gdiff, float* y1, float* m, float* dpre2, float* dpre3, float* partials,
-               hipStream_t s) {
+int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
+               const int64_t* recv, const int64_t* send, const gmp_egnn_params& P,
+               const float* xsave, const float* rsave, const float* gm, const float* gp,
+               float* dA, float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
+               float* dpre3, float* partials, hipStream_t s) {
   const int64_t W = n_waves_for(E);
   const size_t smem = smem_total<D>();
   auto k = egnn_bwd_kernel<D, ACT, MEAN>;
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
-  k<<<(unsigned)(W / kWavesPerBlock), kThreads, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
-                                                           eps, W, gm, gp, dA, dpos_recv, dpre1,
-                                                           gdiff, y1, m, dpre2, dpre3, partials);
+  k<<<(unsigned)(W / kWavesPerBlock), kThreads, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
+                                                           xsave, rsave, gm, gp, dA, dpos_recv,
+                                                           dpre1, gdiff, dpre2, dpre3, partials);
   return launch_status();
 }
 
@@ -777,7 +795,7 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
                           const float* pos, const int64_t* rowptr, const int64_t* recv,
                           const int64_t* send, const gmp_egnn_params* params, int act,
                           int msg_mean, float ln_eps, float* m_aggr, float* pos_aggr,
-                          void* stream) {
+                          float* save_xhat, float* save_rstd, void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
   GMP_CHECK_ARG(params_ok(params) && m_aggr && pos_aggr && rowptr);
@@ -788,9 +806,11 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
   if (rc || n_edges == 0) return rc;
   GMP_CHECK_ARG(AB && pos && recv && send && aligned16(AB) && aligned16(m_aggr));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
+  GMP_CHECK_ARG((save_xhat == nullptr) == (save_rstd == nullptr));
+  GMP_CHECK_ARG(save_xhat == nullptr || aligned16(save_xhat));
 #define GMP_CALL_FWD(DD, AA, MM)                                                              \
   rc = launch_fwd<DD, AA, MM>(n_nodes, n_edges, AB, pos, rowptr, recv, send, *params, ln_eps, \
-                              m_aggr, pos_aggr, s)
+                              m_aggr, pos_aggr, save_xhat, save_rstd, s)
   GMP_EGNN_DISPATCH(GMP_CALL_FWD);
 #undef GMP_CALL_FWD
   return rc;
@@ -801,13 +821,13 @@ int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d) {
   return n_waves_for(n_edges) / kWavesPerBlock;
 }
 
-int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
-                          const float* pos, const int64_t* rowptr, const int64_t* recv,
-                          const int64_t* send, const gmp_egnn_params* params, int act,
-                          int msg_mean, float ln_eps, const float* g_m_aggr,
+int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                          const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                          const gmp_egnn_params* params, int act, int msg_mean,
+                          const float* save_xhat, const float* save_rstd, const float* g_m_aggr,
                           const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
-                          float* gdiff, float* y1, float* m, float* dpre2, float* dpre3,
-                          float* vec_partials, void* stream) {
+                          float* gdiff, float* dpre2, float* dpre3, float* vec_partials,
+                          void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
   GMP_CHECK_ARG(params_ok(params) && dA && dpos_recv && rowptr && vec_partials);
@@ -823,15 +843,15 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
         vec_partials, 0,
         gmp_egnn_edge_bwd_partials_rows(n_edges, d) * (8 * d + 1) * sizeof(float), s));
   }
-  GMP_CHECK_ARG(AB && pos && recv && send && g_m_aggr && g_pos_aggr && dpre1 && gdiff && y1 &&
-                m && dpre2 && dpre3);
-  GMP_CHECK_ARG(aligned16(AB) && aligned16(dA) && aligned16(g_m_aggr) && aligned16(dpre1) &&
-                aligned16(y1) && aligned16(m) && aligned16(dpre2) && aligned16(dpre3));
+  GMP_CHECK_ARG(pos && recv && send && save_xhat && save_rstd && g_m_aggr && g_pos_aggr &&
+                dpre1 && gdiff && dpre2 && dpre3);
+  GMP_CHECK_ARG(aligned16(save_xhat) && aligned16(dA) && aligned16(g_m_aggr) &&
+                aligned16(dpre1) && aligned16(dpre2) && aligned16(dpre3));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
 #define GMP_CALL_BWD(DD, AA, MM)                                                              \
-  rc = launch_bwd<DD, AA, MM>(n_nodes, n_edges, AB, pos, rowptr, recv, send, *params, ln_eps, \
-                              g_m_aggr, g_pos_aggr, dA, dpos_recv, dpre1, gdiff, y1, m, dpre2,  \
-                              dpre3, vec_partials, s)
+  rc = launch_bwd<DD, AA, MM>(n_nodes, n_edges, pos, rowptr, recv, send, *params, save_xhat,  \
+                              save_rstd, g_m_aggr, g_pos_aggr, dA, dpos_recv, dpre1, gdiff,    \
+                              dpre2, dpre3, vec_partials, s)
   GMP_EGNN_DISPATCH(GMP_CALL_BWD);
 #undef GMP_CALL_BWD
   return rc;

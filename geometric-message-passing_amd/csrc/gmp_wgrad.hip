@@ -20,12 +20,31 @@ struct WCfg {
   static constexpr int TW = D / 32;  // 16x16 tiles per wave per dim (wave owns a D/2 x D/2 block)
 };
 
-// One workgroup: edges [k0, k1) -> partial[blockIdx] = A^T B (D x D) and colsum(A) (D).
-template <int D>
+// B-operand prologue: PRO = 0: B as stored; 1: relu(B*w + b); 2: silu(B*w + b) (per column
+// w, b) — the EGNN activations y1 / m rebuilt from the saved LayerNorm outputs at load time.
+template <int PRO>
+__device__ __forceinline__ f32x4 prologue(f32x4 v, f32x4 w, f32x4 b) {
+  if constexpr (PRO == 0) {
+    return v;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float z = v[c] * w[c] + b[c];
+      if constexpr (PRO == 1) v[c] = z > 0.f ? z : 0.f;
+      else v[c] = z * (1.f / (1.f + __expf(-z)));
+    }
+    return v;
+  }
+}
+
+// One workgroup: edges [k0, k1) -> partial[blockIdx] = A^T pro(B) (D x D) and colsum(A) (D).
+template <int D, int PRO>
 __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restrict__ A,
                                                           const float* __restrict__ B, int64_t K,
                                                           int64_t k_per_block,
-                                                          float* __restrict__ partial) {
+                                                          float* __restrict__ partial,
+                                                          const float* __restrict__ bw,
+                                                          const float* __restrict__ bb) {
   constexpr int TW = WCfg<D>::TW;
   constexpr int LD = D + 16;
   __shared__ __attribute__((aligned(16))) float sA[2][kKT * LD];
@@ -52,6 +71,11 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
 
   constexpr int NL = kKT / RS;  // float4 loads per thread per tile, per operand
   f32x4 ra[NL], rb[NL];
+  f32x4 pw = {0.f, 0.f, 0.f, 0.f}, pb = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (PRO != 0) {
+    pw = *reinterpret_cast<const f32x4*>(bw + 4 * c4);
+    pb = *reinterpret_cast<const f32x4*>(bb + 4 * c4);
+  }
   auto fetch = [&](int64_t kb) {  // global -> registers
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
@@ -60,7 +84,7 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
       rb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < k1) {
         ra[j] = *reinterpret_cast<const f32x4*>(A + k * D + 4 * c4);
-        rb[j] = *reinterpret_cast<const f32x4*>(B + k * D + 4 * c4);
+        rb[j] = prologue<PRO>(*reinterpret_cast<const f32x4*>(B + k * D + 4 * c4), pw, pb);
       }
     }
   };
@@ -297,11 +321,11 @@ size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d) {
   return (size_t)(G + ceil_div(G, kGC)) * (size_t)(d * d + d) * sizeof(float);
 }
 
-int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
-                           float* colsum_A, void* workspace, size_t workspace_bytes,
-                           void* stream) {
+static int outer_sum_launch(int64_t K, int64_t d, const float* A, const float* B, int pro,
+                            const float* bw, const float* bb, float* C, float* colsum_A,
+                            void* workspace, size_t workspace_bytes, void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
-  GMP_CHECK_ARG(K >= 0 && C);
+  GMP_CHECK_ARG(K >= 0 && C && pro >= 0 && pro <= 2 && (pro == 0 || (bw && bb)));
   hipStream_t s = as_stream(stream);
   if (K == 0) {
     int rc = hip_check(hipMemsetAsync(C, 0, d * d * sizeof(float), s));
@@ -310,14 +334,23 @@ int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B,
   }
   GMP_CHECK_ARG(A && B && workspace);
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0);
+  GMP_CHECK_ARG(pro == 0 || (reinterpret_cast<uintptr_t>(bw) % 16 == 0 &&
+                             reinterpret_cast<uintptr_t>(bb) % 16 == 0));
   if (workspace_bytes < gmp_edge_outer_sum_workspace_size(K, d)) return GMP_ERR_WORKSPACE;
   const int64_t G = blocks_for(K);
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-  if (d == 128) outer_sum_kernel<128><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part);
-  else if (d == 64) outer_sum_kernel<64><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part);
-  else outer_sum_kernel<32><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part);
+#define GMP_OS(DD, PP) outer_sum_kernel<DD, PP><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part, bw, bb)
+#define GMP_OS_D(PP)                 \
+  if (d == 128) GMP_OS(128, PP);     \
+  else if (d == 64) GMP_OS(64, PP);  \
+  else GMP_OS(32, PP)
+  if (pro == 0) { GMP_OS_D(0); }
+  else if (pro == 1) { GMP_OS_D(1); }
+  else { GMP_OS_D(2); }
+#undef GMP_OS_D
+#undef GMP_OS
   int rc = launch_status();
   if (rc) return rc;
   const int64_t X = d * d + d;
@@ -328,6 +361,22 @@ int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B,
   if (rc) return rc;
   sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, d * d);
   return launch_status();
+}
+
+int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
+                           float* colsum_A, void* workspace, size_t workspace_bytes,
+                           void* stream) {
+  return outer_sum_launch(K, d, A, B, 0, nullptr, nullptr, C, colsum_A, workspace,
+                          workspace_bytes, stream);
+}
+
+int gmp_edge_outer_sum_act_f32(int64_t K, int64_t d, const float* A, const float* X,
+                               const float* w, const float* b, int act, float* C,
+                               float* colsum_A, void* workspace, size_t workspace_bytes,
+                               void* stream) {
+  if (!(act == 0 || act == 1)) return GMP_ERR_ARG;
+  return outer_sum_launch(K, d, A, X, act + 1, w, b, C, colsum_A, workspace, workspace_bytes,
+                          stream);
 }
 
 int64_t rect_blocks_for(int64_t K) {

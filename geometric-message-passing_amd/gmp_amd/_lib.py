@@ -61,10 +61,12 @@ SIGNATURES = {
                                            c_vp, c_vp]),
     "gmp_egnn_edge_fwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
-                                      c_vp, c_vp]),
+                                      c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
     "gmp_edge_outer_sum_workspace_size": (c_size, [c_i64, c_i64]),
     "gmp_edge_outer_sum_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "gmp_edge_outer_sum_act_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
+                                           c_vp, c_vp, c_size, c_vp]),
     "gmp_edge_featurize_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32, c_vp,
                                        c_vp, c_vp, c_vp, c_vp]),
     "gmp_edge_featurize_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32,
@@ -101,10 +103,8 @@ SIGNATURES = {
                                                   c_vp, c_vp]),
     "gmp_symmetric_contraction_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp, c_vp, c_vp]),
-    "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                      ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
-                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                      c_vp]),
+    "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                      ctypes.POINTER(GmpEgnnParams), c_int, c_int] + [c_vp] * 12),
 }
 
 _lib = None

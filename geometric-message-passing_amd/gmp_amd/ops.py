@@ -189,6 +189,24 @@ def edge_outer_sum(A, B, with_colsum=True):
     return C, cs
 
 
+def edge_outer_sum_act(A, X, w, b, act):
+    """(A^T act(X * w + b), colsum(A)) with the activation applied at load time
+    (gmp_edge_outer_sum_act_f32): the EGNN y1 / m weight-gradient operands from x_hat."""
+    lib = _lib.load()
+    A, X, w, b = _f32c(A), _f32c(X), _f32c(w), _f32c(b)
+    _need_cuda(A, X, w, b)
+    K, d = A.shape
+    C = torch.empty((d, d), dtype=torch.float32, device=A.device)
+    cs = torch.empty(d, dtype=torch.float32, device=A.device)
+    ws_bytes = lib.gmp_edge_outer_sum_workspace_size(K, d)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
+    with _timed("edge_outer_sum"):
+        check(lib.gmp_edge_outer_sum_act_f32(K, d, _p(A), _p(X), _p(w), _p(b), _lib.ACT[act],
+                                             _p(C), _p(cs), _p(ws), ws_bytes, _stream()),
+              "gmp_edge_outer_sum_act_f32")
+    return C, cs
+
+
 def _outer_sum_rect_call(A, B):
     lib = _lib.load()
     K, m, n = A.shape[0], A.shape[1], B.shape[1]
@@ -386,26 +404,32 @@ class EgnnEdgeFn(torch.autograd.Function):
         params = tuple(_f32c(t) for t in params)
         _need_cuda(AB, pos, *params)
         N, d = AB.shape[0], AB.shape[1] // 2
+        E = graph.num_edges
         m_aggr = torch.empty((N, d), dtype=torch.float32, device=AB.device)
         pos_aggr = torch.empty((N, 3), dtype=torch.float32, device=AB.device)
+        train = any(ctx.needs_input_grad)
+        xhat = torch.empty((3, E, d), dtype=torch.float32, device=AB.device) if train else None
+        rstd = torch.empty((E, 3), dtype=torch.float32, device=AB.device) if train else None
         P = _egnn_params(params)
         with _timed("egnn_edge_fwd"):
-            check(lib.gmp_egnn_edge_fwd_f32(N, graph.num_edges, d, _p(AB), _p(pos), _p(graph.rowptr),
+            check(lib.gmp_egnn_edge_fwd_f32(N, E, d, _p(AB), _p(pos), _p(graph.rowptr),
                                           _p(graph.recv), _p(graph.send), ctypes.byref(P),
                                           _lib.ACT[act], int(msg_mean), float(eps), _p(m_aggr),
-                                          _p(pos_aggr), _stream()), "gmp_egnn_edge_fwd_f32")
-        ctx.graph, ctx.act, ctx.msg_mean, ctx.eps = graph, act, msg_mean, eps
-        ctx.save_for_backward(AB, pos, *params)
+                                          _p(pos_aggr), _p(xhat), _p(rstd), _stream()),
+                  "gmp_egnn_edge_fwd_f32")
+        ctx.graph, ctx.act, ctx.msg_mean, ctx.eps, ctx.N = graph, act, msg_mean, eps, N
+        if train:
+            ctx.save_for_backward(pos, xhat, rstd, *params)
         return m_aggr, pos_aggr
 
     @staticmethod
     def backward(ctx, g_m, g_p):
         lib = _lib.load()
-        AB, pos, *params = ctx.saved_tensors
+        pos, xhat, rstd, *params = ctx.saved_tensors
         graph = ctx.graph
-        N, d = AB.shape[0], AB.shape[1] // 2
+        N, d = ctx.N, xhat.shape[2]
         E = graph.num_edges
-        dev = AB.device
+        dev = pos.device
         g_m = torch.zeros((N, d), device=dev) if g_m is None else _f32c(g_m)
         g_p = torch.zeros((N, 3), device=dev) if g_p is None else _f32c(g_p)
         f = dict(dtype=torch.float32, device=dev)
@@ -413,28 +437,28 @@ class EgnnEdgeFn(torch.autograd.Function):
         dpos_recv = torch.empty((N, 3), **f)
         dpre1 = torch.empty((E, d), **f)
         gdiff = torch.empty((E, 3), **f)
-        y1 = torch.empty((E, d), **f)
-        m = torch.empty((E, d), **f)
         dpre2 = torch.empty((E, d), **f)
         dpre3 = torch.empty((E, d), **f)
         rows = lib.gmp_egnn_edge_bwd_partials_rows(E, d)
         partials = torch.empty((rows, 8 * d + 1), **f)
         P = _egnn_params(params)
         with _timed("egnn_edge_bwd"):
-            check(lib.gmp_egnn_edge_bwd_f32(N, E, d, _p(AB), _p(pos), _p(graph.rowptr),
-                                          _p(graph.recv), _p(graph.send), ctypes.byref(P),
-                                          _lib.ACT[ctx.act], int(ctx.msg_mean), float(ctx.eps),
-                                          _p(g_m), _p(g_p), _p(dA), _p(dpos_recv), _p(dpre1),
-                                          _p(gdiff), _p(y1), _p(m), _p(dpre2), _p(dpre3),
-                                          _p(partials), _stream()), "gmp_egnn_edge_bwd_f32")
+            check(lib.gmp_egnn_edge_bwd_f32(N, E, d, _p(pos), _p(graph.rowptr), _p(graph.recv),
+                                          _p(graph.send), ctypes.byref(P), _lib.ACT[ctx.act],
+                                          int(ctx.msg_mean), _p(xhat), _p(rstd), _p(g_m),
+                                          _p(g_p), _p(dA), _p(dpos_recv), _p(dpre1), _p(gdiff),
+                                          _p(dpre2), _p(dpre3), _p(partials), _stream()),
+                  "gmp_egnn_edge_bwd_f32")
         # sender-side reductions (deterministic segmented sums over the sender CSR)
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
         dAB = torch.cat([dA, dB], dim=1)
         dpos = dpos_recv - dpos_send
-        # weight gradients: GEMMs over edges (library GEMM) + reductions
-        dW2, db2 = edge_outer_sum(dpre2, y1)
-        dW3, db3 = edge_outer_sum(dpre3, m)
+        # weight gradients: GEMMs over edges, y1 = act(LN1 affine(x_hat1)) and
+        # m = act(LN2 affine(x_hat2)) rebuilt at load time
+        pn = dict(zip(_EGNN_PARAM_NAMES, params))
+        dW2, db2 = edge_outer_sum_act(dpre2, xhat[0], pn["ln1_w"], pn["ln1_b"], ctx.act)
+        dW3, db3 = edge_outer_sum_act(dpre3, xhat[1], pn["ln2_w"], pn["ln2_b"], ctx.act)
         db1 = dA.sum(0)
         v = partials.sum(0)
         dln1w, dln1b, dln2w, dln2b, dln3w, dln3b, dw4, dw1d = v[:8 * d].view(8, d).unbind(0)

@@ -120,13 +120,16 @@ typedef struct gmp_egnn_params {
   const float* b4;   /* (1)  mlp_pos.3.bias   */
 } gmp_egnn_params;
 
+/* save_xhat / save_rstd: NULL (inference) or, for training, (3, E, d) and (E, 3) buffers that
+ * receive the three LayerNorm outputs x_hat1..3 and their 1/std per edge (receiver-sorted rows)
+ * for gmp_egnn_edge_bwd_f32. */
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
                           const float* pos, const int64_t* rowptr, const int64_t* recv,
                           const int64_t* send, const gmp_egnn_params* params, int act,
                           int msg_mean, float ln_eps, float* m_aggr, float* pos_aggr,
-                          void* stream);
+                          float* save_xhat, float* save_rstd, void* stream);
 
-/* Backward of gmp_egnn_edge_fwd_f32 (recomputes the forward chain per edge tile).
+/* Backward of gmp_egnn_edge_fwd_f32 from its saved x_hat / rstd (no forward recompute).
  * Inputs g_m_aggr (N,d), g_pos_aggr (N,3).  Outputs:
  *   dA        (N,d)  receiver part of d(AB)[:, :d]   (segment-summed in-kernel)
  *   dpos_recv (N,3)  receiver part of d(pos)          (segment-summed in-kernel)
@@ -134,19 +137,20 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
  *     dpre1 (E,d)  grad of the first pre-activation   -> caller reduces by sender for
  *                  d(AB)[:, d:], and takes db1 = sum_e dpre1
  *     gdiff (E,3)  grad of rel                         -> caller: dpos[send] -= gdiff
- *     y1, m, dpre2, dpre3 (E,d) each                   -> caller: dW2 = dpre2^T y1,
- *                  dW3 = dpre3^T m, db2 = sum dpre2, db3 = sum dpre3 (GEMMs over edges)
+ *     dpre2, dpre3 (E,d)                               -> caller: dW2 = dpre2^T y1,
+ *                  dW3 = dpre3^T m, db2 = sum dpre2, db3 = sum dpre3, with y1 / m rebuilt
+ *                  from x_hat1 / x_hat2 inside gmp_edge_outer_sum_act_f32
  *   vec_partials (n_blocks, 8*d+1): per-workgroup partial sums of
  *     [dln1_w, dln1_b, dln2_w, dln2_b, dln3_w, dln3_b, dw4, dw1d, db4]   (caller sums rows;
  *     n_blocks from gmp_egnn_edge_bwd_partials_rows). Deterministic. */
 int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d);
-int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
-                          const float* pos, const int64_t* rowptr, const int64_t* recv,
-                          const int64_t* send, const gmp_egnn_params* params, int act,
-                          int msg_mean, float ln_eps, const float* g_m_aggr,
+int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                          const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                          const gmp_egnn_params* params, int act, int msg_mean,
+                          const float* save_xhat, const float* save_rstd, const float* g_m_aggr,
                           const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
-                          float* gdiff, float* y1, float* m, float* dpre2, float* dpre3,
-                          float* vec_partials, void* stream);
+                          float* gdiff, float* dpre2, float* dpre3, float* vec_partials,
+                          void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Edge-reduction GEMM for per-edge Linear weight gradients (egnn_layer.py:28-39 mlp_msg /
@@ -160,6 +164,13 @@ size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d);
 int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
                            float* colsum_A, void* workspace, size_t workspace_bytes,
                            void* stream);
+/* Same with the activation rebuilt from a saved LayerNorm output at load time:
+ * C = A^T act(X * w + b) (+ colsum_A = colsum(A)), w, b per column (d), act 0 = relu, 1 = silu
+ * (the EGNN y1 / m of egnn_layer.py:28-34 from x_hat1 / x_hat2).  Workspace as above. */
+int gmp_edge_outer_sum_act_f32(int64_t K, int64_t d, const float* A, const float* X,
+                               const float* w, const float* b, int act, float* C,
+                               float* colsum_A, void* workspace, size_t workspace_bytes,
+                               void* stream);
 
 /* Rectangular variant (GVP message GVPs, gvp_layer.py:101-170 applied per edge at :319-324):
  * C (m x n) = A^T B, A (K, m), B (K, n) row-major, m, n multiples of 16, m <= 256,
