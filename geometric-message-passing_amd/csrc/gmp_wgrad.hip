@@ -76,7 +76,9 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
     pw = *reinterpret_cast<const f32x4*>(bw + 4 * c4);
     pb = *reinterpret_cast<const f32x4*>(bb + 4 * c4);
   }
-  auto fetch = [&](int64_t kb) {  // global -> registers
+  unsigned vmask = 0;  // rows of the fetched tile that exist (prologue only on those)
+  auto fetch = [&](int64_t kb) {  // global -> registers (stays in flight; no use here)
+    vmask = 0;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int64_t k = kb + r0 + j * RS;
@@ -84,14 +86,16 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
       rb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < k1) {
         ra[j] = *reinterpret_cast<const f32x4*>(A + k * D + 4 * c4);
-        rb[j] = prologue<PRO>(*reinterpret_cast<const f32x4*>(B + k * D + 4 * c4), pw, pb);
+        rb[j] = *reinterpret_cast<const f32x4*>(B + k * D + 4 * c4);
+        vmask |= 1u << j;
       }
     }
   };
-  auto stash = [&](int buf) {  // registers -> LDS (+ colsum of A)
+  auto stash = [&](int buf) {  // registers -> LDS (+ colsum of A), B prologue applied here
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int r = r0 + j * RS;
+      if (PRO != 0 && (vmask >> j) & 1u) rb[j] = prologue<PRO>(rb[j], pw, pb);
       csum += ra[j];
       *reinterpret_cast<f32x4*>(&sA[buf][r * LD + 4 * c4]) = ra[j];
       *reinterpret_cast<f32x4*>(&sB[buf][r * LD + 4 * c4]) = rb[j];

@@ -35,3 +35,16 @@ for (E, m, n) in [(1_000_000, 128, 128), (1_000_000, 128, 144), (1_000_000, 16, 
     t_blas = timeit(lambda: A.t().mm(B))
     line += f"  rocBLAS {t_blas * 1e3:.0f} us"
     print(line, flush=True)
+
+# square outer sum with the activation prologue (EGNN y1 / m from x_hat)
+E, d = 1_000_000, 128
+A = torch.randn(E, d, device="cuda")
+X = torch.randn(E, d, device="cuda")
+w = torch.randn(d, device="cuda")
+b = torch.randn(d, device="cuda")
+t_plain = timeit(lambda: ops.edge_outer_sum(A, X))
+t_act = timeit(lambda: ops.edge_outer_sum_act(A, X, w, b, "relu"))
+ref = ops.edge_outer_sum(A, torch.relu(X * w + b))[0]
+err = (ops.edge_outer_sum_act(A, X, w, b, "relu")[0] - ref).abs().max().item()
+print(f"square E={E} d={d}: plain {t_plain * 1e3:.1f} us, act-prologue {t_act * 1e3:.1f} us, "
+      f"max|diff| vs materialised {err:.2e}")
