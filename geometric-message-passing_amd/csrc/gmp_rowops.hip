@@ -1,0 +1,238 @@
+// K12: fused LayerNorm + activation over rows (node-level MLPs on the path: the EGNN update
+// mlp_upd = Linear -> LayerNorm -> act -> Linear -> LayerNorm -> act, egnn_layer.py:37-39 and
+// :82-86; GVP's scalar LayerNorm, gvp_layer.py:221-243, with act = identity).
+//   forward : xhat = (x - mean) * rstd, rstd = 1/sqrt(var + eps) (biased var, two-pass),
+//             y = act(xhat * gamma + beta); xhat and rstd are saved for the backward
+//   backward: dz = gy * act'(xhat*gamma + beta); dgamma = sum dz*xhat, dbeta = sum dz;
+//             dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dz * gamma
+// One wave per row (lane f handles features f, f + 64, ...); row reductions on DPP + permlane
+// swaps.  gamma/beta gradients: per-workgroup partial rows (registers across a grid-stride
+// loop), summed in workgroup order by the caller-visible second kernel — deterministic.
+#include "gmp_common.h"
+
+namespace gmp {
+namespace {
+
+constexpr int kRowT = 256;        // 4 waves = 4 rows in flight per workgroup
+constexpr int kMaxF = 8;          // features per lane (d <= 512)
+constexpr int kRowBlocks = 1024;  // backward grid (partials rows)
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// sum over all 64 lanes, result in every lane
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dppf<0x128>(v);  // row_ror:8
+  v += dppf<0x124>(v);  // row_ror:4
+  v += dppf<0x122>(v);  // row_ror:2
+  v += dppf<0x121>(v);  // row_ror:1
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  v = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  // lanes summed in different orders: make the result wave-uniform
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// act: 0 relu, 1 silu, 2 identity
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float z) {
+  if (ACT == 0) return z > 0.f ? z : 0.f;
+  if (ACT == 1) return z * (1.f / (1.f + __expf(-z)));
+  return z;
+}
+template <int ACT>
+__device__ __forceinline__ float act_grad(float z) {
+  if (ACT == 0) return z > 0.f ? 1.f : 0.f;
+  if (ACT == 1) {
+    const float sg = 1.f / (1.f + __expf(-z));
+    return sg * (1.f + z * (1.f - sg));
+  }
+  return 1.f;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kRowT) void ln_act_fwd_kernel(
+    int64_t rows, int d, const float* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ y, float* __restrict__ xhat,
+    float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * (kRowT / 64) + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * d;
+  float v[kMaxF];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxF; ++k) {
+    const int f = lane + 64 * k;
+    v[k] = f < d ? xr[f] : 0.f;
+    s += v[k];
+  }
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxF; ++k) {
+    const int f = lane + 64 * k;
+    v[k] = f < d ? v[k] - mean : 0.f;
+    q += v[k] * v[k];
+  }
+  const float rstd = 1.f / sqrtf(wave_sum(q) / (float)d + eps);
+#pragma unroll
+  for (int k = 0; k < kMaxF; ++k) {
+    const int f = lane + 64 * k;
+    if (f < d) {
+      const float xh = v[k] * rstd;
+      xhat[r * d + f] = xh;
+      y[r * d + f] = act_fwd<ACT>(xh * gamma[f] + beta[f]);
+    }
+  }
+  if (lane == 0) rstd_out[r] = rstd;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
+    int64_t rows, int d, const float* __restrict__ gy, const float* __restrict__ xhat,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials) {
+  __shared__ float red[kRowT / 64][2 * 512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float dg[kMaxF], db[kMaxF];
+#pragma unroll
+  for (int k = 0; k < kMaxF; ++k) dg[k] = db[k] = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * (kRowT / 64) + wv; r < rows;
+       r += (int64_t)gridDim.x * (kRowT / 64)) {
+    const float rs = rstd_in[r];
+    float g[kMaxF], xh[kMaxF];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxF; ++k) {
+      const int f = lane + 64 * k;
+      g[k] = 0.f;
+      xh[k] = 0.f;
+      if (f < d) {
+        xh[k] = xhat[r * d + f];
+        const float gm = gamma[f];
+        const float dz = gy[r * d + f] * act_grad<ACT>(xh[k] * gm + beta[f]);
+        dg[k] += dz * xh[k];
+        db[k] += dz;
+        g[k] = dz * gm;
+      }
+      a += g[k];
+      b += g[k] * xh[k];
+    }
+    a = wave_sum(a) / (float)d;
+    b = wave_sum(b) / (float)d;
+#pragma unroll
+    for (int k = 0; k < kMaxF; ++k) {
+      const int f = lane + 64 * k;
+      if (f < d) gx[r * d + f] = rs * (g[k] - a - xh[k] * b);
+    }
+  }
+  // workgroup partial: waves in order
+#pragma unroll
+  for (int k = 0; k < kMaxF; ++k) {
+    const int f = lane + 64 * k;
+    if (f < d) {
+      red[wv][f] = dg[k];
+      red[wv][512 + f] = db[k];
+    }
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < 2 * d; f += kRowT) {
+    const int off = f < d ? f : 512 + (f - d);
+    float s = 0.f;
+    for (int w = 0; w < kRowT / 64; ++w) s += red[w][off];
+    partials[(int64_t)blockIdx.x * 2 * d + f] = s;
+  }
+}
+
+// out[f] = sum over the partial rows (f < 2d: [dgamma | dbeta]) in a fixed order: thread
+// (column c, row group q) sums rows q, q + kSG, ... ; the kSG group sums are then added in
+// group order.  Deterministic.
+constexpr int kSC = 16, kSG = 16;  // columns x row groups per block (256 threads)
+__global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __restrict__ partials,
+                                                             int nrows, int width,
+                                                             float* __restrict__ out) {
+  __shared__ float part[kSG][kSC];
+  const int c = threadIdx.x % kSC, q = threadIdx.x / kSC;
+  const int f = blockIdx.x * kSC + c;
+  float s = 0.f;
+  if (f < width)
+    for (int r = q; r < nrows; r += kSG) s += partials[(int64_t)r * width + f];
+  part[q][c] = s;
+  __syncthreads();
+  if (q == 0 && f < width) {
+    float t = 0.f;
+    for (int g = 0; g < kSG; ++g) t += part[g][c];
+    out[f] = t;
+  }
+}
+
+int bwd_blocks(int64_t rows) {
+  const int64_t b = ceil_div(rows, kRowT / 64);
+  return (int)(b < kRowBlocks ? (b < 1 ? 1 : b) : kRowBlocks);
+}
+
+}  // namespace
+}  // namespace gmp
+
+using namespace gmp;
+
+extern "C" {
+
+int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gamma,
+                       const float* beta, float eps, int act, float* y, float* xhat_save,
+                       float* rstd_save, void* stream) {
+  GMP_CHECK_ARG(rows >= 0 && d > 0 && d <= 64 * kMaxF && act >= 0 && act <= 2);
+  if (rows == 0) return GMP_OK;
+  GMP_CHECK_ARG(x && gamma && beta && y && xhat_save && rstd_save);
+  const unsigned grid = (unsigned)ceil_div(rows, kRowT / 64);
+  hipStream_t s = as_stream(stream);
+  if (act == 0)
+    ln_act_fwd_kernel<0><<<grid, kRowT, 0, s>>>(rows, (int)d, x, gamma, beta, eps, y, xhat_save,
+                                                rstd_save);
+  else if (act == 1)
+    ln_act_fwd_kernel<1><<<grid, kRowT, 0, s>>>(rows, (int)d, x, gamma, beta, eps, y, xhat_save,
+                                                rstd_save);
+  else
+    ln_act_fwd_kernel<2><<<grid, kRowT, 0, s>>>(rows, (int)d, x, gamma, beta, eps, y, xhat_save,
+                                                rstd_save);
+  return launch_status();
+}
+
+size_t gmp_ln_act_bwd_workspace_size(int64_t rows, int64_t d) {
+  return (size_t)bwd_blocks(rows) * 2 * (size_t)d * sizeof(float);
+}
+
+int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float* xhat,
+                       const float* rstd, const float* gamma, const float* beta, int act,
+                       float* grad_x, float* grad_gamma_beta, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  GMP_CHECK_ARG(rows >= 0 && d > 0 && d <= 64 * kMaxF && act >= 0 && act <= 2);
+  GMP_CHECK_ARG(grad_gamma_beta);
+  hipStream_t s = as_stream(stream);
+  if (rows == 0) return hip_check(hipMemsetAsync(grad_gamma_beta, 0, 2 * d * sizeof(float), s));
+  GMP_CHECK_ARG(grad_y && xhat && rstd && gamma && beta && grad_x && workspace);
+  if (workspace_bytes < gmp_ln_act_bwd_workspace_size(rows, d)) return GMP_ERR_WORKSPACE;
+  const int G = bwd_blocks(rows);
+  float* part = reinterpret_cast<float*>(workspace);
+  if (act == 0)
+    ln_act_bwd_kernel<0><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
+                                             grad_x, part);
+  else if (act == 1)
+    ln_act_bwd_kernel<1><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
+                                             grad_x, part);
+  else
+    ln_act_bwd_kernel<2><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
+                                             grad_x, part);
+  int rc = launch_status();
+  if (rc) return rc;
+  sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, G, (int)(2 * d),
+                                                                       grad_gamma_beta);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -84,6 +84,10 @@ class EGNNLayer(MessagePassing):
         """mlp_upd (egnn_layer.py:37-39) with the Linears through ops.linear (node rows: weight
         gradients by the deterministic outer sum instead of small-tile library GEMMs)."""
         l0, n1, l3, n4 = self.mlp_upd[0], self.mlp_upd[1], self.mlp_upd[3], self.mlp_upd[4]
+        if self.norm_name == "layer" and n1.elementwise_affine and n4.elementwise_affine:
+            # LayerNorm + activation fused (K12)
+            x = ops.ln_act(ops.linear(x, l0.weight, l0.bias), n1, self.activation_name)
+            return ops.ln_act(ops.linear(x, l3.weight, l3.bias), n4, self.activation_name)
         x = self.activation(n1(ops.linear(x, l0.weight, l0.bias)))
         return self.activation(n4(ops.linear(x, l3.weight, l3.bias)))
 

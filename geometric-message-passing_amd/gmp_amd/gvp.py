@@ -140,11 +140,11 @@ class LayerNorm(nn.Module):
 
     def forward(self, x):
         if not self.v:
-            return self.scalar_norm(x)
+            return ops.ln_act(x, self.scalar_norm)  # K12 (act = identity)
         s, v = x
         vn = _norm_no_nan(v, axis=-1, keepdims=True, sqrt=False)
         vn = torch.sqrt(torch.mean(vn, dim=-2, keepdim=True))
-        return self.scalar_norm(s), v / vn
+        return ops.ln_act(s, self.scalar_norm), v / vn
 
 
 # ------------------------------------------------------------------------------------ K5g

@@ -277,6 +277,53 @@ class EdgeLinearFn(torch.autograd.Function):
         return dx, dW, (db if ctx.has_b else None)
 
 
+_LN_ACT = {"relu": 0, "swish": 1, "silu": 1, None: 2, "identity": 2}
+
+
+class LnActFn(torch.autograd.Function):
+    """act(LayerNorm(x)) over the last dim (K12 gmp_ln_act_*): one fused kernel each way,
+    deterministic gamma/beta gradients."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, act):
+        lib = _lib.load()
+        shape = x.shape
+        d = shape[-1]
+        x2 = _f32c(x).reshape(-1, d)
+        gamma, beta = _f32c(gamma), _f32c(beta)
+        _need_cuda(x2, gamma, beta)
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        xhat = torch.empty_like(x2)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x2.device)
+        a = _LN_ACT[act]
+        check(lib.gmp_ln_act_fwd_f32(rows, d, _p(x2), _p(gamma), _p(beta), float(eps), a, _p(y),
+                                     _p(xhat), _p(rstd), _stream()), "gmp_ln_act_fwd_f32")
+        ctx.save_for_backward(xhat, rstd, gamma, beta)
+        ctx.act, ctx.shape = a, shape
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = _lib.load()
+        xhat, rstd, gamma, beta = ctx.saved_tensors
+        rows, d = xhat.shape
+        gy = _f32c(gy).reshape(rows, d)
+        gx = torch.empty_like(xhat)
+        gb = torch.empty(2 * d, dtype=torch.float32, device=xhat.device)
+        ws_bytes = lib.gmp_ln_act_bwd_workspace_size(rows, d)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=xhat.device)
+        check(lib.gmp_ln_act_bwd_f32(rows, d, _p(gy), _p(xhat), _p(rstd), _p(gamma), _p(beta),
+                                     ctx.act, _p(gx), _p(gb), _p(ws), ws_bytes, _stream()),
+              "gmp_ln_act_bwd_f32")
+        return gx.view(ctx.shape), gb[:d], gb[d:], None, None
+
+
+def ln_act(x, ln, act=None):
+    """act(ln(x)) for an nn.LayerNorm `ln` (affine) through K12."""
+    return LnActFn.apply(x, ln.weight, ln.bias, ln.eps, act)
+
+
 EDGE_LINEAR_MIN_ROWS = 1 << 15
 
 

@@ -352,6 +352,23 @@ int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_
                          float* torsion, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * K12 fused LayerNorm + activation over rows (node-level MLPs: EGNN mlp_upd,
+ * egnn_layer.py:37-39 / :82-86; GVP scalar LayerNorm, gvp_layer.py:221-243 with act = 2).
+ * x (rows, d), d <= 512; act 0 relu, 1 silu, 2 identity.  Forward writes y = act(LN(x)) and
+ * saves xhat (rows, d) and rstd (rows) for the backward.  Backward: grad_x (rows, d) and
+ * grad_gamma_beta (2d) = [dgamma | dbeta] (deterministic; workspace from
+ * gmp_ln_act_bwd_workspace_size).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gamma,
+                       const float* beta, float eps, int act, float* y, float* xhat_save,
+                       float* rstd_save, void* stream);
+size_t gmp_ln_act_bwd_workspace_size(int64_t rows, int64_t d);
+int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float* xhat,
+                       const float* rstd, const float* gamma, const float* beta, int act,
+                       float* grad_x, float* grad_gamma_beta, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps
  * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)

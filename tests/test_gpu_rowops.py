@@ -1,0 +1,49 @@
+"""K12 fused LayerNorm + activation (gmp_ln_act_*) against the PyTorch fp32 reference
+(nn.LayerNorm + activation), forward and backward, tolerance 1e-5 (scaled)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("rows,d", [(1, 32), (37, 100), (5000, 128), (50_000, 128), (300, 512)])
+@pytest.mark.parametrize("act", ["relu", "silu", None])
+def test_ln_act_matches_torch(rows, d, act):
+    from gmp_amd import ops
+    g = torch.Generator().manual_seed(rows + d)
+    x = (torch.randn(rows, d, generator=g) * 3 + 1).to(DEV)
+    ln = torch.nn.LayerNorm(d).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(d, generator=g))
+        ln.bias.copy_(torch.randn(d, generator=g))
+    gy = torch.randn(rows, d, generator=g).to(DEV)
+    fn = {"relu": F.relu, "silu": F.silu, None: lambda t: t}[act]
+
+    xa = x.clone().requires_grad_(True)
+    y = ops.ln_act(xa, ln, act)
+    (y * gy).sum().backward()
+    got = (y.detach(), xa.grad, ln.weight.grad.clone(), ln.bias.grad.clone())
+    ln.weight.grad = ln.bias.grad = None
+
+    xb = x.clone().requires_grad_(True)
+    yr = fn(ln(xb))
+    (yr * gy).sum().backward()
+    ref = (yr.detach(), xb.grad, ln.weight.grad, ln.bias.grad)
+    for a, b in zip(got, ref):
+        scale = max(1.0, b.abs().max().item())
+        assert (a - b).abs().max().item() <= 1e-5 * scale * (1 + rows ** 0.5 / 10)
+
+
+def test_ln_act_deterministic():
+    from gmp_amd import ops
+    x = torch.randn(20_000, 128, device=DEV)
+    ln = torch.nn.LayerNorm(128).to(DEV)
+    outs = []
+    for _ in range(2):
+        xa = x.clone().requires_grad_(True)
+        ops.ln_act(xa, ln, "relu").sum().backward()
+        outs.append((xa.grad.clone(), ln.weight.grad.clone()))
+        ln.weight.grad = ln.bias.grad = None
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
