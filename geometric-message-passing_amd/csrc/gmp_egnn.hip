@@ -21,8 +21,10 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kThreads = 512;  // 8 waves per workgroup, 1 workgroup per CU (LDS-bound)
-constexpr int kWavesPerBlock = kThreads / 64;
+// One workgroup per CU (W2 + W3 in LDS).  Forward: 12 waves (<= 168 VGPRs -> 3 per SIMD);
+// backward: 8 waves (<= 256 VGPRs -> 2 per SIMD).
+constexpr int kFwdWaves = 12;
+constexpr int kBwdWaves = 8;
 
 template <int D>
 struct Cfg {
@@ -42,9 +44,9 @@ constexpr int carry_stride() { return D / 4 + 4; }
 // LDS: W2 | W3 | NV vectors | per-wave carries [wave][g][d/4 + 4]
 template <int D>
 constexpr size_t smem_params_floats() { return (size_t)2 * D * Cfg<D>::LDW + NV * D; }
-template <int D>
+template <int D, int NW>
 constexpr size_t smem_total() {
-  return (smem_params_floats<D>() + (size_t)kWavesPerBlock * 4 * carry_stride<D>()) * sizeof(float);
+  return (smem_params_floats<D>() + (size_t)NW * 4 * carry_stride<D>()) * sizeof(float);
 }
 
 template <int ACT>
@@ -402,8 +404,9 @@ struct WaveRange {
   int e_lo, e_hi;
 };
 __device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowptr, int64_t n_nodes,
-                                                int64_t n_edges, int64_t n_waves, int wid) {
-  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+                                                int64_t n_edges, int64_t n_waves, int wid,
+                                                int nwb) {
+  const int64_t wave = (int64_t)blockIdx.x * nwb + wid;
   const int64_t nb = node_begin(rowptr, n_nodes, n_edges, wave, n_waves);
   const int64_t ne = node_begin(rowptr, n_nodes, n_edges, wave + 1, n_waves);
   WaveRange r;
@@ -418,7 +421,7 @@ __device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowp
 // SAVE (training): also write the three LayerNorm outputs x_hat1..3 (xsave, (3, E, d), rows in
 // receiver-sorted edge order) and their 1/std (rsave, (E, 3)) for the backward.
 template <int D, int ACT, bool MSG_MEAN, bool SAVE>
-__global__ __launch_bounds__(kThreads, 2) void egnn_fwd_kernel(
+__global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ AB, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
     const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_fwd_kernel(
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* cbuf = smem + smem_params_floats<D>() + (wid * 4 + g) * carry_stride<D>();
-  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid);
+  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, kFwdWaves);
   const float b4 = P.b4[0];
   int carry_node = -1;
 
@@ -522,7 +525,7 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
 // Backward from the forward's saved x_hat1..3 / rstd (no forward recompute, no AB gathers):
 // two transposed GEMMs (W3^T, W2^T) per 16-edge chunk.
 template <int D, int ACT, bool MSG_MEAN>
-__global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
+__global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
     const int64_t* __restrict__ send, gmp_egnn_params P, int64_t n_waves,
@@ -541,7 +544,7 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* cbuf = smem + smem_params_floats<D>() + (wid * 4 + g) * carry_stride<D>();
-  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid);
+  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, kBwdWaves);
   const float b4 = P.b4[0];
   const size_t ED = (size_t)n_edges * D;
 
@@ -713,17 +716,17 @@ __global__ __launch_bounds__(kThreads, 2) void egnn_bwd_kernel(
   __syncthreads();
   for (int t = threadIdx.x; t < RW; t += blockDim.x) {
     float sacc = 0.f;
-    for (int w = 0; w < kWavesPerBlock; ++w) sacc += red[w * RW + t];
+    for (int w = 0; w < kBwdWaves; ++w) sacc += red[w * RW + t];
     partials[(int64_t)blockIdx.x * RW + t] = sacc;
   }
 }
 
-int64_t n_waves_for(int64_t n_edges) {
+int64_t n_waves_for(int64_t n_edges, int nwb) {
   int64_t w = ceil_div(n_edges, 128);  // >= 8 chunks per wave when the chip is full
-  const int64_t cap = (int64_t)device_cu_count() * kWavesPerBlock;
+  const int64_t cap = (int64_t)device_cu_count() * nwb;
   if (w > cap) w = cap;
   if (w < 1) w = 1;
-  return ceil_div(w, kWavesPerBlock) * kWavesPerBlock;
+  return ceil_div(w, nwb) * nwb;
 }
 
 template <class K>
@@ -736,12 +739,12 @@ template <int D, int ACT, bool MEAN>
 int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const int64_t* rowptr,
                const int64_t* recv, const int64_t* send, const gmp_egnn_params& P, float eps,
                float* m_aggr, float* pos_aggr, float* xsave, float* rsave, hipStream_t s) {
-  const int64_t W = n_waves_for(E);
-  const size_t smem = smem_total<D>();
+  const int64_t W = n_waves_for(E, kFwdWaves);
+  const size_t smem = smem_total<D, kFwdWaves>();
   auto k = xsave ? egnn_fwd_kernel<D, ACT, MEAN, true> : egnn_fwd_kernel<D, ACT, MEAN, false>;
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
-  k<<<(unsigned)(W / kWavesPerBlock), kThreads, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
+  k<<<(unsigned)(W / kFwdWaves), kFwdWaves * 64, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
                                                            eps, W, m_aggr, pos_aggr, xsave, rsave);
   return launch_status();
 }
@@ -752,12 +755,12 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
                const float* xsave, const float* rsave, const float* gm, const float* gp,
                float* dA, float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
                float* dpre3, float* partials, hipStream_t s) {
-  const int64_t W = n_waves_for(E);
-  const size_t smem = smem_total<D>();
+  const int64_t W = n_waves_for(E, kBwdWaves);
+  const size_t smem = smem_total<D, kBwdWaves>();
   auto k = egnn_bwd_kernel<D, ACT, MEAN>;
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
-  k<<<(unsigned)(W / kWavesPerBlock), kThreads, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
+  k<<<(unsigned)(W / kBwdWaves), kBwdWaves * 64, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
                                                            xsave, rsave, gm, gp, dA, dpos_recv,
                                                            dpre1, gdiff, dpre2, dpre3, partials);
   return launch_status();
@@ -818,7 +821,7 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
 
 int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d) {
   (void)d;
-  return n_waves_for(n_edges) / kWavesPerBlock;
+  return n_waves_for(n_edges, kBwdWaves) / kBwdWaves;
 }
 
 int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
