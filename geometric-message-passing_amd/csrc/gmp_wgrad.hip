@@ -210,30 +210,46 @@ __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
   for (int r = 0; r < MR; ++r)
 #pragma unroll
     for (int c = 0; c < MC; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float csum = 0.f;
+  float cs[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) cs[r] = 0.f;
   const int CA = M >> 2, CTOT = (M + N) >> 2;
-  const int NLD = kKT * CTOT;
   f32x4 reg[NL];
+  // element tid + q*kT of the tile's (row, float4 column) list: (r0 + q*dR + carry, x...)
+  // computed incrementally — one division per thread, not per element
+  int rq[NL], xq[NL];
+  {
+    const int dR = kT / CTOT, dX = kT - dR * CTOT;
+    int r = tid / CTOT, x = tid - (tid / CTOT) * CTOT;
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      rq[q] = r;
+      xq[q] = x;
+      r += dR;
+      x += dX;
+      if (x >= CTOT) {
+        x -= CTOT;
+        ++r;
+      }
+    }
+  }
   auto fetch = [&](int64_t kb) {
 #pragma unroll
     for (int q = 0; q < NL; ++q) {
-      const int c = tid + q * kT;
       reg[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (c < NLD) {
-        const int r = c / CTOT, x = c - r * CTOT;
-        const int64_t k = kb + r;
-        if (k < k1)
-          reg[q] = (x < CA) ? *reinterpret_cast<const f32x4*>(A + k * M + 4 * x)
-                            : *reinterpret_cast<const f32x4*>(B + k * N + 4 * (x - CA));
+      const int64_t k = kb + rq[q];
+      if (rq[q] < kKT && k < k1) {
+        const int x = xq[q];
+        reg[q] = (x < CA) ? *reinterpret_cast<const f32x4*>(A + k * M + 4 * x)
+                          : *reinterpret_cast<const f32x4*>(B + k * N + 4 * (x - CA));
       }
     }
   };
   auto stash = [&](float* buf) {
 #pragma unroll
     for (int q = 0; q < NL; ++q) {
-      const int c = tid + q * kT;
-      if (c < NLD) {
-        const int r = c / CTOT, x = c - r * CTOT;
+      if (rq[q] < kKT) {
+        const int r = rq[q], x = xq[q];
         float* dst = (x < CA) ? buf + r * LDA + 4 * x : buf + kKT * LDA + r * LDB + 4 * (x - CA);
         *reinterpret_cast<f32x4*>(dst) = reg[q];
       }
@@ -250,8 +266,6 @@ __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
     if (more) fetch(kb + kKT);
     const float* sA = sm + cur * TILE;
     const float* sB = sA + kKT * LDA;
-    if (tid < M)
-      for (int r = 0; r < kKT; ++r) csum += sA[r * LDA + tid];
 #pragma unroll
     for (int st = 0; st < kKT / 4; ++st) {
       const int e = 4 * st + kk;
@@ -266,12 +280,16 @@ __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
         const int tn = rows_mode ? c : w + 4 * c;
         bf[c] = (c < CT) ? sB[e * LDB + 16 * tn + li] : 0.f;
       }
+      // colsum(A) from the A operands already in registers (edges e = kk mod 4 of this lane)
+#pragma unroll
+      for (int r = 0; r < MR; ++r) cs[r] += af[r];
+      // no per-tile guard: out-of-range tiles multiply zero operands (a wave's time is set by
+      // the wave with the most tiles anyway) and are never stored — branch-free MFMA stream
 #pragma unroll
       for (int r = 0; r < MR; ++r)
 #pragma unroll
         for (int c = 0; c < MC; ++c)
-          if (r < RT && c < CT)
-            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[r], bf[c], acc[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[r], bf[c], acc[r][c], 0, 0, 0);
     }
     if (more) stash(sm + (cur ^ 1) * TILE);
     __syncthreads();
@@ -288,7 +306,16 @@ __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) out[(16 * tm + 4 * kk + q) * N + 16 * tn + li] = acc[r][c][q];
       }
-  if (tid < M) out[(int64_t)M * N + tid] = csum;
+  // colsum: add the 4 edge-phase lane groups (l, l^16, l^32, l^48) in a fixed order; each
+  // row tile is owned by one wave (rows mode) or by wave 0 (columns mode: all waves hold it)
+#pragma unroll
+  for (int r = 0; r < MR; ++r) {
+    float v = cs[r];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    const int tm = rows_mode ? w + 4 * r : r;
+    if (kk == 0 && r < RT && (rows_mode || w == 0)) out[(int64_t)M * N + 16 * tm + li] = v;
+  }
 }
 
 // capacity bucket for (M, N): returns 0 if unsupported
@@ -427,9 +454,9 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
   }
   switch (bucket) {
     case 1: GMP_RECT(1, 3, 7, 2) break;
-    case 2: GMP_RECT(2, 5, 9, 1) break;
-    case 3: GMP_RECT(2, 9, 9, 1) break;
-    default: GMP_RECT(4, 4, 9, 1) break;
+    case 2: GMP_RECT(2, 5, 9, 2) break;
+    case 3: GMP_RECT(2, 9, 9, 2) break;
+    default: GMP_RECT(4, 4, 9, 2) break;
   }
 #undef GMP_RECT
   rc = launch_status();
