@@ -319,6 +319,9 @@ __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
 }
 
 // capacity bucket for (M, N): returns 0 if unsupported
+// Tile bucket of an M x N problem: the smallest compiled (MR, MC) covering the per-wave tile
+// counts (the MFMA stream is branch-free, so oversized buckets cost real MFMAs), and the
+// per-thread load count NL in {5, 7, 9}.  Returns MR * 100 + MC * 10 + NL / 2, or 0.
 int rect_bucket(int64_t m, int64_t n) {
   const int64_t TM = m / 16, TN = n / 16;
   int64_t RT, CT;
@@ -326,10 +329,11 @@ int rect_bucket(int64_t m, int64_t n) {
   else { RT = TM; CT = (TN + 3) / 4; }
   const int64_t loads = ceil_div((m + n) / 4 * kKT, kT);
   if (loads > kMaxL) return 0;
-  if (RT <= 1 && CT <= 3 && loads <= 7) return 1;
-  if (RT <= 2 && CT <= 5) return 2;
-  if (RT <= 2 && CT <= 9) return 3;
-  if (RT <= 4 && CT <= 4) return 4;
+  const int nl = loads <= 5 ? 5 : (loads <= 7 ? 7 : 9);
+  static const int kMR[] = {1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 4};
+  static const int kMC[] = {1, 2, 3, 1, 2, 3, 5, 9, 1, 2, 3, 4};
+  for (int b = 0; b < 12; ++b)
+    if (RT <= kMR[b] && CT <= kMC[b]) return kMR[b] * 100 + kMC[b] * 10 + nl / 2;
   return 0;
 }
 
@@ -452,12 +456,18 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
       return rc;                                                                              \
     k<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, per, part);                     \
   }
+#define GMP_RECT_NL(MR, MC)                                   \
+  case MR * 100 + MC * 10 + 2: GMP_RECT(MR, MC, 5, 2) break;  \
+  case MR * 100 + MC * 10 + 3: GMP_RECT(MR, MC, 7, 2) break;  \
+  case MR * 100 + MC * 10 + 4: GMP_RECT(MR, MC, 9, 2) break;
   switch (bucket) {
-    case 1: GMP_RECT(1, 3, 7, 2) break;
-    case 2: GMP_RECT(2, 5, 9, 2) break;
-    case 3: GMP_RECT(2, 9, 9, 2) break;
-    default: GMP_RECT(4, 4, 9, 2) break;
+    GMP_RECT_NL(1, 1) GMP_RECT_NL(1, 2) GMP_RECT_NL(1, 3)
+    GMP_RECT_NL(2, 1) GMP_RECT_NL(2, 2) GMP_RECT_NL(2, 3) GMP_RECT_NL(2, 5) GMP_RECT_NL(2, 9)
+    GMP_RECT_NL(3, 1) GMP_RECT_NL(3, 2) GMP_RECT_NL(3, 3)
+    GMP_RECT_NL(4, 4)
+    default: return GMP_ERR_UNSUPPORTED;
   }
+#undef GMP_RECT_NL
 #undef GMP_RECT
   rc = launch_status();
   if (rc) return rc;
