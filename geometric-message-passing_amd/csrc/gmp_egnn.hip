@@ -352,43 +352,84 @@ __device__ __forceinline__ void carry_apply(const float* cbuf, f32x4 (&x)[D / 16
   for (int c = 0; c < 3; ++c) p3[c] = valid ? p3[c] + (take ? cbuf[D / 4 + c] : 0.f) : 0.f;
 }
 
-// first pre-activation AB[i,:d] + AB[j,d:] + w1d*dist + b1
-template <int D>
-__device__ __forceinline__ void load_pre1(f32x4 (&x)[D / 16], const float* arow, const float* brow,
-                                          const float* sV, float dist, int g) {
-#pragma unroll
-  for (int p = 0; p < D / 16; ++p) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(arow + 16 * p + 4 * g);
-    const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 16 * p + 4 * g);
-    x[p] = (a + b) + (vec4<D>(sV, V_W1D, p, g) * dist + vec4<D>(sV, V_B1, p, g));
-  }
-}
-
 struct EdgeCtx {
-  int e, i, j, seg0, seg1;  // 32-bit (n_nodes, n_edges < 2^31 checked at the C ABI)
+  int e, ec, i, j, seg0, seg1;  // 32-bit (n_nodes, n_edges < 2^31 checked at the C ABI)
   bool valid;
   float rx, ry, rz, dist;
+  float pjx, pjy, pjz;
 };
 
-__device__ __forceinline__ EdgeCtx edge_ctx(int base, int lane_e, int e_hi, int n_nodes,
-                                            const int64_t* __restrict__ recv,
-                                            const int64_t* __restrict__ send,
-                                            const int64_t* __restrict__ rowptr,
+// Receiver / sender of edge e, prefetched one 16-edge chunk ahead so that the gathers that
+// depend on them (rowptr, pos, node rows) are issued together at the start of the next chunk:
+// one exposed memory round trip per chunk instead of a chain of three.  Lanes past the wave's
+// range read the last edge of the graph range (every load stays in bounds and branch-free;
+// results of those lanes are masked by EdgeCtx::valid).
+struct EdgeIJ {
+  int i, j;
+};
+__device__ __forceinline__ int clamp_edge(int e, int e_hi) {
+  e = e < e_hi ? e : e_hi - 1;
+  return e > 0 ? e : 0;
+}
+__device__ __forceinline__ EdgeIJ load_ij(int base, int lane_e, int e_hi,
+                                          const int64_t* __restrict__ recv,
+                                          const int64_t* __restrict__ send) {
+  const int ec = clamp_edge(base + lane_e, e_hi);
+  // low dwords of the int64 indices (values < 2^31)
+  EdgeIJ r;
+  r.i = reinterpret_cast<const int*>(recv)[2 * ec];
+  r.j = reinterpret_cast<const int*>(send)[2 * ec];
+  return r;
+}
+
+__device__ __forceinline__ EdgeCtx edge_ctx(EdgeIJ ij, int base, int lane_e, int e_hi,
+                                            int n_nodes, const int64_t* __restrict__ rowptr,
                                             const float* __restrict__ pos) {
   EdgeCtx c;
   c.e = base + lane_e;
+  c.ec = clamp_edge(c.e, e_hi);
   c.valid = c.e < e_hi;
-  c.i = c.valid ? (int)recv[c.e] : 0;
-  c.j = c.valid ? (int)send[c.e] : 0;
-  if ((unsigned)c.j >= (unsigned)n_nodes) c.j = c.i;  // out-of-range sender (flagged by the CSR
-                                                       // build): never read outside the tables
-  c.seg0 = c.valid ? (int)rowptr[c.i] : c.e;
-  c.seg1 = c.valid ? (int)rowptr[c.i + 1] : c.e + 1;
-  c.rx = pos[3 * c.i + 0] - pos[3 * c.j + 0];  // pos_i - pos_j  (egnn_layer.py:64)
-  c.ry = pos[3 * c.i + 1] - pos[3 * c.j + 1];
-  c.rz = pos[3 * c.i + 2] - pos[3 * c.j + 2];
-  c.dist = sqrtf(c.rx * c.rx + c.ry * c.ry + c.rz * c.rz);
+  c.i = ((unsigned)ij.i < (unsigned)n_nodes) ? ij.i : 0;
+  c.j = ((unsigned)ij.j < (unsigned)n_nodes) ? ij.j : c.i;  // out-of-range sender (flagged by
+                                                            // the CSR build): stay in bounds
+  const int* rp = reinterpret_cast<const int*>(rowptr);
+  c.seg0 = rp[2 * c.i];
+  c.seg1 = rp[2 * c.i + 2];
+  c.rx = pos[3 * c.i + 0];  // pos_i (pos_j subtracted by edge_geom, after the issue burst)
+  c.ry = pos[3 * c.i + 1];
+  c.rz = pos[3 * c.i + 2];
+  c.dist = 0.f;
+  c.pjx = pos[3 * c.j + 0];
+  c.pjy = pos[3 * c.j + 1];
+  c.pjz = pos[3 * c.j + 2];
   return c;
+}
+// rel = pos_i - pos_j (egnn_layer.py:64), dist = |rel|: called once the chunk's loads are issued
+__device__ __forceinline__ void edge_geom(EdgeCtx& c) {
+  c.rx -= c.pjx;
+  c.ry -= c.pjy;
+  c.rz -= c.pjz;
+  c.dist = sqrtf(c.rx * c.rx + c.ry * c.ry + c.rz * c.rz);
+}
+
+// first pre-activation AB[i,:d] + AB[j,d:] + w1d*dist + b1.  All 2*d/4 row loads are issued
+// back to back (one round trip) before any is consumed; the scheduler would otherwise batch
+// them four at a time with a full wait between batches.
+template <int D, class Ctx>
+__device__ __forceinline__ void load_pre1(f32x4 (&x)[D / 16], const float* arow, const float* brow,
+                                          const float* sV, Ctx& c, int g) {
+  f32x4 b[D / 16];
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p) {
+    x[p] = *reinterpret_cast<const f32x4*>(arow + 16 * p + 4 * g);
+    b[p] = *reinterpret_cast<const f32x4*>(brow + 16 * p + 4 * g);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  edge_geom(c);
+  const float dist = c.dist;
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p)
+    x[p] = (x[p] + b[p]) + (vec4<D>(sV, V_W1D, p, g) * dist + vec4<D>(sV, V_B1, p, g));
 }
 
 // row r of a (rows, ld) fp32 tensor (64-bit offset)
@@ -441,14 +482,17 @@ __global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, kFwdWaves);
   const float b4 = P.b4[0];
   int carry_node = -1;
+  EdgeIJ nxt = load_ij(wr.e_lo, li, wr.e_hi, recv, send);
 
   for (int base = wr.e_lo; base < wr.e_hi; base += 16) {
     asm volatile("" ::: "memory");  // keep LDS parameter reads inside the loop
-    const EdgeCtx c = edge_ctx(base, li, wr.e_hi, (int)n_nodes, recv, send, rowptr, pos);
+    const EdgeIJ cur = nxt;
+    nxt = load_ij(base + 16, li, wr.e_hi, recv, send);
+    EdgeCtx c = edge_ctx(cur, base, li, wr.e_hi, (int)n_nodes, rowptr, pos);
 
     const size_t ED = (size_t)n_edges * D;
     f32x4 x[T];  // y1 = act(LN1(pre1))
-    load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c.dist, g);
+    load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);
     const float r1 = ln_normalize<D>(x, eps);
     if (SAVE && c.valid) stream_row<D>(rowp(xsave, c.e, D), x, g);
     affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
@@ -555,26 +599,33 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     for (int k = 0; k < K; ++k) vacc[v][k] = 0.f;
   float db4 = 0.f;
   int carry_node = -1;
+  EdgeIJ nxt = load_ij(wr.e_lo, li, wr.e_hi, recv, send);
 
   for (int base = wr.e_lo; base < wr.e_hi; base += 16) {
     asm volatile("" ::: "memory");
-    const EdgeCtx c = edge_ctx(base, li, wr.e_hi, (int)n_nodes, recv, send, rowptr, pos);
-    const float rstd1 = c.valid ? rsave[3 * (size_t)c.e + 0] : 0.f;
-    const float rstd2 = c.valid ? rsave[3 * (size_t)c.e + 1] : 0.f;
-    const float rstd3 = c.valid ? rsave[3 * (size_t)c.e + 2] : 0.f;
+    const EdgeIJ cur = nxt;
+    nxt = load_ij(base + 16, li, wr.e_hi, recv, send);
+    EdgeCtx c = edge_ctx(cur, base, li, wr.e_hi, (int)n_nodes, rowptr, pos);
+    // every per-chunk load below is issued branch-free at the clamped edge / receiver (one
+    // round trip); lanes past the range are zeroed through ds / gscale / rstd = 0
+    const float rs1 = rsave[3 * (size_t)c.ec + 0];
+    const float rs2 = rsave[3 * (size_t)c.ec + 1];
+    const float rs3 = rsave[3 * (size_t)c.ec + 2];
+    const float gp0 = g_paggr[3 * c.i + 0], gp1 = g_paggr[3 * c.i + 1], gp2 = g_paggr[3 * c.i + 2];
     f32x4 x[T], xh2[T], z[T];
-    if (c.valid) {
-      load_row<D>(z, rowp(xsave + 2 * ED, c.e, D), g);  // z = xhat3
-    } else {
-#pragma unroll
-      for (int p = 0; p < T; ++p) z[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);  // z = xhat3
+    __builtin_amdgcn_sched_barrier(0);
+    edge_geom(c);
+    const float rstd1 = c.valid ? rs1 : 0.f;
+    const float rstd2 = c.valid ? rs2 : 0.f;
+    const float rstd3 = c.valid ? rs3 : 0.f;
 
   // ---------------- pos-branch backward
     const float inv_deg = c.valid ? 1.f / (float)(c.seg1 - c.seg0) : 0.f;
-    const float gpx = c.valid ? g_paggr[3 * c.i + 0] * inv_deg : 0.f;
-    const float gpy = c.valid ? g_paggr[3 * c.i + 1] * inv_deg : 0.f;
-    const float gpz = c.valid ? g_paggr[3 * c.i + 2] * inv_deg : 0.f;
+    const float gscale = MSG_MEAN ? inv_deg : (c.valid ? 1.f : 0.f);
+    const float gpx = gp0 * inv_deg;
+    const float gpy = gp1 * inv_deg;
+    const float gpz = gp2 * inv_deg;
     const float ds = gpx * c.rx + gpy * c.ry + gpz * c.rz;  // dL/ds_e
     if (g == 0) db4 += ds;
 
@@ -596,29 +647,18 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     }, vacc[G_W4], li);
     accumulate_vec<D>([&](int s) { return slot<D>(x, s) * slot<D>(z, s); }, vacc[G_LN3W], li);
     accumulate_vec<D>([&](int s) { return slot<D>(x, s); }, vacc[G_LN3B], li);
+    load_row<D>(xh2, rowp(g_maggr, c.i, D), g);  // g_m_aggr[i] (dm seed, below)
+    __builtin_amdgcn_sched_barrier(0);             // issue it here, ahead of the LN backward
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN3W, p, g);
     ln_backward<D>(x, z, rstd3);  // x = dpre3
     if (c.valid) stream_row<D>(rowp(dpre3_out, c.e, D), x, g);
 
-    // ---------------- dm = g_m_aggr[i] (/deg) + W3^T dpre3   (z)
-    if (c.valid) {
-      load_row<D>(z, rowp(g_maggr, c.i, D), g);
-      if (MSG_MEAN) {
+    // ---------------- dm = g_m_aggr[i] (/deg) + W3^T dpre3   (z); xhat2 -> xh2 in flight
 #pragma unroll
-        for (int p = 0; p < T; ++p) z[p] *= inv_deg;
-      }
-    } else {
-#pragma unroll
-      for (int p = 0; p < T; ++p) z[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int p = 0; p < T; ++p) z[p] = xh2[p] * gscale;
+    load_row<D>(xh2, rowp(xsave + ED, c.ec, D), g);
     gemm_wtx<D>(sW3, x, z, li, g);
-    if (c.valid) {
-      load_row<D>(xh2, rowp(xsave + ED, c.e, D), g);
-    } else {
-#pragma unroll
-      for (int p = 0; p < T; ++p) xh2[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN2W, p, g), b = vec4<D>(sV, V_LN2B, p, g);
@@ -632,16 +672,11 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     ln_backward<D>(z, xh2, rstd2);  // z = dpre2
     if (c.valid) stream_row<D>(rowp(dpre2_out, c.e, D), z, g);
 
-    // ---------------- dy1 = W2^T dpre2 (x); xhat1 recomputed into xh2
+    // ---------------- dy1 = W2^T dpre2 (x); xhat1 -> xh2 in flight
+    load_row<D>(xh2, rowp(xsave, c.ec, D), g);
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
     gemm_wtx<D>(sW2, z, x, li, g);
-    if (c.valid) {  // xh2 <- xhat1
-      load_row<D>(xh2, rowp(xsave, c.e, D), g);
-    } else {
-#pragma unroll
-      for (int p = 0; p < T; ++p) xh2[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN1W, p, g), b = vec4<D>(sV, V_LN1B, p, g);
@@ -801,6 +836,7 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
                           float* save_xhat, float* save_rstd, void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
+  GMP_CHECK_ARG(n_nodes < INT32_MAX && n_edges < INT32_MAX);  // 32-bit edge / node ids
   GMP_CHECK_ARG(params_ok(params) && m_aggr && pos_aggr && rowptr);
   hipStream_t s = as_stream(stream);
   if (n_nodes == 0) return GMP_OK;
@@ -833,6 +869,7 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
                           void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
+  GMP_CHECK_ARG(n_nodes < INT32_MAX && n_edges < INT32_MAX);  // 32-bit edge / node ids
   GMP_CHECK_ARG(params_ok(params) && dA && dpos_recv && rowptr && vec_partials);
   hipStream_t s = as_stream(stream);
   int rc = GMP_OK;
