@@ -63,7 +63,8 @@ __device__ __forceinline__ float act_df(float z) {
 }
 
 // ---------------------------------------------------------------------------------- LDS setup
-template <int D>
+// TRANSPOSE (backward): W2^T / W3^T, so the transposed products read 16-byte rows too
+template <int D, bool TRANSPOSE = false>
 __device__ void load_params_to_lds(float* smem, const gmp_egnn_params& P) {
   constexpr int LDW = Cfg<D>::LDW;
   float* sW2 = smem;
@@ -73,8 +74,15 @@ __device__ void load_params_to_lds(float* smem, const gmp_egnn_params& P) {
     const int o = (4 * i) / D, k = (4 * i) % D;
     const float4 a = reinterpret_cast<const float4*>(P.W2)[i];
     const float4 b = reinterpret_cast<const float4*>(P.W3)[i];
-    *reinterpret_cast<float4*>(sW2 + o * LDW + k) = a;
-    *reinterpret_cast<float4*>(sW3 + o * LDW + k) = b;
+    if (TRANSPOSE) {
+      sW2[(k + 0) * LDW + o] = a.x; sW2[(k + 1) * LDW + o] = a.y;
+      sW2[(k + 2) * LDW + o] = a.z; sW2[(k + 3) * LDW + o] = a.w;
+      sW3[(k + 0) * LDW + o] = b.x; sW3[(k + 1) * LDW + o] = b.y;
+      sW3[(k + 2) * LDW + o] = b.z; sW3[(k + 3) * LDW + o] = b.w;
+    } else {
+      *reinterpret_cast<float4*>(sW2 + o * LDW + k) = a;
+      *reinterpret_cast<float4*>(sW3 + o * LDW + k) = b;
+    }
   }
   const float* vsrc[NV] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
                            P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
@@ -112,26 +120,62 @@ __device__ __forceinline__ void stream_row(float* __restrict__ row, const f32x4 
     __builtin_nontemporal_store(x[p], reinterpret_cast<f32x4*>(row + 16 * p + 4 * g));
 }
 
+// ---------------------------------------------------------------------------------- windows
+// Predicated stores without branches: a buffer descriptor over the rows one 16-edge chunk can
+// touch (wave-uniform base row r0, n rows), and per-lane byte offsets that are pushed out of
+// the window (kOob) for lanes that must not store — the range check drops those.  With no
+// store under a divergent branch the compiler's wait before the next chunk's prefetched ids
+// is a counted vmcnt, not a drain of this chunk's stores.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned kOob = 0x40000000u;  // > any window (<= 16 rows of <= 512 B)
+constexpr int kAuxNT = 2;               // nt: streaming per-edge rows, keep them out of L2
+
+__device__ __forceinline__ rsrc_t rows_window(const float* base, int r0, int n, int ld) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base) + (size_t)(unsigned)r0 * ld, 0,
+                                           n * ld * 4, 0x00020000);
+}
+template <int D, int AUX>
+__device__ __forceinline__ void store_row_w(rsrc_t w, unsigned off, const f32x4 (&x)[D / 16], int g) {
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, x[p]),
+                                           w, off + (16 * p + 4 * g) * 4, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void store3_w(rsrc_t w, unsigned off, float a, float b, float c) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a), w, off, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(b), w, off + 4, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(c), w, off + 8, 0, AUX);
+}
+
 // ---------------------------------------------------------------------------------- MFMA GEMMs
 // GMP_GEMM_FENCE bounds how far the scheduler may hoist LDS operand reads (register pressure).
 #ifndef GMP_GEMM_FENCE
 #define GMP_GEMM_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
 // y[slot(o)] += sum_k W[o][k] x[slot(k)]   (W row-major [o][k] in LDS; lane i = edge = l & 15)
-template <int D>
+// SPLIT > 1: the output tiles in SPLIT groups, so only T/SPLIT A rows are live at a time
+// (register pressure in the backward)
+template <int D, int SPLIT = 1>
 __device__ __forceinline__ void gemm_wx(const float* __restrict__ sW, const f32x4 (&x)[D / 16],
                                         f32x4 (&y)[D / 16], int i, int g) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
+  constexpr int TS = (T % SPLIT == 0) ? T / SPLIT : T;
 #pragma unroll
   for (int p = 0; p < T; ++p) {  // contraction block: features 16p + 4g' + c
-    f32x4 a[T];
 #pragma unroll
-    for (int t = 0; t < T; ++t) a[t] = *reinterpret_cast<const f32x4*>(sW + (16 * t + i) * LDW + 16 * p + 4 * g);
+    for (int t0 = 0; t0 < T; t0 += TS) {
+      f32x4 a[TS];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int t = 0; t < TS; ++t)
+        a[t] = *reinterpret_cast<const f32x4*>(sW + (16 * (t0 + t) + i) * LDW + 16 * p + 4 * g);
 #pragma unroll
-      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][c], x[p][c], y[t], 0, 0, 0);
-    GMP_GEMM_FENCE();
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < TS; ++t)
+          y[t0 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][c], x[p][c], y[t0 + t], 0, 0, 0);
+      GMP_GEMM_FENCE();
+    }
   }
 }
 
@@ -161,7 +205,8 @@ __device__ __forceinline__ void gemm_wtx(const float* __restrict__ sW, const f32
 // DPP within a 16-lane row; lanes without a source get 0
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  // bound_ctrl: lanes without a source read 0, so no "old" operand has to be materialised
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 // the partner of lane i (within its 16-lane row) at reduce-scatter level M: i^8 (row_ror:8),
 // i^7 (row_half_mirror: flips bit 2 like i^4), i^2, i^1 (quad_perm)
@@ -483,6 +528,9 @@ __global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
   const float b4 = P.b4[0];
   int carry_node = -1;
   EdgeIJ nxt = load_ij(wr.e_lo, li, wr.e_hi, recv, send);
+  // land the first ids before the loop, so that the wait at the loop head only has to cover
+  // the ids prefetched by the previous chunk (a counted vmcnt, not a full drain)
+  asm volatile("" ::"v"(nxt.i), "v"(nxt.j));
 
   for (int base = wr.e_lo; base < wr.e_hi; base += 16) {
     asm volatile("" ::: "memory");  // keep LDS parameter reads inside the loop
@@ -494,27 +542,29 @@ __global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
     f32x4 x[T];  // y1 = act(LN1(pre1))
     load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);
     const float r1 = ln_normalize<D>(x, eps);
-    if (SAVE && c.valid) stream_row<D>(rowp(xsave, c.e, D), x, g);
+    // chunk windows: edges [base, base + ne) of the saved tensors, receivers [i0, i1]
+    const int ne = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
+    const int i0 = __builtin_amdgcn_readfirstlane(c.i);
+    const int i1 = __builtin_amdgcn_readlane(c.i, 15);
+    const unsigned eoff = c.valid ? (unsigned)(li * D * 4) : kOob;
+    if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
     affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
 
     f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
     load_vec<D>(m, sV, V_B2, g);
     gemm_wx<D>(sW2, x, m, li, g);
     const float r2 = ln_normalize<D>(m, eps);
-    if (SAVE && c.valid) stream_row<D>(rowp(xsave + ED, c.e, D), m, g);
+    if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave + ED, base, ne, D), eoff, m, g);
     affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);
 
     // y3 = act(LN3(W3 m + b3)); s = w4 . y3 + b4   (x reused)
     load_vec<D>(x, sV, V_B3, g);
     gemm_wx<D>(sW3, m, x, li, g);
     const float r3 = ln_normalize<D>(x, eps);
-    if (SAVE && c.valid) {
-      stream_row<D>(rowp(xsave + 2 * ED, c.e, D), x, g);
-      if (g == 0) {
-        rsave[3 * (size_t)c.e + 0] = r1;
-        rsave[3 * (size_t)c.e + 1] = r2;
-        rsave[3 * (size_t)c.e + 2] = r3;
-      }
+    if (SAVE) {
+      store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
+      store3_w<kAuxNT>(rows_window(rsave, base, ne, 3), (g == 0 && c.valid) ? li * 12u : kOob,
+                       r1, r2, r3);
     }
     affine_act<D, ACT>(x, sV, V_LN3W, V_LN3B, g);
     float sp = 0.f;
@@ -537,18 +587,19 @@ __global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
       seg_scan<1>(pw, li, head);
       pv[0] = pw[0][0]; pv[1] = pw[0][1]; pv[2] = pw[0][2];
     }
-    if (is_end) {
+    {  // receiver rows, stored by the last edge of each segment
       const float deg = (float)(c.seg1 - c.seg0);
-      if (MSG_MEAN) {
+      if (MSG_MEAN) {  // only segment ends (an open segment's m is the next chunk's carry)
+        const float sc = is_end ? 1.f / deg : 1.f;
 #pragma unroll
-        for (int p = 0; p < T; ++p) m[p] *= 1.f / deg;
+        for (int p = 0; p < T; ++p) m[p] *= sc;
       }
-      store_row<D>(rowp(m_aggr, c.i, D), m, g);
-      if (g == 0) {
-        pos_aggr[3 * c.i + 0] = pv[0] / deg;
-        pos_aggr[3 * c.i + 1] = pv[1] / deg;
-        pos_aggr[3 * c.i + 2] = pv[2] / deg;
-      }
+      const int nn = max(i1 - i0 + 1, 0);  // (receiver-sorted: i0 <= i <= i1)
+      store_row_w<D, 0>(rows_window(m_aggr, i0, nn, D), is_end ? (unsigned)((c.i - i0) * D * 4) : kOob,
+                        m, g);
+      store3_w<0>(rows_window(pos_aggr, i0, nn, 3),
+                  (is_end && g == 0) ? (unsigned)((c.i - i0) * 12) : kOob, pv[0] / deg, pv[1] / deg,
+                  pv[2] / deg);
     }
     if (li == 15) carry_store<D>(cbuf, m, pv);
     carry_node = __builtin_amdgcn_readlane(c.i, 15);
@@ -579,10 +630,10 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     float* __restrict__ dpre2_out, float* __restrict__ dpre3_out, float* __restrict__ partials) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW, K = VecAcc<D>::K;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const float* sW2 = smem;
-  const float* sW3 = smem + D * LDW;
+  const float* sW2t = smem;  // W2^T
+  const float* sW3t = smem + D * LDW;  // W3^T
   const float* sV = smem + 2 * D * LDW;
-  load_params_to_lds<D>(smem, P);
+  load_params_to_lds<D, true>(smem, P);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
@@ -600,6 +651,9 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   float db4 = 0.f;
   int carry_node = -1;
   EdgeIJ nxt = load_ij(wr.e_lo, li, wr.e_hi, recv, send);
+  // land the first ids before the loop, so that the wait at the loop head only has to cover
+  // the ids prefetched by the previous chunk (a counted vmcnt, not a full drain)
+  asm volatile("" ::"v"(nxt.i), "v"(nxt.j));
 
   for (int base = wr.e_lo; base < wr.e_hi; base += 16) {
     asm volatile("" ::: "memory");
@@ -652,13 +706,17 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN3W, p, g);
     ln_backward<D>(x, z, rstd3);  // x = dpre3
-    if (c.valid) stream_row<D>(rowp(dpre3_out, c.e, D), x, g);
+    const int ne = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
+    const int i0 = __builtin_amdgcn_readfirstlane(c.i);
+    const int i1 = __builtin_amdgcn_readlane(c.i, 15);
+    const unsigned eoff = c.valid ? (unsigned)(li * D * 4) : kOob;
+    store_row_w<D, kAuxNT>(rows_window(dpre3_out, base, ne, D), eoff, x, g);
 
     // ---------------- dm = g_m_aggr[i] (/deg) + W3^T dpre3   (z); xhat2 -> xh2 in flight
 #pragma unroll
     for (int p = 0; p < T; ++p) z[p] = xh2[p] * gscale;
     load_row<D>(xh2, rowp(xsave + ED, c.ec, D), g);
-    gemm_wtx<D>(sW3, x, z, li, g);
+    gemm_wx<D, 2>(sW3t, x, z, li, g);  // z += W3^T dpre3
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN2W, p, g), b = vec4<D>(sV, V_LN2B, p, g);
@@ -670,13 +728,13 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) z[p] *= vec4<D>(sV, V_LN2W, p, g);
     ln_backward<D>(z, xh2, rstd2);  // z = dpre2
-    if (c.valid) stream_row<D>(rowp(dpre2_out, c.e, D), z, g);
+    store_row_w<D, kAuxNT>(rows_window(dpre2_out, base, ne, D), eoff, z, g);
 
     // ---------------- dy1 = W2^T dpre2 (x); xhat1 -> xh2 in flight
     load_row<D>(xh2, rowp(xsave, c.ec, D), g);
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_wtx<D>(sW2, z, x, li, g);
+    gemm_wx<D, 2>(sW2t, z, x, li, g);  // x = W2^T dpre2
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN1W, p, g), b = vec4<D>(sV, V_LN1B, p, g);
@@ -688,7 +746,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN1W, p, g);
     ln_backward<D>(x, xh2, rstd1);  // x = dpre1
-    if (c.valid) stream_row<D>(rowp(dpre1_out, c.e, D), x, g);
+    store_row_w<D, kAuxNT>(rows_window(dpre1_out, base, ne, D), eoff, x, g);
 
     // dw1d += dpre1 * dist ; d(dist) = w1d . dpre1
     float dd = 0.f;
@@ -703,11 +761,8 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 
     const float rinv = (c.dist > 0.f) ? dd / c.dist : 0.f;
     float gd[3] = {gpx * s_e + rinv * c.rx, gpy * s_e + rinv * c.ry, gpz * s_e + rinv * c.rz};
-    if (c.valid && g == 0) {
-      gdiff_out[3 * c.e + 0] = gd[0];
-      gdiff_out[3 * c.e + 1] = gd[1];
-      gdiff_out[3 * c.e + 2] = gd[2];
-    }
+    store3_w<kAuxNT>(rows_window(gdiff_out, base, ne, 3), (c.valid && g == 0) ? li * 12u : kOob,
+                     gd[0], gd[1], gd[2]);
 
     // ---------------- receiver-side segmented sums: dA (dpre1), dpos_recv (gdiff)
     const int head = c.valid ? (int)((c.seg0 > base) ? (c.seg0 - base) : 0) : li;
@@ -720,13 +775,12 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
       seg_scan<1>(pw, li, head);
       gd[0] = pw[0][0]; gd[1] = pw[0][1]; gd[2] = pw[0][2];
     }
-    if (is_end) {
-      store_row<D>(rowp(dA, c.i, D), x, g);
-      if (g == 0) {
-        dpos_recv[3 * c.i + 0] = gd[0];
-        dpos_recv[3 * c.i + 1] = gd[1];
-        dpos_recv[3 * c.i + 2] = gd[2];
-      }
+    {
+      const int nn = max(i1 - i0 + 1, 0);  // (receiver-sorted: i0 <= i <= i1)
+      store_row_w<D, 0>(rows_window(dA, i0, nn, D), is_end ? (unsigned)((c.i - i0) * D * 4) : kOob,
+                        x, g);
+      store3_w<0>(rows_window(dpos_recv, i0, nn, 3),
+                  (is_end && g == 0) ? (unsigned)((c.i - i0) * 12) : kOob, gd[0], gd[1], gd[2]);
     }
     if (li == 15) carry_store<D>(cbuf, x, gd);
     carry_node = __builtin_amdgcn_readlane(c.i, 15);
