@@ -7,8 +7,10 @@ data, random-init weights.  --workload mace: config C4 (MACE L_max=2, correlatio
 channels, 5 layers, same graph); --workload tfn: config C5's per-GPU shard (TFN L_max=2, 64
 channels, 5 layers, gated, same graph).
 A step = the reference training step (experiments/utils/train_utils.py:128-139): forward,
-L1 loss, backward, Adam step.  Weak scaling: every rank owns its own ~1M-edge graph
-(seed = rank) and gradients are all-reduced by DDP (RCCL over xGMI).
+L1 loss, backward, Adam step (gmp_amd/step.py; weight gradients computed on a side stream and
+accumulated at the end of the backward pass).  Weak scaling: every rank owns its own ~1M-edge
+graph (seed = rank); gradients are averaged with one flat all-reduce per step (RCCL over
+xGMI).  --graph replays the step from a HIP graph instead of launching it eagerly.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -47,6 +49,12 @@ def parse():
     ap.add_argument("--edges", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step from a HIP graph (measured slower than eager launch "
+                         "on ROCm 7 for the EGNN step: off by default)")
+    ap.add_argument("--timing-steps", type=int, default=2,
+                    help="eager steps after the timed region in which the roofline kernel is "
+                         "timed with HIP events (graph mode)")
     return ap.parse_args()
 
 
@@ -215,26 +223,23 @@ def main():
     torch.manual_seed(0)
     model = build_model(gmp_amd, args, g.radius).to(dev)
     core = model
-    # the fused EGNN path gives every parameter a gradient (checked in the gloo rehearsal), so
-    # DDP can skip the per-step unused-parameter traversal there
-    model = gdist.wrap_ddp(model, local if backend == "nccl" else None, bucket_cap_mb=32,
-                           find_unused_parameters=args.workload != "egnn")
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    # capturable Adam keeps its step counter on the device (HIP-graph replay)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, capturable=args.graph)
     batch = g.to(dev)
     y = torch.randn(1, device=dev)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        loss = torch.nn.functional.l1_loss(model(batch).view(-1), y, reduction="sum")
-        loss.backward()
-        opt.step()
+    def loss_fn():
+        return torch.nn.functional.l1_loss(model(batch).view(-1), y, reduction="sum")
 
-    for _ in range(args.warmup):
-        step()
+    # one process per GPU; the step (fwd + L1 + bwd [+ one flat RCCL all-reduce] + Adam) is
+    # captured once and replayed (gmp_amd/step.py); --no-graph runs the same sequence eagerly
+    from gmp_amd.step import GraphedStep
+    step = GraphedStep(model, loss_fn, opt, warmup=args.warmup, use_graph=args.graph)
 
     barrier = gdist.barrier
 
-    ops.KERNEL_TIMERS = {}
+    if not args.graph:
+        ops.KERNEL_TIMERS = {}
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -243,7 +248,14 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = gdist.max_over_ranks(elapsed, dev)
     total_edges = gdist.sum_over_ranks(g.num_edges, dev)
+    if args.graph:
+        # graph replays carry no per-kernel events: time the same kernels in a few eager steps
+        ops.KERNEL_TIMERS = {}
+        for _ in range(max(1, args.timing_steps)):
+            step._eager()
+        torch.cuda.synchronize()
     timers = {k: ops.kernel_time_ms(k) for k in list(ops.KERNEL_TIMERS)}
+    n_timed_steps = args.steps if not args.graph else max(1, args.timing_steps)
     totals = {k: timers[k] * len(v) for k, v in ops.KERNEL_TIMERS.items()}
     ops.KERNEL_TIMERS = None
 
@@ -285,20 +297,20 @@ def main():
             # includes the padded gathers) — MFMA-bound; algorithmic flops per step below
             fl = tp_node_flops(core, g.num_nodes, g.num_edges)
             t_gemm = sum(sum_ms(k) for k in ("tp_node_S", "tp_node_W", "tp_node_dW",
-                                              "tp_node_dZA")) / args.steps
+                                              "tp_node_dZA")) / n_timed_steps
             achieved = fl / (t_gemm * 1e-3) / 1e12
             roof = {"kernel": "tp_node_gemm", "kernel_prefix": "-", "bound": "mfma",
                     "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
                     "flops_per_step": fl, "tp_node_gemm_ms_per_step": t_gemm,
-                    "split_ms_per_step": {k: sum_ms(k) / args.steps for k in
+                    "split_ms_per_step": {k: sum_ms(k) / n_timed_steps for k in
                                           ("tp_node_S", "tp_node_W", "tp_node_dW",
                                            "tp_node_dZA")},
-                    "tp_node_prep_ms_per_step": sum_ms("tp_node_prep") / args.steps,
-                    "tp_node_edge_bwd_ms_per_step": sum_ms("tp_node_edge_bwd") / args.steps,
+                    "tp_node_prep_ms_per_step": sum_ms("tp_node_prep") / n_timed_steps,
+                    "tp_node_edge_bwd_ms_per_step": sum_ms("tp_node_edge_bwd") / n_timed_steps,
                     "symmetric_contraction_ms_per_step":
                         (sum_ms("symmetric_contraction_fwd") +
-                         sum_ms("symmetric_contraction_bwd")) / args.steps}
+                         sum_ms("symmetric_contraction_bwd")) / n_timed_steps}
         t = pmc_traffic(args.workload, roof["kernel_prefix"] if "kernel_prefix" in roof
                         else {"egnn_edge_bwd": "egnn_bwd_kernel",
                               "tp_conv_bwd": "tp_bwd_kernel"}[roof["kernel"]])
@@ -323,7 +335,8 @@ def main():
                                    f"{g.num_nodes} nodes / {g.num_edges} edges per GPU "
                                    f"(r={g.radius}, box={g.box:.3f}, seed=rank)",
                        "global_batch": world, "parallelism": f"dp{world}",
-                       "step": "fwd + L1 loss + bwd + Adam"},
+                       "step": "fwd + L1 loss + bwd + Adam",
+                       "launch": "eager" if not args.graph else "hip graph replay"},
             "roofline": roof,
             "cpu_baseline": None,
         }

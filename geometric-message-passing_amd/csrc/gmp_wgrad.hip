@@ -41,6 +41,7 @@ __device__ __forceinline__ f32x4 prologue(f32x4 v, f32x4 w, f32x4 b) {
 template <int D, int PRO>
 __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restrict__ A,
                                                           const float* __restrict__ B, int64_t K,
+                                                          int64_t lda, int64_t ldb,
                                                           int64_t k_per_block,
                                                           float* __restrict__ partial,
                                                           const float* __restrict__ bw,
@@ -85,8 +86,8 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
       ra[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       rb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < k1) {
-        ra[j] = *reinterpret_cast<const f32x4*>(A + k * D + 4 * c4);
-        rb[j] = *reinterpret_cast<const f32x4*>(B + k * D + 4 * c4);
+        ra[j] = *reinterpret_cast<const f32x4*>(A + k * lda + 4 * c4);
+        rb[j] = *reinterpret_cast<const f32x4*>(B + k * ldb + 4 * c4);
         vmask |= 1u << j;
       }
     }
@@ -169,13 +170,15 @@ __global__ void sum_partials_l1(const float* __restrict__ partial, int64_t G, in
   for (int u = 0; u < kGC; ++u) s += v[u];
   l1[c * X + x] = s;
 }
+// writes C (rows x n, row stride ldc) and colsum (rows) from the dense level-1 slabs
 __global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t X,
-                                float* __restrict__ out, float* __restrict__ colsum, int64_t DD) {
+                                float* __restrict__ out, float* __restrict__ colsum, int64_t DD,
+                                int64_t n, int64_t ldc) {
   const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= X) return;
   float s = 0.f;
   for (int64_t c = 0; c < C; ++c) s += l1[c * X + x];
-  if (x < DD) out[x] = s;
+  if (x < DD) out[(x / n) * ldc + x % n] = s;
   else if (colsum) colsum[x - DD] = s;
 }
 
@@ -193,7 +196,7 @@ constexpr int kMaxL = 9;     // float4 loads per thread per tile (kKT * (M + N) 
 template <int MR, int MC, int NL, int OCC>
 __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
     const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
-    int64_t k_per_block, float* __restrict__ partial) {
+    int64_t lda, int64_t ldb, int64_t k_per_block, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int LDA = rect_ld(M), LDB = rect_ld(N);
   const int TILE = kKT * (LDA + LDB);
@@ -240,8 +243,8 @@ __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
       const int64_t k = kb + rq[q];
       if (rq[q] < kKT && k < k1) {
         const int x = xq[q];
-        reg[q] = (x < CA) ? *reinterpret_cast<const f32x4*>(A + k * M + 4 * x)
-                          : *reinterpret_cast<const f32x4*>(B + k * N + 4 * (x - CA));
+        reg[q] = (x < CA) ? *reinterpret_cast<const f32x4*>(A + k * lda + 4 * x)
+                          : *reinterpret_cast<const f32x4*>(B + k * ldb + 4 * (x - CA));
       }
     }
   };
@@ -356,14 +359,16 @@ size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d) {
   return (size_t)(G + ceil_div(G, kGC)) * (size_t)(d * d + d) * sizeof(float);
 }
 
-static int outer_sum_launch(int64_t K, int64_t d, const float* A, const float* B, int pro,
-                            const float* bw, const float* bb, float* C, float* colsum_A,
-                            void* workspace, size_t workspace_bytes, void* stream) {
+static int outer_sum_launch(int64_t K, int64_t d, const float* A, int64_t lda, const float* B,
+                            int64_t ldb, int pro, const float* bw, const float* bb, float* C,
+                            int64_t ldc, float* colsum_A, void* workspace, size_t workspace_bytes,
+                            void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(K >= 0 && C && pro >= 0 && pro <= 2 && (pro == 0 || (bw && bb)));
+  GMP_CHECK_ARG(lda >= d && ldb >= d && ldc >= d && lda % 4 == 0 && ldb % 4 == 0);
   hipStream_t s = as_stream(stream);
   if (K == 0) {
-    int rc = hip_check(hipMemsetAsync(C, 0, d * d * sizeof(float), s));
+    int rc = hip_check(hipMemset2DAsync(C, ldc * sizeof(float), 0, d * sizeof(float), d, s));
     if (!rc && colsum_A) rc = hip_check(hipMemsetAsync(colsum_A, 0, d * sizeof(float), s));
     return rc;
   }
@@ -376,7 +381,8 @@ static int outer_sum_launch(int64_t K, int64_t d, const float* A, const float* B
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-#define GMP_OS(DD, PP) outer_sum_kernel<DD, PP><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, per, part, bw, bb)
+#define GMP_OS(DD, PP) \
+  outer_sum_kernel<DD, PP><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, lda, ldb, per, part, bw, bb)
 #define GMP_OS_D(PP)                 \
   if (d == 128) GMP_OS(128, PP);     \
   else if (d == 64) GMP_OS(64, PP);  \
@@ -394,14 +400,15 @@ static int outer_sum_launch(int64_t K, int64_t d, const float* A, const float* B
   sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
   rc = launch_status();
   if (rc) return rc;
-  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, d * d);
+  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, d * d, d,
+                                                             ldc);
   return launch_status();
 }
 
 int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
                            float* colsum_A, void* workspace, size_t workspace_bytes,
                            void* stream) {
-  return outer_sum_launch(K, d, A, B, 0, nullptr, nullptr, C, colsum_A, workspace,
+  return outer_sum_launch(K, d, A, d, B, d, 0, nullptr, nullptr, C, d, colsum_A, workspace,
                           workspace_bytes, stream);
 }
 
@@ -410,8 +417,8 @@ int gmp_edge_outer_sum_act_f32(int64_t K, int64_t d, const float* A, const float
                                float* colsum_A, void* workspace, size_t workspace_bytes,
                                void* stream) {
   if (!(act == 0 || act == 1)) return GMP_ERR_ARG;
-  return outer_sum_launch(K, d, A, X, act + 1, w, b, C, colsum_A, workspace, workspace_bytes,
-                          stream);
+  return outer_sum_launch(K, d, A, d, X, d, act + 1, w, b, C, d, colsum_A, workspace,
+                          workspace_bytes, stream);
 }
 
 int64_t rect_blocks_for(int64_t K) {
@@ -426,15 +433,17 @@ size_t gmp_edge_outer_sum_rect_workspace_size(int64_t K, int64_t m, int64_t n) {
   return (size_t)(G + ceil_div(G, kGC)) * (size_t)(m * n + m) * sizeof(float);
 }
 
-int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A, const float* B,
-                                float* C, float* colsum_A, void* workspace,
-                                size_t workspace_bytes, void* stream) {
+static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
+                                 const float* B, int64_t ldb, float* C, int64_t ldc,
+                                 float* colsum_A, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
   GMP_CHECK_ARG(K >= 0 && C && m > 0 && n > 0 && m % 16 == 0 && n % 16 == 0 && m <= kT);
+  GMP_CHECK_ARG(lda >= m && ldb >= n && ldc >= n && lda % 4 == 0 && ldb % 4 == 0);
   const int bucket = rect_bucket(m, n);
   if (!bucket) return GMP_ERR_UNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if (K == 0) {
-    int rc = hip_check(hipMemsetAsync(C, 0, m * n * sizeof(float), s));
+    int rc = hip_check(hipMemset2DAsync(C, ldc * sizeof(float), 0, n * sizeof(float), m, s));
     if (!rc && colsum_A) rc = hip_check(hipMemsetAsync(colsum_A, 0, m * sizeof(float), s));
     return rc;
   }
@@ -454,7 +463,7 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
                                             hipFuncAttributeMaxDynamicSharedMemorySize,      \
                                             (int)smem))))                                     \
       return rc;                                                                              \
-    k<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, per, part);                     \
+    k<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per, part);           \
   }
 #define GMP_RECT_NL(MR, MC)                                   \
   case MR * 100 + MC * 10 + 2: GMP_RECT(MR, MC, 5, 2) break;  \
@@ -477,8 +486,34 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
   sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
   rc = launch_status();
   if (rc) return rc;
-  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, m * n);
+  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, m * n, n,
+                                                             ldc);
   return launch_status();
+}
+
+int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A, const float* B,
+                                float* C, float* colsum_A, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  return outer_sum_rect_launch(K, m, n, A, m, B, n, C, n, colsum_A, workspace, workspace_bytes,
+                               stream);
+}
+
+size_t gmp_edge_outer_sum_ex_workspace_size(int64_t K, int64_t m, int64_t n) {
+  if (m == n && (m == 32 || m == 64 || m == 128)) return gmp_edge_outer_sum_workspace_size(K, m);
+  return gmp_edge_outer_sum_rect_workspace_size(K, m, n);
+}
+
+int gmp_edge_outer_sum_ex_f32(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
+                              const float* B, int64_t ldb, int act, const float* w, const float* b,
+                              float* C, int64_t ldc, float* colsum_A, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  GMP_CHECK_ARG(act >= -1 && act <= 1);
+  if (m == n && (m == 32 || m == 64 || m == 128))
+    return outer_sum_launch(K, m, A, lda, B, ldb, act + 1, w, b, C, ldc, colsum_A, workspace,
+                            workspace_bytes, stream);
+  if (act != -1) return GMP_ERR_UNSUPPORTED;  // activation prologue: square shapes only
+  return outer_sum_rect_launch(K, m, n, A, lda, B, ldb, C, ldc, colsum_A, workspace,
+                               workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -59,6 +59,10 @@ def wrap_ddp(model, local=None, bucket_cap_mb=32, find_unused_parameters=True):
     position MLP, TFN/MACE readout slices), which a plain DDP reducer would wait for forever."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return model
+    # DDP's reducer hooks each parameter's gradient accumulation: weight gradients must reach
+    # autograd, not the end-of-backward deferral (ops.DEFER_WEIGHT_GRADS)
+    from . import ops
+    ops.DEFER_WEIGHT_GRADS = False
     ids = [local] if local is not None else None
     return torch.nn.parallel.DistributedDataParallel(model, device_ids=ids,
                                                      bucket_cap_mb=bucket_cap_mb,

@@ -68,27 +68,26 @@ class EGNNLayer(MessagePassing):
                 and all(ln.elementwise_affine and ln.eps == lns[0].eps for ln in lns))
 
     def fused_propagate(self, edge_index, h, pos):
-        d = self.emb_dim
         graph = ops.egnn_graph(edge_index, h.shape[0])
-        W1 = self.mlp_msg[0].weight
-        AB = ops.linear(h, torch.cat([W1[:, :d], W1[:, d:2 * d]], 0))  # [h W1a^T | h W1b^T]
         m0, ln1, m3, ln2 = self.mlp_msg[0], self.mlp_msg[1], self.mlp_msg[3], self.mlp_msg[4]
         p0, ln3, p3 = self.mlp_pos[0], self.mlp_pos[1], self.mlp_pos[3]
-        params = (W1[:, 2 * d], m0.bias, ln1.weight, ln1.bias, m3.weight, m3.bias, ln2.weight,
-                  ln2.bias, p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias)
-        m_aggr, p_aggr = ops.EgnnEdgeFn.apply(AB, pos, graph, self.activation_name,
-                                              self.aggr == "mean", ln1.eps, *params)
-        return self._mlp_upd(torch.cat([h, m_aggr], dim=-1)), pos + p_aggr
+        m_aggr, p_aggr = ops.EgnnMessageFn.apply(
+            h, pos, graph, self.activation_name, self.aggr == "mean", ln1.eps,
+            m0.weight, m0.bias, ln1.weight, ln1.bias, m3.weight, m3.bias, ln2.weight, ln2.bias,
+            p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias)
+        return self._mlp_upd(h, m_aggr), pos + p_aggr
 
-    def _mlp_upd(self, x):
-        """mlp_upd (egnn_layer.py:37-39) with the Linears through ops.linear (node rows: weight
-        gradients by the deterministic outer sum instead of small-tile library GEMMs)."""
+    def _mlp_upd(self, h, m_aggr):
+        """mlp_upd(cat([h, m_aggr])) (egnn_layer.py:37-39, :84) with the first Linear split over
+        the two inputs (no concatenation) and the Linears through ops (node rows: weight
+        gradients by the deterministic outer sum, deferred to the side stream)."""
         l0, n1, l3, n4 = self.mlp_upd[0], self.mlp_upd[1], self.mlp_upd[3], self.mlp_upd[4]
+        x = ops.split_linear(h, m_aggr, l0.weight, l0.bias)
         if self.norm_name == "layer" and n1.elementwise_affine and n4.elementwise_affine:
             # LayerNorm + activation fused (K12)
-            x = ops.ln_act(ops.linear(x, l0.weight, l0.bias), n1, self.activation_name)
+            x = ops.ln_act(x, n1, self.activation_name)
             return ops.ln_act(ops.linear(x, l3.weight, l3.bias), n4, self.activation_name)
-        x = self.activation(n1(ops.linear(x, l0.weight, l0.bias)))
+        x = self.activation(n1(x))
         return self.activation(n4(ops.linear(x, l3.weight, l3.bias)))
 
     def __repr__(self):

@@ -207,11 +207,46 @@ def edge_outer_sum_act(A, X, w, b, act):
     return C, cs
 
 
-def _outer_sum_rect_call(A, B):
+def _rows_view_ok(t):
+    """(K, m) fp32 CUDA view usable as a strided outer-sum operand: unit column stride, row
+    stride a multiple of 4 floats, 16-byte aligned base."""
+    return (t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+            and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0)
+
+
+def outer_sum_into(A, B, C, colsum=None, act=None, w=None, b=None):
+    """C[:] = A^T act(B) over the rows (gmp_edge_outer_sum_ex_f32), colsum[:] = colsum(A).
+    A (K, m), B (K, n) and C (m, n) may be strided views (row strides; e.g. column blocks of a
+    wider tensor or parameter gradient).  Returns False when the shape is outside the kernels'
+    tile buckets (caller falls back)."""
     lib = _lib.load()
-    K, m, n = A.shape[0], A.shape[1], B.shape[1]
-    if m == n and m in (32, 64, 128):  # square tiles: the faster square kernel (K5)
-        return edge_outer_sum(A, B)
+    _need_cuda(A, B, C)
+    K, m = A.shape
+    n = B.shape[1]
+    if not (_rows_view_ok(A) and _rows_view_ok(B) and C.stride(1) == 1):
+        raise _lib.GmpError("outer_sum_into: operands need unit column stride, 4-float aligned "
+                            "row strides and 16-byte aligned bases")
+    a = -1 if act is None else _lib.ACT[act]
+    ws_bytes = lib.gmp_edge_outer_sum_ex_workspace_size(K, m, n)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
+    with _timed("edge_outer_sum"):
+        rc = lib.gmp_edge_outer_sum_ex_f32(K, m, n, _p(A), A.stride(0), _p(B), B.stride(0), a,
+                                           _p(w), _p(b), _p(C), C.stride(0), _p(colsum), _p(ws),
+                                           ws_bytes, _stream())
+    if rc == _lib.GMP_ERR_UNSUPPORTED:
+        return False
+    check(rc, "gmp_edge_outer_sum_ex_f32")
+    return True
+
+
+def edge_outer_sum_rect(A, B):
+    """(A^T B, colsum(A)) over the rows (edges / nodes) for any widths, deterministic: columns
+    zero-padded to multiples of 16 when needed, wide operands processed as <= 128 x 144 column
+    blocks read in place (strided) and written into their block of C.  None when a block shape
+    is outside the kernels' buckets."""
+    A, B = _f32c(A), _f32c(B)
+    _need_cuda(A, B)
+    m, n = A.shape[1], B.shape[1]
     mp, np_ = -(-m // 16) * 16, -(-n // 16) * 16
     if mp != m:
         A = torch.nn.functional.pad(A, (0, mp - m))
@@ -219,64 +254,173 @@ def _outer_sum_rect_call(A, B):
         B = torch.nn.functional.pad(B, (0, np_ - n))
     C = torch.empty((mp, np_), dtype=torch.float32, device=A.device)
     cs = torch.empty(mp, dtype=torch.float32, device=A.device)
-    ws_bytes = lib.gmp_edge_outer_sum_rect_workspace_size(K, mp, np_)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=A.device)
-    with _timed("edge_outer_sum"):
-        rc = lib.gmp_edge_outer_sum_rect_f32(K, mp, np_, _p(A), _p(B), _p(C), _p(cs), _p(ws),
-                                             ws_bytes, _stream())
-    if rc == _lib.GMP_ERR_UNSUPPORTED:  # shape outside the kernel's tile buckets
-        return None
-    check(rc, "gmp_edge_outer_sum_rect_f32")
+    bn = 144 if np_ <= 144 else 128
+    for m0 in range(0, mp, 128):
+        for n0 in range(0, np_, bn):
+            ok = outer_sum_into(A[:, m0:m0 + 128], B[:, n0:n0 + bn], C[m0:m0 + 128, n0:n0 + bn],
+                                cs[m0:m0 + 128] if n0 == 0 else None)
+            if not ok:
+                return None
     return C[:m, :n], cs[:m]
 
 
-def edge_outer_sum_rect(A, B):
-    """(A^T B, colsum(A)) over the rows (edges / nodes) for any widths, deterministic: columns
-    zero-padded to multiples of 16 for gmp_edge_outer_sum_rect_f32, wide operands split into
-    <= 128 x 144 blocks.  None when a block shape is outside the kernel's buckets."""
-    A, B = _f32c(A), _f32c(B)
-    _need_cuda(A, B)
-    m, n = A.shape[1], B.shape[1]
-    if m <= 128 and n <= 144:
-        return _outer_sum_rect_call(A, B)
-    C = torch.empty((m, n), dtype=torch.float32, device=A.device)
-    cs = torch.empty(m, dtype=torch.float32, device=A.device)
-    for m0 in range(0, m, 128):
-        Am = A[:, m0:m0 + 128].contiguous()
-        for n0 in range(0, n, 128):
-            r = _outer_sum_rect_call(Am, B[:, n0:n0 + 128].contiguous())
-            if r is None:
-                return None
-            C[m0:m0 + 128, n0:n0 + 128] = r[0]
-            if n0 == 0:
-                cs[m0:m0 + 128] = r[1]
-    return C, cs
+# ----------------------------------------------------------------------------------- deferred
+# Weight gradients are leaves of the backward graph: nothing downstream waits for them.  They
+# are computed on a side stream (overlapping the critical path's small node-level kernels and
+# the host launch gaps between them) and accumulated into param.grad by a callback at the end
+# of the backward pass, as DDP does with its reducer.  Disable (DEFER_WEIGHT_GRADS = False)
+# when something must see these gradients through autograd (DDP's per-parameter hooks,
+# torch.autograd.grad on parameters); gmp_amd.dist.wrap_ddp does so.
+DEFER_WEIGHT_GRADS = True
+_SIDE_STREAMS = {}
+_PENDING = []   # (param, grad) accumulated at the end of the backward pass
+_CB_QUEUED = [False]
+
+
+def _side_stream(device):
+    st = _SIDE_STREAMS.get(device)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _SIDE_STREAMS[device] = st
+    return st
+
+
+def _flush_deferred():
+    _CB_QUEUED[0] = False
+    if not _PENDING:
+        return
+    main = torch.cuda.current_stream()
+    for st in _SIDE_STREAMS.values():
+        main.wait_stream(st)
+    for p, g in _PENDING:
+        g.record_stream(main)
+        if p.grad is None:
+            p.grad = g
+        else:
+            p.grad.add_(g)
+    _PENDING.clear()
+
+
+def deferrable(t):
+    return DEFER_WEIGHT_GRADS and t is not None and t.is_leaf and t.requires_grad
+
+
+class side_work:
+    """with side_work(used_tensors) as sw: ... launches on the side stream after everything
+    already queued on the current stream; sw.defer(param, grad) hands a result to the end-of-
+    backward accumulation (or, when deferral is off, sw.join() makes the current stream wait)."""
+
+    def __init__(self, *used):
+        self.used = [t for t in used if t is not None]
+
+    def __enter__(self):
+        self.main = torch.cuda.current_stream()
+        self.side = _side_stream(self.main.device)
+        self.side.wait_stream(self.main)
+        self.ctx = torch.cuda.stream(self.side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self.ctx.__exit__(*exc)
+        for t in self.used:
+            t.record_stream(self.side)
+        return False
+
+    def defer(self, param, grad):
+        _PENDING.append((param, grad))
+        if not _CB_QUEUED[0]:
+            _CB_QUEUED[0] = True
+            torch.autograd.Variable._execution_engine.queue_callback(_flush_deferred)
+
+    def join(self, *results):
+        """results are needed on the current stream now (returned through autograd)."""
+        self.main.wait_stream(self.side)
+        for r in results:
+            if r is not None:
+                r.record_stream(self.main)
 
 
 class EdgeLinearFn(torch.autograd.Function):
     """y = x W^T (+ b) over many rows (edges): forward and dx with the library GEMM (M = rows),
     dW / db with the deterministic edge outer sum (K = rows), which the library's small-tile
-    K-reduction GEMMs run far below the HBM roofline."""
+    K-reduction GEMMs run far below the HBM roofline.  dW / db of leaf parameters are computed
+    on the side stream and accumulated at the end of the backward pass (deferred)."""
 
     @staticmethod
     def forward(ctx, x, W, b):
-        ctx.save_for_backward(x, W)
-        ctx.has_b = b is not None
+        ctx.save_for_backward(x, W, b)
         return torch.addmm(b, x, W.t()) if b is not None else x.mm(W.t())
 
     @staticmethod
     def backward(ctx, g):
-        x, W = ctx.saved_tensors
+        x, W, b = ctx.saved_tensors
         g = g.contiguous()
         dx = g.mm(W) if ctx.needs_input_grad[0] else None
-        dW = db = None
-        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+        need_w = ctx.needs_input_grad[1] or (b is not None and ctx.needs_input_grad[2])
+        if not need_w:
+            return dx, None, None
+        defer = deferrable(W) and (b is None or deferrable(b))
+        with side_work(g, x) as sw:
             r = edge_outer_sum_rect(g, x)
-            if r is None:
-                dW, db = g.t().mm(x), g.sum(0)
-            else:
-                dW, db = r
-        return dx, dW, (db if ctx.has_b else None)
+            dW, db = r if r is not None else (g.t().mm(x), g.sum(0))
+        if defer:
+            sw.defer(W, dW)
+            if b is not None:
+                sw.defer(b, db)
+            return dx, None, None
+        sw.join(dW, db)
+        return dx, dW, (db if b is not None else None)
+
+
+class SplitLinearFn(torch.autograd.Function):
+    """y = [xa | xb] W^T + b without materialising the concatenation (egnn_layer.py:37
+    mlp_upd[0] over cat([h, m_aggr])): two GEMMs forward, two for dx; dW written block-wise
+    into one (out, ina + inb) gradient by the strided outer sum (deferred for leaf params)."""
+
+    @staticmethod
+    def forward(ctx, xa, xb, W, b):
+        da = xa.shape[1]
+        y = torch.addmm(b, xa, W[:, :da].t()) if b is not None else xa.mm(W[:, :da].t())
+        y.addmm_(xb, W[:, da:].t())
+        ctx.save_for_backward(xa, xb, W, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        xa, xb, W, b = ctx.saved_tensors
+        da = xa.shape[1]
+        g = g.contiguous()
+        dxa = g.mm(W[:, :da]) if ctx.needs_input_grad[0] else None
+        dxb = g.mm(W[:, da:]) if ctx.needs_input_grad[1] else None
+        need_w = ctx.needs_input_grad[2] or (b is not None and ctx.needs_input_grad[3])
+        if not need_w:
+            return dxa, dxb, None, None
+        defer = deferrable(W) and (b is None or deferrable(b))
+        with side_work(g, xa, xb) as sw:
+            dW = torch.empty_like(W)
+            db = torch.empty(W.shape[0], dtype=W.dtype, device=W.device)
+            ok = (outer_sum_into(g, xa, dW[:, :da], db)
+                  and outer_sum_into(g, xb, dW[:, da:], None))
+            if not ok:
+                dW = torch.cat([g.t().mm(xa), g.t().mm(xb)], 1)
+                db = g.sum(0)
+        if defer:
+            sw.defer(W, dW)
+            if b is not None:
+                sw.defer(b, db)
+            return dxa, dxb, None, None
+        sw.join(dW, db)
+        return dxa, dxb, dW, (db if b is not None else None)
+
+
+def split_linear(xa, xb, W, b=None):
+    """F.linear(cat([xa, xb], -1), W, b) for 2-D inputs without the concatenation."""
+    if (xa.is_cuda and xa.dim() == 2 and xb.dim() == 2 and xa.dtype == torch.float32
+            and xa.shape[0] >= EDGE_LINEAR_MIN_ROWS and xa.shape[1] % 4 == 0
+            and xb.shape[1] % 4 == 0):
+        return SplitLinearFn.apply(xa.contiguous(), xb.contiguous(), W, b)
+    return torch.nn.functional.linear(torch.cat([xa, xb], -1), W, b)
 
 
 _LN_ACT = {"relu": 0, "swish": 1, "silu": 1, None: 2, "identity": 2}
@@ -438,27 +582,36 @@ def _egnn_params(tensors):
     return _lib.GmpEgnnParams(*[t.data_ptr() for t in tensors])
 
 
-class EgnnEdgeFn(torch.autograd.Function):
-    """Fused EGNN message + aggregation (egnn_layer.py:62-80) on the receiver-sorted graph.
+class EgnnMessageFn(torch.autograd.Function):
+    """The whole EGNN message block of one layer (egnn_layer.py:62-80 with the MLPs of :28-36):
+    the node projections AB = [h W1a^T | h W1b^T] (one GEMM), the fused edge kernel K4 and the
+    aggregation; backward = K4 backward, sender-side segmented sums, dh on the critical path,
+    and every weight gradient (dW1 assembled in place as [dW1a | dW1b | dw1d], dW2, dW3 via
+    the edge outer sums, LayerNorm / vector partials) on the side stream, deferred.
 
-    Inputs: AB = [h W1a^T | h W1b^T] (N, 2d), pos (N, 3), the 14 message/pos-MLP tensors in
-    _EGNN_PARAM_NAMES order.  Returns (m_aggr (N, d), pos_aggr (N, 3)).
+    Parameters in module order: mlp_msg.0.{weight (d, 2d+1), bias}, mlp_msg.1.{weight, bias},
+    mlp_msg.3.{weight, bias}, mlp_msg.4.{weight, bias}, mlp_pos.0.{weight, bias},
+    mlp_pos.1.{weight, bias}, mlp_pos.3.{weight (1, d), bias}.
+    Returns (m_aggr (N, d), pos_aggr (N, 3)).
     """
 
     @staticmethod
-    def forward(ctx, AB, pos, graph, act, msg_mean, eps, *params):
+    def forward(ctx, h, pos, graph, act, msg_mean, eps, W1, b1, ln1w, ln1b, W2, b2, ln2w, ln2b,
+                W3, b3, ln3w, ln3b, w4, b4):
         lib = _lib.load()
-        AB = _f32c(AB)
-        pos = _f32c(pos)
-        params = tuple(_f32c(t) for t in params)
-        _need_cuda(AB, pos, *params)
-        N, d = AB.shape[0], AB.shape[1] // 2
+        h, pos = _f32c(h), _f32c(pos)
+        _need_cuda(h, pos, W1)
+        N, d = h.shape
         E = graph.num_edges
-        m_aggr = torch.empty((N, d), dtype=torch.float32, device=AB.device)
-        pos_aggr = torch.empty((N, 3), dtype=torch.float32, device=AB.device)
+        Wcat = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)
+        AB = h.mm(Wcat.t())  # [h W1a^T | h W1b^T]
+        params = tuple(_f32c(t) for t in (W1[:, 2 * d], b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3,
+                                          b3, ln3w, ln3b, w4, b4))
+        m_aggr = torch.empty((N, d), dtype=torch.float32, device=h.device)
+        pos_aggr = torch.empty((N, 3), dtype=torch.float32, device=h.device)
         train = any(ctx.needs_input_grad)
-        xhat = torch.empty((3, E, d), dtype=torch.float32, device=AB.device) if train else None
-        rstd = torch.empty((E, 3), dtype=torch.float32, device=AB.device) if train else None
+        xhat = torch.empty((3, E, d), dtype=torch.float32, device=h.device) if train else None
+        rstd = torch.empty((E, 3), dtype=torch.float32, device=h.device) if train else None
         P = _egnn_params(params)
         with _timed("egnn_edge_fwd"):
             check(lib.gmp_egnn_edge_fwd_f32(N, E, d, _p(AB), _p(pos), _p(graph.rowptr),
@@ -466,15 +619,15 @@ class EgnnEdgeFn(torch.autograd.Function):
                                           _lib.ACT[act], int(msg_mean), float(eps), _p(m_aggr),
                                           _p(pos_aggr), _p(xhat), _p(rstd), _stream()),
                   "gmp_egnn_edge_fwd_f32")
-        ctx.graph, ctx.act, ctx.msg_mean, ctx.eps, ctx.N = graph, act, msg_mean, eps, N
+        ctx.graph, ctx.act, ctx.msg_mean, ctx.N = graph, act, msg_mean, N
         if train:
-            ctx.save_for_backward(pos, xhat, rstd, *params)
+            ctx.save_for_backward(h, pos, xhat, rstd, W1, *params)
         return m_aggr, pos_aggr
 
     @staticmethod
     def backward(ctx, g_m, g_p):
         lib = _lib.load()
-        pos, xhat, rstd, *params = ctx.saved_tensors
+        h, pos, xhat, rstd, W1, *params = ctx.saved_tensors
         graph = ctx.graph
         N, d = ctx.N, xhat.shape[2]
         E = graph.num_edges
@@ -498,22 +651,40 @@ class EgnnEdgeFn(torch.autograd.Function):
                                           _p(g_p), _p(dA), _p(dpos_recv), _p(dpre1), _p(gdiff),
                                           _p(dpre2), _p(dpre3), _p(partials), _stream()),
                   "gmp_egnn_edge_bwd_f32")
-        # sender-side reductions (deterministic segmented sums over the sender CSR)
+        # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
-        dAB = torch.cat([dA, dB], dim=1)
+        dh = dA.mm(W1[:, :d])
+        dh.addmm_(dB, W1[:, d:2 * d])
         dpos = dpos_recv - dpos_send
-        # weight gradients: GEMMs over edges, y1 = act(LN1 affine(x_hat1)) and
-        # m = act(LN2 affine(x_hat2)) rebuilt at load time
-        pn = dict(zip(_EGNN_PARAM_NAMES, params))
-        dW2, db2 = edge_outer_sum_act(dpre2, xhat[0], pn["ln1_w"], pn["ln1_b"], ctx.act)
-        dW3, db3 = edge_outer_sum_act(dpre3, xhat[1], pn["ln2_w"], pn["ln2_b"], ctx.act)
-        db1 = dA.sum(0)
-        v = partials.sum(0)
-        dln1w, dln1b, dln2w, dln2b, dln3w, dln3b, dw4, dw1d = v[:8 * d].view(8, d).unbind(0)
-        db4 = v[8 * d:8 * d + 1]
-        grads = dict(w1d=dw1d, b1=db1, ln1_w=dln1w, ln1_b=dln1b, W2=dW2, b2=db2, ln2_w=dln2w,
-                     ln2_b=dln2b, W3=dW3, b3=db3, ln3_w=dln3w, ln3_b=dln3b, w4=dw4.view(1, d),
-                     b4=db4)
-        pgrads = tuple(grads[n].reshape(t.shape) for n, t in zip(_EGNN_PARAM_NAMES, params))
-        return (dAB, dpos, None, None, None, None) + pgrads
+
+        # weight gradients: side stream, accumulated at the end of the backward pass
+        (_, b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3, b3, ln3w, ln3b, w4, b4) = params
+        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials) as sw:
+            dW1 = torch.empty((d, 2 * d + 1), **f)
+            db1 = torch.empty(d, **f)
+            outer_sum_into(dA, h, dW1[:, :d], db1)
+            outer_sum_into(dB, h, dW1[:, d:2 * d])
+            v = partials.sum(0)
+            dln1w, dln1b, dln2w, dln2b, dln3w, dln3b, dw4, dw1d = v[:8 * d].view(8, d).unbind(0)
+            dW1[:, 2 * d].copy_(dw1d)
+            dW2, db2 = edge_outer_sum_act(dpre2, xhat[0], ln1w, ln1b, ctx.act)
+            dW3, db3 = edge_outer_sum_act(dpre3, xhat[1], ln2w, ln2b, ctx.act)
+            grads = (dW1, db1, dln1w, dln1b, dW2, db2, dln2w, dln2b, dW3, db3, dln3w, dln3b,
+                     dw4.view(1, d), v[8 * d:8 * d + 1])
+        # the caller's parameter tensors (saved tensors unpack to the same objects): W1 itself,
+        # then b1 ... b4 (params[0] is the contiguous copy of W1's distance column)
+        targets = (W1,) + tuple(params[1:])
+        out, joined = [], False
+        for i, (p, gr) in enumerate(zip(targets, grads)):
+            if not ctx.needs_input_grad[6 + i]:
+                out.append(None)
+            elif deferrable(p):
+                sw.defer(p, gr)
+                out.append(None)
+            else:
+                if not joined:
+                    sw.join(*grads)
+                    joined = True
+                out.append(gr)
+        return (dh, dpos, None, None, None, None) + tuple(out)

@@ -179,6 +179,18 @@ size_t gmp_edge_outer_sum_rect_workspace_size(int64_t K, int64_t m, int64_t n);
 int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A, const float* B,
                                 float* C, float* colsum_A, void* workspace,
                                 size_t workspace_bytes, void* stream);
+/* General form (strided operands and output): C (m x n, row stride ldc) = A^T act(B),
+ * A (K, m) with row stride lda, B (K, n) with row stride ldb (lda, ldb multiples of 4, A and B
+ * 16-byte aligned), colsum_A (m) optional; act -1 = none, 0 = relu(B*w + b), 1 = silu(B*w + b)
+ * (the activation prologue needs m == n in {32, 64, 128}).  Lets a Linear's weight gradient
+ * be written straight into a column block of a wider parameter (egnn_layer.py:28 W1 =
+ * [W1a | W1b | w1d]; :37 mlp_upd[0] over [h | m_aggr]) without concatenated copies.
+ * Square 32/64/128 shapes use the square kernel, others the rectangular one. */
+size_t gmp_edge_outer_sum_ex_workspace_size(int64_t K, int64_t m, int64_t n);
+int gmp_edge_outer_sum_ex_f32(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
+                              const float* B, int64_t ldb, int act, const float* w, const float* b,
+                              float* C, int64_t ldc, float* colsum_A, void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K1 per-edge featurisation (models/mace.py:170-174, models/tfn.py:171-175,

@@ -110,3 +110,52 @@ def test_ddp_gloo_world2_matches_single_process():
         for r in range(world):
             # DDP averages the ranks' (already per-rank averaged) gradients
             torch.testing.assert_close(res[r]["grads"][k], p.grad, atol=1e-6, rtol=1e-5)
+
+
+def _step_worker(rank, world, port, out_dir):
+    """bench.py's step executor (gmp_amd/step.py) in eager mode: parameter broadcast, one flat
+    all-reduce of the gradients, Adam step."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from gmp_amd import dist as gdist
+    from gmp_amd.step import GraphedStep
+    from oracle import egnn as oegnn
+    gdist.init("gloo")
+    torch.manual_seed(rank)  # different init per rank: the executor must broadcast rank 0's
+    model = oegnn.EGNNModel(num_layers=2, emb_dim=16, out_dim=2)
+    g = _graphs()[rank]
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+    step = GraphedStep(model, lambda: _loss(model, g), opt, warmup=0, use_graph=False)
+    for _ in range(2):
+        step()
+    torch.save({k: p.detach().clone() for k, p in model.named_parameters()},
+               os.path.join(out_dir, f"step{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_step_executor_gloo_world2_matches_single_process():
+    from oracle import egnn as oegnn
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_step_worker, args=(world, _free_port(), d), nprocs=world,
+                           start_method="spawn", join=True)
+        res = [torch.load(os.path.join(d, f"step{r}.pt"), weights_only=True)
+               for r in range(world)]
+    # single process: rank 0's init, gradient = mean over the two ranks' graphs, two Adam steps
+    torch.manual_seed(0)
+    ref = oegnn.EGNNModel(num_layers=2, emb_dim=16, out_dim=2)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-2)
+    graphs = _graphs()
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        for r in range(world):
+            (_loss(ref, graphs[r]) / world).backward()
+        for p in ref.parameters():  # the executor all-reduces zeros for unused parameters
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        opt.step()
+    for k, p in ref.named_parameters():
+        for r in range(world):
+            torch.testing.assert_close(res[r][k], p.detach(), atol=1e-5, rtol=1e-5)
