@@ -223,8 +223,10 @@ def main():
     torch.manual_seed(0)
     model = build_model(gmp_amd, args, g.radius).to(dev)
     core = model
-    # capturable Adam keeps its step counter on the device (HIP-graph replay)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, capturable=args.graph)
+    # Adam (the reference optimizer, train_utils.py): the fused multi-tensor implementation
+    # (one launch per step); capturable (step counter on the device) for HIP-graph replay
+    opt = (torch.optim.Adam(model.parameters(), lr=1e-4, capturable=True) if args.graph
+           else torch.optim.Adam(model.parameters(), lr=1e-4, fused=True))
     batch = g.to(dev)
     y = torch.randn(1, device=dev)
 

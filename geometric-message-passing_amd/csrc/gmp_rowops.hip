@@ -212,13 +212,17 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
                        float* grad_x, float* grad_gamma_beta, void* workspace,
                        size_t workspace_bytes, void* stream) {
   GMP_CHECK_ARG(rows >= 0 && d > 0 && d <= 64 * kMaxF && act >= 0 && act <= 2);
-  GMP_CHECK_ARG(grad_gamma_beta);
+  GMP_CHECK_ARG(grad_gamma_beta || workspace);
   hipStream_t s = as_stream(stream);
-  if (rows == 0) return hip_check(hipMemsetAsync(grad_gamma_beta, 0, 2 * d * sizeof(float), s));
-  GMP_CHECK_ARG(grad_y && xhat && rstd && gamma && beta && grad_x && workspace);
-  if (workspace_bytes < gmp_ln_act_bwd_workspace_size(rows, d)) return GMP_ERR_WORKSPACE;
   const int G = bwd_blocks(rows);
   float* part = reinterpret_cast<float*>(workspace);
+  if (rows == 0) {
+    if (grad_gamma_beta)
+      return hip_check(hipMemsetAsync(grad_gamma_beta, 0, 2 * d * sizeof(float), s));
+    return hip_check(hipMemsetAsync(part, 0, (size_t)G * 2 * d * sizeof(float), s));
+  }
+  GMP_CHECK_ARG(grad_y && xhat && rstd && gamma && beta && grad_x && workspace);
+  if (workspace_bytes < gmp_ln_act_bwd_workspace_size(rows, d)) return GMP_ERR_WORKSPACE;
   if (act == 0)
     ln_act_bwd_kernel<0><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
                                              grad_x, part);
@@ -229,9 +233,23 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
     ln_act_bwd_kernel<2><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
                                              grad_x, part);
   int rc = launch_status();
-  if (rc) return rc;
+  if (rc || !grad_gamma_beta) return rc;  // NULL: the caller reduces the partial rows itself
   sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, G, (int)(2 * d),
                                                                        grad_gamma_beta);
+  return launch_status();
+}
+
+int64_t gmp_ln_act_bwd_partial_rows(int64_t rows) { return bwd_blocks(rows); }
+
+int gmp_sum_rows_f32(const float* partials, int64_t nrows, int64_t width, float* out,
+                     void* stream) {
+  GMP_CHECK_ARG(nrows >= 0 && width >= 0 && width <= INT32_MAX && nrows <= INT32_MAX);
+  if (width == 0) return GMP_OK;
+  GMP_CHECK_ARG(out && (nrows == 0 || partials));
+  hipStream_t s = as_stream(stream);
+  if (nrows == 0) return hip_check(hipMemsetAsync(out, 0, width * sizeof(float), s));
+  sum_rows_kernel<<<(unsigned)ceil_div(width, kSC), kSC * kSG, 0, s>>>(partials, (int)nrows,
+                                                                       (int)width, out);
   return launch_status();
 }
 

@@ -203,12 +203,16 @@ class GvpLayerFn(torch.autograd.Function):
                                             ops._p(spre), ops._p(dgate), ops._p(vn), ops._p(vh),
                                             ops._p(dvpre), ops._p(dvh), ops._stream()),
                   "gmp_gvp_layer_bwd_f32")
-        dWs_s, dbs = _osum(dspre, s.view(E, 128))
-        dWs_v, _ = _osum(dspre, vn)
-        dWsv, dbsv = _osum(dgate, spre)
-        dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
-        dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
-        return (ds_in, dv_in, torch.cat([dWs_s, dWs_v], 1), dbs, dWsv, dbsv, dWh, dWv, None)
+        # weight gradients (edge outer sums) on the side stream, deferred to the end of backward
+        with ops.side_work(dspre, s, vn, dgate, spre, dvh, v, dvpre, vh) as sw:
+            dWs_s, dbs = _osum(dspre, s.view(E, 128))
+            dWs_v, _ = _osum(dspre, vn)
+            dWsv, dbsv = _osum(dgate, spre)
+            dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
+            dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
+            dWs = torch.cat([dWs_s, dWs_v], 1)
+        grads = (dWs, dbs, dWsv, dbsv, dWh, dWv)
+        return (ds_in, dv_in) + sw.deliver(ctx.needs_input_grad, 2, W, grads) + (None,)
 
 
 class GvpMsg0Fn(torch.autograd.Function):

@@ -340,6 +340,23 @@ class side_work:
             if r is not None:
                 r.record_stream(self.main)
 
+    def deliver(self, needs_input_grad, first, targets, grads):
+        """Per parameter: defer the gradient (leaf parameter) or hand it back through autograd
+        (after joining the streams).  needs_input_grad[first + i] belongs to targets[i]."""
+        out, joined = [], False
+        for i, (p, gr) in enumerate(zip(targets, grads)):
+            if not needs_input_grad[first + i]:
+                out.append(None)
+            elif deferrable(p):
+                self.defer(p, gr)
+                out.append(None)
+            else:
+                if not joined:
+                    self.join(*grads)
+                    joined = True
+                out.append(gr)
+        return tuple(out)
+
 
 class EdgeLinearFn(torch.autograd.Function):
     """y = x W^T (+ b) over many rows (edges): forward and dx with the library GEMM (M = rows),
@@ -459,6 +476,8 @@ class LnActFn(torch.autograd.Function):
         gb = torch.empty(2 * d, dtype=torch.float32, device=xhat.device)
         ws_bytes = lib.gmp_ln_act_bwd_workspace_size(rows, d)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=xhat.device)
+        # (deferring the [dgamma | dbeta] reduction to the side stream was measured slower: the
+        # extra stream bookkeeping lengthens the host-bound stretch of small node kernels)
         check(lib.gmp_ln_act_bwd_f32(rows, d, _p(gy), _p(xhat), _p(rstd), _p(gamma), _p(beta),
                                      ctx.act, _p(gx), _p(gb), _p(ws), ws_bytes, _stream()),
               "gmp_ln_act_bwd_f32")
@@ -675,16 +694,5 @@ class EgnnMessageFn(torch.autograd.Function):
         # the caller's parameter tensors (saved tensors unpack to the same objects): W1 itself,
         # then b1 ... b4 (params[0] is the contiguous copy of W1's distance column)
         targets = (W1,) + tuple(params[1:])
-        out, joined = [], False
-        for i, (p, gr) in enumerate(zip(targets, grads)):
-            if not ctx.needs_input_grad[6 + i]:
-                out.append(None)
-            elif deferrable(p):
-                sw.defer(p, gr)
-                out.append(None)
-            else:
-                if not joined:
-                    sw.join(*grads)
-                    joined = True
-                out.append(gr)
-        return (dh, dpos, None, None, None, None) + tuple(out)
+        return (dh, dpos, None, None, None, None) + sw.deliver(ctx.needs_input_grad, 6, targets,
+                                                               grads)

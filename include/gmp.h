@@ -369,7 +369,10 @@ int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_
  * x (rows, d), d <= 512; act 0 relu, 1 silu, 2 identity.  Forward writes y = act(LN(x)) and
  * saves xhat (rows, d) and rstd (rows) for the backward.  Backward: grad_x (rows, d) and
  * grad_gamma_beta (2d) = [dgamma | dbeta] (deterministic; workspace from
- * gmp_ln_act_bwd_workspace_size).
+ * gmp_ln_act_bwd_workspace_size).  grad_gamma_beta may be NULL: the workspace then holds
+ * gmp_ln_act_bwd_partial_rows(rows) partial rows of width 2d, to be reduced by the caller
+ * (gmp_sum_rows_f32, e.g. later / on another stream: gamma and beta are leaves of the graph).
+ * gmp_sum_rows_f32: out[c] = sum_r partials[r, c] in a fixed order (deterministic).
  * ------------------------------------------------------------------------------------------ */
 int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gamma,
                        const float* beta, float eps, int act, float* y, float* xhat_save,
@@ -379,6 +382,9 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
                        const float* rstd, const float* gamma, const float* beta, int act,
                        float* grad_x, float* grad_gamma_beta, void* workspace,
                        size_t workspace_bytes, void* stream);
+int64_t gmp_ln_act_bwd_partial_rows(int64_t rows);
+int gmp_sum_rows_f32(const float* partials, int64_t nrows, int64_t width, float* out,
+                     void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with

@@ -1,0 +1,49 @@
+"""Host-side (Python) cost of the EGNN training step (dev tool): cProfile over a few steps of
+bench.py's step, GPU synchronised only at the end.  usage: python scripts/host_profile.py"""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "geometric-message-passing_amd"))
+import gmp_amd  # noqa: E402
+from gmp_amd.graph import radius_graph  # noqa: E402
+
+g = radius_graph(num_nodes=50_000, target_edges=1_000_000, seed=0)
+torch.manual_seed(0)
+dev = torch.device("cuda")
+model = gmp_amd.EGNNModel(num_layers=4, emb_dim=128, in_dim=1, out_dim=1).to(dev)
+opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=os.environ.get("FUSED", "0") == "1")
+batch = g.to(dev)
+y = torch.randn(1, device=dev)
+
+
+def step():
+    opt.zero_grad(set_to_none=True)
+    loss = torch.nn.functional.l1_loss(model(batch).view(-1), y, reduction="sum")
+    loss.backward()
+    opt.step()
+
+
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(5):
+    step()
+t_host = time.perf_counter() - t0
+torch.cuda.synchronize()
+t_all = time.perf_counter() - t0
+print(f"5 steps: host enqueue {t_host * 1e3:.1f} ms, wall {t_all * 1e3:.1f} ms")
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(5):
+    step()
+torch.cuda.synchronize()
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(35)
