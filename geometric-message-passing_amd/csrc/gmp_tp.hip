@@ -530,6 +530,245 @@ size_t smem_bytes(const Desc& d, int cg_len, bool bwd) {
   return f * sizeof(float);
 }
 
+// -------------------------------------------------------------------------------- z, v2
+// Per-edge z / dz kernels of the node form without LDS staging or barriers: one wave per edge
+// (grid-stride), lane owns channels u = lane, lane + 64 (mul1 <= 128), the CG contraction with
+// the edge's SH is unrolled per (l1, l2, lo) at compile time (coefficients are wave-uniform:
+// scalar loads), the per-edge backward accumulates dx in registers per input block (one block
+// per l1) and dY as per-lane partials reduced once per edge.  HBM-bound on the z / dz rows.
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+template <int L1, int L2, int LO>
+__device__ __forceinline__ void t_table(const float* __restrict__ C, const float (&Y)[9],
+                                        float (&T)[2 * L1 + 1][2 * LO + 1]) {
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * LO + 1, YO = L2 * L2;
+#pragma unroll
+  for (int i = 0; i < D1; ++i)
+#pragma unroll
+    for (int k = 0; k < D3; ++k) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < D2; ++j) a += C[(i * D2 + j) * D3 + k] * Y[YO + j];
+      T[i][k] = a;
+    }
+  __builtin_amdgcn_sched_barrier(0);  // consume the coefficients as they arrive
+}
+
+template <int L1, int L2, int LO>
+__device__ __forceinline__ void z_path(const Path& P, const float* __restrict__ C,
+                                       const float (&Y)[9], const float* __restrict__ xrow,
+                                       float* __restrict__ zr, int lane) {
+  constexpr int D1 = 2 * L1 + 1, D3 = 2 * LO + 1;
+  float T[D1][D3];
+  t_table<L1, L2, LO>(C, Y, T);
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) {
+    const int u = lane + 64 * uu;
+    if (u < P.mul1) {
+      float xu[D1];
+#pragma unroll
+      for (int i = 0; i < D1; ++i) xu[i] = xrow[P.x_off + u * D1 + i];
+#pragma unroll
+      for (int k = 0; k < D3; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < D1; ++i) a += xu[i] * T[i][k];
+        zr[k * P.mul1 + u] = P.alpha * a;
+      }
+    }
+  }
+}
+
+struct DxAcc {
+  float d0[2], d1[2][3], d2[2][5];
+};
+
+template <int L1, int L2, int LO>
+__device__ __forceinline__ void z_bwd_path(const Path& P, const float* __restrict__ C,
+                                           const float (&Y)[9], const float* __restrict__ xrow,
+                                           const float* __restrict__ dzr, DxAcc& dx,
+                                           float (&dyp)[9], int lane) {
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * LO + 1, YO = L2 * L2;
+  float T[D1][D3];
+  t_table<L1, L2, LO>(C, Y, T);
+  float M[D3][D1];  // sum over this lane's channels of dz[k] x[i]
+#pragma unroll
+  for (int k = 0; k < D3; ++k)
+#pragma unroll
+    for (int i = 0; i < D1; ++i) M[k][i] = 0.f;
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) {
+    const int u = lane + 64 * uu;
+    if (u < P.mul1) {
+      float xu[D1], dz[D3];
+#pragma unroll
+      for (int i = 0; i < D1; ++i) xu[i] = xrow[P.x_off + u * D1 + i];
+#pragma unroll
+      for (int k = 0; k < D3; ++k) dz[k] = P.alpha * dzr[k * P.mul1 + u];
+#pragma unroll
+      for (int i = 0; i < D1; ++i) {
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < D3; ++k) a += T[i][k] * dz[k];
+        if constexpr (L1 == 0) dx.d0[uu] += a;
+        else if constexpr (L1 == 1) dx.d1[uu][i] += a;
+        else dx.d2[uu][i] += a;
+      }
+#pragma unroll
+      for (int k = 0; k < D3; ++k)
+#pragma unroll
+        for (int i = 0; i < D1; ++i) M[k][i] += dz[k] * xu[i];
+    }
+  }
+  // dY_j += sum_{i,k} C[i, j, k] M[k][i]  (per-lane partial; reduced once per edge)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < D2; ++j) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < D1; ++i)
+#pragma unroll
+      for (int k = 0; k < D3; ++k) a += C[(i * D2 + j) * D3 + k] * M[k][i];
+    dyp[YO + j] += a;
+  }
+}
+
+// (l1, l2, lo) with l <= 2 and |l1 - l2| <= lo <= l1 + l2
+#define GMP_Z_PATHS(X)                                                                         \
+  X(0, 0, 0) X(0, 1, 1) X(0, 2, 2) X(1, 0, 1) X(1, 1, 0) X(1, 1, 1) X(1, 1, 2) X(1, 2, 1)      \
+  X(1, 2, 2) X(2, 0, 2) X(2, 1, 1) X(2, 1, 2) X(2, 2, 0) X(2, 2, 1) X(2, 2, 2)
+
+__device__ __forceinline__ void load_y(const float* __restrict__ sh, int64_t eo, float (&Y)[9]) {
+#pragma unroll
+  for (int j = 0; j < 9; ++j) Y[j] = sh[eo * 9 + j];
+}
+
+__global__ __launch_bounds__(256) void tp_edge_z2_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+    const float* __restrict__ x, const float* __restrict__ sh,
+    const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
+    int64_t e1, float* __restrict__ zbuf) {
+  __shared__ float sC[4096];  // CG table (wave-uniform reads: LDS broadcast)
+  for (int c = threadIdx.x; c < cg_len; c += blockDim.x) sC[c] = cg[c];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t ne = e1 - e0;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
+    const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
+    const int64_t src = src_sorted[e], eo = perm[e];
+    float Y[9];
+    load_y(sh, eo, Y);
+    const float* xrow = x + src * d.in_dim;
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = paths[p];
+      const float* C = sC + P.cg_off;
+      float* zr = zbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
+      switch (P.l1 * 9 + P.l2 * 3 + P.lo) {
+#define GMP_Z_CASE(A, B, O) \
+  case A * 9 + B * 3 + O: z_path<A, B, O>(P, C, Y, xrow, zr, lane); break;
+        GMP_Z_PATHS(GMP_Z_CASE)
+#undef GMP_Z_CASE
+        default: break;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+    const float* __restrict__ x, const float* __restrict__ sh,
+    const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
+    int64_t e1, const float* __restrict__ dzbuf, float* __restrict__ dx_edge,
+    float* __restrict__ dY_edge) {
+  __shared__ float sC[4096];  // CG table (wave-uniform reads: LDS broadcast)
+  for (int c = threadIdx.x; c < cg_len; c += blockDim.x) sC[c] = cg[c];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t ne = e1 - e0;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  // input blocks (one per l1, as the path table lays them out; wave-uniform): the dx row is
+  // written block by block, entries of the row no path reads are written as zero
+  int xoff[3] = {-1, -1, -1}, xmul[3] = {0, 0, 0};
+  for (int p = 0; p < d.n_paths; ++p) {
+    const Path P = paths[p];
+    xoff[P.l1] = P.x_off;
+    xmul[P.l1] = P.mul1;
+  }
+  for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
+    const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
+    const int64_t src = src_sorted[e], eo = perm[e];
+    float Y[9], dyp[9];
+    load_y(sh, eo, Y);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) dyp[j] = 0.f;
+    DxAcc dx;
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) {
+      dx.d0[uu] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) dx.d1[uu][i] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) dx.d2[uu][i] = 0.f;
+    }
+    const float* xrow = x + src * d.in_dim;
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = paths[p];
+      const float* C = sC + P.cg_off;
+      const float* dzr =
+          dzbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
+      switch (P.l1 * 9 + P.l2 * 3 + P.lo) {
+#define GMP_ZB_CASE(A, B, O) \
+  case A * 9 + B * 3 + O: z_bwd_path<A, B, O>(P, C, Y, xrow, dzr, dx, dyp, lane); break;
+        GMP_Z_PATHS(GMP_ZB_CASE)
+#undef GMP_ZB_CASE
+        default: break;
+      }
+    }
+    float* dxr = dx_edge + k * d.in_dim;
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) {
+      const int u = lane + 64 * uu;
+      if (xoff[0] >= 0 && u < xmul[0]) dxr[xoff[0] + u] = dx.d0[uu];
+      if (xoff[1] >= 0 && u < xmul[1]) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) dxr[xoff[1] + 3 * u + i] = dx.d1[uu][i];
+      }
+      if (xoff[2] >= 0 && u < xmul[2]) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) dxr[xoff[2] + 5 * u + i] = dx.d2[uu][i];
+      }
+    }
+    if (xmul[0] + 3 * xmul[1] + 5 * xmul[2] != d.in_dim) {  // rows read by no path: zero
+      for (int c = lane; c < d.in_dim; c += 64) {
+        bool in = false;
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          in |= xoff[b] >= 0 && c >= xoff[b] && c < xoff[b] + xmul[b] * (2 * b + 1);
+        if (!in) dxr[c] = 0.f;
+      }
+    }
+    float dyv = 0.f;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const float v = wave_sum64(dyp[j]);
+      dyv = (lane == j) ? v : dyv;
+    }
+    if (lane < 9) dY_edge[k * 9 + lane] = dyv;
+  }
+}
+
+int64_t z2_blocks(int64_t edges) {
+  const int64_t cap = (int64_t)device_cu_count() * 8;  // 32 resident waves per CU
+  int64_t g = (edges + 3) / 4;
+  g = g < cap ? g : cap;
+  return g < 1 ? 1 : g;
+}
+
 int64_t grid_for_chunk(int64_t edges) {
   const int64_t cap = (int64_t)device_cu_count() * 8;  // ~8 resident waves per CU
   int64_t g = edges < cap ? edges : cap;
@@ -613,10 +852,7 @@ int gmp_tp_edge_z_f32(const void* desc_host, const void* paths_dev, const float*
   GMP_CHECK_ARG(desc_ok(d, d.n_blocks == 3 ? 0 : 1) && cg_len > 0 && cg_len <= 4096);
   GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
   if (e1 == e0) return GMP_OK;
-  const size_t smem = smem_bytes(d, cg_len, false);
-  int rc;
-  if ((rc = set_smem(tp_edge_z_kernel, smem))) return rc;
-  tp_edge_z_kernel<<<(unsigned)grid_for_chunk(e1 - e0), kWave, smem, as_stream(stream)>>>(
+  tp_edge_z2_kernel<<<(unsigned)z2_blocks(e1 - e0), 256, 0, as_stream(stream)>>>(
       d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
   return launch_status();
 }
@@ -631,10 +867,7 @@ int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const fl
   GMP_CHECK_ARG(desc_ok(d, d.n_blocks == 3 ? 0 : 1) && cg_len > 0 && cg_len <= 4096);
   GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
   if (e1 == e0) return GMP_OK;
-  const size_t smem = smem_bytes(d, cg_len, true);
-  int rc;
-  if ((rc = set_smem(tp_edge_z_bwd_kernel, smem))) return rc;
-  tp_edge_z_bwd_kernel<<<(unsigned)grid_for_chunk(e1 - e0), kWave, smem, as_stream(stream)>>>(
+  tp_edge_z2_bwd_kernel<<<(unsigned)z2_blocks(e1 - e0), 256, 0, as_stream(stream)>>>(
       d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf, dx_edge,
       dY_edge);
   return launch_status();
