@@ -19,10 +19,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kNT = 256;          // 4 waves
 constexpr int kRowsPerBlock = 64; // outer: rows (r) per workgroup (one 16-row tile per wave)
-constexpr int kEdgeStage = 16;    // outer: edges staged per LDS pass
+constexpr int kEdgeStage = 32;    // outer: edges staged per LDS pass (in-degree ~20: one pass)
 constexpr int kMaxH = 256;
 
 // ---------------------------------------------------------------------------------- outer
+// grid (ceil(w / (64 kOuterRB)), receivers): the workgroup stages the receiver's hidden radial
+// rows a_e once and produces kOuterRB 64-row blocks of S from them
+constexpr int kOuterRB = 1;
 __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
                                                             const int64_t* __restrict__ eoff,
                                                             const float* __restrict__ Z,
@@ -30,49 +33,63 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
                                                             float* __restrict__ S,
                                                             float* __restrict__ Sb) {
   __shared__ __attribute__((aligned(16))) float sA[kEdgeStage * (kMaxH + 16)];
-  const int n = blockIdx.y, rb = blockIdx.x;
+  const int n = blockIdx.y;
   const int LDA = H + 16;  // 16 mod 64 floats: the 4 edge rows of an MFMA read hit disjoint banks
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, i = lane & 15, kk = lane >> 4;
   const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
-  // D = S^T tile: D[j][r] = sum_e A[e, j] Z[e, r]  (A op = a columns, B op = Z columns), so a
-  // lane holds 4 consecutive j of one row r and stores them as one float4
-  const int r = rb * kRowsPerBlock + wv * 16 + i;  // this lane's output row (B operand column)
   const int TJ = H >> 4;
-  f32x4 acc[kMaxH / 16];
-#pragma unroll
-  for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t eb = 0; eb < deg; eb += kEdgeStage) {
-    __syncthreads();
-    for (int x = tid; x < kEdgeStage * (H >> 2); x += kNT) {
+  float* Sn = S + (int64_t)n * w * H;
+  if (deg <= kEdgeStage) {  // common case: stage a once for all row blocks
+    const int ns = (int)deg, ns4 = (ns + 3) & ~3;
+    for (int x = tid; x < ns4 * (H >> 2); x += kNT) {  // padding rows zeroed (0 * garbage = NaN)
       const int e = x / (H >> 2), q = x - e * (H >> 2);
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (eb + e < deg) v = *reinterpret_cast<const f32x4*>(A + (e0 + eb + e) * H + 4 * q);
+      if (e < ns) v = *reinterpret_cast<const f32x4*>(A + (e0 + e) * H + 4 * q);
       *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
     }
     __syncthreads();
+  }
+  for (int rbi = 0; rbi < kOuterRB; ++rbi) {
+    const int rb = blockIdx.x * kOuterRB + rbi;
+    if (rb * kRowsPerBlock >= w) break;
+    // D = S^T tile: D[j][r] = sum_e A[e, j] Z[e, r]  (A op = a columns, B op = Z columns), so a
+    // lane holds 4 consecutive j of one row r and stores them as one float4
+    const int r = rb * kRowsPerBlock + wv * 16 + i;  // this lane's output row
+    f32x4 acc[kMaxH / 16];
 #pragma unroll
-    for (int s = 0; s < kEdgeStage / 4; ++s) {
-      const int el = 4 * s + kk;
-      const int64_t e = eb + el;
-      const float zv = (e < deg && r < w) ? Z[(e0 + e) * w + r] : 0.f;
+    for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float zsum = 0.f;  // Sb[n, r]: this lane's edges (k phase kk) of the Z column
+    for (int64_t eb = 0; eb < deg; eb += kEdgeStage) {
+      const int ns = (int)((deg - eb) < kEdgeStage ? (deg - eb) : kEdgeStage);
+      const int ns4 = (ns + 3) & ~3;
+      if (deg > kEdgeStage) {
+        __syncthreads();
+        for (int x = tid; x < ns4 * (H >> 2); x += kNT) {
+          const int e = x / (H >> 2), q = x - e * (H >> 2);
+          f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (e < ns) v = *reinterpret_cast<const f32x4*>(A + (e0 + eb + e) * H + 4 * q);
+          *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
+        }
+        __syncthreads();
+      }
+      for (int s = 0; s < (ns4 >> 2); ++s) {
+        const int el = 4 * s + kk;
+        const float zv = (el < ns && r < w) ? Z[(e0 + eb + el) * w + r] : 0.f;
+        zsum += zv;
+#pragma unroll
+        for (int t = 0; t < kMaxH / 16; ++t)
+          if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zv, acc[t], 0, 0, 0);
+      }
+    }
+    if (r < w) {  // streaming stores: S (GBs per chunk) is consumed by the next GEMM from HBM
 #pragma unroll
       for (int t = 0; t < kMaxH / 16; ++t)
-        if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zv, acc[t], 0, 0, 0);
+        if (t < TJ)
+          *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
     }
-  }
-  float* Sn = S + (int64_t)n * w * H;
-  if (r < w) {
-#pragma unroll
-    for (int t = 0; t < kMaxH / 16; ++t)
-      if (t < TJ) *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
-  }
-  if (tid < kRowsPerBlock) {
-    const int row = rb * kRowsPerBlock + tid;
-    if (row < w) {
-      float a = 0.f;
-      for (int64_t e = 0; e < deg; ++e) a += Z[(e0 + e) * w + row];
-      Sb[(int64_t)n * w + row] = a;
-    }
+    zsum += __shfl_xor(zsum, 16);
+    zsum += __shfl_xor(zsum, 32);
+    if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
   }
 }
 
@@ -231,7 +248,7 @@ int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
   GMP_CHECK_ARG(eoff && Z && A && S && Sb);
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0);
   if (n_recv > 65535) return GMP_ERR_UNSUPPORTED;  // grid.y limit: caller chunks receivers
-  const dim3 grid((unsigned)ceil_div(w, kRowsPerBlock), (unsigned)n_recv);
+  const dim3 grid((unsigned)ceil_div(w, kRowsPerBlock * kOuterRB), (unsigned)n_recv);
   tp_node_outer_kernel<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb);
   return launch_status();
 }
