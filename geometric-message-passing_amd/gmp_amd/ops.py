@@ -261,7 +261,9 @@ def edge_outer_sum_rect(A, B):
                                 cs[m0:m0 + 128] if n0 == 0 else None)
             if not ok:
                 return None
-    return C[:m, :n], cs[:m]
+    if (mp, np_) != (m, n):
+        return C[:m, :n].contiguous(), cs[:m]
+    return C, cs
 
 
 # ----------------------------------------------------------------------------------- deferred
@@ -295,7 +297,8 @@ def _flush_deferred():
     for p, g in _PENDING:
         g.record_stream(main)
         if p.grad is None:
-            p.grad = g
+            # AccumulateGrad's layout contract: a dense gradient with the parameter's strides
+            p.grad = g if g.stride() == p.stride() else g.contiguous()
         else:
             p.grad.add_(g)
     _PENDING.clear()
