@@ -5,6 +5,8 @@
 // Split-K over workgroups (each a contiguous edge range), f32 MFMA 16x16x4 with the edge index
 // as the MFMA k dimension, partial slabs in a workspace and an ordered second pass (bitwise
 // deterministic; no atomics).  HBM-bound: reads A and B once.
+#include <stdlib.h>
+
 #include "gmp_common.h"
 
 namespace gmp {
@@ -321,6 +323,325 @@ __global__ __launch_bounds__(kT, OCC) void outer_sum_rect_kernel(
   }
 }
 
+// ------------------------------------------------------------------ f32 through three bf16 planes
+// The edge reduction runs on the bf16 MFMA (16x the f32 MFMA rate on gfx950) without giving up
+// f32 accuracy: every f32 operand is split exactly into three bf16 planes x = x0 + x1 + x2
+// (RNE splits: |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|, each product of two planes exact in the f32
+// accumulator) and the six partial products of order <= 2^-16 are accumulated,
+//     C += A2 B0 + A1 B1 + A0 B2 + A1 B0 + A0 B1 + A0 B0,
+// dropping A1 B2, A2 B1, A2 B2 (<= 2^-26 |a b| together).  Measured error vs fp64
+// (tests/test_gpu_wgrad.py, K = 1M): 1.2e-8 of sum |a b| per entry, 2x the f32-MFMA split-K
+// kernel's, 20x below rocBLAS's f32 GEMM's (f32 unit roundoff: 6e-8).
+// Six 16x16x32 bf16 MFMAs (16 cycles each) replace eight 16x16x4 f32 MFMAs (32 cycles each) per
+// 32 edges x 16 x 16 outputs: 2.7x less matrix time, so the kernel becomes HBM-bound.
+//
+// Layout: 512 threads (8 waves, a WM x WN grid of RT x CT output tiles of 16 x 16 each), one
+// 32-edge stage per MFMA k step.  A thread loads a (4 edges x 4 channels) unit of A or B with
+// four 16-byte loads (8 lanes cover 128 contiguous bytes of a row), splits it and writes each
+// channel's 4 edges per plane as 8 bytes into an LDS image [plane][channel][32 edges] of 64-byte
+// rows whose 16-byte chunk q sits at q ^ ((row >> 1) & 3): 8 lanes fill one row per ds_write_b64
+// and the MFMA operand read (lane: channel l & 15, edges 8(l >> 4) .. +7) is one conflict-free
+// ds_read_b128.  Loads run PD stages ahead in a register ring (branch-free: counted vmcnt
+// waits); two LDS stages.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int kXT = 512;  // threads (8 waves)
+constexpr int kXK = 32;   // edges per stage (= the bf16 MFMA k)
+
+__device__ __forceinline__ void split3(f32x2 x, unsigned& h, unsigned& m, unsigned& l) {
+  const bf16x2 bh = __builtin_convertvector(x, bf16x2);
+  const f32x2 r1 = x - __builtin_convertvector(bh, f32x2);   // exact
+  const bf16x2 bm = __builtin_convertvector(r1, bf16x2);
+  const f32x2 r2 = r1 - __builtin_convertvector(bm, f32x2);  // exact, <= 8 significant bits
+  const bf16x2 bl = __builtin_convertvector(r2, bf16x2);     // exact
+  h = __builtin_bit_cast(unsigned, bh);
+  m = __builtin_bit_cast(unsigned, bm);
+  l = __builtin_bit_cast(unsigned, bl);
+}
+__device__ __forceinline__ int xoff(int row, int chunk) {
+  return row * 64 + 16 * (chunk ^ ((row >> 1) & 3));
+}
+
+template <int RT, int CT, int PRO, int NL, int PD = (NL == 1 ? 4 : 2)>
+__global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
+    const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
+    int64_t lda, int64_t ldb, int64_t k_per_block, float* __restrict__ partial,
+    const float* __restrict__ bw, const float* __restrict__ bb, int WN) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smx[];
+  const int R = M + N;  // LDS rows per plane: A channels, then B channels
+  const int PLANE = (R + 4) * 64, STAGE = 3 * PLANE;  // + 4 rows written by idle loader lanes
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar tile branches
+  const int li = lane & 15, g = lane >> 4;
+  const int wm = w / WN, wn = w - (w / WN) * WN;
+  const int TM = M >> 4, TN = N >> 4;
+  const int64_t k0 = (int64_t)blockIdx.x * k_per_block;
+  const int64_t k1 = (k0 + k_per_block < K) ? k0 + k_per_block : K;
+
+  f32x4 acc[RT][CT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // loader units u = tid + q * kXT: [0, UA) A units, [UA, UA + UB) B units, each range padded
+  // to whole waves (a wave loads from one operand); unit v of an operand: edge quad v % 8,
+  // channel group v / 8
+  const int UA = (2 * M + 63) & ~63, UB = (2 * N + 63) & ~63;
+  int ucg[NL], ueq[NL], lrow[NL];
+  bool uok[NL], isA[NL];
+  f32x4 pw[NL], pb[NL], csum[NL];
+#pragma unroll
+  for (int q = 0; q < NL; ++q) {
+    const int u = tid + q * kXT;
+    isA[q] = 64 * w + q * kXT < UA;  // wave-uniform by the padding
+    const int v = isA[q] ? u : u - UA;
+    uok[q] = isA[q] ? v < 2 * M : (v < 2 * N && u < UA + UB);
+    ueq[q] = uok[q] ? (v & 7) : 0;   // edge quad fastest: 8 lanes fill one 64-B LDS row
+    ucg[q] = uok[q] ? (v >> 3) : 0;  // (conflict-free ds_write_b64), 128-B global row runs
+    // idle lanes load zeros (out-of-range offset) and write them to the spare rows R .. R+3
+    lrow[q] = !uok[q] ? R : (isA[q] ? 4 * ucg[q] : M + 4 * ucg[q]);
+    csum[q] = pw[q] = pb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (PRO != 0 && uok[q] && !isA[q]) {
+      pw[q] = *reinterpret_cast<const f32x4*>(bw + 4 * ucg[q]);
+      pb[q] = *reinterpret_cast<const f32x4*>(bb + 4 * ucg[q]);
+    }
+  }
+  // global -> register ring, PD stages ahead.  Every load is issued (rows clamped to the
+  // block's last row, idle lanes read row k0) and masked to zero in stash: no branches, so the
+  // compiler's vmcnt waits are counted
+  const float* ubase[NL];
+  int64_t uld[NL];
+#pragma unroll
+  for (int q = 0; q < NL; ++q) {
+    uld[q] = isA[q] ? lda : ldb;
+    ubase[q] = (isA[q] ? A : B) + 4 * ucg[q];
+  }
+  f32x4 ring[PD][NL][4];
+  auto fetch = [&](f32x4 (&reg)[NL][4], int st) {
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int64_t k = k0 + st * kXK + 4 * ueq[q] + j;
+        k = k < k1 ? k : k1 - 1;
+        reg[q][j] = *reinterpret_cast<const f32x4*>(ubase[q] + k * uld[q]);
+      }
+    }
+  };
+  auto stash = [&](f32x4 (&reg)[NL][4], unsigned char* buf, int st) {
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool valid = uok[q] && k0 + st * kXK + 4 * ueq[q] + j < k1;
+        const f32x4 y = (PRO != 0 && !isA[q]) ? prologue<PRO>(reg[q][j], pw[q], pb[q]) : reg[q][j];
+        reg[q][j] = valid ? y : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (isA[q]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) csum[q] += reg[q][j];
+      }
+      const int eq = ueq[q];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        unsigned h0, m0, l0, h1, m1, l1;
+        split3(f32x2{reg[q][0][c], reg[q][1][c]}, h0, m0, l0);
+        split3(f32x2{reg[q][2][c], reg[q][3][c]}, h1, m1, l1);
+        const int off = xoff(lrow[q] + c, eq >> 1) + 8 * (eq & 1);
+        *reinterpret_cast<u32x2*>(buf + off) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(buf + PLANE + off) = u32x2{m0, m1};
+        *reinterpret_cast<u32x2*>(buf + 2 * PLANE + off) = u32x2{l0, l1};
+      }
+    }
+  };
+  auto compute = [&](const unsigned char* buf) {
+    bf16x8 a[RT][3];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int tm = wm * RT + r;
+      if (tm < TM) {
+        const int off = xoff(16 * tm + li, g);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[r][p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int tn = wn * CT + c;
+      if (tn < TN) {
+        const int off = xoff(M + 16 * tn + li, g);
+        bf16x8 b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          if (wm * RT + r < TM) {
+            f32x4 t = acc[r][c];
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][2], b[0], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[1], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[2], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[0], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[1], t, 0, 0, 0);
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[0], t, 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+
+  // stages rounded up to whole ring turns and every fetch / stash unconditional (stages past
+  // the block's rows load zeros and add nothing): the same loads are in flight at every wait,
+  // so the compiler's vmcnt waits are counted, PD - 1 stages deep
+  const int nst = k1 > k0 ? (int)((k1 - k0 + kXK - 1) / kXK) : 0;
+  const int nst_pad = (nst + PD - 1) / PD * PD;
+  if (nst > 0) {
+#pragma unroll
+    for (int j = 0; j < PD; ++j) fetch(ring[j], j);
+    stash(ring[0], smx, 0);
+  }
+  __syncthreads();
+  for (int s0 = 0; s0 < nst_pad; s0 += PD) {
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      const int st = s0 + j;
+      fetch(ring[j], st + PD);  // slot j was stashed for stage st
+      compute(smx + (st & 1) * STAGE);
+      stash(ring[(j + 1) % PD], smx + ((st + 1) & 1) * STAGE, st + 1);
+      __syncthreads();
+    }
+  }
+
+  // C/D map of 16x16x32: col = lane & 15, row = 4 * (lane >> 4) + r
+  float* out = partial + (int64_t)blockIdx.x * ((int64_t)M * N + M);
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int tm = wm * RT + r, tn = wn * CT + c;
+      if (tm < TM && tn < TN) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          out[(int64_t)(16 * tm + 4 * g + q) * N + 16 * tn + li] = acc[r][c][q];
+      }
+    }
+  // colsum(A): the 8 edge quads of a channel group added in quad order (deterministic)
+  float* scs = reinterpret_cast<float*>(smx);  // [8][M], after the loop's final barrier
+#pragma unroll
+  for (int q = 0; q < NL; ++q) {
+    if (!uok[q] || !isA[q]) continue;
+    float* d = scs + ueq[q] * M + 4 * ucg[q];
+    d[0] = csum[q][0];
+    d[1] = csum[q][1];
+    d[2] = csum[q][2];
+    d[3] = csum[q][3];
+  }
+  __syncthreads();
+  for (int m = tid; m < M; m += kXT) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += scs[e * M + m];
+    out[(int64_t)M * N + m] = s;
+  }
+}
+
+// (RT, CT) tile shape per wave for an M x N problem: the first of the compiled shapes whose
+// wave grid fits in 8 waves; returns the index into kX3 or -1
+struct X3Shape { int rt, ct; };
+constexpr X3Shape kX3[] = {{1, 1}, {1, 2}, {2, 2}, {2, 4}, {2, 5}};
+int x3_pick(int64_t m, int64_t n, int* wn) {
+  const int64_t TM = m / 16, TN = n / 16;
+  for (int i = 0; i < 5; ++i) {
+    const int64_t WM = ceil_div(TM, (int64_t)kX3[i].rt), WN = ceil_div(TN, (int64_t)kX3[i].ct);
+    if (WM * WN <= kXT / 64) {
+      *wn = (int)WN;
+      return i;
+    }
+  }
+  return -1;
+}
+// 1: the f32-MFMA kernels (A/B and numerics studies); initial value from GMP_WGRAD_F32_MFMA,
+// changed by gmp_wgrad_set_f32_mfma
+int g_wgrad_mode = -1;
+bool wgrad_f32_mfma() {
+  if (g_wgrad_mode < 0) {
+    const char* e = getenv("GMP_WGRAD_F32_MFMA");
+    g_wgrad_mode = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return g_wgrad_mode == 1;
+}
+int64_t x3_blocks_for(int64_t K) {
+  int64_t g = (int64_t)device_cu_count();  // one 8-wave workgroup per CU (LDS ~100 KB)
+  const int64_t min_per = 4 * kXK;
+  if (g * min_per > K) g = ceil_div(K, min_per);
+  return g < 1 ? 1 : g;
+}
+
+// C (m x n, row stride ldc) = A^T pro(B), colsum(A): split-K over x3 blocks + ordered sums.
+// Returns GMP_ERR_UNSUPPORTED for shapes outside the compiled tilings.
+int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
+                        const float* B, int64_t ldb, int pro, const float* bw, const float* bb,
+                        float* C, int64_t ldc, float* colsum_A, void* workspace, hipStream_t s) {
+  // narrow products (m n < 4096) stay on the f32-MFMA kernels: too little matrix work per
+  // loaded byte for the split's VALU and LDS staging to pay (measured: 16 x 128, 48 x 48 slower)
+  if (m * n < 4096) return GMP_ERR_UNSUPPORTED;
+  int wn = 0;
+  const int shape = x3_pick(m, n, &wn);
+  const int64_t R = m + n;
+  if (shape < 0 || R > 412) return GMP_ERR_UNSUPPORTED;  // 2 stages x 3 planes x (R+4) x 64 B
+  GMP_CHECK_ARG(pro == 0 || ((reinterpret_cast<uintptr_t>(bw) | reinterpret_cast<uintptr_t>(bb)) % 16 == 0));
+  const int64_t units = ((2 * m + 63) & ~63) + ((2 * n + 63) & ~63);
+  if (units > 2 * kXT) return GMP_ERR_UNSUPPORTED;
+  const int nl = units <= kXT ? 1 : 2;
+  const int64_t G = x3_blocks_for(K);
+  const int64_t per = ceil_div(ceil_div(K, G), kXK) * kXK;
+  const int64_t Gr = ceil_div(K, per);
+  float* part = reinterpret_cast<float*>(workspace);
+  const size_t smem = (size_t)2 * 3 * (R + 4) * 64;
+  int rc = 0;
+#define GMP_X3(RT, CT, PP, NL)                                                                \
+  {                                                                                           \
+    auto k = outer_sum_x3_kernel<RT, CT, PP, NL>;                                             \
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                   \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                            (int)smem))))                                     \
+      return rc;                                                                              \
+    k<<<(unsigned)Gr, kXT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per, part, bw, bb,  \
+                                      wn);                                                    \
+  }
+#define GMP_X3_NL(RT, CT, PP) \
+  if (nl == 1) GMP_X3(RT, CT, PP, 1) else GMP_X3(RT, CT, PP, 2)
+#define GMP_X3_PRO(RT, CT)                   \
+  if (pro == 0) { GMP_X3_NL(RT, CT, 0) }     \
+  else if (pro == 1) { GMP_X3_NL(RT, CT, 1) } \
+  else { GMP_X3_NL(RT, CT, 2) }
+  switch (shape) {
+    case 0: GMP_X3_PRO(1, 1) break;
+    case 1: GMP_X3_PRO(1, 2) break;
+    case 2: GMP_X3_PRO(2, 2) break;
+    case 3: GMP_X3_PRO(2, 4) break;
+    default: GMP_X3_PRO(2, 5) break;
+  }
+#undef GMP_X3_PRO
+#undef GMP_X3_NL
+#undef GMP_X3
+  rc = launch_status();
+  if (rc) return rc;
+  const int64_t X = m * n + m;
+  const int64_t NC = ceil_div(Gr, kGC);
+  float* l1 = part + Gr * X;
+  sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
+  rc = launch_status();
+  if (rc) return rc;
+  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, m * n, n,
+                                                             ldc);
+  return launch_status();
+}
+
 // capacity bucket for (M, N): returns 0 if unsupported
 // Tile bucket of an M x N problem: the smallest compiled (MR, MC) covering the per-wave tile
 // counts (the MFMA stream is branch-free, so oversized buckets cost real MFMAs), and the
@@ -354,6 +675,12 @@ using namespace gmp;
 
 extern "C" {
 
+int gmp_wgrad_set_f32_mfma(int on) {
+  const int prev = wgrad_f32_mfma() ? 1 : 0;
+  g_wgrad_mode = on ? 1 : 0;
+  return prev;
+}
+
 size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d) {
   const int64_t G = blocks_for(K);
   return (size_t)(G + ceil_div(G, kGC)) * (size_t)(d * d + d) * sizeof(float);
@@ -377,6 +704,11 @@ static int outer_sum_launch(int64_t K, int64_t d, const float* A, int64_t lda, c
   GMP_CHECK_ARG(pro == 0 || (reinterpret_cast<uintptr_t>(bw) % 16 == 0 &&
                              reinterpret_cast<uintptr_t>(bb) % 16 == 0));
   if (workspace_bytes < gmp_edge_outer_sum_workspace_size(K, d)) return GMP_ERR_WORKSPACE;
+  if (!wgrad_f32_mfma()) {
+    const int rc = outer_sum_x3_launch(K, d, d, A, lda, B, ldb, pro, bw, bb, C, ldc, colsum_A,
+                                       workspace, s);
+    if (rc != GMP_ERR_UNSUPPORTED) return rc;
+  }
   const int64_t G = blocks_for(K);
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
@@ -450,6 +782,11 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
   GMP_CHECK_ARG(A && B && workspace);
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0);
   if (workspace_bytes < gmp_edge_outer_sum_rect_workspace_size(K, m, n)) return GMP_ERR_WORKSPACE;
+  if (!wgrad_f32_mfma()) {
+    const int rc2 = outer_sum_x3_launch(K, m, n, A, lda, B, ldb, 0, nullptr, nullptr, C, ldc,
+                                        colsum_A, workspace, s);
+    if (rc2 != GMP_ERR_UNSUPPORTED) return rc2;
+  }
   const int64_t G = rect_blocks_for(K);
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);

@@ -157,9 +157,14 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
  * mlp_pos backward; replaces torch's dW = dpre^T x over E rows):
  *   C (d x d) = A^T B with A (K, d), B (K, d) row-major fp32, K = edges;
  *   colsum_A (d) = sum_k A[k, :] (the bias gradient; may be NULL).
- * Split-K over workgroups with f32 MFMA, partial slabs in `workspace` and an ordered second
- * pass: bitwise deterministic.  d in {32, 64, 128}.
+ * Split-K over workgroups, partial slabs in `workspace` and an ordered second pass: bitwise
+ * deterministic.  d in {32, 64, 128}.  Arithmetic (all outer-sum entry points below): f32
+ * operands split exactly into three bf16 planes on the bf16 MFMA with f32 accumulation, the
+ * six partial products of order <= 2^-16 summed (error vs fp64 <= 2^-26 of sum |a b|, within
+ * 2x of the f32-MFMA kernels', below rocBLAS f32 GEMM's); gmp_wgrad_set_f32_mfma(1) (or GMP_WGRAD_F32_MFMA=1 at load) selects the f32-MFMA
+ * kernels instead, returns the previous setting.
  * ------------------------------------------------------------------------------------------ */
+int gmp_wgrad_set_f32_mfma(int on);
 size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d);
 int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
                            float* colsum_A, void* workspace, size_t workspace_bytes,
