@@ -351,6 +351,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 constexpr int kXT = 512;  // threads (8 waves)
 constexpr int kXK = 32;   // edges per stage (= the bf16 MFMA k)
+constexpr int kXPad = 64; // LDS padding rows per plane (>= 16 * (WN * CT - TN) of any tiling)
 
 __device__ __forceinline__ void split3(f32x2 x, unsigned& h, unsigned& m, unsigned& l) {
   const bf16x2 bh = __builtin_convertvector(x, bf16x2);
@@ -373,7 +374,8 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
     const float* __restrict__ bw, const float* __restrict__ bb, int WN) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smx[];
   const int R = M + N;  // LDS rows per plane: A channels, then B channels
-  const int PLANE = (R + 4) * 64, STAGE = 3 * PLANE;  // + 4 rows written by idle loader lanes
+  // + 64 padding rows: written by idle loader lanes (row R), read by the ragged tiles
+  const int PLANE = (R + kXPad) * 64, STAGE = 3 * PLANE;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar tile branches
   const int li = lane & 15, g = lane >> 4;
@@ -442,10 +444,8 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
         const f32x4 y = (PRO != 0 && !isA[q]) ? prologue<PRO>(reg[q][j], pw[q], pb[q]) : reg[q][j];
         reg[q][j] = valid ? y : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (isA[q]) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) csum[q] += reg[q][j];
-      }
+      for (int j = 0; j < 4; ++j) csum[q] += reg[q][j];  // used for A units only
       const int eq = ueq[q];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -459,37 +459,32 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
       }
     }
   };
+  // branch-free: tiles past TM / TN (ragged wave grids) multiply rows of the LDS padding or of
+  // the other operand and are never stored, so compute and stash form one basic block and the
+  // scheduler can overlap the MFMAs with the next stage's split
   auto compute = [&](const unsigned char* buf) {
     bf16x8 a[RT][3];
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
-      const int tm = wm * RT + r;
-      if (tm < TM) {
-        const int off = xoff(16 * tm + li, g);
+      const int off = xoff(16 * (wm * RT + r) + li, g);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) a[r][p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
-      }
+      for (int p = 0; p < 3; ++p) a[r][p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
     }
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
-      const int tn = wn * CT + c;
-      if (tn < TN) {
-        const int off = xoff(M + 16 * tn + li, g);
-        bf16x8 b[3];
+      const int off = xoff(M + 16 * (wn * CT + c) + li, g);
+      bf16x8 b[3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
+      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
-          if (wm * RT + r < TM) {
-            f32x4 t = acc[r][c];
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][2], b[0], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[1], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[2], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[0], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[1], t, 0, 0, 0);
-            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[0], t, 0, 0, 0);
-          }
-        }
+      for (int r = 0; r < RT; ++r) {
+        f32x4 t = acc[r][c];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][2], b[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[1], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[2], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[1], t, 0, 0, 0);
+        acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[0], t, 0, 0, 0);
       }
     }
   };
@@ -586,13 +581,15 @@ int64_t x3_blocks_for(int64_t K) {
 int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
                         const float* B, int64_t ldb, int pro, const float* bw, const float* bb,
                         float* C, int64_t ldc, float* colsum_A, void* workspace, hipStream_t s) {
-  // narrow products (m n < 4096) stay on the f32-MFMA kernels: too little matrix work per
-  // loaded byte for the split's VALU and LDS staging to pay (measured: 16 x 128, 48 x 48 slower)
-  if (m * n < 4096) return GMP_ERR_UNSUPPORTED;
+  // Narrow products (m n < 4096) stay on the f32-MFMA kernels: too little matrix work per
+  // loaded byte for the split's VALU and LDS staging to pay (measured: 16 x 128, 48 x 48 slower).
+  // Node-level sums (K ~ 50k rows) stay there too: a few stages per block, and the 1-block-per-
+  // CU LDS footprint keeps them from sharing CUs with the concurrent main-stream kernels.
+  if (m * n < 4096 || K < 262144) return GMP_ERR_UNSUPPORTED;
   int wn = 0;
   const int shape = x3_pick(m, n, &wn);
   const int64_t R = m + n;
-  if (shape < 0 || R > 412) return GMP_ERR_UNSUPPORTED;  // 2 stages x 3 planes x (R+4) x 64 B
+  if (shape < 0 || R + kXPad > 416) return GMP_ERR_UNSUPPORTED;  // 2 x 3 x (R + pad) x 64 B
   GMP_CHECK_ARG(pro == 0 || ((reinterpret_cast<uintptr_t>(bw) | reinterpret_cast<uintptr_t>(bb)) % 16 == 0));
   const int64_t units = ((2 * m + 63) & ~63) + ((2 * n + 63) & ~63);
   if (units > 2 * kXT) return GMP_ERR_UNSUPPORTED;
@@ -601,7 +598,7 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   const int64_t per = ceil_div(ceil_div(K, G), kXK) * kXK;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-  const size_t smem = (size_t)2 * 3 * (R + 4) * 64;
+  const size_t smem = (size_t)2 * 3 * (R + kXPad) * 64;
   int rc = 0;
 #define GMP_X3(RT, CT, PP, NL)                                                                \
   {                                                                                           \

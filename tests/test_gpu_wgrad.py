@@ -23,7 +23,7 @@ def _err(C, ref, A, B):
 @pytest.mark.parametrize("m,n", [(16, 16), (16, 48), (48, 48), (16, 128), (128, 16), (16, 144),
                                  (48, 144), (128, 48), (128, 80), (128, 128), (128, 144),
                                  (32, 32), (64, 64), (32, 128)])
-@pytest.mark.parametrize("K", [5, 4097, 300_001])
+@pytest.mark.parametrize("K", [5, 4097, 300_001, 1_000_003])
 def test_outer_sum_split_matches_fp64(m, n, K):
     from gmp_amd import ops
     g = torch.Generator().manual_seed(m * 1000 + n + K)
@@ -45,7 +45,7 @@ def test_outer_sum_strided_blocks():
     """column blocks of wider tensors (lda, ldb, ldc > width) on the split path"""
     from gmp_amd import ops
     g = torch.Generator().manual_seed(7)
-    K = 77_777
+    K = 300_007
     A = torch.randn(K, 272, generator=g).to(DEV)
     B = torch.randn(K, 200, generator=g).to(DEV)
     C = torch.zeros(300, 260, device=DEV)
@@ -59,7 +59,7 @@ def test_outer_sum_strided_blocks():
 def test_outer_sum_act_prologue(act):
     from gmp_amd import ops
     g = torch.Generator().manual_seed(11)
-    K, d = 123_457, 128
+    K, d = 400_009, 128
     A = torch.randn(K, d, generator=g)
     X = torch.randn(K, d, generator=g)
     w, b = torch.randn(d, generator=g), torch.randn(d, generator=g)
