@@ -216,13 +216,20 @@ class GvpLayerFn(torch.autograd.Function):
 
 
 class GvpMsg0Fn(torch.autograd.Function):
-    """First message GVP (gmp_gvp_msg0_{fwd,bwd}_f32) from node projections P, Q."""
+    """First message GVP (gmp_gvp_msg0_{fwd,bwd}_f32) from node projections P, Q.  Takes the
+    leaf parameters (Ws0 = ws.weight, bias, Wv = wv.weight, wsv.*, Wh0 = wh.weight) and slices /
+    pads the per-edge blocks itself, so their weight gradients are leaf gradients: computed on
+    the side stream and accumulated at the end of the backward pass (ops.side_work)."""
 
     @staticmethod
-    def forward(ctx, P, Q, es, ev, We, Wn, b, Wv, Wsv, bsv, wev, send_csr, recv_csr, ei):
+    def forward(ctx, P, Q, es, ev, Ws0, b, Wv, Wsv, bsv, Wh0, send_csr, recv_csr, ei):
         lib = _lib.load()
         P, Q, es, ev = (ops._f32c(t) for t in (P, Q, es, ev))
-        W = [ops._f32c(t) for t in (We, Wn, b, Wv, Wsv, bsv, wev)]
+        pad = torch.nn.functional.pad
+        vi = Wv.shape[1]  # 2 vi + ve = 33
+        W = [ops._f32c(t) for t in (Ws0[:, 128:160], pad(Ws0[:, 288:288 + vi], (0, 48 - vi)),
+                                    b, pad(Wv, (0, 48 - vi)), Wsv, bsv,
+                                    pad(Wh0[:, 16], (0, 48 - Wh0.shape[0])))]
         E = es.shape[0]
         send, recv = ei[0].contiguous(), ei[1].contiguous()
         s_out = torch.empty((E, 128), dtype=torch.float32, device=P.device)
@@ -233,6 +240,7 @@ class GvpMsg0Fn(torch.autograd.Function):
                                            ops._p(s_out), ops._p(v_out), ops._stream()),
                   "gmp_gvp_msg0_fwd_f32")
         ctx.csrs = (send_csr, recv_csr)
+        ctx.leaves = (Ws0, b, Wv, Wsv, bsv, Wh0)
         ctx.save_for_backward(P, Q, es, ev, send, recv, *W)
         return s_out, v_out
 
@@ -241,6 +249,7 @@ class GvpMsg0Fn(torch.autograd.Function):
         lib = _lib.load()
         P, Q, es, ev, send, recv, *W = ctx.saved_tensors
         send_csr, recv_csr = ctx.csrs
+        Ws0, b, Wv, Wsv, bsv, Wh0 = ctx.leaves
         E = es.shape[0]
         ds = ops._f32c(ds) if ds is not None else torch.zeros((E, 128), device=P.device)
         dv = ops._f32c(dv) if dv is not None else torch.zeros((E, 16, 3), device=P.device)
@@ -257,19 +266,57 @@ class GvpMsg0Fn(torch.autograd.Function):
                                            ops._p(dgate), ops._p(vn), ops._p(vh), ops._p(dvpre),
                                            ops._p(dvh), ops._p(des), ops._p(dev), ops._stream()),
                   "gmp_gvp_msg0_bwd_f32")
+        # weight gradients (edge outer sums) on the side stream, as full-size leaf gradients
+        with ops.side_work(dspre, es, vn, dgate, spre, dvpre, vh, ev, dvh) as sw:
+            vi = Wv.shape[1]
+            dWe, db = _osum(dspre, es)
+            dWn, _ = _osum(dspre, vn)
+            dWsv, dbsv = _osum(dgate, spre)
+            dWv = _diag3(_osum(dvpre, vh)[0], 16, 48)
+            M, _ = _osum(torch.nn.functional.pad(ev, (0, 13)), dvh)  # (16, 144): rows x = 0..2
+            dwev = M[:3].reshape(3, 48, 3).diagonal(dim1=0, dim2=2).sum(-1)
+            gWs0 = torch.zeros_like(Ws0)
+            gWs0[:, 128:160] = dWe
+            gWs0[:, 288:288 + vi] = dWn[:, :vi]
+            gWh0 = torch.zeros_like(Wh0)
+            gWh0[:, 16] = dwev[:Wh0.shape[0]]
+            grads = (gWs0, db, dWv[:, :vi].contiguous(), dWsv, dbsv, gWh0)
         # node-projection gradients: deterministic segmented sums at the senders / receivers
         dPa, _ = ops.segment_reduce(dspre, send_csr, "sum")
         dPb, _ = ops.segment_reduce(dspre, recv_csr, "sum")
         dQa, _ = ops.segment_reduce(dvh, send_csr, "sum")
         dQb, _ = ops.segment_reduce(dvh, recv_csr, "sum")
-        dWe, db = _osum(dspre, es)
-        dWn, _ = _osum(dspre, vn)
-        dWsv, dbsv = _osum(dgate, spre)
-        dWv = _diag3(_osum(dvpre, vh)[0], 16, 48)
-        M, _ = _osum(torch.nn.functional.pad(ev, (0, 13)), dvh)  # (16, 144): rows x = 0..2
-        dwev = M[:3].reshape(3, 48, 3).diagonal(dim1=0, dim2=2).sum(-1)
-        return (torch.cat([dPa, dPb], 1), torch.cat([dQa, dQb], 1).view(-1, 288), des, dev,
-                dWe, dWn, db, dWv, dWsv, dbsv, dwev, None, None, None)
+        return ((torch.cat([dPa, dPb], 1), torch.cat([dQa, dQb], 1).view(-1, 288), des, dev)
+                + sw.deliver(ctx.needs_input_grad, 4, ctx.leaves, grads) + (None, None, None))
+
+
+class NodeProjFn(torch.autograd.Function):
+    """P = s [Ws0[:, :si] ; Ws0[:, si + se : 2 si + se]]^T (N, 2 so): the sender / receiver
+    scalar blocks of the first message GVP's Linear applied once per node.  dWs0 (a K = N
+    reduction) on the side stream by the outer-sum kernel, deferred like the edge weights."""
+
+    @staticmethod
+    def forward(ctx, s, Ws0, si, se):
+        Wcat = torch.cat([Ws0[:, :si], Ws0[:, si + se:2 * si + se]], 0)
+        ctx.save_for_backward(s, Wcat)
+        ctx.Ws0, ctx.si, ctx.se = Ws0, si, se
+        return s.matmul(Wcat.t())
+
+    @staticmethod
+    def backward(ctx, dP):
+        s, Wcat = ctx.saved_tensors
+        Ws0, si, se = ctx.Ws0, ctx.si, ctx.se
+        dP = dP.contiguous()
+        ds = dP.mm(Wcat) if ctx.needs_input_grad[0] else None
+        if not ctx.needs_input_grad[1]:
+            return ds, None, None, None
+        so = Ws0.shape[0]
+        with ops.side_work(dP, s) as sw:
+            dWcat, _ = _osum(dP, s)
+            g = torch.zeros_like(Ws0)
+            g[:, :si] = dWcat[:so]
+            g[:, si + se:2 * si + se] = dWcat[so:]
+        return (ds,) + sw.deliver(ctx.needs_input_grad, 1, (Ws0,), (g,)) + (None, None)
 
 
 class GVPConv(MessagePassing):
@@ -321,25 +368,25 @@ class GVPConv(MessagePassing):
         n = s.shape[0]
         g0, g1, g2 = self.message_func
         Ws0, Wh0 = g0.ws.weight, g0.wh.weight
-        P = s.matmul(torch.cat([Ws0[:, :128], Ws0[:, 160:288]], 0).t())   # (N, 256)
+        P = NodeProjFn.apply(s, Ws0, 128, 32)                                 # (N, 256)
         Qa = torch.einsum("oc,ncx->nox", Wh0[:, :16], v)
         Qb = torch.einsum("oc,ncx->nox", Wh0[:, 17:33], v)
         Q = torch.cat([F.pad(Qa, (0, 0, 0, 15)), F.pad(Qb, (0, 0, 0, 15))], 1).reshape(n, 288)
         es, ev = edge_attr
         ei = edge_index
         send_csr, recv_csr = ops.get_csr(ei[0], n), ops.get_csr(ei[1], n)
-        s1, v1 = GvpMsg0Fn.apply(P, Q, es, ev.reshape(-1, 3), Ws0[:, 128:160],
-                                 F.pad(Ws0[:, 288:321], (0, 15)), g0.ws.bias,
-                                 F.pad(g0.wv.weight, (0, 15)), g0.wsv.weight, g0.wsv.bias,
-                                 F.pad(Wh0[:, 16], (0, 15)), send_csr, recv_csr, ei)
+        s1, v1 = GvpMsg0Fn.apply(P, Q, es, ev.reshape(-1, 3), Ws0, g0.ws.bias, g0.wv.weight,
+                                 g0.wsv.weight, g0.wsv.bias, Wh0, send_csr, recv_csr, ei)
         s2, v2 = GvpLayerFn.apply(s1, v1, g1.ws.weight, g1.ws.bias, g1.wsv.weight, g1.wsv.bias,
                                   g1.wh.weight, g1.wv.weight, True)
         s3, v3 = GvpLayerFn.apply(s2, v2, g2.ws.weight, g2.ws.bias, g2.wsv.weight, g2.wsv.bias,
                                   g2.wh.weight, g2.wv.weight, False)
-        msg = torch.cat([s3, v3.reshape(-1, 48)], 1)
+        # aggregate the scalar and vector channels separately (no concatenated (E, 176) copy
+        # forward, no split copies of its gradient backward)
         reduce = "sum" if self.aggr == "add" else self.aggr
-        agg = ops.SegmentReduceFn.apply(msg, recv_csr, reduce)
-        return _split(agg, self.vo)
+        agg_s = ops.SegmentReduceFn.apply(s3, recv_csr, reduce)
+        agg_v = ops.SegmentReduceFn.apply(v3.reshape(-1, 3 * self.vo), recv_csr, reduce)
+        return agg_s, agg_v.view(-1, self.vo, 3)
 
     def forward(self, x, edge_index, edge_attr):
         x_s, x_v = x

@@ -23,20 +23,24 @@ def _stream():
 # Optional per-kernel timing (bench.py): name -> list of (start, end) HIP events recorded on the
 # stream the kernel is launched on (the current stream).  None = disabled (no overhead).
 KERNEL_TIMERS = None
+KERNEL_TIMER_NAMES = None  # None: every timed region; else only these names (host cost: two
+                           # event records per region, on the launch path)
 
 
 class _timed:
     def __init__(self, name):
         self.name = name
+        self.on = KERNEL_TIMERS is not None and (KERNEL_TIMER_NAMES is None
+                                                 or name in KERNEL_TIMER_NAMES)
 
     def __enter__(self):
-        if KERNEL_TIMERS is not None:
+        if self.on:
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self.ev[0].record()
         return self
 
     def __exit__(self, *exc):
-        if KERNEL_TIMERS is not None:
+        if self.on:
             self.ev[1].record()
             KERNEL_TIMERS.setdefault(self.name, []).append(self.ev)
         return False
@@ -277,6 +281,12 @@ DEFER_WEIGHT_GRADS = True
 _SIDE_STREAMS = {}
 _PENDING = []   # (param, grad) accumulated at the end of the backward pass
 _CB_QUEUED = [False]
+# Main-stream tensors read by side-stream work are kept alive here until the main stream has
+# waited for the side stream (flush / join), then dropped: their blocks go straight back to the
+# main stream's pool, stream-ordered after that wait.  (record_stream instead would hold every
+# such block until the allocator sees the side stream's event complete; with the host running a
+# step ahead it then allocated fresh HBM every step and synchronised the host doing so.)
+_KEEPALIVE = []
 
 
 def _side_stream(device):
@@ -294,6 +304,7 @@ def _flush_deferred():
     main = torch.cuda.current_stream()
     for st in _SIDE_STREAMS.values():
         main.wait_stream(st)
+    _KEEPALIVE.clear()
     for p, g in _PENDING:
         g.record_stream(main)
         if p.grad is None:
@@ -326,8 +337,7 @@ class side_work:
 
     def __exit__(self, *exc):
         self.ctx.__exit__(*exc)
-        for t in self.used:
-            t.record_stream(self.side)
+        _KEEPALIVE.extend(self.used)
         return False
 
     def defer(self, param, grad):
@@ -339,6 +349,7 @@ class side_work:
     def join(self, *results):
         """results are needed on the current stream now (returned through autograd)."""
         self.main.wait_stream(self.side)
+        _KEEPALIVE.clear()
         for r in results:
             if r is not None:
                 r.record_stream(self.main)

@@ -1,5 +1,5 @@
 """Host-side (Python) cost of the EGNN training step (dev tool): cProfile over a few steps of
-bench.py's step, GPU synchronised only at the end.  usage: python scripts/host_profile.py"""
+bench.py's step, GPU synchronised only at the end.  usage: python scripts/host_profile.py [egnn|gvp]"""
 import cProfile
 import os
 import pstats
@@ -17,7 +17,11 @@ from gmp_amd.graph import radius_graph  # noqa: E402
 g = radius_graph(num_nodes=50_000, target_edges=1_000_000, seed=0)
 torch.manual_seed(0)
 dev = torch.device("cuda")
-model = gmp_amd.EGNNModel(num_layers=4, emb_dim=128, in_dim=1, out_dim=1).to(dev)
+if len(sys.argv) > 1 and sys.argv[1] == "gvp":
+    model = gmp_amd.GVPGNNModel(num_layers=4, s_dim=128, v_dim=16, s_dim_edge=32, v_dim_edge=1,
+                                in_dim=1, out_dim=1).to(dev)
+else:
+    model = gmp_amd.EGNNModel(num_layers=4, emb_dim=128, in_dim=1, out_dim=1).to(dev)
 opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=os.environ.get("FUSED", "0") == "1")
 batch = g.to(dev)
 y = torch.randn(1, device=dev)
@@ -46,4 +50,6 @@ for _ in range(5):
     step()
 torch.cuda.synchronize()
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(35)
+st = pstats.Stats(pr)
+st.sort_stats("tottime").print_stats(35)
+st.print_callers("item|synchronize|nonzero|tolist|_local_scalar")
