@@ -39,7 +39,50 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
   const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
   const int TJ = H >> 4;
   float* Sn = S + (int64_t)n * w * H;
-  if (deg <= kEdgeStage) {  // common case: stage a once for all row blocks
+  if (kOuterRB == 1 && deg <= kEdgeStage) {
+    // common case (one edge stage): this lane's Z column values for every k step are loaded
+    // up front, in flight together with the a-row staging — no dependent global load inside the
+    // MFMA loop (the block's latency chain was load -> MFMA per step, ~5 HBM round trips)
+    const int ns = (int)deg, nst = (ns + 3) >> 2;
+    const int r = blockIdx.x * kRowsPerBlock + wv * 16 + i;
+    float zr[kEdgeStage / 4];
+#pragma unroll
+    for (int s = 0; s < kEdgeStage / 4; ++s) {
+      const int el = 4 * s + kk;
+      zr[s] = (el < ns && r < w) ? Z[(e0 + el) * w + r] : 0.f;
+    }
+    for (int x = tid; x < 4 * nst * (H >> 2); x += kNT) {  // padding rows zeroed
+      const int e = x / (H >> 2), q = x - e * (H >> 2);
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e < ns) v = *reinterpret_cast<const f32x4*>(A + (e0 + e) * H + 4 * q);
+      *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
+    }
+    __syncthreads();
+    f32x4 acc[kMaxH / 16];
+#pragma unroll
+    for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float zsum = 0.f;
+#pragma unroll
+    for (int s = 0; s < kEdgeStage / 4; ++s) {
+      if (s < nst) {
+        const int el = 4 * s + kk;
+        zsum += zr[s];
+#pragma unroll
+        for (int t = 0; t < kMaxH / 16; ++t)
+          if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zr[s], acc[t], 0, 0, 0);
+      }
+    }
+    if (r < w) {
+#pragma unroll
+      for (int t = 0; t < kMaxH / 16; ++t)
+        if (t < TJ) *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
+    }
+    zsum += __shfl_xor(zsum, 16);
+    zsum += __shfl_xor(zsum, 32);
+    if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
+    return;
+  }
+  if (deg <= kEdgeStage) {  // stage a once for all row blocks
     const int ns = (int)deg, ns4 = (ns + 3) & ~3;
     for (int x = tid; x < ns4 * (H >> 2); x += kNT) {  // padding rows zeroed (0 * garbage = NaN)
       const int e = x / (H >> 2), q = x - e * (H >> 2);
