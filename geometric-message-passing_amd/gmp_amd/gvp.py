@@ -319,6 +319,43 @@ class NodeProjFn(torch.autograd.Function):
         return (ds,) + sw.deliver(ctx.needs_input_grad, 1, (Ws0,), (g,)) + (None, None)
 
 
+class NodeVecProjFn(torch.autograd.Function):
+    """Q (N, 288) = the sender / receiver vector blocks of the first message GVP's wh applied once
+    per node: Q[n, (48 b + o) * 3 + x] = sum_c Wh0[o, 16 b + b + c] v[n, c, x] (b = 0: columns
+    0..15, b = 1: 17..32; rows o >= 33 zero padding).  One GEMM over the 3N (node, xyz) rows;
+    dWh0 (a K = 3N reduction) on the side stream by the outer-sum kernel, deferred."""
+
+    @staticmethod
+    def forward(ctx, v, Wh0, vi):
+        n, ho = v.shape[0], Wh0.shape[0]
+        Wst = v.new_zeros((96, vi))
+        Wst[:ho] = Wh0[:, :vi]
+        Wst[48:48 + ho] = Wh0[:, vi + 1:2 * vi + 1]
+        vt = v.transpose(1, 2).reshape(3 * n, vi).contiguous()
+        Y = vt.mm(Wst.t())                                   # (3N, 96): rows (n, x)
+        ctx.save_for_backward(vt, Wst)
+        ctx.Wh0, ctx.vi, ctx.n = Wh0, vi, n
+        return Y.view(n, 3, 96).transpose(1, 2).reshape(n, 288)
+
+    @staticmethod
+    def backward(ctx, dQ):
+        vt, Wst = ctx.saved_tensors
+        Wh0, vi, n = ctx.Wh0, ctx.vi, ctx.n
+        dY = dQ.reshape(n, 96, 3).transpose(1, 2).reshape(3 * n, 96).contiguous()
+        dv = None
+        if ctx.needs_input_grad[0]:
+            dv = dY.mm(Wst).view(n, 3, vi).transpose(1, 2)
+        if not ctx.needs_input_grad[1]:
+            return dv, None, None
+        ho = Wh0.shape[0]
+        with ops.side_work(dY, vt) as sw:
+            dW, _ = _osum(dY, vt)                            # (96, vi)
+            g = torch.zeros_like(Wh0)
+            g[:, :vi] = dW[:ho]
+            g[:, vi + 1:2 * vi + 1] = dW[48:48 + ho]
+        return (dv,) + sw.deliver(ctx.needs_input_grad, 1, (Wh0,), (g,)) + (None,)
+
+
 class GVPConv(MessagePassing):
     """gvp_layer.py:246-324."""
 
@@ -369,9 +406,7 @@ class GVPConv(MessagePassing):
         g0, g1, g2 = self.message_func
         Ws0, Wh0 = g0.ws.weight, g0.wh.weight
         P = NodeProjFn.apply(s, Ws0, 128, 32)                                 # (N, 256)
-        Qa = torch.einsum("oc,ncx->nox", Wh0[:, :16], v)
-        Qb = torch.einsum("oc,ncx->nox", Wh0[:, 17:33], v)
-        Q = torch.cat([F.pad(Qa, (0, 0, 0, 15)), F.pad(Qb, (0, 0, 0, 15))], 1).reshape(n, 288)
+        Q = NodeVecProjFn.apply(v, Wh0, 16)                                  # (N, 288)
         es, ev = edge_attr
         ei = edge_index
         send_csr, recv_csr = ops.get_csr(ei[0], n), ops.get_csr(ei[1], n)
