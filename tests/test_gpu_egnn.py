@@ -31,10 +31,16 @@ def _assert_grads(model, ref, rtol=1e-4):
         assert err <= rtol * scale + 1e-6, f"{name}: max|d|={err:.3e} scale={scale:.3e}"
 
 
-@pytest.mark.parametrize("d,act,aggr", [(128, "relu", "sum"), (128, "swish", "mean"),
-                                        (64, "relu", "add"), (32, "swish", "sum")])
-def test_egnn_layer_vs_oracle(d, act, aggr):
+@pytest.mark.parametrize("d,act,aggr,defer", [(128, "relu", "sum", True),
+                                              (128, "swish", "mean", True),
+                                              (64, "relu", "add", True), (32, "swish", "sum", True),
+                                              (128, "swish", "sum", False)])
+def test_egnn_layer_vs_oracle(d, act, aggr, defer, monkeypatch):
+    """defer=False: the weight gradients come back through autograd after a stream join (the
+    DDP configuration) instead of the end-of-backward side-stream accumulation."""
     import gmp_amd
+    from gmp_amd import ops
+    monkeypatch.setattr(ops, "DEFER_WEIGHT_GRADS", defer)
     torch.manual_seed(d)
     g = _graph(400, 6000, seed=d)
     ref = oegnn.EGNNLayer(d, act, "layer", aggr)

@@ -59,12 +59,16 @@ def test_gvp_model_golden(golden):
     _scaled(p.grad, d["grad_pos"], 1e-4, "grad_pos")
 
 
-@pytest.mark.parametrize("fast,edge_linear,fused", [(True, True, True), (True, True, False),
-                                                    (True, False, False), (False, True, False)])
-def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, fused, monkeypatch):
+@pytest.mark.parametrize("fast,edge_linear,fused,defer", [
+    (True, True, True, True), (True, True, True, False), (True, True, False, True),
+    (True, False, False, True), (False, True, False, True)])
+def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, fused, defer, monkeypatch):
+    """defer=False: weight gradients returned through autograd after a stream join (the DDP
+    configuration, dist.wrap_ddp) instead of the end-of-backward side-stream accumulation."""
     import gmp_amd.gvp as g
     from gmp_amd import ops
     monkeypatch.setattr(g, "GVP_FUSED", fused)
+    monkeypatch.setattr(ops, "DEFER_WEIGHT_GRADS", defer)
     # small graphs: force the per-edge Linear path (outer-sum dW) on, or off
     monkeypatch.setattr(ops, "EDGE_LINEAR_MIN_ROWS", 1 if edge_linear else 1 << 62)
     from gmp_amd.graph import radius_graph
