@@ -371,7 +371,9 @@ template <int RT, int CT, int PRO, int NL, int PD = (NL == 1 ? 4 : 2)>
 __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
     const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
     int64_t lda, int64_t ldb, int64_t k_per_block, float* __restrict__ partial,
-    const float* __restrict__ bw, const float* __restrict__ bb, int WN) {
+    const float* __restrict__ bw, const float* __restrict__ bb, int WN,
+    const float* __restrict__ B2, int64_t ldb2, int N1) {
+  // B may be two column blocks [B (N1 columns) | B2 (N - N1 columns)] of different tensors
   extern __shared__ __attribute__((aligned(16))) unsigned char smx[];
   const int R = M + N;  // LDS rows per plane: A channels, then B channels
   // + 64 padding rows: written by idle loader lanes (row R), read by the ragged tiles
@@ -420,8 +422,9 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
   int64_t uld[NL];
 #pragma unroll
   for (int q = 0; q < NL; ++q) {
-    uld[q] = isA[q] ? lda : ldb;
-    ubase[q] = (isA[q] ? A : B) + 4 * ucg[q];
+    const bool second = !isA[q] && 4 * ucg[q] >= N1;
+    uld[q] = isA[q] ? lda : (second ? ldb2 : ldb);
+    ubase[q] = isA[q] ? A + 4 * ucg[q] : (second ? B2 + (4 * ucg[q] - N1) : B + 4 * ucg[q]);
   }
   f32x4 ring[PD][NL][4];
   auto fetch = [&](f32x4 (&reg)[NL][4], int st) {
@@ -580,7 +583,9 @@ int64_t x3_blocks_for(int64_t K) {
 // Returns GMP_ERR_UNSUPPORTED for shapes outside the compiled tilings.
 int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
                         const float* B, int64_t ldb, int pro, const float* bw, const float* bb,
-                        float* C, int64_t ldc, float* colsum_A, void* workspace, hipStream_t s) {
+                        float* C, int64_t ldc, float* colsum_A, void* workspace, hipStream_t s,
+                        const float* B2 = nullptr, int64_t ldb2 = 0, int64_t n1 = -1) {
+  if (n1 < 0) n1 = n;  // single B operand
   // Narrow products (m n < 4096) stay on the f32-MFMA kernels: too little matrix work per
   // loaded byte for the split's VALU and LDS staging to pay (measured: 16 x 128, 48 x 48 slower).
   // Node-level sums (K ~ 50k rows) stay there too: a few stages per block, and the 1-block-per-
@@ -608,7 +613,7 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
                                             (int)smem))))                                     \
       return rc;                                                                              \
     k<<<(unsigned)Gr, kXT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per, part, bw, bb,  \
-                                      wn);                                                    \
+                                      wn, B2, ldb2, (int)n1);                                 \
   }
 #define GMP_X3_NL(RT, CT, PP) \
   if (nl == 1) GMP_X3(RT, CT, PP, 1) else GMP_X3(RT, CT, PP, 2)
@@ -835,6 +840,24 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
 size_t gmp_edge_outer_sum_ex_workspace_size(int64_t K, int64_t m, int64_t n) {
   if (m == n && (m == 32 || m == 64 || m == 128)) return gmp_edge_outer_sum_workspace_size(K, m);
   return gmp_edge_outer_sum_rect_workspace_size(K, m, n);
+}
+
+int gmp_edge_outer_sum_ex2_f32(int64_t K, int64_t m, int64_t n1, int64_t n2, const float* A,
+                               int64_t lda, const float* B1, int64_t ldb1, const float* B2,
+                               int64_t ldb2, float* C, int64_t ldc, float* colsum_A,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  const int64_t n = n1 + n2;
+  GMP_CHECK_ARG(K >= 0 && C && m > 0 && n1 > 0 && n2 > 0 && m % 16 == 0 && n1 % 4 == 0 &&
+                n2 % 4 == 0 && n % 16 == 0);
+  GMP_CHECK_ARG(lda >= m && ldb1 >= n1 && ldb2 >= n2 && ldc >= n && lda % 4 == 0 &&
+                ldb1 % 4 == 0 && ldb2 % 4 == 0);
+  if (K == 0 || wgrad_f32_mfma()) return GMP_ERR_UNSUPPORTED;
+  GMP_CHECK_ARG(A && B1 && B2 && workspace);
+  GMP_CHECK_ARG((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B1) |
+                 reinterpret_cast<uintptr_t>(B2)) % 16 == 0);
+  if (workspace_bytes < gmp_edge_outer_sum_rect_workspace_size(K, m, n)) return GMP_ERR_WORKSPACE;
+  return outer_sum_x3_launch(K, m, n, A, lda, B1, ldb1, 0, nullptr, nullptr, C, ldc, colsum_A,
+                             workspace, as_stream(stream), B2, ldb2, n1);
 }
 
 int gmp_edge_outer_sum_ex_f32(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,

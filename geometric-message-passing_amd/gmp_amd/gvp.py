@@ -205,12 +205,15 @@ class GvpLayerFn(torch.autograd.Function):
                   "gmp_gvp_layer_bwd_f32")
         # weight gradients (edge outer sums) on the side stream, deferred to the end of backward
         with ops.side_work(dspre, s, vn, dgate, spre, dvh, v, dvpre, vh) as sw:
-            dWs_s, dbs = _osum(dspre, s.view(E, 128))
-            dWs_v, _ = _osum(dspre, vn)
+            # dWs = dspre^T [s | vn]: one pass over dspre when the split-plane kernel applies
+            dWs, dbs = torch.empty((128, 144), **f), torch.empty(128, **f)
+            if not ops.outer_sum_into2(dspre, s.view(E, 128), vn, dWs, dbs):
+                dWs_s, dbs = _osum(dspre, s.view(E, 128))
+                dWs_v, _ = _osum(dspre, vn)
+                dWs = torch.cat([dWs_s, dWs_v], 1)
             dWsv, dbsv = _osum(dgate, spre)
             dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
             dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
-            dWs = torch.cat([dWs_s, dWs_v], 1)
         grads = (dWs, dbs, dWsv, dbsv, dWh, dWv)
         return (ds_in, dv_in) + sw.deliver(ctx.needs_input_grad, 2, W, grads) + (None,)
 
@@ -269,8 +272,13 @@ class GvpMsg0Fn(torch.autograd.Function):
         # weight gradients (edge outer sums) on the side stream, as full-size leaf gradients
         with ops.side_work(dspre, es, vn, dgate, spre, dvpre, vh, ev, dvh) as sw:
             vi = Wv.shape[1]
-            dWe, db = _osum(dspre, es)
-            dWn, _ = _osum(dspre, vn)
+            # [dWe | dWn] = dspre^T [es | vn]: one pass over dspre when the split path applies
+            Cen, db = torch.empty((128, 80), **f), torch.empty(128, **f)
+            if ops.outer_sum_into2(dspre, es, vn, Cen, db):
+                dWe, dWn = Cen[:, :32], Cen[:, 32:]
+            else:
+                dWe, db = _osum(dspre, es)
+                dWn, _ = _osum(dspre, vn)
             dWsv, dbsv = _osum(dgate, spre)
             dWv = _diag3(_osum(dvpre, vh)[0], 16, 48)
             M, _ = _osum(torch.nn.functional.pad(ev, (0, 13)), dvh)  # (16, 144): rows x = 0..2

@@ -243,6 +243,27 @@ def outer_sum_into(A, B, C, colsum=None, act=None, w=None, b=None):
     return True
 
 
+def outer_sum_into2(A, B1, B2, C, colsum=None):
+    """C[:] = A^T [B1 | B2] (and colsum(A)) in one pass over A (gmp_edge_outer_sum_ex2_f32);
+    False when the split-plane path does not apply (the caller makes two calls)."""
+    lib = _lib.load()
+    _need_cuda(A, B1, B2, C)
+    K, m = A.shape
+    n1, n2 = B1.shape[1], B2.shape[1]
+    if not all(_rows_view_ok(t) for t in (A, B1, B2)) or C.stride(1) != 1:
+        return False
+    ws_bytes = lib.gmp_edge_outer_sum_rect_workspace_size(K, m, n1 + n2)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
+    with _timed("edge_outer_sum"):
+        rc = lib.gmp_edge_outer_sum_ex2_f32(K, m, n1, n2, _p(A), A.stride(0), _p(B1), B1.stride(0),
+                                            _p(B2), B2.stride(0), _p(C), C.stride(0),
+                                            _p(colsum), _p(ws), ws_bytes, _stream())
+    if rc == _lib.GMP_ERR_UNSUPPORTED:
+        return False
+    check(rc, "gmp_edge_outer_sum_ex2_f32")
+    return True
+
+
 def edge_outer_sum_rect(A, B):
     """(A^T B, colsum(A)) over the rows (edges / nodes) for any widths, deterministic: columns
     zero-padded to multiples of 16 when needed, wide operands processed as <= 128 x 144 column

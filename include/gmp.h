@@ -191,6 +191,14 @@ int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A,
  * be written straight into a column block of a wider parameter (egnn_layer.py:28 W1 =
  * [W1a | W1b | w1d]; :37 mlp_upd[0] over [h | m_aggr]) without concatenated copies.
  * Square 32/64/128 shapes use the square kernel, others the rectangular one. */
+/* Two B operands as one: C (m x (n1 + n2)) = A^T [B1 | B2] for outer sums that share A (GVP:
+ * dspre against [s | vn]), one pass over A; workspace gmp_edge_outer_sum_rect_workspace_size(K,
+ * m, n1 + n2).  Split-plane path only: returns GMP_ERR_UNSUPPORTED where it does not apply
+ * (narrow products, node-level K, f32-MFMA mode) — the caller then makes two calls. */
+int gmp_edge_outer_sum_ex2_f32(int64_t K, int64_t m, int64_t n1, int64_t n2, const float* A,
+                               int64_t lda, const float* B1, int64_t ldb1, const float* B2,
+                               int64_t ldb2, float* C, int64_t ldc, float* colsum_A,
+                               void* workspace, size_t workspace_bytes, void* stream);
 size_t gmp_edge_outer_sum_ex_workspace_size(int64_t K, int64_t m, int64_t n);
 int gmp_edge_outer_sum_ex_f32(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
                               const float* B, int64_t ldb, int act, const float* w, const float* b,

@@ -96,3 +96,22 @@ def test_split_error_not_above_f32_mfma(m, n):
     # f32-class: within 3x of the f32-MFMA split-K kernel and no worse than torch's f32 GEMM
     # (measured: split 1.2e-8, f32 MFMA 5.8e-9 of sum |a b| at 128 x 128; f32 u = 6e-8)
     assert errs[0] <= 3 * errs[1] and errs[0] <= errs["torch_f32"], errs
+
+
+@pytest.mark.parametrize("m,n1,n2", [(128, 128, 16), (128, 32, 48), (48, 128, 16)])
+def test_outer_sum_two_b_operands(m, n1, n2):
+    """A^T [B1 | B2] in one pass (gmp_edge_outer_sum_ex2_f32) == the two products side by side"""
+    from gmp_amd import ops
+    g = torch.Generator().manual_seed(m + n1 + n2)
+    K = 400_003
+    A = torch.randn(K, m, generator=g)
+    B1, B2 = torch.randn(K, n1, generator=g), torch.randn(K, n2 + 8, generator=g)
+    Ad, B1d, B2d = A.to(DEV), B1.to(DEV), B2.to(DEV)[:, 4:4 + n2]  # strided second operand
+    C = torch.empty(m, n1 + n2, device=DEV)
+    cs = torch.empty(m, device=DEV)
+    assert ops.outer_sum_into2(Ad, B1d, B2d, C, cs)
+    Bcat = torch.cat([B1, B2[:, 4:4 + n2]], 1)
+    refC, refs = _ref(A, Bcat)
+    assert _err(C, refC, A, Bcat) < 5e-6
+    torch.testing.assert_close(cs.cpu().double(), refs, atol=1e-3, rtol=1e-5)
+    assert not ops.outer_sum_into2(Ad[:1000], B1d[:1000], B2d[:1000], C, cs)  # node-level K
