@@ -550,10 +550,11 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
 // (RT, CT) tile shape per wave for an M x N problem: the first of the compiled shapes whose
 // wave grid fits in 8 waves; returns the index into kX3 or -1
 struct X3Shape { int rt, ct; };
-constexpr X3Shape kX3[] = {{1, 1}, {1, 2}, {2, 2}, {2, 4}, {2, 5}};
+// ({1, 1} would only fit m n <= 2048, which stays on the f32-MFMA kernels)
+constexpr X3Shape kX3[] = {{1, 2}, {2, 2}, {2, 4}, {2, 5}};
 int x3_pick(int64_t m, int64_t n, int* wn) {
   const int64_t TM = m / 16, TN = n / 16;
-  for (int i = 0; i < 5; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const int64_t WM = ceil_div(TM, (int64_t)kX3[i].rt), WN = ceil_div(TN, (int64_t)kX3[i].ct);
     if (WM * WN <= kXT / 64) {
       *wn = (int)WN;
@@ -622,10 +623,9 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   else if (pro == 1) { GMP_X3_NL(RT, CT, 1) } \
   else { GMP_X3_NL(RT, CT, 2) }
   switch (shape) {
-    case 0: GMP_X3_PRO(1, 1) break;
-    case 1: GMP_X3_PRO(1, 2) break;
-    case 2: GMP_X3_PRO(2, 2) break;
-    case 3: GMP_X3_PRO(2, 4) break;
+    case 0: GMP_X3_PRO(1, 2) break;
+    case 1: GMP_X3_PRO(2, 2) break;
+    case 2: GMP_X3_PRO(2, 4) break;
     default: GMP_X3_PRO(2, 5) break;
   }
 #undef GMP_X3_PRO
