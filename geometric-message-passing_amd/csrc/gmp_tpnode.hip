@@ -182,7 +182,17 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
     constexpr int kZL = kAE * kAR / kNT;           // Z loads per thread (4)
     f32x4 regT[kTL];
     float regZ[kZL];
+    // Tb[n, rb + (tid & 31)]: the one bias row value this thread adds in the dZ store loop
+    // (x = tid + kNT q there, so rr = tid & 31), prefetched with the row block instead of a
+    // dependent load after the block's last barrier
+    float regTb = 0.f;
+    static_assert(kNT % kAR == 0, "store-loop row of a thread is tid % kAR");
     auto fetch = [&](int rb) {
+      {
+        const int rr = tid & (kAR - 1);
+        const int nrb0 = (w - rb) < kAR ? (w - rb) : kAR;
+        regTb = rr < nrb0 ? Tb[(int64_t)n * w + rb + rr] : 0.f;
+      }
       const int nrb = (w - rb) < kAR ? (w - rb) : kAR;
 #pragma unroll
       for (int q = 0; q < kTL; ++q) {
@@ -217,6 +227,7 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
         const int e = x / kAR, rr = x - e * kAR;
         sZ[e * kLdZ + rr] = regZ[q];
       }
+      const float tb_cur = regTb;  // this row block's bias value (regTb is refilled below)
       __syncthreads();
       if (r0 + kAR < w) fetch(r0 + kAR);
       // dZ[e, r] = sum_j T[r, j] a[e, j]   (D[row][e]; A op = T rows, B op = a rows)
@@ -255,7 +266,7 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
       for (int x = tid; x < kAE * kAR; x += kNT) {
         const int e = x / kAR, rr = x - e * kAR;
         if (e < ng && rr < nr)
-          dZ[(e0 + g0 + e) * w + r0 + rr] = sDZ[e * kLdZ + rr] + Tb[(int64_t)n * w + r0 + rr];
+          dZ[(e0 + g0 + e) * w + r0 + rr] = sDZ[e * kLdZ + rr] + tb_cur;
       }
     }
     // accumulate into dA (per-path launches on one stream: ordered RMW, deterministic)
