@@ -393,6 +393,13 @@ class side_work:
         return tuple(out)
 
 
+def _mm_wt(g, Wt):
+    """g @ Wt.t() for a contiguous Wt (n, k): the library GEMM's "NT" form, measured ~1.5x
+    faster than the "NN" g @ W for the (50k x 128) x (128 x 128) node GEMMs (22.5 vs 34 us);
+    the transposed weight copy is one small kernel."""
+    return g.mm(Wt.t())
+
+
 class EdgeLinearFn(torch.autograd.Function):
     """y = x W^T (+ b) over many rows (edges): forward and dx with the library GEMM (M = rows),
     dW / db with the deterministic edge outer sum (K = rows), which the library's small-tile
@@ -408,7 +415,7 @@ class EdgeLinearFn(torch.autograd.Function):
     def backward(ctx, g):
         x, W, b = ctx.saved_tensors
         g = g.contiguous()
-        dx = g.mm(W) if ctx.needs_input_grad[0] else None
+        dx = _mm_wt(g, W.t().contiguous()) if ctx.needs_input_grad[0] else None
         need_w = ctx.needs_input_grad[1] or (b is not None and ctx.needs_input_grad[2])
         if not need_w:
             return dx, None, None
@@ -443,8 +450,9 @@ class SplitLinearFn(torch.autograd.Function):
         xa, xb, W, b = ctx.saved_tensors
         da = xa.shape[1]
         g = g.contiguous()
-        dxa = g.mm(W[:, :da]) if ctx.needs_input_grad[0] else None
-        dxb = g.mm(W[:, da:]) if ctx.needs_input_grad[1] else None
+        Wt = W.t().contiguous() if (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) else None
+        dxa = _mm_wt(g, Wt[:da]) if ctx.needs_input_grad[0] else None
+        dxb = _mm_wt(g, Wt[da:]) if ctx.needs_input_grad[1] else None
         need_w = ctx.needs_input_grad[2] or (b is not None and ctx.needs_input_grad[3])
         if not need_w:
             return dxa, dxb, None, None
@@ -708,8 +716,9 @@ class EgnnMessageFn(torch.autograd.Function):
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
-        dh = dA.mm(W1[:, :d])
-        dh.addmm_(dB, W1[:, d:2 * d])
+        W1t = W1[:, :2 * d].t().contiguous()  # [W1a | W1b]^T: NT-form GEMMs for dh
+        dh = _mm_wt(dA, W1t[:d])
+        dh.addmm_(dB, W1t[d:].t())
         dpos = dpos_recv - dpos_send
 
         # weight gradients: side stream, accumulated at the end of the backward pass
