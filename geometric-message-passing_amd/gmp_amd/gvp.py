@@ -315,7 +315,7 @@ class NodeProjFn(torch.autograd.Function):
         s, Wcat = ctx.saved_tensors
         Ws0, si, se = ctx.Ws0, ctx.si, ctx.se
         dP = dP.contiguous()
-        ds = dP.mm(Wcat) if ctx.needs_input_grad[0] else None
+        ds = ops._mm_wt(dP, Wcat.t().contiguous()) if ctx.needs_input_grad[0] else None
         if not ctx.needs_input_grad[1]:
             return ds, None, None, None
         so = Ws0.shape[0]
@@ -352,7 +352,7 @@ class NodeVecProjFn(torch.autograd.Function):
         dY = dQ.reshape(n, 96, 3).transpose(1, 2).reshape(3 * n, 96).contiguous()
         dv = None
         if ctx.needs_input_grad[0]:
-            dv = dY.mm(Wst).view(n, 3, vi).transpose(1, 2)
+            dv = ops._mm_wt(dY, Wst.t().contiguous()).view(n, 3, vi).transpose(1, 2)
         if not ctx.needs_input_grad[1]:
             return dv, None, None
         ho = Wh0.shape[0]
