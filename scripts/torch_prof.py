@@ -34,14 +34,15 @@ def step():
 for _ in range(3):
     step()
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU], record_shapes=True) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
     step()
     torch.cuda.synchronize()
-names = ("aten::copy_", "aten::cat", "aten::contiguous", "aten::clone", "aten::zeros",
+names = ("aten::mm", "aten::addmm", "aten::addmm_", "aten::copy_", "aten::cat", "aten::contiguous", "aten::clone", "aten::zeros",
          "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::mul", "aten::index_select",
          "aten::constant_pad_nd", "aten::sum", "aten::div", "aten::sub")
 tab = prof.key_averages(group_by_input_shape=True)
 rows = [e for e in tab if e.key in names]
 rows.sort(key=lambda e: -e.count)
 for e in rows[:45]:
-    print(f"{e.count:4d}  {e.key:24s} {str(e.input_shapes)[:110]}")
+    dt = getattr(e, "device_time_total", 0.0) or getattr(e, "cuda_time_total", 0.0)
+    print(f"{e.count:4d} {dt:9.1f}us {e.key:18s} {str(e.input_shapes)[:100]}")
