@@ -2,9 +2,12 @@
 // row-major and K = number of edges (~1M), M = N = d.  This is the dW of a per-edge Linear
 // (egnn_layer.py:28-39 mlp_msg / mlp_pos: dW = sum_e dpre_e (x) x_e, db = sum_e dpre_e).
 //
-// Split-K over workgroups (each a contiguous edge range), f32 MFMA 16x16x4 with the edge index
-// as the MFMA k dimension, partial slabs in a workspace and an ordered second pass (bitwise
-// deterministic; no atomics).  HBM-bound: reads A and B once.
+// Split-K over workgroups (each a contiguous edge range) with the edge index as the MFMA k
+// dimension, partial slabs in a workspace and an ordered second pass (bitwise deterministic; no
+// atomics); reads A and B once.  Two arithmetic paths: wide edge-level products run on the bf16
+// MFMA over exact three-plane splits of the f32 operands (outer_sum_x3_kernel, below); narrow
+// products, node-level row counts and gmp_wgrad_set_f32_mfma(1) use the f32 MFMA 16x16x4
+// kernels (outer_sum_kernel, outer_sum_rect_kernel).
 #include <stdlib.h>
 
 #include "gmp_common.h"
