@@ -378,18 +378,24 @@ class side_work:
     def deliver(self, needs_input_grad, first, targets, grads):
         """Per parameter: defer the gradient (leaf parameter) or hand it back through autograd
         (after joining the streams).  needs_input_grad[first + i] belongs to targets[i]."""
-        out, joined = [], False
+        out, joined, deferred = [], False, False
         for i, (p, gr) in enumerate(zip(targets, grads)):
             if not needs_input_grad[first + i]:
                 out.append(None)
             elif deferrable(p):
                 self.defer(p, gr)
+                deferred = True
                 out.append(None)
             else:
                 if not joined:
                     self.join(*grads)
                     joined = True
                 out.append(gr)
+        if not (joined or deferred):
+            # no parameter gradient wanted (e.g. autograd.grad w.r.t. inputs only): nothing will
+            # flush this side work, so join here and release the kept-alive inputs
+            self.main.wait_stream(self.side)
+            _KEEPALIVE.clear()
         return tuple(out)
 
 

@@ -157,3 +157,22 @@ def test_egnn_model_equivariance():
         y1 = model(Batch(g.atoms.to(DEV), g.pos.to(DEV), g.edge_index.to(DEV), num_graphs=1))
         y2 = model(Batch(g.atoms.to(DEV), pos2.to(DEV), g.edge_index.to(DEV), num_graphs=1))
     torch.testing.assert_close(y1, y2, atol=1e-3, rtol=1e-4)
+
+
+def test_frozen_parameters_release_side_stream_inputs():
+    """Backward with no parameter gradient wanted (frozen weights, input gradients only): the
+    side-stream work is joined in place and its kept-alive inputs released (nothing else would
+    flush them)."""
+    import gmp_amd
+    from gmp_amd import ops
+    torch.manual_seed(1)
+    g = _graph(400, 6000, seed=2)
+    lay = gmp_amd.EGNNLayer(128, "relu", "layer", "sum").to(DEV)
+    lay.requires_grad_(False)
+    hd = torch.randn(g.num_nodes, 128, device=DEV, requires_grad=True)
+    pd = g.pos.to(DEV).requires_grad_(True)
+    for _ in range(2):
+        ho, po = lay(hd, pd, g.edge_index.to(DEV))
+        (ho.sum() + po.sum()).backward()
+        assert not ops._KEEPALIVE
+    assert hd.grad is not None and all(p.grad is None for p in lay.parameters())
