@@ -340,6 +340,18 @@ def deferrable(t):
     return DEFER_WEIGHT_GRADS and t is not None and t.is_leaf and t.requires_grad
 
 
+def _engine_accumulates(p):
+    """True when the running backward pass will execute p's AccumulateGrad (loss.backward());
+    False under torch.autograd.grad, which either skips the parameter or captures its gradient
+    as an output — then the gradient must travel through autograd, not into p.grad."""
+    try:
+        with torch.enable_grad():
+            acc = p.view_as(p).grad_fn.next_functions[0][0]
+        return bool(torch._C._will_engine_execute_node(acc))
+    except (RuntimeError, AttributeError, IndexError):
+        return False
+
+
 class side_work:
     """with side_work(used_tensors) as sw: ... launches on the side stream after everything
     already queued on the current stream; sw.defer(param, grad) hands a result to the end-of-
@@ -379,10 +391,13 @@ class side_work:
         """Per parameter: defer the gradient (leaf parameter) or hand it back through autograd
         (after joining the streams).  needs_input_grad[first + i] belongs to targets[i]."""
         out, joined, deferred = [], False, False
+        accum = None  # does this backward pass accumulate into .grad (checked once per call)
         for i, (p, gr) in enumerate(zip(targets, grads)):
+            if deferrable(p) and needs_input_grad[first + i] and accum is None:
+                accum = _engine_accumulates(p)
             if not needs_input_grad[first + i]:
                 out.append(None)
-            elif deferrable(p):
+            elif deferrable(p) and accum:
                 self.defer(p, gr)
                 deferred = True
                 out.append(None)
@@ -425,7 +440,7 @@ class EdgeLinearFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[1] or (b is not None and ctx.needs_input_grad[2])
         if not need_w:
             return dx, None, None
-        defer = deferrable(W) and (b is None or deferrable(b))
+        defer = deferrable(W) and (b is None or deferrable(b)) and _engine_accumulates(W)
         with side_work(g, x) as sw:
             r = edge_outer_sum_rect(g, x)
             dW, db = r if r is not None else (g.t().mm(x), g.sum(0))
@@ -462,7 +477,7 @@ class SplitLinearFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[2] or (b is not None and ctx.needs_input_grad[3])
         if not need_w:
             return dxa, dxb, None, None
-        defer = deferrable(W) and (b is None or deferrable(b))
+        defer = deferrable(W) and (b is None or deferrable(b)) and _engine_accumulates(W)
         with side_work(g, xa, xb) as sw:
             dW = torch.empty_like(W)
             db = torch.empty(W.shape[0], dtype=W.dtype, device=W.device)

@@ -176,3 +176,26 @@ def test_frozen_parameters_release_side_stream_inputs():
         (ho.sum() + po.sum()).backward()
         assert not ops._KEEPALIVE
     assert hd.grad is not None and all(p.grad is None for p in lay.parameters())
+
+
+def test_autograd_grad_inputs_leaves_param_grads_alone():
+    """torch.autograd.grad w.r.t. positions (force-style) must not accumulate into p.grad (the
+    deferred side-stream gradients only go to .grad when the engine accumulates), and
+    autograd.grad w.r.t. a weight returns the same gradient as backward() puts in .grad."""
+    import gmp_amd
+    torch.manual_seed(3)
+    g = _graph(400, 6000, seed=5)
+    lay = gmp_amd.EGNNLayer(128, "relu", "layer", "sum").to(DEV)
+    hd = torch.randn(g.num_nodes, 128, device=DEV, requires_grad=True)
+    pd = g.pos.to(DEV).requires_grad_(True)
+    ei = g.edge_index.to(DEV)
+    ho, po = lay(hd, pd, ei)
+    (gp,) = torch.autograd.grad((ho.sum() + po.sum()), [pd])
+    assert gp is not None and all(p.grad is None for p in lay.parameters())
+    W = lay.mlp_msg[0].weight
+    ho, po = lay(hd, pd, ei)
+    (gw,) = torch.autograd.grad((ho.sum() + po.sum()), [W])
+    assert all(p.grad is None for p in lay.parameters())
+    ho, po = lay(hd, pd, ei)
+    (ho.sum() + po.sum()).backward()
+    torch.testing.assert_close(gw, W.grad, atol=1e-5, rtol=1e-5)
