@@ -296,8 +296,9 @@ def edge_outer_sum_rect(A, B):
 # are computed on a side stream (overlapping the critical path's small node-level kernels and
 # the host launch gaps between them) and accumulated into param.grad by a callback at the end
 # of the backward pass, as DDP does with its reducer.  Disable (DEFER_WEIGHT_GRADS = False)
-# when something must see these gradients through autograd (DDP's per-parameter hooks,
-# torch.autograd.grad on parameters); gmp_amd.dist.wrap_ddp does so.
+# when something must see these gradients through autograd (DDP's per-parameter hooks);
+# gmp_amd.dist.wrap_ddp does so.  Under torch.autograd.grad (the engine runs no AccumulateGrad)
+# they are returned through autograd automatically (_engine_accumulates).
 DEFER_WEIGHT_GRADS = True
 _SIDE_STREAMS = {}
 _PENDING = []   # (param, grad) accumulated at the end of the backward pass
