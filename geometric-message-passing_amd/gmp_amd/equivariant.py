@@ -18,6 +18,7 @@ import math
 import os
 
 import torch
+from torch.autograd.function import once_differentiable
 from torch import nn
 from torch.nn import functional as F
 
@@ -102,6 +103,7 @@ class EdgeFeaturizeFn(torch.autograd.Function):
         return sh, rad
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g_sh, g_rad):
         if not ctx.needs_input_grad[0]:
             return None, None, None, None
@@ -411,6 +413,7 @@ class TPConvFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gout):
         lib = _lib.load()
         x, sh, rad_s, W1, b1, W2, b2 = ctx.saved_tensors
@@ -527,6 +530,7 @@ class TPConvNodeFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gout):
         lib = _lib.load()
         x, sh, rad_s, W1, b1, W2, b2 = ctx.saved_tensors
@@ -742,6 +746,7 @@ class SymmetricContractionFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g):
         lib = _lib.load()
         x, *A = ctx.saved_tensors

@@ -15,6 +15,7 @@ import functools
 import os
 
 import torch
+from torch.autograd.function import once_differentiable
 from torch import nn
 from torch.nn import functional as F
 
@@ -185,6 +186,7 @@ class GvpLayerFn(torch.autograd.Function):
         return s_out, v_out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, ds, dv):
         lib = _lib.load()
         s, v, *W = ctx.saved_tensors
@@ -248,6 +250,7 @@ class GvpMsg0Fn(torch.autograd.Function):
         return s_out, v_out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, ds, dv):
         lib = _lib.load()
         P, Q, es, ev, send, recv, *W = ctx.saved_tensors
@@ -311,6 +314,7 @@ class NodeProjFn(torch.autograd.Function):
         return s.matmul(Wcat.t())
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dP):
         s, Wcat = ctx.saved_tensors
         Ws0, si, se = ctx.Ws0, ctx.si, ctx.se
@@ -346,6 +350,7 @@ class NodeVecProjFn(torch.autograd.Function):
         return Y.view(n, 3, 96).transpose(1, 2).reshape(n, 288)
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dQ):
         vt, Wst = ctx.saved_tensors
         Wh0, vi, n = ctx.Wh0, ctx.vi, ctx.n

@@ -7,6 +7,7 @@ fallback in the product path.
 import ctypes
 
 import torch
+from torch.autograd.function import once_differentiable
 
 from . import _lib
 from ._lib import check
@@ -434,6 +435,7 @@ class EdgeLinearFn(torch.autograd.Function):
         return torch.addmm(b, x, W.t()) if b is not None else x.mm(W.t())
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g):
         x, W, b = ctx.saved_tensors
         g = g.contiguous()
@@ -468,6 +470,7 @@ class SplitLinearFn(torch.autograd.Function):
         return y
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g):
         xa, xb, W, b = ctx.saved_tensors
         da = xa.shape[1]
@@ -532,6 +535,7 @@ class LnActFn(torch.autograd.Function):
         return y.view(shape)
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gy):
         lib = _lib.load()
         xhat, rstd, gamma, beta = ctx.saved_tensors
@@ -592,6 +596,7 @@ class SegmentReduceFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g):
         (argmax,) = ctx.saved_tensors
         gs = segment_reduce_bwd(g.contiguous(), ctx.csr, ctx.reduce,
@@ -608,6 +613,7 @@ class GatherRowsFn(torch.autograd.Function):
         return gather_rows(src2d, index)
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g):
         csr = get_csr(ctx.index, ctx.n_rows)
         out, _ = segment_reduce(g.contiguous(), csr, "sum")
@@ -709,6 +715,7 @@ class EgnnMessageFn(torch.autograd.Function):
         return m_aggr, pos_aggr
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g_m, g_p):
         lib = _lib.load()
         h, pos, xhat, rstd, W1, *params = ctx.saved_tensors

@@ -199,3 +199,18 @@ def test_autograd_grad_inputs_leaves_param_grads_alone():
     ho, po = lay(hd, pd, ei)
     (ho.sum() + po.sum()).backward()
     torch.testing.assert_close(gw, W.grad, atol=1e-5, rtol=1e-5)
+
+
+def test_double_backward_raises():
+    """The HIP backward kernels are not themselves differentiable: a second-order gradient
+    (e.g. training on forces from create_graph=True) must fail loudly, not return zeros."""
+    import gmp_amd
+    torch.manual_seed(4)
+    g = _graph(300, 4000, seed=6)
+    lay = gmp_amd.EGNNLayer(128, "relu", "layer", "sum").to(DEV)
+    hd = torch.randn(g.num_nodes, 128, device=DEV, requires_grad=True)
+    pd = g.pos.to(DEV).requires_grad_(True)
+    ho, po = lay(hd, pd, g.edge_index.to(DEV))
+    (gp,) = torch.autograd.grad(ho.sum() + po.sum(), [pd], create_graph=True)
+    with pytest.raises(RuntimeError):
+        gp.sum().backward()
