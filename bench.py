@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("egnn", "gvp", "mace", "tfn"), default="egnn")
+    ap.add_argument("--workload", choices=("egnn", "gvp", "mace", "tfn", "schnet"),
+                    default="egnn")
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--emb", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=50_000)
@@ -63,6 +64,8 @@ WORKLOADS = {  # name -> (config tag, layers, emb)
     "mace": ("C4 MACE L=2 corr=3", 5, 128),
     "tfn": ("C5 TFN L=2 gated (per-GPU shard)", 5, 64),
     "gvp": ("C3 GVP-GNN s=128 v=16 edge=(32,1)", 4, 128),
+    # C1's model (SchNet 4L, hidden 64, 128 filters, 50 Gaussians, cutoff 10) on the C2 graph
+    "schnet": ("C1-model SchNet hidden=64 filters=128 gaussians=50 cutoff=10", 4, 64),
 }
 
 
@@ -74,6 +77,9 @@ def build_model(mod, args, radius):
     if args.workload == "mace":
         return mod.MACEModel(num_layers=args.layers, emb_dim=args.emb, correlation=3,
                              max_ell=2, in_dim=1, out_dim=1)
+    if args.workload == "schnet":
+        return mod.SchNetModel(hidden_channels=args.emb, in_dim=1, out_dim=1, num_filters=128,
+                               num_layers=args.layers, num_gaussians=50, cutoff=10)
     if args.workload == "gvp":
         return mod.GVPGNNModel(num_layers=args.layers, s_dim=args.emb, v_dim=16, s_dim_edge=32,
                                v_dim_edge=1, in_dim=1, out_dim=1)
@@ -151,6 +157,12 @@ def egnn_flops_per_edge(d):
     return {"egnn_edge_fwd": 2 * gemm, "egnn_edge_bwd": 2 * gemm}  # bwd: W3^T, W2^T
 
 
+def _atom_type(args):
+    """Synthetic atom type: 0 (in_dim = 1 embeddings), 1 for SchNet, whose Embedding(100) keeps
+    row 0 as padding (padding_idx = 0: a zero, gradient-free row)."""
+    return 1 if args.workload == "schnet" else 0
+
+
 def cpu_baseline(g, args):
     """Time the CPU oracle (fwd + L1 + bwd + Adam) on a spatial slab of the same graph."""
     from oracle import egnn as oegnn
@@ -159,7 +171,7 @@ def cpu_baseline(g, args):
 
     threads = min(args.cpu_threads, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    if args.workload in ("egnn", "gvp"):
+    if args.workload in ("egnn", "gvp", "schnet"):
         frac = 0.25 if args.workload == "egnn" else 0.1  # slab x < frac * box
         keep = g.pos[:, 0] < g.box * frac
         shape = "spatial slab"
@@ -173,11 +185,13 @@ def cpu_baseline(g, args):
     remap[idx] = torch.arange(idx.numel())
     ei = g.edge_index
     m = keep[ei[0]] & keep[ei[1]]
-    sub = Batch(torch.zeros(idx.numel(), dtype=torch.long), g.pos[idx], remap[ei[:, m]],
-                num_graphs=1)
+    sub = Batch(torch.full((idx.numel(),), _atom_type(args), dtype=torch.long), g.pos[idx],
+                remap[ei[:, m]], num_graphs=1)
     torch.manual_seed(0)
     from oracle import gvp as ogvp
-    model = build_model({"egnn": oegnn, "gvp": ogvp}.get(args.workload, omace), args, g.radius)
+    from oracle import schnet as oschnet
+    model = build_model({"egnn": oegnn, "gvp": ogvp, "schnet": oschnet}.get(args.workload, omace),
+                        args, g.radius)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     y = torch.zeros(1)
 
@@ -228,6 +242,8 @@ def main():
     opt = (torch.optim.Adam(model.parameters(), lr=1e-4, capturable=True) if args.graph
            else torch.optim.Adam(model.parameters(), lr=1e-4, fused=True))
     batch = g.to(dev)
+    if _atom_type(args):
+        batch.atoms = torch.full_like(batch.atoms, _atom_type(args))
     y = torch.randn(1, device=dev)
 
     def loss_fn():
@@ -289,6 +305,16 @@ def main():
                     "fwd_kernel_ms": ms_fwd,
                     "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
                     / (ms_fwd * 1e-3) / 1e12}
+        elif args.workload == "schnet":
+            # no single dominant HIP kernel: whole step against the fp32 MFMA peak, counting
+            # the CFConv filter network (50 -> F -> F per edge; K6) fwd + 2x bwd per layer
+            F = 128
+            fl = 3 * 2 * (50 * F + F * F) * args.layers
+            achieved = fl * g.num_edges / (elapsed / args.steps) / 1e12
+            roof = {"kernel": "whole step (fwd+bwd, all kernels)", "kernel_prefix": "-",
+                    "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                    "traffic": None, "flops_per_edge": fl}
         elif args.workload == "gvp":
             # no single dominant HIP kernel yet (torch GEMMs on gathered rows): whole step
             fl = gvp_flops_per_edge(args.emb, 16, 32, 1) * 3 * args.layers
