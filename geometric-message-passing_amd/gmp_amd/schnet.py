@@ -5,7 +5,9 @@ state_dict keys (interactions.<k>.mlp.* shared with interactions.<k>.conv.nn.*).
 CFConv keeps PyG's MessagePassing contract (aggr 'add', x_j = x[edge_index[0]], sum at
 edge_index[1] with dim_size = N) through gmp_amd.MessagePassing: the x_j gather is the HIP gather
 kernel and the sum the HIP segmented reduce over the receiver CSR.  Config C1 (k-chains) is
-tiny; the filter network runs as PyTorch GEMMs.  PyG itself is absent: the internals follow
+tiny; on the C2-sized graphs the filter network's edge Linears take ops.linear: library GEMMs
+forward / dx, weight gradients by the deterministic edge outer sum (the library's K = E
+reductions ran at 1.8 ms each, profiles/r01_schnet_kernels.md).  PyG itself is absent: the internals follow
 PyG 2.3.1's published code (parity unpinned, see oracle/schnet.py).
 """
 import math
@@ -50,10 +52,20 @@ class CFConv(MessagePassing):
 
     def forward(self, x, edge_index, edge_weight, edge_attr):
         C = 0.5 * (torch.cos(edge_weight * math.pi / self.cutoff) + 1.0)
-        W = self.nn(edge_attr) * C.view(-1, 1)
+        W = self._filter(edge_attr) * C.view(-1, 1)
         x = self.lin1(x)
         x = self.propagate(edge_index, x=x, W=W)
         return self.lin2(x)
+
+    def _filter(self, edge_attr):
+        """self.nn(edge_attr); the Linear -> act -> Linear filter network goes through
+        ops.linear (same parameters, same arithmetic order per output element)."""
+        m = self.nn
+        if (isinstance(m, nn.Sequential) and len(m) == 3 and isinstance(m[0], nn.Linear)
+                and isinstance(m[2], nn.Linear)):
+            return ops.linear(m[1](ops.linear(edge_attr, m[0].weight, m[0].bias)),
+                              m[2].weight, m[2].bias)
+        return m(edge_attr)
 
     def message(self, x_j, W):
         return x_j * W

@@ -28,9 +28,15 @@ def _batches(kind):
     return collate(g)
 
 
-@pytest.mark.parametrize("kind", ["kchains", "radius"])
-def test_schnet_vs_oracle(kind):
+@pytest.mark.parametrize("kind,edge_path", [("kchains", False), ("radius", False),
+                                             ("kchains", True), ("radius", True)])
+def test_schnet_vs_oracle(kind, edge_path, monkeypatch):
+    """edge_path: force the filter network's edge Linears onto ops.linear's EdgeLinearFn
+    (outer-sum weight gradients, K = 50 zero-padded to 64), which the bench graph takes."""
     import gmp_amd
+    from gmp_amd import ops
+    if edge_path:
+        monkeypatch.setattr(ops, "EDGE_LINEAR_MIN_ROWS", 1)
     from gmp_amd.graph import Batch
     torch.manual_seed(3)
     b = _batches(kind)
