@@ -54,6 +54,10 @@ SIGNATURES = {
     "gmp_csr_build": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_size, c_vp]),
     "gmp_gather_rows_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "gmp_cfconv_aggregate_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
+                                         c_i64, c_vp, c_vp, c_vp]),
+    "gmp_cfconv_wgrad_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                     c_vp, c_vp]),
     "gmp_segment_reduce_workspace_size": (c_size, [c_i64, c_i64, c_i64, c_int]),
     "gmp_segment_reduce_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
                                        c_vp, c_size, c_vp]),

@@ -630,6 +630,68 @@ def gather(src, index, dim=0):
     return out.reshape((index.numel(),) + tuple(shp[1:])).movedim(0, dim)
 
 
+# ----------------------------------------------------------------------------------- CFConv
+_CHECKED_CSR = []  # CSRs whose build-time range flag was already read (once per graph)
+
+
+def _cfconv_csr(index, n):
+    csr = get_csr(index, n)
+    if not any(c is csr for c in _CHECKED_CSR):
+        csr.check_range()  # one host sync per new graph, as torch_scatter raises IndexError
+        _CHECKED_CSR.insert(0, csr)
+        del _CHECKED_CSR[32:]
+    return csr
+
+
+def cfconv_aggregate(x, xidx, w, csr):
+    """out[s] = sum over CSR segment s of x[xidx[e]] * w[e] (K13 gmp_cfconv_aggregate_f32)."""
+    lib = _lib.load()
+    out = torch.empty((csr.n_seg, x.shape[1]), dtype=torch.float32, device=x.device)
+    err = torch.zeros(1, dtype=torch.int32, device=x.device)
+    check(lib.gmp_cfconv_aggregate_f32(_p(x), x.shape[0], _p(xidx), _p(w), w.shape[0],
+                                       x.shape[1], _p(csr.perm), _p(csr.rowptr), csr.n_seg,
+                                       _p(out), _p(err), _stream()), "gmp_cfconv_aggregate_f32")
+    return out
+
+
+class CFConvAggregateFn(torch.autograd.Function):
+    """PyG CFConv propagate (message x_j * W, aggr "add", dim_size = N; schnet.py:72) without
+    the (E, F) message: forward and x-gradient by K13 over the receiver / sender CSR, the
+    W-gradient as the per-edge product grad[dst] * x[src]."""
+
+    @staticmethod
+    def forward(ctx, x, W, src, dst, n):
+        recv = _cfconv_csr(dst, n)
+        ctx.save_for_backward(x, W)
+        ctx.src, ctx.dst, ctx.n = src, dst, n
+        return cfconv_aggregate(x, src, W, recv)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        g = _f32c(g)
+        dx = dW = None
+        if ctx.needs_input_grad[0]:
+            dx = cfconv_aggregate(g, ctx.dst, W, _cfconv_csr(ctx.src, x.shape[0]))
+        if ctx.needs_input_grad[1]:
+            lib = _lib.load()
+            dW = torch.empty_like(W)
+            err = torch.zeros(1, dtype=torch.int32, device=W.device)
+            check(lib.gmp_cfconv_wgrad_f32(_p(g), g.shape[0], _p(ctx.dst), _p(x), x.shape[0],
+                                           _p(ctx.src), W.shape[0], W.shape[1], _p(dW), _p(err),
+                                           _stream()), "gmp_cfconv_wgrad_f32")
+        return dx, dW, None, None, None
+
+
+def cfconv_propagate(edge_index, x, W):
+    """sum_{e: dst[e] = i} x[src[e]] * W[e] for edge_index = (src, dst), N = x.shape[0]."""
+    x, W = _f32c(x), _f32c(W)
+    _need_cuda(x, W)
+    ei = _i64c(edge_index)
+    return CFConvAggregateFn.apply(x, W, ei[0], ei[1], x.shape[0])
+
+
 # ----------------------------------------------------------------------------------- EGNN
 class EgnnGraph:
     """Receiver-sorted view of an edge_index for the fused EGNN kernels (built on device)."""

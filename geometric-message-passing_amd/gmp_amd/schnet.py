@@ -67,6 +67,15 @@ class CFConv(MessagePassing):
                               m[2].weight, m[2].bias)
         return m(edge_attr)
 
+    def fused_supported(self, x, W):
+        return (x.is_cuda and x.dtype == torch.float32 and W.dtype == torch.float32
+                and x.dim() == 2 and W.dim() == 2 and x.shape[1] % 4 == 0
+                and W.shape[1] == x.shape[1])
+
+    def fused_propagate(self, edge_index, x, W):
+        """K13: message x_j * W and the sum at edge_index[1] in one pass over W."""
+        return ops.cfconv_propagate(edge_index, x, W)
+
     def message(self, x_j, W):
         return x_j * W
 

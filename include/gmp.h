@@ -418,6 +418,24 @@ int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int correla
                                       const float* A3, const float* gout, float* dx,
                                       float* dA_partials, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * K13 SchNet CFConv fused message + aggregation (PyG 2.3.1 CFConv.message `x_j * W` and
+ * aggr "add", called at schnet.py:72; replaces the x_j gather, the (E, F) product and the
+ * scatter-sum of a15):
+ *   out[s, :] = sum_{k in [rowptr[s], rowptr[s+1])} x[xidx[perm[k]], :] * w[perm[k], :]
+ * Forward: CSR over dst, xidx = src.  x-gradient: CSR over src, x = grad_out, xidx = dst.
+ * F % 4 == 0, x / w / out 16-byte aligned.  Out-of-range xidx -> zero term, *err = 1.
+ * gmp_cfconv_wgrad_f32: dw[e, :] = g[gidx[e], :] * x[xidx[e], :] (W-gradient, gidx = dst,
+ * xidx = src); out-of-range -> zero row, *err = 1.  Deterministic (no atomics).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_cfconv_aggregate_f32(const float* x, int64_t n_x, const int64_t* xidx, const float* w,
+                             int64_t n_items, int64_t F, const int64_t* perm,
+                             const int64_t* rowptr, int64_t n_seg, float* out, int32_t* err,
+                             void* stream);
+int gmp_cfconv_wgrad_f32(const float* g, int64_t n_g, const int64_t* gidx, const float* x,
+                         int64_t n_x, const int64_t* xidx, int64_t n_items, int64_t F, float* dw,
+                         int32_t* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

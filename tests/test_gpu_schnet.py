@@ -60,3 +60,34 @@ def test_schnet_vs_oracle(kind, edge_path, monkeypatch):
     _scaled(pd.grad, pr.grad, 1e-4, "grad_pos")
     for (k, p), q in zip(model.named_parameters(), ref.parameters()):
         _scaled(p.grad, q.grad, 1e-4, k)
+
+
+@pytest.mark.parametrize("F,n,E", [(128, 300, 5000), (64, 50, 0), (4, 7, 40), (260, 33, 900)])
+def test_cfconv_aggregate_vs_torch(F, n, E):
+    """K13 (gmp_cfconv_aggregate_f32 / gmp_cfconv_wgrad_f32) against the plain-PyTorch fp32
+    restatement of CFConv's propagate: x[src] * W summed at dst (index_add_), and its
+    gradients.  Isolated receivers (n > max dst) come out as zero rows.  Tolerance 1e-5."""
+    from gmp_amd import ops
+    gen = torch.Generator().manual_seed(F + n + E)
+    ei = torch.randint(0, max(n - 3, 1), (2, E), generator=gen)
+    x = torch.randn(n, F, generator=gen)
+    W = torch.randn(E, F, generator=gen)
+    xd, Wd = x.to(DEV).requires_grad_(True), W.to(DEV).requires_grad_(True)
+    y = ops.cfconv_propagate(ei.to(DEV), xd, Wd)
+    xr, Wr = x.clone().requires_grad_(True), W.clone().requires_grad_(True)
+    yr = torch.zeros(n, F).index_add_(0, ei[1], xr[ei[0]] * Wr)
+    torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-5, rtol=1e-5)
+    g = torch.randn(n, F, generator=gen)
+    (y * g.to(DEV)).sum().backward()
+    (yr * g).sum().backward()
+    torch.testing.assert_close(xd.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(Wd.grad.cpu(), Wr.grad, atol=1e-5, rtol=1e-5)
+
+
+def test_cfconv_aggregate_out_of_range_raises():
+    from gmp_amd import ops
+    ei = torch.tensor([[0, 1, 9], [1, 2, 0]], device=DEV)
+    x = torch.randn(4, 8, device=DEV)
+    W = torch.randn(3, 8, device=DEV)
+    with pytest.raises(IndexError):
+        ops.cfconv_propagate(ei.flip(0), x, W)  # dst 9 >= N = 4
