@@ -442,8 +442,11 @@ int gmp_gather_rows_f32(const float* src, int64_t n_rows, int64_t F, const int64
 static int64_t split_parts(int64_t n_items, int64_t n_seg, int reduce) {
   if (reduce == GMP_REDUCE_MAX || n_seg <= 0) return 1;
   const int64_t avg = n_items / n_seg;
-  if (avg < 2048) return 1;
-  int64_t S = ceil_div(avg, 1024);
+  int64_t S = avg < 2048 ? 1 : ceil_div(avg, 1024);
+  // Few segments over many items (an embedding-table gradient: 50k nodes of one atom type
+  // into a 100-row table; pools): one wave per segment would leave the chip idle and run the
+  // longest segment serially, so spread the segments over >= 2048 workgroups.
+  if (n_seg < 2048 && n_items >= 16384) S = std::max<int64_t>(S, ceil_div(2048, n_seg));
   return S > 4096 ? 4096 : S;
 }
 
