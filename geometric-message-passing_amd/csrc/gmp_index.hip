@@ -445,8 +445,10 @@ static int64_t split_parts(int64_t n_items, int64_t n_seg, int reduce) {
   int64_t S = avg < 2048 ? 1 : ceil_div(avg, 1024);
   // Few segments over many items (an embedding-table gradient: 50k nodes of one atom type
   // into a 100-row table; pools): one wave per segment would leave the chip idle and run the
-  // longest segment serially, so spread the segments over >= 2048 workgroups.
-  if (n_seg < 2048 && n_items >= 16384) S = std::max<int64_t>(S, ceil_div(2048, n_seg));
+  // longest segment serially, so spread the segments over up to 2048 workgroups (at most 64
+  // parts each: segment_split_finish sums the parts serially per output element).
+  if (n_seg < 2048 && n_items >= 16384)
+    S = std::max<int64_t>(S, std::min<int64_t>(ceil_div(2048, n_seg), 64));
   return S > 4096 ? 4096 : S;
 }
 
