@@ -1,0 +1,77 @@
+// K14: SchNet's shifted softplus (PyG ShiftedSoftplus: softplus(x) - log 2, applied to the
+// (E, 128) filter-network hidden layer, schnet.py:72 via CFConv's nn, and to node features).
+// torch.nn.functional.softplus semantics (beta 1, threshold 20):
+//   forward : y = (x > 20 ? x : log1p(exp(x))) - shift
+//   backward: dx = x > 20 ? g : g * z / (z + 1), z = exp(x)
+// One float4 per thread, grid-stride: one read + one write pass (the library path ran the
+// softplus and the shift subtraction as separate passes).
+#include "gmp_common.h"
+
+namespace gmp {
+namespace {
+
+__device__ __forceinline__ float ssp1(float x, float shift) {
+  return (x > 20.f ? x : log1pf(expf(x))) - shift;
+}
+
+__device__ __forceinline__ float ssp1_bwd(float x, float g) {
+  if (x > 20.f) return g;
+  const float z = expf(x);
+  return g * z / (z + 1.f);
+}
+
+__global__ __launch_bounds__(256) void ssp_fwd(const float4* __restrict__ x, int64_t n4,
+                                               float shift, float4* __restrict__ y) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n4;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x[t];
+    y[t] = make_float4(ssp1(v.x, shift), ssp1(v.y, shift), ssp1(v.z, shift), ssp1(v.w, shift));
+  }
+}
+
+__global__ __launch_bounds__(256) void ssp_bwd(const float4* __restrict__ x,
+                                               const float4* __restrict__ g, int64_t n4,
+                                               float4* __restrict__ dx) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n4;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x[t], w = g[t];
+    dx[t] = make_float4(ssp1_bwd(v.x, w.x), ssp1_bwd(v.y, w.y), ssp1_bwd(v.z, w.z),
+                        ssp1_bwd(v.w, w.w));
+  }
+}
+
+bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+unsigned grid_for4(int64_t n4) {
+  return (unsigned)std::min<int64_t>(ceil_div(n4, 256), 256 * 32);
+}
+
+}  // namespace
+}  // namespace gmp
+
+using namespace gmp;
+
+extern "C" {
+
+int gmp_ssp_fwd_f32(const float* x, int64_t n, float shift, float* y, void* stream) {
+  GMP_CHECK_ARG(n >= 0);
+  if (n == 0) return GMP_OK;
+  GMP_CHECK_ARG(x && y && n % 4 == 0 && aligned16(x) && aligned16(y));
+  ssp_fwd<<<grid_for4(n / 4), 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<const float4*>(x), n / 4, shift, reinterpret_cast<float4*>(y));
+  return launch_status();
+}
+
+int gmp_ssp_bwd_f32(const float* x, const float* grad_y, int64_t n, float* grad_x,
+                    void* stream) {
+  GMP_CHECK_ARG(n >= 0);
+  if (n == 0) return GMP_OK;
+  GMP_CHECK_ARG(x && grad_y && grad_x && n % 4 == 0 && aligned16(x) && aligned16(grad_y) &&
+                aligned16(grad_x));
+  ssp_bwd<<<grid_for4(n / 4), 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<const float4*>(x), reinterpret_cast<const float4*>(grad_y), n / 4,
+      reinterpret_cast<float4*>(grad_x));
+  return launch_status();
+}
+
+}  // extern "C"

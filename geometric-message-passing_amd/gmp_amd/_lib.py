@@ -58,6 +58,8 @@ SIGNATURES = {
                                          c_i64, c_vp, c_vp, c_vp]),
     "gmp_cfconv_wgrad_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
                                      c_vp, c_vp]),
+    "gmp_ssp_fwd_f32": (c_int, [c_vp, c_i64, c_f32, c_vp, c_vp]),
+    "gmp_ssp_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "gmp_segment_reduce_workspace_size": (c_size, [c_i64, c_i64, c_i64, c_int]),
     "gmp_segment_reduce_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
                                        c_vp, c_size, c_vp]),

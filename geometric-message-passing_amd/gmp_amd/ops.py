@@ -684,6 +684,36 @@ class CFConvAggregateFn(torch.autograd.Function):
         return dx, dW, None, None, None
 
 
+class ShiftedSoftplusFn(torch.autograd.Function):
+    """softplus(x) - shift in one pass each way (K14 gmp_ssp_{fwd,bwd}_f32)."""
+
+    @staticmethod
+    def forward(ctx, x, shift):
+        lib = _lib.load()
+        y = torch.empty_like(x)
+        check(lib.gmp_ssp_fwd_f32(_p(x), x.numel(), float(shift), _p(y), _stream()),
+              "gmp_ssp_fwd_f32")
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        lib = _lib.load()
+        (x,) = ctx.saved_tensors
+        g = _f32c(g)
+        dx = torch.empty_like(x)
+        check(lib.gmp_ssp_bwd_f32(_p(x), _p(g), x.numel(), _p(dx), _stream()), "gmp_ssp_bwd_f32")
+        return dx, None
+
+
+def shifted_softplus(x, shift):
+    """F.softplus(x) - shift through K14 (CUDA fp32, numel % 4 == 0, 16-byte aligned)."""
+    x = _f32c(x)
+    _need_cuda(x)
+    return ShiftedSoftplusFn.apply(x, shift)
+
+
 def cfconv_propagate(edge_index, x, W):
     """sum_{e: dst[e] = i} x[src[e]] * W[e] for edge_index = (src, dst), N = x.shape[0]."""
     x, W = _f32c(x), _f32c(W)

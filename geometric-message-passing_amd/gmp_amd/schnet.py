@@ -27,6 +27,9 @@ class ShiftedSoftplus(nn.Module):
         self.shift = math.log(2.0)
 
     def forward(self, x):
+        if (x.is_cuda and x.dtype == torch.float32 and x.numel() % 4 == 0
+                and x.data_ptr() % 16 == 0):
+            return ops.shifted_softplus(x, self.shift)  # K14: one pass each way
         return F.softplus(x) - self.shift
 
 

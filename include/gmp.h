@@ -436,6 +436,17 @@ int gmp_cfconv_wgrad_f32(const float* g, int64_t n_g, const int64_t* gidx, const
                          int64_t n_x, const int64_t* xidx, int64_t n_items, int64_t F, float* dw,
                          int32_t* err, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * K14 shifted softplus (PyG ShiftedSoftplus, the SchNet filter-network / interaction
+ * activation, schnet.py:72): torch softplus semantics (beta 1, threshold 20) minus `shift`.
+ *   fwd: y = (x > 20 ? x : log1p(exp(x))) - shift
+ *   bwd: grad_x = x > 20 ? grad_y : grad_y * z / (z + 1), z = exp(x)
+ * n % 4 == 0, 16-byte aligned pointers.
+ * ------------------------------------------------------------------------------------------ */
+int gmp_ssp_fwd_f32(const float* x, int64_t n, float shift, float* y, void* stream);
+int gmp_ssp_bwd_f32(const float* x, const float* grad_y, int64_t n, float* grad_x,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

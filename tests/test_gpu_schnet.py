@@ -91,3 +91,22 @@ def test_cfconv_aggregate_out_of_range_raises():
     W = torch.randn(3, 8, device=DEV)
     with pytest.raises(IndexError):
         ops.cfconv_propagate(ei.flip(0), x, W)  # dst 9 >= N = 4
+
+
+def test_shifted_softplus_vs_torch():
+    """K14 (gmp_ssp_{fwd,bwd}_f32) against torch F.softplus(x) - log 2 on CPU fp32, across the
+    threshold (x > 20 is the identity branch) and deep negatives.  Tolerance 1e-6 abs +
+    1e-5 rel."""
+    import math
+    from gmp_amd import ops
+    x = torch.cat([torch.randn(4000) * 8, torch.tensor([-100., -20., 0., 19.99, 20., 20.01,
+                                                         50., 1e-7])])
+    g = torch.randn_like(x)
+    xd = x.to(DEV).requires_grad_(True)
+    y = ops.shifted_softplus(xd, math.log(2.0))
+    y.backward(g.to(DEV))
+    xr = x.clone().requires_grad_(True)
+    yr = torch.nn.functional.softplus(xr) - math.log(2.0)
+    yr.backward(g)
+    torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(xd.grad.cpu(), xr.grad, atol=1e-6, rtol=1e-5)
