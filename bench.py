@@ -1,11 +1,13 @@
 """Benchmark: edges/s forward+backward (one training step) of the geometric message-passing hot
 path on MI355X (BASELINE.json metric).
 
-Workload at N=1 (default, --workload egnn): config C2 — EGNN 4 layers, emb_dim 128, one seeded
-random 3-D radius graph with 50,000 nodes and ~1M directed edges (r = 5, box tuned), synthetic
-data, random-init weights.  --workload mace: config C4 (MACE L_max=2, correlation 3, 128
-channels, 5 layers, same graph); --workload tfn: config C5's per-GPU shard (TFN L_max=2, 64
-channels, 5 layers, gated, same graph).
+Default (--workload egnn+mace): the two halves of the metric in one run, one JSON line.
+`value` is config C2 — EGNN 4 layers, emb_dim 128, one seeded random 3-D radius graph with
+50,000 nodes and ~1M directed edges (r = 5, box tuned), synthetic data, random-init weights;
+the line's "mace" object is config C4 on the same graph (MACE L_max=2, correlation 3, 128
+channels, radial MLP hidden 256, 5 layers) with its own steps, roofline and cpu_baseline.
+--workload tfn: config C5's per-GPU shard (TFN L_max=2, 64 channels, 5 layers, gated, same
+graph); gvp / schnet: C3 / the C1 model on the C2 graph.
 A step = the reference training step (experiments/utils/train_utils.py:128-139): forward,
 L1 loss, backward, Adam step (gmp_amd/step.py; weight gradients computed on a side stream and
 accumulated at the end of the backward pass).  Weak scaling: every rank owns its own ~1M-edge
@@ -42,14 +44,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("egnn", "gvp", "mace", "tfn", "schnet"),
-                    default="egnn")
+    ap.add_argument("--workload", default="egnn+mace",
+                    choices=("egnn+mace", "egnn", "gvp", "mace", "tfn", "schnet"))
+    ap.add_argument("--mace-steps", type=int, default=3,
+                    help="timed steps of the secondary MACE workload (egnn+mace)")
+    ap.add_argument("--mace-warmup", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--emb", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=50_000)
     ap.add_argument("--edges", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: OMP_NUM_THREADS, else the physical "
+                         "cores this process may run on)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a HIP graph (measured slower than eager launch "
                          "on ROCm 7 for the EGNN step: off by default)")
@@ -69,21 +76,21 @@ WORKLOADS = {  # name -> (config tag, layers, emb)
 }
 
 
-def build_model(mod, args, radius):
-    if args.workload == "egnn":
-        return mod.EGNNModel(num_layers=args.layers, emb_dim=args.emb, in_dim=1, out_dim=1)
+def build_model(mod, workload, layers, emb):
+    if workload == "egnn":
+        return mod.EGNNModel(num_layers=layers, emb_dim=emb, in_dim=1, out_dim=1)
     # r_max = 10 (model default) with radius-5 graphs keeps edges away from the cutoff's fp32
     # cancellation near r_max
-    if args.workload == "mace":
-        return mod.MACEModel(num_layers=args.layers, emb_dim=args.emb, correlation=3,
-                             max_ell=2, in_dim=1, out_dim=1)
-    if args.workload == "schnet":
-        return mod.SchNetModel(hidden_channels=args.emb, in_dim=1, out_dim=1, num_filters=128,
-                               num_layers=args.layers, num_gaussians=50, cutoff=10)
-    if args.workload == "gvp":
-        return mod.GVPGNNModel(num_layers=args.layers, s_dim=args.emb, v_dim=16, s_dim_edge=32,
+    if workload == "mace":
+        return mod.MACEModel(num_layers=layers, emb_dim=emb, correlation=3, max_ell=2,
+                             mlp_dim=256, in_dim=1, out_dim=1)
+    if workload == "schnet":
+        return mod.SchNetModel(hidden_channels=emb, in_dim=1, out_dim=1, num_filters=128,
+                               num_layers=layers, num_gaussians=50, cutoff=10)
+    if workload == "gvp":
+        return mod.GVPGNNModel(num_layers=layers, s_dim=emb, v_dim=16, s_dim_edge=32,
                                v_dim_edge=1, in_dim=1, out_dim=1)
-    return mod.TFNModel(num_layers=args.layers, emb_dim=args.emb, max_ell=2, in_dim=1,
+    return mod.TFNModel(num_layers=layers, emb_dim=emb, max_ell=2, mlp_dim=256, in_dim=1,
                         out_dim=1)
 
 
@@ -157,41 +164,86 @@ def egnn_flops_per_edge(d):
     return {"egnn_edge_fwd": 2 * gemm, "egnn_edge_bwd": 2 * gemm}  # bwd: W3^T, W2^T
 
 
-def _atom_type(args):
+def _atom_type(workload):
     """Synthetic atom type: 0 (in_dim = 1 embeddings), 1 for SchNet, whose Embedding(100) keeps
     row 0 as padding (padding_idx = 0: a zero, gradient-free row)."""
-    return 1 if args.workload == "schnet" else 0
+    return 1 if workload == "schnet" else 0
 
 
-def cpu_baseline(g, args):
-    """Time the CPU oracle (fwd + L1 + bwd + Adam) on a spatial slab of the same graph."""
+def cpu_info():
+    """Host CPU model and the physical cores this process may run on (lscpu-equivalent)."""
+    model, cores = None, set()
+    try:
+        allowed = os.sched_getaffinity(0)
+    except AttributeError:  # pragma: no cover
+        allowed = set(range(os.cpu_count() or 1))
+    try:
+        cpu = phys = core = None
+        with open("/proc/cpuinfo") as f:
+            for line in f.read().splitlines() + [""]:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    cpu = int(v)
+                elif k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not line.strip() and cpu is not None:
+                    if cpu in allowed:
+                        cores.add((phys, core, cpu if core is None else None))
+                    cpu = phys = core = None
+    except OSError:  # pragma: no cover
+        pass
+    return model, (len(cores) or len(allowed)), len(allowed)
+
+
+def cpu_threads(args):
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS")
+    _, phys, _ = cpu_info()
+    return min(int(env), phys) if env and env.isdigit() and int(env) > 0 else phys
+
+
+def cpu_baseline(g, args, workload):
+    """Time the CPU oracle (fwd + L1 + bwd + Adam; plain PyTorch on the host cores): the full
+    graph for EGNN (C2 runs full size on the CPU), a spatial sample for the
+    others (the oracle's TP materialises 4 * weight_numel bytes per edge: 721 KB per edge for
+    MACE-128)."""
     from oracle import egnn as oegnn
+    from oracle import gvp as ogvp
     from oracle import mace as omace
+    from oracle import schnet as oschnet
     from gmp_amd.graph import Batch
 
-    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    threads = cpu_threads(args)
     torch.set_num_threads(threads)
-    if args.workload in ("egnn", "gvp", "schnet"):
-        frac = 0.25 if args.workload == "egnn" else 0.1  # slab x < frac * box
-        keep = g.pos[:, 0] < g.box * frac
-        shape = "spatial slab"
+    layers, emb = args.layers_of[workload], args.emb_of[workload]
+    if workload == "egnn":
+        sub, shape, timed = g, "all", 1
     else:
-        # the oracle's TP materialises 4 * weight_numel bytes per edge: a small corner cube
-        frac = 0.003
-        keep = (g.pos < g.box * frac ** (1.0 / 3.0)).all(dim=1)
-        shape = "corner cube"
-    idx = torch.nonzero(keep).view(-1)
-    remap = torch.full((g.num_nodes,), -1, dtype=torch.long)
-    remap[idx] = torch.arange(idx.numel())
-    ei = g.edge_index
-    m = keep[ei[0]] & keep[ei[1]]
-    sub = Batch(torch.full((idx.numel(),), _atom_type(args), dtype=torch.long), g.pos[idx],
-                remap[ei[:, m]], num_graphs=1)
+        if workload in ("gvp", "schnet"):
+            frac = 0.1  # slab x < frac * box
+            keep = g.pos[:, 0] < g.box * frac
+            shape = f"{frac:.0%}-volume spatial slab"
+        else:
+            frac = 0.002
+            keep = (g.pos < g.box * frac ** (1.0 / 3.0)).all(dim=1)
+            shape = f"{frac:.1%}-volume corner cube"
+        idx = torch.nonzero(keep).view(-1)
+        remap = torch.full((g.num_nodes,), -1, dtype=torch.long)
+        remap[idx] = torch.arange(idx.numel())
+        ei = g.edge_index
+        m = keep[ei[0]] & keep[ei[1]]
+        sub = Batch(torch.full((idx.numel(),), _atom_type(workload), dtype=torch.long),
+                    g.pos[idx], remap[ei[:, m]], num_graphs=1)
+        timed = 2 if workload in ("gvp", "schnet") else 1
     torch.manual_seed(0)
-    from oracle import gvp as ogvp
-    from oracle import schnet as oschnet
-    model = build_model({"egnn": oegnn, "gvp": ogvp, "schnet": oschnet}.get(args.workload, omace),
-                        args, g.radius)
+    mod = {"egnn": oegnn, "gvp": ogvp, "schnet": oschnet}.get(workload, omace)
+    model = build_model(mod, workload, layers, emb)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     y = torch.zeros(1)
 
@@ -201,71 +253,77 @@ def cpu_baseline(g, args):
         loss.backward()
         opt.step()
 
-    step()
+    step()  # warm-up (allocator, thread pool)
     ts = []
-    for _ in range(3):
+    for _ in range(timed):
         t0 = time.perf_counter()
         step()
         ts.append(time.perf_counter() - t0)
-    ts.sort()
-    med = ts[len(ts) // 2]
-    return {"value": sub.num_edges / med, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"oracle {args.workload} {args.layers}x{args.emb} fwd+bwd+Adam on a "
-                      f"{frac:.1%}-volume {shape} of the same graph ({sub.num_nodes} nodes, "
-                      f"{sub.num_edges} edges), median of 3 steps"}
+    t = sum(ts) / len(ts)
+    cpu_model, phys, logical = cpu_info()
+    return {"value": sub.num_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model, "host_cores_visible": {"physical": phys, "logical": logical},
+            "sample": f"oracle/{mod.__name__.split('.')[-1]}.py {workload} {layers}L/{emb} "
+                      f"fwd+L1+bwd+Adam (torch {torch.__version__} CPU, {threads} threads) on "
+                      f"{shape} of the bench graph ({sub.num_nodes} nodes, {sub.num_edges} "
+                      f"edges): 1 warm-up + mean of {timed} timed step(s), {t:.2f} s/step"}
 
 
-def main():
-    args = parse()
-    _, d_layers, d_emb = WORKLOADS[args.workload]
-    args.layers = args.layers or d_layers
-    args.emb = args.emb or d_emb
-    from gmp_amd import dist as gdist
-    # GMP_DIST_BACKEND=gloo rehearses the multi-process path with several ranks on one GPU
-    backend = os.environ.get("GMP_DIST_BACKEND", "nccl")
-    rank, world, local = gdist.init(backend)
-    if backend != "nccl":
-        local = 0
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
+def mace_roofline(model, n_nodes, n_edges, timers, n_steps):
+    """Roofline of the dominant MACE kernel from HIP-event timing inside the measured steps:
+    the receiver-factorised TP contraction."""
+    fl = tp_node_flops(model, n_nodes, n_edges)
+    keys = ("tp_node_S", "tp_node_W", "tp_node_dW", "tp_node_dZA")
+    t_gemm = sum(timers.get(k, 0.0) for k in keys) / n_steps
+    achieved = fl / (t_gemm * 1e-3) / 1e12
+    return {"kernel": "tp_node_gemm", "kernel_prefix": "-", "bound": "mfma",
+            "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+            "flops_per_step": fl, "tp_node_gemm_ms_per_step": t_gemm,
+            "split_ms_per_step": {k: timers.get(k, 0.0) / n_steps for k in keys},
+            "tp_node_prep_ms_per_step": timers.get("tp_node_prep", 0.0) / n_steps,
+            "tp_node_edge_bwd_ms_per_step": timers.get("tp_node_edge_bwd", 0.0) / n_steps,
+            "symmetric_contraction_ms_per_step":
+                (timers.get("symmetric_contraction_fwd", 0.0) +
+                 timers.get("symmetric_contraction_bwd", 0.0)) / n_steps}
 
+
+TIMER_NAMES = {"egnn": {"egnn_edge_fwd", "egnn_edge_bwd"}, "gvp": set(), "schnet": set()}
+
+
+def run_workload(workload, args, g, rank, world, dev, steps, warmup):
+    """Build the model, warm up, time `steps` steps (barrier + synchronize on both sides, max
+    over ranks); returns the bench record fields of this workload (rank 0) or None."""
     import gmp_amd
+    from gmp_amd import dist as gdist
     from gmp_amd import ops
-    from gmp_amd.graph import radius_graph
+    from gmp_amd.step import GraphedStep
 
-    g = radius_graph(num_nodes=args.nodes, target_edges=args.edges, seed=rank)
+    layers, emb = args.layers_of[workload], args.emb_of[workload]
     torch.manual_seed(0)
-    model = build_model(gmp_amd, args, g.radius).to(dev)
-    core = model
+    model = build_model(gmp_amd, workload, layers, emb).to(dev)
     # Adam (the reference optimizer, train_utils.py): the fused multi-tensor implementation
     # (one launch per step); capturable (step counter on the device) for HIP-graph replay
     opt = (torch.optim.Adam(model.parameters(), lr=1e-4, capturable=True) if args.graph
            else torch.optim.Adam(model.parameters(), lr=1e-4, fused=True))
     batch = g.to(dev)
-    if _atom_type(args):
-        batch.atoms = torch.full_like(batch.atoms, _atom_type(args))
+    if _atom_type(workload):
+        batch.atoms = torch.full_like(batch.atoms, _atom_type(workload))
     y = torch.randn(1, device=dev)
 
     def loss_fn():
         return torch.nn.functional.l1_loss(model(batch).view(-1), y, reduction="sum")
 
-    # one process per GPU; the step (fwd + L1 + bwd [+ one flat RCCL all-reduce] + Adam) is
-    # captured once and replayed (gmp_amd/step.py); --no-graph runs the same sequence eagerly
-    from gmp_amd.step import GraphedStep
-    step = GraphedStep(model, loss_fn, opt, warmup=args.warmup, use_graph=args.graph)
-
-    barrier = gdist.barrier
-
-    # only the regions the roofline below reads are timed inside the measured steps
-    ops.KERNEL_TIMER_NAMES = {"egnn": {"egnn_edge_fwd", "egnn_edge_bwd"}, "gvp": set()}.get(
-        args.workload)
+    step = GraphedStep(model, loss_fn, opt, warmup=warmup, use_graph=args.graph)
+    # only the regions the roofline reads are timed inside the measured steps
+    ops.KERNEL_TIMER_NAMES = TIMER_NAMES.get(workload)
     if not args.graph:
         ops.KERNEL_TIMERS = {}
-    barrier()
+    gdist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
-    barrier()
+    gdist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = gdist.max_over_ranks(elapsed, dev)
     total_edges = gdist.sum_over_ranks(g.num_edges, dev)
@@ -276,19 +334,16 @@ def main():
             step._eager()
         torch.cuda.synchronize()
     timers = {k: ops.kernel_time_ms(k) for k in list(ops.KERNEL_TIMERS)}
-    n_timed_steps = args.steps if not args.graph else max(1, args.timing_steps)
+    n_timed = steps if not args.graph else max(1, args.timing_steps)
     totals = {k: timers[k] * len(v) for k, v in ops.KERNEL_TIMERS.items()}
     ops.KERNEL_TIMERS = None
-
-    def sum_ms(name):
-        return totals.get(name, 0.0)
-
+    rec = None
     if rank == 0:
-        if args.workload == "egnn":
-            fl = egnn_flops_per_edge(args.emb)
+        if workload == "egnn":
+            fl = egnn_flops_per_edge(emb)
             ms_fwd, ms_bwd = timers["egnn_edge_fwd"], timers["egnn_edge_bwd"]
             tflops = fl["egnn_edge_bwd"] * g.num_edges / (ms_bwd * 1e-3) / 1e12
-            bpe = egnn_bwd_bytes_per_edge(args.emb, g.num_nodes, g.num_edges)
+            bpe = egnn_bwd_bytes_per_edge(emb, g.num_nodes, g.num_edges)
             gbs = bpe * g.num_edges / (ms_bwd * 1e-3) / 1e9
             f_mfma, f_hbm = tflops / FP32_MFMA_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
             # both bounds are reported; the primary one is the closer of the two
@@ -298,81 +353,93 @@ def main():
             else:
                 prim = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": f_hbm}
-            roof = {"kernel": "egnn_edge_bwd", **prim,
+            roof = {"kernel": "egnn_edge_bwd", "kernel_prefix": "egnn_bwd_kernel", **prim,
                     "traffic": None, "ms_per_launch": ms_bwd,
                     "flops_per_edge": fl["egnn_edge_bwd"], "mfma_frac": f_mfma,
                     "bytes_per_edge_min": bpe, "hbm_gbs": gbs, "hbm_frac": f_hbm,
                     "fwd_kernel_ms": ms_fwd,
                     "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
                     / (ms_fwd * 1e-3) / 1e12}
-        elif args.workload == "schnet":
-            # no single dominant HIP kernel: whole step against the fp32 MFMA peak, counting
-            # the CFConv filter network (50 -> F -> F per edge; K6) fwd + 2x bwd per layer
-            F = 128
-            fl = 3 * 2 * (50 * F + F * F) * args.layers
-            achieved = fl * g.num_edges / (elapsed / args.steps) / 1e12
-            roof = {"kernel": "whole step (fwd+bwd, all kernels)", "kernel_prefix": "-",
-                    "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                    "traffic": None, "flops_per_edge": fl}
-        elif args.workload == "gvp":
-            # no single dominant HIP kernel yet (torch GEMMs on gathered rows): whole step
-            fl = gvp_flops_per_edge(args.emb, 16, 32, 1) * 3 * args.layers
-            achieved = fl * g.num_edges / (elapsed / args.steps) / 1e12
+        elif workload in ("schnet", "gvp"):
+            # no single dominant HIP kernel: whole step against the fp32 MFMA peak
+            if workload == "schnet":  # CFConv filter network (50 -> F -> F per edge; K6)
+                F = 128
+                fl = 3 * 2 * (50 * F + F * F) * layers
+            else:
+                fl = gvp_flops_per_edge(emb, 16, 32, 1) * 3 * layers
+            achieved = fl * g.num_edges / (elapsed / steps) / 1e12
             roof = {"kernel": "whole step (fwd+bwd, all kernels)", "kernel_prefix": "-",
                     "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                     "traffic": None, "flops_per_edge": fl}
         else:
-            # receiver-factorised K7: rocBLAS GEMMs over S / T (timed region "tp_node_gemm"
-            # includes the padded gathers) — MFMA-bound; algorithmic flops per step below
-            fl = tp_node_flops(core, g.num_nodes, g.num_edges)
-            t_gemm = sum(sum_ms(k) for k in ("tp_node_S", "tp_node_W", "tp_node_dW",
-                                              "tp_node_dZA")) / n_timed_steps
-            achieved = fl / (t_gemm * 1e-3) / 1e12
-            roof = {"kernel": "tp_node_gemm", "kernel_prefix": "-", "bound": "mfma",
-                    "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                    "flops_per_step": fl, "tp_node_gemm_ms_per_step": t_gemm,
-                    "split_ms_per_step": {k: sum_ms(k) / n_timed_steps for k in
-                                          ("tp_node_S", "tp_node_W", "tp_node_dW",
-                                           "tp_node_dZA")},
-                    "tp_node_prep_ms_per_step": sum_ms("tp_node_prep") / n_timed_steps,
-                    "tp_node_edge_bwd_ms_per_step": sum_ms("tp_node_edge_bwd") / n_timed_steps,
-                    "symmetric_contraction_ms_per_step":
-                        (sum_ms("symmetric_contraction_fwd") +
-                         sum_ms("symmetric_contraction_bwd")) / n_timed_steps}
-        t = pmc_traffic(args.workload, roof["kernel_prefix"] if "kernel_prefix" in roof
-                        else {"egnn_edge_bwd": "egnn_bwd_kernel",
-                              "tp_conv_bwd": "tp_bwd_kernel"}[roof["kernel"]])
+            roof = mace_roofline(model, g.num_nodes, g.num_edges, totals, n_timed)
+        t = pmc_traffic(workload, roof["kernel_prefix"])
         if t is not None:
             roof["traffic"], roof["traffic_source"] = t[0], f"profiles/{t[1]}"
+        rec = {"value": total_edges * steps / elapsed, "unit": "edges/s", "steps": steps,
+               "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
+               "workload": f"{WORKLOADS[workload][0]} {layers}L/{emb} radius graph "
+                           f"{g.num_nodes} nodes / {g.num_edges} edges per GPU "
+                           f"(r={g.radius}, box={g.box:.3f}, seed=rank)",
+               "roofline": roof, "cpu_baseline": None}
+    del step, opt, model, batch
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return rec
+
+
+def main():
+    args = parse()
+    names = args.workload.split("+")
+    args.layers_of = {w: args.layers or WORKLOADS[w][1] for w in names}
+    args.emb_of = {w: args.emb or WORKLOADS[w][2] for w in names}
+    from gmp_amd import dist as gdist
+    # GMP_DIST_BACKEND=gloo rehearses the multi-process path with several ranks on one GPU
+    backend = os.environ.get("GMP_DIST_BACKEND", "nccl")
+    rank, world, local = gdist.init(backend)
+    if backend != "nccl":
+        local = 0
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+    from gmp_amd.graph import radius_graph
+
+    g = radius_graph(num_nodes=args.nodes, target_edges=args.edges, seed=rank)
+    recs = {}
+    for k, w in enumerate(names):
+        steps, warmup = ((args.steps, args.warmup) if k == 0 else
+                         (min(args.steps, args.mace_steps), max(1, min(args.warmup,
+                                                                       args.mace_warmup))))
+        recs[w] = run_workload(w, args, g, rank, world, dev, steps, warmup)
+    if rank == 0:
+        main_rec = recs[names[0]]
         rec = {
             "metric": "edges/sec forward+backward, EGNN & MACE L=2, 1M-edge radius graph, "
                       "1/2/4/8 GPU",
-            "value": total_edges * args.steps / elapsed,
+            "value": main_rec["value"],
             "unit": "edges/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "steps": main_rec["steps"],
+            "warmup": main_rec["warmup"],
+            "ms_per_step": main_rec["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded random radius graph per rank, random-init weights)",
-            "config": {"workload": f"{WORKLOADS[args.workload][0]} {args.layers}L/{args.emb} "
-                                   f"radius graph "
-                                   f"{g.num_nodes} nodes / {g.num_edges} edges per GPU "
-                                   f"(r={g.radius}, box={g.box:.3f}, seed=rank)",
+            "config": {"workload": main_rec["workload"], "value_is": names[0],
                        "global_batch": world, "parallelism": f"dp{world}",
                        "step": "fwd + L1 loss + bwd + Adam",
                        "launch": "eager" if not args.graph else "hip graph replay"},
-            "roofline": roof,
+            "roofline": main_rec["roofline"],
             "cpu_baseline": None,
         }
+        for w in names[1:]:
+            rec[w] = {k: v for k, v in recs[w].items()}
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(g, args)
+            rec["cpu_baseline"] = cpu_baseline(g, args, names[0])
+            for w in names[1:]:
+                rec[w]["cpu_baseline"] = cpu_baseline(g, args, w)
         print(json.dumps(rec), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

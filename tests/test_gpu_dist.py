@@ -1,0 +1,166 @@
+"""Multi-process data-parallel path of the PRODUCT models on the GPU: two gloo
+ranks share the one MI355X (spawned child processes; the parent pytest process touches no
+device tensor), each owning one graph, through
+
+* the bench's executor (gmp_amd/step.py GraphedStep, eager launch): parameter broadcast from
+  rank 0, HIP forward/backward with the weight gradients deferred to the side stream, ONE flat
+  all-reduce of the gradients, fused Adam;
+* DDP (gmp_amd/dist.wrap_ddp: deferral switched off so the reducer's per-parameter hooks see
+  every gradient through autograd, find_unused_parameters for the readout slices).
+
+After two Adam steps the parameters must equal a single process that averages the gradients of
+the same two graphs (rank 0 computes that reference in its own process after the collective
+part).  Tolerance 1e-5 (atol + rtol): the all-reduce sums two per-rank gradients exactly as the
+single process accumulates them (scaling by 1/2 is exact); the rest is fp32 Adam.
+Multi-GPU scaling itself is unmeasured on hardware here (the driver owns 8-GPU runs)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "egnn": dict(num_layers=2, emb_dim=128, in_dim=1, out_dim=1),
+    "tfn": dict(num_layers=2, emb_dim=16, mlp_dim=64, r_max=2.5, in_dim=1, out_dim=1),
+}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _graph(rank):
+    from gmp_amd.graph import radius_graph
+    g = radius_graph(num_nodes=250, target_edges=3000, r=2.5, seed=10 + rank, tol=0.2,
+                     shuffle=True)
+    n = g.num_nodes  # the reference scatters have no dim_size: the last node must receive
+    extra = torch.tensor([[n - 2, n - 1], [n - 1, n - 2]])
+    g.edge_index = torch.cat([g.edge_index, extra], 1)
+    return g
+
+
+def _model(kind):
+    import gmp_amd
+    torch.manual_seed(0)
+    cls = {"egnn": gmp_amd.EGNNModel, "tfn": gmp_amd.TFNModel}[kind]
+    return cls(**CASES[kind])
+
+
+def _loss(model, b, y):
+    return torch.nn.functional.l1_loss(model(b).view(-1), y, reduction="sum")
+
+
+def _rank_worker(rank, world, port, out_dir, kind, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from gmp_amd import dist as gdist
+    from gmp_amd import ops
+    from gmp_amd.step import GraphedStep
+    gdist.init("gloo")
+    dev = torch.device("cuda", 0)  # both ranks on the one GPU of the box
+    torch.cuda.set_device(dev)
+    y = torch.tensor([0.25], device=dev)
+    if mode == "ddp":
+        torch.manual_seed(rank)
+        model = _model(kind).to(dev)
+        if rank != 0:  # a different init on rank 1: DDP must broadcast rank 0's
+            with torch.no_grad():
+                for p in model.parameters():
+                    p.add_(0.01)
+        model = gdist.wrap_ddp(model, local=0)
+        assert not ops.DEFER_WEIGHT_GRADS
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+        b = _graph(rank).to(dev)
+        for it in range(2):
+            opt.zero_grad(set_to_none=True)
+            _loss(model, b, y).backward()
+            if it == 0:
+                grads = {k: p.grad.detach().cpu() for k, p in model.module.named_parameters()
+                         if p.grad is not None}
+            opt.step()
+        params = {k: p.detach().cpu() for k, p in model.module.named_parameters()}
+    else:
+        model = _model(kind).to(dev)
+        if rank != 0:  # the executor must broadcast rank 0's parameters
+            with torch.no_grad():
+                for p in model.parameters():
+                    p.add_(0.01)
+        assert ops.DEFER_WEIGHT_GRADS
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2, fused=True)
+        b = _graph(rank).to(dev)
+        step = GraphedStep(model, lambda: _loss(model, b, y), opt, warmup=0, use_graph=False)
+        for it in range(2):
+            step()
+            if it == 0:
+                torch.cuda.synchronize()
+                grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()
+                         if p.grad is not None}
+        torch.cuda.synchronize()
+        params = {k: p.detach().cpu() for k, p in model.named_parameters()}
+    torch.save({"params": params, "grads": grads}, os.path.join(out_dir, f"{mode}{rank}.pt"))
+    torch.distributed.destroy_process_group()
+    if rank == 0:
+        # single-process reference on the same GPU: mean of the two graphs' gradients
+        ops.DEFER_WEIGHT_GRADS = mode != "ddp"
+        ref = _model(kind).to(dev)
+        opt = torch.optim.Adam(ref.parameters(), lr=1e-2, fused=(mode != "ddp"))
+        graphs = [_graph(r).to(dev) for r in range(world)]
+        for it in range(2):
+            opt.zero_grad(set_to_none=True)
+            for g in graphs:
+                (_loss(ref, g, y) / world).backward()
+            for p in ref.parameters():  # the executor all-reduces zeros for unused parameters
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            if it == 0:
+                torch.cuda.synchronize()
+                grads = {k: p.grad.detach().cpu() for k, p in ref.named_parameters()}
+            opt.step()
+        torch.cuda.synchronize()
+        torch.save({"params": {k: p.detach().cpu() for k, p in ref.named_parameters()},
+                    "grads": grads}, os.path.join(out_dir, f"{mode}_ref.pt"))
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("kind", ["egnn", "tfn"])
+@pytest.mark.parametrize("mode", ["step", "ddp"])
+def test_product_world2_gloo_on_gpu_matches_single_process(kind, mode):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rank_worker, args=(world, _free_port(), d, kind, mode),
+                           nprocs=world, start_method="spawn", join=True)
+        res = [torch.load(os.path.join(d, f"{mode}{r}.pt"), weights_only=True)
+               for r in range(world)]
+        ref = torch.load(os.path.join(d, f"{mode}_ref.pt"), weights_only=True)
+    # the first step's averaged gradients (what the collective delivered to the optimizer)
+    for k, g in ref["grads"].items():
+        for r in range(world):
+            got = res[r]["grads"].get(k, torch.zeros_like(g))
+            err, scale = (got - g).abs().max().item(), g.abs().max().item()
+            print(f"grad {k} rank {r}: max|d| {err:.3e} scale {scale:.3e}")
+            assert err <= 1e-5 * scale + 1e-7, (k, r, err, scale)
+    moved = 0
+    for k, p in ref["params"].items():
+        for r in range(world):
+            got = res[r]["params"][k]
+            err = (got - p).abs().max().item()
+            print(f"param {k} rank {r}: max|d| {err:.3e}")
+            torch.testing.assert_close(got, p, atol=1e-5, rtol=1e-5)
+        moved += int(not torch.equal(p, _init_cpu(kind)[k]))
+    assert moved > len(ref["params"]) // 2  # the steps really trained (not vacuous)
+
+
+_INIT = {}
+
+
+def _init_cpu(kind):
+    if kind not in _INIT:
+        _INIT[kind] = {k: p.detach().clone() for k, p in _model(kind).named_parameters()}
+    return _INIT[kind]

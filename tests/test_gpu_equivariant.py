@@ -230,3 +230,96 @@ def test_symmetric_contraction_k8_golden(golden):
     torch.testing.assert_close(y.detach().cpu(), d["out"], atol=1e-5, rtol=1e-5)
     (y * d["g_out"].to(DEV)).sum().backward()
     torch.testing.assert_close(x.grad.cpu(), d["grad_x"], atol=1e-5, rtol=1e-5)
+
+
+def _fp64_model_check(kind, kw, n, e_per_node, seeds=(1, 2), in_dim=3):
+    """Model forward/backward against the fp32 oracle and its fp64 copy on a 2-graph batch:
+    outputs within 1e-5 * max(1, |y64|) + 2 |y_ref32 - y64|, gradients within 2e-4 of each
+    gradient's scale (the test_model_vs_oracle contract)."""
+    from gmp_amd import equivariant as eq
+    from gmp_amd.graph import Batch, collate
+    torch.manual_seed(11)
+    graphs = [_graph(n, e_per_node * n, seed=s, r=2.5) for s in seeds]
+    for gg in graphs:
+        gg.atoms = torch.randint(0, in_dim, (gg.num_nodes,))
+    b = collate(graphs)
+    kw = dict(kw, in_dim=in_dim)
+    ref = getattr(om, kind)(**kw)
+    model = getattr(eq, kind)(**kw)
+    model.load_state_dict(ref.state_dict())
+    model = model.to(DEV)
+    ref64 = copy.deepcopy(ref).double()
+    bd = Batch(b.atoms.to(DEV), b.pos.to(DEV).requires_grad_(True), b.edge_index.to(DEV),
+               b.batch.to(DEV), num_graphs=b.num_graphs)
+    br = Batch(b.atoms, b.pos.clone().requires_grad_(True), b.edge_index, b.batch,
+               num_graphs=b.num_graphs)
+    b64 = Batch(b.atoms, b.pos.double().requires_grad_(True), b.edge_index, b.batch,
+                num_graphs=b.num_graphs)
+    y, yr, y64 = model(bd), ref(br), ref64(b64)
+    err = (y.detach().cpu().double() - y64.detach()).abs().max().item()
+    err_ref = (yr.detach().double() - y64.detach()).abs().max().item()
+    scale = y64.abs().max().item()
+    assert err <= 1e-5 * max(1.0, scale) + 2 * err_ref, (err, err_ref, scale)
+    y.square().sum().backward()
+    y64.square().sum().backward()
+    for (name, p), q in zip(model.named_parameters(), ref64.parameters()):
+        if q.grad is None:
+            continue
+        _close_scaled(p.grad.double(), q.grad, 2e-4, name)
+    _close_scaled(bd.pos.grad.double(), b64.pos.grad, 2e-4, "dpos")
+    return b.num_edges
+
+
+def test_mace_c4_config_vs_oracle():
+    """Config C4 exactly as benchmarked (MACE L_max=2, correlation 3, 128 channels, radial MLP
+    hidden 256, 5 layers, BatchNorm on; mace.py:27-35 defaults) on a small radius-graph batch."""
+    ne = _fp64_model_check("MACEModel", dict(num_layers=5, emb_dim=128, correlation=3,
+                                             max_ell=2, mlp_dim=256, r_max=10.0), 60, 10)
+    assert ne <= 2000
+
+
+def test_tfn_c5_per_rank_model_vs_oracle():
+    """Config C5's per-rank model (TFN L_max=2, 64 channels, radial hidden 256, 5 layers, gated,
+    first-node pooling; tfn.py:53-60 defaults)."""
+    ne = _fp64_model_check("TFNModel", dict(num_layers=5, emb_dim=64, max_ell=2, mlp_dim=256,
+                                            gate=True, r_max=10.0), 80, 10)
+    assert ne <= 2000
+
+
+def test_mace_c4_full_size_properties():
+    """C4 at full size (50k nodes / ~1M edges, the bench graph): the training step's forward
+    and backward are deterministic (bitwise), and the prediction is invariant to the input edge
+    order and to a rotation + translation of the positions, within 1e-5 relative."""
+    from gmp_amd import equivariant as eq
+    from gmp_amd.graph import Batch, radius_graph
+    g = radius_graph()  # the C2/C4 bench graph, seed 0
+    torch.manual_seed(0)
+    model = eq.MACEModel(num_layers=5, emb_dim=128, correlation=3, max_ell=2, mlp_dim=256,
+                         in_dim=1, out_dim=1).to(DEV)
+    ei = g.edge_index.to(DEV)
+    pos = g.pos.to(DEV)
+    atoms = g.atoms.to(DEV)
+
+    def run(p, e, grad=True):
+        model.zero_grad(set_to_none=True)
+        y = model(Batch(atoms, p, e, num_graphs=1))
+        if not grad:
+            return y.detach().double(), None
+        y.sum().backward()
+        return y.detach().double(), model.convs[2].fc[2].weight.grad.clone()
+
+    # train mode (batch statistics, as in the step): the statistics are themselves invariant
+    with torch.no_grad():
+        y0, _ = run(pos, ei, grad=False)
+        perm = torch.randperm(ei.shape[1], device=DEV)
+        yp, _ = run(pos, ei[:, perm], grad=False)
+        R = oo3.wigner_D(1, *(torch.tensor(a, dtype=torch.float64) for a in (0.3, 1.1, -0.6)))
+        pos_r = (g.pos.double() @ R.T + torch.tensor([0.5, -2.0, 1.0], dtype=torch.float64))
+        yr, _ = run(pos_r.float().to(DEV), ei, grad=False)
+    scale = y0.abs().max().item()
+    assert (yp - y0).abs().max().item() <= 1e-5 * scale, (yp, y0)
+    assert (yr - y0).abs().max().item() <= 1e-5 * scale, (yr, y0)
+    a = run(pos, ei)
+    b = run(pos, ei)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert a[1].abs().max().item() > 0
