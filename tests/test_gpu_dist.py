@@ -8,10 +8,15 @@ device tensor), each owning one graph, through
 * DDP (gmp_amd/dist.wrap_ddp: deferral switched off so the reducer's per-parameter hooks see
   every gradient through autograd, find_unused_parameters for the readout slices).
 
-After two Adam steps the parameters must equal a single process that averages the gradients of
-the same two graphs (rank 0 computes that reference in its own process after the collective
-part).  Tolerance 1e-5 (atol + rtol): the all-reduce sums two per-rank gradients exactly as the
-single process accumulates them (scaling by 1/2 is exact); the rest is fp32 Adam.
+The first step's averaged gradients must equal those of a single process that averages the
+gradients of the same two graphs (rank 0 computes that reference in its own process after the
+collective part), within 1e-5 of each gradient's scale (measured: bitwise equal — the
+all-reduce sums two per-rank gradients exactly as the single process accumulates them; scaling
+by 1/2 is exact).  Parameters after two Adam steps: bitwise equal for the executor; under DDP
+the second step's gradients were measured to differ in the last bits (max 3e-7 on the
+parameters), which Adam's per-coordinate normalisation amplifies where a gradient coordinate
+is near zero (one of 32,896 entries: 1.4e-5 after two lr = 1e-2 steps) — the parameter check
+therefore allows 1e-4 absolute (1 % of one Adam step).
 Multi-GPU scaling itself is unmeasured on hardware here (the driver owns 8-GPU runs)."""
 import os
 import socket
@@ -152,7 +157,7 @@ def test_product_world2_gloo_on_gpu_matches_single_process(kind, mode):
             got = res[r]["params"][k]
             err = (got - p).abs().max().item()
             print(f"param {k} rank {r}: max|d| {err:.3e}")
-            torch.testing.assert_close(got, p, atol=1e-5, rtol=1e-5)
+            torch.testing.assert_close(got, p, atol=1e-4 if mode == "ddp" else 1e-5, rtol=1e-5)
         moved += int(not torch.equal(p, _init_cpu(kind)[k]))
     assert moved > len(ref["params"]) // 2  # the steps really trained (not vacuous)
 
