@@ -159,9 +159,23 @@ __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __rest
   __shared__ float part[kSG][kSC];
   const int c = threadIdx.x % kSC, q = threadIdx.x / kSC;
   const int f = blockIdx.x * kSC + c;
+  // rows q, q + kSG, ... added in that order; their loads are issued kU at a time (one memory
+  // round trip per kU rows instead of one per row: the loop was latency-bound)
+  constexpr int kU = 16;
   float s = 0.f;
-  if (f < width)
-    for (int r = q; r < nrows; r += kSG) s += partials[(int64_t)r * width + f];
+  if (f < width) {
+    for (int r0 = q; r0 < nrows; r0 += kU * kSG) {
+      float v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int r = r0 + u * kSG;
+        v[u] = r < nrows ? partials[(int64_t)r * width + f] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (r0 + u * kSG < nrows) s += v[u];
+    }
+  }
   part[q][c] = s;
   __syncthreads();
   if (q == 0 && f < width) {

@@ -1,0 +1,510 @@
+// K7g: the path GEMMs of the receiver-factorised tensor-product convolution (gmp_tp.hip "node
+// form", tfn_layer.py:73-87 regrouped) on the bf16 MFMA through exact three-plane splits:
+//
+//   forward   out[(n,k), w] += sum_{u,j} S[(n,k), (u,j)] W2p[(u,j), w] + sum_u Sb[(n,k), u] b2p[u, w]
+//   backward  T[(n,k), (u,j)] = sum_w G[(n,k), w] W2p[(u,j), w]
+//
+// as one kernel C (+)= A B^T with A f32 (M x K, split on load) and B pre-split into three bf16
+// planes [3][N][K] (gmp_tp_split_w2_f32, once per pass).  Every f32 operand x = x0 + x1 + x2
+// exactly (RNE splits), and C accumulates the six plane products of order <= 2^-16,
+// A2 B0 + A1 B1 + A0 B2 + A1 B0 + A0 B1 + A0 B0, in f32 (dropped terms <= 2^-26 |ab|; the same
+// arithmetic as the K5 edge outer sums, gmp_wgrad.hip, measured f32-class there).  Six
+// v_mfma_f32_16x16x32_bf16 (16 cycles each) replace eight v_mfma_f32_16x16x4_f32 (32 cycles)
+// per 32-deep k step of a 16 x 16 tile: 2.7x less matrix time than the f32 MFMA (1/16 of the
+// bf16 rate on gfx950, no xf32).
+//
+// Tiling: 512 threads (8 waves as 2 (M) x 4 (N)), a 128 x 128 output tile per workgroup, one
+// 32-deep k stage per step, wave tile 64 x 32 (4 x 2 MFMA tiles).  LDS image per stage: A and B
+// as [plane][row][32 k] bf16 (64-byte rows, 16-byte chunk q at q ^ ((row >> 1) & 3)): the MFMA
+// operand read (row = lane & 15, k = 8 (lane >> 4) .. +7) is one conflict-free ds_read_b128.
+// Loads run two stages ahead in a register ring (no branches: clamped addresses, masked in the
+// stash), two LDS stages (96 KB, one workgroup per CU).  Tiles are grouped (8 M tiles per group,
+// N tiles inside a group) and dealt XCD-contiguously so workgroups that share an operand block
+// share an L2.  A second A operand (A2, K2 columns) continues the k range: the bias term of the
+// forward rides in the same accumulators.  The epilogue stores C at
+//   (r / cgrp) * cldg + (r % cgrp) * cldr + col * cldn
+// so the forward adds its (n, k)-row result straight into the receivers' mul_ir output block
+// (row stride out_dim, k stride 1, w stride 2lo+1) and the backward writes row-major T.
+#include "gmp_common.h"
+
+namespace gmp {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGT = 512;               // threads (8 waves)
+constexpr int kBM = 128, kBN = 128;    // output tile
+constexpr int kBK = 32;                // k per stage (= the bf16 MFMA k)
+constexpr int kPlane = 128 * 64;       // bytes of one plane image (128 rows x 32 bf16)
+constexpr int kStage = 6 * kPlane;     // A planes then B planes
+constexpr int kGroupM = 8;             // M tiles per tile group
+
+__device__ __forceinline__ void split3(f32x2 x, unsigned& h, unsigned& m, unsigned& l) {
+  const bf16x2 bh = __builtin_convertvector(x, bf16x2);
+  const f32x2 r1 = x - __builtin_convertvector(bh, f32x2);   // exact
+  const bf16x2 bm = __builtin_convertvector(r1, bf16x2);
+  const f32x2 r2 = r1 - __builtin_convertvector(bm, f32x2);  // exact, <= 8 significant bits
+  const bf16x2 bl = __builtin_convertvector(r2, bf16x2);     // exact
+  h = __builtin_bit_cast(unsigned, bh);
+  m = __builtin_bit_cast(unsigned, bm);
+  l = __builtin_bit_cast(unsigned, bl);
+}
+
+__device__ __forceinline__ int xoff(int row, int chunk) {
+  return row * 64 + 16 * (chunk ^ ((row >> 1) & 3));
+}
+
+// One k step's MFMA operands of a wave (64 x 32 output block: 4 row tiles x 2 column tiles,
+// three bf16 planes each).  The main loops hold two of them: the fragments of step s + 1 are
+// read from LDS while the MFMAs of step s run (one barrier per step).
+struct Frag {
+  bf16x8 a[4][3];
+  bf16x8 b[2][3];
+};
+
+__device__ __forceinline__ void load_frag(Frag& f, const unsigned char* aimg,
+                                          const unsigned char* bimg, int wm, int wn, int li,
+                                          int g) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int off = xoff(64 * wm + 16 * r + li, g);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f.a[r][p] = *reinterpret_cast<const bf16x8*>(aimg + p * kPlane + off);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int off = xoff(32 * wn + 16 * c + li, g);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f.b[c][p] = *reinterpret_cast<const bf16x8*>(bimg + p * kPlane + off);
+  }
+}
+
+// acc += A B over one 32-deep step: the six plane products, smallest first
+__device__ __forceinline__ void mma_x3(f32x4 (&acc)[4][2], const Frag& f) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      f32x4 t = acc[r][c];
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][2], f.b[c][0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][1], f.b[c][1], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][0], f.b[c][2], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][1], f.b[c][0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][0], f.b[c][1], t, 0, 0, 0);
+      acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][0], f.b[c][0], t, 0, 0, 0);
+    }
+  }
+}
+
+template <bool ACC>
+__global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
+    int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
+    const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
+    int64_t ldb, int64_t bplane, float* __restrict__ C, int64_t cgrp, int64_t cldg,
+    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smg[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wm = w >> 2, wn = w & 3;
+
+  // XCD-contiguous logical id (blocks b, b + 8, ... share an XCD under round-robin dealing;
+  // speed only), then grouped tile order
+  const int64_t nwg = (int64_t)tiles_m * tiles_n;
+  int64_t L;
+  {
+    const int64_t b = blockIdx.x, x = b & 7, q = nwg >> 3, r = nwg & 7;
+    L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int64_t per_group = (int64_t)kGroupM * tiles_n;
+  const int64_t grp = L / per_group;
+  const int64_t first_m = grp * kGroupM;
+  const int64_t gsize = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
+  const int64_t in_grp = L - grp * per_group;
+  const int64_t tm = first_m + in_grp % gsize, tn = in_grp / gsize;
+  const int64_t m0 = tm * kBM, n0 = tn * kBN;
+
+  const int64_t Ktot = K1 + K2;
+  const int nst = (int)(Ktot / kBK);
+
+  // loaders: A units (2 per thread) = (row, float4 of k), B units (3 per thread: one per plane)
+  int arow[2], akq[2];
+  bool aok[2];
+  const float* abase1[2];
+  const float* abase2[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int v = tid + kGT * q;
+    arow[q] = v >> 3;
+    akq[q] = v & 7;
+    const int64_t gr = m0 + arow[q];
+    aok[q] = gr < M;
+    const int64_t grc = gr < M ? gr : M - 1;
+    abase1[q] = A1 + grc * lda1 + 4 * akq[q];
+    abase2[q] = A2 ? A2 + grc * lda2 + 4 * akq[q] : abase1[q];
+  }
+  const int brow = tid >> 2, bch = tid & 3;
+  const bool bok = n0 + brow < N;
+  const unsigned short* bbase =
+      Bp + (n0 + brow < N ? n0 + brow : (int64_t)N - 1) * ldb + 8 * bch;
+
+  f32x4 ringA[2][2];
+  u32x4 ringB[2][3];
+  auto fetch = [&](int slot, int st) {
+    const int stc = st < nst ? st : nst - 1;
+    const int64_t k0 = (int64_t)stc * kBK;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float* p = k0 < K1 ? abase1[q] + k0 : abase2[q] + (k0 - K1);
+      ringA[slot][q] = *reinterpret_cast<const f32x4*>(p);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      ringB[slot][p] = *reinterpret_cast<const u32x4*>(bbase + p * bplane + k0);
+  };
+  auto stash = [&](int slot, unsigned char* buf, int st) {
+    const bool live = st < nst;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      f32x4 v = ringA[slot][q];
+      if (!(live && aok[q])) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      unsigned h0, m0_, l0, h1, m1, l1;
+      split3(f32x2{v[0], v[1]}, h0, m0_, l0);
+      split3(f32x2{v[2], v[3]}, h1, m1, l1);
+      const int off = xoff(arow[q], akq[q] >> 1) + 8 * (akq[q] & 1);
+      *reinterpret_cast<u32x2*>(buf + off) = u32x2{h0, h1};
+      *reinterpret_cast<u32x2*>(buf + kPlane + off) = u32x2{m0_, m1};
+      *reinterpret_cast<u32x2*>(buf + 2 * kPlane + off) = u32x2{l0, l1};
+    }
+    const int off = xoff(brow, bch);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      u32x4 v = ringB[slot][p];
+      if (!(live && bok)) v = u32x4{0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(buf + (3 + p) * kPlane + off) = v;
+    }
+  };
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Pipeline (stage t's registers in ring slot t & 1, its LDS image in buffer t & 1):
+  //   iteration s: read the fragments of s + 1 | MFMAs of s | split + write stage s + 2 into
+  //   the buffer stage s used (its fragments are in registers, read before the last barrier)
+  //   | load stage s + 4 | barrier.
+  // Stages past nst (rounded up to the unroll) load clamped addresses and stash zeros.
+  const int nst_pad = (nst + 1) & ~1;
+  Frag F[2];
+  fetch(0, 0);
+  fetch(1, 1);
+  stash(0, smg, 0);
+  fetch(0, 2);
+  stash(1, smg + kStage, 1);
+  fetch(1, 3);
+  __syncthreads();
+  load_frag(F[0], smg, smg + 3 * kPlane, wm, wn, li, g);
+  __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
+  for (int s0 = 0; s0 < nst_pad; s0 += 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int st = s0 + j;
+      const unsigned char* nb = smg + ((st + 1) & 1) * kStage;
+      load_frag(F[j ^ 1], nb, nb + 3 * kPlane, wm, wn, li, g);
+      mma_x3(acc, F[j]);
+      stash(j, smg + (st & 1) * kStage, st + 2);
+      fetch(j, st + 4);
+      __syncthreads();
+    }
+  }
+
+  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + q
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int64_t col = n0 + 32 * wn + 16 * c + li;
+      if (col >= N) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = m0 + 64 * wm + 16 * r + 4 * g + q;
+        if (row >= M) continue;
+        const int64_t grp_r = row / cgrp;
+        float* dst = C + grp_r * cldg + (row - grp_r * cgrp) * cldr + col * cldn;
+        if (ACC) *dst += acc[r][c][q];
+        else *dst = acc[r][c][q];
+      }
+    }
+  }
+}
+
+// Short-K, wide-N form (the backward T = G W2p^T: K = mul_out <= 128, N = mul1 H ~ 32k): the
+// workgroup splits its 128-row block of A ONCE into LDS (K / 32 resident stage images) and sweeps
+// a range of 128-column tiles, streaming only B (two LDS stages, register ring two stages
+// ahead across tile boundaries); after each tile's K / 32 steps the accumulators go out with
+// non-temporal stores (T is consumed by a later kernel, far past the caches) and restart.
+// Replaces one workgroup per 128 x 128 tile, whose prologue / epilogue dominated at 4 k steps.
+constexpr int kMaxKS = 4;  // K <= 128
+template <int NKS>
+__global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
+    int64_t M, int64_t N, const float* __restrict__ A, int64_t lda,
+    const unsigned short* __restrict__ Bp, int64_t ldb, int64_t bplane, float* __restrict__ C,
+    int64_t ldc, int tiles_m, int tiles_n, int n_split) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
+  unsigned char* sA = smw;                          // NKS x 3 planes
+  unsigned char* sB = smw + NKS * 3 * kPlane;       // 2 stages x 3 planes
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wm = w >> 2, wn = w & 3;
+  // XCD-contiguous logical id; M tile fastest so the n_split workgroups of neighbouring M tiles
+  // that stream the same B columns run side by side
+  const int64_t nwg = (int64_t)tiles_m * n_split;
+  int64_t L;
+  {
+    const int64_t b = blockIdx.x, x = b & 7, q = nwg >> 3, r = nwg & 7;
+    L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int64_t tm = L % tiles_m, sp = L / tiles_m;
+  const int64_t m0 = tm * kBM;
+  const int64_t per = (tiles_n + n_split - 1) / n_split;
+  const int64_t t0 = sp * per, t1 = (t0 + per < tiles_n) ? t0 + per : tiles_n;
+  if (t0 >= t1) return;
+
+  // A block -> resident split planes (rows beyond M are zero)
+#pragma unroll
+  for (int q = 0; q < NKS * 2; ++q) {
+    const int v = tid + kGT * q;                 // (stage, row, float4)
+    const int st = v >> 10, row = (v >> 3) & 127, kq = v & 7;
+    const int64_t gr = m0 + row;
+    f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (gr < M) x = *reinterpret_cast<const f32x4*>(A + gr * lda + 32 * st + 4 * kq);
+    unsigned h0, m_, l0, h1, m1, l1;
+    split3(f32x2{x[0], x[1]}, h0, m_, l0);
+    split3(f32x2{x[2], x[3]}, h1, m1, l1);
+    unsigned char* img = sA + st * 3 * kPlane;
+    const int off = xoff(row, kq >> 1) + 8 * (kq & 1);
+    *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
+    *reinterpret_cast<u32x2*>(img + kPlane + off) = u32x2{m_, m1};
+    *reinterpret_cast<u32x2*>(img + 2 * kPlane + off) = u32x2{l0, l1};
+  }
+
+  const int brow = tid >> 2, bch = tid & 3;
+  const int nst = (int)((t1 - t0) * NKS);
+  u32x4 ringB[2][3];
+  bool bok_slot[2];
+  auto fetch = [&](int slot, int gs) {
+    const int gsc = gs < nst ? gs : nst - 1;
+    const int64_t n = (t0 + gsc / NKS) * kBN + brow;
+    const int64_t k0 = (int64_t)(gsc % NKS) * kBK;
+    bok_slot[slot] = gs < nst && n < N;
+    const unsigned short* p = Bp + (n < N ? n : N - 1) * ldb + k0 + 8 * bch;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) ringB[slot][pl] = *reinterpret_cast<const u32x4*>(p + pl * bplane);
+  };
+  auto stash = [&](int slot, unsigned char* buf) {
+    const int off = xoff(brow, bch);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      u32x4 v = ringB[slot][pl];
+      if (!bok_slot[slot]) v = u32x4{0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(buf + pl * kPlane + off) = v;
+    }
+  };
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto store_tile = [&](int64_t tn) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int64_t col = tn * kBN + 32 * wn + 16 * c + li;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t row = m0 + 64 * wm + 16 * r + 4 * g + q;
+          if (row < M && col < N) __builtin_nontemporal_store(acc[r][c][q], C + row * ldc + col);
+        }
+        acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  // same pipeline as tp_gemm_x3_kernel over the global step index gs (tile t0 + gs / NKS, k
+  // step gs % NKS); A fragments from the resident images, B through two LDS stages
+  Frag F[2];
+  fetch(0, 0);
+  fetch(1, 1);
+  stash(0, sB);
+  fetch(0, 2);
+  stash(1, sB + 3 * kPlane);
+  fetch(1, 3);
+  __syncthreads();  // A images and B stages 0, 1
+  load_frag(F[0], sA, sB, wm, wn, li, g);
+  __syncthreads();
+  const int nst_pad = (nst + 1) & ~1;
+  for (int s0 = 0; s0 < nst_pad; s0 += 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gs = s0 + j;
+      load_frag(F[j ^ 1], sA + ((gs + 1) % NKS) * 3 * kPlane, sB + ((gs + 1) & 1) * 3 * kPlane,
+                wm, wn, li, g);
+      mma_x3(acc, F[j]);
+      if (gs < nst && gs % NKS == NKS - 1) store_tile(t0 + gs / NKS);
+      stash(j, sB + (gs & 1) * 3 * kPlane);
+      fetch(j, gs + 4);
+      __syncthreads();
+    }
+  }
+}
+
+// Planes of one path's second radial Linear block (W2 rows (u, w), H columns; b2 (u, w)):
+//   Bf[p][w][u H + j] = W2[(u mo + w), j],  Bf[p][w][mul1 H + u] = b2[u mo + w]   (forward B)
+//   Bt[p][u H + j][w] = W2[(u mo + w), j]                                         (backward B)
+// grid (H / 64, mul1), 256 threads: the (mo x 64) block of W2 rows u mo .. u mo + mo - 1,
+// columns j0 .. j0 + 63 goes through LDS (transpose for Bf); Bt rows are written directly.
+__global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int H,
+                                                          const float* __restrict__ W2,
+                                                          const float* __restrict__ b2,
+                                                          unsigned short* __restrict__ Bf,
+                                                          unsigned short* __restrict__ Bt) {
+  __shared__ float tile[128][65];
+  const int u = blockIdx.y, j0 = blockIdx.x * 64, tid = threadIdx.x;
+  const int64_t K1 = (int64_t)mul1 * H, ldf = K1 + mul1;
+  const int64_t pf = (int64_t)mo * ldf, pt = K1 * mo;
+  for (int x = tid; x < mo * 64; x += 256) {
+    const int wr = x >> 6, j = x & 63;
+    const float v = (j0 + j < H) ? W2[((int64_t)u * mo + wr) * H + j0 + j] : 0.f;
+    tile[wr][j] = v;
+  }
+  __syncthreads();
+  // Bf[p][w][u H + j0 + j]: rows w, 64 consecutive k
+  for (int x = tid; Bf && x < mo * 64; x += 256) {
+    const int wr = x >> 6, j = x & 63;
+    if (j0 + j >= H) continue;
+    unsigned h, m, l;
+    split3(f32x2{tile[wr][j], 0.f}, h, m, l);
+    const int64_t o = (int64_t)wr * ldf + (int64_t)u * H + j0 + j;
+    Bf[o] = (unsigned short)h;
+    Bf[pf + o] = (unsigned short)m;
+    Bf[2 * pf + o] = (unsigned short)l;
+  }
+  if (Bt) {  // Bt[p][u H + j0 + j][w]: rows k, mo consecutive w
+    for (int x = tid; x < mo * 64; x += 256) {
+      const int j = x / mo, wr = x - j * mo;
+      if (j0 + j >= H) continue;
+      unsigned h, m, l;
+      split3(f32x2{tile[wr][j], 0.f}, h, m, l);
+      const int64_t o = ((int64_t)u * H + j0 + j) * mo + wr;
+      Bt[o] = (unsigned short)h;
+      Bt[pt + o] = (unsigned short)m;
+      Bt[2 * pt + o] = (unsigned short)l;
+    }
+  }
+  if (Bf && blockIdx.x == 0) {  // bias columns of Bf: Bf[p][w][K1 + u]
+    for (int wr = tid; wr < mo; wr += 256) {
+      unsigned h, m, l;
+      split3(f32x2{b2[(int64_t)u * mo + wr], 0.f}, h, m, l);
+      const int64_t o = (int64_t)wr * ldf + K1 + u;
+      Bf[o] = (unsigned short)h;
+      Bf[pf + o] = (unsigned short)m;
+      Bf[2 * pf + o] = (unsigned short)l;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace gmp
+
+using namespace gmp;
+
+extern "C" {
+
+int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
+                        const float* b2p, void* Bf, void* Bt, void* stream) {
+  GMP_CHECK_ARG(mul1 > 0 && mul_out > 0 && mul_out <= 128 && H > 0 && mul1 <= 65535);
+  GMP_CHECK_ARG(W2p && b2p && (Bf || Bt));
+  tp_split_w2_kernel<<<dim3((unsigned)ceil_div(H, 64), (unsigned)mul1), 256, 0,
+                       as_stream(stream)>>>((int)mul1, (int)mul_out, (int)H, W2p, b2p,
+                                            static_cast<unsigned short*>(Bf),
+                                            static_cast<unsigned short*>(Bt));
+  return launch_status();
+}
+
+int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
+                       int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
+                       int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
+                       int64_t cldn, int accumulate, void* stream) {
+  GMP_CHECK_ARG(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && cgrp >= 1);
+  if (M == 0 || N == 0) return GMP_OK;
+  GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2));
+  GMP_CHECK_ARG(K1 % kBK == 0 && K2 % kBK == 0 && K1 + K2 > 0);
+  GMP_CHECK_ARG(lda1 % 4 == 0 && (K2 == 0 || lda2 % 4 == 0) && ldb % 8 == 0 && bplane % 8 == 0);
+  GMP_CHECK_ARG(ldb >= K1 + K2 && lda1 >= K1 && (K2 == 0 || lda2 >= K2));
+  GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A1) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
+  GMP_CHECK_ARG(K2 == 0 || reinterpret_cast<uintptr_t>(A2) % 16 == 0);
+  const int64_t tiles_m = ceil_div(M, kBM), tiles_n = ceil_div(N, kBN);
+  GMP_CHECK_ARG(tiles_m < (1LL << 31) && tiles_n < (1LL << 31));
+  const int64_t nwg = tiles_m * tiles_n;
+  GMP_CHECK_ARG(nwg < (1LL << 32));
+  const size_t smem = 2 * (size_t)kStage;
+  int rc = 0;
+  auto k = accumulate ? tp_gemm_x3_kernel<true> : tp_gemm_x3_kernel<false>;
+  if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)smem))))
+    return rc;
+  k<<<(unsigned)nwg, kGT, smem, as_stream(stream)>>>(
+      M, (int)N, K1, A1, lda1, K2, K2 ? A2 : A1, K2 ? lda2 : lda1,
+      static_cast<const unsigned short*>(Bp), ldb, bplane, C, cgrp, cldg, cldr, cldn,
+      (int)tiles_m, (int)tiles_n);
+  return launch_status();
+}
+
+int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                             const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
+                             void* stream) {
+  GMP_CHECK_ARG(M >= 0 && N >= 0 && K > 0 && K % kBK == 0 && K <= kBK * kMaxKS);
+  if (M == 0 || N == 0) return GMP_OK;
+  GMP_CHECK_ARG(A && Bp && C && lda >= K && lda % 4 == 0 && ldb >= K && ldb % 8 == 0 &&
+                bplane % 8 == 0 && ldc >= N);
+  GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
+  const int64_t tiles_m = ceil_div(M, kBM), tiles_n = ceil_div(N, kBN);
+  GMP_CHECK_ARG(tiles_m < (1LL << 30) && tiles_n < (1LL << 30));
+  // about four workgroups per CU over the launch, each sweeping >= 8 column tiles
+  int64_t n_split = ceil_div(4 * (int64_t)device_cu_count(), tiles_m);
+  const int64_t max_split = ceil_div(tiles_n, 8);
+  if (n_split > max_split) n_split = max_split;
+  if (n_split < 1) n_split = 1;
+  const int64_t nwg = tiles_m * n_split;
+  GMP_CHECK_ARG(nwg < (1LL << 32));
+  const int nks = (int)(K / kBK);
+  const size_t smem = (size_t)(nks * 3 + 6) * kPlane;
+  hipStream_t s = as_stream(stream);
+  const unsigned short* B = static_cast<const unsigned short*>(Bp);
+  int rc = 0;
+#define GMP_WN(NK)                                                                               \
+  {                                                                                              \
+    auto k = tp_gemm_x3_widen_kernel<NK>;                                                        \
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                      \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                            (int)smem))))                                        \
+      return rc;                                                                                 \
+    k<<<(unsigned)nwg, kGT, smem, s>>>(M, N, A, lda, B, ldb, bplane, C, ldc, (int)tiles_m,       \
+                                       (int)tiles_n, (int)n_split);                              \
+  }
+  switch (nks) {
+    case 1: GMP_WN(1) break;
+    case 2: GMP_WN(2) break;
+    case 3: GMP_WN(3) break;
+    default: GMP_WN(4) break;
+  }
+#undef GMP_WN
+  return launch_status();
+}
+
+}  // extern "C"

@@ -181,8 +181,17 @@ __global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t
                                 int64_t n, int64_t ldc) {
   const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= X) return;
+  // the level-1 values are loaded kGC at a time before they are added (in slab order, as a
+  // plain loop would): one memory round trip per kGC slabs instead of one per slab
   float s = 0.f;
-  for (int64_t c = 0; c < C; ++c) s += l1[c * X + x];
+  for (int64_t c0 = 0; c0 < C; c0 += kGC) {
+    float v[kGC];
+#pragma unroll
+    for (int u = 0; u < kGC; ++u) v[u] = (c0 + u < C) ? l1[(c0 + u) * X + x] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kGC; ++u)
+      if (c0 + u < C) s += v[u];
+  }
   if (x < DD) out[(x / n) * ldc + x % n] = s;
   else if (colsum) colsum[x - DD] = s;
 }
@@ -375,8 +384,12 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
     const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
     int64_t lda, int64_t ldb, int64_t k_per_block, float* __restrict__ partial,
     const float* __restrict__ bw, const float* __restrict__ bb, int WN,
-    const float* __restrict__ B2, int64_t ldb2, int N1) {
-  // B may be two column blocks [B (N1 columns) | B2 (N - N1 columns)] of different tensors
+    const float* __restrict__ B2, int64_t ldb2, int N1, int64_t a_col_step) {
+  // B may be two column blocks [B (N1 columns) | B2 (N - N1 columns)] of different tensors.
+  // blockIdx.y > 0 (gmp_outer_sum_cols_f32): column block y of a wide A, A + y a_col_step, its
+  // own row of partial slabs
+  A += (int64_t)blockIdx.y * a_col_step;
+  partial += (int64_t)blockIdx.y * gridDim.x * ((int64_t)M * N + M);
   extern __shared__ __attribute__((aligned(16))) unsigned char smx[];
   const int R = M + N;  // LDS rows per plane: A channels, then B channels
   // + 64 padding rows: written by idle loader lanes (row R), read by the ragged tiles
@@ -617,7 +630,7 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
                                             (int)smem))))                                     \
       return rc;                                                                              \
     k<<<(unsigned)Gr, kXT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per, part, bw, bb,  \
-                                      wn, B2, ldb2, (int)n1);                                 \
+                                      wn, B2, ldb2, (int)n1, 0);                              \
   }
 #define GMP_X3_NL(RT, CT, PP) \
   if (nl == 1) GMP_X3(RT, CT, PP, 1) else GMP_X3(RT, CT, PP, 2)
@@ -645,6 +658,36 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, m * n, n,
                                                              ldc);
   return launch_status();
+}
+
+// Wide A: C (m_total x n, row stride ldc) = A^T B for m_total a multiple of 128 (the TP path
+// GEMM dW2p = S^T G: S (K rows x mul1 H), G (K rows x mul_out)), column blocks of 128 on
+// blockIdx.y, split-K over Gr row ranges per block, then one ordered pass over the Gr slabs.
+constexpr int kColBlk = 128;
+int64_t cols_groups(int64_t K, int64_t Y) {
+  int64_t g = ceil_div(2 * (int64_t)device_cu_count(), Y);
+  const int64_t cap = ceil_div(K, 4 * kXK);
+  if (g > cap) g = cap;
+  return g < 1 ? 1 : g;
+}
+
+__global__ void sum_partials_cols(const float* __restrict__ part, int64_t Gr, int64_t X, int m,
+                                  int n, float* __restrict__ C, int64_t ldc) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t y = blockIdx.y;
+  if (x >= (int64_t)m * n) return;
+  const float* p = part + y * Gr * X + x;
+  float s = 0.f;
+  for (int64_t g0 = 0; g0 < Gr; g0 += kGC) {  // kGC loads in flight, added in slab order
+    float v[kGC];
+#pragma unroll
+    for (int u = 0; u < kGC; ++u) v[u] = (g0 + u < Gr) ? p[(g0 + u) * X] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kGC; ++u)
+      if (g0 + u < Gr) s += v[u];
+  }
+  const int64_t r = x / n, c = x - r * n;
+  C[(y * m + r) * ldc + c] = s;
 }
 
 // capacity bucket for (M, N): returns 0 if unsupported
@@ -874,6 +917,59 @@ int gmp_edge_outer_sum_ex_f32(int64_t K, int64_t m, int64_t n, const float* A, i
   if (act != -1) return GMP_ERR_UNSUPPORTED;  // activation prologue: square shapes only
   return outer_sum_rect_launch(K, m, n, A, lda, B, ldb, C, ldc, colsum_A, workspace,
                                workspace_bytes, stream);
+}
+
+
+size_t gmp_outer_sum_cols_workspace_size(int64_t K, int64_t m_total, int64_t n) {
+  if (m_total <= 0 || n <= 0 || m_total % kColBlk) return 0;
+  const int64_t Y = m_total / kColBlk;
+  return (size_t)(Y * cols_groups(K, Y) * (kColBlk * n + kColBlk)) * sizeof(float);
+}
+
+int gmp_outer_sum_cols_f32(int64_t K, int64_t m_total, int64_t n, const float* A, int64_t lda,
+                           const float* B, int64_t ldb, float* C, int64_t ldc, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  GMP_CHECK_ARG(K >= 0 && m_total > 0 && m_total % kColBlk == 0 && n > 0 && n % 16 == 0);
+  GMP_CHECK_ARG(lda >= m_total && ldb >= n && ldc >= n && lda % 4 == 0 && ldb % 4 == 0);
+  GMP_CHECK_ARG(A && B && C);
+  GMP_CHECK_ARG((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) % 16 == 0);
+  const int64_t m = kColBlk, R = m + n;
+  int wn = 0;
+  const int shape = x3_pick(m, n, &wn);
+  const int64_t units = ((2 * m + 63) & ~63) + ((2 * n + 63) & ~63);
+  if (shape < 0 || shape > 2 || R + kXPad > 416 || units > kXT) return GMP_ERR_UNSUPPORTED;
+  const int64_t Y = m_total / kColBlk;
+  GMP_CHECK_ARG(Y < 65536);
+  hipStream_t s = as_stream(stream);
+  if (K == 0) {
+    for (int64_t r = 0; r < m_total; ++r) {
+      int rc = hip_check(hipMemsetAsync(C + r * ldc, 0, n * sizeof(float), s));
+      if (rc) return rc;
+    }
+    return GMP_OK;
+  }
+  GMP_CHECK_ARG(workspace);
+  if (workspace_bytes < gmp_outer_sum_cols_workspace_size(K, m_total, n)) return GMP_ERR_WORKSPACE;
+  const int64_t G = cols_groups(K, Y);
+  const int64_t per = ceil_div(ceil_div(K, G), kXK) * kXK;
+  const int64_t Gr = ceil_div(K, per);
+  float* part = reinterpret_cast<float*>(workspace);
+  const size_t smem = (size_t)2 * 3 * (R + kXPad) * 64;
+  auto k = shape == 2   ? outer_sum_x3_kernel<2, 4, 0, 1>
+           : shape == 1 ? outer_sum_x3_kernel<2, 2, 0, 1>
+                        : outer_sum_x3_kernel<1, 2, 0, 1>;
+  int rc = hip_check(hipFuncSetAttribute((const void*)k,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  if (rc) return rc;
+  k<<<dim3((unsigned)Gr, (unsigned)Y), kXT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per,
+                                                      part, nullptr, nullptr, wn, nullptr, 0,
+                                                      (int)n, m);
+  rc = launch_status();
+  if (rc) return rc;
+  const int64_t X = m * n + m;
+  sum_partials_cols<<<dim3((unsigned)ceil_div(m * n, 256), (unsigned)Y), 256, 0, s>>>(
+      part, Gr, X, (int)m, (int)n, C, ldc);
+  return launch_status();
 }
 
 }  // extern "C"

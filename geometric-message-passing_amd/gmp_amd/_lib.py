@@ -97,6 +97,14 @@ SIGNATURES = {
     "gmp_tp_node_outer_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_tp_node_apply_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp]),
+    "gmp_tp_split_w2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_tp_gemm_x3_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
+                                   c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp]),
+    "gmp_tp_gemm_x3_widen_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                         c_vp, c_i64, c_vp]),
+    "gmp_outer_sum_cols_workspace_size": (c_size, [c_i64, c_i64, c_i64]),
+    "gmp_outer_sum_cols_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                       c_i64, c_vp, c_size, c_vp]),
     "gmp_gvp_layer_fwd_f32": (c_int, [c_i64, c_int] + [c_vp] * 10 + [c_vp]),
     "gmp_gvp_layer_bwd_f32": (c_int, [c_i64, c_int] + [c_vp] * 19 + [c_vp]),
     "gmp_gvp_msg0_fwd_f32": (c_int, [c_i64] + [c_vp] * 15 + [c_vp]),

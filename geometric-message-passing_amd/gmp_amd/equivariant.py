@@ -490,6 +490,32 @@ def node_form_ok(hidden):
     return hidden % 16 == 0 and hidden <= 256
 
 
+# Path GEMMs of the node form: "x3" = K7g (gmp_tpgemm.hip: bf16 MFMA over exact three-plane f32
+# splits; dW2p by the column-block split-plane outer sum), "torch" = the library f32 GEMMs.
+TP_GEMM = os.environ.get("GMP_TP_GEMM", "x3")
+
+
+def _x3_ok(P, H):
+    """Shapes K7g covers: every k range a multiple of the 32-deep MFMA step, mul_out <= 128."""
+    return (TP_GEMM == "x3" and P["mul1"] % 32 == 0 and P["mul_out"] % 32 == 0
+            and P["mul_out"] <= 128 and H % 32 == 0)
+
+
+def _split_w2(lib, W2, b2, P, fwd):
+    """Three bf16 planes of path P's W2 / b2 block: forward (B = [W2p | b2p]^T as [w][(u, j) ++ u])
+    or backward (B = W2p as [(u, j)][w]) layout (gmp_tp_split_w2_f32)."""
+    m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
+    H = W2.shape[1]
+    n = 3 * mo * (m1 * H + m1) if fwd else 3 * m1 * H * mo
+    planes = torch.empty(n, dtype=torch.int16, device=W2.device)
+    w2p = W2.data_ptr() + 4 * off * H
+    b2p = b2.data_ptr() + 4 * off
+    check(lib.gmp_tp_split_w2_f32(m1, mo, H, ctypes.c_void_p(w2p), ctypes.c_void_p(b2p),
+                                  _p(planes) if fwd else None, None if fwd else _p(planes),
+                                  _stream()), "gmp_tp_split_w2_f32")
+    return planes
+
+
 class TPConvNodeFn(torch.autograd.Function):
     """out = scatter_sum_{ei0}(FCTP(x[ei1], sh, fc(radial)))  (tfn_layer.py:82-87), evaluated in
     receiver-factorised form: with a_e = relu(W1 r_e + b1) (H) the per-edge weights are
@@ -512,17 +538,34 @@ class TPConvNodeFn(torch.autograd.Function):
         H = W1.shape[0]
         out = torch.zeros((N, plan.desc.out_dim), dtype=torch.float32, device=dev)
         rad_s = ops.gather_rows(rad, graph.perm)
-        W2x = [_w2_path(W2, b2, P) for P in plan.instructions]
+        W2c, b2c = W2.contiguous(), b2.contiguous()
+        x3 = [_x3_ok(P, H) for P in plan.instructions]
+        W2x = [None if ok else _w2_path(W2, b2, P) for P, ok in zip(plan.instructions, x3)]
+        Bfs = [None] * len(x3)
         for n0, n1, e0, e1, eoff, a, zbuf, _ in _node_chunks(lib, plan, graph, x, sh, rad_s,
                                                              W1, b1):
             c, ne = n1 - n0, e1 - e0
-            for P, (W2p, b2p), (zoff, w) in zip(plan.instructions, W2x, plan.z_regions):
-                d3 = 2 * P["lo"] + 1
+            for i, (P, (zoff, w)) in enumerate(zip(plan.instructions, plan.z_regions)):
+                d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a)
+                blk = plan.blocks[P["io"]]
+                if x3[i]:
+                    # out[n, blk + w' d3 + k] += [S | Sb][(n, k), :] [W2p ; b2p][:, w'] (K7g)
+                    if Bfs[i] is None:
+                        Bfs[i] = _split_w2(lib, W2c, b2c, P, True)
+                    K1 = m1 * H
+                    ldb = K1 + m1
+                    dst = out[n0:n1, blk[0]:]
+                    with _timed("tp_node_W"):
+                        check(lib.gmp_tp_gemm_x3_f32(c * d3, mo, K1, _p(S), K1, m1, _p(Sb), m1,
+                                                     _p(Bfs[i]), ldb, mo * ldb, _p(dst), d3,
+                                                     out.shape[1], 1, d3, 1, _stream()),
+                              "gmp_tp_gemm_x3_f32")
+                    continue
+                W2p, b2p = W2x[i]
                 with _timed("tp_node_W"):
                     op = torch.addmm(Sb.view(c * d3, -1).mm(b2p), S.view(c * d3, -1), W2p)
-                blk = plan.blocks[P["io"]]
                 out[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, blk[1], d3).add_(
                     op.view(c, d3, -1).transpose(1, 2))
         ctx.plan, ctx.graph = plan, graph
@@ -544,34 +587,65 @@ class TPConvNodeFn(torch.autograd.Function):
         dY = torch.empty((E, 9), **f)
         drad_s = torch.empty_like(rad_s)
         dW1, db1 = torch.zeros_like(W1), torch.zeros_like(b1)
+        W2c, b2c = W2.contiguous(), b2.contiguous()
+        x3 = [_x3_ok(P, H) for P in plan.instructions]
         W2x = [_w2_path(W2, b2, P) for P in plan.instructions]
         dW2x = [(torch.zeros_like(wp), torch.zeros_like(bp)) for wp, bp in W2x]
+        Bts = [None] * len(x3)
+        first = True
         for n0, n1, e0, e1, eoff, a, zbuf, pre in _node_chunks(lib, plan, graph, x, sh, rad_s,
                                                                W1, b1):
             c, ne = n1 - n0, e1 - e0
             dzbuf = torch.empty_like(zbuf)
             da = torch.zeros((ne, H), **f)
-            for P, (W2p, b2p), (dW2p, db2p), (zoff, w) in zip(plan.instructions, W2x, dW2x,
-                                                              plan.z_regions):
-                d3, mo = 2 * P["lo"] + 1, P["mul_out"]
+            for i, (P, (W2p, b2p), (dW2p, db2p), (zoff, w)) in enumerate(
+                    zip(plan.instructions, W2x, dW2x, plan.z_regions)):
+                d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 blk = plan.blocks[P["io"]]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a)
                 G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
-                G = G.reshape(c * d3, mo)
-                with _timed("tp_node_dW"):
-                    dW2p.addmm_(S.view(c * d3, -1).t(), G)
-                    db2p.addmm_(Sb.view(c * d3, -1).t(), G)
-                del S, Sb
-                with _timed("tp_node_W"):
-                    T = G.mm(W2p.t())
-                    Tb = G.mm(b2p.t())
+                G = G.reshape(c * d3, mo).contiguous()  # (d3 = 1: reshape alone is a view)
+                if x3[i]:
+                    K1 = m1 * H
+                    with _timed("tp_node_dW"):
+                        # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
+                        tgt = dW2p if first else torch.empty_like(dW2p)
+                        ws_b = lib.gmp_outer_sum_cols_workspace_size(c * d3, K1, mo)
+                        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=x.device)
+                        check(lib.gmp_outer_sum_cols_f32(c * d3, K1, mo, _p(S), K1, _p(G), mo,
+                                                         _p(tgt), mo, _p(ws), ws_b, _stream()),
+                              "gmp_outer_sum_cols_f32")
+                        del ws
+                        if not first:
+                            dW2p.add_(tgt)
+                        db2p.addmm_(Sb.view(c * d3, -1).t(), G)
+                    del S, Sb
+                    if Bts[i] is None:
+                        Bts[i] = _split_w2(lib, W2c, b2c, P, False)
+                    with _timed("tp_node_W"):
+                        # T[(n, k), (u, j)] = sum_w G[(n, k), w] W2p[(u, j), w]
+                        T = torch.empty((c * d3, K1), **f)
+                        check(lib.gmp_tp_gemm_x3_widen_f32(c * d3, K1, mo, _p(G), mo,
+                                                           _p(Bts[i]), mo, K1 * mo, _p(T), K1,
+                                                           _stream()),
+                              "gmp_tp_gemm_x3_widen_f32")
+                        Tb = G.mm(b2p.t())
+                else:
+                    with _timed("tp_node_dW"):
+                        dW2p.addmm_(S.view(c * d3, -1).t(), G)
+                        db2p.addmm_(Sb.view(c * d3, -1).t(), G)
+                    del S, Sb
+                    with _timed("tp_node_W"):
+                        T = G.mm(W2p.t())
+                        Tb = G.mm(b2p.t())
                 dZp = dzbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 with _timed("tp_node_dZA"):
                     check(lib.gmp_tp_node_apply_f32(c, w, H, _p(eoff), _p(Zp), _p(a), _p(T),
                                                     _p(Tb), _p(dZp), _p(da), _stream()),
                           "gmp_tp_node_apply_f32")
                 del T, Tb
+            first = False
             with _timed("tp_node_edge_bwd"):
                 check(lib.gmp_tp_edge_z_bwd_f32(ctypes.byref(plan.desc), _p(paths_dev),
                                                 _p(cg_dev), cg_dev.numel(), _p(x), _p(sh),

@@ -278,6 +278,40 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
                           const float* Z, const float* A, const float* T, const float* Tb,
                           float* dZ, float* dA, void* stream);
 
+/* K7g path GEMMs of the receiver-factorised TP convolution on the bf16 MFMA through exact
+ * three-plane f32 splits (replaces the library f32 GEMMs out = S W2p + Sb b2p and
+ * T = G W2p^T of tfn_layer.py:73-87 regrouped; f32-class accuracy, see gmp_tpgemm.hip).
+ * split_w2: from one path's block of the second radial Linear, W2p (mul1 * mul_out rows (u, w)
+ *   of H floats) and b2p (mul1 * mul_out), writes (each if not null) the forward B planes Bf
+ *   [3][mul_out][mul1 H + mul1] (bf16: Bf[w][u H + j] = W2[(u, w), j], Bf[w][mul1 H + u] =
+ *   b2[u, w]) and the backward B planes Bt [3][mul1 H][mul_out] (Bt[u H + j][w] = W2[(u, w), j]).
+ * gemm_x3: C (+)= [A1 | A2] B^T for A1 (M x K1, row stride lda1), A2 (M x K2, lda2; K2 may be 0),
+ *   B planes [3][N][ldb] bf16 (plane stride bplane elements, row k range [0, K1 + K2));
+ *   element (r, col) of C at (r / cgrp) cldg + (r % cgrp) cldr + col cldn (accumulate != 0:
+ *   C += result).  K1, K2 multiples of 32; lda*, ldb, bplane multiples of 4 / 8; A, B 16-byte
+ *   aligned.  Deterministic (no atomics, fixed k order). */
+int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
+                        const float* b2p, void* Bf, void* Bt, void* stream);
+int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
+                       int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
+                       int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
+                       int64_t cldn, int accumulate, void* stream);
+/* Short-K, wide-N form of gemm_x3 (the backward T = G W2p^T: K = mul_out <= 128, N = mul1 H):
+ *   C (M x N, row stride ldc) = A B^T, A (M x K, lda) f32, B planes [3][N][ldb] bf16;
+ * K a multiple of 32, <= 128.  Each workgroup keeps its split A rows in LDS and sweeps a range
+ * of column tiles; C is written with non-temporal stores. */
+int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                             const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
+                             void* stream);
+/* Wide edge/row reduction C (m_total x n, row stride ldc) = A^T B over K rows, A (K x m_total,
+ * row stride lda), B (K x n, ldb), m_total a multiple of 128, n a multiple of 16 (<= 128): the
+ * TP path GEMM dW2p = S^T G.  Split-plane bf16 MFMA (the K5 kernel with column blocks of 128),
+ * deterministic split-K reduction through the workspace. */
+size_t gmp_outer_sum_cols_workspace_size(int64_t K, int64_t m_total, int64_t n);
+int gmp_outer_sum_cols_f32(int64_t K, int64_t m_total, int64_t n, const float* A, int64_t lda,
+                           const float* B, int64_t ldb, float* C, int64_t ldc, void* workspace,
+                           size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * K5g GVP-GNN message function (models/layers/gvp_layer.py:101-170 per edge via GVPConv.message
  * :319-324; configuration of models/gvpgnn.py: activations (relu, None), vector_gate, s = 128,
