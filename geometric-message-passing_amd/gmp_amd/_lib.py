@@ -135,10 +135,27 @@ SIGNATURES = {
 }
 
 _lib = None
+TORCH_LIB_PATH = os.environ.get("GMP_TORCH_LIB", os.path.join(_HERE, "libgmp_torch.so"))
+_torch_ops = None
 
 
 class GmpError(RuntimeError):
     pass
+
+
+def torch_ops():
+    """torch.ops.gmp: the TORCH_LIBRARY(gmp) registration of the C ABI (csrc/torch/gmp_torch.cpp,
+    libgmp_torch.so next to libgmp.so; the drop-in boundary of SURVEY §8(b), the same kind as
+    torch_scatter's torch.ops.torch_scatter.*).  Raises if the library is missing."""
+    global _torch_ops
+    if _torch_ops is None:
+        load()  # libgmp.so first: libgmp_torch.so binds to the already-loaded soname
+        if not os.path.exists(TORCH_LIB_PATH):
+            raise GmpError(f"libgmp_torch.so not found at {TORCH_LIB_PATH}: build it first "
+                           "(python -c 'import __graft_entry__ as g; g.build()')")
+        torch.ops.load_library(TORCH_LIB_PATH)
+        _torch_ops = torch.ops.gmp
+    return _torch_ops
 
 
 def load(path=None):

@@ -84,20 +84,13 @@ class EdgeFeaturizeFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pos, edge_index, host_consts, graph):
-        lib = _lib.load()
         w, pref, r_max, p = host_consts
         pos = _f32c(pos)
         ei = edge_index.contiguous()
         _need_cuda(pos, ei)
-        E = ei.shape[1]
-        nb = len(w)
-        sh = torch.empty((E, 9), dtype=torch.float32, device=pos.device)
-        rad = torch.empty((E, nb), dtype=torch.float32, device=pos.device)
-        wbuf = (ctypes.c_float * nb)(*w.tolist())
         with _timed("edge_featurize"):
-            check(lib.gmp_edge_featurize_f32(_p(pos), _p(ei), E, nb, wbuf, pref, r_max, p, None,
-                                             None, _p(sh), _p(rad), _stream()),
-                  "gmp_edge_featurize_f32")
+            sh, rad = _lib.torch_ops().edge_featurize(pos, ei, [float(v) for v in w], pref, r_max,
+                                                      p)
         ctx.save_for_backward(pos, ei)
         ctx.host, ctx.graph = host_consts, graph
         return sh, rad
@@ -107,17 +100,12 @@ class EdgeFeaturizeFn(torch.autograd.Function):
     def backward(ctx, g_sh, g_rad):
         if not ctx.needs_input_grad[0]:
             return None, None, None, None
-        lib = _lib.load()
         pos, ei = ctx.saved_tensors
         w, pref, r_max, p = ctx.host
-        E, N = ei.shape[1], pos.shape[0]
-        g_vec = torch.empty((E, 3), dtype=torch.float32, device=pos.device)
-        wbuf = (ctypes.c_float * len(w))(*w.tolist())
-        check(lib.gmp_edge_featurize_bwd_f32(
-            _p(pos), _p(ei), E, len(w), wbuf, pref, r_max, p,
-            _p(_f32c(g_sh)) if g_sh is not None else None,
-            _p(_f32c(g_rad)) if g_rad is not None else None, _p(g_vec), _stream()),
-            "gmp_edge_featurize_bwd_f32")
+        g_vec = _lib.torch_ops().edge_featurize_bwd(
+            pos, ei, [float(v) for v in w], pref, r_max, p,
+            _f32c(g_sh) if g_sh is not None else None,
+            _f32c(g_rad) if g_rad is not None else None)
         g = ctx.graph  # vectors = pos[ei0] - pos[ei1]: + into receivers, - into senders
         plus, _ = ops.segment_reduce(g_vec, g.recv_csr, "sum")
         minus, _ = ops.segment_reduce(ops.gather_rows(g_vec, g.perm), g.src_csr, "sum")
@@ -503,17 +491,8 @@ def _x3_ok(P, H):
 
 def _split_w2(lib, W2, b2, P, fwd):
     """Three bf16 planes of path P's W2 / b2 block: forward (B = [W2p | b2p]^T as [w][(u, j) ++ u])
-    or backward (B = W2p as [(u, j)][w]) layout (gmp_tp_split_w2_f32)."""
-    m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
-    H = W2.shape[1]
-    n = 3 * mo * (m1 * H + m1) if fwd else 3 * m1 * H * mo
-    planes = torch.empty(n, dtype=torch.int16, device=W2.device)
-    w2p = W2.data_ptr() + 4 * off * H
-    b2p = b2.data_ptr() + 4 * off
-    check(lib.gmp_tp_split_w2_f32(m1, mo, H, ctypes.c_void_p(w2p), ctypes.c_void_p(b2p),
-                                  _p(planes) if fwd else None, None if fwd else _p(planes),
-                                  _stream()), "gmp_tp_split_w2_f32")
-    return planes
+    or backward (B = W2p as [(u, j)][w]) layout (torch.ops.gmp.tp_split_w2)."""
+    return _lib.torch_ops().tp_split_w2(W2, b2, P["w_off"], P["mul1"], P["mul_out"], fwd)
 
 
 class TPConvNodeFn(torch.autograd.Function):
@@ -555,13 +534,11 @@ class TPConvNodeFn(torch.autograd.Function):
                     if Bfs[i] is None:
                         Bfs[i] = _split_w2(lib, W2c, b2c, P, True)
                     K1 = m1 * H
-                    ldb = K1 + m1
-                    dst = out[n0:n1, blk[0]:]
                     with _timed("tp_node_W"):
-                        check(lib.gmp_tp_gemm_x3_f32(c * d3, mo, K1, _p(S), K1, m1, _p(Sb), m1,
-                                                     _p(Bfs[i]), ldb, mo * ldb, _p(dst), d3,
-                                                     out.shape[1], 1, d3, 1, _stream()),
-                              "gmp_tp_gemm_x3_f32")
+                        _lib.torch_ops().tp_gemm_x3(S.view(c * d3, K1), K1, Sb.view(c * d3, m1),
+                                                    m1, Bfs[i], K1 + m1, mo, out,
+                                                    n0 * out.shape[1] + blk[0], d3, out.shape[1],
+                                                    1, d3, True)
                     continue
                 W2p, b2p = W2x[i]
                 with _timed("tp_node_W"):
@@ -610,26 +587,18 @@ class TPConvNodeFn(torch.autograd.Function):
                     K1 = m1 * H
                     with _timed("tp_node_dW"):
                         # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
-                        tgt = dW2p if first else torch.empty_like(dW2p)
-                        ws_b = lib.gmp_outer_sum_cols_workspace_size(c * d3, K1, mo)
-                        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=x.device)
-                        check(lib.gmp_outer_sum_cols_f32(c * d3, K1, mo, _p(S), K1, _p(G), mo,
-                                                         _p(tgt), mo, _p(ws), ws_b, _stream()),
-                              "gmp_outer_sum_cols_f32")
-                        del ws
-                        if not first:
-                            dW2p.add_(tgt)
+                        part = _lib.torch_ops().outer_sum_cols(S.view(c * d3, K1), G)
+                        if first:
+                            dW2p.copy_(part)
+                        else:
+                            dW2p.add_(part)
                         db2p.addmm_(Sb.view(c * d3, -1).t(), G)
                     del S, Sb
                     if Bts[i] is None:
                         Bts[i] = _split_w2(lib, W2c, b2c, P, False)
                     with _timed("tp_node_W"):
                         # T[(n, k), (u, j)] = sum_w G[(n, k), w] W2p[(u, j), w]
-                        T = torch.empty((c * d3, K1), **f)
-                        check(lib.gmp_tp_gemm_x3_widen_f32(c * d3, K1, mo, _p(G), mo,
-                                                           _p(Bts[i]), mo, K1 * mo, _p(T), K1,
-                                                           _stream()),
-                              "gmp_tp_gemm_x3_widen_f32")
+                        T = _lib.torch_ops().tp_gemm_x3_widen(G, Bts[i], K1)
                         Tb = G.mm(b2p.t())
                 else:
                     with _timed("tp_node_dW"):
@@ -641,9 +610,7 @@ class TPConvNodeFn(torch.autograd.Function):
                         Tb = G.mm(b2p.t())
                 dZp = dzbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 with _timed("tp_node_dZA"):
-                    check(lib.gmp_tp_node_apply_f32(c, w, H, _p(eoff), _p(Zp), _p(a), _p(T),
-                                                    _p(Tb), _p(dZp), _p(da), _stream()),
-                          "gmp_tp_node_apply_f32")
+                    _lib.torch_ops().tp_node_apply(eoff, Zp, a, T, Tb.contiguous(), da, dZp)
                 del T, Tb
             first = False
             with _timed("tp_node_edge_bwd"):
@@ -670,12 +637,8 @@ class TPConvNodeFn(torch.autograd.Function):
 
 
 def _node_outer(lib, c, w, H, eoff, Zp, a):
-    S = torch.empty((c, w, H), dtype=torch.float32, device=a.device)
-    Sb = torch.empty((c, w), dtype=torch.float32, device=a.device)
     with _timed("tp_node_S"):
-        check(lib.gmp_tp_node_outer_f32(c, w, H, _p(eoff), _p(Zp), _p(a), _p(S), _p(Sb),
-                                        _stream()), "gmp_tp_node_outer_f32")
-    return S, Sb
+        return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w)
 
 
 def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):
@@ -799,22 +762,17 @@ class Contraction(nn.Module):
 
 
 class SymmetricContractionFn(torch.autograd.Function):
-    """K8 (gmp_symmetric_contraction_{fwd,bwd}_f32): out (N, 9C) from x (N, C, 9) and the
-    stacked per-channel coefficients A_nu (C, 9, 9^nu)."""
+    """K8 (torch.ops.gmp.symmetric_contraction_{fwd,bwd}): out (N, 9C) from x (N, C, 9) and the
+    per-channel coefficients over the symmetric monomial basis A~_nu (C, 9, 9 / 45 / 165)."""
 
     @staticmethod
     def forward(ctx, x, corr, *A):
-        lib = _lib.load()
         x = _f32c(x)
         A = [_f32c(a) for a in A]
         _need_cuda(x, *A)
-        N, C = x.shape[0], x.shape[1]
-        out = torch.empty((N, 9 * C), dtype=torch.float32, device=x.device)
-        Ap = [_p(a) for a in A] + [None] * (3 - len(A))
+        Ao = list(A) + [None] * (3 - len(A))
         with _timed("symmetric_contraction_fwd"):
-            check(lib.gmp_symmetric_contraction_fwd_f32(N, C, corr, _p(x), *Ap, _p(out),
-                                                        _stream()),
-                  "gmp_symmetric_contraction_fwd_f32")
+            out = _lib.torch_ops().symmetric_contraction_fwd(x, corr, *Ao)
         ctx.corr = corr
         ctx.save_for_backward(x, *A)
         return out
@@ -822,21 +780,45 @@ class SymmetricContractionFn(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, g):
-        lib = _lib.load()
         x, *A = ctx.saved_tensors
         g = _f32c(g)
-        N, C = x.shape[0], x.shape[1]
-        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        G = lib.gmp_sc_groups(N)
-        part = torch.empty((G, C, 9, 819), dtype=torch.float32, device=x.device)
-        Ap = [_p(a) for a in A] + [None] * (3 - len(A))
+        Ao = list(A) + [None] * (3 - len(A))
         with _timed("symmetric_contraction_bwd"):
-            check(lib.gmp_symmetric_contraction_bwd_f32(N, C, ctx.corr, _p(x), *Ap, _p(g),
-                                                        _p(dx), _p(part), _stream()),
-                  "gmp_symmetric_contraction_bwd_f32")
+            dx, part = _lib.torch_ops().symmetric_contraction_bwd(x, ctx.corr, *Ao, g)
+        if not ctx.needs_input_grad[0]:
+            dx = None
         dA = part.sum(0)  # fixed-order sum over node groups
-        grads = [dA[..., :9], dA[..., 9:90], dA[..., 90:]][:len(A)]
+        grads = [dA[..., :9], dA[..., 9:54], dA[..., 54:]][:len(A)]
         return (dx, None, *[gg.contiguous() for gg in grads])
+
+
+_SYM_IDX = {}
+
+
+def _sym_index(nu, device):
+    """(n_q, n_perm) flat indices into the 9^nu axis of every distinct permutation of each sorted
+    monomial (i <= j <= k, lexicographic), padded with 9^nu (an appended zero column)."""
+    key = (nu, device)
+    if key not in _SYM_IDX:
+        import itertools
+        rows = []
+        for t in itertools.combinations_with_replacement(range(9), nu):
+            perms = sorted(set(itertools.permutations(t)))
+            rows.append([sum(p * 9 ** (nu - 1 - r) for r, p in enumerate(pm)) for pm in perms])
+        width = max(len(r) for r in rows)
+        idx = torch.tensor([r + [9 ** nu] * (width - len(r)) for r in rows], dtype=torch.int64)
+        _SYM_IDX[key] = idx.to(device)
+    return _SYM_IDX[key]
+
+
+def fold_symmetric(A, nu):
+    """A (C, 9, 9^nu) -> A~ (C, 9, C(8 + nu, nu)): every permutation's coefficient summed into
+    the sorted monomial (differentiable; the adjoint spreads dA~ back to each permutation)."""
+    if nu == 1:
+        return A
+    idx = _sym_index(nu, A.device)
+    Ap = torch.cat([A, A.new_zeros(A.shape[:-1] + (1,))], dim=-1)
+    return Ap[..., idx].sum(-1)
 
 
 class SymmetricContraction(nn.Module):
@@ -870,7 +852,8 @@ class SymmetricContraction(nn.Module):
 
     def forward(self, x, y=None):
         if self._k8 and x.is_cuda:
-            return SymmetricContractionFn.apply(x, self.correlation, *self.coefficients())
+            A = [fold_symmetric(a, nu + 1) for nu, a in enumerate(self.coefficients())]
+            return SymmetricContractionFn.apply(x, self.correlation, *A)
         return torch.cat([c(x) for c in self.contractions.values()], dim=-1)
 
 

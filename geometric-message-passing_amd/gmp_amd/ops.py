@@ -87,27 +87,14 @@ class CSR:
     __slots__ = ("index", "n_seg", "perm", "rowptr", "sorted", "payload_sorted", "err")
 
     def __init__(self, index, n_seg, payload=None):
-        lib = _lib.load()
         index = _i64c(index)
         _need_cuda(index)
-        n = index.numel()
-        dev = index.device
         self.index = index
         self.n_seg = int(n_seg)
-        self.perm = torch.empty(n, dtype=torch.int64, device=dev)
-        self.rowptr = torch.empty(self.n_seg + 1, dtype=torch.int64, device=dev)
-        self.sorted = torch.empty(n, dtype=torch.int64, device=dev)
-        self.payload_sorted = None
-        pl = None
-        if payload is not None:
-            pl = _i64c(payload)
-            self.payload_sorted = torch.empty(n, dtype=torch.int64, device=dev)
-        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        ws_bytes = lib.gmp_csr_workspace_size(n, self.n_seg)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        check(lib.gmp_csr_build(_p(index), n, self.n_seg, _p(pl), _p(self.perm), _p(self.rowptr),
-                                _p(self.sorted), _p(self.payload_sorted), _p(self.err), _p(ws),
-                                ws_bytes, _stream()), "gmp_csr_build")
+        pl = _i64c(payload) if payload is not None else None
+        self.perm, self.rowptr, self.sorted, pls, self.err = _lib.torch_ops().csr_build(
+            index, self.n_seg, pl)
+        self.payload_sorted = pls if pl is not None else None
 
     def counts(self):
         return self.rowptr[1:] - self.rowptr[:-1]
@@ -149,33 +136,19 @@ def clear_cache():
 
 # ----------------------------------------------------------------------------------- raw ops
 def gather_rows(src2d, index):
-    lib = _lib.load()
     src2d = _f32c(src2d)
     index = _i64c(index)
     _need_cuda(src2d, index)
-    out = torch.empty((index.numel(), src2d.shape[1]), dtype=torch.float32, device=src2d.device)
-    check(lib.gmp_gather_rows_f32(_p(src2d), src2d.shape[0], src2d.shape[1], _p(index),
-                                  index.numel(), _p(out), None, _stream()), "gmp_gather_rows_f32")
-    return out
+    return _lib.torch_ops().gather_rows(src2d, index)
 
 
 def segment_reduce(src2d, csr, reduce="sum", use_perm=True):
-    lib = _lib.load()
+    """(out, argmax or None) = torch.ops.gmp.segment_reduce over the CSR's segments."""
     src2d = _f32c(src2d)
     _need_cuda(src2d)
-    F = src2d.shape[1]
-    out = torch.empty((csr.n_seg, F), dtype=torch.float32, device=src2d.device)
-    argmax = None
-    if reduce == "max":
-        argmax = torch.empty((csr.n_seg, F), dtype=torch.int64, device=src2d.device)
-    red = _lib.REDUCE[reduce]
-    ws_bytes = lib.gmp_segment_reduce_workspace_size(src2d.shape[0], csr.n_seg, F, red)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=src2d.device) if ws_bytes else None
-    check(lib.gmp_segment_reduce_f32(_p(src2d), src2d.shape[0], F,
-                                     _p(csr.perm) if use_perm else None, _p(csr.rowptr),
-                                     csr.n_seg, red, _p(out), _p(argmax), _p(ws), ws_bytes,
-                                     _stream()), "gmp_segment_reduce_f32")
-    return out, argmax
+    out, argmax = _lib.torch_ops().segment_reduce(src2d, csr.perm if use_perm else None,
+                                                  csr.rowptr, csr.n_seg, reduce)
+    return out, (argmax if reduce == "max" else None)
 
 
 def edge_outer_sum(A, B, with_colsum=True):
@@ -517,19 +490,13 @@ class LnActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, eps, act):
-        lib = _lib.load()
         shape = x.shape
         d = shape[-1]
         x2 = _f32c(x).reshape(-1, d)
         gamma, beta = _f32c(gamma), _f32c(beta)
         _need_cuda(x2, gamma, beta)
-        rows = x2.shape[0]
-        y = torch.empty_like(x2)
-        xhat = torch.empty_like(x2)
-        rstd = torch.empty(rows, dtype=torch.float32, device=x2.device)
         a = _LN_ACT[act]
-        check(lib.gmp_ln_act_fwd_f32(rows, d, _p(x2), _p(gamma), _p(beta), float(eps), a, _p(y),
-                                     _p(xhat), _p(rstd), _stream()), "gmp_ln_act_fwd_f32")
+        y, xhat, rstd = _lib.torch_ops().ln_act_fwd(x2, gamma, beta, float(eps), a)
         ctx.save_for_backward(xhat, rstd, gamma, beta)
         ctx.act, ctx.shape = a, shape
         return y.view(shape)
@@ -537,19 +504,12 @@ class LnActFn(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, gy):
-        lib = _lib.load()
         xhat, rstd, gamma, beta = ctx.saved_tensors
         rows, d = xhat.shape
         gy = _f32c(gy).reshape(rows, d)
-        gx = torch.empty_like(xhat)
-        gb = torch.empty(2 * d, dtype=torch.float32, device=xhat.device)
-        ws_bytes = lib.gmp_ln_act_bwd_workspace_size(rows, d)
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=xhat.device)
         # (deferring the [dgamma | dbeta] reduction to the side stream was measured slower: the
         # extra stream bookkeeping lengthens the host-bound stretch of small node kernels)
-        check(lib.gmp_ln_act_bwd_f32(rows, d, _p(gy), _p(xhat), _p(rstd), _p(gamma), _p(beta),
-                                     ctx.act, _p(gx), _p(gb), _p(ws), ws_bytes, _stream()),
-              "gmp_ln_act_bwd_f32")
+        gx, gb = _lib.torch_ops().ln_act_bwd(gy, xhat, rstd, gamma, beta, ctx.act)
         return gx.view(ctx.shape), gb[:d], gb[d:], None, None
 
 
@@ -574,14 +534,8 @@ def linear(x, W, b=None):
 
 
 def segment_reduce_bwd(grad_out, csr, reduce, argmax, n_items):
-    lib = _lib.load()
-    grad_out = _f32c(grad_out)
-    F = grad_out.shape[1]
-    gsrc = torch.empty((n_items, F), dtype=torch.float32, device=grad_out.device)
-    check(lib.gmp_segment_reduce_bwd_f32(_p(grad_out), csr.n_seg, F, _p(csr.index), n_items,
-                                         _p(csr.rowptr), _lib.REDUCE[reduce], _p(argmax),
-                                         _p(gsrc), _stream()), "gmp_segment_reduce_bwd_f32")
-    return gsrc
+    return _lib.torch_ops().segment_reduce_bwd(_f32c(grad_out), csr.index, csr.rowptr, reduce,
+                                               argmax, n_items)
 
 
 # ----------------------------------------------------------------------------------- autograd
@@ -602,6 +556,25 @@ class SegmentReduceFn(torch.autograd.Function):
         gs = segment_reduce_bwd(g.contiguous(), ctx.csr, ctx.reduce,
                                 argmax if ctx.reduce == "max" else None, ctx.n)
         return gs, None, None
+
+
+class SegmentMaxFn(torch.autograd.Function):
+    """(out, argmax) of a segmented max (torch_scatter.scatter_max along dim 0): the gradient
+    goes to the arg-max item of each (segment, feature); argmax is not differentiable."""
+
+    @staticmethod
+    def forward(ctx, src2d, csr):
+        out, argmax = segment_reduce(src2d, csr, "max")
+        ctx.csr, ctx.n = csr, src2d.shape[0]
+        ctx.save_for_backward(argmax)
+        ctx.mark_non_differentiable(argmax)
+        return out, argmax
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g, _g_arg):
+        (argmax,) = ctx.saved_tensors
+        return segment_reduce_bwd(g.contiguous(), ctx.csr, "max", argmax, ctx.n), None
 
 
 class GatherRowsFn(torch.autograd.Function):
@@ -645,13 +618,7 @@ def _cfconv_csr(index, n):
 
 def cfconv_aggregate(x, xidx, w, csr):
     """out[s] = sum over CSR segment s of x[xidx[e]] * w[e] (K13 gmp_cfconv_aggregate_f32)."""
-    lib = _lib.load()
-    out = torch.empty((csr.n_seg, x.shape[1]), dtype=torch.float32, device=x.device)
-    err = torch.zeros(1, dtype=torch.int32, device=x.device)
-    check(lib.gmp_cfconv_aggregate_f32(_p(x), x.shape[0], _p(xidx), _p(w), w.shape[0],
-                                       x.shape[1], _p(csr.perm), _p(csr.rowptr), csr.n_seg,
-                                       _p(out), _p(err), _stream()), "gmp_cfconv_aggregate_f32")
-    return out
+    return _lib.torch_ops().cfconv_aggregate(x, _i64c(xidx), w, csr.perm, csr.rowptr, csr.n_seg)
 
 
 class CFConvAggregateFn(torch.autograd.Function):
@@ -675,12 +642,7 @@ class CFConvAggregateFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = cfconv_aggregate(g, ctx.dst, W, _cfconv_csr(ctx.src, x.shape[0]))
         if ctx.needs_input_grad[1]:
-            lib = _lib.load()
-            dW = torch.empty_like(W)
-            err = torch.zeros(1, dtype=torch.int32, device=W.device)
-            check(lib.gmp_cfconv_wgrad_f32(_p(g), g.shape[0], _p(ctx.dst), _p(x), x.shape[0],
-                                           _p(ctx.src), W.shape[0], W.shape[1], _p(dW), _p(err),
-                                           _stream()), "gmp_cfconv_wgrad_f32")
+            dW = _lib.torch_ops().cfconv_wgrad(g, _i64c(ctx.dst), x, _i64c(ctx.src))
         return dx, dW, None, None, None
 
 
@@ -689,22 +651,15 @@ class ShiftedSoftplusFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, shift):
-        lib = _lib.load()
-        y = torch.empty_like(x)
-        check(lib.gmp_ssp_fwd_f32(_p(x), x.numel(), float(shift), _p(y), _stream()),
-              "gmp_ssp_fwd_f32")
+        y = _lib.torch_ops().ssp_fwd(x, float(shift))
         ctx.save_for_backward(x)
         return y
 
     @staticmethod
     @once_differentiable
     def backward(ctx, g):
-        lib = _lib.load()
         (x,) = ctx.saved_tensors
-        g = _f32c(g)
-        dx = torch.empty_like(x)
-        check(lib.gmp_ssp_bwd_f32(_p(x), _p(g), x.numel(), _p(dx), _stream()), "gmp_ssp_bwd_f32")
-        return dx, None
+        return _lib.torch_ops().ssp_bwd(x, _f32c(g)), None
 
 
 def shifted_softplus(x, shift):
@@ -789,18 +744,11 @@ class EgnnMessageFn(torch.autograd.Function):
         AB = h.mm(Wcat.t())  # [h W1a^T | h W1b^T]
         params = tuple(_f32c(t) for t in (W1[:, 2 * d], b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3,
                                           b3, ln3w, ln3b, w4, b4))
-        m_aggr = torch.empty((N, d), dtype=torch.float32, device=h.device)
-        pos_aggr = torch.empty((N, 3), dtype=torch.float32, device=h.device)
         train = any(ctx.needs_input_grad)
-        xhat = torch.empty((3, E, d), dtype=torch.float32, device=h.device) if train else None
-        rstd = torch.empty((E, 3), dtype=torch.float32, device=h.device) if train else None
-        P = _egnn_params(params)
         with _timed("egnn_edge_fwd"):
-            check(lib.gmp_egnn_edge_fwd_f32(N, E, d, _p(AB), _p(pos), _p(graph.rowptr),
-                                          _p(graph.recv), _p(graph.send), ctypes.byref(P),
-                                          _lib.ACT[act], int(msg_mean), float(eps), _p(m_aggr),
-                                          _p(pos_aggr), _p(xhat), _p(rstd), _stream()),
-                  "gmp_egnn_edge_fwd_f32")
+            m_aggr, pos_aggr, xhat, rstd = _lib.torch_ops().egnn_edge_fwd(
+                AB, pos, graph.rowptr, graph.recv, graph.send, list(params), _lib.ACT[act],
+                bool(msg_mean), float(eps), train)
         ctx.graph, ctx.act, ctx.msg_mean, ctx.N = graph, act, msg_mean, N
         if train:
             ctx.save_for_backward(h, pos, xhat, rstd, W1, *params)
@@ -818,22 +766,10 @@ class EgnnMessageFn(torch.autograd.Function):
         g_m = torch.zeros((N, d), device=dev) if g_m is None else _f32c(g_m)
         g_p = torch.zeros((N, 3), device=dev) if g_p is None else _f32c(g_p)
         f = dict(dtype=torch.float32, device=dev)
-        dA = torch.empty((N, d), **f)
-        dpos_recv = torch.empty((N, 3), **f)
-        dpre1 = torch.empty((E, d), **f)
-        gdiff = torch.empty((E, 3), **f)
-        dpre2 = torch.empty((E, d), **f)
-        dpre3 = torch.empty((E, d), **f)
-        rows = lib.gmp_egnn_edge_bwd_partials_rows(E, d)
-        partials = torch.empty((rows, 8 * d + 1), **f)
-        P = _egnn_params(params)
         with _timed("egnn_edge_bwd"):
-            check(lib.gmp_egnn_edge_bwd_f32(N, E, d, _p(pos), _p(graph.rowptr), _p(graph.recv),
-                                          _p(graph.send), ctypes.byref(P), _lib.ACT[ctx.act],
-                                          int(ctx.msg_mean), _p(xhat), _p(rstd), _p(g_m),
-                                          _p(g_p), _p(dA), _p(dpos_recv), _p(dpre1), _p(gdiff),
-                                          _p(dpre2), _p(dpre3), _p(partials), _stream()),
-                  "gmp_egnn_edge_bwd_f32")
+            dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, partials = _lib.torch_ops().egnn_edge_bwd(
+                pos, graph.rowptr, graph.recv, graph.send, list(params), _lib.ACT[ctx.act],
+                bool(ctx.msg_mean), xhat, rstd, g_m, g_p)
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")

@@ -4,8 +4,10 @@ aggregate and pools).
 
 Semantics (torch_scatter 2.x): out rows along `dim` = dim_size or index.max()+1 (the latter
 costs one host sync, as in torch_scatter); empty rows are 0; mean = sum / count.clamp(1);
-max returns values only (empty rows 0).  Reductions are deterministic segmented sums over a
-stable receiver-sorted CSR (gmp_csr_build + gmp_segment_reduce_f32), not atomics.
+scatter(reduce="max"/"min") returns values, scatter_max / scatter_min return (out, arg) with
+arg = src.size(dim) for empty rows (torch_scatter's convention).  Reductions are deterministic
+segmented sums over a stable receiver-sorted CSR (torch.ops.gmp.csr_build +
+torch.ops.gmp.segment_reduce), not atomics; min is -max(-src) (negation is exact).
 """
 import torch
 
@@ -19,8 +21,14 @@ def _rows(index, dim_size):
 
 
 def scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum"):
-    if reduce not in ("sum", "add", "mean", "max"):
+    if reduce not in ("sum", "add", "mean", "max", "min"):
         raise ValueError(f"unsupported reduce {reduce!r}")
+    if reduce in ("max", "min"):
+        o = _scatter_arg(src, index, dim, dim_size, reduce)[0]
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
     dim = dim % src.dim()
     if index.dim() != 1:
         # torch_scatter broadcasts index; the reference always passes a 1-D index along dim
@@ -49,8 +57,41 @@ def scatter_mean(src, index, dim=-1, out=None, dim_size=None):
     return scatter(src, index, dim, out, dim_size, "mean")
 
 
+def _scatter_arg(src, index, dim, dim_size, reduce):
+    dim = dim % src.dim()
+    if index.dim() != 1:
+        raise NotImplementedError("gmp scatter supports 1-D index along `dim`")
+    n = _rows(index, dim_size)
+    x = src.movedim(dim, 0)
+    shp = x.shape
+    x2 = x.reshape(shp[0], -1)
+    csr = ops.get_csr(index, n)
+    if reduce == "min":
+        o, arg = ops.SegmentMaxFn.apply(-x2, csr)
+        o = 0.0 - o  # (+0 for empty rows, not -0)
+    else:
+        o, arg = ops.SegmentMaxFn.apply(x2, csr)
+    o = o.reshape((n,) + tuple(shp[1:])).movedim(0, dim)
+    arg = arg.reshape((n,) + tuple(shp[1:])).movedim(0, dim)
+    return o, arg
+
+
 def scatter_max(src, index, dim=-1, out=None, dim_size=None):
-    return scatter(src, index, dim, out, dim_size, "max")
+    """torch_scatter.scatter_max: (max values, argmax along dim)."""
+    o, arg = _scatter_arg(src, index, dim, dim_size, "max")
+    if out is not None:
+        out.copy_(o)
+        o = out
+    return o, arg
+
+
+def scatter_min(src, index, dim=-1, out=None, dim_size=None):
+    """torch_scatter.scatter_min: (min values, argmin along dim)."""
+    o, arg = _scatter_arg(src, index, dim, dim_size, "min")
+    if out is not None:
+        out.copy_(o)
+        o = out
+    return o, arg
 
 
 def global_add_pool(x, batch, size=None):

@@ -437,11 +437,14 @@ int gmp_sum_rows_f32(const float* partials, int64_t nrows, int64_t width, float*
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all three output irreps
  * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)
- * (irreps_tools.py:63-79).  A_nu (C, 9, 9^nu) = sum_k U_nu[m, ..., k] W_nu[k, c] stacked over
- * the output rows m = [0e | 1o (3) | 2e (5)] (the host builds them from the module's
- * U_matrix_nu buffers and weights).  out (N, 9C) in mul_ir order [0e: C | 1o: 3C | 2e: 5C].
- * Backward: dx (N, C, 9) (may be NULL) and dA partials (gmp_sc_groups(N), C, 9, 819) with
- * monomials q = [deg1 (9) | deg2 (81) | deg3 (729)] (may be NULL); the caller sums the groups.
+ * (irreps_tools.py:63-79).  Coefficients over the SYMMETRIC monomial basis (x_i x_j x_k is
+ * symmetric, so every permutation's coefficient folds into the sorted index tuple):
+ *   A1 (C, 9, 9), A2 (C, 9, 45) over i <= j, A3 (C, 9, 165) over i <= j <= k (lexicographic),
+ *   A_nu[c, m, q] = sum over the distinct permutations p of q of sum_k U_nu[m, p, k] W_nu[k, c]
+ * (the host builds them from the module's U_matrix_nu buffers and weights, differentiably).
+ * out (N, 9C) in mul_ir order [0e: C | 1o: 3C | 2e: 5C].  Backward: dx (N, C, 9) (may be NULL)
+ * and dA partials (gmp_sc_groups(N), C, 9, nq) with nq = 9 / 54 / 219 for correlation 1 / 2 / 3
+ * (monomials [deg1 | deg2 | deg3] as above; may be NULL); the caller sums the groups.
  * ------------------------------------------------------------------------------------------ */
 int gmp_sc_groups(int64_t n_nodes);
 int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int correlation,

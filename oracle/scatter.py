@@ -3,7 +3,9 @@
 Follows the call sites models/layers/egnn_layer.py:77,79, models/layers/tfn_layer.py:87,
 models/layers/gvp_layer.py:415 and PyG's default aggregate / global pools:
   out[index[e]] (+)= src[e]; rows = dim_size or index.max()+1; empty rows are 0;
-  mean = sum / count.clamp(min=1); max: empty rows 0.
+  mean = sum / count.clamp(min=1); max / min: empty rows 0.
+scatter_arg: torch_scatter.scatter_max / scatter_min's (values, arg) with arg = src.size(dim)
+for empty rows and the first (lowest-index) item among ties, by a plain loop (small inputs).
 """
 import torch
 
@@ -31,9 +33,29 @@ def scatter(src, index, dim=0, dim_size=None, reduce="sum"):
         idx = index.view((-1,) + (1,) * (x.dim() - 1)).expand_as(x)
         out = out.scatter_reduce(0, idx, x, reduce="amax", include_self=True)
         out = torch.where(torch.isinf(out) & (out < 0), torch.zeros_like(out), out)
+    elif reduce == "min":
+        out = torch.full(shape, float("inf"), dtype=src.dtype)
+        idx = index.view((-1,) + (1,) * (x.dim() - 1)).expand_as(x)
+        out = out.scatter_reduce(0, idx, x, reduce="amin", include_self=True)
+        out = torch.where(torch.isinf(out) & (out > 0), torch.zeros_like(out), out)
     else:
         raise ValueError(reduce)
     return out.movedim(0, dim)
+
+
+def scatter_arg(src, index, dim_size, reduce):
+    """(values, arg) along dim 0 of a 2-D src for reduce in {max, min}."""
+    n = _rows(index, dim_size)
+    E, F = src.shape
+    val = torch.zeros((n, F), dtype=src.dtype)
+    arg = torch.full((n, F), E, dtype=torch.int64)
+    for e in range(E):
+        s = int(index[e])
+        for f in range(F):
+            v = src[e, f]
+            if arg[s, f] == E or (v > val[s, f] if reduce == "max" else v < val[s, f]):
+                val[s, f], arg[s, f] = v, e
+    return val, arg
 
 
 def global_add_pool(x, batch, size=None):

@@ -51,7 +51,7 @@ def test_gather_rows(F):
     assert torch.equal(out.cpu(), src[idx])  # a gather is bit-exact
 
 
-@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
 @pytest.mark.parametrize("F,n,n_seg", [(1, 500, 40), (3, 2000, 97), (16, 4000, 300),
                                        (128, 20000, 1000), (130, 3000, 211), (1152, 3000, 150),
                                        # long segments -> split path (pools, embedding bwd)
@@ -80,6 +80,82 @@ def test_scatter_matches_oracle(reduce, F, n, n_seg):
     sr = src.clone().requires_grad_(True)
     oscatter(sr, idx, 0, n_seg, reduce).backward(go)
     torch.testing.assert_close(s.grad.cpu(), sr.grad, atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("reduce", ["max", "min"])
+def test_scatter_max_min_return_arg(reduce):
+    """torch_scatter.scatter_max / scatter_min: (values, arg) with arg = src.size(0) for empty
+    rows and the gradient routed to the arg item; ties resolved to the first item."""
+    from gmp_amd import scatter_max, scatter_min
+    from oracle.scatter import scatter_arg
+    g = torch.Generator().manual_seed(11)
+    src = torch.randint(-4, 5, (300, 5), generator=g).float()  # many ties
+    idx = _rand_index(300, 40, 12, skip_tail=2)
+    fn = scatter_max if reduce == "max" else scatter_min
+    s = src.to(DEV).requires_grad_(True)
+    val, arg = fn(s, idx.to(DEV), dim=0, dim_size=40)
+    rv, ra = scatter_arg(src, idx, 40, reduce)
+    assert torch.equal(val.detach().cpu(), rv) and torch.equal(arg.cpu(), ra)
+    assert not torch.signbit(val.detach().cpu()[ra == 300]).any()  # +0 in empty rows
+    go = torch.randn(40, 5, generator=g)
+    val.backward(go.to(DEV))
+    expect = torch.zeros(301, 5)
+    expect.scatter_add_(0, ra, go)
+    assert torch.equal(s.grad.cpu(), expect[:300])
+
+
+def test_torch_ops_boundary_and_compile():
+    """The operators are registered as torch.ops.gmp.* (TORCH_LIBRARY(gmp)); they run directly,
+    trace as single opaque nodes under torch.compile (Meta kernels, no graph break inside an
+    op), and agree with the Python-level path."""
+    import gmp_amd  # noqa: F401
+    from gmp_amd import _lib, ops
+    ops_ = _lib.torch_ops()
+    g = torch.Generator().manual_seed(3)
+    src = torch.randn(5000, 64, generator=g).to(DEV)
+    idx = _rand_index(5000, 300, 4).to(DEV)
+    csr = ops.CSR(idx, 300)
+    out, arg = ops_.segment_reduce(src, csr.perm, csr.rowptr, 300, "sum")
+    assert arg.numel() == 0
+    torch.testing.assert_close(out.cpu(), oscatter(src.cpu(), idx.cpu(), 0, 300, "sum"),
+                               atol=1e-5, rtol=1e-5)
+
+    def f(x, perm, rowptr):
+        y, _ = torch.ops.gmp.segment_reduce(x * 2.0, perm, rowptr, 300, "mean")
+        return y.relu()
+
+    from torch._dynamo.utils import counters
+    counters.clear()
+    cf = torch.compile(f, fullgraph=True, backend="eager")
+    torch.testing.assert_close(cf(src, csr.perm, csr.rowptr), f(src, csr.perm, csr.rowptr))
+    assert not counters["graph_break"]
+    # the fused EGNN edge kernel as an operator
+    from gmp_amd.graph import radius_graph
+    lay = gmp_amd.EGNNLayer(128, "relu", "layer", "sum").to(DEV)
+    gr = radius_graph(num_nodes=300, target_edges=4000, r=2.5, seed=2, tol=0.3)
+    eg = ops.egnn_graph(gr.edge_index.to(DEV), gr.num_nodes)
+    h = torch.randn(gr.num_nodes, 128, device=DEV)
+    pos = gr.pos.to(DEV)
+    W1 = lay.mlp_msg[0].weight
+    AB = h.mm(torch.cat([W1[:, :128], W1[:, 128:256]], 0).t()).contiguous()
+    params = [t.detach().contiguous() for t in (
+        W1[:, 256], lay.mlp_msg[0].bias, lay.mlp_msg[1].weight, lay.mlp_msg[1].bias,
+        lay.mlp_msg[3].weight, lay.mlp_msg[3].bias, lay.mlp_msg[4].weight, lay.mlp_msg[4].bias,
+        lay.mlp_pos[0].weight, lay.mlp_pos[0].bias, lay.mlp_pos[1].weight, lay.mlp_pos[1].bias,
+        lay.mlp_pos[3].weight.view(-1), lay.mlp_pos[3].bias)]
+    m, pa, xh, rs = torch.ops.gmp.egnn_edge_fwd(AB.detach(), pos, eg.rowptr, eg.recv, eg.send,
+                                                params, 0, False, 1e-5, False)
+    with torch.no_grad():
+        m_ref, p_ref = ops.EgnnMessageFn.apply(h, pos, eg, "relu", False, 1e-5,
+                                               *[p for p in (W1, *params[1:])])
+    assert torch.equal(m, m_ref) and torch.equal(pa, p_ref)
+    assert xh.numel() == 0
+    counters.clear()
+    ce = torch.compile(lambda a: torch.ops.gmp.egnn_edge_fwd(a, pos, eg.rowptr, eg.recv, eg.send,
+                                                             params, 0, False, 1e-5, False)[0],
+                       fullgraph=True, backend="eager")
+    assert torch.equal(ce(AB.detach()), m)
+    assert not counters["graph_break"]
 
 
 def test_scatter_dim_size_inference_and_dims():
