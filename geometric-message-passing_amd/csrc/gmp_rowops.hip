@@ -152,7 +152,8 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
 // out[f] = sum over the partial rows (f < 2d: [dgamma | dbeta]) in a fixed order: thread
 // (column c, row group q) sums rows q, q + kSG, ... ; the kSG group sums are then added in
 // group order.  Deterministic.
-constexpr int kSC = 16, kSG = 16;  // columns x row groups per block (256 threads)
+constexpr int kSC = 16, kSG = 64;  // columns x row groups per block (1024 threads): each
+                                   // thread's rows load in one burst for <= 1024 rows
 __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __restrict__ partials,
                                                              int nrows, int width,
                                                              float* __restrict__ out) {
