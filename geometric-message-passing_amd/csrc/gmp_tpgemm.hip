@@ -214,10 +214,15 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     for (int j = 0; j < 2; ++j) {
       const int st = s0 + j;
       const unsigned char* nb = smg + ((st + 1) & 1) * kStage;
+      // sched barriers pin the ring discipline: slot j's registers are consumed by the stash
+      // before its next loads are issued, so the stash waits only for loads two stages old
+      // (counted vmcnt) instead of the scheduler hoisting the new loads and draining vmcnt(0)
+      stash(j, smg + (st & 1) * kStage, st + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      fetch(j, st + 4);
+      __builtin_amdgcn_sched_barrier(0);
       load_frag(F[j ^ 1], nb, nb + 3 * kPlane, wm, wn, li, g);
       mma_x3(acc, F[j]);
-      stash(j, smg + (st & 1) * kStage, st + 2);
-      fetch(j, st + 4);
       __syncthreads();
     }
   }
@@ -351,12 +356,14 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int gs = s0 + j;
+      stash(j, sB + (gs & 1) * 3 * kPlane);
+      __builtin_amdgcn_sched_barrier(0);
+      fetch(j, gs + 4);
+      __builtin_amdgcn_sched_barrier(0);
       load_frag(F[j ^ 1], sA + ((gs + 1) % NKS) * 3 * kPlane, sB + ((gs + 1) & 1) * 3 * kPlane,
                 wm, wn, li, g);
       mma_x3(acc, F[j]);
       if (gs < nst && gs % NKS == NKS - 1) store_tile(t0 + gs / NKS);
-      stash(j, sB + (gs & 1) * 3 * kPlane);
-      fetch(j, gs + 4);
       __syncthreads();
     }
   }

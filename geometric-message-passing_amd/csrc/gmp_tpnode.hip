@@ -24,7 +24,9 @@ constexpr int kMaxH = 256;
 
 // ---------------------------------------------------------------------------------- outer
 // grid (ceil(w / (64 kOuterRB)), receivers): the workgroup stages the receiver's hidden radial
-// rows a_e once and produces kOuterRB 64-row blocks of S from them
+// rows a_e once and produces up to kOuterRB 64-row blocks of S from them (one workgroup per
+// receiver for kOuterRB >= w / 64; measured slower than one 64-row block per workgroup: 10.1
+// vs 9.1 ms for the 32.8 GB MACE-128 lo = 2 path -- fewer workgroups in flight per CU)
 constexpr int kOuterRB = 1;
 __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
                                                             const int64_t* __restrict__ eoff,
@@ -39,18 +41,23 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
   const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
   const int TJ = H >> 4;
   float* Sn = S + (int64_t)n * w * H;
-  if (kOuterRB == 1 && deg <= kEdgeStage) {
-    // common case (one edge stage): this lane's Z column values for every k step are loaded
-    // up front, in flight together with the a-row staging — no dependent global load inside the
-    // MFMA loop (the block's latency chain was load -> MFMA per step, ~5 HBM round trips)
+  const int rb0 = blockIdx.x * kOuterRB;
+  const int rb1 = min(rb0 + kOuterRB, (w + kRowsPerBlock - 1) / kRowsPerBlock);
+  if (deg <= kEdgeStage) {
+    // common case (one edge stage): this lane's Z column values for every k step of the next
+    // row block are loaded while the current block's MFMAs run (register double buffer), the a
+    // rows are staged once; no dependent global load inside the MFMA loop
     const int ns = (int)deg, nst = (ns + 3) >> 2;
-    const int r = blockIdx.x * kRowsPerBlock + wv * 16 + i;
-    float zr[kEdgeStage / 4];
+    float zr[2][kEdgeStage / 4];
+    auto zload = [&](int buf, int rb) {
+      const int r = rb * kRowsPerBlock + wv * 16 + i;
 #pragma unroll
-    for (int s = 0; s < kEdgeStage / 4; ++s) {
-      const int el = 4 * s + kk;
-      zr[s] = (el < ns && r < w) ? Z[(e0 + el) * w + r] : 0.f;
-    }
+      for (int s = 0; s < kEdgeStage / 4; ++s) {
+        const int el = 4 * s + kk;
+        zr[buf][s] = (el < ns && r < w) ? Z[(e0 + el) * w + r] : 0.f;
+      }
+    };
+    zload(0, rb0);
     for (int x = tid; x < 4 * nst * (H >> 2); x += kNT) {  // padding rows zeroed
       const int e = x / (H >> 2), q = x - e * (H >> 2);
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -58,28 +65,34 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
     }
     __syncthreads();
-    f32x4 acc[kMaxH / 16];
+    for (int rb = rb0; rb < rb1; ++rb) {
+      const int cur = (rb - rb0) & 1;
+      if (rb + 1 < rb1) zload(cur ^ 1, rb + 1);
+      const int r = rb * kRowsPerBlock + wv * 16 + i;
+      f32x4 acc[kMaxH / 16];
 #pragma unroll
-    for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float zsum = 0.f;
+      for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float zsum = 0.f;
 #pragma unroll
-    for (int s = 0; s < kEdgeStage / 4; ++s) {
-      if (s < nst) {
-        const int el = 4 * s + kk;
-        zsum += zr[s];
+      for (int s = 0; s < kEdgeStage / 4; ++s) {
+        if (s < nst) {
+          const int el = 4 * s + kk;
+          const float zv = zr[cur][s];
+          zsum += zv;
+#pragma unroll
+          for (int t = 0; t < kMaxH / 16; ++t)
+            if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zv, acc[t], 0, 0, 0);
+        }
+      }
+      if (r < w) {
 #pragma unroll
         for (int t = 0; t < kMaxH / 16; ++t)
-          if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zr[s], acc[t], 0, 0, 0);
+          if (t < TJ) *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
       }
+      zsum += __shfl_xor(zsum, 16);
+      zsum += __shfl_xor(zsum, 32);
+      if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
     }
-    if (r < w) {
-#pragma unroll
-      for (int t = 0; t < kMaxH / 16; ++t)
-        if (t < TJ) *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
-    }
-    zsum += __shfl_xor(zsum, 16);
-    zsum += __shfl_xor(zsum, 32);
-    if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
     return;
   }
   if (deg <= kEdgeStage) {  // stage a once for all row blocks
@@ -92,9 +105,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
     }
     __syncthreads();
   }
-  for (int rbi = 0; rbi < kOuterRB; ++rbi) {
-    const int rb = blockIdx.x * kOuterRB + rbi;
-    if (rb * kRowsPerBlock >= w) break;
+  for (int rb = rb0; rb < rb1; ++rb) {
     // D = S^T tile: D[j][r] = sum_e A[e, j] Z[e, r]  (A op = a columns, B op = Z columns), so a
     // lane holds 4 consecutive j of one row r and stores them as one float4
     const int r = rb * kRowsPerBlock + wv * 16 + i;  // this lane's output row
@@ -287,12 +298,218 @@ __global__ __launch_bounds__(kNT, 2) void tp_node_apply_kernel(int w, int H,
   }
 }
 
+// ---------------------------------------------------------------------------------- apply v2
+// The same contraction on the bf16 MFMA over exact three-plane f32 splits (gmp_tpgemm.hip's
+// arithmetic: six plane products, f32 accumulation).  One 512-thread workgroup per receiver edge
+// group (<= 32 edges); rows of T in blocks of 32 (one k = 2lo+1 row, 32 consecutive u: a
+// contiguous 32 H-float block), split once into an LDS image that serves both products
+// (H % 64 == 0: every thread stages whole float4 units of the block):
+//   dZ tile D[r][e] = sum_j T[r][j] A[e][j]   (waves 0-3: T row reads, ds_read_b128)
+//   dA tile D[e][j] += sum_r Z[e][r] T[r][j]  (waves 4-7: T column reads, ds_read_b64_tr_b16)
+// T image: [plane][half (128 j)][32 rows][256 B] with chunk c of row r at c ^ ((r&3)<<2 |
+// (r>>2)&3) (the dual row / transposed-read image of the CDNA4 guide).  A_n and Z as [plane][k
+// step][32 edges][64 B] (chunk q at q ^ ((row >> 1) & 3)).  T streams through registers two
+// blocks ahead (a double-buffered LDS image with one barrier per block measured slower: 19.7
+// vs 13.2 ms at the MACE-128 lo = 2 shape, 254 VGPRs); 13.2 ms against 13.75 for the f32-MFMA
+// kernel: both wait on the T stream and LDS (2.5-3 TB/s of T).  Requires w % 32 == 0,
+// H % 64 == 0, H <= 256.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kV2T = 512;
+constexpr int kV2R = 32;                    // T rows per block
+constexpr int kV2E = 32;                    // edges per group
+constexpr int kTPlane = 2 * kV2R * 256;     // bytes of one T plane image (two 128-j halves)
+constexpr int kSPlane = kV2E * 64;          // bytes of one 32 x 32 bf16 image
+
+__device__ __forceinline__ void split3v(f32x2_t x, unsigned& h, unsigned& m, unsigned& l) {
+  const bf16x2_t bh = __builtin_convertvector(x, bf16x2_t);
+  const f32x2_t r1 = x - __builtin_convertvector(bh, f32x2_t);
+  const bf16x2_t bm = __builtin_convertvector(r1, bf16x2_t);
+  const f32x2_t r2 = r1 - __builtin_convertvector(bm, f32x2_t);
+  const bf16x2_t bl = __builtin_convertvector(r2, bf16x2_t);
+  h = __builtin_bit_cast(unsigned, bh);
+  m = __builtin_bit_cast(unsigned, bm);
+  l = __builtin_bit_cast(unsigned, bl);
+}
+__device__ __forceinline__ int toff(int r, int ch) {  // ch: 16-byte chunk 0..31 of a 512-B row
+  const int c = ch & 15;
+  return (ch >> 4) * (kV2R * 256) + 256 * r + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+__device__ __forceinline__ int soff(int row, int chunk) {
+  return row * 64 + 16 * (chunk ^ ((row >> 1) & 3));
+}
+// split an f32x4 and write its three 8-byte plane pieces
+__device__ __forceinline__ void put3(unsigned char* base, int plane_bytes, int off, f32x4 v) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split3v(f32x2_t{v[0], v[1]}, h0, m0, l0);
+  split3v(f32x2_t{v[2], v[3]}, h1, m1, l1);
+  *reinterpret_cast<u32x2_t*>(base + off) = u32x2_t{h0, h1};
+  *reinterpret_cast<u32x2_t*>(base + plane_bytes + off) = u32x2_t{m0, m1};
+  *reinterpret_cast<u32x2_t*>(base + 2 * plane_bytes + off) = u32x2_t{l0, l1};
+}
+__device__ __forceinline__ f32x4 mma6(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4 t) {
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], t, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], t, 0, 0, 0);
+}
+
+template <int HS>  // H / 32 k steps (H <= 256)
+__global__ __launch_bounds__(kV2T, 1) void tp_node_apply_x3_kernel(
+    int w, const int64_t* __restrict__ eoff, const float* __restrict__ Z,
+    const float* __restrict__ A, const float* __restrict__ T, const float* __restrict__ Tb,
+    float* __restrict__ dZ, float* __restrict__ dA) {
+  constexpr int H = 32 * HS, H4 = H / 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm2[];
+  unsigned char* sT = sm2;                                // 3 x kTPlane
+  unsigned char* sA = sm2 + 3 * kTPlane;                  // 3 x HS x kSPlane
+  unsigned char* sZ = sA + 3 * HS * kSPlane;              // 3 x kSPlane
+  const int n = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
+  const float* Tn = T + (int64_t)n * w * H;
+  const int nblk = w / kV2R;
+  constexpr int TL = kV2R * H4 / kV2T;  // T float4 units per thread per block (H = 256: 4)
+  for (int64_t g0 = 0; g0 < deg; g0 += kV2E) {
+    const int ng = (int)((deg - g0) < kV2E ? (deg - g0) : kV2E);
+    __syncthreads();  // previous group's readers of sA done
+    // A_n rows (edges x H) -> planes [s][e][32 j]
+    for (int v = tid; v < kV2E * H4; v += kV2T) {
+      const int e = v / H4, c4 = v - e * H4, j = 4 * c4;
+      f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e < ng) x = *reinterpret_cast<const f32x4*>(A + (e0 + g0 + e) * H + j);
+      const int sstep = j >> 5, cq = (j & 31) >> 2;
+      put3(sA + sstep * kSPlane, HS * kSPlane, soff(e, cq >> 1) + 8 * (cq & 1), x);
+    }
+    // register ring: T block (TL float4 per thread) and Z block (one float4, threads < 256)
+    f32x4 rT[2][TL], rZ[2];
+    auto fetch = [&](int slot, int b) {
+      const int bc = b < nblk ? b : nblk - 1;
+      const float* tb = Tn + (int64_t)bc * kV2R * H;
+#pragma unroll
+      for (int q = 0; q < TL; ++q)
+        rT[slot][q] = *reinterpret_cast<const f32x4*>(tb + 4 * (tid + kV2T * q));
+      const int e = (tid >> 3) & 31, c4 = tid & 7;
+      const int64_t ee = (e < ng ? e : 0) + e0 + g0;
+      rZ[slot] = *reinterpret_cast<const f32x4*>(Z + ee * w + bc * kV2R + 4 * c4);
+    };
+    auto stash = [&](int slot) {
+#pragma unroll
+      for (int q = 0; q < TL; ++q) {
+        const int v = tid + kV2T * q;
+        const int r = v / H4, c4 = v - r * H4;
+        put3(sT, kTPlane, toff(r, c4 >> 1) + 8 * (c4 & 1), rT[slot][q]);
+      }
+      if (tid < 256) {
+        const int e = tid >> 3, c4 = tid & 7;
+        f32x4 x = rZ[slot];
+        if (e >= ng) x = f32x4{0.f, 0.f, 0.f, 0.f};
+        put3(sZ, kSPlane, soff(e, c4 >> 1) + 8 * (c4 & 1), x);
+      }
+    };
+    f32x4 accA[HS];  // dA tiles of waves 4-7: e tile (wv - 4) >> 1, j tiles HS ((wv - 4) & 1) + t
+#pragma unroll
+    for (int t = 0; t < HS; ++t) accA[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    fetch(0, 0);
+    fetch(1, 1);
+    for (int b = 0; b < nblk; ++b) {
+      const int slot = b & 1;
+      __syncthreads();  // readers of the previous block's images done (and sA written)
+      stash(slot);
+      __syncthreads();
+      fetch(slot, b + 2);
+      if (wv < 4) {
+        // dZ tile: rows r = 16 rt + .., edges 16 et + ..
+        const int rt = wv & 1, et = wv >> 1;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < HS; ++st) {
+          bf16x8_t a[3], bb[3];
+          const int ta = toff(16 * rt + li, 4 * st + g);
+          const int sb = st * kSPlane + soff(16 * et + li, g);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            a[p] = *reinterpret_cast<const bf16x8_t*>(sT + p * kTPlane + ta);
+            bb[p] = *reinterpret_cast<const bf16x8_t*>(sA + p * HS * kSPlane + sb);
+          }
+          acc = mma6(a, bb, acc);
+        }
+        // lane: D[r = 4g + q][e = li] -> dZ[e][r0 + 16 rt + 4g .. + 3] (+ Tb)
+        const int e = 16 * et + li;
+        if (e < ng) {
+          const int r = b * kV2R + 16 * rt + 4 * g;
+          const f32x4 tb = *reinterpret_cast<const f32x4*>(Tb + (int64_t)n * w + r);
+          *reinterpret_cast<f32x4*>(dZ + (e0 + g0 + e) * w + r) = acc + tb;
+        }
+      } else {
+        const int v = wv - 4, et = v >> 1;
+        bf16x8_t a[3];
+        const int za = soff(16 * et + li, g);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8_t*>(sZ + p * kSPlane + za);
+        const int q = li >> 2, pp = li & 3;
+#pragma unroll
+        for (int t = 0; t < HS; ++t) {
+          const int jt = HS * (v & 1) + t;  // 16-column tile of j
+          bf16x8_t bb[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const unsigned char* base = sT + p * kTPlane;
+            const int o0 = toff(8 * g + q, 2 * jt + (pp >> 1)) + 8 * (pp & 1);
+            const int o1 = toff(8 * g + 4 + q, 2 * jt + (pp >> 1)) + 8 * (pp & 1);
+            const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) i16x4_t*)(base + o0));
+            const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) i16x4_t*)(base + o1));
+            bb[p] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4,
+                                                                           5, 6, 7));
+          }
+          accA[t] = mma6(a, bb, accA[t]);
+        }
+      }
+    }
+    if (wv >= 4) {  // dA[e][j] += (per-path launches on one stream: ordered RMW, deterministic)
+      const int v = wv - 4, et = v >> 1;
+#pragma unroll
+      for (int t = 0; t < HS; ++t) {
+        const int j = 16 * (HS * (v & 1) + t) + li;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = 16 * et + 4 * g + q;
+          if (e < ng) dA[(e0 + g0 + e) * H + j] += accA[t][q];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace gmp
 
 using namespace gmp;
 
+namespace gmp {
+// 1: bf16x3 apply kernel where the shape allows (default); 0: the f32-MFMA kernel
+// (GMP_TP_APPLY_F32=1 or gmp_tp_apply_set_x3(0), A/B studies)
+int g_apply_x3 = getenv("GMP_TP_APPLY_F32") && atoi(getenv("GMP_TP_APPLY_F32")) ? 0 : 1;
+}  // namespace gmp
+
 extern "C" {
+
+int gmp_tp_apply_set_x3(int on) {
+  const int old = g_apply_x3;
+  g_apply_x3 = on ? 1 : 0;
+  return old;
+}
+
 
 int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                           const float* Z, const float* A, float* S, float* Sb, void* stream) {
@@ -314,6 +531,30 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
   if (n_recv == 0) return GMP_OK;
   GMP_CHECK_ARG(eoff && Z && A && T && Tb && dZ && dA);
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(T) % 16 == 0);
+  const bool a16 = ((reinterpret_cast<uintptr_t>(Z) | reinterpret_cast<uintptr_t>(A) |
+                     reinterpret_cast<uintptr_t>(Tb) | reinterpret_cast<uintptr_t>(dZ)) % 16) == 0;
+  if (w % kV2R == 0 && H % 64 == 0 && a16 && g_apply_x3) {  // whole float4 units per thread
+    const int hs = (int)(H / 32);
+    const size_t smem = (size_t)3 * kTPlane + (size_t)3 * hs * kSPlane + 3 * kSPlane;
+    int rc = 0;
+#define GMP_AV2(HS)                                                                              \
+  {                                                                                              \
+    auto k = tp_node_apply_x3_kernel<HS>;                                                        \
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                      \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                            (int)smem))))                                        \
+      return rc;                                                                                 \
+    k<<<(unsigned)n_recv, kV2T, smem, as_stream(stream)>>>((int)w, eoff, Z, A, T, Tb, dZ, dA);   \
+  }
+    switch (hs) {
+      case 2: GMP_AV2(2) break;
+      case 4: GMP_AV2(4) break;
+      case 6: GMP_AV2(6) break;
+      default: GMP_AV2(8) break;
+    }
+#undef GMP_AV2
+    return launch_status();
+  }
   tp_node_apply_kernel<<<(unsigned)n_recv, kNT, 0, as_stream(stream)>>>(
       (int)w, (int)H, eoff, Z, A, T, Tb, dZ, dA);
   return launch_status();

@@ -277,6 +277,10 @@ int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
 int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                           const float* Z, const float* A, const float* T, const float* Tb,
                           float* dZ, float* dA, void* stream);
+/* apply runs on the bf16 MFMA over exact three-plane splits where w % 32 == 0, H % 64 == 0 and
+ * the operands are 16-byte aligned (default), else on the f32 MFMA; set_x3(0) forces the f32
+ * kernel (A/B studies; GMP_TP_APPLY_F32=1 at load).  Returns the previous setting. */
+int gmp_tp_apply_set_x3(int on);
 
 /* K7g path GEMMs of the receiver-factorised TP convolution on the bf16 MFMA through exact
  * three-plane f32 splits (replaces the library f32 GEMMs out = S W2p + Sb b2p and

@@ -216,3 +216,45 @@ def test_tp_gemm_x3_widen_matches_fp64(M, N, K):
     mag = A.double().abs() @ B.double().abs().t()
     err = ((out[:, :N] - ref).abs() / mag).max().item()
     assert err < 1e-6, err
+
+
+@pytest.mark.parametrize("w,H", [(640, 256), (96, 64), (128, 192), (128, 160)])
+@pytest.mark.parametrize("x3", [1, 0])
+def test_node_apply_bf16x3_matches_fp64(w, H, x3):
+    """The apply kernel on the bf16 MFMA over three-plane splits (x3 = 1; shapes with w % 32 == 0
+    and H % 64 == 0; H = 160 takes the f32 kernel either way) and the f32-MFMA kernel (x3 = 0) against fp64, with edge groups of 0, 1,
+    31, 32, 33 and 70 edges (several 32-edge groups): dZ overwritten (+ Tb), dA accumulated onto
+    existing values; error <= 1e-6 of the sum of |terms| per entry."""
+    from gmp_amd import _lib
+    from gmp_amd.ops import _p, _stream
+    lib = _lib.load()
+    degs = [0, 1, 31, 32, 33, 70, 20, 5]
+    eoff, Z, A, ne = _setup(degs, w, H, seed=w + H)
+    c = len(degs)
+    g = torch.Generator().manual_seed(9)
+    T = torch.randn(c, w, H, generator=g) * torch.logspace(-3, 1, H)
+    Tb = torch.randn(c, w, generator=g)
+    dA0 = torch.randn(ne, H, generator=g)
+    dZ = torch.full((ne + 1, w), 7.0, device=DEV)
+    dA = dA0.clone().to(DEV)
+    eo_d, Z_d, A_d, T_d, Tb_d = (t.to(DEV) for t in (eoff, Z, A, T, Tb))
+    old = lib.gmp_tp_apply_set_x3(x3)
+    try:
+        rc = lib.gmp_tp_node_apply_f32(c, w, H, _p(eo_d), _p(Z_d), _p(A_d), _p(T_d), _p(Tb_d),
+                                       _p(dZ), _p(dA), _stream())
+        torch.cuda.synchronize()
+    finally:
+        lib.gmp_tp_apply_set_x3(old)
+    assert rc == 0
+    assert torch.equal(dZ[ne].cpu(), torch.full((w,), 7.0))  # padding row untouched
+    for n in range(c):
+        e0, e1 = int(eoff[n]), int(eoff[n + 1])
+        if e1 == e0:
+            continue
+        rz = A[e0:e1].double() @ T[n].double().t() + Tb[n].double()
+        mz = A[e0:e1].double().abs() @ T[n].double().abs().t() + Tb[n].double().abs()
+        ra = Z[e0:e1].double() @ T[n].double() + dA0[e0:e1].double()
+        ma = Z[e0:e1].double().abs() @ T[n].double().abs() + dA0[e0:e1].double().abs()
+        ez = ((dZ[e0:e1].cpu().double() - rz).abs() / mz).max().item()
+        ea = ((dA[e0:e1].cpu().double() - ra).abs() / ma).max().item()
+        assert ez < 1e-6 and ea < 1e-6, (n, degs[n], ez, ea)
