@@ -269,16 +269,44 @@ def cpu_baseline(g, args, workload):
                       f"edges): 1 warm-up + mean of {timed} timed step(s), {t:.2f} s/step"}
 
 
-def mace_roofline(model, n_nodes, n_edges, timers, n_steps):
+def tp_node_s_bytes(model, n_nodes, n_edges):
+    """Algorithmic HBM bytes of the S-build launches (gmp_tp_node_outer_f32) per
+    training step: one launch per (layer, path, receiver chunk), forward
+    and backward recompute; each reads its z rows (E w) and hidden radial rows a (E H) once and
+    writes S (N w H) and Sb (N w), fp32.  Chunks split E and N, so the per-step sum is
+    chunk-independent (the launch count is read from the timers)."""
+    total = 0
+    for conv in model.convs:
+        H = conv.fc[0].out_features
+        for _, w in conv.plan.z_regions:
+            total += 2 * 4 * (n_edges * (w + H) + n_nodes * w * (H + 1))
+    return total
+
+
+def mace_roofline(model, n_nodes, n_edges, timers, counts, n_steps):
     """Roofline of the dominant MACE kernel from HIP-event timing inside the measured steps:
-    the receiver-factorised TP contraction."""
+    the S build of the receiver-factorised TP contraction (tp_node_outer_kernel, DESIGN.md K7,
+    ~24% of the step; HBM-bound: it writes N w H fp32 per launch).  `achieved` = algorithmic
+    bytes per launch / average launch duration (both averaged over the step's launch mix, the
+    same mix rocprofv3's per-kernel average and the PMC traffic summarise).  The whole
+    node-form contraction (S + path GEMMs + dW2 + apply) is reported beside it against the
+    f32 MFMA peak."""
     fl = tp_node_flops(model, n_nodes, n_edges)
     keys = ("tp_node_S", "tp_node_W", "tp_node_dW", "tp_node_dZA")
     t_gemm = sum(timers.get(k, 0.0) for k in keys) / n_steps
-    achieved = fl / (t_gemm * 1e-3) / 1e12
-    return {"kernel": "tp_node_gemm", "kernel_prefix": "-", "bound": "mfma",
-            "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+    tp_tflops = fl / (t_gemm * 1e-3) / 1e12
+    s_bytes = tp_node_s_bytes(model, n_nodes, n_edges)
+    s_launches = max(1, counts.get("tp_node_S", 0) // n_steps)
+    s_ms = timers.get("tp_node_S", 0.0) / n_steps
+    achieved = s_bytes / (s_ms * 1e-3) / 1e9 if s_ms > 0 else 0.0
+    return {"kernel": "tp_node_outer (S build)", "kernel_prefix": "tp_node_outer_kernel",
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "bytes_per_launch": s_bytes / s_launches, "launches_per_step": s_launches,
+            "ms_per_launch": s_ms / s_launches,
+            "tp_node_all": {"bound": "mfma", "achieved": tp_tflops,
+                            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": tp_tflops / FP32_MFMA_PEAK_TFLOPS},
             "flops_per_step": fl, "tp_node_gemm_ms_per_step": t_gemm,
             "split_ms_per_step": {k: timers.get(k, 0.0) / n_steps for k in keys},
             "tp_node_prep_ms_per_step": timers.get("tp_node_prep", 0.0) / n_steps,
@@ -336,6 +364,7 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
     timers = {k: ops.kernel_time_ms(k) for k in list(ops.KERNEL_TIMERS)}
     n_timed = steps if not args.graph else max(1, args.timing_steps)
     totals = {k: timers[k] * len(v) for k, v in ops.KERNEL_TIMERS.items()}
+    counts = {k: len(v) for k, v in ops.KERNEL_TIMERS.items()}
     ops.KERNEL_TIMERS = None
     rec = None
     if rank == 0:
@@ -373,7 +402,7 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                     "traffic": None, "flops_per_edge": fl}
         else:
-            roof = mace_roofline(model, g.num_nodes, g.num_edges, totals, n_timed)
+            roof = mace_roofline(model, g.num_nodes, g.num_edges, totals, counts, n_timed)
         t = pmc_traffic(workload, roof["kernel_prefix"])
         if t is not None:
             roof["traffic"], roof["traffic_source"] = t[0], f"profiles/{t[1]}"
