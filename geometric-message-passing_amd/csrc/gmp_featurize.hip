@@ -6,6 +6,11 @@
 //   edge_feats = RadialEmbeddingBlock(lengths) = BesselBasis * PolynomialCutoff      (nb)
 // (models/mace_modules/radial.py:44-46, 71-78; blocks.py:91-96).  Bessel weights and the
 // prefactor are read from the module buffers so the fp32 values match the reference exactly.
+// GVP-GNN (models/gvpgnn.py:106-112) takes the same radial block plus the unit vectors
+// nan_to_num(vectors / lengths) (unit_out; zero for a zero-length edge).
+// SchNet (models/schnet.py:66-68 over PyG 2.3.1 SchNet / GaussianSmearing / CFConv):
+//   edge_weight = |pos[row] - pos[col]|, edge_attr[k] = exp(coeff (d - offset[k])^2) and the
+//   CFConv cosine cutoff C = 0.5 (cos(d pi / cutoff) + 1), all from one read of pos per edge.
 #include "gmp_common.h"
 
 namespace gmp {
@@ -34,7 +39,7 @@ __device__ __forceinline__ void sh_l2(float x, float y, float z, float* Y) {
 __global__ void featurize_fwd_kernel(const float* __restrict__ pos, const int64_t* __restrict__ ei,
                                      int64_t E, int nb, FeatConsts c, float* __restrict__ vec_out,
                                      float* __restrict__ len_out, float* __restrict__ sh_out,
-                                     float* __restrict__ rad_out) {
+                                     float* __restrict__ rad_out, float* __restrict__ unit_out) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = ei[e], b = ei[E + e];
@@ -45,6 +50,12 @@ __global__ void featurize_fwd_kernel(const float* __restrict__ pos, const int64_
       vec_out[3 * e] = vx; vec_out[3 * e + 1] = vy; vec_out[3 * e + 2] = vz;
     }
     if (len_out) len_out[e] = r;
+    if (unit_out) {  // torch.nan_to_num(vectors / lengths): 0/0 -> 0
+      const bool z = !(r > 0.f);
+      unit_out[3 * e] = z ? 0.f : vx / r;
+      unit_out[3 * e + 1] = z ? 0.f : vy / r;
+      unit_out[3 * e + 2] = z ? 0.f : vz / r;
+    }
     if (sh_out) {
       const float inv = 1.f / fmaxf(r, 1e-12f);  // F.normalize(eps=1e-12)
       float Y[9];
@@ -67,7 +78,7 @@ __global__ void featurize_fwd_kernel(const float* __restrict__ pos, const int64_
 __global__ void featurize_bwd_kernel(const float* __restrict__ pos, const int64_t* __restrict__ ei,
                                      int64_t E, int nb, FeatConsts c,
                                      const float* __restrict__ g_sh, const float* __restrict__ g_rad,
-                                     float* __restrict__ g_vec) {
+                                     const float* __restrict__ g_unit, float* __restrict__ g_vec) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = ei[e], b = ei[E + e];
@@ -89,6 +100,14 @@ __global__ void featurize_bwd_kernel(const float* __restrict__ pos, const int64_
       gx += (ux - x * dot) * inv;
       gy += (uy - y * dot) * inv;
       gz += (uz - z * dot) * inv;
+    }
+    if (g_unit && r > 0.f) {  // u = v / |v|: dv = (du - u (u . du)) / |v|
+      const float x = vx / r, y = vy / r, z = vz / r;
+      const float ux = g_unit[3 * e], uy = g_unit[3 * e + 1], uz = g_unit[3 * e + 2];
+      const float dot = ux * x + uy * y + uz * z;
+      gx += (ux - x * dot) / r;
+      gy += (uy - y * dot) / r;
+      gz += (uz - z * dot) / r;
     }
     if (g_rad && r > 0.f) {
       const float u = r / c.r_max, p = c.p;
@@ -112,6 +131,91 @@ __global__ void featurize_bwd_kernel(const float* __restrict__ pos, const int64_
     g_vec[3 * e] = gx;
     g_vec[3 * e + 1] = gy;
     g_vec[3 * e + 2] = gz;
+  }
+}
+
+constexpr float kPi = 3.14159265358979323846f;
+
+// SchNet: dist, Gaussians (E, G) and the cosine cutoff per edge.  Offsets come from the
+// module's `offset` buffer (device); G <= kMaxGauss (PyG's default is 50).
+constexpr int kMaxGauss = 256;
+
+__device__ __forceinline__ float edge_dist(const float* __restrict__ pos, int64_t a, int64_t b,
+                                           float& vx, float& vy, float& vz) {
+  vx = pos[3 * a] - pos[3 * b];
+  vy = pos[3 * a + 1] - pos[3 * b + 1];
+  vz = pos[3 * a + 2] - pos[3 * b + 2];
+  return sqrtf(vx * vx + vy * vy + vz * vz);
+}
+
+// 256 threads = 4 waves; each wave takes 64 edges at a time: lane = edge for the scalars
+// (distance, cutoff), then the wave writes the (64, G) Gaussian block as one contiguous float
+// range (lane j: floats j, j + 64, ...; coalesced), reading the distances back from LDS.
+__global__ void __launch_bounds__(256) schnet_featurize_fwd_kernel(
+    const float* __restrict__ pos, const int64_t* __restrict__ ei, int64_t E, int G,
+    const float* __restrict__ offsets, float coeff, float cutoff, float* __restrict__ dist_out,
+    float* __restrict__ rbf_out, float* __restrict__ cut_out) {
+  __shared__ float off[kMaxGauss];
+  __shared__ float dsh[4][64];
+  for (int k = threadIdx.x; k < G; k += blockDim.x) off[k] = offsets[k];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t e0 = wave * 64; e0 < E; e0 += n_waves * 64) {
+    const int ne = (int)(E - e0 < 64 ? E - e0 : 64);
+    const int64_t e = e0 + lane;
+    if (lane < ne) {
+      float vx, vy, vz;
+      const float d = edge_dist(pos, ei[e], ei[E + e], vx, vy, vz);
+      dsh[wv][lane] = d;
+      if (dist_out) dist_out[e] = d;
+      if (cut_out) cut_out[e] = 0.5f * (cosf(d * kPi / cutoff) + 1.f);  // C (CFConv)
+    }
+    if (rbf_out) {
+      __builtin_amdgcn_wave_barrier();  // dsh[wv] is wave-private
+      float* out = rbf_out + e0 * G;
+      const int total = ne * G;
+      for (int i = lane; i < total; i += 64) {
+        const int el = i / G;
+        const float t = dsh[wv][el] - off[i - el * G];
+        out[i] = expf(coeff * (t * t));
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// g_d = g_dist + sum_k g_rbf[k] rbf[k] 2 coeff (d - off[k]) - g_cut 0.5 sin(d pi / c) pi / c
+// (k ascending); g_vec = g_d v / d, zero for a zero-length edge (torch's norm backward).
+// One thread per edge: the backward runs only when pos requires grad.
+__global__ void schnet_featurize_bwd_kernel(const float* __restrict__ pos,
+                                            const int64_t* __restrict__ ei, int64_t E, int G,
+                                            const float* __restrict__ offsets, float coeff,
+                                            float cutoff, const float* __restrict__ g_dist,
+                                            const float* __restrict__ g_rbf,
+                                            const float* __restrict__ g_cut,
+                                            float* __restrict__ g_vec) {
+  __shared__ float off[kMaxGauss];
+  for (int k = threadIdx.x; k < G; k += blockDim.x) off[k] = offsets[k];
+  __syncthreads();
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float vx, vy, vz;
+    const float d = edge_dist(pos, ei[e], ei[E + e], vx, vy, vz);
+    float gd = g_dist ? g_dist[e] : 0.f;
+    if (g_cut) gd -= g_cut[e] * 0.5f * sinf(d * kPi / cutoff) * (kPi / cutoff);
+    if (g_rbf) {
+      const float* g = g_rbf + e * G;
+      for (int k = 0; k < G; ++k) {
+        const float t = d - off[k];
+        gd += g[k] * expf(coeff * (t * t)) * (2.f * coeff * t);
+      }
+    }
+    const bool z = !(d > 0.f);
+    g_vec[3 * e] = z ? 0.f : gd * vx / d;
+    g_vec[3 * e + 1] = z ? 0.f : gd * vy / d;
+    g_vec[3 * e + 2] = z ? 0.f : gd * vz / d;
   }
 }
 
@@ -142,7 +246,7 @@ int gmp_edge_featurize_f32(const float* pos, const int64_t* edge_index, int64_t 
   c.r_max = r_max;
   c.p = p_cutoff;
   featurize_fwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
-      pos, edge_index, n_edges, num_bessel, c, vec_out, len_out, sh_out, radial_out);
+      pos, edge_index, n_edges, num_bessel, c, vec_out, len_out, sh_out, radial_out, nullptr);
   return launch_status();
 }
 
@@ -159,7 +263,66 @@ int gmp_edge_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int6
   c.r_max = r_max;
   c.p = p_cutoff;
   featurize_bwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
-      pos, edge_index, n_edges, num_bessel, c, g_sh, g_radial, g_vec);
+      pos, edge_index, n_edges, num_bessel, c, g_sh, g_radial, nullptr, g_vec);
+  return launch_status();
+}
+
+int gmp_edge_featurize_gvp_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                               int num_bessel, const float* bessel_weights, float prefactor,
+                               float r_max, float p_cutoff, float* len_out, float* radial_out,
+                               float* unit_out, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && num_bessel >= 0 && num_bessel <= kMaxBessel);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(pos && edge_index && (radial_out == nullptr || bessel_weights));
+  FeatConsts c{};
+  for (int n = 0; n < num_bessel && bessel_weights; ++n) c.w[n] = bessel_weights[n];
+  c.prefactor = prefactor;
+  c.r_max = r_max;
+  c.p = p_cutoff;
+  featurize_fwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, num_bessel, c, nullptr, len_out, nullptr, radial_out, unit_out);
+  return launch_status();
+}
+
+int gmp_edge_featurize_gvp_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                   int num_bessel, const float* bessel_weights, float prefactor,
+                                   float r_max, float p_cutoff, const float* g_radial,
+                                   const float* g_unit, float* g_vec, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && num_bessel >= 0 && num_bessel <= kMaxBessel);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(pos && edge_index && g_vec && (g_radial == nullptr || bessel_weights));
+  FeatConsts c{};
+  for (int n = 0; n < num_bessel && bessel_weights; ++n) c.w[n] = bessel_weights[n];
+  c.prefactor = prefactor;
+  c.r_max = r_max;
+  c.p = p_cutoff;
+  featurize_bwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, num_bessel, c, nullptr, g_radial, g_unit, g_vec);
+  return launch_status();
+}
+
+int gmp_schnet_featurize_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                             int num_gaussians, const float* offsets, float coeff, float cutoff,
+                             float* dist_out, float* rbf_out, float* cut_out, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && num_gaussians >= 0 && num_gaussians <= kMaxGauss);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(pos && edge_index && (rbf_out == nullptr || (offsets && num_gaussians > 0)));
+  schnet_featurize_fwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, num_gaussians, offsets, coeff, cutoff, dist_out, rbf_out,
+      cut_out);
+  return launch_status();
+}
+
+int gmp_schnet_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                 int num_gaussians, const float* offsets, float coeff,
+                                 float cutoff, const float* g_dist, const float* g_rbf,
+                                 const float* g_cut, float* g_vec, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && num_gaussians >= 0 && num_gaussians <= kMaxGauss);
+  if (n_edges == 0) return GMP_OK;
+  GMP_CHECK_ARG(pos && edge_index && g_vec && (g_rbf == nullptr || offsets));
+  schnet_featurize_bwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, num_gaussians, offsets, coeff, cutoff, g_dist, g_rbf, g_cut,
+      g_vec);
   return launch_status();
 }
 

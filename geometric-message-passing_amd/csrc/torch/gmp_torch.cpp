@@ -280,6 +280,65 @@ Tensor edge_featurize_bwd(const Tensor& pos, const Tensor& edge_index,
   return gv;
 }
 
+std::tuple<Tensor, Tensor> edge_featurize_gvp(const Tensor& pos, const Tensor& edge_index,
+                                              at::ArrayRef<double> bessel_w, double prefactor,
+                                              double r_max, double p) {
+  f32(pos, "pos");
+  i64(edge_index, "edge_index");
+  const int64_t E = edge_index.size(1), nb = (int64_t)bessel_w.size();
+  std::vector<float> w(bessel_w.begin(), bessel_w.end());
+  Tensor rad = at::empty({E, nb}, pos.options()), unit = at::empty({E, 3}, pos.options());
+  check_rc(gmp_edge_featurize_gvp_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(),
+                                      (float)prefactor, (float)r_max, (float)p, nullptr, fp(rad),
+                                      fp(unit), cur_stream()),
+           "gmp_edge_featurize_gvp_f32");
+  return {rad, unit};
+}
+
+Tensor edge_featurize_gvp_bwd(const Tensor& pos, const Tensor& edge_index,
+                              at::ArrayRef<double> bessel_w, double prefactor, double r_max,
+                              double p, const optional<Tensor>& g_rad,
+                              const optional<Tensor>& g_unit) {
+  f32(pos, "pos");
+  const int64_t E = edge_index.size(1), nb = (int64_t)bessel_w.size();
+  std::vector<float> w(bessel_w.begin(), bessel_w.end());
+  Tensor gv = at::empty({E, 3}, pos.options());
+  check_rc(gmp_edge_featurize_gvp_bwd_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(),
+                                          (float)prefactor, (float)r_max, (float)p, cfp(g_rad),
+                                          cfp(g_unit), fp(gv), cur_stream()),
+           "gmp_edge_featurize_gvp_bwd_f32");
+  return gv;
+}
+
+std::tuple<Tensor, Tensor, Tensor> schnet_featurize(const Tensor& pos, const Tensor& edge_index,
+                                                    const Tensor& offsets, double coeff,
+                                                    double cutoff) {
+  f32(pos, "pos");
+  i64(edge_index, "edge_index");
+  f32(offsets, "offsets");
+  const int64_t E = edge_index.size(1), G = offsets.numel();
+  Tensor d = at::empty({E}, pos.options()), rbf = at::empty({E, G}, pos.options()),
+         cut = at::empty({E}, pos.options());
+  check_rc(gmp_schnet_featurize_f32(fp(pos), ip(edge_index), E, (int)G, fp(offsets),
+                                    (float)coeff, (float)cutoff, fp(d), fp(rbf), fp(cut),
+                                    cur_stream()),
+           "gmp_schnet_featurize_f32");
+  return {d, rbf, cut};
+}
+
+Tensor schnet_featurize_bwd(const Tensor& pos, const Tensor& edge_index, const Tensor& offsets,
+                            double coeff, double cutoff, const optional<Tensor>& g_dist,
+                            const optional<Tensor>& g_rbf, const optional<Tensor>& g_cut) {
+  f32(pos, "pos");
+  const int64_t E = edge_index.size(1), G = offsets.numel();
+  Tensor gv = at::empty({E, 3}, pos.options());
+  check_rc(gmp_schnet_featurize_bwd_f32(fp(pos), ip(edge_index), E, (int)G, fp(offsets),
+                                        (float)coeff, (float)cutoff, cfp(g_dist), cfp(g_rbf),
+                                        cfp(g_cut), fp(gv), cur_stream()),
+           "gmp_schnet_featurize_bwd_f32");
+  return gv;
+}
+
 // ------------------------------------------------------------------ K8 symmetric contraction
 Tensor symmetric_contraction_fwd(const Tensor& x, int64_t corr, const Tensor& A1,
                                  const optional<Tensor>& A2, const optional<Tensor>& A3) {
@@ -463,6 +522,26 @@ Tensor edge_featurize_bwd(const Tensor& pos, const Tensor& ei, at::ArrayRef<doub
                           double, double, const optional<Tensor>&, const optional<Tensor>&) {
   return at::empty({ei.size(1), 3}, pos.options());
 }
+std::tuple<Tensor, Tensor> edge_featurize_gvp(const Tensor& pos, const Tensor& ei,
+                                              at::ArrayRef<double> w, double, double, double) {
+  return {at::empty({ei.size(1), (int64_t)w.size()}, pos.options()),
+          at::empty({ei.size(1), 3}, pos.options())};
+}
+Tensor edge_featurize_gvp_bwd(const Tensor& pos, const Tensor& ei, at::ArrayRef<double>, double,
+                              double, double, const optional<Tensor>&, const optional<Tensor>&) {
+  return at::empty({ei.size(1), 3}, pos.options());
+}
+std::tuple<Tensor, Tensor, Tensor> schnet_featurize(const Tensor& pos, const Tensor& ei,
+                                                    const Tensor& offsets, double, double) {
+  const int64_t E = ei.size(1);
+  return {at::empty({E}, pos.options()), at::empty({E, offsets.numel()}, pos.options()),
+          at::empty({E}, pos.options())};
+}
+Tensor schnet_featurize_bwd(const Tensor& pos, const Tensor& ei, const Tensor&, double, double,
+                            const optional<Tensor>&, const optional<Tensor>&,
+                            const optional<Tensor>&) {
+  return at::empty({ei.size(1), 3}, pos.options());
+}
 Tensor symmetric_contraction_fwd(const Tensor& x, int64_t, const Tensor&, const optional<Tensor>&,
                                  const optional<Tensor>&) {
   return at::empty({x.size(0), 9 * x.size(1)}, x.options());
@@ -528,6 +607,14 @@ TORCH_LIBRARY(gmp, m) {
         "float r_max, float p) -> (Tensor sh, Tensor radial)");
   m.def("edge_featurize_bwd(Tensor pos, Tensor edge_index, float[] bessel_weights, "
         "float prefactor, float r_max, float p, Tensor? g_sh, Tensor? g_radial) -> Tensor");
+  m.def("edge_featurize_gvp(Tensor pos, Tensor edge_index, float[] bessel_weights, "
+        "float prefactor, float r_max, float p) -> (Tensor radial, Tensor unit)");
+  m.def("edge_featurize_gvp_bwd(Tensor pos, Tensor edge_index, float[] bessel_weights, "
+        "float prefactor, float r_max, float p, Tensor? g_radial, Tensor? g_unit) -> Tensor");
+  m.def("schnet_featurize(Tensor pos, Tensor edge_index, Tensor offsets, float coeff, "
+        "float cutoff) -> (Tensor dist, Tensor rbf, Tensor cut)");
+  m.def("schnet_featurize_bwd(Tensor pos, Tensor edge_index, Tensor offsets, float coeff, "
+        "float cutoff, Tensor? g_dist, Tensor? g_rbf, Tensor? g_cut) -> Tensor");
   m.def("symmetric_contraction_fwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
         "Tensor? A3) -> Tensor");
   m.def("symmetric_contraction_bwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
@@ -559,6 +646,10 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("ln_act_bwd", ns ln_act_bwd);                                    \
   m.impl("edge_featurize", ns edge_featurize);                            \
   m.impl("edge_featurize_bwd", ns edge_featurize_bwd);                    \
+  m.impl("edge_featurize_gvp", ns edge_featurize_gvp);                    \
+  m.impl("edge_featurize_gvp_bwd", ns edge_featurize_gvp_bwd);            \
+  m.impl("schnet_featurize", ns schnet_featurize);                        \
+  m.impl("schnet_featurize_bwd", ns schnet_featurize_bwd);                \
   m.impl("symmetric_contraction_fwd", ns symmetric_contraction_fwd);      \
   m.impl("symmetric_contraction_bwd", ns symmetric_contraction_bwd);      \
   m.impl("tp_node_outer", ns tp_node_outer);                              \

@@ -78,6 +78,14 @@ SIGNATURES = {
                                        c_vp, c_vp, c_vp, c_vp]),
     "gmp_edge_featurize_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32,
                                            c_vp, c_vp, c_vp, c_vp]),
+    "gmp_edge_featurize_gvp_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32,
+                                           c_vp, c_vp, c_vp, c_vp]),
+    "gmp_edge_featurize_gvp_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32,
+                                               c_f32, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_schnet_featurize_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_vp, c_vp,
+                                         c_vp, c_vp]),
+    "gmp_schnet_featurize_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_vp,
+                                             c_vp, c_vp, c_vp, c_vp]),
     "gmp_tp_conv_fwd_f32": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                     c_i64, c_i64, c_vp, c_vp]),
     "gmp_tp_conv_bwd_f32": (c_int, [c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,

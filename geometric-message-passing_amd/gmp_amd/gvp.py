@@ -559,11 +559,10 @@ class GVPGNNModel(nn.Module):
 
     def forward(self, batch):
         ei = batch.edge_index
-        vectors = ops.gather(batch.pos, ei[0], 0) - ops.gather(batch.pos, ei[1], 0)
-        lengths = torch.linalg.norm(vectors, dim=-1, keepdim=True)
+        # K1: radial embedding of |vec| and nan_to_num(vec / |vec|) in one pass (gvpgnn.py:106-112)
+        rad, unit = ops.GvpEdgeFeaturizeFn.apply(batch.pos, ei, self.radial_embedding._host)
         h_V = ops.gather(self.emb_in.weight, batch.atoms, 0)
-        h_E = (self.radial_embedding(lengths),
-               torch.nan_to_num(torch.div(vectors, lengths)).unsqueeze_(-2))
+        h_E = (rad, unit.unsqueeze(-2))
         h_V = self.W_v(h_V)
         h_E = self.W_e(h_E)
         for layer in self.layers:

@@ -677,6 +677,72 @@ def cfconv_propagate(edge_index, x, W):
     return CFConvAggregateFn.apply(x, W, ei[0], ei[1], x.shape[0])
 
 
+# ----------------------------------------------------------------------------------- K1 edges
+def edge_vec_to_pos_grad(g_vec, edge_index, n):
+    """d pos from d vec for vec = pos[ei0] - pos[ei1]: deterministic segmented sums over the
+    cached CSRs of ei0 (+) and ei1 (-)."""
+    plus, _ = segment_reduce(g_vec, get_csr(edge_index[0], n), "sum")
+    minus, _ = segment_reduce(g_vec, get_csr(edge_index[1], n), "sum")
+    return plus - minus
+
+
+class GvpEdgeFeaturizeFn(torch.autograd.Function):
+    """GVP-GNN edge features (gvpgnn.py:106-112) in one pass over the edges (K1,
+    gmp_edge_featurize_gvp_f32): (radial (E, nb), unit vectors nan_to_num(vec / |vec|) (E, 3))."""
+
+    @staticmethod
+    def forward(ctx, pos, edge_index, host_consts):
+        w, pref, r_max, p = host_consts
+        pos, ei = _f32c(pos), _i64c(edge_index)
+        _need_cuda(pos, ei)
+        with _timed("edge_featurize"):
+            rad, unit = _lib.torch_ops().edge_featurize_gvp(pos, ei, [float(v) for v in w], pref,
+                                                            r_max, p)
+        ctx.save_for_backward(pos, ei)
+        ctx.host = host_consts
+        return rad, unit
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g_rad, g_unit):
+        if not ctx.needs_input_grad[0]:
+            return None, None, None
+        pos, ei = ctx.saved_tensors
+        w, pref, r_max, p = ctx.host
+        g_vec = _lib.torch_ops().edge_featurize_gvp_bwd(
+            pos, ei, [float(v) for v in w], pref, r_max, p,
+            _f32c(g_rad) if g_rad is not None else None,
+            _f32c(g_unit) if g_unit is not None else None)
+        return edge_vec_to_pos_grad(g_vec, ei, pos.shape[0]), None, None
+
+
+class SchNetFeaturizeFn(torch.autograd.Function):
+    """SchNet edge features (schnet.py:66-68 over PyG SchNet.forward / GaussianSmearing /
+    CFConv.forward) in one pass over the edges (gmp_schnet_featurize_f32): edge_weight (E),
+    Gaussians (E, G) and the CFConv cosine cutoff C (E)."""
+
+    @staticmethod
+    def forward(ctx, pos, edge_index, offsets, coeff, cutoff):
+        pos, ei, off = _f32c(pos), _i64c(edge_index), _f32c(offsets)
+        _need_cuda(pos, ei, off)
+        with _timed("edge_featurize"):
+            d, rbf, cut = _lib.torch_ops().schnet_featurize(pos, ei, off, float(coeff),
+                                                            float(cutoff))
+        ctx.save_for_backward(pos, ei, off)
+        ctx.coeff, ctx.cutoff = float(coeff), float(cutoff)
+        return d, rbf, cut
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g_d, g_rbf, g_cut):
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None, None
+        pos, ei, off = ctx.saved_tensors
+        opt = [_f32c(t) if t is not None else None for t in (g_d, g_rbf, g_cut)]
+        g_vec = _lib.torch_ops().schnet_featurize_bwd(pos, ei, off, ctx.coeff, ctx.cutoff, *opt)
+        return edge_vec_to_pos_grad(g_vec, ei, pos.shape[0]), None, None, None, None
+
+
 # ----------------------------------------------------------------------------------- EGNN
 class EgnnGraph:
     """Receiver-sorted view of an edge_index for the fused EGNN kernels (built on device)."""

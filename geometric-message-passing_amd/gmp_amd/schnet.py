@@ -53,8 +53,13 @@ class CFConv(MessagePassing):
         self.nn = nn_module
         self.cutoff = cutoff
 
-    def forward(self, x, edge_index, edge_weight, edge_attr):
-        C = 0.5 * (torch.cos(edge_weight * math.pi / self.cutoff) + 1.0)
+    def forward(self, x, edge_index, edge_weight, edge_attr, edge_cut=None):
+        """edge_cut: the cosine cutoff C of edge_weight when the caller already has it
+        (SchNetModel computes it once per graph in the featurisation kernel)."""
+        if edge_cut is None:
+            C = 0.5 * (torch.cos(edge_weight * math.pi / self.cutoff) + 1.0)
+        else:
+            C = edge_cut
         W = self._filter(edge_attr) * C.view(-1, 1)
         x = self.lin1(x)
         x = self.propagate(edge_index, x=x, W=W)
@@ -92,8 +97,8 @@ class InteractionBlock(nn.Module):
         self.act = ShiftedSoftplus()
         self.lin = nn.Linear(hidden_channels, hidden_channels)
 
-    def forward(self, x, edge_index, edge_weight, edge_attr):
-        x = self.conv(x, edge_index, edge_weight, edge_attr)
+    def forward(self, x, edge_index, edge_weight, edge_attr, edge_cut=None):
+        x = self.conv(x, edge_index, edge_weight, edge_attr, edge_cut)
         return self.lin(self.act(x))
 
 
@@ -121,10 +126,15 @@ class SchNetModel(nn.Module):
         if pad is not None:  # nn.Embedding(padding_idx): that row receives no gradient
             w = torch.cat([w[:pad], w[pad:pad + 1].detach(), w[pad + 1:]], 0)
         h = ops.gather(w, batch.atoms, 0)
-        row, col = batch.edge_index
-        edge_weight = (ops.gather(batch.pos, row, 0) - ops.gather(batch.pos, col, 0)).norm(dim=-1)
-        edge_attr = self.distance_expansion(edge_weight)
+        # edge_weight, Gaussians and the cosine cutoff from one pass over the edges (K1,
+        # gmp_schnet_featurize_f32); the cutoff is computed once and shared by every CFConv
+        ds = self.distance_expansion
+        edge_weight, edge_attr, C = ops.SchNetFeaturizeFn.apply(
+            batch.pos, batch.edge_index, ds.offset, ds.coeff, self.cutoff)
+        if not all(isinstance(i.conv, CFConv) and i.conv.cutoff == self.cutoff
+                   for i in self.interactions):
+            C = None
         for interaction in self.interactions:
-            h = h + interaction(h, batch.edge_index, edge_weight, edge_attr)
+            h = h + interaction(h, batch.edge_index, edge_weight, edge_attr, C)
         out = self.pool(h, batch.batch, getattr(batch, "num_graphs", None))
         return self.lin2(self.act(self.lin1(out)))

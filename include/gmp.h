@@ -223,6 +223,29 @@ int gmp_edge_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int6
                                int num_bessel, const float* bessel_weights, float prefactor,
                                float r_max, float p_cutoff, const float* g_sh,
                                const float* g_radial, float* g_vec, void* stream);
+/* GVP-GNN edge features (models/gvpgnn.py:106-112): len (E), radial (E,nb) as above and the unit
+ * vectors nan_to_num(vec / len) (E,3; zero rows for zero-length edges).  Backward from g_radial /
+ * g_unit (either may be NULL) to g_vec. */
+int gmp_edge_featurize_gvp_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                               int num_bessel, const float* bessel_weights, float prefactor,
+                               float r_max, float p_cutoff, float* len_out, float* radial_out,
+                               float* unit_out, void* stream);
+int gmp_edge_featurize_gvp_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                   int num_bessel, const float* bessel_weights, float prefactor,
+                                   float r_max, float p_cutoff, const float* g_radial,
+                                   const float* g_unit, float* g_vec, void* stream);
+/* SchNet edge features (models/schnet.py:66-68; PyG 2.3.1 SchNet.forward, GaussianSmearing,
+ * CFConv.forward): dist = |pos[row] - pos[col]| (E), rbf[e, k] = exp(coeff (dist - offsets[k])^2)
+ * (E,G), cut = 0.5 (cos(dist pi / cutoff) + 1) (E).  `offsets` is the module's DEVICE buffer
+ * (G <= 256).  Any output may be NULL.  Backward: g_vec (E,3) from g_dist / g_rbf / g_cut (any
+ * may be NULL); the caller scatters g_vec to pos[row] (+) and pos[col] (-). */
+int gmp_schnet_featurize_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                             int num_gaussians, const float* offsets, float coeff, float cutoff,
+                             float* dist_out, float* rbf_out, float* cut_out, void* stream);
+int gmp_schnet_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                 int num_gaussians, const float* offsets, float coeff,
+                                 float cutoff, const float* g_dist, const float* g_rbf,
+                                 const float* g_cut, float* g_vec, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K7 tensor-product convolution messages (models/layers/tfn_layer.py:82-86): e3nn

@@ -126,7 +126,14 @@ def test_gvp_model_c3_vs_oracle():
     assert err <= 1e-5 * max(1.0, y64.abs().max().item()) + 2 * err_ref, (err, err_ref)
     y.sum().backward()
     yr.sum().backward()
-    _scaled(pd.grad, pr.grad, 2e-4, "grad_pos")
+    # d pos near r_max: the polynomial envelope's derivative is a cancellation of O(100) terms
+    # in fp32 (both sides); judged against fp64 with the fp32 reference's own error as slack
+    p64 = gr.pos.double().requires_grad_(True)
+    ref64(Batch(gr.atoms, p64, gr.edge_index)).sum().backward()
+    eg = (pd.grad.cpu().double() - p64.grad).abs().max().item()
+    eg_ref = (pr.grad.double() - p64.grad).abs().max().item()
+    scale = p64.grad.abs().max().item()
+    assert eg <= 2e-4 * scale + 2 * eg_ref, (eg, eg_ref, scale)
 
 
 @pytest.mark.parametrize("m,n,K", [(128, 144, 7777), (128, 65, 3000), (16, 128, 5000),
@@ -166,3 +173,37 @@ def test_gvp_fused_deterministic_and_model_c3():
     a1, a2 = run(), run()
     for u, v in zip(a1, a2):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("E", [30000, 77, 0])
+def test_gvp_edge_featurize_vs_oracle(E):
+    """K1 GVP featurisation (gmp_edge_featurize_gvp_f32 + backward) against gvpgnn.py:106-112
+    restated on the CPU: RadialEmbeddingBlock(|vec|) and nan_to_num(vec / |vec|); a zero-length
+    edge gives a zero unit vector.  Tolerance 1e-5; d pos within 1e-5 of scale."""
+    from gmp_amd import ops
+    from gmp_amd.equivariant import RadialEmbeddingBlock
+    from oracle.radial import RadialEmbeddingBlock as ORadial
+    gen = torch.Generator().manual_seed(E + 1)
+    n = max(E // 20, 4)
+    pos = torch.rand(n, 3, generator=gen) * 12.0
+    src = torch.randint(0, n, (E,), generator=gen)  # no self-loops: radial(0) is 0/0 upstream
+    ei = torch.stack([src, (src + torch.randint(1, n, (E,), generator=gen)) % n])
+    rad_p, rad_o = RadialEmbeddingBlock(10.0, 8, 5), ORadial(10.0, 8, 5)
+    pd = pos.to(DEV).requires_grad_(True)
+    rad, unit = ops.GvpEdgeFeaturizeFn.apply(pd, ei.to(DEV), rad_p._host)
+    pr = pos.clone().requires_grad_(True)
+    vec = pr[ei[0]] - pr[ei[1]]
+    ln = torch.linalg.norm(vec, dim=-1, keepdim=True)
+    rr, ur = rad_o(ln), torch.nan_to_num(torch.div(vec, ln))
+    torch.testing.assert_close(rad.detach().cpu(), rr.detach(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(unit.detach().cpu(), ur.detach(), atol=1e-6, rtol=1e-5)
+    if E == 0:
+        return
+    g1, g2 = torch.randn_like(rr), torch.randn_like(ur)
+    ((rad * g1.to(DEV)).sum() + (unit * g2.to(DEV)).sum()).backward()
+    ((rr * g1).sum() + (ur * g2).sum()).backward()
+    _scaled(pd.grad, pr.grad, 1e-5, "dpos")
+    # a zero-length edge: zero unit vector
+    z = torch.tensor([[1, 2], [1, 0]], device=DEV)
+    _, u0 = ops.GvpEdgeFeaturizeFn.apply(pos.to(DEV), z, rad_p._host)
+    assert torch.equal(u0[0].cpu(), torch.zeros(3))

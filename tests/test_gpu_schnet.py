@@ -2,6 +2,8 @@
 SchNet (oracle/schnet.py; parity unpinned against PyG itself, which is absent).  Config C1:
 hidden 64, 128 filters, 50 Gaussians, cutoff 10, 4 interactions on the k-chains graphs; plus a
 random radius graph.  Tolerance 1e-5 on outputs, 1e-4 of scale on gradients."""
+import math
+
 import pytest
 import torch
 
@@ -110,3 +112,33 @@ def test_shifted_softplus_vs_torch():
     yr.backward(g)
     torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-6, rtol=1e-5)
     torch.testing.assert_close(xd.grad.cpu(), xr.grad, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("E,G,cutoff", [(20000, 50, 10.0), (333, 7, 4.0), (0, 50, 10.0)])
+def test_schnet_featurize_vs_oracle(E, G, cutoff):
+    """K1 SchNet featurisation (gmp_schnet_featurize_f32 and its backward) against the CPU
+    restatement (oracle/schnet.py: |pos[row] - pos[col]|, GaussianSmearing, CFConv's cosine
+    cutoff), including a zero-length edge (gradient 0, as torch's norm backward) and edges past
+    the cutoff.  Tolerance 1e-5 on the features, 1e-5 of scale on d pos."""
+    from gmp_amd import ops
+    gen = torch.Generator().manual_seed(E + G)
+    n = max(E // 20, 4)
+    pos = torch.rand(n, 3, generator=gen) * 1.5 * cutoff
+    ei = torch.randint(0, n, (2, E), generator=gen)
+    if E:
+        ei[:, 0] = 3  # a zero-length edge
+    gs = osch.GaussianSmearing(0.0, cutoff, G)
+    pd = pos.to(DEV).requires_grad_(True)
+    d, rbf, C = ops.SchNetFeaturizeFn.apply(pd, ei.to(DEV), gs.offset.to(DEV), gs.coeff, cutoff)
+    pr = pos.clone().requires_grad_(True)
+    dr = (pr[ei[0]] - pr[ei[1]]).norm(dim=-1)
+    rbfr = gs(dr)
+    Cr = 0.5 * (torch.cos(dr * math.pi / cutoff) + 1.0)
+    for a, b in ((d, dr), (rbf, rbfr), (C, Cr)):
+        torch.testing.assert_close(a.detach().cpu(), b.detach(), atol=1e-5, rtol=1e-5)
+    if E == 0:
+        return
+    g1, g2, g3 = torch.randn_like(dr), torch.randn_like(rbfr), torch.randn_like(Cr)
+    ((d * g1.to(DEV)).sum() + (rbf * g2.to(DEV)).sum() + (C * g3.to(DEV)).sum()).backward()
+    ((dr * g1).sum() + (rbfr * g2).sum() + (Cr * g3).sum()).backward()
+    _scaled(pd.grad, pr.grad, 1e-5, "dpos")
