@@ -339,6 +339,72 @@ Tensor schnet_featurize_bwd(const Tensor& pos, const Tensor& edge_index, const T
   return gv;
 }
 
+// ------------------------------------------------------------------ K16 Gate / BatchNorm
+Tensor gate_fwd(const Tensor& x, const Tensor& out_map, double c_act, double c_gate) {
+  f32(x, "x");
+  const int64_t B = x.size(0), c_in = x.size(1), c_out = out_map.size(0);
+  Tensor y = at::empty({B, c_out}, x.options());
+  check_rc(gmp_gate_fwd_f32(B, (int)c_in, (int)c_out, out_map.data_ptr<int32_t>(), (float)c_act,
+                            (float)c_gate, fp(x), fp(y), cur_stream()),
+           "gmp_gate_fwd_f32");
+  return y;
+}
+
+Tensor gate_bwd(const Tensor& x, const Tensor& grad_y, const Tensor& in_map, double c_act,
+                double c_gate) {
+  f32(x, "x");
+  f32(grad_y, "grad_y");
+  const int64_t B = x.size(0), c_in = x.size(1), c_out = grad_y.size(1);
+  Tensor gx = at::empty_like(x);
+  check_rc(gmp_gate_bwd_f32(B, (int)c_in, (int)c_out, in_map.data_ptr<int32_t>(), (float)c_act,
+                            (float)c_gate, fp(x), fp(grad_y), fp(gx), cur_stream()),
+           "gmp_gate_bwd_f32");
+  return gx;
+}
+
+std::tuple<Tensor, Tensor, Tensor> irreps_bn_fwd(const Tensor& x, const Tensor& col_chan,
+                                                 const Tensor& chan_col, const Tensor& chan_info,
+                                                 const Tensor& weight,
+                                                 const optional<Tensor>& bias,
+                                                 Tensor running_mean, Tensor running_var,
+                                                 bool training, double momentum, double eps) {
+  f32(x, "x");
+  const int64_t B = x.size(0), C = x.size(1), nf = chan_col.size(0);
+  Tensor y = at::empty_like(x), shift = at::empty({nf}, x.options()),
+         invstd = at::empty({nf}, x.options());
+  const size_t ws_b = gmp_irreps_bn_workspace_size(B, (int)C, (int)nf);
+  Tensor ws = at::empty({(int64_t)ws_b}, x.options().dtype(at::kByte));
+  check_rc(gmp_irreps_bn_fwd_f32(B, (int)C, (int)nf, col_chan.data_ptr<int32_t>(),
+                                 chan_col.data_ptr<int32_t>(), chan_info.data_ptr<int32_t>(),
+                                 fp(x), fp(weight), cfp(bias), fp(running_mean), fp(running_var),
+                                 training ? 1 : 0, (float)momentum, (float)eps, fp(y), fp(shift),
+                                 fp(invstd), ws.data_ptr(), ws_b, cur_stream()),
+           "gmp_irreps_bn_fwd_f32");
+  return {y, shift, invstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor& grad_y,
+                                                 const Tensor& col_chan, const Tensor& chan_col,
+                                                 const Tensor& chan_info, const Tensor& weight,
+                                                 const Tensor& shift, const Tensor& invstd,
+                                                 bool training, int64_t n_scalar) {
+  f32(x, "x");
+  f32(grad_y, "grad_y");
+  const int64_t B = x.size(0), C = x.size(1), nf = chan_col.size(0);
+  Tensor gx = at::empty_like(x), gw = at::empty({nf}, x.options()),
+         gb = at::empty({n_scalar}, x.options());
+  const size_t ws_b = gmp_irreps_bn_workspace_size(B, (int)C, (int)nf);
+  Tensor ws = at::empty({(int64_t)ws_b}, x.options().dtype(at::kByte));
+  check_rc(gmp_irreps_bn_bwd_f32(B, (int)C, (int)nf, col_chan.data_ptr<int32_t>(),
+                                 chan_col.data_ptr<int32_t>(), chan_info.data_ptr<int32_t>(),
+                                 fp(x), fp(grad_y), fp(weight), fp(shift), fp(invstd),
+                                 training ? 1 : 0, fp(gx), fp(gw),
+                                 n_scalar > 0 ? fp(gb) : nullptr, ws.data_ptr(), ws_b,
+                                 cur_stream()),
+           "gmp_irreps_bn_bwd_f32");
+  return {gx, gw, gb};
+}
+
 // ------------------------------------------------------------------ K8 symmetric contraction
 Tensor symmetric_contraction_fwd(const Tensor& x, int64_t corr, const Tensor& A1,
                                  const optional<Tensor>& A2, const optional<Tensor>& A3) {
@@ -542,6 +608,26 @@ Tensor schnet_featurize_bwd(const Tensor& pos, const Tensor& ei, const Tensor&, 
                             const optional<Tensor>&) {
   return at::empty({ei.size(1), 3}, pos.options());
 }
+Tensor gate_fwd(const Tensor& x, const Tensor& out_map, double, double) {
+  return at::empty({x.size(0), out_map.size(0)}, x.options());
+}
+Tensor gate_bwd(const Tensor& x, const Tensor&, const Tensor&, double, double) {
+  return at::empty_like(x);
+}
+std::tuple<Tensor, Tensor, Tensor> irreps_bn_fwd(const Tensor& x, const Tensor&,
+                                                 const Tensor& chan_col, const Tensor&,
+                                                 const Tensor&, const optional<Tensor>&, Tensor,
+                                                 Tensor, bool, double, double) {
+  const int64_t nf = chan_col.size(0);
+  return {at::empty_like(x), at::empty({nf}, x.options()), at::empty({nf}, x.options())};
+}
+std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor&, const Tensor&,
+                                                 const Tensor& chan_col, const Tensor&,
+                                                 const Tensor&, const Tensor&, const Tensor&,
+                                                 bool, int64_t n_scalar) {
+  return {at::empty_like(x), at::empty({chan_col.size(0)}, x.options()),
+          at::empty({n_scalar}, x.options())};
+}
 Tensor symmetric_contraction_fwd(const Tensor& x, int64_t, const Tensor&, const optional<Tensor>&,
                                  const optional<Tensor>&) {
   return at::empty({x.size(0), 9 * x.size(1)}, x.options());
@@ -615,6 +701,14 @@ TORCH_LIBRARY(gmp, m) {
         "float cutoff) -> (Tensor dist, Tensor rbf, Tensor cut)");
   m.def("schnet_featurize_bwd(Tensor pos, Tensor edge_index, Tensor offsets, float coeff, "
         "float cutoff, Tensor? g_dist, Tensor? g_rbf, Tensor? g_cut) -> Tensor");
+  m.def("gate_fwd(Tensor x, Tensor out_map, float c_act, float c_gate) -> Tensor");
+  m.def("gate_bwd(Tensor x, Tensor grad_y, Tensor in_map, float c_act, float c_gate) -> Tensor");
+  m.def("irreps_bn_fwd(Tensor x, Tensor col_chan, Tensor chan_col, Tensor chan_info, "
+        "Tensor weight, Tensor? bias, Tensor(a!) running_mean, Tensor(b!) running_var, "
+        "bool training, float momentum, float eps) -> (Tensor y, Tensor shift, Tensor invstd)");
+  m.def("irreps_bn_bwd(Tensor x, Tensor grad_y, Tensor col_chan, Tensor chan_col, "
+        "Tensor chan_info, Tensor weight, Tensor shift, Tensor invstd, bool training, "
+        "int n_scalar) -> (Tensor grad_x, Tensor grad_weight, Tensor grad_bias)");
   m.def("symmetric_contraction_fwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
         "Tensor? A3) -> Tensor");
   m.def("symmetric_contraction_bwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
@@ -650,6 +744,10 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("edge_featurize_gvp_bwd", ns edge_featurize_gvp_bwd);            \
   m.impl("schnet_featurize", ns schnet_featurize);                        \
   m.impl("schnet_featurize_bwd", ns schnet_featurize_bwd);                \
+  m.impl("gate_fwd", ns gate_fwd);                                        \
+  m.impl("gate_bwd", ns gate_bwd);                                        \
+  m.impl("irreps_bn_fwd", ns irreps_bn_fwd);                              \
+  m.impl("irreps_bn_bwd", ns irreps_bn_bwd);                              \
   m.impl("symmetric_contraction_fwd", ns symmetric_contraction_fwd);      \
   m.impl("symmetric_contraction_bwd", ns symmetric_contraction_bwd);      \
   m.impl("tp_node_outer", ns tp_node_outer);                              \

@@ -82,6 +82,16 @@ SIGNATURES = {
                                            c_vp, c_vp, c_vp, c_vp]),
     "gmp_edge_featurize_gvp_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32,
                                                c_f32, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_gate_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp]),
+    "gmp_gate_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
+                                 c_vp]),
+    "gmp_irreps_bn_workspace_size": (c_size, [c_i64, c_int, c_int]),
+    "gmp_irreps_bn_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp,
+                                      c_size, c_vp]),
+    "gmp_irreps_bn_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_size,
+                                      c_vp]),
     "gmp_schnet_featurize_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_vp, c_vp,
                                          c_vp, c_vp]),
     "gmp_schnet_featurize_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_vp,

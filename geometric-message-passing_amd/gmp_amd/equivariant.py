@@ -159,8 +159,46 @@ class Linear(nn.Module):
         return torch.cat(outs, dim=1)
 
 
+def _dev_table(cache, key_fn, device):
+    t = cache.get(device)
+    if t is None:
+        t = tuple(v.to(device) for v in key_fn())
+        cache[device] = t
+    return t
+
+
+class IrrepsBatchNormFn(torch.autograd.Function):
+    """K16 e3nn BatchNorm (gmp_irreps_bn_{fwd,bwd}_f32): two fixed-order statistics passes and
+    one apply pass forward (running stats updated in place when training), one statistics and
+    one apply pass backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, tables, running_mean, running_var, training, momentum,
+                eps):
+        col_chan, chan_col, chan_info = tables
+        y, shift, invstd = _lib.torch_ops().irreps_bn_fwd(
+            x, col_chan, chan_col, chan_info, weight, bias if bias.numel() else None,
+            running_mean, running_var, bool(training), float(momentum), float(eps))
+        ctx.save_for_backward(x, weight, shift, invstd)
+        ctx.tables, ctx.training, ctx.n_scalar = tables, bool(training), bias.numel()
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        x, weight, shift, invstd = ctx.saved_tensors
+        col_chan, chan_col, chan_info = ctx.tables
+        gx, gw, gb = _lib.torch_ops().irreps_bn_bwd(x, _f32c(gy), col_chan, chan_col, chan_info,
+                                                   weight, shift, invstd, ctx.training,
+                                                   ctx.n_scalar)
+        return gx, gw, gb, None, None, None, None, None, None
+
+
 class BatchNorm(nn.Module):
-    """e3nn nn.BatchNorm(irreps) (eps 1e-5, momentum 0.1, affine, reduce mean, component)."""
+    """e3nn nn.BatchNorm(irreps) (eps 1e-5, momentum 0.1, affine, reduce mean, component) as the
+    fused HIP kernels K16 (tfn_layer.py:89-90; e3nn 0.5 nn/_batchnorm.py semantics): scalars
+    (0e) centred by the batch mean, every channel scaled by weight (mean f^2 + eps)^-1/2,
+    scalars + bias; running_mean / running_var updated with momentum in training."""
 
     def __init__(self, irreps, eps=1e-5, momentum=0.1):
         super().__init__()
@@ -172,49 +210,55 @@ class BatchNorm(nn.Module):
         self.register_buffer("running_var", torch.ones(nf))
         self.weight = nn.Parameter(torch.ones(nf))
         self.bias = nn.Parameter(torch.zeros(ns))
+        self._tables = {}
 
-    def forward(self, x):
-        B = x.shape[0]
-        fields, new_means, new_vars = [], [], []
-        ix = irm = irv = iw = ib = 0
+    def _host_tables(self):
+        col_chan, chan_col, chan_info = [], [], []
+        u = si = col = 0
         for mul, (l, p) in self.irreps:
             d = 2 * l + 1
-            f = x[:, ix:ix + mul * d].reshape(B, mul, d)
-            ix += mul * d
             scalar = (l == 0 and p == 1)
-            if scalar:
-                if self.training:
-                    mean = f.mean(dim=(0, 2))
-                    new_means.append((1 - self.momentum) * self.running_mean[irm:irm + mul]
-                                     + self.momentum * mean.detach())
-                else:
-                    mean = self.running_mean[irm:irm + mul]
-                irm += mul
-                f = f - mean.view(1, mul, 1)
-            if self.training:
-                norm = f.pow(2).mean(2).mean(0)
-                new_vars.append((1 - self.momentum) * self.running_var[irv:irv + mul]
-                                + self.momentum * norm.detach())
-            else:
-                norm = self.running_var[irv:irv + mul]
-            irv += mul
-            scale = (norm + self.eps).pow(-0.5) * self.weight[iw:iw + mul]
-            iw += mul
-            f = f * scale.view(1, mul, 1)
-            if scalar:
-                f = f + self.bias[ib:ib + mul].view(1, mul, 1)
-                ib += mul
-            fields.append(f.reshape(B, mul * d))
-        if self.training:
-            with torch.no_grad():
-                if new_means:
-                    self.running_mean.copy_(torch.cat(new_means))
-                self.running_var.copy_(torch.cat(new_vars))
-        return torch.cat(fields, dim=1)
+            for _ in range(mul):
+                chan_col.append(col)
+                chan_info.append((d, si if scalar else -1))
+                col_chan.extend([u] * d)
+                si += int(scalar)
+                u += 1
+                col += d
+        i32 = dict(dtype=torch.int32)
+        return (torch.tensor(col_chan, **i32), torch.tensor(chan_col, **i32),
+                torch.tensor(chan_info, **i32).view(-1, 2))
+
+    def forward(self, x):
+        x = _f32c(x)
+        _need_cuda(x)
+        tables = _dev_table(self._tables, self._host_tables, x.device)
+        return IrrepsBatchNormFn.apply(x, self.weight, self.bias, tables, self.running_mean,
+                                       self.running_var, self.training, self.momentum, self.eps)
+
+
+class GateFn(torch.autograd.Function):
+    """K16 Gate (gmp_gate_{fwd,bwd}_f32): one pass each way over the node rows."""
+
+    @staticmethod
+    def forward(ctx, x, out_map, in_map, c_act, c_gate):
+        y = _lib.torch_ops().gate_fwd(x, out_map, c_act, c_gate)
+        ctx.save_for_backward(x)
+        ctx.in_map, ctx.c = in_map, (c_act, c_gate)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        return (_lib.torch_ops().gate_bwd(x, _f32c(gy), ctx.in_map, *ctx.c), None, None, None,
+                None)
 
 
 class Gate(nn.Module):
-    """e3nn nn.Gate(scalars, [silu], gates, [sigmoid], gated) (tfn_layer.py:45-63)."""
+    """e3nn nn.Gate(scalars, [silu], gates, [sigmoid], gated) (tfn_layer.py:45-63) as the fused
+    HIP kernel K16, normalize2mom constants baked in:
+    y = [c_act silu(scalars), gated * c_gate sigmoid(gates)]."""
 
     def __init__(self, irreps_scalars, irreps_gates, irreps_gated):
         super().__init__()
@@ -223,21 +267,35 @@ class Gate(nn.Module):
         self.irreps_in = tuple(irreps_scalars) + tuple(irreps_gates) + tuple(irreps_gated)
         self.irreps_out = tuple(irreps_scalars) + tuple(irreps_gated)
         self.c_act, self.c_gate = o3.normalize2mom("silu"), o3.normalize2mom("sigmoid")
+        self._tables = {}
 
-    def forward(self, x):
+    def _host_tables(self):
         ns, ng = o3.irreps_dim(self.irreps_scalars), o3.irreps_dim(self.irreps_gates)
-        B = x.shape[0]
-        outs = [self.c_act * F.silu(x[:, :ns])]
-        g = self.c_gate * torch.sigmoid(x[:, ns:ns + ng])
-        v = x[:, ns + ng:]
-        gi = vi = 0
+        n_gated = sum(m for m, _ in self.irreps_gated)
+        if ng != n_gated:
+            raise ValueError(f"Gate: {ng} gate scalars for {n_gated} gated channels")
+        out_map = [(j, -1) for j in range(ns)]
+        in_map = [(0, j, 0, 0) for j in range(ns)] + [None] * ng
+        gated_in = []
+        k = off = 0
         for mul, (l, _) in self.irreps_gated:
             d = 2 * l + 1
-            outs.append((v[:, vi:vi + mul * d].reshape(B, mul, d)
-                         * g[:, gi:gi + mul].unsqueeze(-1)).reshape(B, mul * d))
-            vi += mul * d
-            gi += mul
-        return torch.cat(outs, dim=1)
+            for _ in range(mul):
+                in_map[ns + k] = (1, ns + off, ns + ng + off, d)
+                for m in range(d):
+                    out_map.append((ns + ng + off + m, ns + k))
+                    gated_in.append((2, ns + off + m, ns + k, 0))
+                k += 1
+                off += d
+        in_map += gated_in
+        i32 = dict(dtype=torch.int32)
+        return (torch.tensor(out_map, **i32).view(-1, 2), torch.tensor(in_map, **i32).view(-1, 4))
+
+    def forward(self, x):
+        x = _f32c(x)
+        _need_cuda(x)
+        out_map, in_map = _dev_table(self._tables, self._host_tables, x.device)
+        return GateFn.apply(x, out_map, in_map, float(self.c_act), float(self.c_gate))
 
 
 # ===================================================================================== TP conv

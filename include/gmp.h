@@ -248,6 +248,37 @@ int gmp_schnet_featurize_bwd_f32(const float* pos, const int64_t* edge_index, in
                                  const float* g_cut, float* g_vec, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * K16 irreps epilogues of the TP convolution (models/layers/tfn_layer.py:89-92), row-major
+ * (B, C) fp32 node features, all tables int32 on the DEVICE (built once per module):
+ * Gate (e3nn nn.Gate, tfn_layer.py:45-63): y = [c_act silu(scalars), gated * c_gate
+ *   sigmoid(gates)]; out_map (c_out, 2) = {source col, gate col or -1}; in_map (c_in, 4) =
+ *   {kind 0 scalar / 1 gate / 2 gated, a, b, d} (gmp_irreps.hip header).
+ * BatchNorm (e3nn nn.BatchNorm, component normalisation, affine): col_chan (C) channel of each
+ *   column, chan_col (nf) first column of each channel, chan_info (nf, 2) = {2l+1, scalar index
+ *   or -1}.  Training: batch statistics (fixed-order partial sums) and running-stat update in
+ *   place (momentum); eval: running statistics.  save_shift / save_invstd (nf) feed the
+ *   backward, which writes grad_x and grad_weight (nf) / grad_bias (number of scalar channels).
+ * ------------------------------------------------------------------------------------------ */
+int gmp_gate_fwd_f32(int64_t B, int c_in, int c_out, const int32_t* out_map, float c_act,
+                     float c_gate, const float* x, float* y, void* stream);
+int gmp_gate_bwd_f32(int64_t B, int c_in, int c_out, const int32_t* in_map, float c_act,
+                     float c_gate, const float* x, const float* grad_y, float* grad_x,
+                     void* stream);
+size_t gmp_irreps_bn_workspace_size(int64_t B, int C, int nf);
+int gmp_irreps_bn_fwd_f32(int64_t B, int C, int nf, const int32_t* col_chan,
+                          const int32_t* chan_col, const int32_t* chan_info, const float* x,
+                          const float* weight, const float* bias, float* running_mean,
+                          float* running_var, int training, float momentum, float eps, float* y,
+                          float* save_shift, float* save_invstd, void* workspace,
+                          size_t workspace_bytes, void* stream);
+int gmp_irreps_bn_bwd_f32(int64_t B, int C, int nf, const int32_t* col_chan,
+                          const int32_t* chan_col, const int32_t* chan_info, const float* x,
+                          const float* grad_y, const float* weight, const float* save_shift,
+                          const float* save_invstd, int training, float* grad_x,
+                          float* grad_weight, float* grad_bias, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * K7 tensor-product convolution messages (models/layers/tfn_layer.py:82-86): e3nn
  * FullyConnectedTensorProduct(in1, 1x0e+1x1o+1x2e, out, shared_weights=False) applied per edge
  * with per-edge weights W (chunk rows x weight_numel, produced by the radial MLP

@@ -323,3 +323,58 @@ def test_mace_c4_full_size_properties():
     b = run(pos, ei)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     assert a[1].abs().max().item() > 0
+
+
+@pytest.mark.parametrize("irr,B", [("8x0e+8x1o+8x2e", 37), ("128x0e+128x1o+128x2e", 20000),
+                                   ("4x1o+2x2e", 300), ("3x0e+2x0o+5x1e", 1000)])
+def test_batchnorm_k16_vs_oracle(irr, B):
+    """K16 e3nn BatchNorm (gmp_irreps_bn_{fwd,bwd}_f32) against oracle/o3.BatchNorm on the CPU:
+    training twice (running-stat update), eval, and the gradients of x / weight / bias in both
+    modes.  Tolerance 1e-5 (outputs, running stats), 1e-4 of scale (gradients)."""
+    from gmp_amd import equivariant as eq
+    torch.manual_seed(B)
+    a, b = eq.BatchNorm(irr), oo3.BatchNorm(irr)
+    with torch.no_grad():
+        b.weight.uniform_(0.5, 1.5)
+        b.bias.normal_()
+    a.load_state_dict(b.state_dict())
+    a = a.to(DEV)
+    C = sum(m * (2 * l + 1) for m, (l, _) in eq.o3.parse_irreps(irr))
+    for mode in ("train", "train", "eval"):
+        if mode == "eval":
+            a.eval(), b.eval()
+        x = torch.randn(B, C) * 2 + 0.5
+        xa, xb = x.to(DEV).requires_grad_(True), x.clone().requires_grad_(True)
+        ya, yb = a(xa), b(xb)
+        torch.testing.assert_close(ya.detach().cpu(), yb.detach(), atol=1e-5, rtol=1e-5)
+        g = torch.randn_like(yb)
+        (ya * g.to(DEV)).sum().backward()
+        (yb * g).sum().backward()
+        _close_scaled(xa.grad, xb.grad, 1e-4, f"{mode} dx")
+        _close_scaled(a.weight.grad, b.weight.grad, 1e-4, f"{mode} dw")
+        if b.bias.numel():
+            _close_scaled(a.bias.grad, b.bias.grad, 1e-4, f"{mode} db")
+        a.zero_grad(), b.zero_grad()
+        torch.testing.assert_close(a.running_mean.cpu(), b.running_mean, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(a.running_var.cpu(), b.running_var, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("irr,B", [("8x0e+8x1o+8x2e", 11), ("64x0e+64x1o+64x2e", 5000),
+                                   ("16x0e+16x1o", 300)])
+def test_gate_k16_vs_oracle(irr, B):
+    """K16 Gate (gmp_gate_{fwd,bwd}_f32) against oracle/o3.Gate (normalize2mom silu / sigmoid)
+    on the CPU, forward and input gradient.  Tolerance 1e-6 / 1e-5 of scale."""
+    from gmp_amd import equivariant as eq
+    from gmp_amd import o3
+    s, g, v = o3.irreps2gate(o3.parse_irreps(irr))
+    ga = eq.Gate(s, g, v)
+    gb = oo3.Gate(*oo3.irreps2gate(oo3.Irreps(irr)))
+    torch.manual_seed(B)
+    x = torch.randn(B, o3.irreps_dim(ga.irreps_in)) * 3
+    xa, xb = x.to(DEV).requires_grad_(True), x.clone().requires_grad_(True)
+    ya, yb = ga(xa), gb(xb)
+    torch.testing.assert_close(ya.detach().cpu(), yb.detach(), atol=1e-6, rtol=1e-5)
+    gy = torch.randn_like(yb)
+    (ya * gy.to(DEV)).sum().backward()
+    (yb * gy).sum().backward()
+    _close_scaled(xa.grad, xb.grad, 1e-5, "dx")
