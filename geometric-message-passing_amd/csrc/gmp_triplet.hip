@@ -180,6 +180,73 @@ int grid_for(int64_t n) {
   return (int)(g > cap ? cap : (g < 1 ? 1 : g));
 }
 
+// Backward of dist and angle w.r.t. pos (dimenet.py:82-89 / spherenet_layer.py:509,531-535
+// under autograd).  theta = atan2(b, a), a = u.v, b = |c|, c = u x v:
+//   d theta = (a db - b da) / (a^2 + b^2);  da/du = v, da/dv = u;
+//   db/du = v x c^, db/dv = c^ x u (c^ = c / b; 0 when b = 0, as torch's norm backward).
+// Rows written (3 floats each): [0, T) vertex -(g_u + g_v), [T, 2T) u end g_u, [2T, 3T) v end
+// g_v, [3T, 3T+E) g_d (p_i - p_j) / d at i, [3T+E, 3T+2E) its negative at j; node[] receives
+// the row's node so one segmented sum over a CSR of node[] yields d pos deterministically.
+__global__ void triplet_geom_bwd_kernel(const float* __restrict__ pos,
+                                        const int64_t* __restrict__ ei, int64_t E,
+                                        const int64_t* __restrict__ idx_kj,
+                                        const int64_t* __restrict__ idx_ji, int64_t T, int mode,
+                                        const float* __restrict__ g_dist,
+                                        const float* __restrict__ g_angle,
+                                        float* __restrict__ rows, int64_t* __restrict__ node) {
+  const int64_t n = T + E;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    if (q < T) {
+      const int64_t t = q, e = idx_ji[t];
+      const int64_t j = ei[e], i = ei[E + e], k = ei[idx_kj[t]];
+      const int64_t vtx = mode == 0 ? j : i, ue = mode == 0 ? i : j;
+      const V3 pv = ld3(pos, vtx), u = sub3(ld3(pos, ue), pv), v = sub3(ld3(pos, k), pv);
+      float gux = 0.f, guy = 0.f, guz = 0.f, gvx = 0.f, gvy = 0.f, gvz = 0.f;
+      const float g = g_angle ? g_angle[t] : 0.f;
+      if (g != 0.f) {
+        const V3 c = cross3(u, v);
+        const float b = norm3(c), a = dot3(u, v);
+        const float den = a * a + b * b;
+        const float ga = -g * b / den, gb = g * a / den;
+        gux = ga * v.x; guy = ga * v.y; guz = ga * v.z;
+        gvx = ga * u.x; gvy = ga * u.y; gvz = ga * u.z;
+        if (b > 0.f) {
+          const V3 ch{c.x / b, c.y / b, c.z / b};
+          gux += gb * (v.y * ch.z - v.z * ch.y);
+          guy += gb * (v.z * ch.x - v.x * ch.z);
+          guz += gb * (v.x * ch.y - v.y * ch.x);
+          gvx += gb * (ch.y * u.z - ch.z * u.y);
+          gvy += gb * (ch.z * u.x - ch.x * u.z);
+          gvz += gb * (ch.x * u.y - ch.y * u.x);
+        }
+      }
+      float* r0 = rows + 3 * t;
+      float* r1 = rows + 3 * (T + t);
+      float* r2 = rows + 3 * (2 * T + t);
+      r0[0] = -(gux + gvx); r0[1] = -(guy + gvy); r0[2] = -(guz + gvz);
+      r1[0] = gux; r1[1] = guy; r1[2] = guz;
+      r2[0] = gvx; r2[1] = gvy; r2[2] = gvz;
+      node[t] = vtx;
+      node[T + t] = ue;
+      node[2 * T + t] = k;
+    } else {
+      const int64_t e = q - T;
+      const int64_t j = ei[e], i = ei[E + e];
+      const V3 d = sub3(ld3(pos, i), ld3(pos, j));
+      const float len = len3(d);
+      const float g = g_dist ? g_dist[e] : 0.f;
+      const float s = (g != 0.f && len > 0.f) ? g / len : 0.f;
+      float* r0 = rows + 3 * (3 * T + e);
+      float* r1 = rows + 3 * (3 * T + E + e);
+      r0[0] = s * d.x; r0[1] = s * d.y; r0[2] = s * d.z;
+      r1[0] = -(s * d.x); r1[1] = -(s * d.y); r1[2] = -(s * d.z);
+      node[3 * T + e] = i;
+      node[3 * T + E + e] = j;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace gmp
 
@@ -211,6 +278,19 @@ int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_
   triplet_fill_kernel<<<(unsigned)ceil_div(n_edges, kFB), kFB, 0, as_stream(stream)>>>(
       pos, edge_index, n_edges, adj_rowptr, adj_src, adj_eid, offsets, mode, idx_kj, idx_ji,
       angle, torsion);
+  return launch_status();
+}
+
+int gmp_triplet_geom_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                             const int64_t* idx_kj, const int64_t* idx_ji, int64_t n_triplets,
+                             int mode, const float* grad_dist, const float* grad_angle,
+                             float* rows, int64_t* node, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && n_triplets >= 0 && (mode == 0 || mode == 1));
+  if (n_edges + n_triplets == 0) return GMP_OK;
+  GMP_CHECK_ARG(pos && edge_index && rows && node && (n_triplets == 0 || (idx_kj && idx_ji)));
+  triplet_geom_bwd_kernel<<<grid_for(n_edges + n_triplets), 256, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, idx_kj, idx_ji, n_triplets, mode, grad_dist, grad_angle, rows,
+      node);
   return launch_status();
 }
 

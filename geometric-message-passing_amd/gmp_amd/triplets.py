@@ -8,8 +8,11 @@ target, row-selected by source); here the adjacency by (target, source) comes fr
 CSR builds (K0), and K11 counts, then fills the triplets with their angles (and SphereNet
 torsions) in one pass, in the reference's order.
 
-Like the reference's use of these features (positions are data, not differentiated), there is
-no backward: a `pos` that requires grad under autograd raises.
+Distances and angles are differentiable w.r.t. `pos` (PyG DimeNet differentiates its angles,
+dimenet.py:79-90, e.g. for forces): the backward kernel gmp_triplet_geom_bwd_f32 writes one
+gradient row per (triplet, corner) and per (edge, end), summed per node over a CSR
+(deterministic).  The SphereNet torsion (a scatter-min over candidates) has no backward: asking
+for it with a `pos` that requires grad raises.
 """
 import torch
 
@@ -31,9 +34,6 @@ def _run(pos, edge_index, num_nodes, mode, want_angle, want_torsion, want_dist):
     ei = ops._i64c(edge_index)
     ops._need_cuda(ei)
     if pos is not None:
-        if pos.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("triplet features have no backward (positions are data in "
-                                      "the reference); detach pos")
         pos = ops._f32c(pos.detach())
         ops._need_cuda(pos)
     dev = ei.device
@@ -59,11 +59,57 @@ def _run(pos, edge_index, num_nodes, mode, want_angle, want_torsion, want_dist):
     return dist, angle, torsion, idx_kj, idx_ji
 
 
+class TripletGeomFn(torch.autograd.Function):
+    """(dist (E), angle (T), idx_kj, idx_ji) with the backward of dist and angle w.r.t. pos."""
+
+    @staticmethod
+    def forward(ctx, pos, edge_index, num_nodes, mode):
+        dist, angle, _, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, mode, True, False, True)
+        ctx.save_for_backward(pos, ops._i64c(edge_index), idx_kj, idx_ji)
+        ctx.mode, ctx.n = mode, int(num_nodes)
+        ctx.mark_non_differentiable(idx_kj, idx_ji)
+        return dist, angle, idx_kj, idx_ji
+
+    @staticmethod
+    def backward(ctx, g_dist, g_angle, _g1, _g2):
+        pos, ei, idx_kj, idx_ji = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        E, T = ei.shape[1], idx_kj.numel()
+        dev = pos.device
+        rows = torch.empty((3 * T + 2 * E, 3), dtype=torch.float32, device=dev)
+        node = torch.empty(3 * T + 2 * E, dtype=torch.int64, device=dev)
+        gd = ops._f32c(g_dist) if g_dist is not None else None
+        ga = ops._f32c(g_angle) if g_angle is not None else None
+        lib = _lib.load()
+        ops.check(lib.gmp_triplet_geom_bwd_f32(ops._p(ops._f32c(pos.detach())), ops._p(ei), E,
+                                               ops._p(idx_kj), ops._p(idx_ji), T, ctx.mode,
+                                               ops._p(gd), ops._p(ga), ops._p(rows),
+                                               ops._p(node), ops._stream()),
+                  "gmp_triplet_geom_bwd_f32")
+        g_pos, _ = ops.segment_reduce(rows, ops.CSR(node, ctx.n), "sum")
+        return g_pos.to(pos.dtype), None, None, None
+
+
+def _geom(pos, edge_index, num_nodes, mode):
+    if pos.requires_grad and torch.is_grad_enabled():
+        return TripletGeomFn.apply(pos, edge_index, num_nodes, mode)
+    dist, angle, _, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, mode, True, False, True)
+    return dist, angle, idx_kj, idx_ji
+
+
 def xyz_to_dat(pos, edge_index, num_nodes, use_torsion=False):
     """spherenet_layer.py:496: -> dist, angle, [torsion,] i, j, idx_kj, idx_ji (edge e = j -> i;
-    angle in [0, pi] at j; torsion in (0, 2*pi])."""
-    dist, angle, torsion, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, 0, True,
-                                                use_torsion, True)
+    angle in [0, pi] at j; torsion in (0, 2*pi]).  dist and angle are differentiable w.r.t.
+    pos; the torsion is not (raises if pos requires grad)."""
+    if use_torsion and pos.requires_grad and torch.is_grad_enabled():
+        raise NotImplementedError("the SphereNet torsion has no backward; detach pos")
+    if use_torsion:
+        dist, angle, torsion, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, 0, True, True,
+                                                    True)
+    else:
+        dist, angle, idx_kj, idx_ji = _geom(pos, edge_index, num_nodes, 0)
+        torsion = None
     j, i = edge_index
     if use_torsion:
         return dist, angle, torsion, i, j, idx_kj, idx_ji
@@ -81,6 +127,6 @@ def dimenet_triplets(edge_index, num_nodes):
 def dimenet_angles(pos, edge_index, num_nodes):
     """dimenet.py:79-90: -> dist (E), angle (T, vertex i), i, j, idx_i, idx_j, idx_k, idx_kj,
     idx_ji."""
-    dist, angle, _, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, 1, True, False, True)
+    dist, angle, idx_kj, idx_ji = _geom(pos, edge_index, num_nodes, 1)
     row, col = edge_index
     return (dist, angle, col, row, col[idx_ji], row[idx_ji], row[idx_kj], idx_kj, idx_ji)

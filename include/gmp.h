@@ -467,6 +467,14 @@ int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_
                          const int64_t* adj_eid, const int64_t* offsets, int64_t n_triplets,
                          int mode, int64_t* idx_kj, int64_t* idx_ji, float* angle,
                          float* torsion, void* stream);
+/* Backward of dist (E) and angle (T) w.r.t. pos (DimeNet / SphereNet under autograd): writes
+ * 3T + 2E rows of 3 floats (`rows`) and their node ids (`node`): vertex, u-end and v-end rows
+ * of every triplet, then +/- rows of every edge's distance; d pos = the segmented sum of rows
+ * by node (the caller's CSR; deterministic).  grad_dist / grad_angle may be NULL (zero). */
+int gmp_triplet_geom_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                             const int64_t* idx_kj, const int64_t* idx_ji, int64_t n_triplets,
+                             int mode, const float* grad_dist, const float* grad_angle,
+                             float* rows, int64_t* node, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K12 fused LayerNorm + activation over rows (node-level MLPs: EGNN mlp_upd,

@@ -87,8 +87,39 @@ def test_edge_cases():
     ref = o_xyz(pos, ei, 4, True)
     _check(out, ref, 3)
     assert out[1].numel() == 0
-    with pytest.raises(NotImplementedError):
-        xyz_to_dat(pos.to(DEV).requires_grad_(True), ei.to(DEV), 4)
+    with pytest.raises(NotImplementedError):  # the torsion has no backward
+        xyz_to_dat(pos.to(DEV).requires_grad_(True), ei.to(DEV), 4, use_torsion=True)
+
+
+@pytest.mark.parametrize("mode", ["spherenet", "dimenet"])
+def test_dist_angle_backward_vs_oracle(mode):
+    """d pos of sum(g_d dist) + sum(g_a angle) through gmp_triplet_geom_bwd_f32 + the CSR
+    segmented sum, against autograd through the oracle's torch ops (dimenet.py:82-89 /
+    spherenet_layer.py:509,531-535 restated).  Tolerance 1e-4 of the gradient's scale (atan2
+    near-collinear triplets amplify last-ulp differences)."""
+    from gmp_amd.triplets import dimenet_angles, xyz_to_dat
+    pos, ei = _graph(400, 6.5, 1.6, 11)
+    n = pos.shape[0]
+    pd = pos.to(DEV).requires_grad_(True)
+    pr = pos.clone().requires_grad_(True)
+    if mode == "spherenet":
+        out, ref = xyz_to_dat(pd, ei.to(DEV), n), o_xyz(pr, ei, n)
+    else:
+        out, ref = dimenet_angles(pd, ei.to(DEV), n), o_dimenet(pr, ei, n)
+    _check(out, [r.detach() for r in ref], 2)
+    g = torch.Generator().manual_seed(1)
+    gd, ga = (torch.randn(ref[0].shape, generator=g), torch.randn(ref[1].shape, generator=g))
+    ((out[0] * gd.to(DEV)).sum() + (out[1] * ga.to(DEV)).sum()).backward()
+    ((ref[0] * gd).sum() + (ref[1] * ga).sum()).backward()
+    scale = pr.grad.abs().max().item()
+    err = (pd.grad.cpu() - pr.grad).abs().max().item()
+    assert err <= 1e-4 * scale, (err, scale)
+    # deterministic
+    g1 = pd.grad.clone()
+    pd.grad = None
+    out = xyz_to_dat(pd, ei.to(DEV), n) if mode == "spherenet" else dimenet_angles(pd, ei.to(DEV), n)
+    ((out[0] * gd.to(DEV)).sum() + (out[1] * ga.to(DEV)).sum()).backward()
+    assert torch.equal(g1, pd.grad)
 
 
 def test_benchmark_size_properties():
