@@ -13,7 +13,14 @@
 //  * W2 / W3 (d x d, row-major) live in LDS with row stride d+4 floats; W.x reads W rows with
 //    ds_read_b128, W^T.g reads W columns with conflict-free ds_read_b32;
 //  * the first Linear(2d+1 -> d) is split into per-node projections AB = [h W1a^T | h W1b^T]
-//    (a node-level GEMM done once per node by the caller) plus a rank-1 distance term.
+//    (a node-level GEMM done once per node by the caller) plus a rank-1 distance term;
+//  * HF path (default): the two d x d products per chunk run on v_mfma_f32_16x16x32_f16 over
+//    2-plane fp16 splits (hi + lo, 22-bit operands; products hi*hi + hi*lo + lo*hi, f32
+//    accumulation) with power-of-two scaling (W per matrix, x per edge) that keeps the planes
+//    in fp16 range; the planes of W take the LDS of the f32 W (gemm_h2 below).  The f32 path
+//    (exact fmaf chains on the f32 MFMA) stays selectable: gmp_egnn_set_f32_mfma(1).
+#include <stdlib.h>
+
 #include "gmp_common.h"
 
 namespace gmp {
@@ -24,6 +31,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // One workgroup per CU (W2 + W3 in LDS).  Forward: 12 waves (<= 168 VGPRs -> 3 per SIMD);
 // backward: 8 waves (<= 256 VGPRs -> 2 per SIMD).
 constexpr int kFwdWaves = 12;
+#ifndef GMP_EGNN_HF_FWD_WAVES
+#define GMP_EGNN_HF_FWD_WAVES 8
+#endif
+// HF forward: 8 waves (<= 256 VGPRs -> 2 per SIMD): its products need fewer MFMA cycles but more
+// live registers (fp16 operand planes) than 168 allow without spills
+template <bool HF>
+constexpr int fwd_waves() { return HF ? GMP_EGNN_HF_FWD_WAVES : kFwdWaves; }
 constexpr int kBwdWaves = 8;
 
 template <int D>
@@ -41,12 +55,31 @@ enum VecId { V_W1D = 0, V_B1, V_LN1W, V_LN1B, V_B2, V_LN2W, V_LN2B, V_B3, V_LN3W
 template <int D>
 constexpr int carry_stride() { return D / 4 + 4; }
 
-// LDS: W2 | W3 | NV vectors | per-wave carries [wave][g][d/4 + 4]
+// HF path: W as hi / lo fp16 planes of W 2^sw, columns in the MFMA k order (see gemm_h2), row
+// stride d + 8 halfs (272 B at d = 128: the 16 rows of a ds_read_b128 fall on distinct banks)
 template <int D>
-constexpr size_t smem_params_floats() { return (size_t)2 * D * Cfg<D>::LDW + NV * D; }
-template <int D, int NW>
+struct HCfg {
+  static constexpr int LDH = D + 8;
+  static constexpr int PLANE = D * LDH;  // halfs
+  static constexpr int MAT = 2 * PLANE;  // halfs per matrix (= floats for two matrices)
+};
+
+// LDS, f32 path: W2 | W3 (rows of d + 4 floats) | NV vectors + 12 | per-wave carries
+// [wave][g][d/4 + 4].  HF path: NV vectors + 12 scalars (scale exponents, max scratch) |
+// carries | W2 planes | W3 planes — the vectors first, so their reads fold into the 16-bit
+// ds_read offset of one base register instead of holding one address register each.
+template <int D, int NW, bool HF>
+constexpr size_t smem_vec_off() { return HF ? 0 : (size_t)2 * D * Cfg<D>::LDW; }
+template <int D, int NW, bool HF>
+constexpr size_t smem_carry_off() { return smem_vec_off<D, NW, HF>() + NV * D + 12; }
+template <int D, int NW, bool HF>
+constexpr size_t smem_mats_off() {
+  return HF ? smem_carry_off<D, NW, HF>() + (size_t)NW * 4 * carry_stride<D>() : 0;
+}
+template <int D, int NW, bool HF>
 constexpr size_t smem_total() {
-  return (smem_params_floats<D>() + (size_t)NW * 4 * carry_stride<D>()) * sizeof(float);
+  return (HF ? smem_mats_off<D, NW, HF>() + HCfg<D>::MAT
+             : smem_carry_off<D, NW, HF>() + (size_t)NW * 4 * carry_stride<D>()) * sizeof(float);
 }
 
 template <int ACT>
@@ -87,6 +120,85 @@ __device__ void load_params_to_lds(float* smem, const gmp_egnn_params& P) {
   const float* vsrc[NV] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
                            P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
   for (int i = threadIdx.x; i < NV * D; i += blockDim.x) sV[i] = vsrc[i / D][i % D];
+}
+
+// exponent s with max|v| 2^s < 2^15 (fp16 range with headroom), clamped to [-60, 60]
+__device__ __forceinline__ int scale_exp(float mx) {
+  if (!(mx > 0.f) || !(mx < 3.0e38f)) return 0;
+  int e;
+  (void)frexpf(mx, &e);  // mx < 2^e
+  const int s = 15 - e;
+  return s < -60 ? -60 : (s > 60 ? 60 : s);
+}
+
+// HF: hi / lo planes of W2 and W3 (or their transposes) scaled by 2^sw (one exponent per matrix
+// from a block-wide max |W|, kept as floats after the vectors).  Natural column k = 16 tt + 4 g
+// + q goes to position 32 (tt >> 1) + 8 g + 4 (tt & 1) + q: the 8 halfs a lane feeds one
+// 16x16x32 MFMA (k = 8 g + j of block p) are then the slots x[2p][0..3], x[2p + 1][0..3] it
+// already holds.
+__device__ __forceinline__ int hf_pos(int k) {
+  const int tt = k >> 4, gg = (k >> 2) & 3, q = k & 3;
+  return 32 * (tt >> 1) + 8 * gg + 4 * (tt & 1) + q;
+}
+template <int D, bool TRANSPOSE>
+__device__ void load_params_hf(float* sV, _Float16* hW, const gmp_egnn_params& P) {
+  using H = HCfg<D>;
+  // scalars after the vectors: [0] [1] exponents of W2 / W3, [2] [3] static input exponents of
+  // the forward products (below), [4..7] max scratch
+  unsigned* mxw = reinterpret_cast<unsigned*>(sV + NV * D + 4);
+  if (threadIdx.x < 6) mxw[threadIdx.x] = 0u;
+  __syncthreads();
+  unsigned m2 = 0u, m3 = 0u;  // |w| bit patterns order like the values
+  for (int i = threadIdx.x; i < D * D / 4; i += blockDim.x) {
+    const float4 a = reinterpret_cast<const float4*>(P.W2)[i];
+    const float4 b = reinterpret_cast<const float4*>(P.W3)[i];
+    m2 = max(m2, max(max(__float_as_uint(fabsf(a.x)), __float_as_uint(fabsf(a.y))),
+                     max(__float_as_uint(fabsf(a.z)), __float_as_uint(fabsf(a.w)))));
+    m3 = max(m3, max(max(__float_as_uint(fabsf(b.x)), __float_as_uint(fabsf(b.y))),
+                     max(__float_as_uint(fabsf(b.z)), __float_as_uint(fabsf(b.w)))));
+  }
+  atomicMax(&mxw[0], m2);
+  atomicMax(&mxw[1], m3);
+  // forward inputs of W2 / W3 are act(x_hat * w + b) of a LayerNorm over d features:
+  // |x_hat| <= sqrt(d - 1), |act(z)| <= |z| (relu, silu) => |input| <= sqrt(d) max|w| + max|b|
+  if (!TRANSPOSE && threadIdx.x < 64) {
+    unsigned a = 0u, b = 0u, c = 0u, e = 0u;
+    for (int k = threadIdx.x; k < D; k += 64) {
+      a = max(a, __float_as_uint(fabsf(P.ln1_w[k])));
+      b = max(b, __float_as_uint(fabsf(P.ln1_b[k])));
+      c = max(c, __float_as_uint(fabsf(P.ln2_w[k])));
+      e = max(e, __float_as_uint(fabsf(P.ln2_b[k])));
+    }
+    atomicMax(&mxw[2], a);
+    atomicMax(&mxw[3], b);
+    atomicMax(&mxw[4], c);
+    atomicMax(&mxw[5], e);
+  }
+  __syncthreads();
+  const int s2 = scale_exp(__uint_as_float(mxw[0])), s3 = scale_exp(__uint_as_float(mxw[1]));
+  const float rd = sqrtf((float)D);
+  const int sx2 = scale_exp(rd * __uint_as_float(mxw[2]) + __uint_as_float(mxw[3]));
+  const int sx3 = scale_exp(rd * __uint_as_float(mxw[4]) + __uint_as_float(mxw[5]));
+  __syncthreads();  // (the scratch words are overwritten below)
+  for (int i = threadIdx.x; i < 2 * D * D; i += blockDim.x) {
+    const int mat = i / (D * D), e = i - mat * D * D;
+    const int o = e / D, k = e - o * D;  // W[o][k]
+    const float w = ldexpf((mat ? P.W3 : P.W2)[e], mat ? s3 : s2);
+    const int r = TRANSPOSE ? k : o, c = TRANSPOSE ? o : k;
+    const _Float16 hi = (_Float16)w;
+    _Float16* dst = hW + mat * H::MAT + r * H::LDH + hf_pos(c);
+    dst[0] = hi;
+    dst[H::PLANE] = (_Float16)(w - (float)hi);
+  }
+  const float* vsrc[NV] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
+                           P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
+  for (int i = threadIdx.x; i < NV * D; i += blockDim.x) sV[i] = vsrc[i / D][i % D];
+  if (threadIdx.x == 0) {
+    sV[NV * D + 0] = (float)s2;
+    sV[NV * D + 1] = (float)s3;
+    sV[NV * D + 2] = (float)sx2;
+    sV[NV * D + 3] = (float)sx3;
+  }
 }
 
 // this lane's 4 consecutive slots (4p..4p+3) of LDS vector v
@@ -177,6 +289,75 @@ __device__ __forceinline__ void gemm_wx(const float* __restrict__ sW, const f32x
       GMP_GEMM_FENCE();
     }
   }
+}
+
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+#ifndef HF_TILES_PER_FENCE
+#define HF_TILES_PER_FENCE 2
+#endif
+
+__device__ __forceinline__ float max_groups(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// HF: y[slot(o)] += sum_k W[o][k] x[slot(k)] on the f16 MFMA.  x of this lane's edge is scaled
+// by 2^sx (max |x| 2^sx < 2^15, from the 4 lane groups of the edge), W sits in LDS as planes of
+// W 2^sw; y is brought to scale 2^(sx + sw), accumulated with lo*hi + hi*lo + hi*hi per k block
+// (22-bit operands; the dropped lo*lo term is ~2^-22 relative) and scaled back.  Power-of-two
+// scalings are exact, so the f32 accumulation rounds as on unscaled values.
+// DYN: the x exponent from this edge's max |x| (backward: gradients have no a-priori bound);
+// otherwise sx_static (forward: bounded LayerNorm-activation inputs, load_params_hf) — the
+// per-edge reduction ahead of the products costs live registers the forward does not have.
+template <int D, bool DYN>
+__device__ __forceinline__ void gemm_h2(const _Float16* __restrict__ hW, int sw, int sx_static,
+                                        const f32x4 (&x)[D / 16], f32x4 (&y)[D / 16], int i,
+                                        int g) {
+  using H = HCfg<D>;
+  constexpr int T = D / 16, PB = D / 32;
+  int sx = sx_static;
+  if constexpr (DYN) {
+    float mx = 0.f;
+#pragma unroll
+    for (int p = 0; p < T; ++p)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) mx = fmaxf(mx, fabsf(x[p][c]));
+    sx = scale_exp(max_groups(mx));
+  }
+  sx = sx < -100 - sw ? -100 - sw : (sx > 100 - sw ? 100 - sw : sx);
+  const float fx = ldexpf(1.f, sx), up = ldexpf(1.f, sx + sw), down = ldexpf(1.f, -(sx + sw));
+#pragma unroll
+  for (int t = 0; t < T; ++t) y[t] *= up;
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    h16x8 bh, bl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = x[2 * p + (j >> 2)][j & 3] * fx;
+      const _Float16 h = (_Float16)v;
+      bh[j] = h;
+      bl[j] = (_Float16)(v - (float)h);
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      // compiler-level fence: keeps the A reads from being hoisted ahead of the operand split
+      // (and out of registers' reach) as a block
+      if (t % HF_TILES_PER_FENCE == 0) asm volatile("" ::: "memory");
+      const _Float16* row = hW + (16 * t + i) * H::LDH + 32 * p + 8 * g;
+      const h16x8 ah = *reinterpret_cast<const h16x8*>(row);
+      const h16x8 al = *reinterpret_cast<const h16x8*>(row + H::PLANE);
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, y[t], 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
+      y[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
+      if (t % HF_TILES_PER_FENCE == HF_TILES_PER_FENCE - 1) GMP_GEMM_FENCE();  // bounds hoisted reads
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) y[t] *= down;
 }
 
 // y[slot(k)] += sum_o W[o][k] gin[slot(o)]   (transposed product for the backward)
@@ -506,8 +687,8 @@ __device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowp
 // ================================================================================== forward
 // SAVE (training): also write the three LayerNorm outputs x_hat1..3 (xsave, (3, E, d), rows in
 // receiver-sorted edge order) and their 1/std (rsave, (E, 3)) for the backward.
-template <int D, int ACT, bool MSG_MEAN, bool SAVE>
-__global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
+template <int D, int ACT, bool MSG_MEAN, bool SAVE, bool HF>
+__global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egnn_fwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ AB, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
     const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
@@ -517,14 +698,21 @@ __global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2 = smem;
   const float* sW3 = smem + D * LDW;
-  const float* sV = smem + 2 * D * LDW;
-  load_params_to_lds<D>(smem, P);
+  _Float16* hW = reinterpret_cast<_Float16*>(smem + smem_mats_off<D, fwd_waves<HF>(), HF>());
+  const _Float16* hW2 = hW;
+  const _Float16* hW3 = hW + HCfg<D>::MAT;
+  float* sVw = smem + smem_vec_off<D, fwd_waves<HF>(), HF>();
+  const float* sV = sVw;
+  if constexpr (HF) load_params_hf<D, false>(sVw, hW, P);
+  else load_params_to_lds<D>(smem, P);
   __syncthreads();
+  const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
+  const int sx2 = HF ? (int)sV[NV * D + 2] : 0, sx3 = HF ? (int)sV[NV * D + 3] : 0;
 
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* cbuf = smem + smem_params_floats<D>() + (wid * 4 + g) * carry_stride<D>();
-  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, kFwdWaves);
+  float* cbuf = smem + smem_carry_off<D, fwd_waves<HF>(), HF>() + (wid * 4 + g) * carry_stride<D>();
+  const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, fwd_waves<HF>());
   const float b4 = P.b4[0];
   int carry_node = -1;
   EdgeIJ nxt = load_ij(wr.e_lo, li, wr.e_hi, recv, send);
@@ -552,14 +740,16 @@ __global__ __launch_bounds__(kFwdWaves * 64, 3) void egnn_fwd_kernel(
 
     f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
     load_vec<D>(m, sV, V_B2, g);
-    gemm_wx<D>(sW2, x, m, li, g);
+    if constexpr (HF) gemm_h2<D, false>(hW2, sw2, sx2, x, m, li, g);
+    else gemm_wx<D>(sW2, x, m, li, g);
     const float r2 = ln_normalize<D>(m, eps);
     if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave + ED, base, ne, D), eoff, m, g);
     affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);
 
     // y3 = act(LN3(W3 m + b3)); s = w4 . y3 + b4   (x reused)
     load_vec<D>(x, sV, V_B3, g);
-    gemm_wx<D>(sW3, m, x, li, g);
+    if constexpr (HF) gemm_h2<D, false>(hW3, sw3, sx3, m, x, li, g);
+    else gemm_wx<D>(sW3, m, x, li, g);
     const float r3 = ln_normalize<D>(x, eps);
     if (SAVE) {
       store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
@@ -619,7 +809,7 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
 
 // Backward from the forward's saved x_hat1..3 / rstd (no forward recompute, no AB gathers):
 // two transposed GEMMs (W3^T, W2^T) per 16-edge chunk.
-template <int D, int ACT, bool MSG_MEAN>
+template <int D, int ACT, bool MSG_MEAN, bool HF>
 __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
@@ -632,13 +822,19 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2t = smem;  // W2^T
   const float* sW3t = smem + D * LDW;  // W3^T
-  const float* sV = smem + 2 * D * LDW;
-  load_params_to_lds<D, true>(smem, P);
+  _Float16* hW = reinterpret_cast<_Float16*>(smem + smem_mats_off<D, kBwdWaves, HF>());
+  const _Float16* hW2t = hW;
+  const _Float16* hW3t = hW + HCfg<D>::MAT;
+  float* sVw = smem + smem_vec_off<D, kBwdWaves, HF>();
+  const float* sV = sVw;
+  if constexpr (HF) load_params_hf<D, true>(sVw, hW, P);
+  else load_params_to_lds<D, true>(smem, P);
   __syncthreads();
+  const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
 
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* cbuf = smem + smem_params_floats<D>() + (wid * 4 + g) * carry_stride<D>();
+  float* cbuf = smem + smem_carry_off<D, kBwdWaves, HF>() + (wid * 4 + g) * carry_stride<D>();
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, kBwdWaves);
   const float b4 = P.b4[0];
   const size_t ED = (size_t)n_edges * D;
@@ -716,7 +912,8 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) z[p] = xh2[p] * gscale;
     load_row<D>(xh2, rowp(xsave + ED, c.ec, D), g);
-    gemm_wx<D, 2>(sW3t, x, z, li, g);  // z += W3^T dpre3
+    if constexpr (HF) gemm_h2<D, true>(hW3t, sw3, 0, x, z, li, g);  // z += W3^T dpre3
+    else gemm_wx<D, 2>(sW3t, x, z, li, g);
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN2W, p, g), b = vec4<D>(sV, V_LN2B, p, g);
@@ -734,7 +931,8 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     load_row<D>(xh2, rowp(xsave, c.ec, D), g);
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_wx<D, 2>(sW2t, z, x, li, g);  // x = W2^T dpre2
+    if constexpr (HF) gemm_h2<D, true>(hW2t, sw2, 0, z, x, li, g);  // x = W2^T dpre2
+    else gemm_wx<D, 2>(sW2t, z, x, li, g);
 #pragma unroll
     for (int p = 0; p < T; ++p) {
       const f32x4 w = vec4<D>(sV, V_LN1W, p, g), b = vec4<D>(sV, V_LN1B, p, g);
@@ -818,6 +1016,17 @@ int64_t n_waves_for(int64_t n_edges, int nwb) {
   return ceil_div(w, nwb) * nwb;
 }
 
+// 1: the f32-MFMA (exact fmaf chain) products instead of the HF path; initial value from
+// GMP_EGNN_F32_MFMA, changed by gmp_egnn_set_f32_mfma
+int g_egnn_f32 = -1;
+bool egnn_f32() {
+  if (g_egnn_f32 < 0) {
+    const char* e = getenv("GMP_EGNN_F32_MFMA");
+    g_egnn_f32 = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return g_egnn_f32 == 1;
+}
+
 template <class K>
 int prep_kernel(K k, size_t smem) {
   return hip_check(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -828,12 +1037,18 @@ template <int D, int ACT, bool MEAN>
 int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const int64_t* rowptr,
                const int64_t* recv, const int64_t* send, const gmp_egnn_params& P, float eps,
                float* m_aggr, float* pos_aggr, float* xsave, float* rsave, hipStream_t s) {
-  const int64_t W = n_waves_for(E, kFwdWaves);
-  const size_t smem = smem_total<D, kFwdWaves>();
-  auto k = xsave ? egnn_fwd_kernel<D, ACT, MEAN, true> : egnn_fwd_kernel<D, ACT, MEAN, false>;
+  const bool hf = !egnn_f32();
+  const int nwb = hf ? fwd_waves<true>() : fwd_waves<false>();
+  const int64_t W = n_waves_for(E, nwb);
+  const size_t smem = hf ? smem_total<D, fwd_waves<true>(), true>()
+                         : smem_total<D, fwd_waves<false>(), false>();
+  auto k = xsave ? (hf ? egnn_fwd_kernel<D, ACT, MEAN, true, true>
+                       : egnn_fwd_kernel<D, ACT, MEAN, true, false>)
+                 : (hf ? egnn_fwd_kernel<D, ACT, MEAN, false, true>
+                       : egnn_fwd_kernel<D, ACT, MEAN, false, false>);
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
-  k<<<(unsigned)(W / kFwdWaves), kFwdWaves * 64, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
+  k<<<(unsigned)(W / nwb), nwb * 64, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
                                                            eps, W, m_aggr, pos_aggr, xsave, rsave);
   return launch_status();
 }
@@ -845,8 +1060,9 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
                float* dA, float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
                float* dpre3, float* partials, hipStream_t s) {
   const int64_t W = n_waves_for(E, kBwdWaves);
-  const size_t smem = smem_total<D, kBwdWaves>();
-  auto k = egnn_bwd_kernel<D, ACT, MEAN>;
+  const bool hf = !egnn_f32();
+  const size_t smem = hf ? smem_total<D, kBwdWaves, true>() : smem_total<D, kBwdWaves, false>();
+  auto k = hf ? egnn_bwd_kernel<D, ACT, MEAN, true> : egnn_bwd_kernel<D, ACT, MEAN, false>;
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / kBwdWaves), kBwdWaves * 64, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
@@ -882,6 +1098,12 @@ using namespace gmp;
   } while (0)
 
 extern "C" {
+
+int gmp_egnn_set_f32_mfma(int on) {
+  const int prev = egnn_f32() ? 1 : 0;
+  g_egnn_f32 = on ? 1 : 0;
+  return prev;
+}
 
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
                           const float* pos, const int64_t* rowptr, const int64_t* recv,

@@ -589,8 +589,13 @@ bool wgrad_f32_mfma() {
   }
   return g_wgrad_mode == 1;
 }
+// Cap on the split-K workgroup count of the outer sums (0: none; gmp_wgrad_set_grid_cap): the
+// side-stream weight gradients leave CUs free for the critical path's node-level kernels.
+int g_grid_cap = 0;
+int64_t capped(int64_t g) { return g_grid_cap > 0 && g > g_grid_cap ? g_grid_cap : g; }
+
 int64_t x3_blocks_for(int64_t K) {
-  int64_t g = (int64_t)device_cu_count();  // one 8-wave workgroup per CU (LDS ~100 KB)
+  int64_t g = capped((int64_t)device_cu_count());  // one 8-wave workgroup per CU (LDS ~100 KB)
   const int64_t min_per = 4 * kXK;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
@@ -710,7 +715,7 @@ int rect_bucket(int64_t m, int64_t n) {
 }
 
 int64_t blocks_for(int64_t K) {
-  int64_t g = (int64_t)device_cu_count() * 2;  // two resident workgroups per CU
+  int64_t g = capped((int64_t)device_cu_count() * 2);  // two resident workgroups per CU
   const int64_t min_per = 4 * kKT;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
@@ -722,6 +727,12 @@ int64_t blocks_for(int64_t K) {
 using namespace gmp;
 
 extern "C" {
+
+int gmp_wgrad_set_grid_cap(int blocks) {
+  const int prev = g_grid_cap;
+  g_grid_cap = blocks > 0 ? blocks : 0;
+  return prev;
+}
 
 int gmp_wgrad_set_f32_mfma(int on) {
   const int prev = wgrad_f32_mfma() ? 1 : 0;
@@ -802,7 +813,7 @@ int gmp_edge_outer_sum_act_f32(int64_t K, int64_t d, const float* A, const float
 }
 
 int64_t rect_blocks_for(int64_t K) {
-  int64_t g = (int64_t)device_cu_count() * 2;
+  int64_t g = capped((int64_t)device_cu_count() * 2);
   const int64_t min_per = 4 * kKT;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;

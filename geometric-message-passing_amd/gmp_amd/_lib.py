@@ -69,6 +69,8 @@ SIGNATURES = {
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
                                       c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
+    "gmp_egnn_set_f32_mfma": (c_int, [c_int]),
+    "gmp_wgrad_set_grid_cap": (c_int, [c_int]),
     "gmp_wgrad_set_f32_mfma": (c_int, [c_int]),
     "gmp_edge_outer_sum_workspace_size": (c_size, [c_i64, c_i64]),
     "gmp_edge_outer_sum_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),

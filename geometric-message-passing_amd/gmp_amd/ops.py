@@ -6,6 +6,8 @@ fallback in the product path.
 """
 import ctypes
 
+import os
+
 import torch
 from torch.autograd.function import once_differentiable
 
@@ -327,13 +329,20 @@ def _engine_accumulates(p):
         return False
 
 
+# Split-K workgroup cap of the side-stream outer sums (gmp_wgrad_set_grid_cap; 0 = none): with
+# fewer workgroups the weight gradients leave CUs to the critical path's node-level kernels.
+SIDE_GRID_CAP = int(os.environ.get("GMP_SIDE_GRID_CAP", "0") or 0)
+
+
 class side_work:
     """with side_work(used_tensors) as sw: ... launches on the side stream after everything
     already queued on the current stream; sw.defer(param, grad) hands a result to the end-of-
-    backward accumulation (or, when deferral is off, sw.join() makes the current stream wait)."""
+    backward accumulation (or, when deferral is off, sw.join() makes the current stream wait).
+    tail=True: nothing on the critical path follows (no split-K grid cap)."""
 
-    def __init__(self, *used):
+    def __init__(self, *used, tail=False):
         self.used = [t for t in used if t is not None]
+        self.cap = 0 if tail else SIDE_GRID_CAP
 
     def __enter__(self):
         self.main = torch.cuda.current_stream()
@@ -341,9 +350,12 @@ class side_work:
         self.side.wait_stream(self.main)
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
+        self.prev_cap = _lib.load().gmp_wgrad_set_grid_cap(self.cap) if self.cap else None
         return self
 
     def __exit__(self, *exc):
+        if self.prev_cap is not None:
+            _lib.load().gmp_wgrad_set_grid_cap(self.prev_cap)
         self.ctx.__exit__(*exc)
         _KEEPALIVE.extend(self.used)
         return False

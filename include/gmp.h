@@ -123,6 +123,11 @@ typedef struct gmp_egnn_params {
 /* save_xhat / save_rstd: NULL (inference) or, for training, (3, E, d) and (E, 3) buffers that
  * receive the three LayerNorm outputs x_hat1..3 and their 1/std per edge (receiver-sorted rows)
  * for gmp_egnn_edge_bwd_f32. */
+/* The two d x d products per edge chunk run by default on the f16 MFMA over 2-plane (hi + lo)
+ * splits of the operands with power-of-two scaling (22-bit operands, f32 accumulation; relative
+ * error ~2^-21 per product); gmp_egnn_set_f32_mfma(1) (or GMP_EGNN_F32_MFMA=1 at load) selects
+ * the exact f32-MFMA fmaf chains.  Returns the previous setting. */
+int gmp_egnn_set_f32_mfma(int on);
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
                           const float* pos, const int64_t* rowptr, const int64_t* recv,
                           const int64_t* send, const gmp_egnn_params* params, int act,
@@ -165,6 +170,9 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
  * kernels instead, returns the previous setting.
  * ------------------------------------------------------------------------------------------ */
 int gmp_wgrad_set_f32_mfma(int on);
+/* Cap the split-K workgroup count of the outer sums (0 = none, the default: 1-2 per CU); returns
+ * the previous cap.  Host-side setting read at launch (and by the workspace-size queries). */
+int gmp_wgrad_set_grid_cap(int blocks);
 size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d);
 int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
                            float* colsum_A, void* workspace, size_t workspace_bytes,

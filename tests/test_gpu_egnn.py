@@ -214,3 +214,53 @@ def test_double_backward_raises():
     (gp,) = torch.autograd.grad(ho.sum() + po.sum(), [pd], create_graph=True)
     with pytest.raises(RuntimeError):
         gp.sum().backward()
+
+
+@pytest.mark.parametrize("d", [128, 64])
+def test_egnn_hf_products_vs_fp64(d):
+    """The default (HF) K4 products — f16 MFMA over 2-plane splits with power-of-two scaling —
+    against the fp64 oracle, next to the exact f32-MFMA path (gmp_egnn_set_f32_mfma(1)): the HF
+    error stays within 2x the f32 path's error + 1e-6 of scale on outputs and input / parameter
+    gradients, including gradients scaled down by 2^-40 (the per-edge backward scaling)."""
+    import copy
+    import gmp_amd
+    from gmp_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(d + 1)
+    g = _graph(500, 8000, seed=d + 1)
+    ref = oegnn.EGNNLayer(d, "swish", "layer", "sum")
+    with torch.no_grad():
+        for p in ref.parameters():
+            if p.dim() == 1:
+                p.add_(0.1 * torch.randn_like(p))
+    ref64 = copy.deepcopy(ref).double()
+    h = torch.randn(g.num_nodes, d)
+    gh, gp = torch.randn(g.num_nodes, d), torch.randn(g.num_nodes, 3)
+    hr, pr = h.double().requires_grad_(True), g.pos.double().requires_grad_(True)
+    yr, qr = ref64(hr, pr, g.edge_index)
+    ((yr * gh.double()).sum() + (qr * gp.double()).sum()).backward()
+    want = [yr.detach(), qr.detach(), hr.grad, pr.grad] + [q.grad for q in ref64.parameters()]
+
+    def run(f32, gscale):
+        prev = lib.gmp_egnn_set_f32_mfma(f32)
+        try:
+            lay = gmp_amd.EGNNLayer(d, "swish", "layer", "sum")
+            lay.load_state_dict(ref.state_dict())
+            lay = lay.to(DEV)
+            hd, pd = h.to(DEV).requires_grad_(True), g.pos.to(DEV).requires_grad_(True)
+            y, q = lay(hd, pd, g.edge_index.to(DEV))
+            ((y * (gh * gscale).to(DEV)).sum() + (q * (gp * gscale).to(DEV)).sum()).backward()
+            got = [y.detach(), q.detach(), hd.grad / gscale, pd.grad / gscale]
+            got += [p.grad / gscale for p in lay.parameters()]
+            return [t.double().cpu() for t in got]
+        finally:
+            lib.gmp_egnn_set_f32_mfma(prev)
+
+    exact = run(1, 1.0)
+    for gscale in (1.0, 2.0 ** -40):
+        hf = run(0, gscale)
+        for k, (a, b, w) in enumerate(zip(hf, exact, want)):
+            scale = w.abs().max().item() + 1e-30
+            e_hf = (a - w).abs().max().item()
+            e_f32 = (b - w).abs().max().item()
+            assert e_hf <= 2 * e_f32 + 1e-6 * scale, (k, gscale, e_hf, e_f32, scale)
