@@ -183,28 +183,29 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd
 
 // ------------------------------------------------------------------ SchNet CFConv, SSP
 Tensor cfconv_aggregate(const Tensor& x, const Tensor& xidx, const Tensor& w, const Tensor& perm,
-                        const Tensor& rowptr, int64_t n_seg) {
+                        const Tensor& rowptr, int64_t n_seg, const optional<Tensor>& escale) {
   f32(x, "x");
   f32(w, "w");
   i64(xidx, "xidx");
   Tensor out = at::empty({n_seg, x.size(1)}, x.options());
   Tensor err = at::zeros({1}, x.options().dtype(at::kInt));
-  check_rc(gmp_cfconv_aggregate_f32(fp(x), x.size(0), ip(xidx), fp(w), w.size(0), x.size(1),
-                                    ip(perm), ip(rowptr), n_seg, fp(out),
-                                    err.data_ptr<int32_t>(), cur_stream()),
-           "gmp_cfconv_aggregate_f32");
+  check_rc(gmp_cfconv_aggregate_scaled_f32(fp(x), x.size(0), ip(xidx), fp(w), cfp(escale),
+                                           w.size(0), x.size(1), ip(perm), ip(rowptr), n_seg,
+                                           fp(out), err.data_ptr<int32_t>(), cur_stream()),
+           "gmp_cfconv_aggregate_scaled_f32");
   return out;
 }
 
-Tensor cfconv_wgrad(const Tensor& g, const Tensor& gidx, const Tensor& x, const Tensor& xidx) {
+Tensor cfconv_wgrad(const Tensor& g, const Tensor& gidx, const Tensor& x, const Tensor& xidx,
+                    const optional<Tensor>& escale) {
   f32(g, "g");
   f32(x, "x");
   Tensor dw = at::empty({gidx.numel(), x.size(1)}, x.options());
   Tensor err = at::zeros({1}, x.options().dtype(at::kInt));
-  check_rc(gmp_cfconv_wgrad_f32(fp(g), g.size(0), ip(gidx), fp(x), x.size(0), ip(xidx),
-                                gidx.numel(), x.size(1), fp(dw), err.data_ptr<int32_t>(),
-                                cur_stream()),
-           "gmp_cfconv_wgrad_f32");
+  check_rc(gmp_cfconv_wgrad_scaled_f32(fp(g), g.size(0), ip(gidx), fp(x), x.size(0), ip(xidx),
+                                       cfp(escale), gidx.numel(), x.size(1), fp(dw),
+                                       err.data_ptr<int32_t>(), cur_stream()),
+           "gmp_cfconv_wgrad_scaled_f32");
   return dw;
 }
 
@@ -563,10 +564,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd
           at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o)};
 }
 Tensor cfconv_aggregate(const Tensor& x, const Tensor&, const Tensor&, const Tensor&,
-                        const Tensor&, int64_t n_seg) {
+                        const Tensor&, int64_t n_seg, const optional<Tensor>&) {
   return at::empty({n_seg, x.size(1)}, x.options());
 }
-Tensor cfconv_wgrad(const Tensor&, const Tensor& gidx, const Tensor& x, const Tensor&) {
+Tensor cfconv_wgrad(const Tensor&, const Tensor& gidx, const Tensor& x, const Tensor&,
+                    const optional<Tensor>&) {
   return at::empty({gidx.numel(), x.size(1)}, x.options());
 }
 Tensor ssp_fwd(const Tensor& x, double) { return at::empty_like(x); }
@@ -681,8 +683,9 @@ TORCH_LIBRARY(gmp, m) {
         "(Tensor dA, Tensor dpos_recv, Tensor dpre1, Tensor gdiff, Tensor dpre2, Tensor dpre3, "
         "Tensor partials)");
   m.def("cfconv_aggregate(Tensor x, Tensor xidx, Tensor w, Tensor perm, Tensor rowptr, "
-        "int n_seg) -> Tensor");
-  m.def("cfconv_wgrad(Tensor g, Tensor gidx, Tensor x, Tensor xidx) -> Tensor");
+        "int n_seg, Tensor? escale=None) -> Tensor");
+  m.def("cfconv_wgrad(Tensor g, Tensor gidx, Tensor x, Tensor xidx, Tensor? escale=None) -> "
+        "Tensor");
   m.def("ssp_fwd(Tensor x, float shift) -> Tensor");
   m.def("ssp_bwd(Tensor x, Tensor grad_y) -> Tensor");
   m.def("ln_act_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, int act) -> "

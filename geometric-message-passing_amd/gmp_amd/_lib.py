@@ -86,6 +86,10 @@ SIGNATURES = {
                                                c_f32, c_vp, c_vp, c_vp, c_vp]),
     "gmp_triplet_geom_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_vp,
                                          c_vp, c_vp, c_vp, c_vp]),
+    "gmp_cfconv_aggregate_scaled_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                                c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "gmp_cfconv_wgrad_scaled_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                            c_i64, c_vp, c_vp, c_vp]),
     "gmp_gate_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp]),
     "gmp_gate_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
                                  c_vp]),

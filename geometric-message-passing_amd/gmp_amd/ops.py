@@ -628,34 +628,40 @@ def _cfconv_csr(index, n):
     return csr
 
 
-def cfconv_aggregate(x, xidx, w, csr):
-    """out[s] = sum over CSR segment s of x[xidx[e]] * w[e] (K13 gmp_cfconv_aggregate_f32)."""
-    return _lib.torch_ops().cfconv_aggregate(x, _i64c(xidx), w, csr.perm, csr.rowptr, csr.n_seg)
+def cfconv_aggregate(x, xidx, w, csr, escale=None):
+    """out[s] = sum over CSR segment s of x[xidx[e]] * (w[e] (* escale[e])) (K13
+    gmp_cfconv_aggregate_scaled_f32)."""
+    return _lib.torch_ops().cfconv_aggregate(x, _i64c(xidx), w, csr.perm, csr.rowptr, csr.n_seg,
+                                             escale)
 
 
 class CFConvAggregateFn(torch.autograd.Function):
     """PyG CFConv propagate (message x_j * W, aggr "add", dim_size = N; schnet.py:72) without
     the (E, F) message: forward and x-gradient by K13 over the receiver / sender CSR, the
-    W-gradient as the per-edge product grad[dst] * x[src]."""
+    W-gradient as the per-edge product grad[dst] * x[src].  C (optional, no gradient): the
+    per-edge cosine cutoff multiplying W (W * C.view(-1, 1) in CFConv.forward), applied at load
+    time; the W-gradient is then the gradient w.r.t. the unscaled W."""
 
     @staticmethod
-    def forward(ctx, x, W, src, dst, n):
+    def forward(ctx, x, W, src, dst, n, C=None):
         recv = _cfconv_csr(dst, n)
-        ctx.save_for_backward(x, W)
+        ctx.save_for_backward(x, W, C)
         ctx.src, ctx.dst, ctx.n = src, dst, n
-        return cfconv_aggregate(x, src, W, recv)
+        return cfconv_aggregate(x, src, W, recv, C)
 
     @staticmethod
     @once_differentiable
     def backward(ctx, g):
-        x, W = ctx.saved_tensors
+        x, W, C = ctx.saved_tensors
         g = _f32c(g)
         dx = dW = None
         if ctx.needs_input_grad[0]:
-            dx = cfconv_aggregate(g, ctx.dst, W, _cfconv_csr(ctx.src, x.shape[0]))
+            dx = cfconv_aggregate(g, ctx.dst, W, _cfconv_csr(ctx.src, x.shape[0]), C)
         if ctx.needs_input_grad[1]:
-            dW = _lib.torch_ops().cfconv_wgrad(g, _i64c(ctx.dst), x, _i64c(ctx.src))
-        return dx, dW, None, None, None
+            dW = _lib.torch_ops().cfconv_wgrad(g, _i64c(ctx.dst), x, _i64c(ctx.src), C)
+        if ctx.needs_input_grad[5]:
+            raise RuntimeError("cfconv_propagate: C must not require grad (use W * C instead)")
+        return dx, dW, None, None, None, None
 
 
 class ShiftedSoftplusFn(torch.autograd.Function):
@@ -681,12 +687,17 @@ def shifted_softplus(x, shift):
     return ShiftedSoftplusFn.apply(x, shift)
 
 
-def cfconv_propagate(edge_index, x, W):
-    """sum_{e: dst[e] = i} x[src[e]] * W[e] for edge_index = (src, dst), N = x.shape[0]."""
+def cfconv_propagate(edge_index, x, W, C=None):
+    """sum_{e: dst[e] = i} x[src[e]] * W[e] (* C[e]) for edge_index = (src, dst), N =
+    x.shape[0]; C (E,) is a per-edge factor without gradient (SchNet's cosine cutoff)."""
     x, W = _f32c(x), _f32c(W)
     _need_cuda(x, W)
+    if C is not None:
+        if C.requires_grad and torch.is_grad_enabled():
+            raise ValueError("cfconv_propagate: C must not require grad")
+        C = _f32c(C.detach().reshape(-1))
     ei = _i64c(edge_index)
-    return CFConvAggregateFn.apply(x, W, ei[0], ei[1], x.shape[0])
+    return CFConvAggregateFn.apply(x, W, ei[0], ei[1], x.shape[0], C)
 
 
 # ----------------------------------------------------------------------------------- K1 edges

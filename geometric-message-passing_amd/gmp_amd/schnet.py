@@ -60,9 +60,13 @@ class CFConv(MessagePassing):
             C = 0.5 * (torch.cos(edge_weight * math.pi / self.cutoff) + 1.0)
         else:
             C = edge_cut
-        W = self._filter(edge_attr) * C.view(-1, 1)
+        W = self._filter(edge_attr)
         x = self.lin1(x)
-        x = self.propagate(edge_index, x=x, W=W)
+        if (not (C.requires_grad and torch.is_grad_enabled()) and self.fused_supported(x, W)):
+            # K13 with the cutoff applied to W at load time: W * C is never materialised
+            x = ops.cfconv_propagate(edge_index, x, W, C)
+        else:
+            x = self.propagate(edge_index, x=x, W=W * C.view(-1, 1))
         return self.lin2(x)
 
     def _filter(self, edge_attr):

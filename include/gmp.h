@@ -546,6 +546,18 @@ int gmp_cfconv_aggregate_f32(const float* x, int64_t n_x, const int64_t* xidx, c
 int gmp_cfconv_wgrad_f32(const float* g, int64_t n_g, const int64_t* gidx, const float* x,
                          int64_t n_x, const int64_t* xidx, int64_t n_items, int64_t F, float* dw,
                          int32_t* err, void* stream);
+/* Scaled forms (SchNet W = filter(edge_attr) * C with the per-edge cosine cutoff C, never
+ * materialised): the aggregate uses W[e] * escale[e] (rounded per element as the reference's
+ * product); the W-gradient is written as (g[gidx[e]] * x[xidx[e]]) * escale[e], the gradient
+ * w.r.t. filter(edge_attr).  escale may be NULL (= the unscaled entry points). */
+int gmp_cfconv_aggregate_scaled_f32(const float* x, int64_t n_x, const int64_t* xidx,
+                                    const float* w, const float* escale, int64_t n_items,
+                                    int64_t F, const int64_t* perm, const int64_t* rowptr,
+                                    int64_t n_seg, float* out, int32_t* err, void* stream);
+int gmp_cfconv_wgrad_scaled_f32(const float* g, int64_t n_g, const int64_t* gidx, const float* x,
+                                int64_t n_x, const int64_t* xidx, const float* escale,
+                                int64_t n_items, int64_t F, float* dw, int32_t* err,
+                                void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K14 shifted softplus (PyG ShiftedSoftplus, the SchNet filter-network / interaction

@@ -30,11 +30,14 @@ def _batches(kind):
     return collate(g)
 
 
-@pytest.mark.parametrize("kind,edge_path", [("kchains", False), ("radius", False),
-                                             ("kchains", True), ("radius", True)])
-def test_schnet_vs_oracle(kind, edge_path, monkeypatch):
+@pytest.mark.parametrize("kind,edge_path,pos_grad", [
+    ("kchains", False, True), ("radius", False, True), ("kchains", True, True),
+    ("radius", True, True), ("radius", True, False), ("kchains", False, False)])
+def test_schnet_vs_oracle(kind, edge_path, pos_grad, monkeypatch):
     """edge_path: force the filter network's edge Linears onto ops.linear's EdgeLinearFn
-    (outer-sum weight gradients, K = 50 zero-padded to 64), which the bench graph takes."""
+    (outer-sum weight gradients, K = 50 zero-padded to 64), which the bench graph takes.
+    pos_grad=False (the training-step configuration): the cosine cutoff has no gradient and is
+    applied inside K13 (gmp_cfconv_*_scaled_f32) instead of materialising W * C."""
     import gmp_amd
     from gmp_amd import ops
     if edge_path:
@@ -50,16 +53,17 @@ def test_schnet_vs_oracle(kind, edge_path, monkeypatch):
                                 num_gaussians=50, cutoff=10, out_dim=2)
     model.load_state_dict(ref.state_dict(), strict=True)
     model = model.to(DEV)
-    pd = b.pos.to(DEV).requires_grad_(True)
+    pd = b.pos.to(DEV).requires_grad_(pos_grad)
     y = model(Batch(b.atoms.to(DEV), pd, b.edge_index.to(DEV), b.batch.to(DEV),
                     num_graphs=b.num_graphs))
-    pr = b.pos.clone().requires_grad_(True)
+    pr = b.pos.clone().requires_grad_(pos_grad)
     yr = ref(Batch(b.atoms, pr, b.edge_index, b.batch, num_graphs=b.num_graphs))
     torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-5, rtol=1e-5)
     g = torch.randn_like(yr)
     (y * g.to(DEV)).sum().backward()
     (yr * g).sum().backward()
-    _scaled(pd.grad, pr.grad, 1e-4, "grad_pos")
+    if pos_grad:
+        _scaled(pd.grad, pr.grad, 1e-4, "grad_pos")
     for (k, p), q in zip(model.named_parameters(), ref.parameters()):
         _scaled(p.grad, q.grad, 1e-4, k)
 
@@ -84,6 +88,29 @@ def test_cfconv_aggregate_vs_torch(F, n, E):
     (yr * g).sum().backward()
     torch.testing.assert_close(xd.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(Wd.grad.cpu(), Wr.grad, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("F,n,E", [(128, 300, 5000), (4, 7, 40)])
+def test_cfconv_scaled_vs_torch(F, n, E):
+    """K13 scaled forms: x[src] * (W * C) summed at dst with the per-edge factor C applied at
+    load time, against torch's (W * C.view(-1, 1)) message and index_add_; gradients of x and
+    W (w.r.t. the unscaled W).  Tolerance 1e-5."""
+    from gmp_amd import ops
+    gen = torch.Generator().manual_seed(F + E)
+    ei = torch.randint(0, n, (2, E), generator=gen)
+    x, W, C = torch.randn(n, F, generator=gen), torch.randn(E, F, generator=gen), torch.rand(E, generator=gen)
+    xd, Wd = x.to(DEV).requires_grad_(True), W.to(DEV).requires_grad_(True)
+    y = ops.cfconv_propagate(ei.to(DEV), xd, Wd, C.to(DEV))
+    xr, Wr = x.clone().requires_grad_(True), W.clone().requires_grad_(True)
+    yr = torch.zeros(n, F).index_add_(0, ei[1], xr[ei[0]] * (Wr * C.view(-1, 1)))
+    torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-5, rtol=1e-5)
+    g = torch.randn(n, F, generator=gen)
+    (y * g.to(DEV)).sum().backward()
+    (yr * g).sum().backward()
+    torch.testing.assert_close(xd.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(Wd.grad.cpu(), Wr.grad, atol=1e-5, rtol=1e-5)
+    with pytest.raises(ValueError):
+        ops.cfconv_propagate(ei.to(DEV), xd, Wd, C.to(DEV).requires_grad_(True))
 
 
 def test_cfconv_aggregate_out_of_range_raises():
