@@ -25,6 +25,13 @@
 //   (r / cgrp) * cldg + (r % cgrp) * cldr + col * cldn
 // so the forward adds its (n, k)-row result straight into the receivers' mul_ir output block
 // (row stride out_dim, k stride 1, w stride 2lo+1) and the backward writes row-major T.
+//
+// H2 form (NP = 2, gmp_tp_*_h2_f32, the default on the TP path): the same kernels over TWO
+// fp16 planes (x = hi + lo, 22-bit operands) of the operands scaled by powers of two — A by
+// 2^sa from a device-side max |A| (the S kernel's running max, or gmp_absmax_f32), B by 2^sb
+// from max |W2p| — with three products lo*hi + hi*lo + hi*hi per k step (dropped lo*lo
+// ~2^-22 relative) and the accumulators scaled back by 2^-(sa + sb) (exact) in the epilogue:
+// half the MFMAs, two thirds of the LDS image and of the split arithmetic of the x3 form.
 #include "gmp_common.h"
 
 namespace gmp {
@@ -34,6 +41,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -41,7 +50,6 @@ constexpr int kGT = 512;               // threads (8 waves)
 constexpr int kBM = 128, kBN = 128;    // output tile
 constexpr int kBK = 32;                // k per stage (= the bf16 MFMA k)
 constexpr int kPlane = 128 * 64;       // bytes of one plane image (128 rows x 32 bf16)
-constexpr int kStage = 6 * kPlane;     // A planes then B planes
 constexpr int kGroupM = 8;             // M tiles per tile group
 
 __device__ __forceinline__ void split3(f32x2 x, unsigned& h, unsigned& m, unsigned& l) {
@@ -55,6 +63,38 @@ __device__ __forceinline__ void split3(f32x2 x, unsigned& h, unsigned& m, unsign
   l = __builtin_bit_cast(unsigned, bl);
 }
 
+// H2: hi / lo fp16 planes of x (already scaled): x = hi + lo to 22 bits
+__device__ __forceinline__ void split2h(f32x2 x, unsigned& h, unsigned& l) {
+  const h16x2 hh = __builtin_convertvector(x, h16x2);
+  const f32x2 r = x - __builtin_convertvector(hh, f32x2);  // exact
+  const h16x2 hl = __builtin_convertvector(r, h16x2);
+  h = __builtin_bit_cast(unsigned, hh);
+  l = __builtin_bit_cast(unsigned, hl);
+}
+
+// exponent s with max 2^s < 2^15 (fp16 range with headroom) from a max |x| bit pattern
+__device__ __forceinline__ int scale_exp_bits(unsigned mx_bits) {
+  const float mx = __uint_as_float(mx_bits);
+  if (!(mx > 0.f) || !(mx < 3.0e38f)) return 0;
+  int e;
+  (void)frexpf(mx, &e);
+  const int s = 15 - e;
+  return s < -60 ? -60 : (s > 60 ? 60 : s);
+}
+
+// split of 4 f32 into NP planes (x3: bf16 hi / mid / lo; H2: fp16 hi / lo of x * fs)
+template <int NP>
+__device__ __forceinline__ void split_planes(f32x4 v, float fs, unsigned (&p)[3][2]) {
+  if constexpr (NP == 3) {
+    split3(f32x2{v[0], v[1]}, p[0][0], p[1][0], p[2][0]);
+    split3(f32x2{v[2], v[3]}, p[0][1], p[1][1], p[2][1]);
+  } else {
+    split2h(f32x2{v[0] * fs, v[1] * fs}, p[0][0], p[1][0]);
+    split2h(f32x2{v[2] * fs, v[3] * fs}, p[0][1], p[1][1]);
+    p[2][0] = p[2][1] = 0u;
+  }
+}
+
 __device__ __forceinline__ int xoff(int row, int chunk) {
   return row * 64 + 16 * (chunk ^ ((row >> 1) & 3));
 }
@@ -62,52 +102,83 @@ __device__ __forceinline__ int xoff(int row, int chunk) {
 // One k step's MFMA operands of a wave (64 x 32 output block: 4 row tiles x 2 column tiles,
 // three bf16 planes each).  The main loops hold two of them: the fragments of step s + 1 are
 // read from LDS while the MFMAs of step s run (one barrier per step).
+template <int NP>
 struct Frag {
-  bf16x8 a[4][3];
-  bf16x8 b[2][3];
+  u32x4 a[4][NP];
+  u32x4 b[2][NP];
 };
 
-__device__ __forceinline__ void load_frag(Frag& f, const unsigned char* aimg,
+template <int NP>
+__device__ __forceinline__ void load_frag(Frag<NP>& f, const unsigned char* aimg,
                                           const unsigned char* bimg, int wm, int wn, int li,
                                           int g) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int off = xoff(64 * wm + 16 * r + li, g);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) f.a[r][p] = *reinterpret_cast<const bf16x8*>(aimg + p * kPlane + off);
+    for (int p = 0; p < NP; ++p) f.a[r][p] = *reinterpret_cast<const u32x4*>(aimg + p * kPlane + off);
   }
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int off = xoff(32 * wn + 16 * c + li, g);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) f.b[c][p] = *reinterpret_cast<const bf16x8*>(bimg + p * kPlane + off);
+    for (int p = 0; p < NP; ++p) f.b[c][p] = *reinterpret_cast<const u32x4*>(bimg + p * kPlane + off);
   }
 }
 
-// acc += A B over one 32-deep step: the six plane products, smallest first
-__device__ __forceinline__ void mma_x3(f32x4 (&acc)[4][2], const Frag& f) {
+__device__ __forceinline__ bf16x8 asb(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+__device__ __forceinline__ h16x8 ash(u32x4 v) { return __builtin_bit_cast(h16x8, v); }
+
+// acc += A B over one 32-deep step, smallest products first: x3 the six bf16 plane products,
+// H2 the three fp16 ones
+template <int NP>
+__device__ __forceinline__ void mma_np(f32x4 (&acc)[4][2], const Frag<NP>& f) {
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       f32x4 t = acc[r][c];
-      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][2], f.b[c][0], t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][1], f.b[c][1], t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][0], f.b[c][2], t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][1], f.b[c][0], t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][0], f.b[c][1], t, 0, 0, 0);
-      acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[r][0], f.b[c][0], t, 0, 0, 0);
+      if constexpr (NP == 3) {
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][2]), asb(f.b[c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][1]), asb(f.b[c][1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][0]), asb(f.b[c][2]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][1]), asb(f.b[c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][0]), asb(f.b[c][1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][0]), asb(f.b[c][0]), t, 0, 0, 0);
+      } else {
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ash(f.a[r][1]), ash(f.b[c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ash(f.a[r][0]), ash(f.b[c][1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ash(f.a[r][0]), ash(f.b[c][0]), t, 0, 0, 0);
+      }
+      acc[r][c] = t;
     }
   }
 }
 
-template <bool ACC>
+// H2 scale factors of a launch: x A by 2^sa before the split, results by 2^-(sa + sb)
+struct H2Scale {
+  float fa, down;
+};
+template <int NP>
+__device__ __forceinline__ H2Scale h2_scale(const unsigned* amax, const unsigned* wmax) {
+  if constexpr (NP == 3) {
+    return H2Scale{1.f, 1.f};
+  } else {
+    const int sa = scale_exp_bits(amax[0]), sb = scale_exp_bits(wmax[0]);
+    return H2Scale{ldexpf(1.f, sa), ldexpf(1.f, -(sa + sb))};
+  }
+}
+
+template <bool ACC, int NP>
 __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
     const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
     int64_t ldb, int64_t bplane, float* __restrict__ C, int64_t cgrp, int64_t cldg,
-    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n) {
+    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const unsigned* __restrict__ amax,
+    const unsigned* __restrict__ wmax) {
+  constexpr int STG = 2 * NP * kPlane;  // LDS bytes per stage (A planes, then B planes)
   extern __shared__ __attribute__((aligned(16))) unsigned char smg[];
+  const H2Scale hs = h2_scale<NP>(amax, wmax);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
@@ -154,7 +225,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       Bp + (n0 + brow < N ? n0 + brow : (int64_t)N - 1) * ldb + 8 * bch;
 
   f32x4 ringA[2][2];
-  u32x4 ringB[2][3];
+  u32x4 ringB[2][NP];
   auto fetch = [&](int slot, int st) {
     const int stc = st < nst ? st : nst - 1;
     const int64_t k0 = (int64_t)stc * kBK;
@@ -164,7 +235,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       ringA[slot][q] = *reinterpret_cast<const f32x4*>(p);
     }
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NP; ++p)
       ringB[slot][p] = *reinterpret_cast<const u32x4*>(bbase + p * bplane + k0);
   };
   auto stash = [&](int slot, unsigned char* buf, int st) {
@@ -173,20 +244,19 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     for (int q = 0; q < 2; ++q) {
       f32x4 v = ringA[slot][q];
       if (!(live && aok[q])) v = f32x4{0.f, 0.f, 0.f, 0.f};
-      unsigned h0, m0_, l0, h1, m1, l1;
-      split3(f32x2{v[0], v[1]}, h0, m0_, l0);
-      split3(f32x2{v[2], v[3]}, h1, m1, l1);
+      unsigned pl[3][2];
+      split_planes<NP>(v, hs.fa, pl);
       const int off = xoff(arow[q], akq[q] >> 1) + 8 * (akq[q] & 1);
-      *reinterpret_cast<u32x2*>(buf + off) = u32x2{h0, h1};
-      *reinterpret_cast<u32x2*>(buf + kPlane + off) = u32x2{m0_, m1};
-      *reinterpret_cast<u32x2*>(buf + 2 * kPlane + off) = u32x2{l0, l1};
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        *reinterpret_cast<u32x2*>(buf + p * kPlane + off) = u32x2{pl[p][0], pl[p][1]};
     }
     const int off = xoff(brow, bch);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < NP; ++p) {
       u32x4 v = ringB[slot][p];
       if (!(live && bok)) v = u32x4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(buf + (3 + p) * kPlane + off) = v;
+      *reinterpret_cast<u32x4*>(buf + (NP + p) * kPlane + off) = v;
     }
   };
 
@@ -199,30 +269,30 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   //   | load stage s + 4 | barrier.
   // Stages past nst (rounded up to the unroll) load clamped addresses and stash zeros.
   const int nst_pad = (nst + 1) & ~1;
-  Frag F[2];
+  Frag<NP> F[2];
   fetch(0, 0);
   fetch(1, 1);
   stash(0, smg, 0);
   fetch(0, 2);
-  stash(1, smg + kStage, 1);
+  stash(1, smg + STG, 1);
   fetch(1, 3);
   __syncthreads();
-  load_frag(F[0], smg, smg + 3 * kPlane, wm, wn, li, g);
+  load_frag<NP>(F[0], smg, smg + NP * kPlane, wm, wn, li, g);
   __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
   for (int s0 = 0; s0 < nst_pad; s0 += 2) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int st = s0 + j;
-      const unsigned char* nb = smg + ((st + 1) & 1) * kStage;
+      const unsigned char* nb = smg + ((st + 1) & 1) * STG;
       // sched barriers pin the ring discipline: slot j's registers are consumed by the stash
       // before its next loads are issued, so the stash waits only for loads two stages old
       // (counted vmcnt) instead of the scheduler hoisting the new loads and draining vmcnt(0)
-      stash(j, smg + (st & 1) * kStage, st + 2);
+      stash(j, smg + (st & 1) * STG, st + 2);
       __builtin_amdgcn_sched_barrier(0);
       fetch(j, st + 4);
       __builtin_amdgcn_sched_barrier(0);
-      load_frag(F[j ^ 1], nb, nb + 3 * kPlane, wm, wn, li, g);
-      mma_x3(acc, F[j]);
+      load_frag<NP>(F[j ^ 1], nb, nb + NP * kPlane, wm, wn, li, g);
+      mma_np<NP>(acc, F[j]);
       __syncthreads();
     }
   }
@@ -240,8 +310,9 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
         if (row >= M) continue;
         const int64_t grp_r = row / cgrp;
         float* dst = C + grp_r * cldg + (row - grp_r * cgrp) * cldr + col * cldn;
-        if (ACC) *dst += acc[r][c][q];
-        else *dst = acc[r][c][q];
+        const float v = NP == 3 ? acc[r][c][q] : acc[r][c][q] * hs.down;
+        if (ACC) *dst += v;
+        else *dst = v;
       }
     }
   }
@@ -254,14 +325,16 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
 // non-temporal stores (T is consumed by a later kernel, far past the caches) and restart.
 // Replaces one workgroup per 128 x 128 tile, whose prologue / epilogue dominated at 4 k steps.
 constexpr int kMaxKS = 4;  // K <= 128
-template <int NKS>
+template <int NKS, int NP>
 __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
     int64_t M, int64_t N, const float* __restrict__ A, int64_t lda,
     const unsigned short* __restrict__ Bp, int64_t ldb, int64_t bplane, float* __restrict__ C,
-    int64_t ldc, int tiles_m, int tiles_n, int n_split) {
+    int64_t ldc, int tiles_m, int tiles_n, int n_split, const unsigned* __restrict__ amax,
+    const unsigned* __restrict__ wmax) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
-  unsigned char* sA = smw;                          // NKS x 3 planes
-  unsigned char* sB = smw + NKS * 3 * kPlane;       // 2 stages x 3 planes
+  unsigned char* sA = smw;                          // NKS x NP planes
+  unsigned char* sB = smw + NKS * NP * kPlane;      // 2 stages x NP planes
+  const H2Scale hs = h2_scale<NP>(amax, wmax);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
@@ -288,19 +361,18 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
     const int64_t gr = m0 + row;
     f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
     if (gr < M) x = *reinterpret_cast<const f32x4*>(A + gr * lda + 32 * st + 4 * kq);
-    unsigned h0, m_, l0, h1, m1, l1;
-    split3(f32x2{x[0], x[1]}, h0, m_, l0);
-    split3(f32x2{x[2], x[3]}, h1, m1, l1);
-    unsigned char* img = sA + st * 3 * kPlane;
+    unsigned pl[3][2];
+    split_planes<NP>(x, hs.fa, pl);
+    unsigned char* img = sA + st * NP * kPlane;
     const int off = xoff(row, kq >> 1) + 8 * (kq & 1);
-    *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
-    *reinterpret_cast<u32x2*>(img + kPlane + off) = u32x2{m_, m1};
-    *reinterpret_cast<u32x2*>(img + 2 * kPlane + off) = u32x2{l0, l1};
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      *reinterpret_cast<u32x2*>(img + p * kPlane + off) = u32x2{pl[p][0], pl[p][1]};
   }
 
   const int brow = tid >> 2, bch = tid & 3;
   const int nst = (int)((t1 - t0) * NKS);
-  u32x4 ringB[2][3];
+  u32x4 ringB[2][NP];
   bool bok_slot[2];
   auto fetch = [&](int slot, int gs) {
     const int gsc = gs < nst ? gs : nst - 1;
@@ -309,12 +381,12 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
     bok_slot[slot] = gs < nst && n < N;
     const unsigned short* p = Bp + (n < N ? n : N - 1) * ldb + k0 + 8 * bch;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) ringB[slot][pl] = *reinterpret_cast<const u32x4*>(p + pl * bplane);
+    for (int pl = 0; pl < NP; ++pl) ringB[slot][pl] = *reinterpret_cast<const u32x4*>(p + pl * bplane);
   };
   auto stash = [&](int slot, unsigned char* buf) {
     const int off = xoff(brow, bch);
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < NP; ++pl) {
       u32x4 v = ringB[slot][pl];
       if (!bok_slot[slot]) v = u32x4{0u, 0u, 0u, 0u};
       *reinterpret_cast<u32x4*>(buf + pl * kPlane + off) = v;
@@ -332,7 +404,9 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int64_t row = m0 + 64 * wm + 16 * r + 4 * g + q;
-          if (row < M && col < N) __builtin_nontemporal_store(acc[r][c][q], C + row * ldc + col);
+          if (row < M && col < N)
+            __builtin_nontemporal_store(NP == 3 ? acc[r][c][q] : acc[r][c][q] * hs.down,
+                                        C + row * ldc + col);
         }
         acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -341,28 +415,28 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
 
   // same pipeline as tp_gemm_x3_kernel over the global step index gs (tile t0 + gs / NKS, k
   // step gs % NKS); A fragments from the resident images, B through two LDS stages
-  Frag F[2];
+  Frag<NP> F[2];
   fetch(0, 0);
   fetch(1, 1);
   stash(0, sB);
   fetch(0, 2);
-  stash(1, sB + 3 * kPlane);
+  stash(1, sB + NP * kPlane);
   fetch(1, 3);
   __syncthreads();  // A images and B stages 0, 1
-  load_frag(F[0], sA, sB, wm, wn, li, g);
+  load_frag<NP>(F[0], sA, sB, wm, wn, li, g);
   __syncthreads();
   const int nst_pad = (nst + 1) & ~1;
   for (int s0 = 0; s0 < nst_pad; s0 += 2) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int gs = s0 + j;
-      stash(j, sB + (gs & 1) * 3 * kPlane);
+      stash(j, sB + (gs & 1) * NP * kPlane);
       __builtin_amdgcn_sched_barrier(0);
       fetch(j, gs + 4);
       __builtin_amdgcn_sched_barrier(0);
-      load_frag(F[j ^ 1], sA + ((gs + 1) % NKS) * 3 * kPlane, sB + ((gs + 1) & 1) * 3 * kPlane,
-                wm, wn, li, g);
-      mma_x3(acc, F[j]);
+      load_frag<NP>(F[j ^ 1], sA + ((gs + 1) % NKS) * NP * kPlane,
+                    sB + ((gs + 1) & 1) * NP * kPlane, wm, wn, li, g);
+      mma_np<NP>(acc, F[j]);
       if (gs < nst && gs % NKS == NKS - 1) store_tile(t0 + gs / NKS);
       __syncthreads();
     }
@@ -374,12 +448,25 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
 //   Bt[p][u H + j][w] = W2[(u mo + w), j]                                         (backward B)
 // grid (H / 64, mul1), 256 threads: the (mo x 64) block of W2 rows u mo .. u mo + mo - 1,
 // columns j0 .. j0 + 63 goes through LDS (transpose for Bf); Bt rows are written directly.
+// (NP = 2: hi / lo fp16 planes of the values scaled by 2^sb, sb from *wmax = max |W2p|, |b2p|)
+template <int NP>
+__device__ __forceinline__ void split1(float v, float fs, unsigned (&p)[3]) {
+  if constexpr (NP == 3) {
+    split3(f32x2{v, 0.f}, p[0], p[1], p[2]);
+  } else {
+    split2h(f32x2{v * fs, 0.f}, p[0], p[1]);
+    p[2] = 0u;
+  }
+}
+template <int NP>
 __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int H,
                                                           const float* __restrict__ W2,
                                                           const float* __restrict__ b2,
                                                           unsigned short* __restrict__ Bf,
-                                                          unsigned short* __restrict__ Bt) {
+                                                          unsigned short* __restrict__ Bt,
+                                                          const unsigned* __restrict__ wmax) {
   __shared__ float tile[128][65];
+  const float fs = NP == 3 ? 1.f : ldexpf(1.f, scale_exp_bits(wmax ? wmax[0] : 0u));
   const int u = blockIdx.y, j0 = blockIdx.x * 64, tid = threadIdx.x;
   const int64_t K1 = (int64_t)mul1 * H, ldf = K1 + mul1;
   const int64_t pf = (int64_t)mo * ldf, pt = K1 * mo;
@@ -393,33 +480,30 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
   for (int x = tid; Bf && x < mo * 64; x += 256) {
     const int wr = x >> 6, j = x & 63;
     if (j0 + j >= H) continue;
-    unsigned h, m, l;
-    split3(f32x2{tile[wr][j], 0.f}, h, m, l);
+    unsigned p[3];
+    split1<NP>(tile[wr][j], fs, p);
     const int64_t o = (int64_t)wr * ldf + (int64_t)u * H + j0 + j;
-    Bf[o] = (unsigned short)h;
-    Bf[pf + o] = (unsigned short)m;
-    Bf[2 * pf + o] = (unsigned short)l;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) Bf[q * pf + o] = (unsigned short)p[q];
   }
   if (Bt) {  // Bt[p][u H + j0 + j][w]: rows k, mo consecutive w
     for (int x = tid; x < mo * 64; x += 256) {
       const int j = x / mo, wr = x - j * mo;
       if (j0 + j >= H) continue;
-      unsigned h, m, l;
-      split3(f32x2{tile[wr][j], 0.f}, h, m, l);
+      unsigned p[3];
+      split1<NP>(tile[wr][j], fs, p);
       const int64_t o = ((int64_t)u * H + j0 + j) * mo + wr;
-      Bt[o] = (unsigned short)h;
-      Bt[pt + o] = (unsigned short)m;
-      Bt[2 * pt + o] = (unsigned short)l;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) Bt[q * pt + o] = (unsigned short)p[q];
     }
   }
   if (Bf && blockIdx.x == 0) {  // bias columns of Bf: Bf[p][w][K1 + u]
     for (int wr = tid; wr < mo; wr += 256) {
-      unsigned h, m, l;
-      split3(f32x2{b2[(int64_t)u * mo + wr], 0.f}, h, m, l);
+      unsigned p[3];
+      split1<NP>(b2[(int64_t)u * mo + wr], fs, p);
       const int64_t o = (int64_t)wr * ldf + K1 + u;
-      Bf[o] = (unsigned short)h;
-      Bf[pf + o] = (unsigned short)m;
-      Bf[2 * pf + o] = (unsigned short)l;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) Bf[q * pf + o] = (unsigned short)p[q];
     }
   }
 }
@@ -429,26 +513,26 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
 
 using namespace gmp;
 
-extern "C" {
-
-int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
-                        const float* b2p, void* Bf, void* Bt, void* stream) {
+template <int NP>
+int split_w2_launch(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p, const float* b2p,
+                    const unsigned* wmax, void* Bf, void* Bt, void* stream) {
   GMP_CHECK_ARG(mul1 > 0 && mul_out > 0 && mul_out <= 128 && H > 0 && mul1 <= 65535);
-  GMP_CHECK_ARG(W2p && b2p && (Bf || Bt));
-  tp_split_w2_kernel<<<dim3((unsigned)ceil_div(H, 64), (unsigned)mul1), 256, 0,
-                       as_stream(stream)>>>((int)mul1, (int)mul_out, (int)H, W2p, b2p,
-                                            static_cast<unsigned short*>(Bf),
-                                            static_cast<unsigned short*>(Bt));
+  GMP_CHECK_ARG(W2p && b2p && (Bf || Bt) && (NP == 3 || wmax));
+  tp_split_w2_kernel<NP><<<dim3((unsigned)ceil_div(H, 64), (unsigned)mul1), 256, 0,
+                           as_stream(stream)>>>((int)mul1, (int)mul_out, (int)H, W2p, b2p,
+                                                static_cast<unsigned short*>(Bf),
+                                                static_cast<unsigned short*>(Bt), wmax);
   return launch_status();
 }
 
-int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
-                       int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
-                       int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
-                       int64_t cldn, int accumulate, void* stream) {
+template <int NP>
+int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1, int64_t K2,
+                const float* A2, int64_t lda2, const void* Bp, int64_t ldb, int64_t bplane,
+                const unsigned* amax, const unsigned* wmax, float* C, int64_t cgrp,
+                int64_t cldg, int64_t cldr, int64_t cldn, int accumulate, void* stream) {
   GMP_CHECK_ARG(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && cgrp >= 1);
   if (M == 0 || N == 0) return GMP_OK;
-  GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2));
+  GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2) && (NP == 3 || (amax && wmax)));
   GMP_CHECK_ARG(K1 % kBK == 0 && K2 % kBK == 0 && K1 + K2 > 0);
   GMP_CHECK_ARG(lda1 % 4 == 0 && (K2 == 0 || lda2 % 4 == 0) && ldb % 8 == 0 && bplane % 8 == 0);
   GMP_CHECK_ARG(ldb >= K1 + K2 && lda1 >= K1 && (K2 == 0 || lda2 >= K2));
@@ -458,9 +542,9 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
   GMP_CHECK_ARG(tiles_m < (1LL << 31) && tiles_n < (1LL << 31));
   const int64_t nwg = tiles_m * tiles_n;
   GMP_CHECK_ARG(nwg < (1LL << 32));
-  const size_t smem = 2 * (size_t)kStage;
+  const size_t smem = 2 * (size_t)(2 * NP * kPlane);
   int rc = 0;
-  auto k = accumulate ? tp_gemm_x3_kernel<true> : tp_gemm_x3_kernel<false>;
+  auto k = accumulate ? tp_gemm_x3_kernel<true, NP> : tp_gemm_x3_kernel<false, NP>;
   if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)smem))))
@@ -468,17 +552,18 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
   k<<<(unsigned)nwg, kGT, smem, as_stream(stream)>>>(
       M, (int)N, K1, A1, lda1, K2, K2 ? A2 : A1, K2 ? lda2 : lda1,
       static_cast<const unsigned short*>(Bp), ldb, bplane, C, cgrp, cldg, cldr, cldn,
-      (int)tiles_m, (int)tiles_n);
+      (int)tiles_m, (int)tiles_n, amax, wmax);
   return launch_status();
 }
 
-int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
-                             const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
-                             void* stream) {
+template <int NP>
+int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const void* Bp,
+                 int64_t ldb, int64_t bplane, const unsigned* amax, const unsigned* wmax,
+                 float* C, int64_t ldc, void* stream) {
   GMP_CHECK_ARG(M >= 0 && N >= 0 && K > 0 && K % kBK == 0 && K <= kBK * kMaxKS);
   if (M == 0 || N == 0) return GMP_OK;
   GMP_CHECK_ARG(A && Bp && C && lda >= K && lda % 4 == 0 && ldb >= K && ldb % 8 == 0 &&
-                bplane % 8 == 0 && ldc >= N);
+                bplane % 8 == 0 && ldc >= N && (NP == 3 || (amax && wmax)));
   GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
   const int64_t tiles_m = ceil_div(M, kBM), tiles_n = ceil_div(N, kBN);
   GMP_CHECK_ARG(tiles_m < (1LL << 30) && tiles_n < (1LL << 30));
@@ -490,19 +575,19 @@ int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, in
   const int64_t nwg = tiles_m * n_split;
   GMP_CHECK_ARG(nwg < (1LL << 32));
   const int nks = (int)(K / kBK);
-  const size_t smem = (size_t)(nks * 3 + 6) * kPlane;
+  const size_t smem = (size_t)(nks * NP + 2 * NP) * kPlane;
   hipStream_t s = as_stream(stream);
   const unsigned short* B = static_cast<const unsigned short*>(Bp);
   int rc = 0;
 #define GMP_WN(NK)                                                                               \
   {                                                                                              \
-    auto k = tp_gemm_x3_widen_kernel<NK>;                                                        \
+    auto k = tp_gemm_x3_widen_kernel<NK, NP>;                                                    \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                      \
                                             hipFuncAttributeMaxDynamicSharedMemorySize,         \
                                             (int)smem))))                                        \
       return rc;                                                                                 \
     k<<<(unsigned)nwg, kGT, smem, s>>>(M, N, A, lda, B, ldb, bplane, C, ldc, (int)tiles_m,       \
-                                       (int)tiles_n, (int)n_split);                              \
+                                       (int)tiles_n, (int)n_split, amax, wmax);                  \
   }
   switch (nks) {
     case 1: GMP_WN(1) break;
@@ -512,6 +597,48 @@ int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, in
   }
 #undef GMP_WN
   return launch_status();
+}
+
+extern "C" {
+
+int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
+                        const float* b2p, void* Bf, void* Bt, void* stream) {
+  return split_w2_launch<3>(mul1, mul_out, H, W2p, b2p, nullptr, Bf, Bt, stream);
+}
+
+int gmp_tp_split_w2_h2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
+                           const float* b2p, const uint32_t* wmax, void* Bf, void* Bt,
+                           void* stream) {
+  return split_w2_launch<2>(mul1, mul_out, H, W2p, b2p, wmax, Bf, Bt, stream);
+}
+
+int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
+                       int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
+                       int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
+                       int64_t cldn, int accumulate, void* stream) {
+  return gemm_launch<3>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, nullptr, nullptr, C,
+                        cgrp, cldg, cldr, cldn, accumulate, stream);
+}
+
+int gmp_tp_gemm_h2_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
+                       int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
+                       int64_t bplane, const uint32_t* amax, const uint32_t* wmax, float* C,
+                       int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, int accumulate,
+                       void* stream) {
+  return gemm_launch<2>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, amax, wmax, C, cgrp,
+                        cldg, cldr, cldn, accumulate, stream);
+}
+
+int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                             const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
+                             void* stream) {
+  return widen_launch<3>(M, N, K, A, lda, Bp, ldb, bplane, nullptr, nullptr, C, ldc, stream);
+}
+
+int gmp_tp_gemm_h2_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                             const void* Bp, int64_t ldb, int64_t bplane, const uint32_t* amax,
+                             const uint32_t* wmax, float* C, int64_t ldc, void* stream) {
+  return widen_launch<2>(M, N, K, A, lda, Bp, ldb, bplane, amax, wmax, C, ldc, stream);
 }
 
 }  // extern "C"

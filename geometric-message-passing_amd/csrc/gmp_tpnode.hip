@@ -28,12 +28,23 @@ constexpr int kMaxH = 256;
 // receiver for kOuterRB >= w / 64; measured slower than one 64-row block per workgroup: 10.1
 // vs 9.1 ms for the 32.8 GB MACE-128 lo = 2 path -- fewer workgroups in flight per CU)
 constexpr int kOuterRB = 1;
+// max |S|, |Sb| of the launch into *amax (float bit pattern, atomicMax; NULL = off): the scale
+// of the H2 path GEMM's A operand
+__device__ __forceinline__ void amax_commit(unsigned* amax, float v) {
+  if (!amax) return;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(v));
+}
+
 __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
                                                             const int64_t* __restrict__ eoff,
                                                             const float* __restrict__ Z,
                                                             const float* __restrict__ A,
                                                             float* __restrict__ S,
-                                                            float* __restrict__ Sb) {
+                                                            float* __restrict__ Sb,
+                                                            unsigned* __restrict__ amax) {
+  float lmax = 0.f;
   __shared__ __attribute__((aligned(16))) float sA[kEdgeStage * (kMaxH + 16)];
   const int n = blockIdx.y;
   const int LDA = H + 16;  // 16 mod 64 floats: the 4 edge rows of an MFMA read hit disjoint banks
@@ -87,12 +98,18 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       if (r < w) {
 #pragma unroll
         for (int t = 0; t < kMaxH / 16; ++t)
-          if (t < TJ) *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
+          if (t < TJ) {
+            *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
+            lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
+                                     fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
+          }
       }
       zsum += __shfl_xor(zsum, 16);
       zsum += __shfl_xor(zsum, 32);
       if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
+      if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
     }
+    amax_commit(amax, lmax);
     return;
   }
   if (deg <= kEdgeStage) {  // stage a once for all row blocks
@@ -138,13 +155,18 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
     if (r < w) {  // streaming stores: S (GBs per chunk) is consumed by the next GEMM from HBM
 #pragma unroll
       for (int t = 0; t < kMaxH / 16; ++t)
-        if (t < TJ)
+        if (t < TJ) {
           *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
+          lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
+                                   fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
+        }
     }
     zsum += __shfl_xor(zsum, 16);
     zsum += __shfl_xor(zsum, 32);
     if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
+    if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
   }
+  amax_commit(amax, lmax);
 }
 
 // ---------------------------------------------------------------------------------- apply
@@ -511,8 +533,9 @@ int gmp_tp_apply_set_x3(int on) {
 }
 
 
-int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
-                          const float* Z, const float* A, float* S, float* Sb, void* stream) {
+int gmp_tp_node_outer_amax_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
+                               const float* Z, const float* A, float* S, float* Sb,
+                               uint32_t* amax, void* stream) {
   GMP_CHECK_ARG(n_recv >= 0 && w > 0 && H > 0 && H <= kMaxH && H % 16 == 0);
   GMP_CHECK_ARG(n_recv <= 65535 * 1024);
   if (n_recv == 0) return GMP_OK;
@@ -520,8 +543,14 @@ int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0);
   if (n_recv > 65535) return GMP_ERR_UNSUPPORTED;  // grid.y limit: caller chunks receivers
   const dim3 grid((unsigned)ceil_div(w, kRowsPerBlock * kOuterRB), (unsigned)n_recv);
-  tp_node_outer_kernel<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb);
+  tp_node_outer_kernel<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb,
+                                                             amax);
   return launch_status();
+}
+
+int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
+                          const float* Z, const float* A, float* S, float* Sb, void* stream) {
+  return gmp_tp_node_outer_amax_f32(n_recv, w, H, eoff, Z, A, S, Sb, nullptr, stream);
 }
 
 int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,

@@ -435,14 +435,69 @@ std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t co
 }
 
 // ------------------------------------------------------------------ K7 node form
+uint32_t* u32p(const optional<Tensor>& t) {
+  return t.has_value() ? reinterpret_cast<uint32_t*>(t->data_ptr<int32_t>()) : nullptr;
+}
+const uint32_t* u32p(const Tensor& t) {
+  return reinterpret_cast<const uint32_t*>(t.data_ptr<int32_t>());
+}
+
 std::tuple<Tensor, Tensor> tp_node_outer(const Tensor& eoff, const Tensor& Z, const Tensor& A,
-                                         int64_t w) {
+                                         int64_t w, const optional<Tensor>& amax) {
   const int64_t c = eoff.numel() - 1, H = A.size(1);
   Tensor S = at::empty({c, w, H}, A.options()), Sb = at::empty({c, w}, A.options());
-  check_rc(gmp_tp_node_outer_f32(c, w, H, ip(i64(eoff, "eoff")), fp(Z), fp(f32(A, "A")), fp(S),
-                                 fp(Sb), cur_stream()),
-           "gmp_tp_node_outer_f32");
+  check_rc(gmp_tp_node_outer_amax_f32(c, w, H, ip(i64(eoff, "eoff")), fp(Z), fp(f32(A, "A")),
+                                      fp(S), fp(Sb), u32p(amax), cur_stream()),
+           "gmp_tp_node_outer_amax_f32");
   return {S, Sb};
+}
+
+void absmax(const Tensor& x, Tensor amax) {
+  f32(x, "x");
+  check_rc(gmp_absmax_f32(fp(x), x.numel(), reinterpret_cast<uint32_t*>(amax.data_ptr<int32_t>()),
+                          cur_stream()),
+           "gmp_absmax_f32");
+}
+
+Tensor tp_split_w2_h2(const Tensor& W2, const Tensor& b2, int64_t off, int64_t mul1, int64_t mo,
+                      bool fwd, const Tensor& wmax) {
+  f32(W2, "W2");
+  f32(b2, "b2");
+  const int64_t H = W2.size(1), K1 = mul1 * H;
+  Tensor planes = at::empty({fwd ? 2 * mo * (K1 + mul1) : 2 * K1 * mo},
+                            W2.options().dtype(at::kShort));
+  check_rc(gmp_tp_split_w2_h2_f32(mul1, mo, H, fp(W2) + off * H, fp(b2) + off, u32p(wmax),
+                                  fwd ? planes.data_ptr() : nullptr,
+                                  fwd ? nullptr : planes.data_ptr(), cur_stream()),
+           "gmp_tp_split_w2_h2_f32");
+  return planes;
+}
+
+void tp_gemm_h2(const Tensor& A1, int64_t K1, const optional<Tensor>& A2, int64_t K2,
+                const Tensor& Bp, int64_t ldb, int64_t N, Tensor C, int64_t c_offset,
+                int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, bool accumulate,
+                const Tensor& amax, const Tensor& wmax) {
+  f32(A1, "A1");
+  need(Bp, at::kShort, "B planes");
+  TORCH_CHECK(C.is_cuda() && C.scalar_type() == at::kFloat, "gmp.tp_gemm_h2: C");
+  const int64_t M = A1.size(0);
+  check_rc(gmp_tp_gemm_h2_f32(M, N, K1, fp(A1), A1.size(1), K2, cfp(A2),
+                              A2.has_value() ? A2->size(1) : 0, Bp.data_ptr(), ldb, N * ldb,
+                              u32p(amax), u32p(wmax), C.data_ptr<float>() + c_offset, cgrp, cldg,
+                              cldr, cldn, accumulate, cur_stream()),
+           "gmp_tp_gemm_h2_f32");
+}
+
+Tensor tp_gemm_h2_widen(const Tensor& A, const Tensor& Bp, int64_t N, const Tensor& amax,
+                        const Tensor& wmax) {
+  f32(A, "A");
+  need(Bp, at::kShort, "B planes");
+  const int64_t M = A.size(0), K = A.size(1);
+  Tensor C = at::empty({M, N}, A.options());
+  check_rc(gmp_tp_gemm_h2_widen_f32(M, N, K, fp(A), K, Bp.data_ptr(), K, N * K, u32p(amax),
+                                    u32p(wmax), fp(C), N, cur_stream()),
+           "gmp_tp_gemm_h2_widen_f32");
+  return C;
 }
 
 void tp_node_apply(const Tensor& eoff, const Tensor& Z, const Tensor& A, const Tensor& T,
@@ -642,9 +697,22 @@ std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t co
                                        x.options())};
 }
 std::tuple<Tensor, Tensor> tp_node_outer(const Tensor& eoff, const Tensor&, const Tensor& A,
-                                         int64_t w) {
+                                         int64_t w, const optional<Tensor>&) {
   const int64_t c = eoff.numel() - 1;
   return {at::empty({c, w, A.size(1)}, A.options()), at::empty({c, w}, A.options())};
+}
+void absmax(const Tensor&, Tensor) {}
+Tensor tp_split_w2_h2(const Tensor& W2, const Tensor&, int64_t, int64_t mul1, int64_t mo,
+                      bool fwd, const Tensor&) {
+  const int64_t K1 = mul1 * W2.size(1);
+  return at::empty({fwd ? 2 * mo * (K1 + mul1) : 2 * K1 * mo}, W2.options().dtype(at::kShort));
+}
+void tp_gemm_h2(const Tensor&, int64_t, const optional<Tensor>&, int64_t, const Tensor&, int64_t,
+                int64_t, Tensor, int64_t, int64_t, int64_t, int64_t, int64_t, bool,
+                const Tensor&, const Tensor&) {}
+Tensor tp_gemm_h2_widen(const Tensor& A, const Tensor&, int64_t N, const Tensor&,
+                        const Tensor&) {
+  return at::empty({A.size(0), N}, A.options());
 }
 void tp_node_apply(const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&,
                    Tensor, Tensor) {}
@@ -716,7 +784,15 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor? A3) -> Tensor");
   m.def("symmetric_contraction_bwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
         "Tensor? A3, Tensor gout) -> (Tensor dx, Tensor dA_partials)");
-  m.def("tp_node_outer(Tensor eoff, Tensor Z, Tensor A, int w) -> (Tensor S, Tensor Sb)");
+  m.def("tp_node_outer(Tensor eoff, Tensor Z, Tensor A, int w, Tensor(a!)? amax=None) -> "
+        "(Tensor S, Tensor Sb)");
+  m.def("absmax(Tensor x, Tensor(a!) amax) -> ()");
+  m.def("tp_split_w2_h2(Tensor W2, Tensor b2, int off, int mul1, int mul_out, bool fwd, "
+        "Tensor wmax) -> Tensor");
+  m.def("tp_gemm_h2(Tensor A1, int K1, Tensor? A2, int K2, Tensor Bp, int ldb, int N, "
+        "Tensor(a!) C, int c_offset, int cgrp, int cldg, int cldr, int cldn, bool accumulate, "
+        "Tensor amax, Tensor wmax) -> ()");
+  m.def("tp_gemm_h2_widen(Tensor A, Tensor Bp, int N, Tensor amax, Tensor wmax) -> Tensor");
   m.def("tp_node_apply(Tensor eoff, Tensor Z, Tensor A, Tensor T, Tensor Tb, Tensor(a!) dA, "
         "Tensor(b!) dZ) -> ()");
   m.def("tp_split_w2(Tensor W2, Tensor b2, int off, int mul1, int mul_out, bool fwd) -> Tensor");
@@ -754,6 +830,10 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("symmetric_contraction_fwd", ns symmetric_contraction_fwd);      \
   m.impl("symmetric_contraction_bwd", ns symmetric_contraction_bwd);      \
   m.impl("tp_node_outer", ns tp_node_outer);                              \
+  m.impl("absmax", ns absmax);                                            \
+  m.impl("tp_split_w2_h2", ns tp_split_w2_h2);                            \
+  m.impl("tp_gemm_h2", ns tp_gemm_h2);                                    \
+  m.impl("tp_gemm_h2_widen", ns tp_gemm_h2_widen);                        \
   m.impl("tp_node_apply", ns tp_node_apply);                              \
   m.impl("tp_split_w2", ns tp_split_w2);                                  \
   m.impl("tp_gemm_x3", ns tp_gemm_x3);                                    \

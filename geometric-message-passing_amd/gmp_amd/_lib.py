@@ -90,6 +90,16 @@ SIGNATURES = {
                                                 c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "gmp_cfconv_wgrad_scaled_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                             c_i64, c_vp, c_vp, c_vp]),
+    "gmp_tp_split_w2_h2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                       c_vp]),
+    "gmp_tp_gemm_h2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
+                                   c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
+                                   c_int, c_vp]),
+    "gmp_tp_gemm_h2_widen_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                         c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "gmp_absmax_f32": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "gmp_tp_node_outer_amax_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp]),
     "gmp_gate_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp]),
     "gmp_gate_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
                                  c_vp]),

@@ -539,6 +539,11 @@ def node_form_ok(hidden):
 # Path GEMMs of the node form: "x3" = K7g (gmp_tpgemm.hip: bf16 MFMA over exact three-plane f32
 # splits; dW2p by the column-block split-plane outer sum), "torch" = the library f32 GEMMs.
 TP_GEMM = os.environ.get("GMP_TP_GEMM", "x3")
+# K7g's forward and T GEMMs in the H2 form (two fp16 planes with power-of-two scaling from
+# device-side max words, three MFMA products per step; gmp_tp_gemm_h2_f32): off by default —
+# measured slower on C4 (2.89 vs 2.66 s/step: every wave of the S kernel folds its max into
+# one word) and its 2^-21 products exceed the C4 rotation-invariance bound at 1M edges.
+TP_H2 = os.environ.get("GMP_TP_H2", "0") == "1"
 
 
 def _x3_ok(P, H):
@@ -547,10 +552,28 @@ def _x3_ok(P, H):
             and P["mul_out"] <= 128 and H % 32 == 0)
 
 
-def _split_w2(lib, W2, b2, P, fwd):
+def _split_w2(lib, W2, b2, P, fwd, wmax=None):
     """Three bf16 planes of path P's W2 / b2 block: forward (B = [W2p | b2p]^T as [w][(u, j) ++ u])
-    or backward (B = W2p as [(u, j)][w]) layout (torch.ops.gmp.tp_split_w2)."""
+    or backward (B = W2p as [(u, j)][w]) layout (torch.ops.gmp.tp_split_w2); with `wmax` (the
+    path block's max-|x| word, _w2_max) the two scaled fp16 planes of the H2 form."""
+    if wmax is not None:
+        return _lib.torch_ops().tp_split_w2_h2(W2, b2, P["w_off"], P["mul1"], P["mul_out"], fwd,
+                                               wmax)
     return _lib.torch_ops().tp_split_w2(W2, b2, P["w_off"], P["mul1"], P["mul_out"], fwd)
+
+
+def _amax_word(device):
+    return torch.zeros(1, dtype=torch.int32, device=device)
+
+
+def _w2_max(W2, b2, P):
+    """max |W2p|, |b2p| of path P as a device word (float bit pattern) for the H2 B scale."""
+    m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
+    w = _amax_word(W2.device)
+    ops_ = _lib.torch_ops()
+    ops_.absmax(W2[off:off + m1 * mo], w)
+    ops_.absmax(b2[off:off + m1 * mo], w)
+    return w
 
 
 class TPConvNodeFn(torch.autograd.Function):
@@ -579,24 +602,33 @@ class TPConvNodeFn(torch.autograd.Function):
         x3 = [_x3_ok(P, H) for P in plan.instructions]
         W2x = [None if ok else _w2_path(W2, b2, P) for P, ok in zip(plan.instructions, x3)]
         Bfs = [None] * len(x3)
+        wmaxs = [_w2_max(W2c, b2c, P) if (ok and TP_H2) else None
+                 for P, ok in zip(plan.instructions, x3)]
         for n0, n1, e0, e1, eoff, a, zbuf, _ in _node_chunks(lib, plan, graph, x, sh, rad_s,
                                                              W1, b1):
             c, ne = n1 - n0, e1 - e0
             for i, (P, (zoff, w)) in enumerate(zip(plan.instructions, plan.z_regions)):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a)
+                amax = _amax_word(dev) if wmaxs[i] is not None else None
+                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a, amax)
                 blk = plan.blocks[P["io"]]
                 if x3[i]:
                     # out[n, blk + w' d3 + k] += [S | Sb][(n, k), :] [W2p ; b2p][:, w'] (K7g)
                     if Bfs[i] is None:
-                        Bfs[i] = _split_w2(lib, W2c, b2c, P, True)
+                        Bfs[i] = _split_w2(lib, W2c, b2c, P, True, wmaxs[i])
                     K1 = m1 * H
                     with _timed("tp_node_W"):
-                        _lib.torch_ops().tp_gemm_x3(S.view(c * d3, K1), K1, Sb.view(c * d3, m1),
-                                                    m1, Bfs[i], K1 + m1, mo, out,
-                                                    n0 * out.shape[1] + blk[0], d3, out.shape[1],
-                                                    1, d3, True)
+                        if amax is not None:
+                            _lib.torch_ops().tp_gemm_h2(
+                                S.view(c * d3, K1), K1, Sb.view(c * d3, m1), m1, Bfs[i], K1 + m1,
+                                mo, out, n0 * out.shape[1] + blk[0], d3, out.shape[1], 1, d3,
+                                True, amax, wmaxs[i])
+                        else:
+                            _lib.torch_ops().tp_gemm_x3(
+                                S.view(c * d3, K1), K1, Sb.view(c * d3, m1), m1, Bfs[i], K1 + m1,
+                                mo, out, n0 * out.shape[1] + blk[0], d3, out.shape[1], 1, d3,
+                                True)
                     continue
                 W2p, b2p = W2x[i]
                 with _timed("tp_node_W"):
@@ -627,6 +659,8 @@ class TPConvNodeFn(torch.autograd.Function):
         W2x = [_w2_path(W2, b2, P) for P in plan.instructions]
         dW2x = [(torch.zeros_like(wp), torch.zeros_like(bp)) for wp, bp in W2x]
         Bts = [None] * len(x3)
+        wmaxs = [_w2_max(W2c, b2c, P) if (ok and TP_H2) else None
+                 for P, ok in zip(plan.instructions, x3)]
         first = True
         for n0, n1, e0, e1, eoff, a, zbuf, pre in _node_chunks(lib, plan, graph, x, sh, rad_s,
                                                                W1, b1):
@@ -653,10 +687,15 @@ class TPConvNodeFn(torch.autograd.Function):
                         db2p.addmm_(Sb.view(c * d3, -1).t(), G)
                     del S, Sb
                     if Bts[i] is None:
-                        Bts[i] = _split_w2(lib, W2c, b2c, P, False)
+                        Bts[i] = _split_w2(lib, W2c, b2c, P, False, wmaxs[i])
                     with _timed("tp_node_W"):
                         # T[(n, k), (u, j)] = sum_w G[(n, k), w] W2p[(u, j), w]
-                        T = _lib.torch_ops().tp_gemm_x3_widen(G, Bts[i], K1)
+                        if wmaxs[i] is not None:
+                            gmax = _amax_word(G.device)
+                            _lib.torch_ops().absmax(G, gmax)
+                            T = _lib.torch_ops().tp_gemm_h2_widen(G, Bts[i], K1, gmax, wmaxs[i])
+                        else:
+                            T = _lib.torch_ops().tp_gemm_x3_widen(G, Bts[i], K1)
                         Tb = G.mm(b2p.t())
                 else:
                     with _timed("tp_node_dW"):
@@ -694,9 +733,9 @@ class TPConvNodeFn(torch.autograd.Function):
         return dx, dsh, drad, dW1, db1, dW2, db2, None, None
 
 
-def _node_outer(lib, c, w, H, eoff, Zp, a):
+def _node_outer(lib, c, w, H, eoff, Zp, a, amax=None):
     with _timed("tp_node_S"):
-        return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w)
+        return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w, amax)
 
 
 def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):

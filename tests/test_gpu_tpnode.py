@@ -258,3 +258,91 @@ def test_node_apply_bf16x3_matches_fp64(w, H, x3):
         ez = ((dZ[e0:e1].cpu().double() - rz).abs() / mz).max().item()
         ea = ((dA[e0:e1].cpu().double() - ra).abs() / ma).max().item()
         assert ez < 1e-6 and ea < 1e-6, (n, degs[n], ez, ea)
+
+
+def _h2_case(m1, mo, H, seed, wscale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    W2 = torch.randn(m1 * mo, H, generator=g) * torch.logspace(-3, 1, H) * wscale
+    b2 = torch.randn(m1 * mo, generator=g) * wscale
+    W = W2.double().view(m1, mo, H)
+    Bf = torch.cat([W.permute(1, 0, 2).reshape(mo, m1 * H), b2.double().view(m1, mo).t()], 1)
+    Bt = W.permute(0, 2, 1).reshape(m1 * H, mo)
+    return W2, b2, Bf, Bt
+
+
+@pytest.mark.parametrize("M,m1,mo,H,grp,ascale", [(1000, 32, 128, 64, 5, 1.0),
+                                                  (333, 64, 64, 32, 1, 1e-20),
+                                                  (130, 32, 96, 128, 3, 1e12)])
+def test_tp_gemm_h2_matches_fp64(M, m1, mo, H, grp, ascale):
+    """The H2 forward path GEMM (torch.ops.gmp.tp_split_w2_h2 + tp_gemm_h2: two fp16 planes
+    with power-of-two scaling from device max words) against fp64: error per entry <= 4e-6 of
+    sum |a b| (22-bit operands), ragged tiles, the bias operand, grouped epilogue accumulation,
+    and operands 1e-20 / 1e12 in scale (the dynamic scaling keeps them in fp16 range)."""
+    from gmp_amd import _lib
+    tops = _lib.torch_ops()
+    W2, b2, Bf, _ = _h2_case(m1, mo, H, M + H)
+    g = torch.Generator().manual_seed(M)
+    K1 = m1 * H
+    S = torch.randn(M, K1, generator=g) * torch.logspace(-2, 1, K1) * ascale
+    Sb = torch.randn(M, m1, generator=g) * ascale
+    W2d, b2d = W2.to(DEV), b2.to(DEV)
+    wmax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    tops.absmax(W2d, wmax)
+    tops.absmax(b2d, wmax)
+    planes = tops.tp_split_w2_h2(W2d, b2d, 0, m1, mo, True, wmax)
+    Sd, Sbd = S.to(DEV), Sb.to(DEV)
+    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    tops.absmax(Sd, amax)
+    tops.absmax(Sbd, amax)
+    nr = -(-M // grp)
+    C0 = torch.randn(nr, mo * grp + 5, generator=g) * ascale
+    C = C0.clone().to(DEV)
+    tops.tp_gemm_h2(Sd, K1, Sbd, m1, planes, K1 + m1, mo, C, 0, grp, mo * grp + 5, 1, grp, True,
+                    amax, wmax)
+    A = torch.cat([S, Sb], 1).double()
+    ref = A @ Bf.t()
+    mag = A.abs() @ Bf.abs().t()
+    got = C.cpu().double() - C0.double()
+    rows = torch.arange(M)
+    out = torch.empty(M, mo, dtype=torch.float64)
+    for col in range(mo):
+        out[:, col] = got[rows // grp, rows % grp + col * grp]
+    err = ((out - ref).abs() / mag.clamp_min(1e-300)).max().item()
+    assert err < 4e-6, err
+
+
+@pytest.mark.parametrize("M,m1,mo,H", [(700, 32, 128, 64), (129, 64, 32, 32), (64, 32, 96, 96)])
+def test_tp_gemm_h2_widen_matches_fp64(M, m1, mo, H):
+    """The H2 backward T GEMM (tp_gemm_h2_widen, A = G scaled by its absmax word) against fp64
+    within 4e-6 of sum |a b| per entry."""
+    from gmp_amd import _lib
+    tops = _lib.torch_ops()
+    W2, b2, _, Bt = _h2_case(m1, mo, H, M + mo)
+    g = torch.Generator().manual_seed(M + 1)
+    G = torch.randn(M, mo, generator=g) * torch.logspace(-4, 0, mo)
+    W2d, b2d = W2.to(DEV), b2.to(DEV)
+    wmax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    tops.absmax(W2d, wmax)
+    tops.absmax(b2d, wmax)
+    planes = tops.tp_split_w2_h2(W2d, b2d, 0, m1, mo, False, wmax)
+    Gd = G.to(DEV)
+    gmax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    tops.absmax(Gd, gmax)
+    T = tops.tp_gemm_h2_widen(Gd, planes, m1 * H, gmax, wmax)
+    ref = G.double() @ Bt.t()
+    mag = G.double().abs() @ Bt.abs().t()
+    err = ((T.cpu().double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
+    assert err < 4e-6, err
+
+
+def test_tp_node_outer_amax_word():
+    """gmp_tp_node_outer_amax_f32 folds max |S|, |Sb| into the device word (float bits)."""
+    from gmp_amd import _lib
+    degs = [0, 1, 31, 32, 33, 70, 20, 5]
+    w, H = 96, 64
+    eoff, Z, A, ne = _setup(degs, w, H, seed=3)
+    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    S, Sb = _lib.torch_ops().tp_node_outer(eoff.to(DEV), Z.to(DEV), A.to(DEV), w, amax)
+    want = max(S.abs().max().item(), Sb.abs().max().item())
+    got = amax.cpu().view(torch.float32).item()
+    assert got == want, (got, want)
