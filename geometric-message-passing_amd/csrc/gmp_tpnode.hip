@@ -37,6 +37,7 @@ __device__ __forceinline__ void amax_commit(unsigned* amax, float v) {
   if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(v));
 }
 
+template <bool AMAX>
 __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
                                                             const int64_t* __restrict__ eoff,
                                                             const float* __restrict__ Z,
@@ -100,16 +101,17 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
         for (int t = 0; t < kMaxH / 16; ++t)
           if (t < TJ) {
             *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
-            lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
-                                     fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
+            if (AMAX)
+              lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
+                                       fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
           }
       }
       zsum += __shfl_xor(zsum, 16);
       zsum += __shfl_xor(zsum, 32);
       if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
-      if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
+      if (AMAX && r < w) lmax = fmaxf(lmax, fabsf(zsum));
     }
-    amax_commit(amax, lmax);
+    if (AMAX) amax_commit(amax, lmax);
     return;
   }
   if (deg <= kEdgeStage) {  // stage a once for all row blocks
@@ -157,16 +159,17 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       for (int t = 0; t < kMaxH / 16; ++t)
         if (t < TJ) {
           *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
-          lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
-                                   fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
+          if (AMAX)
+            lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
+                                     fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
         }
     }
     zsum += __shfl_xor(zsum, 16);
     zsum += __shfl_xor(zsum, 32);
     if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
-    if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
+    if (AMAX && r < w) lmax = fmaxf(lmax, fabsf(zsum));
   }
-  amax_commit(amax, lmax);
+  if (AMAX) amax_commit(amax, lmax);
 }
 
 // ---------------------------------------------------------------------------------- apply
@@ -543,8 +546,12 @@ int gmp_tp_node_outer_amax_f32(int64_t n_recv, int64_t w, int64_t H, const int64
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0);
   if (n_recv > 65535) return GMP_ERR_UNSUPPORTED;  // grid.y limit: caller chunks receivers
   const dim3 grid((unsigned)ceil_div(w, kRowsPerBlock * kOuterRB), (unsigned)n_recv);
-  tp_node_outer_kernel<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb,
-                                                             amax);
+  if (amax)
+    tp_node_outer_kernel<true><<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A,
+                                                                   S, Sb, amax);
+  else
+    tp_node_outer_kernel<false><<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A,
+                                                                    S, Sb, nullptr);
   return launch_status();
 }
 
