@@ -797,6 +797,22 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
 }
 
 // ================================================================================== backward
+// max |x| over the wave's 16 edges x d features (row_ror butterfly inside each 16-lane row,
+// then the 4 lane groups), folded into an LDS word by one lane
+template <int D>
+__device__ __forceinline__ void fold_max(unsigned* word, const f32x4 (&x)[D / 16], int lane) {
+  float v = 0.f;
+#pragma unroll
+  for (int p = 0; p < D / 16; ++p)
+    v = fmaxf(v, fmaxf(fmaxf(fabsf(x[p][0]), fabsf(x[p][1])), fmaxf(fabsf(x[p][2]), fabsf(x[p][3]))));
+  v = fmaxf(v, dpp<0x128>(v));
+  v = fmaxf(v, dpp<0x124>(v));
+  v = fmaxf(v, dpp<0x122>(v));
+  v = fmaxf(v, dpp<0x121>(v));
+  v = max_groups(v);
+  if (lane == 0) atomicMax(word, __float_as_uint(v));
+}
+
 constexpr int NVG = 8;  // vector-gradient outputs: ln1w ln1b ln2w ln2b ln3w ln3b w4 w1d
 enum GradVec { G_LN1W = 0, G_LN1B, G_LN2W, G_LN2B, G_LN3W, G_LN3B, G_W4, G_W1D };
 
@@ -809,7 +825,9 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
 
 // Backward from the forward's saved x_hat1..3 / rstd (no forward recompute, no AB gathers):
 // two transposed GEMMs (W3^T, W2^T) per 16-edge chunk.
-template <int D, int ACT, bool MSG_MEAN, bool HF>
+// AMAX: fold max |dpre2|, |dpre3| into amax[0], amax[1] (float bit patterns; the scales of the
+// HF weight-gradient outer sums, gmp_edge_outer_sum_act_hf_f32)
+template <int D, int ACT, bool MSG_MEAN, bool HF, bool AMAX>
 __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
@@ -817,7 +835,8 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     const float* __restrict__ xsave, const float* __restrict__ rsave,
     const float* __restrict__ g_maggr, const float* __restrict__ g_paggr, float* __restrict__ dA,
     float* __restrict__ dpos_recv, float* __restrict__ dpre1_out, float* __restrict__ gdiff_out,
-    float* __restrict__ dpre2_out, float* __restrict__ dpre3_out, float* __restrict__ partials) {
+    float* __restrict__ dpre2_out, float* __restrict__ dpre3_out, float* __restrict__ partials,
+    unsigned* __restrict__ amax) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW, K = VecAcc<D>::K;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2t = smem;  // W2^T
@@ -831,6 +850,13 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   else load_params_to_lds<D, true>(smem, P);
   __syncthreads();
   const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
+  // AMAX: per-chunk wave maxima go to two LDS words (no loop-carried registers: the kernel sits
+  // at 256 VGPRs), folded into amax[] once per workgroup at the end
+  unsigned* lmx = reinterpret_cast<unsigned*>(const_cast<float*>(sV) + NV * D + 10);
+  if (AMAX) {
+    if (threadIdx.x < 2) lmx[threadIdx.x] = 0u;
+    __syncthreads();
+  }
 
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -902,6 +928,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] *= vec4<D>(sV, V_LN3W, p, g);
     ln_backward<D>(x, z, rstd3);  // x = dpre3
+    if (AMAX) fold_max<D>(lmx + 1, x, lane);
     const int ne = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
     const int i0 = __builtin_amdgcn_readfirstlane(c.i);
     const int i1 = __builtin_amdgcn_readlane(c.i, 15);
@@ -925,6 +952,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 #pragma unroll
     for (int p = 0; p < T; ++p) z[p] *= vec4<D>(sV, V_LN2W, p, g);
     ln_backward<D>(z, xh2, rstd2);  // z = dpre2
+    if (AMAX) fold_max<D>(lmx, z, lane);
     store_row_w<D, kAuxNT>(rows_window(dpre2_out, base, ne, D), eoff, z, g);
 
     // ---------------- dy1 = W2^T dpre2 (x); xhat1 -> xh2 in flight
@@ -986,6 +1014,11 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
 
   // ---------------- workgroup reduction of the vector grads -> partials[blockIdx]
   __syncthreads();  // every wave is done with W2/W3: reuse that LDS as scratch
+  if (AMAX && threadIdx.x == 0) {  // (invalid lanes held zeros: gscale / rstd = 0)
+    atomicMax(&amax[0], lmx[0]);
+    atomicMax(&amax[1], lmx[1]);
+  }
+  __syncthreads();
   float* red = smem;  // [wave][NVG*D + 1]
   constexpr int RW = NVG * D + 1;
   for (int t = lane; t < RW; t += 64) red[wid * RW + t] = 0.f;
@@ -1058,16 +1091,20 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
                const int64_t* recv, const int64_t* send, const gmp_egnn_params& P,
                const float* xsave, const float* rsave, const float* gm, const float* gp,
                float* dA, float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
-               float* dpre3, float* partials, hipStream_t s) {
+               float* dpre3, float* partials, unsigned* amax, hipStream_t s) {
   const int64_t W = n_waves_for(E, kBwdWaves);
   const bool hf = !egnn_f32();
   const size_t smem = hf ? smem_total<D, kBwdWaves, true>() : smem_total<D, kBwdWaves, false>();
-  auto k = hf ? egnn_bwd_kernel<D, ACT, MEAN, true> : egnn_bwd_kernel<D, ACT, MEAN, false>;
+  auto k = hf ? (amax ? egnn_bwd_kernel<D, ACT, MEAN, true, true>
+                      : egnn_bwd_kernel<D, ACT, MEAN, true, false>)
+              : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true>
+                      : egnn_bwd_kernel<D, ACT, MEAN, false, false>);
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / kBwdWaves), kBwdWaves * 64, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
                                                            xsave, rsave, gm, gp, dA, dpos_recv,
-                                                           dpre1, gdiff, dpre2, dpre3, partials);
+                                                           dpre1, gdiff, dpre2, dpre3, partials,
+                                                           amax);
   return launch_status();
 }
 
@@ -1136,13 +1173,13 @@ int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d) {
   return n_waves_for(n_edges, kBwdWaves) / kBwdWaves;
 }
 
-int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
-                          const int64_t* rowptr, const int64_t* recv, const int64_t* send,
-                          const gmp_egnn_params* params, int act, int msg_mean,
-                          const float* save_xhat, const float* save_rstd, const float* g_m_aggr,
-                          const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
-                          float* gdiff, float* dpre2, float* dpre3, float* vec_partials,
-                          void* stream) {
+int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                               const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                               const gmp_egnn_params* params, int act, int msg_mean,
+                               const float* save_xhat, const float* save_rstd,
+                               const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                               float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
+                               float* dpre3, float* vec_partials, uint32_t* amax, void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
   GMP_CHECK_ARG(n_nodes < INT32_MAX && n_edges < INT32_MAX);  // 32-bit edge / node ids
@@ -1167,10 +1204,23 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
 #define GMP_CALL_BWD(DD, AA, MM)                                                              \
   rc = launch_bwd<DD, AA, MM>(n_nodes, n_edges, pos, rowptr, recv, send, *params, save_xhat,  \
                               save_rstd, g_m_aggr, g_pos_aggr, dA, dpos_recv, dpre1, gdiff,    \
-                              dpre2, dpre3, vec_partials, s)
+                              dpre2, dpre3, vec_partials, amax, s)
   GMP_EGNN_DISPATCH(GMP_CALL_BWD);
 #undef GMP_CALL_BWD
   return rc;
+}
+
+int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                          const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                          const gmp_egnn_params* params, int act, int msg_mean,
+                          const float* save_xhat, const float* save_rstd, const float* g_m_aggr,
+                          const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
+                          float* gdiff, float* dpre2, float* dpre3, float* vec_partials,
+                          void* stream) {
+  return gmp_egnn_edge_bwd_amax_f32(n_nodes, n_edges, d, pos, rowptr, recv, send, params, act,
+                                    msg_mean, save_xhat, save_rstd, g_m_aggr, g_pos_aggr, dA,
+                                    dpos_recv, dpre1, gdiff, dpre2, dpre3, vec_partials, nullptr,
+                                    stream);
 }
 
 }  // extern "C"

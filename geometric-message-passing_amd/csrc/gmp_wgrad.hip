@@ -379,12 +379,35 @@ __device__ __forceinline__ int xoff(int row, int chunk) {
   return row * 64 + 16 * (chunk ^ ((row >> 1) & 3));
 }
 
-template <int RT, int CT, int PRO, int NL, int PD = (NL == 1 ? 4 : 2)>
+// HF form (NP = 2; gmp_edge_outer_sum_act_hf_f32): two fp16 planes (x = hi + lo, 22 bits) of
+// the operands scaled by powers of two, three products lo*hi + hi*lo + hi*hi per stage, partial
+// slabs scaled back exactly.  A's scale from a device max word (the EGNN backward kernel folds
+// max |dpre| into it); B = act(X w + b) of LayerNorm rows X (|X| <= sqrt(N)): bounded by
+// sqrt(N) max|w| + max|b|, computed per block from w, b.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split2h(f32x2 x, unsigned& h, unsigned& l) {
+  const h16x2 hh = __builtin_convertvector(x, h16x2);
+  const f32x2 r = x - __builtin_convertvector(hh, f32x2);  // exact
+  const h16x2 hl = __builtin_convertvector(r, h16x2);
+  h = __builtin_bit_cast(unsigned, hh);
+  l = __builtin_bit_cast(unsigned, hl);
+}
+__device__ __forceinline__ int hf_scale_exp(float mx) {
+  if (!(mx > 0.f) || !(mx < 3.0e38f)) return 0;
+  int e;
+  (void)frexpf(mx, &e);
+  const int s = 15 - e;
+  return s < -120 ? -120 : (s > 120 ? 120 : s);
+}
+
+template <int RT, int CT, int PRO, int NL, int NP = 3, int PD = (NL == 1 ? 4 : 2)>
 __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
     const float* __restrict__ A, const float* __restrict__ B, int64_t K, int M, int N,
     int64_t lda, int64_t ldb, int64_t k_per_block, float* __restrict__ partial,
     const float* __restrict__ bw, const float* __restrict__ bb, int WN,
-    const float* __restrict__ B2, int64_t ldb2, int N1, int64_t a_col_step) {
+    const float* __restrict__ B2, int64_t ldb2, int N1, int64_t a_col_step,
+    const unsigned* __restrict__ amaxA) {
   // B may be two column blocks [B (N1 columns) | B2 (N - N1 columns)] of different tensors.
   // blockIdx.y > 0 (gmp_outer_sum_cols_f32): column block y of a wide A, A + y a_col_step, its
   // own row of partial slabs
@@ -393,8 +416,27 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smx[];
   const int R = M + N;  // LDS rows per plane: A channels, then B channels
   // + 64 padding rows: written by idle loader lanes (row R), read by the ragged tiles
-  const int PLANE = (R + kXPad) * 64, STAGE = 3 * PLANE;
+  const int PLANE = (R + kXPad) * 64, STAGE = NP * PLANE;
   const int tid = threadIdx.x, lane = tid & 63;
+  // HF scales: fa = 2^sa (A), fb = 2^sb (B), partials x 2^-sa x 2^-sb (two exact steps)
+  float fa = 1.f, fb = 1.f, da = 1.f, db = 1.f;
+  if constexpr (NP == 2) {
+    __shared__ unsigned bmx[2];
+    if (tid < 2) bmx[tid] = 0u;
+    __syncthreads();
+    if (tid < N) {
+      atomicMax(&bmx[0], __float_as_uint(fabsf(bw[tid])));
+      atomicMax(&bmx[1], __float_as_uint(fabsf(bb[tid])));
+    }
+    __syncthreads();
+    const int sa = hf_scale_exp(__uint_as_float(amaxA[0]));
+    const int sb = hf_scale_exp(sqrtf((float)N) * __uint_as_float(bmx[0]) +
+                                __uint_as_float(bmx[1]));
+    fa = ldexpf(1.f, sa);
+    fb = ldexpf(1.f, sb);
+    da = ldexpf(1.f, -sa);
+    db = ldexpf(1.f, -sb);
+  }
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar tile branches
   const int li = lane & 15, g = lane >> 4;
   const int wm = w / WN, wn = w - (w / WN) * WN;
@@ -466,15 +508,24 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) csum[q] += reg[q][j];  // used for A units only
       const int eq = ueq[q];
+      const float fs = isA[q] ? fa : fb;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        unsigned h0, m0, l0, h1, m1, l1;
-        split3(f32x2{reg[q][0][c], reg[q][1][c]}, h0, m0, l0);
-        split3(f32x2{reg[q][2][c], reg[q][3][c]}, h1, m1, l1);
         const int off = xoff(lrow[q] + c, eq >> 1) + 8 * (eq & 1);
-        *reinterpret_cast<u32x2*>(buf + off) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(buf + PLANE + off) = u32x2{m0, m1};
-        *reinterpret_cast<u32x2*>(buf + 2 * PLANE + off) = u32x2{l0, l1};
+        if constexpr (NP == 3) {
+          unsigned h0, m0, l0, h1, m1, l1;
+          split3(f32x2{reg[q][0][c], reg[q][1][c]}, h0, m0, l0);
+          split3(f32x2{reg[q][2][c], reg[q][3][c]}, h1, m1, l1);
+          *reinterpret_cast<u32x2*>(buf + off) = u32x2{h0, h1};
+          *reinterpret_cast<u32x2*>(buf + PLANE + off) = u32x2{m0, m1};
+          *reinterpret_cast<u32x2*>(buf + 2 * PLANE + off) = u32x2{l0, l1};
+        } else {
+          unsigned h0, l0, h1, l1;
+          split2h(f32x2{reg[q][0][c] * fs, reg[q][1][c] * fs}, h0, l0);
+          split2h(f32x2{reg[q][2][c] * fs, reg[q][3][c] * fs}, h1, l1);
+          *reinterpret_cast<u32x2*>(buf + off) = u32x2{h0, h1};
+          *reinterpret_cast<u32x2*>(buf + PLANE + off) = u32x2{l0, l1};
+        }
       }
     }
   };
@@ -482,28 +533,52 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
   // the other operand and are never stored, so compute and stash form one basic block and the
   // scheduler can overlap the MFMAs with the next stage's split
   auto compute = [&](const unsigned char* buf) {
-    bf16x8 a[RT][3];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int off = xoff(16 * (wm * RT + r) + li, g);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) a[r][p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
-    }
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      const int off = xoff(M + 16 * (wn * CT + c) + li, g);
-      bf16x8 b[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
+    if constexpr (NP == 3) {
+      bf16x8 a[RT][3];
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        f32x4 t = acc[r][c];
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][2], b[0], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[1], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[2], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[0], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[1], t, 0, 0, 0);
-        acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[0], t, 0, 0, 0);
+        const int off = xoff(16 * (wm * RT + r) + li, g);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[r][p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
+      }
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int off = xoff(M + 16 * (wn * CT + c) + li, g);
+        bf16x8 b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(buf + p * PLANE + off);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          f32x4 t = acc[r][c];
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][2], b[0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[2], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], b[0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[1], t, 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], b[0], t, 0, 0, 0);
+        }
+      }
+    } else {
+      h16x8 a[RT][2];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const int off = xoff(16 * (wm * RT + r) + li, g);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) a[r][p] = *reinterpret_cast<const h16x8*>(buf + p * PLANE + off);
+      }
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int off = xoff(M + 16 * (wn * CT + c) + li, g);
+        h16x8 b[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) b[p] = *reinterpret_cast<const h16x8*>(buf + p * PLANE + off);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          f32x4 t = acc[r][c];
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r][1], b[0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r][0], b[1], t, 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r][0], b[0], t, 0, 0, 0);
+        }
       }
     }
   };
@@ -540,7 +615,8 @@ __global__ __launch_bounds__(kXT, 1) void outer_sum_x3_kernel(
       if (tm < TM && tn < TN) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          out[(int64_t)(16 * tm + 4 * g + q) * N + 16 * tn + li] = acc[r][c][q];
+          out[(int64_t)(16 * tm + 4 * g + q) * N + 16 * tn + li] =
+              NP == 3 ? acc[r][c][q] : (acc[r][c][q] * da) * db;
       }
     }
   // colsum(A): the 8 edge quads of a channel group added in quad order (deterministic)
@@ -606,7 +682,10 @@ int64_t x3_blocks_for(int64_t K) {
 int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
                         const float* B, int64_t ldb, int pro, const float* bw, const float* bb,
                         float* C, int64_t ldc, float* colsum_A, void* workspace, hipStream_t s,
-                        const float* B2 = nullptr, int64_t ldb2 = 0, int64_t n1 = -1) {
+                        const float* B2 = nullptr, int64_t ldb2 = 0, int64_t n1 = -1,
+                        const unsigned* amaxA = nullptr) {
+  const bool hf = amaxA != nullptr;  // HF form: act prologue (pro != 0), single B operand
+  if (hf && (pro == 0 || B2 || n > kXT)) return GMP_ERR_UNSUPPORTED;
   if (n1 < 0) n1 = n;  // single B operand
   // Narrow products (m n < 4096) stay on the f32-MFMA kernels: too little matrix work per
   // loaded byte for the split's VALU and LDS staging to pay (measured: 16 x 128, 48 x 48 slower).
@@ -625,17 +704,17 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   const int64_t per = ceil_div(ceil_div(K, G), kXK) * kXK;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-  const size_t smem = (size_t)2 * 3 * (R + kXPad) * 64;
+  const size_t smem = (size_t)2 * (hf ? 2 : 3) * (R + kXPad) * 64;
   int rc = 0;
 #define GMP_X3(RT, CT, PP, NL)                                                                \
   {                                                                                           \
-    auto k = outer_sum_x3_kernel<RT, CT, PP, NL>;                                             \
+    auto k = hf ? outer_sum_x3_kernel<RT, CT, PP, NL, 2> : outer_sum_x3_kernel<RT, CT, PP, NL>; \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                   \
                                             hipFuncAttributeMaxDynamicSharedMemorySize,      \
                                             (int)smem))))                                     \
       return rc;                                                                              \
     k<<<(unsigned)Gr, kXT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per, part, bw, bb,  \
-                                      wn, B2, ldb2, (int)n1, 0);                              \
+                                      wn, B2, ldb2, (int)n1, 0, amaxA);                       \
   }
 #define GMP_X3_NL(RT, CT, PP) \
   if (nl == 1) GMP_X3(RT, CT, PP, 1) else GMP_X3(RT, CT, PP, 2)
@@ -812,6 +891,29 @@ int gmp_edge_outer_sum_act_f32(int64_t K, int64_t d, const float* A, const float
                           workspace_bytes, stream);
 }
 
+int gmp_edge_outer_sum_act_hf_f32(int64_t K, int64_t d, const float* A, const float* X,
+                                  const float* w, const float* b, int act, const uint32_t* amax_A,
+                                  float* C, float* colsum_A, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  if (!(act == 0 || act == 1)) return GMP_ERR_ARG;
+  GMP_CHECK_ARG(amax_A && w && b && C && K >= 0);
+  if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
+  if (workspace_bytes < gmp_edge_outer_sum_workspace_size(K, d)) return GMP_ERR_WORKSPACE;
+  hipStream_t s = as_stream(stream);
+  if (K > 0) {
+    GMP_CHECK_ARG(A && X && workspace);
+    GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(X) |
+                    reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(b)) % 16) == 0);
+    if (!wgrad_f32_mfma()) {
+      const int rc = outer_sum_x3_launch(K, d, d, A, d, X, d, act + 1, w, b, C, d, colsum_A,
+                                         workspace, s, nullptr, 0, -1, amax_A);
+      if (rc != GMP_ERR_UNSUPPORTED) return rc;
+    }
+  }
+  return outer_sum_launch(K, d, A, d, X, d, act + 1, w, b, C, d, colsum_A, workspace,
+                          workspace_bytes, stream);
+}
+
 int64_t rect_blocks_for(int64_t K) {
   int64_t g = capped((int64_t)device_cu_count() * 2);
   const int64_t min_per = 4 * kKT;
@@ -974,7 +1076,7 @@ int gmp_outer_sum_cols_f32(int64_t K, int64_t m_total, int64_t n, const float* A
   if (rc) return rc;
   k<<<dim3((unsigned)Gr, (unsigned)Y), kXT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per,
                                                       part, nullptr, nullptr, wn, nullptr, 0,
-                                                      (int)n, m);
+                                                      (int)n, m, nullptr);
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;

@@ -162,7 +162,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
     const Tensor& pos, const Tensor& rowptr, const Tensor& recv, const Tensor& send,
     const std::vector<Tensor>& params, int64_t act, bool msg_mean, const Tensor& xhat,
-    const Tensor& rstd, const Tensor& g_m, const Tensor& g_p) {
+    const Tensor& rstd, const Tensor& g_m, const Tensor& g_p, const optional<Tensor>& amax) {
   f32(pos, "pos");
   f32(xhat, "xhat");
   f32(rstd, "rstd");
@@ -174,10 +174,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd
   Tensor dA = at::empty({N, d}, o), dpr = at::empty({N, 3}, o), dp1 = at::empty({E, d}, o);
   Tensor gd = at::empty({E, 3}, o), dp2 = at::empty({E, d}, o), dp3 = at::empty({E, d}, o);
   Tensor part = at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o);
-  check_rc(gmp_egnn_edge_bwd_f32(N, E, d, fp(pos), ip(rowptr), ip(recv), ip(send), &P, (int)act,
-                                 msg_mean, fp(xhat), fp(rstd), fp(g_m), fp(g_p), fp(dA), fp(dpr),
-                                 fp(dp1), fp(gd), fp(dp2), fp(dp3), fp(part), cur_stream()),
-           "gmp_egnn_edge_bwd_f32");
+  TORCH_CHECK(!amax.has_value() || amax->numel() >= 2, "gmp.egnn_edge_bwd: amax has 2 words");
+  check_rc(gmp_egnn_edge_bwd_amax_f32(
+               N, E, d, fp(pos), ip(rowptr), ip(recv), ip(send), &P, (int)act, msg_mean,
+               fp(xhat), fp(rstd), fp(g_m), fp(g_p), fp(dA), fp(dpr), fp(dp1), fp(gd), fp(dp2),
+               fp(dp3), fp(part),
+               amax.has_value() ? reinterpret_cast<uint32_t*>(amax->data_ptr<int32_t>())
+                                : nullptr,
+               cur_stream()),
+           "gmp_egnn_edge_bwd_amax_f32");
   return {dA, dpr, dp1, gd, dp2, dp3, part};
 }
 
@@ -611,7 +616,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(const Tensor& AB, const
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
     const Tensor& pos, const Tensor&, const Tensor& recv, const Tensor&,
     const std::vector<Tensor>&, int64_t, bool, const Tensor& xhat, const Tensor&, const Tensor&,
-    const Tensor&) {
+    const Tensor&, const optional<Tensor>&) {
   const int64_t N = pos.size(0), E = recv.numel(), d = xhat.size(2);
   auto o = pos.options();
   return {at::empty({N, d}, o), at::empty({N, 3}, o), at::empty({E, d}, o), at::empty({E, 3}, o),
@@ -747,9 +752,9 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor[] params, int act, bool msg_mean, float eps, bool train) -> "
         "(Tensor m_aggr, Tensor pos_aggr, Tensor xhat, Tensor rstd)");
   m.def("egnn_edge_bwd(Tensor pos, Tensor rowptr, Tensor recv, Tensor send, Tensor[] params, "
-        "int act, bool msg_mean, Tensor xhat, Tensor rstd, Tensor g_m_aggr, Tensor g_pos_aggr) -> "
-        "(Tensor dA, Tensor dpos_recv, Tensor dpre1, Tensor gdiff, Tensor dpre2, Tensor dpre3, "
-        "Tensor partials)");
+        "int act, bool msg_mean, Tensor xhat, Tensor rstd, Tensor g_m_aggr, Tensor g_pos_aggr, "
+        "Tensor(a!)? amax=None) -> (Tensor dA, Tensor dpos_recv, Tensor dpre1, Tensor gdiff, "
+        "Tensor dpre2, Tensor dpre3, Tensor partials)");
   m.def("cfconv_aggregate(Tensor x, Tensor xidx, Tensor w, Tensor perm, Tensor rowptr, "
         "int n_seg, Tensor? escale=None) -> Tensor");
   m.def("cfconv_wgrad(Tensor g, Tensor gidx, Tensor x, Tensor xidx, Tensor? escale=None) -> "

@@ -100,6 +100,11 @@ SIGNATURES = {
     "gmp_absmax_f32": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "gmp_tp_node_outer_amax_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp]),
+    "gmp_edge_outer_sum_act_hf_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,
+                                              c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "gmp_egnn_edge_bwd_amax_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_gate_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp]),
     "gmp_gate_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
                                  c_vp]),

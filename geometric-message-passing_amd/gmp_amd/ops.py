@@ -169,9 +169,11 @@ def edge_outer_sum(A, B, with_colsum=True):
     return C, cs
 
 
-def edge_outer_sum_act(A, X, w, b, act):
+def edge_outer_sum_act(A, X, w, b, act, amax=None):
     """(A^T act(X * w + b), colsum(A)) with the activation applied at load time
-    (gmp_edge_outer_sum_act_f32): the EGNN y1 / m weight-gradient operands from x_hat."""
+    (gmp_edge_outer_sum_act_f32): the EGNN y1 / m weight-gradient operands from x_hat.  With
+    `amax` (device word, max |A| as float bits; X LayerNorm rows) the HF form
+    (gmp_edge_outer_sum_act_hf_f32: scaled fp16 planes, three products)."""
     lib = _lib.load()
     A, X, w, b = _f32c(A), _f32c(X), _f32c(w), _f32c(b)
     _need_cuda(A, X, w, b)
@@ -181,9 +183,16 @@ def edge_outer_sum_act(A, X, w, b, act):
     ws_bytes = lib.gmp_edge_outer_sum_workspace_size(K, d)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
     with _timed("edge_outer_sum"):
-        check(lib.gmp_edge_outer_sum_act_f32(K, d, _p(A), _p(X), _p(w), _p(b), _lib.ACT[act],
-                                             _p(C), _p(cs), _p(ws), ws_bytes, _stream()),
-              "gmp_edge_outer_sum_act_f32")
+        if amax is not None:
+            check(lib.gmp_edge_outer_sum_act_hf_f32(K, d, _p(A), _p(X), _p(w), _p(b),
+                                                    _lib.ACT[act], _p(amax), _p(C), _p(cs),
+                                                    _p(ws), ws_bytes, _stream()),
+                  "gmp_edge_outer_sum_act_hf_f32")
+        else:
+            check(lib.gmp_edge_outer_sum_act_f32(K, d, _p(A), _p(X), _p(w), _p(b),
+                                                 _lib.ACT[act], _p(C), _p(cs), _p(ws), ws_bytes,
+                                                 _stream()),
+                  "gmp_edge_outer_sum_act_f32")
     return C, cs
 
 
@@ -808,6 +817,10 @@ def _egnn_params(tensors):
     return _lib.GmpEgnnParams(*[t.data_ptr() for t in tensors])
 
 
+# EGNN dW2 / dW3 on the HF outer sums (two scaled fp16 planes; "0": split-plane x3)
+EGNN_WGRAD_HF = os.environ.get("GMP_EGNN_WGRAD_HF", "1") != "0"
+
+
 class EgnnMessageFn(torch.autograd.Function):
     """The whole EGNN message block of one layer (egnn_layer.py:62-80 with the MLPs of :28-36):
     the node projections AB = [h W1a^T | h W1b^T] (one GEMM), the fused edge kernel K4 and the
@@ -855,10 +868,13 @@ class EgnnMessageFn(torch.autograd.Function):
         g_m = torch.zeros((N, d), device=dev) if g_m is None else _f32c(g_m)
         g_p = torch.zeros((N, 3), device=dev) if g_p is None else _f32c(g_p)
         f = dict(dtype=torch.float32, device=dev)
+        # HF weight-gradient outer sums: the backward kernel folds max |dpre2|, |dpre3| into
+        # two device words that scale their fp16 planes
+        amax = torch.zeros(2, dtype=torch.int32, device=dev) if EGNN_WGRAD_HF else None
         with _timed("egnn_edge_bwd"):
             dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, partials = _lib.torch_ops().egnn_edge_bwd(
                 pos, graph.rowptr, graph.recv, graph.send, list(params), _lib.ACT[ctx.act],
-                bool(ctx.msg_mean), xhat, rstd, g_m, g_p)
+                bool(ctx.msg_mean), xhat, rstd, g_m, g_p, amax)
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
@@ -869,7 +885,7 @@ class EgnnMessageFn(torch.autograd.Function):
 
         # weight gradients: side stream, accumulated at the end of the backward pass
         (_, b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3, b3, ln3w, ln3b, w4, b4) = params
-        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials) as sw:
+        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials, amax) as sw:
             dW1 = torch.empty((d, 2 * d + 1), **f)
             db1 = torch.empty(d, **f)
             outer_sum_into(dA, h, dW1[:, :d], db1)
@@ -877,8 +893,10 @@ class EgnnMessageFn(torch.autograd.Function):
             v = partials.sum(0)
             dln1w, dln1b, dln2w, dln2b, dln3w, dln3b, dw4, dw1d = v[:8 * d].view(8, d).unbind(0)
             dW1[:, 2 * d].copy_(dw1d)
-            dW2, db2 = edge_outer_sum_act(dpre2, xhat[0], ln1w, ln1b, ctx.act)
-            dW3, db3 = edge_outer_sum_act(dpre3, xhat[1], ln2w, ln2b, ctx.act)
+            dW2, db2 = edge_outer_sum_act(dpre2, xhat[0], ln1w, ln1b, ctx.act,
+                                          amax[0:1] if amax is not None else None)
+            dW3, db3 = edge_outer_sum_act(dpre3, xhat[1], ln2w, ln2b, ctx.act,
+                                          amax[1:2] if amax is not None else None)
             grads = (dW1, db1, dln1w, dln1b, dW2, db2, dln2w, dln2b, dW3, db3, dln3w, dln3b,
                      dw4.view(1, d), v[8 * d:8 * d + 1])
         # the caller's parameter tensors (saved tensors unpack to the same objects): W1 itself,

@@ -156,6 +156,16 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
                           const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
                           float* gdiff, float* dpre2, float* dpre3, float* vec_partials,
                           void* stream);
+/* As gmp_egnn_edge_bwd_f32, also folding max |dpre2| and max |dpre3| into amax[0], amax[1]
+ * (float bit patterns, atomic max; caller zeroes): the A scales of the HF weight-gradient outer
+ * sums (gmp_edge_outer_sum_act_hf_f32). */
+int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                               const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                               const gmp_egnn_params* params, int act, int msg_mean,
+                               const float* save_xhat, const float* save_rstd,
+                               const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                               float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
+                               float* dpre3, float* vec_partials, uint32_t* amax, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Edge-reduction GEMM for per-edge Linear weight gradients (egnn_layer.py:28-39 mlp_msg /
@@ -184,6 +194,16 @@ int gmp_edge_outer_sum_act_f32(int64_t K, int64_t d, const float* A, const float
                                const float* w, const float* b, int act, float* C,
                                float* colsum_A, void* workspace, size_t workspace_bytes,
                                void* stream);
+/* HF form of gmp_edge_outer_sum_act_f32 for LayerNorm rows X (|X| <= sqrt(d), the EGNN x_hat):
+ * two scaled fp16 planes per operand, three MFMA products per stage (22-bit operands, f32
+ * accumulation; ~2^-21 relative per product).  amax_A: device word holding max |A| as a float
+ * bit pattern (gmp_egnn_edge_bwd_amax_f32 produces it for dpre2 / dpre3); B's scale comes from
+ * sqrt(d) max|w| + max|b|.  Falls back to the split-plane x3 / f32-MFMA paths where those apply
+ * (node-level K, gmp_wgrad_set_f32_mfma(1)). */
+int gmp_edge_outer_sum_act_hf_f32(int64_t K, int64_t d, const float* A, const float* X,
+                                  const float* w, const float* b, int act, const uint32_t* amax_A,
+                                  float* C, float* colsum_A, void* workspace,
+                                  size_t workspace_bytes, void* stream);
 
 /* Rectangular variant (GVP message GVPs, gvp_layer.py:101-170 applied per edge at :319-324):
  * C (m x n) = A^T B, A (K, m), B (K, n) row-major, m, n multiples of 16, m <= 256,

@@ -115,3 +115,31 @@ def test_outer_sum_two_b_operands(m, n1, n2):
     assert _err(C, refC, A, Bcat) < 5e-6
     torch.testing.assert_close(cs.cpu().double(), refs, atol=1e-3, rtol=1e-5)
     assert not ops.outer_sum_into2(Ad[:1000], B1d[:1000], B2d[:1000], C, cs)  # node-level K
+
+
+@pytest.mark.parametrize("d,act,ascale", [(128, "relu", 1.0), (128, "swish", 1e-30),
+                                          (64, "swish", 1e20)])
+def test_edge_outer_sum_act_hf_vs_fp64(d, act, ascale):
+    """The HF weight-gradient outer sum (gmp_edge_outer_sum_act_hf_f32: A scaled by its device
+    max word, B = act(X w + b) of LayerNorm rows scaled by sqrt(d) max|w| + max|b|, two fp16
+    planes, three products) against fp64 at K = 300k: per entry within 4e-6 of sum |a b|;
+    colsum(A) as the x3 kernel's; A scaled by 1e-30 / 1e20 stays exact in relative terms."""
+    from gmp_amd import ops
+    g = torch.Generator().manual_seed(d)
+    K = 300_000
+    A = torch.randn(K, d, generator=g) * torch.logspace(-3, 0, d) * ascale
+    X = torch.randn(K, d, generator=g)
+    X = (X - X.mean(1, keepdim=True)) / X.std(1, unbiased=False, keepdim=True)
+    w, b = torch.randn(d, generator=g), torch.randn(d, generator=g) * 0.1
+    Ad, Xd, wd, bd = A.to(DEV), X.to(DEV), w.to(DEV), b.to(DEV)
+    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    amax[0] = torch.tensor([A.abs().max().item()]).view(torch.int32)[0]
+    C, cs = ops.edge_outer_sum_act(Ad, Xd, wd, bd, act, amax)
+    z = X.double() * w.double() + b.double()
+    B = torch.relu(z) if act == "relu" else z * torch.sigmoid(z)
+    ref = A.double().t() @ B
+    mag = A.double().abs().t() @ B.abs()
+    err = ((C.cpu().double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
+    assert err < 4e-6, err
+    cs_ref = A.double().sum(0)
+    assert ((cs.cpu().double() - cs_ref).abs() / A.double().abs().sum(0)).max().item() < 1e-6
