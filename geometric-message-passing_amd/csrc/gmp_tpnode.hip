@@ -569,7 +569,10 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(T) % 16 == 0);
   const bool a16 = ((reinterpret_cast<uintptr_t>(Z) | reinterpret_cast<uintptr_t>(A) |
                      reinterpret_cast<uintptr_t>(Tb) | reinterpret_cast<uintptr_t>(dZ)) % 16) == 0;
-  if (w % kV2R == 0 && H % 64 == 0 && a16 && g_apply_x3) {  // whole float4 units per thread
+  // x3 form only for wide paths: measured (scripts/mb_apply_shapes.py, 50k receivers x 20
+  // edges, H = 256) 13.3 vs 13.7 ms at w = 640, but slower at w <= 384 (9.1 vs 8.9 ms at 384,
+  // 3.8 vs 3.2 at 64)
+  if (w >= 512 && w % kV2R == 0 && H % 64 == 0 && a16 && g_apply_x3) {  // whole float4 units
     const int hs = (int)(H / 32);
     const size_t smem = (size_t)3 * kTPlane + (size_t)3 * hs * kSPlane + 3 * kSPlane;
     int rc = 0;

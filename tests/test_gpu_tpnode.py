@@ -218,11 +218,11 @@ def test_tp_gemm_x3_widen_matches_fp64(M, N, K):
     assert err < 1e-6, err
 
 
-@pytest.mark.parametrize("w,H", [(640, 256), (96, 64), (128, 192), (128, 160)])
+@pytest.mark.parametrize("w,H", [(640, 256), (544, 64), (96, 64), (128, 192), (128, 160)])
 @pytest.mark.parametrize("x3", [1, 0])
 def test_node_apply_bf16x3_matches_fp64(w, H, x3):
-    """The apply kernel on the bf16 MFMA over three-plane splits (x3 = 1; shapes with w % 32 == 0
-    and H % 64 == 0; H = 160 takes the f32 kernel either way) and the f32-MFMA kernel (x3 = 0) against fp64, with edge groups of 0, 1,
+    """The apply kernel on the bf16 MFMA over three-plane splits (x3 = 1; shapes with w >= 512,
+    w % 32 == 0 and H % 64 == 0; the others take the f32 kernel either way) and the f32-MFMA kernel (x3 = 0) against fp64, with edge groups of 0, 1,
     31, 32, 33 and 70 edges (several 32-edge groups): dZ overwritten (+ Tb), dA accumulated onto
     existing values; error <= 1e-6 of the sum of |terms| per entry."""
     from gmp_amd import _lib
