@@ -547,9 +547,12 @@ TP_H2 = os.environ.get("GMP_TP_H2", "0") == "1"
 
 
 def _x3_ok(P, H):
-    """Shapes K7g covers: every k range a multiple of the 32-deep MFMA step, mul_out <= 128."""
+    """Shapes K7g covers (every k range a multiple of the 32-deep MFMA step, mul_out <= 128) and
+    where it pays: wide paths (mul1 mul_out >= 128 x 128, C4 MACE: 2.66 -> 2.41 s/step); on the
+    64 x 64 paths of C5 TFN the library f32 GEMMs measured faster (1.234 vs 1.270 s/step)."""
     return (TP_GEMM == "x3" and P["mul1"] % 32 == 0 and P["mul_out"] % 32 == 0
-            and P["mul_out"] <= 128 and H % 32 == 0)
+            and P["mul_out"] <= 128 and H % 32 == 0
+            and P["mul1"] * P["mul_out"] >= 128 * 128)
 
 
 def _split_w2(lib, W2, b2, P, fwd, wmax=None):
