@@ -2,7 +2,7 @@
 // (E, 128) filter-network hidden layer, schnet.py:72 via CFConv's nn, and to node features).
 // torch.nn.functional.softplus semantics (beta 1, threshold 20):
 //   forward : y = (x > 20 ? x : log1p(exp(x))) - shift
-//   backward: dx = x > 20 ? g : g * z / (z + 1), z = exp(x)
+//   backward: dx = x > 20 ? g : g * sigmoid(x)
 // One float4 per thread, grid-stride: one read + one write pass (the library path ran the
 // softplus and the shift subtraction as separate passes).
 #include "gmp_common.h"
@@ -10,14 +10,17 @@
 namespace gmp {
 namespace {
 
+// softplus(x) = max(x, 0) + log(1 + exp(-|x|)) with the native exp / log (absolute error
+// ~1e-7: 1 + exp(-|x|) lies in [1, 2]); for x > 20 the correction is below half an ulp of x, so
+// torch's threshold-20 identity branch comes out the same.  r01's log1pf(expf(x)) form ran at
+// 2.4 TB/s, limited by the accurate library calls.
 __device__ __forceinline__ float ssp1(float x, float shift) {
-  return (x > 20.f ? x : log1pf(expf(x))) - shift;
+  return (fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x)))) - shift;
 }
 
+// d softplus = sigmoid(x) = 1 / (1 + exp(-x)) (exp(-x) = inf for x << 0 gives 0)
 __device__ __forceinline__ float ssp1_bwd(float x, float g) {
-  if (x > 20.f) return g;
-  const float z = expf(x);
-  return g * z / (z + 1.f);
+  return g / (1.f + __expf(-x));
 }
 
 __global__ __launch_bounds__(256) void ssp_fwd(const float4* __restrict__ x, int64_t n4,

@@ -686,7 +686,10 @@ class ShiftedSoftplusFn(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, g):
         (x,) = ctx.saved_tensors
-        return _lib.torch_ops().ssp_bwd(x, _f32c(g)), None
+        g = _f32c(g)
+        if g.data_ptr() % 16:  # a contiguous view at an odd offset: K14 needs 16-byte rows
+            g = g.clone()
+        return _lib.torch_ops().ssp_bwd(x, g), None
 
 
 def shifted_softplus(x, shift):

@@ -169,3 +169,23 @@ def test_schnet_featurize_vs_oracle(E, G, cutoff):
     ((d * g1.to(DEV)).sum() + (rbf * g2.to(DEV)).sum() + (C * g3.to(DEV)).sum()).backward()
     ((dr * g1).sum() + (rbfr * g2).sum() + (Cr * g3).sum()).backward()
     _scaled(pd.grad, pr.grad, 1e-5, "dpos")
+
+
+@pytest.mark.parametrize("n,offset", [(4000, 0), (4001, 0), (4008, 1), (4000, 3)])
+def test_shifted_softplus_module_gate_and_fallback(n, offset):
+    """ShiftedSoftplus through the module: odd numel and misaligned views take the torch path,
+    aligned ones K14 (n = 4000, offset 0); the upstream gradient always arrives misaligned (a
+    contiguous view at an odd offset), which K14's backward must accept.  Outputs and
+    gradients vs torch."""
+    import math
+    from gmp_amd.schnet import ShiftedSoftplus
+    m = ShiftedSoftplus()
+    base = torch.randn(n + offset, device=DEV) * 6
+    x = base[offset:].detach().requires_grad_(True)
+    y = m(x)
+    yr = torch.nn.functional.softplus(x.detach().cpu()) - math.log(2.0)
+    torch.testing.assert_close(y.detach().cpu(), yr, atol=1e-6, rtol=1e-5)
+    g = torch.randn(n + 1, device=DEV)[1:]
+    y.backward(g)
+    gr = g.cpu() * torch.sigmoid(x.detach().cpu())
+    torch.testing.assert_close(x.grad.cpu(), gr, atol=1e-6, rtol=1e-5)
