@@ -967,13 +967,20 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
   case MR * 100 + MC * 10 + 2: GMP_RECT(MR, MC, 5, 2) break;  \
   case MR * 100 + MC * 10 + 3: GMP_RECT(MR, MC, 7, 2) break;  \
   case MR * 100 + MC * 10 + 4: GMP_RECT(MR, MC, 9, 2) break;
+// the widest buckets need > 256 VGPRs at 7-9 loads per thread: one workgroup per CU (the
+// compiler then has the AGPRs as well; at two per CU they spilled 40-152 B/lane to scratch)
+#define GMP_RECT_NL_WIDE(MR, MC)                              \
+  case MR * 100 + MC * 10 + 2: GMP_RECT(MR, MC, 5, 2) break;  \
+  case MR * 100 + MC * 10 + 3: GMP_RECT(MR, MC, 7, 1) break;  \
+  case MR * 100 + MC * 10 + 4: GMP_RECT(MR, MC, 9, 1) break;
   switch (bucket) {
     GMP_RECT_NL(1, 1) GMP_RECT_NL(1, 2) GMP_RECT_NL(1, 3)
-    GMP_RECT_NL(2, 1) GMP_RECT_NL(2, 2) GMP_RECT_NL(2, 3) GMP_RECT_NL(2, 5) GMP_RECT_NL(2, 9)
+    GMP_RECT_NL(2, 1) GMP_RECT_NL(2, 2) GMP_RECT_NL(2, 3) GMP_RECT_NL(2, 5) GMP_RECT_NL_WIDE(2, 9)
     GMP_RECT_NL(3, 1) GMP_RECT_NL(3, 2) GMP_RECT_NL(3, 3)
-    GMP_RECT_NL(4, 4)
+    GMP_RECT_NL_WIDE(4, 4)
     default: return GMP_ERR_UNSUPPORTED;
   }
+#undef GMP_RECT_NL_WIDE
 #undef GMP_RECT_NL
 #undef GMP_RECT
   rc = launch_status();
