@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a HIP graph (measured slower than eager launch "
                          "on ROCm 7 for the EGNN step: off by default)")
+    ap.add_argument("--fresh-graph", action="store_true",
+                    help="hand the model a new edge_index tensor every step (as a data loader "
+                         "would), so the receiver / sender CSRs (K0) are rebuilt inside the "
+                         "timed steps instead of coming from the per-graph cache")
     ap.add_argument("--timing-steps", type=int, default=2,
                     help="eager steps after the timed region in which the roofline kernel is "
                          "timed with HIP events (graph mode)")
@@ -346,6 +350,8 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
     y = torch.randn(1, device=dev)
 
     def loss_fn():
+        if args.fresh_graph:  # a new tensor object: the CSR caches miss, K0 runs every step
+            batch.edge_index = batch.edge_index.clone()
         return torch.nn.functional.l1_loss(model(batch).view(-1), y, reduction="sum")
 
     step = GraphedStep(model, loss_fn, opt, warmup=warmup, use_graph=args.graph)
@@ -471,7 +477,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded random radius graph per rank, random-init weights)",
-            "config": {"workload": main_rec["workload"], "value_is": names[0],
+            "config": {"fresh_graph": bool(args.fresh_graph), "workload": main_rec["workload"], "value_is": names[0],
                        "global_batch": world, "parallelism": f"dp{world}",
                        "step": "fwd + L1 loss + bwd + Adam",
                        "launch": "eager" if not args.graph else "hip graph replay"},
