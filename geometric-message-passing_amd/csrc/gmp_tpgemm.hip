@@ -26,12 +26,15 @@
 // so the forward adds its (n, k)-row result straight into the receivers' mul_ir output block
 // (row stride out_dim, k stride 1, w stride 2lo+1) and the backward writes row-major T.
 //
-// H2 form (NP = 2, gmp_tp_*_h2_f32, the default on the TP path): the same kernels over TWO
-// fp16 planes (x = hi + lo, 22-bit operands) of the operands scaled by powers of two — A by
-// 2^sa from a device-side max |A| (the S kernel's running max, or gmp_absmax_f32), B by 2^sb
-// from max |W2p| — with three products lo*hi + hi*lo + hi*hi per k step (dropped lo*lo
-// ~2^-22 relative) and the accumulators scaled back by 2^-(sa + sb) (exact) in the epilogue:
-// half the MFMAs, two thirds of the LDS image and of the split arithmetic of the x3 form.
+// H2 form (NP = 2, gmp_tp_*_h2_f32): the same kernels over TWO fp16 planes (x = hi + lo,
+// 22-bit operands) of the operands scaled by powers of two — B by 2^sb from max |W2p|, A by a
+// per-ROW 2^sa(r) (the forward GEMM: from the S kernel's per-wave row-block maxima, max over
+// the row's `nparts` words; the widen kernel: one device-side max |G| word) — with three
+// products lo*hi + hi*lo + hi*hi per k step (dropped lo*lo ~2^-22 relative) and each output
+// row scaled back by 2^-(sa(r) + sb) (exact) in the epilogue: half the MFMAs, two thirds of the
+// LDS image and of the split arithmetic of the x3 form.  Per-row scales keep every row at
+// 22-bit precision relative to its own magnitude (a launch-wide scale did not: rows far below
+// the launch max lost bits and the C4 1M-edge rotation-invariance bound failed).
 #include "gmp_common.h"
 
 namespace gmp {
@@ -80,6 +83,16 @@ __device__ __forceinline__ int scale_exp_bits(unsigned mx_bits) {
   (void)frexpf(mx, &e);
   const int s = 15 - e;
   return s < -60 ? -60 : (s > 60 ? 60 : s);
+}
+
+// per-row A exponent of the H2 forward GEMM: as scale_exp_bits with a +-120 range (applied and
+// undone with v_ldexp, so sa + sb never has to be a representable power of two)
+__device__ __forceinline__ int row_exp(float mx) {
+  if (!(mx > 0.f) || !(mx < 3.0e38f)) return 0;
+  int e;
+  (void)frexpf(mx, &e);
+  const int s = 15 - e;
+  return s < -120 ? -120 : (s > 120 ? 120 : s);
 }
 
 // split of 4 f32 into NP planes (x3: bf16 hi / mid / lo; H2: fp16 hi / lo of x * fs)
@@ -174,11 +187,11 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
     const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
     int64_t ldb, int64_t bplane, float* __restrict__ C, int64_t cgrp, int64_t cldg,
-    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const unsigned* __restrict__ amax,
-    const unsigned* __restrict__ wmax) {
+    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const float* __restrict__ arow,
+    int nparts, const unsigned* __restrict__ wmax) {
   constexpr int STG = 2 * NP * kPlane;  // LDS bytes per stage (A planes, then B planes)
   extern __shared__ __attribute__((aligned(16))) unsigned char smg[];
-  const H2Scale hs = h2_scale<NP>(amax, wmax);
+  int* sexp = reinterpret_cast<int*>(smg + 2 * STG);  // H2: the tile's 128 row exponents
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
@@ -202,18 +215,32 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
 
   const int64_t Ktot = K1 + K2;
   const int nst = (int)(Ktot / kBK);
+  int sb = 0;
+  if constexpr (NP == 2) {
+    sb = scale_exp_bits(wmax[0]);
+    if (tid < kBM) {
+      const int64_t r = m0 + tid;
+      float mx = 0.f;
+      if (r < M)
+        for (int p = 0; p < nparts; ++p) mx = fmaxf(mx, arow[r * nparts + p]);
+      sexp[tid] = row_exp(mx);
+    }
+    __syncthreads();
+  }
 
   // loaders: A units (2 per thread) = (row, float4 of k), B units (3 per thread: one per plane)
-  int arow[2], akq[2];
+  int arow_[2], akq[2];
   bool aok[2];
+  float fa[2];
   const float* abase1[2];
   const float* abase2[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int v = tid + kGT * q;
-    arow[q] = v >> 3;
+    arow_[q] = v >> 3;
     akq[q] = v & 7;
-    const int64_t gr = m0 + arow[q];
+    fa[q] = NP == 2 ? ldexpf(1.f, sexp[arow_[q]]) : 1.f;
+    const int64_t gr = m0 + arow_[q];
     aok[q] = gr < M;
     const int64_t grc = gr < M ? gr : M - 1;
     abase1[q] = A1 + grc * lda1 + 4 * akq[q];
@@ -245,8 +272,8 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       f32x4 v = ringA[slot][q];
       if (!(live && aok[q])) v = f32x4{0.f, 0.f, 0.f, 0.f};
       unsigned pl[3][2];
-      split_planes<NP>(v, hs.fa, pl);
-      const int off = xoff(arow[q], akq[q] >> 1) + 8 * (akq[q] & 1);
+      split_planes<NP>(v, fa[q], pl);
+      const int off = xoff(arow_[q], akq[q] >> 1) + 8 * (akq[q] & 1);
 #pragma unroll
       for (int p = 0; p < NP; ++p)
         *reinterpret_cast<u32x2*>(buf + p * kPlane + off) = u32x2{pl[p][0], pl[p][1]};
@@ -306,11 +333,12 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       if (col >= N) continue;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t row = m0 + 64 * wm + 16 * r + 4 * g + q;
+        const int lr = 64 * wm + 16 * r + 4 * g + q;
+        const int64_t row = m0 + lr;
         if (row >= M) continue;
         const int64_t grp_r = row / cgrp;
         float* dst = C + grp_r * cldg + (row - grp_r * cgrp) * cldr + col * cldn;
-        const float v = NP == 3 ? acc[r][c][q] : acc[r][c][q] * hs.down;
+        const float v = NP == 3 ? acc[r][c][q] : ldexpf(acc[r][c][q], -(sexp[lr] + sb));
         if (ACC) *dst += v;
         else *dst = v;
       }
@@ -528,11 +556,12 @@ int split_w2_launch(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p, 
 template <int NP>
 int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1, int64_t K2,
                 const float* A2, int64_t lda2, const void* Bp, int64_t ldb, int64_t bplane,
-                const unsigned* amax, const unsigned* wmax, float* C, int64_t cgrp,
+                const float* arow, int64_t nparts, const unsigned* wmax, float* C, int64_t cgrp,
                 int64_t cldg, int64_t cldr, int64_t cldn, int accumulate, void* stream) {
   GMP_CHECK_ARG(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && cgrp >= 1);
   if (M == 0 || N == 0) return GMP_OK;
-  GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2) && (NP == 3 || (amax && wmax)));
+  GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2) &&
+                (NP == 3 || (arow && wmax && nparts >= 1 && nparts <= 4096)));
   GMP_CHECK_ARG(K1 % kBK == 0 && K2 % kBK == 0 && K1 + K2 > 0);
   GMP_CHECK_ARG(lda1 % 4 == 0 && (K2 == 0 || lda2 % 4 == 0) && ldb % 8 == 0 && bplane % 8 == 0);
   GMP_CHECK_ARG(ldb >= K1 + K2 && lda1 >= K1 && (K2 == 0 || lda2 >= K2));
@@ -542,7 +571,7 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   GMP_CHECK_ARG(tiles_m < (1LL << 31) && tiles_n < (1LL << 31));
   const int64_t nwg = tiles_m * tiles_n;
   GMP_CHECK_ARG(nwg < (1LL << 32));
-  const size_t smem = 2 * (size_t)(2 * NP * kPlane);
+  const size_t smem = 2 * (size_t)(2 * NP * kPlane) + (NP == 2 ? kBM * sizeof(int) : 0);
   int rc = 0;
   auto k = accumulate ? tp_gemm_x3_kernel<true, NP> : tp_gemm_x3_kernel<false, NP>;
   if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
@@ -552,7 +581,7 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   k<<<(unsigned)nwg, kGT, smem, as_stream(stream)>>>(
       M, (int)N, K1, A1, lda1, K2, K2 ? A2 : A1, K2 ? lda2 : lda1,
       static_cast<const unsigned short*>(Bp), ldb, bplane, C, cgrp, cldg, cldr, cldn,
-      (int)tiles_m, (int)tiles_n, amax, wmax);
+      (int)tiles_m, (int)tiles_n, arow, (int)nparts, wmax);
   return launch_status();
 }
 
@@ -616,17 +645,17 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
                        int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
                        int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
                        int64_t cldn, int accumulate, void* stream) {
-  return gemm_launch<3>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, nullptr, nullptr, C,
-                        cgrp, cldg, cldr, cldn, accumulate, stream);
+  return gemm_launch<3>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, nullptr, 0, nullptr,
+                        C, cgrp, cldg, cldr, cldn, accumulate, stream);
 }
 
 int gmp_tp_gemm_h2_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
                        int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
-                       int64_t bplane, const uint32_t* amax, const uint32_t* wmax, float* C,
-                       int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, int accumulate,
-                       void* stream) {
-  return gemm_launch<2>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, amax, wmax, C, cgrp,
-                        cldg, cldr, cldn, accumulate, stream);
+                       int64_t bplane, const float* arow, int64_t nparts, const uint32_t* wmax,
+                       float* C, int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn,
+                       int accumulate, void* stream) {
+  return gemm_launch<2>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, arow, nparts, wmax, C,
+                        cgrp, cldg, cldr, cldn, accumulate, stream);
 }
 
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,

@@ -28,24 +28,24 @@ constexpr int kMaxH = 256;
 // receiver for kOuterRB >= w / 64; measured slower than one 64-row block per workgroup: 10.1
 // vs 9.1 ms for the 32.8 GB MACE-128 lo = 2 path -- fewer workgroups in flight per CU)
 constexpr int kOuterRB = 1;
-// max |S|, |Sb| of the launch into *amax (float bit pattern, atomicMax; NULL = off): the scale
-// of the H2 path GEMM's A operand
-__device__ __forceinline__ void amax_commit(unsigned* amax, float v) {
-  if (!amax) return;
+// RMAX: each wave's max |S|, |Sb| over its 16 rows r0 .. r0 + 15 (all H columns) into
+// rmax[n (w / 16) + r0 / 16] (w % 16 == 0), no atomics: with mul1 % 16 == 0 the path GEMM's A
+// row (n, k) (columns (u, j) ++ u) owns the mul1 / 16 consecutive words from (n d3 + k) mul1 / 16
+// -- the per-row scales of its H2 form (gmp_tp_gemm_h2_f32)
+__device__ __forceinline__ void rmax_commit(float* rmax, int64_t n, int w, int r0, float v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(v));
+  if ((threadIdx.x & 63) == 0 && r0 < w) rmax[n * (w >> 4) + (r0 >> 4)] = v;
 }
 
-template <bool AMAX>
+template <bool RMAX>
 __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
                                                             const int64_t* __restrict__ eoff,
                                                             const float* __restrict__ Z,
                                                             const float* __restrict__ A,
                                                             float* __restrict__ S,
                                                             float* __restrict__ Sb,
-                                                            unsigned* __restrict__ amax) {
-  float lmax = 0.f;
+                                                            float* __restrict__ rmax) {
   __shared__ __attribute__((aligned(16))) float sA[kEdgeStage * (kMaxH + 16)];
   const int n = blockIdx.y;
   const int LDA = H + 16;  // 16 mod 64 floats: the 4 edge rows of an MFMA read hit disjoint banks
@@ -81,6 +81,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       const int cur = (rb - rb0) & 1;
       if (rb + 1 < rb1) zload(cur ^ 1, rb + 1);
       const int r = rb * kRowsPerBlock + wv * 16 + i;
+      float lmax = 0.f;
       f32x4 acc[kMaxH / 16];
 #pragma unroll
       for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
         for (int t = 0; t < kMaxH / 16; ++t)
           if (t < TJ) {
             *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
-            if (AMAX)
+            if (RMAX)
               lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
                                        fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
           }
@@ -109,9 +110,11 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       zsum += __shfl_xor(zsum, 16);
       zsum += __shfl_xor(zsum, 32);
       if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
-      if (AMAX && r < w) lmax = fmaxf(lmax, fabsf(zsum));
+      if (RMAX) {
+        if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
+        rmax_commit(rmax, n, w, rb * kRowsPerBlock + wv * 16, lmax);
+      }
     }
-    if (AMAX) amax_commit(amax, lmax);
     return;
   }
   if (deg <= kEdgeStage) {  // stage a once for all row blocks
@@ -128,6 +131,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
     // D = S^T tile: D[j][r] = sum_e A[e, j] Z[e, r]  (A op = a columns, B op = Z columns), so a
     // lane holds 4 consecutive j of one row r and stores them as one float4
     const int r = rb * kRowsPerBlock + wv * 16 + i;  // this lane's output row
+    float lmax = 0.f;
     f32x4 acc[kMaxH / 16];
 #pragma unroll
     for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       for (int t = 0; t < kMaxH / 16; ++t)
         if (t < TJ) {
           *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
-          if (AMAX)
+          if (RMAX)
             lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
                                      fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
         }
@@ -167,9 +171,11 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
     zsum += __shfl_xor(zsum, 16);
     zsum += __shfl_xor(zsum, 32);
     if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
-    if (AMAX && r < w) lmax = fmaxf(lmax, fabsf(zsum));
+    if (RMAX) {
+      if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
+      rmax_commit(rmax, n, w, rb * kRowsPerBlock + wv * 16, lmax);
+    }
   }
-  if (AMAX) amax_commit(amax, lmax);
 }
 
 // ---------------------------------------------------------------------------------- apply
@@ -536,19 +542,19 @@ int gmp_tp_apply_set_x3(int on) {
 }
 
 
-int gmp_tp_node_outer_amax_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
+int gmp_tp_node_outer_rmax_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                                const float* Z, const float* A, float* S, float* Sb,
-                               uint32_t* amax, void* stream) {
+                               float* rmax, void* stream) {
   GMP_CHECK_ARG(n_recv >= 0 && w > 0 && H > 0 && H <= kMaxH && H % 16 == 0);
   GMP_CHECK_ARG(n_recv <= 65535 * 1024);
   if (n_recv == 0) return GMP_OK;
-  GMP_CHECK_ARG(eoff && Z && A && S && Sb);
+  GMP_CHECK_ARG(eoff && Z && A && S && Sb && (!rmax || w % 16 == 0));
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0);
   if (n_recv > 65535) return GMP_ERR_UNSUPPORTED;  // grid.y limit: caller chunks receivers
   const dim3 grid((unsigned)ceil_div(w, kRowsPerBlock * kOuterRB), (unsigned)n_recv);
-  if (amax)
+  if (rmax)
     tp_node_outer_kernel<true><<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A,
-                                                                   S, Sb, amax);
+                                                                   S, Sb, rmax);
   else
     tp_node_outer_kernel<false><<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A,
                                                                     S, Sb, nullptr);
@@ -557,7 +563,7 @@ int gmp_tp_node_outer_amax_f32(int64_t n_recv, int64_t w, int64_t H, const int64
 
 int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                           const float* Z, const float* A, float* S, float* Sb, void* stream) {
-  return gmp_tp_node_outer_amax_f32(n_recv, w, H, eoff, Z, A, S, Sb, nullptr, stream);
+  return gmp_tp_node_outer_rmax_f32(n_recv, w, H, eoff, Z, A, S, Sb, nullptr, stream);
 }
 
 int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,

@@ -448,12 +448,17 @@ const uint32_t* u32p(const Tensor& t) {
 }
 
 std::tuple<Tensor, Tensor> tp_node_outer(const Tensor& eoff, const Tensor& Z, const Tensor& A,
-                                         int64_t w, const optional<Tensor>& amax) {
+                                         int64_t w, const optional<Tensor>& rmax) {
   const int64_t c = eoff.numel() - 1, H = A.size(1);
   Tensor S = at::empty({c, w, H}, A.options()), Sb = at::empty({c, w}, A.options());
-  check_rc(gmp_tp_node_outer_amax_f32(c, w, H, ip(i64(eoff, "eoff")), fp(Z), fp(f32(A, "A")),
-                                      fp(S), fp(Sb), u32p(amax), cur_stream()),
-           "gmp_tp_node_outer_amax_f32");
+  if (rmax.has_value()) {
+    f32(*rmax, "rmax");
+    TORCH_CHECK(rmax->numel() >= c * (w / 16), "gmp.tp_node_outer: rmax holds n_recv * w / 16");
+  }
+  check_rc(gmp_tp_node_outer_rmax_f32(c, w, H, ip(i64(eoff, "eoff")), fp(Z), fp(f32(A, "A")),
+                                      fp(S), fp(Sb), rmax.has_value() ? fp(*rmax) : nullptr,
+                                      cur_stream()),
+           "gmp_tp_node_outer_rmax_f32");
   return {S, Sb};
 }
 
@@ -481,15 +486,18 @@ Tensor tp_split_w2_h2(const Tensor& W2, const Tensor& b2, int64_t off, int64_t m
 void tp_gemm_h2(const Tensor& A1, int64_t K1, const optional<Tensor>& A2, int64_t K2,
                 const Tensor& Bp, int64_t ldb, int64_t N, Tensor C, int64_t c_offset,
                 int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, bool accumulate,
-                const Tensor& amax, const Tensor& wmax) {
+                const Tensor& arow, const Tensor& wmax) {
   f32(A1, "A1");
+  f32(arow, "arow");
   need(Bp, at::kShort, "B planes");
   TORCH_CHECK(C.is_cuda() && C.scalar_type() == at::kFloat, "gmp.tp_gemm_h2: C");
   const int64_t M = A1.size(0);
+  TORCH_CHECK(M > 0 && arow.numel() % M == 0, "gmp.tp_gemm_h2: arow holds M * nparts words");
   check_rc(gmp_tp_gemm_h2_f32(M, N, K1, fp(A1), A1.size(1), K2, cfp(A2),
                               A2.has_value() ? A2->size(1) : 0, Bp.data_ptr(), ldb, N * ldb,
-                              u32p(amax), u32p(wmax), C.data_ptr<float>() + c_offset, cgrp, cldg,
-                              cldr, cldn, accumulate, cur_stream()),
+                              fp(arow), arow.numel() / M, u32p(wmax),
+                              C.data_ptr<float>() + c_offset, cgrp, cldg, cldr, cldn, accumulate,
+                              cur_stream()),
            "gmp_tp_gemm_h2_f32");
 }
 
@@ -789,14 +797,14 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor? A3) -> Tensor");
   m.def("symmetric_contraction_bwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
         "Tensor? A3, Tensor gout) -> (Tensor dx, Tensor dA_partials)");
-  m.def("tp_node_outer(Tensor eoff, Tensor Z, Tensor A, int w, Tensor(a!)? amax=None) -> "
+  m.def("tp_node_outer(Tensor eoff, Tensor Z, Tensor A, int w, Tensor(a!)? rmax=None) -> "
         "(Tensor S, Tensor Sb)");
   m.def("absmax(Tensor x, Tensor(a!) amax) -> ()");
   m.def("tp_split_w2_h2(Tensor W2, Tensor b2, int off, int mul1, int mul_out, bool fwd, "
         "Tensor wmax) -> Tensor");
   m.def("tp_gemm_h2(Tensor A1, int K1, Tensor? A2, int K2, Tensor Bp, int ldb, int N, "
         "Tensor(a!) C, int c_offset, int cgrp, int cldg, int cldr, int cldn, bool accumulate, "
-        "Tensor amax, Tensor wmax) -> ()");
+        "Tensor arow, Tensor wmax) -> ()");
   m.def("tp_gemm_h2_widen(Tensor A, Tensor Bp, int N, Tensor amax, Tensor wmax) -> Tensor");
   m.def("tp_node_apply(Tensor eoff, Tensor Z, Tensor A, Tensor T, Tensor Tb, Tensor(a!) dA, "
         "Tensor(b!) dZ) -> ()");

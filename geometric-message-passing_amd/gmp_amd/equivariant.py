@@ -539,10 +539,13 @@ def node_form_ok(hidden):
 # Path GEMMs of the node form: "x3" = K7g (gmp_tpgemm.hip: bf16 MFMA over exact three-plane f32
 # splits; dW2p by the column-block split-plane outer sum), "torch" = the library f32 GEMMs.
 TP_GEMM = os.environ.get("GMP_TP_GEMM", "x3")
-# K7g's forward and T GEMMs in the H2 form (two fp16 planes with power-of-two scaling from
-# device-side max words, three MFMA products per step; gmp_tp_gemm_h2_f32): off by default —
-# measured slower on C4 (2.89 vs 2.66 s/step: every wave of the S kernel folds its max into
-# one word) and its 2^-21 products exceed the C4 rotation-invariance bound at 1M edges.
+# K7g's forward GEMM in the H2 form (two fp16 planes, three MFMA products per step;
+# gmp_tp_gemm_h2_f32) with per-row A scales from the S kernel's row-block maxima
+# (gmp_tp_node_outer_rmax_f32): off by default.  It is faster (9.1 vs 13.4 ms at the C4 lo = 2
+# shape, scripts/mb_tpgemm.py) but its operands carry 22 bits, not f32's 24: the C4 1M-edge
+# rotation-invariance check (test_mace_c4_full_size_properties, 1e-5 relative) measured
+# 2.9e-5 with it, so the f32-contract path stays three-plane.  The backward T GEMM is always
+# three-plane (bound by its T stores; the H2 widen kernel measured 13.7 vs 12.6 ms).
 TP_H2 = os.environ.get("GMP_TP_H2", "0") == "1"
 
 
@@ -605,7 +608,7 @@ class TPConvNodeFn(torch.autograd.Function):
         x3 = [_x3_ok(P, H) for P in plan.instructions]
         W2x = [None if ok else _w2_path(W2, b2, P) for P, ok in zip(plan.instructions, x3)]
         Bfs = [None] * len(x3)
-        wmaxs = [_w2_max(W2c, b2c, P) if (ok and TP_H2) else None
+        wmaxs = [_w2_max(W2c, b2c, P) if (ok and TP_H2 and P["mul1"] % 16 == 0) else None
                  for P, ok in zip(plan.instructions, x3)]
         for n0, n1, e0, e1, eoff, a, zbuf, _ in _node_chunks(lib, plan, graph, x, sh, rad_s,
                                                              W1, b1):
@@ -613,8 +616,9 @@ class TPConvNodeFn(torch.autograd.Function):
             for i, (P, (zoff, w)) in enumerate(zip(plan.instructions, plan.z_regions)):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                amax = _amax_word(dev) if wmaxs[i] is not None else None
-                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a, amax)
+                rmax = (torch.empty(c * (w // 16), dtype=torch.float32, device=dev)
+                        if wmaxs[i] is not None else None)
+                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a, rmax)
                 blk = plan.blocks[P["io"]]
                 if x3[i]:
                     # out[n, blk + w' d3 + k] += [S | Sb][(n, k), :] [W2p ; b2p][:, w'] (K7g)
@@ -622,11 +626,11 @@ class TPConvNodeFn(torch.autograd.Function):
                         Bfs[i] = _split_w2(lib, W2c, b2c, P, True, wmaxs[i])
                     K1 = m1 * H
                     with _timed("tp_node_W"):
-                        if amax is not None:
+                        if rmax is not None:
                             _lib.torch_ops().tp_gemm_h2(
                                 S.view(c * d3, K1), K1, Sb.view(c * d3, m1), m1, Bfs[i], K1 + m1,
                                 mo, out, n0 * out.shape[1] + blk[0], d3, out.shape[1], 1, d3,
-                                True, amax, wmaxs[i])
+                                True, rmax, wmaxs[i])
                         else:
                             _lib.torch_ops().tp_gemm_x3(
                                 S.view(c * d3, K1), K1, Sb.view(c * d3, m1), m1, Bfs[i], K1 + m1,
@@ -662,8 +666,7 @@ class TPConvNodeFn(torch.autograd.Function):
         W2x = [_w2_path(W2, b2, P) for P in plan.instructions]
         dW2x = [(torch.zeros_like(wp), torch.zeros_like(bp)) for wp, bp in W2x]
         Bts = [None] * len(x3)
-        wmaxs = [_w2_max(W2c, b2c, P) if (ok and TP_H2) else None
-                 for P, ok in zip(plan.instructions, x3)]
+        wmaxs = [None] * len(x3)  # the T GEMM stays three-plane (see TP_H2)
         first = True
         for n0, n1, e0, e1, eoff, a, zbuf, pre in _node_chunks(lib, plan, graph, x, sh, rad_s,
                                                                W1, b1):
@@ -736,9 +739,9 @@ class TPConvNodeFn(torch.autograd.Function):
         return dx, dsh, drad, dW1, db1, dW2, db2, None, None
 
 
-def _node_outer(lib, c, w, H, eoff, Zp, a, amax=None):
+def _node_outer(lib, c, w, H, eoff, Zp, a, rmax=None):
     with _timed("tp_node_S"):
-        return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w, amax)
+        return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w, rmax)
 
 
 def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):

@@ -270,39 +270,47 @@ def _h2_case(m1, mo, H, seed, wscale=1.0):
     return W2, b2, Bf, Bt
 
 
-@pytest.mark.parametrize("M,m1,mo,H,grp,ascale", [(1000, 32, 128, 64, 5, 1.0),
-                                                  (333, 64, 64, 32, 1, 1e-20),
-                                                  (130, 32, 96, 128, 3, 1e12)])
-def test_tp_gemm_h2_matches_fp64(M, m1, mo, H, grp, ascale):
-    """The H2 forward path GEMM (torch.ops.gmp.tp_split_w2_h2 + tp_gemm_h2: two fp16 planes
-    with power-of-two scaling from device max words) against fp64: error per entry <= 4e-6 of
-    sum |a b| (22-bit operands), ragged tiles, the bias operand, grouped epilogue accumulation,
-    and operands 1e-20 / 1e12 in scale (the dynamic scaling keeps them in fp16 range)."""
+@pytest.mark.parametrize("M,m1,mo,H,grp,ascale,nparts", [(1000, 32, 128, 64, 5, 1.0, 1),
+                                                         (333, 64, 64, 32, 1, 1e-20, 4),
+                                                         (130, 32, 96, 128, 3, 1e12, 2),
+                                                         (517, 32, 128, 64, 5, None, 2)])
+def test_tp_gemm_h2_matches_fp64(M, m1, mo, H, grp, ascale, nparts):
+    """The H2 forward path GEMM (torch.ops.gmp.tp_split_w2_h2 + tp_gemm_h2: two fp16 planes,
+    B scaled by its max word, A per row by the max of its `nparts` words) against fp64: error per
+    entry <= 4e-6 of sum |a b| (22-bit operands), ragged tiles, the bias operand, grouped
+    epilogue accumulation, operands 1e-20 / 1e12 in scale, and (ascale None) rows spread over
+    1e-30 .. 1e12 in one launch: each row keeps its own precision."""
     from gmp_amd import _lib
     tops = _lib.torch_ops()
     W2, b2, Bf, _ = _h2_case(m1, mo, H, M + H)
     g = torch.Generator().manual_seed(M)
     K1 = m1 * H
-    S = torch.randn(M, K1, generator=g) * torch.logspace(-2, 1, K1) * ascale
-    Sb = torch.randn(M, m1, generator=g) * ascale
+    rs = (torch.logspace(-30, 12, M)[torch.randperm(M, generator=g)].unsqueeze(1)
+          if ascale is None else ascale)
+    S = torch.randn(M, K1, generator=g) * torch.logspace(-2, 1, K1) * rs
+    Sb = torch.randn(M, m1, generator=g) * rs
     W2d, b2d = W2.to(DEV), b2.to(DEV)
     wmax = torch.zeros(1, dtype=torch.int32, device=DEV)
     tops.absmax(W2d, wmax)
     tops.absmax(b2d, wmax)
     planes = tops.tp_split_w2_h2(W2d, b2d, 0, m1, mo, True, wmax)
     Sd, Sbd = S.to(DEV), Sb.to(DEV)
-    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
-    tops.absmax(Sd, amax)
-    tops.absmax(Sbd, amax)
+    # per-row words: max |.| over nparts column chunks of [S | Sb] (the row max is their max)
+    arow = torch.stack([c.abs().amax(1) for c in torch.cat([S, Sb], 1).chunk(nparts, 1)], 1)
     nr = -(-M // grp)
-    C0 = torch.randn(nr, mo * grp + 5, generator=g) * ascale
+    C0 = torch.randn(nr, mo * grp + 5, generator=g) * (1.0 if ascale is None else ascale)
     C = C0.clone().to(DEV)
     tops.tp_gemm_h2(Sd, K1, Sbd, m1, planes, K1 + m1, mo, C, 0, grp, mo * grp + 5, 1, grp, True,
-                    amax, wmax)
+                    arow.contiguous().to(DEV), wmax)
     A = torch.cat([S, Sb], 1).double()
     ref = A @ Bf.t()
     mag = A.abs() @ Bf.abs().t()
     got = C.cpu().double() - C0.double()
+    if ascale is None:  # C0's entries are far above the small rows' results: compare C alone
+        C.zero_()
+        tops.tp_gemm_h2(Sd, K1, Sbd, m1, planes, K1 + m1, mo, C, 0, grp, mo * grp + 5, 1, grp,
+                        True, arow.contiguous().to(DEV), wmax)
+        got = C.cpu().double()
     rows = torch.arange(M)
     out = torch.empty(M, mo, dtype=torch.float64)
     for col in range(mo):
@@ -335,14 +343,18 @@ def test_tp_gemm_h2_widen_matches_fp64(M, m1, mo, H):
     assert err < 4e-6, err
 
 
-def test_tp_node_outer_amax_word():
-    """gmp_tp_node_outer_amax_f32 folds max |S|, |Sb| into the device word (float bits)."""
+@pytest.mark.parametrize("w", [96, 80])
+def test_tp_node_outer_rmax_words(w):
+    """gmp_tp_node_outer_rmax_f32 writes, for every receiver and 16-row block, max |S|, |Sb|
+    over the block (bit-exact: a max of the stored values), in both S-kernel branches
+    (in-degree <= 32 and above) and with a partial last 64-row block (w = 80)."""
     from gmp_amd import _lib
     degs = [0, 1, 31, 32, 33, 70, 20, 5]
-    w, H = 96, 64
+    H = 64
     eoff, Z, A, ne = _setup(degs, w, H, seed=3)
-    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
-    S, Sb = _lib.torch_ops().tp_node_outer(eoff.to(DEV), Z.to(DEV), A.to(DEV), w, amax)
-    want = max(S.abs().max().item(), Sb.abs().max().item())
-    got = amax.cpu().view(torch.float32).item()
-    assert got == want, (got, want)
+    rmax = torch.full((len(degs) * (w // 16),), -1.0, device=DEV)
+    S, Sb = _lib.torch_ops().tp_node_outer(eoff.to(DEV), Z.to(DEV), A.to(DEV), w, rmax)
+    n = len(degs)
+    want = torch.maximum(S.abs().view(n, w // 16, 16, H).amax((2, 3)),
+                         Sb.abs().view(n, w // 16, 16).amax(2))
+    assert torch.equal(rmax.view(n, w // 16), want)
