@@ -38,22 +38,35 @@ __device__ __forceinline__ void rmax_commit(float* rmax, int64_t n, int w, int r
   if ((threadIdx.x & 63) == 0 && r0 < w) rmax[n * (w >> 4) + (r0 >> 4)] = v;
 }
 
-template <bool RMAX>
-__global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
+// CS: the workgroup covers H / CS of the columns (grid.x = row blocks x CS, column part fastest):
+// CS = 2 halves the staged a rows (18 KB of LDS: 8 workgroups per CU instead of 4) at the cost
+// of loading each Z column twice (Z is ~1/H of the S bytes).
+// STG: the common branch's S rows leave through LDS (after the MFMAs, sA is free): per 64-column
+// chunk each wave parks its 16 x 64 tile and stores it back as whole 256-byte row segments (four
+// rows per store instruction) instead of sixteen 64-byte pieces per instruction.
+template <bool RMAX, bool STG, int CS>
+__global__ __launch_bounds__(kNT, CS == 2 ? 5 : 1) void tp_node_outer_kernel(int w, int H,
                                                             const int64_t* __restrict__ eoff,
                                                             const float* __restrict__ Z,
                                                             const float* __restrict__ A,
                                                             float* __restrict__ S,
                                                             float* __restrict__ Sb,
                                                             float* __restrict__ rmax) {
-  __shared__ __attribute__((aligned(16))) float sA[kEdgeStage * (kMaxH + 16)];
+  static_assert(!RMAX || CS == 1, "row maxima need every column of the row block");
+  constexpr int kMaxT = kMaxH / 16 / CS;  // 16-column tiles per workgroup (max)
+  __shared__ __attribute__((aligned(16))) float sA[kEdgeStage * (kMaxH / CS + 16)];
   const int n = blockIdx.y;
-  const int LDA = H + 16;  // 16 mod 64 floats: the 4 edge rows of an MFMA read hit disjoint banks
+  const int hc = H / CS, c0 = (CS == 1 ? 0 : (int)(blockIdx.x % CS)) * hc;
+  const int LDA = hc + 16;  // 16 mod 64 floats: the 4 edge rows of an MFMA read hit disjoint banks
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, i = lane & 15, kk = lane >> 4;
   const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
-  const int TJ = H >> 4;
-  float* Sn = S + (int64_t)n * w * H;
-  const int rb0 = blockIdx.x * kOuterRB;
+  // CS = 2 runs at H = kMaxH only, with the tile count a constant (a runtime bound on the
+  // predicated MFMAs made the compiler shuffle accumulators through thousands of moves)
+  const int TJ = CS > 1 ? kMaxT : hc >> 4;
+  const bool sb_out = c0 == 0;  // one column part writes Sb
+  float* Sn = S + (int64_t)n * w * H + c0;
+  const float* Ac = A + c0;
+  const int rb0 = (int)(blockIdx.x / CS) * kOuterRB;
   const int rb1 = min(rb0 + kOuterRB, (w + kRowsPerBlock - 1) / kRowsPerBlock);
   if (deg <= kEdgeStage) {
     // common case (one edge stage): this lane's Z column values for every k step of the next
@@ -70,10 +83,10 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       }
     };
     zload(0, rb0);
-    for (int x = tid; x < 4 * nst * (H >> 2); x += kNT) {  // padding rows zeroed
-      const int e = x / (H >> 2), q = x - e * (H >> 2);
+    for (int x = tid; x < 4 * nst * (hc >> 2); x += kNT) {  // padding rows zeroed
+      const int e = x / (hc >> 2), q = x - e * (hc >> 2);
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (e < ns) v = *reinterpret_cast<const f32x4*>(A + (e0 + e) * H + 4 * q);
+      if (e < ns) v = *reinterpret_cast<const f32x4*>(Ac + (e0 + e) * H + 4 * q);
       *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
     }
     __syncthreads();
@@ -82,9 +95,9 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
       if (rb + 1 < rb1) zload(cur ^ 1, rb + 1);
       const int r = rb * kRowsPerBlock + wv * 16 + i;
       float lmax = 0.f;
-      f32x4 acc[kMaxH / 16];
+      f32x4 acc[kMaxT];
 #pragma unroll
-      for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < kMaxT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       float zsum = 0.f;
 #pragma unroll
       for (int s = 0; s < kEdgeStage / 4; ++s) {
@@ -93,23 +106,52 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
           const float zv = zr[cur][s];
           zsum += zv;
 #pragma unroll
-          for (int t = 0; t < kMaxH / 16; ++t)
+          for (int t = 0; t < kMaxT; ++t)
             if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zv, acc[t], 0, 0, 0);
+          // keep the LDS operand reads inside their k step (hoisted, the narrow CS = 2 form
+          // held all of them at once: 246 VGPRs, one wave per SIMD)
+          if constexpr (CS > 1) asm volatile("" ::: "memory");
         }
       }
-      if (r < w) {
+      if (RMAX && r < w) {
 #pragma unroll
-        for (int t = 0; t < kMaxH / 16; ++t)
-          if (t < TJ) {
-            *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
-            if (RMAX)
-              lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
-                                       fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
+        for (int t = 0; t < kMaxT; ++t)
+          if (t < TJ)
+            lmax = fmaxf(lmax, fmaxf(fmaxf(fabsf(acc[t][0]), fabsf(acc[t][1])),
+                                     fmaxf(fabsf(acc[t][2]), fabsf(acc[t][3]))));
+      }
+      if constexpr (STG) {
+        static_assert(kOuterRB == 1, "the parked tiles overwrite the staged a rows");
+        constexpr int LDW = 68;  // 64 + 4 floats: the 16 rows of a parked tile spread banks
+        static_assert(4 * 16 * LDW <= kEdgeStage * (kMaxH / CS + 16), "park fits in sA");
+        float* park = sA + wv * 16 * LDW;
+        const int r0 = rb * kRowsPerBlock + wv * 16;
+#pragma unroll
+        for (int h = 0; h < (kMaxT + 3) / 4; ++h) {
+          if (4 * h >= TJ) break;  // uniform
+          __syncthreads();  // every wave is done with sA (MFMA operands / previous chunk)
+#pragma unroll
+          for (int t = 4 * h; t < 4 * h + 4; ++t)
+            if (t < TJ)
+              *reinterpret_cast<f32x4*>(park + i * LDW + 16 * (t - 4 * h) + 4 * kk) = acc[t];
+          __syncthreads();
+          const int cols = 16 * (min(TJ, 4 * h + 4) - 4 * h);  // this chunk's columns (<= 64)
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            const int idx = it * 64 + lane, row = idx >> 4, c4 = 4 * (idx & 15);
+            if (c4 < cols && r0 + row < w)
+              *reinterpret_cast<f32x4*>(Sn + (int64_t)(r0 + row) * H + 64 * h + c4) =
+                  *reinterpret_cast<const f32x4*>(park + row * LDW + c4);
           }
+        }
+      } else if (r < w) {
+#pragma unroll
+        for (int t = 0; t < kMaxT; ++t)
+          if (t < TJ) *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
       }
       zsum += __shfl_xor(zsum, 16);
       zsum += __shfl_xor(zsum, 32);
-      if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
+      if (kk == 0 && r < w && sb_out) Sb[(int64_t)n * w + r] = zsum;
       if (RMAX) {
         if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
         rmax_commit(rmax, n, w, rb * kRowsPerBlock + wv * 16, lmax);
@@ -117,50 +159,38 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
     }
     return;
   }
-  if (deg <= kEdgeStage) {  // stage a once for all row blocks
-    const int ns = (int)deg, ns4 = (ns + 3) & ~3;
-    for (int x = tid; x < ns4 * (H >> 2); x += kNT) {  // padding rows zeroed (0 * garbage = NaN)
-      const int e = x / (H >> 2), q = x - e * (H >> 2);
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (e < ns) v = *reinterpret_cast<const f32x4*>(A + (e0 + e) * H + 4 * q);
-      *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
-    }
-    __syncthreads();
-  }
   for (int rb = rb0; rb < rb1; ++rb) {
     // D = S^T tile: D[j][r] = sum_e A[e, j] Z[e, r]  (A op = a columns, B op = Z columns), so a
     // lane holds 4 consecutive j of one row r and stores them as one float4
     const int r = rb * kRowsPerBlock + wv * 16 + i;  // this lane's output row
     float lmax = 0.f;
-    f32x4 acc[kMaxH / 16];
+    f32x4 acc[kMaxT];
 #pragma unroll
-    for (int t = 0; t < kMaxH / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < kMaxT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float zsum = 0.f;  // Sb[n, r]: this lane's edges (k phase kk) of the Z column
     for (int64_t eb = 0; eb < deg; eb += kEdgeStage) {
       const int ns = (int)((deg - eb) < kEdgeStage ? (deg - eb) : kEdgeStage);
       const int ns4 = (ns + 3) & ~3;
-      if (deg > kEdgeStage) {
-        __syncthreads();
-        for (int x = tid; x < ns4 * (H >> 2); x += kNT) {
-          const int e = x / (H >> 2), q = x - e * (H >> 2);
-          f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (e < ns) v = *reinterpret_cast<const f32x4*>(A + (e0 + eb + e) * H + 4 * q);
-          *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
-        }
-        __syncthreads();
+      __syncthreads();
+      for (int x = tid; x < ns4 * (hc >> 2); x += kNT) {  // padding rows zeroed
+        const int e = x / (hc >> 2), q = x - e * (hc >> 2);
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (e < ns) v = *reinterpret_cast<const f32x4*>(Ac + (e0 + eb + e) * H + 4 * q);
+        *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
       }
+      __syncthreads();
       for (int s = 0; s < (ns4 >> 2); ++s) {
         const int el = 4 * s + kk;
         const float zv = (el < ns && r < w) ? Z[(e0 + eb + el) * w + r] : 0.f;
         zsum += zv;
 #pragma unroll
-        for (int t = 0; t < kMaxH / 16; ++t)
+        for (int t = 0; t < kMaxT; ++t)
           if (t < TJ) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[el * LDA + 16 * t + i], zv, acc[t], 0, 0, 0);
       }
     }
-    if (r < w) {  // streaming stores: S (GBs per chunk) is consumed by the next GEMM from HBM
+    if (r < w) {
 #pragma unroll
-      for (int t = 0; t < kMaxH / 16; ++t)
+      for (int t = 0; t < kMaxT; ++t)
         if (t < TJ) {
           *reinterpret_cast<f32x4*>(Sn + (int64_t)r * H + 16 * t + 4 * kk) = acc[t];
           if (RMAX)
@@ -170,7 +200,7 @@ __global__ __launch_bounds__(kNT) void tp_node_outer_kernel(int w, int H,
     }
     zsum += __shfl_xor(zsum, 16);
     zsum += __shfl_xor(zsum, 32);
-    if (kk == 0 && r < w) Sb[(int64_t)n * w + r] = zsum;
+    if (kk == 0 && r < w && sb_out) Sb[(int64_t)n * w + r] = zsum;
     if (RMAX) {
       if (r < w) lmax = fmaxf(lmax, fabsf(zsum));
       rmax_commit(rmax, n, w, rb * kRowsPerBlock + wv * 16, lmax);
@@ -531,6 +561,9 @@ namespace gmp {
 // 1: bf16x3 apply kernel where the shape allows (default); 0: the f32-MFMA kernel
 // (GMP_TP_APPLY_F32=1 or gmp_tp_apply_set_x3(0), A/B studies)
 int g_apply_x3 = getenv("GMP_TP_APPLY_F32") && atoi(getenv("GMP_TP_APPLY_F32")) ? 0 : 1;
+// S kernel stores through LDS (GMP_TP_OUTER_STAGE=0: direct MFMA-layout stores)
+int g_outer_stage = getenv("GMP_TP_OUTER_STAGE") ? atoi(getenv("GMP_TP_OUTER_STAGE")) : 1;
+int g_outer_cs = getenv("GMP_TP_OUTER_CS") ? atoi(getenv("GMP_TP_OUTER_CS")) : 2;
 }  // namespace gmp
 
 extern "C" {
@@ -551,13 +584,16 @@ int gmp_tp_node_outer_rmax_f32(int64_t n_recv, int64_t w, int64_t H, const int64
   GMP_CHECK_ARG(eoff && Z && A && S && Sb && (!rmax || w % 16 == 0));
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0);
   if (n_recv > 65535) return GMP_ERR_UNSUPPORTED;  // grid.y limit: caller chunks receivers
-  const dim3 grid((unsigned)ceil_div(w, kRowsPerBlock * kOuterRB), (unsigned)n_recv);
-  if (rmax)
-    tp_node_outer_kernel<true><<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A,
-                                                                   S, Sb, rmax);
-  else
-    tp_node_outer_kernel<false><<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A,
-                                                                    S, Sb, nullptr);
+  // two column parts for wide H without row maxima (GMP_TP_OUTER_CS=1: one)
+  const int cs = (!rmax && H == kMaxH && g_outer_cs == 2) ? 2 : 1;
+  const dim3 grid((unsigned)(ceil_div(w, kRowsPerBlock * kOuterRB) * cs), (unsigned)n_recv);
+  auto k = rmax ? (g_outer_stage ? tp_node_outer_kernel<true, true, 1>
+                                 : tp_node_outer_kernel<true, false, 1>)
+           : cs == 2 ? (g_outer_stage ? tp_node_outer_kernel<false, true, 2>
+                                      : tp_node_outer_kernel<false, false, 2>)
+                     : (g_outer_stage ? tp_node_outer_kernel<false, true, 1>
+                                      : tp_node_outer_kernel<false, false, 1>);
+  k<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb, rmax);
   return launch_status();
 }
 
