@@ -102,33 +102,51 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
   float dg[kMaxF], db[kMaxF];
 #pragma unroll
   for (int k = 0; k < kMaxF; ++k) dg[k] = db[k] = 0.f;
-  for (int64_t r = (int64_t)blockIdx.x * (kRowT / 64) + wv; r < rows;
-       r += (int64_t)gridDim.x * (kRowT / 64)) {
-    const float rs = rstd_in[r];
-    float g[kMaxF], xh[kMaxF];
-    float a = 0.f, b = 0.f;
+  // kRB consecutive rows per wave and step: their loads are issued together (the one-row loop
+  // was latency-bound: ~1 TB/s); the gamma / beta sums still add rows in increasing order
+  constexpr int kRB = 2;
+  const int64_t stride = (int64_t)gridDim.x * (kRowT / 64) * kRB;
+  for (int64_t r0 = ((int64_t)blockIdx.x * (kRowT / 64) + wv) * kRB; r0 < rows; r0 += stride) {
+    float rs[kRB], xh[kRB][kMaxF], gv[kRB][kMaxF];
 #pragma unroll
-    for (int k = 0; k < kMaxF; ++k) {
-      const int f = lane + 64 * k;
-      g[k] = 0.f;
-      xh[k] = 0.f;
-      if (f < d) {
-        xh[k] = xhat[r * d + f];
-        const float gm = gamma[f];
-        const float dz = gy[r * d + f] * act_grad<ACT>(xh[k] * gm + beta[f]);
-        dg[k] += dz * xh[k];
-        db[k] += dz;
-        g[k] = dz * gm;
+    for (int j = 0; j < kRB; ++j) {
+      const int64_t r = r0 + j;
+      const bool ok = r < rows;
+      rs[j] = ok ? rstd_in[r] : 0.f;
+#pragma unroll
+      for (int k = 0; k < kMaxF; ++k) {
+        const int f = lane + 64 * k;
+        xh[j][k] = (ok && f < d) ? xhat[r * d + f] : 0.f;
+        gv[j][k] = (ok && f < d) ? gy[r * d + f] : 0.f;
       }
-      a += g[k];
-      b += g[k] * xh[k];
     }
-    a = wave_sum(a) / (float)d;
-    b = wave_sum(b) / (float)d;
 #pragma unroll
-    for (int k = 0; k < kMaxF; ++k) {
-      const int f = lane + 64 * k;
-      if (f < d) gx[r * d + f] = rs * (g[k] - a - xh[k] * b);
+    for (int j = 0; j < kRB; ++j) {
+      const int64_t r = r0 + j;
+      if (r >= rows) break;  // wave-uniform
+      float g[kMaxF];
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < kMaxF; ++k) {
+        const int f = lane + 64 * k;
+        g[k] = 0.f;
+        if (f < d) {
+          const float gm = gamma[f];
+          const float dz = gv[j][k] * act_grad<ACT>(xh[j][k] * gm + beta[f]);
+          dg[k] += dz * xh[j][k];
+          db[k] += dz;
+          g[k] = dz * gm;
+        }
+        a += g[k];
+        b += g[k] * xh[j][k];
+      }
+      a = wave_sum(a) / (float)d;
+      b = wave_sum(b) / (float)d;
+#pragma unroll
+      for (int k = 0; k < kMaxF; ++k) {
+        const int f = lane + 64 * k;
+        if (f < d) gx[r * d + f] = rs[j] * (g[k] - a - xh[j][k] * b);
+      }
     }
   }
   // workgroup partial: waves in order

@@ -168,6 +168,56 @@ __device__ __forceinline__ void mma_np(f32x4 (&acc)[4][2], const Frag<NP>& f) {
   }
 }
 
+// The forward kernel's B operand comes straight from global memory in MFMA fragment order
+// (gmp_tp_split_w2_f32 writes it so): one 16-byte load per lane per (column tile, plane) and
+// k step, no LDS image.  Element (plane p, column n, k) of an N-column, K-deep operand sits at
+//   ((((k / 32) * (N / 16) + n / 16) * NP + p) * 64 + n % 16 + 16 * ((k % 32) / 8)) * 8 + k % 8
+// (ushort units): lane l of the (k step, column tile, plane) block holds B[16 ct + l % 16]
+// [32 ks + 8 (l / 16) .. + 7], exactly the B operand of v_mfma_f32_16x16x32_{bf16,f16}.
+__host__ __device__ __forceinline__ int64_t bfrag_index(int64_t p, int64_t n, int64_t k,
+                                                        int64_t ct_total, int np) {
+  return ((((k >> 5) * ct_total + (n >> 4)) * np + p) * 64 + (n & 15) + 16 * ((k & 31) >> 3)) *
+             8 + (k & 7);
+}
+template <int NP>
+struct FragA {
+  u32x4 a[4][NP];
+};
+template <int NP>
+__device__ __forceinline__ void load_frag_a(FragA<NP>& f, const unsigned char* aimg, int wm,
+                                            int li, int g) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int off = xoff(64 * wm + 16 * r + li, g);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) f.a[r][p] = *reinterpret_cast<const u32x4*>(aimg + p * kPlane + off);
+  }
+}
+template <int NP>
+__device__ __forceinline__ void mma_ab(f32x4 (&acc)[4][2], const FragA<NP>& f,
+                                       const u32x4 (&b)[2][NP]) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      f32x4 t = acc[r][c];
+      if constexpr (NP == 3) {
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][2]), asb(b[c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][1]), asb(b[c][1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][0]), asb(b[c][2]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][1]), asb(b[c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][0]), asb(b[c][1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(f.a[r][0]), asb(b[c][0]), t, 0, 0, 0);
+      } else {
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ash(f.a[r][1]), ash(b[c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ash(f.a[r][0]), ash(b[c][1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ash(f.a[r][0]), ash(b[c][0]), t, 0, 0, 0);
+      }
+      acc[r][c] = t;
+    }
+  }
+}
+
 // H2 scale factors of a launch: x A by 2^sa before the split, results by 2^-(sa + sb)
 struct H2Scale {
   float fa, down;
@@ -189,7 +239,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t ldb, int64_t bplane, float* __restrict__ C, int64_t cgrp, int64_t cldg,
     int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const float* __restrict__ arow,
     int nparts, const unsigned* __restrict__ wmax) {
-  constexpr int STG = 2 * NP * kPlane;  // LDS bytes per stage (A planes, then B planes)
+  constexpr int STG = NP * kPlane;  // LDS bytes per stage (A planes; B skips LDS)
   extern __shared__ __attribute__((aligned(16))) unsigned char smg[];
   int* sexp = reinterpret_cast<int*>(smg + 2 * STG);  // H2: the tile's 128 row exponents
   const int tid = threadIdx.x, lane = tid & 63;
@@ -246,13 +296,20 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     abase1[q] = A1 + grc * lda1 + 4 * akq[q];
     abase2[q] = A2 ? A2 + grc * lda2 + 4 * akq[q] : abase1[q];
   }
-  const int brow = tid >> 2, bch = tid & 3;
-  const bool bok = n0 + brow < N;
-  const unsigned short* bbase =
-      Bp + (n0 + brow < N ? n0 + brow : (int64_t)N - 1) * ldb + 8 * bch;
+  // this wave's two B column tiles (fragment order; tiles past N read tile 0, zeroed)
+  const int64_t ct_total = N / 16;
+  int64_t bct[2];
+  bool bok[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int64_t ct = (n0 >> 4) + 2 * wn + c;
+    bok[c] = ct < ct_total;
+    bct[c] = bok[c] ? ct : 0;
+  }
+  const unsigned short* bl = Bp + 8 * lane;
 
   f32x4 ringA[2][2];
-  u32x4 ringB[2][NP];
+  u32x4 ringB[2][2][NP];
   auto fetch = [&](int slot, int st) {
     const int stc = st < nst ? st : nst - 1;
     const int64_t k0 = (int64_t)stc * kBK;
@@ -261,9 +318,16 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       const float* p = k0 < K1 ? abase1[q] + k0 : abase2[q] + (k0 - K1);
       ringA[slot][q] = *reinterpret_cast<const f32x4*>(p);
     }
+  };
+  auto fetch_b = [&](int slot, int st) {
+    const int64_t stc = st < nst ? st : nst - 1;
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-      ringB[slot][p] = *reinterpret_cast<const u32x4*>(bbase + p * bplane + k0);
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        u32x4 v = *reinterpret_cast<const u32x4*>(bl + ((stc * ct_total + bct[c]) * NP + p) * 512);
+        ringB[slot][c][p] = bok[c] ? v : u32x4{0u, 0u, 0u, 0u};
+      }
   };
   auto stash = [&](int slot, unsigned char* buf, int st) {
     const bool live = st < nst;
@@ -278,33 +342,29 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       for (int p = 0; p < NP; ++p)
         *reinterpret_cast<u32x2*>(buf + p * kPlane + off) = u32x2{pl[p][0], pl[p][1]};
     }
-    const int off = xoff(brow, bch);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      u32x4 v = ringB[slot][p];
-      if (!(live && bok)) v = u32x4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(buf + (NP + p) * kPlane + off) = v;
-    }
   };
 
   f32x4 acc[4][2];
 #pragma unroll
   for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // Pipeline (stage t's registers in ring slot t & 1, its LDS image in buffer t & 1):
-  //   iteration s: read the fragments of s + 1 | MFMAs of s | split + write stage s + 2 into
-  //   the buffer stage s used (its fragments are in registers, read before the last barrier)
-  //   | load stage s + 4 | barrier.
-  // Stages past nst (rounded up to the unroll) load clamped addresses and stash zeros.
+  // Pipeline (stage t's A registers in ring slot t & 1, its LDS image in buffer t & 1; its B
+  // fragments in ringB[t & 1], loaded two stages ahead):
+  //   iteration s: split + write A of stage s + 2 into the buffer stage s used (its fragments
+  //   are in registers, read before the last barrier) | load A of s + 4 | read the A fragments
+  //   of s + 1 | MFMAs of s | load B of s + 2 into the slot they read | barrier.
+  // Stages past nst load clamped addresses; their A is stashed as zeros.
   const int nst_pad = (nst + 1) & ~1;
-  Frag<NP> F[2];
+  FragA<NP> F[2];
   fetch(0, 0);
   fetch(1, 1);
+  fetch_b(0, 0);
+  fetch_b(1, 1);
   stash(0, smg, 0);
   fetch(0, 2);
   stash(1, smg + STG, 1);
   fetch(1, 3);
   __syncthreads();
-  load_frag<NP>(F[0], smg, smg + NP * kPlane, wm, wn, li, g);
+  load_frag_a<NP>(F[0], smg, wm, li, g);
   __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
   for (int s0 = 0; s0 < nst_pad; s0 += 2) {
 #pragma unroll
@@ -318,8 +378,10 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       __builtin_amdgcn_sched_barrier(0);
       fetch(j, st + 4);
       __builtin_amdgcn_sched_barrier(0);
-      load_frag<NP>(F[j ^ 1], nb, nb + NP * kPlane, wm, wn, li, g);
-      mma_np<NP>(acc, F[j]);
+      load_frag_a<NP>(F[j ^ 1], nb, wm, li, g);
+      mma_ab<NP>(acc, F[j], ringB[j]);
+      __builtin_amdgcn_sched_barrier(0);
+      fetch_b(j, st + 2);  // the slot the MFMAs above just read: two stages of lead
       __syncthreads();
     }
   }
@@ -360,8 +422,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
     int64_t ldc, int tiles_m, int tiles_n, int n_split, const unsigned* __restrict__ amax,
     const unsigned* __restrict__ wmax) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
-  unsigned char* sA = smw;                          // NKS x NP planes
-  unsigned char* sB = smw + NKS * NP * kPlane;      // 2 stages x NP planes
+  unsigned char* sA = smw;  // NKS x NP planes (B goes straight to registers, fragment order)
   const H2Scale hs = h2_scale<NP>(amax, wmax);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -398,26 +459,25 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
       *reinterpret_cast<u32x2*>(img + p * kPlane + off) = u32x2{pl[p][0], pl[p][1]};
   }
 
-  const int brow = tid >> 2, bch = tid & 3;
   const int nst = (int)((t1 - t0) * NKS);
-  u32x4 ringB[2][NP];
-  bool bok_slot[2];
-  auto fetch = [&](int slot, int gs) {
+  const int64_t ct_total = N / 16;
+  const unsigned short* bl = Bp + 8 * lane;
+  u32x4 ringB[2][2][NP];
+  // B fragments of global step gs (tile t0 + gs / NKS, k step gs % NKS) for this wave's two
+  // column tiles; steps past the range and tiles past N read a clamped block and are zeroed
+  auto fetch_b = [&](int slot, int gs) {
     const int gsc = gs < nst ? gs : nst - 1;
-    const int64_t n = (t0 + gsc / NKS) * kBN + brow;
-    const int64_t k0 = (int64_t)(gsc % NKS) * kBK;
-    bok_slot[slot] = gs < nst && n < N;
-    const unsigned short* p = Bp + (n < N ? n : N - 1) * ldb + k0 + 8 * bch;
+    const int64_t ks = gsc % NKS;
 #pragma unroll
-    for (int pl = 0; pl < NP; ++pl) ringB[slot][pl] = *reinterpret_cast<const u32x4*>(p + pl * bplane);
-  };
-  auto stash = [&](int slot, unsigned char* buf) {
-    const int off = xoff(brow, bch);
+    for (int c = 0; c < 2; ++c) {
+      const int64_t ct = (t0 + gsc / NKS) * (kBN / 16) + 2 * wn + c;
+      const bool ok = gs < nst && ct < ct_total;
+      const int64_t ctc = ct < ct_total ? ct : ct_total - 1;
 #pragma unroll
-    for (int pl = 0; pl < NP; ++pl) {
-      u32x4 v = ringB[slot][pl];
-      if (!bok_slot[slot]) v = u32x4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(buf + pl * kPlane + off) = v;
+      for (int p = 0; p < NP; ++p) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(bl + ((ks * ct_total + ctc) * NP + p) * 512);
+        ringB[slot][c][p] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+      }
     }
   };
   f32x4 acc[4][2];
@@ -441,32 +501,24 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
     }
   };
 
-  // same pipeline as tp_gemm_x3_kernel over the global step index gs (tile t0 + gs / NKS, k
-  // step gs % NKS); A fragments from the resident images, B through two LDS stages
-  Frag<NP> F[2];
-  fetch(0, 0);
-  fetch(1, 1);
-  stash(0, sB);
-  fetch(0, 2);
-  stash(1, sB + NP * kPlane);
-  fetch(1, 3);
-  __syncthreads();  // A images and B stages 0, 1
-  load_frag<NP>(F[0], sA, sB, wm, wn, li, g);
-  __syncthreads();
+  // over the global step index gs: A fragments from the resident images (read one step ahead),
+  // B fragments from global memory two steps ahead (into the ring slot the MFMAs just read);
+  // nothing is written to LDS after the A images, so the loop has no barrier
+  FragA<NP> F[2];
+  fetch_b(0, 0);
+  fetch_b(1, 1);
+  __syncthreads();  // A images
+  load_frag_a<NP>(F[0], sA, wm, li, g);
   const int nst_pad = (nst + 1) & ~1;
   for (int s0 = 0; s0 < nst_pad; s0 += 2) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int gs = s0 + j;
-      stash(j, sB + (gs & 1) * NP * kPlane);
+      load_frag_a<NP>(F[j ^ 1], sA + ((gs + 1) % NKS) * NP * kPlane, wm, li, g);
+      mma_ab<NP>(acc, F[j], ringB[j]);
       __builtin_amdgcn_sched_barrier(0);
-      fetch(j, gs + 4);
-      __builtin_amdgcn_sched_barrier(0);
-      load_frag<NP>(F[j ^ 1], sA + ((gs + 1) % NKS) * NP * kPlane,
-                    sB + ((gs + 1) & 1) * NP * kPlane, wm, wn, li, g);
-      mma_np<NP>(acc, F[j]);
+      fetch_b(j, gs + 2);
       if (gs < nst && gs % NKS == NKS - 1) store_tile(t0 + gs / NKS);
-      __syncthreads();
     }
   }
 }
@@ -496,8 +548,7 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
   __shared__ float tile[128][65];
   const float fs = NP == 3 ? 1.f : ldexpf(1.f, scale_exp_bits(wmax ? wmax[0] : 0u));
   const int u = blockIdx.y, j0 = blockIdx.x * 64, tid = threadIdx.x;
-  const int64_t K1 = (int64_t)mul1 * H, ldf = K1 + mul1;
-  const int64_t pf = (int64_t)mo * ldf, pt = K1 * mo;
+  const int64_t K1 = (int64_t)mul1 * H;
   for (int x = tid; x < mo * 64; x += 256) {
     const int wr = x >> 6, j = x & 63;
     const float v = (j0 + j < H) ? W2[((int64_t)u * mo + wr) * H + j0 + j] : 0.f;
@@ -510,9 +561,9 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
     if (j0 + j >= H) continue;
     unsigned p[3];
     split1<NP>(tile[wr][j], fs, p);
-    const int64_t o = (int64_t)wr * ldf + (int64_t)u * H + j0 + j;
 #pragma unroll
-    for (int q = 0; q < NP; ++q) Bf[q * pf + o] = (unsigned short)p[q];
+    for (int q = 0; q < NP; ++q)
+      Bf[bfrag_index(q, wr, (int64_t)u * H + j0 + j, mo / 16, NP)] = (unsigned short)p[q];
   }
   if (Bt) {  // Bt[p][u H + j0 + j][w]: rows k, mo consecutive w
     for (int x = tid; x < mo * 64; x += 256) {
@@ -520,18 +571,18 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
       if (j0 + j >= H) continue;
       unsigned p[3];
       split1<NP>(tile[wr][j], fs, p);
-      const int64_t o = ((int64_t)u * H + j0 + j) * mo + wr;
 #pragma unroll
-      for (int q = 0; q < NP; ++q) Bt[q * pt + o] = (unsigned short)p[q];
+      for (int q = 0; q < NP; ++q)
+        Bt[bfrag_index(q, (int64_t)u * H + j0 + j, wr, K1 / 16, NP)] = (unsigned short)p[q];
     }
   }
   if (Bf && blockIdx.x == 0) {  // bias columns of Bf: Bf[p][w][K1 + u]
     for (int wr = tid; wr < mo; wr += 256) {
       unsigned p[3];
       split1<NP>(b2[(int64_t)u * mo + wr], fs, p);
-      const int64_t o = (int64_t)wr * ldf + K1 + u;
 #pragma unroll
-      for (int q = 0; q < NP; ++q) Bf[q * pf + o] = (unsigned short)p[q];
+      for (int q = 0; q < NP; ++q)
+        Bf[bfrag_index(q, wr, K1 + u, mo / 16, NP)] = (unsigned short)p[q];
     }
   }
 }
@@ -546,6 +597,9 @@ int split_w2_launch(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p, 
                     const unsigned* wmax, void* Bf, void* Bt, void* stream) {
   GMP_CHECK_ARG(mul1 > 0 && mul_out > 0 && mul_out <= 128 && H > 0 && mul1 <= 65535);
   GMP_CHECK_ARG(W2p && b2p && (Bf || Bt) && (NP == 3 || wmax));
+  // fragment order: Bf (mul_out x (mul1 H + mul1)), Bt (mul1 H x mul_out)
+  GMP_CHECK_ARG(!Bf || (mul_out % 16 == 0 && (mul1 * H + mul1) % 32 == 0));
+  GMP_CHECK_ARG(!Bt || (mul_out % 32 == 0 && (mul1 * H) % 16 == 0));
   tp_split_w2_kernel<NP><<<dim3((unsigned)ceil_div(H, 64), (unsigned)mul1), 256, 0,
                            as_stream(stream)>>>((int)mul1, (int)mul_out, (int)H, W2p, b2p,
                                                 static_cast<unsigned short*>(Bf),
@@ -562,16 +616,18 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   if (M == 0 || N == 0) return GMP_OK;
   GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2) &&
                 (NP == 3 || (arow && wmax && nparts >= 1 && nparts <= 4096)));
-  GMP_CHECK_ARG(K1 % kBK == 0 && K2 % kBK == 0 && K1 + K2 > 0);
-  GMP_CHECK_ARG(lda1 % 4 == 0 && (K2 == 0 || lda2 % 4 == 0) && ldb % 8 == 0 && bplane % 8 == 0);
-  GMP_CHECK_ARG(ldb >= K1 + K2 && lda1 >= K1 && (K2 == 0 || lda2 >= K2));
+  GMP_CHECK_ARG(K1 % kBK == 0 && K2 % kBK == 0 && K1 + K2 > 0 && N % 16 == 0);
+  GMP_CHECK_ARG(lda1 % 4 == 0 && (K2 == 0 || lda2 % 4 == 0));
+  // B is fragment-ordered (bfrag_index): the row-major strides it replaced must be the dense ones
+  GMP_CHECK_ARG(ldb == K1 + K2 && bplane == N * (K1 + K2));
+  GMP_CHECK_ARG(lda1 >= K1 && (K2 == 0 || lda2 >= K2));
   GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A1) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
   GMP_CHECK_ARG(K2 == 0 || reinterpret_cast<uintptr_t>(A2) % 16 == 0);
   const int64_t tiles_m = ceil_div(M, kBM), tiles_n = ceil_div(N, kBN);
   GMP_CHECK_ARG(tiles_m < (1LL << 31) && tiles_n < (1LL << 31));
   const int64_t nwg = tiles_m * tiles_n;
   GMP_CHECK_ARG(nwg < (1LL << 32));
-  const size_t smem = 2 * (size_t)(2 * NP * kPlane) + (NP == 2 ? kBM * sizeof(int) : 0);
+  const size_t smem = 2 * (size_t)(NP * kPlane) + (NP == 2 ? kBM * sizeof(int) : 0);
   int rc = 0;
   auto k = accumulate ? tp_gemm_x3_kernel<true, NP> : tp_gemm_x3_kernel<false, NP>;
   if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
@@ -591,8 +647,9 @@ int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
                  float* C, int64_t ldc, void* stream) {
   GMP_CHECK_ARG(M >= 0 && N >= 0 && K > 0 && K % kBK == 0 && K <= kBK * kMaxKS);
   if (M == 0 || N == 0) return GMP_OK;
-  GMP_CHECK_ARG(A && Bp && C && lda >= K && lda % 4 == 0 && ldb >= K && ldb % 8 == 0 &&
-                bplane % 8 == 0 && ldc >= N && (NP == 3 || (amax && wmax)));
+  GMP_CHECK_ARG(A && Bp && C && lda >= K && lda % 4 == 0 && ldc >= N && N % 16 == 0 &&
+                (NP == 3 || (amax && wmax)));
+  GMP_CHECK_ARG(ldb == K && bplane == N * K);  // B fragment-ordered (bfrag_index)
   GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
   const int64_t tiles_m = ceil_div(M, kBM), tiles_n = ceil_div(N, kBN);
   GMP_CHECK_ARG(tiles_m < (1LL << 30) && tiles_n < (1LL << 30));
@@ -604,7 +661,7 @@ int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
   const int64_t nwg = tiles_m * n_split;
   GMP_CHECK_ARG(nwg < (1LL << 32));
   const int nks = (int)(K / kBK);
-  const size_t smem = (size_t)(nks * NP + 2 * NP) * kPlane;
+  const size_t smem = (size_t)(nks * NP) * kPlane;
   hipStream_t s = as_stream(stream);
   const unsigned short* B = static_cast<const unsigned short*>(Bp);
   int rc = 0;

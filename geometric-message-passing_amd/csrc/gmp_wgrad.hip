@@ -158,40 +158,40 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
   }
 }
 
-// Ordered two-level reduction of the G partial slabs: level 1 sums chunks of kGC slabs
-// (grid = X/256 x ceil(G/kGC)), level 2 sums the level-1 results in chunk order.
-constexpr int kGC = 16;
-__global__ void sum_partials_l1(const float* __restrict__ partial, int64_t G, int64_t X,
-                                float* __restrict__ l1) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t c = blockIdx.y;
-  if (x >= X) return;
-  const int64_t g0 = c * kGC, g1 = (g0 + kGC < G) ? g0 + kGC : G;
-  float v[kGC];
-#pragma unroll
-  for (int u = 0; u < kGC; ++u) v[u] = (g0 + u < g1) ? partial[(g0 + u) * X + x] : 0.f;
+constexpr int kGC = 16;  // slab loads in flight per lane in the ordered partial sums
+
+// One-pass ordered sum of the G partial slabs (replaces l1 + l2 on the split-K paths): a
+// workgroup owns 64 columns x; its 4 waves each add a contiguous quarter of the slabs (slab
+// order, 16 loads in flight per lane), then wave 0 adds the 4 quarter sums in wave order --
+// a fixed order independent of timing (deterministic), 4 x the parallelism of l2 and one
+// launch instead of two.
+constexpr int kSumW = 4;
+__global__ __launch_bounds__(64 * kSumW) void sum_partials_one(const float* __restrict__ part,
+                                                               int64_t G, int64_t X,
+                                                               float* __restrict__ out,
+                                                               float* __restrict__ colsum,
+                                                               int64_t DD, int64_t n,
+                                                               int64_t ldc) {
+  __shared__ float red[kSumW][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t x = blockIdx.x * (int64_t)64 + lane;
+  const int64_t q = (G + kSumW - 1) / kSumW, g0 = wv * q, g1 = (g0 + q < G) ? g0 + q : G;
   float s = 0.f;
+  if (x < X) {
+    for (int64_t c0 = g0; c0 < g1; c0 += kGC) {
+      float v[kGC];
 #pragma unroll
-  for (int u = 0; u < kGC; ++u) s += v[u];
-  l1[c * X + x] = s;
-}
-// writes C (rows x n, row stride ldc) and colsum (rows) from the dense level-1 slabs
-__global__ void sum_partials_l2(const float* __restrict__ l1, int64_t C, int64_t X,
-                                float* __restrict__ out, float* __restrict__ colsum, int64_t DD,
-                                int64_t n, int64_t ldc) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= X) return;
-  // the level-1 values are loaded kGC at a time before they are added (in slab order, as a
-  // plain loop would): one memory round trip per kGC slabs instead of one per slab
-  float s = 0.f;
-  for (int64_t c0 = 0; c0 < C; c0 += kGC) {
-    float v[kGC];
+      for (int u = 0; u < kGC; ++u) v[u] = (c0 + u < g1) ? part[(c0 + u) * X + x] : 0.f;
 #pragma unroll
-    for (int u = 0; u < kGC; ++u) v[u] = (c0 + u < C) ? l1[(c0 + u) * X + x] : 0.f;
-#pragma unroll
-    for (int u = 0; u < kGC; ++u)
-      if (c0 + u < C) s += v[u];
+      for (int u = 0; u < kGC; ++u)
+        if (c0 + u < g1) s += v[u];
+    }
   }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv != 0 || x >= X) return;
+#pragma unroll
+  for (int w = 1; w < kSumW; ++w) s += red[w][lane];
   if (x < DD) out[(x / n) * ldc + x % n] = s;
   else if (colsum) colsum[x - DD] = s;
 }
@@ -734,13 +734,8 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;
-  const int64_t NC = ceil_div(Gr, kGC);
-  float* l1 = part + Gr * X;
-  sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
-  rc = launch_status();
-  if (rc) return rc;
-  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, m * n, n,
-                                                             ldc);
+  sum_partials_one<<<(unsigned)ceil_div(X, 64), 64 * kSumW, 0, s>>>(part, Gr, X, C, colsum_A,
+                                                                    m * n, n, ldc);
   return launch_status();
 }
 
@@ -865,13 +860,8 @@ static int outer_sum_launch(int64_t K, int64_t d, const float* A, int64_t lda, c
   int rc = launch_status();
   if (rc) return rc;
   const int64_t X = d * d + d;
-  const int64_t NC = ceil_div(Gr, kGC);
-  float* l1 = part + Gr * X;
-  sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
-  rc = launch_status();
-  if (rc) return rc;
-  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, d * d, d,
-                                                             ldc);
+  sum_partials_one<<<(unsigned)ceil_div(X, 64), 64 * kSumW, 0, s>>>(part, Gr, X, C, colsum_A,
+                                                                    d * d, d, ldc);
   return launch_status();
 }
 
@@ -986,13 +976,8 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;
-  const int64_t NC = ceil_div(Gr, kGC);
-  float* l1 = part + Gr * X;
-  sum_partials_l1<<<dim3((unsigned)ceil_div(X, 256), (unsigned)NC), 256, 0, s>>>(part, Gr, X, l1);
-  rc = launch_status();
-  if (rc) return rc;
-  sum_partials_l2<<<(unsigned)ceil_div(X, 256), 256, 0, s>>>(l1, NC, X, C, colsum_A, m * n, n,
-                                                             ldc);
+  sum_partials_one<<<(unsigned)ceil_div(X, 64), 64 * kSumW, 0, s>>>(part, Gr, X, C, colsum_A,
+                                                                    m * n, n, ldc);
   return launch_status();
 }
 

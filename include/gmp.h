@@ -376,13 +376,18 @@ int gmp_tp_apply_set_x3(int on);
  * T = G W2p^T of tfn_layer.py:73-87 regrouped; f32-class accuracy, see gmp_tpgemm.hip).
  * split_w2: from one path's block of the second radial Linear, W2p (mul1 * mul_out rows (u, w)
  *   of H floats) and b2p (mul1 * mul_out), writes (each if not null) the forward B planes Bf
- *   [3][mul_out][mul1 H + mul1] (bf16: Bf[w][u H + j] = W2[(u, w), j], Bf[w][mul1 H + u] =
- *   b2[u, w]) and the backward B planes Bt [3][mul1 H][mul_out] (Bt[u H + j][w] = W2[(u, w), j]).
+ *   (bf16 values B[p][w][u H + j] = W2[(u, w), j], B[p][w][mul1 H + u] = b2[u, w], stored in
+ *   MFMA fragment order, below; mul_out % 16 == 0) and the backward B planes Bt (values
+ *   B[p][u H + j][w] = W2[(u, w), j], an N = mul1 H by K = mul_out operand in the same fragment
+ *   order; mul_out % 32 == 0).
  * gemm_x3: C (+)= [A1 | A2] B^T for A1 (M x K1, row stride lda1), A2 (M x K2, lda2; K2 may be 0),
- *   B planes [3][N][ldb] bf16 (plane stride bplane elements, row k range [0, K1 + K2));
- *   element (r, col) of C at (r / cgrp) cldg + (r % cgrp) cldr + col cldn (accumulate != 0:
- *   C += result).  K1, K2 multiples of 32; lda*, ldb, bplane multiples of 4 / 8; A, B 16-byte
- *   aligned.  Deterministic (no atomics, fixed k order). */
+ *   B = 3 bf16 planes of an N x (K1 + K2) operand in fragment order: value (p, n, k) at
+ *   ((((k / 32) (N / 16) + n / 16) 3 + p) 64 + n % 16 + 16 ((k % 32) / 8)) 8 + k % 8 (each
+ *   64-lane block is one v_mfma_f32_16x16x32 B operand; the kernel loads it straight into
+ *   registers); ldb = K1 + K2 and bplane = N ldb are checked (the dense sizes); N % 16 == 0.
+ *   Element (r, col) of C at (r / cgrp) cldg + (r % cgrp) cldr + col cldn (accumulate != 0:
+ *   C += result).  K1, K2 multiples of 32; lda* multiples of 4; A, B 16-byte aligned.
+ *   Deterministic (no atomics, fixed k order). */
 int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
                         const float* b2p, void* Bf, void* Bt, void* stream);
 int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
@@ -390,9 +395,11 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
                        int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
                        int64_t cldn, int accumulate, void* stream);
 /* Short-K, wide-N form of gemm_x3 (the backward T = G W2p^T: K = mul_out <= 128, N = mul1 H):
- *   C (M x N, row stride ldc) = A B^T, A (M x K, lda) f32, B planes [3][N][ldb] bf16;
+ *   C (M x N, row stride ldc) = A B^T, A (M x K, lda) f32, B = 3 bf16 planes of the N x K
+ *   operand in gemm_x3's fragment order (ldb = K, bplane = N K checked; N % 16 == 0);
  * K a multiple of 32, <= 128.  Each workgroup keeps its split A rows in LDS and sweeps a range
- * of column tiles; C is written with non-temporal stores. */
+ * of column tiles with B loaded straight into registers; C is written with non-temporal
+ * stores. */
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                              const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
                              void* stream);

@@ -82,10 +82,24 @@ def _planes_to_f64(planes, shape):
     return p[0] + p[1] + p[2]
 
 
+def _frag_order(P):
+    """(NP, N, K) row-major planes -> the forward GEMM's MFMA fragment order (gmp.h,
+    gmp_tp_gemm_x3_f32): blocks (k step, column tile, plane) of 64 lanes x 8 values, lane
+    l = n % 16 + 16 ((k % 32) / 8)."""
+    NP, N, K = P.shape
+    x = P.reshape(NP, N // 16, 16, K // 32, 4, 8)  # p, ct, li, ks, g, e
+    return x.permute(3, 1, 0, 4, 2, 5).contiguous().view(-1)
+
+
+def _from_frag_order(flat, NP, N, K):
+    x = flat.reshape(K // 32, N // 16, NP, 4, 16, 8)  # ks, ct, p, g, li, e
+    return x.permute(2, 1, 4, 0, 3, 5).reshape(NP, N, K)
+
+
 @pytest.mark.parametrize("m1,mo,H", [(128, 128, 256), (64, 64, 256), (32, 128, 64)])
 def test_split_w2_planes_exact(m1, mo, H):
     """gmp_tp_split_w2_f32: the three bf16 planes of every W2 / b2 entry sum to it exactly, in
-    the forward [w][(u, j) ++ u] and backward [(u, j)][w] layouts."""
+    the forward [w][(u, j) ++ u] (in MFMA fragment order) and backward [(u, j)][w] layouts."""
     from gmp_amd import _lib
     from gmp_amd.ops import _p, _stream
     lib = _lib.load()
@@ -98,10 +112,10 @@ def test_split_w2_planes_exact(m1, mo, H):
     assert lib.gmp_tp_split_w2_f32(m1, mo, H, _p(W2), _p(b2), _p(Bf), _p(Bt), _stream()) == 0
     torch.cuda.synchronize()
     W = W2.cpu().double().view(m1, mo, H)                      # [u][w][j]
-    f = _planes_to_f64(Bf.cpu(), (mo, K1 + m1))
+    f = _planes_to_f64(_from_frag_order(Bf.cpu(), 3, mo, K1 + m1).contiguous(), (mo, K1 + m1))
     assert torch.equal(f[:, :K1], W.permute(1, 0, 2).reshape(mo, K1))
     assert torch.equal(f[:, K1:], b2.cpu().double().view(m1, mo).t())
-    t = _planes_to_f64(Bt.cpu(), (K1, mo))
+    t = _planes_to_f64(_from_frag_order(Bt.cpu(), 3, K1, mo).contiguous(), (K1, mo))
     assert torch.equal(t, W.permute(0, 2, 1).reshape(K1, mo))
 
 
@@ -124,7 +138,7 @@ def test_tp_gemm_x3_matches_fp64(M, N, K1, K2, grp):
     r1 = B - b0.float()
     b1 = r1.to(torch.bfloat16)
     b2 = (r1 - b1.float()).to(torch.bfloat16)
-    Bp = torch.stack([b0, b1, b2]).contiguous().view(torch.int16).to(DEV)
+    Bp = _frag_order(torch.stack([b0, b1, b2]).contiguous().view(torch.int16)).to(DEV)
     ref = A1.double() @ B[:, :K1].double().t()
     mag = A1.double().abs() @ B[:, :K1].double().abs().t()
     if K2:
@@ -204,7 +218,7 @@ def test_tp_gemm_x3_widen_matches_fp64(M, N, K):
     r1 = B - b0.float()
     b1 = r1.to(torch.bfloat16)
     b2 = (r1 - b1.float()).to(torch.bfloat16)
-    Bp = torch.stack([b0, b1, b2]).contiguous().view(torch.int16).to(DEV)
+    Bp = _frag_order(torch.stack([b0, b1, b2]).contiguous().view(torch.int16)).to(DEV)
     Ad = A.to(DEV)
     C = torch.full((M, N + 3), 7.0, device=DEV)
     assert lib.gmp_tp_gemm_x3_widen_f32(M, N, K, _p(Ad), K, _p(Bp), K, N * K, _p(C), N + 3,
