@@ -232,7 +232,7 @@ __device__ __forceinline__ H2Scale h2_scale(const unsigned* amax, const unsigned
   }
 }
 
-template <bool ACC, int NP>
+template <bool ACC, int NP, int RA>
 __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
     const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
@@ -308,7 +308,11 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   }
   const unsigned short* bl = Bp + 8 * lane;
 
-  f32x4 ringA[2][2];
+  // A ring: RA register slots (slot t % RA holds stage t); a stage's loads are issued RA
+  // iterations before its split + LDS write.  RA = 2 kept 32 KB of the A stream (the S rows) in
+  // flight per CU; measured at the MACE-128 lo = 2 shape (scripts/mb_tpgemm.py): RA = 2 11.33 ms,
+  // 4 10.74 ms, 8 10.55 ms (230 VGPRs, no scratch) -- the A stream was only part of the limit.
+  f32x4 ringA[RA][2];
   u32x4 ringB[2][2][NP];
   auto fetch = [&](int slot, int st) {
     const int stc = st < nst ? st : nst - 1;
@@ -353,35 +357,36 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   //   are in registers, read before the last barrier) | load A of s + 4 | read the A fragments
   //   of s + 1 | MFMAs of s | load B of s + 2 into the slot they read | barrier.
   // Stages past nst load clamped addresses; their A is stashed as zeros.
-  const int nst_pad = (nst + 1) & ~1;
+  const int nst_pad = (nst + RA - 1) / RA * RA;
   FragA<NP> F[2];
-  fetch(0, 0);
-  fetch(1, 1);
+#pragma unroll
+  for (int q = 0; q < RA; ++q) fetch(q, q);
   fetch_b(0, 0);
   fetch_b(1, 1);
   stash(0, smg, 0);
-  fetch(0, 2);
+  fetch(0, RA);
   stash(1, smg + STG, 1);
-  fetch(1, 3);
+  fetch(1, RA + 1);
   __syncthreads();
   load_frag_a<NP>(F[0], smg, wm, li, g);
   __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
-  for (int s0 = 0; s0 < nst_pad; s0 += 2) {
+  for (int s0 = 0; s0 < nst_pad; s0 += RA) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < RA; ++j) {
       const int st = s0 + j;
+      const int sl = (j + 2) % RA;  // ring slot of stage st + 2
       const unsigned char* nb = smg + ((st + 1) & 1) * STG;
-      // sched barriers pin the ring discipline: slot j's registers are consumed by the stash
-      // before its next loads are issued, so the stash waits only for loads two stages old
+      // sched barriers pin the ring discipline: slot sl's registers are consumed by the stash
+      // before its next loads are issued, so the stash waits only for loads RA stages old
       // (counted vmcnt) instead of the scheduler hoisting the new loads and draining vmcnt(0)
-      stash(j, smg + (st & 1) * STG, st + 2);
+      stash(sl, smg + (st & 1) * STG, st + 2);
       __builtin_amdgcn_sched_barrier(0);
-      fetch(j, st + 4);
+      fetch(sl, st + 2 + RA);
       __builtin_amdgcn_sched_barrier(0);
-      load_frag_a<NP>(F[j ^ 1], nb, wm, li, g);
-      mma_ab<NP>(acc, F[j], ringB[j]);
+      load_frag_a<NP>(F[(j & 1) ^ 1], nb, wm, li, g);
+      mma_ab<NP>(acc, F[j & 1], ringB[j & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      fetch_b(j, st + 2);  // the slot the MFMAs above just read: two stages of lead
+      fetch_b(j & 1, st + 2);  // the slot the MFMAs above just read: two stages of lead
       __syncthreads();
     }
   }
@@ -592,6 +597,11 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
 
 using namespace gmp;
 
+namespace gmp {
+// forward path GEMM: A-stream register ring depth (GMP_TPGEMM_RING=2: the r02 form)
+int g_tpgemm_ring = getenv("GMP_TPGEMM_RING") ? atoi(getenv("GMP_TPGEMM_RING")) : 8;
+}  // namespace gmp
+
 template <int NP>
 int split_w2_launch(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p, const float* b2p,
                     const unsigned* wmax, void* Bf, void* Bt, void* stream) {
@@ -629,7 +639,12 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   GMP_CHECK_ARG(nwg < (1LL << 32));
   const size_t smem = 2 * (size_t)(NP * kPlane) + (NP == 2 ? kBM * sizeof(int) : 0);
   int rc = 0;
-  auto k = accumulate ? tp_gemm_x3_kernel<true, NP> : tp_gemm_x3_kernel<false, NP>;
+  auto k = g_tpgemm_ring >= 8   ? (accumulate ? tp_gemm_x3_kernel<true, NP, 8>
+                                              : tp_gemm_x3_kernel<false, NP, 8>)
+           : g_tpgemm_ring >= 4 ? (accumulate ? tp_gemm_x3_kernel<true, NP, 4>
+                                              : tp_gemm_x3_kernel<false, NP, 4>)
+                                : (accumulate ? tp_gemm_x3_kernel<true, NP, 2>
+                                              : tp_gemm_x3_kernel<false, NP, 2>);
   if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)smem))))
