@@ -232,7 +232,7 @@ __device__ __forceinline__ H2Scale h2_scale(const unsigned* amax, const unsigned
   }
 }
 
-template <bool ACC, int NP, int RA>
+template <bool ACC, int NP, int RA, int RBB = 2>
 __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
     const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
@@ -312,8 +312,9 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   // iterations before its split + LDS write.  RA = 2 kept 32 KB of the A stream (the S rows) in
   // flight per CU; measured at the MACE-128 lo = 2 shape (scripts/mb_tpgemm.py): RA = 2 11.33 ms,
   // 4 10.74 ms, 8 10.55 ms (230 VGPRs, no scratch) -- the A stream was only part of the limit.
+  static_assert(RA % RBB == 0, "the unrolled loop indexes both rings statically");
   f32x4 ringA[RA][2];
-  u32x4 ringB[2][2][NP];
+  u32x4 ringB[RBB][2][NP];  // B (W2p planes, from the Infinity Cache): RBB steps ahead
   auto fetch = [&](int slot, int st) {
     const int stc = st < nst ? st : nst - 1;
     const int64_t k0 = (int64_t)stc * kBK;
@@ -361,8 +362,8 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   FragA<NP> F[2];
 #pragma unroll
   for (int q = 0; q < RA; ++q) fetch(q, q);
-  fetch_b(0, 0);
-  fetch_b(1, 1);
+#pragma unroll
+  for (int q = 0; q < RBB; ++q) fetch_b(q, q);
   stash(0, smg, 0);
   fetch(0, RA);
   stash(1, smg + STG, 1);
@@ -384,9 +385,9 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       fetch(sl, st + 2 + RA);
       __builtin_amdgcn_sched_barrier(0);
       load_frag_a<NP>(F[(j & 1) ^ 1], nb, wm, li, g);
-      mma_ab<NP>(acc, F[j & 1], ringB[j & 1]);
+      mma_ab<NP>(acc, F[j & 1], ringB[j % RBB]);
       __builtin_amdgcn_sched_barrier(0);
-      fetch_b(j & 1, st + 2);  // the slot the MFMAs above just read: two stages of lead
+      fetch_b(j % RBB, st + RBB);  // the slot the MFMAs above just read: RBB stages of lead
       __syncthreads();
     }
   }
@@ -420,7 +421,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
 // non-temporal stores (T is consumed by a later kernel, far past the caches) and restart.
 // Replaces one workgroup per 128 x 128 tile, whose prologue / epilogue dominated at 4 k steps.
 constexpr int kMaxKS = 4;  // K <= 128
-template <int NKS, int NP>
+template <int NKS, int NP, int RB>
 __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
     int64_t M, int64_t N, const float* __restrict__ A, int64_t lda,
     const unsigned short* __restrict__ Bp, int64_t ldb, int64_t bplane, float* __restrict__ C,
@@ -467,7 +468,10 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
   const int nst = (int)((t1 - t0) * NKS);
   const int64_t ct_total = N / 16;
   const unsigned short* bl = Bp + 8 * lane;
-  u32x4 ringB[2][2][NP];
+  // B ring: RB register slots (slot gs % RB holds step gs), loaded RB steps ahead (W2p's planes,
+  // 25 MB at the MACE-128 shape, stream from the Infinity Cache, not L2).  Measured at the lo = 2
+  // shape: RB = 2 11.70 ms, RB = 4 11.41 ms (238 VGPRs, no scratch); MACE 2314 -> 2278 ms/step
+  u32x4 ringB[RB][2][NP];
   // B fragments of global step gs (tile t0 + gs / NKS, k step gs % NKS) for this wave's two
   // column tiles; steps past the range and tiles past N read a clamped block and are zeroed
   auto fetch_b = [&](int slot, int gs) {
@@ -510,19 +514,19 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
   // B fragments from global memory two steps ahead (into the ring slot the MFMAs just read);
   // nothing is written to LDS after the A images, so the loop has no barrier
   FragA<NP> F[2];
-  fetch_b(0, 0);
-  fetch_b(1, 1);
+#pragma unroll
+  for (int q = 0; q < RB; ++q) fetch_b(q, q);
   __syncthreads();  // A images
   load_frag_a<NP>(F[0], sA, wm, li, g);
-  const int nst_pad = (nst + 1) & ~1;
-  for (int s0 = 0; s0 < nst_pad; s0 += 2) {
+  const int nst_pad = (nst + RB - 1) / RB * RB;
+  for (int s0 = 0; s0 < nst_pad; s0 += RB) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < RB; ++j) {
       const int gs = s0 + j;
-      load_frag_a<NP>(F[j ^ 1], sA + ((gs + 1) % NKS) * NP * kPlane, wm, li, g);
-      mma_ab<NP>(acc, F[j], ringB[j]);
+      load_frag_a<NP>(F[(j & 1) ^ 1], sA + ((gs + 1) % NKS) * NP * kPlane, wm, li, g);
+      mma_ab<NP>(acc, F[j & 1], ringB[j]);
       __builtin_amdgcn_sched_barrier(0);
-      fetch_b(j, gs + 2);
+      fetch_b(j, gs + RB);
       if (gs < nst && gs % NKS == NKS - 1) store_tile(t0 + gs / NKS);
     }
   }
@@ -600,6 +604,8 @@ using namespace gmp;
 namespace gmp {
 // forward path GEMM: A-stream register ring depth (GMP_TPGEMM_RING=2: the r02 form)
 int g_tpgemm_ring = getenv("GMP_TPGEMM_RING") ? atoi(getenv("GMP_TPGEMM_RING")) : 8;
+// T GEMM (widen): B-stream register ring depth (GMP_TPGEMM_WIDEN_RING=2: the r02 form)
+int g_widen_ring = getenv("GMP_TPGEMM_WIDEN_RING") ? atoi(getenv("GMP_TPGEMM_WIDEN_RING")) : 4;
 }  // namespace gmp
 
 template <int NP>
@@ -639,7 +645,9 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   GMP_CHECK_ARG(nwg < (1LL << 32));
   const size_t smem = 2 * (size_t)(NP * kPlane) + (NP == 2 ? kBM * sizeof(int) : 0);
   int rc = 0;
-  auto k = g_tpgemm_ring >= 8   ? (accumulate ? tp_gemm_x3_kernel<true, NP, 8>
+  auto k = g_tpgemm_ring == 44  ? (accumulate ? tp_gemm_x3_kernel<true, NP, 4, 4>
+                                              : tp_gemm_x3_kernel<false, NP, 4, 4>)
+           : g_tpgemm_ring >= 8 ? (accumulate ? tp_gemm_x3_kernel<true, NP, 8>
                                               : tp_gemm_x3_kernel<false, NP, 8>)
            : g_tpgemm_ring >= 4 ? (accumulate ? tp_gemm_x3_kernel<true, NP, 4>
                                               : tp_gemm_x3_kernel<false, NP, 4>)
@@ -682,7 +690,8 @@ int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
   int rc = 0;
 #define GMP_WN(NK)                                                                               \
   {                                                                                              \
-    auto k = tp_gemm_x3_widen_kernel<NK, NP>;                                                    \
+    auto k = g_widen_ring >= 4 ? tp_gemm_x3_widen_kernel<NK, NP, 4>                              \
+                               : tp_gemm_x3_widen_kernel<NK, NP, 2>;                             \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                      \
                                             hipFuncAttributeMaxDynamicSharedMemorySize,         \
                                             (int)smem))))                                        \
