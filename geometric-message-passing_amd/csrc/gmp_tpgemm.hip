@@ -711,6 +711,13 @@ int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
 
 extern "C" {
 
+int gmp_tp_gemm_set_rings(int a_ring, int b_ring) {
+  const int old = g_tpgemm_ring * 16 + g_widen_ring;
+  g_tpgemm_ring = a_ring;
+  g_widen_ring = b_ring;
+  return old;
+}
+
 int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
                         const float* b2p, void* Bf, void* Bt, void* stream) {
   return split_w2_launch<3>(mul1, mul_out, H, W2p, b2p, nullptr, Bf, Bt, stream);

@@ -371,6 +371,13 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
  * kernel (A/B studies; GMP_TP_APPLY_F32=1 at load).  Returns the previous setting. */
 int gmp_tp_apply_set_x3(int on);
 
+/* Register-ring depths of the K7g path GEMMs (A/B studies; results are bitwise identical for
+ * every setting: the rings change when operands are fetched, not the accumulation order).
+ * a_ring: stages of the forward GEMM's A stream in flight (2, 4, 8; 44 = A and B rings of 4);
+ * b_ring: steps of the T GEMM's B stream in flight (2 or 4).  Defaults 8 / 4
+ * (GMP_TPGEMM_RING / GMP_TPGEMM_WIDEN_RING).  Returns the previous a_ring * 16 + b_ring. */
+int gmp_tp_gemm_set_rings(int a_ring, int b_ring);
+
 /* K7g path GEMMs of the receiver-factorised TP convolution on the bf16 MFMA through exact
  * three-plane f32 splits (replaces the library f32 GEMMs out = S W2p + Sb b2p and
  * T = G W2p^T of tfn_layer.py:73-87 regrouped; f32-class accuracy, see gmp_tpgemm.hip).

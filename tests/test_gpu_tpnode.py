@@ -119,13 +119,25 @@ def test_split_w2_planes_exact(m1, mo, H):
     assert torch.equal(t, W.permute(0, 2, 1).reshape(K1, mo))
 
 
+@pytest.mark.parametrize("ring", [8, 4, 44, 2])
 @pytest.mark.parametrize("M,N,K1,K2,grp", [(1000, 128, 256, 32, 5), (333, 64, 128, 0, 1),
-                                           (257, 4096, 128, 0, 1), (130, 128, 4096, 128, 3)])
-def test_tp_gemm_x3_matches_fp64(M, N, K1, K2, grp):
+                                           (257, 4096, 128, 0, 1), (130, 128, 4096, 128, 3),
+                                           (65, 32, 96, 32, 1)])
+def test_tp_gemm_x3_matches_fp64(M, N, K1, K2, grp, ring):
     """gmp_tp_gemm_x3_f32 (bf16 MFMA over three-plane splits) against fp64: error per entry
     <= 1e-6 of sum |a b| (f32-class; f32 unit roundoff 6e-8, a K-term f32 sum ~ sqrt(K) of it),
     ragged M / N tiles, the second A operand, the grouped (r / grp) epilogue addressing with
-    accumulation into an existing output."""
+    accumulation into an existing output; every register-ring depth (k-step counts that are and
+    are not multiples of the ring: 9, 4 and 132 steps)."""
+    from gmp_amd import _lib
+    old_rings = _lib.load().gmp_tp_gemm_set_rings(ring, 4)
+    try:
+        _tp_gemm_x3_case(M, N, K1, K2, grp)
+    finally:
+        _lib.load().gmp_tp_gemm_set_rings(old_rings // 16, old_rings % 16)
+
+
+def _tp_gemm_x3_case(M, N, K1, K2, grp):
     from gmp_amd import _lib
     from gmp_amd.ops import _p, _stream
     lib = _lib.load()
@@ -203,14 +215,24 @@ def test_outer_sum_cols_matches_fp64(K, m_total, n):
     assert err < 1e-6, err
 
 
+@pytest.mark.parametrize("bring", [4, 2])
 @pytest.mark.parametrize("M,N,K", [(1000, 8192, 128), (333, 4096 + 64, 64), (130, 1024, 96),
-                                   (17, 256, 32)])
-def test_tp_gemm_x3_widen_matches_fp64(M, N, K):
+                                   (17, 256, 32), (40, 384, 96)])
+def test_tp_gemm_x3_widen_matches_fp64(M, N, K, bring):
     """gmp_tp_gemm_x3_widen_f32 (resident A, swept column tiles): C = A B^T within 1e-6 of
-    sum |a b| per entry, ragged M and N, every K / 32 variant."""
+    sum |a b| per entry, ragged M and N, every K / 32 variant, both B-ring depths."""
     from gmp_amd import _lib
     from gmp_amd.ops import _p, _stream
     lib = _lib.load()
+    old_rings = lib.gmp_tp_gemm_set_rings(8, bring)
+    try:
+        _widen_case(lib, M, N, K)
+    finally:
+        lib.gmp_tp_gemm_set_rings(old_rings // 16, old_rings % 16)
+
+
+def _widen_case(lib, M, N, K):
+    from gmp_amd.ops import _p, _stream
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g)
     B = torch.randn(N, K, generator=g) * torch.logspace(-4, 1, K)
