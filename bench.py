@@ -60,8 +60,8 @@ def parse():
     ap.add_argument("--edges", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=None,
-                    help="CPU baseline threads (default: OMP_NUM_THREADS, else the physical "
-                         "cores this process may run on)")
+                    help="CPU baseline threads (default: OMP_NUM_THREADS = the job's CPU share on "
+                         "the GPU box, else the physical cores this process may run on)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a HIP graph (measured slower than eager launch "
                          "on ROCm 7 for the EGNN step: off by default)")
@@ -210,6 +210,9 @@ def cpu_info():
 
 
 def cpu_threads(args):
+    """Threads of the CPU baseline: --cpu-threads, else the job's CPU share (OMP_NUM_THREADS: the
+    GPU pool grants a 1-GPU job 16 of the host's cores, which serve all eight GPUs' jobs), else
+    every physical core this process may run on."""
     if args.cpu_threads:
         return args.cpu_threads
     env = os.environ.get("OMP_NUM_THREADS")
@@ -217,11 +220,20 @@ def cpu_threads(args):
     return min(int(env), phys) if env and env.isdigit() and int(env) > 0 else phys
 
 
+# CPU-baseline samples of the bench graph (bounded: ~10-30 s of CPU work per workload) and the
+# timed steps (median): EGNN / GVP / SchNet a slab x < frac * box; MACE / TFN a corner cube of
+# frac of the volume.  The reference's TP materialises the per-edge weights (721 KB per edge and
+# layer for MACE-128: ~28 TFLOP per step at 20k edges, minutes per step on the CPU), so its sample
+# is small; its timing is overhead-light from ~1k edges on (r03 probe: 27 edges/s at 662 edges,
+# 64 at 7.3k on 8 threads here).
+CPU_SAMPLE = {"egnn": ("slab", 0.2, 5), "gvp": ("slab", 0.1, 5), "schnet": ("slab", 0.1, 5),
+              "mace": ("cube", 0.003, 3), "tfn": ("cube", 0.003, 3)}
+
+
 def cpu_baseline(g, args, workload):
-    """Time the CPU oracle (fwd + L1 + bwd + Adam; plain PyTorch on the host cores): the full
-    graph for EGNN (C2 runs full size on the CPU), a spatial sample for the
-    others (the oracle's TP materialises 4 * weight_numel bytes per edge: 721 KB per edge for
-    MACE-128)."""
+    """Time the CPU oracle (fwd + L1 + bwd + Adam; plain PyTorch on the host cores, the
+    reference's torch_scatter / PyG / e3nn CPU path restated) on a bounded spatial sample of
+    the bench graph: one warm-up step, then the median of the timed steps (CPU_SAMPLE)."""
     from oracle import egnn as oegnn
     from oracle import gvp as ogvp
     from oracle import mace as omace
@@ -231,25 +243,20 @@ def cpu_baseline(g, args, workload):
     threads = cpu_threads(args)
     torch.set_num_threads(threads)
     layers, emb = args.layers_of[workload], args.emb_of[workload]
-    if workload == "egnn":
-        sub, shape, timed = g, "all", 1
+    kind, frac, timed = CPU_SAMPLE[workload]
+    if kind == "slab":
+        keep = g.pos[:, 0] < g.box * frac
+        shape = f"{frac:.0%}-volume spatial slab"
     else:
-        if workload in ("gvp", "schnet"):
-            frac = 0.1  # slab x < frac * box
-            keep = g.pos[:, 0] < g.box * frac
-            shape = f"{frac:.0%}-volume spatial slab"
-        else:
-            frac = 0.002
-            keep = (g.pos < g.box * frac ** (1.0 / 3.0)).all(dim=1)
-            shape = f"{frac:.1%}-volume corner cube"
-        idx = torch.nonzero(keep).view(-1)
-        remap = torch.full((g.num_nodes,), -1, dtype=torch.long)
-        remap[idx] = torch.arange(idx.numel())
-        ei = g.edge_index
-        m = keep[ei[0]] & keep[ei[1]]
-        sub = Batch(torch.full((idx.numel(),), _atom_type(workload), dtype=torch.long),
-                    g.pos[idx], remap[ei[:, m]], num_graphs=1)
-        timed = 2 if workload in ("gvp", "schnet") else 1
+        keep = (g.pos < g.box * frac ** (1.0 / 3.0)).all(dim=1)
+        shape = f"{frac:.1%}-volume corner cube"
+    idx = torch.nonzero(keep).view(-1)
+    remap = torch.full((g.num_nodes,), -1, dtype=torch.long)
+    remap[idx] = torch.arange(idx.numel())
+    ei = g.edge_index
+    m = keep[ei[0]] & keep[ei[1]]
+    sub = Batch(torch.full((idx.numel(),), _atom_type(workload), dtype=torch.long),
+                g.pos[idx], remap[ei[:, m]], num_graphs=1)
     torch.manual_seed(0)
     mod = {"egnn": oegnn, "gvp": ogvp, "schnet": oschnet}.get(workload, omace)
     model = build_model(mod, workload, layers, emb)
@@ -268,22 +275,23 @@ def cpu_baseline(g, args, workload):
         t0 = time.perf_counter()
         step()
         ts.append(time.perf_counter() - t0)
-    t = sum(ts) / len(ts)
+    t = sorted(ts)[len(ts) // 2]
     cpu_model, phys, logical = cpu_info()
     return {"value": sub.num_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
             "cpu": cpu_model, "host_cores_visible": {"physical": phys, "logical": logical},
+            "step_s": ts,
             "sample": f"oracle/{mod.__name__.split('.')[-1]}.py {workload} {layers}L/{emb} "
-                      f"fwd+L1+bwd+Adam (torch {torch.__version__} CPU, {threads} threads) on "
+                      f"fwd+L1+bwd+Adam (torch {torch.__version__} CPU, {threads} threads = "
+                      f"this job's CPU share of the host's {phys} physical cores) on the "
                       f"{shape} of the bench graph ({sub.num_nodes} nodes, {sub.num_edges} "
-                      f"edges): 1 warm-up + mean of {timed} timed step(s), {t:.2f} s/step"}
+                      f"edges): 1 warm-up + median of {timed} timed steps, {t:.2f} s/step"}
 
 
 def tp_node_s_bytes(model, n_nodes, n_edges):
-    """Algorithmic HBM bytes of the S-build launches (gmp_tp_node_outer_f32) per
-    training step: one launch per (layer, path, receiver chunk), forward
-    and backward recompute; each reads its z rows (E w) and hidden radial rows a (E H) once and
-    writes S (N w H) and Sb (N w), fp32.  Chunks split E and N, so the per-step sum is
-    chunk-independent (the launch count is read from the timers)."""
+    """HBM bytes the S-build launches (gmp_tp_node_outer_f32) move per training
+    step: one launch per (layer, path, receiver chunk), forward and backward recompute; each reads
+    its z rows (E w) and hidden radial rows a (E H) once and writes S (N w H) and Sb (N w), fp32.
+    S is an intermediate of this design, not algorithmic work: reported beside the roofline."""
     total = 0
     for conv in model.convs:
         H = conv.fc[0].out_features
@@ -292,38 +300,85 @@ def tp_node_s_bytes(model, n_nodes, n_edges):
     return total
 
 
-def mace_roofline(model, n_nodes, n_edges, timers, counts, n_steps):
-    """Roofline of the dominant MACE kernel from HIP-event timing inside the measured steps:
-    the S build of the receiver-factorised TP contraction (tp_node_outer_kernel, DESIGN.md K7,
-    ~24% of the step; HBM-bound: it writes N w H fp32 per launch).  `achieved` = algorithmic
-    bytes per launch / average launch duration (both averaged over the step's launch mix, the
-    same mix rocprofv3's per-kernel average and the PMC traffic summarise).  The whole
-    node-form contraction (S + path GEMMs + dW2 + apply) is reported beside it against the
-    f32 MFMA peak."""
+def tp_algorithmic_bytes(model, n_edges):
+    """SURVEY §8(d) minimum HBM bytes of the TP convolutions per training step: per layer and
+    edge 16 (indices) + 4 in_dim (sender row) + 36 (Y) + 32 (radial) + 4 out_dim (receiver row),
+    9,300 B at a MACE-128 hidden layer; x 3 for forward + backward."""
+    return sum(3 * n_edges * (16 + 4 * c.plan.desc.in_dim + 36 + 32 + 4 * c.plan.desc.out_dim)
+               for c in model.convs)
+
+
+# kernels of the node-form TP contraction (the roofline's kernel set; prefixes as rocprofv3
+# names them in profiles/<round>_<workload>_kernels.json)
+TP_KERNELS = ("tp_node_outer_kernel", "tp_gemm_x3_kernel", "tp_gemm_x3_widen_kernel",
+              "outer_sum_x3_kernel", "sum_partials_cols", "tp_node_apply", "tp_split_w2_kernel")
+
+
+def pmc_step(workload):
+    """(kernel ms per step of the TP kernel set, HBM bytes per step over every kernel, profile
+    file) from the newest committed rocprofv3 summary that records its step count, or None."""
+    import glob
+    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles",
+                                                       f"r*_{workload}_kernels.json")))):
+        with open(path) as f:
+            d = json.load(f)
+        n = d.get("steps_in_trace")
+        if not n:
+            continue
+        rows = d["kernels"]
+        tp_ms = sum(r["total_ms"] for r in rows if r["kernel"].startswith(TP_KERNELS)) / n
+        if any(r["hbm_read_bytes_per_launch"] is None for r in rows):
+            return tp_ms, None, os.path.basename(path)
+        hbm = sum(r["calls"] * (r["hbm_read_bytes_per_launch"] + r["hbm_write_bytes_per_launch"])
+                  for r in rows) / n
+        return tp_ms, hbm, os.path.basename(path)
+    return None
+
+
+def mace_roofline(model, n_nodes, n_edges, timers, counts, n_steps, workload="mace"):
+    """Roofline of the MACE / TFN step's dominant work, the receiver-factorised TP contraction
+    (S build, K7g path GEMMs, dW2p, apply; ~90 % of the step), against the ceiling
+    of the arithmetic it runs: bf16 MFMA dense peak / 6 (three-plane split products) = 419 TF
+    f32-equivalent.  achieved = algorithmic FLOP per step (tp_node_flops) / the contraction's
+    device time per step, measured with HIP events around its launches inside the timed steps.
+    traffic = HBM bytes per step of the whole step from the committed PMC summary
+    (FETCH_SIZE x2 + WRITE_SIZE), against SURVEY §8(d)'s algorithmic bytes of the TP
+    convolutions (~9.3 KB per edge and hidden layer, x 3 for fwd + bwd): waste_ratio says how
+    much of it the S / T intermediates add."""
     fl = tp_node_flops(model, n_nodes, n_edges)
     keys = ("tp_node_S", "tp_node_W", "tp_node_dW", "tp_node_dZA")
-    t_gemm = sum(timers.get(k, 0.0) for k in keys) / n_steps
-    tp_tflops = fl / (t_gemm * 1e-3) / 1e12
+    t_tp = sum(timers.get(k, 0.0) for k in keys) / n_steps
+    tflops = fl / (t_tp * 1e-3) / 1e12 if t_tp > 0 else 0.0
+    algo = tp_algorithmic_bytes(model, n_edges)
     s_bytes = tp_node_s_bytes(model, n_nodes, n_edges)
-    s_launches = max(1, counts.get("tp_node_S", 0) // n_steps)
     s_ms = timers.get("tp_node_S", 0.0) / n_steps
-    achieved = s_bytes / (s_ms * 1e-3) / 1e9 if s_ms > 0 else 0.0
-    return {"kernel": "tp_node_outer (S build)", "kernel_prefix": "tp_node_outer_kernel",
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "bytes_per_launch": s_bytes / s_launches, "launches_per_step": s_launches,
-            "ms_per_launch": s_ms / s_launches,
-            "tp_node_all": {"bound": "mfma", "achieved": tp_tflops,
-                            "peak": X3_PEAK_TFLOPS, "unit": "TFLOP/s (f32-equivalent)",
-                            "frac": tp_tflops / X3_PEAK_TFLOPS,
-                            "peak_note": "bf16 MFMA dense peak / 6 (three-plane split products)"},
-            "flops_per_step": fl, "tp_node_gemm_ms_per_step": t_gemm,
+    roof = {"kernel": "TP contraction (K7 S build + K7g path GEMMs + dW2p + apply)",
+            "kernel_prefix": list(TP_KERNELS), "bound": "mfma", "achieved": tflops,
+            "peak": X3_PEAK_TFLOPS, "unit": "TFLOP/s (f32-equivalent)",
+            "frac": tflops / X3_PEAK_TFLOPS,
+            "peak_note": "bf16 MFMA dense peak / 6 (three-plane split products)",
+            "flops_per_step": fl,
+            "flops_formula": "per layer 4 x 2 E J z_size + 3 x 2 N J sum_p (2lo+1) mul1 mul_out "
+                             "(J = radial hidden + 1; DESIGN.md §4)",
+            "tp_ms_per_step": t_tp,
+            "traffic": None, "traffic_unit": "HBM bytes per step (all kernels)",
+            "algorithmic_bytes_per_step": algo, "waste_ratio": None,
             "split_ms_per_step": {k: timers.get(k, 0.0) / n_steps for k in keys},
+            "s_build": {"hbm_bytes_per_step": s_bytes, "ms_per_step": s_ms,
+                        "gbs": s_bytes / (s_ms * 1e-3) / 1e9 if s_ms > 0 else None},
             "tp_node_prep_ms_per_step": timers.get("tp_node_prep", 0.0) / n_steps,
             "tp_node_edge_bwd_ms_per_step": timers.get("tp_node_edge_bwd", 0.0) / n_steps,
             "symmetric_contraction_ms_per_step":
                 (timers.get("symmetric_contraction_fwd", 0.0) +
                  timers.get("symmetric_contraction_bwd", 0.0)) / n_steps}
+    p = pmc_step(workload)
+    if p is not None:
+        tp_ms, hbm, src = p
+        roof["profile"] = {"source": f"profiles/{src}", "tp_kernel_ms_per_step": tp_ms,
+                           "frac_from_profile": fl / (tp_ms * 1e-3) / 1e12 / X3_PEAK_TFLOPS}
+        if hbm is not None:
+            roof["traffic"], roof["waste_ratio"] = hbm, hbm / algo
+    return roof
 
 
 TIMER_NAMES = {"egnn": {"egnn_edge_fwd", "egnn_edge_bwd"}, "gvp": set(), "schnet": set()}
@@ -423,8 +478,9 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                     "traffic": None, "flops_per_edge": fl}
         else:
-            roof = mace_roofline(model, g.num_nodes, g.num_edges, totals, counts, n_timed)
-        t = pmc_traffic(workload, roof["kernel_prefix"])
+            roof = mace_roofline(model, g.num_nodes, g.num_edges, totals, counts, n_timed,
+                                 workload)
+        t = None if workload in ("mace", "tfn") else pmc_traffic(workload, roof["kernel_prefix"])
         if t is not None:
             roof["traffic"], roof["traffic_source"] = t[0], f"profiles/{t[1]}"
         rec = {"value": total_edges * steps / elapsed, "unit": "edges/s", "steps": steps,

@@ -209,19 +209,6 @@ int bwd_blocks(int64_t rows) {
   return (int)(b < kRowBlocks ? (b < 1 ? 1 : b) : kRowBlocks);
 }
 
-// max |x| over n floats into *amax (float bit pattern, atomicMax: the caller zeroes *amax);
-// the dynamic scale of an H2 GEMM operand
-__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t n,
-                                                     unsigned* __restrict__ amax) {
-  float m = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(x[i]));
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
-}
-
 }  // namespace
 }  // namespace gmp
 
@@ -296,17 +283,6 @@ int gmp_sum_rows_f32(const float* partials, int64_t nrows, int64_t width, float*
   if (nrows == 0) return hip_check(hipMemsetAsync(out, 0, width * sizeof(float), s));
   sum_rows_kernel<<<(unsigned)ceil_div(width, kSC), kSC * kSG, 0, s>>>(partials, (int)nrows,
                                                                        (int)width, out);
-  return launch_status();
-}
-
-int gmp_absmax_f32(const float* x, int64_t n, uint32_t* amax, void* stream) {
-  GMP_CHECK_ARG(n >= 0 && amax);
-  if (n == 0) return GMP_OK;
-  GMP_CHECK_ARG(x);
-  int64_t g = ceil_div(n, 256 * 8);
-  const int64_t cap = (int64_t)device_cu_count() * 8;
-  if (g > cap) g = cap;
-  absmax_kernel<<<(unsigned)g, 256, 0, as_stream(stream)>>>(x, n, amax);
   return launch_status();
 }
 

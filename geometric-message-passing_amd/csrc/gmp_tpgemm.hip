@@ -723,12 +723,6 @@ int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W
   return split_w2_launch<3>(mul1, mul_out, H, W2p, b2p, nullptr, Bf, Bt, stream);
 }
 
-int gmp_tp_split_w2_h2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
-                           const float* b2p, const uint32_t* wmax, void* Bf, void* Bt,
-                           void* stream) {
-  return split_w2_launch<2>(mul1, mul_out, H, W2p, b2p, wmax, Bf, Bt, stream);
-}
-
 int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
                        int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
                        int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
@@ -737,25 +731,10 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
                         C, cgrp, cldg, cldr, cldn, accumulate, stream);
 }
 
-int gmp_tp_gemm_h2_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
-                       int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
-                       int64_t bplane, const float* arow, int64_t nparts, const uint32_t* wmax,
-                       float* C, int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn,
-                       int accumulate, void* stream) {
-  return gemm_launch<2>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, arow, nparts, wmax, C,
-                        cgrp, cldg, cldr, cldn, accumulate, stream);
-}
-
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                              const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
                              void* stream) {
   return widen_launch<3>(M, N, K, A, lda, Bp, ldb, bplane, nullptr, nullptr, C, ldc, stream);
-}
-
-int gmp_tp_gemm_h2_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
-                             const void* Bp, int64_t ldb, int64_t bplane, const uint32_t* amax,
-                             const uint32_t* wmax, float* C, int64_t ldc, void* stream) {
-  return widen_launch<2>(M, N, K, A, lda, Bp, ldb, bplane, amax, wmax, C, ldc, stream);
 }
 
 }  // extern "C"

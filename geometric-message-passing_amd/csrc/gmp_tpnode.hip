@@ -575,9 +575,9 @@ int gmp_tp_apply_set_x3(int on) {
 }
 
 
-int gmp_tp_node_outer_rmax_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
-                               const float* Z, const float* A, float* S, float* Sb,
-                               float* rmax, void* stream) {
+int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
+                          const float* Z, const float* A, float* S, float* Sb, void* stream) {
+  float* rmax = nullptr;  // (the per-row maxima of the retired H2 path GEMM: template arm kept)
   GMP_CHECK_ARG(n_recv >= 0 && w > 0 && H > 0 && H <= kMaxH && H % 16 == 0);
   GMP_CHECK_ARG(n_recv <= 65535 * 1024);
   if (n_recv == 0) return GMP_OK;
@@ -595,11 +595,6 @@ int gmp_tp_node_outer_rmax_f32(int64_t n_recv, int64_t w, int64_t H, const int64
                                       : tp_node_outer_kernel<false, false, 1>);
   k<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb, rmax);
   return launch_status();
-}
-
-int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
-                          const float* Z, const float* A, float* S, float* Sb, void* stream) {
-  return gmp_tp_node_outer_rmax_f32(n_recv, w, H, eoff, Z, A, S, Sb, nullptr, stream);
 }
 
 int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,

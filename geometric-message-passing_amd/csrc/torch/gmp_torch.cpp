@@ -5,13 +5,16 @@
 // scatter` at models/layers/egnn_layer.py:4 and models/layers/tfn_layer.py:2).
 // This file is the same kind of boundary for the MI355X kernels: one schema per C-ABI entry
 // point, a CUDA(HIP)-key implementation that allocates outputs through the caching allocator,
-// launches on the current stream and maps error codes to RuntimeError (TORCH_CHECK, as
-// torch_scatter does), and a Meta implementation (shapes only) so torch.compile / FakeTensor
-// tracing treats every op as one opaque node.  No GPU work happens here; no CPU fallback.
+// launches on the current stream OF THE INPUTS' DEVICE (device guard, as torch_scatter's
+// CUDAGuard), checks dtype / device / contiguity / shape of every tensor argument and maps error
+// codes to RuntimeError (TORCH_CHECK), and a Meta implementation (shapes only) so torch.compile /
+// FakeTensor tracing treats every op as one opaque node.  No CPU fallback.
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <ATen/ATen.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -22,6 +25,26 @@ namespace {
 using at::Tensor;
 using c10::optional;
 
+// ------------------------------------------------------------------ device guard + checks
+// Every CUDA implementation opens an OpGuard on its first tensor argument: the current device
+// becomes that tensor's device (so the current stream is that device's stream), and every
+// tensor checked afterwards must live on the same device.
+thread_local int g_op_device = -1;
+
+struct OpGuard {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard;
+  int prev;
+  static c10::Device dev_of(const Tensor& t, const char* op) {
+    TORCH_CHECK(t.defined() && t.is_cuda(), "gmp.", op,
+                ": inputs must be HIP device tensors (no CPU fallback)");
+    return t.device();
+  }
+  OpGuard(const Tensor& t, const char* op) : guard(dev_of(t, op)), prev(g_op_device) {
+    g_op_device = t.device().index();
+  }
+  ~OpGuard() { g_op_device = prev; }
+};
+
 void* cur_stream() {
   return reinterpret_cast<void*>(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
 }
@@ -31,20 +54,43 @@ void check_rc(int rc, const char* name) {
               ", hip error ", gmp_last_hip_error(), ")");
 }
 
-void need(const Tensor& t, at::ScalarType st, const char* what) {
+void on_device(const Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda(), "gmp: ", what, " must be a HIP device tensor (no CPU fallback)");
+  TORCH_CHECK(g_op_device < 0 || t.device().index() == g_op_device, "gmp: ", what,
+              " is on device ", t.device(), " but the op's inputs are on cuda:", g_op_device);
+}
+void need(const Tensor& t, at::ScalarType st, const char* what) {
+  on_device(t, what);
   TORCH_CHECK(t.scalar_type() == st, "gmp: ", what, " has dtype ", t.scalar_type(), ", expected ",
               st);
   TORCH_CHECK(t.is_contiguous(), "gmp: ", what, " must be contiguous");
 }
-Tensor f32(const Tensor& t, const char* what) {
+const Tensor& f32(const Tensor& t, const char* what) {
   need(t, at::kFloat, what);
   return t;
 }
-Tensor i64(const Tensor& t, const char* what) {
+const Tensor& i64(const Tensor& t, const char* what) {
   need(t, at::kLong, what);
   return t;
 }
+const Tensor& i32(const Tensor& t, const char* what) {
+  need(t, at::kInt, what);
+  return t;
+}
+// shape check: t.sizes() == s
+void shape(const Tensor& t, at::IntArrayRef s, const char* what) {
+  TORCH_CHECK(t.sizes() == s, "gmp: ", what, " has shape ", t.sizes(), ", expected ", s);
+}
+void numel(const Tensor& t, int64_t n, const char* what) {
+  TORCH_CHECK(t.numel() == n, "gmp: ", what, " has ", t.numel(), " elements, expected ", n);
+}
+void opt_f32(const optional<Tensor>& t, at::IntArrayRef s, const char* what) {
+  if (t.has_value() && t->defined()) {
+    f32(*t, what);
+    shape(*t, s, what);
+  }
+}
+
 float* fp(const Tensor& t) { return t.defined() && t.numel() ? t.data_ptr<float>() : nullptr; }
 const float* cfp(const optional<Tensor>& t) {
   return t.has_value() && t->defined() && t->numel() ? t->data_ptr<float>() : nullptr;
@@ -62,11 +108,17 @@ int reduce_code(const std::string& r) {
 // ------------------------------------------------------------------ index: CSR, gather, reduce
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> csr_build(const Tensor& index, int64_t n_seg,
                                                              const optional<Tensor>& payload) {
+  OpGuard g(index, "csr_build");
   i64(index, "index");
+  TORCH_CHECK(n_seg >= 0, "gmp.csr_build: n_seg >= 0");
   const int64_t n = index.numel();
   auto o = index.options();
   Tensor perm = at::empty({n}, o), rowptr = at::empty({n_seg + 1}, o), sorted = at::empty({n}, o);
-  Tensor pl = payload.has_value() ? i64(*payload, "payload") : Tensor();
+  Tensor pl;
+  if (payload.has_value()) {
+    pl = i64(*payload, "payload");
+    numel(pl, n, "payload");
+  }
   Tensor pls = at::empty({pl.defined() ? n : 0}, o);
   Tensor err = at::zeros({1}, o.dtype(at::kInt));
   const size_t ws_b = gmp_csr_workspace_size(n, n_seg);
@@ -79,6 +131,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> csr_build(const Tensor& index
 }
 
 Tensor gather_rows(const Tensor& src, const Tensor& index) {
+  OpGuard g(src, "gather_rows");
   f32(src, "src");
   i64(index, "index");
   TORCH_CHECK(src.dim() == 2, "gmp.gather_rows: src must be 2-D");
@@ -92,16 +145,22 @@ Tensor gather_rows(const Tensor& src, const Tensor& index) {
 std::tuple<Tensor, Tensor> segment_reduce(const Tensor& src, const optional<Tensor>& perm,
                                           const Tensor& rowptr, int64_t n_seg,
                                           const std::string& reduce) {
+  OpGuard g(src, "segment_reduce");
   f32(src, "src");
   i64(rowptr, "rowptr");
-  TORCH_CHECK(src.dim() == 2 && rowptr.numel() == n_seg + 1, "gmp.segment_reduce: shapes");
+  TORCH_CHECK(src.dim() == 2 && rowptr.numel() == n_seg + 1,
+              "gmp.segment_reduce: src must be 2-D and rowptr hold n_seg + 1 offsets");
   const int red = reduce_code(reduce);
   const int64_t F = src.size(1);
+  Tensor pm;
+  if (perm.has_value()) {
+    pm = i64(*perm, "perm");
+    numel(pm, src.size(0), "perm");
+  }
   Tensor out = at::empty({n_seg, F}, src.options());
   Tensor argmax = at::empty({red == GMP_REDUCE_MAX ? n_seg : 0, F}, rowptr.options());
   const size_t ws_b = gmp_segment_reduce_workspace_size(src.size(0), n_seg, F, red);
   Tensor ws = at::empty({(int64_t)ws_b}, src.options().dtype(at::kByte));
-  Tensor pm = perm.has_value() ? i64(*perm, "perm") : Tensor();
   check_rc(gmp_segment_reduce_f32(fp(src), src.size(0), F, pm.defined() ? ip(pm) : nullptr,
                                   ip(rowptr), n_seg, red, fp(out),
                                   red == GMP_REDUCE_MAX ? ip(argmax) : nullptr,
@@ -113,24 +172,38 @@ std::tuple<Tensor, Tensor> segment_reduce(const Tensor& src, const optional<Tens
 Tensor segment_reduce_bwd(const Tensor& grad_out, const Tensor& index, const Tensor& rowptr,
                           const std::string& reduce, const optional<Tensor>& argmax,
                           int64_t n_items) {
+  OpGuard g(grad_out, "segment_reduce_bwd");
   f32(grad_out, "grad_out");
   i64(index, "index");
   i64(rowptr, "rowptr");
+  TORCH_CHECK(grad_out.dim() == 2 && rowptr.numel() == grad_out.size(0) + 1 &&
+                  index.numel() == n_items,
+              "gmp.segment_reduce_bwd: grad_out (n_seg, F), rowptr (n_seg + 1), index (n_items)");
   const int red = reduce_code(reduce);
-  Tensor am = argmax.has_value() ? i64(*argmax, "argmax") : Tensor();
+  Tensor am;
+  if (argmax.has_value()) {
+    am = i64(*argmax, "argmax");
+    shape(am, grad_out.sizes(), "argmax");
+  }
   TORCH_CHECK(red != GMP_REDUCE_MAX || am.defined(), "gmp.segment_reduce_bwd: max needs argmax");
-  Tensor g = at::empty({n_items, grad_out.size(1)}, grad_out.options());
+  Tensor gs = at::empty({n_items, grad_out.size(1)}, grad_out.options());
   check_rc(gmp_segment_reduce_bwd_f32(fp(grad_out), grad_out.size(0), grad_out.size(1),
                                       ip(index), n_items, ip(rowptr), red,
-                                      am.defined() ? ip(am) : nullptr, fp(g), cur_stream()),
+                                      am.defined() ? ip(am) : nullptr, fp(gs), cur_stream()),
            "gmp_segment_reduce_bwd_f32");
-  return g;
+  return gs;
 }
 
 // ------------------------------------------------------------------ EGNN fused edge kernels
-gmp_egnn_params egnn_params(const std::vector<Tensor>& p) {
+gmp_egnn_params egnn_params(const std::vector<Tensor>& p, int64_t d) {
   TORCH_CHECK(p.size() == 14, "gmp.egnn: 14 parameter tensors expected");
-  for (size_t k = 0; k < p.size(); ++k) f32(p[k], "egnn parameter");
+  // w1d, b1, ln1_w, ln1_b, W2, b2, ln2_w, ln2_b, W3, b3, ln3_w, ln3_b, w4, b4
+  static const int kind[14] = {1, 1, 1, 1, 2, 1, 1, 1, 2, 1, 1, 1, 1, 0};
+  for (size_t k = 0; k < p.size(); ++k) {
+    f32(p[k], "egnn parameter");
+    const int64_t want = kind[k] == 2 ? d * d : (kind[k] == 1 ? d : 1);
+    numel(p[k], want, "egnn parameter");
+  }
   gmp_egnn_params P;
   P.w1d = fp(p[0]); P.b1 = fp(p[1]); P.ln1_w = fp(p[2]); P.ln1_b = fp(p[3]);
   P.W2 = fp(p[4]); P.b2 = fp(p[5]); P.ln2_w = fp(p[6]); P.ln2_b = fp(p[7]);
@@ -139,17 +212,28 @@ gmp_egnn_params egnn_params(const std::vector<Tensor>& p) {
   return P;
 }
 
-std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(
-    const Tensor& AB, const Tensor& pos, const Tensor& rowptr, const Tensor& recv,
-    const Tensor& send, const std::vector<Tensor>& params, int64_t act, bool msg_mean, double eps,
-    bool train) {
-  f32(AB, "AB");
+void egnn_graph_checks(const Tensor& pos, const Tensor& rowptr, const Tensor& recv,
+                       const Tensor& send) {
   f32(pos, "pos");
   i64(rowptr, "rowptr");
   i64(recv, "recv");
   i64(send, "send");
+  TORCH_CHECK(pos.dim() == 2 && pos.size(1) == 3, "gmp.egnn: pos must be (N, 3)");
+  numel(rowptr, pos.size(0) + 1, "rowptr");
+  numel(send, recv.numel(), "send");
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(
+    const Tensor& AB, const Tensor& pos, const Tensor& rowptr, const Tensor& recv,
+    const Tensor& send, const std::vector<Tensor>& params, int64_t act, bool msg_mean, double eps,
+    bool train) {
+  OpGuard g(AB, "egnn_edge_fwd");
+  f32(AB, "AB");
+  egnn_graph_checks(pos, rowptr, recv, send);
+  TORCH_CHECK(AB.dim() == 2 && AB.size(1) % 2 == 0 && AB.size(0) == pos.size(0),
+              "gmp.egnn_edge_fwd: AB must be (N, 2d)");
   const int64_t N = pos.size(0), E = recv.numel(), d = AB.size(1) / 2;
-  gmp_egnn_params P = egnn_params(params);
+  gmp_egnn_params P = egnn_params(params, d);
   Tensor m = at::empty({N, d}, fopt(AB)), pa = at::empty({N, 3}, fopt(AB));
   Tensor xh = at::empty({train ? 3 : 0, E, d}, fopt(AB)), rs = at::empty({train ? E : 0, 3}, fopt(AB));
   check_rc(gmp_egnn_edge_fwd_f32(N, E, d, fp(AB), fp(pos), ip(rowptr), ip(recv), ip(send), &P,
@@ -163,18 +247,27 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd
     const Tensor& pos, const Tensor& rowptr, const Tensor& recv, const Tensor& send,
     const std::vector<Tensor>& params, int64_t act, bool msg_mean, const Tensor& xhat,
     const Tensor& rstd, const Tensor& g_m, const Tensor& g_p, const optional<Tensor>& amax) {
-  f32(pos, "pos");
+  OpGuard g(pos, "egnn_edge_bwd");
+  egnn_graph_checks(pos, rowptr, recv, send);
   f32(xhat, "xhat");
   f32(rstd, "rstd");
   f32(g_m, "g_m_aggr");
   f32(g_p, "g_pos_aggr");
+  TORCH_CHECK(xhat.dim() == 3, "gmp.egnn_edge_bwd: xhat must be (3, E, d)");
   const int64_t N = pos.size(0), E = recv.numel(), d = xhat.size(2);
-  gmp_egnn_params P = egnn_params(params);
+  shape(xhat, {3, E, d}, "xhat");
+  shape(rstd, {E, 3}, "rstd");
+  shape(g_m, {N, d}, "g_m_aggr");
+  shape(g_p, {N, 3}, "g_pos_aggr");
+  gmp_egnn_params P = egnn_params(params, d);
+  if (amax.has_value()) {
+    i32(*amax, "amax");
+    TORCH_CHECK(amax->numel() >= 2, "gmp.egnn_edge_bwd: amax has 2 words");
+  }
   auto o = fopt(pos);
   Tensor dA = at::empty({N, d}, o), dpr = at::empty({N, 3}, o), dp1 = at::empty({E, d}, o);
   Tensor gd = at::empty({E, 3}, o), dp2 = at::empty({E, d}, o), dp3 = at::empty({E, d}, o);
   Tensor part = at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o);
-  TORCH_CHECK(!amax.has_value() || amax->numel() >= 2, "gmp.egnn_edge_bwd: amax has 2 words");
   check_rc(gmp_egnn_edge_bwd_amax_f32(
                N, E, d, fp(pos), ip(rowptr), ip(recv), ip(send), &P, (int)act, msg_mean,
                fp(xhat), fp(rstd), fp(g_m), fp(g_p), fp(dA), fp(dpr), fp(dp1), fp(gd), fp(dp2),
@@ -189,32 +282,51 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd
 // ------------------------------------------------------------------ SchNet CFConv, SSP
 Tensor cfconv_aggregate(const Tensor& x, const Tensor& xidx, const Tensor& w, const Tensor& perm,
                         const Tensor& rowptr, int64_t n_seg, const optional<Tensor>& escale) {
+  OpGuard g(x, "cfconv_aggregate");
   f32(x, "x");
   f32(w, "w");
   i64(xidx, "xidx");
+  i64(perm, "perm");
+  i64(rowptr, "rowptr");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == x.size(1),
+              "gmp.cfconv_aggregate: x (N, F), w (E, F)");
+  const int64_t E = w.size(0);
+  numel(xidx, E, "xidx");
+  numel(perm, E, "perm");
+  numel(rowptr, n_seg + 1, "rowptr");
+  opt_f32(escale, {E}, "escale");
   Tensor out = at::empty({n_seg, x.size(1)}, x.options());
   Tensor err = at::zeros({1}, x.options().dtype(at::kInt));
-  check_rc(gmp_cfconv_aggregate_scaled_f32(fp(x), x.size(0), ip(xidx), fp(w), cfp(escale),
-                                           w.size(0), x.size(1), ip(perm), ip(rowptr), n_seg,
-                                           fp(out), err.data_ptr<int32_t>(), cur_stream()),
+  check_rc(gmp_cfconv_aggregate_scaled_f32(fp(x), x.size(0), ip(xidx), fp(w), cfp(escale), E,
+                                           x.size(1), ip(perm), ip(rowptr), n_seg, fp(out),
+                                           err.data_ptr<int32_t>(), cur_stream()),
            "gmp_cfconv_aggregate_scaled_f32");
   return out;
 }
 
-Tensor cfconv_wgrad(const Tensor& g, const Tensor& gidx, const Tensor& x, const Tensor& xidx,
+Tensor cfconv_wgrad(const Tensor& gr, const Tensor& gidx, const Tensor& x, const Tensor& xidx,
                     const optional<Tensor>& escale) {
-  f32(g, "g");
+  OpGuard g(gr, "cfconv_wgrad");
+  f32(gr, "g");
   f32(x, "x");
-  Tensor dw = at::empty({gidx.numel(), x.size(1)}, x.options());
+  i64(gidx, "gidx");
+  i64(xidx, "xidx");
+  TORCH_CHECK(gr.dim() == 2 && x.dim() == 2 && gr.size(1) == x.size(1),
+              "gmp.cfconv_wgrad: g (N, F), x (N, F)");
+  const int64_t E = gidx.numel();
+  numel(xidx, E, "xidx");
+  opt_f32(escale, {E}, "escale");
+  Tensor dw = at::empty({E, x.size(1)}, x.options());
   Tensor err = at::zeros({1}, x.options().dtype(at::kInt));
-  check_rc(gmp_cfconv_wgrad_scaled_f32(fp(g), g.size(0), ip(gidx), fp(x), x.size(0), ip(xidx),
-                                       cfp(escale), gidx.numel(), x.size(1), fp(dw),
+  check_rc(gmp_cfconv_wgrad_scaled_f32(fp(gr), gr.size(0), ip(gidx), fp(x), x.size(0), ip(xidx),
+                                       cfp(escale), E, x.size(1), fp(dw),
                                        err.data_ptr<int32_t>(), cur_stream()),
            "gmp_cfconv_wgrad_scaled_f32");
   return dw;
 }
 
 Tensor ssp_fwd(const Tensor& x, double shift) {
+  OpGuard g(x, "ssp_fwd");
   f32(x, "x");
   Tensor y = at::empty_like(x);
   check_rc(gmp_ssp_fwd_f32(fp(x), x.numel(), (float)shift, fp(y), cur_stream()), "gmp_ssp_fwd_f32");
@@ -222,8 +334,10 @@ Tensor ssp_fwd(const Tensor& x, double shift) {
 }
 
 Tensor ssp_bwd(const Tensor& x, const Tensor& gy) {
+  OpGuard g(x, "ssp_bwd");
   f32(x, "x");
   f32(gy, "grad_y");
+  shape(gy, x.sizes(), "grad_y");
   Tensor gx = at::empty_like(x);
   check_rc(gmp_ssp_bwd_f32(fp(x), fp(gy), x.numel(), fp(gx), cur_stream()), "gmp_ssp_bwd_f32");
   return gx;
@@ -232,37 +346,56 @@ Tensor ssp_bwd(const Tensor& x, const Tensor& gy) {
 // ------------------------------------------------------------------ LayerNorm + activation rows
 std::tuple<Tensor, Tensor, Tensor> ln_act_fwd(const Tensor& x, const Tensor& gamma,
                                               const Tensor& beta, double eps, int64_t act) {
+  OpGuard g(x, "ln_act_fwd");
   f32(x, "x");
   const int64_t d = x.size(-1), rows = x.numel() / d;
+  f32(gamma, "gamma");
+  f32(beta, "beta");
+  numel(gamma, d, "gamma");
+  numel(beta, d, "beta");
   Tensor y = at::empty_like(x), xh = at::empty_like(x), rs = at::empty({rows}, x.options());
-  check_rc(gmp_ln_act_fwd_f32(rows, d, fp(x), fp(f32(gamma, "gamma")), fp(f32(beta, "beta")),
-                              (float)eps, (int)act, fp(y), fp(xh), fp(rs), cur_stream()),
+  check_rc(gmp_ln_act_fwd_f32(rows, d, fp(x), fp(gamma), fp(beta), (float)eps, (int)act, fp(y),
+                              fp(xh), fp(rs), cur_stream()),
            "gmp_ln_act_fwd_f32");
   return {y, xh, rs};
 }
 
 std::tuple<Tensor, Tensor> ln_act_bwd(const Tensor& gy, const Tensor& xhat, const Tensor& rstd,
                                       const Tensor& gamma, const Tensor& beta, int64_t act) {
+  OpGuard g(gy, "ln_act_bwd");
   f32(gy, "grad_y");
   f32(xhat, "xhat");
+  f32(rstd, "rstd");
+  f32(gamma, "gamma");
+  f32(beta, "beta");
   const int64_t d = xhat.size(-1), rows = xhat.numel() / d;
+  shape(gy, xhat.sizes(), "grad_y");
+  numel(rstd, rows, "rstd");
+  numel(gamma, d, "gamma");
+  numel(beta, d, "beta");
   Tensor gx = at::empty_like(xhat), gb = at::empty({2 * d}, xhat.options());
   const size_t ws_b = gmp_ln_act_bwd_workspace_size(rows, d);
   Tensor ws = at::empty({(int64_t)ws_b + 1}, xhat.options().dtype(at::kByte));
-  check_rc(gmp_ln_act_bwd_f32(rows, d, fp(gy), fp(xhat), fp(f32(rstd, "rstd")), fp(gamma),
-                              fp(beta), (int)act, fp(gx), fp(gb), ws.data_ptr(), ws_b,
-                              cur_stream()),
+  check_rc(gmp_ln_act_bwd_f32(rows, d, fp(gy), fp(xhat), fp(rstd), fp(gamma), fp(beta), (int)act,
+                              fp(gx), fp(gb), ws.data_ptr(), ws_b, cur_stream()),
            "gmp_ln_act_bwd_f32");
   return {gx, gb};
 }
 
 // ------------------------------------------------------------------ K1 featurisation
+int64_t edge_checks(const Tensor& pos, const Tensor& edge_index) {
+  f32(pos, "pos");
+  i64(edge_index, "edge_index");
+  TORCH_CHECK(pos.dim() == 2 && pos.size(1) == 3, "gmp: pos must be (N, 3)");
+  TORCH_CHECK(edge_index.dim() == 2 && edge_index.size(0) == 2, "gmp: edge_index must be (2, E)");
+  return edge_index.size(1);
+}
+
 std::tuple<Tensor, Tensor> edge_featurize(const Tensor& pos, const Tensor& edge_index,
                                           at::ArrayRef<double> bessel_w, double prefactor,
                                           double r_max, double p) {
-  f32(pos, "pos");
-  i64(edge_index, "edge_index");
-  const int64_t E = edge_index.size(1), nb = (int64_t)bessel_w.size();
+  OpGuard g(pos, "edge_featurize");
+  const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
   Tensor sh = at::empty({E, 9}, pos.options()), rad = at::empty({E, nb}, pos.options());
   check_rc(gmp_edge_featurize_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(), (float)prefactor,
@@ -275,8 +408,10 @@ std::tuple<Tensor, Tensor> edge_featurize(const Tensor& pos, const Tensor& edge_
 Tensor edge_featurize_bwd(const Tensor& pos, const Tensor& edge_index,
                           at::ArrayRef<double> bessel_w, double prefactor, double r_max, double p,
                           const optional<Tensor>& g_sh, const optional<Tensor>& g_rad) {
-  f32(pos, "pos");
-  const int64_t E = edge_index.size(1), nb = (int64_t)bessel_w.size();
+  OpGuard g(pos, "edge_featurize_bwd");
+  const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
+  opt_f32(g_sh, {E, 9}, "g_sh");
+  opt_f32(g_rad, {E, nb}, "g_radial");
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
   Tensor gv = at::empty({E, 3}, pos.options());
   check_rc(gmp_edge_featurize_bwd_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(),
@@ -289,9 +424,8 @@ Tensor edge_featurize_bwd(const Tensor& pos, const Tensor& edge_index,
 std::tuple<Tensor, Tensor> edge_featurize_gvp(const Tensor& pos, const Tensor& edge_index,
                                               at::ArrayRef<double> bessel_w, double prefactor,
                                               double r_max, double p) {
-  f32(pos, "pos");
-  i64(edge_index, "edge_index");
-  const int64_t E = edge_index.size(1), nb = (int64_t)bessel_w.size();
+  OpGuard g(pos, "edge_featurize_gvp");
+  const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
   Tensor rad = at::empty({E, nb}, pos.options()), unit = at::empty({E, 3}, pos.options());
   check_rc(gmp_edge_featurize_gvp_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(),
@@ -305,8 +439,10 @@ Tensor edge_featurize_gvp_bwd(const Tensor& pos, const Tensor& edge_index,
                               at::ArrayRef<double> bessel_w, double prefactor, double r_max,
                               double p, const optional<Tensor>& g_rad,
                               const optional<Tensor>& g_unit) {
-  f32(pos, "pos");
-  const int64_t E = edge_index.size(1), nb = (int64_t)bessel_w.size();
+  OpGuard g(pos, "edge_featurize_gvp_bwd");
+  const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
+  opt_f32(g_rad, {E, nb}, "g_radial");
+  opt_f32(g_unit, {E, 3}, "g_unit");
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
   Tensor gv = at::empty({E, 3}, pos.options());
   check_rc(gmp_edge_featurize_gvp_bwd_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(),
@@ -319,10 +455,10 @@ Tensor edge_featurize_gvp_bwd(const Tensor& pos, const Tensor& edge_index,
 std::tuple<Tensor, Tensor, Tensor> schnet_featurize(const Tensor& pos, const Tensor& edge_index,
                                                     const Tensor& offsets, double coeff,
                                                     double cutoff) {
-  f32(pos, "pos");
-  i64(edge_index, "edge_index");
+  OpGuard g(pos, "schnet_featurize");
+  const int64_t E = edge_checks(pos, edge_index);
   f32(offsets, "offsets");
-  const int64_t E = edge_index.size(1), G = offsets.numel();
+  const int64_t G = offsets.numel();
   Tensor d = at::empty({E}, pos.options()), rbf = at::empty({E, G}, pos.options()),
          cut = at::empty({E}, pos.options());
   check_rc(gmp_schnet_featurize_f32(fp(pos), ip(edge_index), E, (int)G, fp(offsets),
@@ -335,8 +471,13 @@ std::tuple<Tensor, Tensor, Tensor> schnet_featurize(const Tensor& pos, const Ten
 Tensor schnet_featurize_bwd(const Tensor& pos, const Tensor& edge_index, const Tensor& offsets,
                             double coeff, double cutoff, const optional<Tensor>& g_dist,
                             const optional<Tensor>& g_rbf, const optional<Tensor>& g_cut) {
-  f32(pos, "pos");
-  const int64_t E = edge_index.size(1), G = offsets.numel();
+  OpGuard g(pos, "schnet_featurize_bwd");
+  const int64_t E = edge_checks(pos, edge_index);
+  f32(offsets, "offsets");
+  const int64_t G = offsets.numel();
+  opt_f32(g_dist, {E}, "g_dist");
+  opt_f32(g_rbf, {E, G}, "g_rbf");
+  opt_f32(g_cut, {E}, "g_cut");
   Tensor gv = at::empty({E, 3}, pos.options());
   check_rc(gmp_schnet_featurize_bwd_f32(fp(pos), ip(edge_index), E, (int)G, fp(offsets),
                                         (float)coeff, (float)cutoff, cfp(g_dist), cfp(g_rbf),
@@ -347,7 +488,11 @@ Tensor schnet_featurize_bwd(const Tensor& pos, const Tensor& edge_index, const T
 
 // ------------------------------------------------------------------ K16 Gate / BatchNorm
 Tensor gate_fwd(const Tensor& x, const Tensor& out_map, double c_act, double c_gate) {
+  OpGuard g(x, "gate_fwd");
   f32(x, "x");
+  i32(out_map, "out_map");
+  TORCH_CHECK(x.dim() == 2 && out_map.dim() == 2 && out_map.size(1) == 2,
+              "gmp.gate_fwd: x (B, c_in), out_map (c_out, 2)");
   const int64_t B = x.size(0), c_in = x.size(1), c_out = out_map.size(0);
   Tensor y = at::empty({B, c_out}, x.options());
   check_rc(gmp_gate_fwd_f32(B, (int)c_in, (int)c_out, out_map.data_ptr<int32_t>(), (float)c_act,
@@ -358,8 +503,13 @@ Tensor gate_fwd(const Tensor& x, const Tensor& out_map, double c_act, double c_g
 
 Tensor gate_bwd(const Tensor& x, const Tensor& grad_y, const Tensor& in_map, double c_act,
                 double c_gate) {
+  OpGuard g(x, "gate_bwd");
   f32(x, "x");
   f32(grad_y, "grad_y");
+  i32(in_map, "in_map");
+  TORCH_CHECK(x.dim() == 2 && grad_y.dim() == 2 && grad_y.size(0) == x.size(0),
+              "gmp.gate_bwd: x (B, c_in), grad_y (B, c_out)");
+  shape(in_map, {x.size(1), 4}, "in_map");
   const int64_t B = x.size(0), c_in = x.size(1), c_out = grad_y.size(1);
   Tensor gx = at::empty_like(x);
   check_rc(gmp_gate_bwd_f32(B, (int)c_in, (int)c_out, in_map.data_ptr<int32_t>(), (float)c_act,
@@ -368,14 +518,36 @@ Tensor gate_bwd(const Tensor& x, const Tensor& grad_y, const Tensor& in_map, dou
   return gx;
 }
 
+void bn_table_checks(const Tensor& x, const Tensor& col_chan, const Tensor& chan_col,
+                     const Tensor& chan_info, const Tensor& weight) {
+  f32(x, "x");
+  i32(col_chan, "col_chan");
+  i32(chan_col, "chan_col");
+  i32(chan_info, "chan_info");
+  f32(weight, "weight");
+  TORCH_CHECK(x.dim() == 2, "gmp.irreps_bn: x must be (B, C)");
+  numel(col_chan, x.size(1), "col_chan");
+  const int64_t nf = chan_col.numel();
+  shape(chan_info, {nf, 2}, "chan_info");
+  numel(weight, nf, "weight");
+}
+
 std::tuple<Tensor, Tensor, Tensor> irreps_bn_fwd(const Tensor& x, const Tensor& col_chan,
                                                  const Tensor& chan_col, const Tensor& chan_info,
                                                  const Tensor& weight,
                                                  const optional<Tensor>& bias,
                                                  Tensor running_mean, Tensor running_var,
                                                  bool training, double momentum, double eps) {
-  f32(x, "x");
+  OpGuard g(x, "irreps_bn_fwd");
+  bn_table_checks(x, col_chan, chan_col, chan_info, weight);
+  f32(running_mean, "running_mean");
+  f32(running_var, "running_var");
   const int64_t B = x.size(0), C = x.size(1), nf = chan_col.size(0);
+  numel(running_var, nf, "running_var");
+  if (bias.has_value() && bias->defined() && bias->numel()) {
+    f32(*bias, "bias");
+    numel(*bias, running_mean.numel(), "bias");
+  }
   Tensor y = at::empty_like(x), shift = at::empty({nf}, x.options()),
          invstd = at::empty({nf}, x.options());
   const size_t ws_b = gmp_irreps_bn_workspace_size(B, (int)C, (int)nf);
@@ -394,9 +566,15 @@ std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor& 
                                                  const Tensor& chan_info, const Tensor& weight,
                                                  const Tensor& shift, const Tensor& invstd,
                                                  bool training, int64_t n_scalar) {
-  f32(x, "x");
+  OpGuard g(x, "irreps_bn_bwd");
+  bn_table_checks(x, col_chan, chan_col, chan_info, weight);
   f32(grad_y, "grad_y");
+  f32(shift, "shift");
+  f32(invstd, "invstd");
+  shape(grad_y, x.sizes(), "grad_y");
   const int64_t B = x.size(0), C = x.size(1), nf = chan_col.size(0);
+  numel(shift, nf, "shift");
+  numel(invstd, nf, "invstd");
   Tensor gx = at::empty_like(x), gw = at::empty({nf}, x.options()),
          gb = at::empty({n_scalar}, x.options());
   const size_t ws_b = gmp_irreps_bn_workspace_size(B, (int)C, (int)nf);
@@ -412,9 +590,24 @@ std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor& 
 }
 
 // ------------------------------------------------------------------ K8 symmetric contraction
+void sc_checks(const Tensor& x, int64_t corr, const Tensor& A1, const optional<Tensor>& A2,
+               const optional<Tensor>& A3) {
+  f32(x, "x");
+  TORCH_CHECK(x.dim() == 3 && x.size(2) == 9, "gmp.symmetric_contraction: x must be (N, C, 9)");
+  TORCH_CHECK(corr >= 1 && corr <= 3, "gmp.symmetric_contraction: correlation 1..3");
+  const int64_t C = x.size(1);
+  f32(A1, "A1");
+  shape(A1, {C, 9, 9}, "A1");
+  TORCH_CHECK(corr < 2 || A2.has_value(), "gmp.symmetric_contraction: A2 needed");
+  TORCH_CHECK(corr < 3 || A3.has_value(), "gmp.symmetric_contraction: A3 needed");
+  if (corr >= 2) opt_f32(A2, {C, 9, 45}, "A2");
+  if (corr >= 3) opt_f32(A3, {C, 9, 165}, "A3");
+}
+
 Tensor symmetric_contraction_fwd(const Tensor& x, int64_t corr, const Tensor& A1,
                                  const optional<Tensor>& A2, const optional<Tensor>& A3) {
-  f32(x, "x");
+  OpGuard g(x, "symmetric_contraction_fwd");
+  sc_checks(x, corr, A1, A2, A3);
   const int64_t N = x.size(0), C = x.size(1);
   Tensor out = at::empty({N, 9 * C}, x.options());
   check_rc(gmp_symmetric_contraction_fwd_f32(N, (int)C, (int)corr, fp(x), fp(A1), cfp(A2),
@@ -427,9 +620,11 @@ std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t co
                                                      const Tensor& A1, const optional<Tensor>& A2,
                                                      const optional<Tensor>& A3,
                                                      const Tensor& gout) {
-  f32(x, "x");
+  OpGuard g(x, "symmetric_contraction_bwd");
+  sc_checks(x, corr, A1, A2, A3);
   f32(gout, "gout");
   const int64_t N = x.size(0), C = x.size(1);
+  shape(gout, {N, 9 * C}, "gout");
   Tensor dx = at::empty_like(x);
   const int64_t nq = corr == 1 ? 9 : (corr == 2 ? 54 : 219);
   Tensor part = at::empty({gmp_sc_groups(N), C, 9, nq}, x.options());
@@ -439,93 +634,171 @@ std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t co
   return {dx, part};
 }
 
-// ------------------------------------------------------------------ K7 node form
-uint32_t* u32p(const optional<Tensor>& t) {
-  return t.has_value() ? reinterpret_cast<uint32_t*>(t->data_ptr<int32_t>()) : nullptr;
+// ------------------------------------------------------------------ K7 per-edge z rows
+// The host descriptor travels as int[] (n_paths, in_dim, out_dim, sh_dim, weight_numel, z_size,
+// n_blocks, blk_off[4], blk_mul[4], blk_l[4]); the 64-byte path records as a device uint8 tensor.
+struct TpDescHost {
+  int n_paths, in_dim, out_dim, sh_dim;
+  long long weight_numel;
+  int z_size, n_blocks;
+  int blk_off[4], blk_mul[4], blk_l[4];
+};
+static_assert(sizeof(TpDescHost) == 80, "descriptor layout (include/gmp.h)");
+
+TpDescHost tp_desc(at::IntArrayRef d) {
+  TORCH_CHECK(d.size() == 19, "gmp.tp: descriptor has 19 ints");
+  TpDescHost h;
+  h.n_paths = (int)d[0]; h.in_dim = (int)d[1]; h.out_dim = (int)d[2]; h.sh_dim = (int)d[3];
+  h.weight_numel = d[4]; h.z_size = (int)d[5]; h.n_blocks = (int)d[6];
+  for (int k = 0; k < 4; ++k) {
+    h.blk_off[k] = (int)d[7 + k];
+    h.blk_mul[k] = (int)d[11 + k];
+    h.blk_l[k] = (int)d[15 + k];
+  }
+  return h;
 }
-const uint32_t* u32p(const Tensor& t) {
-  return reinterpret_cast<const uint32_t*>(t.data_ptr<int32_t>());
+
+void tp_edge_checks(const TpDescHost& h, const Tensor& paths, const Tensor& cg, const Tensor& x,
+                    const Tensor& sh, const Tensor& src_sorted, const Tensor& perm, int64_t e0,
+                    int64_t e1) {
+  need(paths, at::kByte, "paths");
+  numel(paths, 64 * (int64_t)h.n_paths, "paths");
+  f32(cg, "cg");
+  f32(x, "x");
+  f32(sh, "sh");
+  i64(src_sorted, "src_sorted");
+  i64(perm, "perm");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) == h.in_dim, "gmp.tp_edge_z: x must be (N, in_dim)");
+  const int64_t E = src_sorted.numel();
+  shape(sh, {E, (int64_t)h.sh_dim}, "sh");
+  numel(perm, E, "perm");
+  TORCH_CHECK(0 <= e0 && e0 <= e1 && e1 <= E, "gmp.tp_edge_z: 0 <= e0 <= e1 <= E");
+}
+
+Tensor tp_edge_z(at::IntArrayRef desc, const Tensor& paths, const Tensor& cg, const Tensor& x,
+                 const Tensor& sh, const Tensor& src_sorted, const Tensor& perm, int64_t e0,
+                 int64_t e1) {
+  OpGuard g(x, "tp_edge_z");
+  const TpDescHost h = tp_desc(desc);
+  tp_edge_checks(h, paths, cg, x, sh, src_sorted, perm, e0, e1);
+  Tensor z = at::empty({(e1 - e0 + 1) * h.z_size}, x.options());
+  check_rc(gmp_tp_edge_z_f32(&h, paths.data_ptr(), fp(cg), (int)cg.numel(), fp(x), fp(sh),
+                             ip(src_sorted), ip(perm), e0, e1, fp(z), cur_stream()),
+           "gmp_tp_edge_z_f32");
+  return z;
+}
+
+std::tuple<Tensor, Tensor> tp_edge_z_bwd(at::IntArrayRef desc, const Tensor& paths,
+                                         const Tensor& cg, const Tensor& x, const Tensor& sh,
+                                         const Tensor& src_sorted, const Tensor& perm, int64_t e0,
+                                         int64_t e1, const Tensor& dz) {
+  OpGuard g(x, "tp_edge_z_bwd");
+  const TpDescHost h = tp_desc(desc);
+  tp_edge_checks(h, paths, cg, x, sh, src_sorted, perm, e0, e1);
+  f32(dz, "dz");
+  numel(dz, (e1 - e0 + 1) * h.z_size, "dz");
+  Tensor dx = at::empty({e1 - e0, (int64_t)h.in_dim}, x.options());
+  Tensor dY = at::empty({e1 - e0, (int64_t)h.sh_dim}, x.options());
+  check_rc(gmp_tp_edge_z_bwd_f32(&h, paths.data_ptr(), fp(cg), (int)cg.numel(), fp(x), fp(sh),
+                                 ip(src_sorted), ip(perm), e0, e1, fp(dz), fp(dx), fp(dY),
+                                 cur_stream()),
+           "gmp_tp_edge_z_bwd_f32");
+  return {dx, dY};
+}
+
+// per-edge-weight form (GMP_TP_MODE=edge, or radial hidden sizes outside the node form): the
+// chunk [c0, c1) of receiver-sorted edges with its weights W (c1 - c0, weight_numel)
+void tp_conv_fwd(int64_t layout, at::IntArrayRef desc, const Tensor& paths, const Tensor& cg,
+                 const Tensor& x, const Tensor& sh, const Tensor& W, const Tensor& src_sorted,
+                 const Tensor& perm, int64_t c0, int64_t c1, Tensor msg) {
+  OpGuard g(x, "tp_conv_fwd");
+  const TpDescHost h = tp_desc(desc);
+  tp_edge_checks(h, paths, cg, x, sh, src_sorted, perm, c0, c1);
+  f32(W, "W");
+  f32(msg, "msg");
+  shape(W, {c1 - c0, (int64_t)h.weight_numel}, "W");
+  shape(msg, {src_sorted.numel(), (int64_t)h.out_dim}, "msg");
+  check_rc(gmp_tp_conv_fwd_f32((int)layout, &h, paths.data_ptr(), fp(cg), (int)cg.numel(), fp(x),
+                               fp(sh), fp(W), ip(src_sorted), ip(perm), c0, c1, fp(msg),
+                               cur_stream()),
+           "gmp_tp_conv_fwd_f32");
+}
+
+Tensor tp_conv_bwd(int64_t layout, at::IntArrayRef desc, const Tensor& paths, const Tensor& cg,
+                   const Tensor& x, const Tensor& sh, const Tensor& W, const Tensor& recv_sorted,
+                   const Tensor& src_sorted, const Tensor& perm, int64_t c0, int64_t c1,
+                   const Tensor& gout, Tensor dx_edge, Tensor dY_edge) {
+  OpGuard g(x, "tp_conv_bwd");
+  const TpDescHost h = tp_desc(desc);
+  tp_edge_checks(h, paths, cg, x, sh, src_sorted, perm, c0, c1);
+  const int64_t E = src_sorted.numel();
+  f32(W, "W");
+  i64(recv_sorted, "recv_sorted");
+  f32(gout, "gout");
+  f32(dx_edge, "dx_edge");
+  f32(dY_edge, "dY_edge");
+  shape(W, {c1 - c0, (int64_t)h.weight_numel}, "W");
+  numel(recv_sorted, E, "recv_sorted");
+  TORCH_CHECK(gout.dim() == 2 && gout.size(1) == h.out_dim, "gmp.tp_conv_bwd: gout (N, out_dim)");
+  shape(dx_edge, {E, (int64_t)h.in_dim}, "dx_edge");
+  shape(dY_edge, {E, (int64_t)h.sh_dim}, "dY_edge");
+  Tensor dW = at::empty_like(W);
+  check_rc(gmp_tp_conv_bwd_f32((int)layout, &h, paths.data_ptr(), fp(cg), (int)cg.numel(), fp(x),
+                               fp(sh), fp(W), ip(recv_sorted), ip(src_sorted), ip(perm), c0, c1,
+                               fp(gout), fp(dW), fp(dx_edge), fp(dY_edge), cur_stream()),
+           "gmp_tp_conv_bwd_f32");
+  return dW;
+}
+
+// ------------------------------------------------------------------ K7 node form
+void node_checks(const Tensor& eoff, const Tensor& Z, const Tensor& A, int64_t w) {
+  i64(eoff, "eoff");
+  f32(Z, "Z");
+  f32(A, "A");
+  TORCH_CHECK(eoff.numel() >= 1, "gmp.tp_node: eoff holds n_recv + 1 offsets");
+  TORCH_CHECK(A.dim() == 2, "gmp.tp_node: A must be (n_e, H)");
+  TORCH_CHECK(Z.dim() == 2 && Z.size(1) == w && Z.size(0) >= A.size(0),
+              "gmp.tp_node: Z must be (>= n_e, w)");
 }
 
 std::tuple<Tensor, Tensor> tp_node_outer(const Tensor& eoff, const Tensor& Z, const Tensor& A,
-                                         int64_t w, const optional<Tensor>& rmax) {
+                                         int64_t w) {
+  OpGuard g(A, "tp_node_outer");
+  node_checks(eoff, Z, A, w);
   const int64_t c = eoff.numel() - 1, H = A.size(1);
   Tensor S = at::empty({c, w, H}, A.options()), Sb = at::empty({c, w}, A.options());
-  if (rmax.has_value()) {
-    f32(*rmax, "rmax");
-    TORCH_CHECK(rmax->numel() >= c * (w / 16), "gmp.tp_node_outer: rmax holds n_recv * w / 16");
-  }
-  check_rc(gmp_tp_node_outer_rmax_f32(c, w, H, ip(i64(eoff, "eoff")), fp(Z), fp(f32(A, "A")),
-                                      fp(S), fp(Sb), rmax.has_value() ? fp(*rmax) : nullptr,
-                                      cur_stream()),
-           "gmp_tp_node_outer_rmax_f32");
+  check_rc(gmp_tp_node_outer_f32(c, w, H, ip(eoff), fp(Z), fp(A), fp(S), fp(Sb), cur_stream()),
+           "gmp_tp_node_outer_f32");
   return {S, Sb};
-}
-
-void absmax(const Tensor& x, Tensor amax) {
-  f32(x, "x");
-  check_rc(gmp_absmax_f32(fp(x), x.numel(), reinterpret_cast<uint32_t*>(amax.data_ptr<int32_t>()),
-                          cur_stream()),
-           "gmp_absmax_f32");
-}
-
-Tensor tp_split_w2_h2(const Tensor& W2, const Tensor& b2, int64_t off, int64_t mul1, int64_t mo,
-                      bool fwd, const Tensor& wmax) {
-  f32(W2, "W2");
-  f32(b2, "b2");
-  const int64_t H = W2.size(1), K1 = mul1 * H;
-  Tensor planes = at::empty({fwd ? 2 * mo * (K1 + mul1) : 2 * K1 * mo},
-                            W2.options().dtype(at::kShort));
-  check_rc(gmp_tp_split_w2_h2_f32(mul1, mo, H, fp(W2) + off * H, fp(b2) + off, u32p(wmax),
-                                  fwd ? planes.data_ptr() : nullptr,
-                                  fwd ? nullptr : planes.data_ptr(), cur_stream()),
-           "gmp_tp_split_w2_h2_f32");
-  return planes;
-}
-
-void tp_gemm_h2(const Tensor& A1, int64_t K1, const optional<Tensor>& A2, int64_t K2,
-                const Tensor& Bp, int64_t ldb, int64_t N, Tensor C, int64_t c_offset,
-                int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, bool accumulate,
-                const Tensor& arow, const Tensor& wmax) {
-  f32(A1, "A1");
-  f32(arow, "arow");
-  need(Bp, at::kShort, "B planes");
-  TORCH_CHECK(C.is_cuda() && C.scalar_type() == at::kFloat, "gmp.tp_gemm_h2: C");
-  const int64_t M = A1.size(0);
-  TORCH_CHECK(M > 0 && arow.numel() % M == 0, "gmp.tp_gemm_h2: arow holds M * nparts words");
-  check_rc(gmp_tp_gemm_h2_f32(M, N, K1, fp(A1), A1.size(1), K2, cfp(A2),
-                              A2.has_value() ? A2->size(1) : 0, Bp.data_ptr(), ldb, N * ldb,
-                              fp(arow), arow.numel() / M, u32p(wmax),
-                              C.data_ptr<float>() + c_offset, cgrp, cldg, cldr, cldn, accumulate,
-                              cur_stream()),
-           "gmp_tp_gemm_h2_f32");
-}
-
-Tensor tp_gemm_h2_widen(const Tensor& A, const Tensor& Bp, int64_t N, const Tensor& amax,
-                        const Tensor& wmax) {
-  f32(A, "A");
-  need(Bp, at::kShort, "B planes");
-  const int64_t M = A.size(0), K = A.size(1);
-  Tensor C = at::empty({M, N}, A.options());
-  check_rc(gmp_tp_gemm_h2_widen_f32(M, N, K, fp(A), K, Bp.data_ptr(), K, N * K, u32p(amax),
-                                    u32p(wmax), fp(C), N, cur_stream()),
-           "gmp_tp_gemm_h2_widen_f32");
-  return C;
 }
 
 void tp_node_apply(const Tensor& eoff, const Tensor& Z, const Tensor& A, const Tensor& T,
                    const Tensor& Tb, Tensor dA, Tensor dZ) {
-  const int64_t c = eoff.numel() - 1, w = Z.size(1), H = A.size(1);
-  TORCH_CHECK(dZ.sizes() == Z.sizes(), "gmp.tp_node_apply: dZ shape");
-  check_rc(gmp_tp_node_apply_f32(c, w, H, ip(eoff), fp(Z), fp(A), fp(f32(T, "T")), fp(Tb),
-                                 fp(f32(dZ, "dZ")), fp(f32(dA, "dA")), cur_stream()),
+  OpGuard g(A, "tp_node_apply");
+  const int64_t w = Z.size(1);
+  node_checks(eoff, Z, A, w);
+  const int64_t c = eoff.numel() - 1, H = A.size(1);
+  f32(T, "T");
+  f32(Tb, "Tb");
+  f32(dA, "dA");
+  f32(dZ, "dZ");
+  numel(T, c * w * H, "T");
+  numel(Tb, c * w, "Tb");
+  shape(dA, A.sizes(), "dA");
+  shape(dZ, Z.sizes(), "dZ");
+  check_rc(gmp_tp_node_apply_f32(c, w, H, ip(eoff), fp(Z), fp(A), fp(T), fp(Tb), fp(dZ), fp(dA),
+                                 cur_stream()),
            "gmp_tp_node_apply_f32");
 }
 
 Tensor tp_split_w2(const Tensor& W2, const Tensor& b2, int64_t off, int64_t mul1, int64_t mo,
                    bool fwd) {
+  OpGuard g(W2, "tp_split_w2");
   f32(W2, "W2");
   f32(b2, "b2");
+  TORCH_CHECK(W2.dim() == 2 && b2.numel() == W2.size(0), "gmp.tp_split_w2: W2 (wn, H), b2 (wn)");
+  TORCH_CHECK(off >= 0 && mul1 > 0 && mo > 0 && off + mul1 * mo <= W2.size(0),
+              "gmp.tp_split_w2: path block outside W2");
   const int64_t H = W2.size(1), K1 = mul1 * H;
   Tensor planes = at::empty({fwd ? 3 * mo * (K1 + mul1) : 3 * K1 * mo},
                             W2.options().dtype(at::kShort));
@@ -540,21 +813,42 @@ Tensor tp_split_w2(const Tensor& W2, const Tensor& b2, int64_t off, int64_t mul1
 void tp_gemm_x3(const Tensor& A1, int64_t K1, const optional<Tensor>& A2, int64_t K2,
                 const Tensor& Bp, int64_t ldb, int64_t N, Tensor C, int64_t c_offset,
                 int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, bool accumulate) {
+  OpGuard g(A1, "tp_gemm_x3");
   f32(A1, "A1");
   need(Bp, at::kShort, "B planes");
-  TORCH_CHECK(C.is_cuda() && C.scalar_type() == at::kFloat, "gmp.tp_gemm_x3: C");
+  f32(C, "C");
+  TORCH_CHECK(A1.dim() == 2 && K1 <= A1.size(1), "gmp.tp_gemm_x3: A1 must be (M, >= K1)");
   const int64_t M = A1.size(0);
+  if (A2.has_value() && A2->defined()) {
+    f32(*A2, "A2");
+    TORCH_CHECK(A2->dim() == 2 && A2->size(0) == M && K2 <= A2->size(1),
+                "gmp.tp_gemm_x3: A2 must be (M, >= K2)");
+  } else {
+    TORCH_CHECK(K2 == 0, "gmp.tp_gemm_x3: K2 > 0 needs A2");
+  }
+  TORCH_CHECK(ldb == K1 + K2 && Bp.numel() >= 3 * N * ldb, "gmp.tp_gemm_x3: B planes hold 3 N ldb");
+  TORCH_CHECK(cgrp > 0 && c_offset >= 0 && cldg >= 0 && cldr >= 0 && cldn >= 0,
+              "gmp.tp_gemm_x3: epilogue addressing");
+  if (M > 0 && N > 0) {
+    const int64_t last = c_offset + ((M - 1) / cgrp) * cldg + std::min(cgrp - 1, M - 1) * cldr +
+                         (N - 1) * cldn;
+    TORCH_CHECK(last < C.numel(), "gmp.tp_gemm_x3: the output block reaches element ", last,
+                " of C (", C.numel(), " elements)");
+  }
   check_rc(gmp_tp_gemm_x3_f32(M, N, K1, fp(A1), A1.size(1), K2, cfp(A2),
-                              A2.has_value() ? A2->size(1) : 0, Bp.data_ptr(), ldb, N * ldb,
-                              C.data_ptr<float>() + c_offset, cgrp, cldg, cldr, cldn, accumulate,
-                              cur_stream()),
+                              A2.has_value() && A2->defined() ? A2->size(1) : 0, Bp.data_ptr(),
+                              ldb, N * ldb, C.data_ptr<float>() + c_offset, cgrp, cldg, cldr, cldn,
+                              accumulate, cur_stream()),
            "gmp_tp_gemm_x3_f32");
 }
 
 Tensor tp_gemm_x3_widen(const Tensor& A, const Tensor& Bp, int64_t N) {
+  OpGuard g(A, "tp_gemm_x3_widen");
   f32(A, "A");
   need(Bp, at::kShort, "B planes");
+  TORCH_CHECK(A.dim() == 2, "gmp.tp_gemm_x3_widen: A must be (M, K)");
   const int64_t M = A.size(0), K = A.size(1);
+  TORCH_CHECK(Bp.numel() >= 3 * N * K, "gmp.tp_gemm_x3_widen: B planes hold 3 N K");
   Tensor C = at::empty({M, N}, A.options());
   check_rc(gmp_tp_gemm_x3_widen_f32(M, N, K, fp(A), K, Bp.data_ptr(), K, N * K, fp(C), N,
                                     cur_stream()),
@@ -563,8 +857,11 @@ Tensor tp_gemm_x3_widen(const Tensor& A, const Tensor& Bp, int64_t N) {
 }
 
 Tensor outer_sum_cols(const Tensor& A, const Tensor& B) {
+  OpGuard g(A, "outer_sum_cols");
   f32(A, "A");
   f32(B, "B");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0),
+              "gmp.outer_sum_cols: A (K, m), B (K, n)");
   const int64_t K = A.size(0), m = A.size(1), n = B.size(1);
   Tensor C = at::empty({m, n}, A.options());
   const size_t ws_b = gmp_outer_sum_cols_workspace_size(K, m, n);
@@ -577,16 +874,268 @@ Tensor outer_sum_cols(const Tensor& A, const Tensor& B) {
 
 // ------------------------------------------------------------------ edge outer sums (K5)
 std::tuple<Tensor, Tensor> edge_outer_sum(const Tensor& A, const Tensor& B) {
+  OpGuard g(A, "edge_outer_sum");
   f32(A, "A");
   f32(B, "B");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0),
+              "gmp.edge_outer_sum: A (K, m), B (K, n)");
   const int64_t K = A.size(0), m = A.size(1), n = B.size(1);
   Tensor C = at::empty({m, n}, A.options()), cs = at::empty({m}, A.options());
   const size_t ws_b = gmp_edge_outer_sum_ex_workspace_size(K, m, n);
   Tensor ws = at::empty({(int64_t)ws_b + 1}, A.options().dtype(at::kByte));
-  check_rc(gmp_edge_outer_sum_ex_f32(K, m, n, fp(A), m, fp(B), n, -1, nullptr, nullptr, fp(C), n,
-                                     fp(cs), ws.data_ptr(), ws_b, cur_stream()),
-           "gmp_edge_outer_sum_ex_f32");
+  const int rc = gmp_edge_outer_sum_ex_f32(K, m, n, fp(A), m, fp(B), n, -1, nullptr, nullptr,
+                                           fp(C), n, fp(cs), ws.data_ptr(), ws_b, cur_stream());
+  if (rc == GMP_ERR_UNSUPPORTED) {  // outside the tile buckets: the library GEMM on the device
+    at::mm_out(C, A.t(), B);
+    at::sum_out(cs, A, {0});
+  } else {
+    check_rc(rc, "gmp_edge_outer_sum_ex_f32");
+  }
   return {C, cs};
+}
+
+// operand view usable by the strided outer-sum kernels: (K, m) f32 on the op's device, unit
+// column stride, row stride a multiple of 4 floats, 16-byte aligned base
+bool rows_view_ok(const Tensor& t) {
+  return t.dim() == 2 && t.stride(1) == 1 && t.stride(0) % 4 == 0 &&
+         reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
+}
+Tensor rows_view(const Tensor& t, const char* what) {
+  on_device(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 2, "gmp: ", what, " must be 2-D f32");
+  return rows_view_ok(t) ? t : t.contiguous();
+}
+void out_view(const Tensor& C, int64_t m, int64_t n, const char* what) {
+  on_device(C, what);
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 2 && C.stride(1) == 1,
+              "gmp: ", what, " must be a 2-D f32 view with unit column stride");
+  shape(C, {m, n}, what);
+}
+
+// act(B * w + b) rows as the edge outer sums' prologue computes them (act 0 relu, 1 silu)
+Tensor act_rows(const Tensor& B, int64_t act, const optional<Tensor>& w,
+                const optional<Tensor>& b) {
+  if (act < 0) return B;
+  Tensor y = B * w->view({1, -1}) + b->view({1, -1});
+  return act == 0 ? at::relu(y) : at::silu(y);
+}
+
+// C[:] = A^T act(B) (+ colsum[:] = colsum(A)) into strided views; returns 0 when the split-plane
+// / f32-MFMA kernels ran, 1 when the shape was outside their buckets and the library GEMM did.
+int64_t edge_outer_sum_ex(const Tensor& A_, const Tensor& B_, Tensor C,
+                          const optional<Tensor>& colsum, int64_t act, const optional<Tensor>& w,
+                          const optional<Tensor>& b) {
+  OpGuard g(A_, "edge_outer_sum_ex");
+  Tensor A = rows_view(A_, "A"), B = rows_view(B_, "B");
+  TORCH_CHECK(A.size(0) == B.size(0), "gmp.edge_outer_sum_ex: A (K, m), B (K, n)");
+  const int64_t K = A.size(0), m = A.size(1), n = B.size(1);
+  out_view(C, m, n, "C");
+  TORCH_CHECK(act >= -1 && act <= 1, "gmp.edge_outer_sum_ex: act -1, 0 or 1");
+  if (act >= 0) {
+    TORCH_CHECK(w.has_value() && b.has_value(), "gmp.edge_outer_sum_ex: act needs w, b");
+    f32(*w, "w");
+    f32(*b, "b");
+    numel(*w, n, "w");
+    numel(*b, n, "b");
+  }
+  if (colsum.has_value()) {
+    f32(*colsum, "colsum");
+    numel(*colsum, m, "colsum");
+  }
+  const size_t ws_b = gmp_edge_outer_sum_ex_workspace_size(K, m, n);
+  Tensor ws = at::empty({(int64_t)ws_b + 1}, A.options().dtype(at::kByte));
+  const int rc = gmp_edge_outer_sum_ex_f32(
+      K, m, n, fp(A), A.stride(0), fp(B), B.stride(0), (int)act, act >= 0 ? fp(*w) : nullptr,
+      act >= 0 ? fp(*b) : nullptr, C.data_ptr<float>(), C.stride(0),
+      colsum.has_value() ? fp(*colsum) : nullptr, ws.data_ptr(), ws_b, cur_stream());
+  if (rc != GMP_ERR_UNSUPPORTED) {
+    check_rc(rc, "gmp_edge_outer_sum_ex_f32");
+    return 0;
+  }
+  C.copy_(at::mm(A.t(), act_rows(B, act, w, b)));
+  if (colsum.has_value()) colsum->copy_(A.sum(0));
+  return 1;
+}
+
+// C[:] = A^T [B1 | B2] (+ colsum) in one pass over A where the split-plane kernel applies (0),
+// else two edge_outer_sum_ex products (1)
+int64_t edge_outer_sum_ex2(const Tensor& A_, const Tensor& B1_, const Tensor& B2_, Tensor C,
+                           const optional<Tensor>& colsum) {
+  OpGuard g(A_, "edge_outer_sum_ex2");
+  Tensor A = rows_view(A_, "A"), B1 = rows_view(B1_, "B1"), B2 = rows_view(B2_, "B2");
+  TORCH_CHECK(A.size(0) == B1.size(0) && A.size(0) == B2.size(0),
+              "gmp.edge_outer_sum_ex2: A (K, m), B1 (K, n1), B2 (K, n2)");
+  const int64_t K = A.size(0), m = A.size(1), n1 = B1.size(1), n2 = B2.size(1);
+  out_view(C, m, n1 + n2, "C");
+  if (colsum.has_value()) {
+    f32(*colsum, "colsum");
+    numel(*colsum, m, "colsum");
+  }
+  const size_t ws_b = gmp_edge_outer_sum_rect_workspace_size(K, m, n1 + n2);
+  Tensor ws = at::empty({(int64_t)ws_b + 1}, A.options().dtype(at::kByte));
+  const int rc = gmp_edge_outer_sum_ex2_f32(K, m, n1, n2, fp(A), A.stride(0), fp(B1),
+                                            B1.stride(0), fp(B2), B2.stride(0),
+                                            C.data_ptr<float>(), C.stride(0),
+                                            colsum.has_value() ? fp(*colsum) : nullptr,
+                                            ws.data_ptr(), ws_b, cur_stream());
+  if (rc != GMP_ERR_UNSUPPORTED) {
+    check_rc(rc, "gmp_edge_outer_sum_ex2_f32");
+    return 0;
+  }
+  edge_outer_sum_ex(A, B1, C.narrow(1, 0, n1), colsum, -1, c10::nullopt, c10::nullopt);
+  edge_outer_sum_ex(A, B2, C.narrow(1, n1, n2), c10::nullopt, -1, c10::nullopt, c10::nullopt);
+  return 1;
+}
+
+// (A^T act(X w + b), colsum(A)) for the EGNN y1 / m operands rebuilt from x_hat; with amax (the
+// max |A| device word) the HF two-plane form
+std::tuple<Tensor, Tensor> edge_outer_sum_act(const Tensor& A, const Tensor& X, const Tensor& w,
+                                              const Tensor& b, int64_t act,
+                                              const optional<Tensor>& amax) {
+  OpGuard g(A, "edge_outer_sum_act");
+  f32(A, "A");
+  f32(X, "X");
+  f32(w, "w");
+  f32(b, "b");
+  TORCH_CHECK(A.dim() == 2 && A.sizes() == X.sizes() && A.size(1) == w.numel() &&
+                  b.numel() == w.numel(),
+              "gmp.edge_outer_sum_act: A, X (K, d), w, b (d)");
+  TORCH_CHECK(act == 0 || act == 1, "gmp.edge_outer_sum_act: act 0 (relu) or 1 (silu)");
+  const int64_t K = A.size(0), d = A.size(1);
+  Tensor C = at::empty({d, d}, A.options()), cs = at::empty({d}, A.options());
+  const size_t ws_b = gmp_edge_outer_sum_workspace_size(K, d);
+  Tensor ws = at::empty({(int64_t)ws_b + 1}, A.options().dtype(at::kByte));
+  int rc;
+  if (amax.has_value()) {
+    i32(*amax, "amax");
+    rc = gmp_edge_outer_sum_act_hf_f32(
+        K, d, fp(A), fp(X), fp(w), fp(b), (int)act,
+        reinterpret_cast<const uint32_t*>(amax->data_ptr<int32_t>()), fp(C), fp(cs),
+        ws.data_ptr(), ws_b, cur_stream());
+  } else {
+    rc = gmp_edge_outer_sum_act_f32(K, d, fp(A), fp(X), fp(w), fp(b), (int)act, fp(C), fp(cs),
+                                    ws.data_ptr(), ws_b, cur_stream());
+  }
+  if (rc == GMP_ERR_UNSUPPORTED) {
+    C.copy_(at::mm(A.t(), act_rows(X, act, w, b)));
+    cs.copy_(A.sum(0));
+  } else {
+    check_rc(rc, amax.has_value() ? "gmp_edge_outer_sum_act_hf_f32" : "gmp_edge_outer_sum_act_f32");
+  }
+  return {C, cs};
+}
+
+// ------------------------------------------------------------------ K5g GVP message GVPs
+void gvp_w_checks(const std::vector<Tensor>& W, const std::vector<std::vector<int64_t>>& shp) {
+  TORCH_CHECK(W.size() == shp.size(), "gmp.gvp: ", shp.size(), " weight tensors expected");
+  for (size_t k = 0; k < W.size(); ++k) {
+    f32(W[k], "gvp weight");
+    shape(W[k], shp[k], "gvp weight");
+  }
+}
+// gvp_layer weights: Ws (128, 144), bs (128), Wsv (16, 128), bsv (16), Wh (16, 16), Wv (16, 16)
+const std::vector<std::vector<int64_t>> kGvpLayerW = {{128, 144}, {128}, {16, 128}, {16},
+                                                      {16, 16}, {16, 16}};
+// gvp_msg0 weights: We (128, 32), Wn (128, 48), b (128), Wv (16, 48), Wsv (16, 128), bsv (16),
+// wev (48)
+const std::vector<std::vector<int64_t>> kGvpMsg0W = {{128, 32}, {128, 48}, {128}, {16, 48},
+                                                     {16, 128}, {16}, {48}};
+
+int64_t gvp_rows(const Tensor& s, const Tensor& v) {
+  f32(s, "s");
+  f32(v, "v");
+  TORCH_CHECK(s.dim() == 2 && s.size(1) == 128, "gmp.gvp_layer: s must be (E, 128)");
+  TORCH_CHECK(v.numel() == s.size(0) * 48, "gmp.gvp_layer: v must be (E, 16, 3)");
+  return s.size(0);
+}
+
+std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
+                                         const std::vector<Tensor>& W, bool relu) {
+  OpGuard g(s, "gvp_layer_fwd");
+  const int64_t E = gvp_rows(s, v);
+  gvp_w_checks(W, kGvpLayerW);
+  Tensor so = at::empty_like(s), vo = at::empty_like(v);
+  check_rc(gmp_gvp_layer_fwd_f32(E, relu ? 1 : 0, fp(s), fp(v), fp(W[0]), fp(W[1]), fp(W[2]),
+                                 fp(W[3]), fp(W[4]), fp(W[5]), fp(so), fp(vo), cur_stream()),
+           "gmp_gvp_layer_fwd_f32");
+  return {so, vo};
+}
+
+std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>& W,
+                                  const Tensor& ds, const Tensor& dv, bool relu) {
+  OpGuard g(s, "gvp_layer_bwd");
+  const int64_t E = gvp_rows(s, v);
+  gvp_w_checks(W, kGvpLayerW);
+  f32(ds, "ds");
+  f32(dv, "dv");
+  shape(ds, s.sizes(), "ds");
+  shape(dv, v.sizes(), "dv");
+  auto o = fopt(s);
+  Tensor ds_in = at::empty_like(s), dv_in = at::empty_like(v);
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({E, 128}, o);
+  Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 16}, o);
+  Tensor vh = at::empty({E, 48}, o), dvpre = at::empty({E, 48}, o), dvh = at::empty({E, 48}, o);
+  check_rc(gmp_gvp_layer_bwd_f32(E, relu ? 1 : 0, fp(s), fp(v), fp(W[0]), fp(W[1]), fp(W[2]),
+                                 fp(W[3]), fp(W[4]), fp(W[5]), fp(ds), fp(dv), fp(ds_in),
+                                 fp(dv_in), fp(dspre), fp(spre), fp(dgate), fp(vn), fp(vh),
+                                 fp(dvpre), fp(dvh), cur_stream()),
+           "gmp_gvp_layer_bwd_f32");
+  return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
+}
+
+int64_t gvp_msg0_checks(const Tensor& send, const Tensor& recv, const Tensor& P, const Tensor& Q,
+                        const Tensor& es, const Tensor& ev, const std::vector<Tensor>& W) {
+  i64(send, "send");
+  i64(recv, "recv");
+  f32(P, "P");
+  f32(Q, "Q");
+  f32(es, "es");
+  f32(ev, "ev");
+  const int64_t E = send.numel();
+  numel(recv, E, "recv");
+  TORCH_CHECK(P.dim() == 2 && P.size(1) == 256, "gmp.gvp_msg0: P must be (N, 256)");
+  shape(Q, {P.size(0), 288}, "Q");
+  shape(es, {E, 32}, "es");
+  shape(ev, {E, 3}, "ev");
+  gvp_w_checks(W, kGvpMsg0W);
+  return E;
+}
+
+std::tuple<Tensor, Tensor> gvp_msg0_fwd(const Tensor& send, const Tensor& recv, const Tensor& P,
+                                        const Tensor& Q, const Tensor& es, const Tensor& ev,
+                                        const std::vector<Tensor>& W) {
+  OpGuard g(P, "gvp_msg0_fwd");
+  const int64_t E = gvp_msg0_checks(send, recv, P, Q, es, ev, W);
+  auto o = fopt(P);
+  Tensor so = at::empty({E, 128}, o), vo = at::empty({E, 16, 3}, o);
+  check_rc(gmp_gvp_msg0_fwd_f32(E, ip(send), ip(recv), fp(P), fp(Q), fp(es), fp(ev), fp(W[0]),
+                                fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]), fp(W[6]),
+                                fp(so), fp(vo), cur_stream()),
+           "gmp_gvp_msg0_fwd_f32");
+  return {so, vo};
+}
+
+std::vector<Tensor> gvp_msg0_bwd(const Tensor& send, const Tensor& recv, const Tensor& P,
+                                 const Tensor& Q, const Tensor& es, const Tensor& ev,
+                                 const std::vector<Tensor>& W, const Tensor& ds,
+                                 const Tensor& dv) {
+  OpGuard g(P, "gvp_msg0_bwd");
+  const int64_t E = gvp_msg0_checks(send, recv, P, Q, es, ev, W);
+  f32(ds, "ds");
+  f32(dv, "dv");
+  shape(ds, {E, 128}, "ds");
+  numel(dv, E * 48, "dv");
+  auto o = fopt(P);
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({E, 128}, o);
+  Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 48}, o);
+  Tensor vh = at::empty({E, 144}, o), dvh = at::empty({E, 144}, o);
+  Tensor dvpre = at::empty({E, 48}, o), des = at::empty({E, 32}, o), dev = at::empty({E, 3}, o);
+  check_rc(gmp_gvp_msg0_bwd_f32(E, ip(send), ip(recv), fp(P), fp(Q), fp(es), fp(ev), fp(W[0]),
+                                fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]), fp(W[6]),
+                                fp(ds), fp(dv), fp(dspre), fp(spre), fp(dgate), fp(vn), fp(vh),
+                                fp(dvpre), fp(dvh), fp(des), fp(dev), cur_stream()),
+           "gmp_gvp_msg0_bwd_f32");
+  return {dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev};
 }
 
 // ------------------------------------------------------------------ Meta (shape) kernels
@@ -709,23 +1258,27 @@ std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t co
   return {at::empty_like(x), at::empty({gmp_sc_groups(x.size(0)), x.size(1), 9, nq},
                                        x.options())};
 }
+Tensor tp_edge_z(at::IntArrayRef desc, const Tensor&, const Tensor&, const Tensor& x,
+                 const Tensor&, const Tensor&, const Tensor&, int64_t e0, int64_t e1) {
+  return at::empty({(e1 - e0 + 1) * desc[5]}, x.options());
+}
+std::tuple<Tensor, Tensor> tp_edge_z_bwd(at::IntArrayRef desc, const Tensor&, const Tensor&,
+                                         const Tensor& x, const Tensor&, const Tensor&,
+                                         const Tensor&, int64_t e0, int64_t e1, const Tensor&) {
+  return {at::empty({e1 - e0, desc[1]}, x.options()), at::empty({e1 - e0, desc[3]}, x.options())};
+}
+void tp_conv_fwd(int64_t, at::IntArrayRef, const Tensor&, const Tensor&, const Tensor&,
+                 const Tensor&, const Tensor&, const Tensor&, const Tensor&, int64_t, int64_t,
+                 Tensor) {}
+Tensor tp_conv_bwd(int64_t, at::IntArrayRef, const Tensor&, const Tensor&, const Tensor&,
+                   const Tensor&, const Tensor& W, const Tensor&, const Tensor&, const Tensor&,
+                   int64_t, int64_t, const Tensor&, Tensor, Tensor) {
+  return at::empty_like(W);
+}
 std::tuple<Tensor, Tensor> tp_node_outer(const Tensor& eoff, const Tensor&, const Tensor& A,
-                                         int64_t w, const optional<Tensor>&) {
+                                         int64_t w) {
   const int64_t c = eoff.numel() - 1;
   return {at::empty({c, w, A.size(1)}, A.options()), at::empty({c, w}, A.options())};
-}
-void absmax(const Tensor&, Tensor) {}
-Tensor tp_split_w2_h2(const Tensor& W2, const Tensor&, int64_t, int64_t mul1, int64_t mo,
-                      bool fwd, const Tensor&) {
-  const int64_t K1 = mul1 * W2.size(1);
-  return at::empty({fwd ? 2 * mo * (K1 + mul1) : 2 * K1 * mo}, W2.options().dtype(at::kShort));
-}
-void tp_gemm_h2(const Tensor&, int64_t, const optional<Tensor>&, int64_t, const Tensor&, int64_t,
-                int64_t, Tensor, int64_t, int64_t, int64_t, int64_t, int64_t, bool,
-                const Tensor&, const Tensor&) {}
-Tensor tp_gemm_h2_widen(const Tensor& A, const Tensor&, int64_t N, const Tensor&,
-                        const Tensor&) {
-  return at::empty({A.size(0), N}, A.options());
 }
 void tp_node_apply(const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&,
                    Tensor, Tensor) {}
@@ -743,6 +1296,45 @@ Tensor outer_sum_cols(const Tensor& A, const Tensor& B) {
 }
 std::tuple<Tensor, Tensor> edge_outer_sum(const Tensor& A, const Tensor& B) {
   return {at::empty({A.size(1), B.size(1)}, A.options()), at::empty({A.size(1)}, A.options())};
+}
+int64_t edge_outer_sum_ex(const Tensor&, const Tensor&, Tensor, const optional<Tensor>&, int64_t,
+                          const optional<Tensor>&, const optional<Tensor>&) {
+  return 0;
+}
+int64_t edge_outer_sum_ex2(const Tensor&, const Tensor&, const Tensor&, Tensor,
+                           const optional<Tensor>&) {
+  return 0;
+}
+std::tuple<Tensor, Tensor> edge_outer_sum_act(const Tensor& A, const Tensor&, const Tensor&,
+                                              const Tensor&, int64_t, const optional<Tensor>&) {
+  return {at::empty({A.size(1), A.size(1)}, A.options()), at::empty({A.size(1)}, A.options())};
+}
+std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
+                                         const std::vector<Tensor>&, bool) {
+  return {at::empty_like(s), at::empty_like(v)};
+}
+std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&,
+                                  const Tensor&, const Tensor&, bool) {
+  const int64_t E = s.size(0);
+  auto o = s.options();
+  return {at::empty_like(s),      at::empty_like(v),     at::empty({E, 128}, o),
+          at::empty({E, 128}, o), at::empty({E, 16}, o), at::empty({E, 16}, o),
+          at::empty({E, 48}, o),  at::empty({E, 48}, o), at::empty({E, 48}, o)};
+}
+std::tuple<Tensor, Tensor> gvp_msg0_fwd(const Tensor& send, const Tensor&, const Tensor& P,
+                                        const Tensor&, const Tensor&, const Tensor&,
+                                        const std::vector<Tensor>&) {
+  const int64_t E = send.numel();
+  return {at::empty({E, 128}, P.options()), at::empty({E, 16, 3}, P.options())};
+}
+std::vector<Tensor> gvp_msg0_bwd(const Tensor& send, const Tensor&, const Tensor& P,
+                                 const Tensor&, const Tensor&, const Tensor&,
+                                 const std::vector<Tensor>&, const Tensor&, const Tensor&) {
+  const int64_t E = send.numel();
+  auto o = P.options();
+  return {at::empty({E, 128}, o), at::empty({E, 128}, o), at::empty({E, 16}, o),
+          at::empty({E, 48}, o),  at::empty({E, 144}, o), at::empty({E, 48}, o),
+          at::empty({E, 144}, o), at::empty({E, 32}, o),  at::empty({E, 3}, o)};
 }
 }  // namespace meta
 
@@ -797,15 +1389,17 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor? A3) -> Tensor");
   m.def("symmetric_contraction_bwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
         "Tensor? A3, Tensor gout) -> (Tensor dx, Tensor dA_partials)");
-  m.def("tp_node_outer(Tensor eoff, Tensor Z, Tensor A, int w, Tensor(a!)? rmax=None) -> "
-        "(Tensor S, Tensor Sb)");
-  m.def("absmax(Tensor x, Tensor(a!) amax) -> ()");
-  m.def("tp_split_w2_h2(Tensor W2, Tensor b2, int off, int mul1, int mul_out, bool fwd, "
-        "Tensor wmax) -> Tensor");
-  m.def("tp_gemm_h2(Tensor A1, int K1, Tensor? A2, int K2, Tensor Bp, int ldb, int N, "
-        "Tensor(a!) C, int c_offset, int cgrp, int cldg, int cldr, int cldn, bool accumulate, "
-        "Tensor arow, Tensor wmax) -> ()");
-  m.def("tp_gemm_h2_widen(Tensor A, Tensor Bp, int N, Tensor amax, Tensor wmax) -> Tensor");
+  m.def("tp_edge_z(int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, Tensor src_sorted, "
+        "Tensor perm, int e0, int e1) -> Tensor");
+  m.def("tp_edge_z_bwd(int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, "
+        "Tensor src_sorted, Tensor perm, int e0, int e1, Tensor dz) -> "
+        "(Tensor dx_edge, Tensor dY_edge)");
+  m.def("tp_conv_fwd(int layout, int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, "
+        "Tensor W, Tensor src_sorted, Tensor perm, int c0, int c1, Tensor(a!) msg) -> ()");
+  m.def("tp_conv_bwd(int layout, int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, "
+        "Tensor W, Tensor recv_sorted, Tensor src_sorted, Tensor perm, int c0, int c1, "
+        "Tensor gout, Tensor(a!) dx_edge, Tensor(b!) dY_edge) -> Tensor dW");
+  m.def("tp_node_outer(Tensor eoff, Tensor Z, Tensor A, int w) -> (Tensor S, Tensor Sb)");
   m.def("tp_node_apply(Tensor eoff, Tensor Z, Tensor A, Tensor T, Tensor Tb, Tensor(a!) dA, "
         "Tensor(b!) dZ) -> ()");
   m.def("tp_split_w2(Tensor W2, Tensor b2, int off, int mul1, int mul_out, bool fwd) -> Tensor");
@@ -815,6 +1409,20 @@ TORCH_LIBRARY(gmp, m) {
   m.def("tp_gemm_x3_widen(Tensor A, Tensor Bp, int N) -> Tensor");
   m.def("outer_sum_cols(Tensor A, Tensor B) -> Tensor");
   m.def("edge_outer_sum(Tensor A, Tensor B) -> (Tensor C, Tensor colsum)");
+  m.def("edge_outer_sum_ex(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int act, "
+        "Tensor? w, Tensor? b) -> int");
+  m.def("edge_outer_sum_ex2(Tensor A, Tensor B1, Tensor B2, Tensor(a!) C, Tensor(b!)? colsum) "
+        "-> int");
+  m.def("edge_outer_sum_act(Tensor A, Tensor X, Tensor w, Tensor b, int act, Tensor? amax=None) "
+        "-> (Tensor C, Tensor colsum)");
+  m.def("gvp_layer_fwd(Tensor s, Tensor v, Tensor[] W, bool relu) -> (Tensor s_out, "
+        "Tensor v_out)");
+  m.def("gvp_layer_bwd(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, bool relu) -> "
+        "Tensor[]");
+  m.def("gvp_msg0_fwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
+        "Tensor[] W) -> (Tensor s_out, Tensor v_out)");
+  m.def("gvp_msg0_bwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
+        "Tensor[] W, Tensor ds, Tensor dv) -> Tensor[]");
 }
 
 #define GMP_IMPL(m, ns)                                                    \
@@ -842,17 +1450,24 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("irreps_bn_bwd", ns irreps_bn_bwd);                              \
   m.impl("symmetric_contraction_fwd", ns symmetric_contraction_fwd);      \
   m.impl("symmetric_contraction_bwd", ns symmetric_contraction_bwd);      \
+  m.impl("tp_edge_z", ns tp_edge_z);                                      \
+  m.impl("tp_edge_z_bwd", ns tp_edge_z_bwd);                              \
+  m.impl("tp_conv_fwd", ns tp_conv_fwd);                                  \
+  m.impl("tp_conv_bwd", ns tp_conv_bwd);                                  \
   m.impl("tp_node_outer", ns tp_node_outer);                              \
-  m.impl("absmax", ns absmax);                                            \
-  m.impl("tp_split_w2_h2", ns tp_split_w2_h2);                            \
-  m.impl("tp_gemm_h2", ns tp_gemm_h2);                                    \
-  m.impl("tp_gemm_h2_widen", ns tp_gemm_h2_widen);                        \
   m.impl("tp_node_apply", ns tp_node_apply);                              \
   m.impl("tp_split_w2", ns tp_split_w2);                                  \
   m.impl("tp_gemm_x3", ns tp_gemm_x3);                                    \
   m.impl("tp_gemm_x3_widen", ns tp_gemm_x3_widen);                        \
   m.impl("outer_sum_cols", ns outer_sum_cols);                            \
-  m.impl("edge_outer_sum", ns edge_outer_sum);
+  m.impl("edge_outer_sum", ns edge_outer_sum);                            \
+  m.impl("edge_outer_sum_ex", ns edge_outer_sum_ex);                      \
+  m.impl("edge_outer_sum_ex2", ns edge_outer_sum_ex2);                    \
+  m.impl("edge_outer_sum_act", ns edge_outer_sum_act);                    \
+  m.impl("gvp_layer_fwd", ns gvp_layer_fwd);                              \
+  m.impl("gvp_layer_bwd", ns gvp_layer_bwd);                              \
+  m.impl("gvp_msg0_fwd", ns gvp_msg0_fwd);                                \
+  m.impl("gvp_msg0_bwd", ns gvp_msg0_bwd);
 
 TORCH_LIBRARY_IMPL(gmp, CUDA, m) { GMP_IMPL(m, ) }
 TORCH_LIBRARY_IMPL(gmp, Meta, m) { GMP_IMPL(m, meta::) }

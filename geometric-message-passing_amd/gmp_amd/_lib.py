@@ -90,16 +90,6 @@ SIGNATURES = {
                                                 c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "gmp_cfconv_wgrad_scaled_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                             c_i64, c_vp, c_vp, c_vp]),
-    "gmp_tp_split_w2_h2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                       c_vp]),
-    "gmp_tp_gemm_h2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
-                                   c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64,
-                                   c_i64, c_int, c_vp]),
-    "gmp_tp_gemm_h2_widen_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
-                                         c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "gmp_absmax_f32": (c_int, [c_vp, c_i64, c_vp, c_vp]),
-    "gmp_tp_node_outer_rmax_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                           c_vp, c_vp]),
     "gmp_edge_outer_sum_act_hf_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,
                                               c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "gmp_egnn_edge_bwd_amax_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,

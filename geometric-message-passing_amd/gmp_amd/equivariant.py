@@ -13,7 +13,6 @@ GEMM so that the per-edge weights (721 KB per edge for MACE-128, 721 GB at 1M ed
 all at once; the HIP TP kernels stream each chunk once.  Node-level pieces (BatchNorm, Gate,
 o3.Linear, symmetric contraction) are PyTorch ops on N-row tensors.
 """
-import ctypes
 import math
 import os
 
@@ -24,7 +23,7 @@ from torch.nn import functional as F
 
 from . import _lib, ops
 from . import o3
-from .ops import _p, _stream, check, _f32c, _need_cuda, _timed
+from .ops import _f32c, _need_cuda, _timed
 from .scatter import global_add_pool, global_mean_pool
 
 CHUNK_BYTES = int(os.environ.get("GMP_TP_CHUNK_BYTES", str(6 << 30)))
@@ -353,6 +352,8 @@ _TP_GRAPHS = []
 
 
 def tp_graph(edge_index, num_nodes):
+    if ops.compiling():
+        return TPGraph(edge_index, num_nodes)
     for t, ver, n, g in _TP_GRAPHS:
         if t is edge_index and ver == edge_index._version and n == num_nodes:
             return g
@@ -404,16 +405,27 @@ class TPPlan:
         for b, (m, (l, _)) in enumerate(irreps_out):
             self.desc.blk_off[b], self.desc.blk_mul[b], self.desc.blk_l[b] = oo[b], m, l
         self.blocks = [(oo[b], m) for b, (m, _) in enumerate(irreps_out)]
+        # plain-int copies (the autograd Functions read these, never the ctypes descriptor)
+        self.in_dim, self.out_dim = self.desc.in_dim, self.desc.out_dim
+        self.z_size = self.desc.z_size
+        d = self.desc  # the descriptor as torch.ops.gmp.tp_* take it (int[19])
+        self.desc_list = ([d.n_paths, d.in_dim, d.out_dim, d.sh_dim, d.weight_numel, d.z_size,
+                           d.n_blocks] + list(d.blk_off) + list(d.blk_mul) + list(d.blk_l))
         # node form: path p's z rows (mul1 * (2lo+1) floats) at z_off_p * (n_e + 1)
         self.z_regions = [(paths[k].z_off, ins["mul1"] * (2 * ins["lo"] + 1))
                           for k, ins in enumerate(self.instructions)]
         self.max_block_rows = max(w for _, w in self.z_regions)
         self._dev = {}
 
+    def host_tables(self):
+        """(path records as uint8 bytes, concatenated CG floats) on the host."""
+        return (torch.frombuffer(bytearray(bytes(self.paths_host)), dtype=torch.uint8),
+                self.cg_host.clone())
+
     def device_tables(self, device):
         if device not in self._dev:
-            raw = torch.frombuffer(bytearray(bytes(self.paths_host)), dtype=torch.uint8)
-            self._dev[device] = (raw.to(device), self.cg_host.to(device))
+            raw, cg = self.host_tables()
+            self._dev[device] = (raw.to(device), cg.to(device))
         return self._dev[device]
 
     def chunk_edges(self):
@@ -429,46 +441,41 @@ class TPConvFn(torch.autograd.Function):
     into the receiver rows.  Backward recomputes the chunk's weights."""
 
     @staticmethod
-    def forward(ctx, x, sh, rad, W1, b1, W2, b2, plan, graph):
-        lib = _lib.load()
+    def forward(ctx, x, sh, rad, W1, b1, W2, b2, plan, graph, paths_dev, cg_dev):
         x, sh, rad = _f32c(x), _f32c(sh), _f32c(rad)
         _need_cuda(x, sh, rad)
         dev = x.device
-        paths_dev, cg_dev = plan.device_tables(dev)
         N, E = graph.num_nodes, graph.num_edges
-        msg = torch.empty((E, plan.desc.out_dim), dtype=torch.float32, device=dev)
+        msg = torch.empty((E, plan.out_dim), dtype=torch.float32, device=dev)
         rad_s = ops.gather_rows(rad, graph.perm)  # radial features in receiver-sorted order
         ce = plan.chunk_edges()
+        tops = _lib.torch_ops()
         for c0 in range(0, E, ce):
             c1 = min(E, c0 + ce)
             with _timed("radial_gemm"):
                 a = torch.relu(torch.addmm(b1, rad_s[c0:c1], W1.t()))
                 Wc = torch.addmm(b2, a, W2.t())
             with _timed("tp_conv_fwd"):
-                check(lib.gmp_tp_conv_fwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
-                                              _p(cg_dev), cg_dev.numel(), _p(x), _p(sh), _p(Wc),
-                                              _p(graph.src_sorted), _p(graph.perm), c0, c1,
-                                              _p(msg), _stream()),
-                      "gmp_tp_conv_fwd_f32")
+                tops.tp_conv_fwd(plan.layout, plan.desc_list, paths_dev, cg_dev, x, sh, Wc,
+                                 graph.src_sorted, graph.perm, c0, c1, msg)
             del Wc, a
         # receiver sums over the sorted messages (deterministic, chunk-independent)
         out, _ = ops.segment_reduce(msg, graph.recv_csr, "sum", use_perm=False)
         del msg
-        ctx.plan, ctx.graph = plan, graph
+        ctx.plan, ctx.graph, ctx.tables = plan, graph, (paths_dev, cg_dev)
         ctx.save_for_backward(x, sh, rad_s, W1, b1, W2, b2)
         return out
 
     @staticmethod
     @once_differentiable
     def backward(ctx, gout):
-        lib = _lib.load()
         x, sh, rad_s, W1, b1, W2, b2 = ctx.saved_tensors
         plan, graph = ctx.plan, ctx.graph
-        paths_dev, cg_dev = plan.device_tables(x.device)
+        paths_dev, cg_dev = ctx.tables
         gout = _f32c(gout)
         N, E = graph.num_nodes, graph.num_edges
         f = dict(dtype=torch.float32, device=x.device)
-        dx_edge = torch.empty((E, plan.desc.in_dim), **f)
+        dx_edge = torch.empty((E, plan.in_dim), **f)
         dY = torch.empty((E, 9), **f)
         drad_s = torch.empty_like(rad_s)
         dW2 = torch.zeros_like(W2)
@@ -476,6 +483,7 @@ class TPConvFn(torch.autograd.Function):
         dW1 = torch.zeros_like(W1)
         db1 = torch.zeros_like(b1)
         ce = plan.chunk_edges()
+        tops = _lib.torch_ops()
         for c0 in range(0, E, ce):
             c1 = min(E, c0 + ce)
             r = rad_s[c0:c1]
@@ -483,14 +491,10 @@ class TPConvFn(torch.autograd.Function):
                 pre = torch.addmm(b1, r, W1.t())
                 a = torch.relu(pre)
                 Wc = torch.addmm(b2, a, W2.t())
-            dWc = torch.empty_like(Wc)
             with _timed("tp_conv_bwd"):
-                check(lib.gmp_tp_conv_bwd_f32(plan.layout, ctypes.byref(plan.desc), _p(paths_dev),
-                                              _p(cg_dev), cg_dev.numel(), _p(x), _p(sh), _p(Wc),
-                                              _p(graph.recv_sorted), _p(graph.src_sorted),
-                                              _p(graph.perm), c0, c1, _p(gout), _p(dWc),
-                                              _p(dx_edge), _p(dY), _stream()),
-                      "gmp_tp_conv_bwd_f32")
+                dWc = tops.tp_conv_bwd(plan.layout, plan.desc_list, paths_dev, cg_dev, x, sh, Wc,
+                                       graph.recv_sorted, graph.src_sorted, graph.perm, c0, c1,
+                                       gout, dx_edge, dY)
             del Wc
             with _timed("radial_gemm"):
                 dW2.addmm_(dWc.t(), a)
@@ -504,7 +508,7 @@ class TPConvFn(torch.autograd.Function):
         dx, _ = ops.segment_reduce(dx_edge, graph.src_csr, "sum")
         dsh = torch.empty_like(sh).index_copy_(0, graph.perm, dY)
         drad = torch.empty((E, rad_s.shape[1]), **f).index_copy_(0, graph.perm, drad_s)
-        return dx, dsh, drad, dW1, db1, dW2, db2, None, None
+        return dx, dsh, drad, dW1, db1, dW2, db2, None, None, None, None
 
 
 # Receiver chunk of the node form, in bytes of S (+ T) for the widest path.  Larger chunks give
@@ -515,11 +519,15 @@ NODE_CHUNK_BYTES = (int(os.environ["GMP_TP_NODE_CHUNK_BYTES"])
                     if "GMP_TP_NODE_CHUNK_BYTES" in os.environ else None)
 
 
+_HBM_BYTES = {}
+
+
 def node_chunk_bytes(device):
     if NODE_CHUNK_BYTES is not None:
         return NODE_CHUNK_BYTES
-    total = torch.cuda.get_device_properties(device).total_memory
-    return int(min(64 << 30, total // 4))
+    if device not in _HBM_BYTES:
+        _HBM_BYTES[device] = torch.cuda.get_device_properties(device).total_memory
+    return int(min(64 << 30, _HBM_BYTES[device] // 4))
 TP_MODE = os.environ.get("GMP_TP_MODE", "node")  # "node" (receiver-factorised) | "edge"
 
 
@@ -539,16 +547,6 @@ def node_form_ok(hidden):
 # Path GEMMs of the node form: "x3" = K7g (gmp_tpgemm.hip: bf16 MFMA over exact three-plane f32
 # splits; dW2p by the column-block split-plane outer sum), "torch" = the library f32 GEMMs.
 TP_GEMM = os.environ.get("GMP_TP_GEMM", "x3")
-# K7g's forward GEMM in the H2 form (two fp16 planes, three MFMA products per step;
-# gmp_tp_gemm_h2_f32) with per-row A scales from the S kernel's row-block maxima
-# (gmp_tp_node_outer_rmax_f32): off by default.  It is faster (9.1 vs 13.4 ms at the C4 lo = 2
-# shape, scripts/mb_tpgemm.py) but its operands carry 22 bits, not f32's 24: the C4 1M-edge
-# rotation-invariance check (test_mace_c4_full_size_properties, 1e-5 relative) measured
-# 2.9e-5 with it, so the f32-contract path stays three-plane.  The backward T GEMM is always
-# three-plane (bound by its T stores; the H2 widen kernel measured 13.7 vs 12.6 ms).
-TP_H2 = os.environ.get("GMP_TP_H2", "0") == "1"
-
-
 def _x3_ok(P, H):
     """Shapes K7g covers (every k range a multiple of the 32-deep MFMA step, mul_out <= 128) and
     where it pays: wide paths (mul1 mul_out >= 128 x 128, C4 MACE: 2.66 -> 2.41 s/step); on the
@@ -558,28 +556,10 @@ def _x3_ok(P, H):
             and P["mul1"] * P["mul_out"] >= 128 * 128)
 
 
-def _split_w2(lib, W2, b2, P, fwd, wmax=None):
+def _split_w2(W2, b2, P, fwd):
     """Three bf16 planes of path P's W2 / b2 block: forward (B = [W2p | b2p]^T as [w][(u, j) ++ u])
-    or backward (B = W2p as [(u, j)][w]) layout (torch.ops.gmp.tp_split_w2); with `wmax` (the
-    path block's max-|x| word, _w2_max) the two scaled fp16 planes of the H2 form."""
-    if wmax is not None:
-        return _lib.torch_ops().tp_split_w2_h2(W2, b2, P["w_off"], P["mul1"], P["mul_out"], fwd,
-                                               wmax)
+    or backward (B = W2p as [(u, j)][w]) layout (torch.ops.gmp.tp_split_w2)."""
     return _lib.torch_ops().tp_split_w2(W2, b2, P["w_off"], P["mul1"], P["mul_out"], fwd)
-
-
-def _amax_word(device):
-    return torch.zeros(1, dtype=torch.int32, device=device)
-
-
-def _w2_max(W2, b2, P):
-    """max |W2p|, |b2p| of path P as a device word (float bit pattern) for the H2 B scale."""
-    m1, mo, off = P["mul1"], P["mul_out"], P["w_off"]
-    w = _amax_word(W2.device)
-    ops_ = _lib.torch_ops()
-    ops_.absmax(W2[off:off + m1 * mo], w)
-    ops_.absmax(b2[off:off + m1 * mo], w)
-    return w
 
 
 class TPConvNodeFn(torch.autograd.Function):
@@ -595,69 +575,58 @@ class TPConvNodeFn(torch.autograd.Function):
     da = z.T per edge (gmp_tp_node_apply_f32); dW2 = G^T S, db2 = G^T Sb."""
 
     @staticmethod
-    def forward(ctx, x, sh, rad, W1, b1, W2, b2, plan, graph):
-        lib = _lib.load()
+    def forward(ctx, x, sh, rad, W1, b1, W2, b2, plan, graph, paths_dev, cg_dev):
         x, sh, rad = _f32c(x), _f32c(sh), _f32c(rad)
         _need_cuda(x, sh, rad)
         dev = x.device
         N, E = graph.num_nodes, graph.num_edges
         H = W1.shape[0]
-        out = torch.zeros((N, plan.desc.out_dim), dtype=torch.float32, device=dev)
+        tops = _lib.torch_ops()
+        out = torch.zeros((N, plan.out_dim), dtype=torch.float32, device=dev)
         rad_s = ops.gather_rows(rad, graph.perm)
         W2c, b2c = W2.contiguous(), b2.contiguous()
         x3 = [_x3_ok(P, H) for P in plan.instructions]
         W2x = [None if ok else _w2_path(W2, b2, P) for P, ok in zip(plan.instructions, x3)]
         Bfs = [None] * len(x3)
-        wmaxs = [_w2_max(W2c, b2c, P) if (ok and TP_H2 and P["mul1"] % 16 == 0) else None
-                 for P, ok in zip(plan.instructions, x3)]
-        for n0, n1, e0, e1, eoff, a, zbuf, _ in _node_chunks(lib, plan, graph, x, sh, rad_s,
-                                                             W1, b1):
+        for n0, n1, e0, e1, eoff, a, zbuf, _ in _node_chunks(plan, graph, x, sh, rad_s, W1, b1,
+                                                             paths_dev, cg_dev):
             c, ne = n1 - n0, e1 - e0
             for i, (P, (zoff, w)) in enumerate(zip(plan.instructions, plan.z_regions)):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                rmax = (torch.empty(c * (w // 16), dtype=torch.float32, device=dev)
-                        if wmaxs[i] is not None else None)
-                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a, rmax)
+                S, Sb = _node_outer(eoff, Zp, a, w)
                 blk = plan.blocks[P["io"]]
                 if x3[i]:
                     # out[n, blk + w' d3 + k] += [S | Sb][(n, k), :] [W2p ; b2p][:, w'] (K7g)
                     if Bfs[i] is None:
-                        Bfs[i] = _split_w2(lib, W2c, b2c, P, True, wmaxs[i])
+                        Bfs[i] = _split_w2(W2c, b2c, P, True)
                     K1 = m1 * H
                     with _timed("tp_node_W"):
-                        if rmax is not None:
-                            _lib.torch_ops().tp_gemm_h2(
-                                S.view(c * d3, K1), K1, Sb.view(c * d3, m1), m1, Bfs[i], K1 + m1,
-                                mo, out, n0 * out.shape[1] + blk[0], d3, out.shape[1], 1, d3,
-                                True, rmax, wmaxs[i])
-                        else:
-                            _lib.torch_ops().tp_gemm_x3(
-                                S.view(c * d3, K1), K1, Sb.view(c * d3, m1), m1, Bfs[i], K1 + m1,
-                                mo, out, n0 * out.shape[1] + blk[0], d3, out.shape[1], 1, d3,
-                                True)
+                        tops.tp_gemm_x3(S.view(c * d3, K1), K1, Sb.view(c * d3, m1), m1, Bfs[i],
+                                        K1 + m1, mo, out, n0 * out.shape[1] + blk[0], d3,
+                                        out.shape[1], 1, d3, True)
                     continue
                 W2p, b2p = W2x[i]
                 with _timed("tp_node_W"):
                     op = torch.addmm(Sb.view(c * d3, -1).mm(b2p), S.view(c * d3, -1), W2p)
                 out[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, blk[1], d3).add_(
                     op.view(c, d3, -1).transpose(1, 2))
-        ctx.plan, ctx.graph = plan, graph
+        ctx.plan, ctx.graph, ctx.tables = plan, graph, (paths_dev, cg_dev)
         ctx.save_for_backward(x, sh, rad_s, W1, b1, W2, b2)
         return out
 
     @staticmethod
     @once_differentiable
     def backward(ctx, gout):
-        lib = _lib.load()
         x, sh, rad_s, W1, b1, W2, b2 = ctx.saved_tensors
         plan, graph = ctx.plan, ctx.graph
-        paths_dev, cg_dev = plan.device_tables(x.device)
+        paths_dev, cg_dev = ctx.tables
+        tops = _lib.torch_ops()
         gout = _f32c(gout)
         N, E = graph.num_nodes, graph.num_edges
         H = W1.shape[0]
         f = dict(dtype=torch.float32, device=x.device)
-        dx_edge = torch.empty((E, plan.desc.in_dim), **f)
+        dx_edge = torch.empty((E, plan.in_dim), **f)
         dY = torch.empty((E, 9), **f)
         drad_s = torch.empty_like(rad_s)
         dW1, db1 = torch.zeros_like(W1), torch.zeros_like(b1)
@@ -666,10 +635,9 @@ class TPConvNodeFn(torch.autograd.Function):
         W2x = [_w2_path(W2, b2, P) for P in plan.instructions]
         dW2x = [(torch.zeros_like(wp), torch.zeros_like(bp)) for wp, bp in W2x]
         Bts = [None] * len(x3)
-        wmaxs = [None] * len(x3)  # the T GEMM stays three-plane (see TP_H2)
         first = True
-        for n0, n1, e0, e1, eoff, a, zbuf, pre in _node_chunks(lib, plan, graph, x, sh, rad_s,
-                                                               W1, b1):
+        for n0, n1, e0, e1, eoff, a, zbuf, pre in _node_chunks(plan, graph, x, sh, rad_s, W1,
+                                                               b1, paths_dev, cg_dev):
             c, ne = n1 - n0, e1 - e0
             dzbuf = torch.empty_like(zbuf)
             da = torch.zeros((ne, H), **f)
@@ -678,14 +646,14 @@ class TPConvNodeFn(torch.autograd.Function):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 blk = plan.blocks[P["io"]]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                S, Sb = _node_outer(lib, c, w, H, eoff, Zp, a)
+                S, Sb = _node_outer(eoff, Zp, a, w)
                 G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
                 G = G.reshape(c * d3, mo).contiguous()  # (d3 = 1: reshape alone is a view)
                 if x3[i]:
                     K1 = m1 * H
                     with _timed("tp_node_dW"):
                         # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
-                        part = _lib.torch_ops().outer_sum_cols(S.view(c * d3, K1), G)
+                        part = tops.outer_sum_cols(S.view(c * d3, K1), G)
                         if first:
                             dW2p.copy_(part)
                         else:
@@ -693,15 +661,10 @@ class TPConvNodeFn(torch.autograd.Function):
                         db2p.addmm_(Sb.view(c * d3, -1).t(), G)
                     del S, Sb
                     if Bts[i] is None:
-                        Bts[i] = _split_w2(lib, W2c, b2c, P, False, wmaxs[i])
+                        Bts[i] = _split_w2(W2c, b2c, P, False)
                     with _timed("tp_node_W"):
                         # T[(n, k), (u, j)] = sum_w G[(n, k), w] W2p[(u, j), w]
-                        if wmaxs[i] is not None:
-                            gmax = _amax_word(G.device)
-                            _lib.torch_ops().absmax(G, gmax)
-                            T = _lib.torch_ops().tp_gemm_h2_widen(G, Bts[i], K1, gmax, wmaxs[i])
-                        else:
-                            T = _lib.torch_ops().tp_gemm_x3_widen(G, Bts[i], K1)
+                        T = tops.tp_gemm_x3_widen(G, Bts[i], K1)
                         Tb = G.mm(b2p.t())
                 else:
                     with _timed("tp_node_dW"):
@@ -713,16 +676,14 @@ class TPConvNodeFn(torch.autograd.Function):
                         Tb = G.mm(b2p.t())
                 dZp = dzbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 with _timed("tp_node_dZA"):
-                    _lib.torch_ops().tp_node_apply(eoff, Zp, a, T, Tb.contiguous(), da, dZp)
+                    tops.tp_node_apply(eoff, Zp, a, T, Tb.contiguous(), da, dZp)
                 del T, Tb
             first = False
             with _timed("tp_node_edge_bwd"):
-                check(lib.gmp_tp_edge_z_bwd_f32(ctypes.byref(plan.desc), _p(paths_dev),
-                                                _p(cg_dev), cg_dev.numel(), _p(x), _p(sh),
-                                                _p(graph.src_sorted), _p(graph.perm), e0, e1,
-                                                _p(dzbuf), _p(dx_edge[e0:e1]), _p(dY[e0:e1]),
-                                                _stream()),
-                      "gmp_tp_edge_z_bwd_f32")
+                dxc, dYc = tops.tp_edge_z_bwd(plan.desc_list, paths_dev, cg_dev, x, sh,
+                                              graph.src_sorted, graph.perm, e0, e1, dzbuf)
+                dx_edge[e0:e1] = dxc
+                dY[e0:e1] = dYc
             dpre = da * (pre > 0)
             r = rad_s[e0:e1]
             dW1.addmm_(dpre.t(), r)
@@ -736,37 +697,33 @@ class TPConvNodeFn(torch.autograd.Function):
         dx, _ = ops.segment_reduce(dx_edge, graph.src_csr, "sum")
         dsh = torch.empty_like(sh).index_copy_(0, graph.perm, dY)
         drad = torch.empty((E, rad_s.shape[1]), **f).index_copy_(0, graph.perm, drad_s)
-        return dx, dsh, drad, dW1, db1, dW2, db2, None, None
+        return dx, dsh, drad, dW1, db1, dW2, db2, None, None, None, None
 
 
-def _node_outer(lib, c, w, H, eoff, Zp, a, rmax=None):
+def _node_outer(eoff, Zp, a, w):
     with _timed("tp_node_S"):
-        return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w, rmax)
+        return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w)
 
 
-def _node_chunks(lib, plan, graph, x, sh, rad_s, W1, b1):
+def _node_chunks(plan, graph, x, sh, rad_s, W1, b1, paths_dev, cg_dev):
     """Receiver chunks with their chunk-local edge offsets, hidden radial rows a and z rows
-    (recomputed per pass)."""
-    paths_dev, cg_dev = plan.device_tables(x.device)
+    (recomputed per pass).  One chunk (the 1M-edge configs) needs no host copy of rowptr."""
     if graph.num_edges == 0:
         return
     H = W1.shape[0]
     per_node = plan.max_block_rows * H * 4 * 2  # S (+ T) of the widest path
     npc = max(1, min(65535, node_chunk_bytes(x.device) // per_node))
-    for n0, n1, e0, e1 in graph.node_chunks(npc):
+    chunks = ([(0, graph.num_nodes, 0, graph.num_edges)] if npc >= graph.num_nodes
+              else graph.node_chunks(npc))
+    for n0, n1, e0, e1 in chunks:
         if e1 == e0:
             continue
-        ne = e1 - e0
         eoff = graph.rowptr[n0:n1 + 1] - e0
         with _timed("tp_node_prep"):
             pre = torch.addmm(b1, rad_s[e0:e1], W1.t())
             a = torch.relu(pre)
-            zbuf = torch.empty(((ne + 1) * plan.desc.z_size,), dtype=torch.float32,
-                               device=x.device)
-            check(lib.gmp_tp_edge_z_f32(ctypes.byref(plan.desc), _p(paths_dev), _p(cg_dev),
-                                        cg_dev.numel(), _p(x), _p(sh), _p(graph.src_sorted),
-                                        _p(graph.perm), e0, e1, _p(zbuf), _stream()),
-                  "gmp_tp_edge_z_f32")
+            zbuf = _lib.torch_ops().tp_edge_z(plan.desc_list, paths_dev, cg_dev, x, sh,
+                                              graph.src_sorted, graph.perm, e0, e1)
         yield n0, n1, e0, e1, eoff, a, zbuf, pre
 
 
@@ -788,6 +745,11 @@ class TensorProductConvLayer(nn.Module):
         else:
             self.gate = None
         self.plan = TPPlan(self.in_irreps, self.sh_irreps, self.out_irreps)
+        # the plan's constant tables as (non-persistent) buffers: they follow the module's
+        # .to(device), and torch.compile sees them as module state
+        paths, cg = self.plan.host_tables()
+        self.register_buffer("_tp_paths", paths, persistent=False)
+        self.register_buffer("_tp_cg", cg, persistent=False)
         self.fc = nn.Sequential(nn.Linear(edge_feats_dim, mlp_dim), nn.ReLU(),
                                 nn.Linear(mlp_dim, self.plan.weight_numel))
         self.batch_norm = BatchNorm(self.out_irreps) if batch_norm else None
@@ -796,8 +758,11 @@ class TensorProductConvLayer(nn.Module):
         graph = tp_graph(edge_index, node_attr.shape[0])
         fn = TPConvNodeFn if (TP_MODE == "node" and node_form_ok(self.fc[0].out_features)) \
             else TPConvFn
+        paths, cg = self._tp_paths, self._tp_cg
+        if paths.device != node_attr.device or cg.dtype != torch.float32:
+            paths, cg = self.plan.device_tables(node_attr.device)
         out = fn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight, self.fc[0].bias,
-                       self.fc[2].weight, self.fc[2].bias, self.plan, graph)
+                       self.fc[2].weight, self.fc[2].bias, self.plan, graph, paths, cg)
         if self.aggr == "mean":
             out = out / graph.recv_csr.counts().clamp(min=1).unsqueeze(1).to(out.dtype)
         elif self.aggr not in ("add", "sum"):

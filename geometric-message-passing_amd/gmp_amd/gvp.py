@@ -20,7 +20,6 @@ from torch import nn
 from torch.nn import functional as F
 
 from . import _lib, ops
-from ._lib import check
 from .message_passing import MessagePassing
 from .scatter import global_add_pool, global_mean_pool
 
@@ -159,10 +158,7 @@ def _diag3(M, a, b):
 
 
 def _osum(A, B):
-    r = ops.edge_outer_sum_rect(A, B)
-    if r is None:
-        return A.t().mm(B), A.sum(0)
-    return r
+    return ops.edge_outer_sum_rect(A, B)
 
 
 class GvpLayerFn(torch.autograd.Function):
@@ -170,17 +166,11 @@ class GvpLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, s, v, Ws, bs, Wsv, bsv, Wh, Wv, relu):
-        lib = _lib.load()
         s, v = ops._f32c(s), ops._f32c(v)
         ops._need_cuda(s, v)
-        E = s.shape[0]
         W = [ops._f32c(t) for t in (Ws, bs, Wsv, bsv, Wh, Wv)]
-        s_out = torch.empty_like(s)
-        v_out = torch.empty_like(v)
         with ops._timed("gvp_layer_fwd"):
-            check(lib.gmp_gvp_layer_fwd_f32(E, int(relu), ops._p(s), ops._p(v),
-                                            *[ops._p(t) for t in W], ops._p(s_out),
-                                            ops._p(v_out), ops._stream()), "gmp_gvp_layer_fwd_f32")
+            s_out, v_out = _lib.torch_ops().gvp_layer_fwd(s, v, W, bool(relu))
         ctx.relu = relu
         ctx.save_for_backward(s, v, *W)
         return s_out, v_out
@@ -188,31 +178,19 @@ class GvpLayerFn(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, ds, dv):
-        lib = _lib.load()
         s, v, *W = ctx.saved_tensors
         E = s.shape[0]
         ds = ops._f32c(ds) if ds is not None else torch.zeros_like(s)
         dv = ops._f32c(dv) if dv is not None else torch.zeros_like(v)
         f = dict(dtype=torch.float32, device=s.device)
-        ds_in, dv_in = torch.empty_like(s), torch.empty_like(v)
-        dspre, spre = torch.empty((E, 128), **f), torch.empty((E, 128), **f)
-        dgate, vn = torch.empty((E, 16), **f), torch.empty((E, 16), **f)
-        vh, dvpre, dvh = (torch.empty((E, 48), **f) for _ in range(3))
         with ops._timed("gvp_layer_bwd"):
-            check(lib.gmp_gvp_layer_bwd_f32(E, int(ctx.relu), ops._p(s), ops._p(v),
-                                            *[ops._p(t) for t in W], ops._p(ds), ops._p(dv),
-                                            ops._p(ds_in), ops._p(dv_in), ops._p(dspre),
-                                            ops._p(spre), ops._p(dgate), ops._p(vn), ops._p(vh),
-                                            ops._p(dvpre), ops._p(dvh), ops._stream()),
-                  "gmp_gvp_layer_bwd_f32")
+            ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh = _lib.torch_ops().gvp_layer_bwd(
+                s, v, W, ds, dv, bool(ctx.relu))
         # weight gradients (edge outer sums) on the side stream, deferred to the end of backward
         with ops.side_work(dspre, s, vn, dgate, spre, dvh, v, dvpre, vh) as sw:
-            # dWs = dspre^T [s | vn]: one pass over dspre when the split-plane kernel applies
+            # dWs = dspre^T [s | vn]: one pass over dspre where the split-plane kernel applies
             dWs, dbs = torch.empty((128, 144), **f), torch.empty(128, **f)
-            if not ops.outer_sum_into2(dspre, s.view(E, 128), vn, dWs, dbs):
-                dWs_s, dbs = _osum(dspre, s.view(E, 128))
-                dWs_v, _ = _osum(dspre, vn)
-                dWs = torch.cat([dWs_s, dWs_v], 1)
+            ops.outer_sum_into2(dspre, s.view(E, 128), vn, dWs, dbs)
             dWsv, dbsv = _osum(dgate, spre)
             dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
             dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
@@ -228,22 +206,15 @@ class GvpMsg0Fn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, P, Q, es, ev, Ws0, b, Wv, Wsv, bsv, Wh0, send_csr, recv_csr, ei):
-        lib = _lib.load()
         P, Q, es, ev = (ops._f32c(t) for t in (P, Q, es, ev))
         pad = torch.nn.functional.pad
         vi = Wv.shape[1]  # 2 vi + ve = 33
         W = [ops._f32c(t) for t in (Ws0[:, 128:160], pad(Ws0[:, 288:288 + vi], (0, 48 - vi)),
                                     b, pad(Wv, (0, 48 - vi)), Wsv, bsv,
                                     pad(Wh0[:, 16], (0, 48 - Wh0.shape[0])))]
-        E = es.shape[0]
         send, recv = ei[0].contiguous(), ei[1].contiguous()
-        s_out = torch.empty((E, 128), dtype=torch.float32, device=P.device)
-        v_out = torch.empty((E, 16, 3), dtype=torch.float32, device=P.device)
         with ops._timed("gvp_msg0_fwd"):
-            check(lib.gmp_gvp_msg0_fwd_f32(E, ops._p(send), ops._p(recv), ops._p(P), ops._p(Q),
-                                           ops._p(es), ops._p(ev), *[ops._p(t) for t in W],
-                                           ops._p(s_out), ops._p(v_out), ops._stream()),
-                  "gmp_gvp_msg0_fwd_f32")
+            s_out, v_out = _lib.torch_ops().gvp_msg0_fwd(send, recv, P, Q, es, ev, W)
         ctx.csrs = (send_csr, recv_csr)
         ctx.leaves = (Ws0, b, Wv, Wsv, bsv, Wh0)
         ctx.save_for_backward(P, Q, es, ev, send, recv, *W)
@@ -252,7 +223,6 @@ class GvpMsg0Fn(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, ds, dv):
-        lib = _lib.load()
         P, Q, es, ev, send, recv, *W = ctx.saved_tensors
         send_csr, recv_csr = ctx.csrs
         Ws0, b, Wv, Wsv, bsv, Wh0 = ctx.leaves
@@ -260,28 +230,16 @@ class GvpMsg0Fn(torch.autograd.Function):
         ds = ops._f32c(ds) if ds is not None else torch.zeros((E, 128), device=P.device)
         dv = ops._f32c(dv) if dv is not None else torch.zeros((E, 16, 3), device=P.device)
         f = dict(dtype=torch.float32, device=P.device)
-        dspre, spre = torch.empty((E, 128), **f), torch.empty((E, 128), **f)
-        dgate, vn = torch.empty((E, 16), **f), torch.empty((E, 48), **f)
-        vh, dvh = torch.empty((E, 144), **f), torch.empty((E, 144), **f)
-        dvpre = torch.empty((E, 48), **f)
-        des, dev = torch.empty((E, 32), **f), torch.empty((E, 3), **f)
         with ops._timed("gvp_msg0_bwd"):
-            check(lib.gmp_gvp_msg0_bwd_f32(E, ops._p(send), ops._p(recv), ops._p(P), ops._p(Q),
-                                           ops._p(es), ops._p(ev), *[ops._p(t) for t in W],
-                                           ops._p(ds), ops._p(dv), ops._p(dspre), ops._p(spre),
-                                           ops._p(dgate), ops._p(vn), ops._p(vh), ops._p(dvpre),
-                                           ops._p(dvh), ops._p(des), ops._p(dev), ops._stream()),
-                  "gmp_gvp_msg0_bwd_f32")
+            dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev = _lib.torch_ops().gvp_msg0_bwd(
+                send, recv, P, Q, es, ev, W, ds, dv)
         # weight gradients (edge outer sums) on the side stream, as full-size leaf gradients
         with ops.side_work(dspre, es, vn, dgate, spre, dvpre, vh, ev, dvh) as sw:
             vi = Wv.shape[1]
             # [dWe | dWn] = dspre^T [es | vn]: one pass over dspre when the split path applies
             Cen, db = torch.empty((128, 80), **f), torch.empty(128, **f)
-            if ops.outer_sum_into2(dspre, es, vn, Cen, db):
-                dWe, dWn = Cen[:, :32], Cen[:, 32:]
-            else:
-                dWe, db = _osum(dspre, es)
-                dWn, _ = _osum(dspre, vn)
+            ops.outer_sum_into2(dspre, es, vn, Cen, db)
+            dWe, dWn = Cen[:, :32], Cen[:, 32:]
             dWsv, dbsv = _osum(dgate, spre)
             dWv = _diag3(_osum(dvpre, vh)[0], 16, 48)
             M, _ = _osum(torch.nn.functional.pad(ev, (0, 13)), dvh)  # (16, 144): rows x = 0..2

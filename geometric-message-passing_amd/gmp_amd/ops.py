@@ -121,6 +121,8 @@ def _tkey(t):
 
 def get_csr(index, n_seg, payload=None):
     """Cached CSR for `index` (keyed on storage/geometry/version; holds a strong ref)."""
+    if compiling():
+        return CSR(index, n_seg, payload)
     key = (_tkey(index), int(n_seg), _tkey(payload))
     for k, (kk, _, _, csr) in enumerate(_CSR_CACHE):
         if kk == key:
@@ -153,107 +155,48 @@ def segment_reduce(src2d, csr, reduce="sum", use_perm=True):
     return out, (argmax if reduce == "max" else None)
 
 
-def edge_outer_sum(A, B, with_colsum=True):
-    """(A^T B, colsum(A)) over the edge dimension (gmp_edge_outer_sum_f32), deterministic."""
-    lib = _lib.load()
+def edge_outer_sum(A, B):
+    """(A^T B, colsum(A)) over the edge dimension (torch.ops.gmp.edge_outer_sum), deterministic."""
     A, B = _f32c(A), _f32c(B)
     _need_cuda(A, B)
-    K, d = A.shape
-    C = torch.empty((d, d), dtype=torch.float32, device=A.device)
-    cs = torch.empty(d, dtype=torch.float32, device=A.device) if with_colsum else None
-    ws_bytes = lib.gmp_edge_outer_sum_workspace_size(K, d)
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
     with _timed("edge_outer_sum"):
-        check(lib.gmp_edge_outer_sum_f32(K, d, _p(A), _p(B), _p(C), _p(cs), _p(ws), ws_bytes,
-                                         _stream()), "gmp_edge_outer_sum_f32")
-    return C, cs
+        return _lib.torch_ops().edge_outer_sum(A, B)
 
 
 def edge_outer_sum_act(A, X, w, b, act, amax=None):
     """(A^T act(X * w + b), colsum(A)) with the activation applied at load time
-    (gmp_edge_outer_sum_act_f32): the EGNN y1 / m weight-gradient operands from x_hat.  With
-    `amax` (device word, max |A| as float bits; X LayerNorm rows) the HF form
-    (gmp_edge_outer_sum_act_hf_f32: scaled fp16 planes, three products)."""
-    lib = _lib.load()
+    (torch.ops.gmp.edge_outer_sum_act): the EGNN y1 / m weight-gradient operands from x_hat.
+    With `amax` (device word, max |A| as float bits; X LayerNorm rows) the HF form (scaled fp16
+    planes, three products)."""
     A, X, w, b = _f32c(A), _f32c(X), _f32c(w), _f32c(b)
     _need_cuda(A, X, w, b)
-    K, d = A.shape
-    C = torch.empty((d, d), dtype=torch.float32, device=A.device)
-    cs = torch.empty(d, dtype=torch.float32, device=A.device)
-    ws_bytes = lib.gmp_edge_outer_sum_workspace_size(K, d)
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
     with _timed("edge_outer_sum"):
-        if amax is not None:
-            check(lib.gmp_edge_outer_sum_act_hf_f32(K, d, _p(A), _p(X), _p(w), _p(b),
-                                                    _lib.ACT[act], _p(amax), _p(C), _p(cs),
-                                                    _p(ws), ws_bytes, _stream()),
-                  "gmp_edge_outer_sum_act_hf_f32")
-        else:
-            check(lib.gmp_edge_outer_sum_act_f32(K, d, _p(A), _p(X), _p(w), _p(b),
-                                                 _lib.ACT[act], _p(C), _p(cs), _p(ws), ws_bytes,
-                                                 _stream()),
-                  "gmp_edge_outer_sum_act_f32")
-    return C, cs
-
-
-def _rows_view_ok(t):
-    """(K, m) fp32 CUDA view usable as a strided outer-sum operand: unit column stride, row
-    stride a multiple of 4 floats, 16-byte aligned base."""
-    return (t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
-            and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0)
+        return _lib.torch_ops().edge_outer_sum_act(A, X, w, b, _lib.ACT[act], amax)
 
 
 def outer_sum_into(A, B, C, colsum=None, act=None, w=None, b=None):
-    """C[:] = A^T act(B) over the rows (gmp_edge_outer_sum_ex_f32), colsum[:] = colsum(A).
-    A (K, m), B (K, n) and C (m, n) may be strided views (row strides; e.g. column blocks of a
-    wider tensor or parameter gradient).  Returns False when the shape is outside the kernels'
-    tile buckets (caller falls back)."""
-    lib = _lib.load()
+    """C[:] = A^T act(B) over the rows (torch.ops.gmp.edge_outer_sum_ex), colsum[:] =
+    colsum(A).  A (K, m), B (K, n) and C (m, n) may be strided views (unit column stride; e.g.
+    column blocks of a wider tensor or parameter gradient).  Shapes outside the kernels' tile
+    buckets run the library GEMM inside the op.  Returns True when the outer-sum kernels ran."""
     _need_cuda(A, B, C)
-    K, m = A.shape
-    n = B.shape[1]
-    if not (_rows_view_ok(A) and _rows_view_ok(B) and C.stride(1) == 1):
-        raise _lib.GmpError("outer_sum_into: operands need unit column stride, 4-float aligned "
-                            "row strides and 16-byte aligned bases")
     a = -1 if act is None else _lib.ACT[act]
-    ws_bytes = lib.gmp_edge_outer_sum_ex_workspace_size(K, m, n)
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
     with _timed("edge_outer_sum"):
-        rc = lib.gmp_edge_outer_sum_ex_f32(K, m, n, _p(A), A.stride(0), _p(B), B.stride(0), a,
-                                           _p(w), _p(b), _p(C), C.stride(0), _p(colsum), _p(ws),
-                                           ws_bytes, _stream())
-    if rc == _lib.GMP_ERR_UNSUPPORTED:
-        return False
-    check(rc, "gmp_edge_outer_sum_ex_f32")
-    return True
+        return _lib.torch_ops().edge_outer_sum_ex(A, B, C, colsum, a, w, b) == 0
 
 
 def outer_sum_into2(A, B1, B2, C, colsum=None):
-    """C[:] = A^T [B1 | B2] (and colsum(A)) in one pass over A (gmp_edge_outer_sum_ex2_f32);
-    False when the split-plane path does not apply (the caller makes two calls)."""
-    lib = _lib.load()
+    """C[:] = A^T [B1 | B2] (and colsum(A)) in one pass over A where the split-plane kernel
+    applies (returns True), else as two products inside the op (returns False)."""
     _need_cuda(A, B1, B2, C)
-    K, m = A.shape
-    n1, n2 = B1.shape[1], B2.shape[1]
-    if not all(_rows_view_ok(t) for t in (A, B1, B2)) or C.stride(1) != 1:
-        return False
-    ws_bytes = lib.gmp_edge_outer_sum_rect_workspace_size(K, m, n1 + n2)
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=A.device)
     with _timed("edge_outer_sum"):
-        rc = lib.gmp_edge_outer_sum_ex2_f32(K, m, n1, n2, _p(A), A.stride(0), _p(B1), B1.stride(0),
-                                            _p(B2), B2.stride(0), _p(C), C.stride(0),
-                                            _p(colsum), _p(ws), ws_bytes, _stream())
-    if rc == _lib.GMP_ERR_UNSUPPORTED:
-        return False
-    check(rc, "gmp_edge_outer_sum_ex2_f32")
-    return True
+        return _lib.torch_ops().edge_outer_sum_ex2(A, B1, B2, C, colsum) == 0
 
 
 def edge_outer_sum_rect(A, B):
     """(A^T B, colsum(A)) over the rows (edges / nodes) for any widths, deterministic: columns
     zero-padded to multiples of 16 when needed, wide operands processed as <= 128 x 144 column
-    blocks read in place (strided) and written into their block of C.  None when a block shape
-    is outside the kernels' buckets."""
+    blocks read in place (strided) and written into their block of C."""
     A, B = _f32c(A), _f32c(B)
     _need_cuda(A, B)
     m, n = A.shape[1], B.shape[1]
@@ -267,10 +210,8 @@ def edge_outer_sum_rect(A, B):
     bn = 144 if np_ <= 144 else 128
     for m0 in range(0, mp, 128):
         for n0 in range(0, np_, bn):
-            ok = outer_sum_into(A[:, m0:m0 + 128], B[:, n0:n0 + bn], C[m0:m0 + 128, n0:n0 + bn],
-                                cs[m0:m0 + 128] if n0 == 0 else None)
-            if not ok:
-                return None
+            outer_sum_into(A[:, m0:m0 + 128], B[:, n0:n0 + bn], C[m0:m0 + 128, n0:n0 + bn],
+                           cs[m0:m0 + 128] if n0 == 0 else None)
     if (mp, np_) != (m, n):
         return C[:m, :n].contiguous(), cs[:m]
     return C, cs
@@ -343,17 +284,27 @@ def _engine_accumulates(p):
 SIDE_GRID_CAP = int(os.environ.get("GMP_SIDE_GRID_CAP", "0") or 0)
 
 
+def compiling():
+    """True while torch.compile (dynamo) traces: the ops then run inline on the current stream,
+    without the per-graph caches, side streams or end-of-backward callbacks of eager mode."""
+    return torch.compiler.is_compiling()
+
+
 class side_work:
     """with side_work(used_tensors) as sw: ... launches on the side stream after everything
-    already queued on the current stream; sw.defer(param, grad) hands a result to the end-of-
-    backward accumulation (or, when deferral is off, sw.join() makes the current stream wait).
-    tail=True: nothing on the critical path follows (no split-K grid cap)."""
+    already queued on the current stream; sw.deliver(...) hands each result to the end-of-
+    backward accumulation (deferred leaf gradients) or back through autograd (after joining the
+    streams).  tail=True: nothing on the critical path follows (no split-K grid cap).  Under
+    torch.compile the work runs inline and every gradient goes back through autograd."""
 
     def __init__(self, *used, tail=False):
         self.used = [t for t in used if t is not None]
         self.cap = 0 if tail else SIDE_GRID_CAP
+        self.inline = compiling()
 
     def __enter__(self):
+        if self.inline:
+            return self
         self.main = torch.cuda.current_stream()
         self.side = _side_stream(self.main.device)
         self.side.wait_stream(self.main)
@@ -363,6 +314,8 @@ class side_work:
         return self
 
     def __exit__(self, *exc):
+        if self.inline:
+            return False
         if self.prev_cap is not None:
             _lib.load().gmp_wgrad_set_grid_cap(self.prev_cap)
         self.ctx.__exit__(*exc)
@@ -386,6 +339,9 @@ class side_work:
     def deliver(self, needs_input_grad, first, targets, grads):
         """Per parameter: defer the gradient (leaf parameter) or hand it back through autograd
         (after joining the streams).  needs_input_grad[first + i] belongs to targets[i]."""
+        if self.inline:
+            return tuple(gr if needs_input_grad[first + i] else None
+                         for i, gr in enumerate(grads))
         out, joined, deferred = [], False, False
         accum = None  # does this backward pass accumulate into .grad (checked once per call)
         for i, (p, gr) in enumerate(zip(targets, grads)):
@@ -399,7 +355,7 @@ class side_work:
                 out.append(None)
             else:
                 if not joined:
-                    self.join(*grads)
+                    self.join(*[g for g in grads if g is not None])
                     joined = True
                 out.append(gr)
         if not (joined or deferred):
@@ -437,17 +393,9 @@ class EdgeLinearFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[1] or (b is not None and ctx.needs_input_grad[2])
         if not need_w:
             return dx, None, None
-        defer = deferrable(W) and (b is None or deferrable(b)) and _engine_accumulates(W)
         with side_work(g, x) as sw:
-            r = edge_outer_sum_rect(g, x)
-            dW, db = r if r is not None else (g.t().mm(x), g.sum(0))
-        if defer:
-            sw.defer(W, dW)
-            if b is not None:
-                sw.defer(b, db)
-            return dx, None, None
-        sw.join(dW, db)
-        return dx, dW, (db if b is not None else None)
+            dW, db = edge_outer_sum_rect(g, x)
+        return (dx,) + sw.deliver(ctx.needs_input_grad, 1, (W, b), (dW, db))
 
 
 class SplitLinearFn(torch.autograd.Function):
@@ -475,22 +423,12 @@ class SplitLinearFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[2] or (b is not None and ctx.needs_input_grad[3])
         if not need_w:
             return dxa, dxb, None, None
-        defer = deferrable(W) and (b is None or deferrable(b)) and _engine_accumulates(W)
         with side_work(g, xa, xb) as sw:
             dW = torch.empty_like(W)
             db = torch.empty(W.shape[0], dtype=W.dtype, device=W.device)
-            ok = (outer_sum_into(g, xa, dW[:, :da], db)
-                  and outer_sum_into(g, xb, dW[:, da:], None))
-            if not ok:
-                dW = torch.cat([g.t().mm(xa), g.t().mm(xb)], 1)
-                db = g.sum(0)
-        if defer:
-            sw.defer(W, dW)
-            if b is not None:
-                sw.defer(b, db)
-            return dxa, dxb, None, None
-        sw.join(dW, db)
-        return dxa, dxb, dW, (db if b is not None else None)
+            outer_sum_into(g, xa, dW[:, :da], db)
+            outer_sum_into(g, xb, dW[:, da:], None)
+        return (dxa, dxb) + sw.deliver(ctx.needs_input_grad, 2, (W, b), (dW, db))
 
 
 def split_linear(xa, xb, W, b=None):
@@ -630,6 +568,8 @@ _CHECKED_CSR = []  # CSRs whose build-time range flag was already read (once per
 
 def _cfconv_csr(index, n):
     csr = get_csr(index, n)
+    if compiling():
+        return csr
     if not any(c is csr for c in _CHECKED_CSR):
         csr.check_range()  # one host sync per new graph, as torch_scatter raises IndexError
         _CHECKED_CSR.insert(0, csr)
@@ -803,6 +743,8 @@ _EGNN_GRAPHS = []
 
 
 def egnn_graph(edge_index, num_nodes):
+    if compiling():
+        return EgnnGraph(edge_index, num_nodes)
     for k, (t, ver, n, g) in enumerate(_EGNN_GRAPHS):
         if t is edge_index and ver == edge_index._version and n == num_nodes:
             return g
@@ -840,7 +782,6 @@ class EgnnMessageFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, pos, graph, act, msg_mean, eps, W1, b1, ln1w, ln1b, W2, b2, ln2w, ln2b,
                 W3, b3, ln3w, ln3b, w4, b4):
-        lib = _lib.load()
         h, pos = _f32c(h), _f32c(pos)
         _need_cuda(h, pos, W1)
         N, d = h.shape
@@ -862,7 +803,6 @@ class EgnnMessageFn(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, g_m, g_p):
-        lib = _lib.load()
         h, pos, xhat, rstd, W1, *params = ctx.saved_tensors
         graph = ctx.graph
         N, d = ctx.N, xhat.shape[2]

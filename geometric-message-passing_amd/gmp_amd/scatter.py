@@ -8,6 +8,9 @@ scatter(reduce="max"/"min") returns values, scatter_max / scatter_min return (ou
 arg = src.size(dim) for empty rows (torch_scatter's convention).  Reductions are deterministic
 segmented sums over a stable receiver-sorted CSR (torch.ops.gmp.csr_build +
 torch.ops.gmp.segment_reduce), not atomics; min is -max(-src) (negation is exact).
+out= follows torch_scatter too: rows = out.size(dim); sum adds into out, mean divides
+(out + sum) by the clamped count, max / min include out's values (rows that receive nothing keep
+them, arg = src.size(dim) where out's value wins).
 """
 import torch
 
@@ -20,30 +23,37 @@ def _rows(index, dim_size):
     return int(index.max().item()) + 1 if index.numel() else 0
 
 
+def _bcast(v, like, dim):
+    """(n,) per-row values broadcast along `dim` of `like`."""
+    shp = [1] * like.dim()
+    shp[dim] = -1
+    return v.view(shp)
+
+
 def scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum"):
     if reduce not in ("sum", "add", "mean", "max", "min"):
         raise ValueError(f"unsupported reduce {reduce!r}")
     if reduce in ("max", "min"):
-        o = _scatter_arg(src, index, dim, dim_size, reduce)[0]
-        if out is not None:
-            out.copy_(o)
-            return out
+        o = _scatter_arg(src, index, dim, dim_size, reduce, out)[0]
         return o
     dim = dim % src.dim()
     if index.dim() != 1:
         # torch_scatter broadcasts index; the reference always passes a 1-D index along dim
         raise NotImplementedError("gmp scatter supports 1-D index along `dim`")
-    n = _rows(index, dim_size)
+    n = out.shape[dim] if out is not None else _rows(index, dim_size)
     x = src.movedim(dim, 0)
     shp = x.shape
     x2 = x.reshape(shp[0], -1)
     csr = ops.get_csr(index, n)
     red = "sum" if reduce == "add" else reduce
-    o = ops.SegmentReduceFn.apply(x2, csr, red).reshape((n,) + tuple(shp[1:])).movedim(0, dim)
-    if out is not None:
-        out.copy_(o)
-        return out
-    return o
+    if out is None:
+        return ops.SegmentReduceFn.apply(x2, csr, red).reshape((n,) + tuple(shp[1:])).movedim(0,
+                                                                                            dim)
+    o = ops.SegmentReduceFn.apply(x2, csr, "sum").reshape((n,) + tuple(shp[1:])).movedim(0, dim)
+    out.add_(o)
+    if red == "mean":
+        out.div_(_bcast(csr.counts().clamp(min=1).to(out.dtype), out, dim))
+    return out
 
 
 def scatter_sum(src, index, dim=-1, out=None, dim_size=None):
@@ -57,11 +67,11 @@ def scatter_mean(src, index, dim=-1, out=None, dim_size=None):
     return scatter(src, index, dim, out, dim_size, "mean")
 
 
-def _scatter_arg(src, index, dim, dim_size, reduce):
+def _scatter_arg(src, index, dim, dim_size, reduce, out=None):
     dim = dim % src.dim()
     if index.dim() != 1:
         raise NotImplementedError("gmp scatter supports 1-D index along `dim`")
-    n = _rows(index, dim_size)
+    n = out.shape[dim] if out is not None else _rows(index, dim_size)
     x = src.movedim(dim, 0)
     shp = x.shape
     x2 = x.reshape(shp[0], -1)
@@ -73,25 +83,25 @@ def _scatter_arg(src, index, dim, dim_size, reduce):
         o, arg = ops.SegmentMaxFn.apply(x2, csr)
     o = o.reshape((n,) + tuple(shp[1:])).movedim(0, dim)
     arg = arg.reshape((n,) + tuple(shp[1:])).movedim(0, dim)
+    if out is not None:
+        # out's values take part in the reduction: a segment value wins where it is >= (max) /
+        # <= (min) out's and the segment is not empty; elsewhere out keeps its value
+        nonempty = _bcast(csr.counts() > 0, o, dim)
+        win = nonempty & ((o >= out) if reduce == "max" else (o <= out))
+        arg = torch.where(win, arg, torch.full_like(arg, src.shape[dim]))
+        out.copy_(torch.where(win, o, out))
+        o = out
     return o, arg
 
 
 def scatter_max(src, index, dim=-1, out=None, dim_size=None):
     """torch_scatter.scatter_max: (max values, argmax along dim)."""
-    o, arg = _scatter_arg(src, index, dim, dim_size, "max")
-    if out is not None:
-        out.copy_(o)
-        o = out
-    return o, arg
+    return _scatter_arg(src, index, dim, dim_size, "max", out)
 
 
 def scatter_min(src, index, dim=-1, out=None, dim_size=None):
     """torch_scatter.scatter_min: (min values, argmin along dim)."""
-    o, arg = _scatter_arg(src, index, dim, dim_size, "min")
-    if out is not None:
-        out.copy_(o)
-        o = out
-    return o, arg
+    return _scatter_arg(src, index, dim, dim_size, "min", out)
 
 
 def global_add_pool(x, batch, size=None):

@@ -356,13 +356,6 @@ int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const fl
  * (T = G [W2_p]^T, Tb = G b2_p^T from the path GEMMs; dA is accumulated, dZ overwritten). */
 int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                           const float* Z, const float* A, float* S, float* Sb, void* stream);
-/* As gmp_tp_node_outer_f32, also writing rmax[n (w / 16) + r / 16] = max |S[n, r', :]|,
- * |Sb[n, r']| over the 16 rows r' = r .. r + 15 (w % 16 == 0; NULL = off; every word written,
- * no atomics): the per-row A scales of the H2 forward path GEMM (row (n, k) of a path with
- * mul1 % 16 == 0 owns the mul1 / 16 words from (n d3 + k) mul1 / 16). */
-int gmp_tp_node_outer_rmax_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
-                               const float* Z, const float* A, float* S, float* Sb,
-                               float* rmax, void* stream);
 int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                           const float* Z, const float* A, const float* T, const float* Tb,
                           float* dZ, float* dA, void* stream);
@@ -410,26 +403,6 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                              const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
                              void* stream);
-/* H2 forms: two fp16 planes (hi + lo, 22-bit operands) instead of three bf16 planes, three
- * MFMA products per k step instead of six; operands scaled by powers of two (exponent s with
- * max 2^s < 2^15): B by the device word `wmax` (float bit pattern of max |W2p|, |b2p|:
- * gmp_absmax_f32 over both before gmp_tp_split_w2_h2_f32); gemm_h2's A per ROW r by
- * max_p arow[r nparts + p] (gmp_tp_node_outer_rmax_f32's words, nparts = mul1 / 16, or any
- * per-row bound); gemm_h2_widen's A by one word `amax` (gmp_absmax_f32).  Results are scaled
- * back exactly; dropped terms ~2^-22 relative.  Planes: [2][...] fp16 (as uint16). */
-int gmp_tp_split_w2_h2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
-                           const float* b2p, const uint32_t* wmax, void* Bf, void* Bt,
-                           void* stream);
-int gmp_tp_gemm_h2_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
-                       int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
-                       int64_t bplane, const float* arow, int64_t nparts, const uint32_t* wmax,
-                       float* C, int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn,
-                       int accumulate, void* stream);
-int gmp_tp_gemm_h2_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
-                             const void* Bp, int64_t ldb, int64_t bplane, const uint32_t* amax,
-                             const uint32_t* wmax, float* C, int64_t ldc, void* stream);
-/* max |x| over n floats folded into *amax (float bit pattern, atomic max; caller zeroes). */
-int gmp_absmax_f32(const float* x, int64_t n, uint32_t* amax, void* stream);
 /* Wide edge/row reduction C (m_total x n, row stride ldc) = A^T B over K rows, A (K x m_total,
  * row stride lda), B (K x n, ldb), m_total a multiple of 128, n a multiple of 16 (<= 128): the
  * TP path GEMM dW2p = S^T G.  Split-plane bf16 MFMA (the K5 kernel with column blocks of 128),

@@ -6,6 +6,10 @@ models/layers/gvp_layer.py:415 and PyG's default aggregate / global pools (SURVE
   mean = sum / count.clamp(min=1); max / min: empty rows 0.
 scatter_arg: torch_scatter.scatter_max / scatter_min's (values, arg) with arg = src.size(dim)
 for empty rows and the first (lowest-index) item among ties, by a plain loop (small inputs).
+out= (torch_scatter 2.x, restated: scatter.py / scatter_{max,min} of that package): rows =
+out.size(dim); sum adds into out (out.scatter_add_), mean = (out + sum) / count.clamp(1);
+max / min include out's values in the reduction (rows that receive nothing keep them; arg =
+src.size(dim) where out's value wins).
 """
 import torch
 
@@ -16,8 +20,23 @@ def _rows(index, dim_size):
     return int(index.max()) + 1 if index.numel() else 0
 
 
-def scatter(src, index, dim=0, dim_size=None, reduce="sum"):
+def scatter(src, index, dim=0, dim_size=None, reduce="sum", out=None):
     dim = dim % src.dim()
+    if out is not None:
+        o = out.movedim(dim, 0)
+        n = o.shape[0]
+        x = src.movedim(dim, 0)
+        if reduce in ("sum", "add", "mean"):
+            r = o + scatter(src, index, dim, n, "sum").movedim(dim, 0)
+            if reduce == "mean":
+                cnt = torch.zeros(n, dtype=src.dtype)
+                cnt.index_add_(0, index, torch.ones(index.shape[0], dtype=src.dtype))
+                r = r / cnt.clamp(min=1).view((n,) + (1,) * (r.dim() - 1))
+        else:
+            idx = index.view((-1,) + (1,) * (x.dim() - 1)).expand_as(x)
+            r = o.scatter_reduce(0, idx, x, reduce="amax" if reduce == "max" else "amin",
+                                 include_self=True)
+        return r.movedim(0, dim)
     n = _rows(index, dim_size)
     x = src.movedim(dim, 0)
     shape = (n,) + tuple(x.shape[1:])
@@ -43,18 +62,25 @@ def scatter(src, index, dim=0, dim_size=None, reduce="sum"):
     return out.movedim(0, dim)
 
 
-def scatter_arg(src, index, dim_size, reduce):
-    """(values, arg) along dim 0 of a 2-D src for reduce in {max, min}."""
-    n = _rows(index, dim_size)
+def scatter_arg(src, index, dim_size, reduce, out=None):
+    """(values, arg) along dim 0 of a 2-D src for reduce in {max, min}; with `out` its values
+    take part (torch_scatter: a src item equal to out's value wins the arg)."""
+    n = out.shape[0] if out is not None else _rows(index, dim_size)
     E, F = src.shape
-    val = torch.zeros((n, F), dtype=src.dtype)
+    val = torch.zeros((n, F), dtype=src.dtype) if out is None else out.clone()
     arg = torch.full((n, F), E, dtype=torch.int64)
+    seen = torch.zeros((n, F), dtype=torch.bool) if out is None else torch.ones((n, F),
+                                                                               dtype=torch.bool)
     for e in range(E):
         s = int(index[e])
         for f in range(F):
             v = src[e, f]
-            if arg[s, f] == E or (v > val[s, f] if reduce == "max" else v < val[s, f]):
-                val[s, f], arg[s, f] = v, e
+            if out is not None and arg[s, f] == E:
+                better = (v >= val[s, f]) if reduce == "max" else (v <= val[s, f])
+            else:
+                better = (v > val[s, f]) if reduce == "max" else (v < val[s, f])
+            if not seen[s, f] or better:
+                val[s, f], arg[s, f], seen[s, f] = v, e, True
     return val, arg
 
 

@@ -32,7 +32,7 @@ def load_counters(path, counter):
     return per
 
 
-def main(src, workload, tag):
+def main(src, workload, tag, steps=None):
     stats = os.path.join(src, "stats_kernel_stats.csv")
     rows = []
     with open(stats) as f:
@@ -57,9 +57,19 @@ def main(src, workload, tag):
     with open(base + ".json", "w") as f:
         json.dump({"workload": workload, "source": "rocprofv3 --kernel-trace --stats; "
                    "--pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE in separate passes",
-                   "kernels": out}, f, indent=1)
+                   # training steps the traced run executed (warm-up + timed): calls / steps =
+                   # launches per step (bench.py reads per-step kernel time and HBM bytes)
+                   "steps_in_trace": steps, "kernels": out}, f, indent=1)
     with open(base + ".md", "w") as f:
         f.write(f"# rocprofv3 kernel summary — {workload} ({tag})\n\n")
+        if steps:
+            tot = sum(o["total_ms"] for o in out) / steps
+            f.write(f"{steps} training steps in the trace; kernel time {tot:.1f} ms per step")
+            if all(o["hbm_read_bytes_per_launch"] is not None for o in out):
+                hbm = sum(o["calls"] * (o["hbm_read_bytes_per_launch"] +
+                                        o["hbm_write_bytes_per_launch"]) for o in out) / steps
+                f.write(f"; HBM traffic (PMC) {hbm / 1e9:.1f} GB per step")
+            f.write(".\n\n")
         f.write("| kernel | calls | avg µs | % time | HBM read MB/launch | HBM write MB/launch |\n")
         f.write("|---|---|---|---|---|---|\n")
         for o in out[:40]:
@@ -73,4 +83,5 @@ def main(src, workload, tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "r01")
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "r01",
+         int(sys.argv[4]) if len(sys.argv) > 4 else None)

@@ -294,103 +294,3 @@ def test_node_apply_bf16x3_matches_fp64(w, H, x3):
         ez = ((dZ[e0:e1].cpu().double() - rz).abs() / mz).max().item()
         ea = ((dA[e0:e1].cpu().double() - ra).abs() / ma).max().item()
         assert ez < 1e-6 and ea < 1e-6, (n, degs[n], ez, ea)
-
-
-def _h2_case(m1, mo, H, seed, wscale=1.0):
-    g = torch.Generator().manual_seed(seed)
-    W2 = torch.randn(m1 * mo, H, generator=g) * torch.logspace(-3, 1, H) * wscale
-    b2 = torch.randn(m1 * mo, generator=g) * wscale
-    W = W2.double().view(m1, mo, H)
-    Bf = torch.cat([W.permute(1, 0, 2).reshape(mo, m1 * H), b2.double().view(m1, mo).t()], 1)
-    Bt = W.permute(0, 2, 1).reshape(m1 * H, mo)
-    return W2, b2, Bf, Bt
-
-
-@pytest.mark.parametrize("M,m1,mo,H,grp,ascale,nparts", [(1000, 32, 128, 64, 5, 1.0, 1),
-                                                         (333, 64, 64, 32, 1, 1e-20, 4),
-                                                         (130, 32, 96, 128, 3, 1e12, 2),
-                                                         (517, 32, 128, 64, 5, None, 2)])
-def test_tp_gemm_h2_matches_fp64(M, m1, mo, H, grp, ascale, nparts):
-    """The H2 forward path GEMM (torch.ops.gmp.tp_split_w2_h2 + tp_gemm_h2: two fp16 planes,
-    B scaled by its max word, A per row by the max of its `nparts` words) against fp64: error per
-    entry <= 4e-6 of sum |a b| (22-bit operands), ragged tiles, the bias operand, grouped
-    epilogue accumulation, operands 1e-20 / 1e12 in scale, and (ascale None) rows spread over
-    1e-30 .. 1e12 in one launch: each row keeps its own precision."""
-    from gmp_amd import _lib
-    tops = _lib.torch_ops()
-    W2, b2, Bf, _ = _h2_case(m1, mo, H, M + H)
-    g = torch.Generator().manual_seed(M)
-    K1 = m1 * H
-    rs = (torch.logspace(-30, 12, M)[torch.randperm(M, generator=g)].unsqueeze(1)
-          if ascale is None else ascale)
-    S = torch.randn(M, K1, generator=g) * torch.logspace(-2, 1, K1) * rs
-    Sb = torch.randn(M, m1, generator=g) * rs
-    W2d, b2d = W2.to(DEV), b2.to(DEV)
-    wmax = torch.zeros(1, dtype=torch.int32, device=DEV)
-    tops.absmax(W2d, wmax)
-    tops.absmax(b2d, wmax)
-    planes = tops.tp_split_w2_h2(W2d, b2d, 0, m1, mo, True, wmax)
-    Sd, Sbd = S.to(DEV), Sb.to(DEV)
-    # per-row words: max |.| over nparts column chunks of [S | Sb] (the row max is their max)
-    arow = torch.stack([c.abs().amax(1) for c in torch.cat([S, Sb], 1).chunk(nparts, 1)], 1)
-    nr = -(-M // grp)
-    C0 = torch.randn(nr, mo * grp + 5, generator=g) * (1.0 if ascale is None else ascale)
-    C = C0.clone().to(DEV)
-    tops.tp_gemm_h2(Sd, K1, Sbd, m1, planes, K1 + m1, mo, C, 0, grp, mo * grp + 5, 1, grp, True,
-                    arow.contiguous().to(DEV), wmax)
-    A = torch.cat([S, Sb], 1).double()
-    ref = A @ Bf.t()
-    mag = A.abs() @ Bf.abs().t()
-    got = C.cpu().double() - C0.double()
-    if ascale is None:  # C0's entries are far above the small rows' results: compare C alone
-        C.zero_()
-        tops.tp_gemm_h2(Sd, K1, Sbd, m1, planes, K1 + m1, mo, C, 0, grp, mo * grp + 5, 1, grp,
-                        True, arow.contiguous().to(DEV), wmax)
-        got = C.cpu().double()
-    rows = torch.arange(M)
-    out = torch.empty(M, mo, dtype=torch.float64)
-    for col in range(mo):
-        out[:, col] = got[rows // grp, rows % grp + col * grp]
-    err = ((out - ref).abs() / mag.clamp_min(1e-300)).max().item()
-    assert err < 4e-6, err
-
-
-@pytest.mark.parametrize("M,m1,mo,H", [(700, 32, 128, 64), (129, 64, 32, 32), (64, 32, 96, 96)])
-def test_tp_gemm_h2_widen_matches_fp64(M, m1, mo, H):
-    """The H2 backward T GEMM (tp_gemm_h2_widen, A = G scaled by its absmax word) against fp64
-    within 4e-6 of sum |a b| per entry."""
-    from gmp_amd import _lib
-    tops = _lib.torch_ops()
-    W2, b2, _, Bt = _h2_case(m1, mo, H, M + mo)
-    g = torch.Generator().manual_seed(M + 1)
-    G = torch.randn(M, mo, generator=g) * torch.logspace(-4, 0, mo)
-    W2d, b2d = W2.to(DEV), b2.to(DEV)
-    wmax = torch.zeros(1, dtype=torch.int32, device=DEV)
-    tops.absmax(W2d, wmax)
-    tops.absmax(b2d, wmax)
-    planes = tops.tp_split_w2_h2(W2d, b2d, 0, m1, mo, False, wmax)
-    Gd = G.to(DEV)
-    gmax = torch.zeros(1, dtype=torch.int32, device=DEV)
-    tops.absmax(Gd, gmax)
-    T = tops.tp_gemm_h2_widen(Gd, planes, m1 * H, gmax, wmax)
-    ref = G.double() @ Bt.t()
-    mag = G.double().abs() @ Bt.abs().t()
-    err = ((T.cpu().double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
-    assert err < 4e-6, err
-
-
-@pytest.mark.parametrize("w", [96, 80])
-def test_tp_node_outer_rmax_words(w):
-    """gmp_tp_node_outer_rmax_f32 writes, for every receiver and 16-row block, max |S|, |Sb|
-    over the block (bit-exact: a max of the stored values), in both S-kernel branches
-    (in-degree <= 32 and above) and with a partial last 64-row block (w = 80)."""
-    from gmp_amd import _lib
-    degs = [0, 1, 31, 32, 33, 70, 20, 5]
-    H = 64
-    eoff, Z, A, ne = _setup(degs, w, H, seed=3)
-    rmax = torch.full((len(degs) * (w // 16),), -1.0, device=DEV)
-    S, Sb = _lib.torch_ops().tp_node_outer(eoff.to(DEV), Z.to(DEV), A.to(DEV), w, rmax)
-    n = len(degs)
-    want = torch.maximum(S.abs().view(n, w // 16, 16, H).amax((2, 3)),
-                         Sb.abs().view(n, w // 16, 16).amax(2))
-    assert torch.equal(rmax.view(n, w // 16), want)

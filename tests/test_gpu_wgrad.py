@@ -114,7 +114,11 @@ def test_outer_sum_two_b_operands(m, n1, n2):
     refC, refs = _ref(A, Bcat)
     assert _err(C, refC, A, Bcat) < 5e-6
     torch.testing.assert_close(cs.cpu().double(), refs, atol=1e-3, rtol=1e-5)
-    assert not ops.outer_sum_into2(Ad[:1000], B1d[:1000], B2d[:1000], C, cs)  # node-level K
+    # node-level K: outside the split-plane kernel, the op makes two products (same result)
+    assert not ops.outer_sum_into2(Ad[:1000], B1d[:1000], B2d[:1000], C, cs)
+    refC, refs = _ref(A[:1000], Bcat[:1000])
+    assert _err(C, refC, A[:1000], Bcat[:1000]) < 5e-6
+    torch.testing.assert_close(cs.cpu().double(), refs, atol=1e-4, rtol=1e-5)
 
 
 @pytest.mark.parametrize("d,act,ascale", [(128, "relu", 1.0), (128, "swish", 1e-30),
