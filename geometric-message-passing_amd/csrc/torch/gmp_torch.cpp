@@ -920,9 +920,9 @@ Tensor act_rows(const Tensor& B, int64_t act, const optional<Tensor>& w,
   return act == 0 ? at::relu(y) : at::silu(y);
 }
 
-// C[:] = A^T act(B) (+ colsum[:] = colsum(A)) into strided views; returns 0 when the split-plane
-// / f32-MFMA kernels ran, 1 when the shape was outside their buckets and the library GEMM did.
-int64_t edge_outer_sum_ex(const Tensor& A_, const Tensor& B_, Tensor C,
+// C[:] = A^T act(B) (+ colsum[:] = colsum(A)) into strided views: the split-plane / f32-MFMA
+// kernels, or the library GEMM on the device where the shape is outside their buckets.
+void edge_outer_sum_ex(const Tensor& A_, const Tensor& B_, Tensor C,
                           const optional<Tensor>& colsum, int64_t act, const optional<Tensor>& w,
                           const optional<Tensor>& b) {
   OpGuard g(A_, "edge_outer_sum_ex");
@@ -950,16 +950,15 @@ int64_t edge_outer_sum_ex(const Tensor& A_, const Tensor& B_, Tensor C,
       colsum.has_value() ? fp(*colsum) : nullptr, ws.data_ptr(), ws_b, cur_stream());
   if (rc != GMP_ERR_UNSUPPORTED) {
     check_rc(rc, "gmp_edge_outer_sum_ex_f32");
-    return 0;
+    return;
   }
   C.copy_(at::mm(A.t(), act_rows(B, act, w, b)));
   if (colsum.has_value()) colsum->copy_(A.sum(0));
-  return 1;
 }
 
-// C[:] = A^T [B1 | B2] (+ colsum) in one pass over A where the split-plane kernel applies (0),
-// else two edge_outer_sum_ex products (1)
-int64_t edge_outer_sum_ex2(const Tensor& A_, const Tensor& B1_, const Tensor& B2_, Tensor C,
+// C[:] = A^T [B1 | B2] (+ colsum) in one pass over A where the split-plane kernel applies, else
+// as two edge_outer_sum_ex products
+void edge_outer_sum_ex2(const Tensor& A_, const Tensor& B1_, const Tensor& B2_, Tensor C,
                            const optional<Tensor>& colsum) {
   OpGuard g(A_, "edge_outer_sum_ex2");
   Tensor A = rows_view(A_, "A"), B1 = rows_view(B1_, "B1"), B2 = rows_view(B2_, "B2");
@@ -980,11 +979,10 @@ int64_t edge_outer_sum_ex2(const Tensor& A_, const Tensor& B1_, const Tensor& B2
                                             ws.data_ptr(), ws_b, cur_stream());
   if (rc != GMP_ERR_UNSUPPORTED) {
     check_rc(rc, "gmp_edge_outer_sum_ex2_f32");
-    return 0;
+    return;
   }
   edge_outer_sum_ex(A, B1, C.narrow(1, 0, n1), colsum, -1, c10::nullopt, c10::nullopt);
   edge_outer_sum_ex(A, B2, C.narrow(1, n1, n2), c10::nullopt, -1, c10::nullopt, c10::nullopt);
-  return 1;
 }
 
 // (A^T act(X w + b), colsum(A)) for the EGNN y1 / m operands rebuilt from x_hat; with amax (the
@@ -1297,14 +1295,10 @@ Tensor outer_sum_cols(const Tensor& A, const Tensor& B) {
 std::tuple<Tensor, Tensor> edge_outer_sum(const Tensor& A, const Tensor& B) {
   return {at::empty({A.size(1), B.size(1)}, A.options()), at::empty({A.size(1)}, A.options())};
 }
-int64_t edge_outer_sum_ex(const Tensor&, const Tensor&, Tensor, const optional<Tensor>&, int64_t,
-                          const optional<Tensor>&, const optional<Tensor>&) {
-  return 0;
-}
-int64_t edge_outer_sum_ex2(const Tensor&, const Tensor&, const Tensor&, Tensor,
-                           const optional<Tensor>&) {
-  return 0;
-}
+void edge_outer_sum_ex(const Tensor&, const Tensor&, Tensor, const optional<Tensor>&, int64_t,
+                       const optional<Tensor>&, const optional<Tensor>&) {}
+void edge_outer_sum_ex2(const Tensor&, const Tensor&, const Tensor&, Tensor,
+                        const optional<Tensor>&) {}
 std::tuple<Tensor, Tensor> edge_outer_sum_act(const Tensor& A, const Tensor&, const Tensor&,
                                               const Tensor&, int64_t, const optional<Tensor>&) {
   return {at::empty({A.size(1), A.size(1)}, A.options()), at::empty({A.size(1)}, A.options())};
@@ -1410,9 +1404,9 @@ TORCH_LIBRARY(gmp, m) {
   m.def("outer_sum_cols(Tensor A, Tensor B) -> Tensor");
   m.def("edge_outer_sum(Tensor A, Tensor B) -> (Tensor C, Tensor colsum)");
   m.def("edge_outer_sum_ex(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int act, "
-        "Tensor? w, Tensor? b) -> int");
+        "Tensor? w, Tensor? b) -> ()");
   m.def("edge_outer_sum_ex2(Tensor A, Tensor B1, Tensor B2, Tensor(a!) C, Tensor(b!)? colsum) "
-        "-> int");
+        "-> ()");
   m.def("edge_outer_sum_act(Tensor A, Tensor X, Tensor w, Tensor b, int act, Tensor? amax=None) "
         "-> (Tensor C, Tensor colsum)");
   m.def("gvp_layer_fwd(Tensor s, Tensor v, Tensor[] W, bool relu) -> (Tensor s_out, "
@@ -1470,4 +1464,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("gvp_msg0_bwd", ns gvp_msg0_bwd);
 
 TORCH_LIBRARY_IMPL(gmp, CUDA, m) { GMP_IMPL(m, ) }
+// CPU tensors reach the same implementations, whose device guard rejects them with the
+// boundary's message ("... must be HIP device tensors (no CPU fallback)"), as a RuntimeError
+TORCH_LIBRARY_IMPL(gmp, CPU, m) { GMP_IMPL(m, ) }
 TORCH_LIBRARY_IMPL(gmp, Meta, m) { GMP_IMPL(m, meta::) }

@@ -178,19 +178,19 @@ def outer_sum_into(A, B, C, colsum=None, act=None, w=None, b=None):
     """C[:] = A^T act(B) over the rows (torch.ops.gmp.edge_outer_sum_ex), colsum[:] =
     colsum(A).  A (K, m), B (K, n) and C (m, n) may be strided views (unit column stride; e.g.
     column blocks of a wider tensor or parameter gradient).  Shapes outside the kernels' tile
-    buckets run the library GEMM inside the op.  Returns True when the outer-sum kernels ran."""
+    buckets run the library GEMM inside the op."""
     _need_cuda(A, B, C)
     a = -1 if act is None else _lib.ACT[act]
     with _timed("edge_outer_sum"):
-        return _lib.torch_ops().edge_outer_sum_ex(A, B, C, colsum, a, w, b) == 0
+        _lib.torch_ops().edge_outer_sum_ex(A, B, C, colsum, a, w, b)
 
 
 def outer_sum_into2(A, B1, B2, C, colsum=None):
     """C[:] = A^T [B1 | B2] (and colsum(A)) in one pass over A where the split-plane kernel
-    applies (returns True), else as two products inside the op (returns False)."""
+    applies, else as two products inside the op."""
     _need_cuda(A, B1, B2, C)
     with _timed("edge_outer_sum"):
-        return _lib.torch_ops().edge_outer_sum_ex2(A, B1, B2, C, colsum) == 0
+        _lib.torch_ops().edge_outer_sum_ex2(A, B1, B2, C, colsum)
 
 
 def edge_outer_sum_rect(A, B):

@@ -44,3 +44,37 @@ def test_product_refuses_cpu_tensors():
         pytest.skip("libgmp.so not built")
     with pytest.raises(_lib.GmpError):
         ops.gather_rows(torch.zeros(4, 4), torch.zeros(2, dtype=torch.long))
+
+
+def test_torch_ops_registered_and_reject_cpu_tensors():
+    """TORCH_LIBRARY(gmp) (libgmp_torch.so): every hot-path operator is registered with a Meta
+    kernel (shape inference, no device work) and a CPU tensor raises the boundary's error."""
+    import torch
+    from gmp_amd import _lib
+    if not os.path.exists(_lib.TORCH_LIB_PATH):
+        pytest.skip("libgmp_torch.so not built")
+    tops = _lib.torch_ops()
+    for name in ("csr_build", "gather_rows", "segment_reduce", "egnn_edge_fwd", "egnn_edge_bwd",
+                 "tp_edge_z", "tp_edge_z_bwd", "tp_node_outer", "tp_node_apply", "tp_gemm_x3",
+                 "tp_gemm_x3_widen", "outer_sum_cols", "edge_outer_sum_ex",
+                 "edge_outer_sum_ex2", "edge_outer_sum_act", "gvp_layer_fwd", "gvp_layer_bwd",
+                 "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd"):
+        assert hasattr(tops, name), name
+    with pytest.raises(RuntimeError, match="HIP device"):
+        tops.gather_rows(torch.zeros(4, 4), torch.zeros(2, dtype=torch.long))
+    # Meta: shapes only
+    s = torch.empty(1000, 128, device="meta")
+    v = torch.empty(1000, 16, 3, device="meta")
+    W = [torch.empty(*sh, device="meta") for sh in ((128, 144), (128,), (16, 128), (16,),
+                                                   (16, 16), (16, 16))]
+    out = tops.gvp_layer_bwd(s, v, W, s, v, True)
+    assert [tuple(t.shape) for t in out] == [(1000, 128), (1000, 16, 3), (1000, 128),
+                                            (1000, 128), (1000, 16), (1000, 16), (1000, 48),
+                                            (1000, 48), (1000, 48)]
+    z = tops.tp_edge_z([11, 1152, 1152, 9, 180224, 4480, 3] + [0] * 12,
+                       torch.empty(11 * 64, dtype=torch.uint8, device="meta"),
+                       torch.empty(10, device="meta"), torch.empty(50, 1152, device="meta"),
+                       torch.empty(700, 9, device="meta"),
+                       torch.empty(700, dtype=torch.long, device="meta"),
+                       torch.empty(700, dtype=torch.long, device="meta"), 0, 700)
+    assert tuple(z.shape) == (701 * 4480,)

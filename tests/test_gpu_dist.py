@@ -31,6 +31,9 @@ pytestmark = pytest.mark.gpu
 CASES = {
     "egnn": dict(num_layers=2, emb_dim=128, in_dim=1, out_dim=1),
     "tfn": dict(num_layers=2, emb_dim=16, mlp_dim=64, r_max=2.5, in_dim=1, out_dim=1),
+    # config C5's per-rank model at its widths (tfn.py:51-60 defaults: 64 channels, radial
+    # hidden 256, 5 layers, gated): the K7g path GEMMs and the 307 MB-class gradient all-reduce
+    "tfn_c5": dict(num_layers=5, emb_dim=64, mlp_dim=256, r_max=2.5, in_dim=1, out_dim=1),
 }
 
 
@@ -53,7 +56,7 @@ def _graph(rank):
 def _model(kind):
     import gmp_amd
     torch.manual_seed(0)
-    cls = {"egnn": gmp_amd.EGNNModel, "tfn": gmp_amd.TFNModel}[kind]
+    cls = {"egnn": gmp_amd.EGNNModel, "tfn": gmp_amd.TFNModel, "tfn_c5": gmp_amd.TFNModel}[kind]
     return cls(**CASES[kind])
 
 
@@ -134,7 +137,7 @@ def _rank_worker(rank, world, port, out_dir, kind, mode):
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("kind", ["egnn", "tfn"])
+@pytest.mark.parametrize("kind", ["egnn", "tfn", "tfn_c5"])
 @pytest.mark.parametrize("mode", ["step", "ddp"])
 def test_product_world2_gloo_on_gpu_matches_single_process(kind, mode):
     world = 2

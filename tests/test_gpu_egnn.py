@@ -296,3 +296,43 @@ def test_egnn_c2_full_size_vs_fp64_oracle():
         scale = b.abs().max().item() + 1e-12
         e = (a - b).abs().max().item()
         assert e <= 1e-4 * scale, (k, e, scale)
+
+
+def test_egnn_c2_full_size_properties_hf():
+    """C2 at full size with the default HF (2-plane f16) products in K4 and the dW2 / dW3 sums:
+    the same 1e-5 bar the C4 MACE check applies (test_mace_c4_full_size_properties) — the
+    prediction is invariant to the input edge order and to a rotation + translation of the
+    positions within 1e-5 relative, and forward / backward are bitwise deterministic.
+    (EGNN is E(3)-invariant in h: egnn_layer.py:62-86 sees positions only through |x_i - x_j|.)"""
+    import gmp_amd
+    from gmp_amd import _lib
+    from gmp_amd.graph import Batch, radius_graph
+    from oracle import o3 as oo3
+    lib = _lib.load()
+    assert lib.gmp_egnn_set_f32_mfma(0) == 0  # the HF products are the default
+    g = radius_graph()
+    torch.manual_seed(0)
+    model = gmp_amd.EGNNModel(num_layers=4, emb_dim=128, in_dim=1, out_dim=1).to(DEV)
+    ei, pos, atoms = g.edge_index.to(DEV), g.pos.to(DEV), g.atoms.to(DEV)
+
+    def run(p, e, grad=True):
+        model.zero_grad(set_to_none=True)
+        y = model(Batch(atoms, p, e, num_graphs=1))
+        if not grad:
+            return y.detach().double(), None
+        y.sum().backward()
+        torch.cuda.synchronize()
+        return y.detach().double(), model.convs[1].mlp_msg[3].weight.grad.clone()
+
+    with torch.no_grad():
+        y0, _ = run(pos, ei, grad=False)
+        yp, _ = run(pos, ei[:, torch.randperm(ei.shape[1], device=DEV)], grad=False)
+        R = oo3.wigner_D(1, *(torch.tensor(a, dtype=torch.float64) for a in (0.3, 1.1, -0.6)))
+        pos_r = g.pos.double() @ R.T + torch.tensor([0.5, -2.0, 1.0], dtype=torch.float64)
+        yr, _ = run(pos_r.float().to(DEV), ei, grad=False)
+    scale = y0.abs().max().item()
+    assert (yp - y0).abs().max().item() <= 1e-5 * scale, (yp, y0)
+    assert (yr - y0).abs().max().item() <= 1e-5 * scale, (yr, y0)
+    a, b = run(pos, ei), run(pos, ei)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert a[1].abs().max().item() > 0

@@ -106,13 +106,18 @@ def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, fused, defer, mon
             _scaled(p.grad, q.grad, 1e-4, k)
 
 
+C3 = dict(num_layers=4, s_dim=128, v_dim=16, s_dim_edge=32, v_dim_edge=1)  # gvpgnn.py:13-27
+
+
 def test_gvp_model_c3_vs_oracle():
+    """Config C3 exactly (GVP-GNN 4 layers, s = 128, v = 16, edge (32, 1); gvpgnn.py:103-127)
+    against the fp32 oracle and its fp64 copy (eval mode: Dropout off on both)."""
     import gmp_amd.gvp as g
     from gmp_amd.graph import Batch, radius_graph
     torch.manual_seed(6)
     gr = radius_graph(num_nodes=500, target_edges=7000, r=2.0, seed=8, tol=0.2, shuffle=True)
-    ref = ogvp.GVPGNNModel(r_max=2.0, num_layers=2, in_dim=1, out_dim=1).eval()
-    model = g.GVPGNNModel(r_max=2.0, num_layers=2, in_dim=1, out_dim=1)
+    ref = ogvp.GVPGNNModel(r_max=2.0, in_dim=1, out_dim=1, **C3).eval()
+    model = g.GVPGNNModel(r_max=2.0, in_dim=1, out_dim=1, **C3)
     model.load_state_dict(ref.state_dict(), strict=True)
     model = model.to(DEV).eval()
     ref64 = copy.deepcopy(ref).double()
@@ -207,3 +212,37 @@ def test_gvp_edge_featurize_vs_oracle(E):
     z = torch.tensor([[1, 2], [1, 0]], device=DEV)
     _, u0 = ops.GvpEdgeFeaturizeFn.apply(pos.to(DEV), z, rad_p._host)
     assert torch.equal(u0[0].cpu(), torch.zeros(3))
+
+
+def test_gvp_c3_full_size_properties():
+    """C3 at full size (the 1M-edge bench graph), eval mode: forward and backward are bitwise
+    deterministic, and the prediction is invariant to the input edge order and to a rotation +
+    translation of the positions within 1e-5 relative (gvpgnn.py:103-127 is E(3)-invariant)."""
+    import gmp_amd.gvp as g
+    from gmp_amd.graph import Batch, radius_graph
+    from oracle import o3 as oo3
+    gr = radius_graph()  # the C2/C3 bench graph, seed 0
+    torch.manual_seed(0)
+    model = g.GVPGNNModel(in_dim=1, out_dim=1, **C3).to(DEV).eval()
+    ei, pos, atoms = gr.edge_index.to(DEV), gr.pos.to(DEV), gr.atoms.to(DEV)
+
+    def run(p, e, grad=True):
+        model.zero_grad(set_to_none=True)
+        y = model(Batch(atoms, p, e, num_graphs=1))
+        if not grad:
+            return y.detach().double(), None
+        y.sum().backward()
+        return y.detach().double(), model.layers[1].conv.message_func[1].ws.weight.grad.clone()
+
+    with torch.no_grad():
+        y0, _ = run(pos, ei, grad=False)
+        yp, _ = run(pos, ei[:, torch.randperm(ei.shape[1], device=DEV)], grad=False)
+        R = oo3.wigner_D(1, *(torch.tensor(a, dtype=torch.float64) for a in (0.3, 1.1, -0.6)))
+        pos_r = gr.pos.double() @ R.T + torch.tensor([0.5, -2.0, 1.0], dtype=torch.float64)
+        yr, _ = run(pos_r.float().to(DEV), ei, grad=False)
+    scale = y0.abs().max().item()
+    assert (yp - y0).abs().max().item() <= 1e-5 * scale, (yp, y0)
+    assert (yr - y0).abs().max().item() <= 1e-5 * scale, (yr, y0)
+    a, b = run(pos, ei), run(pos, ei)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert a[1].abs().max().item() > 0

@@ -31,9 +31,9 @@ def test_outer_sum_split_matches_fp64(m, n, K):
     B = torch.randn(K, n, generator=g)
     C = torch.empty(m, n, device=DEV)
     cs = torch.empty(m, device=DEV)
-    assert ops.outer_sum_into(A.to(DEV), B.to(DEV), C, cs)
+    ops.outer_sum_into(A.to(DEV), B.to(DEV), C, cs)
     C2 = torch.empty_like(C)
-    assert ops.outer_sum_into(A.to(DEV), B.to(DEV), C2)
+    ops.outer_sum_into(A.to(DEV), B.to(DEV), C2)
     assert torch.equal(C, C2)  # deterministic
     refC, refs = _ref(A, B)
     assert _err(C, refC, A, B) < 5e-6
@@ -49,7 +49,7 @@ def test_outer_sum_strided_blocks():
     A = torch.randn(K, 272, generator=g).to(DEV)
     B = torch.randn(K, 200, generator=g).to(DEV)
     C = torch.zeros(300, 260, device=DEV)
-    assert ops.outer_sum_into(A[:, 16:144], B[:, 40:184], C[8:136, 100:244])
+    ops.outer_sum_into(A[:, 16:144], B[:, 40:184], C[8:136, 100:244])
     ref = A[:, 16:144].double().t() @ B[:, 40:184].double()
     torch.testing.assert_close(C[8:136, 100:244].double(), ref, atol=2e-3, rtol=1e-5)
     assert C[:8].abs().sum() == 0 and C[:, :100].abs().sum() == 0
@@ -87,7 +87,7 @@ def test_split_error_not_above_f32_mfma(m, n):
         prev = lib.gmp_wgrad_set_f32_mfma(mode)
         try:
             C = torch.empty(m, n, device=DEV)
-            assert ops.outer_sum_into(Ad, Bd, C)
+            ops.outer_sum_into(Ad, Bd, C)
             torch.cuda.synchronize()
         finally:
             lib.gmp_wgrad_set_f32_mfma(prev)
@@ -109,13 +109,13 @@ def test_outer_sum_two_b_operands(m, n1, n2):
     Ad, B1d, B2d = A.to(DEV), B1.to(DEV), B2.to(DEV)[:, 4:4 + n2]  # strided second operand
     C = torch.empty(m, n1 + n2, device=DEV)
     cs = torch.empty(m, device=DEV)
-    assert ops.outer_sum_into2(Ad, B1d, B2d, C, cs)
+    ops.outer_sum_into2(Ad, B1d, B2d, C, cs)
     Bcat = torch.cat([B1, B2[:, 4:4 + n2]], 1)
     refC, refs = _ref(A, Bcat)
     assert _err(C, refC, A, Bcat) < 5e-6
     torch.testing.assert_close(cs.cpu().double(), refs, atol=1e-3, rtol=1e-5)
     # node-level K: outside the split-plane kernel, the op makes two products (same result)
-    assert not ops.outer_sum_into2(Ad[:1000], B1d[:1000], B2d[:1000], C, cs)
+    ops.outer_sum_into2(Ad[:1000], B1d[:1000], B2d[:1000], C, cs)
     refC, refs = _ref(A[:1000], Bcat[:1000])
     assert _err(C, refC, A[:1000], Bcat[:1000]) < 5e-6
     torch.testing.assert_close(cs.cpu().double(), refs, atol=1e-4, rtol=1e-5)
