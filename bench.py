@@ -17,10 +17,13 @@ xGMI).  --graph replays the step from a HIP graph instead of launching it eagerl
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (egnn_edge_bwd, fp32 MFMA
-bound), timed with HIP events on the stream it is launched on; `cpu_baseline` times the CPU
-oracle (oracle/egnn.py, plain PyTorch on the host cores) on a bounded spatial slab of the same
-graph.
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel of the value's workload
+(EGNN: egnn_edge_bwd, both bounds, the closer one primary), timed with HIP events on the stream
+it is launched on; the `mace` object's roofline is the whole TP contraction's algorithmic FLOP
+against the three-plane bf16 ceiling, with the step's PMC HBM bytes against SURVEY §8(d)'s
+algorithmic bytes as `traffic` / `waste_ratio` (mace_roofline).  `cpu_baseline` times the CPU
+oracle (oracle/*.py, plain PyTorch on the host cores: the reference's CPU path restated) on a
+bounded spatial sample of the same graph, median of the timed steps (CPU_SAMPLE).
 """
 import argparse
 import json
@@ -69,6 +72,10 @@ def parse():
                     help="hand the model a new edge_index tensor every step (as a data loader "
                          "would), so the receiver / sender CSRs (K0) are rebuilt inside the "
                          "timed steps instead of coming from the per-graph cache")
+    ap.add_argument("--blas", default=os.environ.get("GMP_BLAS", "default"),
+                    choices=("default", "hipblaslt", "rocblas"),
+                    help="library for the node-level PyTorch GEMMs (torch.backends.cuda."
+                         "preferred_blas_library)")
     ap.add_argument("--timing-steps", type=int, default=2,
                     help="eager steps after the timed region in which the roofline kernel is "
                          "timed with HIP events (graph mode)")
@@ -508,6 +515,8 @@ def main():
         local = 0
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
+    if args.blas != "default":
+        torch.backends.cuda.preferred_blas_library(args.blas)
     from gmp_amd.graph import radius_graph
 
     g = radius_graph(num_nodes=args.nodes, target_edges=args.edges, seed=rank)
@@ -536,7 +545,8 @@ def main():
             "config": {"fresh_graph": bool(args.fresh_graph), "workload": main_rec["workload"], "value_is": names[0],
                        "global_batch": world, "parallelism": f"dp{world}",
                        "step": "fwd + L1 loss + bwd + Adam",
-                       "launch": "eager" if not args.graph else "hip graph replay"},
+                       "launch": "eager" if not args.graph else "hip graph replay",
+                       "blas": str(torch.backends.cuda.preferred_blas_library())},
             "roofline": main_rec["roofline"],
             "cpu_baseline": None,
         }

@@ -15,7 +15,7 @@ namespace {
 
 constexpr int kRowT = 256;        // 4 waves = 4 rows in flight per workgroup
 constexpr int kMaxF = 8;          // features per lane (d <= 512)
-constexpr int kRowBlocks = 1024;  // backward grid (partials rows)
+constexpr int kRowBlocks = 256;   // backward grid (partials rows; ~50 rows per wave at 50k)
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -170,8 +170,9 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
 // out[f] = sum over the partial rows (f < 2d: [dgamma | dbeta]) in a fixed order: thread
 // (column c, row group q) sums rows q, q + kSG, ... ; the kSG group sums are then added in
 // group order.  Deterministic.
-constexpr int kSC = 16, kSG = 64;  // columns x row groups per block (1024 threads): each
-                                   // thread's rows load in one burst for <= 1024 rows
+constexpr int kSC = 16, kSG = 16;  // columns x row groups per block (256 threads: fits beside
+                                   // the side stream's kernels); each thread's rows load in
+                                   // one burst for <= 256 rows
 __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __restrict__ partials,
                                                              int nrows, int width,
                                                              float* __restrict__ out) {

@@ -232,20 +232,27 @@ __device__ __forceinline__ H2Scale h2_scale(const unsigned* amax, const unsigned
   }
 }
 
-template <bool ACC, int NP, int RA, int RBB = 2>
+// The forward kernel in two tile shapes: WGM = 2 (waves 2 (M) x 4 (N), a 128 x 128 output tile:
+// mul_out = 128) and WGM = 4 (waves 4 x 2, a 256 x 64 tile: the 64-channel paths of config C5,
+// which a 128-column tile would run with half of its MFMAs on zero B columns).  The wave tile is
+// 64 x 32 in both; the A stage image holds BM = 64 WGM rows.
+template <bool ACC, int RA, int RBB, int WGM>
 __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
     const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
     int64_t ldb, int64_t bplane, float* __restrict__ C, int64_t cgrp, int64_t cldg,
-    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const float* __restrict__ arow,
-    int nparts, const unsigned* __restrict__ wmax) {
-  constexpr int STG = NP * kPlane;  // LDS bytes per stage (A planes; B skips LDS)
+    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n) {
+  constexpr int NP = 3;
+  constexpr int WGN = 8 / WGM;              // waves along N
+  constexpr int BM = 64 * WGM, BN = 32 * WGN;
+  constexpr int PL = BM * 64;               // bytes of one plane image (BM rows x 32 bf16)
+  constexpr int STG = NP * PL;              // LDS bytes per stage (A planes; B skips LDS)
+  constexpr int AU = BM / 64;               // A load units (row, float4) per thread and stage
   extern __shared__ __attribute__((aligned(16))) unsigned char smg[];
-  int* sexp = reinterpret_cast<int*>(smg + 2 * STG);  // H2: the tile's 128 row exponents
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / WGN, wn = w % WGN;
 
   // XCD-contiguous logical id (blocks b, b + 8, ... share an XCD under round-robin dealing;
   // speed only), then grouped tile order
@@ -261,35 +268,21 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   const int64_t gsize = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
   const int64_t in_grp = L - grp * per_group;
   const int64_t tm = first_m + in_grp % gsize, tn = in_grp / gsize;
-  const int64_t m0 = tm * kBM, n0 = tn * kBN;
+  const int64_t m0 = tm * BM, n0 = tn * BN;
 
   const int64_t Ktot = K1 + K2;
   const int nst = (int)(Ktot / kBK);
-  int sb = 0;
-  if constexpr (NP == 2) {
-    sb = scale_exp_bits(wmax[0]);
-    if (tid < kBM) {
-      const int64_t r = m0 + tid;
-      float mx = 0.f;
-      if (r < M)
-        for (int p = 0; p < nparts; ++p) mx = fmaxf(mx, arow[r * nparts + p]);
-      sexp[tid] = row_exp(mx);
-    }
-    __syncthreads();
-  }
 
-  // loaders: A units (2 per thread) = (row, float4 of k), B units (3 per thread: one per plane)
-  int arow_[2], akq[2];
-  bool aok[2];
-  float fa[2];
-  const float* abase1[2];
-  const float* abase2[2];
+  // loaders: A units (AU per thread) = (row, float4 of k); B straight into registers
+  int arow_[AU], akq[AU];
+  bool aok[AU];
+  const float* abase1[AU];
+  const float* abase2[AU];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < AU; ++q) {
     const int v = tid + kGT * q;
     arow_[q] = v >> 3;
     akq[q] = v & 7;
-    fa[q] = NP == 2 ? ldexpf(1.f, sexp[arow_[q]]) : 1.f;
     const int64_t gr = m0 + arow_[q];
     aok[q] = gr < M;
     const int64_t grc = gr < M ? gr : M - 1;
@@ -313,13 +306,13 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   // flight per CU; measured at the MACE-128 lo = 2 shape (scripts/mb_tpgemm.py): RA = 2 11.33 ms,
   // 4 10.74 ms, 8 10.55 ms (230 VGPRs, no scratch) -- the A stream was only part of the limit.
   static_assert(RA % RBB == 0, "the unrolled loop indexes both rings statically");
-  f32x4 ringA[RA][2];
+  f32x4 ringA[RA][AU];
   u32x4 ringB[RBB][2][NP];  // B (W2p planes, from the Infinity Cache): RBB steps ahead
   auto fetch = [&](int slot, int st) {
     const int stc = st < nst ? st : nst - 1;
     const int64_t k0 = (int64_t)stc * kBK;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < AU; ++q) {
       const float* p = k0 < K1 ? abase1[q] + k0 : abase2[q] + (k0 - K1);
       ringA[slot][q] = *reinterpret_cast<const f32x4*>(p);
     }
@@ -337,15 +330,24 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   auto stash = [&](int slot, unsigned char* buf, int st) {
     const bool live = st < nst;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < AU; ++q) {
       f32x4 v = ringA[slot][q];
       if (!(live && aok[q])) v = f32x4{0.f, 0.f, 0.f, 0.f};
       unsigned pl[3][2];
-      split_planes<NP>(v, fa[q], pl);
+      split_planes<NP>(v, 1.f, pl);
       const int off = xoff(arow_[q], akq[q] >> 1) + 8 * (akq[q] & 1);
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        *reinterpret_cast<u32x2*>(buf + p * kPlane + off) = u32x2{pl[p][0], pl[p][1]};
+        *reinterpret_cast<u32x2*>(buf + p * PL + off) = u32x2{pl[p][0], pl[p][1]};
+    }
+  };
+  auto load_a = [&](FragA<NP>& f, const unsigned char* aimg) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int off = xoff(64 * wm + 16 * r + li, g);
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        f.a[r][p] = *reinterpret_cast<const u32x4*>(aimg + p * PL + off);
     }
   };
 
@@ -369,7 +371,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   stash(1, smg + STG, 1);
   fetch(1, RA + 1);
   __syncthreads();
-  load_frag_a<NP>(F[0], smg, wm, li, g);
+  load_a(F[0], smg);
   __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
   for (int s0 = 0; s0 < nst_pad; s0 += RA) {
 #pragma unroll
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       __builtin_amdgcn_sched_barrier(0);
       fetch(sl, st + 2 + RA);
       __builtin_amdgcn_sched_barrier(0);
-      load_frag_a<NP>(F[(j & 1) ^ 1], nb, wm, li, g);
+      load_a(F[(j & 1) ^ 1], nb);
       mma_ab<NP>(acc, F[j & 1], ringB[j % RBB]);
       __builtin_amdgcn_sched_barrier(0);
       fetch_b(j % RBB, st + RBB);  // the slot the MFMAs above just read: RBB stages of lead
@@ -406,9 +408,8 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
         if (row >= M) continue;
         const int64_t grp_r = row / cgrp;
         float* dst = C + grp_r * cldg + (row - grp_r * cgrp) * cldr + col * cldn;
-        const float v = NP == 3 ? acc[r][c][q] : ldexpf(acc[r][c][q], -(sexp[lr] + sb));
-        if (ACC) *dst += v;
-        else *dst = v;
+        if (ACC) *dst += acc[r][c][q];
+        else *dst = acc[r][c][q];
       }
     }
   }
@@ -606,6 +607,8 @@ namespace gmp {
 int g_tpgemm_ring = getenv("GMP_TPGEMM_RING") ? atoi(getenv("GMP_TPGEMM_RING")) : 8;
 // T GEMM (widen): B-stream register ring depth (GMP_TPGEMM_WIDEN_RING=2: the r02 form)
 int g_widen_ring = getenv("GMP_TPGEMM_WIDEN_RING") ? atoi(getenv("GMP_TPGEMM_WIDEN_RING")) : 4;
+// forward path GEMM: the 256 x 64 tile for mul_out <= 64 (GMP_TPGEMM_NARROW=0: 128 x 128)
+int g_tpgemm_narrow = getenv("GMP_TPGEMM_NARROW") ? atoi(getenv("GMP_TPGEMM_NARROW")) : 1;
 }  // namespace gmp
 
 template <int NP>
@@ -623,15 +626,13 @@ int split_w2_launch(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p, 
   return launch_status();
 }
 
-template <int NP>
 int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1, int64_t K2,
                 const float* A2, int64_t lda2, const void* Bp, int64_t ldb, int64_t bplane,
-                const float* arow, int64_t nparts, const unsigned* wmax, float* C, int64_t cgrp,
-                int64_t cldg, int64_t cldr, int64_t cldn, int accumulate, void* stream) {
+                float* C, int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, int accumulate,
+                void* stream) {
   GMP_CHECK_ARG(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && cgrp >= 1);
   if (M == 0 || N == 0) return GMP_OK;
-  GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2) &&
-                (NP == 3 || (arow && wmax && nparts >= 1 && nparts <= 4096)));
+  GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2));
   GMP_CHECK_ARG(K1 % kBK == 0 && K2 % kBK == 0 && K1 + K2 > 0 && N % 16 == 0);
   GMP_CHECK_ARG(lda1 % 4 == 0 && (K2 == 0 || lda2 % 4 == 0));
   // B is fragment-ordered (bfrag_index): the row-major strides it replaced must be the dense ones
@@ -639,20 +640,28 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   GMP_CHECK_ARG(lda1 >= K1 && (K2 == 0 || lda2 >= K2));
   GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A1) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
   GMP_CHECK_ARG(K2 == 0 || reinterpret_cast<uintptr_t>(A2) % 16 == 0);
-  const int64_t tiles_m = ceil_div(M, kBM), tiles_n = ceil_div(N, kBN);
+  // narrow outputs (mul_out <= 64: C5's 64-channel paths) take the 256 x 64 tile
+  const bool narrow = N <= 64 && g_tpgemm_narrow;
+  const int64_t bm = narrow ? 256 : 128, bn = narrow ? 64 : 128;
+  const int64_t tiles_m = ceil_div(M, bm), tiles_n = ceil_div(N, bn);
   GMP_CHECK_ARG(tiles_m < (1LL << 31) && tiles_n < (1LL << 31));
   const int64_t nwg = tiles_m * tiles_n;
   GMP_CHECK_ARG(nwg < (1LL << 32));
-  const size_t smem = 2 * (size_t)(NP * kPlane) + (NP == 2 ? kBM * sizeof(int) : 0);
+  const size_t smem = 2 * (size_t)(3 * bm * 64);
   int rc = 0;
-  auto k = g_tpgemm_ring == 44  ? (accumulate ? tp_gemm_x3_kernel<true, NP, 4, 4>
-                                              : tp_gemm_x3_kernel<false, NP, 4, 4>)
-           : g_tpgemm_ring >= 8 ? (accumulate ? tp_gemm_x3_kernel<true, NP, 8>
-                                              : tp_gemm_x3_kernel<false, NP, 8>)
-           : g_tpgemm_ring >= 4 ? (accumulate ? tp_gemm_x3_kernel<true, NP, 4>
-                                              : tp_gemm_x3_kernel<false, NP, 4>)
-                                : (accumulate ? tp_gemm_x3_kernel<true, NP, 2>
-                                              : tp_gemm_x3_kernel<false, NP, 2>);
+  decltype(&tp_gemm_x3_kernel<true, 8, 2, 2>) k;
+  if (narrow) {  // 4 A units per thread: a 4-deep ring holds the same bytes as 8 x 2
+    k = accumulate ? tp_gemm_x3_kernel<true, 4, 2, 4> : tp_gemm_x3_kernel<false, 4, 2, 4>;
+  } else {
+    k = g_tpgemm_ring == 44  ? (accumulate ? tp_gemm_x3_kernel<true, 4, 4, 2>
+                                           : tp_gemm_x3_kernel<false, 4, 4, 2>)
+        : g_tpgemm_ring >= 8 ? (accumulate ? tp_gemm_x3_kernel<true, 8, 2, 2>
+                                           : tp_gemm_x3_kernel<false, 8, 2, 2>)
+        : g_tpgemm_ring >= 4 ? (accumulate ? tp_gemm_x3_kernel<true, 4, 2, 2>
+                                           : tp_gemm_x3_kernel<false, 4, 2, 2>)
+                             : (accumulate ? tp_gemm_x3_kernel<true, 2, 2, 2>
+                                           : tp_gemm_x3_kernel<false, 2, 2, 2>);
+  }
   if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)smem))))
@@ -660,7 +669,7 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   k<<<(unsigned)nwg, kGT, smem, as_stream(stream)>>>(
       M, (int)N, K1, A1, lda1, K2, K2 ? A2 : A1, K2 ? lda2 : lda1,
       static_cast<const unsigned short*>(Bp), ldb, bplane, C, cgrp, cldg, cldr, cldn,
-      (int)tiles_m, (int)tiles_n, arow, (int)nparts, wmax);
+      (int)tiles_m, (int)tiles_n);
   return launch_status();
 }
 
@@ -727,8 +736,8 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
                        int64_t K2, const float* A2, int64_t lda2, const void* Bp, int64_t ldb,
                        int64_t bplane, float* C, int64_t cgrp, int64_t cldg, int64_t cldr,
                        int64_t cldn, int accumulate, void* stream) {
-  return gemm_launch<3>(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, nullptr, 0, nullptr,
-                        C, cgrp, cldg, cldr, cldn, accumulate, stream);
+  return gemm_launch(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, C, cgrp, cldg, cldr,
+                     cldn, accumulate, stream);
 }
 
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,

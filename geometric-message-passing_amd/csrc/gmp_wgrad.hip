@@ -790,7 +790,10 @@ int rect_bucket(int64_t m, int64_t n) {
 
 int64_t blocks_for(int64_t K) {
   int64_t g = capped((int64_t)device_cu_count() * 2);  // two resident workgroups per CU
-  const int64_t min_per = 4 * kKT;
+  // >= 16 edge tiles per workgroup: a node-level sum (K = 50k rows) then takes ~100 CUs and
+  // writes ~100 partial slabs instead of 391 (r03 trace: the 391-slab form and its reduction
+  // held the side stream 3.3 ms per EGNN step, beside the critical path's kernels)
+  const int64_t min_per = 16 * kKT;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
 }
@@ -906,7 +909,7 @@ int gmp_edge_outer_sum_act_hf_f32(int64_t K, int64_t d, const float* A, const fl
 
 int64_t rect_blocks_for(int64_t K) {
   int64_t g = capped((int64_t)device_cu_count() * 2);
-  const int64_t min_per = 4 * kKT;
+  const int64_t min_per = 16 * kKT;  // as blocks_for
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
 }

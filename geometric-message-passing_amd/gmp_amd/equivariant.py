@@ -548,12 +548,10 @@ def node_form_ok(hidden):
 # splits; dW2p by the column-block split-plane outer sum), "torch" = the library f32 GEMMs.
 TP_GEMM = os.environ.get("GMP_TP_GEMM", "x3")
 def _x3_ok(P, H):
-    """Shapes K7g covers (every k range a multiple of the 32-deep MFMA step, mul_out <= 128) and
-    where it pays: wide paths (mul1 mul_out >= 128 x 128, C4 MACE: 2.66 -> 2.41 s/step); on the
-    64 x 64 paths of C5 TFN the library f32 GEMMs measured faster (1.234 vs 1.270 s/step)."""
+    """Shapes K7g covers: every k range a multiple of the 32-deep MFMA step and mul_out <= 128
+    (128 x 128 output tiles; 256 x 64 for the 64-channel paths of config C5)."""
     return (TP_GEMM == "x3" and P["mul1"] % 32 == 0 and P["mul_out"] % 32 == 0
-            and P["mul_out"] <= 128 and H % 32 == 0
-            and P["mul1"] * P["mul_out"] >= 128 * 128)
+            and P["mul_out"] <= 128 and H % 32 == 0)
 
 
 def _split_w2(W2, b2, P, fwd):
@@ -654,11 +652,15 @@ class TPConvNodeFn(torch.autograd.Function):
                     with _timed("tp_node_dW"):
                         # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
                         part = tops.outer_sum_cols(S.view(c * d3, K1), G)
+                        # db2p[u, w] = sum_(n, k) Sb[(n, k), u] G[(n, k), w]: the deterministic
+                        # outer sum (the library's K = 250k reduction GEMM ran 0.4 ms per path)
+                        pb, _ = ops.edge_outer_sum_rect(Sb.view(c * d3, m1), G)
                         if first:
                             dW2p.copy_(part)
+                            db2p.copy_(pb)
                         else:
                             dW2p.add_(part)
-                        db2p.addmm_(Sb.view(c * d3, -1).t(), G)
+                            db2p.add_(pb)
                     del S, Sb
                     if Bts[i] is None:
                         Bts[i] = _split_w2(W2c, b2c, P, False)
@@ -686,8 +688,10 @@ class TPConvNodeFn(torch.autograd.Function):
                 dY[e0:e1] = dYc
             dpre = da * (pre > 0)
             r = rad_s[e0:e1]
-            dW1.addmm_(dpre.t(), r)
-            db1.add_(dpre.sum(0))
+            # dW1 = dpre^T r, db1 = colsum(dpre): one deterministic edge outer sum over E rows
+            gw1, gb1 = ops.edge_outer_sum_rect(dpre, r)
+            dW1.add_(gw1)
+            db1.add_(gb1)
             drad_s[e0:e1] = dpre.mm(W1)
         dW2, db2 = torch.empty_like(W2), torch.empty_like(b2)
         for P, (gw, gb) in zip(plan.instructions, dW2x):

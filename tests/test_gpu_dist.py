@@ -15,8 +15,9 @@ all-reduce sums two per-rank gradients exactly as the single process accumulates
 by 1/2 is exact).  Parameters after two Adam steps: bitwise equal for the executor; under DDP
 the second step's gradients were measured to differ in the last bits (max 3e-7 on the
 parameters), which Adam's per-coordinate normalisation amplifies where a gradient coordinate
-is near zero (one of 32,896 entries: 1.4e-5 after two lr = 1e-2 steps) — the parameter check
-therefore allows 1e-4 absolute (1 % of one Adam step).
+is near zero (one of 32,896 entries: 1.4e-5 after two lr = 1e-2 steps; at C5's widths 1.1e-4) —
+the DDP parameter check therefore allows 5e-4 absolute (5 % of one Adam step) and requires all
+but 0.1 % of the coordinates to agree to 1e-5.
 Multi-GPU scaling itself is unmeasured on hardware here (the driver owns 8-GPU runs)."""
 import os
 import socket
@@ -160,7 +161,16 @@ def test_product_world2_gloo_on_gpu_matches_single_process(kind, mode):
             got = res[r]["params"][k]
             err = (got - p).abs().max().item()
             print(f"param {k} rank {r}: max|d| {err:.3e}")
-            torch.testing.assert_close(got, p, atol=1e-4 if mode == "ddp" else 1e-5, rtol=1e-5)
+            if mode == "ddp":
+                # DDP's bucketed all-reduce reorders the second step's sums (last-bit gradient
+                # differences); Adam's g / sqrt(v) amplifies them at coordinates whose gradient
+                # is near zero.  Bound: 5 % of one lr = 1e-2 step anywhere, and f32-close on all
+                # but a sliver of the coordinates (C5 widths: 5.2M weights in one layer)
+                d = (got - p).abs()
+                assert err <= 5e-4, (k, r, err)
+                assert (d > 1e-5 + 1e-5 * p.abs()).float().mean().item() < 1e-3, (k, r)
+            else:
+                torch.testing.assert_close(got, p, atol=1e-5, rtol=1e-5)
         moved += int(not torch.equal(p, _init_cpu(kind)[k]))
     assert moved > len(ref["params"]) // 2  # the steps really trained (not vacuous)
 

@@ -122,13 +122,15 @@ def test_split_w2_planes_exact(m1, mo, H):
 @pytest.mark.parametrize("ring", [8, 4, 44, 2])
 @pytest.mark.parametrize("M,N,K1,K2,grp", [(1000, 128, 256, 32, 5), (333, 64, 128, 0, 1),
                                            (257, 4096, 128, 0, 1), (130, 128, 4096, 128, 3),
-                                           (65, 32, 96, 32, 1)])
+                                           (65, 32, 96, 32, 1), (5003, 64, 1024, 64, 3),
+                                           (700, 48, 256, 32, 5)])
 def test_tp_gemm_x3_matches_fp64(M, N, K1, K2, grp, ring):
     """gmp_tp_gemm_x3_f32 (bf16 MFMA over three-plane splits) against fp64: error per entry
     <= 1e-6 of sum |a b| (f32-class; f32 unit roundoff 6e-8, a K-term f32 sum ~ sqrt(K) of it),
     ragged M / N tiles, the second A operand, the grouped (r / grp) epilogue addressing with
     accumulation into an existing output; every register-ring depth (k-step counts that are and
-    are not multiples of the ring: 9, 4 and 132 steps)."""
+    are not multiples of the ring: 9, 4 and 132 steps); N <= 64 runs the 256 x 64 tile (C5's
+    64-channel paths; ragged rows of its 256-row tile)."""
     from gmp_amd import _lib
     old_rings = _lib.load().gmp_tp_gemm_set_rings(ring, 4)
     try:
