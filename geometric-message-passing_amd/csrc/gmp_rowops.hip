@@ -205,9 +205,11 @@ __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __rest
   }
 }
 
+// backward grid cap (GMP_LN_BWD_BLOCKS; A/B)
+int g_ln_blocks = getenv("GMP_LN_BWD_BLOCKS") ? atoi(getenv("GMP_LN_BWD_BLOCKS")) : kRowBlocks;
 int bwd_blocks(int64_t rows) {
   const int64_t b = ceil_div(rows, kRowT / 64);
-  return (int)(b < kRowBlocks ? (b < 1 ? 1 : b) : kRowBlocks);
+  return (int)(b < g_ln_blocks ? (b < 1 ? 1 : b) : g_ln_blocks);
 }
 
 }  // namespace

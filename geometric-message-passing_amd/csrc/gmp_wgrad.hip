@@ -669,6 +669,8 @@ bool wgrad_f32_mfma() {
 // side-stream weight gradients leave CUs free for the critical path's node-level kernels.
 int g_grid_cap = 0;
 int64_t capped(int64_t g) { return g_grid_cap > 0 && g > g_grid_cap ? g_grid_cap : g; }
+// minimum edge tiles per workgroup of the f32-MFMA split-K sums (GMP_WGRAD_MIN_TILES; A/B)
+int g_min_tiles = getenv("GMP_WGRAD_MIN_TILES") ? atoi(getenv("GMP_WGRAD_MIN_TILES")) : 16;
 
 int64_t x3_blocks_for(int64_t K) {
   int64_t g = capped((int64_t)device_cu_count());  // one 8-wave workgroup per CU (LDS ~100 KB)
@@ -793,7 +795,7 @@ int64_t blocks_for(int64_t K) {
   // >= 16 edge tiles per workgroup: a node-level sum (K = 50k rows) then takes ~100 CUs and
   // writes ~100 partial slabs instead of 391 (r03 trace: the 391-slab form and its reduction
   // held the side stream 3.3 ms per EGNN step, beside the critical path's kernels)
-  const int64_t min_per = 16 * kKT;
+  const int64_t min_per = g_min_tiles * kKT;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
 }
@@ -909,7 +911,7 @@ int gmp_edge_outer_sum_act_hf_f32(int64_t K, int64_t d, const float* A, const fl
 
 int64_t rect_blocks_for(int64_t K) {
   int64_t g = capped((int64_t)device_cu_count() * 2);
-  const int64_t min_per = 16 * kKT;  // as blocks_for
+  const int64_t min_per = g_min_tiles * kKT;  // as blocks_for
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
 }
