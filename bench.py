@@ -73,7 +73,7 @@ def parse():
                          "would), so the receiver / sender CSRs (K0) are rebuilt inside the "
                          "timed steps instead of coming from the per-graph cache")
     ap.add_argument("--blas", default=os.environ.get("GMP_BLAS", "default"),
-                    choices=("default", "hipblaslt", "rocblas"),
+                    choices=("default", "hipblaslt", "hipblas"),
                     help="library for the node-level PyTorch GEMMs (torch.backends.cuda."
                          "preferred_blas_library)")
     ap.add_argument("--timing-steps", type=int, default=2,

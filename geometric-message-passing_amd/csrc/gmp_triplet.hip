@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kFB) void triplet_fill_kernel(
     const int64_t* __restrict__ arow, const int64_t* __restrict__ asrc,
     const int64_t* __restrict__ aeid, const int64_t* __restrict__ offs, int mode,
     int64_t* __restrict__ idx_kj, int64_t* __restrict__ idx_ji, float* __restrict__ angle,
-    float* __restrict__ torsion) {
+    float* __restrict__ torsion, int64_t* __restrict__ torsion_kn) {
   __shared__ int64_t s_off[kFB + 1];
   __shared__ int64_t s_i[kFB], s_j[kFB], s_r0[kFB], s_r1[kFB], s_p[kFB], s_q[kFB];
   const int64_t e0 = (int64_t)blockIdx.x * kFB;
@@ -158,6 +158,7 @@ __global__ __launch_bounds__(kFB) void triplet_fill_kernel(
       const float dji = len3(vji);
       const V3 plane1 = cross3(vji, vj0);
       float best = 3.402823466e38f;  // torch_scatter min: identity FLT_MAX, NaN never wins
+      int64_t arg = -1;                // the winning candidate k_n (first among equal minima)
       for (int64_t m = r0; m < r1; ++m) {
         const int64_t kn = asrc[m];
         if (kn == i) continue;
@@ -167,9 +168,13 @@ __global__ __launch_bounds__(kFB) void triplet_fill_kernel(
         const float b = __fdiv_rn(dot3(cross3(plane1, plane2), vji), dji);
         float t1 = atan2f(b, a);
         if (t1 <= 0.f) t1 = __fadd_rn(t1, kTwoPi);
-        if (t1 < best) best = t1;
+        if (t1 < best) {
+          best = t1;
+          arg = kn;
+        }
       }
       torsion[t] = best == 3.402823466e38f ? 0.f : best;
+      if (torsion_kn) torsion_kn[t] = arg;
     }
   }
 }
@@ -247,6 +252,66 @@ __global__ void triplet_geom_bwd_kernel(const float* __restrict__ pos,
   }
 }
 
+// Backward of the SphereNet torsion w.r.t. pos (spherenet_layer.py:535-559 under autograd): the
+// scatter-min routes the gradient to the winning candidate k_n (torch_scatter's arg), whose
+// torsion1 = atan2(b, a) with u = p_i - p_j, v = p_k - p_j, w = p_kn - p_j,
+//   P = u x v, Q = u x w, a = P.Q, R = P x Q, c = R.u, L = |u|, b = c / L
+// (the 2 pi shift of torsion1 <= 0 has unit derivative).  Reverse mode:
+//   ga = -g b / (a^2 + b^2), gb = g a / (a^2 + b^2), gc = gb / L, gL = -gb c / L^2;
+//   gu = gL u / L + gc R;  gR = gc u;  gP = Q x gR + ga Q;  gQ = gR x P + ga P;
+//   gu += v x gP + w x gQ;  gv = gP x u;  gw = gQ x u;
+// rows [0, T) at i (gu), [T, 2T) at j (-(gu + gv + gw)), [2T, 3T) at k (gv), [3T, 4T) at k_n (gw);
+// triplets without a candidate (k_n < 0) write zero rows.
+__device__ __forceinline__ V3 xf(V3 a, V3 b) {
+  return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__global__ void triplet_torsion_bwd_kernel(const float* __restrict__ pos,
+                                           const int64_t* __restrict__ ei, int64_t E,
+                                           const int64_t* __restrict__ idx_kj,
+                                           const int64_t* __restrict__ idx_ji,
+                                           const int64_t* __restrict__ kn_of, int64_t T,
+                                           const float* __restrict__ g_tor,
+                                           float* __restrict__ rows, int64_t* __restrict__ node) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < T;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = idx_ji[t];
+    const int64_t j = ei[e], i = ei[E + e], k = ei[idx_kj[t]], kn = kn_of[t];
+    const float g = g_tor[t];
+    V3 gu{0.f, 0.f, 0.f}, gv{0.f, 0.f, 0.f}, gw{0.f, 0.f, 0.f};
+    if (kn >= 0 && g != 0.f) {
+      const V3 pj = ld3(pos, j);
+      const V3 u = sub3(ld3(pos, i), pj), v = sub3(ld3(pos, k), pj), w = sub3(ld3(pos, kn), pj);
+      const V3 P = cross3(u, v), Q = cross3(u, w), R = cross3(P, Q);
+      const float a = dot3(P, Q), c = dot3(R, u), L = len3(u);
+      const float b = c / L;
+      const float den = a * a + b * b;
+      const float ga = -g * b / den, gb = g * a / den;
+      const float gc = gb / L, gL = -gb * c / (L * L);
+      gu = V3{gL * u.x / L + gc * R.x, gL * u.y / L + gc * R.y, gL * u.z / L + gc * R.z};
+      const V3 gR{gc * u.x, gc * u.y, gc * u.z};
+      V3 gP = xf(Q, gR), gQ = xf(gR, P);
+      gP = V3{gP.x + ga * Q.x, gP.y + ga * Q.y, gP.z + ga * Q.z};
+      gQ = V3{gQ.x + ga * P.x, gQ.y + ga * P.y, gQ.z + ga * P.z};
+      const V3 a1 = xf(v, gP), a2 = xf(w, gQ);
+      gu = V3{gu.x + a1.x + a2.x, gu.y + a1.y + a2.y, gu.z + a1.z + a2.z};
+      gv = xf(gP, u);
+      gw = xf(gQ, u);
+    }
+    float* r = rows + 3 * t;
+    r[0] = gu.x; r[1] = gu.y; r[2] = gu.z;
+    r = rows + 3 * (T + t);
+    r[0] = -(gu.x + gv.x + gw.x); r[1] = -(gu.y + gv.y + gw.y); r[2] = -(gu.z + gv.z + gw.z);
+    r = rows + 3 * (2 * T + t);
+    r[0] = gv.x; r[1] = gv.y; r[2] = gv.z;
+    r = rows + 3 * (3 * T + t);
+    r[0] = gw.x; r[1] = gw.y; r[2] = gw.z;
+    node[t] = i;
+    node[T + t] = j;
+    node[2 * T + t] = k;
+    node[3 * T + t] = kn >= 0 ? kn : i;
+  }
+}
+
 }  // namespace
 }  // namespace gmp
 
@@ -269,15 +334,16 @@ int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_
                          int64_t n_nodes, const int64_t* adj_rowptr, const int64_t* adj_src,
                          const int64_t* adj_eid, const int64_t* offsets, int64_t n_triplets,
                          int mode, int64_t* idx_kj, int64_t* idx_ji, float* angle,
-                         float* torsion, void* stream) {
+                         float* torsion, int64_t* torsion_kn, void* stream) {
   GMP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && n_triplets >= 0 && (mode == 0 || mode == 1));
   GMP_CHECK_ARG(mode == 0 || !torsion);
+  GMP_CHECK_ARG(!torsion_kn || torsion);
   if (n_triplets == 0) return GMP_OK;
   GMP_CHECK_ARG(n_edges > 0 && edge_index && adj_rowptr && adj_src && adj_eid && offsets &&
                 idx_kj && idx_ji && (pos || (!angle && !torsion)));
   triplet_fill_kernel<<<(unsigned)ceil_div(n_edges, kFB), kFB, 0, as_stream(stream)>>>(
       pos, edge_index, n_edges, adj_rowptr, adj_src, adj_eid, offsets, mode, idx_kj, idx_ji,
-      angle, torsion);
+      angle, torsion, torsion_kn);
   return launch_status();
 }
 
@@ -291,6 +357,20 @@ int gmp_triplet_geom_bwd_f32(const float* pos, const int64_t* edge_index, int64_
   triplet_geom_bwd_kernel<<<grid_for(n_edges + n_triplets), 256, 0, as_stream(stream)>>>(
       pos, edge_index, n_edges, idx_kj, idx_ji, n_triplets, mode, grad_dist, grad_angle, rows,
       node);
+  return launch_status();
+}
+
+int gmp_triplet_torsion_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                const int64_t* idx_kj, const int64_t* idx_ji,
+                                const int64_t* torsion_kn, int64_t n_triplets,
+                                const float* grad_torsion, float* rows, int64_t* node,
+                                void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && n_triplets >= 0);
+  if (n_triplets == 0) return GMP_OK;
+  GMP_CHECK_ARG(pos && edge_index && idx_kj && idx_ji && torsion_kn && grad_torsion && rows &&
+                node);
+  triplet_torsion_bwd_kernel<<<grid_for(n_triplets), 256, 0, as_stream(stream)>>>(
+      pos, edge_index, n_edges, idx_kj, idx_ji, torsion_kn, n_triplets, grad_torsion, rows, node);
   return launch_status();
 }
 

@@ -150,7 +150,9 @@ SIGNATURES = {
     "gmp_batch_collate": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "gmp_triplet_count": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_triplet_fill_f32": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
-                                     c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                     c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_triplet_torsion_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                            c_vp, c_vp, c_vp]),
     "gmp_ln_act_fwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_int, c_vp, c_vp,
                                    c_vp, c_vp]),
     "gmp_ln_act_bwd_workspace_size": (c_size, [c_i64, c_i64]),

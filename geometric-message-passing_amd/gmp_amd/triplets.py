@@ -11,8 +11,10 @@ torsions) in one pass, in the reference's order.
 Distances and angles are differentiable w.r.t. `pos` (PyG DimeNet differentiates its angles,
 dimenet.py:79-90, e.g. for forces): the backward kernel gmp_triplet_geom_bwd_f32 writes one
 gradient row per (triplet, corner) and per (edge, end), summed per node over a CSR
-(deterministic).  The SphereNet torsion (a scatter-min over candidates) has no backward: asking
-for it with a `pos` that requires grad raises.
+(deterministic).  The SphereNet torsion (a scatter-min over candidates k_n,
+spherenet_layer.py:535-559) is differentiable too: the fill kernel records the winning k_n of
+every triplet and gmp_triplet_torsion_bwd_f32 routes the gradient to that candidate only, as
+torch_scatter's scatter_min backward does (first index among equal minima).
 """
 import torch
 
@@ -29,7 +31,7 @@ def adjacency_by_target(edge_index, num_nodes):
     return by_dst.rowptr, src[order], order
 
 
-def _run(pos, edge_index, num_nodes, mode, want_angle, want_torsion, want_dist):
+def _run(pos, edge_index, num_nodes, mode, want_angle, want_torsion, want_dist, want_kn=False):
     lib = _lib.load()
     ei = ops._i64c(edge_index)
     ops._need_cuda(ei)
@@ -52,64 +54,75 @@ def _run(pos, edge_index, num_nodes, mode, want_angle, want_torsion, want_dist):
     idx_ji = torch.empty(T, dtype=torch.int64, device=dev)
     angle = torch.empty(T, dtype=torch.float32, device=dev) if want_angle else None
     torsion = torch.empty(T, dtype=torch.float32, device=dev) if want_torsion else None
+    kn = torch.empty(T, dtype=torch.int64, device=dev) if want_kn else None
     ops.check(lib.gmp_triplet_fill_f32(ops._p(pos), ops._p(ei), E, N, ops._p(rowptr),
                                        ops._p(asrc), ops._p(aeid), ops._p(offs), T, mode,
                                        ops._p(idx_kj), ops._p(idx_ji), ops._p(angle),
-                                       ops._p(torsion), s), "gmp_triplet_fill_f32")
+                                       ops._p(torsion), ops._p(kn), s), "gmp_triplet_fill_f32")
+    if want_kn:
+        return dist, angle, torsion, idx_kj, idx_ji, kn
     return dist, angle, torsion, idx_kj, idx_ji
 
 
 class TripletGeomFn(torch.autograd.Function):
-    """(dist (E), angle (T), idx_kj, idx_ji) with the backward of dist and angle w.r.t. pos."""
+    """(dist (E), angle (T), torsion (T, or empty without use_torsion), idx_kj, idx_ji) with the
+    backward of dist, angle and torsion w.r.t. pos."""
 
     @staticmethod
-    def forward(ctx, pos, edge_index, num_nodes, mode):
-        dist, angle, _, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, mode, True, False, True)
-        ctx.save_for_backward(pos, ops._i64c(edge_index), idx_kj, idx_ji)
-        ctx.mode, ctx.n = mode, int(num_nodes)
+    def forward(ctx, pos, edge_index, num_nodes, mode, use_torsion):
+        res = _run(pos, edge_index, num_nodes, mode, True, use_torsion, True, use_torsion)
+        dist, angle, torsion, idx_kj, idx_ji = res[:5]
+        kn = res[5] if use_torsion else None
+        if torsion is None:
+            torsion = torch.empty(0, dtype=torch.float32, device=dist.device)
+            kn = torch.empty(0, dtype=torch.int64, device=dist.device)
+        ctx.save_for_backward(pos, ops._i64c(edge_index), idx_kj, idx_ji, kn)
+        ctx.mode, ctx.n, ctx.use_torsion = mode, int(num_nodes), use_torsion
         ctx.mark_non_differentiable(idx_kj, idx_ji)
-        return dist, angle, idx_kj, idx_ji
+        return dist, angle, torsion, idx_kj, idx_ji
 
     @staticmethod
-    def backward(ctx, g_dist, g_angle, _g1, _g2):
-        pos, ei, idx_kj, idx_ji = ctx.saved_tensors
+    def backward(ctx, g_dist, g_angle, g_torsion, _g1, _g2):
+        pos, ei, idx_kj, idx_ji, kn = ctx.saved_tensors
         if not ctx.needs_input_grad[0]:
-            return None, None, None, None
+            return None, None, None, None, None
         E, T = ei.shape[1], idx_kj.numel()
         dev = pos.device
-        rows = torch.empty((3 * T + 2 * E, 3), dtype=torch.float32, device=dev)
-        node = torch.empty(3 * T + 2 * E, dtype=torch.int64, device=dev)
+        p32 = ops._f32c(pos.detach())
+        nt = 4 * T if (ctx.use_torsion and g_torsion is not None) else 0
+        rows = torch.empty((3 * T + 2 * E + nt, 3), dtype=torch.float32, device=dev)
+        node = torch.empty(3 * T + 2 * E + nt, dtype=torch.int64, device=dev)
         gd = ops._f32c(g_dist) if g_dist is not None else None
         ga = ops._f32c(g_angle) if g_angle is not None else None
         lib = _lib.load()
-        ops.check(lib.gmp_triplet_geom_bwd_f32(ops._p(ops._f32c(pos.detach())), ops._p(ei), E,
-                                               ops._p(idx_kj), ops._p(idx_ji), T, ctx.mode,
-                                               ops._p(gd), ops._p(ga), ops._p(rows),
-                                               ops._p(node), ops._stream()),
+        s = ops._stream()
+        ops.check(lib.gmp_triplet_geom_bwd_f32(ops._p(p32), ops._p(ei), E, ops._p(idx_kj),
+                                               ops._p(idx_ji), T, ctx.mode, ops._p(gd),
+                                               ops._p(ga), ops._p(rows), ops._p(node), s),
                   "gmp_triplet_geom_bwd_f32")
+        if nt:
+            m = 3 * T + 2 * E
+            ops.check(lib.gmp_triplet_torsion_bwd_f32(ops._p(p32), ops._p(ei), E,
+                                                      ops._p(idx_kj), ops._p(idx_ji),
+                                                      ops._p(kn), T,
+                                                      ops._p(ops._f32c(g_torsion)),
+                                                      ops._p(rows[m:]), ops._p(node[m:]), s),
+                      "gmp_triplet_torsion_bwd_f32")
         g_pos, _ = ops.segment_reduce(rows, ops.CSR(node, ctx.n), "sum")
-        return g_pos.to(pos.dtype), None, None, None
+        return g_pos.to(pos.dtype), None, None, None, None
 
 
-def _geom(pos, edge_index, num_nodes, mode):
+def _geom(pos, edge_index, num_nodes, mode, use_torsion=False):
     if pos.requires_grad and torch.is_grad_enabled():
-        return TripletGeomFn.apply(pos, edge_index, num_nodes, mode)
-    dist, angle, _, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, mode, True, False, True)
-    return dist, angle, idx_kj, idx_ji
+        return TripletGeomFn.apply(pos, edge_index, num_nodes, mode, use_torsion)
+    return _run(pos, edge_index, num_nodes, mode, True, use_torsion, True)
 
 
 def xyz_to_dat(pos, edge_index, num_nodes, use_torsion=False):
     """spherenet_layer.py:496: -> dist, angle, [torsion,] i, j, idx_kj, idx_ji (edge e = j -> i;
-    angle in [0, pi] at j; torsion in (0, 2*pi]).  dist and angle are differentiable w.r.t.
-    pos; the torsion is not (raises if pos requires grad)."""
-    if use_torsion and pos.requires_grad and torch.is_grad_enabled():
-        raise NotImplementedError("the SphereNet torsion has no backward; detach pos")
-    if use_torsion:
-        dist, angle, torsion, idx_kj, idx_ji = _run(pos, edge_index, num_nodes, 0, True, True,
-                                                    True)
-    else:
-        dist, angle, idx_kj, idx_ji = _geom(pos, edge_index, num_nodes, 0)
-        torsion = None
+    angle in [0, pi] at j; torsion in (0, 2*pi]).  dist, angle and torsion are differentiable
+    w.r.t. pos."""
+    dist, angle, torsion, idx_kj, idx_ji = _geom(pos, edge_index, num_nodes, 0, use_torsion)
     j, i = edge_index
     if use_torsion:
         return dist, angle, torsion, i, j, idx_kj, idx_ji
@@ -127,6 +140,6 @@ def dimenet_triplets(edge_index, num_nodes):
 def dimenet_angles(pos, edge_index, num_nodes):
     """dimenet.py:79-90: -> dist (E), angle (T, vertex i), i, j, idx_i, idx_j, idx_k, idx_kj,
     idx_ji."""
-    dist, angle, idx_kj, idx_ji = _geom(pos, edge_index, num_nodes, 1)
+    dist, angle, _, idx_kj, idx_ji = _geom(pos, edge_index, num_nodes, 1)
     row, col = edge_index
     return (dist, angle, col, row, col[idx_ji], row[idx_ji], row[idx_kj], idx_kj, idx_ji)

@@ -508,7 +508,7 @@ int gmp_triplet_fill_f32(const float* pos, const int64_t* edge_index, int64_t n_
                          int64_t n_nodes, const int64_t* adj_rowptr, const int64_t* adj_src,
                          const int64_t* adj_eid, const int64_t* offsets, int64_t n_triplets,
                          int mode, int64_t* idx_kj, int64_t* idx_ji, float* angle,
-                         float* torsion, void* stream);
+                         float* torsion, int64_t* torsion_kn, void* stream);
 /* Backward of dist (E) and angle (T) w.r.t. pos (DimeNet / SphereNet under autograd): writes
  * 3T + 2E rows of 3 floats (`rows`) and their node ids (`node`): vertex, u-end and v-end rows
  * of every triplet, then +/- rows of every edge's distance; d pos = the segmented sum of rows
@@ -517,6 +517,15 @@ int gmp_triplet_geom_bwd_f32(const float* pos, const int64_t* edge_index, int64_
                              const int64_t* idx_kj, const int64_t* idx_ji, int64_t n_triplets,
                              int mode, const float* grad_dist, const float* grad_angle,
                              float* rows, int64_t* node, void* stream);
+/* Backward of the SphereNet torsion (spherenet_layer.py:535-559 under autograd) w.r.t. pos:
+ * torsion_kn (T, from gmp_triplet_fill_f32; -1 = no candidate) is the scatter-min's winning
+ * k_n, which alone receives the gradient (torch_scatter's arg routing).  Writes 4T rows of 3
+ * floats and their node ids (i, j, k, k_n blocks of T); d pos = their segmented sum by node. */
+int gmp_triplet_torsion_bwd_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                const int64_t* idx_kj, const int64_t* idx_ji,
+                                const int64_t* torsion_kn, int64_t n_triplets,
+                                const float* grad_torsion, float* rows, int64_t* node,
+                                void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K12 fused LayerNorm + activation over rows (node-level MLPs: EGNN mlp_upd,

@@ -73,10 +73,56 @@ def xyz_to_dat(pos, edge_index, num_nodes, use_torsion=False):
     # torch_scatter min: rows = max(index) + 1, untouched rows 0, NaN never wins
     n = int(t_of.max()) + 1 if t_of.numel() else 0
     big = torch.finfo(torch.float32).max
-    torsion = torch.full((n,), big).scatter_reduce(0, t_of, torch.nan_to_num(torsion1, nan=big),
+    torsion = torch.full((n,), big, dtype=torsion1.dtype).scatter_reduce(0, t_of, torch.nan_to_num(torsion1, nan=big),
                                                    "amin", include_self=True)
     torsion[torsion == big] = 0
     return dist, angle, torsion, i, j, idx_kj, idx_ji
+
+
+def torsion_with_scatter_min_grad(pos, edge_index, num_nodes):
+    """The torsion of xyz_to_dat (spherenet_layer.py:535-559) as a differentiable function of
+    pos with torch_scatter's scatter_min backward: the gradient of each triplet reaches only its
+    arg candidate (the first k_n among equal minima), untouched triplets get none.  (The
+    reference's scatter-min is torch_scatter's; torch's own scatter_reduce("amin") would split
+    ties and saves its output, so the in-place `torsion[torsion == big] = 0` above is not
+    differentiable through it.)"""
+    idx_i, idx_j, idx_k, _, _ = triplets(edge_index, num_nodes)
+    rowptr, asrc, _ = adjacency_by_target(edge_index, num_nodes)
+    deg = rowptr[1:] - rowptr[:-1]
+    n_c = deg[idx_j]
+    t_of = torch.repeat_interleave(torch.arange(idx_i.numel()), n_c)
+    first = torch.repeat_interleave(torch.cumsum(n_c, 0) - n_c, n_c)
+    k_n = asrc[torch.repeat_interleave(rowptr[idx_j], n_c) + torch.arange(t_of.numel()) - first]
+    keep = idx_i[t_of] != k_n
+    t_of, k_n = t_of[keep], k_n[keep]
+    def t1_of(p, t, kn):
+        it, jt, kt = idx_i[t], idx_j[t], idx_k[t]
+        pos_ji = p[it] - p[jt]
+        plane1 = torch.cross(pos_ji, p[kt] - p[jt], dim=-1)
+        plane2 = torch.cross(pos_ji, p[kn] - p[jt], dim=-1)
+        a = (plane1 * plane2).sum(dim=-1)
+        b = ((torch.cross(plane1, plane2, dim=-1) * pos_ji).sum(dim=-1)
+             / pos_ji.pow(2).sum(-1).sqrt())
+        t1 = torch.atan2(b, a)
+        return torch.where(t1 <= 0, t1 + 2 * math.pi, t1)
+
+    # select the winners on detached values, then differentiate the winners only (a losing
+    # candidate may sit at atan2(0, 0), whose autograd is NaN even with a zero incoming grad)
+    T = idx_i.numel()
+    big = torch.finfo(torch.float32).max
+    v = torch.nan_to_num(t1_of(pos.detach(), t_of, k_n), nan=big)
+    mn = torch.full((T,), big, dtype=v.dtype).scatter_reduce(0, t_of, v, "amin",
+                                                             include_self=True)
+    m = torch.arange(t_of.numel())
+    cand = torch.where(v == mn[t_of], m, torch.full_like(m, t_of.numel()))
+    arg = torch.full((T,), t_of.numel()).scatter_reduce(0, t_of, cand, "amin",
+                                                        include_self=True)
+    has = ((arg < t_of.numel()) & (mn < big)).nonzero()[:, 0]
+    # values: the full-batch forward's (torch's CPU cross may round a re-evaluated subset
+    # differently); gradient: the winners' atan2 path
+    tw = t1_of(pos, t_of[arg[has]], k_n[arg[has]])
+    out = torch.zeros(T, dtype=pos.dtype)
+    return out.index_put((has,), v[arg[has]] + (tw - tw.detach()))
 
 
 def dimenet_angles(pos, edge_index, num_nodes):

@@ -149,12 +149,15 @@ def test_product_world2_gloo_on_gpu_matches_single_process(kind, mode):
                for r in range(world)]
         ref = torch.load(os.path.join(d, f"{mode}_ref.pt"), weights_only=True)
     # the first step's averaged gradients (what the collective delivered to the optimizer)
+    bad = []
     for k, g in ref["grads"].items():
         for r in range(world):
             got = res[r]["grads"].get(k, torch.zeros_like(g))
             err, scale = (got - g).abs().max().item(), g.abs().max().item()
             print(f"grad {k} rank {r}: max|d| {err:.3e} scale {scale:.3e}")
-            assert err <= 1e-5 * scale + 1e-7, (k, r, err, scale)
+            if err > 1e-5 * scale + 1e-7:
+                bad.append((k, r, err, scale))
+    assert not bad, bad
     moved = 0
     for k, p in ref["params"].items():
         for r in range(world):

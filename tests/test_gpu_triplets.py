@@ -87,8 +87,11 @@ def test_edge_cases():
     ref = o_xyz(pos, ei, 4, True)
     _check(out, ref, 3)
     assert out[1].numel() == 0
-    with pytest.raises(NotImplementedError):  # the torsion has no backward
-        xyz_to_dat(pos.to(DEV).requires_grad_(True), ei.to(DEV), 4, use_torsion=True)
+    # torsion under autograd with no triplets: zero gradient, no launch over empty arrays
+    pd = pos.to(DEV).requires_grad_(True)
+    out = xyz_to_dat(pd, ei.to(DEV), 4, use_torsion=True)
+    (out[0].sum() + out[2].sum()).backward()
+    assert pd.grad.shape == (4, 3) and bool(torch.isfinite(pd.grad).all())
 
 
 @pytest.mark.parametrize("mode", ["spherenet", "dimenet"])
@@ -119,6 +122,47 @@ def test_dist_angle_backward_vs_oracle(mode):
     pd.grad = None
     out = xyz_to_dat(pd, ei.to(DEV), n) if mode == "spherenet" else dimenet_angles(pd, ei.to(DEV), n)
     ((out[0] * gd.to(DEV)).sum() + (out[1] * ga.to(DEV)).sum()).backward()
+    assert torch.equal(g1, pd.grad)
+
+
+def test_torsion_backward_vs_oracle():
+    """d pos of sum(g_d dist) + sum(g_a angle) + sum(g_t torsion) with the torsion's
+    scatter-min backward (gmp_triplet_torsion_bwd_f32: the gradient reaches the winning k_n
+    only, spherenet_layer.py:535-559), against autograd through the oracle's torch ops with
+    torch_scatter's arg routing (oracle.triplets.torsion_with_scatter_min_grad).  The forward
+    torsions agree bit-for-bit, so both pick the same winners; tolerance 1e-4 of the gradient's
+    scale plus a 1e-3-of-scale bound at the few near-degenerate triplets (|a| + |b| tiny, where
+    atan2's derivative amplifies last-ulp differences)."""
+    from oracle.triplets import torsion_with_scatter_min_grad
+    from gmp_amd.triplets import xyz_to_dat
+    pos, ei = _graph(400, 6.5, 1.6, 13)
+    n = pos.shape[0]
+    pd = pos.to(DEV).requires_grad_(True)
+    pr = pos.clone().requires_grad_(True)
+    out = xyz_to_dat(pd, ei.to(DEV), n, use_torsion=True)
+    ref = o_xyz(pr.detach(), ei, n, True)
+    _check(out, ref, 3)
+    tr = torsion_with_scatter_min_grad(pr, ei, n)
+    assert torch.equal(tr.detach(), ref[2])
+    g = torch.Generator().manual_seed(2)
+    gd, ga, gt = (torch.randn(ref[k].shape, generator=g) for k in range(3))
+    ((out[0] * gd.to(DEV)).sum() + (out[1] * ga.to(DEV)).sum()
+     + (out[2] * gt.to(DEV)).sum()).backward()
+    d, a = o_xyz(pr, ei, n)[:2]
+    ((d * gd).sum() + (a * ga).sum() + (tr * gt).sum()).backward()
+    scale = pr.grad.abs().max().item()
+    err = (pd.grad.cpu() - pr.grad).abs()
+    assert err.max().item() <= 1e-3 * scale, (err.max().item(), scale)
+    assert (err > 1e-4 * scale).float().mean().item() < 0.01, err.max().item()
+    # only the torsion term: the gradient is non-trivial and deterministic
+    pd.grad = None
+    out = xyz_to_dat(pd, ei.to(DEV), n, use_torsion=True)
+    (out[2] * gt.to(DEV)).sum().backward()
+    g1 = pd.grad.clone()
+    assert g1.abs().max().item() > 0
+    pd.grad = None
+    out = xyz_to_dat(pd, ei.to(DEV), n, use_torsion=True)
+    (out[2] * gt.to(DEV)).sum().backward()
     assert torch.equal(g1, pd.grad)
 
 

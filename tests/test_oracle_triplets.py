@@ -46,3 +46,33 @@ def test_spherenet_angle_right_angle():
     ei = torch.tensor([[0, 1, 1, 2], [1, 0, 2, 1]])
     dist, angle, i, j, idx_kj, idx_ji = xyz_to_dat(pos, ei, 3)
     assert torch.allclose(angle, torch.full((2,), math.pi / 2))
+
+
+def test_oracle_torsion_gradient_matches_finite_differences():
+    """The torsion gradient restatement (arg routing of torch_scatter's scatter_min) has the
+    same values as xyz_to_dat and, in fp64 on a small graph, its Jacobian equals central finite
+    differences wherever the winning candidate does not change under the step (the k_n = k
+    candidate's torsion is a rounding residual whose sign flips under any perturbation, so
+    entries that jump are not derivatives)."""
+    from oracle.triplets import torsion_with_scatter_min_grad
+    g = torch.Generator().manual_seed(5)
+    pos = (torch.rand(24, 3, generator=g) * 2.5).double()
+    d = torch.cdist(pos, pos)
+    ei = torch.nonzero((d < 1.3) & (d > 0)).T.flip(0).contiguous()
+    t0 = torsion_with_scatter_min_grad(pos, ei, 24)
+    assert torch.equal(t0, xyz_to_dat(pos, ei, 24, use_torsion=True)[2])
+    J = torch.autograd.functional.jacobian(
+        lambda p: torsion_with_scatter_min_grad(p, ei, 24), pos).reshape(t0.numel(), -1)
+    h = 1e-6
+    n_ok = 0
+    for q in range(pos.numel()):
+        pp, pm = pos.clone().view(-1), pos.clone().view(-1)
+        pp[q] += h
+        pm[q] -= h
+        tp = torsion_with_scatter_min_grad(pp.view(24, 3), ei, 24)
+        tm = torsion_with_scatter_min_grad(pm.view(24, 3), ei, 24)
+        ok = ((tp - t0).abs() < 1e-4) & ((tm - t0).abs() < 1e-4) & (t0.abs() > 1e-9)
+        fd = (tp - tm) / (2 * h)
+        assert torch.allclose(J[ok, q], fd[ok], rtol=1e-4, atol=1e-5), q
+        n_ok += int(ok.sum())
+    assert n_ok > 0.5 * J.numel() * 0.5  # most entries checked
