@@ -30,6 +30,10 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // Number of CUs on the device the stream belongs to (cached per process; MI355X: 256).
 int device_cu_count();
 
+// A zeroed completion-ticket word for last-workgroup reductions on stream s (NULL if none can
+// be provided, e.g. during a graph capture before first use).
+unsigned* stream_ticket(hipStream_t s);
+
 }  // namespace gmp
 
 #define GMP_CHECK_ARG(cond) \

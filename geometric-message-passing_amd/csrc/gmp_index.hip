@@ -2,6 +2,10 @@
 // its backward.  All HBM-bound; see DESIGN.md §Kernels for the per-unit byte counts.
 #include <hipcub/hipcub.hpp>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "gmp_common.h"
 
 namespace gmp {
@@ -18,6 +22,35 @@ int device_cu_count() {
     if (cus <= 0) cus = 256;
   }
   return cus;
+}
+
+// Completion tickets of the kernels that end in a last-workgroup reduction: one zeroed word per
+// (device, stream), allocated on first use (kernels on one stream run in order, and the last
+// workgroup resets its ticket, so a word serves every later launch on that stream).
+unsigned* stream_ticket(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> slots;
+  static std::map<int, std::pair<unsigned*, int>> pools;  // device -> (64 words, next free)
+  constexpr int kSlots = 64;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = slots.find({dev, s});
+  if (it != slots.end()) return it->second;
+  auto& pool = pools[dev];
+  if (!pool.first) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      return nullptr;  // no allocation inside a capture: the caller uses its two-kernel form
+    unsigned* p = nullptr;
+    if (hipMalloc(&p, kSlots * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, kSlots * sizeof(unsigned)) != hipSuccess) return nullptr;
+    pool = {p, 0};
+  }
+  if (pool.second >= kSlots) return nullptr;
+  unsigned* t = pool.first + pool.second++;
+  slots[{dev, s}] = t;
+  return t;
 }
 
 namespace {

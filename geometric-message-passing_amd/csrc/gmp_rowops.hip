@@ -96,8 +96,10 @@ template <int ACT>
 __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
     int64_t rows, int d, const float* __restrict__ gy, const float* __restrict__ xhat,
     const float* __restrict__ rstd_in, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials) {
+    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials,
+    float* __restrict__ out_gb, unsigned* __restrict__ ticket) {
   __shared__ float red[kRowT / 64][2 * 512];
+  __shared__ unsigned is_last;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float dg[kMaxF], db[kMaxF];
 #pragma unroll
@@ -165,6 +167,30 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
     for (int w = 0; w < kRowT / 64; ++w) s += red[w][off];
     partials[(int64_t)blockIdx.x * 2 * d + f] = s;
   }
+  if (!out_gb) return;
+  // last-workgroup reduction (threadfence pattern): every workgroup publishes its partial row,
+  // takes a ticket; the last one adds the rows in workgroup order (deterministic) and resets
+  // the ticket for the next launch on this stream
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) is_last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  const int G = (int)gridDim.x;
+  for (int f = threadIdx.x; f < 2 * d; f += kRowT) {
+    float s = 0.f;
+    for (int g0 = 0; g0 < G; g0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = g0 + u < G ? partials[(int64_t)(g0 + u) * 2 * d + f] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (g0 + u < G) s += v[u];
+    }
+    out_gb[f] = s;
+  }
+  if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
 // out[f] = sum over the partial rows (f < 2d: [dgamma | dbeta]) in a fixed order: thread
@@ -205,6 +231,8 @@ __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __rest
   }
 }
 
+// [dgamma | dbeta] inside the backward kernel (last workgroup; GMP_LN_FUSED_SUM=0: sum_rows)
+int g_ln_fused_sum = getenv("GMP_LN_FUSED_SUM") ? atoi(getenv("GMP_LN_FUSED_SUM")) : 1;
 // backward grid cap (GMP_LN_BWD_BLOCKS; A/B)
 int g_ln_blocks = getenv("GMP_LN_BWD_BLOCKS") ? atoi(getenv("GMP_LN_BWD_BLOCKS")) : kRowBlocks;
 int bwd_blocks(int64_t rows) {
@@ -259,17 +287,21 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
   }
   GMP_CHECK_ARG(grad_y && xhat && rstd && gamma && beta && grad_x && workspace);
   if (workspace_bytes < gmp_ln_act_bwd_workspace_size(rows, d)) return GMP_ERR_WORKSPACE;
+  // [dgamma | dbeta] by the kernel's last workgroup when a ticket is available (one launch);
+  // otherwise (or GMP_LN_FUSED_SUM=0) the partial rows go through sum_rows_kernel
+  unsigned* ticket = (grad_gamma_beta && g_ln_fused_sum) ? stream_ticket(s) : nullptr;
+  float* ogb = ticket ? grad_gamma_beta : nullptr;
   if (act == 0)
     ln_act_bwd_kernel<0><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
-                                             grad_x, part);
+                                             grad_x, part, ogb, ticket);
   else if (act == 1)
     ln_act_bwd_kernel<1><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
-                                             grad_x, part);
+                                             grad_x, part, ogb, ticket);
   else
     ln_act_bwd_kernel<2><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
-                                             grad_x, part);
+                                             grad_x, part, ogb, ticket);
   int rc = launch_status();
-  if (rc || !grad_gamma_beta) return rc;  // NULL: the caller reduces the partial rows itself
+  if (rc || !grad_gamma_beta || ticket) return rc;  // NULL: the caller reduces the partials
   sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, G, (int)(2 * d),
                                                                        grad_gamma_beta);
   return launch_status();

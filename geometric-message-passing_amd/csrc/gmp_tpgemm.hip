@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
     const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
     int64_t ldb, int64_t bplane, float* __restrict__ C, int64_t cgrp, int64_t cldg,
-    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n) {
+    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const float* __restrict__ bias) {
   constexpr int NP = 3;
   constexpr int WGN = 8 / WGM;              // waves along N
   constexpr int BM = 64 * WGM, BN = 32 * WGN;
@@ -401,6 +401,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     for (int c = 0; c < 2; ++c) {
       const int64_t col = n0 + 32 * wn + 16 * c + li;
       if (col >= N) continue;
+      const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int lr = 64 * wm + 16 * r + 4 * g + q;
@@ -408,8 +409,8 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
         if (row >= M) continue;
         const int64_t grp_r = row / cgrp;
         float* dst = C + grp_r * cldg + (row - grp_r * cgrp) * cldr + col * cldn;
-        if (ACC) *dst += acc[r][c][q];
-        else *dst = acc[r][c][q];
+        if (ACC) *dst += acc[r][c][q] + bv;
+        else *dst = acc[r][c][q] + bv;
       }
     }
   }
@@ -597,6 +598,23 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
   }
 }
 
+// Planes of a general operand for the C = A B^T kernel: element (n, k) = src[n sn + k sk]
+// (sn = K, sk = 1: B row-major, e.g. a Linear weight W (out, in) for y = x W^T; sn = 1, sk = N:
+// its transpose, for dx = g W), written in fragment order (bfrag_index).  One thread per
+// element (the weights are KB-sized: one small launch per pass).
+__global__ __launch_bounds__(256) void split_x3_kernel(int64_t N, int64_t K,
+                                                       const float* __restrict__ src, int64_t sn,
+                                                       int64_t sk,
+                                                       unsigned short* __restrict__ Bp) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= N * K) return;
+  const int64_t n = x / K, k = x - n * K;
+  unsigned p[3];
+  split3(f32x2{src[n * sn + k * sk], 0.f}, p[0], p[1], p[2]);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) Bp[bfrag_index(q, n, k, N / 16, 3)] = (unsigned short)p[q];
+}
+
 }  // namespace
 }  // namespace gmp
 
@@ -629,7 +647,7 @@ int split_w2_launch(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p, 
 int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1, int64_t K2,
                 const float* A2, int64_t lda2, const void* Bp, int64_t ldb, int64_t bplane,
                 float* C, int64_t cgrp, int64_t cldg, int64_t cldr, int64_t cldn, int accumulate,
-                void* stream) {
+                void* stream, const float* bias = nullptr) {
   GMP_CHECK_ARG(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && cgrp >= 1);
   if (M == 0 || N == 0) return GMP_OK;
   GMP_CHECK_ARG(A1 && Bp && C && (K2 == 0 || A2));
@@ -650,7 +668,11 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   const size_t smem = 2 * (size_t)(3 * bm * 64);
   int rc = 0;
   decltype(&tp_gemm_x3_kernel<true, 8, 2, 2>) k;
-  if (narrow) {  // 4 A units per thread: a 4-deep ring holds the same bytes as 8 x 2
+  if ((K1 + K2) <= 8 * kBK && !narrow) {
+    // short k ranges (node-level Linears, K <= 256): a 2-deep A ring; the deep rings would only
+    // prefetch clamped copies of the last stage
+    k = accumulate ? tp_gemm_x3_kernel<true, 2, 2, 2> : tp_gemm_x3_kernel<false, 2, 2, 2>;
+  } else if (narrow) {  // 4 A units per thread: a 4-deep ring holds the same bytes as 8 x 2
     k = accumulate ? tp_gemm_x3_kernel<true, 4, 2, 4> : tp_gemm_x3_kernel<false, 4, 2, 4>;
   } else {
     k = g_tpgemm_ring == 44  ? (accumulate ? tp_gemm_x3_kernel<true, 4, 4, 2>
@@ -669,7 +691,7 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   k<<<(unsigned)nwg, kGT, smem, as_stream(stream)>>>(
       M, (int)N, K1, A1, lda1, K2, K2 ? A2 : A1, K2 ? lda2 : lda1,
       static_cast<const unsigned short*>(Bp), ldb, bplane, C, cgrp, cldg, cldr, cldn,
-      (int)tiles_m, (int)tiles_n);
+      (int)tiles_m, (int)tiles_n, bias);
   return launch_status();
 }
 
@@ -738,6 +760,24 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
                        int64_t cldn, int accumulate, void* stream) {
   return gemm_launch(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, C, cgrp, cldg, cldr,
                      cldn, accumulate, stream);
+}
+
+int gmp_split_x3_f32(int64_t N, int64_t K, const float* B, int64_t sn, int64_t sk, void* Bp,
+                     void* stream) {
+  GMP_CHECK_ARG(N >= 0 && K >= 0 && N % 16 == 0 && K % kBK == 0);
+  if (N == 0 || K == 0) return GMP_OK;
+  GMP_CHECK_ARG(B && Bp && sn >= 0 && sk >= 0);
+  split_x3_kernel<<<(unsigned)ceil_div(N * K, 256), 256, 0, as_stream(stream)>>>(
+      N, K, B, sn, sk, static_cast<unsigned short*>(Bp));
+  return launch_status();
+}
+
+int gmp_gemm_x3_f32(int64_t M, int64_t N, const float* A1, int64_t K1, int64_t lda1,
+                    const float* A2, int64_t K2, int64_t lda2, const void* Bp, const float* bias,
+                    float* C, int64_t ldc, int accumulate, void* stream) {
+  GMP_CHECK_ARG(ldc >= N);
+  return gemm_launch(M, N, K1, A1, lda1, K2, A2, lda2, Bp, K1 + K2, N * (K1 + K2), C, M > 0 ? M : 1,
+                     0, ldc, 1, accumulate, stream, bias);
 }
 
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,

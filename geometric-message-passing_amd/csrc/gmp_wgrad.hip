@@ -161,21 +161,22 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
 constexpr int kGC = 16;  // slab loads in flight per lane in the ordered partial sums
 
 // One-pass ordered sum of the G partial slabs (replaces l1 + l2 on the split-K paths): a
-// workgroup owns 64 columns x; its 4 waves each add a contiguous quarter of the slabs (slab
-// order, 16 loads in flight per lane), then wave 0 adds the 4 quarter sums in wave order --
-// a fixed order independent of timing (deterministic), 4 x the parallelism of l2 and one
-// launch instead of two.
-constexpr int kSumW = 4;
-__global__ __launch_bounds__(64 * kSumW) void sum_partials_one(const float* __restrict__ part,
-                                                               int64_t G, int64_t X,
-                                                               float* __restrict__ out,
-                                                               float* __restrict__ colsum,
-                                                               int64_t DD, int64_t n,
-                                                               int64_t ldc) {
-  __shared__ float red[kSumW][64];
+// workgroup owns 64 columns x; its SW waves each add a contiguous 1/SW of the slabs (slab
+// order, 16 loads in flight per lane), then wave 0 adds the SW partial sums in wave order -- a
+// fixed order independent of timing (deterministic).  SW = 16 (1024 threads): a 256-slab
+// reduction is ONE burst of loads per lane (4 waves took four dependent bursts: the r03 EGNN
+// trace had 2.2 ms of these sums per step on the side stream, latency-bound under the main
+// stream's HBM traffic).  GMP_SUM_WAVES=4 selects the r03 form.
+template <int SW>
+__global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restrict__ part,
+                                                            int64_t G, int64_t X,
+                                                            float* __restrict__ out,
+                                                            float* __restrict__ colsum,
+                                                            int64_t DD, int64_t n, int64_t ldc) {
+  __shared__ float red[SW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t x = blockIdx.x * (int64_t)64 + lane;
-  const int64_t q = (G + kSumW - 1) / kSumW, g0 = wv * q, g1 = (g0 + q < G) ? g0 + q : G;
+  const int64_t q = (G + SW - 1) / SW, g0 = wv * q, g1 = (g0 + q < G) ? g0 + q : G;
   float s = 0.f;
   if (x < X) {
     for (int64_t c0 = g0; c0 < g1; c0 += kGC) {
@@ -191,9 +192,21 @@ __global__ __launch_bounds__(64 * kSumW) void sum_partials_one(const float* __re
   __syncthreads();
   if (wv != 0 || x >= X) return;
 #pragma unroll
-  for (int w = 1; w < kSumW; ++w) s += red[w][lane];
+  for (int w = 1; w < SW; ++w) s += red[w][lane];
   if (x < DD) out[(x / n) * ldc + x % n] = s;
   else if (colsum) colsum[x - DD] = s;
+}
+
+int g_sum_waves = getenv("GMP_SUM_WAVES") ? atoi(getenv("GMP_SUM_WAVES")) : 16;
+
+// out (row stride ldc, n columns) = the ordered sum of G slabs of X = DD (+ colsum) floats
+void sum_partials(const float* part, int64_t G, int64_t X, float* out, float* colsum,
+                  int64_t DD, int64_t n, int64_t ldc, hipStream_t s) {
+  const unsigned grid = (unsigned)ceil_div(X, 64);
+  if (g_sum_waves == 4)
+    sum_partials_one<4><<<grid, 256, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
+  else
+    sum_partials_one<16><<<grid, 1024, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
 }
 
 // Rectangular variant for the other per-edge Linears (GVP message GVPs: 128 x 144, 128 x 80,
@@ -736,8 +749,7 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;
-  sum_partials_one<<<(unsigned)ceil_div(X, 64), 64 * kSumW, 0, s>>>(part, Gr, X, C, colsum_A,
-                                                                    m * n, n, ldc);
+  sum_partials(part, Gr, X, C, colsum_A, m * n, n, ldc, s);
   return launch_status();
 }
 
@@ -865,8 +877,7 @@ static int outer_sum_launch(int64_t K, int64_t d, const float* A, int64_t lda, c
   int rc = launch_status();
   if (rc) return rc;
   const int64_t X = d * d + d;
-  sum_partials_one<<<(unsigned)ceil_div(X, 64), 64 * kSumW, 0, s>>>(part, Gr, X, C, colsum_A,
-                                                                    d * d, d, ldc);
+  sum_partials(part, Gr, X, C, colsum_A, d * d, d, ldc, s);
   return launch_status();
 }
 
@@ -981,8 +992,7 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;
-  sum_partials_one<<<(unsigned)ceil_div(X, 64), 64 * kSumW, 0, s>>>(part, Gr, X, C, colsum_A,
-                                                                    m * n, n, ldc);
+  sum_partials(part, Gr, X, C, colsum_A, m * n, n, ldc, s);
   return launch_status();
 }
 

@@ -842,6 +842,55 @@ void tp_gemm_x3(const Tensor& A1, int64_t K1, const optional<Tensor>& A2, int64_
            "gmp_tp_gemm_x3_f32");
 }
 
+// three bf16 planes of the (N x K) operand B = W (transpose = false: rows n of W) or W^T
+// (transpose = true: W is (K x N)) in fragment order
+Tensor split_x3(const Tensor& W, bool transpose) {
+  OpGuard g(W, "split_x3");
+  on_device(W, "W");
+  TORCH_CHECK(W.scalar_type() == at::kFloat, "gmp: W has dtype ", W.scalar_type(),
+              ", expected float");
+  TORCH_CHECK(W.dim() == 2, "gmp.split_x3: W must be 2-D");  // any strides (weight slices)
+  const int64_t N = transpose ? W.size(1) : W.size(0), K = transpose ? W.size(0) : W.size(1);
+  TORCH_CHECK(N % 16 == 0 && K % 32 == 0, "gmp.split_x3: needs N % 16 == 0 and K % 32 == 0, got ",
+              N, " x ", K);
+  Tensor planes = at::empty({3 * N * K}, W.options().dtype(at::kShort));
+  const int64_t s0 = W.stride(0), s1 = W.stride(1);
+  check_rc(gmp_split_x3_f32(N, K, W.numel() ? W.data_ptr<float>() : nullptr,
+                            transpose ? s1 : s0, transpose ? s0 : s1, planes.data_ptr(),
+                            cur_stream()),
+           "gmp_split_x3_f32");
+  return planes;
+}
+
+// C = [A1 | A2] B^T + bias (B as split_x3 planes, N columns)
+Tensor gemm_x3(const Tensor& A1, const optional<Tensor>& A2, const Tensor& Bp, int64_t N,
+               const optional<Tensor>& bias) {
+  OpGuard g(A1, "gemm_x3");
+  f32(A1, "A1");
+  need(Bp, at::kShort, "B planes");
+  TORCH_CHECK(A1.dim() == 2, "gmp.gemm_x3: A1 must be (M, K1)");
+  const int64_t M = A1.size(0), K1 = A1.size(1);
+  const bool two = A2.has_value() && A2->defined();
+  int64_t K2 = 0;
+  if (two) {
+    f32(*A2, "A2");
+    TORCH_CHECK(A2->dim() == 2 && A2->size(0) == M, "gmp.gemm_x3: A2 must be (M, K2)");
+    K2 = A2->size(1);
+  }
+  TORCH_CHECK(K1 % 32 == 0 && K2 % 32 == 0 && N % 16 == 0 && N > 0,
+              "gmp.gemm_x3: K1, K2 multiples of 32 and N of 16");
+  TORCH_CHECK(Bp.numel() == 3 * N * (K1 + K2), "gmp.gemm_x3: B planes hold 3 N (K1 + K2)");
+  if (bias.has_value() && bias->defined()) {
+    f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N, "gmp.gemm_x3: bias must hold N values");
+  }
+  Tensor C = at::empty({M, N}, A1.options());
+  check_rc(gmp_gemm_x3_f32(M, N, fp(A1), K1, K1, two ? fp(*A2) : nullptr, K2, two ? K2 : 0,
+                           Bp.data_ptr(), cfp(bias), fp(C), N, 0, cur_stream()),
+           "gmp_gemm_x3_f32");
+  return C;
+}
+
 Tensor tp_gemm_x3_widen(const Tensor& A, const Tensor& Bp, int64_t N) {
   OpGuard g(A, "tp_gemm_x3_widen");
   f32(A, "A");
@@ -1286,6 +1335,13 @@ Tensor tp_split_w2(const Tensor& W2, const Tensor&, int64_t, int64_t mul1, int64
 }
 void tp_gemm_x3(const Tensor&, int64_t, const optional<Tensor>&, int64_t, const Tensor&, int64_t,
                 int64_t, Tensor, int64_t, int64_t, int64_t, int64_t, int64_t, bool) {}
+Tensor split_x3(const Tensor& W, bool) {
+  return at::empty({3 * W.numel()}, W.options().dtype(at::kShort));
+}
+Tensor gemm_x3(const Tensor& A1, const optional<Tensor>&, const Tensor&, int64_t N,
+               const optional<Tensor>&) {
+  return at::empty({A1.size(0), N}, A1.options());
+}
 Tensor tp_gemm_x3_widen(const Tensor& A, const Tensor&, int64_t N) {
   return at::empty({A.size(0), N}, A.options());
 }
@@ -1401,6 +1457,8 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor(a!) C, int c_offset, int cgrp, int cldg, int cldr, int cldn, bool accumulate) "
         "-> ()");
   m.def("tp_gemm_x3_widen(Tensor A, Tensor Bp, int N) -> Tensor");
+  m.def("split_x3(Tensor W, bool transpose) -> Tensor");
+  m.def("gemm_x3(Tensor A1, Tensor? A2, Tensor Bp, int N, Tensor? bias) -> Tensor");
   m.def("outer_sum_cols(Tensor A, Tensor B) -> Tensor");
   m.def("edge_outer_sum(Tensor A, Tensor B) -> (Tensor C, Tensor colsum)");
   m.def("edge_outer_sum_ex(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int act, "
@@ -1453,6 +1511,8 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("tp_split_w2", ns tp_split_w2);                                  \
   m.impl("tp_gemm_x3", ns tp_gemm_x3);                                    \
   m.impl("tp_gemm_x3_widen", ns tp_gemm_x3_widen);                        \
+  m.impl("split_x3", ns split_x3);                                        \
+  m.impl("gemm_x3", ns gemm_x3);                                          \
   m.impl("outer_sum_cols", ns outer_sum_cols);                            \
   m.impl("edge_outer_sum", ns edge_outer_sum);                            \
   m.impl("edge_outer_sum_ex", ns edge_outer_sum_ex);                      \

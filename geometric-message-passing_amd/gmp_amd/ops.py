@@ -373,6 +373,35 @@ def _mm_wt(g, Wt):
     return g.mm(Wt.t())
 
 
+# Row-level Linears (node rows of the EGNN update MLP and message projections, edge rows of the
+# per-edge Linears) on the K7g kernel: [a1 | a2] B^T + b on the bf16 MFMA over exact three-plane
+# f32 splits (gmp_gemm_x3_f32; f32-class, see gmp_tpgemm.hip).  Off by default (GMP_ROW_GEMM=x3
+# turns it on): the K7g tile is built for long k ranges and measured slower than the library f32
+# GEMMs at K <= 256 (scripts/mb_rowgemm.py: 50k x 128 x 128 36 vs 38 us, 50k x 256 x 128 66 vs
+# 55 us, 1M x 128 x 128 508 vs 415 us; EGNN step 80 vs 87 M edges/s on one box).
+ROW_GEMM = os.environ.get("GMP_ROW_GEMM", "torch")
+
+
+def _x3_fits(n, *ks):
+    return ROW_GEMM == "x3" and n % 16 == 0 and n > 0 and all(k % 32 == 0 for k in ks)
+
+
+def linear_x3(a1, a2, W, b=None, transpose=False):
+    """[a1 | a2] @ B^T (+ b) with B = W (W (n, k): y = x W^T) or, transpose=True, B = W^T
+    (W (k, n): dx = g W); W may be a strided slice of a parameter."""
+    tops = _lib.torch_ops()
+    n = W.shape[1] if transpose else W.shape[0]
+    return tops.gemm_x3(_f32c(a1), None if a2 is None else _f32c(a2),
+                        tops.split_x3(W, transpose), n, b)
+
+
+def _dx(g, W):
+    """g @ W for the dx of y = x W^T (W (n_out, n_in))."""
+    if _x3_fits(W.shape[1], W.shape[0]):
+        return linear_x3(g, None, W, None, True)
+    return _mm_wt(g, W.t().contiguous())
+
+
 class EdgeLinearFn(torch.autograd.Function):
     """y = x W^T (+ b) over many rows (edges): forward and dx with the library GEMM (M = rows),
     dW / db with the deterministic edge outer sum (K = rows), which the library's small-tile
@@ -382,6 +411,8 @@ class EdgeLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W, b)
+        if _x3_fits(W.shape[0], W.shape[1]):
+            return linear_x3(x, None, W, b)
         return torch.addmm(b, x, W.t()) if b is not None else x.mm(W.t())
 
     @staticmethod
@@ -389,7 +420,7 @@ class EdgeLinearFn(torch.autograd.Function):
     def backward(ctx, g):
         x, W, b = ctx.saved_tensors
         g = g.contiguous()
-        dx = _mm_wt(g, W.t().contiguous()) if ctx.needs_input_grad[0] else None
+        dx = _dx(g, W) if ctx.needs_input_grad[0] else None
         need_w = ctx.needs_input_grad[1] or (b is not None and ctx.needs_input_grad[2])
         if not need_w:
             return dx, None, None
@@ -406,9 +437,11 @@ class SplitLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xa, xb, W, b):
         da = xa.shape[1]
+        ctx.save_for_backward(xa, xb, W, b)
+        if _x3_fits(W.shape[0], da, xb.shape[1]):
+            return linear_x3(xa, xb, W, b)  # one GEMM over the two K ranges
         y = torch.addmm(b, xa, W[:, :da].t()) if b is not None else xa.mm(W[:, :da].t())
         y.addmm_(xb, W[:, da:].t())
-        ctx.save_for_backward(xa, xb, W, b)
         return y
 
     @staticmethod
@@ -417,9 +450,8 @@ class SplitLinearFn(torch.autograd.Function):
         xa, xb, W, b = ctx.saved_tensors
         da = xa.shape[1]
         g = g.contiguous()
-        Wt = W.t().contiguous() if (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) else None
-        dxa = _mm_wt(g, Wt[:da]) if ctx.needs_input_grad[0] else None
-        dxb = _mm_wt(g, Wt[da:]) if ctx.needs_input_grad[1] else None
+        dxa = _dx(g, W[:, :da]) if ctx.needs_input_grad[0] else None
+        dxb = _dx(g, W[:, da:]) if ctx.needs_input_grad[1] else None
         need_w = ctx.needs_input_grad[2] or (b is not None and ctx.needs_input_grad[3])
         if not need_w:
             return dxa, dxb, None, None
@@ -787,7 +819,8 @@ class EgnnMessageFn(torch.autograd.Function):
         N, d = h.shape
         E = graph.num_edges
         Wcat = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)
-        AB = h.mm(Wcat.t())  # [h W1a^T | h W1b^T]
+        # [h W1a^T | h W1b^T]
+        AB = linear_x3(h, None, Wcat) if _x3_fits(2 * d, d) else h.mm(Wcat.t())
         params = tuple(_f32c(t) for t in (W1[:, 2 * d], b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3,
                                           b3, ln3w, ln3b, w4, b4))
         train = any(ctx.needs_input_grad)
@@ -821,9 +854,13 @@ class EgnnMessageFn(torch.autograd.Function):
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
-        W1t = W1[:, :2 * d].t().contiguous()  # [W1a | W1b]^T: NT-form GEMMs for dh
-        dh = _mm_wt(dA, W1t[:d])
-        dh.addmm_(dB, W1t[d:].t())
+        if _x3_fits(d, d, d):
+            # dh = [dA | dB] [W1a ; W1b]: one GEMM over the two K ranges
+            dh = linear_x3(dA, dB, torch.cat([W1[:, :d], W1[:, d:2 * d]], 0), None, True)
+        else:
+            W1t = W1[:, :2 * d].t().contiguous()  # [W1a | W1b]^T: NT-form GEMMs for dh
+            dh = _mm_wt(dA, W1t[:d])
+            dh.addmm_(dB, W1t[d:].t())
         dpos = dpos_recv - dpos_send
 
         # weight gradients: side stream, accumulated at the end of the backward pass

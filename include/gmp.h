@@ -400,6 +400,18 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
  * K a multiple of 32, <= 128.  Each workgroup keeps its split A rows in LDS and sweeps a range
  * of column tiles with B loaded straight into registers; C is written with non-temporal
  * stores. */
+/* Node-level Linears on the same kernel (K7g tile, A split on load, B pre-split): replaces the
+ * library f32 GEMMs of torch.nn.functional.linear / Tensor.mm over the node rows (egnn_layer.py
+ * :37-39 mlp_upd, :28 the node projections of mlp_msg[0]; their dx GEMMs).
+ * gmp_split_x3_f32: the three bf16 planes of the N x K operand B[n][k] = B[n sn + k sk] in MFMA
+ *   fragment order (3 N K unsigned shorts; N % 16 == 0, K % 32 == 0).
+ * gmp_gemm_x3_f32: C[m][n] (+)= sum_k [A1 | A2][m][k] B[n][k] + bias[n] (bias may be NULL;
+ *   A2 may be NULL with K2 = 0; K1, K2 multiples of 32; C row stride ldc). */
+int gmp_split_x3_f32(int64_t N, int64_t K, const float* B, int64_t sn, int64_t sk, void* Bp,
+                     void* stream);
+int gmp_gemm_x3_f32(int64_t M, int64_t N, const float* A1, int64_t K1, int64_t lda1,
+                    const float* A2, int64_t K2, int64_t lda2, const void* Bp, const float* bias,
+                    float* C, int64_t ldc, int accumulate, void* stream);
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                              const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
                              void* stream);

@@ -1,55 +1,42 @@
-"""Host-side (Python) cost of the EGNN training step (dev tool): cProfile over a few steps of
-bench.py's step, GPU synchronised only at the end.  usage: python scripts/host_profile.py [egnn|gvp]"""
+"""Host-side cost of one EGNN training step (GPU box): cProfile over steps of a tiny graph,
+where the step is host-bound; prints the top functions by own time and by cumulative time."""
 import cProfile
 import os
 import pstats
 import sys
-import time
 
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "geometric-message-passing_amd"))
-import gmp_amd  # noqa: E402
-from gmp_amd.graph import radius_graph  # noqa: E402
+sys.path[:0] = [ROOT, os.path.join(ROOT, "geometric-message-passing_amd")]
 
-g = radius_graph(num_nodes=50_000, target_edges=1_000_000, seed=0)
-torch.manual_seed(0)
-dev = torch.device("cuda")
-if len(sys.argv) > 1 and sys.argv[1] == "gvp":
-    model = gmp_amd.GVPGNNModel(num_layers=4, s_dim=128, v_dim=16, s_dim_edge=32, v_dim_edge=1,
-                                in_dim=1, out_dim=1).to(dev)
-else:
+
+def main():
+    import gmp_amd
+    from gmp_amd.graph import radius_graph
+    from gmp_amd.step import GraphedStep
+    dev = torch.device("cuda", 0)
+    g = radius_graph(num_nodes=500, target_edges=10000, seed=0).to(dev)
     model = gmp_amd.EGNNModel(num_layers=4, emb_dim=128, in_dim=1, out_dim=1).to(dev)
-opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=os.environ.get("FUSED", "0") == "1")
-batch = g.to(dev)
-y = torch.randn(1, device=dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    y = torch.zeros(1, device=dev)
+    step = GraphedStep(model, lambda: torch.nn.functional.l1_loss(model(g).view(-1), y), opt,
+                       warmup=0, use_graph=False)
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    n = 50
+    pr.enable()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    pr.disable()
+    st = pstats.Stats(pr)
+    print(f"host time per step: {st.total_tt / n * 1e3:.2f} ms")
+    st.sort_stats("tottime").print_stats(30)
+    st.sort_stats("cumulative").print_stats(40)
 
 
-def step():
-    opt.zero_grad(set_to_none=True)
-    loss = torch.nn.functional.l1_loss(model(batch).view(-1), y, reduction="sum")
-    loss.backward()
-    opt.step()
-
-
-for _ in range(3):
-    step()
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-for _ in range(5):
-    step()
-t_host = time.perf_counter() - t0
-torch.cuda.synchronize()
-t_all = time.perf_counter() - t0
-print(f"5 steps: host enqueue {t_host * 1e3:.1f} ms, wall {t_all * 1e3:.1f} ms")
-pr = cProfile.Profile()
-pr.enable()
-for _ in range(5):
-    step()
-torch.cuda.synchronize()
-pr.disable()
-st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(35)
-st.print_callers("item|synchronize|nonzero|tolist|_local_scalar")
+if __name__ == "__main__":
+    main()
