@@ -404,8 +404,7 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
     model = build_model(gmp_amd, workload, layers, emb).to(dev)
     # Adam (the reference optimizer, train_utils.py): the fused multi-tensor implementation
     # (one launch per step); capturable (step counter on the device) for HIP-graph replay
-    opt = (torch.optim.Adam(model.parameters(), lr=1e-4, capturable=True) if args.graph
-           else torch.optim.Adam(model.parameters(), lr=1e-4, fused=True))
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True, capturable=args.graph)
     batch = g.to(dev)
     if _atom_type(workload):
         batch.atoms = torch.full_like(batch.atoms, _atom_type(workload))

@@ -842,6 +842,30 @@ void tp_gemm_x3(const Tensor& A1, int64_t K1, const optional<Tensor>& A2, int64_
            "gmp_tp_gemm_x3_f32");
 }
 
+// dW2p of one path with S built in-kernel (K7f): Z (edges (+1 pad row) x d3 mul1), A (edges x H),
+// G (n_recv d3 x mul_out), eoff (n_recv + 1) -> dW (mul1 H x mul_out)
+Tensor tp_node_dw(const Tensor& eoff, const Tensor& Z, const Tensor& A, const Tensor& G,
+                  int64_t d3, int64_t mul1) {
+  OpGuard g(Z, "tp_node_dw");
+  i64(eoff, "eoff");
+  f32(Z, "Z");
+  f32(A, "A");
+  f32(G, "G");
+  TORCH_CHECK(eoff.dim() == 1 && eoff.numel() >= 1, "gmp.tp_node_dw: eoff (n_recv + 1)");
+  const int64_t n = eoff.numel() - 1;
+  TORCH_CHECK(A.dim() == 2 && Z.dim() == 2 && Z.size(1) == d3 * mul1 && Z.size(0) >= A.size(0),
+              "gmp.tp_node_dw: Z (edges, d3 mul1), A (edges, H)");
+  TORCH_CHECK(G.dim() == 2 && G.size(0) == n * d3, "gmp.tp_node_dw: G (n_recv d3, mul_out)");
+  const int64_t H = A.size(1), mo = G.size(1);
+  Tensor dW = at::empty({mul1 * H, mo}, Z.options());
+  const size_t ws_b = gmp_tp_node_dw_workspace_size(n, d3, mul1, H, mo);
+  Tensor ws = at::empty({(int64_t)ws_b + 1}, Z.options().dtype(at::kByte));
+  check_rc(gmp_tp_node_dw_f32(n, d3, mul1, H, mo, ip(eoff), fp(Z), fp(A), fp(G), fp(dW),
+                              ws.data_ptr(), ws_b, cur_stream()),
+           "gmp_tp_node_dw_f32");
+  return dW;
+}
+
 // three bf16 planes of the (N x K) operand B = W (transpose = false: rows n of W) or W^T
 // (transpose = true: W is (K x N)) in fragment order
 Tensor split_x3(const Tensor& W, bool transpose) {
@@ -1335,6 +1359,10 @@ Tensor tp_split_w2(const Tensor& W2, const Tensor&, int64_t, int64_t mul1, int64
 }
 void tp_gemm_x3(const Tensor&, int64_t, const optional<Tensor>&, int64_t, const Tensor&, int64_t,
                 int64_t, Tensor, int64_t, int64_t, int64_t, int64_t, int64_t, bool) {}
+Tensor tp_node_dw(const Tensor&, const Tensor&, const Tensor& A, const Tensor& G, int64_t,
+                  int64_t mul1) {
+  return at::empty({mul1 * A.size(1), G.size(1)}, A.options());
+}
 Tensor split_x3(const Tensor& W, bool) {
   return at::empty({3 * W.numel()}, W.options().dtype(at::kShort));
 }
@@ -1458,6 +1486,7 @@ TORCH_LIBRARY(gmp, m) {
         "-> ()");
   m.def("tp_gemm_x3_widen(Tensor A, Tensor Bp, int N) -> Tensor");
   m.def("split_x3(Tensor W, bool transpose) -> Tensor");
+  m.def("tp_node_dw(Tensor eoff, Tensor Z, Tensor A, Tensor G, int d3, int mul1) -> Tensor");
   m.def("gemm_x3(Tensor A1, Tensor? A2, Tensor Bp, int N, Tensor? bias) -> Tensor");
   m.def("outer_sum_cols(Tensor A, Tensor B) -> Tensor");
   m.def("edge_outer_sum(Tensor A, Tensor B) -> (Tensor C, Tensor colsum)");
@@ -1512,6 +1541,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("tp_gemm_x3", ns tp_gemm_x3);                                    \
   m.impl("tp_gemm_x3_widen", ns tp_gemm_x3_widen);                        \
   m.impl("split_x3", ns split_x3);                                        \
+  m.impl("tp_node_dw", ns tp_node_dw);                                    \
   m.impl("gemm_x3", ns gemm_x3);                                          \
   m.impl("outer_sum_cols", ns outer_sum_cols);                            \
   m.impl("edge_outer_sum", ns edge_outer_sum);                            \

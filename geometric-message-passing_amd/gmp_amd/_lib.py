@@ -132,6 +132,9 @@ SIGNATURES = {
     "gmp_tp_gemm_set_rings": (c_int, [c_int, c_int]),
     "gmp_tp_split_w2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_split_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "gmp_tp_node_dw_workspace_size": (c_size, [c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "gmp_tp_node_dw_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp, c_vp, c_size, c_vp]),
     "gmp_gemm_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp,
                                 c_vp, c_i64, c_int, c_vp]),
     "gmp_tp_gemm_x3_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,

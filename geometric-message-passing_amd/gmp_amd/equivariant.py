@@ -554,6 +554,19 @@ def _x3_ok(P, H):
             and P["mul_out"] <= 128 and H % 32 == 0)
 
 
+# K7f (gmp_tpdw.hip): the backward's dW2p with S built inside the outer sum, GMP_TP_DW_FUSED=1.
+# Off by default: correct (tests/test_gpu_tpnode.py) and HBM-light (7 GB vs 66 GB of S traffic
+# per MACE-128 lo = 2 path) but slower than the S kernel + column-block outer sum it replaces
+# (scripts/mb_tpdw.py: 29.7 vs 22.1 ms at lo = 2; PMC: 40 % of wave cycles waiting, 33 % issue
+# stalls, MFMA busy 25 % -- two waves per SIMD in lock-step stages do not hide the S-build loads)
+TP_DW_FUSED = os.environ.get("GMP_TP_DW_FUSED", "0") == "1"
+
+
+def _dw_fused_ok(P, H):
+    return (TP_DW_FUSED and P["mul1"] % 16 == 0 and H % 16 == 0
+            and P["mul_out"] in (64, 128))
+
+
 def _split_w2(W2, b2, P, fwd):
     """Three bf16 planes of path P's W2 / b2 block: forward (B = [W2p | b2p]^T as [w][(u, j) ++ u])
     or backward (B = W2p as [(u, j)][w]) layout (torch.ops.gmp.tp_split_w2)."""
@@ -644,14 +657,21 @@ class TPConvNodeFn(torch.autograd.Function):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 blk = plan.blocks[P["io"]]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                S, Sb = _node_outer(eoff, Zp, a, w)
                 G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
                 G = G.reshape(c * d3, mo).contiguous()  # (d3 = 1: reshape alone is a view)
                 if x3[i]:
                     K1 = m1 * H
                     with _timed("tp_node_dW"):
-                        # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
-                        part = tops.outer_sum_cols(S.view(c * d3, K1), G)
+                        if _dw_fused_ok(P, H):
+                            # K7f: dW2p with the S rows built in-kernel (S never in HBM); Sb
+                            # (the bias rows) = the per-receiver sum of the z rows
+                            part = tops.tp_node_dw(eoff, Zp, a, G, d3, m1)
+                            Sb, _ = tops.segment_reduce(Zp, None, eoff, c, "sum")
+                        else:
+                            S, Sb = _node_outer(eoff, Zp, a, w)
+                            # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
+                            part = tops.outer_sum_cols(S.view(c * d3, K1), G)
+                            del S
                         # db2p[u, w] = sum_(n, k) Sb[(n, k), u] G[(n, k), w]: the deterministic
                         # outer sum (the library's K = 250k reduction GEMM ran 0.4 ms per path)
                         pb, _ = ops.edge_outer_sum_rect(Sb.view(c * d3, m1), G)
@@ -661,7 +681,7 @@ class TPConvNodeFn(torch.autograd.Function):
                         else:
                             dW2p.add_(part)
                             db2p.add_(pb)
-                    del S, Sb
+                    del Sb
                     if Bts[i] is None:
                         Bts[i] = _split_w2(W2c, b2c, P, False)
                     with _timed("tp_node_W"):
@@ -669,6 +689,7 @@ class TPConvNodeFn(torch.autograd.Function):
                         T = tops.tp_gemm_x3_widen(G, Bts[i], K1)
                         Tb = G.mm(b2p.t())
                 else:
+                    S, Sb = _node_outer(eoff, Zp, a, w)
                     with _timed("tp_node_dW"):
                         dW2p.addmm_(S.view(c * d3, -1).t(), G)
                         db2p.addmm_(Sb.view(c * d3, -1).t(), G)

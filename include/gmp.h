@@ -415,6 +415,18 @@ int gmp_gemm_x3_f32(int64_t M, int64_t N, const float* A1, int64_t K1, int64_t l
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                              const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
                              void* stream);
+/* K7f: dW2p of one TP path without the S intermediate in HBM (backward of the node form):
+ *   dW[(u H + j) mul_out + w] = sum_(n, k) S[(n, k), (u, j)] G[(n k-major rows), w],
+ *   S[(n, k), (u, j)] = sum_{eoff[n] <= e < eoff[n+1]} Z[e, k mul1 + u] A[e, j]
+ * Z (edges x d3 mul1, row-major), A (edges x H), G (n_recv d3 x mul_out), eoff (n_recv + 1,
+ * chunk-local).  mul1 % 16 == 0, H % 16 == 0, mul_out in {64, 128} (GMP_ERR_UNSUPPORTED
+ * otherwise).  Deterministic (partial slabs summed in range order).  Replaces the S write of
+ * gmp_tp_node_outer_f32 + the S read of gmp_outer_sum_cols_f32 (tfn_layer.py:73-87). */
+size_t gmp_tp_node_dw_workspace_size(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H,
+                                     int64_t mul_out);
+int gmp_tp_node_dw_f32(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H, int64_t mul_out,
+                       const int64_t* eoff, const float* Z, const float* A, const float* G,
+                       float* dW, void* workspace, size_t workspace_bytes, void* stream);
 /* Wide edge/row reduction C (m_total x n, row stride ldc) = A^T B over K rows, A (K x m_total,
  * row stride lda), B (K x n, ldb), m_total a multiple of 128, n a multiple of 16 (<= 128): the
  * TP path GEMM dW2p = S^T G.  Split-plane bf16 MFMA (the K5 kernel with column blocks of 128),

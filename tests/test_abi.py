@@ -58,7 +58,7 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
                  "tp_edge_z", "tp_edge_z_bwd", "tp_node_outer", "tp_node_apply", "tp_gemm_x3",
                  "tp_gemm_x3_widen", "outer_sum_cols", "edge_outer_sum_ex",
                  "edge_outer_sum_ex2", "edge_outer_sum_act", "gvp_layer_fwd", "gvp_layer_bwd",
-                 "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd", "split_x3",
+                 "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd", "split_x3", "tp_node_dw",
                  "gemm_x3"):
         assert hasattr(tops, name), name
     with pytest.raises(RuntimeError, match="HIP device"):

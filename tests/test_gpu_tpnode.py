@@ -296,3 +296,42 @@ def test_node_apply_bf16x3_matches_fp64(w, H, x3):
         ez = ((dZ[e0:e1].cpu().double() - rz).abs() / mz).max().item()
         ea = ((dA[e0:e1].cpu().double() - ra).abs() / ma).max().item()
         assert ez < 1e-6 and ea < 1e-6, (n, degs[n], ez, ea)
+
+
+@pytest.mark.parametrize("d3,mul1,H,mo,nrecv,seed", [
+    (5, 32, 32, 128, 23, 0), (3, 16, 48, 64, 41, 1), (1, 64, 32, 64, 70, 2),
+    (5, 128, 256, 128, 13, 3), (3, 64, 256, 64, 35, 4)])
+def test_node_dw_fused_matches_fp64(d3, mul1, H, mo, nrecv, seed):
+    """K7f (gmp_tp_node_dw_f32 via torch.ops.gmp.tp_node_dw): dW2p[(u, j), w] =
+    sum_(n, k) S[(n, k), (u, j)] G[(n, k), w] with S built in-kernel from z and a, against the
+    fp64 evaluation; receivers of in-degree 0, 1 and > 32 (the edge-chunk loop), receiver counts
+    that are not a multiple of a stage (32 // d3 receivers).  Bound: f32 S (edge sums) times the
+    three-plane products, 4e-6 of sum |S| |G|."""
+    from gmp_amd import _lib
+    tops = _lib.torch_ops()
+    g = torch.Generator().manual_seed(seed)
+    degs = torch.randint(0, 30, (nrecv,), generator=g)
+    degs[0], degs[1] = 0, 45
+    if nrecv > 5:
+        degs[5] = 1
+    w = d3 * mul1
+    eoff, Z, A, ne = _setup(degs.tolist(), w, H, seed=seed)
+    G = torch.randn(nrecv * d3, mo, generator=g)
+    dW = tops.tp_node_dw(eoff.to(DEV), Z.to(DEV), A.to(DEV), G.to(DEV), d3, mul1).cpu().double()
+    S = torch.zeros(nrecv, w, H, dtype=torch.float64)
+    Sa = torch.zeros(nrecv, w, H, dtype=torch.float64)
+    for n in range(nrecv):
+        e0, e1 = int(eoff[n]), int(eoff[n + 1])
+        S[n] = Z[e0:e1].double().t() @ A[e0:e1].double()
+        Sa[n] = Z[e0:e1].double().abs().t() @ A[e0:e1].double().abs()
+    # rows (n, k) x columns (u, j)
+    Sk = S.view(nrecv, d3, mul1, H).reshape(nrecv * d3, mul1 * H)
+    Sak = Sa.view(nrecv, d3, mul1, H).reshape(nrecv * d3, mul1 * H)
+    ref = Sk.t() @ G.double()
+    bound = Sak.t() @ G.double().abs()
+    assert dW.shape == (mul1 * H, mo)
+    err = (dW - ref).abs()
+    assert bool((err <= 4e-6 * bound + 1e-6).all()), (err / bound.clamp_min(1e-30)).max().item()
+    # deterministic
+    dW2 = tops.tp_node_dw(eoff.to(DEV), Z.to(DEV), A.to(DEV), G.to(DEV), d3, mul1).cpu().double()
+    assert torch.equal(dW, dW2)
