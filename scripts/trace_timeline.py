@@ -2,7 +2,7 @@
 step = the span between the first launches of a marker kernel in consecutive steps (marker: a
 kernel name prefix launched `per_step` times per step); per stream: busy time, idle gaps and
 the kernels with the most time; gaps > 5 us listed with the kernels around them.
-    python3 scripts/trace_timeline.py <trace.csv> [marker] [per_step]"""
+    python3 scripts/trace_timeline.py <trace.csv> [marker] [per_step] [step_idx]"""
 import csv
 import sys
 from collections import defaultdict
@@ -43,4 +43,4 @@ def main(path, marker="egnn_fwd_kernel", per_step=4, step_idx=-2, top=12):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], *(sys.argv[2:3]), *(int(x) for x in sys.argv[3:4]))
+    main(sys.argv[1], *(sys.argv[2:3]), *(int(x) for x in sys.argv[3:5]))
