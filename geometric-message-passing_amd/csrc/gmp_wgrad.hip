@@ -372,6 +372,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 constexpr int kXT = 512;  // threads (8 waves)
@@ -783,6 +784,168 @@ __global__ void sum_partials_cols(const float* __restrict__ part, int64_t Gr, in
   C[(y * m + r) * ldc + c] = s;
 }
 
+// dW2p column-block outer sum with G pre-split ("pre-split G once per pass
+// instead of per column block"): B = three bf16 planes of G in MFMA fragment order, k padded
+// to 32 (split_g_kernel, once per call), read straight into registers PD stages ahead; only A
+// (the S columns of the block) goes through LDS.  The r03 kernel staged and split both operands
+// per column block: ~196 KB of LDS traffic per 32-deep stage against 1536 MFMA cycles (LDS-
+// bound, 29 % bank conflicts).  Here: 24 KB of A writes + 96 KB of A fragment reads per stage.
+// 512 threads, wave grid 2 (M) x 4 (N): wave tile 64 x 16 CT.
+__device__ __forceinline__ int64_t gfrag_index(int64_t p, int64_t n, int64_t k, int64_t ct_total) {
+  return ((((k >> 5) * ct_total + (n >> 4)) * 3 + p) * 64 + (n & 15) + 16 * ((k & 31) >> 3)) * 8 +
+         (k & 7);
+}
+// lane l of block (k step ks, column tile ct): rows 32 ks + 8 (l >> 4) .. + 7 of column
+// 16 ct + (l & 15) -> three 16-byte plane pieces (coalesced reads along G rows, contiguous writes)
+__global__ __launch_bounds__(256) void split_g_kernel(const float* __restrict__ G, int64_t K,
+                                                      int64_t nks, int n,
+                                                      unsigned short* __restrict__ Bp) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (ks, ct) block per wave
+  const int ct_total = n >> 4;
+  if (t >= nks * ct_total) return;
+  const int64_t ks = t / ct_total, ct = t - ks * ct_total;
+  const int l = threadIdx.x & 63;
+  const int64_t col = 16 * ct + (l & 15), k0 = 32 * ks + 8 * (l >> 4);
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = k0 + i < K ? G[(k0 + i) * n + col] : 0.f;
+  u32x4 pl[3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    unsigned h, m, lo;
+    split3(f32x2{v[2 * i], v[2 * i + 1]}, h, m, lo);
+    pl[0][i] = h;
+    pl[1][i] = m;
+    pl[2][i] = lo;
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    *reinterpret_cast<u32x4*>(Bp + ((t * 3 + p) * 64 + l) * 8) = pl[p];
+}
+
+template <int CT, int PD, int OCC>
+__global__ __launch_bounds__(kXT, OCC) void outer_cols_x3g_kernel(
+    const float* __restrict__ A, int64_t K, int64_t lda, const unsigned short* __restrict__ Bp,
+    int n, int64_t k_per_block, int64_t X, float* __restrict__ partial) {
+  constexpr int RT = 4;
+  constexpr int PL = kColBlk * 64, STG = 3 * PL;  // one plane image: 128 rows x 32 bf16
+  __shared__ __attribute__((aligned(16))) unsigned char sa[2 * STG];
+  A += (int64_t)blockIdx.y * kColBlk;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wm = w >> 2, wn = w & 3;
+  const int64_t k0 = (int64_t)blockIdx.x * k_per_block;
+  const int64_t k1 = (k0 + k_per_block < K) ? k0 + k_per_block : K;
+  const int nst = k1 > k0 ? (int)((k1 - k0 + kXK - 1) / kXK) : 0;
+  // A loader (waves 0-3): edge quad eq (4 rows k), channel group cg (4 columns); measured
+  // faster than spreading the block over all 8 waves (12.8 vs 11.7 ms at the MACE lo = 2
+  // shape: twice the LDS store instructions at half the width)
+  const bool loader = w < 4;
+  const int eq = tid & 7, cg = (tid >> 3) & 31;
+  const float* abase = A + 4 * cg;
+  f32x4 ra[PD][4];
+  auto fetch_a = [&](int slot, int st) {
+    if (!loader) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int64_t k = k0 + (int64_t)st * kXK + 4 * eq + j;
+      k = k < k1 ? k : k1 - 1;
+      ra[slot][j] = *reinterpret_cast<const f32x4*>(abase + k * lda);
+    }
+  };
+  auto stash_a = [&](int slot, unsigned char* buf, int st) {
+    if (!loader) return;
+    f32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = k0 + (int64_t)st * kXK + 4 * eq + j < k1;
+      v[j] = ok ? ra[slot][j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int off = xoff(4 * cg + c, eq >> 1) + 8 * (eq & 1);
+      unsigned h0, m0, l0, h1, m1, l1;
+      split3(f32x2{v[0][c], v[1][c]}, h0, m0, l0);
+      split3(f32x2{v[2][c], v[3][c]}, h1, m1, l1);
+      *reinterpret_cast<u32x2*>(buf + off) = u32x2{h0, h1};
+      *reinterpret_cast<u32x2*>(buf + PL + off) = u32x2{m0, m1};
+      *reinterpret_cast<u32x2*>(buf + 2 * PL + off) = u32x2{l0, l1};
+    }
+  };
+  const int64_t ct_total = n >> 4;
+  const unsigned short* bl = Bp + 8 * lane;
+  u32x4 rb[PD][CT][3];
+  auto fetch_b = [&](int slot, int st) {
+    const int64_t ks = (k0 >> 5) + (st < nst ? st : (nst > 0 ? nst - 1 : 0));
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        rb[slot][c][p] = *reinterpret_cast<const u32x4*>(
+            bl + ((ks * ct_total + wn * CT + c) * 3 + p) * 512);
+  };
+  f32x4 acc[RT][CT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const unsigned char* buf, int slot) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int off = xoff(64 * wm + 16 * r + li, g);
+      bf16x8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(buf + p * PL + off);
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        f32x4 t = acc[r][c];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], __builtin_bit_cast(bf16x8, rb[slot][c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], __builtin_bit_cast(bf16x8, rb[slot][c][1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], __builtin_bit_cast(bf16x8, rb[slot][c][2]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], __builtin_bit_cast(bf16x8, rb[slot][c][0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], __builtin_bit_cast(bf16x8, rb[slot][c][1]), t, 0, 0, 0);
+        acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], __builtin_bit_cast(bf16x8, rb[slot][c][0]), t, 0, 0, 0);
+      }
+    }
+  };
+  if (nst > 0) {
+#pragma unroll
+    for (int q = 0; q < PD; ++q) {
+      fetch_a(q, q);
+      fetch_b(q, q);
+    }
+    stash_a(0, sa, 0);
+  }
+  __syncthreads();
+  const int nst_pad = (nst + PD - 1) / PD * PD;
+  for (int s0 = 0; s0 < nst_pad; s0 += PD) {
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      const int st = s0 + j;
+      fetch_a(j, st + PD);  // slot j was stashed for stage st
+      compute(sa + (st & 1) * STG, j);
+      __builtin_amdgcn_sched_barrier(0);
+      fetch_b(j, st + PD);  // the slot the MFMAs above just read
+      stash_a((j + 1) % PD, sa + ((st + 1) & 1) * STG, st + 1);
+      __syncthreads();
+    }
+  }
+  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + q; slab layout as the r03
+  // kernel's (X floats per (column block, range): m n values, the colsum tail unused here)
+  float* out = partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * X;
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[(int64_t)(64 * wm + 16 * r + 4 * g + q) * n + 16 * (wn * CT + c) + li] = acc[r][c][q];
+}
+
+// GMP_OSC_PRESPLIT=0: the r03 column-block kernel (both operands split per block)
+int g_osc_presplit = getenv("GMP_OSC_PRESPLIT") ? atoi(getenv("GMP_OSC_PRESPLIT")) : 1;
+
 // capacity bucket for (M, N): returns 0 if unsupported
 // Tile bucket of an M x N problem: the smallest compiled (MR, MC) covering the per-wave tile
 // counts (the MFMA stream is branch-free, so oversized buckets cost real MFMAs), and the
@@ -1043,7 +1206,9 @@ int gmp_edge_outer_sum_ex_f32(int64_t K, int64_t m, int64_t n, const float* A, i
 size_t gmp_outer_sum_cols_workspace_size(int64_t K, int64_t m_total, int64_t n) {
   if (m_total <= 0 || n <= 0 || m_total % kColBlk) return 0;
   const int64_t Y = m_total / kColBlk;
-  return (size_t)(Y * cols_groups(K, Y) * (kColBlk * n + kColBlk)) * sizeof(float);
+  // partial slabs, then (pre-split path) G's three bf16 planes with k padded to 32
+  return (size_t)(Y * cols_groups(K, Y) * (kColBlk * n + kColBlk)) * sizeof(float) +
+         (size_t)3 * n * ceil_div(K, kXK) * kXK * sizeof(unsigned short) + 16;
 }
 
 int gmp_outer_sum_cols_f32(int64_t K, int64_t m_total, int64_t n, const float* A, int64_t lda,
@@ -1074,6 +1239,28 @@ int gmp_outer_sum_cols_f32(int64_t K, int64_t m_total, int64_t n, const float* A
   const int64_t per = ceil_div(ceil_div(K, G), kXK) * kXK;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
+  if (g_osc_presplit && (n == 64 || n == 128) && ldb == n) {
+    const int64_t X = m * n + m;
+    const int64_t nks = ceil_div(K, kXK);
+    unsigned short* planes = reinterpret_cast<unsigned short*>(
+        reinterpret_cast<unsigned char*>(workspace) +
+        ((Y * Gr * X * sizeof(float) + 15) & ~(size_t)15));
+    split_g_kernel<<<(unsigned)ceil_div(nks * (n / 16), 4), 256, 0, s>>>(B, K, nks, (int)n,
+                                                                          planes);
+    int rc = launch_status();
+    if (rc) return rc;
+    if (n == 128)
+      outer_cols_x3g_kernel<2, 3, 1><<<dim3((unsigned)Gr, (unsigned)Y), kXT, 0, s>>>(
+          A, K, lda, planes, (int)n, per, X, part);
+    else
+      outer_cols_x3g_kernel<1, 3, 2><<<dim3((unsigned)Gr, (unsigned)Y), kXT, 0, s>>>(
+          A, K, lda, planes, (int)n, per, X, part);
+    rc = launch_status();
+    if (rc) return rc;
+    sum_partials_cols<<<dim3((unsigned)ceil_div(m * n, 256), (unsigned)Y), 256, 0, s>>>(
+        part, Gr, X, (int)m, (int)n, C, ldc);
+    return launch_status();
+  }
   const size_t smem = (size_t)2 * 3 * (R + kXPad) * 64;
   auto k = shape == 2   ? outer_sum_x3_kernel<2, 4, 0, 1>
            : shape == 1 ? outer_sum_x3_kernel<2, 2, 0, 1>

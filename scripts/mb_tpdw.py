@@ -44,6 +44,12 @@ def main():
                 tops.tp_node_dw(eoff, Z, A, G, d3, mul1)
             torch.cuda.synchronize()
             return
+        if only == "unfused":
+            S, _ = tops.tp_node_outer(eoff, Z, A, w)
+            for _ in range(3):
+                tops.outer_sum_cols(S.view(N * d3, mul1 * H), G)
+            torch.cuda.synchronize()
+            return
         t_f = timeit(lambda: tops.tp_node_dw(eoff, Z, A, G, d3, mul1))
 
         def unfused():
