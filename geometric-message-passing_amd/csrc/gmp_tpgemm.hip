@@ -423,6 +423,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
 // non-temporal stores (T is consumed by a later kernel, far past the caches) and restart.
 // Replaces one workgroup per 128 x 128 tile, whose prologue / epilogue dominated at 4 k steps.
 constexpr int kMaxKS = 4;  // K <= 128
+constexpr int kParkLd = 36;  // widen epilogue LDS slab row stride (floats): 32 + 4
 template <int NKS, int NP, int RB>
 __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
     int64_t M, int64_t N, const float* __restrict__ A, int64_t lda,
@@ -494,21 +495,42 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
   f32x4 acc[4][2];
 #pragma unroll
   for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // epilogue through a wave-private LDS slab (16 rows x 32 columns per row tile): the
+  // accumulators (lane: 4 rows of one column) are parked, then leave as whole 128-byte row
+  // segments, 16 bytes per lane (direct 4-byte stores of the accumulator layout wrote 64-byte
+  // pieces with the non-temporal hint: 2.5-3.2 TB/s of T at the TFN / MACE shapes)
+  float* park = reinterpret_cast<float*>(smw + NKS * NP * kPlane) + w * (16 * kParkLd);
+  const bool vec_st = (ldc % 4 == 0) && (N % 4 == 0) && (reinterpret_cast<uintptr_t>(C) % 16 == 0);
   auto store_tile = [&](int64_t tn) {
+    const int64_t c0 = tn * kBN + 32 * wn;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int64_t col = tn * kBN + 32 * wn + 16 * c + li;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t row = m0 + 64 * wm + 16 * r + 4 * g + q;
-          if (row < M && col < N)
-            __builtin_nontemporal_store(NP == 3 ? acc[r][c][q] : acc[r][c][q] * hs.down,
-                                        C + row * ldc + col);
-        }
+        for (int q = 0; q < 4; ++q)
+          park[(4 * g + q) * kParkLd + 16 * c + li] =
+              NP == 3 ? acc[r][c][q] : acc[r][c][q] * hs.down;
         acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+      __builtin_amdgcn_wave_barrier();  // park is wave-private
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rr = 8 * h + (lane >> 3), c4 = 4 * (lane & 7);
+        const int64_t row = m0 + 64 * wm + 16 * r + rr;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(park + rr * kParkLd + c4);
+        if (row < M && c0 + c4 < N) {
+          float* dst = C + row * ldc + c0 + c4;
+          if (vec_st) {
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+          } else {  // unaligned rows (ldc % 4 != 0) or a ragged last column group
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (c0 + c4 + e < N) __builtin_nontemporal_store(v[e], dst + e);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   };
 
@@ -817,7 +839,8 @@ int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
   const int64_t nwg = tiles_m * n_split;
   GMP_CHECK_ARG(nwg < (1LL << 32));
   const int nks = (int)(K / kBK);
-  const size_t smem = (size_t)(nks * NP) * kPlane;
+  // resident A planes + the epilogue's per-wave 16 x 32 parking slabs
+  const size_t smem = (size_t)(nks * NP) * kPlane + (size_t)(kGT / 64) * 16 * kParkLd * 4;
   hipStream_t s = as_stream(stream);
   const unsigned short* B = static_cast<const unsigned short*>(Bp);
   int rc = 0;
