@@ -318,7 +318,9 @@ def tp_algorithmic_bytes(model, n_edges):
 # kernels of the node-form TP contraction (the roofline's kernel set; prefixes as rocprofv3
 # names them in profiles/<round>_<workload>_kernels.json)
 TP_KERNELS = ("tp_node_outer_kernel", "tp_gemm_x3_kernel", "tp_gemm_x3_widen_kernel",
-              "outer_sum_x3_kernel", "sum_partials_cols", "tp_node_apply", "tp_split_w2_kernel")
+              "outer_sum_x3_kernel", "outer_cols_x3g_kernel", "split_g_kernel",
+              "sum_partials_cols", "tp_node_apply", "tp_split_w2_kernel", "tp_node_dw_kernel",
+              "tp_dw_sum_kernel")
 
 
 def pmc_step(workload):

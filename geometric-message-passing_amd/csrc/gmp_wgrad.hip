@@ -686,8 +686,11 @@ int64_t capped(int64_t g) { return g_grid_cap > 0 && g > g_grid_cap ? g_grid_cap
 // minimum edge tiles per workgroup of the f32-MFMA split-K sums (GMP_WGRAD_MIN_TILES; A/B)
 int g_min_tiles = getenv("GMP_WGRAD_MIN_TILES") ? atoi(getenv("GMP_WGRAD_MIN_TILES")) : 16;
 
+// split-K workgroups of the edge-level x3 sums (GMP_X3_BLOCKS; default one per CU)
+int g_x3_blocks = getenv("GMP_X3_BLOCKS") ? atoi(getenv("GMP_X3_BLOCKS")) : 0;
 int64_t x3_blocks_for(int64_t K) {
-  int64_t g = capped((int64_t)device_cu_count());  // one 8-wave workgroup per CU (LDS ~100 KB)
+  // one 8-wave workgroup per CU (LDS ~100 KB)
+  int64_t g = capped(g_x3_blocks > 0 ? (int64_t)g_x3_blocks : (int64_t)device_cu_count());
   const int64_t min_per = 4 * kXK;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
