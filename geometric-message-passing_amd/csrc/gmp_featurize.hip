@@ -36,10 +36,43 @@ __device__ __forceinline__ void sh_l2(float x, float y, float z, float* Y) {
   Y[8] = s15 / 2.f * (z * z - x * x);
 }
 
+// l = 3 block of e3nn's SphericalHarmonics (normalization='component') at a unit vector: the
+// e3nn recursion's polynomials (sh_3_m of e3nn/o3/_spherical_harmonics.py) times sqrt(7);
+// pinned by equivariance under the oracle's D^3 and the CG recursion (tests/test_oracle_o3.py)
+constexpr float kS3 = 1.7320508075688772f, kR7 = 2.6457513110645907f;
+constexpr float kA3 = 0.9128709291752769f /* sqrt(5/6) */, kB3 = 2.23606797749979f /* sqrt 5 */,
+                kC3 = 0.6123724356957945f /* sqrt(3/8) */;
+__device__ __forceinline__ void sh_l3(float x, float y, float z, float* Y) {
+  const float q = 4.f * y * y - (x * x + z * z);
+  Y[0] = kR7 * kA3 * kS3 * (1.5f * x * z * z - 0.5f * x * x * x);
+  Y[1] = kR7 * kB3 * kS3 * x * y * z;
+  Y[2] = kR7 * kC3 * q * x;
+  Y[3] = kR7 * 0.5f * y * (2.f * y * y - 3.f * (x * x + z * z));
+  Y[4] = kR7 * kC3 * z * q;
+  Y[5] = kR7 * kB3 * kS3 * 0.5f * (z * z - x * x) * y;
+  Y[6] = kR7 * kA3 * kS3 * (0.5f * z * z * z - 1.5f * x * x * z);
+}
+// gradient of sum_m g[m] Y3_m w.r.t. the unit vector (x, y, z), added to (ux, uy, uz)
+__device__ __forceinline__ void sh_l3_grad(float x, float y, float z, const float* g, float& ux,
+                                           float& uy, float& uz) {
+  const float k0 = kR7 * kA3 * kS3, k1 = kR7 * kB3 * kS3, k2 = kR7 * kC3, k3 = kR7 * 0.5f,
+              k5 = kR7 * kB3 * kS3 * 0.5f;
+  ux += g[0] * k0 * (1.5f * z * z - 1.5f * x * x) + g[1] * k1 * y * z +
+        g[2] * k2 * (4.f * y * y - 3.f * x * x - z * z) + g[3] * k3 * (-6.f * x * y) +
+        g[4] * k2 * (-2.f * x * z) + g[5] * k5 * (-2.f * x * y) + g[6] * k0 * (-3.f * x * z);
+  uy += g[1] * k1 * x * z + g[2] * k2 * 8.f * x * y +
+        g[3] * k3 * (6.f * y * y - 3.f * (x * x + z * z)) + g[4] * k2 * 8.f * y * z +
+        g[5] * k5 * (z * z - x * x);
+  uz += g[0] * k0 * 3.f * x * z + g[1] * k1 * x * y + g[2] * k2 * (-2.f * x * z) +
+        g[3] * k3 * (-6.f * y * z) + g[4] * k2 * (4.f * y * y - x * x - 3.f * z * z) +
+        g[5] * k5 * 2.f * z * y + g[6] * k0 * (1.5f * z * z - 1.5f * x * x);
+}
+
 __global__ void featurize_fwd_kernel(const float* __restrict__ pos, const int64_t* __restrict__ ei,
                                      int64_t E, int nb, FeatConsts c, float* __restrict__ vec_out,
                                      float* __restrict__ len_out, float* __restrict__ sh_out,
-                                     float* __restrict__ rad_out, float* __restrict__ unit_out) {
+                                     float* __restrict__ rad_out, float* __restrict__ unit_out,
+                                     int lmax) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = ei[e], b = ei[E + e];
@@ -58,10 +91,13 @@ __global__ void featurize_fwd_kernel(const float* __restrict__ pos, const int64_
     }
     if (sh_out) {
       const float inv = 1.f / fmaxf(r, 1e-12f);  // F.normalize(eps=1e-12)
-      float Y[9];
+      float Y[16];
       sh_l2(vx * inv, vy * inv, vz * inv, Y);
+      if (lmax >= 3) sh_l3(vx * inv, vy * inv, vz * inv, Y + 9);
+      const int nsh = (lmax + 1) * (lmax + 1);
 #pragma unroll
-      for (int k = 0; k < 9; ++k) sh_out[9 * e + k] = Y[k];
+      for (int k = 0; k < 16; ++k)
+        if (k < nsh) sh_out[(int64_t)nsh * e + k] = Y[k];
     }
     if (rad_out) {
       const float u = r / c.r_max;
@@ -78,7 +114,8 @@ __global__ void featurize_fwd_kernel(const float* __restrict__ pos, const int64_
 __global__ void featurize_bwd_kernel(const float* __restrict__ pos, const int64_t* __restrict__ ei,
                                      int64_t E, int nb, FeatConsts c,
                                      const float* __restrict__ g_sh, const float* __restrict__ g_rad,
-                                     const float* __restrict__ g_unit, float* __restrict__ g_vec) {
+                                     const float* __restrict__ g_unit, float* __restrict__ g_vec,
+                                     int lmax) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = ei[e], b = ei[E + e];
@@ -90,11 +127,16 @@ __global__ void featurize_bwd_kernel(const float* __restrict__ pos, const int64_
       const float inv = 1.f / r;
       const float x = vx * inv, y = vy * inv, z = vz * inv;
       const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, s15 = 3.872983346207417f;
-      const float* g = g_sh + 9 * e;
-      // gradient w.r.t. the unit vector u = (x, y, z)
-      float ux = s3 * g[1] + s15 * z * g[4] + s15 * y * g[5] - s5 * x * g[6] - s15 * x * g[8];
-      float uy = s3 * g[2] + s15 * x * g[5] + 2.f * s5 * y * g[6] + s15 * z * g[7];
-      float uz = s3 * g[3] + s15 * x * g[4] - s5 * z * g[6] + s15 * y * g[7] + s15 * z * g[8];
+      const int nsh = (lmax + 1) * (lmax + 1);
+      const float* g = g_sh + (int64_t)nsh * e;
+      // gradient w.r.t. the unit vector u = (x, y, z) (components past lmax read as zero)
+      float gl[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) gl[k] = k < nsh ? g[k] : 0.f;
+      float ux = s3 * gl[1] + s15 * z * gl[4] + s15 * y * gl[5] - s5 * x * gl[6] - s15 * x * gl[8];
+      float uy = s3 * gl[2] + s15 * x * gl[5] + 2.f * s5 * y * gl[6] + s15 * z * gl[7];
+      float uz = s3 * gl[3] + s15 * x * gl[4] - s5 * z * gl[6] + s15 * y * gl[7] + s15 * z * gl[8];
+      if (lmax >= 3) sh_l3_grad(x, y, z, g + 9, ux, uy, uz);
       // through u = v / |v|: dv = (du - u (u . du)) / |v|
       const float dot = ux * x + uy * y + uz * z;
       gx += (ux - x * dot) * inv;
@@ -236,6 +278,16 @@ int gmp_edge_featurize_f32(const float* pos, const int64_t* edge_index, int64_t 
                            int num_bessel, const float* bessel_weights, float prefactor,
                            float r_max, float p_cutoff, float* vec_out, float* len_out,
                            float* sh_out, float* radial_out, void* stream) {
+  return gmp_edge_featurize_lmax_f32(pos, edge_index, n_edges, 2, num_bessel, bessel_weights,
+                                     prefactor, r_max, p_cutoff, vec_out, len_out, sh_out,
+                                     radial_out, stream);
+}
+
+int gmp_edge_featurize_lmax_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                int lmax, int num_bessel, const float* bessel_weights,
+                                float prefactor, float r_max, float p_cutoff, float* vec_out,
+                                float* len_out, float* sh_out, float* radial_out, void* stream) {
+  GMP_CHECK_ARG(lmax >= 0 && lmax <= 3);
   GMP_CHECK_ARG(n_edges >= 0 && num_bessel >= 0 && num_bessel <= kMaxBessel);
   if (n_edges == 0) return GMP_OK;
   GMP_CHECK_ARG(pos && edge_index && (radial_out == nullptr || bessel_weights));
@@ -246,7 +298,8 @@ int gmp_edge_featurize_f32(const float* pos, const int64_t* edge_index, int64_t 
   c.r_max = r_max;
   c.p = p_cutoff;
   featurize_fwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
-      pos, edge_index, n_edges, num_bessel, c, vec_out, len_out, sh_out, radial_out, nullptr);
+      pos, edge_index, n_edges, num_bessel, c, vec_out, len_out, sh_out, radial_out, nullptr,
+      lmax);
   return launch_status();
 }
 
@@ -254,6 +307,17 @@ int gmp_edge_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int6
                                int num_bessel, const float* bessel_weights, float prefactor,
                                float r_max, float p_cutoff, const float* g_sh,
                                const float* g_radial, float* g_vec, void* stream) {
+  return gmp_edge_featurize_lmax_bwd_f32(pos, edge_index, n_edges, 2, num_bessel,
+                                         bessel_weights, prefactor, r_max, p_cutoff, g_sh,
+                                         g_radial, g_vec, stream);
+}
+
+int gmp_edge_featurize_lmax_bwd_f32(const float* pos, const int64_t* edge_index,
+                                    int64_t n_edges, int lmax, int num_bessel,
+                                    const float* bessel_weights, float prefactor, float r_max,
+                                    float p_cutoff, const float* g_sh, const float* g_radial,
+                                    float* g_vec, void* stream) {
+  GMP_CHECK_ARG(lmax >= 0 && lmax <= 3);
   GMP_CHECK_ARG(n_edges >= 0 && num_bessel >= 0 && num_bessel <= kMaxBessel);
   if (n_edges == 0) return GMP_OK;
   GMP_CHECK_ARG(pos && edge_index && g_vec && (g_radial == nullptr || bessel_weights));
@@ -263,7 +327,7 @@ int gmp_edge_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int6
   c.r_max = r_max;
   c.p = p_cutoff;
   featurize_bwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
-      pos, edge_index, n_edges, num_bessel, c, g_sh, g_radial, nullptr, g_vec);
+      pos, edge_index, n_edges, num_bessel, c, g_sh, g_radial, nullptr, g_vec, lmax);
   return launch_status();
 }
 
@@ -280,7 +344,8 @@ int gmp_edge_featurize_gvp_f32(const float* pos, const int64_t* edge_index, int6
   c.r_max = r_max;
   c.p = p_cutoff;
   featurize_fwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
-      pos, edge_index, n_edges, num_bessel, c, nullptr, len_out, nullptr, radial_out, unit_out);
+      pos, edge_index, n_edges, num_bessel, c, nullptr, len_out, nullptr, radial_out, unit_out,
+      2);
   return launch_status();
 }
 
@@ -297,7 +362,7 @@ int gmp_edge_featurize_gvp_bwd_f32(const float* pos, const int64_t* edge_index, 
   c.r_max = r_max;
   c.p = p_cutoff;
   featurize_bwd_kernel<<<grid_for_edges(n_edges), 256, 0, as_stream(stream)>>>(
-      pos, edge_index, n_edges, num_bessel, c, nullptr, g_radial, g_unit, g_vec);
+      pos, edge_index, n_edges, num_bessel, c, nullptr, g_radial, g_unit, g_vec, 2);
   return launch_status();
 }
 

@@ -21,7 +21,10 @@
 namespace gmp {
 namespace {
 
-constexpr int kMaxPaths = 16;
+constexpr int kMaxPaths = 32;   // TFN / MACE at l <= 3: 27 paths
+constexpr int kMaxBlocks = 6;   // output irreps blocks (TFN gated l <= 3: 0e, 0e, 1o, 2e, 3o)
+constexpr int kMaxSh = 16;      // SH components (l <= 3) of the node-form z kernels
+constexpr int kMaxCg = 4096;    // CG floats of a descriptor (TFN l <= 3: 1,959)
 constexpr int kMaxIn = 1152;     // max in1 row dim
 constexpr int kMaxMul = 128;     // max mul1 / mul_out of a path
 constexpr int kMaxOut = 2048;    // max out row dim
@@ -36,7 +39,7 @@ struct Desc {
   int n_paths, in_dim, out_dim, sh_dim;
   long long weight_numel;
   int z_size, n_blocks;
-  int blk_off[4], blk_mul[4], blk_l[4];
+  int blk_off[kMaxBlocks], blk_mul[kMaxBlocks], blk_l[kMaxBlocks];
 };
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -524,6 +527,14 @@ bool desc_ok(const Desc& d, int layout) {
   return dim == d.out_dim;
 }
 
+// node-form z / dz kernels: any output block structure (the path GEMMs scatter the outputs),
+// l <= 3 everywhere (paths are checked by the host plan), SH rows of (lmax + 1)^2 floats
+bool desc_ok_z(const Desc& d) {
+  return d.n_paths > 0 && d.n_paths <= kMaxPaths && d.in_dim > 0 && d.in_dim <= kMaxIn &&
+         (d.sh_dim == 1 || d.sh_dim == 4 || d.sh_dim == 9 || d.sh_dim == kMaxSh) &&
+         d.z_size > 0 && d.n_blocks > 0 && d.n_blocks <= kMaxBlocks;
+}
+
 size_t smem_bytes(const Desc& d, int cg_len, bool bwd) {
   size_t f = (size_t)((cg_len + 3) & ~3) + ((d.in_dim + 3) & ~3) + 16 + 32 + kMaxMul * 5;
   if (bwd) f += (size_t)((d.out_dim + 3) & ~3) + d.in_dim;
@@ -543,7 +554,7 @@ __device__ __forceinline__ float wave_sum64(float v) {
 }
 
 template <int L1, int L2, int LO>
-__device__ __forceinline__ void t_table(const float* __restrict__ C, const float (&Y)[9],
+__device__ __forceinline__ void t_table(const float* __restrict__ C, const float (&Y)[kMaxSh],
                                         float (&T)[2 * L1 + 1][2 * LO + 1]) {
   constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * LO + 1, YO = L2 * L2;
 #pragma unroll
@@ -560,7 +571,7 @@ __device__ __forceinline__ void t_table(const float* __restrict__ C, const float
 
 template <int L1, int L2, int LO>
 __device__ __forceinline__ void z_path(const Path& P, const float* __restrict__ C,
-                                       const float (&Y)[9], const float* __restrict__ xrow,
+                                       const float (&Y)[kMaxSh], const float* __restrict__ xrow,
                                        float* __restrict__ zr, int lane) {
   constexpr int D1 = 2 * L1 + 1, D3 = 2 * LO + 1;
   float T[D1][D3];
@@ -584,14 +595,15 @@ __device__ __forceinline__ void z_path(const Path& P, const float* __restrict__ 
 }
 
 struct DxAcc {
-  float d0[2], d1[2][3], d2[2][5];
+  float d0[2], d1[2][3], d2[2][5], d3[2][7];
 };
 
 template <int L1, int L2, int LO>
 __device__ __forceinline__ void z_bwd_path(const Path& P, const float* __restrict__ C,
-                                           const float (&Y)[9], const float* __restrict__ xrow,
+                                           const float (&Y)[kMaxSh],
+                                           const float* __restrict__ xrow,
                                            const float* __restrict__ dzr, DxAcc& dx,
-                                           float (&dyp)[9], int lane) {
+                                           float (&dyp)[kMaxSh], int lane) {
   constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * LO + 1, YO = L2 * L2;
   float T[D1][D3];
   t_table<L1, L2, LO>(C, Y, T);
@@ -616,7 +628,8 @@ __device__ __forceinline__ void z_bwd_path(const Path& P, const float* __restric
         for (int k = 0; k < D3; ++k) a += T[i][k] * dz[k];
         if constexpr (L1 == 0) dx.d0[uu] += a;
         else if constexpr (L1 == 1) dx.d1[uu][i] += a;
-        else dx.d2[uu][i] += a;
+        else if constexpr (L1 == 2) dx.d2[uu][i] += a;
+        else dx.d3[uu][i] += a;
       }
 #pragma unroll
       for (int k = 0; k < D3; ++k)
@@ -637,14 +650,19 @@ __device__ __forceinline__ void z_bwd_path(const Path& P, const float* __restric
   }
 }
 
-// (l1, l2, lo) with l <= 2 and |l1 - l2| <= lo <= l1 + l2
+// (l1, l2, lo) with l <= 3 and |l1 - l2| <= lo <= l1 + l2 (every triangle, any parities)
 #define GMP_Z_PATHS(X)                                                                         \
-  X(0, 0, 0) X(0, 1, 1) X(0, 2, 2) X(1, 0, 1) X(1, 1, 0) X(1, 1, 1) X(1, 1, 2) X(1, 2, 1)      \
-  X(1, 2, 2) X(2, 0, 2) X(2, 1, 1) X(2, 1, 2) X(2, 2, 0) X(2, 2, 1) X(2, 2, 2)
+  X(0, 0, 0) X(0, 1, 1) X(0, 2, 2) X(0, 3, 3) X(1, 0, 1) X(1, 1, 0) X(1, 1, 1) X(1, 1, 2)      \
+  X(1, 2, 1) X(1, 2, 2) X(1, 2, 3) X(1, 3, 2) X(1, 3, 3) X(2, 0, 2) X(2, 1, 1) X(2, 1, 2)      \
+  X(2, 1, 3) X(2, 2, 0) X(2, 2, 1) X(2, 2, 2) X(2, 2, 3) X(2, 3, 1) X(2, 3, 2) X(2, 3, 3)      \
+  X(3, 0, 3) X(3, 1, 2) X(3, 1, 3) X(3, 2, 1) X(3, 2, 2) X(3, 2, 3) X(3, 3, 0) X(3, 3, 1)      \
+  X(3, 3, 2) X(3, 3, 3)
 
-__device__ __forceinline__ void load_y(const float* __restrict__ sh, int64_t eo, float (&Y)[9]) {
+// SH row of the edge: sh_dim = (lmax + 1)^2 in {1, 4, 9, 16} components (zeros past sh_dim)
+__device__ __forceinline__ void load_y(const float* __restrict__ sh, int64_t eo, int sh_dim,
+                                       float (&Y)[kMaxSh]) {
 #pragma unroll
-  for (int j = 0; j < 9; ++j) Y[j] = sh[eo * 9 + j];
+  for (int j = 0; j < kMaxSh; ++j) Y[j] = j < sh_dim ? sh[eo * sh_dim + j] : 0.f;
 }
 
 __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
@@ -652,7 +670,7 @@ __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
     const float* __restrict__ x, const float* __restrict__ sh,
     const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
     int64_t e1, float* __restrict__ zbuf) {
-  __shared__ float sC[4096];  // CG table (wave-uniform reads: LDS broadcast)
+  __shared__ float sC[kMaxCg];  // CG table (wave-uniform reads: LDS broadcast)
   for (int c = threadIdx.x; c < cg_len; c += blockDim.x) sC[c] = cg[c];
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -661,16 +679,16 @@ __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
   for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
     const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
     const int64_t src = src_sorted[e], eo = perm[e];
-    float Y[9];
-    load_y(sh, eo, Y);
+    float Y[kMaxSh];
+    load_y(sh, eo, d.sh_dim, Y);
     const float* xrow = x + src * d.in_dim;
     for (int p = 0; p < d.n_paths; ++p) {
       const Path P = paths[p];
       const float* C = sC + P.cg_off;
       float* zr = zbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
-      switch (P.l1 * 9 + P.l2 * 3 + P.lo) {
+      switch (P.l1 * 16 + P.l2 * 4 + P.lo) {
 #define GMP_Z_CASE(A, B, O) \
-  case A * 9 + B * 3 + O: z_path<A, B, O>(P, C, Y, xrow, zr, lane); break;
+  case A * 16 + B * 4 + O: z_path<A, B, O>(P, C, Y, xrow, zr, lane); break;
         GMP_Z_PATHS(GMP_Z_CASE)
 #undef GMP_Z_CASE
         default: break;
@@ -685,7 +703,7 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
     const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
     int64_t e1, const float* __restrict__ dzbuf, float* __restrict__ dx_edge,
     float* __restrict__ dY_edge) {
-  __shared__ float sC[4096];  // CG table (wave-uniform reads: LDS broadcast)
+  __shared__ float sC[kMaxCg];  // CG table (wave-uniform reads: LDS broadcast)
   for (int c = threadIdx.x; c < cg_len; c += blockDim.x) sC[c] = cg[c];
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -693,7 +711,7 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
   const int64_t nw = (int64_t)gridDim.x * 4;
   // input blocks (one per l1, as the path table lays them out; wave-uniform): the dx row is
   // written block by block, entries of the row no path reads are written as zero
-  int xoff[3] = {-1, -1, -1}, xmul[3] = {0, 0, 0};
+  int xoff[4] = {-1, -1, -1, -1}, xmul[4] = {0, 0, 0, 0};
   for (int p = 0; p < d.n_paths; ++p) {
     const Path P = paths[p];
     xoff[P.l1] = P.x_off;
@@ -702,10 +720,10 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
   for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
     const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
     const int64_t src = src_sorted[e], eo = perm[e];
-    float Y[9], dyp[9];
-    load_y(sh, eo, Y);
+    float Y[kMaxSh], dyp[kMaxSh];
+    load_y(sh, eo, d.sh_dim, Y);
 #pragma unroll
-    for (int j = 0; j < 9; ++j) dyp[j] = 0.f;
+    for (int j = 0; j < kMaxSh; ++j) dyp[j] = 0.f;
     DxAcc dx;
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
@@ -714,6 +732,8 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
       for (int i = 0; i < 3; ++i) dx.d1[uu][i] = 0.f;
 #pragma unroll
       for (int i = 0; i < 5; ++i) dx.d2[uu][i] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) dx.d3[uu][i] = 0.f;
     }
     const float* xrow = x + src * d.in_dim;
     for (int p = 0; p < d.n_paths; ++p) {
@@ -721,9 +741,9 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
       const float* C = sC + P.cg_off;
       const float* dzr =
           dzbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
-      switch (P.l1 * 9 + P.l2 * 3 + P.lo) {
+      switch (P.l1 * 16 + P.l2 * 4 + P.lo) {
 #define GMP_ZB_CASE(A, B, O) \
-  case A * 9 + B * 3 + O: z_bwd_path<A, B, O>(P, C, Y, xrow, dzr, dx, dyp, lane); break;
+  case A * 16 + B * 4 + O: z_bwd_path<A, B, O>(P, C, Y, xrow, dzr, dx, dyp, lane); break;
         GMP_Z_PATHS(GMP_ZB_CASE)
 #undef GMP_ZB_CASE
         default: break;
@@ -742,23 +762,29 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
 #pragma unroll
         for (int i = 0; i < 5; ++i) dxr[xoff[2] + 5 * u + i] = dx.d2[uu][i];
       }
+      if (xoff[3] >= 0 && u < xmul[3]) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) dxr[xoff[3] + 7 * u + i] = dx.d3[uu][i];
+      }
     }
-    if (xmul[0] + 3 * xmul[1] + 5 * xmul[2] != d.in_dim) {  // rows read by no path: zero
-      for (int c = lane; c < d.in_dim; c += 64) {
+    if (xmul[0] + 3 * xmul[1] + 5 * xmul[2] + 7 * xmul[3] != d.in_dim) {
+      for (int c = lane; c < d.in_dim; c += 64) {  // rows read by no path: zero
         bool in = false;
 #pragma unroll
-        for (int b = 0; b < 3; ++b)
+        for (int b = 0; b < 4; ++b)
           in |= xoff[b] >= 0 && c >= xoff[b] && c < xoff[b] + xmul[b] * (2 * b + 1);
         if (!in) dxr[c] = 0.f;
       }
     }
     float dyv = 0.f;
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const float v = wave_sum64(dyp[j]);
-      dyv = (lane == j) ? v : dyv;
+    for (int j = 0; j < kMaxSh; ++j) {
+      if (j < d.sh_dim) {  // wave-uniform
+        const float v = wave_sum64(dyp[j]);
+        dyv = (lane == j) ? v : dyv;
+      }
     }
-    if (lane < 9) dY_edge[k * 9 + lane] = dyv;
+    if (lane < d.sh_dim) dY_edge[k * d.sh_dim + lane] = dyv;
   }
 }
 
@@ -849,7 +875,7 @@ int gmp_tp_edge_z_f32(const void* desc_host, const void* paths_dev, const float*
                       const int64_t* perm, int64_t e0, int64_t e1, float* zbuf, void* stream) {
   GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && zbuf);
   const Desc d = *reinterpret_cast<const Desc*>(desc_host);
-  GMP_CHECK_ARG(desc_ok(d, d.n_blocks == 3 ? 0 : 1) && cg_len > 0 && cg_len <= 4096);
+  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= kMaxCg);
   GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
   if (e1 == e0) return GMP_OK;
   tp_edge_z2_kernel<<<(unsigned)z2_blocks(e1 - e0), 256, 0, as_stream(stream)>>>(
@@ -864,7 +890,7 @@ int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const fl
   GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && dzbuf &&
                 dx_edge && dY_edge);
   const Desc d = *reinterpret_cast<const Desc*>(desc_host);
-  GMP_CHECK_ARG(desc_ok(d, d.n_blocks == 3 ? 0 : 1) && cg_len > 0 && cg_len <= 4096);
+  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= kMaxCg);
   GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
   if (e1 == e0) return GMP_OK;
   tp_edge_z2_bwd_kernel<<<(unsigned)z2_blocks(e1 - e0), 256, 0, as_stream(stream)>>>(

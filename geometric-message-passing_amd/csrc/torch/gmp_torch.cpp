@@ -393,31 +393,35 @@ int64_t edge_checks(const Tensor& pos, const Tensor& edge_index) {
 
 std::tuple<Tensor, Tensor> edge_featurize(const Tensor& pos, const Tensor& edge_index,
                                           at::ArrayRef<double> bessel_w, double prefactor,
-                                          double r_max, double p) {
+                                          double r_max, double p, int64_t lmax) {
   OpGuard g(pos, "edge_featurize");
   const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
+  TORCH_CHECK(0 <= lmax && lmax <= 3, "gmp.edge_featurize: lmax in 0..3");
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
-  Tensor sh = at::empty({E, 9}, pos.options()), rad = at::empty({E, nb}, pos.options());
-  check_rc(gmp_edge_featurize_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(), (float)prefactor,
-                                  (float)r_max, (float)p, nullptr, nullptr, fp(sh), fp(rad),
-                                  cur_stream()),
-           "gmp_edge_featurize_f32");
+  Tensor sh = at::empty({E, (lmax + 1) * (lmax + 1)}, pos.options());
+  Tensor rad = at::empty({E, nb}, pos.options());
+  check_rc(gmp_edge_featurize_lmax_f32(fp(pos), ip(edge_index), E, (int)lmax, (int)nb, w.data(),
+                                       (float)prefactor, (float)r_max, (float)p, nullptr, nullptr,
+                                       fp(sh), fp(rad), cur_stream()),
+           "gmp_edge_featurize_lmax_f32");
   return {sh, rad};
 }
 
 Tensor edge_featurize_bwd(const Tensor& pos, const Tensor& edge_index,
                           at::ArrayRef<double> bessel_w, double prefactor, double r_max, double p,
-                          const optional<Tensor>& g_sh, const optional<Tensor>& g_rad) {
+                          const optional<Tensor>& g_sh, const optional<Tensor>& g_rad,
+                          int64_t lmax) {
   OpGuard g(pos, "edge_featurize_bwd");
   const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
-  opt_f32(g_sh, {E, 9}, "g_sh");
+  TORCH_CHECK(0 <= lmax && lmax <= 3, "gmp.edge_featurize_bwd: lmax in 0..3");
+  opt_f32(g_sh, {E, (lmax + 1) * (lmax + 1)}, "g_sh");
   opt_f32(g_rad, {E, nb}, "g_radial");
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
   Tensor gv = at::empty({E, 3}, pos.options());
-  check_rc(gmp_edge_featurize_bwd_f32(fp(pos), ip(edge_index), E, (int)nb, w.data(),
-                                      (float)prefactor, (float)r_max, (float)p, cfp(g_sh),
-                                      cfp(g_rad), fp(gv), cur_stream()),
-           "gmp_edge_featurize_bwd_f32");
+  check_rc(gmp_edge_featurize_lmax_bwd_f32(fp(pos), ip(edge_index), E, (int)lmax, (int)nb,
+                                           w.data(), (float)prefactor, (float)r_max, (float)p,
+                                           cfp(g_sh), cfp(g_rad), fp(gv), cur_stream()),
+           "gmp_edge_featurize_lmax_bwd_f32");
   return gv;
 }
 
@@ -636,24 +640,24 @@ std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t co
 
 // ------------------------------------------------------------------ K7 per-edge z rows
 // The host descriptor travels as int[] (n_paths, in_dim, out_dim, sh_dim, weight_numel, z_size,
-// n_blocks, blk_off[4], blk_mul[4], blk_l[4]); the 64-byte path records as a device uint8 tensor.
+// n_blocks, blk_off[6], blk_mul[6], blk_l[6]); the 64-byte path records as a device uint8 tensor.
 struct TpDescHost {
   int n_paths, in_dim, out_dim, sh_dim;
   long long weight_numel;
   int z_size, n_blocks;
-  int blk_off[4], blk_mul[4], blk_l[4];
+  int blk_off[6], blk_mul[6], blk_l[6];
 };
-static_assert(sizeof(TpDescHost) == 80, "descriptor layout (include/gmp.h)");
+static_assert(sizeof(TpDescHost) == 104, "descriptor layout (include/gmp.h)");
 
 TpDescHost tp_desc(at::IntArrayRef d) {
-  TORCH_CHECK(d.size() == 19, "gmp.tp: descriptor has 19 ints");
+  TORCH_CHECK(d.size() == 25, "gmp.tp: descriptor has 25 ints");
   TpDescHost h;
   h.n_paths = (int)d[0]; h.in_dim = (int)d[1]; h.out_dim = (int)d[2]; h.sh_dim = (int)d[3];
   h.weight_numel = d[4]; h.z_size = (int)d[5]; h.n_blocks = (int)d[6];
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 6; ++k) {
     h.blk_off[k] = (int)d[7 + k];
-    h.blk_mul[k] = (int)d[11 + k];
-    h.blk_l[k] = (int)d[15 + k];
+    h.blk_mul[k] = (int)d[13 + k];
+    h.blk_l[k] = (int)d[19 + k];
   }
   return h;
 }
@@ -1270,12 +1274,14 @@ std::tuple<Tensor, Tensor> ln_act_bwd(const Tensor&, const Tensor& xhat, const T
   return {at::empty_like(xhat), at::empty({2 * xhat.size(-1)}, xhat.options())};
 }
 std::tuple<Tensor, Tensor> edge_featurize(const Tensor& pos, const Tensor& ei,
-                                          at::ArrayRef<double> w, double, double, double) {
-  return {at::empty({ei.size(1), 9}, pos.options()),
+                                          at::ArrayRef<double> w, double, double, double,
+                                          int64_t lmax) {
+  return {at::empty({ei.size(1), (lmax + 1) * (lmax + 1)}, pos.options()),
           at::empty({ei.size(1), (int64_t)w.size()}, pos.options())};
 }
 Tensor edge_featurize_bwd(const Tensor& pos, const Tensor& ei, at::ArrayRef<double>, double,
-                          double, double, const optional<Tensor>&, const optional<Tensor>&) {
+                          double, double, const optional<Tensor>&, const optional<Tensor>&,
+                          int64_t) {
   return at::empty({ei.size(1), 3}, pos.options());
 }
 std::tuple<Tensor, Tensor> edge_featurize_gvp(const Tensor& pos, const Tensor& ei,
@@ -1444,9 +1450,10 @@ TORCH_LIBRARY(gmp, m) {
   m.def("ln_act_bwd(Tensor grad_y, Tensor xhat, Tensor rstd, Tensor gamma, Tensor beta, "
         "int act) -> (Tensor grad_x, Tensor grad_gamma_beta)");
   m.def("edge_featurize(Tensor pos, Tensor edge_index, float[] bessel_weights, float prefactor, "
-        "float r_max, float p) -> (Tensor sh, Tensor radial)");
+        "float r_max, float p, int lmax=2) -> (Tensor sh, Tensor radial)");
   m.def("edge_featurize_bwd(Tensor pos, Tensor edge_index, float[] bessel_weights, "
-        "float prefactor, float r_max, float p, Tensor? g_sh, Tensor? g_radial) -> Tensor");
+        "float prefactor, float r_max, float p, Tensor? g_sh, Tensor? g_radial, int lmax=2) "
+        "-> Tensor");
   m.def("edge_featurize_gvp(Tensor pos, Tensor edge_index, float[] bessel_weights, "
         "float prefactor, float r_max, float p) -> (Tensor radial, Tensor unit)");
   m.def("edge_featurize_gvp_bwd(Tensor pos, Tensor edge_index, float[] bessel_weights, "

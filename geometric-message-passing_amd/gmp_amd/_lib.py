@@ -40,10 +40,10 @@ class TpPath(ctypes.Structure):
 class TpDesc(ctypes.Structure):
     _fields_ = [("n_paths", c_int), ("in_dim", c_int), ("out_dim", c_int), ("sh_dim", c_int),
                 ("weight_numel", ctypes.c_longlong), ("z_size", c_int), ("n_blocks", c_int),
-                ("blk_off", c_int * 4), ("blk_mul", c_int * 4), ("blk_l", c_int * 4)]
+                ("blk_off", c_int * 6), ("blk_mul", c_int * 6), ("blk_l", c_int * 6)]
 
 
-assert ctypes.sizeof(TpPath) == 64 and ctypes.sizeof(TpDesc) == 80
+assert ctypes.sizeof(TpPath) == 64 and ctypes.sizeof(TpDesc) == 104
 
 # name -> (restype, argtypes); must mirror include/gmp.h exactly
 SIGNATURES = {
@@ -80,6 +80,10 @@ SIGNATURES = {
                                        c_vp, c_vp, c_vp, c_vp]),
     "gmp_edge_featurize_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32,
                                            c_vp, c_vp, c_vp, c_vp]),
+    "gmp_edge_featurize_lmax_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_f32, c_f32,
+                                            c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_edge_featurize_lmax_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_f32,
+                                                c_f32, c_f32, c_vp, c_vp, c_vp, c_vp]),
     "gmp_edge_featurize_gvp_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32, c_f32,
                                            c_vp, c_vp, c_vp, c_vp]),
     "gmp_edge_featurize_gvp_bwd_f32": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_f32, c_f32,

@@ -79,36 +79,37 @@ class RadialEmbeddingBlock(nn.Module):
 
 
 class EdgeFeaturizeFn(torch.autograd.Function):
-    """K1: (pos, edge_index) -> (edge_sh (E,9), edge_feats (E,nb)) in one pass over the edges."""
+    """K1: (pos, edge_index) -> (edge_sh (E, (lmax+1)^2), edge_feats (E,nb)) in one pass over the
+    edges (lmax <= 3: the models' max_ell)."""
 
     @staticmethod
-    def forward(ctx, pos, edge_index, host_consts, graph):
+    def forward(ctx, pos, edge_index, host_consts, graph, lmax=2):
         w, pref, r_max, p = host_consts
         pos = _f32c(pos)
         ei = edge_index.contiguous()
         _need_cuda(pos, ei)
         with _timed("edge_featurize"):
             sh, rad = _lib.torch_ops().edge_featurize(pos, ei, [float(v) for v in w], pref, r_max,
-                                                      p)
+                                                      p, lmax)
         ctx.save_for_backward(pos, ei)
-        ctx.host, ctx.graph = host_consts, graph
+        ctx.host, ctx.graph, ctx.lmax = host_consts, graph, lmax
         return sh, rad
 
     @staticmethod
     @once_differentiable
     def backward(ctx, g_sh, g_rad):
         if not ctx.needs_input_grad[0]:
-            return None, None, None, None
+            return None, None, None, None, None
         pos, ei = ctx.saved_tensors
         w, pref, r_max, p = ctx.host
         g_vec = _lib.torch_ops().edge_featurize_bwd(
             pos, ei, [float(v) for v in w], pref, r_max, p,
             _f32c(g_sh) if g_sh is not None else None,
-            _f32c(g_rad) if g_rad is not None else None)
+            _f32c(g_rad) if g_rad is not None else None, ctx.lmax)
         g = ctx.graph  # vectors = pos[ei0] - pos[ei1]: + into receivers, - into senders
         plus, _ = ops.segment_reduce(g_vec, g.recv_csr, "sum")
         minus, _ = ops.segment_reduce(ops.gather_rows(g_vec, g.perm), g.src_csr, "sum")
-        return plus - minus, None, None, None
+        return plus - minus, None, None, None, None
 
 
 def spherical_harmonics_l2(vec, normalize=True):
@@ -374,11 +375,18 @@ class TPPlan:
         self.instructions, self.weight_numel = o3.fctp_instructions(irreps_in, irreps_sh,
                                                                     irreps_out)
         key = tuple(ir for _, ir in irreps_out)
-        if key not in _LAYOUTS or any(m > 128 or m % 4 for m, _ in irreps_out) or \
-                any(m > 128 for m, _ in irreps_in) or \
-                any(m != 1 for m, _ in irreps_sh) or o3.irreps_dim(irreps_sh) != 9:
-            raise NotImplementedError(f"TP layout {o3.irreps_str(irreps_out)} not supported by K7")
-        self.layout = _LAYOUTS[key]
+        sh_dim = o3.irreps_dim(irreps_sh)
+        if any(m != 1 for m, _ in irreps_sh) or sh_dim not in (1, 4, 9, 16) or \
+                any(m > 128 for m, _ in irreps_in) or len(irreps_out) > 6 or \
+                any(ir[0] > 3 for _, ir in tuple(irreps_in) + tuple(irreps_out)) or \
+                len(self.instructions) > 32:
+            raise NotImplementedError(f"TP {o3.irreps_str(irreps_in)} x {o3.irreps_str(irreps_sh)}"
+                                      f" -> {o3.irreps_str(irreps_out)} not supported by K7")
+        # the per-edge-weight kernels (GMP_TP_MODE=edge) take the two l <= 2 layouts; the node
+        # form (default) any block structure with l <= 3
+        edge_ok = (key in _LAYOUTS and sh_dim == 9 and
+                   not any(m > 128 or m % 4 for m, _ in irreps_out))
+        self.layout = _LAYOUTS[key] if edge_ok else None
         xo, yo, oo = (o3.irreps_offsets(irreps_in), o3.irreps_offsets(irreps_sh),
                       o3.irreps_offsets(irreps_out))
         paths = (_lib.TpPath * len(self.instructions))()
@@ -398,17 +406,18 @@ class TPPlan:
         self.desc.n_paths = len(self.instructions)
         self.desc.in_dim = o3.irreps_dim(irreps_in)
         self.desc.out_dim = o3.irreps_dim(irreps_out)
-        self.desc.sh_dim = 9
+        self.desc.sh_dim = sh_dim
+        self.sh_dim = sh_dim
         self.desc.weight_numel = self.weight_numel
         self.desc.z_size = z_off
         self.desc.n_blocks = len(irreps_out)
         for b, (m, (l, _)) in enumerate(irreps_out):
             self.desc.blk_off[b], self.desc.blk_mul[b], self.desc.blk_l[b] = oo[b], m, l
-        self.blocks = [(oo[b], m) for b, (m, _) in enumerate(irreps_out)]
+        self.blocks = [(oo[b], m) for b, (m, _) in enumerate(irreps_out)]  # (offset, mul)
         # plain-int copies (the autograd Functions read these, never the ctypes descriptor)
         self.in_dim, self.out_dim = self.desc.in_dim, self.desc.out_dim
         self.z_size = self.desc.z_size
-        d = self.desc  # the descriptor as torch.ops.gmp.tp_* take it (int[19])
+        d = self.desc  # the descriptor as torch.ops.gmp.tp_* take it (int[25])
         self.desc_list = ([d.n_paths, d.in_dim, d.out_dim, d.sh_dim, d.weight_numel, d.z_size,
                            d.n_blocks] + list(d.blk_off) + list(d.blk_mul) + list(d.blk_l))
         # node form: path p's z rows (mul1 * (2lo+1) floats) at z_off_p * (n_e + 1)
@@ -476,7 +485,7 @@ class TPConvFn(torch.autograd.Function):
         N, E = graph.num_nodes, graph.num_edges
         f = dict(dtype=torch.float32, device=x.device)
         dx_edge = torch.empty((E, plan.in_dim), **f)
-        dY = torch.empty((E, 9), **f)
+        dY = torch.empty((E, plan.sh_dim), **f)
         drad_s = torch.empty_like(rad_s)
         dW2 = torch.zeros_like(W2)
         db2 = torch.zeros_like(b2)
@@ -638,7 +647,7 @@ class TPConvNodeFn(torch.autograd.Function):
         H = W1.shape[0]
         f = dict(dtype=torch.float32, device=x.device)
         dx_edge = torch.empty((E, plan.in_dim), **f)
-        dY = torch.empty((E, 9), **f)
+        dY = torch.empty((E, plan.sh_dim), **f)
         drad_s = torch.empty_like(rad_s)
         dW1, db1 = torch.zeros_like(W1), torch.zeros_like(b1)
         W2c, b2c = W2.contiguous(), b2.contiguous()
@@ -783,6 +792,9 @@ class TensorProductConvLayer(nn.Module):
         graph = tp_graph(edge_index, node_attr.shape[0])
         fn = TPConvNodeFn if (TP_MODE == "node" and node_form_ok(self.fc[0].out_features)) \
             else TPConvFn
+        if fn is TPConvFn and self.plan.layout is None:
+            raise NotImplementedError("the per-edge-weight TP kernels take l <= 2 layouts only; "
+                                      "use the node form (GMP_TP_MODE=node, mlp_dim % 16 == 0)")
         paths, cg = self._tp_paths, self._tp_cg
         if paths.device != node_attr.device or cg.dtype != torch.float32:
             paths, cg = self.plan.device_tables(node_attr.device)
@@ -972,7 +984,8 @@ class EquivariantProductBasisBlock(nn.Module):
 # ===================================================================================== models
 def _edge_features(model, batch):
     graph = tp_graph(batch.edge_index, batch.pos.shape[0])
-    return EdgeFeaturizeFn.apply(batch.pos, batch.edge_index, model.radial_embedding._host, graph)
+    return EdgeFeaturizeFn.apply(batch.pos, batch.edge_index, model.radial_embedding._host, graph,
+                                 model.max_ell)
 
 
 class MACEModel(nn.Module):
@@ -1038,8 +1051,9 @@ class TFNModel(nn.Module):
                  aggr="sum", pool="first", gate=True, batch_norm=False, residual=True,
                  equivariant_pred=False):
         super().__init__()
-        if max_ell != 2:
-            raise NotImplementedError("K1/K7 are specialised to l <= 2 (the configs' L_max)")
+        if max_ell not in (1, 2, 3):
+            raise NotImplementedError("K1 / K7 take max_ell <= 3")
+        self.max_ell = max_ell
         self.emb_dim, self.residual, self.equivariant_pred = emb_dim, residual, equivariant_pred
         self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)
         sh = o3.sh_irreps(max_ell)

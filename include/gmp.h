@@ -251,6 +251,18 @@ int gmp_edge_featurize_bwd_f32(const float* pos, const int64_t* edge_index, int6
                                int num_bessel, const float* bessel_weights, float prefactor,
                                float r_max, float p_cutoff, const float* g_sh,
                                const float* g_radial, float* g_vec, void* stream);
+/* The same for SphericalHarmonics(lmax) with 0 <= lmax <= 3 (max_ell of models/tfn.py:51 /
+ * mace.py:25): sh rows of (lmax + 1)^2 floats, the l = 3 block being e3nn's component-
+ * normalised sh_3_m (the lmax = 2 entries above are these with lmax = 2). */
+int gmp_edge_featurize_lmax_f32(const float* pos, const int64_t* edge_index, int64_t n_edges,
+                                int lmax, int num_bessel, const float* bessel_weights,
+                                float prefactor, float r_max, float p_cutoff, float* vec_out,
+                                float* len_out, float* sh_out, float* radial_out, void* stream);
+int gmp_edge_featurize_lmax_bwd_f32(const float* pos, const int64_t* edge_index,
+                                    int64_t n_edges, int lmax, int num_bessel,
+                                    const float* bessel_weights, float prefactor, float r_max,
+                                    float p_cutoff, const float* g_sh, const float* g_radial,
+                                    float* g_vec, void* stream);
 /* GVP-GNN edge features (models/gvpgnn.py:106-112): len (E), radial (E,nb) as above and the unit
  * vectors nan_to_num(vec / len) (E,3; zero rows for zero-length edges).  Backward from g_radial /
  * g_unit (either may be NULL) to g_vec. */
@@ -317,7 +329,10 @@ int gmp_irreps_bn_bwd_f32(int64_t B, int C, int nf, const int32_t* col_chan,
  * x (N, in_dim) mul_ir; sh (E, 9) in ORIGINAL edge order; W row r = sorted edge c0 + r.
  * Forward writes msg rows c0..c1-1 (E x out_dim, sorted positions).
  * desc_host: host pointer to the descriptor {int n_paths, in_dim, out_dim, sh_dim;
- *   int64 weight_numel; int z_size, n_blocks; int blk_off[4], blk_mul[4], blk_l[4];}
+ *   int64 weight_numel; int z_size, n_blocks; int blk_off[6], blk_mul[6], blk_l[6];}
+ *   (104 bytes; <= 32 paths).  The per-edge-weight kernels below take l <= 2 (sh_dim 9, the
+ *   two layouts); the node-form z / dz kernels (gmp_tp_edge_z*) take l <= 3 (sh_dim (lmax+1)^2
+ *   <= 16, any block structure: max_ell = 3 models).
  * paths_dev: device array of 64-byte path records {int l1, l2, lo, mul1, mul_out, x_off, y_off,
  *   io, out_off, z_off, cg_off, pad; int64 w_off; float alpha, pad}; cg_dev: concatenated
  *   real CG tensors (cg_len floats).  layout: 0 = out blocks (0e,1o,2e), 1 = (0e,0e,1o,2e).

@@ -185,10 +185,10 @@ def _hidden_irreps(emb_dim, max_ell):
     return o3.Irreps([(emb_dim, (l, (-1) ** l)) for l in range(max_ell + 1)])
 
 
-def edge_features(pos, edge_index, radial):
+def edge_features(pos, edge_index, radial, max_ell=2):
     vectors = pos[edge_index[0]] - pos[edge_index[1]]          # mace.py:170 / tfn.py:171
     lengths = torch.linalg.norm(vectors, dim=-1, keepdim=True)  # mace.py:171
-    return o3.spherical_harmonics_l2(vectors), radial(lengths)
+    return o3.spherical_harmonics(vectors, max_ell), radial(lengths)
 
 
 class MACEModel(nn.Module):
@@ -240,14 +240,15 @@ def first_node_pooling(x, batch, size=None):
 
 
 class TFNModel(nn.Module):
-    """models/tfn.py:42-190 (max_ell = 2)."""
+    """models/tfn.py:42-190 (max_ell <= 3)."""
 
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
                  num_layers=5, emb_dim=64, mlp_dim=256, in_dim=1, out_dim=1, aggr="sum",
                  pool="first", gate=True, batch_norm=False, residual=True,
                  equivariant_pred=False):
         super().__init__()
-        assert max_ell == 2
+        assert 1 <= max_ell <= 3
+        self.max_ell = max_ell
         self.emb_dim, self.residual, self.equivariant_pred = emb_dim, residual, equivariant_pred
         self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)
         sh = o3.spherical_harmonics_irreps(max_ell)
@@ -268,7 +269,8 @@ class TFNModel(nn.Module):
 
     def forward(self, batch):
         h = self.emb_in(batch.atoms)
-        edge_sh, edge_feats = edge_features(batch.pos, batch.edge_index, self.radial_embedding)
+        edge_sh, edge_feats = edge_features(batch.pos, batch.edge_index, self.radial_embedding,
+                                            self.max_ell)
         for conv in self.convs:
             hu = conv(h, batch.edge_index, edge_sh, edge_feats)
             h = hu + F.pad(h, (0, hu.shape[-1] - h.shape[-1])) if self.residual else hu

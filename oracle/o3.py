@@ -85,6 +85,35 @@ def spherical_harmonics_l2(vec, normalize=True):
     ], dim=-1)
 
 
+def spherical_harmonics(vec, lmax, normalize=True):
+    """e3nn SphericalHarmonics(range(lmax+1), normalize, 'component') -> (..., (lmax+1)^2),
+    lmax <= 3.  e3nn 0.5.1 o3/_spherical_harmonics.py generates each l from l-1 by the CG
+    recursion and scales l by sqrt(2l+1); the l = 3 block restated here in closed form
+    (checked against that recursion, unit-vector norm 2l+1 and equivariance in
+    tests/test_oracle_o3.py)."""
+    assert 0 <= lmax <= 3
+    Y = spherical_harmonics_l2(vec, normalize)[..., :(lmax + 1) ** 2]
+    if lmax < 3:
+        return Y
+    if normalize:
+        vec = torch.nn.functional.normalize(vec, dim=-1)
+    x, y, z = vec[..., 0], vec[..., 1], vec[..., 2]
+    s20 = math.sqrt(3.0) * x * z                 # e3nn's un-normalised sh_2_0 / sh_2_4
+    s24 = math.sqrt(3.0) / 2.0 * (z * z - x * x)
+    q = 4.0 * y * y - x * x - z * z
+    s7 = math.sqrt(7.0)
+    l3 = torch.stack([
+        math.sqrt(5.0 / 6.0) * (s20 * z + s24 * x),
+        math.sqrt(5.0) * s20 * y,
+        math.sqrt(3.0 / 8.0) * q * x,
+        0.5 * y * (2.0 * y * y - 3.0 * (x * x + z * z)),
+        math.sqrt(3.0 / 8.0) * z * q,
+        math.sqrt(5.0) * s24 * y,
+        math.sqrt(5.0 / 6.0) * (s24 * z - s20 * x),
+    ], dim=-1) * s7
+    return torch.cat([Y, l3], dim=-1)
+
+
 # ----------------------------------------------------------------------------------- CG
 
 

@@ -72,7 +72,7 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
     assert [tuple(t.shape) for t in out] == [(1000, 128), (1000, 16, 3), (1000, 128),
                                             (1000, 128), (1000, 16), (1000, 16), (1000, 48),
                                             (1000, 48), (1000, 48)]
-    z = tops.tp_edge_z([11, 1152, 1152, 9, 180224, 4480, 3] + [0] * 12,
+    z = tops.tp_edge_z([11, 1152, 1152, 9, 180224, 4480, 3] + [0] * 18,
                        torch.empty(11 * 64, dtype=torch.uint8, device="meta"),
                        torch.empty(10, device="meta"), torch.empty(50, 1152, device="meta"),
                        torch.empty(700, 9, device="meta"),

@@ -41,7 +41,8 @@ def _grads(model, ref, rtol=1e-4):
         _close_scaled(p.grad, q.grad, rtol, name)
 
 
-def test_featurize_vs_oracle():
+@pytest.mark.parametrize("lmax", [2, 3, 1])
+def test_featurize_vs_oracle(lmax):
     from gmp_amd import equivariant as eq
     g = _graph(500, 8000, seed=3)
     rad_p = eq.RadialEmbeddingBlock(2.0, 8, 5)
@@ -49,10 +50,11 @@ def test_featurize_vs_oracle():
     pos_d = g.pos.to(DEV).requires_grad_(True)
     ei_d = g.edge_index.to(DEV)
     graph = eq.tp_graph(ei_d, g.num_nodes)
-    sh, rad = eq.EdgeFeaturizeFn.apply(pos_d, ei_d, rad_p._host, graph)
+    sh, rad = eq.EdgeFeaturizeFn.apply(pos_d, ei_d, rad_p._host, graph, lmax)
+    assert sh.shape == (g.num_edges, (lmax + 1) ** 2)
     pos_o = g.pos.clone().requires_grad_(True)
     vec = pos_o[g.edge_index[0]] - pos_o[g.edge_index[1]]
-    sh_o = oo3.spherical_harmonics_l2(vec)
+    sh_o = oo3.spherical_harmonics(vec, lmax)
     rad_o_v = rad_o(torch.linalg.norm(vec, dim=-1, keepdim=True))
     torch.testing.assert_close(sh.cpu(), sh_o.detach(), atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(rad.cpu(), rad_o_v.detach(), atol=1e-5, rtol=1e-5)
@@ -99,6 +101,53 @@ def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp, mode, monkeypatc
     for a, b, nm in zip(xs, xr, ("dx", "dsh", "dedge_feat")):
         _close_scaled(a.grad, b.grad, 1e-4, nm)
     _grads(lay, ref)
+
+
+@pytest.mark.parametrize("inp,out,gate,mlp", [
+    ("16x0e", "16x0e+16x1o+16x2e+16x3o", True, 32),
+    ("16x0e+16x1o+16x2e+16x3o", "16x0e+16x1o+16x2e+16x3o", True, 32),
+    ("32x0e+32x1o+32x2e+32x3o", "32x0e+32x1o+32x2e+32x3o", False, 64),
+    ("32x0e+32x1o+32x2e+32x3o", "32x0e+32x1o+32x2e+32x3o", True, 64),
+])
+def test_tp_conv_layer_l3_vs_oracle(inp, out, gate, mlp):
+    """max_ell = 3 (TFN's max_ell kwarg, tfn.py:47): 16-dim SH, l = 3 hidden blocks, up to 27
+    paths (34 with the l=3 x l=3 couplings); node form only (the per-edge-weight layouts are
+    l <= 2 and refuse)."""
+    from gmp_amd import equivariant as eq
+    torch.manual_seed(len(inp) + mlp)
+    n = 300
+    g = _graph(n, 12 * n, seed=mlp)
+    ref = om.TensorProductConvLayer(inp, out, oo3.spherical_harmonics_irreps(3), 8, mlp, "add",
+                                    gate=gate)
+    lay = eq.TensorProductConvLayer(inp, out, eq.o3.sh_irreps(3), 8, mlp, "add", gate=gate)
+    assert lay.plan.layout is None and lay.plan.sh_dim == 16
+    lay.load_state_dict(ref.state_dict())
+    lay = lay.to(DEV)
+    x = torch.randn(g.num_nodes, oo3.Irreps(inp).dim)
+    sh = oo3.spherical_harmonics(g.pos[g.edge_index[0]] - g.pos[g.edge_index[1]], 3)
+    ef = torch.rand(g.num_edges, 8)
+    xs = [t.clone().to(DEV).requires_grad_(True) for t in (x, sh, ef)]
+    xr = [t.clone().requires_grad_(True) for t in (x, sh, ef)]
+    y = lay(xs[0], g.edge_index.to(DEV), xs[1], xs[2])
+    yr = ref(xr[0], g.edge_index, xr[1], xr[2])
+    torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-5, rtol=1e-5)
+    gy = torch.randn_like(yr)
+    (y * gy.to(DEV)).sum().backward()
+    (yr * gy).sum().backward()
+    for a, b, nm in zip(xs, xr, ("dx", "dsh", "dedge_feat")):
+        _close_scaled(a.grad, b.grad, 1e-4, nm)
+    _grads(lay, ref)
+
+
+def test_tp_conv_layer_l3_edge_form_refuses(monkeypatch):
+    from gmp_amd import equivariant as eq
+    monkeypatch.setattr(eq, "TP_MODE", "edge")
+    irr = "8x0e+8x1o+8x2e+8x3o"
+    lay = eq.TensorProductConvLayer(irr, irr, eq.o3.sh_irreps(3), 8, 16, "add").to(DEV)
+    g = _graph(50, 400, seed=5)
+    with pytest.raises(NotImplementedError, match="l <= 2"):
+        lay(torch.randn(g.num_nodes, 128, device=DEV), g.edge_index.to(DEV),
+            torch.randn(g.num_edges, 16, device=DEV), torch.rand(g.num_edges, 8, device=DEV))
 
 
 @pytest.mark.parametrize("mode", ["node", "edge"])
@@ -283,6 +332,14 @@ def test_tfn_c5_per_rank_model_vs_oracle():
     first-node pooling; tfn.py:53-60 defaults)."""
     ne = _fp64_model_check("TFNModel", dict(num_layers=5, emb_dim=64, max_ell=2, mlp_dim=256,
                                             gate=True, r_max=10.0), 80, 10)
+    assert ne <= 2000
+
+
+def test_tfn_max_ell3_model_vs_oracle():
+    """TFN with max_ell=3 (tfn.py:47 kwarg; the 64-channel gated blocks of C5 widened by 3o:
+    27 paths per layer, the 192-wide gate block on the library-GEMM fallback, the rest on K7g)."""
+    ne = _fp64_model_check("TFNModel", dict(num_layers=2, emb_dim=64, max_ell=3, mlp_dim=256,
+                                            gate=True, r_max=10.0), 60, 10)
     assert ne <= 2000
 
 

@@ -39,6 +39,51 @@ def test_sh_known_values():
     torch.testing.assert_close(o3.spherical_harmonics_l2(3.7 * v), Yv)
 
 
+def test_sh_l3_norm_equivariance_and_recursion():
+    """l = 3 (TFN max_ell=3): unit norm 2l+1, the polar-axis value, equivariance under D^3, and
+    e3nn's generation rule Y3 proportional to the l=2 (x) l=1 -> 3 CG coupling of (Y2, Y1)."""
+    v = torch.randn(200, 3, dtype=torch.float64)
+    Y = o3.spherical_harmonics(v, 3)
+    assert Y.shape == (200, 16)
+    torch.testing.assert_close(Y[:, :9], o3.spherical_harmonics_l2(v))
+    torch.testing.assert_close(Y[:, 9:].pow(2).sum(-1), torch.full((200,), 7.0, dtype=torch.float64))
+    yhat = o3.spherical_harmonics(torch.tensor([[0.0, 2.0, 0.0]], dtype=torch.float64), 3)[0, 9:]
+    torch.testing.assert_close(yhat, math.sqrt(7) * torch.tensor([0, 0, 0, 1.0, 0, 0, 0],
+                                                                  dtype=torch.float64))
+    D3, R = _D(3, *ANG), _D(1, *ANG)
+    torch.testing.assert_close(o3.spherical_harmonics(v @ R.T, 3)[:, 9:], Y[:, 9:] @ D3.T,
+                               atol=1e-12, rtol=0)
+    C = o3.wigner_3j(2, 1, 3)
+    rec = torch.einsum("ei,ej,ijk->ek", Y[:, 4:9], Y[:, 1:4], C)
+    ratio = (rec * Y[:, 9:]).sum() / Y[:, 9:].pow(2).sum()
+    assert ratio > 0
+    torch.testing.assert_close(rec, ratio * Y[:, 9:], atol=1e-12, rtol=0)
+    torch.testing.assert_close(o3.spherical_harmonics(3.7 * v, 3), Y)
+    for lmax in range(3):
+        assert o3.spherical_harmonics(v, lmax).shape == (200, (lmax + 1) ** 2)
+
+
+def test_tfn_max_ell3_invariant():
+    """The oracle TFN at max_ell=3 (27-path first-layer-on TP, 1959 CG floats) stays invariant."""
+    torch.manual_seed(1)
+    m = om.TFNModel(num_layers=2, emb_dim=8, max_ell=3, mlp_dim=16, in_dim=3).double()
+    n = 12
+    pos = torch.randn(n, 3, dtype=torch.float64)
+    ei = torch.stack(torch.meshgrid(torch.arange(n), torch.arange(n), indexing="ij")).reshape(2, -1)
+    ei = ei[:, ei[0] != ei[1]]
+    R = _D(1, *ANG)
+
+    class B:
+        pass
+    b = B()
+    b.atoms, b.edge_index = torch.randint(0, 3, (n,)), ei
+    b.batch = torch.zeros(n, dtype=torch.long)
+    b.pos = pos
+    y0 = m(b)
+    b.pos = pos @ R.T
+    torch.testing.assert_close(m(b), y0, atol=1e-9, rtol=1e-9)
+
+
 def test_cg_known_values():
     for l in range(3):
         C = o3.wigner_3j(0, l, l)[0]
