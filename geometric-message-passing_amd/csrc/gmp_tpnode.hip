@@ -10,6 +10,9 @@
 // as the k dimension; every receiver's sums are formed inside one workgroup in edge order
 // (deterministic).  f32 MFMA 16x16x4: lane l supplies A[i = l&15][k = l>>4] and B[k = l>>4][j =
 // l&15]; D[row = 4(l>>4) + q][col = l&15].
+#include <cstring>
+#include <type_traits>
+
 #include "gmp_common.h"
 
 namespace gmp {
@@ -552,15 +555,249 @@ __global__ __launch_bounds__(kV2T, 1) void tp_node_apply_x3_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------- apply v3
+// The same contraction and arithmetic as v2, re-partitioned so that T never passes through a
+// workgroup-shared LDS image: 256 threads (4 waves) per receiver edge group (<= 32 edges), wave
+// q owns the j quarter [64q, 64q + 64) of H = 256.  Per 32-row block of T_n:
+//   * each wave loads ITS 32 x 64 quarter of the block straight from HBM into registers in the
+//     A-operand fragment order of the dZ product (lane: row 16 rt + (l & 15), 8 consecutive j),
+//     one block ahead of use, and splits it into the three bf16 planes in registers;
+//   * dZ partial D[r][e] = sum_{j in quarter} T[r][j] A[e][j] on those registers (A_n's planes
+//     for the quarter stay in registers for the whole receiver); the four quarter partials are
+//     summed in fixed order through a double-buffered LDS slab (one barrier per block) and the
+//     wave owning tile (rt, et) adds Tb and stores dZ;
+//   * dA D[e][j] += sum_r Z[e][r] T[r][j] for the quarter's 4 j tiles: the planes go to a
+//     wave-private LDS slab and come back transposed (ds_read_b64_tr_b16), no barrier.
+// v2 staged the whole block for all 8 waves behind two barriers and re-read A_n from LDS for
+// every block (~300 KB of LDS reads per 32-row block); here ~24 KB per wave, the T stream
+// overlaps the MFMAs of the previous block, and 80 KB of LDS lets two workgroups share a CU.
+// Edge groups with <= 16 edges run half the MFMAs.  Requires H == 256, w % 32 == 0, 16-byte
+// aligned Z, A, T, Tb, dZ.
+constexpr int kV3T = 256;
+constexpr int kV3H = 256;
+constexpr int kV3Q = kV3H / 4;                 // j per wave
+constexpr int kV3Plane = 32 * 128;             // one plane of a wave's slab: 32 rows x 64 bf16
+constexpr int kV3Slab = 3 * kV3Plane;          // a wave's transposition slab
+constexpr int kV3Red = 4 * 4 * 64 * 16;        // [wave][tile][lane] f32x4 partials
+constexpr int kV3Smem = 4 * kV3Slab + 2 * kV3Red;
+#ifndef GMP_V3_ZD
+#define GMP_V3_ZD 1
+#endif
+
+// byte offset of (row, bf16 column jc) in a slab plane: 16-byte chunk jc / 8 XOR f(row) with
+// f = (row & 7) ^ ((row & 8) >> 1) -- rows 0..7 of a ds_write_b128 lane group hit 8 distinct
+// chunks of a 128-byte bank row, and the 8 rows of a ds_read_b64_tr_b16 half-wave (8g + 0..3,
+// 8g + 8 .. 11) cover all 64 banks once
+__device__ __forceinline__ int v3off(int row, int jc) {
+  const int f = (row & 7) ^ ((row & 8) >> 1);
+  return row * 128 + 16 * ((jc >> 3) ^ f) + 2 * (jc & 7);
+}
+
+// 8 consecutive f32 (two float4) -> the three bf16x8 planes of one MFMA fragment
+__device__ __forceinline__ void split8(f32x4 x0, f32x4 x1, bf16x8_t (&p)[3]) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  unsigned h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+  split3v(f32x2_t{x0[0], x0[1]}, h0, m0, l0);
+  split3v(f32x2_t{x0[2], x0[3]}, h1, m1, l1);
+  split3v(f32x2_t{x1[0], x1[1]}, h2, m2, l2);
+  split3v(f32x2_t{x1[2], x1[3]}, h3, m3, l3);
+  p[0] = __builtin_bit_cast(bf16x8_t, u32x4_t{h0, h1, h2, h3});
+  p[1] = __builtin_bit_cast(bf16x8_t, u32x4_t{m0, m1, m2, m3});
+  p[2] = __builtin_bit_cast(bf16x8_t, u32x4_t{l0, l1, l2, l3});
+}
+
+template <int V>
+using ic_t = std::integral_constant<int, V>;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ f32x4 ld4(rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// T (the large stream) and Z run two blocks ahead in a register ring whose slot is a
+// compile-time index (the block loop is unrolled by two); A_n's quarter is held as raw f32 and
+// split per use (VALU is idle beside the MFMAs; the registers go to the ring)
+template <int ZD>  // Z / Tb ring depth (T: 2)
+__global__ __launch_bounds__(kV3T, 2) void tp_node_apply_v3_kernel(
+    int w, const int64_t* __restrict__ eoff, const float* __restrict__ Z,
+    const float* __restrict__ A, const float* __restrict__ T, const float* __restrict__ Tb,
+    float* __restrict__ dZ, float* __restrict__ dA) {
+  constexpr int H = kV3H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm3[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  unsigned char* slab = sm3 + wv * kV3Slab;
+  unsigned char* red = sm3 + 4 * kV3Slab;
+  const int n = blockIdx.x;
+  const int64_t e0 = eoff[n], deg = eoff[n + 1] - e0;
+  const rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (int64_t)n * w * H,
+                                                      0, w * H * 4, 0x00020000);
+  const rsrc_t tbr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Tb) + (int64_t)n * w, 0,
+                                                       w * 4, 0x00020000);
+  const int jq = wv * kV3Q;
+  const int nblk = w >> 5;
+  const int my_rt = wv & 1, my_et = wv >> 1;  // the dZ tile this wave reduces and stores
+  const f32x4 zero4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  int parity = 0;
+  for (int64_t g0 = 0; g0 < deg; g0 += 32) {
+    const int ng = (int)((deg - g0) < 32 ? (deg - g0) : 32);
+    const bool two = ng > 16;  // uniform
+    const int64_t eb = e0 + g0;
+    // buffer descriptors over this group's rows (edges past ng read as zeros: the range check)
+    // and 32-bit lane offsets: one address VGPR per stream instead of a 64-bit pointer per load
+    const rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Z) + eb * w, 0,
+                                                        ng * w * 4, 0x00020000);
+    const rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A) + eb * H, 0,
+                                                        ng * H * 4, 0x00020000);
+    // A_n's quarter (dZ's B operand: k = j, n = edge), split once per group
+    bf16x8_t pa[2][2][3];
+#pragma unroll
+    for (int et = 0; et < 2; ++et) {
+      const unsigned off = ((16 * et + li) * H + jq + 8 * g) * 4;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        split8(ld4(ar, off + 128 * ks, 0), ld4(ar, off + 128 * ks + 16, 0), pa[et][ks]);
+    }
+    f32x4 rT[2][2][2][2], rZ[ZD][2][2], rTb[ZD];
+    const unsigned t_off = (li * H + jq + 8 * g) * 4;
+    const unsigned z_off = (li * w + 8 * g) * 4;
+    auto fetch_t = [&](auto slot, int b, int rt) {
+      const int so = (32 * b + 16 * rt) * H * 4;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        rT[slot][rt][ks][0] = ld4(tr, t_off + 128 * ks, so);
+        rT[slot][rt][ks][1] = ld4(tr, t_off + 128 * ks + 16, so);
+      }
+    };
+    auto fetch_z = [&](auto slot, int b) {
+#pragma unroll
+      for (int et = 0; et < 2; ++et) {
+        const int so = (16 * et * w + 32 * b) * 4;
+        rZ[slot][et][0] = ld4(zr, z_off, so);
+        rZ[slot][et][1] = ld4(zr, z_off + 16, so);
+      }
+      rTb[slot] = ld4(tbr, (16 * my_rt + 4 * g) * 4, 32 * b * 4);
+    };
+    f32x4 accA[2][4];
+#pragma unroll
+    for (int et = 0; et < 2; ++et)
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) accA[et][jt] = zero4;
+    auto body = [&](auto slot, int b) {
+      const bool more = b + 2 < nblk;
+      constexpr int zs = ZD == 2 ? decltype(slot)::value : 0;
+      bf16x8_t pz[2][3];
+#pragma unroll
+      for (int et = 0; et < 2; ++et) split8(rZ[zs][et][0], rZ[zs][et][1], pz[et]);
+      const f32x4 tb = rTb[zs];
+      if (b + ZD < nblk) fetch_z(ic_t<zs>{}, b + ZD);
+      unsigned char* rb = red + parity * kV3Red;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        bf16x8_t pt[2][3];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) split8(rT[slot][rt][ks][0], rT[slot][rt][ks][1], pt[ks]);
+        if (more) fetch_t(slot, b + 2, rt);
+        // planes into the wave's slab ([plane][row][64 j]); read back transposed below (one
+        // wave's LDS operations complete in order: no barrier, no wait)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            *reinterpret_cast<bf16x8_t*>(slab + p * kV3Plane +
+                                         v3off(16 * rt + li, 32 * ks + 8 * g)) = pt[ks][p];
+        // dZ quarter partials -> reduction buffer [wave][tile = rt + 2 et][lane]
+#pragma unroll
+        for (int et = 0; et < 2; ++et) {
+          f32x4 acc = zero4;
+          if (et == 0 || two) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) acc = mma6(pt[ks], pa[et][ks], acc);
+          }
+          *reinterpret_cast<f32x4*>(rb + ((wv * 4 + rt + 2 * et) * 64 + lane) * 16) = acc;
+        }
+      }
+      __asm__ volatile("" ::: "memory");
+      // dA for the quarter's 4 j tiles (B operand: rows 8g .. 8g + 7 of column 16 jt + li)
+      {
+        const int q = li >> 2, pp = li & 3;
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) {
+          bf16x8_t bt[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            unsigned char* base = slab + p * kV3Plane;
+            const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) i16x4_t*)(base +
+                                                             v3off(8 * g + q, 16 * jt + 4 * pp)));
+            const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) i16x4_t*)(base +
+                                                             v3off(8 * g + 4 + q, 16 * jt + 4 * pp)));
+            bt[p] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5,
+                                                                           6, 7));
+          }
+          accA[0][jt] = mma6(pz[0], bt, accA[0][jt]);
+          if (two) accA[1][jt] = mma6(pz[1], bt, accA[1][jt]);
+          __asm__ volatile("" ::: "memory");  // one j tile's transposed reads live at a time
+        }
+      }
+      __syncthreads();  // all quarter partials of this block are in rb
+      {
+        const int t = my_rt + 2 * my_et;
+        f32x4 s = *reinterpret_cast<const f32x4*>(rb + ((0 * 4 + t) * 64 + lane) * 16);
+        s += *reinterpret_cast<const f32x4*>(rb + ((1 * 4 + t) * 64 + lane) * 16);
+        s += *reinterpret_cast<const f32x4*>(rb + ((2 * 4 + t) * 64 + lane) * 16);
+        s += *reinterpret_cast<const f32x4*>(rb + ((3 * 4 + t) * 64 + lane) * 16);
+        const int e = 16 * my_et + li;
+        if (e < ng)
+          *reinterpret_cast<f32x4*>(dZ + (eb + e) * w + 32 * b + 16 * my_rt + 4 * g) = s + tb;
+      }
+      parity ^= 1;
+    };
+    fetch_t(ic_t<0>{}, 0, 0);
+    fetch_t(ic_t<0>{}, 0, 1);
+    fetch_z(ic_t<0>{}, 0);
+    if (nblk > 1) {
+      fetch_t(ic_t<1>{}, 1, 0);
+      fetch_t(ic_t<1>{}, 1, 1);
+      if constexpr (ZD == 2) fetch_z(ic_t<ZD - 1>{}, 1);
+    }
+    for (int b = 0; b < nblk; b += 2) {
+      body(ic_t<0>{}, b);
+      if (b + 1 < nblk) body(ic_t<1>{}, b + 1);
+    }
+    // dA[e][j] += (per-path launches on one stream: ordered RMW, deterministic)
+#pragma unroll
+    for (int et = 0; et < 2; ++et) {
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = 16 * et + 4 * g + q;
+          if (e < ng) dA[(eb + e) * H + jq + 16 * jt + li] += accA[et][jt][q];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace gmp
 
 using namespace gmp;
 
 namespace gmp {
-// 1: bf16x3 apply kernel where the shape allows (default); 0: the f32-MFMA kernel
-// (GMP_TP_APPLY_F32=1 or gmp_tp_apply_set_x3(0), A/B studies)
-int g_apply_x3 = getenv("GMP_TP_APPLY_F32") && atoi(getenv("GMP_TP_APPLY_F32")) ? 0 : 1;
+// apply kernel: 2 = v3 (per-wave j quarters, T straight to registers; default where the shape
+// allows), 1 = v2 (bf16x3, shared LDS image), 0 = the f32-MFMA kernel.  GMP_TP_APPLY=f32|x3|v3,
+// gmp_tp_apply_set_x3(mode) for A/B studies (GMP_TP_APPLY_F32=1: the f32 kernel, as before)
+int g_apply_x3 = getenv("GMP_TP_APPLY_F32") && atoi(getenv("GMP_TP_APPLY_F32"))
+                     ? 0
+                     : (getenv("GMP_TP_APPLY") ? (strcmp(getenv("GMP_TP_APPLY"), "f32") == 0
+                                                      ? 0
+                                                      : strcmp(getenv("GMP_TP_APPLY"), "x3") == 0
+                                                            ? 1
+                                                            : 2)
+                                               : 2);
 // S kernel stores through LDS (GMP_TP_OUTER_STAGE=0: direct MFMA-layout stores)
 int g_outer_stage = getenv("GMP_TP_OUTER_STAGE") ? atoi(getenv("GMP_TP_OUTER_STAGE")) : 1;
 int g_outer_cs = getenv("GMP_TP_OUTER_CS") ? atoi(getenv("GMP_TP_OUTER_CS")) : 2;
@@ -570,7 +807,7 @@ extern "C" {
 
 int gmp_tp_apply_set_x3(int on) {
   const int old = g_apply_x3;
-  g_apply_x3 = on ? 1 : 0;
+  g_apply_x3 = on < 0 ? 0 : (on > 2 ? 2 : on);
   return old;
 }
 
@@ -606,6 +843,15 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(T) % 16 == 0);
   const bool a16 = ((reinterpret_cast<uintptr_t>(Z) | reinterpret_cast<uintptr_t>(A) |
                      reinterpret_cast<uintptr_t>(Tb) | reinterpret_cast<uintptr_t>(dZ)) % 16) == 0;
+  if (g_apply_x3 == 2 && H == kV3H && w % 32 == 0 && a16) {
+    auto k = tp_node_apply_v3_kernel<GMP_V3_ZD>;
+    int rc = 0;
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, kV3Smem))))
+      return rc;
+    k<<<(unsigned)n_recv, kV3T, kV3Smem, as_stream(stream)>>>((int)w, eoff, Z, A, T, Tb, dZ, dA);
+    return launch_status();
+  }
   // x3 form only for wide paths: measured (scripts/mb_apply_shapes.py, 50k receivers x 20
   // edges, H = 256) 13.3 vs 13.7 ms at w = 640, but slower at w <= 384 (9.1 vs 8.9 ms at 384,
   // 3.8 vs 3.2 at 64)

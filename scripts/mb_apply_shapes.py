@@ -1,4 +1,4 @@
-"""Microbenchmark of the K7 apply kernel, f32-MFMA vs x3 form, over the path widths of C4 MACE
+"""Microbenchmark of the K7 apply kernel, f32-MFMA vs x3 (v2) vs v3 forms, over the path widths of C4 MACE
 (w = 128, 384, 640) and C5 TFN (w = 64, 192, 320) at H = 256, 50k receivers x 20 edges."""
 import os
 import sys
@@ -21,7 +21,7 @@ for w in (64, 128, 192, 320, 384, 640):
     dZ = torch.empty(E + 1, w, device="cuda")
     dA = torch.zeros(E, H, device="cuda")
     res = []
-    for x3 in (0, 1):
+    for x3 in (0, 1, 2):
         lib.gmp_tp_apply_set_x3(x3)
         f = lambda: lib.gmp_tp_node_apply_f32(N, w, H, _p(eoff), _p(Z), _p(A), _p(T), _p(Tb),
                                               _p(dZ), _p(dA), _stream())
@@ -34,5 +34,7 @@ for w in (64, 128, 192, 320, 384, 640):
         e1.record()
         torch.cuda.synchronize()
         res.append(e0.elapsed_time(e1) / 5)
-    print(f"w={w:4d} f32 {res[0]:7.3f} ms  x3 {res[1]:7.3f} ms", flush=True)
+    tb = N * w * H * 4 / 1e9
+    print(f"w={w:4d} f32 {res[0]:7.3f} ms  x3 {res[1]:7.3f} ms  v3 {res[2]:7.3f} ms "
+          f"(T {tb:.1f} GB: {tb / res[2]:.2f} TB/s)", flush=True)
     del Z, T, Tb, dZ, dA

@@ -256,17 +256,20 @@ def _widen_case(lib, M, N, K):
     assert err < 1e-6, err
 
 
-@pytest.mark.parametrize("w,H", [(640, 256), (544, 64), (96, 64), (128, 192), (128, 160)])
-@pytest.mark.parametrize("x3", [1, 0])
+@pytest.mark.parametrize("w,H", [(640, 256), (544, 64), (96, 64), (128, 192), (128, 160),
+                                 (192, 256), (32, 256), (96, 256)])
+@pytest.mark.parametrize("x3", [2, 1, 0])
 def test_node_apply_bf16x3_matches_fp64(w, H, x3):
-    """The apply kernel on the bf16 MFMA over three-plane splits (x3 = 1; shapes with w >= 512,
-    w % 32 == 0 and H % 64 == 0; the others take the f32 kernel either way) and the f32-MFMA kernel (x3 = 0) against fp64, with edge groups of 0, 1,
-    31, 32, 33 and 70 edges (several 32-edge groups): dZ overwritten (+ Tb), dA accumulated onto
-    existing values; error <= 1e-6 of the sum of |terms| per entry."""
+    """The apply kernels against fp64: x3 = 2 the v3 kernel (per-wave j quarters; H = 256,
+    w % 32 == 0), x3 = 1 the v2 bf16x3 kernel (w >= 512, w % 32 == 0, H % 64 == 0), x3 = 0 the
+    f32-MFMA kernel; shapes outside a form's range take the next one.  Edge groups of 0, 1, 16,
+    17, 31, 32, 33 and 70 edges (one or two 16-edge tiles, several 32-edge groups): dZ
+    overwritten (+ Tb), dA accumulated onto existing values; error <= 1e-6 of the sum of |terms|
+    per entry."""
     from gmp_amd import _lib
     from gmp_amd.ops import _p, _stream
     lib = _lib.load()
-    degs = [0, 1, 31, 32, 33, 70, 20, 5]
+    degs = [0, 1, 31, 32, 33, 70, 20, 5, 16, 17]
     eoff, Z, A, ne = _setup(degs, w, H, seed=w + H)
     c = len(degs)
     g = torch.Generator().manual_seed(9)
