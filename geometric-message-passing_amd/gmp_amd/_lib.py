@@ -71,6 +71,8 @@ SIGNATURES = {
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
     "gmp_egnn_set_f32_mfma": (c_int, [c_int]),
     "gmp_wgrad_set_grid_cap": (c_int, [c_int]),
+    "gmp_stream_create_cu_share": (c_int, [c_int, ctypes.POINTER(c_vp)]),
+    "gmp_stream_destroy": (c_int, [c_vp]),
     "gmp_wgrad_set_f32_mfma": (c_int, [c_int]),
     "gmp_edge_outer_sum_workspace_size": (c_size, [c_i64, c_i64]),
     "gmp_edge_outer_sum_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),

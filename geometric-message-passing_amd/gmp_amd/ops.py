@@ -237,10 +237,23 @@ _CB_QUEUED = [False]
 _KEEPALIVE = []
 
 
+# CUs the side stream may dispatch onto (gmp_stream_create_cu_share; 0 = an ordinary stream over
+# the whole chip): a hardware partition that keeps the split-K weight-gradient sums off the rest
+# of the CUs, where the critical path's node-level kernels run.
+SIDE_CUS = int(os.environ.get("GMP_SIDE_CUS", "0") or 0)
+
+
 def _side_stream(device):
     st = _SIDE_STREAMS.get(device)
     if st is None:
-        st = torch.cuda.Stream(device=device)
+        if SIDE_CUS > 0:
+            ptr = ctypes.c_void_p()
+            with torch.cuda.device(device):
+                _lib.check(_lib.load().gmp_stream_create_cu_share(SIDE_CUS, ctypes.byref(ptr)),
+                           "gmp_stream_create_cu_share")
+            st = torch.cuda.ExternalStream(ptr.value, device=device)
+        else:
+            st = torch.cuda.Stream(device=device)
         _SIDE_STREAMS[device] = st
     return st
 

@@ -183,6 +183,13 @@ int gmp_wgrad_set_f32_mfma(int on);
 /* Cap the split-K workgroup count of the outer sums (0 = none, the default: 1-2 per CU); returns
  * the previous cap.  Host-side setting read at launch (and by the workspace-size queries). */
 int gmp_wgrad_set_grid_cap(int blocks);
+/* CU-partitioned stream (no reference counterpart: the reference runs every op on one stream).
+ * Creates a non-blocking stream of the current device whose kernels dispatch only onto `cus`
+ * CUs spread evenly over the CU index space (hipExtStreamCreateWithCUMask; cus >= the CU count:
+ * an unmasked stream); the side-stream weight gradients run there so the critical path's
+ * kernels keep the other CUs.  *stream receives the hipStream_t; gmp_stream_destroy frees it. */
+int gmp_stream_create_cu_share(int cus, void** stream);
+int gmp_stream_destroy(void* stream);
 size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d);
 int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
                            float* colsum_A, void* workspace, size_t workspace_bytes,
