@@ -516,6 +516,10 @@ def main():
         local = 0
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
+    if os.environ.get("GMP_MAIN_STREAM", "0") == "1":
+        # the step on a non-default stream: a CU-masked side stream (GMP_SIDE_CUS) is a blocking
+        # stream and would serialise with the legacy default stream
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if args.blas != "default":
         torch.backends.cuda.preferred_blas_library(args.blas)
     from gmp_amd.graph import radius_graph

@@ -60,29 +60,11 @@ timeit("fwd_gemm", lambda: lib.gmp_tp_gemm_x3_f32(N * d3, mo, K1, _p(S), K1, m1,
                                                   _p(Bf), K1 + m1, mo * (K1 + m1), _p(out[:, 512:]),
                                                   d3, 1152, 1, d3, 1, _stream()),
        2 * N * d3 * (K1 + m1) * mo, 4 * N * w * H)
-amax = torch.full((1,), 0x47000000, dtype=torch.int32, device=dev)  # 32768.0
-wmax = torch.full((1,), 0x3f800000, dtype=torch.int32, device=dev)  # 1.0
-Bf2 = torch.empty(2 * mo * (K1 + m1), dtype=torch.int16, device=dev)
-Bt2 = torch.empty(2 * K1 * mo, dtype=torch.int16, device=dev)
-lib.gmp_tp_split_w2_h2_f32(m1, mo, H, _p(W2), _p(b2), _p(wmax), _p(Bf2), _p(Bt2), _stream())
-rmax = torch.empty(N * w // 16, device=dev)
-timeit("outer_rmax", lambda: lib.gmp_tp_node_outer_rmax_f32(N, w, H, _p(eoff), _p(Z), _p(A), _p(S),
-                                                            _p(Sb), _p(rmax), _stream()),
-       2 * E * w * H, 4 * (N * w * H + E * (w + H)))
-timeit("fwd_gemm_h2", lambda: lib.gmp_tp_gemm_h2_f32(N * d3, mo, K1, _p(S), K1, m1, _p(Sb), m1,
-                                                     _p(Bf2), K1 + m1, mo * (K1 + m1), _p(rmax),
-                                                     m1 // 16, _p(wmax), _p(out[:, 512:]), d3,
-                                                     1152, 1, d3, 1, _stream()),
-       2 * N * d3 * (K1 + m1) * mo, 4 * N * w * H)
 G = torch.randn(N * d3, mo, device=dev)
 del S
 T = torch.empty(N * d3, K1, device=dev)
 timeit("T_gemm", lambda: lib.gmp_tp_gemm_x3_widen_f32(N * d3, K1, mo, _p(G), mo, _p(Bt), mo,
                                                       K1 * mo, _p(T), K1, _stream()),
-       2 * N * d3 * K1 * mo, 4 * N * w * H)
-timeit("T_gemm_h2", lambda: lib.gmp_tp_gemm_h2_widen_f32(N * d3, K1, mo, _p(G), mo, _p(Bt2), mo,
-                                                         K1 * mo, _p(amax), _p(wmax), _p(T), K1,
-                                                         _stream()),
        2 * N * d3 * K1 * mo, 4 * N * w * H)
 dZ = torch.empty(E + 1, w, device=dev)
 dA = torch.zeros(E, H, device=dev)
