@@ -754,7 +754,7 @@ def _node_outer(eoff, Zp, a, w):
 # S of the next path is built on a side stream while the current path's GEMMs run
 # (GMP_TP_S_PREFETCH=0: one stream): the S kernel is bound by its HBM writes, the K7g GEMMs by
 # the MFMA pipe, so the two overlap instead of alternating on one stream.
-TP_S_PREFETCH = os.environ.get("GMP_TP_S_PREFETCH", "1") == "1"
+TP_S_PREFETCH = os.environ.get("GMP_TP_S_PREFETCH", "0") == "1"
 _S_STREAMS = {}
 
 
