@@ -379,7 +379,9 @@ class TPPlan:
         if any(m != 1 for m, _ in irreps_sh) or sh_dim not in (1, 4, 9, 16) or \
                 any(m > 128 for m, _ in irreps_in) or len(irreps_out) > 6 or \
                 any(ir[0] > 3 for _, ir in tuple(irreps_in) + tuple(irreps_out)) or \
-                len(self.instructions) > 32:
+                len(self.instructions) > 32 or \
+                len({ir[0] for _, ir in irreps_in}) != len(tuple(irreps_in)):
+            # (the per-edge z / dz kernels hold one input block per l1)
             raise NotImplementedError(f"TP {o3.irreps_str(irreps_in)} x {o3.irreps_str(irreps_sh)}"
                                       f" -> {o3.irreps_str(irreps_out)} not supported by K7")
         # the per-edge-weight kernels (GMP_TP_MODE=edge) take the two l <= 2 layouts; the node
