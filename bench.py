@@ -517,8 +517,9 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
     if os.environ.get("GMP_MAIN_STREAM", "0") == "1":
-        # the step on a non-default stream: a CU-masked side stream (GMP_SIDE_CUS) is a blocking
-        # stream and would serialise with the legacy default stream
+        # the step on its own (non-default) stream, so that the weight-gradient side stream may be
+        # CU-masked (gmp_amd.ops.SIDE_CUS: a masked stream is a blocking stream and would
+        # serialise with the legacy default stream; ops uses it only off the default stream)
         torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if args.blas != "default":
         torch.backends.cuda.preferred_blas_library(args.blas)

@@ -4,6 +4,7 @@ Every op launches on the current PyTorch HIP stream, allocates its outputs throu
 caching allocator and never synchronises.  Inputs must be CUDA (HIP) tensors: there is no CPU
 fallback in the product path.
 """
+import atexit
 import ctypes
 
 import os
@@ -239,22 +240,39 @@ _KEEPALIVE = []
 
 # CUs the side stream may dispatch onto (gmp_stream_create_cu_share; 0 = an ordinary stream over
 # the whole chip): a hardware partition that keeps the split-K weight-gradient sums off the rest
-# of the CUs, where the critical path's node-level kernels run.
+# of the CUs, where the critical path's node-level kernels run.  A CU-masked stream is a
+# blocking stream (it synchronises with the legacy default stream), so it is used only when the
+# caller's stream is not the default stream (bench.py GMP_MAIN_STREAM=1 runs the step on its own
+# stream).  Off by default: EGNN C2 measured 98.05 / 97.52 vs 98.15 / 97.45 M edges/s unmasked
+# (64 CUs; 32-192 within the same noise) -- the step is bound by total kernel work, not by
+# the side stream crowding the critical path's kernels.
 SIDE_CUS = int(os.environ.get("GMP_SIDE_CUS", "0") or 0)
 
 
-def _side_stream(device):
-    st = _SIDE_STREAMS.get(device)
+def _destroy_stream(ptr):
+    # before interpreter teardown: the runtime's own finalisers must not meet a live masked
+    # stream (a rocprofv3-traced run crashed in __cxa_finalize without this)
+    try:
+        torch.cuda.synchronize()
+        _lib.load().gmp_stream_destroy(ctypes.c_void_p(ptr))
+    except Exception:  # pragma: no cover - best effort at exit
+        pass
+
+
+def _side_stream(device, masked=False):
+    key = (device, masked and SIDE_CUS > 0)
+    st = _SIDE_STREAMS.get(key)
     if st is None:
-        if SIDE_CUS > 0:
+        if key[1]:
             ptr = ctypes.c_void_p()
             with torch.cuda.device(device):
                 _lib.check(_lib.load().gmp_stream_create_cu_share(SIDE_CUS, ctypes.byref(ptr)),
                            "gmp_stream_create_cu_share")
             st = torch.cuda.ExternalStream(ptr.value, device=device)
+            atexit.register(_destroy_stream, ptr.value)
         else:
             st = torch.cuda.Stream(device=device)
-        _SIDE_STREAMS[device] = st
+        _SIDE_STREAMS[key] = st
     return st
 
 
@@ -322,7 +340,7 @@ class side_work:
         if self.inline:
             return self
         self.main = torch.cuda.current_stream()
-        self.side = _side_stream(self.main.device)
+        self.side = _side_stream(self.main.device, masked=self.main.cuda_stream != 0)
         self.side.wait_stream(self.main)
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
