@@ -197,76 +197,13 @@ __global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restr
   else if (colsum) colsum[x - DD] = s;
 }
 
-// Two-level form of the same ordered sum with single-wave workgroups (GMP_SUM_WAVES=1): a
-// 1024-thread workgroup needs 16 free wave slots on one CU at once, which the concurrent
-// main-stream kernels rarely leave (the r03 trace shows ~70-86 us per call for ~10 MB of
-// slabs); one-wave workgroups start on any CU with a free slot.  Level 1: workgroup (x, y)
-// adds slabs 16y .. 16y + 15 of 256 columns (float4 per lane, one burst) into scratch row y;
-// level 2 adds the scratch rows in row order.  Fixed order: deterministic.  Requires X % 4 == 0
-// and 16-byte aligned slabs (X = m n + m with m, n multiples of 16).
-__global__ __launch_bounds__(64) void sum_slab_groups(const float* __restrict__ part,
-                                                      int64_t G, int64_t X,
-                                                      float* __restrict__ rows_out) {
-  const int64_t x4 = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (4 * x4 >= X) return;
-  const int64_t g0 = (int64_t)blockIdx.y * kGC, g1 = g0 + kGC < G ? g0 + kGC : G;
-  f32x4 v[kGC];
-#pragma unroll
-  for (int u = 0; u < kGC; ++u)
-    v[u] = (g0 + u < g1) ? *reinterpret_cast<const f32x4*>(part + (g0 + u) * X + 4 * x4)
-                         : f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 s = v[0];
-#pragma unroll
-  for (int u = 1; u < kGC; ++u)
-    if (g0 + u < g1) s += v[u];
-  *reinterpret_cast<f32x4*>(rows_out + blockIdx.y * X + 4 * x4) = s;
-}
-
-__global__ __launch_bounds__(64) void sum_rows_out(const float* __restrict__ rows, int64_t R,
-                                                   int64_t X, float* __restrict__ out,
-                                                   float* __restrict__ colsum, int64_t DD,
-                                                   int64_t n, int64_t ldc) {
-  const int64_t x4 = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (4 * x4 >= X) return;
-  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t r0 = 0; r0 < R; r0 += kGC) {
-    f32x4 v[kGC];
-#pragma unroll
-    for (int u = 0; u < kGC; ++u)
-      v[u] = (r0 + u < R) ? *reinterpret_cast<const f32x4*>(rows + (r0 + u) * X + 4 * x4)
-                          : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < kGC; ++u)
-      if (r0 + u < R) s += v[u];
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int64_t x = 4 * x4 + c;
-    if (x < DD) out[(x / n) * ldc + x % n] = s[c];
-    else if (colsum) colsum[x - DD] = s[c];
-  }
-}
-
 int g_sum_waves = getenv("GMP_SUM_WAVES") ? atoi(getenv("GMP_SUM_WAVES")) : 16;
 
 // out (row stride ldc, n columns) = the ordered sum of G slabs of X = DD (+ colsum) floats.
-// The two-level form uses the ceil(G / 16) slabs after the G partial slabs as scratch (every
-// outer-sum workspace size includes them).
+// (r03: a two-level form with single-wave workgroups measured neutral on the EGNN step; removed)
 void sum_partials(const float* part, int64_t G, int64_t X, float* out, float* colsum,
                   int64_t DD, int64_t n, int64_t ldc, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(X, 64);
-  if (g_sum_waves == 1 && X % 4 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0) {
-    const unsigned gx = (unsigned)ceil_div(X, 256);
-    if (G <= 2 * kGC) {
-      sum_rows_out<<<gx, 64, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
-      return;
-    }
-    const int64_t SG = ceil_div(G, kGC);
-    float* rows = const_cast<float*>(part) + G * X;
-    sum_slab_groups<<<dim3(gx, (unsigned)SG), 64, 0, s>>>(part, G, X, rows);
-    sum_rows_out<<<gx, 64, 0, s>>>(rows, SG, X, out, colsum, DD, n, ldc);
-    return;
-  }
   if (g_sum_waves == 4)
     sum_partials_one<4><<<grid, 256, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
   else

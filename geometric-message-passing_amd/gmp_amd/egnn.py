@@ -39,10 +39,6 @@ class EGNNLayer(MessagePassing):
         self.mlp_upd = nn.Sequential(nn.Linear(2 * d, d), self.norm(d), self.activation,
                                      nn.Linear(d, d), self.norm(d), self.activation)
 
-    # set by EGNNModel on its first layer: its backward is the last of the pass (ops.EgnnMessageFn
-    # `tail`: weight gradients on the main stream)
-    bwd_tail = False
-
     def forward(self, h, pos, edge_index):
         return self.propagate(edge_index, h=h, pos=pos)
 
@@ -78,7 +74,7 @@ class EGNNLayer(MessagePassing):
         m_aggr, p_aggr = ops.EgnnMessageFn.apply(
             h, pos, graph, self.activation_name, self.aggr == "mean", ln1.eps,
             m0.weight, m0.bias, ln1.weight, ln1.bias, m3.weight, m3.bias, ln2.weight, ln2.bias,
-            p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias, self.bwd_tail)
+            p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias)
         return self._mlp_upd(h, m_aggr), pos + p_aggr
 
     def _mlp_upd(self, h, m_aggr):
@@ -109,7 +105,6 @@ class EGNNModel(nn.Module):
         self.emb_in = nn.Embedding(in_dim, emb_dim)
         self.convs = nn.ModuleList(EGNNLayer(emb_dim, activation, norm, aggr)
                                    for _ in range(num_layers))
-        self.convs[0].bwd_tail = True
         self.pool = {"mean": global_mean_pool, "sum": global_add_pool}[pool]
         if equivariant_pred:
             self.pred = nn.Linear(emb_dim + 3, out_dim)

@@ -613,12 +613,10 @@ class TPConvNodeFn(torch.autograd.Function):
         for n0, n1, e0, e1, eoff, a, zbuf, _ in _node_chunks(plan, graph, x, sh, rad_s, W1, b1,
                                                              paths_dev, cg_dev):
             c, ne = n1 - n0, e1 - e0
-            Zs = [zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                  for zoff, w in plan.z_regions]
-            pipe = _SPipeline(eoff, Zs, a, [w for _, w in plan.z_regions], [True] * len(Zs))
-            for i, P in enumerate(plan.instructions):
+            for i, (P, (zoff, w)) in enumerate(zip(plan.instructions, plan.z_regions)):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
-                S, Sb = pipe.get(i)
+                Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
+                S, Sb = _node_outer(eoff, Zp, a, w)
                 blk = plan.blocks[P["io"]]
                 if x3[i]:
                     # out[n, blk + w' d3 + k] += [S | Sb][(n, k), :] [W2p ; b2p][:, w'] (K7g)
@@ -637,7 +635,6 @@ class TPConvNodeFn(torch.autograd.Function):
                         op.view(c, d3, -1).transpose(1, 2))
                     del op
                 del S, Sb
-                pipe.release()
         ctx.plan, ctx.graph, ctx.tables = plan, graph, (paths_dev, cg_dev)
         ctx.save_for_backward(x, sh, rad_s, W1, b1, W2, b2)
         return out
@@ -668,16 +665,11 @@ class TPConvNodeFn(torch.autograd.Function):
             c, ne = n1 - n0, e1 - e0
             dzbuf = torch.empty_like(zbuf)
             da = torch.zeros((ne, H), **f)
-            Zs = [zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                  for zoff, w in plan.z_regions]
-            pipe = _SPipeline(eoff, Zs, a, [w for _, w in plan.z_regions],
-                              [not (x3[i] and _dw_fused_ok(P, H))
-                               for i, P in enumerate(plan.instructions)])
             for i, (P, (W2p, b2p), (dW2p, db2p), (zoff, w)) in enumerate(
                     zip(plan.instructions, W2x, dW2x, plan.z_regions)):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 blk = plan.blocks[P["io"]]
-                Zp = Zs[i]
+                Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 G = gout[n0:n1, blk[0]:blk[0] + blk[1] * d3].view(c, mo, d3).transpose(1, 2)
                 G = G.reshape(c * d3, mo).contiguous()  # (d3 = 1: reshape alone is a view)
                 if x3[i]:
@@ -689,7 +681,7 @@ class TPConvNodeFn(torch.autograd.Function):
                             part = tops.tp_node_dw(eoff, Zp, a, G, d3, m1)
                             Sb, _ = tops.segment_reduce(Zp, None, eoff, c, "sum")
                         else:
-                            S, Sb = pipe.get(i)
+                            S, Sb = _node_outer(eoff, Zp, a, w)
                             # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
                             part = tops.outer_sum_cols(S.view(c * d3, K1), G)
                             del S
@@ -703,7 +695,6 @@ class TPConvNodeFn(torch.autograd.Function):
                             dW2p.add_(part)
                             db2p.add_(pb)
                     del Sb
-                    pipe.release()
                     if Bts[i] is None:
                         Bts[i] = _split_w2(W2c, b2c, P, False)
                     with _timed("tp_node_W"):
@@ -711,12 +702,11 @@ class TPConvNodeFn(torch.autograd.Function):
                         T = tops.tp_gemm_x3_widen(G, Bts[i], K1)
                         Tb = G.mm(b2p.t())
                 else:
-                    S, Sb = pipe.get(i)
+                    S, Sb = _node_outer(eoff, Zp, a, w)
                     with _timed("tp_node_dW"):
                         dW2p.addmm_(S.view(c * d3, -1).t(), G)
                         db2p.addmm_(Sb.view(c * d3, -1).t(), G)
                     del S, Sb
-                    pipe.release()
                     with _timed("tp_node_W"):
                         T = G.mm(W2p.t())
                         Tb = G.mm(b2p.t())
@@ -751,58 +741,6 @@ class TPConvNodeFn(torch.autograd.Function):
 def _node_outer(eoff, Zp, a, w):
     with _timed("tp_node_S"):
         return _lib.torch_ops().tp_node_outer(eoff, Zp, a, w)
-
-
-# S of the next path is built on a side stream while the current path's GEMMs run
-# (GMP_TP_S_PREFETCH=0: one stream): the S kernel is bound by its HBM writes, the K7g GEMMs by
-# the MFMA pipe, so the two overlap instead of alternating on one stream.
-TP_S_PREFETCH = os.environ.get("GMP_TP_S_PREFETCH", "0") == "1"
-_S_STREAMS = {}
-
-
-class _SPipeline:
-    """S / Sb of the paths of one receiver chunk, path i + 1's built on a side stream while path
-    i's consumers run on the current stream (at most two S buffers live).
-
-    get(i) enqueues the next path's build on the side stream, then makes the current stream wait
-    for S_i's build; release() is called once the last consumer of S_i has been enqueued and the
-    caller has dropped S_i: the side stream is then ordered after those consumers, so the block
-    of S_i (it lives in the side stream's pool) is only rewritten after they ran."""
-
-    def __init__(self, eoff, Zs, a, widths, need):
-        self.eoff, self.Zs, self.a, self.widths = eoff, Zs, a, widths
-        self.order = [i for i, n in enumerate(need) if n]
-        self.on = TP_S_PREFETCH and not ops.compiling() and len(self.order) > 1
-        self.ready = {}
-        if self.on:
-            self.main = torch.cuda.current_stream()
-            dev = self.main.device
-            if dev not in _S_STREAMS:
-                _S_STREAMS[dev] = torch.cuda.Stream(device=dev)
-            self.side = _S_STREAMS[dev]
-            self.side.wait_stream(self.main)  # z rows, a rows, eoff are main-stream products
-            self._build(self.order[0])
-
-    def _build(self, i):
-        with torch.cuda.stream(self.side):
-            S, Sb = _node_outer(self.eoff, self.Zs[i], self.a, self.widths[i])
-            ev = torch.cuda.Event()
-            ev.record(self.side)
-        self.ready[i] = (S, Sb, ev)
-
-    def get(self, i):
-        if not self.on:
-            return _node_outer(self.eoff, self.Zs[i], self.a, self.widths[i])
-        k = self.order.index(i)
-        if k + 1 < len(self.order):
-            self._build(self.order[k + 1])
-        S, Sb, ev = self.ready.pop(i)
-        self.main.wait_event(ev)
-        return S, Sb
-
-    def release(self):
-        if self.on:
-            self.side.wait_stream(self.main)
 
 
 def _node_chunks(plan, graph, x, sh, rad_s, W1, b1, paths_dev, cg_dev):

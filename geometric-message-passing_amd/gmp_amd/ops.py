@@ -328,13 +328,10 @@ class side_work:
     streams).  tail=True: nothing on the critical path follows (no split-K grid cap).  Under
     torch.compile the work runs inline and every gradient goes back through autograd."""
 
-    def __init__(self, *used, tail=False, inline=False):
+    def __init__(self, *used, tail=False):
         self.used = [t for t in used if t is not None]
         self.cap = 0 if tail else SIDE_GRID_CAP
-        # inline: on the current stream, gradients back through autograd (under torch.compile;
-        # or the last layer of a backward pass, where nothing is left for a side stream to
-        # overlap with and the whole chip is free)
-        self.inline = inline or compiling()
+        self.inline = compiling()
 
     def __enter__(self):
         if self.inline:
@@ -832,12 +829,6 @@ def _egnn_params(tensors):
 EGNN_WGRAD_HF = os.environ.get("GMP_EGNN_WGRAD_HF", "1") != "0"
 
 
-# The first layer's weight gradients (the last work of the backward pass) on the main stream over
-# the whole chip instead of the side stream (GMP_EGNN_TAIL_INLINE=1; measured neutral: 98.0 M
-# edges/s either way on one box, so off)
-EGNN_TAIL_INLINE = os.environ.get("GMP_EGNN_TAIL_INLINE", "0") == "1"
-
-
 class EgnnMessageFn(torch.autograd.Function):
     """The whole EGNN message block of one layer (egnn_layer.py:62-80 with the MLPs of :28-36):
     the node projections AB = [h W1a^T | h W1b^T] (one GEMM), the fused edge kernel K4 and the
@@ -853,7 +844,7 @@ class EgnnMessageFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, pos, graph, act, msg_mean, eps, W1, b1, ln1w, ln1b, W2, b2, ln2w, ln2b,
-                W3, b3, ln3w, ln3b, w4, b4, tail=False):
+                W3, b3, ln3w, ln3b, w4, b4):
         h, pos = _f32c(h), _f32c(pos)
         _need_cuda(h, pos, W1)
         N, d = h.shape
@@ -868,7 +859,7 @@ class EgnnMessageFn(torch.autograd.Function):
             m_aggr, pos_aggr, xhat, rstd = _lib.torch_ops().egnn_edge_fwd(
                 AB, pos, graph.rowptr, graph.recv, graph.send, list(params), _lib.ACT[act],
                 bool(msg_mean), float(eps), train)
-        ctx.graph, ctx.act, ctx.msg_mean, ctx.N, ctx.tail = graph, act, msg_mean, N, tail
+        ctx.graph, ctx.act, ctx.msg_mean, ctx.N = graph, act, msg_mean, N
         if train:
             ctx.save_for_backward(h, pos, xhat, rstd, W1, *params)
         return m_aggr, pos_aggr
@@ -905,8 +896,7 @@ class EgnnMessageFn(torch.autograd.Function):
 
         # weight gradients: side stream, accumulated at the end of the backward pass
         (_, b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3, b3, ln3w, ln3b, w4, b4) = params
-        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials, amax,
-                       inline=ctx.tail and EGNN_TAIL_INLINE) as sw:
+        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials, amax) as sw:
             dW1 = torch.empty((d, 2 * d + 1), **f)
             db1 = torch.empty(d, **f)
             outer_sum_into(dA, h, dW1[:, :d], db1)
@@ -923,5 +913,5 @@ class EgnnMessageFn(torch.autograd.Function):
         # the caller's parameter tensors (saved tensors unpack to the same objects): W1 itself,
         # then b1 ... b4 (params[0] is the contiguous copy of W1's distance column)
         targets = (W1,) + tuple(params[1:])
-        return ((dh, dpos, None, None, None, None)
-                + sw.deliver(ctx.needs_input_grad, 6, targets, grads) + (None,))
+        return (dh, dpos, None, None, None, None) + sw.deliver(ctx.needs_input_grad, 6, targets,
+                                                               grads)
