@@ -650,13 +650,18 @@ __device__ __forceinline__ void z_bwd_path(const Path& P, const float* __restric
   }
 }
 
-// (l1, l2, lo) with l <= 3 and |l1 - l2| <= lo <= l1 + l2 (every triangle, any parities)
-#define GMP_Z_PATHS(X)                                                                         \
-  X(0, 0, 0) X(0, 1, 1) X(0, 2, 2) X(0, 3, 3) X(1, 0, 1) X(1, 1, 0) X(1, 1, 1) X(1, 1, 2)      \
-  X(1, 2, 1) X(1, 2, 2) X(1, 2, 3) X(1, 3, 2) X(1, 3, 3) X(2, 0, 2) X(2, 1, 1) X(2, 1, 2)      \
-  X(2, 1, 3) X(2, 2, 0) X(2, 2, 1) X(2, 2, 2) X(2, 2, 3) X(2, 3, 1) X(2, 3, 2) X(2, 3, 3)      \
-  X(3, 0, 3) X(3, 1, 2) X(3, 1, 3) X(3, 2, 1) X(3, 2, 2) X(3, 2, 3) X(3, 3, 0) X(3, 3, 1)      \
-  X(3, 3, 2) X(3, 3, 3)
+// (l1, l2, lo) with l <= 3 and |l1 - l2| <= lo <= l1 + l2 (every triangle, any parities): the
+// l <= 2 paths (GMP_Z_PATHS2) and those with an l = 3 (GMP_Z_PATHS3)
+#define GMP_Z_PATHS3(X)                                                                        \
+  X(0, 3, 3) X(1, 2, 3) X(1, 3, 2) X(1, 3, 3) X(2, 1, 3) X(2, 2, 3) X(2, 3, 1) X(2, 3, 2)      \
+  X(2, 3, 3) X(3, 0, 3) X(3, 1, 2) X(3, 1, 3) X(3, 2, 1) X(3, 2, 2) X(3, 2, 3) X(3, 3, 0)      \
+  X(3, 3, 1) X(3, 3, 2) X(3, 3, 3)
+
+// the l <= 2 subset (LM = 2 kernels: the l = 3 cases compiled out, so their registers are too --
+// MACE-128 / TFN max_ell = 2: 59 instead of 91 VGPRs for z, 5 -> 8 waves per SIMD)
+#define GMP_Z_PATHS2(X)                                                                        \
+  X(0, 0, 0) X(0, 1, 1) X(0, 2, 2) X(1, 0, 1) X(1, 1, 0) X(1, 1, 1) X(1, 1, 2) X(1, 2, 1)      \
+  X(1, 2, 2) X(2, 0, 2) X(2, 1, 1) X(2, 1, 2) X(2, 2, 0) X(2, 2, 1) X(2, 2, 2)
 
 // SH row of the edge: sh_dim = (lmax + 1)^2 in {1, 4, 9, 16} components (zeros past sh_dim)
 __device__ __forceinline__ void load_y(const float* __restrict__ sh, int64_t eo, int sh_dim,
@@ -665,6 +670,8 @@ __device__ __forceinline__ void load_y(const float* __restrict__ sh, int64_t eo,
   for (int j = 0; j < kMaxSh; ++j) Y[j] = j < sh_dim ? sh[eo * sh_dim + j] : 0.f;
 }
 
+// LM: the largest l of any path (host-supplied; an LM = 2 kernel skips l = 3 paths)
+template <int LM>
 __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
     Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
     const float* __restrict__ x, const float* __restrict__ sh,
@@ -689,15 +696,24 @@ __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
       switch (P.l1 * 16 + P.l2 * 4 + P.lo) {
 #define GMP_Z_CASE(A, B, O) \
   case A * 16 + B * 4 + O: z_path<A, B, O>(P, C, Y, xrow, zr, lane); break;
-        GMP_Z_PATHS(GMP_Z_CASE)
+        GMP_Z_PATHS2(GMP_Z_CASE)
 #undef GMP_Z_CASE
+#define GMP_Z_CASE3(A, B, O)                                                 \
+  case A * 16 + B * 4 + O:                                                   \
+    if constexpr (LM == 3) z_path<A, B, O>(P, C, Y, xrow, zr, lane);         \
+    break;
+        GMP_Z_PATHS3(GMP_Z_CASE3)
+#undef GMP_Z_CASE3
         default: break;
       }
     }
   }
 }
 
-__global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
+// OCC: workgroups per CU the register budget is sized for (LM = 2: 187 VGPRs free-running = 2;
+// 3 caps them at 168 with 28 B/lane of scratch)
+template <int LM, int OCC>
+__global__ __launch_bounds__(256, OCC) void tp_edge_z2_bwd_kernel(
     Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
     const float* __restrict__ x, const float* __restrict__ sh,
     const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
@@ -744,8 +760,14 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
       switch (P.l1 * 16 + P.l2 * 4 + P.lo) {
 #define GMP_ZB_CASE(A, B, O) \
   case A * 16 + B * 4 + O: z_bwd_path<A, B, O>(P, C, Y, xrow, dzr, dx, dyp, lane); break;
-        GMP_Z_PATHS(GMP_ZB_CASE)
+        GMP_Z_PATHS2(GMP_ZB_CASE)
 #undef GMP_ZB_CASE
+#define GMP_ZB_CASE3(A, B, O)                                                          \
+  case A * 16 + B * 4 + O:                                                             \
+    if constexpr (LM == 3) z_bwd_path<A, B, O>(P, C, Y, xrow, dzr, dx, dyp, lane);     \
+    break;
+        GMP_Z_PATHS3(GMP_ZB_CASE3)
+#undef GMP_ZB_CASE3
         default: break;
       }
     }
@@ -787,6 +809,9 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
     if (lane < d.sh_dim) dY_edge[k * d.sh_dim + lane] = dyv;
   }
 }
+
+// dz kernel occupancy target at l <= 2 (GMP_TP_ZB_OCC=3: 168-VGPR cap; A/B)
+int g_zb_occ = getenv("GMP_TP_ZB_OCC") ? atoi(getenv("GMP_TP_ZB_OCC")) : 1;
 
 int64_t z2_blocks(int64_t edges) {
   const int64_t cap = (int64_t)device_cu_count() * 8;  // 32 resident waves per CU
@@ -870,16 +895,56 @@ int gmp_tp_conv_bwd_f32(int layout, const void* desc_host, const void* paths_dev
   return launch_status();
 }
 
-int gmp_tp_edge_z_f32(const void* desc_host, const void* paths_dev, const float* cg_dev,
-                      int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
-                      const int64_t* perm, int64_t e0, int64_t e1, float* zbuf, void* stream) {
+int gmp_tp_edge_z_lmax_f32(const void* desc_host, int l_max, const void* paths_dev,
+                           const float* cg_dev, int cg_len, const float* x, const float* sh,
+                           const int64_t* src_sorted, const int64_t* perm, int64_t e0, int64_t e1,
+                           float* zbuf, void* stream) {
   GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && zbuf);
   const Desc d = *reinterpret_cast<const Desc*>(desc_host);
   GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= kMaxCg);
-  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
+  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 3);
   if (e1 == e0) return GMP_OK;
-  tp_edge_z2_kernel<<<(unsigned)z2_blocks(e1 - e0), 256, 0, as_stream(stream)>>>(
-      d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
+  const unsigned grid = (unsigned)z2_blocks(e1 - e0);
+  if (l_max <= 2 && d.sh_dim <= 9)
+    tp_edge_z2_kernel<2><<<grid, 256, 0, as_stream(stream)>>>(
+        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
+  else
+    tp_edge_z2_kernel<3><<<grid, 256, 0, as_stream(stream)>>>(
+        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
+  return launch_status();
+}
+
+int gmp_tp_edge_z_f32(const void* desc_host, const void* paths_dev, const float* cg_dev,
+                      int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
+                      const int64_t* perm, int64_t e0, int64_t e1, float* zbuf, void* stream) {
+  return gmp_tp_edge_z_lmax_f32(desc_host, 3, paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm,
+                                e0, e1, zbuf, stream);
+}
+
+int gmp_tp_edge_z_bwd_lmax_f32(const void* desc_host, int l_max, const void* paths_dev,
+                               const float* cg_dev, int cg_len, const float* x, const float* sh,
+                               const int64_t* src_sorted, const int64_t* perm, int64_t e0,
+                               int64_t e1, const float* dzbuf, float* dx_edge, float* dY_edge,
+                               void* stream) {
+  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && dzbuf &&
+                dx_edge && dY_edge);
+  const Desc d = *reinterpret_cast<const Desc*>(desc_host);
+  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= kMaxCg);
+  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 3);
+  if (e1 == e0) return GMP_OK;
+  const unsigned grid = (unsigned)z2_blocks(e1 - e0);
+  if (l_max <= 2 && d.sh_dim <= 9 && g_zb_occ == 3)
+    tp_edge_z2_bwd_kernel<2, 3><<<grid, 256, 0, as_stream(stream)>>>(
+        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
+        dx_edge, dY_edge);
+  else if (l_max <= 2 && d.sh_dim <= 9)
+    tp_edge_z2_bwd_kernel<2, 1><<<grid, 256, 0, as_stream(stream)>>>(
+        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
+        dx_edge, dY_edge);
+  else
+    tp_edge_z2_bwd_kernel<3, 1><<<grid, 256, 0, as_stream(stream)>>>(
+        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
+        dx_edge, dY_edge);
   return launch_status();
 }
 
@@ -887,16 +952,8 @@ int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const fl
                           int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
                           const int64_t* perm, int64_t e0, int64_t e1, const float* dzbuf,
                           float* dx_edge, float* dY_edge, void* stream) {
-  GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && dzbuf &&
-                dx_edge && dY_edge);
-  const Desc d = *reinterpret_cast<const Desc*>(desc_host);
-  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= kMaxCg);
-  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0);
-  if (e1 == e0) return GMP_OK;
-  tp_edge_z2_bwd_kernel<<<(unsigned)z2_blocks(e1 - e0), 256, 0, as_stream(stream)>>>(
-      d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf, dx_edge,
-      dY_edge);
-  return launch_status();
+  return gmp_tp_edge_z_bwd_lmax_f32(desc_host, 3, paths_dev, cg_dev, cg_len, x, sh, src_sorted,
+                                    perm, e0, e1, dzbuf, dx_edge, dY_edge, stream);
 }
 
 }  // extern "C"

@@ -640,7 +640,8 @@ std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t co
 
 // ------------------------------------------------------------------ K7 per-edge z rows
 // The host descriptor travels as int[] (n_paths, in_dim, out_dim, sh_dim, weight_numel, z_size,
-// n_blocks, blk_off[6], blk_mul[6], blk_l[6]); the 64-byte path records as a device uint8 tensor.
+// n_blocks, blk_off[6], blk_mul[6], blk_l[6] [, l_max]); the 64-byte path records as a device
+// uint8 tensor.  l_max (the largest l of any path; default 3) picks the z kernels' instantiation.
 struct TpDescHost {
   int n_paths, in_dim, out_dim, sh_dim;
   long long weight_numel;
@@ -650,7 +651,7 @@ struct TpDescHost {
 static_assert(sizeof(TpDescHost) == 104, "descriptor layout (include/gmp.h)");
 
 TpDescHost tp_desc(at::IntArrayRef d) {
-  TORCH_CHECK(d.size() == 25, "gmp.tp: descriptor has 25 ints");
+  TORCH_CHECK(d.size() == 25 || d.size() == 26, "gmp.tp: descriptor has 25 (+ l_max) ints");
   TpDescHost h;
   h.n_paths = (int)d[0]; h.in_dim = (int)d[1]; h.out_dim = (int)d[2]; h.sh_dim = (int)d[3];
   h.weight_numel = d[4]; h.z_size = (int)d[5]; h.n_blocks = (int)d[6];
@@ -660,6 +661,12 @@ TpDescHost tp_desc(at::IntArrayRef d) {
     h.blk_l[k] = (int)d[19 + k];
   }
   return h;
+}
+
+int tp_lmax(at::IntArrayRef d) {
+  const int l = d.size() == 26 ? (int)d[25] : 3;
+  TORCH_CHECK(0 <= l && l <= 3, "gmp.tp: l_max in 0..3");
+  return l;
 }
 
 void tp_edge_checks(const TpDescHost& h, const Tensor& paths, const Tensor& cg, const Tensor& x,
@@ -686,9 +693,10 @@ Tensor tp_edge_z(at::IntArrayRef desc, const Tensor& paths, const Tensor& cg, co
   const TpDescHost h = tp_desc(desc);
   tp_edge_checks(h, paths, cg, x, sh, src_sorted, perm, e0, e1);
   Tensor z = at::empty({(e1 - e0 + 1) * h.z_size}, x.options());
-  check_rc(gmp_tp_edge_z_f32(&h, paths.data_ptr(), fp(cg), (int)cg.numel(), fp(x), fp(sh),
-                             ip(src_sorted), ip(perm), e0, e1, fp(z), cur_stream()),
-           "gmp_tp_edge_z_f32");
+  check_rc(gmp_tp_edge_z_lmax_f32(&h, tp_lmax(desc), paths.data_ptr(), fp(cg), (int)cg.numel(),
+                                  fp(x), fp(sh), ip(src_sorted), ip(perm), e0, e1, fp(z),
+                                  cur_stream()),
+           "gmp_tp_edge_z_lmax_f32");
   return z;
 }
 
@@ -703,10 +711,10 @@ std::tuple<Tensor, Tensor> tp_edge_z_bwd(at::IntArrayRef desc, const Tensor& pat
   numel(dz, (e1 - e0 + 1) * h.z_size, "dz");
   Tensor dx = at::empty({e1 - e0, (int64_t)h.in_dim}, x.options());
   Tensor dY = at::empty({e1 - e0, (int64_t)h.sh_dim}, x.options());
-  check_rc(gmp_tp_edge_z_bwd_f32(&h, paths.data_ptr(), fp(cg), (int)cg.numel(), fp(x), fp(sh),
-                                 ip(src_sorted), ip(perm), e0, e1, fp(dz), fp(dx), fp(dY),
-                                 cur_stream()),
-           "gmp_tp_edge_z_bwd_f32");
+  check_rc(gmp_tp_edge_z_bwd_lmax_f32(&h, tp_lmax(desc), paths.data_ptr(), fp(cg),
+                                      (int)cg.numel(), fp(x), fp(sh), ip(src_sorted), ip(perm),
+                                      e0, e1, fp(dz), fp(dx), fp(dY), cur_stream()),
+           "gmp_tp_edge_z_bwd_lmax_f32");
   return {dx, dY};
 }
 

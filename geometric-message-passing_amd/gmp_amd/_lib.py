@@ -123,6 +123,10 @@ SIGNATURES = {
                                   c_vp, c_vp]),
     "gmp_tp_edge_z_bwd_f32": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_i64,
                                       c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_tp_edge_z_lmax_f32": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
+                                       c_i64, c_i64, c_vp, c_vp]),
+    "gmp_tp_edge_z_bwd_lmax_f32": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                           c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "gmp_edge_outer_sum_ex2_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64,
                                            c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
     "gmp_edge_outer_sum_ex_workspace_size": (c_size, [c_i64, c_i64, c_i64]),

@@ -419,9 +419,11 @@ class TPPlan:
         # plain-int copies (the autograd Functions read these, never the ctypes descriptor)
         self.in_dim, self.out_dim = self.desc.in_dim, self.desc.out_dim
         self.z_size = self.desc.z_size
-        d = self.desc  # the descriptor as torch.ops.gmp.tp_* take it (int[25])
+        d = self.desc  # the descriptor as torch.ops.gmp.tp_* take it (int[25] + l_max)
+        self.l_max = max(max(i["l1"], i["l2"], i["lo"]) for i in self.instructions)
         self.desc_list = ([d.n_paths, d.in_dim, d.out_dim, d.sh_dim, d.weight_numel, d.z_size,
-                           d.n_blocks] + list(d.blk_off) + list(d.blk_mul) + list(d.blk_l))
+                           d.n_blocks] + list(d.blk_off) + list(d.blk_mul) + list(d.blk_l)
+                          + [self.l_max])
         # node form: path p's z rows (mul1 * (2lo+1) floats) at z_off_p * (n_e + 1)
         self.z_regions = [(paths[k].z_off, ins["mul1"] * (2 * ins["lo"] + 1))
                           for k, ins in enumerate(self.instructions)]
@@ -794,9 +796,10 @@ class TensorProductConvLayer(nn.Module):
 
     def forward(self, node_attr, edge_index, edge_sh, edge_feat):
         graph = tp_graph(edge_index, node_attr.shape[0])
-        fn = TPConvNodeFn if (TP_MODE == "node" and node_form_ok(self.fc[0].out_features)) \
-            else TPConvFn
-        if fn is TPConvFn and self.plan.layout is None:
+        node = TP_MODE == "node" and node_form_ok(self.fc[0].out_features)
+        fn = TPConvNodeFn if node else TPConvFn
+        # (a plain bool: torch.compile cannot trace `is` between autograd Function classes)
+        if not node and self.plan.layout is None:
             raise NotImplementedError("the per-edge-weight TP kernels take l <= 2 layouts only; "
                                       "use the node form (GMP_TP_MODE=node, mlp_dim % 16 == 0)")
         paths, cg = self._tp_paths, self._tp_cg

@@ -369,6 +369,18 @@ int gmp_tp_edge_z_bwd_f32(const void* desc_host, const void* paths_dev, const fl
                           int cg_len, const float* x, const float* sh, const int64_t* src_sorted,
                           const int64_t* perm, int64_t e0, int64_t e1, const float* dzbuf,
                           float* dx_edge, float* dY_edge, void* stream);
+/* Same with l_max = the largest l of any path (input, SH or output irreps; 0..3): with
+ * l_max <= 2 the kernels are the l <= 2 instantiation (fewer registers, more waves per SIMD).
+ * The plain entries above are l_max = 3 (any path). */
+int gmp_tp_edge_z_lmax_f32(const void* desc_host, int l_max, const void* paths_dev,
+                           const float* cg_dev, int cg_len, const float* x, const float* sh,
+                           const int64_t* src_sorted, const int64_t* perm, int64_t e0, int64_t e1,
+                           float* zbuf, void* stream);
+int gmp_tp_edge_z_bwd_lmax_f32(const void* desc_host, int l_max, const void* paths_dev,
+                               const float* cg_dev, int cg_len, const float* x, const float* sh,
+                               const int64_t* src_sorted, const int64_t* perm, int64_t e0,
+                               int64_t e1, const float* dzbuf, float* dx_edge, float* dY_edge,
+                               void* stream);
 
 /* K7 receiver-factorised per-receiver kernels (tfn_layer.py:73-87 regrouped): for the
  * receivers n of a chunk with chunk-local edge offsets eoff[n]..eoff[n+1] (receiver-sorted),
