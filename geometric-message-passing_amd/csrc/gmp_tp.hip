@@ -710,10 +710,8 @@ __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
   }
 }
 
-// OCC: workgroups per CU the register budget is sized for (LM = 2: 187 VGPRs free-running = 2;
-// 3 caps them at 168 with 28 B/lane of scratch)
-template <int LM, int OCC>
-__global__ __launch_bounds__(256, OCC) void tp_edge_z2_bwd_kernel(
+template <int LM>
+__global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
     Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
     const float* __restrict__ x, const float* __restrict__ sh,
     const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
@@ -810,8 +808,11 @@ __global__ __launch_bounds__(256, OCC) void tp_edge_z2_bwd_kernel(
   }
 }
 
-// dz kernel occupancy target at l <= 2 (GMP_TP_ZB_OCC=3: 168-VGPR cap; A/B)
-int g_zb_occ = getenv("GMP_TP_ZB_OCC") ? atoi(getenv("GMP_TP_ZB_OCC")) : 1;
+// GMP_TP_Z_GENERIC=1: always the l <= 3 instantiation.  r03 A/B: the l <= 2 instantiation (z 59
+// vs 91 VGPRs, 8 vs 5 waves per SIMD; dz 187 vs 249, and a 168-VGPR / 3-wave cap with 52 B of
+// scratch) measured within noise on the MACE / TFN steps (481.5 / 483.3 / 483.7 k; 998 / 994 /
+// 1,009 k edges/s): these kernels are not occupancy-bound
+int g_z_generic = getenv("GMP_TP_Z_GENERIC") ? atoi(getenv("GMP_TP_Z_GENERIC")) : 0;
 
 int64_t z2_blocks(int64_t edges) {
   const int64_t cap = (int64_t)device_cu_count() * 8;  // 32 resident waves per CU
@@ -905,7 +906,7 @@ int gmp_tp_edge_z_lmax_f32(const void* desc_host, int l_max, const void* paths_d
   GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 3);
   if (e1 == e0) return GMP_OK;
   const unsigned grid = (unsigned)z2_blocks(e1 - e0);
-  if (l_max <= 2 && d.sh_dim <= 9)
+  if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
     tp_edge_z2_kernel<2><<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
   else
@@ -933,16 +934,12 @@ int gmp_tp_edge_z_bwd_lmax_f32(const void* desc_host, int l_max, const void* pat
   GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 3);
   if (e1 == e0) return GMP_OK;
   const unsigned grid = (unsigned)z2_blocks(e1 - e0);
-  if (l_max <= 2 && d.sh_dim <= 9 && g_zb_occ == 3)
-    tp_edge_z2_bwd_kernel<2, 3><<<grid, 256, 0, as_stream(stream)>>>(
-        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
-        dx_edge, dY_edge);
-  else if (l_max <= 2 && d.sh_dim <= 9)
-    tp_edge_z2_bwd_kernel<2, 1><<<grid, 256, 0, as_stream(stream)>>>(
+  if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
+    tp_edge_z2_bwd_kernel<2><<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
         dx_edge, dY_edge);
   else
-    tp_edge_z2_bwd_kernel<3, 1><<<grid, 256, 0, as_stream(stream)>>>(
+    tp_edge_z2_bwd_kernel<3><<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
         dx_edge, dY_edge);
   return launch_status();
