@@ -676,14 +676,16 @@ class TPConvNodeFn(torch.autograd.Function):
                 G = G.reshape(c * d3, mo).contiguous()  # (d3 = 1: reshape alone is a view)
                 if x3[i]:
                     K1 = m1 * H
+                    fused = _dw_fused_ok(P, H)
+                    if not fused:  # (timed as tp_node_S, outside the dW region)
+                        S, Sb = _node_outer(eoff, Zp, a, w)
                     with _timed("tp_node_dW"):
-                        if _dw_fused_ok(P, H):
+                        if fused:
                             # K7f: dW2p with the S rows built in-kernel (S never in HBM); Sb
                             # (the bias rows) = the per-receiver sum of the z rows
                             part = tops.tp_node_dw(eoff, Zp, a, G, d3, m1)
                             Sb, _ = tops.segment_reduce(Zp, None, eoff, c, "sum")
                         else:
-                            S, Sb = _node_outer(eoff, Zp, a, w)
                             # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
                             part = tops.outer_sum_cols(S.view(c * d3, K1), G)
                             del S
