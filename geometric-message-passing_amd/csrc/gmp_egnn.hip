@@ -161,7 +161,7 @@ __device__ void load_params_hf(float* sV, _Float16* hW, const gmp_egnn_params& P
   atomicMax(&mxw[1], m3);
   // forward inputs of W2 / W3 are act(x_hat * w + b) of a LayerNorm over d features:
   // |x_hat| <= sqrt(d - 1), |act(z)| <= |z| (relu, silu) => |input| <= sqrt(d) max|w| + max|b|
-  if (!TRANSPOSE && threadIdx.x < 64) {
+  if (threadIdx.x < 64) {  // (the backward's x_hat3 recompute uses sx3 too)
     unsigned a = 0u, b = 0u, c = 0u, e = 0u;
     for (int k = threadIdx.x; k < D; k += 64) {
       a = max(a, __float_as_uint(fabsf(P.ln1_w[k])));
@@ -360,6 +360,62 @@ __device__ __forceinline__ void gemm_h2(const _Float16* __restrict__ hW, int sw,
   for (int t = 0; t < T; ++t) y[t] *= down;
 }
 
+// HF, the FORWARD product y[slot(o)] += sum_k W[o][k] x[slot(k)] read from the TRANSPOSED planes
+// (rows k, columns hf_pos(o): the backward's LDS image) with ds_read_b64_tr_b16.  Per 16-lane
+// group g and k block p, two transposed reads per plane (lane 4q + c of the group supplies row
+// 32p + 4g + q resp. 32p + 16 + 4g + q, physical columns hf_pos(16t + 4c .. 4c + 3), which are
+// contiguous) deliver to lane i the 8 halfs W[16t + i][32p + 16h + 4g + q] of the A fragment
+// that gemm_h2 reads as one row.  Same planes, scales and MFMA order: bitwise the forward's
+// product (the backward recomputes x_hat3 instead of reading it, gmp_egnn_set_save_xhat3).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ h16x4 lds_tr16(const _Float16* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(h16x4, v);
+}
+
+template <int D>
+__device__ __forceinline__ void gemm_h2_tr(const _Float16* __restrict__ hWt, int sw, int sx,
+                                           const f32x4 (&x)[D / 16], f32x4 (&y)[D / 16],
+                                           int lane, int g) {
+  using H = HCfg<D>;
+  constexpr int T = D / 16, PB = D / 32;
+  sx = sx < -100 - sw ? -100 - sw : (sx > 100 - sw ? 100 - sw : sx);
+  const float fx = ldexpf(1.f, sx), up = ldexpf(1.f, sx + sw), down = ldexpf(1.f, -(sx + sw));
+  const int q = (lane & 15) >> 2, c = lane & 3;
+#pragma unroll
+  for (int t = 0; t < T; ++t) y[t] *= up;
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    h16x8 bh, bl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = x[2 * p + (j >> 2)][j & 3] * fx;
+      const _Float16 h = (_Float16)v;
+      bh[j] = h;
+      bl[j] = (_Float16)(v - (float)h);
+    }
+    const _Float16* rowk = hWt + (32 * p + 4 * g + q) * H::LDH + 8 * c;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if (t % HF_TILES_PER_FENCE == 0) asm volatile("" ::: "memory");
+      const _Float16* a0 = rowk + 32 * (t >> 1) + 4 * (t & 1);
+      const _Float16* a1 = a0 + 16 * H::LDH;
+      const h16x4 h0 = lds_tr16(a0), h1 = lds_tr16(a1);
+      const h16x4 l0 = lds_tr16(a0 + H::PLANE), l1 = lds_tr16(a1 + H::PLANE);
+      const h16x8 ah = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      const h16x8 al = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, y[t], 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
+      y[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
+      if (t % HF_TILES_PER_FENCE == HF_TILES_PER_FENCE - 1) GMP_GEMM_FENCE();
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) y[t] *= down;
+}
+
 // y[slot(k)] += sum_o W[o][k] gin[slot(o)]   (transposed product for the backward)
 template <int D>
 __device__ __forceinline__ void gemm_wtx(const float* __restrict__ sW, const f32x4 (&gin)[D / 16],
@@ -429,6 +485,22 @@ __device__ __forceinline__ float ln_normalize(f32x4 (&x)[D / 16], float eps) {
 #pragma unroll
   for (int p = 0; p < T; ++p) x[p] *= rstd;
   return rstd;
+}
+
+// x <- (x - mean(x)) * rstd with the forward's own rstd (ln_normalize's first pass): x_hat from
+// the recomputed pre-LayerNorm row, bitwise the forward's
+template <int D>
+__device__ __forceinline__ void ln_recenter(f32x4 (&x)[D / 16], float rstd) {
+  constexpr int T = D / 16;
+  float s = 0.f;
+#pragma unroll
+  for (int p = 0; p < T; ++p) s += (x[p][0] + x[p][1]) + (x[p][2] + x[p][3]);
+  const float mean = sum_groups(s) * (1.f / D);
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+    x[p] -= mean;
+    x[p] *= rstd;
+  }
 }
 
 // dpre = rstd * (gr - mean(gr) - xhat * mean(gr * xhat)), gr = dL/dxhat ; in place on gr
@@ -693,7 +765,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
     const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
     float* __restrict__ m_aggr, float* __restrict__ pos_aggr, float* __restrict__ xsave,
-    float* __restrict__ rsave) {
+    float* __restrict__ rsave, int save3) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2 = smem;
@@ -752,7 +824,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     else gemm_wx<D>(sW3, m, x, li, g);
     const float r3 = ln_normalize<D>(x, eps);
     if (SAVE) {
-      store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
+      if (save3) store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
       store3_w<kAuxNT>(rows_window(rsave, base, ne, 3), (g == 0 && c.valid) ? li * 12u : kOob,
                        r1, r2, r3);
     }
@@ -827,7 +899,9 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
 // two transposed GEMMs (W3^T, W2^T) per 16-edge chunk.
 // AMAX: fold max |dpre2|, |dpre3| into amax[0], amax[1] (float bit patterns; the scales of the
 // HF weight-gradient outer sums, gmp_edge_outer_sum_act_hf_f32)
-template <int D, int ACT, bool MSG_MEAN, bool HF, bool AMAX>
+// REC: x_hat3 recomputed from x_hat2 (W3 from the W3^T image, the forward's rstd3) instead of
+// read: 2 d floats per edge less HBM traffic (the forward does not write it), bitwise the same
+template <int D, int ACT, bool MSG_MEAN, bool HF, bool AMAX, bool REC>
 __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
@@ -850,6 +924,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   else load_params_to_lds<D, true>(smem, P);
   __syncthreads();
   const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
+  const int sx3 = HF ? (int)sV[NV * D + 3] : 0;  // the forward's static W3-input exponent
   // AMAX: per-chunk wave maxima go to two LDS words (no loop-carried registers: the kernel sits
   // at 256 VGPRs), folded into amax[] once per workgroup at the end
   unsigned* lmx = reinterpret_cast<unsigned*>(const_cast<float*>(sV) + NV * D + 10);
@@ -889,12 +964,22 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     const float rs3 = rsave[3 * (size_t)c.ec + 2];
     const float gp0 = g_paggr[3 * c.i + 0], gp1 = g_paggr[3 * c.i + 1], gp2 = g_paggr[3 * c.i + 2];
     f32x4 x[T], xh2[T], z[T];
-    load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);  // z = xhat3
+    if constexpr (REC) load_row<D>(x, rowp(xsave + ED, c.ec, D), g);  // x = xhat2
+    else load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);            // z = xhat3
     __builtin_amdgcn_sched_barrier(0);
     edge_geom(c);
     const float rstd1 = c.valid ? rs1 : 0.f;
     const float rstd2 = c.valid ? rs2 : 0.f;
     const float rstd3 = c.valid ? rs3 : 0.f;
+    if constexpr (REC) {
+      // z = xhat3 = LN3(W3 act(LN2 affine(xhat2)) + b3) with the forward's 1/std: the forward's
+      // products (same operands, planes, scales and MFMA order) -> bitwise its x_hat3
+      affine_act<D, ACT>(x, sV, V_LN2W, V_LN2B, g);
+      load_vec<D>(z, sV, V_B3, g);
+      if constexpr (HF) gemm_h2_tr<D>(hW3t, sw3, sx3, x, z, lane, g);
+      else gemm_wtx<D>(sW3t, x, z, li, g);
+      ln_recenter<D>(z, rs3);
+    }
 
   // ---------------- pos-branch backward
     const float inv_deg = c.valid ? 1.f / (float)(c.seg1 - c.seg0) : 0.f;
@@ -1052,6 +1137,10 @@ int64_t n_waves_for(int64_t n_edges, int nwb) {
 // 1: the f32-MFMA (exact fmaf chain) products instead of the HF path; initial value from
 // GMP_EGNN_F32_MFMA, changed by gmp_egnn_set_f32_mfma
 int g_egnn_f32 = -1;
+// 1: the forward writes x_hat3 and the backward reads it (r02 form); 0 (default): the backward
+// recomputes it (GMP_EGNN_SAVE_XHAT3, gmp_egnn_set_save_xhat3)
+int g_save_xhat3 = getenv("GMP_EGNN_SAVE_XHAT3") ? atoi(getenv("GMP_EGNN_SAVE_XHAT3")) : 0;
+
 bool egnn_f32() {
   if (g_egnn_f32 < 0) {
     const char* e = getenv("GMP_EGNN_F32_MFMA");
@@ -1082,7 +1171,8 @@ int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const in
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / nwb), nwb * 64, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
-                                                           eps, W, m_aggr, pos_aggr, xsave, rsave);
+                                                           eps, W, m_aggr, pos_aggr, xsave, rsave,
+                                                           g_save_xhat3);
   return launch_status();
 }
 
@@ -1095,10 +1185,13 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
   const int64_t W = n_waves_for(E, kBwdWaves);
   const bool hf = !egnn_f32();
   const size_t smem = hf ? smem_total<D, kBwdWaves, true>() : smem_total<D, kBwdWaves, false>();
-  auto k = hf ? (amax ? egnn_bwd_kernel<D, ACT, MEAN, true, true>
-                      : egnn_bwd_kernel<D, ACT, MEAN, true, false>)
-              : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true>
-                      : egnn_bwd_kernel<D, ACT, MEAN, false, false>);
+#define GMP_BWD_K(REC)                                                  \
+  (hf ? (amax ? egnn_bwd_kernel<D, ACT, MEAN, true, true, REC>          \
+              : egnn_bwd_kernel<D, ACT, MEAN, true, false, REC>)        \
+      : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true, REC>         \
+              : egnn_bwd_kernel<D, ACT, MEAN, false, false, REC>))
+  auto k = g_save_xhat3 ? GMP_BWD_K(false) : GMP_BWD_K(true);
+#undef GMP_BWD_K
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / kBwdWaves), kBwdWaves * 64, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
@@ -1135,6 +1228,12 @@ using namespace gmp;
   } while (0)
 
 extern "C" {
+
+int gmp_egnn_set_save_xhat3(int on) {
+  const int prev = g_save_xhat3 ? 1 : 0;
+  g_save_xhat3 = on ? 1 : 0;
+  return prev;
+}
 
 int gmp_egnn_set_f32_mfma(int on) {
   const int prev = egnn_f32() ? 1 : 0;

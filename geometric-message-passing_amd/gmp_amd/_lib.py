@@ -70,6 +70,7 @@ SIGNATURES = {
                                       c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
     "gmp_egnn_set_f32_mfma": (c_int, [c_int]),
+    "gmp_egnn_set_save_xhat3": (c_int, [c_int]),
     "gmp_wgrad_set_grid_cap": (c_int, [c_int]),
     "gmp_stream_create_cu_share": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "gmp_stream_destroy": (c_int, [c_vp]),

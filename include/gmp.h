@@ -128,6 +128,12 @@ typedef struct gmp_egnn_params {
  * error ~2^-21 per product); gmp_egnn_set_f32_mfma(1) (or GMP_EGNN_F32_MFMA=1 at load) selects
  * the exact f32-MFMA fmaf chains.  Returns the previous setting. */
 int gmp_egnn_set_f32_mfma(int on);
+/* x_hat3 (the position-branch LayerNorm output) is by default NOT written by the forward: the
+ * backward recomputes it from x_hat2 and the saved 1/std (bitwise the forward's value), saving
+ * 2 d floats of HBM traffic per edge; plane 2 of save_xhat is then scratch.  on = 1 restores the
+ * saved form (set it before the forward whose buffers the backward consumes).  Returns the
+ * previous setting (initial value from GMP_EGNN_SAVE_XHAT3). */
+int gmp_egnn_set_save_xhat3(int on);
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
                           const float* pos, const int64_t* rowptr, const int64_t* recv,
                           const int64_t* send, const gmp_egnn_params* params, int act,

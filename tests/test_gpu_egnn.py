@@ -178,6 +178,47 @@ def test_frozen_parameters_release_side_stream_inputs():
     assert hd.grad is not None and all(p.grad is None for p in lay.parameters())
 
 
+@pytest.mark.parametrize("f32,act", [(False, "relu"), (False, "swish"), (True, "relu")])
+def test_xhat3_recompute_bitwise(f32, act):
+    """The K4 backward recomputing x_hat3 from x_hat2 and the saved 1/std (default) gives
+    bitwise the outputs and gradients of the saved-x_hat3 form (gmp_egnn_set_save_xhat3(1)),
+    for the HF (transposed-read W3 planes) and the exact-f32 products."""
+    import gmp_amd
+    from gmp_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(7)
+    g = _graph(3000, 60000, seed=8)
+    lay = gmp_amd.EGNNLayer(128, act, "layer", "sum").to(DEV)
+    with torch.no_grad():
+        for p in lay.parameters():
+            if p.dim() == 1:
+                p.add_(0.1 * torch.randn_like(p))
+    h = torch.randn(g.num_nodes, 128, device=DEV)
+    pos, ei = g.pos.to(DEV), g.edge_index.to(DEV)
+
+    def run():
+        lay.zero_grad(set_to_none=True)
+        hd, pd = h.clone().requires_grad_(True), pos.clone().requires_grad_(True)
+        ho, po = lay(hd, pd, ei)
+        (ho.square().sum() + (po * pos).sum()).backward()
+        torch.cuda.synchronize()
+        return [ho.detach(), po.detach(), hd.grad, pd.grad] + [p.grad.clone()
+                                                               for p in lay.parameters()]
+
+    prev_f = lib.gmp_egnn_set_f32_mfma(int(f32))
+    prev = lib.gmp_egnn_set_save_xhat3(1)
+    try:
+        a = run()
+        lib.gmp_egnn_set_save_xhat3(0)
+        b = run()
+    finally:
+        lib.gmp_egnn_set_save_xhat3(prev)
+        lib.gmp_egnn_set_f32_mfma(prev_f)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert b[2].abs().max().item() > 0
+
+
 def test_cu_masked_side_stream_same_gradients(monkeypatch):
     """With GMP_SIDE_CUS set, off the default stream the weight gradients run on a CU-masked
     side stream (gmp_stream_create_cu_share); the step must give bitwise the same loss and
