@@ -765,7 +765,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
     const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
     float* __restrict__ m_aggr, float* __restrict__ pos_aggr, float* __restrict__ xsave,
-    float* __restrict__ rsave, int save3) {
+    float* __restrict__ rsave, int save_mode) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2 = smem;
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     const int i0 = __builtin_amdgcn_readfirstlane(c.i);
     const int i1 = __builtin_amdgcn_readlane(c.i, 15);
     const unsigned eoff = c.valid ? (unsigned)(li * D * 4) : kOob;
-    if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
+    if (SAVE && save_mode >= 1) store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
     affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
 
     f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
@@ -815,7 +815,8 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     if constexpr (HF) gemm_h2<D, false>(hW2, sw2, sx2, x, m, li, g);
     else gemm_wx<D>(sW2, x, m, li, g);
     const float r2 = ln_normalize<D>(m, eps);
-    if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave + ED, base, ne, D), eoff, m, g);
+    if (SAVE && save_mode >= 1)
+      store_row_w<D, kAuxNT>(rows_window(xsave + ED, base, ne, D), eoff, m, g);
     affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);
 
     // y3 = act(LN3(W3 m + b3)); s = w4 . y3 + b4   (x reused)
@@ -824,7 +825,8 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     else gemm_wx<D>(sW3, m, x, li, g);
     const float r3 = ln_normalize<D>(x, eps);
     if (SAVE) {
-      if (save3) store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
+      if (save_mode == 2)
+        store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
       store3_w<kAuxNT>(rows_window(rsave, base, ne, 3), (g == 0 && c.valid) ? li * 12u : kOob,
                        r1, r2, r3);
     }
@@ -899,9 +901,13 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
 // two transposed GEMMs (W3^T, W2^T) per 16-edge chunk.
 // AMAX: fold max |dpre2|, |dpre3| into amax[0], amax[1] (float bit patterns; the scales of the
 // HF weight-gradient outer sums, gmp_edge_outer_sum_act_hf_f32)
-// REC: x_hat3 recomputed from x_hat2 (W3 from the W3^T image, the forward's rstd3) instead of
-// read: 2 d floats per edge less HBM traffic (the forward does not write it), bitwise the same
-template <int D, int ACT, bool MSG_MEAN, bool HF, bool AMAX, bool REC>
+// RC (what the backward recomputes instead of reading; bitwise the forward's values, with the
+// forward's saved 1/std and W2 / W3 from the W^T images by transposed reads):
+//   0: nothing (the forward saved x_hat1..3);
+//   1: x_hat3 from x_hat2 (the forward saved x_hat1, x_hat2);
+//   2: all three from the node projections AB (the forward saved only 1/std); x_hat1, x_hat2 are
+//      written to xw (the weight-gradient outer sums read them) and re-read from there.
+template <int D, int ACT, bool MSG_MEAN, bool HF, bool AMAX, int RC>
 __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
@@ -910,7 +916,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     const float* __restrict__ g_maggr, const float* __restrict__ g_paggr, float* __restrict__ dA,
     float* __restrict__ dpos_recv, float* __restrict__ dpre1_out, float* __restrict__ gdiff_out,
     float* __restrict__ dpre2_out, float* __restrict__ dpre3_out, float* __restrict__ partials,
-    unsigned* __restrict__ amax) {
+    unsigned* __restrict__ amax, const float* __restrict__ AB, float* __restrict__ xw) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW, K = VecAcc<D>::K;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2t = smem;  // W2^T
@@ -924,7 +930,10 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   else load_params_to_lds<D, true>(smem, P);
   __syncthreads();
   const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
-  const int sx3 = HF ? (int)sV[NV * D + 3] : 0;  // the forward's static W3-input exponent
+  const int sx2 = HF ? (int)sV[NV * D + 2] : 0;  // the forward's static W2 / W3 input exponents
+  const int sx3 = HF ? (int)sV[NV * D + 3] : 0;
+  // x_hat1 / x_hat2 as the rest of the body reads them (RC = 2: this kernel's own rows in xw)
+  const float* xr = RC == 2 ? (const float*)xw : xsave;
   // AMAX: per-chunk wave maxima go to two LDS words (no loop-carried registers: the kernel sits
   // at 256 VGPRs), folded into amax[] once per workgroup at the end
   unsigned* lmx = reinterpret_cast<unsigned*>(const_cast<float*>(sV) + NV * D + 10);
@@ -964,14 +973,33 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     const float rs3 = rsave[3 * (size_t)c.ec + 2];
     const float gp0 = g_paggr[3 * c.i + 0], gp1 = g_paggr[3 * c.i + 1], gp2 = g_paggr[3 * c.i + 2];
     f32x4 x[T], xh2[T], z[T];
-    if constexpr (REC) load_row<D>(x, rowp(xsave + ED, c.ec, D), g);  // x = xhat2
-    else load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);            // z = xhat3
-    __builtin_amdgcn_sched_barrier(0);
-    edge_geom(c);
+    if constexpr (RC == 2) {
+      load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);  // + edge_geom
+    } else {
+      if constexpr (RC == 1) load_row<D>(x, rowp(xsave + ED, c.ec, D), g);  // x = xhat2
+      else load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);               // z = xhat3
+      __builtin_amdgcn_sched_barrier(0);
+      edge_geom(c);
+    }
     const float rstd1 = c.valid ? rs1 : 0.f;
     const float rstd2 = c.valid ? rs2 : 0.f;
     const float rstd3 = c.valid ? rs3 : 0.f;
-    if constexpr (REC) {
+    if constexpr (RC == 2) {
+      // xhat1 = LN1(pre1), xhat2 = LN2(W2 act(LN1 affine(xhat1)) + b2): the forward's chain
+      const int nw = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
+      const unsigned woff = c.valid ? (unsigned)(li * D * 4) : kOob;
+      ln_recenter<D>(x, rs1);
+      store_row_w<D, 0>(rows_window(xw, base, nw, D), woff, x, g);  // (L2: re-read below)
+      affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
+      load_vec<D>(z, sV, V_B2, g);
+      if constexpr (HF) gemm_h2_tr<D>(hW2t, sw2, sx2, x, z, lane, g);
+      else gemm_wtx<D>(sW2t, x, z, li, g);
+      ln_recenter<D>(z, rs2);
+      store_row_w<D, 0>(rows_window(xw + ED, base, nw, D), woff, z, g);
+#pragma unroll
+      for (int p = 0; p < T; ++p) x[p] = z[p];
+    }
+    if constexpr (RC >= 1) {
       // z = xhat3 = LN3(W3 act(LN2 affine(xhat2)) + b3) with the forward's 1/std: the forward's
       // products (same operands, planes, scales and MFMA order) -> bitwise its x_hat3
       affine_act<D, ACT>(x, sV, V_LN2W, V_LN2B, g);
@@ -1023,7 +1051,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     // ---------------- dm = g_m_aggr[i] (/deg) + W3^T dpre3   (z); xhat2 -> xh2 in flight
 #pragma unroll
     for (int p = 0; p < T; ++p) z[p] = xh2[p] * gscale;
-    load_row<D>(xh2, rowp(xsave + ED, c.ec, D), g);
+    load_row<D>(xh2, rowp(xr + ED, c.ec, D), g);
     if constexpr (HF) gemm_h2<D, true>(hW3t, sw3, 0, x, z, li, g);  // z += W3^T dpre3
     else gemm_wx<D, 2>(sW3t, x, z, li, g);
 #pragma unroll
@@ -1041,7 +1069,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     store_row_w<D, kAuxNT>(rows_window(dpre2_out, base, ne, D), eoff, z, g);
 
     // ---------------- dy1 = W2^T dpre2 (x); xhat1 -> xh2 in flight
-    load_row<D>(xh2, rowp(xsave, c.ec, D), g);
+    load_row<D>(xh2, rowp(xr, c.ec, D), g);
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (HF) gemm_h2<D, true>(hW2t, sw2, 0, z, x, li, g);  // x = W2^T dpre2
@@ -1137,9 +1165,10 @@ int64_t n_waves_for(int64_t n_edges, int nwb) {
 // 1: the f32-MFMA (exact fmaf chain) products instead of the HF path; initial value from
 // GMP_EGNN_F32_MFMA, changed by gmp_egnn_set_f32_mfma
 int g_egnn_f32 = -1;
-// 1: the forward writes x_hat3 and the backward reads it (r02 form); 0 (default): the backward
-// recomputes it (GMP_EGNN_SAVE_XHAT3, gmp_egnn_set_save_xhat3)
-int g_save_xhat3 = getenv("GMP_EGNN_SAVE_XHAT3") ? atoi(getenv("GMP_EGNN_SAVE_XHAT3")) : 0;
+// which LayerNorm outputs the forward saves for the backward (gmp_egnn_set_xhat_mode,
+// GMP_EGNN_XHAT_MODE): 2 = x_hat1..3 (r02 form), 1 = x_hat1, x_hat2 (x_hat3 recomputed),
+// 0 = none (all recomputed from AB; the backward then needs AB and writes x_hat1, x_hat2)
+int g_xhat_mode = getenv("GMP_EGNN_XHAT_MODE") ? atoi(getenv("GMP_EGNN_XHAT_MODE")) : 1;
 
 bool egnn_f32() {
   if (g_egnn_f32 < 0) {
@@ -1164,7 +1193,7 @@ int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const in
   const int64_t W = n_waves_for(E, nwb);
   const size_t smem = hf ? smem_total<D, fwd_waves<true>(), true>()
                          : smem_total<D, fwd_waves<false>(), false>();
-  auto k = xsave ? (hf ? egnn_fwd_kernel<D, ACT, MEAN, true, true>
+  auto k = rsave ? (hf ? egnn_fwd_kernel<D, ACT, MEAN, true, true>
                        : egnn_fwd_kernel<D, ACT, MEAN, true, false>)
                  : (hf ? egnn_fwd_kernel<D, ACT, MEAN, false, true>
                        : egnn_fwd_kernel<D, ACT, MEAN, false, false>);
@@ -1172,7 +1201,7 @@ int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const in
   if (rc) return rc;
   k<<<(unsigned)(W / nwb), nwb * 64, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
                                                            eps, W, m_aggr, pos_aggr, xsave, rsave,
-                                                           g_save_xhat3);
+                                                           g_xhat_mode);
   return launch_status();
 }
 
@@ -1181,23 +1210,24 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
                const int64_t* recv, const int64_t* send, const gmp_egnn_params& P,
                const float* xsave, const float* rsave, const float* gm, const float* gp,
                float* dA, float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
-               float* dpre3, float* partials, unsigned* amax, hipStream_t s) {
+               float* dpre3, float* partials, unsigned* amax, const float* AB, float* xw,
+               hipStream_t s) {
   const int64_t W = n_waves_for(E, kBwdWaves);
   const bool hf = !egnn_f32();
   const size_t smem = hf ? smem_total<D, kBwdWaves, true>() : smem_total<D, kBwdWaves, false>();
-#define GMP_BWD_K(REC)                                                  \
-  (hf ? (amax ? egnn_bwd_kernel<D, ACT, MEAN, true, true, REC>          \
-              : egnn_bwd_kernel<D, ACT, MEAN, true, false, REC>)        \
-      : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true, REC>         \
-              : egnn_bwd_kernel<D, ACT, MEAN, false, false, REC>))
-  auto k = g_save_xhat3 ? GMP_BWD_K(false) : GMP_BWD_K(true);
+#define GMP_BWD_K(RC)                                                  \
+  (hf ? (amax ? egnn_bwd_kernel<D, ACT, MEAN, true, true, RC>          \
+              : egnn_bwd_kernel<D, ACT, MEAN, true, false, RC>)        \
+      : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true, RC>         \
+              : egnn_bwd_kernel<D, ACT, MEAN, false, false, RC>))
+  auto k = g_xhat_mode == 2 ? GMP_BWD_K(0) : (g_xhat_mode == 1 ? GMP_BWD_K(1) : GMP_BWD_K(2));
 #undef GMP_BWD_K
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / kBwdWaves), kBwdWaves * 64, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
                                                            xsave, rsave, gm, gp, dA, dpos_recv,
                                                            dpre1, gdiff, dpre2, dpre3, partials,
-                                                           amax);
+                                                           amax, AB, xw);
   return launch_status();
 }
 
@@ -1229,9 +1259,9 @@ using namespace gmp;
 
 extern "C" {
 
-int gmp_egnn_set_save_xhat3(int on) {
-  const int prev = g_save_xhat3 ? 1 : 0;
-  g_save_xhat3 = on ? 1 : 0;
+int gmp_egnn_set_xhat_mode(int mode) {
+  const int prev = g_xhat_mode;
+  if (mode >= 0 && mode <= 2) g_xhat_mode = mode;
   return prev;
 }
 
@@ -1257,7 +1287,9 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
   if (rc || n_edges == 0) return rc;
   GMP_CHECK_ARG(AB && pos && recv && send && aligned16(AB) && aligned16(m_aggr));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
-  GMP_CHECK_ARG((save_xhat == nullptr) == (save_rstd == nullptr));
+  // training: save_rstd always, save_xhat unless x_hat mode 0 (nothing saved but 1/std)
+  GMP_CHECK_ARG(save_rstd != nullptr || save_xhat == nullptr);
+  GMP_CHECK_ARG(save_rstd == nullptr || g_xhat_mode == 0 || save_xhat != nullptr);
   GMP_CHECK_ARG(save_xhat == nullptr || aligned16(save_xhat));
 #define GMP_CALL_FWD(DD, AA, MM)                                                              \
   rc = launch_fwd<DD, AA, MM>(n_nodes, n_edges, AB, pos, rowptr, recv, send, *params, ln_eps, \
@@ -1272,13 +1304,14 @@ int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d) {
   return n_waves_for(n_edges, kBwdWaves) / kBwdWaves;
 }
 
-int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
-                               const int64_t* rowptr, const int64_t* recv, const int64_t* send,
-                               const gmp_egnn_params* params, int act, int msg_mean,
-                               const float* save_xhat, const float* save_rstd,
-                               const float* g_m_aggr, const float* g_pos_aggr, float* dA,
-                               float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
-                               float* dpre3, float* vec_partials, uint32_t* amax, void* stream) {
+int gmp_egnn_edge_bwd_ab_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                             const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                             const gmp_egnn_params* params, int act, int msg_mean,
+                             const float* AB, const float* save_xhat, const float* save_rstd,
+                             const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                             float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
+                             float* dpre3, float* vec_partials, uint32_t* amax, float* xhat12,
+                             void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
   GMP_CHECK_ARG(n_nodes < INT32_MAX && n_edges < INT32_MAX);  // 32-bit edge / node ids
@@ -1295,18 +1328,34 @@ int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, cons
         vec_partials, 0,
         gmp_egnn_edge_bwd_partials_rows(n_edges, d) * (8 * d + 1) * sizeof(float), s));
   }
-  GMP_CHECK_ARG(pos && recv && send && save_xhat && save_rstd && g_m_aggr && g_pos_aggr &&
-                dpre1 && gdiff && dpre2 && dpre3);
-  GMP_CHECK_ARG(aligned16(save_xhat) && aligned16(dA) && aligned16(g_m_aggr) &&
+  GMP_CHECK_ARG(pos && recv && send && save_rstd && g_m_aggr && g_pos_aggr && dpre1 && gdiff &&
+                dpre2 && dpre3);
+  // mode 0 (nothing saved): the backward rebuilds x_hat1..3 from AB and writes x_hat1, x_hat2
+  GMP_CHECK_ARG(g_xhat_mode != 0 || (AB && xhat12 && aligned16(AB) && aligned16(xhat12)));
+  GMP_CHECK_ARG(g_xhat_mode == 0 || save_xhat);
+  GMP_CHECK_ARG((!save_xhat || aligned16(save_xhat)) && aligned16(dA) && aligned16(g_m_aggr) &&
                 aligned16(dpre1) && aligned16(dpre2) && aligned16(dpre3));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
 #define GMP_CALL_BWD(DD, AA, MM)                                                              \
   rc = launch_bwd<DD, AA, MM>(n_nodes, n_edges, pos, rowptr, recv, send, *params, save_xhat,  \
                               save_rstd, g_m_aggr, g_pos_aggr, dA, dpos_recv, dpre1, gdiff,    \
-                              dpre2, dpre3, vec_partials, amax, s)
+                              dpre2, dpre3, vec_partials, amax, AB, xhat12, s)
   GMP_EGNN_DISPATCH(GMP_CALL_BWD);
 #undef GMP_CALL_BWD
   return rc;
+}
+
+int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                               const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                               const gmp_egnn_params* params, int act, int msg_mean,
+                               const float* save_xhat, const float* save_rstd,
+                               const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                               float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
+                               float* dpre3, float* vec_partials, uint32_t* amax, void* stream) {
+  return gmp_egnn_edge_bwd_ab_f32(n_nodes, n_edges, d, pos, rowptr, recv, send, params, act,
+                                  msg_mean, nullptr, save_xhat, save_rstd, g_m_aggr, g_pos_aggr,
+                                  dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, vec_partials, amax,
+                                  nullptr, stream);
 }
 
 int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,

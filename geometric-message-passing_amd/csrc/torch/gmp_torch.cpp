@@ -235,27 +235,37 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(
   const int64_t N = pos.size(0), E = recv.numel(), d = AB.size(1) / 2;
   gmp_egnn_params P = egnn_params(params, d);
   Tensor m = at::empty({N, d}, fopt(AB)), pa = at::empty({N, 3}, fopt(AB));
-  Tensor xh = at::empty({train ? 3 : 0, E, d}, fopt(AB)), rs = at::empty({train ? E : 0, 3}, fopt(AB));
+  // x_hat mode 0 (gmp_egnn_set_xhat_mode): the forward saves only 1/std (xhat is (0, E, d))
+  const bool save_x = train && gmp_egnn_set_xhat_mode(-1) != 0;
+  Tensor xh = at::empty({save_x ? 3 : 0, E, d}, fopt(AB)), rs = at::empty({train ? E : 0, 3}, fopt(AB));
   check_rc(gmp_egnn_edge_fwd_f32(N, E, d, fp(AB), fp(pos), ip(rowptr), ip(recv), ip(send), &P,
                                  (int)act, msg_mean, (float)eps, fp(m), fp(pa),
-                                 train ? fp(xh) : nullptr, train ? fp(rs) : nullptr, cur_stream()),
+                                 save_x ? fp(xh) : nullptr, train ? fp(rs) : nullptr, cur_stream()),
            "gmp_egnn_edge_fwd_f32");
   return {m, pa, xh, rs};
 }
 
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
     const Tensor& pos, const Tensor& rowptr, const Tensor& recv, const Tensor& send,
     const std::vector<Tensor>& params, int64_t act, bool msg_mean, const Tensor& xhat,
-    const Tensor& rstd, const Tensor& g_m, const Tensor& g_p, const optional<Tensor>& amax) {
+    const Tensor& rstd, const Tensor& g_m, const Tensor& g_p, const optional<Tensor>& amax,
+    const optional<Tensor>& AB) {
   OpGuard g(pos, "egnn_edge_bwd");
   egnn_graph_checks(pos, rowptr, recv, send);
   f32(xhat, "xhat");
   f32(rstd, "rstd");
   f32(g_m, "g_m_aggr");
   f32(g_p, "g_pos_aggr");
-  TORCH_CHECK(xhat.dim() == 3, "gmp.egnn_edge_bwd: xhat must be (3, E, d)");
+  TORCH_CHECK(xhat.dim() == 3, "gmp.egnn_edge_bwd: xhat must be (3 or 0, E, d)");
   const int64_t N = pos.size(0), E = recv.numel(), d = xhat.size(2);
-  shape(xhat, {3, E, d}, "xhat");
+  const bool rebuild = gmp_egnn_set_xhat_mode(-1) == 0;  // x_hat1..3 rebuilt from AB
+  shape(xhat, {rebuild ? xhat.size(0) : 3, E, d}, "xhat");
+  TORCH_CHECK(xhat.size(0) == 3 || xhat.size(0) == 0, "gmp.egnn_edge_bwd: xhat (3 or 0, E, d)");
+  if (rebuild) {
+    TORCH_CHECK(AB.has_value(), "gmp.egnn_edge_bwd: x_hat mode 0 needs the forward's AB");
+    f32(*AB, "AB");
+    shape(*AB, {N, 2 * d}, "AB");
+  }
   shape(rstd, {E, 3}, "rstd");
   shape(g_m, {N, d}, "g_m_aggr");
   shape(g_p, {N, 3}, "g_pos_aggr");
@@ -268,15 +278,17 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd
   Tensor dA = at::empty({N, d}, o), dpr = at::empty({N, 3}, o), dp1 = at::empty({E, d}, o);
   Tensor gd = at::empty({E, 3}, o), dp2 = at::empty({E, d}, o), dp3 = at::empty({E, d}, o);
   Tensor part = at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o);
-  check_rc(gmp_egnn_edge_bwd_amax_f32(
+  // x_hat1, x_hat2 as rebuilt by the backward (mode 0; else empty: the forward's xhat holds them)
+  Tensor x12 = at::empty({rebuild ? 2 : 0, E, d}, o);
+  check_rc(gmp_egnn_edge_bwd_ab_f32(
                N, E, d, fp(pos), ip(rowptr), ip(recv), ip(send), &P, (int)act, msg_mean,
-               fp(xhat), fp(rstd), fp(g_m), fp(g_p), fp(dA), fp(dpr), fp(dp1), fp(gd), fp(dp2),
-               fp(dp3), fp(part),
+               rebuild ? fp(*AB) : nullptr, xhat.numel() ? fp(xhat) : nullptr, fp(rstd), fp(g_m),
+               fp(g_p), fp(dA), fp(dpr), fp(dp1), fp(gd), fp(dp2), fp(dp3), fp(part),
                amax.has_value() ? reinterpret_cast<uint32_t*>(amax->data_ptr<int32_t>())
                                 : nullptr,
-               cur_stream()),
-           "gmp_egnn_edge_bwd_amax_f32");
-  return {dA, dpr, dp1, gd, dp2, dp3, part};
+               rebuild ? fp(x12) : nullptr, cur_stream()),
+           "gmp_egnn_edge_bwd_ab_f32");
+  return {dA, dpr, dp1, gd, dp2, dp3, part, x12};
 }
 
 // ------------------------------------------------------------------ SchNet CFConv, SSP
@@ -1250,18 +1262,20 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(const Tensor& AB, const
                                                          int64_t, bool, double, bool train) {
   const int64_t N = pos.size(0), E = recv.numel(), d = AB.size(1) / 2;
   auto o = AB.options();
-  return {at::empty({N, d}, o), at::empty({N, 3}, o), at::empty({train ? 3 : 0, E, d}, o),
+  const bool save_x = train && gmp_egnn_set_xhat_mode(-1) != 0;
+  return {at::empty({N, d}, o), at::empty({N, 3}, o), at::empty({save_x ? 3 : 0, E, d}, o),
           at::empty({train ? E : 0, 3}, o)};
 }
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
     const Tensor& pos, const Tensor&, const Tensor& recv, const Tensor&,
     const std::vector<Tensor>&, int64_t, bool, const Tensor& xhat, const Tensor&, const Tensor&,
-    const Tensor&, const optional<Tensor>&) {
+    const Tensor&, const optional<Tensor>&, const optional<Tensor>&) {
   const int64_t N = pos.size(0), E = recv.numel(), d = xhat.size(2);
   auto o = pos.options();
   return {at::empty({N, d}, o), at::empty({N, 3}, o), at::empty({E, d}, o), at::empty({E, 3}, o),
           at::empty({E, d}, o), at::empty({E, d}, o),
-          at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o)};
+          at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o),
+          at::empty({gmp_egnn_set_xhat_mode(-1) == 0 ? 2 : 0, E, d}, o)};
 }
 Tensor cfconv_aggregate(const Tensor& x, const Tensor&, const Tensor&, const Tensor&,
                         const Tensor&, int64_t n_seg, const optional<Tensor>&) {
@@ -1445,8 +1459,9 @@ TORCH_LIBRARY(gmp, m) {
         "(Tensor m_aggr, Tensor pos_aggr, Tensor xhat, Tensor rstd)");
   m.def("egnn_edge_bwd(Tensor pos, Tensor rowptr, Tensor recv, Tensor send, Tensor[] params, "
         "int act, bool msg_mean, Tensor xhat, Tensor rstd, Tensor g_m_aggr, Tensor g_pos_aggr, "
-        "Tensor(a!)? amax=None) -> (Tensor dA, Tensor dpos_recv, Tensor dpre1, Tensor gdiff, "
-        "Tensor dpre2, Tensor dpre3, Tensor partials)");
+        "Tensor(a!)? amax=None, Tensor? AB=None) -> (Tensor dA, Tensor dpos_recv, "
+        "Tensor dpre1, Tensor gdiff, Tensor dpre2, Tensor dpre3, Tensor partials, "
+        "Tensor xhat12)");
   m.def("cfconv_aggregate(Tensor x, Tensor xidx, Tensor w, Tensor perm, Tensor rowptr, "
         "int n_seg, Tensor? escale=None) -> Tensor");
   m.def("cfconv_wgrad(Tensor g, Tensor gidx, Tensor x, Tensor xidx, Tensor? escale=None) -> "

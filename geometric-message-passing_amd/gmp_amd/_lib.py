@@ -70,7 +70,7 @@ SIGNATURES = {
                                       c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
     "gmp_egnn_set_f32_mfma": (c_int, [c_int]),
-    "gmp_egnn_set_save_xhat3": (c_int, [c_int]),
+    "gmp_egnn_set_xhat_mode": (c_int, [c_int]),
     "gmp_wgrad_set_grid_cap": (c_int, [c_int]),
     "gmp_stream_create_cu_share": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "gmp_stream_destroy": (c_int, [c_vp]),
@@ -99,6 +99,9 @@ SIGNATURES = {
                                             c_i64, c_vp, c_vp, c_vp]),
     "gmp_edge_outer_sum_act_hf_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,
                                               c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "gmp_egnn_edge_bwd_ab_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_amax_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -861,13 +861,15 @@ class EgnnMessageFn(torch.autograd.Function):
                 bool(msg_mean), float(eps), train)
         ctx.graph, ctx.act, ctx.msg_mean, ctx.N = graph, act, msg_mean, N
         if train:
-            ctx.save_for_backward(h, pos, xhat, rstd, W1, *params)
+            # AB: the backward rebuilds the LayerNorm outputs from it when the forward saved none
+            # (x_hat mode 0, gmp_egnn_set_xhat_mode; 51 MB at C2 against 1 GB of x_hat1, x_hat2)
+            ctx.save_for_backward(h, pos, xhat, rstd, AB, W1, *params)
         return m_aggr, pos_aggr
 
     @staticmethod
     @once_differentiable
     def backward(ctx, g_m, g_p):
-        h, pos, xhat, rstd, W1, *params = ctx.saved_tensors
+        h, pos, xhat, rstd, AB, W1, *params = ctx.saved_tensors
         graph = ctx.graph
         N, d = ctx.N, xhat.shape[2]
         E = graph.num_edges
@@ -879,9 +881,12 @@ class EgnnMessageFn(torch.autograd.Function):
         # two device words that scale their fp16 planes
         amax = torch.zeros(2, dtype=torch.int32, device=dev) if EGNN_WGRAD_HF else None
         with _timed("egnn_edge_bwd"):
-            dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, partials = _lib.torch_ops().egnn_edge_bwd(
-                pos, graph.rowptr, graph.recv, graph.send, list(params), _lib.ACT[ctx.act],
-                bool(ctx.msg_mean), xhat, rstd, g_m, g_p, amax)
+            dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, partials, x12 = \
+                _lib.torch_ops().egnn_edge_bwd(pos, graph.rowptr, graph.recv, graph.send,
+                                               list(params), _lib.ACT[ctx.act],
+                                               bool(ctx.msg_mean), xhat, rstd, g_m, g_p, amax, AB)
+        if x12.numel():  # x_hat1, x_hat2 rebuilt by the backward (x_hat mode 0)
+            xhat = x12
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")

@@ -128,12 +128,14 @@ typedef struct gmp_egnn_params {
  * error ~2^-21 per product); gmp_egnn_set_f32_mfma(1) (or GMP_EGNN_F32_MFMA=1 at load) selects
  * the exact f32-MFMA fmaf chains.  Returns the previous setting. */
 int gmp_egnn_set_f32_mfma(int on);
-/* x_hat3 (the position-branch LayerNorm output) is by default NOT written by the forward: the
- * backward recomputes it from x_hat2 and the saved 1/std (bitwise the forward's value), saving
- * 2 d floats of HBM traffic per edge; plane 2 of save_xhat is then scratch.  on = 1 restores the
- * saved form (set it before the forward whose buffers the backward consumes).  Returns the
- * previous setting (initial value from GMP_EGNN_SAVE_XHAT3). */
-int gmp_egnn_set_save_xhat3(int on);
+/* Which LayerNorm outputs the forward saves for the backward (mode 2 = x_hat1..3 into save_xhat
+ * planes 0..2; 1 (default) = x_hat1, x_hat2 — the backward recomputes x_hat3 from x_hat2 and the
+ * saved 1/std, bitwise the forward's value; 0 = none, save_xhat may be NULL — the backward
+ * rebuilds all three from the node projections AB (gmp_egnn_edge_bwd_ab_f32 only) and writes
+ * x_hat1, x_hat2 to its xhat12 output for the weight-gradient sums).  Set it before the forward
+ * whose buffers a backward consumes.  Returns the previous mode (mode outside 0..2: query only;
+ * initial value from GMP_EGNN_XHAT_MODE). */
+int gmp_egnn_set_xhat_mode(int mode);
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
                           const float* pos, const int64_t* rowptr, const int64_t* recv,
                           const int64_t* send, const gmp_egnn_params* params, int act,
@@ -165,6 +167,17 @@ int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
 /* As gmp_egnn_edge_bwd_f32, also folding max |dpre2| and max |dpre3| into amax[0], amax[1]
  * (float bit patterns, atomic max; caller zeroes): the A scales of the HF weight-gradient outer
  * sums (gmp_edge_outer_sum_act_hf_f32). */
+/* Backward with the node projections AB (N, 2d) of the forward (x_hat mode 0: the LayerNorm
+ * outputs are rebuilt from them) and xhat12 (2, E, d) receiving x_hat1, x_hat2 in that mode
+ * (AB / xhat12 may be NULL in modes 1, 2).  Other arguments as gmp_egnn_edge_bwd_amax_f32. */
+int gmp_egnn_edge_bwd_ab_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                             const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                             const gmp_egnn_params* params, int act, int msg_mean,
+                             const float* AB, const float* save_xhat, const float* save_rstd,
+                             const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                             float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
+                             float* dpre3, float* vec_partials, uint32_t* amax, float* xhat12,
+                             void* stream);
 int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
                                const int64_t* rowptr, const int64_t* recv, const int64_t* send,
                                const gmp_egnn_params* params, int act, int msg_mean,

@@ -178,17 +178,19 @@ def test_frozen_parameters_release_side_stream_inputs():
     assert hd.grad is not None and all(p.grad is None for p in lay.parameters())
 
 
-@pytest.mark.parametrize("f32,act", [(False, "relu"), (False, "swish"), (True, "relu")])
-def test_xhat3_recompute_bitwise(f32, act):
-    """The K4 backward recomputing x_hat3 from x_hat2 and the saved 1/std (default) gives
-    bitwise the outputs and gradients of the saved-x_hat3 form (gmp_egnn_set_save_xhat3(1)),
-    for the HF (transposed-read W3 planes) and the exact-f32 products."""
+@pytest.mark.parametrize("f32,act,aggr", [(False, "relu", "sum"), (False, "swish", "mean"),
+                                          (True, "relu", "sum")])
+def test_xhat_recompute_bitwise(f32, act, aggr):
+    """The K4 backward rebuilding the LayerNorm outputs (x_hat mode 1: x_hat3 from x_hat2; mode
+    0: all three from the node projections AB, W2 / W3 read transposed from the backward's W^T
+    image, the forward's saved 1/std) gives bitwise the outputs and gradients of the form that
+    saves x_hat1..3 (mode 2), for the HF and the exact-f32 products."""
     import gmp_amd
     from gmp_amd import _lib
     lib = _lib.load()
     torch.manual_seed(7)
     g = _graph(3000, 60000, seed=8)
-    lay = gmp_amd.EGNNLayer(128, act, "layer", "sum").to(DEV)
+    lay = gmp_amd.EGNNLayer(128, act, "layer", aggr).to(DEV)
     with torch.no_grad():
         for p in lay.parameters():
             if p.dim() == 1:
@@ -206,17 +208,18 @@ def test_xhat3_recompute_bitwise(f32, act):
                                                                for p in lay.parameters()]
 
     prev_f = lib.gmp_egnn_set_f32_mfma(int(f32))
-    prev = lib.gmp_egnn_set_save_xhat3(1)
+    prev = lib.gmp_egnn_set_xhat_mode(2)
     try:
-        a = run()
-        lib.gmp_egnn_set_save_xhat3(0)
-        b = run()
+        ref = run()
+        for mode in (1, 0):
+            lib.gmp_egnn_set_xhat_mode(mode)
+            got = run()
+            for k, (x, y) in enumerate(zip(ref, got)):
+                assert torch.equal(x, y), (mode, k)
     finally:
-        lib.gmp_egnn_set_save_xhat3(prev)
+        lib.gmp_egnn_set_xhat_mode(prev)
         lib.gmp_egnn_set_f32_mfma(prev_f)
-    for x, y in zip(a, b):
-        assert torch.equal(x, y)
-    assert b[2].abs().max().item() > 0
+    assert ref[2].abs().max().item() > 0
 
 
 def test_cu_masked_side_stream_same_gradients(monkeypatch):
