@@ -156,13 +156,23 @@ def tp_node_flops(model, n_nodes, n_edges):
     return total
 
 
-def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges):
-    """Minimum HBM bytes per edge of the fused EGNN edge backward: indices 16,
-    pos 24, the forward's saved x_hat1..3 (3 x d x 4) and rstd (12) read, dpre1..3 (3 x d x 4)
-    and gdiff (12) written; per-node rows (g_m_aggr + g_pos_aggr read, dA + dpos_recv
-    written) once per node, amortised over the edges."""
+def egnn_xhat_planes():
+    """LayerNorm outputs the EGNN forward saves and the backward reads (gmp_egnn_set_xhat_mode:
+    2 = x_hat1..3, 1 = x_hat1, x_hat2 with x_hat3 recomputed (default), 0 = none)."""
+    from gmp_amd import _lib
+    return {2: 3, 1: 2, 0: 0}[_lib.load().gmp_egnn_set_xhat_mode(-1)]
+
+
+def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges, planes=3):
+    """HBM bytes per edge the fused EGNN edge backward must move in this design:
+    indices 16, pos 24, the forward's saved LayerNorm outputs (`planes` x d x 4; x_hat3 is
+    recomputed in the default mode) and rstd (12) read, dpre1..3 (3 x d x 4) and gdiff (12)
+    written; per-node rows (g_m_aggr + g_pos_aggr read, dA + dpos_recv written) once per node,
+    amortised over the edges.  (Mode 0 also writes the rebuilt x_hat1, x_hat2: 2 d x 4.)"""
     per_node = 2 * (d * 4 + 12)
-    return 16 + 24 + 3 * d * 4 + 12 + 3 * d * 4 + 12 + per_node * n_nodes / n_edges
+    rebuilt = 2 * d * 4 if planes == 0 else 0
+    return (16 + 24 + planes * d * 4 + 12 + 3 * d * 4 + 12 + rebuilt
+            + per_node * n_nodes / n_edges)
 
 
 def gvp_flops_per_edge(s, v, se, ve):
@@ -174,10 +184,12 @@ def gvp_flops_per_edge(s, v, se, ve):
     return 2 * (g0 + 2 * g1)
 
 
-def egnn_flops_per_edge(d):
-    """Algorithmic fp32 FLOPs per edge of the two fused edge kernels."""
+def egnn_flops_per_edge(d, planes=3):
+    """fp32 FLOPs per edge of the two fused edge kernels: the backward's W3^T,
+    W2^T products plus the recomputation products of what the forward did not save (W3 for
+    x_hat3; W2 as well in mode 0)."""
     gemm = 2 * d * d
-    return {"egnn_edge_fwd": 2 * gemm, "egnn_edge_bwd": 2 * gemm}  # bwd: W3^T, W2^T
+    return {"egnn_edge_fwd": 2 * gemm, "egnn_edge_bwd": (2 + {3: 0, 2: 1, 0: 2}[planes]) * gemm}
 
 
 def _atom_type(workload):
@@ -444,10 +456,11 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
     rec = None
     if rank == 0:
         if workload == "egnn":
-            fl = egnn_flops_per_edge(emb)
+            planes = egnn_xhat_planes()
+            fl = egnn_flops_per_edge(emb, planes)
             ms_fwd, ms_bwd = timers["egnn_edge_fwd"], timers["egnn_edge_bwd"]
             tflops = fl["egnn_edge_bwd"] * g.num_edges / (ms_bwd * 1e-3) / 1e12
-            bpe = egnn_bwd_bytes_per_edge(emb, g.num_nodes, g.num_edges)
+            bpe = egnn_bwd_bytes_per_edge(emb, g.num_nodes, g.num_edges, planes)
             gbs = bpe * g.num_edges / (ms_bwd * 1e-3) / 1e9
             from gmp_amd import _lib
             lib = _lib.load()
@@ -469,7 +482,8 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
                     "flops_per_edge": fl["egnn_edge_bwd"], "mfma_frac": f_mfma,
                     "mfma_peak": peak, "products": "f32 MFMA" if f32_mode else
                     "f16 MFMA, 2-plane split operands (3 products per f32 product)",
-                    "bytes_per_edge_min": bpe, "hbm_gbs": gbs, "hbm_frac": f_hbm,
+                    "bytes_per_edge_min": bpe, "xhat_planes_saved": planes,
+                    "hbm_gbs": gbs, "hbm_frac": f_hbm,
                     "fwd_kernel_ms": ms_fwd,
                     "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
                     / (ms_fwd * 1e-3) / 1e12}
