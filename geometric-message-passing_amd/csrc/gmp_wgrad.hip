@@ -687,6 +687,8 @@ int64_t capped(int64_t g) { return g_grid_cap > 0 && g > g_grid_cap ? g_grid_cap
 // minimum edge tiles per workgroup of the f32-MFMA split-K sums (GMP_WGRAD_MIN_TILES; A/B)
 int g_min_tiles = getenv("GMP_WGRAD_MIN_TILES") ? atoi(getenv("GMP_WGRAD_MIN_TILES")) : 16;
 
+// smallest K (rows) routed to the split-plane sums (GMP_X3_MIN_K; A/B of the node-level sums)
+int64_t g_x3_min_k = getenv("GMP_X3_MIN_K") ? atoll(getenv("GMP_X3_MIN_K")) : 262144;
 // split-K workgroups of the edge-level x3 sums (GMP_X3_BLOCKS; default one per CU)
 int g_x3_blocks = getenv("GMP_X3_BLOCKS") ? atoi(getenv("GMP_X3_BLOCKS")) : 0;
 int64_t x3_blocks_for(int64_t K) {
@@ -711,7 +713,7 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   // loaded byte for the split's VALU and LDS staging to pay (measured: 16 x 128, 48 x 48 slower).
   // Node-level sums (K ~ 50k rows) stay there too: a few stages per block, and the 1-block-per-
   // CU LDS footprint keeps them from sharing CUs with the concurrent main-stream kernels.
-  if (m * n < 4096 || K < 262144) return GMP_ERR_UNSUPPORTED;
+  if (m * n < 4096 || K < g_x3_min_k) return GMP_ERR_UNSUPPORTED;
   int wn = 0;
   const int shape = x3_pick(m, n, &wn);
   const int64_t R = m + n;
