@@ -158,9 +158,9 @@ def tp_node_flops(model, n_nodes, n_edges):
 
 def egnn_xhat_planes():
     """LayerNorm outputs the EGNN forward saves and the backward reads (gmp_egnn_set_xhat_mode:
-    2 = x_hat1..3, 1 = x_hat1, x_hat2 with x_hat3 recomputed (default), 0 = none)."""
+    2 = x_hat1..3, 1 = x_hat1, x_hat2 with x_hat3 recomputed (default), 3 = x_hat2, 0 = none)."""
     from gmp_amd import _lib
-    return {2: 3, 1: 2, 0: 0}[_lib.load().gmp_egnn_set_xhat_mode(-1)]
+    return {2: 3, 1: 2, 3: 1, 0: 0}[_lib.load().gmp_egnn_set_xhat_mode(-1)]
 
 
 def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges, planes=3):
@@ -168,9 +168,10 @@ def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges, planes=3):
     indices 16, pos 24, the forward's saved LayerNorm outputs (`planes` x d x 4; x_hat3 is
     recomputed in the default mode) and rstd (12) read, dpre1..3 (3 x d x 4) and gdiff (12)
     written; per-node rows (g_m_aggr + g_pos_aggr read, dA + dpos_recv written) once per node,
-    amortised over the edges.  (Mode 0 also writes the rebuilt x_hat1, x_hat2: 2 d x 4.)"""
+    amortised over the edges.  (Modes 0 / 3 also write the rebuilt x_hat1 (, x_hat2) for the
+    weight sums: 2 - planes rows of d x 4.)"""
     per_node = 2 * (d * 4 + 12)
-    rebuilt = 2 * d * 4 if planes == 0 else 0
+    rebuilt = (2 - planes) * d * 4 if planes < 2 else 0
     return (16 + 24 + planes * d * 4 + 12 + 3 * d * 4 + 12 + rebuilt
             + per_node * n_nodes / n_edges)
 
@@ -189,7 +190,8 @@ def egnn_flops_per_edge(d, planes=3):
     W2^T products plus the recomputation products of what the forward did not save (W3 for
     x_hat3; W2 as well in mode 0)."""
     gemm = 2 * d * d
-    return {"egnn_edge_fwd": 2 * gemm, "egnn_edge_bwd": (2 + {3: 0, 2: 1, 0: 2}[planes]) * gemm}
+    return {"egnn_edge_fwd": 2 * gemm,
+            "egnn_edge_bwd": (2 + {3: 0, 2: 1, 1: 1, 0: 2}[planes]) * gemm}
 
 
 def _atom_type(workload):

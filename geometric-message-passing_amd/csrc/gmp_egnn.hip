@@ -807,7 +807,8 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     const int i0 = __builtin_amdgcn_readfirstlane(c.i);
     const int i1 = __builtin_amdgcn_readlane(c.i, 15);
     const unsigned eoff = c.valid ? (unsigned)(li * D * 4) : kOob;
-    if (SAVE && save_mode >= 1) store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
+    if (SAVE && (save_mode == 1 || save_mode == 2))
+      store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
     affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
 
     f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
@@ -906,7 +907,9 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
 //   0: nothing (the forward saved x_hat1..3);
 //   1: x_hat3 from x_hat2 (the forward saved x_hat1, x_hat2);
 //   2: all three from the node projections AB (the forward saved only 1/std); x_hat1, x_hat2 are
-//      written to xw (the weight-gradient outer sums read them) and re-read from there.
+//      written to xw (the weight-gradient outer sums read them) and re-read from there;
+//   3: x_hat1 from AB (no product: LN1 of the gathered projections) and x_hat3 from x_hat2 (the
+//      forward saved x_hat2 only); x_hat1 is written to xw plane 0 and re-read from there.
 template <int D, int ACT, bool MSG_MEAN, bool HF, bool AMAX, int RC>
 __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
@@ -933,7 +936,8 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   const int sx2 = HF ? (int)sV[NV * D + 2] : 0;  // the forward's static W2 / W3 input exponents
   const int sx3 = HF ? (int)sV[NV * D + 3] : 0;
   // x_hat1 / x_hat2 as the rest of the body reads them (RC = 2: this kernel's own rows in xw)
-  const float* xr = RC == 2 ? (const float*)xw : xsave;
+  const float* xr1 = RC >= 2 ? (const float*)xw : xsave;
+  const float* xr2 = (RC == 2 ? (const float*)xw : xsave) + (size_t)n_edges * D;
   // AMAX: per-chunk wave maxima go to two LDS words (no loop-carried registers: the kernel sits
   // at 256 VGPRs), folded into amax[] once per workgroup at the end
   unsigned* lmx = reinterpret_cast<unsigned*>(const_cast<float*>(sV) + NV * D + 10);
@@ -975,6 +979,9 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     f32x4 x[T], xh2[T], z[T];
     if constexpr (RC == 2) {
       load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);  // + edge_geom
+    } else if constexpr (RC == 3) {
+      load_row<D>(xh2, rowp(xsave + ED, c.ec, D), g);  // xhat2, in flight with the AB gathers
+      load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);  // + edge_geom
     } else {
       if constexpr (RC == 1) load_row<D>(x, rowp(xsave + ED, c.ec, D), g);  // x = xhat2
       else load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);               // z = xhat3
@@ -998,6 +1005,14 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
       store_row_w<D, 0>(rows_window(xw + ED, base, nw, D), woff, z, g);
 #pragma unroll
       for (int p = 0; p < T; ++p) x[p] = z[p];
+    }
+    if constexpr (RC == 3) {
+      const int nw = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
+      const unsigned woff = c.valid ? (unsigned)(li * D * 4) : kOob;
+      ln_recenter<D>(x, rs1);  // xhat1 = LN1(pre1): for the dW2 sum and the reload below
+      store_row_w<D, 0>(rows_window(xw, base, nw, D), woff, x, g);
+#pragma unroll
+      for (int p = 0; p < T; ++p) x[p] = xh2[p];
     }
     if constexpr (RC >= 1) {
       // z = xhat3 = LN3(W3 act(LN2 affine(xhat2)) + b3) with the forward's 1/std: the forward's
@@ -1051,7 +1066,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     // ---------------- dm = g_m_aggr[i] (/deg) + W3^T dpre3   (z); xhat2 -> xh2 in flight
 #pragma unroll
     for (int p = 0; p < T; ++p) z[p] = xh2[p] * gscale;
-    load_row<D>(xh2, rowp(xr + ED, c.ec, D), g);
+    load_row<D>(xh2, rowp(xr2, c.ec, D), g);
     if constexpr (HF) gemm_h2<D, true>(hW3t, sw3, 0, x, z, li, g);  // z += W3^T dpre3
     else gemm_wx<D, 2>(sW3t, x, z, li, g);
 #pragma unroll
@@ -1069,7 +1084,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     store_row_w<D, kAuxNT>(rows_window(dpre2_out, base, ne, D), eoff, z, g);
 
     // ---------------- dy1 = W2^T dpre2 (x); xhat1 -> xh2 in flight
-    load_row<D>(xh2, rowp(xr, c.ec, D), g);
+    load_row<D>(xh2, rowp(xr1, c.ec, D), g);
 #pragma unroll
     for (int p = 0; p < T; ++p) x[p] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (HF) gemm_h2<D, true>(hW2t, sw2, 0, z, x, li, g);  // x = W2^T dpre2
@@ -1167,7 +1182,8 @@ int64_t n_waves_for(int64_t n_edges, int nwb) {
 int g_egnn_f32 = -1;
 // which LayerNorm outputs the forward saves for the backward (gmp_egnn_set_xhat_mode,
 // GMP_EGNN_XHAT_MODE): 2 = x_hat1..3 (r02 form), 1 = x_hat1, x_hat2 (x_hat3 recomputed),
-// 0 = none (all recomputed from AB; the backward then needs AB and writes x_hat1, x_hat2)
+// 0 = none (all recomputed from AB; the backward then needs AB and writes x_hat1, x_hat2),
+// 3 = x_hat2 (x_hat1 rebuilt from AB and written by the backward, x_hat3 recomputed)
 int g_xhat_mode = getenv("GMP_EGNN_XHAT_MODE") ? atoi(getenv("GMP_EGNN_XHAT_MODE")) : 1;
 
 bool egnn_f32() {
@@ -1220,7 +1236,9 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
               : egnn_bwd_kernel<D, ACT, MEAN, true, false, RC>)        \
       : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true, RC>         \
               : egnn_bwd_kernel<D, ACT, MEAN, false, false, RC>))
-  auto k = g_xhat_mode == 2 ? GMP_BWD_K(0) : (g_xhat_mode == 1 ? GMP_BWD_K(1) : GMP_BWD_K(2));
+  auto k = g_xhat_mode == 2 ? GMP_BWD_K(0)
+          : g_xhat_mode == 1 ? GMP_BWD_K(1)
+          : g_xhat_mode == 3 ? GMP_BWD_K(3) : GMP_BWD_K(2);
 #undef GMP_BWD_K
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
@@ -1261,7 +1279,7 @@ extern "C" {
 
 int gmp_egnn_set_xhat_mode(int mode) {
   const int prev = g_xhat_mode;
-  if (mode >= 0 && mode <= 2) g_xhat_mode = mode;
+  if (mode >= 0 && mode <= 3) g_xhat_mode = mode;
   return prev;
 }
 
@@ -1331,7 +1349,8 @@ int gmp_egnn_edge_bwd_ab_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const 
   GMP_CHECK_ARG(pos && recv && send && save_rstd && g_m_aggr && g_pos_aggr && dpre1 && gdiff &&
                 dpre2 && dpre3);
   // mode 0 (nothing saved): the backward rebuilds x_hat1..3 from AB and writes x_hat1, x_hat2
-  GMP_CHECK_ARG(g_xhat_mode != 0 || (AB && xhat12 && aligned16(AB) && aligned16(xhat12)));
+  GMP_CHECK_ARG((g_xhat_mode != 0 && g_xhat_mode != 3) ||
+                (AB && xhat12 && aligned16(AB) && aligned16(xhat12)));
   GMP_CHECK_ARG(g_xhat_mode == 0 || save_xhat);
   GMP_CHECK_ARG((!save_xhat || aligned16(save_xhat)) && aligned16(dA) && aligned16(g_m_aggr) &&
                 aligned16(dpre1) && aligned16(dpre2) && aligned16(dpre3));

@@ -258,11 +258,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_
   f32(g_p, "g_pos_aggr");
   TORCH_CHECK(xhat.dim() == 3, "gmp.egnn_edge_bwd: xhat must be (3 or 0, E, d)");
   const int64_t N = pos.size(0), E = recv.numel(), d = xhat.size(2);
-  const bool rebuild = gmp_egnn_set_xhat_mode(-1) == 0;  // x_hat1..3 rebuilt from AB
-  shape(xhat, {rebuild ? xhat.size(0) : 3, E, d}, "xhat");
+  const int mode = gmp_egnn_set_xhat_mode(-1);
+  const bool rebuild = mode == 0 || mode == 3;  // x_hat1 (mode 0: x_hat1..3) rebuilt from AB
+  shape(xhat, {mode == 0 ? xhat.size(0) : 3, E, d}, "xhat");
   TORCH_CHECK(xhat.size(0) == 3 || xhat.size(0) == 0, "gmp.egnn_edge_bwd: xhat (3 or 0, E, d)");
   if (rebuild) {
-    TORCH_CHECK(AB.has_value(), "gmp.egnn_edge_bwd: x_hat mode 0 needs the forward's AB");
+    TORCH_CHECK(AB.has_value(), "gmp.egnn_edge_bwd: x_hat modes 0 / 3 need the forward's AB");
     f32(*AB, "AB");
     shape(*AB, {N, 2 * d}, "AB");
   }
@@ -278,8 +279,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_
   Tensor dA = at::empty({N, d}, o), dpr = at::empty({N, 3}, o), dp1 = at::empty({E, d}, o);
   Tensor gd = at::empty({E, 3}, o), dp2 = at::empty({E, d}, o), dp3 = at::empty({E, d}, o);
   Tensor part = at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o);
-  // x_hat1, x_hat2 as rebuilt by the backward (mode 0; else empty: the forward's xhat holds them)
-  Tensor x12 = at::empty({rebuild ? 2 : 0, E, d}, o);
+  // x_hat1 (, x_hat2) as rebuilt by the backward (modes 3 / 0; else empty: the forward's xhat)
+  Tensor x12 = at::empty({mode == 0 ? 2 : (mode == 3 ? 1 : 0), E, d}, o);
   check_rc(gmp_egnn_edge_bwd_ab_f32(
                N, E, d, fp(pos), ip(rowptr), ip(recv), ip(send), &P, (int)act, msg_mean,
                rebuild ? fp(*AB) : nullptr, xhat.numel() ? fp(xhat) : nullptr, fp(rstd), fp(g_m),
@@ -1275,7 +1276,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_
   return {at::empty({N, d}, o), at::empty({N, 3}, o), at::empty({E, d}, o), at::empty({E, 3}, o),
           at::empty({E, d}, o), at::empty({E, d}, o),
           at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o),
-          at::empty({gmp_egnn_set_xhat_mode(-1) == 0 ? 2 : 0, E, d}, o)};
+          at::empty({gmp_egnn_set_xhat_mode(-1) == 0 ? 2 : (gmp_egnn_set_xhat_mode(-1) == 3 ? 1 : 0),
+                     E, d}, o)};
 }
 Tensor cfconv_aggregate(const Tensor& x, const Tensor&, const Tensor&, const Tensor&,
                         const Tensor&, int64_t n_seg, const optional<Tensor>&) {

@@ -885,8 +885,10 @@ class EgnnMessageFn(torch.autograd.Function):
                 _lib.torch_ops().egnn_edge_bwd(pos, graph.rowptr, graph.recv, graph.send,
                                                list(params), _lib.ACT[ctx.act],
                                                bool(ctx.msg_mean), xhat, rstd, g_m, g_p, amax, AB)
-        if x12.numel():  # x_hat1, x_hat2 rebuilt by the backward (x_hat mode 0)
-            xhat = x12
+        # x_hat1, x_hat2 for the dW2 / dW3 sums: the forward's, or rebuilt by the backward
+        # (x_hat mode 0: both; mode 3: x_hat1)
+        xh1 = x12[0] if x12.shape[0] >= 1 else xhat[0]
+        xh2 = x12[1] if x12.shape[0] == 2 else xhat[1]
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
@@ -901,7 +903,7 @@ class EgnnMessageFn(torch.autograd.Function):
 
         # weight gradients: side stream, accumulated at the end of the backward pass
         (_, b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3, b3, ln3w, ln3b, w4, b4) = params
-        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials, amax) as sw:
+        with side_work(h, dA, dB, dpre2, dpre3, xhat, x12, partials, amax) as sw:
             dW1 = torch.empty((d, 2 * d + 1), **f)
             db1 = torch.empty(d, **f)
             outer_sum_into(dA, h, dW1[:, :d], db1)
@@ -909,9 +911,9 @@ class EgnnMessageFn(torch.autograd.Function):
             v = partials.sum(0)
             dln1w, dln1b, dln2w, dln2b, dln3w, dln3b, dw4, dw1d = v[:8 * d].view(8, d).unbind(0)
             dW1[:, 2 * d].copy_(dw1d)
-            dW2, db2 = edge_outer_sum_act(dpre2, xhat[0], ln1w, ln1b, ctx.act,
+            dW2, db2 = edge_outer_sum_act(dpre2, xh1, ln1w, ln1b, ctx.act,
                                           amax[0:1] if amax is not None else None)
-            dW3, db3 = edge_outer_sum_act(dpre3, xhat[1], ln2w, ln2b, ctx.act,
+            dW3, db3 = edge_outer_sum_act(dpre3, xh2, ln2w, ln2b, ctx.act,
                                           amax[1:2] if amax is not None else None)
             grads = (dW1, db1, dln1w, dln1b, dW2, db2, dln2w, dln2b, dW3, db3, dln3w, dln3b,
                      dw4.view(1, d), v[8 * d:8 * d + 1])

@@ -133,7 +133,9 @@ int gmp_egnn_set_f32_mfma(int on);
  * saved 1/std, bitwise the forward's value; 0 = none, save_xhat may be NULL — the backward
  * rebuilds all three from the node projections AB (gmp_egnn_edge_bwd_ab_f32 only) and writes
  * x_hat1, x_hat2 to its xhat12 output for the weight-gradient sums).  Set it before the forward
- * whose buffers a backward consumes.  Returns the previous mode (mode outside 0..2: query only;
+ * whose buffers a backward consumes; 3 = x_hat2 only — the _ab backward rebuilds x_hat1 from AB
+ * (no product) into xhat12 plane 0 and recomputes x_hat3.  Returns the previous mode (mode
+ * outside 0..3: query only;
  * initial value from GMP_EGNN_XHAT_MODE). */
 int gmp_egnn_set_xhat_mode(int mode);
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,

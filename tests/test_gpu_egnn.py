@@ -211,7 +211,7 @@ def test_xhat_recompute_bitwise(f32, act, aggr):
     prev = lib.gmp_egnn_set_xhat_mode(2)
     try:
         ref = run()
-        for mode in (1, 0):
+        for mode in (1, 0, 3):
             lib.gmp_egnn_set_xhat_mode(mode)
             got = run()
             for k, (x, y) in enumerate(zip(ref, got)):
