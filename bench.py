@@ -17,6 +17,10 @@ xGMI).  --graph replays the step from a HIP graph instead of launching it eagerl
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+`python bench.py --gpus N` (N > 1) without torchrun's environment starts the N rank processes
+itself (torch.distributed.run, 127.0.0.1 rendezvous) before this process touches the GPU and exits
+with their status; under torchrun, WORLD_SIZE must equal N (else exit status 2).
+
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel of the value's workload
 (EGNN: egnn_edge_bwd, both bounds, the closer one primary), timed with HIP events on the stream
 it is launched on; the `mace` object's roofline is the whole TP contraction's algorithmic FLOP
@@ -52,11 +56,17 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="egnn+mace",
-                    choices=("egnn+mace", "egnn", "gvp", "mace", "tfn", "schnet"))
+    ap.add_argument("--workload", default="egnn+mace+gvp+tfn",
+                    help="'+'-joined workloads (egnn, mace, gvp, tfn, schnet); the first is the "
+                         "line's value, the others its secondary objects")
     ap.add_argument("--mace-steps", type=int, default=3,
-                    help="timed steps of the secondary MACE workload (egnn+mace)")
+                    help="timed steps of the secondary MACE / TFN workloads")
     ap.add_argument("--mace-warmup", type=int, default=1)
+    ap.add_argument("--no-f32-exact", action="store_true",
+                    help="skip the egnn_f32_exact leg (EGNN steps with every product on the "
+                         "exact f32 MFMA)")
+    ap.add_argument("--no-forward", action="store_true",
+                    help="skip the forward-only (inference) timing of each workload")
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--emb", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=50_000)
@@ -76,6 +86,9 @@ def parse():
                     choices=("default", "hipblaslt", "hipblas"),
                     help="library for the node-level PyTorch GEMMs (torch.backends.cuda."
                          "preferred_blas_library)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="launcher / rank / timing path only, on the CPU (gloo) with a small torch "
+                         "model in place of the GPU workload (tests/test_bench_launch.py)")
     ap.add_argument("--timing-steps", type=int, default=2,
                     help="eager steps after the timed region in which the roofline kernel is "
                          "timed with HIP events (graph mode)")
@@ -157,10 +170,10 @@ def tp_node_flops(model, n_nodes, n_edges):
 
 
 def egnn_xhat_planes():
-    """LayerNorm outputs the EGNN forward saves and the backward reads (gmp_egnn_set_xhat_mode:
-    2 = x_hat1..3, 1 = x_hat1, x_hat2 with x_hat3 recomputed (default), 3 = x_hat2, 0 = none)."""
-    from gmp_amd import _lib
-    return {2: 3, 1: 2, 3: 1, 0: 0}[_lib.load().gmp_egnn_set_xhat_mode(-1)]
+    """LayerNorm outputs the EGNN forward saves and the backward reads (ops.EGNN_XHAT_PLANES:
+    2 = x_hat1, x_hat2 with x_hat3 recomputed (default), 3 = x_hat1..3)."""
+    from gmp_amd import ops
+    return ops.EGNN_XHAT_PLANES
 
 
 def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges, planes=3):
@@ -174,6 +187,69 @@ def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges, planes=3):
     rebuilt = (2 - planes) * d * 4 if planes < 2 else 0
     return (16 + 24 + planes * d * 4 + 12 + 3 * d * 4 + 12 + rebuilt
             + per_node * n_nodes / n_edges)
+
+
+# SURVEY §8(d) algorithmic bytes per edge and layer of the EGNN forward (fused minimum: idx 16 +
+# pos 24 + h_i, h_j 1,024 + message scatter 512 + pos 12 + count 4)
+EGNN_SURVEY_BYTES_PER_EDGE = 1592
+
+
+def tp_forward_flops(model, n_nodes, n_edges):
+    """Algorithmic FLOPs of the TP convolutions' forward (tp_node_flops' forward share: per layer
+    S = 2 E J z_size plus the path GEMMs 2 N J sum_p (2lo+1) mul1 mul_out)."""
+    total = 0
+    for conv in model.convs:
+        pl = conv.plan
+        J = conv.fc[0].out_features + 1
+        total += 2 * n_edges * J * pl.desc.z_size
+        total += 2 * n_nodes * J * sum((2 * i["lo"] + 1) * i["mul1"] * i["mul_out"]
+                                       for i in pl.instructions)
+    return total
+
+
+def time_forward(model, batch, reps):
+    """Inference forward (no autograd; the kernels save nothing for a backward): average wall
+    seconds per pass over `reps` passes after one warm-up pass, synchronised on both sides, and
+    the per-region kernel times recorded meanwhile (ops timers)."""
+    from gmp_amd import ops
+    with torch.no_grad():
+        model(batch)
+        torch.cuda.synchronize()
+        ops.KERNEL_TIMERS = {}
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            model(batch)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+    timers = {k: ops.kernel_time_ms(k) * len(v) / reps for k, v in ops.KERNEL_TIMERS.items()}
+    ops.KERNEL_TIMERS = None
+    return dt, timers
+
+
+def forward_roofline(workload, model, g, layers, dt, timers):
+    """north_star's forward target (>= 50 % of the HBM roofline on EGNN + MACE forward): the
+    inference forward's rate and its fraction of 8 TB/s for SURVEY §8(d)'s algorithmic bytes (and,
+    for the TP models, of the three-plane MFMA ceiling for the contraction's FLOPs)."""
+    E = g.num_edges
+    out = {"edges_per_s": E / dt, "ms": dt * 1e3, "mode": "inference (torch.no_grad)"}
+    if workload == "egnn":
+        algo = EGNN_SURVEY_BYTES_PER_EDGE * E * layers
+        k4 = timers.get("egnn_edge_fwd")
+        out.update({"survey_bytes_per_edge_layer": EGNN_SURVEY_BYTES_PER_EDGE,
+                    "hbm_frac_model": algo / dt / 1e9 / HBM_PEAK_GBS,
+                    "k4_fwd_ms_per_layer": None if k4 is None else k4 / layers,
+                    "hbm_frac_k4": None if not k4 else
+                    EGNN_SURVEY_BYTES_PER_EDGE * E / (k4 / layers * 1e-3) / 1e9 / HBM_PEAK_GBS})
+    elif workload in ("mace", "tfn"):
+        algo = tp_algorithmic_bytes(model, E) / 3  # the forward's third
+        fl = tp_forward_flops(model, g.num_nodes, E)
+        t_tp = sum(timers.get(k, 0.0) for k in ("tp_node_S", "tp_node_W"))
+        out.update({"survey_bytes": algo, "hbm_frac_model": algo / dt / 1e9 / HBM_PEAK_GBS,
+                    "tp_flops": fl, "tp_ms": t_tp,
+                    "tp_mfma_frac": (fl / (t_tp * 1e-3) / 1e12 / X3_PEAK_TFLOPS) if t_tp else None,
+                    "bound_note": "the TP contraction is MFMA-bound (arithmetic intensity far "
+                                  "above the ridge): its MFMA fraction is the binding one"})
+    return out
 
 
 def gvp_flops_per_edge(s, v, se, ve):
@@ -407,7 +483,7 @@ def mace_roofline(model, n_nodes, n_edges, timers, counts, n_steps, workload="ma
 TIMER_NAMES = {"egnn": {"egnn_edge_fwd", "egnn_edge_bwd"}, "gvp": set(), "schnet": set()}
 
 
-def run_workload(workload, args, g, rank, world, dev, steps, warmup):
+def run_workload(workload, args, g, rank, world, dev, steps, warmup, exact=False):
     """Build the model, warm up, time `steps` steps (barrier + synchronize on both sides, max
     over ranks); returns the bench record fields of this workload (rank 0) or None."""
     import gmp_amd
@@ -416,6 +492,9 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
     from gmp_amd.step import GraphedStep
 
     layers, emb = args.layers_of[workload], args.emb_of[workload]
+    if exact:  # every product on the exact f32 MFMA (K4 and the weight-gradient outer sums)
+        from gmp_amd import _lib
+        prev = (_lib.load().gmp_egnn_set_f32_mfma(1), _lib.load().gmp_wgrad_set_f32_mfma(1))
     torch.manual_seed(0)
     model = build_model(gmp_amd, workload, layers, emb).to(dev)
     # Adam (the reference optimizer, train_utils.py): the fused multi-tensor implementation
@@ -455,6 +534,25 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
     totals = {k: timers[k] * len(v) for k, v in ops.KERNEL_TIMERS.items()}
     counts = {k: len(v) for k, v in ops.KERNEL_TIMERS.items()}
     ops.KERNEL_TIMERS = None
+    if exact:
+        _lib.load().gmp_egnn_set_f32_mfma(prev[0])
+        _lib.load().gmp_wgrad_set_f32_mfma(prev[1])
+        rec = None
+        if rank == 0:
+            rec = {"value": total_edges * steps / elapsed, "unit": "edges/s", "steps": steps,
+                   "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
+                   "products": "exact f32 MFMA everywhere (gmp_egnn_set_f32_mfma(1), "
+                               "gmp_wgrad_set_f32_mfma(1)): the A/B rate of the line's "
+                               "split-operand products"}
+        del step, opt, model, batch
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        return rec
+    fwd = None
+    if not args.no_forward:
+        ops.KERNEL_TIMER_NAMES = None
+        dt, ftimers = time_forward(model, batch, 1 if workload in ("mace", "tfn") else 5)
+        fwd = forward_roofline(workload, model, g, layers, dt, ftimers)
     rec = None
     if rank == 0:
         if workload == "egnn":
@@ -479,7 +577,14 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
             else:
                 prim = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": f_hbm}
+            # SURVEY §8(d)'s algorithmic bytes (1,592 B per edge and layer) instead of the bytes
+            # this design's backward moves (saved x_hat planes, dpre rows for the weight sums)
+            frac_survey = EGNN_SURVEY_BYTES_PER_EDGE * g.num_edges / (ms_bwd * 1e-3) / 1e9 \
+                / HBM_PEAK_GBS
             roof = {"kernel": "egnn_edge_bwd", "kernel_prefix": "egnn_bwd_kernel", **prim,
+                    "frac_survey": frac_survey,
+                    "frac_survey_note": "SURVEY §8(d) 1,592 B/edge per layer over this kernel's "
+                                        "time at 8 TB/s",
                     "traffic": None, "ms_per_launch": ms_bwd,
                     "flops_per_edge": fl["egnn_edge_bwd"], "mfma_frac": f_mfma,
                     "mfma_peak": peak, "products": "f32 MFMA" if f32_mode else
@@ -512,16 +617,80 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup):
                "workload": f"{WORKLOADS[workload][0]} {layers}L/{emb} radius graph "
                            f"{g.num_nodes} nodes / {g.num_edges} edges per GPU "
                            f"(r={g.radius}, box={g.box:.3f}, seed=rank)",
-               "roofline": roof, "cpu_baseline": None}
+               "roofline": roof, "forward": fwd, "cpu_baseline": None}
     del step, opt, model, batch
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return rec
 
 
+def launch_ranks(args):
+    """--gpus N: under torchrun (WORLD_SIZE set) the world must be N; without it and N > 1, start
+    N rank processes as children (torch.distributed.run, one per GPU, 127.0.0.1 rendezvous) —
+    before anything here touches the GPU — and exit with their status."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} ranks were launched",
+                  file=sys.stderr, flush=True)
+            sys.exit(2)
+        return
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.gpus == 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def run_plumbing(args):
+    """--plumbing: this script's launcher / rank / barrier / max-over-ranks / JSON path on the
+    CPU (gloo), with a small torch model stepped by the same executor (GraphedStep, flat
+    all-reduce) in place of the GPU workload."""
+    from gmp_amd import dist as gdist
+    from gmp_amd.step import GraphedStep
+    rank, world, _ = gdist.init("gloo")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 1))
+    x = torch.randn(64, 16, generator=torch.Generator().manual_seed(rank))
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    step = GraphedStep(model, lambda: model(x).abs().sum(), opt, warmup=args.warmup,
+                       use_graph=False)
+    gdist.barrier(cuda=False)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    gdist.barrier(cuda=False)
+    elapsed = gdist.max_over_ranks(time.perf_counter() - t0)
+    rows = gdist.sum_over_ranks(x.shape[0])
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing rows/s (CPU, gloo)", "value": rows * args.steps /
+                          elapsed, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "config": {"workload": "plumbing", "parallelism": f"dp{world}"}}),
+              flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
+    launch_ranks(args)
+    if args.plumbing:
+        run_plumbing(args)
+        return
     names = args.workload.split("+")
+    for w in names:
+        if w not in WORKLOADS:
+            raise SystemExit(f"bench.py: unknown workload {w!r} (choices: {', '.join(WORKLOADS)})")
     args.layers_of = {w: args.layers or WORKLOADS[w][1] for w in names}
     args.emb_of = {w: args.emb or WORKLOADS[w][2] for w in names}
     from gmp_amd import dist as gdist
@@ -536,7 +705,11 @@ def main():
         # the step on its own (non-default) stream, so that the weight-gradient side stream may be
         # CU-masked (gmp_amd.ops.SIDE_CUS: a masked stream is a blocking stream and would
         # serialise with the legacy default stream; ops uses it only off the default stream)
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+        # GMP_MAIN_PRIO=1: at the device's highest stream priority, so the critical path's
+        # kernels take free CUs ahead of the weight-gradient side stream's
+        prio = torch.cuda.Stream.priority_range()[1] if os.environ.get("GMP_MAIN_PRIO") == "1" \
+            else 0
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=prio))
     if args.blas != "default":
         torch.backends.cuda.preferred_blas_library(args.blas)
     from gmp_amd.graph import radius_graph
@@ -544,10 +717,18 @@ def main():
     g = radius_graph(num_nodes=args.nodes, target_edges=args.edges, seed=rank)
     recs = {}
     for k, w in enumerate(names):
-        steps, warmup = ((args.steps, args.warmup) if k == 0 else
-                         (min(args.steps, args.mace_steps), max(1, min(args.warmup,
-                                                                       args.mace_warmup))))
+        if k == 0:
+            steps, warmup = args.steps, args.warmup
+        elif w in ("mace", "tfn"):
+            steps = min(args.steps, args.mace_steps)
+            warmup = max(1, min(args.warmup, args.mace_warmup))
+        else:
+            steps, warmup = min(args.steps, 10), max(1, min(args.warmup, 2))
         recs[w] = run_workload(w, args, g, rank, world, dev, steps, warmup)
+    exact = None
+    if names[0] == "egnn" and not args.no_f32_exact:
+        exact = run_workload("egnn", args, g, rank, world, dev, min(args.steps, 5),
+                             max(1, min(args.warmup, 2)), exact=True)
     if rank == 0:
         main_rec = recs[names[0]]
         rec = {
@@ -563,6 +744,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "precision": "f32 storage and f32 accumulation throughout; products on split-operand "
+                         "MFMA: EGNN K4 and its dW2/dW3 sums 2-plane f16 (22-bit operands), "
+                         "the TP GEMMs and other weight sums 3-plane bf16 (24-bit); "
+                         "egnn_f32_exact is the EGNN rate with every product on the exact f32 "
+                         "MFMA",
             "data": "synthetic (seeded random radius graph per rank, random-init weights)",
             "config": {"fresh_graph": bool(args.fresh_graph), "workload": main_rec["workload"], "value_is": names[0],
                        "global_batch": world, "parallelism": f"dp{world}",
@@ -572,6 +758,9 @@ def main():
             "roofline": main_rec["roofline"],
             "cpu_baseline": None,
         }
+        if exact is not None:
+            rec["egnn_f32_exact"] = exact
+        rec["forward"] = main_rec.get("forward")
         for w in names[1:]:
             rec[w] = {k: v for k, v in recs[w].items()}
         if world == 1 and not args.no_cpu_baseline:

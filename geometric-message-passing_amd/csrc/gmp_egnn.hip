@@ -757,15 +757,16 @@ __device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowp
 }
 
 // ================================================================================== forward
-// SAVE (training): also write the three LayerNorm outputs x_hat1..3 (xsave, (3, E, d), rows in
-// receiver-sorted edge order) and their 1/std (rsave, (E, 3)) for the backward.
+// SAVE (training): also write the LayerNorm outputs x_hat1, x_hat2 (and x_hat3 when save_planes
+// is 3) into xsave ((save_planes, E, d), rows in receiver-sorted edge order) and their 1/std
+// (rsave, (E, 3)) for the backward.
 template <int D, int ACT, bool MSG_MEAN, bool SAVE, bool HF>
 __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egnn_fwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ AB, const float* __restrict__ pos,
     const int64_t* __restrict__ rowptr, const int64_t* __restrict__ recv,
     const int64_t* __restrict__ send, gmp_egnn_params P, float eps, int64_t n_waves,
     float* __restrict__ m_aggr, float* __restrict__ pos_aggr, float* __restrict__ xsave,
-    float* __restrict__ rsave, int save_mode) {
+    float* __restrict__ rsave, int save_planes) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2 = smem;
@@ -807,8 +808,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     const int i0 = __builtin_amdgcn_readfirstlane(c.i);
     const int i1 = __builtin_amdgcn_readlane(c.i, 15);
     const unsigned eoff = c.valid ? (unsigned)(li * D * 4) : kOob;
-    if (SAVE && (save_mode == 1 || save_mode == 2))
-      store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
+    if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
     affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
 
     f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
@@ -816,8 +816,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     if constexpr (HF) gemm_h2<D, false>(hW2, sw2, sx2, x, m, li, g);
     else gemm_wx<D>(sW2, x, m, li, g);
     const float r2 = ln_normalize<D>(m, eps);
-    if (SAVE && save_mode >= 1)
-      store_row_w<D, kAuxNT>(rows_window(xsave + ED, base, ne, D), eoff, m, g);
+    if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave + ED, base, ne, D), eoff, m, g);
     affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);
 
     // y3 = act(LN3(W3 m + b3)); s = w4 . y3 + b4   (x reused)
@@ -826,7 +825,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     else gemm_wx<D>(sW3, m, x, li, g);
     const float r3 = ln_normalize<D>(x, eps);
     if (SAVE) {
-      if (save_mode == 2)
+      if (save_planes == 3)
         store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
       store3_w<kAuxNT>(rows_window(rsave, base, ne, 3), (g == 0 && c.valid) ? li * 12u : kOob,
                        r1, r2, r3);
@@ -903,13 +902,10 @@ __device__ __forceinline__ float vslot(const float* sV, int v, int s, int g) {
 // AMAX: fold max |dpre2|, |dpre3| into amax[0], amax[1] (float bit patterns; the scales of the
 // HF weight-gradient outer sums, gmp_edge_outer_sum_act_hf_f32)
 // RC (what the backward recomputes instead of reading; bitwise the forward's values, with the
-// forward's saved 1/std and W2 / W3 from the W^T images by transposed reads):
-//   0: nothing (the forward saved x_hat1..3);
-//   1: x_hat3 from x_hat2 (the forward saved x_hat1, x_hat2);
-//   2: all three from the node projections AB (the forward saved only 1/std); x_hat1, x_hat2 are
-//      written to xw (the weight-gradient outer sums read them) and re-read from there;
-//   3: x_hat1 from AB (no product: LN1 of the gathered projections) and x_hat3 from x_hat2 (the
-//      forward saved x_hat2 only); x_hat1 is written to xw plane 0 and re-read from there.
+// forward's saved 1/std and W3 from the W3^T image by transposed reads):
+//   0: nothing (the forward saved x_hat1..3: save_planes 3);
+//   1: x_hat3 from x_hat2 (the forward saved x_hat1, x_hat2: save_planes 2, the default).
+// (r03 also measured rebuilding x_hat1 / x_hat2 from the node projections AB: slower, removed.)
 template <int D, int ACT, bool MSG_MEAN, bool HF, bool AMAX, int RC>
 __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     int64_t n_nodes, int64_t n_edges, const float* __restrict__ pos,
@@ -919,7 +915,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     const float* __restrict__ g_maggr, const float* __restrict__ g_paggr, float* __restrict__ dA,
     float* __restrict__ dpos_recv, float* __restrict__ dpre1_out, float* __restrict__ gdiff_out,
     float* __restrict__ dpre2_out, float* __restrict__ dpre3_out, float* __restrict__ partials,
-    unsigned* __restrict__ amax, const float* __restrict__ AB, float* __restrict__ xw) {
+    unsigned* __restrict__ amax) {
   constexpr int T = Cfg<D>::T, LDW = Cfg<D>::LDW, K = VecAcc<D>::K;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const float* sW2t = smem;  // W2^T
@@ -933,11 +929,9 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   else load_params_to_lds<D, true>(smem, P);
   __syncthreads();
   const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
-  const int sx2 = HF ? (int)sV[NV * D + 2] : 0;  // the forward's static W2 / W3 input exponents
-  const int sx3 = HF ? (int)sV[NV * D + 3] : 0;
-  // x_hat1 / x_hat2 as the rest of the body reads them (RC = 2: this kernel's own rows in xw)
-  const float* xr1 = RC >= 2 ? (const float*)xw : xsave;
-  const float* xr2 = (RC == 2 ? (const float*)xw : xsave) + (size_t)n_edges * D;
+  const int sx3 = HF ? (int)sV[NV * D + 3] : 0;  // the forward's static W3 input exponent
+  const float* xr1 = xsave;
+  const float* xr2 = xsave + (size_t)n_edges * D;
   // AMAX: per-chunk wave maxima go to two LDS words (no loop-carried registers: the kernel sits
   // at 256 VGPRs), folded into amax[] once per workgroup at the end
   unsigned* lmx = reinterpret_cast<unsigned*>(const_cast<float*>(sV) + NV * D + 10);
@@ -977,44 +971,14 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     const float rs3 = rsave[3 * (size_t)c.ec + 2];
     const float gp0 = g_paggr[3 * c.i + 0], gp1 = g_paggr[3 * c.i + 1], gp2 = g_paggr[3 * c.i + 2];
     f32x4 x[T], xh2[T], z[T];
-    if constexpr (RC == 2) {
-      load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);  // + edge_geom
-    } else if constexpr (RC == 3) {
-      load_row<D>(xh2, rowp(xsave + ED, c.ec, D), g);  // xhat2, in flight with the AB gathers
-      load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);  // + edge_geom
-    } else {
-      if constexpr (RC == 1) load_row<D>(x, rowp(xsave + ED, c.ec, D), g);  // x = xhat2
-      else load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);               // z = xhat3
-      __builtin_amdgcn_sched_barrier(0);
-      edge_geom(c);
-    }
+    if constexpr (RC == 1) load_row<D>(x, rowp(xsave + ED, c.ec, D), g);  // x = xhat2
+    else load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);               // z = xhat3
+    __builtin_amdgcn_sched_barrier(0);
+    edge_geom(c);
     const float rstd1 = c.valid ? rs1 : 0.f;
     const float rstd2 = c.valid ? rs2 : 0.f;
     const float rstd3 = c.valid ? rs3 : 0.f;
-    if constexpr (RC == 2) {
-      // xhat1 = LN1(pre1), xhat2 = LN2(W2 act(LN1 affine(xhat1)) + b2): the forward's chain
-      const int nw = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
-      const unsigned woff = c.valid ? (unsigned)(li * D * 4) : kOob;
-      ln_recenter<D>(x, rs1);
-      store_row_w<D, 0>(rows_window(xw, base, nw, D), woff, x, g);  // (L2: re-read below)
-      affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
-      load_vec<D>(z, sV, V_B2, g);
-      if constexpr (HF) gemm_h2_tr<D>(hW2t, sw2, sx2, x, z, lane, g);
-      else gemm_wtx<D>(sW2t, x, z, li, g);
-      ln_recenter<D>(z, rs2);
-      store_row_w<D, 0>(rows_window(xw + ED, base, nw, D), woff, z, g);
-#pragma unroll
-      for (int p = 0; p < T; ++p) x[p] = z[p];
-    }
-    if constexpr (RC == 3) {
-      const int nw = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
-      const unsigned woff = c.valid ? (unsigned)(li * D * 4) : kOob;
-      ln_recenter<D>(x, rs1);  // xhat1 = LN1(pre1): for the dW2 sum and the reload below
-      store_row_w<D, 0>(rows_window(xw, base, nw, D), woff, x, g);
-#pragma unroll
-      for (int p = 0; p < T; ++p) x[p] = xh2[p];
-    }
-    if constexpr (RC >= 1) {
+    if constexpr (RC == 1) {
       // z = xhat3 = LN3(W3 act(LN2 affine(xhat2)) + b3) with the forward's 1/std: the forward's
       // products (same operands, planes, scales and MFMA order) -> bitwise its x_hat3
       affine_act<D, ACT>(x, sV, V_LN2W, V_LN2B, g);
@@ -1180,11 +1144,6 @@ int64_t n_waves_for(int64_t n_edges, int nwb) {
 // 1: the f32-MFMA (exact fmaf chain) products instead of the HF path; initial value from
 // GMP_EGNN_F32_MFMA, changed by gmp_egnn_set_f32_mfma
 int g_egnn_f32 = -1;
-// which LayerNorm outputs the forward saves for the backward (gmp_egnn_set_xhat_mode,
-// GMP_EGNN_XHAT_MODE): 2 = x_hat1..3 (r02 form), 1 = x_hat1, x_hat2 (x_hat3 recomputed),
-// 0 = none (all recomputed from AB; the backward then needs AB and writes x_hat1, x_hat2),
-// 3 = x_hat2 (x_hat1 rebuilt from AB and written by the backward, x_hat3 recomputed)
-int g_xhat_mode = getenv("GMP_EGNN_XHAT_MODE") ? atoi(getenv("GMP_EGNN_XHAT_MODE")) : 1;
 
 bool egnn_f32() {
   if (g_egnn_f32 < 0) {
@@ -1203,7 +1162,8 @@ int prep_kernel(K k, size_t smem) {
 template <int D, int ACT, bool MEAN>
 int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const int64_t* rowptr,
                const int64_t* recv, const int64_t* send, const gmp_egnn_params& P, float eps,
-               float* m_aggr, float* pos_aggr, float* xsave, float* rsave, hipStream_t s) {
+               float* m_aggr, float* pos_aggr, float* xsave, int save_planes, float* rsave,
+               hipStream_t s) {
   const bool hf = !egnn_f32();
   const int nwb = hf ? fwd_waves<true>() : fwd_waves<false>();
   const int64_t W = n_waves_for(E, nwb);
@@ -1217,17 +1177,16 @@ int launch_fwd(int64_t N, int64_t E, const float* AB, const float* pos, const in
   if (rc) return rc;
   k<<<(unsigned)(W / nwb), nwb * 64, smem, s>>>(N, E, AB, pos, rowptr, recv, send, P,
                                                            eps, W, m_aggr, pos_aggr, xsave, rsave,
-                                                           g_xhat_mode);
+                                                           save_planes);
   return launch_status();
 }
 
 template <int D, int ACT, bool MEAN>
 int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
                const int64_t* recv, const int64_t* send, const gmp_egnn_params& P,
-               const float* xsave, const float* rsave, const float* gm, const float* gp,
-               float* dA, float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
-               float* dpre3, float* partials, unsigned* amax, const float* AB, float* xw,
-               hipStream_t s) {
+               const float* xsave, int save_planes, const float* rsave, const float* gm,
+               const float* gp, float* dA, float* dpos_recv, float* dpre1, float* gdiff,
+               float* dpre2, float* dpre3, float* partials, unsigned* amax, hipStream_t s) {
   const int64_t W = n_waves_for(E, kBwdWaves);
   const bool hf = !egnn_f32();
   const size_t smem = hf ? smem_total<D, kBwdWaves, true>() : smem_total<D, kBwdWaves, false>();
@@ -1236,16 +1195,14 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
               : egnn_bwd_kernel<D, ACT, MEAN, true, false, RC>)        \
       : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true, RC>         \
               : egnn_bwd_kernel<D, ACT, MEAN, false, false, RC>))
-  auto k = g_xhat_mode == 2 ? GMP_BWD_K(0)
-          : g_xhat_mode == 1 ? GMP_BWD_K(1)
-          : g_xhat_mode == 3 ? GMP_BWD_K(3) : GMP_BWD_K(2);
+  auto k = save_planes == 3 ? GMP_BWD_K(0) : GMP_BWD_K(1);
 #undef GMP_BWD_K
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / kBwdWaves), kBwdWaves * 64, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
                                                            xsave, rsave, gm, gp, dA, dpos_recv,
                                                            dpre1, gdiff, dpre2, dpre3, partials,
-                                                           amax, AB, xw);
+                                                           amax);
   return launch_status();
 }
 
@@ -1277,12 +1234,6 @@ using namespace gmp;
 
 extern "C" {
 
-int gmp_egnn_set_xhat_mode(int mode) {
-  const int prev = g_xhat_mode;
-  if (mode >= 0 && mode <= 3) g_xhat_mode = mode;
-  return prev;
-}
-
 int gmp_egnn_set_f32_mfma(int on) {
   const int prev = egnn_f32() ? 1 : 0;
   g_egnn_f32 = on ? 1 : 0;
@@ -1293,11 +1244,14 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
                           const float* pos, const int64_t* rowptr, const int64_t* recv,
                           const int64_t* send, const gmp_egnn_params* params, int act,
                           int msg_mean, float ln_eps, float* m_aggr, float* pos_aggr,
-                          float* save_xhat, float* save_rstd, void* stream) {
+                          float* save_xhat, int save_planes, float* save_rstd, void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
   GMP_CHECK_ARG(n_nodes < INT32_MAX && n_edges < INT32_MAX);  // 32-bit edge / node ids
   GMP_CHECK_ARG(params_ok(params) && m_aggr && pos_aggr && rowptr);
+  // training: save_rstd and save_xhat together, 2 (x_hat1, x_hat2) or 3 planes
+  GMP_CHECK_ARG((save_rstd == nullptr) == (save_xhat == nullptr));
+  GMP_CHECK_ARG(save_xhat == nullptr || save_planes == 2 || save_planes == 3);
   hipStream_t s = as_stream(stream);
   if (n_nodes == 0) return GMP_OK;
   int rc = hip_check(hipMemsetAsync(m_aggr, 0, n_nodes * d * sizeof(float), s));
@@ -1305,13 +1259,10 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
   if (rc || n_edges == 0) return rc;
   GMP_CHECK_ARG(AB && pos && recv && send && aligned16(AB) && aligned16(m_aggr));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
-  // training: save_rstd always, save_xhat unless x_hat mode 0 (nothing saved but 1/std)
-  GMP_CHECK_ARG(save_rstd != nullptr || save_xhat == nullptr);
-  GMP_CHECK_ARG(save_rstd == nullptr || g_xhat_mode == 0 || save_xhat != nullptr);
   GMP_CHECK_ARG(save_xhat == nullptr || aligned16(save_xhat));
 #define GMP_CALL_FWD(DD, AA, MM)                                                              \
   rc = launch_fwd<DD, AA, MM>(n_nodes, n_edges, AB, pos, rowptr, recv, send, *params, ln_eps, \
-                              m_aggr, pos_aggr, save_xhat, save_rstd, s)
+                              m_aggr, pos_aggr, save_xhat, save_planes, save_rstd, s)
   GMP_EGNN_DISPATCH(GMP_CALL_FWD);
 #undef GMP_CALL_FWD
   return rc;
@@ -1322,18 +1273,18 @@ int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d) {
   return n_waves_for(n_edges, kBwdWaves) / kBwdWaves;
 }
 
-int gmp_egnn_edge_bwd_ab_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
-                             const int64_t* rowptr, const int64_t* recv, const int64_t* send,
-                             const gmp_egnn_params* params, int act, int msg_mean,
-                             const float* AB, const float* save_xhat, const float* save_rstd,
-                             const float* g_m_aggr, const float* g_pos_aggr, float* dA,
-                             float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
-                             float* dpre3, float* vec_partials, uint32_t* amax, float* xhat12,
-                             void* stream) {
+int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
+                               const int64_t* rowptr, const int64_t* recv, const int64_t* send,
+                               const gmp_egnn_params* params, int act, int msg_mean,
+                               const float* save_xhat, int save_planes, const float* save_rstd,
+                               const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                               float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
+                               float* dpre3, float* vec_partials, uint32_t* amax, void* stream) {
   if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
   GMP_CHECK_ARG(n_nodes >= 0 && n_edges >= 0 && (act == 0 || act == 1));
   GMP_CHECK_ARG(n_nodes < INT32_MAX && n_edges < INT32_MAX);  // 32-bit edge / node ids
   GMP_CHECK_ARG(params_ok(params) && dA && dpos_recv && rowptr && vec_partials);
+  GMP_CHECK_ARG(save_planes == 2 || save_planes == 3);
   hipStream_t s = as_stream(stream);
   int rc = GMP_OK;
   if (n_nodes > 0) {
@@ -1346,48 +1297,31 @@ int gmp_egnn_edge_bwd_ab_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const 
         vec_partials, 0,
         gmp_egnn_edge_bwd_partials_rows(n_edges, d) * (8 * d + 1) * sizeof(float), s));
   }
-  GMP_CHECK_ARG(pos && recv && send && save_rstd && g_m_aggr && g_pos_aggr && dpre1 && gdiff &&
-                dpre2 && dpre3);
-  // mode 0 (nothing saved): the backward rebuilds x_hat1..3 from AB and writes x_hat1, x_hat2
-  GMP_CHECK_ARG((g_xhat_mode != 0 && g_xhat_mode != 3) ||
-                (AB && xhat12 && aligned16(AB) && aligned16(xhat12)));
-  GMP_CHECK_ARG(g_xhat_mode == 0 || save_xhat);
-  GMP_CHECK_ARG((!save_xhat || aligned16(save_xhat)) && aligned16(dA) && aligned16(g_m_aggr) &&
+  GMP_CHECK_ARG(pos && recv && send && save_xhat && save_rstd && g_m_aggr && g_pos_aggr &&
+                dpre1 && gdiff && dpre2 && dpre3);
+  GMP_CHECK_ARG(aligned16(save_xhat) && aligned16(dA) && aligned16(g_m_aggr) &&
                 aligned16(dpre1) && aligned16(dpre2) && aligned16(dpre3));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
 #define GMP_CALL_BWD(DD, AA, MM)                                                              \
   rc = launch_bwd<DD, AA, MM>(n_nodes, n_edges, pos, rowptr, recv, send, *params, save_xhat,  \
-                              save_rstd, g_m_aggr, g_pos_aggr, dA, dpos_recv, dpre1, gdiff,    \
-                              dpre2, dpre3, vec_partials, amax, AB, xhat12, s)
+                              save_planes, save_rstd, g_m_aggr, g_pos_aggr, dA, dpos_recv,    \
+                              dpre1, gdiff, dpre2, dpre3, vec_partials, amax, s)
   GMP_EGNN_DISPATCH(GMP_CALL_BWD);
 #undef GMP_CALL_BWD
   return rc;
 }
 
-int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
-                               const int64_t* rowptr, const int64_t* recv, const int64_t* send,
-                               const gmp_egnn_params* params, int act, int msg_mean,
-                               const float* save_xhat, const float* save_rstd,
-                               const float* g_m_aggr, const float* g_pos_aggr, float* dA,
-                               float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
-                               float* dpre3, float* vec_partials, uint32_t* amax, void* stream) {
-  return gmp_egnn_edge_bwd_ab_f32(n_nodes, n_edges, d, pos, rowptr, recv, send, params, act,
-                                  msg_mean, nullptr, save_xhat, save_rstd, g_m_aggr, g_pos_aggr,
-                                  dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, vec_partials, amax,
-                                  nullptr, stream);
-}
-
 int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
                           const int64_t* rowptr, const int64_t* recv, const int64_t* send,
                           const gmp_egnn_params* params, int act, int msg_mean,
-                          const float* save_xhat, const float* save_rstd, const float* g_m_aggr,
-                          const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
-                          float* gdiff, float* dpre2, float* dpre3, float* vec_partials,
-                          void* stream) {
+                          const float* save_xhat, int save_planes, const float* save_rstd,
+                          const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                          float* dpos_recv, float* dpre1, float* gdiff, float* dpre2, float* dpre3,
+                          float* vec_partials, void* stream) {
   return gmp_egnn_edge_bwd_amax_f32(n_nodes, n_edges, d, pos, rowptr, recv, send, params, act,
-                                    msg_mean, save_xhat, save_rstd, g_m_aggr, g_pos_aggr, dA,
-                                    dpos_recv, dpre1, gdiff, dpre2, dpre3, vec_partials, nullptr,
-                                    stream);
+                                    msg_mean, save_xhat, save_planes, save_rstd, g_m_aggr,
+                                    g_pos_aggr, dA, dpos_recv, dpre1, gdiff, dpre2, dpre3,
+                                    vec_partials, nullptr, stream);
 }
 
 }  // extern "C"

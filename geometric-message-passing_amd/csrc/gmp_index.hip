@@ -53,6 +53,25 @@ unsigned* stream_ticket(hipStream_t s) {
   return t;
 }
 
+unsigned* stream_ticket_block(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> blocks;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = blocks.find({dev, s});
+  if (it != blocks.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return nullptr;
+  if (blocks.size() >= 64) return nullptr;
+  unsigned* p = nullptr;
+  if (hipMalloc(&p, kTicketWords * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, kTicketWords * sizeof(unsigned)) != hipSuccess) return nullptr;
+  blocks[{dev, s}] = p;
+  return p;
+}
+
 namespace {
 
 constexpr size_t kAlign = 256;

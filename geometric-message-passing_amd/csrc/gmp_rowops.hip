@@ -193,6 +193,81 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
   if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
+// r04 form for d = 64 F (F = 1, 2, 4): lane l holds the F consecutive features F l .. F l + F - 1
+// of a row (one 4F-byte load per lane and tensor), each wave takes kRB4 rows per iteration (their
+// loads issued together) over a short grid-stride loop; the grid is sized to give every SIMD
+// several waves (r03's 256-workgroup grid ran one wave per SIMD through ~25 dependent rounds:
+// 70 us for 50k x 128).  [dgamma | dbeta] leaves through tree_finish (two-level last-workgroup
+// sums in fixed order) instead of a second kernel.
+constexpr int kRB4 = 4;
+template <int ACT, int F>
+__global__ __launch_bounds__(kRowT) void ln_act_bwd_vec_kernel(
+    int64_t rows, const float* __restrict__ gy, const float* __restrict__ xhat,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials,
+    float* __restrict__ grows, float* __restrict__ out_gb, unsigned* __restrict__ tickets) {
+  constexpr int D = 64 * F;
+  typedef float fv __attribute__((ext_vector_type(F)));
+  __shared__ float red[kRowT / 64][2 * D];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const fv gm = *reinterpret_cast<const fv*>(gamma + F * lane);
+  const fv bt = *reinterpret_cast<const fv*>(beta + F * lane);
+  fv dg = {}, db = {};
+  const int64_t stride = (int64_t)gridDim.x * (kRowT / 64) * kRB4;
+  for (int64_t r0 = ((int64_t)blockIdx.x * (kRowT / 64) + wv) * kRB4; r0 < rows; r0 += stride) {
+    float rs[kRB4];
+    fv xh[kRB4], gv[kRB4];
+#pragma unroll
+    for (int j = 0; j < kRB4; ++j) {
+      const int64_t r = r0 + j < rows ? r0 + j : rows - 1;  // clamped: loads stay in bounds
+      rs[j] = rstd_in[r];
+      xh[j] = *reinterpret_cast<const fv*>(xhat + r * D + F * lane);
+      gv[j] = *reinterpret_cast<const fv*>(gy + r * D + F * lane);
+    }
+#pragma unroll
+    for (int j = 0; j < kRB4; ++j) {
+      const int64_t r = r0 + j;
+      if (r >= rows) break;  // wave-uniform
+      fv g;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < F; ++k) {
+        const float dz = gv[j][k] * act_grad<ACT>(xh[j][k] * gm[k] + bt[k]);
+        dg[k] += dz * xh[j][k];
+        db[k] += dz;
+        g[k] = dz * gm[k];
+        a += g[k];
+        b += g[k] * xh[j][k];
+      }
+      a = wave_sum(a) * (1.f / D);
+      b = wave_sum(b) * (1.f / D);
+      fv o;
+#pragma unroll
+      for (int k = 0; k < F; ++k) o[k] = rs[j] * (g[k] - a - xh[j][k] * b);
+      *reinterpret_cast<fv*>(gx + r * D + F * lane) = o;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < F; ++k) {
+    red[wv][F * lane + k] = dg[k];
+    red[wv][D + F * lane + k] = db[k];
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < 2 * D; f += kRowT) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int w = 0; w < kRowT / 64; ++w) sacc += red[w][f];
+    partials[(int64_t)blockIdx.x * 2 * D + f] = sacc;
+  }
+  if (out_gb) tree_finish(partials, grows, (int)gridDim.x, 2 * D, out_gb, tickets);
+}
+
+// vec-kernel grid: ~16 rows per wave (four iterations of kRB4), at most 1024 workgroups
+int vec_blocks(int64_t rows) {
+  const int64_t b = ceil_div(rows, (kRowT / 64) * kRB4 * 4);
+  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
 // out[f] = sum over the partial rows (f < 2d: [dgamma | dbeta]) in a fixed order: thread
 // (column c, row group q) sums rows q, q + kSG, ... ; the kSG group sums are then added in
 // group order.  Deterministic.
@@ -234,6 +309,8 @@ __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __rest
 // [dgamma | dbeta] inside the backward kernel (last workgroup) with GMP_LN_FUSED_SUM=1; off by
 // default: measured 99.1 vs 101.0-101.6 M EGNN edges/s (the last workgroup sums 256 rows alone)
 int g_ln_fused_sum = getenv("GMP_LN_FUSED_SUM") ? atoi(getenv("GMP_LN_FUSED_SUM")) : 0;
+// GMP_LN_R03=1: the r03 one-wave-per-SIMD kernel + separate column sum (A/B)
+int g_ln_r03 = getenv("GMP_LN_R03") ? atoi(getenv("GMP_LN_R03")) : 0;
 // backward grid cap (GMP_LN_BWD_BLOCKS; A/B)
 int g_ln_blocks = getenv("GMP_LN_BWD_BLOCKS") ? atoi(getenv("GMP_LN_BWD_BLOCKS")) : kRowBlocks;
 int bwd_blocks(int64_t rows) {
@@ -268,7 +345,11 @@ int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gam
   return launch_status();
 }
 
+bool vec_form(int64_t d) { return d == 64 || d == 128 || d == 256; }
+
 size_t gmp_ln_act_bwd_workspace_size(int64_t rows, int64_t d) {
+  if (vec_form(d))  // partial rows + the tree_finish group rows
+    return (size_t)(vec_blocks(rows) + kTicketWords) * 2 * (size_t)d * sizeof(float);
   return (size_t)bwd_blocks(rows) * 2 * (size_t)d * sizeof(float);
 }
 
@@ -288,6 +369,25 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
   }
   GMP_CHECK_ARG(grad_y && xhat && rstd && gamma && beta && grad_x && workspace);
   if (workspace_bytes < gmp_ln_act_bwd_workspace_size(rows, d)) return GMP_ERR_WORKSPACE;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(grad_y) | reinterpret_cast<uintptr_t>(xhat) |
+                       reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
+                       reinterpret_cast<uintptr_t>(grad_x);
+  if (vec_form(d) && grad_gamma_beta && !g_ln_r03 && al % (d / 16) == 0) {
+    unsigned* tk = stream_ticket_block(s);
+    if (tk) {
+      const int GV = vec_blocks(rows);
+      float* grows = part + (size_t)GV * 2 * d;
+#define GMP_LNV(A, F)                                                                        \
+  ln_act_bwd_vec_kernel<A, F><<<GV, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, beta,    \
+                                                   grad_x, part, grows, grad_gamma_beta, tk)
+#define GMP_LNV_F(A) \
+  if (d == 64) GMP_LNV(A, 1); else if (d == 128) GMP_LNV(A, 2); else GMP_LNV(A, 4)
+      if (act == 0) { GMP_LNV_F(0); } else if (act == 1) { GMP_LNV_F(1); } else { GMP_LNV_F(2); }
+#undef GMP_LNV_F
+#undef GMP_LNV
+      return launch_status();
+    }
+  }
   // [dgamma | dbeta] by the kernel's last workgroup when a ticket is available (one launch);
   // otherwise (or GMP_LN_FUSED_SUM=0) the partial rows go through sum_rows_kernel
   unsigned* ticket = (grad_gamma_beta && g_ln_fused_sum) ? stream_ticket(s) : nullptr;

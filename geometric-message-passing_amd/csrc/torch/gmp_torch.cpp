@@ -226,8 +226,9 @@ void egnn_graph_checks(const Tensor& pos, const Tensor& rowptr, const Tensor& re
 std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(
     const Tensor& AB, const Tensor& pos, const Tensor& rowptr, const Tensor& recv,
     const Tensor& send, const std::vector<Tensor>& params, int64_t act, bool msg_mean, double eps,
-    bool train) {
+    bool train, int64_t xhat_planes) {
   OpGuard g(AB, "egnn_edge_fwd");
+  TORCH_CHECK(xhat_planes == 2 || xhat_planes == 3, "gmp.egnn_edge_fwd: xhat_planes is 2 or 3");
   f32(AB, "AB");
   egnn_graph_checks(pos, rowptr, recv, send);
   TORCH_CHECK(AB.dim() == 2 && AB.size(1) % 2 == 0 && AB.size(0) == pos.size(0),
@@ -235,38 +236,33 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(
   const int64_t N = pos.size(0), E = recv.numel(), d = AB.size(1) / 2;
   gmp_egnn_params P = egnn_params(params, d);
   Tensor m = at::empty({N, d}, fopt(AB)), pa = at::empty({N, 3}, fopt(AB));
-  // x_hat mode 0 (gmp_egnn_set_xhat_mode): the forward saves only 1/std (xhat is (0, E, d))
-  const bool save_x = train && gmp_egnn_set_xhat_mode(-1) != 0;
-  Tensor xh = at::empty({save_x ? 3 : 0, E, d}, fopt(AB)), rs = at::empty({train ? E : 0, 3}, fopt(AB));
+  // training: the saved LayerNorm outputs, exactly the planes the forward writes (x_hat1, x_hat2
+  // [, x_hat3]); the backward reads their count from xhat.size(0)
+  Tensor xh = at::empty({train ? xhat_planes : 0, E, d}, fopt(AB));
+  Tensor rs = at::empty({train ? E : 0, 3}, fopt(AB));
   check_rc(gmp_egnn_edge_fwd_f32(N, E, d, fp(AB), fp(pos), ip(rowptr), ip(recv), ip(send), &P,
                                  (int)act, msg_mean, (float)eps, fp(m), fp(pa),
-                                 save_x ? fp(xh) : nullptr, train ? fp(rs) : nullptr, cur_stream()),
+                                 train ? fp(xh) : nullptr, (int)xhat_planes,
+                                 train ? fp(rs) : nullptr, cur_stream()),
            "gmp_egnn_edge_fwd_f32");
   return {m, pa, xh, rs};
 }
 
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
     const Tensor& pos, const Tensor& rowptr, const Tensor& recv, const Tensor& send,
     const std::vector<Tensor>& params, int64_t act, bool msg_mean, const Tensor& xhat,
-    const Tensor& rstd, const Tensor& g_m, const Tensor& g_p, const optional<Tensor>& amax,
-    const optional<Tensor>& AB) {
+    const Tensor& rstd, const Tensor& g_m, const Tensor& g_p, const optional<Tensor>& amax) {
   OpGuard g(pos, "egnn_edge_bwd");
   egnn_graph_checks(pos, rowptr, recv, send);
   f32(xhat, "xhat");
   f32(rstd, "rstd");
   f32(g_m, "g_m_aggr");
   f32(g_p, "g_pos_aggr");
-  TORCH_CHECK(xhat.dim() == 3, "gmp.egnn_edge_bwd: xhat must be (3 or 0, E, d)");
+  // the forward's saved planes: (2, E, d) = x_hat1, x_hat2 (x_hat3 recomputed), or (3, E, d)
+  TORCH_CHECK(xhat.dim() == 3 && (xhat.size(0) == 2 || xhat.size(0) == 3),
+              "gmp.egnn_edge_bwd: xhat must be the forward's (2 or 3, E, d) planes");
   const int64_t N = pos.size(0), E = recv.numel(), d = xhat.size(2);
-  const int mode = gmp_egnn_set_xhat_mode(-1);
-  const bool rebuild = mode == 0 || mode == 3;  // x_hat1 (mode 0: x_hat1..3) rebuilt from AB
-  shape(xhat, {mode == 0 ? xhat.size(0) : 3, E, d}, "xhat");
-  TORCH_CHECK(xhat.size(0) == 3 || xhat.size(0) == 0, "gmp.egnn_edge_bwd: xhat (3 or 0, E, d)");
-  if (rebuild) {
-    TORCH_CHECK(AB.has_value(), "gmp.egnn_edge_bwd: x_hat modes 0 / 3 need the forward's AB");
-    f32(*AB, "AB");
-    shape(*AB, {N, 2 * d}, "AB");
-  }
+  shape(xhat, {xhat.size(0), E, d}, "xhat");
   shape(rstd, {E, 3}, "rstd");
   shape(g_m, {N, d}, "g_m_aggr");
   shape(g_p, {N, 3}, "g_pos_aggr");
@@ -279,17 +275,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_
   Tensor dA = at::empty({N, d}, o), dpr = at::empty({N, 3}, o), dp1 = at::empty({E, d}, o);
   Tensor gd = at::empty({E, 3}, o), dp2 = at::empty({E, d}, o), dp3 = at::empty({E, d}, o);
   Tensor part = at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o);
-  // x_hat1 (, x_hat2) as rebuilt by the backward (modes 3 / 0; else empty: the forward's xhat)
-  Tensor x12 = at::empty({mode == 0 ? 2 : (mode == 3 ? 1 : 0), E, d}, o);
-  check_rc(gmp_egnn_edge_bwd_ab_f32(
+  check_rc(gmp_egnn_edge_bwd_amax_f32(
                N, E, d, fp(pos), ip(rowptr), ip(recv), ip(send), &P, (int)act, msg_mean,
-               rebuild ? fp(*AB) : nullptr, xhat.numel() ? fp(xhat) : nullptr, fp(rstd), fp(g_m),
-               fp(g_p), fp(dA), fp(dpr), fp(dp1), fp(gd), fp(dp2), fp(dp3), fp(part),
+               E > 0 ? fp(xhat) : nullptr, (int)xhat.size(0), fp(rstd), fp(g_m), fp(g_p), fp(dA),
+               fp(dpr), fp(dp1), fp(gd), fp(dp2), fp(dp3), fp(part),
                amax.has_value() ? reinterpret_cast<uint32_t*>(amax->data_ptr<int32_t>())
                                 : nullptr,
-               rebuild ? fp(x12) : nullptr, cur_stream()),
-           "gmp_egnn_edge_bwd_ab_f32");
-  return {dA, dpr, dp1, gd, dp2, dp3, part, x12};
+               cur_stream()),
+           "gmp_egnn_edge_bwd_amax_f32");
+  return {dA, dpr, dp1, gd, dp2, dp3, part};
 }
 
 // ------------------------------------------------------------------ SchNet CFConv, SSP
@@ -676,9 +670,20 @@ TpDescHost tp_desc(at::IntArrayRef d) {
   return h;
 }
 
+// l_max the z / dz kernels are instantiated for: it must cover every input block's l and the SH
+// order (sh_dim = (l_sh + 1)^2), else the l <= 2 instantiation would skip an l = 3 path and leave
+// its z rows unwritten
 int tp_lmax(at::IntArrayRef d) {
   const int l = d.size() == 26 ? (int)d[25] : 3;
   TORCH_CHECK(0 <= l && l <= 3, "gmp.tp: l_max in 0..3");
+  const TpDescHost h = tp_desc(d);
+  TORCH_CHECK(0 < h.n_blocks && h.n_blocks <= 6, "gmp.tp: 1..6 input blocks");
+  for (int k = 0; k < h.n_blocks; ++k)
+    TORCH_CHECK(h.blk_l[k] <= l, "gmp.tp: l_max ", l, " below input block l ", h.blk_l[k]);
+  int l_sh = 0;
+  while ((l_sh + 1) * (l_sh + 1) < h.sh_dim) ++l_sh;
+  TORCH_CHECK((l_sh + 1) * (l_sh + 1) == h.sh_dim, "gmp.tp: sh_dim must be (l + 1)^2");
+  TORCH_CHECK(l_sh <= l, "gmp.tp: l_max ", l, " below the spherical-harmonics order ", l_sh);
   return l;
 }
 
@@ -889,6 +894,33 @@ Tensor tp_node_dw(const Tensor& eoff, const Tensor& Z, const Tensor& A, const Te
                               ws.data_ptr(), ws_b, cur_stream()),
            "gmp_tp_node_dw_f32");
   return dW;
+}
+
+// forward of one path with S built in-kernel (K7s): C[c_offset + n cldg + w d3 + k] += ...
+void tp_node_fwd_fused(const Tensor& eoff, const Tensor& Z, const Tensor& A, const Tensor& Bf,
+                       int64_t d3, int64_t mul1, int64_t mul_out, Tensor C, int64_t c_offset,
+                       int64_t cldg) {
+  OpGuard g(Z, "tp_node_fwd_fused");
+  i64(eoff, "eoff");
+  f32(Z, "Z");
+  f32(A, "A");
+  f32(C, "C");
+  need(Bf, at::kShort, "B planes");
+  TORCH_CHECK(eoff.dim() == 1 && eoff.numel() >= 1, "gmp.tp_node_fwd_fused: eoff (n_recv + 1)");
+  const int64_t n = eoff.numel() - 1;
+  TORCH_CHECK(A.dim() == 2 && Z.dim() == 2 && Z.size(1) == d3 * mul1 && Z.size(0) >= A.size(0),
+              "gmp.tp_node_fwd_fused: Z (edges, d3 mul1), A (edges, H)");
+  const int64_t H = A.size(1);
+  TORCH_CHECK(Bf.numel() >= 3 * mul_out * (mul1 * H + mul1),
+              "gmp.tp_node_fwd_fused: B planes hold 3 mul_out (mul1 H + mul1)");
+  TORCH_CHECK(c_offset >= 0 && cldg > 0, "gmp.tp_node_fwd_fused: epilogue addressing");
+  if (n > 0)
+    TORCH_CHECK(c_offset + (n - 1) * cldg + (mul_out - 1) * d3 + d3 - 1 < C.numel(),
+                "gmp.tp_node_fwd_fused: the output block exceeds C");
+  check_rc(gmp_tp_node_fwd_fused_f32(n, d3, mul1, H, mul_out, ip(eoff), fp(Z), fp(A),
+                                     Bf.data_ptr(), C.data_ptr<float>() + c_offset, cldg,
+                                     cur_stream()),
+           "gmp_tp_node_fwd_fused_f32");
 }
 
 // three bf16 planes of the (N x K) operand B = W (transpose = false: rows n of W) or W^T
@@ -1260,24 +1292,22 @@ Tensor segment_reduce_bwd(const Tensor& grad_out, const Tensor&, const Tensor&, 
 std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(const Tensor& AB, const Tensor& pos,
                                                          const Tensor&, const Tensor& recv,
                                                          const Tensor&, const std::vector<Tensor>&,
-                                                         int64_t, bool, double, bool train) {
+                                                         int64_t, bool, double, bool train,
+                                                         int64_t xhat_planes) {
   const int64_t N = pos.size(0), E = recv.numel(), d = AB.size(1) / 2;
   auto o = AB.options();
-  const bool save_x = train && gmp_egnn_set_xhat_mode(-1) != 0;
-  return {at::empty({N, d}, o), at::empty({N, 3}, o), at::empty({save_x ? 3 : 0, E, d}, o),
-          at::empty({train ? E : 0, 3}, o)};
+  return {at::empty({N, d}, o), at::empty({N, 3}, o),
+          at::empty({train ? xhat_planes : 0, E, d}, o), at::empty({train ? E : 0, 3}, o)};
 }
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
     const Tensor& pos, const Tensor&, const Tensor& recv, const Tensor&,
     const std::vector<Tensor>&, int64_t, bool, const Tensor& xhat, const Tensor&, const Tensor&,
-    const Tensor&, const optional<Tensor>&, const optional<Tensor>&) {
+    const Tensor&, const optional<Tensor>&) {
   const int64_t N = pos.size(0), E = recv.numel(), d = xhat.size(2);
   auto o = pos.options();
   return {at::empty({N, d}, o), at::empty({N, 3}, o), at::empty({E, d}, o), at::empty({E, 3}, o),
           at::empty({E, d}, o), at::empty({E, d}, o),
-          at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o),
-          at::empty({gmp_egnn_set_xhat_mode(-1) == 0 ? 2 : (gmp_egnn_set_xhat_mode(-1) == 3 ? 1 : 0),
-                     E, d}, o)};
+          at::empty({gmp_egnn_edge_bwd_partials_rows(E, d), 8 * d + 1}, o)};
 }
 Tensor cfconv_aggregate(const Tensor& x, const Tensor&, const Tensor&, const Tensor&,
                         const Tensor&, int64_t n_seg, const optional<Tensor>&) {
@@ -1393,6 +1423,8 @@ Tensor tp_node_dw(const Tensor&, const Tensor&, const Tensor& A, const Tensor& G
                   int64_t mul1) {
   return at::empty({mul1 * A.size(1), G.size(1)}, A.options());
 }
+void tp_node_fwd_fused(const Tensor&, const Tensor&, const Tensor&, const Tensor&, int64_t,
+                       int64_t, int64_t, Tensor, int64_t, int64_t) {}
 Tensor split_x3(const Tensor& W, bool) {
   return at::empty({3 * W.numel()}, W.options().dtype(at::kShort));
 }
@@ -1457,13 +1489,12 @@ TORCH_LIBRARY(gmp, m) {
   m.def("segment_reduce_bwd(Tensor grad_out, Tensor index, Tensor rowptr, str reduce, "
         "Tensor? argmax, int n_items) -> Tensor");
   m.def("egnn_edge_fwd(Tensor AB, Tensor pos, Tensor rowptr, Tensor recv, Tensor send, "
-        "Tensor[] params, int act, bool msg_mean, float eps, bool train) -> "
+        "Tensor[] params, int act, bool msg_mean, float eps, bool train, int xhat_planes=2) -> "
         "(Tensor m_aggr, Tensor pos_aggr, Tensor xhat, Tensor rstd)");
   m.def("egnn_edge_bwd(Tensor pos, Tensor rowptr, Tensor recv, Tensor send, Tensor[] params, "
         "int act, bool msg_mean, Tensor xhat, Tensor rstd, Tensor g_m_aggr, Tensor g_pos_aggr, "
-        "Tensor(a!)? amax=None, Tensor? AB=None) -> (Tensor dA, Tensor dpos_recv, "
-        "Tensor dpre1, Tensor gdiff, Tensor dpre2, Tensor dpre3, Tensor partials, "
-        "Tensor xhat12)");
+        "Tensor(a!)? amax=None) -> (Tensor dA, Tensor dpos_recv, "
+        "Tensor dpre1, Tensor gdiff, Tensor dpre2, Tensor dpre3, Tensor partials)");
   m.def("cfconv_aggregate(Tensor x, Tensor xidx, Tensor w, Tensor perm, Tensor rowptr, "
         "int n_seg, Tensor? escale=None) -> Tensor");
   m.def("cfconv_wgrad(Tensor g, Tensor gidx, Tensor x, Tensor xidx, Tensor? escale=None) -> "
@@ -1519,6 +1550,8 @@ TORCH_LIBRARY(gmp, m) {
   m.def("tp_gemm_x3_widen(Tensor A, Tensor Bp, int N) -> Tensor");
   m.def("split_x3(Tensor W, bool transpose) -> Tensor");
   m.def("tp_node_dw(Tensor eoff, Tensor Z, Tensor A, Tensor G, int d3, int mul1) -> Tensor");
+  m.def("tp_node_fwd_fused(Tensor eoff, Tensor Z, Tensor A, Tensor Bf, int d3, int mul1, "
+        "int mul_out, Tensor(a!) C, int c_offset, int cldg) -> ()");
   m.def("gemm_x3(Tensor A1, Tensor? A2, Tensor Bp, int N, Tensor? bias) -> Tensor");
   m.def("outer_sum_cols(Tensor A, Tensor B) -> Tensor");
   m.def("edge_outer_sum(Tensor A, Tensor B) -> (Tensor C, Tensor colsum)");
@@ -1574,6 +1607,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("tp_gemm_x3_widen", ns tp_gemm_x3_widen);                        \
   m.impl("split_x3", ns split_x3);                                        \
   m.impl("tp_node_dw", ns tp_node_dw);                                    \
+  m.impl("tp_node_fwd_fused", ns tp_node_fwd_fused);                      \
   m.impl("gemm_x3", ns gemm_x3);                                          \
   m.impl("outer_sum_cols", ns outer_sum_cols);                            \
   m.impl("edge_outer_sum", ns edge_outer_sum);                            \

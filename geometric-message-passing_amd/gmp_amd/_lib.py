@@ -67,10 +67,9 @@ SIGNATURES = {
                                            c_vp, c_vp]),
     "gmp_egnn_edge_fwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_f32, c_vp,
-                                      c_vp, c_vp, c_vp, c_vp]),
+                                      c_vp, c_vp, c_int, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
     "gmp_egnn_set_f32_mfma": (c_int, [c_int]),
-    "gmp_egnn_set_xhat_mode": (c_int, [c_int]),
     "gmp_wgrad_set_grid_cap": (c_int, [c_int]),
     "gmp_stream_create_cu_share": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "gmp_stream_destroy": (c_int, [c_vp]),
@@ -99,12 +98,9 @@ SIGNATURES = {
                                             c_i64, c_vp, c_vp, c_vp]),
     "gmp_edge_outer_sum_act_hf_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,
                                               c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
-    "gmp_egnn_edge_bwd_ab_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                         c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_amax_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                           c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                           c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_gate_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp]),
     "gmp_gate_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
                                  c_vp]),
@@ -147,6 +143,8 @@ SIGNATURES = {
     "gmp_tp_split_w2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_split_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "gmp_tp_node_dw_workspace_size": (c_size, [c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "gmp_tp_node_fwd_fused_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp,
+                                          c_vp, c_vp, c_i64, c_vp]),
     "gmp_tp_node_dw_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
                                    c_vp, c_vp, c_size, c_vp]),
     "gmp_gemm_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp,
@@ -186,9 +184,13 @@ SIGNATURES = {
     "gmp_symmetric_contraction_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
-                                      ctypes.POINTER(GmpEgnnParams), c_int, c_int] + [c_vp] * 12),
+                                      ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_vp, c_int]
+                              + [c_vp] * 11),
 }
 
+# include/gmp.h GMP_ABI_VERSION (2: r04 — EGNN save_planes arguments, the x_hat mode global and
+# gmp_egnn_edge_bwd_ab_f32 removed; r03's torsion_kn argument of gmp_triplet_fill_f32)
+ABI_VERSION = 2
 _lib = None
 TORCH_LIB_PATH = os.environ.get("GMP_TORCH_LIB", os.path.join(_HERE, "libgmp_torch.so"))
 _torch_ops = None
@@ -227,7 +229,7 @@ def load(path=None):
         fn = getattr(lib, name)  # AttributeError if the symbol is not exported
         fn.restype = res
         fn.argtypes = args
-    if lib.gmp_abi_version() != 1:
+    if lib.gmp_abi_version() != ABI_VERSION:
         raise GmpError("libgmp ABI version mismatch")
     if path is None:
         _lib = lib

@@ -580,6 +580,18 @@ def _dw_fused_ok(P, H):
             and P["mul_out"] in (64, 128))
 
 
+# K7s (gmp_tpfwd.hip): the forward's path contraction with S built inside the GEMM (S never in
+# HBM: 66 GB of S writes + reads per MACE-128 lo = 2 path avoided); lo >= 1 paths of the K7g
+# shapes (the lo = 0 paths keep the S kernel + K7g GEMM: d3 = 1 would leave 15 of 16 S-MFMA rows
+# idle).  GMP_TP_FWD_FUSED=0 restores the unfused forward.
+TP_FWD_FUSED = os.environ.get("GMP_TP_FWD_FUSED", "1") == "1"
+
+
+def _fwd_fused_ok(P, H):
+    return (TP_FWD_FUSED and 2 * P["lo"] + 1 in (3, 5, 7) and P["mul1"] % 32 == 0
+            and P["mul_out"] in (64, 128) and H % 32 == 0)
+
+
 def _split_w2(W2, b2, P, fwd):
     """Three bf16 planes of path P's W2 / b2 block: forward (B = [W2p | b2p]^T as [w][(u, j) ++ u])
     or backward (B = W2p as [(u, j)][w]) layout (torch.ops.gmp.tp_split_w2)."""
@@ -618,8 +630,16 @@ class TPConvNodeFn(torch.autograd.Function):
             for i, (P, (zoff, w)) in enumerate(zip(plan.instructions, plan.z_regions)):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
-                S, Sb = _node_outer(eoff, Zp, a, w)
                 blk = plan.blocks[P["io"]]
+                if x3[i] and _fwd_fused_ok(P, H):
+                    # K7s: S built in-kernel, accumulated into the receivers' output block
+                    if Bfs[i] is None:
+                        Bfs[i] = _split_w2(W2c, b2c, P, True)
+                    with _timed("tp_node_W"):
+                        tops.tp_node_fwd_fused(eoff, Zp, a, Bfs[i], d3, m1, mo, out,
+                                               n0 * out.shape[1] + blk[0], out.shape[1])
+                    continue
+                S, Sb = _node_outer(eoff, Zp, a, w)
                 if x3[i]:
                     # out[n, blk + w' d3 + k] += [S | Sb][(n, k), :] [W2p ; b2p][:, w'] (K7g)
                     if Bfs[i] is None:

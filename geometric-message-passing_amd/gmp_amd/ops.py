@@ -629,7 +629,9 @@ def gather(src, index, dim=0):
 _CHECKED_CSR = []  # CSRs whose build-time range flag was already read (once per graph)
 
 
-def _cfconv_csr(index, n):
+def checked_csr(index, n):
+    """get_csr plus the build's out-of-range flag read once per new graph (one host sync, as
+    torch_scatter raises for an index outside the output rows fixed by dim_size / out=)."""
     csr = get_csr(index, n)
     if compiling():
         return csr
@@ -638,6 +640,9 @@ def _cfconv_csr(index, n):
         _CHECKED_CSR.insert(0, csr)
         del _CHECKED_CSR[32:]
     return csr
+
+
+_cfconv_csr = checked_csr
 
 
 def cfconv_aggregate(x, xidx, w, csr, escale=None):
@@ -827,6 +832,11 @@ def _egnn_params(tensors):
 
 # EGNN dW2 / dW3 on the HF outer sums (two scaled fp16 planes; "0": split-plane x3)
 EGNN_WGRAD_HF = os.environ.get("GMP_EGNN_WGRAD_HF", "1") != "0"
+# LayerNorm outputs the EGNN forward saves for the backward: 2 = x_hat1, x_hat2 (x_hat3 recomputed
+# in the backward, bitwise the forward's; default), 3 = x_hat1..3 (the r02 form, for A/B).  The
+# backward follows the saved tensor's plane count, so changing this between a forward and its
+# backward is harmless.
+EGNN_XHAT_PLANES = int(os.environ.get("GMP_EGNN_XHAT_PLANES", "2"))
 
 
 class EgnnMessageFn(torch.autograd.Function):
@@ -858,18 +868,16 @@ class EgnnMessageFn(torch.autograd.Function):
         with _timed("egnn_edge_fwd"):
             m_aggr, pos_aggr, xhat, rstd = _lib.torch_ops().egnn_edge_fwd(
                 AB, pos, graph.rowptr, graph.recv, graph.send, list(params), _lib.ACT[act],
-                bool(msg_mean), float(eps), train)
+                bool(msg_mean), float(eps), train, EGNN_XHAT_PLANES)
         ctx.graph, ctx.act, ctx.msg_mean, ctx.N = graph, act, msg_mean, N
         if train:
-            # AB: the backward rebuilds the LayerNorm outputs from it when the forward saved none
-            # (x_hat mode 0, gmp_egnn_set_xhat_mode; 51 MB at C2 against 1 GB of x_hat1, x_hat2)
-            ctx.save_for_backward(h, pos, xhat, rstd, AB, W1, *params)
+            ctx.save_for_backward(h, pos, xhat, rstd, W1, *params)
         return m_aggr, pos_aggr
 
     @staticmethod
     @once_differentiable
     def backward(ctx, g_m, g_p):
-        h, pos, xhat, rstd, AB, W1, *params = ctx.saved_tensors
+        h, pos, xhat, rstd, W1, *params = ctx.saved_tensors
         graph = ctx.graph
         N, d = ctx.N, xhat.shape[2]
         E = graph.num_edges
@@ -881,14 +889,11 @@ class EgnnMessageFn(torch.autograd.Function):
         # two device words that scale their fp16 planes
         amax = torch.zeros(2, dtype=torch.int32, device=dev) if EGNN_WGRAD_HF else None
         with _timed("egnn_edge_bwd"):
-            dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, partials, x12 = \
+            dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, partials = \
                 _lib.torch_ops().egnn_edge_bwd(pos, graph.rowptr, graph.recv, graph.send,
                                                list(params), _lib.ACT[ctx.act],
-                                               bool(ctx.msg_mean), xhat, rstd, g_m, g_p, amax, AB)
-        # x_hat1, x_hat2 for the dW2 / dW3 sums: the forward's, or rebuilt by the backward
-        # (x_hat mode 0: both; mode 3: x_hat1)
-        xh1 = x12[0] if x12.shape[0] >= 1 else xhat[0]
-        xh2 = x12[1] if x12.shape[0] == 2 else xhat[1]
+                                               bool(ctx.msg_mean), xhat, rstd, g_m, g_p, amax)
+        xh1, xh2 = xhat[0], xhat[1]  # for the dW2 / dW3 sums
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
@@ -903,7 +908,7 @@ class EgnnMessageFn(torch.autograd.Function):
 
         # weight gradients: side stream, accumulated at the end of the backward pass
         (_, b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3, b3, ln3w, ln3b, w4, b4) = params
-        with side_work(h, dA, dB, dpre2, dpre3, xhat, x12, partials, amax) as sw:
+        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials, amax) as sw:
             dW1 = torch.empty((d, 2 * d + 1), **f)
             db1 = torch.empty(d, **f)
             outer_sum_into(dA, h, dW1[:, :d], db1)

@@ -23,6 +23,13 @@ def _rows(index, dim_size):
     return int(index.max().item()) + 1 if index.numel() else 0
 
 
+def _csr(index, n, fixed):
+    """The segment CSR of `index`; when out= or dim_size fixes the row count, an index outside it
+    raises IndexError (checked once per graph), as torch_scatter does — max(index) + 1 rows
+    cannot be exceeded."""
+    return ops.checked_csr(index, n) if fixed else ops.get_csr(index, n)
+
+
 def _bcast(v, like, dim):
     """(n,) per-row values broadcast along `dim` of `like`."""
     shp = [1] * like.dim()
@@ -44,7 +51,7 @@ def scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum"):
     x = src.movedim(dim, 0)
     shp = x.shape
     x2 = x.reshape(shp[0], -1)
-    csr = ops.get_csr(index, n)
+    csr = _csr(index, n, out is not None or dim_size is not None)
     red = "sum" if reduce == "add" else reduce
     if out is None:
         return ops.SegmentReduceFn.apply(x2, csr, red).reshape((n,) + tuple(shp[1:])).movedim(0,
@@ -75,7 +82,7 @@ def _scatter_arg(src, index, dim, dim_size, reduce, out=None):
     x = src.movedim(dim, 0)
     shp = x.shape
     x2 = x.reshape(shp[0], -1)
-    csr = ops.get_csr(index, n)
+    csr = _csr(index, n, out is not None or dim_size is not None)
     if reduce == "min":
         o, arg = ops.SegmentMaxFn.apply(-x2, csr)
         o = 0.0 - o  # (+0 for empty rows, not -0)

@@ -26,7 +26,9 @@
 extern "C" {
 #endif
 
-#define GMP_ABI_VERSION 1
+/* 2 (r04): EGNN forward / backward take save_planes; gmp_egnn_set_xhat_mode and
+ * gmp_egnn_edge_bwd_ab_f32 removed.  (r03 changed gmp_triplet_fill_f32 under version 1.) */
+#define GMP_ABI_VERSION 2
 
 enum {
   GMP_OK = 0,
@@ -120,32 +122,25 @@ typedef struct gmp_egnn_params {
   const float* b4;   /* (1)  mlp_pos.3.bias   */
 } gmp_egnn_params;
 
-/* save_xhat / save_rstd: NULL (inference) or, for training, (3, E, d) and (E, 3) buffers that
- * receive the three LayerNorm outputs x_hat1..3 and their 1/std per edge (receiver-sorted rows)
- * for gmp_egnn_edge_bwd_f32. */
+/* save_xhat / save_rstd: both NULL (inference) or, for training, (save_planes, E, d) and (E, 3)
+ * buffers that receive the LayerNorm outputs and their 1/std per edge (receiver-sorted rows) for
+ * gmp_egnn_edge_bwd_f32: save_planes = 2 (default form) stores x_hat1, x_hat2 — the backward
+ * recomputes x_hat3 from x_hat2 and the saved 1/std, bitwise the forward's value; 3 also stores
+ * x_hat3.  The backward takes the same save_planes (the caller keeps it with the buffer). */
 /* The two d x d products per edge chunk run by default on the f16 MFMA over 2-plane (hi + lo)
  * splits of the operands with power-of-two scaling (22-bit operands, f32 accumulation; relative
  * error ~2^-21 per product); gmp_egnn_set_f32_mfma(1) (or GMP_EGNN_F32_MFMA=1 at load) selects
  * the exact f32-MFMA fmaf chains.  Returns the previous setting. */
 int gmp_egnn_set_f32_mfma(int on);
-/* Which LayerNorm outputs the forward saves for the backward (mode 2 = x_hat1..3 into save_xhat
- * planes 0..2; 1 (default) = x_hat1, x_hat2 — the backward recomputes x_hat3 from x_hat2 and the
- * saved 1/std, bitwise the forward's value; 0 = none, save_xhat may be NULL — the backward
- * rebuilds all three from the node projections AB (gmp_egnn_edge_bwd_ab_f32 only) and writes
- * x_hat1, x_hat2 to its xhat12 output for the weight-gradient sums).  Set it before the forward
- * whose buffers a backward consumes; 3 = x_hat2 only — the _ab backward rebuilds x_hat1 from AB
- * (no product) into xhat12 plane 0 and recomputes x_hat3.  Returns the previous mode (mode
- * outside 0..3: query only;
- * initial value from GMP_EGNN_XHAT_MODE). */
-int gmp_egnn_set_xhat_mode(int mode);
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
                           const float* pos, const int64_t* rowptr, const int64_t* recv,
                           const int64_t* send, const gmp_egnn_params* params, int act,
                           int msg_mean, float ln_eps, float* m_aggr, float* pos_aggr,
-                          float* save_xhat, float* save_rstd, void* stream);
+                          float* save_xhat, int save_planes, float* save_rstd, void* stream);
 
 /* Backward of gmp_egnn_edge_fwd_f32 from its saved x_hat / rstd (no forward recompute).
- * Inputs g_m_aggr (N,d), g_pos_aggr (N,3).  Outputs:
+ * Inputs g_m_aggr (N,d), g_pos_aggr (N,3), the forward's save_xhat (save_planes, E, d) and
+ * save_rstd (E, 3).  Outputs:
  *   dA        (N,d)  receiver part of d(AB)[:, :d]   (segment-summed in-kernel)
  *   dpos_recv (N,3)  receiver part of d(pos)          (segment-summed in-kernel)
  *   per edge, in receiver-sorted order (row e):
@@ -162,28 +157,17 @@ int64_t gmp_egnn_edge_bwd_partials_rows(int64_t n_edges, int64_t d);
 int gmp_egnn_edge_bwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
                           const int64_t* rowptr, const int64_t* recv, const int64_t* send,
                           const gmp_egnn_params* params, int act, int msg_mean,
-                          const float* save_xhat, const float* save_rstd, const float* g_m_aggr,
-                          const float* g_pos_aggr, float* dA, float* dpos_recv, float* dpre1,
-                          float* gdiff, float* dpre2, float* dpre3, float* vec_partials,
-                          void* stream);
+                          const float* save_xhat, int save_planes, const float* save_rstd,
+                          const float* g_m_aggr, const float* g_pos_aggr, float* dA,
+                          float* dpos_recv, float* dpre1, float* gdiff, float* dpre2, float* dpre3,
+                          float* vec_partials, void* stream);
 /* As gmp_egnn_edge_bwd_f32, also folding max |dpre2| and max |dpre3| into amax[0], amax[1]
  * (float bit patterns, atomic max; caller zeroes): the A scales of the HF weight-gradient outer
  * sums (gmp_edge_outer_sum_act_hf_f32). */
-/* Backward with the node projections AB (N, 2d) of the forward (x_hat mode 0: the LayerNorm
- * outputs are rebuilt from them) and xhat12 (2, E, d) receiving x_hat1, x_hat2 in that mode
- * (AB / xhat12 may be NULL in modes 1, 2).  Other arguments as gmp_egnn_edge_bwd_amax_f32. */
-int gmp_egnn_edge_bwd_ab_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
-                             const int64_t* rowptr, const int64_t* recv, const int64_t* send,
-                             const gmp_egnn_params* params, int act, int msg_mean,
-                             const float* AB, const float* save_xhat, const float* save_rstd,
-                             const float* g_m_aggr, const float* g_pos_aggr, float* dA,
-                             float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
-                             float* dpre3, float* vec_partials, uint32_t* amax, float* xhat12,
-                             void* stream);
 int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* pos,
                                const int64_t* rowptr, const int64_t* recv, const int64_t* send,
                                const gmp_egnn_params* params, int act, int msg_mean,
-                               const float* save_xhat, const float* save_rstd,
+                               const float* save_xhat, int save_planes, const float* save_rstd,
                                const float* g_m_aggr, const float* g_pos_aggr, float* dA,
                                float* dpos_recv, float* dpre1, float* gdiff, float* dpre2,
                                float* dpre3, float* vec_partials, uint32_t* amax, void* stream);
@@ -479,6 +463,16 @@ int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, in
  * gmp_tp_node_outer_f32 + the S read of gmp_outer_sum_cols_f32 (tfn_layer.py:73-87). */
 size_t gmp_tp_node_dw_workspace_size(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H,
                                      int64_t mul_out);
+/* K7s: forward of one TP path without the S intermediate in HBM (tfn_layer.py:73-87 regrouped):
+ *   C[n cldg + w d3 + k] += sum_{u,j} S[(n, k), (u, j)] W2p[(u, j), w] + sum_u Sb[(n, k), u] b2p[u, w]
+ * with S, Sb as for gmp_tp_node_dw_f32 (Z (edges x d3 mul1), A (edges x H), eoff (n_recv + 1,
+ * chunk-local)) and Bf the forward B planes of gmp_tp_split_w2_f32 (fwd = 1: [W2p | b2p]^T).
+ * d3 in {3, 5, 7}, mul_out in {64, 128}, mul1 % 32 == 0, H % 32 == 0 (GMP_ERR_UNSUPPORTED
+ * otherwise).  Deterministic.  Replaces gmp_tp_node_outer_f32 + gmp_tp_gemm_x3_f32 (forward). */
+int gmp_tp_node_fwd_fused_f32(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H,
+                              int64_t mul_out, const int64_t* eoff, const float* Z,
+                              const float* A, const void* Bf, float* C, int64_t cldg,
+                              void* stream);
 int gmp_tp_node_dw_f32(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H, int64_t mul_out,
                        const int64_t* eoff, const float* Z, const float* A, const float* G,
                        float* dW, void* workspace, size_t workspace_bytes, void* stream);

@@ -41,6 +41,22 @@ def test_scatter_out_semantics(reduce):
         assert torch.equal(out.cpu()[7], out0[7]) and (arg.cpu()[7] == 400).all()
 
 
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("how", ["out", "dim_size"])
+def test_scatter_fixed_rows_range_checked(reduce, how):
+    """An index outside the rows fixed by out= or dim_size raises IndexError, as torch_scatter
+    raises, instead of dropping the item."""
+    from gmp_amd import scatter
+    src = torch.randn(40, 3, device=DEV)
+    idx = torch.arange(40, device=DEV) % 12  # rows 0..11
+    kw = {"out": torch.zeros(10, 3, device=DEV)} if how == "out" else {"dim_size": 10}
+    with pytest.raises(IndexError):
+        scatter(src, idx, 0, reduce=reduce, **kw)
+    kw = {"out": torch.zeros(12, 3, device=DEV)} if how == "out" else {"dim_size": 12}
+    scatter(src, idx, 0, reduce=reduce, **kw)  # in range: fine
+    torch.cuda.synchronize()
+
+
 def test_cpu_tensor_raises():
     ops_ = _ops()
     with pytest.raises(RuntimeError, match="HIP device"):
@@ -62,7 +78,7 @@ def test_shape_checks_index_and_egnn():
     _bad(ops_.segment_reduce, src, torch.arange(9, device=DEV), rp, 2, "sum", match="perm")
     _bad(ops_.segment_reduce, src.double(), None, rp, 2, "sum", match="dtype")
     _bad(ops_.segment_reduce, src.t(), None, rp, 2, "sum", match="contiguous")
-    # EGNN backward: xhat must be (3, E, d), g_m (N, d)
+    # EGNN backward: xhat must be (2 or 3, E, d), g_m (N, d)
     N, E, d = 6, 10, 32
     pos = torch.randn(N, 3, **f)
     rowptr = torch.tensor([0, 2, 4, 6, 8, 10, 10], device=DEV)
@@ -73,7 +89,7 @@ def test_shape_checks_index_and_egnn():
         [torch.randn(d, **f) for _ in range(4)] + [torch.randn(1, **f)]
     xh, rs = torch.randn(3, E, d, **f), torch.randn(E, 3, **f)
     gm, gp = torch.randn(N, d, **f), torch.randn(N, 3, **f)
-    _bad(ops_.egnn_edge_bwd, pos, rowptr, recv, send, params, 0, False, xh[:2], rs, gm, gp,
+    _bad(ops_.egnn_edge_bwd, pos, rowptr, recv, send, params, 0, False, xh[:1], rs, gm, gp,
          match="xhat")
     _bad(ops_.egnn_edge_bwd, pos, rowptr, recv, send, params, 0, False, xh, rs[:5], gm, gp,
          match="rstd")

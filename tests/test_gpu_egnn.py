@@ -180,13 +180,15 @@ def test_frozen_parameters_release_side_stream_inputs():
 
 @pytest.mark.parametrize("f32,act,aggr", [(False, "relu", "sum"), (False, "swish", "mean"),
                                           (True, "relu", "sum")])
-def test_xhat_recompute_bitwise(f32, act, aggr):
-    """The K4 backward rebuilding the LayerNorm outputs (x_hat mode 1: x_hat3 from x_hat2; mode
-    0: all three from the node projections AB, W2 / W3 read transposed from the backward's W^T
-    image, the forward's saved 1/std) gives bitwise the outputs and gradients of the form that
-    saves x_hat1..3 (mode 2), for the HF and the exact-f32 products."""
+def test_xhat_recompute_bitwise(f32, act, aggr, monkeypatch):
+    """The K4 backward rebuilding x_hat3 from the saved x_hat2 (ops.EGNN_XHAT_PLANES = 2, the
+    default: W3 read transposed from the backward's W^T image, the forward's saved 1/std) gives
+    bitwise the outputs and gradients of the form that saves x_hat1..3 (3 planes), for the HF and
+    the exact-f32 products.  The backward follows the plane count of the tensor its forward saved:
+    switching the setting between a forward and its backward changes nothing (the
+    mode used to be a process global read again by the backward)."""
     import gmp_amd
-    from gmp_amd import _lib
+    from gmp_amd import _lib, ops
     lib = _lib.load()
     torch.manual_seed(7)
     g = _graph(3000, 60000, seed=8)
@@ -198,28 +200,52 @@ def test_xhat_recompute_bitwise(f32, act, aggr):
     h = torch.randn(g.num_nodes, 128, device=DEV)
     pos, ei = g.pos.to(DEV), g.edge_index.to(DEV)
 
-    def run():
+    def run(planes_fwd, planes_bwd):
         lay.zero_grad(set_to_none=True)
         hd, pd = h.clone().requires_grad_(True), pos.clone().requires_grad_(True)
+        monkeypatch.setattr(ops, "EGNN_XHAT_PLANES", planes_fwd)
         ho, po = lay(hd, pd, ei)
+        monkeypatch.setattr(ops, "EGNN_XHAT_PLANES", planes_bwd)
         (ho.square().sum() + (po * pos).sum()).backward()
         torch.cuda.synchronize()
         return [ho.detach(), po.detach(), hd.grad, pd.grad] + [p.grad.clone()
                                                                for p in lay.parameters()]
 
     prev_f = lib.gmp_egnn_set_f32_mfma(int(f32))
-    prev = lib.gmp_egnn_set_xhat_mode(2)
     try:
-        ref = run()
-        for mode in (1, 0, 3):
-            lib.gmp_egnn_set_xhat_mode(mode)
-            got = run()
+        ref = run(3, 3)
+        for fb in ((2, 2), (2, 3), (3, 2)):
+            got = run(*fb)
             for k, (x, y) in enumerate(zip(ref, got)):
-                assert torch.equal(x, y), (mode, k)
+                assert torch.equal(x, y), (fb, k)
     finally:
-        lib.gmp_egnn_set_xhat_mode(prev)
         lib.gmp_egnn_set_f32_mfma(prev_f)
     assert ref[2].abs().max().item() > 0
+
+
+def test_xhat_saved_planes_only():
+    """The training forward allocates exactly the planes it writes (a (3, E, d)
+    buffer held one or two unused planes until the backward)."""
+    from gmp_amd import _lib, ops
+    g = _graph(400, 4000, seed=2)
+    graph = ops.egnn_graph(g.edge_index.to(DEV), g.num_nodes)
+    d = 64
+    params = [torch.randn(d, device=DEV), torch.randn(d, device=DEV), torch.ones(d, device=DEV),
+              torch.zeros(d, device=DEV), torch.randn(d, d, device=DEV) / 8,
+              torch.zeros(d, device=DEV), torch.ones(d, device=DEV), torch.zeros(d, device=DEV),
+              torch.randn(d, d, device=DEV) / 8, torch.zeros(d, device=DEV),
+              torch.ones(d, device=DEV), torch.zeros(d, device=DEV), torch.randn(d, device=DEV),
+              torch.zeros(1, device=DEV)]
+    AB = torch.randn(g.num_nodes, 2 * d, device=DEV)
+    for planes in (2, 3):
+        _, _, xhat, rstd = _lib.torch_ops().egnn_edge_fwd(
+            AB, g.pos.to(DEV), graph.rowptr, graph.recv, graph.send, params, 0, False, 1e-5,
+            True, planes)
+        assert tuple(xhat.shape) == (planes, g.num_edges, d)
+        assert tuple(rstd.shape) == (g.num_edges, 3)
+    with pytest.raises(RuntimeError):
+        _lib.torch_ops().egnn_edge_fwd(AB, g.pos.to(DEV), graph.rowptr, graph.recv, graph.send,
+                                       params, 0, False, 1e-5, True, 1)
 
 
 def test_cu_masked_side_stream_same_gradients(monkeypatch):

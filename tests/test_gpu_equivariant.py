@@ -382,6 +382,48 @@ def test_mace_c4_full_size_properties():
     assert a[1].abs().max().item() > 0
 
 
+def test_tfn_c5_full_size_properties():
+    """C5's per-GPU shard at full size (TFN L_max=2, 64 channels, radial hidden 256, 5 layers,
+    gated; one 50k-node / ~1M-edge bench graph, seed 0), the configuration bench.py's `tfn`
+    object runs: the 256 x 64 K7g tile and the l <= 2 z / dz instantiation at that size.  The
+    training step's forward and backward are bitwise deterministic; the prediction is invariant
+    to the input edge order and to a rotation + translation of the positions within 1e-5
+    relative (tfn.py:166-190: first-node pooling of invariant scalars)."""
+    from gmp_amd import equivariant as eq
+    from gmp_amd.graph import Batch, radius_graph
+    g = radius_graph()
+    torch.manual_seed(0)
+    model = eq.TFNModel(num_layers=5, emb_dim=64, max_ell=2, mlp_dim=256, in_dim=1,
+                        out_dim=1).to(DEV)
+    ei = g.edge_index.to(DEV)
+    pos = g.pos.to(DEV)
+    atoms = g.atoms.to(DEV)
+
+    def run(p, e, grad=True):
+        model.zero_grad(set_to_none=True)
+        y = model(Batch(atoms, p, e, num_graphs=1))
+        if not grad:
+            return y.detach().double(), None
+        y.sum().backward()
+        return y.detach().double(), model.convs[2].fc[2].weight.grad.clone()
+
+    with torch.no_grad():
+        y0, _ = run(pos, ei, grad=False)
+        perm = torch.randperm(ei.shape[1], device=DEV)
+        yp, _ = run(pos, ei[:, perm], grad=False)
+        R = oo3.wigner_D(1, *(torch.tensor(a, dtype=torch.float64) for a in (0.3, 1.1, -0.6)))
+        pos_r = (g.pos.double() @ R.T + torch.tensor([0.5, -2.0, 1.0], dtype=torch.float64))
+        yr, _ = run(pos_r.float().to(DEV), ei, grad=False)
+    scale = y0.abs().max().item()
+    assert scale > 0
+    assert (yp - y0).abs().max().item() <= 1e-5 * scale, (yp, y0)
+    assert (yr - y0).abs().max().item() <= 1e-5 * scale, (yr, y0)
+    a = run(pos, ei)
+    b = run(pos, ei)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert a[1].abs().max().item() > 0
+
+
 @pytest.mark.parametrize("irr,B", [("8x0e+8x1o+8x2e", 37), ("128x0e+128x1o+128x2e", 20000),
                                    ("4x1o+2x2e", 300), ("3x0e+2x0o+5x1e", 1000)])
 def test_batchnorm_k16_vs_oracle(irr, B):

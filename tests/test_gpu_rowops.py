@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("rows,d", [(1, 32), (37, 100), (5000, 128), (50_000, 128), (300, 512)])
+@pytest.mark.parametrize("rows,d", [(1, 32), (37, 100), (5000, 128), (50_000, 128), (300, 512),
+                                    (200_000, 128), (3000, 64), (7000, 256), (1, 128)])
 @pytest.mark.parametrize("act", ["relu", "silu", None])
 def test_ln_act_matches_torch(rows, d, act):
     from gmp_amd import ops
@@ -47,3 +48,23 @@ def test_ln_act_deterministic():
         outs.append((xa.grad.clone(), ln.weight.grad.clone()))
         ln.weight.grad = ln.bias.grad = None
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_ln_act_bwd_tickets_reset_across_calls():
+    """The vectorised backward's two-level last-workgroup sums (tree_finish) leave their ticket
+    words zeroed: interleaved launches of different sizes on one stream give the same results
+    as each alone."""
+    from gmp_amd import ops
+    torch.manual_seed(3)
+    res = {}
+    for rows in (64_000, 900, 64_000, 130_000, 900):
+        x = torch.randn(rows, 128, device=DEV, generator=None)
+        torch.manual_seed(rows)
+        x = torch.randn(rows, 128, device=DEV)
+        ln = torch.nn.LayerNorm(128).to(DEV)
+        xa = x.clone().requires_grad_(True)
+        ops.ln_act(xa, ln, "silu").square().sum().backward()
+        got = (xa.grad.clone(), ln.weight.grad.clone(), ln.bias.grad.clone())
+        if rows in res:
+            assert all(torch.equal(a, b) for a, b in zip(res[rows], got)), rows
+        res[rows] = got

@@ -338,3 +338,55 @@ def test_node_dw_fused_matches_fp64(d3, mul1, H, mo, nrecv, seed):
     # deterministic
     dW2 = tops.tp_node_dw(eoff.to(DEV), Z.to(DEV), A.to(DEV), G.to(DEV), d3, mul1).cpu().double()
     assert torch.equal(dW, dW2)
+
+
+@pytest.mark.parametrize("d3,mul1,H,mo,nrecv,seed", [
+    (5, 64, 64, 128, 50, 1), (3, 32, 96, 128, 45, 2), (7, 32, 64, 64, 23, 3),
+    (5, 128, 256, 128, 30, 4), (3, 64, 32, 64, 100, 5), (5, 32, 32, 64, 13, 6)])
+def test_node_fwd_fused_matches_fp64(d3, mul1, H, mo, nrecv, seed):
+    """K7s (gmp_tp_node_fwd_fused_f32 via torch.ops.gmp.tp_node_fwd_fused): the forward path
+    contraction out[n, w d3 + k] += sum_{u,j} S[(n, k), (u, j)] W2p[(u, j), w] + sum_u Sb[(n, k), u]
+    b2p[u, w] with S / Sb built in-kernel from z and a, accumulated into a strided output block
+    (row stride cldg > mul_out d3, a column offset), against the fp64 evaluation; receivers of
+    in-degree 0, 1 and > 24 (past the prefetched operands), a last tile with fewer receivers.
+    Bound: f32 edge sums times the three-plane products, 4e-6 of sum |terms|."""
+    from gmp_amd import _lib
+    tops = _lib.torch_ops()
+    g = torch.Generator().manual_seed(seed)
+    degs = torch.randint(0, 30, (nrecv,), generator=g)
+    degs[0], degs[1] = 0, 45
+    if nrecv > 5:
+        degs[5] = 1
+    w = d3 * mul1
+    eoff, Z, A, ne = _setup(degs.tolist(), w, H, seed=seed)
+    off = 16 * mo  # the path's block of W2 rows (u, w) starts past other paths' rows
+    W2 = torch.randn(off + mul1 * mo + 8, H, generator=g) / H ** 0.5
+    b2 = torch.randn(off + mul1 * mo + 8, generator=g)
+    Bf = tops.tp_split_w2(W2.to(DEV), b2.to(DEV), off, mul1, mo, True)
+    cldg, c0 = mo * d3 + 11, 7
+    C0 = torch.randn(nrecv * cldg + c0 + 5, generator=g)
+    C = C0.to(DEV)
+    tops.tp_node_fwd_fused(eoff.to(DEV), Z.to(DEV), A.to(DEV), Bf, d3, mul1, mo, C, c0, cldg)
+    got = C.cpu().double()
+    W2p = W2[off:off + mul1 * mo].double().view(mul1, mo, H)   # [u, w, j]
+    b2p = b2[off:off + mul1 * mo].double().view(mul1, mo)      # [u, w]
+    ref = C0.double().clone()
+    bnd = torch.zeros_like(ref)
+    for n in range(nrecv):
+        e0, e1 = int(eoff[n]), int(eoff[n + 1])
+        z = Z[e0:e1].double().view(-1, d3, mul1)               # [e, k, u]
+        a = A[e0:e1].double()                                  # [e, j]
+        S = torch.einsum("eku,ej->kuj", z, a)
+        Sa = torch.einsum("eku,ej->kuj", z.abs(), a.abs())
+        Sb, Sba = z.sum(0), z.abs().sum(0)                     # [k, u]
+        o = torch.einsum("kuj,uwj->wk", S, W2p) + (Sb @ b2p).t()     # [w, k]
+        ob = torch.einsum("kuj,uwj->wk", Sa, W2p.abs()) + (Sba @ b2p.abs()).t()
+        base = c0 + n * cldg
+        ref[base:base + mo * d3] += o.reshape(-1)
+        bnd[base:base + mo * d3] += ob.reshape(-1)
+    err = (got - ref).abs()
+    assert bool((err <= 4e-6 * bnd + 1e-6).all()), (err / bnd.clamp_min(1e-30)).max().item()
+    # deterministic, and nothing outside the output block was touched
+    C2 = C0.to(DEV)
+    tops.tp_node_fwd_fused(eoff.to(DEV), Z.to(DEV), A.to(DEV), Bf, d3, mul1, mo, C2, c0, cldg)
+    assert torch.equal(C2.cpu().double(), got)
