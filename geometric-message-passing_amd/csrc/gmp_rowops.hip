@@ -309,6 +309,9 @@ __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __rest
 // [dgamma | dbeta] inside the backward kernel (last workgroup) with GMP_LN_FUSED_SUM=1; off by
 // default: measured 99.1 vs 101.0-101.6 M EGNN edges/s (the last workgroup sums 256 rows alone)
 int g_ln_fused_sum = getenv("GMP_LN_FUSED_SUM") ? atoi(getenv("GMP_LN_FUSED_SUM")) : 0;
+// GMP_LN_TREE=1: the vectorised kernel finishes [dgamma | dbeta] itself (tree_finish); measured
+// slower on the EGNN step (96 vs 102 M edges/s: every workgroup's __threadfence writes back L2)
+int g_ln_tree = getenv("GMP_LN_TREE") ? atoi(getenv("GMP_LN_TREE")) : 0;
 // GMP_LN_R03=1: the r03 one-wave-per-SIMD kernel + separate column sum (A/B)
 int g_ln_r03 = getenv("GMP_LN_R03") ? atoi(getenv("GMP_LN_R03")) : 0;
 // backward grid cap (GMP_LN_BWD_BLOCKS; A/B)
@@ -373,20 +376,24 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
                        reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
                        reinterpret_cast<uintptr_t>(grad_x);
   if (vec_form(d) && grad_gamma_beta && !g_ln_r03 && al % (d / 16) == 0) {
-    unsigned* tk = stream_ticket_block(s);
-    if (tk) {
-      const int GV = vec_blocks(rows);
-      float* grows = part + (size_t)GV * 2 * d;
+    // [dgamma | dbeta]: the two-level in-kernel finish (GMP_LN_TREE=1) or the column-sum kernel
+    unsigned* tk = g_ln_tree ? stream_ticket_block(s) : nullptr;
+    const int GV = vec_blocks(rows);
+    float* grows = part + (size_t)GV * 2 * d;
+    float* ogb = tk ? grad_gamma_beta : nullptr;
 #define GMP_LNV(A, F)                                                                        \
   ln_act_bwd_vec_kernel<A, F><<<GV, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, beta,    \
-                                                   grad_x, part, grows, grad_gamma_beta, tk)
+                                                   grad_x, part, grows, ogb, tk)
 #define GMP_LNV_F(A) \
   if (d == 64) GMP_LNV(A, 1); else if (d == 128) GMP_LNV(A, 2); else GMP_LNV(A, 4)
-      if (act == 0) { GMP_LNV_F(0); } else if (act == 1) { GMP_LNV_F(1); } else { GMP_LNV_F(2); }
+    if (act == 0) { GMP_LNV_F(0); } else if (act == 1) { GMP_LNV_F(1); } else { GMP_LNV_F(2); }
 #undef GMP_LNV_F
 #undef GMP_LNV
-      return launch_status();
-    }
+    int rc = launch_status();
+    if (rc || tk) return rc;
+    sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, GV, (int)(2 * d),
+                                                                         grad_gamma_beta);
+    return launch_status();
   }
   // [dgamma | dbeta] by the kernel's last workgroup when a ticket is available (one launch);
   // otherwise (or GMP_LN_FUSED_SUM=0) the partial rows go through sum_rows_kernel

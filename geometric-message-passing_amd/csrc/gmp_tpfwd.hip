@@ -120,6 +120,30 @@ __global__ __launch_bounds__(kFT, 1) void tp_node_fwd_fused_kernel(
   const int k_in = li / U, uu_in = li - (li / U) * U;
   const bool row_in = li < F::NC;
 
+  // the tile's z / a rows through buffer descriptors (32-bit lane offsets from the tile's first
+  // edge; a lane offset past the descriptor (kOobF) loads 0: absent edges and combos need no
+  // branch or select).  Z has a pad row after the last edge: the last u step's combos past mul1
+  // read at most U - 1 floats past a row (into its image chunks that are never consumed).
+  const int nlast = min(n0 + RT, n_recv);
+  const int64_t te0 = eoff[n0], te1 = eoff[nlast];
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(Z) + te0 * w, 0, (int)((te1 - te0 + 1) * w * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A) + te0 * H, 0, (int)((te1 - te0) * H * 4), 0x00020000);
+  constexpr unsigned kOobF = 0x80000000u;
+  unsigned zo[NCH][PF], ao[NCH][PF];  // byte offsets of this lane's operands of MFMA step t
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int jb = (wv + 8 * i) / RT;
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+      const int el = ce0[i] - (int)te0 + 4 * t + g;
+      const bool ok = ce0[i] + 4 * t + g < ce1[i];
+      zo[i][t] = (ok && row_in) ? (unsigned)(el * w + k_in * mul1 + uu_in) * 4u : kOobF;
+      ao[i][t] = ok ? (unsigned)(el * H + jb * 16 + li) * 4u : kOobF;
+    }
+  }
+
   // step -> (bias?, u0, jc)
   auto step_u0 = [&](int s) { return s < NBS ? s * U : ((s - NBS) / HB) * U; };
   auto step_jc = [&](int s) { return s < NBS ? -1 : (s - NBS) % HB; };
@@ -138,22 +162,14 @@ __global__ __launch_bounds__(kFT, 1) void tp_node_fwd_fused_kernel(
   float zp[NCH][PF], ap[NCH][PF];  // prefetched operands of the first PF MFMA steps per chain
   auto prefetch = [&](int s) {
     if (s >= nsteps || s < NBS) return;
-    const int u0 = step_u0(s), jc = step_jc(s);
-    const int ucol = k_in * mul1 + u0 + uu_in;
-    const bool zok = row_in && u0 + uu_in < mul1;
+    const unsigned zs = 4u * step_u0(s), as = 128u * step_jc(s);
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int jb = (wv + 8 * i) / RT;
-      const float* zc = Z + ucol;
-      const float* ac = A + jc * 32 + jb * 16 + li;
+    for (int i = 0; i < NCH; ++i)
 #pragma unroll
       for (int t = 0; t < PF; ++t) {
-        const int e = ce0[i] + 4 * t + g;
-        const bool ok = e < ce1[i];
-        zp[i][t] = (ok && zok) ? zc[(int64_t)e * w] : 0.f;
-        ap[i][t] = ok ? ac[(int64_t)e * H] : 0.f;
+        zp[i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zrs, zo[i][t] + zs, 0, 0));
+        ap[i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, ao[i][t] + as, 0, 0));
       }
-    }
   };
   auto produce = [&](int s, unsigned char* img) {
     if (s >= nsteps) return;
@@ -181,9 +197,7 @@ __global__ __launch_bounds__(kFT, 1) void tp_node_fwd_fused_kernel(
       }
       return;
     }
-    const int u0 = step_u0(s), jc = step_jc(s);
-    const int ucol = k_in * mul1 + u0 + uu_in;
-    const bool zok = row_in && u0 + uu_in < mul1;
+    const unsigned zs = 4u * step_u0(s), as = 128u * step_jc(s);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = wv + 8 * i;
@@ -194,30 +208,31 @@ __global__ __launch_bounds__(kFT, 1) void tp_node_fwd_fused_kernel(
 #pragma unroll
       for (int t = 0; t < PF; ++t)
         if (t < nq) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zp[i][t], ap[i][t], acc, 0, 0, 0);
-      if (nq > PF) {  // in-degree > 4 PF: the rest directly
-        const float* zc = Z + ucol;
-        const float* ac = A + jc * 32 + jb * 16 + li;
-        for (int t = PF; t < nq; ++t) {
-          const int e = ce0[i] + 4 * t + g;
-          const bool ok = e < ce1[i];
-          const float zv = (ok && zok) ? zc[(int64_t)e * w] : 0.f;
-          const float av = ok ? ac[(int64_t)e * H] : 0.f;
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, av, acc, 0, 0, 0);
-        }
+      for (int t = PF; t < nq; ++t) {  // in-degree > 4 PF: the rest directly
+        const int el = ce0[i] - (int)te0 + 4 * t + g;
+        const bool ok = ce0[i] + 4 * t + g < ce1[i];
+        const unsigned zv = ok && row_in ? (unsigned)(el * w + k_in * mul1 + uu_in) * 4u + zs : kOobF;
+        const unsigned av = ok ? (unsigned)(el * H + jb * 16 + li) * 4u + as : kOobF;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zrs, zv, 0, 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, av, 0, 0)), acc,
+            0, 0, 0);
       }
-      // lane (li, g): S[combo m = 4 g + q][j = jb 16 + li] -> image chunk uu, row rho d3 + k
+      // lane (li, g): S[combo m = 4 g + q][j = jb 16 + li] -> image chunk uu, row rho d3 + k;
+      // pairs of values split together (one f32x2 pass), written as 16-bit halves
+      unsigned ph[2], pm[2], pl[2];
+      split3p(f32x2{acc[0], acc[1]}, ph[0], pm[0], pl[0]);
+      split3p(f32x2{acc[2], acc[3]}, ph[1], pm[1], pl[1]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int m = 4 * g + q;
         if (m < F::NC) {
           const int k = m / U, uu = m - (m / U) * U;
-          unsigned short h, mi, lo;
-          split3v(acc[q], h, mi, lo);
-          const int off = ioff(rho * D3 + k, jb * 16 + li);
-          unsigned char* base = img + uu * 3 * kChunkB + off;
-          *reinterpret_cast<unsigned short*>(base) = h;
-          *reinterpret_cast<unsigned short*>(base + kChunkB) = mi;
-          *reinterpret_cast<unsigned short*>(base + 2 * kChunkB) = lo;
+          const int sh = 16 * (q & 1);
+          unsigned char* base = img + uu * 3 * kChunkB + ioff(rho * D3 + k, jb * 16 + li);
+          *reinterpret_cast<unsigned short*>(base) = (unsigned short)(ph[q >> 1] >> sh);
+          *reinterpret_cast<unsigned short*>(base + kChunkB) = (unsigned short)(pm[q >> 1] >> sh);
+          *reinterpret_cast<unsigned short*>(base + 2 * kChunkB) = (unsigned short)(pl[q >> 1] >> sh);
         }
       }
     }
@@ -229,17 +244,22 @@ __global__ __launch_bounds__(kFT, 1) void tp_node_fwd_fused_kernel(
   f32x4 acc[RTW];
 #pragma unroll
   for (int r = 0; r < RTW; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const unsigned short* bl = Bf + 8 * lane;
   const int ct = wn;  // this wave's 16-column tile
+  // B planes through a descriptor: the lane / column-tile part of the offset is fixed, the chunk
+  // part is wave-uniform (scalar offset): no per-load address arithmetic
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(Bf), 0, 0x7fffffff, 0x00020000);
+  const unsigned bvo = 16u * lane + (unsigned)ct * 3u * 1024u;
   u32x4 bst[U][3];
   auto load_b_step = [&](int s) {
 #pragma unroll
     for (int uu = 0; uu < U; ++uu) {
       int64_t ch = s < nsteps ? chunk_of(s, uu) : -1;
       if (ch < 0) ch = 0;  // absent chunk: a valid address, never consumed
+      const int so = (int)(ch * ct_total * 3 * 1024);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        bst[uu][p] = *reinterpret_cast<const u32x4*>(bl + ((ch * ct_total + ct) * 3 + p) * 512);
+        bst[uu][p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(brs, bvo, so + p * 1024, 0));
     }
   };
   auto consume = [&](int s, const unsigned char* img) {

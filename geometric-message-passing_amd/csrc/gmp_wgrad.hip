@@ -949,6 +949,144 @@ __global__ __launch_bounds__(kXT, OCC) void outer_cols_x3g_kernel(
         out[(int64_t)(64 * wm + 16 * r + 4 * g + q) * n + 16 * (wn * CT + c) + li] = acc[r][c][q];
 }
 
+// Node-level sums (r04): C (m x n, m, n multiples of 64, <= 256) = A^T B (+ colsum(A)) over K
+// rows with the OUTPUT split into 64 x 64 quadrants as well as K into row ranges: 4-wave
+// workgroups (32 KB of LDS, two per CU) of ~400 rows each, so a 50k-row sum spreads over ~512
+// short workgroups instead of ~100 long ones (r03: outer_sum_kernel<128, 0> 107-115 us per 50k x
+// 128 x 128 sum on the side stream, holding CUs the critical path's node kernels wait for).
+// f32 MFMA 16x16x4 (exact f32 products, the rows as the MFMA k dimension), stages of 32 rows
+// double-buffered through LDS; slabs summed in range order by sum_partials_one<4>.
+constexpr int kQT = 256;
+constexpr int kQK = 32;
+constexpr int kQLd = 64 + 4;
+__global__ __launch_bounds__(kQT, 2) void outer_sum_quad_kernel(
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, int64_t K,
+    int m, int n, int64_t per, float* __restrict__ part, int64_t X) {
+  __shared__ __attribute__((aligned(16))) float sA[2][kQK * kQLd];
+  __shared__ __attribute__((aligned(16))) float sB[2][kQK * kQLd];
+  __shared__ float sCol[16][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, kk = lane >> 4;
+  const int nq = n >> 6;
+  const int qm = blockIdx.y / nq, qn = blockIdx.y - qm * nq;
+  const int m0 = 64 * qm, n0 = 64 * qn;
+  const int64_t k0 = (int64_t)blockIdx.x * per;
+  const int64_t k1 = (k0 + per < K) ? k0 + per : K;
+  const int wm = w >> 1, wn = w & 1;
+  const bool colsum = qn == 0;
+  // loader: v = tid + 256 q (q < 2) -> stage row v / 16, float4 column group v % 16 (the same
+  // column group for both q: the thread's colsum stays in registers)
+  const int cq = tid & 15, r0 = tid >> 4;
+  f32x4 ra[2], rb[2], csum = {0.f, 0.f, 0.f, 0.f};
+  auto fetch = [&](int64_t kb) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t k = kb + r0 + 16 * q;
+      ra[q] = rb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k < k1) {
+        ra[q] = *reinterpret_cast<const f32x4*>(A + k * lda + m0 + 4 * cq);
+        rb[q] = *reinterpret_cast<const f32x4*>(B + k * ldb + n0 + 4 * cq);
+      }
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = r0 + 16 * q;
+      csum += ra[q];
+      *reinterpret_cast<f32x4*>(&sA[buf][r * kQLd + 4 * cq]) = ra[q];
+      *reinterpret_cast<f32x4*>(&sB[buf][r * kQLd + 4 * cq]) = rb[q];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) acc[a][0] = acc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int buf = 0;
+  if (k0 < k1) {
+    fetch(k0);
+    stash(0);
+  }
+  __syncthreads();
+  for (int64_t kb = k0; kb < k1; kb += kQK) {
+    const bool more = kb + kQK < k1;
+    if (more) fetch(kb + kQK);  // in flight while this stage is computed
+    const float* a_s = sA[buf];
+    const float* b_s = sB[buf];
+#pragma unroll
+    for (int st = 0; st < kQK / 4; ++st) {
+      const int e = 4 * st + kk;
+      float af[2], bf[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        af[t] = a_s[e * kQLd + 32 * wm + 16 * t + li];
+        bf[t] = b_s[e * kQLd + 32 * wn + 16 * t + li];
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+    if (more) stash(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // C/D map of 16x16x4: col = lane & 15, row = 4 (lane >> 4) + r
+  float* out = part + (int64_t)blockIdx.x * X;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(int64_t)(m0 + 32 * wm + 16 * a + 4 * kk + r) * n + n0 + 32 * wn + 16 * b + li] =
+            acc[a][b][r];
+  if (colsum) {  // the 16 row groups of each column group, added in row-group order
+    *reinterpret_cast<f32x4*>(&sCol[r0][4 * cq]) = csum;
+    __syncthreads();
+    if (tid < 64) {
+      float t = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < 16; ++g2) t += sCol[g2][tid];
+      out[(int64_t)m * n + m0 + tid] = t;
+    }
+  }
+}
+
+// GMP_WGRAD_QUAD=0: node-level sums on the r03 split-K kernels (A/B)
+int g_quad = getenv("GMP_WGRAD_QUAD") ? atoi(getenv("GMP_WGRAD_QUAD")) : 1;
+int64_t quad_splits(int64_t K, int64_t quads) {
+  int64_t s = ceil_div(2 * (int64_t)device_cu_count(), quads);  // ~2 workgroups per CU
+  const int64_t cap = ceil_div(K, 256);                          // >= 256 rows each
+  if (s > cap) s = cap;
+  return s < 1 ? 1 : s;
+}
+bool quad_ok(int64_t K, int64_t m, int64_t n, int pro, int64_t lda, int64_t ldb) {
+  return g_quad && pro == 0 && K < g_x3_min_k && K > 0 && m % 64 == 0 && n % 64 == 0 &&
+         m <= 256 && n <= 256 && lda % 4 == 0 && ldb % 4 == 0;
+}
+size_t quad_workspace(int64_t K, int64_t m, int64_t n) {
+  return (size_t)quad_splits(K, (m / 64) * (n / 64)) * (size_t)(m * n + m) * sizeof(float);
+}
+int outer_sum_quad_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
+                          const float* B, int64_t ldb, float* C, int64_t ldc, float* colsum_A,
+                          void* workspace, hipStream_t s) {
+  const int64_t quads = (m / 64) * (n / 64);
+  const int64_t S = quad_splits(K, quads);
+  const int64_t per = ceil_div(ceil_div(K, S), kQK) * kQK;
+  const int64_t Sr = ceil_div(K, per);
+  const int64_t X = m * n + m;
+  float* part = reinterpret_cast<float*>(workspace);
+  outer_sum_quad_kernel<<<dim3((unsigned)Sr, (unsigned)quads), kQT, 0, s>>>(A, lda, B, ldb, K,
+                                                                           (int)m, (int)n, per,
+                                                                           part, X);
+  int rc = launch_status();
+  if (rc) return rc;
+  sum_partials_one<4><<<(unsigned)ceil_div(X, 64), 256, 0, s>>>(part, Sr, X, C, colsum_A, m * n,
+                                                                n, ldc);
+  return launch_status();
+}
+
 // GMP_OSC_PRESPLIT=0: the r03 column-block kernel (both operands split per block)
 int g_osc_presplit = getenv("GMP_OSC_PRESPLIT") ? atoi(getenv("GMP_OSC_PRESPLIT")) : 1;
 
@@ -1002,7 +1140,9 @@ int gmp_wgrad_set_f32_mfma(int on) {
 
 size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d) {
   const int64_t G = blocks_for(K);
-  return (size_t)(G + ceil_div(G, kGC)) * (size_t)(d * d + d) * sizeof(float);
+  const size_t ws = (size_t)(G + ceil_div(G, kGC)) * (size_t)(d * d + d) * sizeof(float);
+  const size_t wq = quad_ok(K, d, d, 0, d, d) ? quad_workspace(K, d, d) : 0;
+  return ws > wq ? ws : wq;
 }
 
 static int outer_sum_launch(int64_t K, int64_t d, const float* A, int64_t lda, const float* B,
@@ -1028,6 +1168,9 @@ static int outer_sum_launch(int64_t K, int64_t d, const float* A, int64_t lda, c
                                        workspace, s);
     if (rc != GMP_ERR_UNSUPPORTED) return rc;
   }
+  if (quad_ok(K, d, d, pro, lda, ldb) && d >= 64 &&
+      reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0)
+    return outer_sum_quad_launch(K, d, d, A, lda, B, ldb, C, ldc, colsum_A, workspace, s);
   const int64_t G = blocks_for(K);
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
@@ -1098,7 +1241,9 @@ int64_t rect_blocks_for(int64_t K) {
 
 size_t gmp_edge_outer_sum_rect_workspace_size(int64_t K, int64_t m, int64_t n) {
   const int64_t G = rect_blocks_for(K);
-  return (size_t)(G + ceil_div(G, kGC)) * (size_t)(m * n + m) * sizeof(float);
+  const size_t ws = (size_t)(G + ceil_div(G, kGC)) * (size_t)(m * n + m) * sizeof(float);
+  const size_t wq = quad_ok(K, m, n, 0, m, n) ? quad_workspace(K, m, n) : 0;
+  return ws > wq ? ws : wq;
 }
 
 static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t lda,
@@ -1108,7 +1253,7 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
   GMP_CHECK_ARG(K >= 0 && C && m > 0 && n > 0 && m % 16 == 0 && n % 16 == 0 && m <= kT);
   GMP_CHECK_ARG(lda >= m && ldb >= n && ldc >= n && lda % 4 == 0 && ldb % 4 == 0);
   const int bucket = rect_bucket(m, n);
-  if (!bucket) return GMP_ERR_UNSUPPORTED;
+  if (!bucket && !quad_ok(K, m, n, 0, lda, ldb)) return GMP_ERR_UNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if (K == 0) {
     int rc = hip_check(hipMemset2DAsync(C, ldc * sizeof(float), 0, n * sizeof(float), m, s));
@@ -1123,6 +1268,9 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
                                         colsum_A, workspace, s);
     if (rc2 != GMP_ERR_UNSUPPORTED) return rc2;
   }
+  if (quad_ok(K, m, n, 0, lda, ldb))
+    return outer_sum_quad_launch(K, m, n, A, lda, B, ldb, C, ldc, colsum_A, workspace, s);
+  if (!bucket) return GMP_ERR_UNSUPPORTED;
   const int64_t G = rect_blocks_for(K);
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);

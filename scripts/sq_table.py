@@ -19,18 +19,19 @@ def main(path):
             order.append(k)
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
     print("| kernel | MFMA instrs | VALU instrs | VALU / MFMA | LDS instrs | LDS bank-conflict / "
-          "LDS-active cycles | wait / wave cycles |")
-    print("|---|---|---|---|---|---|---|")
+          "LDS-active cycles | issue-stall / wave cycles | waitcnt+barrier / wave cycles |")
+    print("|---|---|---|---|---|---|---|---|")
     for k in order:
         c = tot[k]
         mf, va = c.get("SQ_INSTS_MFMA", 0.0), c.get("SQ_INSTS_VALU", 0.0)
         lds_act = c.get("SQ_LDS_IDX_ACTIVE", 0.0)
         wave = c.get("SQ_WAVE_CYCLES", 0.0)
+        wany = c.get("SQ_WAIT_ANY")
         print(f"| `{k}` | {mf:.3g} | {va:.3g} | {va / mf if mf else float('nan'):.2f} | "
               f"{c.get('SQ_INSTS_LDS', 0.0):.3g} | "
               f"{c.get('SQ_LDS_BANK_CONFLICT', 0.0) / lds_act if lds_act else 0.0:.2f} | "
-              f"{c.get('SQ_WAIT_INST_ANY', 0.0) / wave if wave else 0.0:.2f} |")
-
+              f"{c.get('SQ_WAIT_INST_ANY', 0.0) / wave if wave else 0.0:.2f} | "
+              f"{'-' if wany is None or not wave else f'{wany / wave:.2f}'} |")
 
 if __name__ == "__main__":
     main(*sys.argv[1:])

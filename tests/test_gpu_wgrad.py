@@ -23,7 +23,7 @@ def _err(C, ref, A, B):
 @pytest.mark.parametrize("m,n", [(16, 16), (16, 48), (48, 48), (16, 128), (128, 16), (16, 144),
                                  (48, 144), (128, 48), (128, 80), (128, 128), (128, 144),
                                  (32, 32), (64, 64), (32, 128)])
-@pytest.mark.parametrize("K", [5, 4097, 300_001, 1_000_003])
+@pytest.mark.parametrize("K", [5, 4097, 50_021, 300_001, 1_000_003])
 def test_outer_sum_split_matches_fp64(m, n, K):
     from gmp_amd import ops
     g = torch.Generator().manual_seed(m * 1000 + n + K)
@@ -41,11 +41,12 @@ def test_outer_sum_split_matches_fp64(m, n, K):
                                rtol=1e-5)
 
 
-def test_outer_sum_strided_blocks():
-    """column blocks of wider tensors (lda, ldb, ldc > width) on the split path"""
+@pytest.mark.parametrize("K", [300_007, 49_999])
+def test_outer_sum_strided_blocks(K):
+    """column blocks of wider tensors (lda, ldb, ldc > width) on the split path (K = 300k) and
+    on the node-level quadrant kernel (K = 50k)"""
     from gmp_amd import ops
     g = torch.Generator().manual_seed(7)
-    K = 300_007
     A = torch.randn(K, 272, generator=g).to(DEV)
     B = torch.randn(K, 200, generator=g).to(DEV)
     C = torch.zeros(300, 260, device=DEV)
@@ -53,6 +54,28 @@ def test_outer_sum_strided_blocks():
     ref = A[:, 16:144].double().t() @ B[:, 40:184].double()
     torch.testing.assert_close(C[8:136, 100:244].double(), ref, atol=2e-3, rtol=1e-5)
     assert C[:8].abs().sum() == 0 and C[:, :100].abs().sum() == 0
+
+
+@pytest.mark.parametrize("m,n", [(128, 128), (64, 64), (128, 256), (256, 64)])
+def test_outer_sum_node_level_quadrants(m, n):
+    """Node-level sums (K < 256k rows: the quadrant kernel, outer_sum_quad_kernel) with strided
+    operands and output (column blocks of wider tensors) against fp64, colsum included, and
+    bitwise determinism."""
+    from gmp_amd import ops
+    g = torch.Generator().manual_seed(m + n)
+    K = 50_003
+    A = torch.randn(K, m + 24, generator=g).to(DEV)
+    B = torch.randn(K, n + 40, generator=g).to(DEV)
+    C = torch.zeros(m + 20, n + 120, device=DEV)
+    cs = torch.zeros(m, device=DEV)
+    ops.outer_sum_into(A[:, 8:8 + m], B[:, 20:20 + n], C[4:4 + m, 100:100 + n], cs)
+    refC, refs = _ref(A[:, 8:8 + m].cpu(), B[:, 20:20 + n].cpu())
+    assert _err(C[4:4 + m, 100:100 + n], refC, A[:, 8:8 + m].cpu(), B[:, 20:20 + n].cpu()) < 5e-6
+    torch.testing.assert_close(cs.cpu().double(), refs, atol=1e-5 * K ** 0.5, rtol=1e-5)
+    assert C[:4].abs().sum() == 0 and C[:, :100].abs().sum() == 0
+    C2 = torch.zeros_like(C)
+    ops.outer_sum_into(A[:, 8:8 + m], B[:, 20:20 + n], C2[4:4 + m, 100:100 + n])
+    assert torch.equal(C, C2)
 
 
 @pytest.mark.parametrize("act", ["relu", "silu"])
