@@ -908,8 +908,9 @@ void tp_node_fwd_fused(const Tensor& eoff, const Tensor& Z, const Tensor& A, con
   need(Bf, at::kShort, "B planes");
   TORCH_CHECK(eoff.dim() == 1 && eoff.numel() >= 1, "gmp.tp_node_fwd_fused: eoff (n_recv + 1)");
   const int64_t n = eoff.numel() - 1;
-  TORCH_CHECK(A.dim() == 2 && Z.dim() == 2 && Z.size(1) == d3 * mul1 && Z.size(0) >= A.size(0),
-              "gmp.tp_node_fwd_fused: Z (edges, d3 mul1), A (edges, H)");
+  TORCH_CHECK(A.dim() == 2 && Z.dim() == 3 && Z.size(2) == 16 && Z.size(1) >= A.size(0) &&
+                  Z.size(0) == (mul1 + 16 / d3 - 1) / (16 / d3),
+              "gmp.tp_node_fwd_fused: Z in the K7s layout (u steps, rows, 16), A (edges, H)");
   const int64_t H = A.size(1);
   TORCH_CHECK(Bf.numel() >= 3 * mul_out * (mul1 * H + mul1),
               "gmp.tp_node_fwd_fused: B planes hold 3 mul_out (mul1 H + mul1)");
@@ -917,10 +918,23 @@ void tp_node_fwd_fused(const Tensor& eoff, const Tensor& Z, const Tensor& A, con
   if (n > 0)
     TORCH_CHECK(c_offset + (n - 1) * cldg + (mul_out - 1) * d3 + d3 - 1 < C.numel(),
                 "gmp.tp_node_fwd_fused: the output block exceeds C");
-  check_rc(gmp_tp_node_fwd_fused_f32(n, d3, mul1, H, mul_out, ip(eoff), fp(Z), fp(A),
+  check_rc(gmp_tp_node_fwd_fused_f32(n, d3, mul1, H, mul_out, ip(eoff), fp(Z), Z.size(1), fp(A),
                                      Bf.data_ptr(), C.data_ptr<float>() + c_offset, cldg,
                                      cur_stream()),
            "gmp_tp_node_fwd_fused_f32");
+}
+
+// z rows (rows, d3 mul1) -> the K7s layout (ceil(mul1 / U), rows, 16), U = 16 / d3
+Tensor tp_z_fused_layout(const Tensor& Z, int64_t d3, int64_t mul1) {
+  OpGuard g(Z, "tp_z_fused_layout");
+  f32(Z, "Z");
+  TORCH_CHECK(d3 >= 1 && d3 <= 16 && Z.dim() == 2 && Z.size(1) == d3 * mul1,
+              "gmp.tp_z_fused_layout: Z (rows, d3 mul1)");
+  const int64_t U = 16 / d3;
+  Tensor Zf = at::empty({(mul1 + U - 1) / U, Z.size(0), 16}, Z.options());
+  check_rc(gmp_tp_z_fused_layout_f32(fp(Z), Z.size(0), d3, mul1, fp(Zf), cur_stream()),
+           "gmp_tp_z_fused_layout_f32");
+  return Zf;
 }
 
 // three bf16 planes of the (N x K) operand B = W (transpose = false: rows n of W) or W^T
@@ -1425,6 +1439,10 @@ Tensor tp_node_dw(const Tensor&, const Tensor&, const Tensor& A, const Tensor& G
 }
 void tp_node_fwd_fused(const Tensor&, const Tensor&, const Tensor&, const Tensor&, int64_t,
                        int64_t, int64_t, Tensor, int64_t, int64_t) {}
+Tensor tp_z_fused_layout(const Tensor& Z, int64_t d3, int64_t mul1) {
+  const int64_t U = 16 / d3;
+  return at::empty({(mul1 + U - 1) / U, Z.size(0), 16}, Z.options());
+}
 Tensor split_x3(const Tensor& W, bool) {
   return at::empty({3 * W.numel()}, W.options().dtype(at::kShort));
 }
@@ -1552,6 +1570,7 @@ TORCH_LIBRARY(gmp, m) {
   m.def("tp_node_dw(Tensor eoff, Tensor Z, Tensor A, Tensor G, int d3, int mul1) -> Tensor");
   m.def("tp_node_fwd_fused(Tensor eoff, Tensor Z, Tensor A, Tensor Bf, int d3, int mul1, "
         "int mul_out, Tensor(a!) C, int c_offset, int cldg) -> ()");
+  m.def("tp_z_fused_layout(Tensor Z, int d3, int mul1) -> Tensor");
   m.def("gemm_x3(Tensor A1, Tensor? A2, Tensor Bp, int N, Tensor? bias) -> Tensor");
   m.def("outer_sum_cols(Tensor A, Tensor B) -> Tensor");
   m.def("edge_outer_sum(Tensor A, Tensor B) -> (Tensor C, Tensor colsum)");
@@ -1608,6 +1627,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("split_x3", ns split_x3);                                        \
   m.impl("tp_node_dw", ns tp_node_dw);                                    \
   m.impl("tp_node_fwd_fused", ns tp_node_fwd_fused);                      \
+  m.impl("tp_z_fused_layout", ns tp_z_fused_layout);                      \
   m.impl("gemm_x3", ns gemm_x3);                                          \
   m.impl("outer_sum_cols", ns outer_sum_cols);                            \
   m.impl("edge_outer_sum", ns edge_outer_sum);                            \

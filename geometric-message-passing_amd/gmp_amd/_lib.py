@@ -143,8 +143,10 @@ SIGNATURES = {
     "gmp_tp_split_w2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_split_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "gmp_tp_node_dw_workspace_size": (c_size, [c_i64, c_i64, c_i64, c_i64, c_i64]),
-    "gmp_tp_node_fwd_fused_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp,
-                                          c_vp, c_vp, c_i64, c_vp]),
+    "gmp_tp_node_fwd_fused_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64,
+                                          c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "gmp_tp_z_fused_layout_floats": (c_i64, [c_i64, c_i64, c_i64]),
+    "gmp_tp_z_fused_layout_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "gmp_tp_node_dw_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
                                    c_vp, c_vp, c_size, c_vp]),
     "gmp_gemm_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp,

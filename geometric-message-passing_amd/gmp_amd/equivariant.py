@@ -583,8 +583,10 @@ def _dw_fused_ok(P, H):
 # K7s (gmp_tpfwd.hip): the forward's path contraction with S built inside the GEMM (S never in
 # HBM: 66 GB of S writes + reads per MACE-128 lo = 2 path avoided); lo >= 1 paths of the K7g
 # shapes (the lo = 0 paths keep the S kernel + K7g GEMM: d3 = 1 would leave 15 of 16 S-MFMA rows
-# idle).  GMP_TP_FWD_FUSED=0 restores the unfused forward.
-TP_FWD_FUSED = os.environ.get("GMP_TP_FWD_FUSED", "1") == "1"
+# idle).  Opt-in (GMP_TP_FWD_FUSED=1): parity-green but measured slower than the unfused pair at
+# the MACE-128 shapes (r04, 50k receivers / 1M edges: d3 = 5 25.1 vs 21.6 ms, d3 = 3 18.3 vs
+# 12.9 ms; DESIGN.md "K7s").
+TP_FWD_FUSED = os.environ.get("GMP_TP_FWD_FUSED", "0") == "1"
 
 
 def _fwd_fused_ok(P, H):
@@ -636,8 +638,10 @@ class TPConvNodeFn(torch.autograd.Function):
                     if Bfs[i] is None:
                         Bfs[i] = _split_w2(W2c, b2c, P, True)
                     with _timed("tp_node_W"):
-                        tops.tp_node_fwd_fused(eoff, Zp, a, Bfs[i], d3, m1, mo, out,
+                        Zf = tops.tp_z_fused_layout(Zp, d3, m1)
+                        tops.tp_node_fwd_fused(eoff, Zf, a, Bfs[i], d3, m1, mo, out,
                                                n0 * out.shape[1] + blk[0], out.shape[1])
+                        del Zf
                     continue
                 S, Sb = _node_outer(eoff, Zp, a, w)
                 if x3[i]:

@@ -465,13 +465,19 @@ size_t gmp_tp_node_dw_workspace_size(int64_t n_recv, int64_t d3, int64_t mul1, i
                                      int64_t mul_out);
 /* K7s: forward of one TP path without the S intermediate in HBM (tfn_layer.py:73-87 regrouped):
  *   C[n cldg + w d3 + k] += sum_{u,j} S[(n, k), (u, j)] W2p[(u, j), w] + sum_u Sb[(n, k), u] b2p[u, w]
- * with S, Sb as for gmp_tp_node_dw_f32 (Z (edges x d3 mul1), A (edges x H), eoff (n_recv + 1,
- * chunk-local)) and Bf the forward B planes of gmp_tp_split_w2_f32 (fwd = 1: [W2p | b2p]^T).
- * d3 in {3, 5, 7}, mul_out in {64, 128}, mul1 % 32 == 0, H % 32 == 0 (GMP_ERR_UNSUPPORTED
- * otherwise).  Deterministic.  Replaces gmp_tp_node_outer_f32 + gmp_tp_gemm_x3_f32 (forward). */
+ * with S, Sb as for gmp_tp_node_dw_f32 (z rows, A (edges x H), eoff (n_recv + 1, chunk-local))
+ * and Bf the forward B planes of gmp_tp_split_w2_f32 (fwd = 1: [W2p | b2p]^T).  The z rows come
+ * in the K7s layout Zf (gmp_tp_z_fused_layout_f32 of the (zrows x d3 mul1) rows).  d3 in {3, 5,
+ * 7}, mul_out in {64, 128}, mul1 % 32 == 0, H % 32 == 0 (GMP_ERR_UNSUPPORTED otherwise).
+ * Deterministic.  Replaces gmp_tp_node_outer_f32 + gmp_tp_gemm_x3_f32 (forward). */
 int gmp_tp_node_fwd_fused_f32(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H,
-                              int64_t mul_out, const int64_t* eoff, const float* Z,
-                              const float* A, const void* Bf, float* C, int64_t cldg,
+                              int64_t mul_out, const int64_t* eoff, const float* Zf,
+                              int64_t zrows, const float* A, const void* Bf, float* C,
+                              int64_t cldg, void* stream);
+/* The K7s z layout: Zf[us][e][16] = z[e][k mul1 + us U + uu] at c = k U + uu < d3 U (U = 16 / d3),
+ * zero elsewhere (and for us U + uu >= mul1); us < ceil(mul1 / U).  _floats: the size of Zf. */
+int64_t gmp_tp_z_fused_layout_floats(int64_t rows, int64_t d3, int64_t mul1);
+int gmp_tp_z_fused_layout_f32(const float* Z, int64_t rows, int64_t d3, int64_t mul1, float* Zf,
                               void* stream);
 int gmp_tp_node_dw_f32(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H, int64_t mul_out,
                        const int64_t* eoff, const float* Z, const float* A, const float* G,

@@ -20,8 +20,10 @@ dev = "cuda"
 torch.manual_seed(0)
 N, E, m1, mo, H = 50_000, 1_000_000, 128, 128, 256
 K1 = m1 * H
-deg = torch.randint(12, 29, (N,))  # ~20 +- 5 (the radius graph's in-degrees)
-deg = (deg * (E / deg.sum())).round().long().clamp(min=0)
+DLO, DHI = (int(x) for x in os.environ.get("MB_DEG", "12,28").split(","))
+deg = torch.randint(DLO, DHI + 1, (N,))  # default ~20 +- 5 (the radius graph's in-degrees)
+if DLO != DHI:
+    deg = (deg * (E / deg.sum())).round().long().clamp(min=0)
 E = int(deg.sum())
 eoff = torch.zeros(N + 1, dtype=torch.int64, device=dev)
 eoff[1:] = torch.cumsum(deg, 0).to(dev)
@@ -58,9 +60,13 @@ for d3 in d3s:
         lib.gmp_tp_gemm_x3_f32(N * d3, mo, K1, _p(S), K1, m1, _p(Sb), m1, _p(Bf), K1 + m1,
                                mo * (K1 + m1), _p(out_u), d3, mo * d3, 1, d3, 1, _stream())
 
+    U = 16 // d3
+    Zf = torch.empty(lib.gmp_tp_z_fused_layout_floats(E + 1, d3, m1), device=dev)
+    lib.gmp_tp_z_fused_layout_f32(_p(Z), E + 1, d3, m1, _p(Zf), _stream())
+
     def fused():
-        lib.gmp_tp_node_fwd_fused_f32(N, d3, m1, H, mo, _p(eoff), _p(Z), _p(A), _p(Bf), _p(out_f),
-                                      mo * d3, _stream())
+        lib.gmp_tp_node_fwd_fused_f32(N, d3, m1, H, mo, _p(eoff), _p(Zf), E + 1, _p(A), _p(Bf),
+                                      _p(out_f), mo * d3, _stream())
 
     tu = timeit(unfused)
     del S, Sb
@@ -68,5 +74,7 @@ for d3 in d3s:
     rel = ((out_f - out_u).abs().max() / out_u.abs().max()).item()
     print(f"d3={d3}: unfused {tu:8.3f} ms ({fl / tu / 1e9:6.1f} TF)   fused {tf:8.3f} ms "
           f"({fl / tf / 1e9:6.1f} TF)   max rel diff {rel:.2e}", flush=True)
-    del Z, out_u, out_f
+    tl = timeit(lambda: lib.gmp_tp_z_fused_layout_f32(_p(Z), E + 1, d3, m1, _p(Zf), _stream()))
+    print(f"d3={d3}: z layout conversion {tl:8.3f} ms", flush=True)
+    del Z, Zf, out_u, out_f
     torch.cuda.empty_cache()

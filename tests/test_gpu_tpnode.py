@@ -366,7 +366,8 @@ def test_node_fwd_fused_matches_fp64(d3, mul1, H, mo, nrecv, seed):
     cldg, c0 = mo * d3 + 11, 7
     C0 = torch.randn(nrecv * cldg + c0 + 5, generator=g)
     C = C0.to(DEV)
-    tops.tp_node_fwd_fused(eoff.to(DEV), Z.to(DEV), A.to(DEV), Bf, d3, mul1, mo, C, c0, cldg)
+    Zf = tops.tp_z_fused_layout(Z.to(DEV), d3, mul1)
+    tops.tp_node_fwd_fused(eoff.to(DEV), Zf, A.to(DEV), Bf, d3, mul1, mo, C, c0, cldg)
     got = C.cpu().double()
     W2p = W2[off:off + mul1 * mo].double().view(mul1, mo, H)   # [u, w, j]
     b2p = b2[off:off + mul1 * mo].double().view(mul1, mo)      # [u, w]
@@ -388,5 +389,12 @@ def test_node_fwd_fused_matches_fp64(d3, mul1, H, mo, nrecv, seed):
     assert bool((err <= 4e-6 * bnd + 1e-6).all()), (err / bnd.clamp_min(1e-30)).max().item()
     # deterministic, and nothing outside the output block was touched
     C2 = C0.to(DEV)
-    tops.tp_node_fwd_fused(eoff.to(DEV), Z.to(DEV), A.to(DEV), Bf, d3, mul1, mo, C2, c0, cldg)
+    tops.tp_node_fwd_fused(eoff.to(DEV), Zf, A.to(DEV), Bf, d3, mul1, mo, C2, c0, cldg)
+    # the layout itself
+    U = 16 // d3
+    zf = Zf.cpu()
+    for us, e, c in ((0, 0, 0), (1, 3, 16 - 1), (Zf.shape[0] - 1, ne, d3 * U - 1), (2, 7, 5)):
+        k, u = c // U, us * U + c % U
+        want = Z[e, k * mul1 + u] if (k < d3 and u < mul1 and c < d3 * U) else 0.0
+        assert float(zf[us, e, c]) == float(want), (us, e, c)
     assert torch.equal(C2.cpu().double(), got)
