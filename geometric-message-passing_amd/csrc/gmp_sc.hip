@@ -1,228 +1,480 @@
 // K8: MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188,
-// element_dependent=False) for node features x (B, C, 9) = C channels of 0e+1o+2e (reshape_irreps,
-// irreps_tools.py:63-79), all three output irreps (0e, 1o, 2e; M = 1 + 3 + 5 = 9 rows) at once.
+// element_dependent=False) for node features x (B, C, D) = C channels of 0e+1o(+2e(+3o)) --
+// D = (L+1)^2 for max_ell L = 1, 2, 3 (reshape_irreps, irreps_tools.py:63-79) -- all L+1 output
+// irreps (M = D rows) at once.
 //
 // With the per-channel coefficient tensors A_nu[c] = sum_k U_nu[..., k] W_nu[k, c] (prepared by
-// the host), the reference's nested contraction ((A3 x + A2) x + A1) x is the polynomial
-//   out[b, c, m] = sum_ijk A3[c, m, ijk] x_i x_j x_k + sum_ij A2[c, m, ij] x_i x_j
-//                + sum_i A1[c, m, i] x_i          (x = x[b, c, :])
-// written directly in the mul_ir output layout [0e: c | 1o: C + 3c + m' | 2e: 4C + 5c + m''].
-// evaluated over the symmetric monomial basis below (the caller passes the folded coefficients).
-// One thread per (node, channel) with the channel's coefficients (219 x 9 floats, monomial-major)
-// in LDS.  Backward: dx by the product rule (same loop), dA~ = sum_b g[b,c,m] (monomial of
-// x[b,c]) reduced over node groups into per-group partials (summed in fixed order by the caller).
+// the host), the reference's nested contraction (((A4 x + A3) x + A2) x + A1) x is the polynomial
+//   out[b, c, m] = sum_{nu <= corr} sum_{i1..inu} A_nu[c, m, i1..inu] x_i1 ... x_inu
+// (x = x[b, c, :]) written directly in the mul_ir output layout [0e: c | 1o: C + 3c + m' |
+// 2e: 4C + 5c + m'' | 3o: 9C + 7c + m'''], evaluated over the symmetric monomial basis below
+// (the caller passes the folded coefficients).  One thread per (node, channel), grid-stride over
+// nodes, with the channel's coefficients (NQ x D floats, monomial-major) in LDS.  Backward: dx by
+// the product rule (same loop), dA~ = sum_b g[b,c,m] (monomial of x[b,c]) reduced over node groups
+// into per-group partials (summed in fixed order by the caller).
+#include <cstdlib>
+
 #include "gmp_common.h"
 
 namespace gmp {
 namespace {
 
-constexpr int kM = 9;                 // output rows (0e, 1o x3, 2e x5)
 // Symmetric monomial basis: x_i x_j x_k is symmetric in its indices, so the host folds every
 // permutation's coefficient into the sorted one (A~_nu[c, m, q] = sum over the distinct
 // permutations of q of A_nu[c, m, .]; exact algebra, fp32 re-association only) and the
-// contraction runs over 9 + 45 + 165 = 219 monomials instead of 9 + 81 + 729 = 819 (3.7x
-// fewer multiply-adds in all three kernels).  Order: deg1 i | deg2 i <= j | deg3 i <= j <= k,
-// lexicographic.
-constexpr int kQ1 = 9, kQ2 = 45, kQ3 = 165;
-constexpr int kQ = kQ1 + kQ2 + kQ3;   // 219
+// contraction runs over C(D + nu - 1, nu) monomials of degree nu instead of D^nu (D = 9, nu = 3:
+// 165 instead of 729).  Order: deg1 i | deg2 i <= j | deg3 i <= j <= k | deg4 i <= j <= k <= l,
+// lexicographic within a degree.
+__host__ __device__ constexpr int nq_deg(int D, int deg) {
+  return deg == 1 ? D
+       : deg == 2 ? D * (D + 1) / 2
+       : deg == 3 ? D * (D + 1) * (D + 2) / 6
+                  : D * (D + 1) * (D + 2) * (D + 3) / 24;
+}
+__host__ __device__ constexpr int nq_total(int D, int corr) {
+  return (corr >= 1 ? nq_deg(D, 1) : 0) + (corr >= 2 ? nq_deg(D, 2) : 0) +
+         (corr >= 3 ? nq_deg(D, 3) : 0) + (corr >= 4 ? nq_deg(D, 4) : 0);
+}
 constexpr int kSC = 256;
+constexpr int kNodeBlocks = 16;  // node blocks per channel (grid-stride: coefficients load once)
 
-template <int CORR>
-constexpr int nq() { return CORR == 1 ? kQ1 : (CORR == 2 ? kQ1 + kQ2 : kQ); }
+// compiled (D, corr): D in {4, 9, 16}; corr <= 4 for D <= 9, <= 3 for D = 16 (the D = 16, nu = 4
+// table, 4844 x 16 floats, exceeds LDS)
+__host__ __device__ constexpr bool sc_supported(int D, int corr) {
+  return corr >= 1 && ((D == 4 || D == 9) ? corr <= 4 : (D == 16 ? corr <= 3 : false));
+}
 
-// LDS coefficient layout: a[q * 9 + m] (monomial-major: one q's 9 rows are contiguous and every
+// LDS coefficient layout: a[q * D + m] (monomial-major: one q's D rows are contiguous and every
 // lane of the block reads the same address -> broadcast reads)
-template <int CORR>
+template <int D, int CORR>
 __device__ __forceinline__ void load_coeffs(int c, const float* __restrict__ A1,
                                             const float* __restrict__ A2,
-                                            const float* __restrict__ A3, float* a) {
-  for (int e = threadIdx.x; e < kM * kQ1; e += blockDim.x) {
-    const int m = e / kQ1, q = e - m * kQ1;
-    a[q * kM + m] = A1[((int64_t)c * kM + m) * kQ1 + q];
+                                            const float* __restrict__ A3,
+                                            const float* __restrict__ A4, float* a) {
+  const float* As[4] = {A1, A2, A3, A4};
+  int q0 = 0;
+#pragma unroll
+  for (int nu = 1; nu <= CORR; ++nu) {
+    const int nqd = nq_deg(D, nu);
+    const float* An = As[nu - 1];
+    for (int e = threadIdx.x; e < D * nqd; e += blockDim.x) {
+      const int m = e / nqd, q = e - m * nqd;
+      a[(q0 + q) * D + m] = An[((int64_t)c * D + m) * nqd + q];
+    }
+    q0 += nqd;
   }
-  if (CORR >= 2)
-    for (int e = threadIdx.x; e < kM * kQ2; e += blockDim.x) {
-      const int m = e / kQ2, q = e - m * kQ2;
-      a[(kQ1 + q) * kM + m] = A2[((int64_t)c * kM + m) * kQ2 + q];
-    }
-  if (CORR >= 3)
-    for (int e = threadIdx.x; e < kM * kQ3; e += blockDim.x) {
-      const int m = e / kQ3, q = e - m * kQ3;
-      a[(kQ1 + kQ2 + q) * kM + m] = A3[((int64_t)c * kM + m) * kQ3 + q];
-    }
 }
 
+// output column of row m (irrep block l = floor(sqrt(m)), component m - l^2) of channel c
 __device__ __forceinline__ int out_col(int C, int c, int m) {
-  return m == 0 ? c : (m < 4 ? C + 3 * c + (m - 1) : 4 * C + 5 * c + (m - 4));
+  const int l = m >= 9 ? 3 : (m >= 4 ? 2 : (m >= 1 ? 1 : 0));
+  return l * l * C + (2 * l + 1) * c + (m - l * l);
 }
 
-// visit every monomial q (in basis order) with its factors: f(q, z, i, j, k, deg)
-template <int CORR, class F>
-__device__ __forceinline__ void for_monomials(const float (&xv)[9], F&& f) {
+// visit every monomial q (in basis order) with its factor indices: f(q, z, i, j, k, l, deg)
+template <int D, int CORR, class F>
+__device__ __forceinline__ void for_monomials(const float (&xv)[D], F&& f) {
 #pragma unroll
-  for (int i = 0; i < 9; ++i) f(i, xv[i], i, 0, 0, 1);
-  if (CORR >= 2) {
-    int q = kQ1;
+  for (int i = 0; i < D; ++i) f(i, xv[i], i, 0, 0, 0, 1);
+  if constexpr (CORR >= 2) {
+    int q = nq_deg(D, 1);
 #pragma unroll
-    for (int i = 0; i < 9; ++i)
+    for (int i = 0; i < D; ++i)
 #pragma unroll
-      for (int j = i; j < 9; ++j) {
-        f(q, xv[i] * xv[j], i, j, 0, 2);
+      for (int j = i; j < D; ++j) {
+        f(q, xv[i] * xv[j], i, j, 0, 0, 2);
         ++q;
       }
   }
-  if (CORR >= 3) {
-    int q = kQ1 + kQ2;
+  if constexpr (CORR >= 3) {
+    int q = nq_total(D, 2);
 #pragma unroll
-    for (int i = 0; i < 9; ++i)
+    for (int i = 0; i < D; ++i)
 #pragma unroll
-      for (int j = i; j < 9; ++j) {
+      for (int j = i; j < D; ++j) {
         const float xij = xv[i] * xv[j];
 #pragma unroll
-        for (int k = j; k < 9; ++k) {
-          f(q, xij * xv[k], i, j, k, 3);
+        for (int k = j; k < D; ++k) {
+          f(q, xij * xv[k], i, j, k, 0, 3);
           ++q;
+        }
+      }
+  }
+  if constexpr (CORR >= 4) {
+    int q = nq_total(D, 3);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int j = i; j < D; ++j) {
+        const float xij = xv[i] * xv[j];
+#pragma unroll
+        for (int k = j; k < D; ++k) {
+          const float xijk = xij * xv[k];
+#pragma unroll
+          for (int l = k; l < D; ++l) {
+            f(q, xijk * xv[l], i, j, k, l, 4);
+            ++q;
+          }
         }
       }
   }
 }
 
-template <int CORR>
+template <int D, int CORR>
 __global__ __launch_bounds__(kSC) void sc_fwd_kernel(int64_t B, int C, const float* __restrict__ x,
                                                      const float* __restrict__ A1,
                                                      const float* __restrict__ A2,
                                                      const float* __restrict__ A3,
+                                                     const float* __restrict__ A4,
                                                      float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float a[kQ * kM];
+  extern __shared__ __attribute__((aligned(16))) float a[];
   const int c = blockIdx.y;
-  load_coeffs<CORR>(c, A1, A2, A3, a);
+  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
   __syncthreads();
-  const int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x;
-  if (b >= B) return;
-  float xv[9];
-  const float* xr = x + (b * C + c) * 9;
+  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
+    float xv[D];
+    const float* xr = x + (b * C + c) * D;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) xv[i] = xr[i];
-  float acc[kM];
+    for (int i = 0; i < D; ++i) xv[i] = xr[i];
+    float acc[D];
 #pragma unroll
-  for (int m = 0; m < kM; ++m) acc[m] = 0.f;
-  for_monomials<CORR>(xv, [&](int q, float z, int, int, int, int) {
-    const float* ar = a + q * kM;
+    for (int m = 0; m < D; ++m) acc[m] = 0.f;
+    for_monomials<D, CORR>(xv, [&](int q, float z, int, int, int, int, int) {
+      const float* ar = a + q * D;
 #pragma unroll
-    for (int m = 0; m < kM; ++m) acc[m] += ar[m] * z;
-  });
-  float* orow = out + b * (int64_t)(9 * C);
+      for (int m = 0; m < D; ++m) acc[m] += ar[m] * z;
+    });
+    float* orow = out + b * (int64_t)(D * C);
 #pragma unroll
-  for (int m = 0; m < kM; ++m) orow[out_col(C, c, m)] = acc[m];
+    for (int m = 0; m < D; ++m) orow[out_col(C, c, m)] = acc[m];
+  }
 }
 
-template <int CORR>
+template <int D, int CORR>
 __global__ __launch_bounds__(kSC) void sc_bwd_x_kernel(int64_t B, int C,
                                                        const float* __restrict__ x,
                                                        const float* __restrict__ A1,
                                                        const float* __restrict__ A2,
                                                        const float* __restrict__ A3,
+                                                       const float* __restrict__ A4,
                                                        const float* __restrict__ gout,
                                                        float* __restrict__ dx) {
-  __shared__ __attribute__((aligned(16))) float a[kQ * kM];
+  extern __shared__ __attribute__((aligned(16))) float a[];
   const int c = blockIdx.y;
-  load_coeffs<CORR>(c, A1, A2, A3, a);
+  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
   __syncthreads();
-  const int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x;
-  if (b >= B) return;
-  float xv[9], g[kM], d[9];
-  const float* xr = x + (b * C + c) * 9;
-  const float* gr = gout + b * (int64_t)(9 * C);
+  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
+    float xv[D], g[D], d[D];
+    const float* xr = x + (b * C + c) * D;
+    const float* gr = gout + b * (int64_t)(D * C);
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    xv[i] = xr[i];
-    d[i] = 0.f;
-  }
-#pragma unroll
-  for (int m = 0; m < kM; ++m) g[m] = gr[out_col(C, c, m)];
-  // d/dx_t of (gA_q * x_i x_j x_k) = gA_q * (x_j x_k [t = i] + x_i x_k [t = j] + x_i x_j [t = k])
-  // (repeated indices add up to the power rule)
-  for_monomials<CORR>(xv, [&](int q, float, int i, int j, int k, int deg) {
-    const float* ar = a + q * kM;
-    float gA = 0.f;
-#pragma unroll
-    for (int m = 0; m < kM; ++m) gA += ar[m] * g[m];
-    if (deg == 1) {
-      d[i] += gA;
-    } else if (deg == 2) {
-      d[i] += gA * xv[j];
-      d[j] += gA * xv[i];
-    } else {
-      d[i] += gA * (xv[j] * xv[k]);
-      d[j] += gA * (xv[i] * xv[k]);
-      d[k] += gA * (xv[i] * xv[j]);
+    for (int i = 0; i < D; ++i) {
+      xv[i] = xr[i];
+      d[i] = 0.f;
     }
-  });
-  float* dr = dx + (b * C + c) * 9;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) dr[i] = d[i];
+    for (int m = 0; m < D; ++m) g[m] = gr[out_col(C, c, m)];
+    // d/dx_t of (gA_q x_i x_j x_k x_l) = gA_q (the product of the other factors) for each
+    // factor equal to t (repeated indices add up to the power rule)
+    for_monomials<D, CORR>(xv, [&](int q, float, int i, int j, int k, int l, int deg) {
+      const float* ar = a + q * D;
+      float gA = 0.f;
+#pragma unroll
+      for (int m = 0; m < D; ++m) gA += ar[m] * g[m];
+      if (deg == 1) {
+        d[i] += gA;
+      } else if (deg == 2) {
+        d[i] += gA * xv[j];
+        d[j] += gA * xv[i];
+      } else if (deg == 3) {
+        d[i] += gA * (xv[j] * xv[k]);
+        d[j] += gA * (xv[i] * xv[k]);
+        d[k] += gA * (xv[i] * xv[j]);
+      } else {
+        const float xij = xv[i] * xv[j], xkl = xv[k] * xv[l];
+        d[i] += gA * (xv[j] * xkl);
+        d[j] += gA * (xv[i] * xkl);
+        d[k] += gA * (xij * xv[l]);
+        d[l] += gA * (xij * xv[k]);
+      }
+    });
+    float* dr = dx + (b * C + c) * D;
+#pragma unroll
+    for (int i = 0; i < D; ++i) dr[i] = d[i];
+  }
+}
+
+// Runtime-loop forms (D = 4, 16 and correlation 4): the fully unrolled monomial walk above is
+// kept for the benchmarked D = 9, correlation <= 3 (config C4); the others walk the same basis in
+// the same order with rolled loops (compile time), this thread's x and dx in a private LDS row.
+template <int D, int CORR, class F>
+__device__ __forceinline__ void for_monomials_rt(const float* xv, F&& f) {
+  int q = 0;
+#pragma unroll 1
+  for (int i = 0; i < D; ++i) f(q++, xv[i], i, 0, 0, 0, 1);
+  if constexpr (CORR >= 2) {
+#pragma unroll 1
+    for (int i = 0; i < D; ++i)
+#pragma unroll 1
+      for (int j = i; j < D; ++j) f(q++, xv[i] * xv[j], i, j, 0, 0, 2);
+  }
+  if constexpr (CORR >= 3) {
+#pragma unroll 1
+    for (int i = 0; i < D; ++i)
+#pragma unroll 1
+      for (int j = i; j < D; ++j) {
+        const float xij = xv[i] * xv[j];
+#pragma unroll 1
+        for (int k = j; k < D; ++k) f(q++, xij * xv[k], i, j, k, 0, 3);
+      }
+  }
+  if constexpr (CORR >= 4) {
+#pragma unroll 1
+    for (int i = 0; i < D; ++i)
+#pragma unroll 1
+      for (int j = i; j < D; ++j) {
+        const float xij = xv[i] * xv[j];
+#pragma unroll 1
+        for (int k = j; k < D; ++k) {
+          const float xijk = xij * xv[k];
+#pragma unroll 1
+          for (int l = k; l < D; ++l) f(q++, xijk * xv[l], i, j, k, l, 4);
+        }
+      }
+  }
+}
+
+template <int D, int CORR>
+__global__ __launch_bounds__(kSC) void sc_fwd_rt_kernel(int64_t B, int C,
+                                                        const float* __restrict__ x,
+                                                        const float* __restrict__ A1,
+                                                        const float* __restrict__ A2,
+                                                        const float* __restrict__ A3,
+                                                        const float* __restrict__ A4,
+                                                        float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float a[];
+  float* xt = a + nq_total(D, CORR) * D + threadIdx.x * (D + 1);  // this thread's x row
+  const int c = blockIdx.y;
+  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
+  __syncthreads();
+  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
+    const float* xr = x + (b * C + c) * D;
+    for (int i = 0; i < D; ++i) xt[i] = xr[i];
+    float acc[D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) acc[m] = 0.f;
+    for_monomials_rt<D, CORR>(xt, [&](int q, float z, int, int, int, int, int) {
+      const float* ar = a + q * D;
+#pragma unroll
+      for (int m = 0; m < D; ++m) acc[m] += ar[m] * z;
+    });
+    float* orow = out + b * (int64_t)(D * C);
+#pragma unroll
+    for (int m = 0; m < D; ++m) orow[out_col(C, c, m)] = acc[m];
+  }
+}
+
+template <int D, int CORR>
+__global__ __launch_bounds__(kSC) void sc_bwd_x_rt_kernel(int64_t B, int C,
+                                                          const float* __restrict__ x,
+                                                          const float* __restrict__ A1,
+                                                          const float* __restrict__ A2,
+                                                          const float* __restrict__ A3,
+                                                          const float* __restrict__ A4,
+                                                          const float* __restrict__ gout,
+                                                          float* __restrict__ dx) {
+  extern __shared__ __attribute__((aligned(16))) float a[];
+  float* xt = a + nq_total(D, CORR) * D + threadIdx.x * (2 * D + 1);  // x row | dx row
+  float* dt = xt + D;
+  const int c = blockIdx.y;
+  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
+  __syncthreads();
+  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
+    float g[D];
+    const float* xr = x + (b * C + c) * D;
+    const float* gr = gout + b * (int64_t)(D * C);
+    for (int i = 0; i < D; ++i) {
+      xt[i] = xr[i];
+      dt[i] = 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < D; ++m) g[m] = gr[out_col(C, c, m)];
+    for_monomials_rt<D, CORR>(xt, [&](int q, float, int i, int j, int k, int l, int deg) {
+      const float* ar = a + q * D;
+      float gA = 0.f;
+#pragma unroll
+      for (int m = 0; m < D; ++m) gA += ar[m] * g[m];
+      if (deg == 1) {
+        dt[i] += gA;
+      } else if (deg == 2) {
+        dt[i] += gA * xt[j];
+        dt[j] += gA * xt[i];
+      } else if (deg == 3) {
+        dt[i] += gA * (xt[j] * xt[k]);
+        dt[j] += gA * (xt[i] * xt[k]);
+        dt[k] += gA * (xt[i] * xt[j]);
+      } else {
+        const float xij = xt[i] * xt[j], xkl = xt[k] * xt[l];
+        dt[i] += gA * (xt[j] * xkl);
+        dt[j] += gA * (xt[i] * xkl);
+        dt[k] += gA * (xij * xt[l]);
+        dt[l] += gA * (xij * xt[k]);
+      }
+    });
+    float* dr = dx + (b * C + c) * D;
+    for (int i = 0; i < D; ++i) dr[i] = dt[i];
+  }
+}
+
+// factor indices of monomial q of degree deg (q counted within its degree, lexicographic)
+__device__ __forceinline__ void decode_monomial(int D, int deg, int r, int (&f)[4]) {
+  int lo = 0;
+  for (int t = 0; t < deg; ++t) {
+    // number of sorted (deg - t - 1)-tuples over [v, D) for each candidate first index v
+    const int rest = deg - t - 1;
+    int v = lo;
+    while (true) {
+      const int n = D - v;  // values available from v on
+      int cnt = 1;          // C(n - 1 + rest, rest): sorted tuples starting with v
+      for (int s = 1; s <= rest; ++s) cnt = cnt * (n - 1 + s) / s;
+      if (r < cnt) break;
+      r -= cnt;
+      ++v;
+    }
+    f[t] = v;
+    lo = v;
+  }
 }
 
 // dA~ partials: part[grp, c, m, q] = sum_{b in group grp} g[b, c, m] * mono_q(x[b, c]).
-// One thread per monomial q (its factor indices fixed) and all 9 rows m; nodes staged through
+// Thread t owns monomials t, t + kSC, ... (QPT of them) and all D rows m; nodes staged through
 // LDS in batches, their x and g rows read as broadcasts.
 constexpr int kNodeBatch = 32;
 
-template <int CORR>
+template <int D, int CORR>
 __global__ __launch_bounds__(kSC) void sc_bwd_a_kernel(int64_t B, int C, int64_t nodes_per_group,
                                                        const float* __restrict__ x,
                                                        const float* __restrict__ gout,
                                                        float* __restrict__ part) {
-  constexpr int NQ = nq<CORR>();
-  __shared__ float xs[kNodeBatch][9];
-  __shared__ float gs[kNodeBatch][kM];
+  constexpr int NQ = nq_total(D, CORR);
+  constexpr int QPT = (NQ + kSC - 1) / kSC;
+  __shared__ float xs[kNodeBatch][D];
+  __shared__ float gs[kNodeBatch][D];
   const int c = blockIdx.y;
   const int64_t grp = blockIdx.x;
   const int64_t b0 = grp * nodes_per_group;
   const int64_t b1 = (b0 + nodes_per_group < B) ? b0 + nodes_per_group : B;
-  // this thread's monomial (q < NQ): factor indices (i, j, k) and degree
-  const int q = threadIdx.x;
-  int fi = 0, fj = 0, fk = 0, deg = 0;
-  if (q < kQ1) {
-    fi = q; deg = 1;
-  } else if (q < kQ1 + kQ2) {
-    int r = q - kQ1, i = 0;
-    while (r >= 9 - i) { r -= 9 - i; ++i; }
-    fi = i; fj = i + r; deg = 2;
-  } else if (q < kQ) {
-    int r = q - kQ1 - kQ2, i = 0;
-    while (r >= (9 - i) * (10 - i) / 2) { r -= (9 - i) * (10 - i) / 2; ++i; }
-    int j = i;
-    while (r >= 9 - j) { r -= 9 - j; ++j; }
-    fi = i; fj = j; fk = j + r; deg = 3;
-  }
-  float acc[kM];
+  int fac[QPT][4], deg[QPT];
 #pragma unroll
-  for (int m = 0; m < kM; ++m) acc[m] = 0.f;
+  for (int u = 0; u < QPT; ++u) {
+    const int q = threadIdx.x + u * kSC;
+    fac[u][0] = fac[u][1] = fac[u][2] = fac[u][3] = 0;
+    deg[u] = 0;
+    int r = q;
+    for (int dg = 1; dg <= CORR && q < NQ; ++dg) {
+      if (r < nq_deg(D, dg)) {
+        deg[u] = dg;
+        decode_monomial(D, dg, r, fac[u]);
+        break;
+      }
+      r -= nq_deg(D, dg);
+    }
+  }
+  float acc[QPT][D];
+#pragma unroll
+  for (int u = 0; u < QPT; ++u)
+#pragma unroll
+    for (int m = 0; m < D; ++m) acc[u][m] = 0.f;
   for (int64_t bb = b0; bb < b1; bb += kNodeBatch) {
     const int nb = (int)((b1 - bb) < kNodeBatch ? (b1 - bb) : kNodeBatch);
     __syncthreads();
-    for (int e = threadIdx.x; e < kNodeBatch * 9; e += kSC) {
-      const int n = e / 9, t = e - n * 9;
-      xs[n][t] = (n < nb) ? x[((bb + n) * C + c) * 9 + t] : 0.f;
-      gs[n][t] = (n < nb) ? gout[(bb + n) * (int64_t)(9 * C) + out_col(C, c, t)] : 0.f;
+    for (int e = threadIdx.x; e < kNodeBatch * D; e += kSC) {
+      const int n = e / D, t = e - n * D;
+      xs[n][t] = (n < nb) ? x[((bb + n) * C + c) * D + t] : 0.f;
+      gs[n][t] = (n < nb) ? gout[(bb + n) * (int64_t)(D * C) + out_col(C, c, t)] : 0.f;
     }
     __syncthreads();
-    if (q < NQ) {
-      for (int n = 0; n < nb; ++n) {
-        float z = xs[n][fi];
-        if (deg >= 2) z *= xs[n][fj];
-        if (deg >= 3) z *= xs[n][fk];
+    for (int n = 0; n < nb; ++n) {
 #pragma unroll
-        for (int m = 0; m < kM; ++m) acc[m] += gs[n][m] * z;
+      for (int u = 0; u < QPT; ++u) {
+        if (deg[u] == 0) continue;
+        float z = xs[n][fac[u][0]];
+        if (deg[u] >= 2) z *= xs[n][fac[u][1]];
+        if (deg[u] >= 3) z *= xs[n][fac[u][2]];
+        if (deg[u] >= 4) z *= xs[n][fac[u][3]];
+#pragma unroll
+        for (int m = 0; m < D; ++m) acc[u][m] += gs[n][m] * z;
       }
     }
   }
-  if (q < NQ) {
-    float* pr = part + (grp * C + c) * (int64_t)(kM * NQ);
+  float* pr = part + (grp * C + c) * (int64_t)(D * NQ);
 #pragma unroll
-    for (int m = 0; m < kM; ++m) pr[m * NQ + q] = acc[m];
+  for (int u = 0; u < QPT; ++u) {
+    const int q = threadIdx.x + u * kSC;
+    if (q >= NQ) continue;
+#pragma unroll
+    for (int m = 0; m < D; ++m) pr[m * NQ + q] = acc[u][m];
   }
+}
+
+// GMP_SC_ROLLED=1: the rolled-loop kernels for D = 9, correlation <= 3 as well (A/B)
+int g_sc_rolled = getenv("GMP_SC_ROLLED") ? atoi(getenv("GMP_SC_ROLLED")) : 0;
+
+template <int D, int CORR>
+int sc_launch(int64_t n_nodes, int channels, const float* x, const float* A1, const float* A2,
+              const float* A3, const float* A4, float* out, const float* gout, float* dx,
+              float* dA_partials, hipStream_t s) {
+  constexpr int NQ = nq_total(D, CORR);
+  constexpr bool kFull = D == 9 && CORR <= 3;  // unrolled walk (config C4) vs rolled loops
+  const bool full = kFull && !g_sc_rolled;
+  const int smem_f = (NQ * D + (full ? 0 : kSC * (D + 1))) * 4;
+  const int smem_b = (NQ * D + (full ? 0 : kSC * (2 * D + 1))) * 4;
+  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(n_nodes, kSC), kNodeBlocks),
+                  (unsigned)channels);
+  int rc;
+  auto fwd_k = sc_fwd_rt_kernel<D, CORR>;
+  auto bwd_k = sc_bwd_x_rt_kernel<D, CORR>;
+  if constexpr (kFull) {
+    if (full) {
+      fwd_k = sc_fwd_kernel<D, CORR>;
+      bwd_k = sc_bwd_x_kernel<D, CORR>;
+    }
+  }
+  if (out) {
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)fwd_k,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem_f))))
+      return rc;
+    fwd_k<<<grid, kSC, smem_f, s>>>(n_nodes, channels, x, A1, A2, A3, A4, out);
+    if ((rc = launch_status())) return rc;
+  }
+  if (dx) {
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)bwd_k,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem_b))))
+      return rc;
+    bwd_k<<<grid, kSC, smem_b, s>>>(n_nodes, channels, x, A1, A2, A3, A4, gout, dx);
+    if ((rc = launch_status())) return rc;
+  }
+  if (dA_partials) {
+    const int G = gmp_sc_groups(n_nodes);
+    const int64_t per = ceil_div(n_nodes, (int64_t)G);
+    sc_bwd_a_kernel<D, CORR><<<dim3((unsigned)G, (unsigned)channels), kSC, 0, s>>>(
+        n_nodes, channels, per, x, gout, dA_partials);
+    if ((rc = launch_status())) return rc;
+  }
+  return GMP_OK;
+}
+
+int sc_dispatch(int64_t n_nodes, int channels, int dim, int corr, const float* x,
+                const float* A1, const float* A2, const float* A3, const float* A4, float* out,
+                const float* gout, float* dx, float* dA_partials, hipStream_t s) {
+#define GMP_SC(DD, CR)                                                                     \
+  if (dim == DD && corr == CR)                                                             \
+    return sc_launch<DD, CR>(n_nodes, channels, x, A1, A2, A3, A4, out, gout, dx, dA_partials, s);
+  GMP_SC(9, 1) GMP_SC(9, 2) GMP_SC(9, 3) GMP_SC(9, 4)
+  GMP_SC(4, 1) GMP_SC(4, 2) GMP_SC(4, 3) GMP_SC(4, 4)
+  GMP_SC(16, 1) GMP_SC(16, 2) GMP_SC(16, 3)
+#undef GMP_SC
+  return GMP_ERR_UNSUPPORTED;
 }
 
 }  // namespace
@@ -239,53 +491,34 @@ int gmp_sc_groups(int64_t n_nodes) {
   return (int)(g < 1 ? 1 : g);
 }
 
-int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int correlation,
-                                      const float* x, const float* A1, const float* A2,
-                                      const float* A3, float* out, void* stream) {
-  GMP_CHECK_ARG(n_nodes >= 0 && channels > 0 && channels <= 65535);
-  GMP_CHECK_ARG(correlation >= 1 && correlation <= 3);
-  GMP_CHECK_ARG(x && A1 && out && (correlation < 2 || A2) && (correlation < 3 || A3));
-  if (n_nodes == 0) return GMP_OK;
-  const dim3 grid((unsigned)ceil_div(n_nodes, kSC), (unsigned)channels);
-  hipStream_t s = as_stream(stream);
-#define GMP_SC_FWD(CR) \
-  sc_fwd_kernel<CR><<<grid, kSC, 0, s>>>(n_nodes, channels, x, A1, A2, A3, out);
-  if (correlation == 3) { GMP_SC_FWD(3) } else if (correlation == 2) { GMP_SC_FWD(2) } else { GMP_SC_FWD(1) }
-#undef GMP_SC_FWD
-  return launch_status();
+int gmp_sc_monomials(int dim, int correlation) {
+  return sc_supported(dim, correlation) ? nq_total(dim, correlation) : -1;
 }
 
-int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int correlation,
+int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
                                       const float* x, const float* A1, const float* A2,
-                                      const float* A3, const float* gout, float* dx,
-                                      float* dA_partials, void* stream) {
+                                      const float* A3, const float* A4, float* out,
+                                      void* stream) {
   GMP_CHECK_ARG(n_nodes >= 0 && channels > 0 && channels <= 65535);
-  GMP_CHECK_ARG(correlation >= 1 && correlation <= 3);
-  GMP_CHECK_ARG(x && A1 && gout && (correlation < 2 || A2) && (correlation < 3 || A3));
+  if (!sc_supported(dim, correlation)) return GMP_ERR_UNSUPPORTED;
+  GMP_CHECK_ARG(x && A1 && out && (correlation < 2 || A2) && (correlation < 3 || A3) &&
+                (correlation < 4 || A4));
   if (n_nodes == 0) return GMP_OK;
-  hipStream_t s = as_stream(stream);
-  int rc;
-  if (dx) {
-    const dim3 grid((unsigned)ceil_div(n_nodes, kSC), (unsigned)channels);
-#define GMP_SC_BWDX(CR) \
-  sc_bwd_x_kernel<CR><<<grid, kSC, 0, s>>>(n_nodes, channels, x, A1, A2, A3, gout, dx);
-    if (correlation == 3) { GMP_SC_BWDX(3) } else if (correlation == 2) { GMP_SC_BWDX(2) } else { GMP_SC_BWDX(1) }
-#undef GMP_SC_BWDX
-    if ((rc = launch_status())) return rc;
-  }
-  if (dA_partials) {
-    const int G = gmp_sc_groups(n_nodes);
-    const int64_t per = ceil_div(n_nodes, G);
-    const dim3 grid((unsigned)G, (unsigned)channels);
-    if (correlation == 3)
-      sc_bwd_a_kernel<3><<<grid, kSC, 0, s>>>(n_nodes, channels, per, x, gout, dA_partials);
-    else if (correlation == 2)
-      sc_bwd_a_kernel<2><<<grid, kSC, 0, s>>>(n_nodes, channels, per, x, gout, dA_partials);
-    else
-      sc_bwd_a_kernel<1><<<grid, kSC, 0, s>>>(n_nodes, channels, per, x, gout, dA_partials);
-    if ((rc = launch_status())) return rc;
-  }
-  return GMP_OK;
+  return sc_dispatch(n_nodes, channels, dim, correlation, x, A1, A2, A3, A4, out, nullptr,
+                     nullptr, nullptr, as_stream(stream));
+}
+
+int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
+                                      const float* x, const float* A1, const float* A2,
+                                      const float* A3, const float* A4, const float* gout,
+                                      float* dx, float* dA_partials, void* stream) {
+  GMP_CHECK_ARG(n_nodes >= 0 && channels > 0 && channels <= 65535);
+  if (!sc_supported(dim, correlation)) return GMP_ERR_UNSUPPORTED;
+  GMP_CHECK_ARG(x && A1 && gout && (correlation < 2 || A2) && (correlation < 3 || A3) &&
+                (correlation < 4 || A4));
+  if (n_nodes == 0) return GMP_OK;
+  return sc_dispatch(n_nodes, channels, dim, correlation, x, A1, A2, A3, A4, nullptr, gout, dx,
+                     dA_partials, as_stream(stream));
 }
 
 }  // extern "C"

@@ -21,8 +21,8 @@
 namespace gmp {
 namespace {
 
-constexpr int kMaxPaths = 32;   // TFN / MACE at l <= 3: 27 paths
-constexpr int kMaxBlocks = 6;   // output irreps blocks (TFN gated l <= 3: 0e, 0e, 1o, 2e, 3o)
+constexpr int kMaxPaths = 48;   // TFN / MACE at l <= 3: 27 paths; both parities, gated: 33
+constexpr int kMaxBlocks = 8;   // output irreps blocks (TFN gated both parities l <= 2: 7)
 constexpr int kMaxSh = 16;      // SH components (l <= 3) of the node-form z kernels
 constexpr int kMaxCg = 4096;    // CG floats of a descriptor (TFN l <= 3: 1,959)
 constexpr int kMaxIn = 1152;     // max in1 row dim
@@ -529,8 +529,9 @@ bool desc_ok(const Desc& d, int layout) {
 
 // node-form z / dz kernels: any output block structure (the path GEMMs scatter the outputs),
 // l <= 3 everywhere (paths are checked by the host plan), SH rows of (lmax + 1)^2 floats
+// (x rows are read straight from global memory: no LDS bound on in_dim)
 bool desc_ok_z(const Desc& d) {
-  return d.n_paths > 0 && d.n_paths <= kMaxPaths && d.in_dim > 0 && d.in_dim <= kMaxIn &&
+  return d.n_paths > 0 && d.n_paths <= kMaxPaths && d.in_dim > 0 && d.in_dim <= (1 << 16) &&
          (d.sh_dim == 1 || d.sh_dim == 4 || d.sh_dim == 9 || d.sh_dim == kMaxSh) &&
          d.z_size > 0 && d.n_blocks > 0 && d.n_blocks <= kMaxBlocks;
 }
@@ -724,21 +725,29 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
   const int64_t ne = e1 - e0;
   const int64_t nw = (int64_t)gridDim.x * 4;
   // input blocks (one per l1, as the path table lays them out; wave-uniform): the dx row is
-  // written block by block, entries of the row no path reads are written as zero
+  // written block by block, entries of the row no path reads are written as zero.  Input irreps
+  // with a repeated l (both parities: 0e + 0o, ..) take the grouped form: per input block (its
+  // first path, sblk) the paths reading it accumulate in registers, then the block is stored.
+  __shared__ int sblk[kMaxPaths + 1];  // [count, first path of each distinct input block ..]
   int xoff[4] = {-1, -1, -1, -1}, xmul[4] = {0, 0, 0, 0};
+  bool grouped = false;
   for (int p = 0; p < d.n_paths; ++p) {
     const Path P = paths[p];
+    grouped |= xoff[P.l1] >= 0 && xoff[P.l1] != P.x_off;
     xoff[P.l1] = P.x_off;
     xmul[P.l1] = P.mul1;
   }
-  for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
-    const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
-    const int64_t src = src_sorted[e], eo = perm[e];
-    float Y[kMaxSh], dyp[kMaxSh];
-    load_y(sh, eo, d.sh_dim, Y);
-#pragma unroll
-    for (int j = 0; j < kMaxSh; ++j) dyp[j] = 0.f;
-    DxAcc dx;
+  if (grouped && threadIdx.x == 0) {
+    int nb = 0;
+    for (int p = 0; p < d.n_paths; ++p) {
+      bool first = true;
+      for (int q = 0; q < p; ++q) first &= paths[q].x_off != paths[p].x_off;
+      if (first) sblk[1 + nb++] = p;
+    }
+    sblk[0] = nb;
+  }
+  __syncthreads();
+  auto zero_dx = [&](DxAcc& dx) {
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu) {
       dx.d0[uu] = 0.f;
@@ -749,9 +758,19 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < 7; ++i) dx.d3[uu][i] = 0.f;
     }
+  };
+  for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
+    const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
+    const int64_t src = src_sorted[e], eo = perm[e];
+    float Y[kMaxSh], dyp[kMaxSh];
+    load_y(sh, eo, d.sh_dim, Y);
+#pragma unroll
+    for (int j = 0; j < kMaxSh; ++j) dyp[j] = 0.f;
+    DxAcc dx;
+    zero_dx(dx);
     const float* xrow = x + src * d.in_dim;
-    for (int p = 0; p < d.n_paths; ++p) {
-      const Path P = paths[p];
+    float* dxr = dx_edge + k * d.in_dim;
+    auto run_path = [&](const Path& P) {
       const float* C = sC + P.cg_off;
       const float* dzr =
           dzbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
@@ -768,31 +787,54 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
 #undef GMP_ZB_CASE3
         default: break;
       }
+    };
+    // this lane's channels of input block (offset, mul, l) from the l-slot of dx
+    auto store_block = [&](int off, int mul, int l) {
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+        const int u = lane + 64 * uu;
+        if (u >= mul) continue;
+        if (l == 0) {
+          dxr[off + u] = dx.d0[uu];
+        } else if (l == 1) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) dxr[off + 3 * u + i] = dx.d1[uu][i];
+        } else if (l == 2) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) dxr[off + 5 * u + i] = dx.d2[uu][i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 7; ++i) dxr[off + 7 * u + i] = dx.d3[uu][i];
+        }
+      }
+    };
+    int covered = 0;
+    if (!grouped) {
+      for (int p = 0; p < d.n_paths; ++p) run_path(paths[p]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (xoff[b] >= 0) store_block(xoff[b], xmul[b], b);
+      covered = xmul[0] + 3 * xmul[1] + 5 * xmul[2] + 7 * xmul[3];
+    } else {
+      const int nb = sblk[0];
+      for (int b = 0; b < nb; ++b) {
+        const Path Pb = paths[sblk[1 + b]];
+        zero_dx(dx);
+        for (int p = sblk[1 + b]; p < d.n_paths; ++p) {
+          const Path P = paths[p];
+          if (P.x_off == Pb.x_off) run_path(P);
+        }
+        store_block(Pb.x_off, Pb.mul1, Pb.l1);
+        covered += Pb.mul1 * (2 * Pb.l1 + 1);
+      }
     }
-    float* dxr = dx_edge + k * d.in_dim;
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu) {
-      const int u = lane + 64 * uu;
-      if (xoff[0] >= 0 && u < xmul[0]) dxr[xoff[0] + u] = dx.d0[uu];
-      if (xoff[1] >= 0 && u < xmul[1]) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) dxr[xoff[1] + 3 * u + i] = dx.d1[uu][i];
-      }
-      if (xoff[2] >= 0 && u < xmul[2]) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) dxr[xoff[2] + 5 * u + i] = dx.d2[uu][i];
-      }
-      if (xoff[3] >= 0 && u < xmul[3]) {
-#pragma unroll
-        for (int i = 0; i < 7; ++i) dxr[xoff[3] + 7 * u + i] = dx.d3[uu][i];
-      }
-    }
-    if (xmul[0] + 3 * xmul[1] + 5 * xmul[2] + 7 * xmul[3] != d.in_dim) {
+    if (covered != d.in_dim) {
       for (int c = lane; c < d.in_dim; c += 64) {  // rows read by no path: zero
         bool in = false;
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          in |= xoff[b] >= 0 && c >= xoff[b] && c < xoff[b] + xmul[b] * (2 * b + 1);
+        for (int p = 0; p < d.n_paths; ++p) {
+          const Path P = paths[p];
+          in |= c >= P.x_off && c < P.x_off + P.mul1 * (2 * P.l1 + 1);
+        }
         if (!in) dxr[c] = 0.f;
       }
     }

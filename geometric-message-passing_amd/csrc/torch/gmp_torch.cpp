@@ -601,28 +601,43 @@ std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor& 
 }
 
 // ------------------------------------------------------------------ K8 symmetric contraction
+int64_t sc_nq(int64_t D, int64_t corr) {
+  const int nq = gmp_sc_monomials((int)D, (int)corr);
+  TORCH_CHECK(nq > 0, "gmp.symmetric_contraction: unsupported (dim ", D, ", correlation ", corr,
+              "): dim 4 / 9 with correlation 1..4, dim 16 with 1..3");
+  return nq;
+}
+int64_t sc_nq_deg(int64_t D, int64_t nu) {
+  int64_t c = 1;
+  for (int64_t s = 1; s <= nu; ++s) c = c * (D - 1 + s) / s;
+  return c;
+}
+
 void sc_checks(const Tensor& x, int64_t corr, const Tensor& A1, const optional<Tensor>& A2,
-               const optional<Tensor>& A3) {
+               const optional<Tensor>& A3, const optional<Tensor>& A4) {
   f32(x, "x");
-  TORCH_CHECK(x.dim() == 3 && x.size(2) == 9, "gmp.symmetric_contraction: x must be (N, C, 9)");
-  TORCH_CHECK(corr >= 1 && corr <= 3, "gmp.symmetric_contraction: correlation 1..3");
-  const int64_t C = x.size(1);
+  TORCH_CHECK(x.dim() == 3, "gmp.symmetric_contraction: x must be (N, C, D)");
+  const int64_t C = x.size(1), D = x.size(2);
+  sc_nq(D, corr);
   f32(A1, "A1");
-  shape(A1, {C, 9, 9}, "A1");
-  TORCH_CHECK(corr < 2 || A2.has_value(), "gmp.symmetric_contraction: A2 needed");
-  TORCH_CHECK(corr < 3 || A3.has_value(), "gmp.symmetric_contraction: A3 needed");
-  if (corr >= 2) opt_f32(A2, {C, 9, 45}, "A2");
-  if (corr >= 3) opt_f32(A3, {C, 9, 165}, "A3");
+  shape(A1, {C, D, D}, "A1");
+  const optional<Tensor>* As[3] = {&A2, &A3, &A4};
+  const char* names[3] = {"A2", "A3", "A4"};
+  for (int64_t nu = 2; nu <= corr; ++nu) {
+    TORCH_CHECK(As[nu - 2]->has_value(), "gmp.symmetric_contraction: ", names[nu - 2], " needed");
+    opt_f32(*As[nu - 2], {C, D, sc_nq_deg(D, nu)}, names[nu - 2]);
+  }
 }
 
 Tensor symmetric_contraction_fwd(const Tensor& x, int64_t corr, const Tensor& A1,
-                                 const optional<Tensor>& A2, const optional<Tensor>& A3) {
+                                 const optional<Tensor>& A2, const optional<Tensor>& A3,
+                                 const optional<Tensor>& A4) {
   OpGuard g(x, "symmetric_contraction_fwd");
-  sc_checks(x, corr, A1, A2, A3);
-  const int64_t N = x.size(0), C = x.size(1);
-  Tensor out = at::empty({N, 9 * C}, x.options());
-  check_rc(gmp_symmetric_contraction_fwd_f32(N, (int)C, (int)corr, fp(x), fp(A1), cfp(A2),
-                                             cfp(A3), fp(out), cur_stream()),
+  sc_checks(x, corr, A1, A2, A3, A4);
+  const int64_t N = x.size(0), C = x.size(1), D = x.size(2);
+  Tensor out = at::empty({N, D * C}, x.options());
+  check_rc(gmp_symmetric_contraction_fwd_f32(N, (int)C, (int)D, (int)corr, fp(x), fp(A1),
+                                             cfp(A2), cfp(A3), cfp(A4), fp(out), cur_stream()),
            "gmp_symmetric_contraction_fwd_f32");
   return out;
 }
@@ -630,42 +645,43 @@ Tensor symmetric_contraction_fwd(const Tensor& x, int64_t corr, const Tensor& A1
 std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t corr,
                                                      const Tensor& A1, const optional<Tensor>& A2,
                                                      const optional<Tensor>& A3,
+                                                     const optional<Tensor>& A4,
                                                      const Tensor& gout) {
   OpGuard g(x, "symmetric_contraction_bwd");
-  sc_checks(x, corr, A1, A2, A3);
+  sc_checks(x, corr, A1, A2, A3, A4);
   f32(gout, "gout");
-  const int64_t N = x.size(0), C = x.size(1);
-  shape(gout, {N, 9 * C}, "gout");
+  const int64_t N = x.size(0), C = x.size(1), D = x.size(2);
+  shape(gout, {N, D * C}, "gout");
   Tensor dx = at::empty_like(x);
-  const int64_t nq = corr == 1 ? 9 : (corr == 2 ? 54 : 219);
-  Tensor part = at::empty({gmp_sc_groups(N), C, 9, nq}, x.options());
-  check_rc(gmp_symmetric_contraction_bwd_f32(N, (int)C, (int)corr, fp(x), fp(A1), cfp(A2),
-                                             cfp(A3), fp(gout), fp(dx), fp(part), cur_stream()),
+  Tensor part = at::empty({gmp_sc_groups(N), C, D, sc_nq(D, corr)}, x.options());
+  check_rc(gmp_symmetric_contraction_bwd_f32(N, (int)C, (int)D, (int)corr, fp(x), fp(A1),
+                                             cfp(A2), cfp(A3), cfp(A4), fp(gout), fp(dx),
+                                             fp(part), cur_stream()),
            "gmp_symmetric_contraction_bwd_f32");
   return {dx, part};
 }
 
 // ------------------------------------------------------------------ K7 per-edge z rows
 // The host descriptor travels as int[] (n_paths, in_dim, out_dim, sh_dim, weight_numel, z_size,
-// n_blocks, blk_off[6], blk_mul[6], blk_l[6] [, l_max]); the 64-byte path records as a device
+// n_blocks, blk_off[8], blk_mul[8], blk_l[8] [, l_max]); the 64-byte path records as a device
 // uint8 tensor.  l_max (the largest l of any path; default 3) picks the z kernels' instantiation.
 struct TpDescHost {
   int n_paths, in_dim, out_dim, sh_dim;
   long long weight_numel;
   int z_size, n_blocks;
-  int blk_off[6], blk_mul[6], blk_l[6];
+  int blk_off[8], blk_mul[8], blk_l[8];
 };
-static_assert(sizeof(TpDescHost) == 104, "descriptor layout (include/gmp.h)");
+static_assert(sizeof(TpDescHost) == 128, "descriptor layout (include/gmp.h)");
 
 TpDescHost tp_desc(at::IntArrayRef d) {
-  TORCH_CHECK(d.size() == 25 || d.size() == 26, "gmp.tp: descriptor has 25 (+ l_max) ints");
+  TORCH_CHECK(d.size() == 31 || d.size() == 32, "gmp.tp: descriptor has 31 (+ l_max) ints");
   TpDescHost h;
   h.n_paths = (int)d[0]; h.in_dim = (int)d[1]; h.out_dim = (int)d[2]; h.sh_dim = (int)d[3];
   h.weight_numel = d[4]; h.z_size = (int)d[5]; h.n_blocks = (int)d[6];
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < 8; ++k) {
     h.blk_off[k] = (int)d[7 + k];
-    h.blk_mul[k] = (int)d[13 + k];
-    h.blk_l[k] = (int)d[19 + k];
+    h.blk_mul[k] = (int)d[15 + k];
+    h.blk_l[k] = (int)d[23 + k];
   }
   return h;
 }
@@ -674,12 +690,12 @@ TpDescHost tp_desc(at::IntArrayRef d) {
 // order (sh_dim = (l_sh + 1)^2), else the l <= 2 instantiation would skip an l = 3 path and leave
 // its z rows unwritten
 int tp_lmax(at::IntArrayRef d) {
-  const int l = d.size() == 26 ? (int)d[25] : 3;
+  const int l = d.size() == 32 ? (int)d[31] : 3;
   TORCH_CHECK(0 <= l && l <= 3, "gmp.tp: l_max in 0..3");
   const TpDescHost h = tp_desc(d);
-  TORCH_CHECK(0 < h.n_blocks && h.n_blocks <= 6, "gmp.tp: 1..6 input blocks");
+  TORCH_CHECK(0 < h.n_blocks && h.n_blocks <= 8, "gmp.tp: 1..8 output blocks");
   for (int k = 0; k < h.n_blocks; ++k)
-    TORCH_CHECK(h.blk_l[k] <= l, "gmp.tp: l_max ", l, " below input block l ", h.blk_l[k]);
+    TORCH_CHECK(h.blk_l[k] <= l, "gmp.tp: l_max ", l, " below output block l ", h.blk_l[k]);
   int l_sh = 0;
   while ((l_sh + 1) * (l_sh + 1) < h.sh_dim) ++l_sh;
   TORCH_CHECK((l_sh + 1) * (l_sh + 1) == h.sh_dim, "gmp.tp: sh_dim must be (l + 1)^2");
@@ -1393,15 +1409,15 @@ std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor&,
           at::empty({n_scalar}, x.options())};
 }
 Tensor symmetric_contraction_fwd(const Tensor& x, int64_t, const Tensor&, const optional<Tensor>&,
-                                 const optional<Tensor>&) {
-  return at::empty({x.size(0), 9 * x.size(1)}, x.options());
+                                 const optional<Tensor>&, const optional<Tensor>&) {
+  return at::empty({x.size(0), x.size(2) * x.size(1)}, x.options());
 }
 std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t corr,
                                                      const Tensor&, const optional<Tensor>&,
+                                                     const optional<Tensor>&,
                                                      const optional<Tensor>&, const Tensor&) {
-  const int64_t nq = corr == 1 ? 9 : (corr == 2 ? 54 : 219);
-  return {at::empty_like(x), at::empty({gmp_sc_groups(x.size(0)), x.size(1), 9, nq},
-                                       x.options())};
+  return {at::empty_like(x), at::empty({gmp_sc_groups(x.size(0)), x.size(1), x.size(2),
+                                        sc_nq(x.size(2), corr)}, x.options())};
 }
 Tensor tp_edge_z(at::IntArrayRef desc, const Tensor&, const Tensor&, const Tensor& x,
                  const Tensor&, const Tensor&, const Tensor&, int64_t e0, int64_t e1) {
@@ -1545,9 +1561,9 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor chan_info, Tensor weight, Tensor shift, Tensor invstd, bool training, "
         "int n_scalar) -> (Tensor grad_x, Tensor grad_weight, Tensor grad_bias)");
   m.def("symmetric_contraction_fwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
-        "Tensor? A3) -> Tensor");
+        "Tensor? A3, Tensor? A4=None) -> Tensor");
   m.def("symmetric_contraction_bwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
-        "Tensor? A3, Tensor gout) -> (Tensor dx, Tensor dA_partials)");
+        "Tensor? A3, Tensor? A4, Tensor gout) -> (Tensor dx, Tensor dA_partials)");
   m.def("tp_edge_z(int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, Tensor src_sorted, "
         "Tensor perm, int e0, int e1) -> Tensor");
   m.def("tp_edge_z_bwd(int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, "

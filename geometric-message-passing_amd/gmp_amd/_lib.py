@@ -40,10 +40,10 @@ class TpPath(ctypes.Structure):
 class TpDesc(ctypes.Structure):
     _fields_ = [("n_paths", c_int), ("in_dim", c_int), ("out_dim", c_int), ("sh_dim", c_int),
                 ("weight_numel", ctypes.c_longlong), ("z_size", c_int), ("n_blocks", c_int),
-                ("blk_off", c_int * 6), ("blk_mul", c_int * 6), ("blk_l", c_int * 6)]
+                ("blk_off", c_int * 8), ("blk_mul", c_int * 8), ("blk_l", c_int * 8)]
 
 
-assert ctypes.sizeof(TpPath) == 64 and ctypes.sizeof(TpDesc) == 104
+assert ctypes.sizeof(TpPath) == 64 and ctypes.sizeof(TpDesc) == 128
 
 # name -> (restype, argtypes); must mirror include/gmp.h exactly
 SIGNATURES = {
@@ -181,18 +181,19 @@ SIGNATURES = {
     "gmp_ln_act_bwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp,
                                    c_vp, c_size, c_vp]),
     "gmp_sc_groups": (c_int, [c_i64]),
-    "gmp_symmetric_contraction_fwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
-                                                  c_vp, c_vp]),
-    "gmp_symmetric_contraction_bwd_f32": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+    "gmp_sc_monomials": (c_int, [c_int, c_int]),
+    "gmp_symmetric_contraction_fwd_f32": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp, c_vp, c_vp]),
+    "gmp_symmetric_contraction_bwd_f32": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_vp, c_int]
                               + [c_vp] * 11),
 }
 
-# include/gmp.h GMP_ABI_VERSION (2: r04 — EGNN save_planes arguments, the x_hat mode global and
-# gmp_egnn_edge_bwd_ab_f32 removed; r03's torsion_kn argument of gmp_triplet_fill_f32)
-ABI_VERSION = 2
+# include/gmp.h GMP_ABI_VERSION (3: r04 — K8 dim / A4 arguments; 2: r04 — EGNN save_planes
+# arguments, the x_hat mode global and gmp_egnn_edge_bwd_ab_f32 removed)
+ABI_VERSION = 3
 _lib = None
 TORCH_LIB_PATH = os.environ.get("GMP_TORCH_LIB", os.path.join(_HERE, "libgmp_torch.so"))
 _torch_ops = None

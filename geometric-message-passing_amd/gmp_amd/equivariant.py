@@ -376,12 +376,11 @@ class TPPlan:
                                                                     irreps_out)
         key = tuple(ir for _, ir in irreps_out)
         sh_dim = o3.irreps_dim(irreps_sh)
+        # (input irreps with a repeated l -- both parities -- take the dz kernel's grouped form)
         if any(m != 1 for m, _ in irreps_sh) or sh_dim not in (1, 4, 9, 16) or \
-                any(m > 128 for m, _ in irreps_in) or len(irreps_out) > 6 or \
+                any(m > 128 for m, _ in irreps_in) or len(irreps_out) > 8 or \
                 any(ir[0] > 3 for _, ir in tuple(irreps_in) + tuple(irreps_out)) or \
-                len(self.instructions) > 32 or \
-                len({ir[0] for _, ir in irreps_in}) != len(tuple(irreps_in)):
-            # (the per-edge z / dz kernels hold one input block per l1)
+                len(self.instructions) > 48:
             raise NotImplementedError(f"TP {o3.irreps_str(irreps_in)} x {o3.irreps_str(irreps_sh)}"
                                       f" -> {o3.irreps_str(irreps_out)} not supported by K7")
         # the per-edge-weight kernels (GMP_TP_MODE=edge) take the two l <= 2 layouts; the node
@@ -899,16 +898,20 @@ class Contraction(nn.Module):
         return torch.cat(outs, dim=0)
 
 
+def _nq_deg(D, nu):
+    return math.comb(D + nu - 1, nu)
+
+
 class SymmetricContractionFn(torch.autograd.Function):
-    """K8 (torch.ops.gmp.symmetric_contraction_{fwd,bwd}): out (N, 9C) from x (N, C, 9) and the
-    per-channel coefficients over the symmetric monomial basis A~_nu (C, 9, 9 / 45 / 165)."""
+    """K8 (torch.ops.gmp.symmetric_contraction_{fwd,bwd}): out (N, D C) from x (N, C, D) and the
+    per-channel coefficients over the symmetric monomial basis A~_nu (C, D, C(D+nu-1, nu))."""
 
     @staticmethod
     def forward(ctx, x, corr, *A):
         x = _f32c(x)
         A = [_f32c(a) for a in A]
         _need_cuda(x, *A)
-        Ao = list(A) + [None] * (3 - len(A))
+        Ao = list(A) + [None] * (4 - len(A))
         with _timed("symmetric_contraction_fwd"):
             out = _lib.torch_ops().symmetric_contraction_fwd(x, corr, *Ao)
         ctx.corr = corr
@@ -920,43 +923,54 @@ class SymmetricContractionFn(torch.autograd.Function):
     def backward(ctx, g):
         x, *A = ctx.saved_tensors
         g = _f32c(g)
-        Ao = list(A) + [None] * (3 - len(A))
+        Ao = list(A) + [None] * (4 - len(A))
         with _timed("symmetric_contraction_bwd"):
             dx, part = _lib.torch_ops().symmetric_contraction_bwd(x, ctx.corr, *Ao, g)
         if not ctx.needs_input_grad[0]:
             dx = None
         dA = part.sum(0)  # fixed-order sum over node groups
-        grads = [dA[..., :9], dA[..., 9:54], dA[..., 54:]][:len(A)]
-        return (dx, None, *[gg.contiguous() for gg in grads])
+        D, grads, q0 = x.shape[2], [], 0
+        for nu in range(1, len(A) + 1):
+            n = _nq_deg(D, nu)
+            grads.append(dA[..., q0:q0 + n].contiguous())
+            q0 += n
+        return (dx, None, *grads)
 
 
 _SYM_IDX = {}
 
 
-def _sym_index(nu, device):
-    """(n_q, n_perm) flat indices into the 9^nu axis of every distinct permutation of each sorted
-    monomial (i <= j <= k, lexicographic), padded with 9^nu (an appended zero column)."""
-    key = (nu, device)
+def _sym_index(nu, device, D=9):
+    """(n_q, n_perm) flat indices into the D^nu axis of every distinct permutation of each
+    sorted monomial (i <= j <= k, lexicographic), padded with D^nu (an appended zero column)."""
+    key = (nu, D, device)
     if key not in _SYM_IDX:
         import itertools
         rows = []
-        for t in itertools.combinations_with_replacement(range(9), nu):
+        for t in itertools.combinations_with_replacement(range(D), nu):
             perms = sorted(set(itertools.permutations(t)))
-            rows.append([sum(p * 9 ** (nu - 1 - r) for r, p in enumerate(pm)) for pm in perms])
+            rows.append([sum(p * D ** (nu - 1 - r) for r, p in enumerate(pm)) for pm in perms])
         width = max(len(r) for r in rows)
-        idx = torch.tensor([r + [9 ** nu] * (width - len(r)) for r in rows], dtype=torch.int64)
+        idx = torch.tensor([r + [D ** nu] * (width - len(r)) for r in rows], dtype=torch.int64)
         _SYM_IDX[key] = idx.to(device)
     return _SYM_IDX[key]
 
 
 def fold_symmetric(A, nu):
-    """A (C, 9, 9^nu) -> A~ (C, 9, C(8 + nu, nu)): every permutation's coefficient summed into
-    the sorted monomial (differentiable; the adjoint spreads dA~ back to each permutation)."""
+    """A (C, M, D^nu) -> A~ (C, M, C(D - 1 + nu, nu)): every permutation's coefficient summed
+    into the sorted monomial (differentiable; the adjoint spreads dA~ back to each permutation)."""
     if nu == 1:
         return A
-    idx = _sym_index(nu, A.device)
+    D = round(A.shape[-1] ** (1.0 / nu))
+    idx = _sym_index(nu, A.device, D)
     Ap = torch.cat([A, A.new_zeros(A.shape[:-1] + (1,))], dim=-1)
     return Ap[..., idx].sum(-1)
+
+
+# K8's compiled (per-channel dim, correlation) pairs: C x (0e+1o[+2e[+3o]]) -> the same irreps
+_K8_IRREPS = {4: ((0, 1), (1, -1)), 9: ((0, 1), (1, -1), (2, 1)),
+              16: ((0, 1), (1, -1), (2, 1), (3, -1))}
+_K8_MAX_CORR = {4: 4, 9: 4, 16: 3}
 
 
 class SymmetricContraction(nn.Module):
@@ -966,16 +980,20 @@ class SymmetricContraction(nn.Module):
         self.correlation = correlation
         irreps_in = o3.parse_irreps(irreps_in)
         C = irreps_in[0][0]
-        # K8 applies to C x (0e + 1o + 2e) -> the same irreps, correlation <= 3 (configs C4)
-        self._k8 = (tuple(ir for _, ir in irreps_in) == ((0, 1), (1, -1), (2, 1)) and
-                    all(m == C for m, _ in irreps_in) and
-                    tuple(self.irreps_out) == tuple(irreps_in) and 1 <= correlation <= 3)
+        irs = tuple(ir for _, ir in irreps_in)
+        D = sum(2 * l + 1 for l, _ in irs)
+        # K8 applies to C x (0e + 1o [+ 2e [+ 3o]]) -> the same irreps (max_ell 1..3), correlation
+        # <= 4 (<= 3 at max_ell 3); other irreps (both parities, repeated l) run the per-irrep
+        # contraction below (torch on the GPU)
+        self._k8 = (_K8_IRREPS.get(D) == irs and all(m == C for m, _ in irreps_in) and
+                    tuple(self.irreps_out) == tuple(irreps_in) and
+                    1 <= correlation <= _K8_MAX_CORR[D])
         self.contractions = nn.ModuleDict({
             f"{m}x{l}{'e' if p == 1 else 'o'}": Contraction(irreps_in, (l, p), correlation)
             for m, (l, p) in self.irreps_out})
 
     def coefficients(self):
-        """A_nu (C, 9, 9^nu): per-channel coefficient tensors, output rows [0e | 1o | 2e]."""
+        """A_nu (C, D, D^nu): per-channel coefficient tensors, output rows [0e | 1o | 2e ..]."""
         out = []
         for nu in range(1, self.correlation + 1):
             rows = []
@@ -1022,15 +1040,16 @@ def _edge_features(model, batch):
 
 
 class MACEModel(nn.Module):
-    """models/mace.py:9-190 (same kwargs/defaults; max_ell = 2)."""
+    """models/mace.py:9-190 (same kwargs/defaults; max_ell 1..3: K1 / K7 node form take l <= 3,
+    K8 the 0e+1o[+2e[+3o]] hidden irreps, other hidden irreps the per-irrep contraction)."""
 
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
                  correlation=3, num_layers=5, emb_dim=64, hidden_irreps=None, mlp_dim=256,
                  in_dim=1, out_dim=1, aggr="sum", pool="sum", batch_norm=True, residual=True,
                  equivariant_pred=False):
         super().__init__()
-        if max_ell != 2:
-            raise NotImplementedError("K1/K7 are specialised to l <= 2 (the configs' L_max)")
+        if max_ell not in (1, 2, 3):
+            raise NotImplementedError("K1 / K7 take max_ell <= 3")
         self.r_max, self.max_ell, self.num_layers = r_max, max_ell, num_layers
         self.emb_dim, self.mlp_dim, self.residual = emb_dim, mlp_dim, residual
         self.batch_norm, self.equivariant_pred = batch_norm, equivariant_pred

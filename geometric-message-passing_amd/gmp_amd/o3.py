@@ -145,9 +145,10 @@ def fctp_instructions(irreps_in1, irreps_in2, irreps_out):
 
 
 # ----------------------------------------------------------------------------------- MACE U
-def _cg_chain(irreps_list):
+def _cg_chain(irreps_list, filter_ir=None):
     """Generalised CG of a product of irreps (cg.py:_wigner_nj, component normalisation):
-    list of (irrep_out, tensor (2lo+1, d, ..., d)) sorted (stably) by irrep."""
+    list of (irrep_out, tensor (2lo+1, d, ..., d)) sorted (stably) by irrep.  filter_ir: the
+    irreps allowed at every coupling step (cg.py:_wigner_nj filter_ir_mid)."""
     if len(irreps_list) == 1:
         irreps = irreps_list[0]
         dim = irreps_dim(irreps)
@@ -163,11 +164,13 @@ def _cg_chain(irreps_list):
     dims_left = [irreps_dim(x) for x in left]
     dr = irreps_dim(right)
     out = []
-    for ir_left, C_left in _cg_chain(left):
+    for ir_left, C_left in _cg_chain(left, filter_ir):
         i = 0
         for m, ir in right:
             d = 2 * ir[0] + 1
             for ir_out in product_irreps(ir_left, ir):
+                if filter_ir is not None and tuple(ir_out) not in filter_ir:
+                    continue
                 lo = ir_out[0]
                 C = wigner_3j(lo, ir_left[0], ir[0]) * math.sqrt(2 * lo + 1)
                 C = np.einsum("jk,ijl->ikl", C_left.reshape(C_left.shape[0], -1), C)
@@ -182,8 +185,10 @@ def _cg_chain(irreps_list):
 
 
 def u_matrix(coupling_irreps, ir_out, nu):
-    """cg.py U_matrix_real(coupling, ir_out, nu)[-1]: (2lo+1 [squeezed if 1], d^nu..., K)."""
-    blocks = [C for ir, C in _cg_chain([coupling_irreps] * nu) if ir == tuple(ir_out)]
+    """cg.py U_matrix_real(coupling, ir_out, nu)[-1]: (2lo+1 [squeezed if 1], d^nu..., K).
+    correlation 4 couples through the natural-parity irreps l < 12 only (cg.py:101-115)."""
+    filt = {(l, (-1) ** l) for l in range(12)} if nu == 4 else None
+    blocks = [C for ir, C in _cg_chain([coupling_irreps] * nu, filt) if ir == tuple(ir_out)]
     stacked = np.stack([np.squeeze(C) for C in blocks], axis=-1)
     return stacked
 

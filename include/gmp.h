@@ -26,9 +26,11 @@
 extern "C" {
 #endif
 
-/* 2 (r04): EGNN forward / backward take save_planes; gmp_egnn_set_xhat_mode and
+/* 3 (r04): K8 symmetric contraction takes the per-channel dim and A4 (gmp_sc_monomials added);
+ * the TP descriptor holds 8 output blocks (128 bytes), <= 48 paths.
+ * 2 (r04): EGNN forward / backward take save_planes; gmp_egnn_set_xhat_mode and
  * gmp_egnn_edge_bwd_ab_f32 removed.  (r03 changed gmp_triplet_fill_f32 under version 1.) */
-#define GMP_ABI_VERSION 2
+#define GMP_ABI_VERSION 3
 
 enum {
   GMP_OK = 0,
@@ -341,8 +343,8 @@ int gmp_irreps_bn_bwd_f32(int64_t B, int C, int nf, const int32_t* col_chan,
  * x (N, in_dim) mul_ir; sh (E, 9) in ORIGINAL edge order; W row r = sorted edge c0 + r.
  * Forward writes msg rows c0..c1-1 (E x out_dim, sorted positions).
  * desc_host: host pointer to the descriptor {int n_paths, in_dim, out_dim, sh_dim;
- *   int64 weight_numel; int z_size, n_blocks; int blk_off[6], blk_mul[6], blk_l[6];}
- *   (104 bytes; <= 32 paths).  The per-edge-weight kernels below take l <= 2 (sh_dim 9, the
+ *   int64 weight_numel; int z_size, n_blocks; int blk_off[8], blk_mul[8], blk_l[8];}
+ *   (128 bytes since ABI 3; <= 48 paths, <= 8 output blocks).  The per-edge-weight kernels below take l <= 2 (sh_dim 9, the
  *   two layouts); the node-form z / dz kernels (gmp_tp_edge_z*) take l <= 3 (sh_dim (lmax+1)^2
  *   <= 16, any block structure: max_ell = 3 models).
  * paths_dev: device array of 64-byte path records {int l1, l2, lo, mul1, mul_out, x_off, y_off,
@@ -631,25 +633,29 @@ int gmp_sum_rows_f32(const float* partials, int64_t nrows, int64_t width, float*
 
 /* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
- * element_dependent=False, called per output irrep at :176-185), all three output irreps
- * (0e, 1o, 2e) of C channels at once.  x (N, C, 9) = reshape_irreps of C x (0e+1o+2e)
- * (irreps_tools.py:63-79).  Coefficients over the SYMMETRIC monomial basis (x_i x_j x_k is
- * symmetric, so every permutation's coefficient folds into the sorted index tuple):
- *   A1 (C, 9, 9), A2 (C, 9, 45) over i <= j, A3 (C, 9, 165) over i <= j <= k (lexicographic),
+ * element_dependent=False, called per output irrep at :176-185), all output irreps of C channels
+ * at once.  x (N, C, D) = reshape_irreps of C x (0e+1o[+2e[+3o]]) (irreps_tools.py:63-79),
+ * D = (L+1)^2 for max_ell L = 1, 2, 3 (D = 4, 9, 16).  Coefficients over the SYMMETRIC monomial
+ * basis (x_i x_j x_k is symmetric, so every permutation's coefficient folds into the sorted index
+ * tuple): A_nu (C, D, C(D+nu-1, nu)) over i1 <= .. <= inu (lexicographic),
  *   A_nu[c, m, q] = sum over the distinct permutations p of q of sum_k U_nu[m, p, k] W_nu[k, c]
  * (the host builds them from the module's U_matrix_nu buffers and weights, differentiably).
- * out (N, 9C) in mul_ir order [0e: C | 1o: 3C | 2e: 5C].  Backward: dx (N, C, 9) (may be NULL)
- * and dA partials (gmp_sc_groups(N), C, 9, nq) with nq = 9 / 54 / 219 for correlation 1 / 2 / 3
- * (monomials [deg1 | deg2 | deg3] as above; may be NULL); the caller sums the groups.
+ * correlation 1..4 for D = 4, 9; 1..3 for D = 16 (else GMP_ERR_UNSUPPORTED); A_nu for nu >
+ * correlation may be NULL.  out (N, D C) in mul_ir order [0e: C | 1o: 3C | 2e: 5C | 3o: 7C].
+ * Backward: dx (N, C, D) (may be NULL) and dA partials (gmp_sc_groups(N), C, D, nq) with
+ * nq = gmp_sc_monomials(D, correlation) (monomials [deg1 | deg2 | ..] as above; may be NULL);
+ * the caller sums the groups.  (ABI 3: the dim argument and A4 are new.)
  * ------------------------------------------------------------------------------------------ */
 int gmp_sc_groups(int64_t n_nodes);
-int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int correlation,
+int gmp_sc_monomials(int dim, int correlation);
+int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
                                       const float* x, const float* A1, const float* A2,
-                                      const float* A3, float* out, void* stream);
-int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int correlation,
+                                      const float* A3, const float* A4, float* out,
+                                      void* stream);
+int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
                                       const float* x, const float* A1, const float* A2,
-                                      const float* A3, const float* gout, float* dx,
-                                      float* dA_partials, void* stream);
+                                      const float* A3, const float* A4, const float* gout,
+                                      float* dx, float* dA_partials, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K13 SchNet CFConv fused message + aggregation (PyG 2.3.1 CFConv.message `x_j * W` and

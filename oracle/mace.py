@@ -192,18 +192,21 @@ def edge_features(pos, edge_index, radial, max_ell=2):
 
 
 class MACEModel(nn.Module):
-    """models/mace.py:9-190 (max_ell = 2 only: the SH restatement is l <= 2)."""
+    """models/mace.py:9-190 (max_ell <= 3: the SH restatement is l <= 3; hidden_irreps as
+    mace.py:90-93)."""
 
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
                  correlation=3, num_layers=5, emb_dim=64, mlp_dim=256, in_dim=1, out_dim=1,
-                 aggr="sum", pool="sum", batch_norm=True, residual=True, equivariant_pred=False):
+                 aggr="sum", pool="sum", batch_norm=True, residual=True, equivariant_pred=False,
+                 hidden_irreps=None):
         super().__init__()
-        assert max_ell == 2
+        assert 1 <= max_ell <= 3
+        self.max_ell = max_ell
         self.emb_dim, self.residual, self.equivariant_pred = emb_dim, residual, equivariant_pred
         self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)
         sh = o3.spherical_harmonics_irreps(max_ell)
         self.emb_in = nn.Embedding(in_dim, emb_dim)
-        hidden = _hidden_irreps(emb_dim, max_ell)
+        hidden = o3.Irreps(hidden_irreps) if hidden_irreps else _hidden_irreps(emb_dim, max_ell)
         self.hidden_irreps = hidden
         self.convs, self.prods = nn.ModuleList(), nn.ModuleList()
         for k in range(num_layers):
@@ -221,7 +224,8 @@ class MACEModel(nn.Module):
 
     def forward(self, batch):
         h = self.emb_in(batch.atoms)
-        edge_sh, edge_feats = edge_features(batch.pos, batch.edge_index, self.radial_embedding)
+        edge_sh, edge_feats = edge_features(batch.pos, batch.edge_index, self.radial_embedding,
+                                            self.max_ell)
         for conv, prod in zip(self.convs, self.prods):
             hu = conv(h, batch.edge_index, edge_sh, edge_feats)
             sc = F.pad(h, (0, hu.shape[-1] - h.shape[-1]))
@@ -245,7 +249,7 @@ class TFNModel(nn.Module):
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
                  num_layers=5, emb_dim=64, mlp_dim=256, in_dim=1, out_dim=1, aggr="sum",
                  pool="first", gate=True, batch_norm=False, residual=True,
-                 equivariant_pred=False):
+                 equivariant_pred=False, hidden_irreps=None):
         super().__init__()
         assert 1 <= max_ell <= 3
         self.max_ell = max_ell
@@ -253,7 +257,7 @@ class TFNModel(nn.Module):
         self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)
         sh = o3.spherical_harmonics_irreps(max_ell)
         self.emb_in = nn.Embedding(in_dim, emb_dim)
-        hidden = _hidden_irreps(emb_dim, max_ell)
+        hidden = o3.Irreps(hidden_irreps) if hidden_irreps else _hidden_irreps(emb_dim, max_ell)
         self.convs = nn.ModuleList()
         for k in range(num_layers):
             inp = o3.Irreps(f"{emb_dim}x0e") if k == 0 else hidden

@@ -13,6 +13,8 @@ Modules exercised (all pure-torch arithmetic in the reference):
   models/layers/gvp_layer.py    GVP / GVPConv / GVPConvLayer (101-438)
   models/gvpgnn.py              GVPGNNModel (103-127)
   models/layers/spherenet_layer.py xyz_to_dat (496-564)   [`python make_golden.py triplets`]
+  models/mace_modules/{cg,symmetric_contraction}.py at correlation 4 and max_ell 3
+                                                         [`python make_golden.py mace_widening`]
 """
 import os
 import sys
@@ -130,7 +132,42 @@ def make_triplets(mods):
     return "triplets.pt"
 
 
+def make_mace_widening():
+    """Symmetric contractions beyond config C4 (r04 widening), reference cg.py +
+    symmetric_contraction.py: correlation 4 (cg.py's natural-parity coupling filter) on
+    0e+1o+2e and correlation 3 at max_ell 3 (0e+1o+2e+3o)."""
+    mm = _ref_stubs.load_mace_contraction(REF)
+    o3l = sys.modules["e3nn.o3"]
+    out = []
+    for name, irr, corr, seed in [("mace_symmetric_contraction_c4.pt", "4x0e+4x1o+4x2e", 4, 21),
+                                  ("mace_symmetric_contraction_l3.pt", "4x0e+4x1o+4x2e+4x3o", 3,
+                                   22)]:
+        torch.manual_seed(seed)
+        irreps = o3l.Irreps(irr)
+        SC = mm["models.mace_modules.symmetric_contraction"].SymmetricContraction(
+            irreps_in=irreps, irreps_out=irreps, correlation=corr, element_dependent=False,
+            num_elements=1)
+        D = sum(2 * ir.l + 1 for _, ir in irreps)
+        x = torch.randn(23, 4, D, requires_grad=True)
+        y = SC(x, None)
+        gy = torch.randn_like(y)
+        (y * gy).sum().backward()
+        d = {"x": x.detach(), "out": y.detach(), "g_out": gy, "grad_x": x.grad}
+        # weights only: the U_matrix buffers (up to 9^4 x 9 x K floats) are rebuilt by the
+        # module under test, and the outputs pin them
+        d.update({f"param.{k}": v.detach().clone() for k, v in SC.state_dict().items()
+                  if "U_matrix" not in k})
+        d.update(grads_dict(SC))
+        torch.save(d, os.path.join(HERE, name))
+        out.append(name)
+    return out
+
+
 def main(only=None):
+    if only == "mace_widening":
+        for f in make_mace_widening():
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+        return
     mods = _ref_stubs.load_reference(REF)
     if only == "triplets":
         f = make_triplets(mods)

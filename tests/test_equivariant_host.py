@@ -17,7 +17,13 @@ def _eq():
 @pytest.mark.parametrize("kind,kw", [("MACEModel", dict(num_layers=3, emb_dim=16, correlation=3)),
                                      ("TFNModel", dict(num_layers=3, emb_dim=16)),
                                      ("MACEModel", dict(num_layers=2, emb_dim=128)),
-                                     ("TFNModel", dict(num_layers=2, emb_dim=64, batch_norm=True))])
+                                     ("TFNModel", dict(num_layers=2, emb_dim=64, batch_norm=True)),
+                                     ("MACEModel", dict(num_layers=2, emb_dim=8, max_ell=3)),
+                                     ("MACEModel", dict(num_layers=1, emb_dim=8, correlation=4)),
+                                     ("MACEModel", dict(num_layers=1, emb_dim=8, correlation=2,
+                                                        hidden_irreps="8x0e+8x0o+8x1e+8x1o+8x2e+8x2o")),
+                                     ("TFNModel", dict(num_layers=2, emb_dim=8,
+                                                       hidden_irreps="8x0e+8x0o+8x1e+8x1o+8x2e+8x2o"))])
 def test_state_dict_keys_and_shapes(kind, kw):
     eq = _eq()
     ours, ref = getattr(eq, kind)(**kw), getattr(om, kind)(**kw)
@@ -44,7 +50,7 @@ def test_tp_plan_tables():
         assert p.w_off == ins["w_off"] and abs(p.alpha - ins["path_weight"]) < 1e-7
     assert plan.cg_host.numel() == sum(
         (2 * i["l1"] + 1) * (2 * i["l2"] + 1) * (2 * i["lo"] + 1) for i in plan.instructions)
-    assert ctypes_size(_lib.TpPath) == 64 and ctypes_size(_lib.TpDesc) == 104
+    assert ctypes_size(_lib.TpPath) == 64 and ctypes_size(_lib.TpDesc) == 128
     s, g, v = o3.irreps2gate(o3.hidden_irreps(64, 2))
     gated = s + g + v
     plan_g = eq.TPPlan(o3.parse_irreps("64x0e"), o3.sh_irreps(2), gated)
@@ -55,14 +61,19 @@ def test_tp_plan_tables():
     p3 = eq.TPPlan(o3.parse_irreps("64x0e+64x1o+64x2e+64x3o"), o3.sh_irreps(3),
                    o3.parse_irreps("64x0e+192x0e+64x1o+64x2e+64x3o"))
     assert p3.layout is None and p3.sh_dim == 16 and p3.desc.n_paths == 27
-    assert p3.cg_host.numel() == 1959 and p3.z_size == 6592 and len(p3.desc_list) == 26
+    assert p3.cg_host.numel() == 1959 and p3.z_size == 6592 and len(p3.desc_list) == 32
     assert p3.l_max == 3 and p3.desc_list[-1] == 3
     with pytest.raises(NotImplementedError):
         eq.TPPlan(hid, o3.sh_irreps(2), o3.parse_irreps("8x4e"))
     with pytest.raises(NotImplementedError):
         eq.TPPlan(hid, o3.sh_irreps(4), hid)
     with pytest.raises(NotImplementedError):
-        eq.TPPlan(hid, o3.sh_irreps(2), o3.parse_irreps("8x0e+8x1o+8x0e+8x1o+8x0e+8x1o+8x2e"))
+        eq.TPPlan(hid, o3.sh_irreps(2),
+                  o3.parse_irreps("8x0e+8x1o+8x0e+8x1o+8x0e+8x1o+8x0e+8x1o+8x2e"))  # 9 blocks
+    # both parities / repeated l (the incompleteness configs): node form
+    bp = o3.parse_irreps("32x0e+32x0o+32x1e+32x1o+32x2e+32x2o")
+    pb = eq.TPPlan(bp, o3.sh_irreps(2), bp)
+    assert pb.layout is None and pb.desc.n_paths == 30 and pb.desc.n_blocks == 6
 
 
 def ctypes_size(t):
@@ -82,14 +93,20 @@ def test_node_ops_vs_oracle():
     # BatchNorm and Gate are HIP kernels (K16): tests/test_gpu_equivariant.py
 
 
-@pytest.mark.parametrize("corr", [1, 2, 3])
-def test_symmetric_contraction_vs_oracle(corr):
+@pytest.mark.parametrize("corr,irr", [(1, "8x0e+8x1o+8x2e"), (2, "8x0e+8x1o+8x2e"),
+                                      (3, "8x0e+8x1o+8x2e"), (4, "4x0e+4x1o+4x2e"),
+                                      (4, "4x0e+4x1o"), (3, "4x0e+4x1o+4x2e+4x3o"),
+                                      (2, "4x0e+4x0o+4x1e+4x1o+4x2e+4x2o")])
+def test_symmetric_contraction_vs_oracle(corr, irr):
+    """The per-irrep contraction (the torch path for irreps K8 does not take; K8's own host
+    logic, coefficients() and fold_symmetric, is checked through it on the GPU) vs the oracle,
+    max_ell 1..3, correlation 4 (natural-parity coupling filter), both parities."""
     eq = _eq()
     torch.manual_seed(corr)
-    irr = "8x0e+8x1o+8x2e"
     a, b = eq.SymmetricContraction(irr, irr, corr), om.SymmetricContraction(irr, irr, corr)
     a.load_state_dict(b.state_dict())
-    x = torch.randn(50, 8, 9)
+    C = int(irr.split("x")[0])
+    x = torch.randn(50, C, sum(2 * int(t.split("x")[1][:-1]) + 1 for t in irr.split("+")))
     xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
     eq.Contraction.node_chunk = 16  # exercise node chunking + checkpoint
     try:
@@ -145,3 +162,27 @@ def test_schnet_oracle_known_answers():
     assert conv.nn is m.interactions[0].mlp
     C = 0.5 * (math.cos(math.pi) + 1.0)
     assert abs(C) < 1e-12  # filter vanishes at the cutoff
+
+
+_WIDENING = [("mace_symmetric_contraction_c4.pt", "4x0e+4x1o+4x2e", 4),
+             ("mace_symmetric_contraction_l3.pt", "4x0e+4x1o+4x2e+4x3o", 3)]
+
+
+@pytest.mark.parametrize("name,irr,corr", _WIDENING)
+def test_symmetric_contraction_widening_golden(golden, name, irr, corr):
+    """The reference's own symmetric contraction at correlation 4 (cg.py's natural-parity
+    coupling filter) and at max_ell 3 (tests/golden/make_golden.py mace_widening): the oracle and
+    the product module's per-irrep path reproduce outputs and gradients."""
+    eq = _eq()
+    d = golden(name)
+    params = {k[6:]: v for k, v in d.items() if k.startswith("param.")}
+    for mod in (eq.SymmetricContraction(irr, irr, corr), om.SymmetricContraction(irr, irr, corr)):
+        missing, unexpected = mod.load_state_dict(params, strict=False)
+        assert not unexpected and all("U_matrix" in k for k in missing)
+        x = d["x"].clone().requires_grad_(True)
+        y = mod(x)
+        torch.testing.assert_close(y, d["out"], atol=1e-5, rtol=1e-5)
+        (y * d["g_out"]).sum().backward()
+        torch.testing.assert_close(x.grad, d["grad_x"], atol=1e-5, rtol=1e-5)
+        for k, p in mod.named_parameters():
+            torch.testing.assert_close(p.grad, d["grad." + k], atol=1e-5, rtol=1e-5, msg=k)

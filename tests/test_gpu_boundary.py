@@ -134,8 +134,14 @@ def test_shape_checks_irreps_sc_gate():
     xs = torch.randn(7, 4, 9, **f)
     _bad(ops_.symmetric_contraction_fwd, xs, 3, torch.randn(4, 9, 9, **f),
          torch.randn(4, 9, 45, **f), torch.randn(4, 9, 160, **f), match="A3")
-    _bad(ops_.symmetric_contraction_bwd, xs, 1, torch.randn(4, 9, 9, **f), None, None,
+    _bad(ops_.symmetric_contraction_bwd, xs, 1, torch.randn(4, 9, 9, **f), None, None, None,
          torch.randn(7, 35, **f), match="gout")
+    _bad(ops_.symmetric_contraction_fwd, torch.randn(7, 4, 16, **f), 4,
+         torch.randn(4, 16, 16, **f), torch.randn(4, 16, 136, **f), torch.randn(4, 16, 816, **f),
+         torch.randn(4, 16, 3876, **f), match="unsupported")
+    _bad(ops_.symmetric_contraction_fwd, torch.randn(7, 4, 9, **f), 4,
+         torch.randn(4, 9, 9, **f), torch.randn(4, 9, 45, **f), torch.randn(4, 9, 165, **f),
+         None, match="A4")
 
 
 def test_shape_checks_tp_and_outer_sums():

@@ -226,6 +226,16 @@ def test_tp_conv_chunking_and_determinism(monkeypatch, mode):
     ("TFNModel", dict(num_layers=2, emb_dim=32, r_max=2.0, gate=False, batch_norm=True,
                       pool="sum")),
     ("MACEModel", dict(num_layers=2, emb_dim=128, correlation=3, r_max=2.0, mlp_dim=64)),
+    # widening (r04): max_ell 3 and 1 (K8 at D = 16 / 4), correlation 4 (cg.py's natural-parity
+    # filter), both-parity hidden irreps of the incompleteness experiment (experiments/
+    # incompleteness.ipynb: MACE 32x(0e+0o+1e+1o+2e+2o), TFN 64x the same; per-irrep contraction)
+    ("MACEModel", dict(num_layers=2, emb_dim=16, correlation=3, max_ell=3, r_max=2.0)),
+    ("MACEModel", dict(num_layers=2, emb_dim=16, correlation=4, r_max=2.0)),
+    ("MACEModel", dict(num_layers=1, emb_dim=16, correlation=4, max_ell=1, r_max=2.0)),
+    ("MACEModel", dict(num_layers=1, emb_dim=16, correlation=3, r_max=2.0,
+                       hidden_irreps="16x0e+16x0o+16x1e+16x1o+16x2e+16x2o")),
+    ("TFNModel", dict(num_layers=2, emb_dim=16, r_max=2.0,
+                      hidden_irreps="16x0e+16x0o+16x1e+16x1o+16x2e+16x2o")),
 ])
 def test_model_vs_oracle(kind, kw):
     from gmp_amd import equivariant as eq
@@ -275,18 +285,21 @@ def test_mace_rotation_invariance_gpu():
     _close_scaled(y2, y1, 1e-4, "rotated")
 
 
-@pytest.mark.parametrize("C,corr", [(16, 3), (128, 3), (32, 2), (8, 1)])
-def test_symmetric_contraction_k8_vs_oracle(C, corr):
-    """K8 HIP symmetric contraction vs the oracle (the reference's nested einsum chain)."""
+@pytest.mark.parametrize("C,corr,lmax", [(16, 3, 2), (128, 3, 2), (32, 2, 2), (8, 1, 2),
+                                         (16, 4, 2), (32, 4, 1), (8, 2, 1), (16, 3, 3), (8, 1, 3),
+                                         (128, 2, 3)])
+def test_symmetric_contraction_k8_vs_oracle(C, corr, lmax):
+    """K8 HIP symmetric contraction vs the oracle (the reference's nested einsum chain) for
+    C x (0e+1o[+2e[+3o]]) (D = 4, 9, 16) up to correlation 4 (3 at D = 16)."""
     from gmp_amd import equivariant as eq
     torch.manual_seed(C + corr)
-    irr = f"{C}x0e+{C}x1o+{C}x2e"
+    irr = "+".join(f"{C}x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
     ref = om.SymmetricContraction(irr, irr, corr)
     sc = eq.SymmetricContraction(irr, irr, corr)
     sc.load_state_dict(ref.state_dict())
     sc = sc.to(DEV)
     assert sc._k8
-    x = torch.randn(700, C, 9)
+    x = torch.randn(700, C, (lmax + 1) ** 2)
     xd = x.to(DEV).requires_grad_(True)
     xr = x.clone().requires_grad_(True)
     y, yr = sc(xd), ref(xr)
@@ -310,6 +323,27 @@ def test_symmetric_contraction_k8_golden(golden):
     torch.testing.assert_close(y.detach().cpu(), d["out"], atol=1e-5, rtol=1e-5)
     (y * d["g_out"].to(DEV)).sum().backward()
     torch.testing.assert_close(x.grad.cpu(), d["grad_x"], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("name,irr,corr", [
+    ("mace_symmetric_contraction_c4.pt", "4x0e+4x1o+4x2e", 4),
+    ("mace_symmetric_contraction_l3.pt", "4x0e+4x1o+4x2e+4x3o", 3)])
+def test_symmetric_contraction_k8_widening_golden(golden, name, irr, corr):
+    """K8 at correlation 4 (D = 9) and max_ell 3 (D = 16) against the reference's own outputs
+    (tests/golden/make_golden.py mace_widening)."""
+    from gmp_amd import equivariant as eq
+    d = golden(name)
+    sc = eq.SymmetricContraction(irr, irr, corr)
+    sc.load_state_dict({k[6:]: v for k, v in d.items() if k.startswith("param.")}, strict=False)
+    sc = sc.to(DEV)
+    assert sc._k8
+    x = d["x"].clone().to(DEV).requires_grad_(True)
+    y = sc(x)
+    torch.testing.assert_close(y.detach().cpu(), d["out"], atol=1e-5, rtol=1e-5)
+    (y * d["g_out"].to(DEV)).sum().backward()
+    torch.testing.assert_close(x.grad.cpu(), d["grad_x"], atol=1e-5, rtol=1e-5)
+    for k, p in sc.named_parameters():
+        torch.testing.assert_close(p.grad.cpu(), d["grad." + k], atol=1e-5, rtol=1e-5, msg=k)
 
 
 def _fp64_model_check(kind, kw, n, e_per_node, seeds=(1, 2), in_dim=3):
