@@ -12,8 +12,6 @@
 // nodes, with the channel's coefficients (NQ x D floats, monomial-major) in LDS.  Backward: dx by
 // the product rule (same loop), dA~ = sum_b g[b,c,m] (monomial of x[b,c]) reduced over node groups
 // into per-group partials (summed in fixed order by the caller).
-#include <cstdlib>
-
 #include "gmp_common.h"
 
 namespace gmp {
@@ -71,144 +69,13 @@ __device__ __forceinline__ int out_col(int C, int c, int m) {
   return l * l * C + (2 * l + 1) * c + (m - l * l);
 }
 
-// visit every monomial q (in basis order) with its factor indices: f(q, z, i, j, k, l, deg)
+// The monomial walk: rolled loops over the basis in order, this thread's x (and dx) in a private
+// LDS row.  (r04: a fully unrolled walk with x and dx in registers measured slower at the C4
+// shape -- 1.75 / 3.80 ms against 1.05 / 3.03 ms forward / backward at 50k nodes x 128
+// channels, scripts/mb_sc.py: 256 VGPRs and 404 B of scratch per lane in its backward -- and
+// compiled for minutes at D = 16.)
 template <int D, int CORR, class F>
-__device__ __forceinline__ void for_monomials(const float (&xv)[D], F&& f) {
-#pragma unroll
-  for (int i = 0; i < D; ++i) f(i, xv[i], i, 0, 0, 0, 1);
-  if constexpr (CORR >= 2) {
-    int q = nq_deg(D, 1);
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int j = i; j < D; ++j) {
-        f(q, xv[i] * xv[j], i, j, 0, 0, 2);
-        ++q;
-      }
-  }
-  if constexpr (CORR >= 3) {
-    int q = nq_total(D, 2);
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int j = i; j < D; ++j) {
-        const float xij = xv[i] * xv[j];
-#pragma unroll
-        for (int k = j; k < D; ++k) {
-          f(q, xij * xv[k], i, j, k, 0, 3);
-          ++q;
-        }
-      }
-  }
-  if constexpr (CORR >= 4) {
-    int q = nq_total(D, 3);
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int j = i; j < D; ++j) {
-        const float xij = xv[i] * xv[j];
-#pragma unroll
-        for (int k = j; k < D; ++k) {
-          const float xijk = xij * xv[k];
-#pragma unroll
-          for (int l = k; l < D; ++l) {
-            f(q, xijk * xv[l], i, j, k, l, 4);
-            ++q;
-          }
-        }
-      }
-  }
-}
-
-template <int D, int CORR>
-__global__ __launch_bounds__(kSC) void sc_fwd_kernel(int64_t B, int C, const float* __restrict__ x,
-                                                     const float* __restrict__ A1,
-                                                     const float* __restrict__ A2,
-                                                     const float* __restrict__ A3,
-                                                     const float* __restrict__ A4,
-                                                     float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float a[];
-  const int c = blockIdx.y;
-  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
-  __syncthreads();
-  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
-    float xv[D];
-    const float* xr = x + (b * C + c) * D;
-#pragma unroll
-    for (int i = 0; i < D; ++i) xv[i] = xr[i];
-    float acc[D];
-#pragma unroll
-    for (int m = 0; m < D; ++m) acc[m] = 0.f;
-    for_monomials<D, CORR>(xv, [&](int q, float z, int, int, int, int, int) {
-      const float* ar = a + q * D;
-#pragma unroll
-      for (int m = 0; m < D; ++m) acc[m] += ar[m] * z;
-    });
-    float* orow = out + b * (int64_t)(D * C);
-#pragma unroll
-    for (int m = 0; m < D; ++m) orow[out_col(C, c, m)] = acc[m];
-  }
-}
-
-template <int D, int CORR>
-__global__ __launch_bounds__(kSC) void sc_bwd_x_kernel(int64_t B, int C,
-                                                       const float* __restrict__ x,
-                                                       const float* __restrict__ A1,
-                                                       const float* __restrict__ A2,
-                                                       const float* __restrict__ A3,
-                                                       const float* __restrict__ A4,
-                                                       const float* __restrict__ gout,
-                                                       float* __restrict__ dx) {
-  extern __shared__ __attribute__((aligned(16))) float a[];
-  const int c = blockIdx.y;
-  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
-  __syncthreads();
-  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
-    float xv[D], g[D], d[D];
-    const float* xr = x + (b * C + c) * D;
-    const float* gr = gout + b * (int64_t)(D * C);
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      xv[i] = xr[i];
-      d[i] = 0.f;
-    }
-#pragma unroll
-    for (int m = 0; m < D; ++m) g[m] = gr[out_col(C, c, m)];
-    // d/dx_t of (gA_q x_i x_j x_k x_l) = gA_q (the product of the other factors) for each
-    // factor equal to t (repeated indices add up to the power rule)
-    for_monomials<D, CORR>(xv, [&](int q, float, int i, int j, int k, int l, int deg) {
-      const float* ar = a + q * D;
-      float gA = 0.f;
-#pragma unroll
-      for (int m = 0; m < D; ++m) gA += ar[m] * g[m];
-      if (deg == 1) {
-        d[i] += gA;
-      } else if (deg == 2) {
-        d[i] += gA * xv[j];
-        d[j] += gA * xv[i];
-      } else if (deg == 3) {
-        d[i] += gA * (xv[j] * xv[k]);
-        d[j] += gA * (xv[i] * xv[k]);
-        d[k] += gA * (xv[i] * xv[j]);
-      } else {
-        const float xij = xv[i] * xv[j], xkl = xv[k] * xv[l];
-        d[i] += gA * (xv[j] * xkl);
-        d[j] += gA * (xv[i] * xkl);
-        d[k] += gA * (xij * xv[l]);
-        d[l] += gA * (xij * xv[k]);
-      }
-    });
-    float* dr = dx + (b * C + c) * D;
-#pragma unroll
-    for (int i = 0; i < D; ++i) dr[i] = d[i];
-  }
-}
-
-// Runtime-loop forms (D = 4, 16 and correlation 4): the fully unrolled monomial walk above is
-// kept for the benchmarked D = 9, correlation <= 3 (config C4); the others walk the same basis in
-// the same order with rolled loops (compile time), this thread's x and dx in a private LDS row.
-template <int D, int CORR, class F>
-__device__ __forceinline__ void for_monomials_rt(const float* xv, F&& f) {
+__device__ __forceinline__ void for_monomials(const float* xv, F&& f) {
   int q = 0;
 #pragma unroll 1
   for (int i = 0; i < D; ++i) f(q++, xv[i], i, 0, 0, 0, 1);
@@ -245,7 +112,7 @@ __device__ __forceinline__ void for_monomials_rt(const float* xv, F&& f) {
 }
 
 template <int D, int CORR>
-__global__ __launch_bounds__(kSC) void sc_fwd_rt_kernel(int64_t B, int C,
+__global__ __launch_bounds__(kSC) void sc_fwd_kernel(int64_t B, int C,
                                                         const float* __restrict__ x,
                                                         const float* __restrict__ A1,
                                                         const float* __restrict__ A2,
@@ -263,7 +130,7 @@ __global__ __launch_bounds__(kSC) void sc_fwd_rt_kernel(int64_t B, int C,
     float acc[D];
 #pragma unroll
     for (int m = 0; m < D; ++m) acc[m] = 0.f;
-    for_monomials_rt<D, CORR>(xt, [&](int q, float z, int, int, int, int, int) {
+    for_monomials<D, CORR>(xt, [&](int q, float z, int, int, int, int, int) {
       const float* ar = a + q * D;
 #pragma unroll
       for (int m = 0; m < D; ++m) acc[m] += ar[m] * z;
@@ -275,7 +142,7 @@ __global__ __launch_bounds__(kSC) void sc_fwd_rt_kernel(int64_t B, int C,
 }
 
 template <int D, int CORR>
-__global__ __launch_bounds__(kSC) void sc_bwd_x_rt_kernel(int64_t B, int C,
+__global__ __launch_bounds__(kSC) void sc_bwd_x_kernel(int64_t B, int C,
                                                           const float* __restrict__ x,
                                                           const float* __restrict__ A1,
                                                           const float* __restrict__ A2,
@@ -299,7 +166,7 @@ __global__ __launch_bounds__(kSC) void sc_bwd_x_rt_kernel(int64_t B, int C,
     }
 #pragma unroll
     for (int m = 0; m < D; ++m) g[m] = gr[out_col(C, c, m)];
-    for_monomials_rt<D, CORR>(xt, [&](int q, float, int i, int j, int k, int l, int deg) {
+    for_monomials<D, CORR>(xt, [&](int q, float, int i, int j, int k, int l, int deg) {
       const float* ar = a + q * D;
       float gA = 0.f;
 #pragma unroll
@@ -417,29 +284,18 @@ __global__ __launch_bounds__(kSC) void sc_bwd_a_kernel(int64_t B, int C, int64_t
   }
 }
 
-// GMP_SC_ROLLED=1: the rolled-loop kernels for D = 9, correlation <= 3 as well (A/B)
-int g_sc_rolled = getenv("GMP_SC_ROLLED") ? atoi(getenv("GMP_SC_ROLLED")) : 0;
-
 template <int D, int CORR>
 int sc_launch(int64_t n_nodes, int channels, const float* x, const float* A1, const float* A2,
               const float* A3, const float* A4, float* out, const float* gout, float* dx,
               float* dA_partials, hipStream_t s) {
   constexpr int NQ = nq_total(D, CORR);
-  constexpr bool kFull = D == 9 && CORR <= 3;  // unrolled walk (config C4) vs rolled loops
-  const bool full = kFull && !g_sc_rolled;
-  const int smem_f = (NQ * D + (full ? 0 : kSC * (D + 1))) * 4;
-  const int smem_b = (NQ * D + (full ? 0 : kSC * (2 * D + 1))) * 4;
+  const int smem_f = (NQ * D + kSC * (D + 1)) * 4;
+  const int smem_b = (NQ * D + kSC * (2 * D + 1)) * 4;
   const dim3 grid((unsigned)std::min<int64_t>(ceil_div(n_nodes, kSC), kNodeBlocks),
                   (unsigned)channels);
   int rc;
-  auto fwd_k = sc_fwd_rt_kernel<D, CORR>;
-  auto bwd_k = sc_bwd_x_rt_kernel<D, CORR>;
-  if constexpr (kFull) {
-    if (full) {
-      fwd_k = sc_fwd_kernel<D, CORR>;
-      bwd_k = sc_bwd_x_kernel<D, CORR>;
-    }
-  }
+  auto fwd_k = sc_fwd_kernel<D, CORR>;
+  auto bwd_k = sc_bwd_x_kernel<D, CORR>;
   if (out) {
     if ((rc = hip_check(hipFuncSetAttribute((const void*)fwd_k,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, smem_f))))
