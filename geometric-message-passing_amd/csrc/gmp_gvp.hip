@@ -297,7 +297,7 @@ __global__ __launch_bounds__(kGT) void gvp_layer_bwd_kernel(int64_t E, const flo
     gemm_wtx<S / 16, 1>(sWsv, LD128, dgate, s, i, g);  // dspre += Wsv^T dgate
     if (k.valid) {
       st_row<S / 16>(O.dspre + k.e * S, s, g);
-      st_row<S / 16>(O.spre + k.e * S, F.spre, g);
+      if (O.spre) st_row<S / 16>(O.spre + k.e * S, F.spre, g);  // (optional: see gmp.h)
       st_row<1>(O.dgate + k.e * V, dgate, g);
       st_row<1>(O.vn + k.e * V, F.vn, g);
       st_vrow<1>(O.vh + k.e * (3 * V), F.vh, g);
@@ -610,7 +610,7 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   GMP_CHECK_ARG(n_edges >= 0);
   if (n_edges == 0) return GMP_OK;
   GMP_CHECK_ARG(s_in && v_in && Ws && bs && Wsv && bsv && Wh && Wv && ds_out && dv_out);
-  GMP_CHECK_ARG(ds_in && dv_in && dspre && spre && dgate && vn && vh && dvpre && dvh);
+  GMP_CHECK_ARG(ds_in && dv_in && dspre && dgate && vn && vh && dvpre && dvh);
   GMP_CHECK_ARG(al16(s_in) && al16(v_in) && al16(ds_out) && al16(dv_out) && al16(ds_in) &&
                 al16(dv_in) && al16(dspre) && al16(spre) && al16(dgate) && al16(vn) &&
                 al16(vh) && al16(dvpre) && al16(dvh));

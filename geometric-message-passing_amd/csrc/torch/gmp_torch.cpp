@@ -1220,7 +1220,7 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
 }
 
 std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>& W,
-                                  const Tensor& ds, const Tensor& dv, bool relu) {
+                                  const Tensor& ds, const Tensor& dv, bool relu, bool want_spre) {
   OpGuard g(s, "gvp_layer_bwd");
   const int64_t E = gvp_rows(s, v);
   gvp_w_checks(W, kGvpLayerW);
@@ -1230,13 +1230,13 @@ std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::v
   shape(dv, v.sizes(), "dv");
   auto o = fopt(s);
   Tensor ds_in = at::empty_like(s), dv_in = at::empty_like(v);
-  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({E, 128}, o);
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({want_spre ? E : 0, 128}, o);
   Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 16}, o);
   Tensor vh = at::empty({E, 48}, o), dvpre = at::empty({E, 48}, o), dvh = at::empty({E, 48}, o);
   check_rc(gmp_gvp_layer_bwd_f32(E, relu ? 1 : 0, fp(s), fp(v), fp(W[0]), fp(W[1]), fp(W[2]),
                                  fp(W[3]), fp(W[4]), fp(W[5]), fp(ds), fp(dv), fp(ds_in),
-                                 fp(dv_in), fp(dspre), fp(spre), fp(dgate), fp(vn), fp(vh),
-                                 fp(dvpre), fp(dvh), cur_stream()),
+                                 fp(dv_in), fp(dspre), want_spre ? fp(spre) : nullptr, fp(dgate),
+                                 fp(vn), fp(vh), fp(dvpre), fp(dvh), cur_stream()),
            "gmp_gvp_layer_bwd_f32");
   return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
 }
@@ -1488,11 +1488,11 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
   return {at::empty_like(s), at::empty_like(v)};
 }
 std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&,
-                                  const Tensor&, const Tensor&, bool) {
+                                  const Tensor&, const Tensor&, bool, bool want_spre) {
   const int64_t E = s.size(0);
   auto o = s.options();
   return {at::empty_like(s),      at::empty_like(v),     at::empty({E, 128}, o),
-          at::empty({E, 128}, o), at::empty({E, 16}, o), at::empty({E, 16}, o),
+          at::empty({want_spre ? E : 0, 128}, o), at::empty({E, 16}, o), at::empty({E, 16}, o),
           at::empty({E, 48}, o),  at::empty({E, 48}, o), at::empty({E, 48}, o)};
 }
 std::tuple<Tensor, Tensor> gvp_msg0_fwd(const Tensor& send, const Tensor&, const Tensor& P,
@@ -1598,7 +1598,8 @@ TORCH_LIBRARY(gmp, m) {
         "-> (Tensor C, Tensor colsum)");
   m.def("gvp_layer_fwd(Tensor s, Tensor v, Tensor[] W, bool relu) -> (Tensor s_out, "
         "Tensor v_out)");
-  m.def("gvp_layer_bwd(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, bool relu) -> "
+  m.def("gvp_layer_bwd(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, bool relu, "
+        "bool want_spre=True) -> "
         "Tensor[]");
   m.def("gvp_msg0_fwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
         "Tensor[] W) -> (Tensor s_out, Tensor v_out)");

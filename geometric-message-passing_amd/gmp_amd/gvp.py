@@ -184,14 +184,18 @@ class GvpLayerFn(torch.autograd.Function):
         dv = ops._f32c(dv) if dv is not None else torch.zeros_like(v)
         f = dict(dtype=torch.float32, device=s.device)
         with ops._timed("gvp_layer_bwd"):
-            ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh = _lib.torch_ops().gvp_layer_bwd(
-                s, v, W, ds, dv, bool(ctx.relu))
+            ds_in, dv_in, dspre, _, dgate, vn, vh, dvpre, dvh = _lib.torch_ops().gvp_layer_bwd(
+                s, v, W, ds, dv, bool(ctx.relu), False)
         # weight gradients (edge outer sums) on the side stream, deferred to the end of backward
-        with ops.side_work(dspre, s, vn, dgate, spre, dvh, v, dvpre, vh) as sw:
+        with ops.side_work(dspre, s, vn, dgate, dvh, v, dvpre, vh) as sw:
             # dWs = dspre^T [s | vn]: one pass over dspre where the split-plane kernel applies
             dWs, dbs = torch.empty((128, 144), **f), torch.empty(128, **f)
             ops.outer_sum_into2(dspre, s.view(E, 128), vn, dWs, dbs)
-            dWsv, dbsv = _osum(dgate, spre)
+            # dWsv = sum_e dgate (x) spre with spre = Ws [s | vn] + bs, without the (E, 128) spre
+            # rows: (sum_e dgate (x) [s | vn]) Ws^T + (sum_e dgate) (x) bs
+            Gx, dbsv = torch.empty((16, 144), **f), torch.empty(16, **f)
+            ops.outer_sum_into2(dgate, s.view(E, 128), vn, Gx, dbsv)
+            dWsv = torch.addmm(torch.outer(dbsv, W[1]), Gx, W[0].t())
             dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
             dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
         grads = (dWs, dbs, dWsv, dbsv, dWh, dWv)

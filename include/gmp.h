@@ -512,6 +512,9 @@ int gmp_gvp_layer_fwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
                           const float* Ws, const float* bs, const float* Wsv, const float* bsv,
                           const float* Wh, const float* Wv, float* s_out, float* v_out,
                           void* stream);
+/* gmp_gvp_layer_bwd_f32: spre (the pre-activation scalar rows, only the dWsv weight sum reads
+ * them) may be NULL -- the caller then forms dWsv = (sum_e dgate_e (x) [s_e | vn_e]) Ws^T +
+ * (sum_e dgate_e) (x) bs without them (r04: 1 KB per edge of HBM traffic less). */
 int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
                           const float* Ws, const float* bs, const float* Wsv, const float* bsv,
                           const float* Wh, const float* Wv, const float* ds_out,
