@@ -241,7 +241,8 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     int64_t M, int N, int64_t K1, const float* __restrict__ A1, int64_t lda1, int64_t K2,
     const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
     int64_t ldb, int64_t bplane, float* __restrict__ C, int64_t cgrp, int64_t cldg,
-    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const float* __restrict__ bias) {
+    int64_t cldr, int64_t cldn, int tiles_m, int tiles_n, const float* __restrict__ bias,
+    int prio) {
   constexpr int NP = 3;
   constexpr int WGN = 8 / WGM;              // waves along N
   constexpr int BM = 64 * WGM, BN = 32 * WGN;
@@ -289,17 +290,18 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
     abase1[q] = A1 + grc * lda1 + 4 * akq[q];
     abase2[q] = A2 ? A2 + grc * lda2 + 4 * akq[q] : abase1[q];
   }
-  // this wave's two B column tiles (fragment order; tiles past N read tile 0, zeroed)
+  // this wave's two B column tiles (fragment order) through a buffer descriptor: a tile past N
+  // gets an out-of-range offset (loads zeros, no select); the stage part of the offset is
+  // wave-uniform
   const int64_t ct_total = N / 16;
-  int64_t bct[2];
-  bool bok[2];
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(Bp), 0, 0x7fffffff, 0x00020000);
+  unsigned boff[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int64_t ct = (n0 >> 4) + 2 * wn + c;
-    bok[c] = ct < ct_total;
-    bct[c] = bok[c] ? ct : 0;
+    boff[c] = ct < ct_total ? (unsigned)((ct * NP * 512 + 8 * lane) * 2) : 0x80000000u;
   }
-  const unsigned short* bl = Bp + 8 * lane;
 
   // A ring: RA register slots (slot t % RA holds stage t); a stage's loads are issued RA
   // iterations before its split + LDS write.  RA = 2 kept 32 KB of the A stream (the S rows) in
@@ -319,13 +321,13 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   };
   auto fetch_b = [&](int slot, int st) {
     const int64_t stc = st < nst ? st : nst - 1;
+    const int so = (int)(stc * ct_total * NP * 512 * 2);  // bytes, wave-uniform
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        u32x4 v = *reinterpret_cast<const u32x4*>(bl + ((stc * ct_total + bct[c]) * NP + p) * 512);
-        ringB[slot][c][p] = bok[c] ? v : u32x4{0u, 0u, 0u, 0u};
-      }
+      for (int p = 0; p < NP; ++p)
+        ringB[slot][c][p] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(brs, boff[c], so + p * 1024, 0));
   };
   auto stash = [&](int slot, unsigned char* buf, int st) {
     const bool live = st < nst;
@@ -373,6 +375,9 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   __syncthreads();
   load_a(F[0], smg);
   __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
+  // optional static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per
+  // SIMD, item 4); A/B knob GMP_GEMM_PRIO
+  if (prio && w >= 4) __builtin_amdgcn_s_setprio(1);
   for (int s0 = 0; s0 < nst_pad; s0 += RA) {
 #pragma unroll
     for (int j = 0; j < RA; ++j) {
@@ -751,6 +756,8 @@ int g_tpgemm_ring = getenv("GMP_TPGEMM_RING") ? atoi(getenv("GMP_TPGEMM_RING")) 
 int g_widen_ring = getenv("GMP_TPGEMM_WIDEN_RING") ? atoi(getenv("GMP_TPGEMM_WIDEN_RING")) : 4;
 // forward path GEMM: the 256 x 64 tile for mul_out <= 64 (GMP_TPGEMM_NARROW=0: 128 x 128)
 int g_tpgemm_narrow = getenv("GMP_TPGEMM_NARROW") ? atoi(getenv("GMP_TPGEMM_NARROW")) : 1;
+// 1: s_setprio 1 for waves 4-7 of the forward path GEMM (A/B)
+int g_gemm_prio = getenv("GMP_GEMM_PRIO") ? atoi(getenv("GMP_GEMM_PRIO")) : 0;
 }  // namespace gmp
 
 template <int NP>
@@ -815,7 +822,7 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   k<<<(unsigned)nwg, kGT, smem, as_stream(stream)>>>(
       M, (int)N, K1, A1, lda1, K2, K2 ? A2 : A1, K2 ? lda2 : lda1,
       static_cast<const unsigned short*>(Bp), ldb, bplane, C, cgrp, cldg, cldr, cldn,
-      (int)tiles_m, (int)tiles_n, bias);
+      (int)tiles_m, (int)tiles_n, bias, g_gemm_prio);
   return launch_status();
 }
 
