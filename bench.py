@@ -153,6 +153,24 @@ def pmc_traffic(workload, kernel):
     return None
 
 
+def step_traffic(workload):
+    """HBM bytes per training step (all kernels) from the newest committed PMC summary
+    (profiles/<round>_<workload>_kernels.json with steps_in_trace), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_kernels.json")))
+    for path in reversed(files):
+        with open(path) as f:
+            d = json.load(f)
+        steps = d.get("steps_in_trace")
+        rows = d["kernels"]
+        if not steps or any(r["hbm_read_bytes_per_launch"] is None or
+                            r["hbm_write_bytes_per_launch"] is None for r in rows):
+            continue
+        return (sum(r["calls"] * (r["hbm_read_bytes_per_launch"] + r["hbm_write_bytes_per_launch"])
+                    for r in rows) / steps, os.path.basename(path))
+    return None
+
+
 def tp_node_flops(model, n_nodes, n_edges):
     """Algorithmic FLOPs per training step of the receiver-factorised TP convolutions
     (DESIGN.md §K7): per layer, S = sum_e z_e (x) a_e (2 E 257 z_size) and the path GEMMs
@@ -606,6 +624,19 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup, exact=False
                     "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                     "traffic": None, "flops_per_edge": fl}
+            st = step_traffic(workload)
+            if st is not None:
+                # the step moves more bytes per second than it computes: HBM is the binding
+                # bound (DESIGN.md §3 "Round 4", GVP); the MFMA figures stay as secondary fields
+                gbs = st[0] / (elapsed / steps) / 1e9
+                roof = {"kernel": "whole step (fwd+bwd, all kernels)", "kernel_prefix": "-",
+                        "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": gbs / HBM_PEAK_GBS, "traffic": st[0],
+                        "traffic_note": "PMC HBM bytes per training step (FETCH_SIZE x2 + "
+                                        "WRITE_SIZE) of the committed profile",
+                        "traffic_source": f"profiles/{st[1]}",
+                        "mfma_achieved": achieved, "mfma_peak": FP32_MFMA_PEAK_TFLOPS,
+                        "mfma_frac": achieved / FP32_MFMA_PEAK_TFLOPS, "flops_per_edge": fl}
         else:
             roof = mace_roofline(model, g.num_nodes, g.num_edges, totals, counts, n_timed,
                                  workload)
