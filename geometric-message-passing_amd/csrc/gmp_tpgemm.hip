@@ -377,7 +377,10 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
   // optional static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per
   // SIMD, item 4); A/B knob GMP_GEMM_PRIO
-  if (prio && w >= 4) __builtin_amdgcn_s_setprio(1);
+  if ((prio & 1) && w >= 4) __builtin_amdgcn_s_setprio(1);
+  // prio bit 1 (A/B): waves 4-7, the SIMD partners of waves 0-3, run each stage's MFMAs before
+  // its split / LDS stash, so one wave of a SIMD pair splits while the other multiplies
+  const bool late = (prio & 2) && w >= 4;
   for (int s0 = 0; s0 < nst_pad; s0 += RA) {
 #pragma unroll
     for (int j = 0; j < RA; ++j) {
@@ -387,14 +390,22 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
       // sched barriers pin the ring discipline: slot sl's registers are consumed by the stash
       // before its next loads are issued, so the stash waits only for loads RA stages old
       // (counted vmcnt) instead of the scheduler hoisting the new loads and draining vmcnt(0)
-      stash(sl, smg + (st & 1) * STG, st + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      fetch(sl, st + 2 + RA);
-      __builtin_amdgcn_sched_barrier(0);
+      if (!late) {
+        stash(sl, smg + (st & 1) * STG, st + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        fetch(sl, st + 2 + RA);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       load_a(F[(j & 1) ^ 1], nb);
       mma_ab<NP>(acc, F[j & 1], ringB[j % RBB]);
       __builtin_amdgcn_sched_barrier(0);
       fetch_b(j % RBB, st + RBB);  // the slot the MFMAs above just read: RBB stages of lead
+      if (late) {  // (the stash writes the buffer stage st used: its fragments are in registers)
+        __builtin_amdgcn_sched_barrier(0);
+        stash(sl, smg + (st & 1) * STG, st + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        fetch(sl, st + 2 + RA);
+      }
       __syncthreads();
     }
   }
@@ -756,8 +767,10 @@ int g_tpgemm_ring = getenv("GMP_TPGEMM_RING") ? atoi(getenv("GMP_TPGEMM_RING")) 
 int g_widen_ring = getenv("GMP_TPGEMM_WIDEN_RING") ? atoi(getenv("GMP_TPGEMM_WIDEN_RING")) : 4;
 // forward path GEMM: the 256 x 64 tile for mul_out <= 64 (GMP_TPGEMM_NARROW=0: 128 x 128)
 int g_tpgemm_narrow = getenv("GMP_TPGEMM_NARROW") ? atoi(getenv("GMP_TPGEMM_NARROW")) : 1;
-// 1: s_setprio 1 for waves 4-7 of the forward path GEMM (A/B)
-int g_gemm_prio = getenv("GMP_GEMM_PRIO") ? atoi(getenv("GMP_GEMM_PRIO")) : 0;
+// forward path GEMM schedule (GMP_GEMM_PRIO): bit 0 s_setprio 1 for waves 4-7, bit 1 waves 4-7
+// run their MFMAs before the stage's split / stash.  MACE-128 lo = 2 shape, one box: 0: 12.80 /
+// 12.73 ms, 2: 12.50, 3: 12.43 (default)
+int g_gemm_prio = getenv("GMP_GEMM_PRIO") ? atoi(getenv("GMP_GEMM_PRIO")) : 3;
 }  // namespace gmp
 
 template <int NP>

@@ -868,9 +868,14 @@ __global__ __launch_bounds__(kXT, OCC) void outer_cols_x3g_kernel(
       const bool ok = k0 + (int64_t)st * kXK + 4 * eq + j < k1;
       v[j] = ok ? ra[slot][j] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    // column 4 cg + c goes to image row 4 cg + (c ^ 2 (cg & 1)): the two channel groups of a
+    // 16-lane store group then land 2 or 6 rows apart (128 B mod the 256-byte bank period)
+    // instead of 4 (the same banks: a 2-way conflict on every store); the epilogue undoes the
+    // permutation
+    const int cx = 2 * (cg & 1);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const int off = xoff(4 * cg + c, eq >> 1) + 8 * (eq & 1);
+      const int off = xoff(4 * cg + (c ^ cx), eq >> 1) + 8 * (eq & 1);
       unsigned h0, m0, l0, h1, m1, l1;
       split3(f32x2{v[0][c], v[1][c]}, h0, m0, l0);
       split3(f32x2{v[2][c], v[3][c]}, h1, m1, l1);
@@ -946,7 +951,9 @@ __global__ __launch_bounds__(kXT, OCC) void outer_cols_x3g_kernel(
     for (int c = 0; c < CT; ++c)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        out[(int64_t)(64 * wm + 16 * r + 4 * g + q) * n + 16 * (wn * CT + c) + li] = acc[r][c][q];
+        // image row 64 wm + 16 r + 4 g + q holds column 64 wm + 16 r + 4 g + (q ^ 2 (g & 1))
+        out[(int64_t)(64 * wm + 16 * r + 4 * g + (q ^ (2 * (g & 1)))) * n + 16 * (wn * CT + c) +
+            li] = acc[r][c][q];
 }
 
 // Node-level sums (r04): C (m x n, m, n multiples of 64, <= 256) = A^T B (+ colsum(A)) over K
@@ -1055,8 +1062,11 @@ __global__ __launch_bounds__(kQT, 2) void outer_sum_quad_kernel(
 
 // GMP_WGRAD_QUAD=0: node-level sums on the r03 split-K kernels (A/B)
 int g_quad = getenv("GMP_WGRAD_QUAD") ? atoi(getenv("GMP_WGRAD_QUAD")) : 1;
+// workgroups per CU x 2 of the node-level quadrant sums (GMP_QUAD_WG2; A/B: fewer workgroups
+// = fewer partial slabs for the ordered reduction, more rows each)
+int g_quad_wg2 = getenv("GMP_QUAD_WG2") ? atoi(getenv("GMP_QUAD_WG2")) : 4;
 int64_t quad_splits(int64_t K, int64_t quads) {
-  int64_t s = ceil_div(2 * (int64_t)device_cu_count(), quads);  // ~2 workgroups per CU
+  int64_t s = ceil_div((int64_t)g_quad_wg2 * device_cu_count() / 2, quads);  // ~2 per CU
   const int64_t cap = ceil_div(K, 256);                          // >= 256 rows each
   if (s > cap) s = cap;
   return s < 1 ? 1 : s;
