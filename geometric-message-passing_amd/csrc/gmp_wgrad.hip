@@ -868,11 +868,11 @@ __global__ __launch_bounds__(kXT, OCC) void outer_cols_x3g_kernel(
       const bool ok = k0 + (int64_t)st * kXK + 4 * eq + j < k1;
       v[j] = ok ? ra[slot][j] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    // column 4 cg + c goes to image row 4 cg + (c ^ 2 (cg & 1)): the two channel groups of a
-    // 16-lane store group then land 2 or 6 rows apart (128 B mod the 256-byte bank period)
-    // instead of 4 (the same banks: a 2-way conflict on every store); the epilogue undoes the
-    // permutation
-    const int cx = 2 * (cg & 1);
+    // column 4 cg + c goes to image row 4 cg + (c ^ (cg & 1)): the two channel groups of a
+    // 16-lane ds_write_b64 group (banks (a / 4) mod 32: a 128-byte period) then land 3 or 5
+    // rows apart (64 B mod 128) instead of 4 (the same banks: a 2-way conflict on every store);
+    // the epilogue undoes the permutation
+    const int cx = cg & 1;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int off = xoff(4 * cg + (c ^ cx), eq >> 1) + 8 * (eq & 1);
@@ -951,9 +951,9 @@ __global__ __launch_bounds__(kXT, OCC) void outer_cols_x3g_kernel(
     for (int c = 0; c < CT; ++c)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        // image row 64 wm + 16 r + 4 g + q holds column 64 wm + 16 r + 4 g + (q ^ 2 (g & 1))
-        out[(int64_t)(64 * wm + 16 * r + 4 * g + (q ^ (2 * (g & 1)))) * n + 16 * (wn * CT + c) +
-            li] = acc[r][c][q];
+        // image row 64 wm + 16 r + 4 g + q holds column 64 wm + 16 r + 4 g + (q ^ (g & 1))
+        out[(int64_t)(64 * wm + 16 * r + 4 * g + (q ^ (g & 1))) * n + 16 * (wn * CT + c) + li] =
+            acc[r][c][q];
 }
 
 // Node-level sums (r04): C (m x n, m, n multiples of 64, <= 256) = A^T B (+ colsum(A)) over K

@@ -259,8 +259,8 @@ def _destroy_stream(ptr):
         pass
 
 
-def _side_stream(device, masked=False):
-    key = (device, masked and SIDE_CUS > 0)
+def _side_stream(device, masked=False, lane=0):
+    key = (device, masked and SIDE_CUS > 0, lane)
     st = _SIDE_STREAMS.get(key)
     if st is None:
         if key[1]:
@@ -314,6 +314,13 @@ def _engine_accumulates(p):
 # fewer workgroups the weight gradients leave CUs to the critical path's node-level kernels.
 SIDE_GRID_CAP = int(os.environ.get("GMP_SIDE_GRID_CAP", "0") or 0)
 
+# side-stream lane of the EGNN edge-level weight sums (dW2, dW3); 0 = the node-level sums' stream.
+# A second lane removes the first layer's tail (the sums start when their inputs are ready
+# instead of behind the node-level sums) but measured slower on the whole step (C2, one box:
+# 103.5 / 102.2 vs 104.4 / 103.8 M edges/s): the concurrent sums crowd the critical path's
+# node kernels for CUs.  Default 0.
+EDGE_SUM_LANE = int(os.environ.get("GMP_EDGE_SUM_LANE", "0") or 0)
+
 
 def compiling():
     """True while torch.compile (dynamo) traces: the ops then run inline on the current stream,
@@ -326,18 +333,24 @@ class side_work:
     already queued on the current stream; sw.deliver(...) hands each result to the end-of-
     backward accumulation (deferred leaf gradients) or back through autograd (after joining the
     streams).  tail=True: nothing on the critical path follows (no split-K grid cap).  Under
-    torch.compile the work runs inline and every gradient goes back through autograd."""
+    torch.compile the work runs inline and every gradient goes back through autograd.  lane > 0
+    picks another side stream: work that must not queue behind the first side stream's (the
+    EGNN edge-level sums behind the node-level ones) runs concurrently with it; deliver(...,
+    extra=(other side_work, ..)) joins those streams too."""
 
-    def __init__(self, *used, tail=False):
+    def __init__(self, *used, tail=False, lane=0):
         self.used = [t for t in used if t is not None]
         self.cap = 0 if tail else SIDE_GRID_CAP
         self.inline = compiling()
+        self.lane = lane
+        self.extra = ()
 
     def __enter__(self):
         if self.inline:
             return self
         self.main = torch.cuda.current_stream()
-        self.side = _side_stream(self.main.device, masked=self.main.cuda_stream != 0)
+        self.side = _side_stream(self.main.device, masked=self.main.cuda_stream != 0,
+                                 lane=self.lane)
         self.side.wait_stream(self.main)
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
@@ -362,14 +375,17 @@ class side_work:
     def join(self, *results):
         """results are needed on the current stream now (returned through autograd)."""
         self.main.wait_stream(self.side)
+        for o in self.extra:
+            self.main.wait_stream(o.side)
         _KEEPALIVE.clear()
         for r in results:
             if r is not None:
                 r.record_stream(self.main)
 
-    def deliver(self, needs_input_grad, first, targets, grads):
+    def deliver(self, needs_input_grad, first, targets, grads, extra=()):
         """Per parameter: defer the gradient (leaf parameter) or hand it back through autograd
         (after joining the streams).  needs_input_grad[first + i] belongs to targets[i]."""
+        self.extra = tuple(o for o in extra if not o.inline)
         if self.inline:
             return tuple(gr if needs_input_grad[first + i] else None
                          for i, gr in enumerate(grads))
@@ -393,6 +409,8 @@ class side_work:
             # no parameter gradient wanted (e.g. autograd.grad w.r.t. inputs only): nothing will
             # flush this side work, so join here and release the kept-alive inputs
             self.main.wait_stream(self.side)
+            for o in self.extra:
+                self.main.wait_stream(o.side)
             _KEEPALIVE.clear()
         return tuple(out)
 
@@ -908,7 +926,14 @@ class EgnnMessageFn(torch.autograd.Function):
 
         # weight gradients: side stream, accumulated at the end of the backward pass
         (_, b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3, b3, ln3w, ln3b, w4, b4) = params
-        with side_work(h, dA, dB, dpre2, dpre3, xhat, partials, amax) as sw:
+        # the edge-level sums (dW2, dW3: ~0.2 ms each), on a side-stream lane of their own when
+        # EDGE_SUM_LANE > 0
+        with side_work(dpre2, dpre3, xhat, amax, lane=EDGE_SUM_LANE) as sw2:
+            dW2, db2 = edge_outer_sum_act(dpre2, xh1, ln1w, ln1b, ctx.act,
+                                          amax[0:1] if amax is not None else None)
+            dW3, db3 = edge_outer_sum_act(dpre3, xh2, ln2w, ln2b, ctx.act,
+                                          amax[1:2] if amax is not None else None)
+        with side_work(h, dA, dB, partials) as sw:
             dW1 = torch.empty((d, 2 * d + 1), **f)
             db1 = torch.empty(d, **f)
             outer_sum_into(dA, h, dW1[:, :d], db1)
@@ -916,14 +941,10 @@ class EgnnMessageFn(torch.autograd.Function):
             v = partials.sum(0)
             dln1w, dln1b, dln2w, dln2b, dln3w, dln3b, dw4, dw1d = v[:8 * d].view(8, d).unbind(0)
             dW1[:, 2 * d].copy_(dw1d)
-            dW2, db2 = edge_outer_sum_act(dpre2, xh1, ln1w, ln1b, ctx.act,
-                                          amax[0:1] if amax is not None else None)
-            dW3, db3 = edge_outer_sum_act(dpre3, xh2, ln2w, ln2b, ctx.act,
-                                          amax[1:2] if amax is not None else None)
             grads = (dW1, db1, dln1w, dln1b, dW2, db2, dln2w, dln2b, dW3, db3, dln3w, dln3b,
                      dw4.view(1, d), v[8 * d:8 * d + 1])
         # the caller's parameter tensors (saved tensors unpack to the same objects): W1 itself,
         # then b1 ... b4 (params[0] is the contiguous copy of W1's distance column)
         targets = (W1,) + tuple(params[1:])
         return (dh, dpos, None, None, None, None) + sw.deliver(ctx.needs_input_grad, 6, targets,
-                                                               grads)
+                                                               grads, extra=(sw2,))
