@@ -532,7 +532,8 @@ bool desc_ok(const Desc& d, int layout) {
 // (x rows are read straight from global memory: no LDS bound on in_dim)
 bool desc_ok_z(const Desc& d) {
   return d.n_paths > 0 && d.n_paths <= kMaxPaths && d.in_dim > 0 && d.in_dim <= (1 << 16) &&
-         (d.sh_dim == 1 || d.sh_dim == 4 || d.sh_dim == 9 || d.sh_dim == kMaxSh) &&
+         (d.sh_dim == 1 || d.sh_dim == 4 || d.sh_dim == 9 || d.sh_dim == kMaxSh ||
+          d.sh_dim == 25 || d.sh_dim == 36) &&
          d.z_size > 0 && d.n_blocks > 0 && d.n_blocks <= kMaxBlocks;
 }
 
@@ -850,6 +851,155 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------- z, runtime l <= 5
+// Plans with an l of 4 or 5 (TFN / MACE max_ell = 5, experiments/rotsym.ipynb) take these
+// kernels: the same per-edge arithmetic with runtime (l1, l2, lo) loops.  One wave per edge; the
+// edge's SH row (36 floats) and each path's T = C . Y table (<= 11 x 11) go through a per-wave
+// LDS slice (computed once by the wave's lanes, read as broadcasts), the CG table through LDS /
+// global as the fixed-l kernels.  Not tuned (widening configs at one layer).
+constexpr int kMaxShG = 36, kMaxTG = 121;
+constexpr int kMaxCgG = 8192;  // CG floats of a descriptor (generic kernels)
+
+__device__ __forceinline__ void gen_t_table(const float* C, const float* sY, int d1, int d2,
+                                            int d3, int yo, float* sT, int lane) {
+  for (int t = lane; t < d1 * d3; t += 64) {
+    const int i = t / d3, k = t - i * d3;
+    float a = 0.f;
+    for (int j = 0; j < d2; ++j) a += C[(i * d2 + j) * d3 + k] * sY[yo + j];
+    sT[t] = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void tp_edge_z_gen_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+    const float* __restrict__ x, const float* __restrict__ sh,
+    const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
+    int64_t e1, float* __restrict__ zbuf) {
+  __shared__ float sC[kMaxCgG];
+  __shared__ float sYT[4][kMaxShG + kMaxTG];
+  for (int c = threadIdx.x; c < cg_len; c += blockDim.x) sC[c] = cg[c];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* sY = sYT[wv];
+  float* sT = sYT[wv] + kMaxShG;
+  const int64_t ne = e1 - e0;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t k = (int64_t)blockIdx.x * 4 + wv; k < ne; k += nw) {
+    const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
+    const int64_t src = src_sorted[e], eo = perm[e];
+    if (lane < d.sh_dim) sY[lane] = sh[eo * d.sh_dim + lane];
+    const float* xrow = x + src * d.in_dim;
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = paths[p];
+      const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1;
+      __builtin_amdgcn_wave_barrier();  // the slice's previous readers are this wave's lanes
+      gen_t_table(sC + P.cg_off, sY, d1, d2, d3, P.l2 * P.l2, sT, lane);
+      __builtin_amdgcn_wave_barrier();
+      float* zr = zbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)(d3 * P.mul1);
+      for (int u = lane; u < P.mul1; u += 64) {
+        const float* xu = xrow + P.x_off + u * d1;
+        for (int kk = 0; kk < d3; ++kk) {
+          float a = 0.f;
+          for (int i = 0; i < d1; ++i) a += xu[i] * sT[i * d3 + kk];
+          zr[kk * P.mul1 + u] = P.alpha * a;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(256) void tp_edge_z_gen_bwd_kernel(
+    Desc d, const Path* __restrict__ paths, const float* __restrict__ cg, int cg_len,
+    const float* __restrict__ x, const float* __restrict__ sh,
+    const int64_t* __restrict__ src_sorted, const int64_t* __restrict__ perm, int64_t e0,
+    int64_t e1, const float* __restrict__ dzbuf, float* __restrict__ dx_edge,
+    float* __restrict__ dY_edge) {
+  __shared__ float sC[kMaxCgG];
+  __shared__ float sYT[4][kMaxShG + kMaxTG];
+  __shared__ float sdY[4][kMaxShG];
+  for (int c = threadIdx.x; c < cg_len; c += blockDim.x) sC[c] = cg[c];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* sY = sYT[wv];
+  float* sT = sYT[wv] + kMaxShG;
+  const int64_t ne = e1 - e0;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t k = (int64_t)blockIdx.x * 4 + wv; k < ne; k += nw) {
+    const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
+    const int64_t src = src_sorted[e], eo = perm[e];
+    __builtin_amdgcn_wave_barrier();
+    if (lane < d.sh_dim) {
+      sY[lane] = sh[eo * d.sh_dim + lane];
+      sdY[wv][lane] = 0.f;
+    }
+    const float* xrow = x + src * d.in_dim;
+    float* dxr = dx_edge + k * d.in_dim;
+    // the dx row: zero (each entry by the lane that will accumulate it: u = lane + 64 t),
+    // entries no path reads included, then one read-modify-write pass per path
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = paths[p];
+      const int d1 = 2 * P.l1 + 1;
+      for (int u = lane; u < P.mul1; u += 64)
+        for (int i = 0; i < d1; ++i) dxr[P.x_off + u * d1 + i] = 0.f;
+    }
+    for (int c = lane; c < d.in_dim; c += 64) {
+      bool in = false;
+      for (int p = 0; p < d.n_paths; ++p) {
+        const Path P = paths[p];
+        in |= c >= P.x_off && c < P.x_off + P.mul1 * (2 * P.l1 + 1);
+      }
+      if (!in) dxr[c] = 0.f;
+    }
+    for (int p = 0; p < d.n_paths; ++p) {
+      const Path P = paths[p];
+      const int d1 = 2 * P.l1 + 1, d2 = 2 * P.l2 + 1, d3 = 2 * P.lo + 1, yo = P.l2 * P.l2;
+      __builtin_amdgcn_wave_barrier();
+      gen_t_table(sC + P.cg_off, sY, d1, d2, d3, yo, sT, lane);
+      __builtin_amdgcn_wave_barrier();
+      const float* C = sC + P.cg_off;
+      const float* dzr = dzbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)(d3 * P.mul1);
+      // per lane: dx[u, i] += alpha sum_k T[i, k] dz[u, k]; dY_j partials
+      // sum_{u, i, k} C[i, j, k] x[u, i] alpha dz[u, k]
+      float dyp[11];
+      for (int j = 0; j < 11; ++j) dyp[j] = 0.f;
+      for (int u = lane; u < P.mul1; u += 64) {
+        const float* xu = xrow + P.x_off + u * d1;
+        float dz[11];
+#pragma unroll
+        for (int kk = 0; kk < 11; ++kk) dz[kk] = kk < d3 ? P.alpha * dzr[kk * P.mul1 + u] : 0.f;
+        for (int i = 0; i < d1; ++i) {
+          float a = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < 11; ++kk)
+            if (kk < d3) a += sT[i * d3 + kk] * dz[kk];
+          dxr[P.x_off + u * d1 + i] += a;
+          const float xi = xu[i];
+#pragma unroll
+          for (int j = 0; j < 11; ++j) {
+            if (j < d2) {
+              float c = 0.f;
+#pragma unroll
+              for (int kk = 0; kk < 11; ++kk)
+                if (kk < d3) c += C[(i * d2 + j) * d3 + kk] * dz[kk];
+              dyp[j] += xi * c;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 11; ++j) {
+        if (j < d2) {  // wave-uniform
+          const float v = wave_sum64(dyp[j]);
+          if (lane == 0) sdY[wv][yo + j] += v;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < d.sh_dim) dY_edge[k * d.sh_dim + lane] = sdY[wv][lane];
+  }
+}
+
 // GMP_TP_Z_GENERIC=1: always the l <= 3 instantiation.  r03 A/B: the l <= 2 instantiation (z 59
 // vs 91 VGPRs, 8 vs 5 waves per SIMD; dz 187 vs 249, and a 168-VGPR / 3-wave cap with 52 B of
 // scratch) measured within noise on the MACE / TFN steps (481.5 / 483.3 / 483.7 k; 998 / 994 /
@@ -944,11 +1094,14 @@ int gmp_tp_edge_z_lmax_f32(const void* desc_host, int l_max, const void* paths_d
                            float* zbuf, void* stream) {
   GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && zbuf);
   const Desc d = *reinterpret_cast<const Desc*>(desc_host);
-  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= kMaxCg);
-  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 3);
+  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= (l_max > 3 ? kMaxCgG : kMaxCg));
+  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 5);
   if (e1 == e0) return GMP_OK;
   const unsigned grid = (unsigned)z2_blocks(e1 - e0);
-  if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
+  if (l_max > 3 || d.sh_dim > kMaxSh)
+    tp_edge_z_gen_kernel<<<grid, 256, 0, as_stream(stream)>>>(
+        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
+  else if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
     tp_edge_z2_kernel<2><<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
   else
@@ -972,11 +1125,15 @@ int gmp_tp_edge_z_bwd_lmax_f32(const void* desc_host, int l_max, const void* pat
   GMP_CHECK_ARG(desc_host && paths_dev && cg_dev && x && sh && src_sorted && perm && dzbuf &&
                 dx_edge && dY_edge);
   const Desc d = *reinterpret_cast<const Desc*>(desc_host);
-  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= kMaxCg);
-  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 3);
+  GMP_CHECK_ARG(desc_ok_z(d) && cg_len > 0 && cg_len <= (l_max > 3 ? kMaxCgG : kMaxCg));
+  GMP_CHECK_ARG(e0 >= 0 && e1 >= e0 && l_max >= 0 && l_max <= 5);
   if (e1 == e0) return GMP_OK;
   const unsigned grid = (unsigned)z2_blocks(e1 - e0);
-  if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
+  if (l_max > 3 || d.sh_dim > kMaxSh)
+    tp_edge_z_gen_bwd_kernel<<<grid, 256, 0, as_stream(stream)>>>(
+        d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
+        dx_edge, dY_edge);
+  else if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
     tp_edge_z2_bwd_kernel<2><<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
         dx_edge, dY_edge);

@@ -403,7 +403,7 @@ std::tuple<Tensor, Tensor> edge_featurize(const Tensor& pos, const Tensor& edge_
                                           double r_max, double p, int64_t lmax) {
   OpGuard g(pos, "edge_featurize");
   const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
-  TORCH_CHECK(0 <= lmax && lmax <= 3, "gmp.edge_featurize: lmax in 0..3");
+  TORCH_CHECK(0 <= lmax && lmax <= 5, "gmp.edge_featurize: lmax in 0..5");
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
   Tensor sh = at::empty({E, (lmax + 1) * (lmax + 1)}, pos.options());
   Tensor rad = at::empty({E, nb}, pos.options());
@@ -420,7 +420,7 @@ Tensor edge_featurize_bwd(const Tensor& pos, const Tensor& edge_index,
                           int64_t lmax) {
   OpGuard g(pos, "edge_featurize_bwd");
   const int64_t E = edge_checks(pos, edge_index), nb = (int64_t)bessel_w.size();
-  TORCH_CHECK(0 <= lmax && lmax <= 3, "gmp.edge_featurize_bwd: lmax in 0..3");
+  TORCH_CHECK(0 <= lmax && lmax <= 5, "gmp.edge_featurize_bwd: lmax in 0..5");
   opt_f32(g_sh, {E, (lmax + 1) * (lmax + 1)}, "g_sh");
   opt_f32(g_rad, {E, nb}, "g_radial");
   std::vector<float> w(bessel_w.begin(), bessel_w.end());
@@ -691,7 +691,7 @@ TpDescHost tp_desc(at::IntArrayRef d) {
 // its z rows unwritten
 int tp_lmax(at::IntArrayRef d) {
   const int l = d.size() == 32 ? (int)d[31] : 3;
-  TORCH_CHECK(0 <= l && l <= 3, "gmp.tp: l_max in 0..3");
+  TORCH_CHECK(0 <= l && l <= 5, "gmp.tp: l_max in 0..5");
   const TpDescHost h = tp_desc(d);
   TORCH_CHECK(0 < h.n_blocks && h.n_blocks <= 8, "gmp.tp: 1..8 output blocks");
   for (int k = 0; k < h.n_blocks; ++k)

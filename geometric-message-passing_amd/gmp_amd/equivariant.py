@@ -80,7 +80,7 @@ class RadialEmbeddingBlock(nn.Module):
 
 class EdgeFeaturizeFn(torch.autograd.Function):
     """K1: (pos, edge_index) -> (edge_sh (E, (lmax+1)^2), edge_feats (E,nb)) in one pass over the
-    edges (lmax <= 3: the models' max_ell)."""
+    edges (lmax <= 5: the models' max_ell; l = 4, 5 by e3nn's CG recursion)."""
 
     @staticmethod
     def forward(ctx, pos, edge_index, host_consts, graph, lmax=2):
@@ -377,14 +377,18 @@ class TPPlan:
         key = tuple(ir for _, ir in irreps_out)
         sh_dim = o3.irreps_dim(irreps_sh)
         # (input irreps with a repeated l -- both parities -- take the dz kernel's grouped form)
-        if any(m != 1 for m, _ in irreps_sh) or sh_dim not in (1, 4, 9, 16) or \
-                any(m > 128 for m, _ in irreps_in) or len(irreps_out) > 8 or \
-                any(ir[0] > 3 for _, ir in tuple(irreps_in) + tuple(irreps_out)) or \
-                len(self.instructions) > 48:
+        # (l = 4, 5: the runtime-l z / dz kernels, CG table <= 8192 floats; l <= 3 the fixed-l
+        # ones, <= 4096)
+        lmx = max(ir[0] for _, ir in tuple(irreps_in) + tuple(irreps_out) + tuple(irreps_sh))
+        cg_floats = sum((2 * i["l1"] + 1) * (2 * i["l2"] + 1) * (2 * i["lo"] + 1)
+                        for i in self.instructions)
+        if any(m != 1 for m, _ in irreps_sh) or sh_dim not in (1, 4, 9, 16, 25, 36) or \
+                any(m > 128 for m, _ in irreps_in) or len(irreps_out) > 8 or lmx > 5 or \
+                len(self.instructions) > 48 or cg_floats > (8192 if lmx > 3 else 4096):
             raise NotImplementedError(f"TP {o3.irreps_str(irreps_in)} x {o3.irreps_str(irreps_sh)}"
                                       f" -> {o3.irreps_str(irreps_out)} not supported by K7")
         # the per-edge-weight kernels (GMP_TP_MODE=edge) take the two l <= 2 layouts; the node
-        # form (default) any block structure with l <= 3
+        # form (default) any block structure with l <= 5
         edge_ok = (key in _LAYOUTS and sh_dim == 9 and
                    not any(m > 128 or m % 4 for m, _ in irreps_out))
         self.layout = _LAYOUTS[key] if edge_ok else None
@@ -1040,7 +1044,7 @@ def _edge_features(model, batch):
 
 
 class MACEModel(nn.Module):
-    """models/mace.py:9-190 (same kwargs/defaults; max_ell 1..3: K1 / K7 node form take l <= 3,
+    """models/mace.py:9-190 (same kwargs/defaults; max_ell 1..5: K1 / K7 node form take l <= 5,
     K8 the 0e+1o[+2e[+3o]] hidden irreps, other hidden irreps the per-irrep contraction)."""
 
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
@@ -1048,8 +1052,8 @@ class MACEModel(nn.Module):
                  in_dim=1, out_dim=1, aggr="sum", pool="sum", batch_norm=True, residual=True,
                  equivariant_pred=False):
         super().__init__()
-        if max_ell not in (1, 2, 3):
-            raise NotImplementedError("K1 / K7 take max_ell <= 3")
+        if max_ell not in (1, 2, 3, 4, 5):
+            raise NotImplementedError("K1 / K7 take max_ell <= 5")
         self.r_max, self.max_ell, self.num_layers = r_max, max_ell, num_layers
         self.emb_dim, self.mlp_dim, self.residual = emb_dim, mlp_dim, residual
         self.batch_norm, self.equivariant_pred = batch_norm, equivariant_pred
@@ -1096,15 +1100,16 @@ def first_node_pooling(x, batch, size=None):
 
 
 class TFNModel(nn.Module):
-    """models/tfn.py:42-190 (same kwargs/defaults; max_ell = 2)."""
+    """models/tfn.py:42-190 (same kwargs/defaults; max_ell 1..5, l = 4, 5 on the runtime-l z / dz
+    kernels: experiments/rotsym.ipynb's max_ell = 5 at one layer)."""
 
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
                  num_layers=5, emb_dim=64, hidden_irreps=None, mlp_dim=256, in_dim=1, out_dim=1,
                  aggr="sum", pool="first", gate=True, batch_norm=False, residual=True,
                  equivariant_pred=False):
         super().__init__()
-        if max_ell not in (1, 2, 3):
-            raise NotImplementedError("K1 / K7 take max_ell <= 3")
+        if max_ell not in (1, 2, 3, 4, 5):
+            raise NotImplementedError("K1 / K7 take max_ell <= 5")
         self.max_ell = max_ell
         self.emb_dim, self.residual, self.equivariant_pred = emb_dim, residual, equivariant_pred
         self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)

@@ -48,7 +48,7 @@ def sh_irreps(lmax):
 
 
 def hidden_irreps(emb_dim, lmax):
-    """(sh_irreps * emb_dim).sort().simplify() for lmax <= 3 (models/mace.py:96)."""
+    """(sh_irreps * emb_dim).sort().simplify() for lmax <= 5 (models/mace.py:96)."""
     return tuple((emb_dim, (l, (-1) ** l)) for l in range(lmax + 1))
 
 

@@ -192,7 +192,7 @@ def edge_features(pos, edge_index, radial, max_ell=2):
 
 
 class MACEModel(nn.Module):
-    """models/mace.py:9-190 (max_ell <= 3: the SH restatement is l <= 3; hidden_irreps as
+    """models/mace.py:9-190 (max_ell <= 5: the SH restatement is l <= 5; hidden_irreps as
     mace.py:90-93)."""
 
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
@@ -200,7 +200,7 @@ class MACEModel(nn.Module):
                  aggr="sum", pool="sum", batch_norm=True, residual=True, equivariant_pred=False,
                  hidden_irreps=None):
         super().__init__()
-        assert 1 <= max_ell <= 3
+        assert 1 <= max_ell <= 5
         self.max_ell = max_ell
         self.emb_dim, self.residual, self.equivariant_pred = emb_dim, residual, equivariant_pred
         self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)
@@ -244,14 +244,14 @@ def first_node_pooling(x, batch, size=None):
 
 
 class TFNModel(nn.Module):
-    """models/tfn.py:42-190 (max_ell <= 3)."""
+    """models/tfn.py:42-190 (max_ell <= 5)."""
 
     def __init__(self, r_max=10.0, num_bessel=8, num_polynomial_cutoff=5, max_ell=2,
                  num_layers=5, emb_dim=64, mlp_dim=256, in_dim=1, out_dim=1, aggr="sum",
                  pool="first", gate=True, batch_norm=False, residual=True,
                  equivariant_pred=False, hidden_irreps=None):
         super().__init__()
-        assert 1 <= max_ell <= 3
+        assert 1 <= max_ell <= 5
         self.max_ell = max_ell
         self.emb_dim, self.residual, self.equivariant_pred = emb_dim, residual, equivariant_pred
         self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, num_polynomial_cutoff)

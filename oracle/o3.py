@@ -85,13 +85,33 @@ def spherical_harmonics_l2(vec, normalize=True):
     ], dim=-1)
 
 
+@lru_cache(maxsize=None)
+def _sh_recursion(l):
+    """(C, c_l) of Y_l[k] = c_l sum_ij C[i, j, k] Y_{l-1}[i] u_j with C = wigner_3j(l-1, 1, l)
+    and c_l > 0 such that |Y_l|^2 = 2l + 1 on the unit sphere (the contraction's norm there is
+    a constant: measured on a fixed set of unit vectors)."""
+    C = wigner_3j(l - 1, 1, l)
+    g = torch.Generator().manual_seed(l)
+    u = torch.nn.functional.normalize(torch.randn(64, 3, generator=g, dtype=torch.float64),
+                                      dim=-1)
+    Yp = spherical_harmonics(u, l - 1)[:, (l - 1) ** 2:l * l]
+    n2 = torch.einsum("ijk,ni,nj->nk", C, Yp, u).pow(2).sum(-1)
+    assert float(n2.max() - n2.min()) < 1e-9 * float(n2.max())
+    return C, math.sqrt((2 * l + 1) / float(n2.mean()))
+
+
+def sh_recursion_table(l):
+    return _sh_recursion(l)
+
+
 def spherical_harmonics(vec, lmax, normalize=True):
     """e3nn SphericalHarmonics(range(lmax+1), normalize, 'component') -> (..., (lmax+1)^2),
-    lmax <= 3.  e3nn 0.5.1 o3/_spherical_harmonics.py generates each l from l-1 by the CG
-    recursion and scales l by sqrt(2l+1); the l = 3 block restated here in closed form
-    (checked against that recursion, unit-vector norm 2l+1 and equivariance in
-    tests/test_oracle_o3.py)."""
-    assert 0 <= lmax <= 3
+    lmax <= 5.  e3nn 0.5.1 o3/_spherical_harmonics.py generates each l from l-1 by the CG
+    recursion and scales l by sqrt(2l+1); the l = 3 block restated here in closed form, the
+    l = 4, 5 blocks by that recursion (Y_l = c_l wigner_3j(l-1, 1, l) . (Y_{l-1} (x) u), which
+    reproduces the closed-form l = 2, 3 blocks: tests/test_oracle_o3.py; unit-vector norm 2l+1
+    and equivariance checked there too)."""
+    assert 0 <= lmax <= 5
     Y = spherical_harmonics_l2(vec, normalize)[..., :(lmax + 1) ** 2]
     if lmax < 3:
         return Y
@@ -111,7 +131,12 @@ def spherical_harmonics(vec, lmax, normalize=True):
         math.sqrt(5.0) * s24 * y,
         math.sqrt(5.0 / 6.0) * (s24 * z - s20 * x),
     ], dim=-1) * s7
-    return torch.cat([Y, l3], dim=-1)
+    blocks = [Y, l3]
+    u = torch.stack([x, y, z], dim=-1)
+    for l in range(4, lmax + 1):
+        C, c = _sh_recursion(l)
+        blocks.append(c * torch.einsum("ijk,...i,...j->...k", C.to(u.dtype), blocks[-1], u))
+    return torch.cat(blocks, dim=-1)
 
 
 # ----------------------------------------------------------------------------------- CG

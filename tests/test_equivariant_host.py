@@ -64,9 +64,9 @@ def test_tp_plan_tables():
     assert p3.cg_host.numel() == 1959 and p3.z_size == 6592 and len(p3.desc_list) == 32
     assert p3.l_max == 3 and p3.desc_list[-1] == 3
     with pytest.raises(NotImplementedError):
-        eq.TPPlan(hid, o3.sh_irreps(2), o3.parse_irreps("8x4e"))
+        eq.TPPlan(hid, o3.sh_irreps(2), o3.parse_irreps("8x6e"))  # l <= 5
     with pytest.raises(NotImplementedError):
-        eq.TPPlan(hid, o3.sh_irreps(4), hid)
+        eq.TPPlan(hid, o3.sh_irreps(6), hid)
     with pytest.raises(NotImplementedError):
         eq.TPPlan(hid, o3.sh_irreps(2),
                   o3.parse_irreps("8x0e+8x1o+8x0e+8x1o+8x0e+8x1o+8x0e+8x1o+8x2e"))  # 9 blocks

@@ -41,7 +41,7 @@ def _grads(model, ref, rtol=1e-4):
         _close_scaled(p.grad, q.grad, rtol, name)
 
 
-@pytest.mark.parametrize("lmax", [2, 3, 1])
+@pytest.mark.parametrize("lmax", [2, 3, 1, 4, 5])
 def test_featurize_vs_oracle(lmax):
     from gmp_amd import equivariant as eq
     g = _graph(500, 8000, seed=3)
@@ -236,6 +236,12 @@ def test_tp_conv_chunking_and_determinism(monkeypatch, mode):
                        hidden_irreps="16x0e+16x0o+16x1e+16x1o+16x2e+16x2o")),
     ("TFNModel", dict(num_layers=2, emb_dim=16, r_max=2.0,
                       hidden_irreps="16x0e+16x0o+16x1e+16x1o+16x2e+16x2o")),
+    # max_ell = 5 at one layer with an equivariant head (experiments/rotsym.ipynb): SH l = 4, 5
+    # by e3nn's recursion, the runtime-l z / dz kernels
+    ("TFNModel", dict(num_layers=1, emb_dim=32, max_ell=5, r_max=2.0, equivariant_pred=True,
+                      out_dim=2)),
+    ("MACEModel", dict(num_layers=1, emb_dim=32, max_ell=5, correlation=2, r_max=2.0,
+                       equivariant_pred=True, out_dim=2)),
 ])
 def test_model_vs_oracle(kind, kw):
     from gmp_amd import equivariant as eq

@@ -63,6 +63,37 @@ def test_sh_l3_norm_equivariance_and_recursion():
         assert o3.spherical_harmonics(v, lmax).shape == (200, (lmax + 1) ** 2)
 
 
+@pytest.mark.parametrize("l", [4, 5])
+def test_sh_l45_norm_equivariance_and_recursion(l):
+    """l = 4, 5 (the reference's rotational-symmetry experiment runs TFN / MACE at max_ell = 5,
+    experiments/rotsym.ipynb): the recursion Y_l = c_l C(l-1, 1, l).(Y_{l-1} (x) u) that
+    reproduces the closed-form l = 2, 3 blocks up to the positive normalisation, unit-vector
+    norm 2l+1, equivariance under D^l, the polar-axis value and degree-0 homogeneity."""
+    v = torch.randn(200, 3, dtype=torch.float64)
+    Y = o3.spherical_harmonics(v, l)
+    assert Y.shape == (200, (l + 1) ** 2)
+    torch.testing.assert_close(Y[:, :16], o3.spherical_harmonics(v, 3))
+    blk = Y[:, l * l:]
+    torch.testing.assert_close(blk.pow(2).sum(-1), torch.full((200,), 2.0 * l + 1,
+                                                            dtype=torch.float64))
+    Dl, R = _D(l, *ANG), _D(1, *ANG)
+    torch.testing.assert_close(o3.spherical_harmonics(v @ R.T, l)[:, l * l:], blk @ Dl.T,
+                               atol=1e-10, rtol=0)
+    yhat = o3.spherical_harmonics(torch.tensor([[0.0, 1.0, 0.0]], dtype=torch.float64), l)[0]
+    e = torch.zeros(2 * l + 1, dtype=torch.float64)
+    e[l] = math.sqrt(2 * l + 1)  # e3nn: the m = 0 component along the polar (y) axis
+    torch.testing.assert_close(yhat[l * l:].abs(), e, atol=1e-12, rtol=0)
+    torch.testing.assert_close(o3.spherical_harmonics(2.5 * v, l), Y)
+    # the same recursion at l = 2, 3 gives the closed forms with a positive factor
+    u = torch.nn.functional.normalize(v, dim=-1)
+    for lo in (2, 3):
+        rec = torch.einsum("ijk,ei,ej->ek", o3.wigner_3j(lo - 1, 1, lo),
+                           Y[:, (lo - 1) ** 2:lo * lo], u)
+        ratio = (rec * Y[:, lo * lo:(lo + 1) ** 2]).sum() / rec.pow(2).sum()
+        assert ratio > 0
+        torch.testing.assert_close(ratio * rec, Y[:, lo * lo:(lo + 1) ** 2], atol=1e-12, rtol=0)
+
+
 def test_tfn_max_ell3_invariant():
     """The oracle TFN at max_ell=3 (27-path first-layer-on TP, 1959 CG floats) stays invariant."""
     torch.manual_seed(1)
