@@ -24,7 +24,7 @@ from torch.nn import functional as F
 from . import _lib, ops
 from . import o3
 from .ops import _f32c, _need_cuda, _timed
-from .scatter import global_add_pool, global_mean_pool
+from .scatter import global_add_pool, global_mean_pool, scatter
 
 CHUNK_BYTES = int(os.environ.get("GMP_TP_CHUNK_BYTES", str(6 << 30)))
 
@@ -302,17 +302,19 @@ class Gate(nn.Module):
 class TPGraph:
     """Receiver (edge_index[0])-sorted CSR for the TP convolution (scatter target ei0,
     gather source ei1: tfn_layer.py:83-87), plus the CSR of the gather source over sorted
-    positions for the backward segmented sums."""
+    positions for the backward segmented sums.  num_src: rows of the gathered features when they
+    differ from the receivers' (the per-edge-message graph of aggr max / min)."""
 
-    def __init__(self, edge_index, num_nodes):
+    def __init__(self, edge_index, num_nodes, num_src=None):
         ei = edge_index.contiguous()
         self.num_nodes, self.num_edges = int(num_nodes), ei.shape[1]
+        self.num_src = self.num_nodes if num_src is None else int(num_src)
         self.recv_csr = ops.CSR(ei[0], self.num_nodes, payload=ei[1])
         self.rowptr = self.recv_csr.rowptr
         self.perm = self.recv_csr.perm
         self.src_sorted = self.recv_csr.payload_sorted
         self.recv_sorted = self.recv_csr.sorted
-        self.src_csr = ops.CSR(self.src_sorted, self.num_nodes)
+        self.src_csr = ops.CSR(self.src_sorted, self.num_src)
         self._node_form = None
 
     def node_form(self):
@@ -352,14 +354,15 @@ class TPGraph:
 _TP_GRAPHS = []
 
 
-def tp_graph(edge_index, num_nodes):
+def tp_graph(edge_index, num_nodes, num_src=None):
     if ops.compiling():
-        return TPGraph(edge_index, num_nodes)
+        return TPGraph(edge_index, num_nodes, num_src)
+    key = (num_nodes, num_src)
     for t, ver, n, g in _TP_GRAPHS:
-        if t is edge_index and ver == edge_index._version and n == num_nodes:
+        if t is edge_index and ver == edge_index._version and n == key:
             return g
-    g = TPGraph(edge_index, num_nodes)
-    _TP_GRAPHS.insert(0, (edge_index, edge_index._version, num_nodes, g))
+    g = TPGraph(edge_index, num_nodes, num_src)
+    _TP_GRAPHS.insert(0, (edge_index, edge_index._version, key, g))
     del _TP_GRAPHS[4:]
     return g
 
@@ -824,6 +827,8 @@ class TensorProductConvLayer(nn.Module):
         self.batch_norm = BatchNorm(self.out_irreps) if batch_norm else None
 
     def forward(self, node_attr, edge_index, edge_sh, edge_feat):
+        if self.aggr in ("max", "min"):
+            return self._forward_extremum(node_attr, edge_index, edge_sh, edge_feat)
         graph = tp_graph(edge_index, node_attr.shape[0])
         node = TP_MODE == "node" and node_form_ok(self.fc[0].out_features)
         fn = TPConvNodeFn if node else TPConvFn
@@ -840,11 +845,37 @@ class TensorProductConvLayer(nn.Module):
             out = out / graph.recv_csr.counts().clamp(min=1).unsqueeze(1).to(out.dtype)
         elif self.aggr not in ("add", "sum"):
             raise NotImplementedError(f"aggr={self.aggr}")
+        return self._epilogue(out)
+
+    def _epilogue(self, out):
         if self.gate is not None:
             out = self.gate(out)
         if self.batch_norm is not None:
             out = self.batch_norm(out)
         return out
+
+    def _forward_extremum(self, node_attr, edge_index, edge_sh, edge_feat):
+        """aggr = max / min (tfn_layer.py:87 passes aggr to torch_scatter's scatter): the per-edge
+        messages through the node-form kernels on a graph where every edge is its own receiver
+        (edge e -> receiver e, sender edge_index[1][e]), then the deterministic segmented max /
+        min (K3) over edge_index[0] with torch_scatter's arg routing of the gradient.  The
+        receiver sum of the node form is what makes it cheap; per-edge messages cost ~ the
+        in-degree times more (not a benchmark path)."""
+        if not node_form_ok(self.fc[0].out_features):
+            raise NotImplementedError(f"aggr={self.aggr}: the node-form kernels need "
+                                      "mlp_dim % 16 == 0 and <= 256")
+        E = edge_index.shape[1]
+        ar = torch.arange(E, device=edge_index.device, dtype=edge_index.dtype)
+        ei_e = torch.stack([ar, edge_index[1]])
+        graph = tp_graph(ei_e, E, num_src=node_attr.shape[0])
+        paths, cg = self._tp_paths, self._tp_cg
+        if paths.device != node_attr.device or cg.dtype != torch.float32:
+            paths, cg = self.plan.device_tables(node_attr.device)
+        msg = TPConvNodeFn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight,
+                                 self.fc[0].bias, self.fc[2].weight, self.fc[2].bias, self.plan,
+                                 graph, paths, cg)
+        out = scatter(msg, edge_index[0], dim=0, dim_size=node_attr.shape[0], reduce=self.aggr)
+        return self._epilogue(out)
 
 
 # ===================================================================================== MACE node

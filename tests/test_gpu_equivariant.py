@@ -71,6 +71,9 @@ def test_featurize_vs_oracle(lmax):
     ("8x0e", "8x0e+8x1o+8x2e", True, False, "add", 16),
     ("128x0e+128x1o+128x2e", "128x0e+128x1o+128x2e", False, True, "add", 64),
     ("64x0e+64x1o+64x2e", "64x0e+64x1o+64x2e", True, False, "add", 64),
+    # aggr max / min (tfn_layer.py:87 passes aggr to scatter): per-edge messages + K3 max / min
+    ("16x0e+16x1o+16x2e", "16x0e+16x1o+16x2e", False, True, "max", 32),
+    ("16x0e", "16x0e+16x1o+16x2e", True, False, "min", 32),
 ])
 @pytest.mark.parametrize("mode", ["node", "edge"])
 def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp, mode, monkeypatch):
