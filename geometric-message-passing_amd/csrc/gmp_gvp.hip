@@ -555,6 +555,305 @@ __global__ __launch_bounds__(kGT) void gvp_msg0_bwd_kernel(int64_t E, const int6
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// r04: the GVP layer's 128 x 128 products (W_s's scalar block: Ws[:, :128] s in the forward and
+// its recompute, Ws[:, :128]^T dspre in the backward) on the bf16 MFMA over exact three-plane
+// splits (x = hi + mid + lo, six products hi.hi + hi.mid + mid.hi + hi.lo + lo.hi + mid.mid in
+// f32 accumulation: f32-class, no scaling -- bf16 keeps f32's exponent range).  16x16x32 bf16
+// = 16 cycles for 6 x 16 x 16 x 32 products against 8 x 32 cycles of 16x16x4 f32 for the same
+// 16 x 16 x 32 f32 product: 2.7x fewer MFMA cycles on the kernel's dominant products.  The small
+// products (vn block of Ws, Wsv, Wh, Wv: K = 16 or 16 outputs) stay on the exact f32 MFMA.
+// Image: 3 planes x 128 rows x LDH bf16 (272-byte rows: the 16 rows of a 16-byte A read fall on
+// distinct banks); columns in the hf_pos order (the 8 halfs a lane feeds one 16x16x32 MFMA,
+// k = 8 g + j of block p, are its slots x[2p][0..3], x[2p + 1][0..3]).  The forward kernel
+// stores W (rows o); the backward stores W^T (rows k) and reads W for the recompute with
+// ds_read_b64_tr_b16 (same address pattern as the EGNN backward's x_hat3 recompute).
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int XLDH = S + 8;              // bf16 per image row
+constexpr int XPLANE = S * XLDH;         // bf16 per plane
+constexpr int kXImgFloats = 3 * XPLANE / 2;
+// LDS (floats): image | Ws vn block (128 x LD16) | Wsv (16 x LD128) | Wh | Wv | bs | bsv
+constexpr int kLayerSmemX3 = kXImgFloats + S * LD16 + V * LD128 + 2 * V * LD16 + S + V;
+
+__device__ __forceinline__ int x3_pos(int k) {
+  const int tt = k >> 4, gg = (k >> 2) & 3, q = k & 3;
+  return 32 * (tt >> 1) + 8 * gg + 4 * (tt & 1) + q;
+}
+
+__device__ __forceinline__ void split3(f32x2_t x, unsigned& h, unsigned& m, unsigned& l) {
+  const bf16x2_t bh = __builtin_convertvector(x, bf16x2_t);
+  const f32x2_t r1 = x - __builtin_convertvector(bh, f32x2_t);
+  const bf16x2_t bm = __builtin_convertvector(r1, bf16x2_t);
+  const f32x2_t r2 = r1 - __builtin_convertvector(bm, f32x2_t);
+  const bf16x2_t bl = __builtin_convertvector(r2, bf16x2_t);
+  h = __builtin_bit_cast(unsigned, bh);
+  m = __builtin_bit_cast(unsigned, bm);
+  l = __builtin_bit_cast(unsigned, bl);
+}
+// slots x[2p], x[2p + 1] of this lane -> the three bf16x8 planes of one B fragment
+__device__ __forceinline__ void split_slots(const f32x4& x0, const f32x4& x1, bf16x8_t (&b)[3]) {
+  unsigned h[4], m[4], l[4];
+  split3(f32x2_t{x0[0], x0[1]}, h[0], m[0], l[0]);
+  split3(f32x2_t{x0[2], x0[3]}, h[1], m[1], l[1]);
+  split3(f32x2_t{x1[0], x1[1]}, h[2], m[2], l[2]);
+  split3(f32x2_t{x1[2], x1[3]}, h[3], m[3], l[3]);
+  b[0] = __builtin_bit_cast(bf16x8_t, u32x4_t{h[0], h[1], h[2], h[3]});
+  b[1] = __builtin_bit_cast(bf16x8_t, u32x4_t{m[0], m[1], m[2], m[3]});
+  b[2] = __builtin_bit_cast(bf16x8_t, u32x4_t{l[0], l[1], l[2], l[3]});
+}
+__device__ __forceinline__ f32x4 mma6(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4 t) {
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], t, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], t, 0, 0, 0);
+}
+
+// image of Ws[:, :128] (TRANSPOSE: of its transpose), plus the f32 remainder
+template <bool TRANSPOSE>
+__device__ void layer_to_lds_x3(float* sm, const LayerW& P) {
+  __bf16* img = reinterpret_cast<__bf16*>(sm);
+  float* sWsV = sm + kXImgFloats;
+  float* sWsv = sWsV + S * LD16;
+  float* sWh = sWsv + V * LD128;
+  float* sWv = sWh + V * LD16;
+  float* sbs = sWv + V * LD16;
+  float* sbsv = sbs + S;
+  for (int x = threadIdx.x; x < S * S / 2; x += blockDim.x) {
+    const int o = (2 * x) / S, k = (2 * x) % S;  // W[o][k], W[o][k + 1]
+    const f32x2_t w = *reinterpret_cast<const f32x2_t*>(P.Ws + o * (S + V) + k);
+    unsigned h, m, l;
+    split3(w, h, m, l);
+    const unsigned pl[3] = {h, m, l};
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = TRANSPOSE ? k + u : o, c = TRANSPOSE ? o : k + u;
+        reinterpret_cast<unsigned short*>(img)[p * XPLANE + r * XLDH + x3_pos(c)] =
+            (unsigned short)(pl[p] >> (16 * u));
+      }
+  }
+  for (int x = threadIdx.x; x < S * V; x += blockDim.x)
+    sWsV[(x / V) * LD16 + x % V] = P.Ws[(x / V) * (S + V) + S + x % V];
+  for (int x = threadIdx.x; x < V * S; x += blockDim.x) sWsv[(x / S) * LD128 + x % S] = P.Wsv[x];
+  for (int x = threadIdx.x; x < V * V; x += blockDim.x) {
+    sWh[(x / V) * LD16 + x % V] = P.Wh[x];
+    sWv[(x / V) * LD16 + x % V] = P.Wv[x];
+  }
+  for (int x = threadIdx.x; x < S; x += blockDim.x) sbs[x] = P.bs[x];
+  for (int x = threadIdx.x; x < V; x += blockDim.x) sbsv[x] = P.bsv[x];
+}
+
+// y[slot(r)] += sum_c IMG[r][c] x[slot(c)]  (A rows read directly)
+__device__ __forceinline__ void gemm_x3(const __bf16* __restrict__ img, const f32x4 (&x)[S / 16],
+                                        f32x4 (&y)[S / 16], int i, int g) {
+#pragma unroll
+  for (int p = 0; p < S / 32; ++p) {
+    bf16x8_t b[3];
+    split_slots(x[2 * p], x[2 * p + 1], b);
+#pragma unroll
+    for (int t = 0; t < S / 16; ++t) {
+      const __bf16* row = img + (16 * t + i) * XLDH + 32 * p + 8 * g;
+      bf16x8_t a[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const bf16x8_t*>(row + pl * XPLANE);
+      y[t] = mma6(a, b, y[t]);
+      if (t % 2 == 1) asm volatile("" ::: "memory");  // bounds hoisted A reads (registers)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ s16x4_t lds_tr16(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
+}
+// y[slot(c)] += sum_r IMG[r][c] x[slot(r)]: the product with the image's transpose, A fragments
+// by transposed 8-byte reads (lane 4q + c of group g supplies row 32p + 4g + q (+ 16))
+__device__ __forceinline__ void gemm_x3_tr(const __bf16* __restrict__ img, const f32x4 (&x)[S / 16],
+                                           f32x4 (&y)[S / 16], int lane, int g) {
+  const int q = (lane & 15) >> 2, c = lane & 3;
+#pragma unroll
+  for (int p = 0; p < S / 32; ++p) {
+    bf16x8_t b[3];
+    split_slots(x[2 * p], x[2 * p + 1], b);
+    const __bf16* rowk = img + (32 * p + 4 * g + q) * XLDH + 8 * c;
+#pragma unroll
+    for (int t = 0; t < S / 16; ++t) {
+      const __bf16* a0 = rowk + 32 * (t >> 1) + 4 * (t & 1);
+      bf16x8_t a[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const s16x4_t h0 = lds_tr16(a0 + pl * XPLANE), h1 = lds_tr16(a0 + pl * XPLANE + 16 * XLDH);
+        a[pl] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      y[t] = mma6(a, b, y[t]);
+      if (t % 2 == 1) asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// forward of one GVP layer for this lane's edge on the image (TR: the image holds W^T)
+template <bool TR>
+__device__ __forceinline__ void layer_forward_x3(const float* sm, const f32x4 (&s)[S / 16],
+                                                 const f32x4 (&v)[3][1], LayerFwd& F, int lane,
+                                                 int i, int g) {
+  const __bf16* img = reinterpret_cast<const __bf16*>(sm);
+  const float* sWsV = sm + kXImgFloats;
+  const float* sWsv = sWsV + S * LD16;
+  const float* sWh = sWsv + V * LD128;
+  const float* sWv = sWh + V * LD16;
+  const float* sbs = sWv + V * LD16;
+  const float* sbsv = sbs + S;
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    zero(F.vh[x]);
+    gemm_wx<1, 1>(sWh, LD16, v[x], F.vh[x], i, g);
+  }
+  vnorm<1>(F.vh, F.vn, F.sq);
+  ld_vec<S / 16>(F.spre, sbs, g);
+  if constexpr (TR) gemm_x3_tr(img, s, F.spre, lane, g);
+  else gemm_x3(img, s, F.spre, i, g);
+  gemm_wx<S / 16, 1>(sWsV, LD16, F.vn, F.spre, i, g);
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    zero(F.vpre[x]);
+    gemm_wx<1, 1>(sWv, LD16, F.vh[x], F.vpre[x], i, g);
+  }
+  f32x4 gate[1];
+  ld_vec<1>(gate, sbsv, g);
+  gemm_wx<1, S / 16>(sWsv, LD128, F.spre, gate, i, g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) F.sg[0][q] = sigm(gate[0][q]);
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kGT) void gvp_layer_fwd_x3_kernel(int64_t E, const float* __restrict__ s_in,
+                                                               const float* __restrict__ v_in, LayerW P,
+                                                               float* __restrict__ s_out,
+                                                               float* __restrict__ v_out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  layer_to_lds_x3<false>(sm, P);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nchunks = (E + 15) / 16;
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const Chunk k = chunk_edge(c, i, E);
+    f32x4 s[S / 16], v[3][1];
+    ld_row<S / 16>(s, s_in + k.e * S, g);
+    ld_vrow<1>(v, v_in + k.e * (3 * V), g);
+    LayerFwd F;
+    layer_forward_x3<false>(sm, s, v, F, lane, i, g);
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F.vpre[x][0][q] *= F.sg[0][q];
+    if (ACT) {
+#pragma unroll
+      for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F.spre[p][q] = fmaxf(F.spre[p][q], 0.f);
+    }
+    if (k.valid) {
+      st_row<S / 16>(s_out + k.e * S, F.spre, g);
+      st_vrow<1>(v_out + k.e * (3 * V), F.vpre, g);
+    }
+  }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kGT) void gvp_layer_bwd_x3_kernel(int64_t E, const float* __restrict__ s_in,
+                                                               const float* __restrict__ v_in, LayerW P,
+                                                               const float* __restrict__ ds_out,
+                                                               const float* __restrict__ dv_out,
+                                                               LayerGrads O) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  layer_to_lds_x3<true>(sm, P);
+  __syncthreads();
+  const __bf16* img = reinterpret_cast<const __bf16*>(sm);  // W^T
+  const float* sWsV = sm + kXImgFloats;
+  const float* sWsv = sWsV + S * LD16;
+  const float* sWh = sWsv + V * LD128;
+  const float* sWv = sWh + V * LD16;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nchunks = (E + 15) / 16;
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const Chunk k = chunk_edge(c, i, E);
+    f32x4 s[S / 16], v[3][1];
+    ld_row<S / 16>(s, s_in + k.e * S, g);
+    ld_vrow<1>(v, v_in + k.e * (3 * V), g);
+    LayerFwd F;
+    layer_forward_x3<true>(sm, s, v, F, lane, i, g);
+    ld_row<S / 16>(s, ds_out + k.e * S, g);
+    if (ACT) {
+#pragma unroll
+      for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[p][q] = F.spre[p][q] > 0.f ? s[p][q] : 0.f;
+    }
+    f32x4 dv[3][1];
+    ld_vrow<1>(dv, dv_out + k.e * (3 * V), g);
+    f32x4 dgate[1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float dsg = dv[0][0][q] * F.vpre[0][0][q] + dv[1][0][q] * F.vpre[1][0][q] + dv[2][0][q] * F.vpre[2][0][q];
+      dgate[0][q] = dsg * F.sg[0][q] * (1.f - F.sg[0][q]);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) dv[x][0][q] *= F.sg[0][q];  // dvpre
+    }
+    gemm_wtx<S / 16, 1>(sWsv, LD128, dgate, s, i, g);  // dspre += Wsv^T dgate
+    if (k.valid) {
+      st_row<S / 16>(O.dspre + k.e * S, s, g);
+      if (O.spre) st_row<S / 16>(O.spre + k.e * S, F.spre, g);
+      st_row<1>(O.dgate + k.e * V, dgate, g);
+      st_row<1>(O.vn + k.e * V, F.vn, g);
+      st_vrow<1>(O.vh + k.e * (3 * V), F.vh, g);
+      st_vrow<1>(O.dvpre + k.e * (3 * V), dv, g);
+    }
+    // ds_in = Ws_s^T dspre (image rows k) ; dvn = Ws_v^T dspre (f32)
+    f32x4 dsin[S / 16], dvn[1];
+    zero(dsin);
+    zero(dvn);
+    gemm_x3(img, s, dsin, i, g);
+    gemm_wtx<1, S / 16>(sWsV, LD16, s, dvn, i, g);
+    if (k.valid) st_row<S / 16>(O.ds_in + k.e * S, dsin, g);
+    f32x4 dvh[3][1];
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      zero(dvh[x]);
+      gemm_wtx<1, 1>(sWv, LD16, dv[x], dvh[x], i, g);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float f = F.sq[0][q] > 1e-8f ? dvn[0][q] / F.vn[0][q] : 0.f;
+#pragma unroll
+      for (int x = 0; x < 3; ++x) dvh[x][0][q] += f * F.vh[x][0][q];
+    }
+    if (k.valid) st_vrow<1>(O.dvh + k.e * (3 * V), dvh, g);
+    f32x4 dvin[3][1];
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      zero(dvin[x]);
+      gemm_wtx<1, 1>(sWh, LD16, dvh[x], dvin[x], i, g);
+    }
+    if (k.valid) st_vrow<1>(O.dv_in + k.e * (3 * V), dvin, g);
+  }
+}
+
+// GMP_GVP_X3=0: the layer kernels on the f32 MFMA only (A/B; exact fmaf chains)
+int g_gvp_x3 = getenv("GMP_GVP_X3") ? atoi(getenv("GMP_GVP_X3")) : 1;
+
 int64_t grid_for(int64_t E) {
   const int64_t chunks = ceil_div(E, (int64_t)16);
   int64_t b = ceil_div(chunks, (int64_t)(kGT / 64));
@@ -587,10 +886,17 @@ int gmp_gvp_layer_fwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   GMP_CHECK_ARG(s_in && v_in && Ws && bs && Wsv && bsv && Wh && Wv && s_out && v_out);
   GMP_CHECK_ARG(al16(s_in) && al16(v_in) && al16(s_out) && al16(v_out));
   const LayerW P{Ws, bs, Wsv, bsv, Wh, Wv};
-  const size_t smem = kLayerSmem * sizeof(float);
   const unsigned G = (unsigned)grid_for(n_edges);
   hipStream_t s = as_stream(stream);
   int rc;
+  if (g_gvp_x3) {
+    const size_t smx = kLayerSmemX3 * sizeof(float);
+    auto k = relu ? gvp_layer_fwd_x3_kernel<1> : gvp_layer_fwd_x3_kernel<0>;
+    if ((rc = set_smem(k, smx))) return rc;
+    k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
+    return launch_status();
+  }
+  const size_t smem = kLayerSmem * sizeof(float);
   if (relu) {
     if ((rc = set_smem(gvp_layer_fwd_kernel<1>, smem))) return rc;
     gvp_layer_fwd_kernel<1><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
@@ -616,10 +922,17 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
                 al16(vh) && al16(dvpre) && al16(dvh));
   const LayerW P{Ws, bs, Wsv, bsv, Wh, Wv};
   const LayerGrads O{ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
-  const size_t smem = kLayerSmem * sizeof(float);
   const unsigned G = (unsigned)grid_for(n_edges);
   hipStream_t s = as_stream(stream);
   int rc;
+  if (g_gvp_x3) {
+    const size_t smx = kLayerSmemX3 * sizeof(float);
+    auto k = relu ? gvp_layer_bwd_x3_kernel<1> : gvp_layer_bwd_x3_kernel<0>;
+    if ((rc = set_smem(k, smx))) return rc;
+    k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
+    return launch_status();
+  }
+  const size_t smem = kLayerSmem * sizeof(float);
   if (relu) {
     if ((rc = set_smem(gvp_layer_bwd_kernel<1>, smem))) return rc;
     gvp_layer_bwd_kernel<1><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);

@@ -92,6 +92,34 @@ __global__ __launch_bounds__(kRowT) void ln_act_fwd_kernel(
   if (lane == 0) rstd_out[r] = rstd;
 }
 
+// narrow rows (D = 8, 16, 32): 64 / D rows per wave instruction, row sums by xor butterflies
+// inside the D-lane group (same two-pass statistics as above)
+template <int D>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int m = D / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+template <int ACT, int D>
+__global__ __launch_bounds__(kRowT) void ln_act_fwd_small_kernel(
+    int64_t rows, const float* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ y, float* __restrict__ xhat,
+    float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63, f = lane % D;
+  const int64_t r = ((int64_t)blockIdx.x * (kRowT / 64) + (threadIdx.x >> 6)) * (64 / D) + lane / D;
+  const int64_t rc = r < rows ? r : rows - 1;
+  const float v0 = x[rc * D + f];
+  const float mean = group_sum<D>(v0) * (1.f / D);
+  const float v = v0 - mean;
+  const float rstd = 1.f / sqrtf(group_sum<D>(v * v) / (float)D + eps);
+  if (r >= rows) return;
+  const float xh = v * rstd;
+  xhat[r * D + f] = xh;
+  y[r * D + f] = act_fwd<ACT>(xh * gamma[f] + beta[f]);
+  if (f == 0) rstd_out[r] = rstd;
+}
+
 template <int ACT>
 __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
     int64_t rows, int d, const float* __restrict__ gy, const float* __restrict__ xhat,
@@ -262,6 +290,61 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_vec_kernel(
   if (out_gb) tree_finish(partials, grows, (int)gridDim.x, 2 * D, out_gb, tickets);
 }
 
+// r04 form for narrow rows, D = 8, 16, 32 (GVP's edge-scalar LayerNorm: 1M rows of 32): a wave
+// instruction covers R = 64 / D rows (lane l: row l / D, feature l % D), kRB4 such row groups per
+// iteration with their loads issued together; row sums by xor butterflies inside the D-lane
+// group (every lane of a group gets the same sum).  The generic kernel ran one row per wave
+// instruction with 64 - D idle lanes and ~500 dependent iterations per wave (0.65 ms for 1M x 32).
+// [dgamma | dbeta]: per-lane sums over the lane's rows, then the (wave, row slot) partials of
+// each feature added in fixed order -> one partial row per workgroup (sum_rows_kernel).
+template <int ACT, int D>
+__global__ __launch_bounds__(kRowT) void ln_act_bwd_small_kernel(
+    int64_t rows, const float* __restrict__ gy, const float* __restrict__ xhat,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials) {
+  constexpr int R = 64 / D;
+  __shared__ float red[kRowT / 64 * R][2 * D];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int f = lane % D, rsub = lane / D;
+  const float gm = gamma[f], bt = beta[f];
+  float dg = 0.f, db = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * (kRowT / 64) * R * kRB4;
+  for (int64_t r0 = ((int64_t)blockIdx.x * (kRowT / 64) + wv) * R * kRB4; r0 < rows;
+       r0 += stride) {
+    float rs[kRB4], xh[kRB4], gv[kRB4];
+#pragma unroll
+    for (int j = 0; j < kRB4; ++j) {
+      int64_t r = r0 + j * R + rsub;
+      r = r < rows ? r : rows - 1;  // clamped: loads stay in bounds
+      rs[j] = rstd_in[r];
+      xh[j] = xhat[r * D + f];
+      gv[j] = gy[r * D + f];
+    }
+#pragma unroll
+    for (int j = 0; j < kRB4; ++j) {
+      const int64_t r = r0 + j * R + rsub;
+      const float dz = gv[j] * act_grad<ACT>(xh[j] * gm + bt);
+      const float g = dz * gm;
+      const float a = group_sum<D>(g) * (1.f / D);
+      const float b = group_sum<D>(g * xh[j]) * (1.f / D);
+      if (r < rows) {
+        dg += dz * xh[j];
+        db += dz;
+        gx[r * D + f] = rs[j] * (g - a - xh[j] * b);
+      }
+    }
+  }
+  red[wv * R + rsub][f] = dg;
+  red[wv * R + rsub][D + f] = db;
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += kRowT) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int w = 0; w < kRowT / 64 * R; ++w) sacc += red[w][c];
+    partials[(int64_t)blockIdx.x * 2 * D + c] = sacc;
+  }
+}
+
 // vec-kernel grid: ~16 rows per wave (four iterations of kRB4), at most 1024 workgroups
 int vec_blocks(int64_t rows) {
   const int64_t b = ceil_div(rows, (kRowT / 64) * kRB4 * 4);
@@ -321,6 +404,10 @@ int bwd_blocks(int64_t rows) {
   return (int)(b < g_ln_blocks ? (b < 1 ? 1 : b) : g_ln_blocks);
 }
 
+// GMP_LN_SMALL=0: narrow rows on the generic kernels (A/B)
+int g_ln_small = getenv("GMP_LN_SMALL") ? atoi(getenv("GMP_LN_SMALL")) : 1;
+bool small_form(int64_t d) { return g_ln_small && (d == 8 || d == 16 || d == 32); }
+
 }  // namespace
 }  // namespace gmp
 
@@ -334,8 +421,19 @@ int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gam
   GMP_CHECK_ARG(rows >= 0 && d > 0 && d <= 64 * kMaxF && act >= 0 && act <= 2);
   if (rows == 0) return GMP_OK;
   GMP_CHECK_ARG(x && gamma && beta && y && xhat_save && rstd_save);
-  const unsigned grid = (unsigned)ceil_div(rows, kRowT / 64);
   hipStream_t s = as_stream(stream);
+  if (small_form(d)) {
+    const unsigned gs = (unsigned)ceil_div(rows, (kRowT / 64) * (64 / d));
+#define GMP_LNF(A, D) \
+  ln_act_fwd_small_kernel<A, D><<<gs, kRowT, 0, s>>>(rows, x, gamma, beta, eps, y, xhat_save, rstd_save)
+#define GMP_LNF_D(A) \
+  if (d == 8) GMP_LNF(A, 8); else if (d == 16) GMP_LNF(A, 16); else GMP_LNF(A, 32)
+    if (act == 0) { GMP_LNF_D(0); } else if (act == 1) { GMP_LNF_D(1); } else { GMP_LNF_D(2); }
+#undef GMP_LNF_D
+#undef GMP_LNF
+    return launch_status();
+  }
+  const unsigned grid = (unsigned)ceil_div(rows, kRowT / 64);
   if (act == 0)
     ln_act_fwd_kernel<0><<<grid, kRowT, 0, s>>>(rows, (int)d, x, gamma, beta, eps, y, xhat_save,
                                                 rstd_save);
@@ -351,6 +449,7 @@ int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gam
 bool vec_form(int64_t d) { return d == 64 || d == 128 || d == 256; }
 
 size_t gmp_ln_act_bwd_workspace_size(int64_t rows, int64_t d) {
+  if (small_form(d)) return (size_t)vec_blocks(rows) * 2 * (size_t)d * sizeof(float);
   if (vec_form(d))  // partial rows + the tree_finish group rows
     return (size_t)(vec_blocks(rows) + kTicketWords) * 2 * (size_t)d * sizeof(float);
   return (size_t)bwd_blocks(rows) * 2 * (size_t)d * sizeof(float);
@@ -375,6 +474,21 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
   const uintptr_t al = reinterpret_cast<uintptr_t>(grad_y) | reinterpret_cast<uintptr_t>(xhat) |
                        reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
                        reinterpret_cast<uintptr_t>(grad_x);
+  if (small_form(d) && grad_gamma_beta && !g_ln_r03) {
+    const int GV = vec_blocks(rows);
+#define GMP_LNS(A, D) \
+  ln_act_bwd_small_kernel<A, D><<<GV, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, beta, grad_x, part)
+#define GMP_LNS_D(A) \
+  if (d == 8) GMP_LNS(A, 8); else if (d == 16) GMP_LNS(A, 16); else GMP_LNS(A, 32)
+    if (act == 0) { GMP_LNS_D(0); } else if (act == 1) { GMP_LNS_D(1); } else { GMP_LNS_D(2); }
+#undef GMP_LNS_D
+#undef GMP_LNS
+    int rc = launch_status();
+    if (rc) return rc;
+    sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, GV, (int)(2 * d),
+                                                                         grad_gamma_beta);
+    return launch_status();
+  }
   if (vec_form(d) && grad_gamma_beta && !g_ln_r03 && al % (d / 16) == 0) {
     // [dgamma | dbeta]: the two-level in-kernel finish (GMP_LN_TREE=1) or the column-sum kernel
     unsigned* tk = g_ln_tree ? stream_ticket_block(s) : nullptr;

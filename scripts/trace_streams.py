@@ -29,7 +29,7 @@ for sid in streams:
     for r in ks:
         c[r["k"][:56]] += (r["e"] - r["s"]) / 1e6
     print(f"== stream {sid}: {len(ks)} kernels, busy {sum(c.values()):.2f} ms")
-    for k, v in sorted(c.items(), key=lambda x: -x[1])[:16]:
+    for k, v in sorted(c.items(), key=lambda x: -x[1])[:int(__import__("os").environ.get("TOPN","16"))]:
         print(f"   {v:7.2f} {k}")
 iv = sorted((r["s"], r["e"]) for r in step)
 u, (cs, ce) = 0, iv[0]
