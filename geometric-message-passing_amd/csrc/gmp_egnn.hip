@@ -56,10 +56,15 @@ template <int D>
 constexpr int carry_stride() { return D / 4 + 4; }
 
 // HF path: W as hi / lo fp16 planes of W 2^sw, columns in the MFMA k order (see gemm_h2), row
-// stride d + 8 halfs (272 B at d = 128: the 16 rows of a ds_read_b128 fall on distinct banks)
+// stride d + 16 halfs (below)
 template <int D>
 struct HCfg {
-  static constexpr int LDH = D + 8;
+  // row stride d + 16 halfs (288 B at d = 128; 16-byte units = 2 mod 16): the four 16-lane
+  // groups of a ds_read_b128 A read hit 64 distinct banks and the transposed 8-byte reads of the
+  // x_hat3 recompute are 2-way (the floor for 8-byte pieces of 16-byte-aligned rows).  r03 / r04
+  // used d + 8 (272 B): 2-way / 4-way, 0.34 / 0.51 of the forward / backward LDS cycles in bank
+  // conflicts (SQ counters, r04).
+  static constexpr int LDH = D + 16;
   static constexpr int PLANE = D * LDH;  // halfs
   static constexpr int MAT = 2 * PLANE;  // halfs per matrix (= floats for two matrices)
 };

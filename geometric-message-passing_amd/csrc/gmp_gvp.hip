@@ -574,7 +574,12 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int XLDH = S + 8;              // bf16 per image row
+// 320-byte rows (80 dwords = 16 mod 64) with the 16-byte chunks of row r XOR-swizzled by
+// x3_swz(r): the 16-lane groups of a 16-byte A read (lanes {0-3,12-15,20-27}, ...) hit 64
+// distinct banks, and the transposed 8-byte reads are 2-way (the floor for 8-byte pieces of
+// 16-byte-aligned rows).  The r04 first form (272-byte rows) measured 0.48 / 0.62 of its LDS
+// cycles in bank conflicts (2-way / 4-way).
+constexpr int XLDH = S + 32;             // bf16 per image row
 constexpr int XPLANE = S * XLDH;         // bf16 per plane
 constexpr int kXImgFloats = 3 * XPLANE / 2;
 // LDS (floats): image | Ws vn block (128 x LD16) | Wsv (16 x LD128) | Wh | Wv | bs | bsv
@@ -584,6 +589,8 @@ __device__ __forceinline__ int x3_pos(int k) {
   const int tt = k >> 4, gg = (k >> 2) & 3, q = k & 3;
   return 32 * (tt >> 1) + 8 * gg + 4 * (tt & 1) + q;
 }
+
+__device__ __forceinline__ int x3_swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // {0,2,3,1}
 
 __device__ __forceinline__ void split3(f32x2_t x, unsigned& h, unsigned& m, unsigned& l) {
   const bf16x2_t bh = __builtin_convertvector(x, bf16x2_t);
@@ -636,7 +643,8 @@ __device__ void layer_to_lds_x3(float* sm, const LayerW& P) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = TRANSPOSE ? k + u : o, c = TRANSPOSE ? o : k + u;
-        reinterpret_cast<unsigned short*>(img)[p * XPLANE + r * XLDH + x3_pos(c)] =
+        const int pos = x3_pos(c);
+        reinterpret_cast<unsigned short*>(img)[p * XPLANE + r * XLDH + (pos ^ (x3_swz(r) << 3))] =
             (unsigned short)(pl[p] >> (16 * u));
       }
   }
@@ -660,7 +668,7 @@ __device__ __forceinline__ void gemm_x3(const __bf16* __restrict__ img, const f3
     split_slots(x[2 * p], x[2 * p + 1], b);
 #pragma unroll
     for (int t = 0; t < S / 16; ++t) {
-      const __bf16* row = img + (16 * t + i) * XLDH + 32 * p + 8 * g;
+      const __bf16* row = img + (16 * t + i) * XLDH + 32 * p + 8 * (g ^ x3_swz(i));
       bf16x8_t a[3];
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const bf16x8_t*>(row + pl * XPLANE);
@@ -683,7 +691,7 @@ __device__ __forceinline__ void gemm_x3_tr(const __bf16* __restrict__ img, const
   for (int p = 0; p < S / 32; ++p) {
     bf16x8_t b[3];
     split_slots(x[2 * p], x[2 * p + 1], b);
-    const __bf16* rowk = img + (32 * p + 4 * g + q) * XLDH + 8 * c;
+    const __bf16* rowk = img + (32 * p + 4 * g + q) * XLDH + 8 * (c ^ x3_swz(4 * g));
 #pragma unroll
     for (int t = 0; t < S / 16; ++t) {
       const __bf16* a0 = rowk + 32 * (t >> 1) + 4 * (t & 1);
