@@ -64,7 +64,10 @@ struct HCfg {
   // x_hat3 recompute are 2-way (the floor for 8-byte pieces of 16-byte-aligned rows).  r03 / r04
   // used d + 8 (272 B): 2-way / 4-way, 0.34 / 0.51 of the forward / backward LDS cycles in bank
   // conflicts (SQ counters, r04).
-  static constexpr int LDH = D + 16;
+#ifndef GMP_K4_LDH_PAD
+#define GMP_K4_LDH_PAD 16  // (8 = the r03 layout, for A/B builds)
+#endif
+  static constexpr int LDH = D + GMP_K4_LDH_PAD;
   static constexpr int PLANE = D * LDH;  // halfs
   static constexpr int MAT = 2 * PLANE;  // halfs per matrix (= floats for two matrices)
 };
