@@ -777,7 +777,8 @@ def main():
             "dtype": "f32",
             "precision": "f32 storage and f32 accumulation throughout; products on split-operand "
                          "MFMA: EGNN K4 and its dW2/dW3 sums 2-plane f16 (22-bit operands), "
-                         "the TP GEMMs and other weight sums 3-plane bf16 (24-bit); "
+                         "the TP GEMMs, the GVP layer GVPs' 128 x 128 products and other "
+                         "weight sums 3-plane bf16 (24-bit); "
                          "egnn_f32_exact is the EGNN rate with every product on the exact f32 "
                          "MFMA",
             "data": "synthetic (seeded random radius graph per rank, random-init weights)",
