@@ -404,6 +404,82 @@ int bwd_blocks(int64_t rows) {
   return (int)(b < g_ln_blocks ? (b < 1 ? 1 : b) : g_ln_blocks);
 }
 
+// GVP vector LayerNorm (gvp_layer.py:232-243 with the clamp of _norm_no_nan, :66-73): rows of C
+// channels x 3 (xyz), out = v / sqrt(mean_c max(|v_c|^2, 1e-8)).  A G-lane group per row (G =
+// the power of two >= C, lane = channel, its 3 floats contiguous with the neighbours': coalesced
+// 12-byte pieces), 64 / G rows per wave; the mean by xor butterflies inside the group (the same
+// sum in every lane of it).  Backward recomputes the norm from v:
+//   dv_c = g_c / vn - (sum_c' g_c'.v_c') v_c [|v_c|^2 >= eps] / (C vn^3)
+// (clamp passes the gradient where the input reaches the bound, as torch's clamp_min does).
+template <int G>
+__device__ __forceinline__ float gsum(float v) {
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+template <int G, bool BWD>
+__global__ __launch_bounds__(kRowT) void vec_norm_kernel(int64_t rows, int C,
+                                                         const float* __restrict__ v,
+                                                         const float* __restrict__ gout,
+                                                         float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, c = lane % G;
+  const int64_t r = ((int64_t)blockIdx.x * (kRowT / 64) + (threadIdx.x >> 6)) * (64 / G) + lane / G;
+  const bool ok = r < rows && c < C;
+  const int64_t o = (r < rows ? r : rows - 1) * 3 * (int64_t)C + 3 * (c < C ? c : 0);
+  float x = 0.f, y = 0.f, z = 0.f;
+  if (ok) {
+    x = v[o];
+    y = v[o + 1];
+    z = v[o + 2];
+  }
+  const float q = x * x + y * y + z * z;
+  const float s2 = ok ? fmaxf(q, 1e-8f) : 0.f;
+  const float m = gsum<G>(s2) / (float)C;
+  const float vn = sqrtf(m), inv = 1.f / vn;
+  if constexpr (!BWD) {
+    if (ok) {
+      out[o] = x / vn;
+      out[o + 1] = y / vn;
+      out[o + 2] = z / vn;
+    }
+  } else {
+    float gx = 0.f, gy = 0.f, gz = 0.f;
+    if (ok) {
+      gx = gout[o];
+      gy = gout[o + 1];
+      gz = gout[o + 2];
+    }
+    const float dot = gsum<G>(gx * x + gy * y + gz * z);
+    const float k = (q >= 1e-8f) ? dot * inv * inv * inv / (float)C : 0.f;
+    if (ok) {
+      out[o] = gx / vn - k * x;
+      out[o + 1] = gy / vn - k * y;
+      out[o + 2] = gz / vn - k * z;
+    }
+  }
+}
+
+template <bool BWD>
+int vec_norm_launch(int64_t rows, int64_t C, const float* v, const float* g, float* out,
+                    hipStream_t s) {
+  const int G = C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64;
+  const unsigned grid = (unsigned)ceil_div(rows, (int64_t)(kRowT / 64) * (64 / G));
+#define GMP_VN(GG) \
+  vec_norm_kernel<GG, BWD><<<grid, kRowT, 0, s>>>(rows, (int)C, v, g, out)
+  switch (G) {
+    case 1: GMP_VN(1); break;
+    case 2: GMP_VN(2); break;
+    case 4: GMP_VN(4); break;
+    case 8: GMP_VN(8); break;
+    case 16: GMP_VN(16); break;
+    case 32: GMP_VN(32); break;
+    default: GMP_VN(64); break;
+  }
+#undef GMP_VN
+  return launch_status();
+}
+
 // GMP_LN_SMALL=0: narrow rows on the generic kernels (A/B)
 int g_ln_small = getenv("GMP_LN_SMALL") ? atoi(getenv("GMP_LN_SMALL")) : 1;
 bool small_form(int64_t d) { return g_ln_small && (d == 8 || d == 16 || d == 32); }
@@ -527,6 +603,22 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
   sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, G, (int)(2 * d),
                                                                        grad_gamma_beta);
   return launch_status();
+}
+
+int gmp_vec_norm_fwd_f32(int64_t rows, int64_t channels, const float* v, float* out,
+                         void* stream) {
+  GMP_CHECK_ARG(rows >= 0 && channels >= 1 && channels <= 64);
+  if (rows == 0) return GMP_OK;
+  GMP_CHECK_ARG(v && out);
+  return vec_norm_launch<false>(rows, channels, v, nullptr, out, as_stream(stream));
+}
+
+int gmp_vec_norm_bwd_f32(int64_t rows, int64_t channels, const float* v, const float* grad_out,
+                         float* grad_v, void* stream) {
+  GMP_CHECK_ARG(rows >= 0 && channels >= 1 && channels <= 64);
+  if (rows == 0) return GMP_OK;
+  GMP_CHECK_ARG(v && grad_out && grad_v);
+  return vec_norm_launch<true>(rows, channels, v, grad_out, grad_v, as_stream(stream));
 }
 
 int64_t gmp_ln_act_bwd_partial_rows(int64_t rows) { return bwd_blocks(rows); }

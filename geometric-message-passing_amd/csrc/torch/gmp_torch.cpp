@@ -389,6 +389,29 @@ std::tuple<Tensor, Tensor> ln_act_bwd(const Tensor& gy, const Tensor& xhat, cons
   return {gx, gb};
 }
 
+// GVP vector LayerNorm rows (N, C, 3)
+Tensor vec_norm_fwd(const Tensor& v) {
+  OpGuard g(v, "vec_norm_fwd");
+  f32(v, "v");
+  TORCH_CHECK(v.dim() == 3 && v.size(2) == 3, "vec_norm_fwd: v must be (rows, channels, 3)");
+  Tensor out = at::empty_like(v);
+  check_rc(gmp_vec_norm_fwd_f32(v.size(0), v.size(1), fp(v), fp(out), cur_stream()),
+           "gmp_vec_norm_fwd_f32");
+  return out;
+}
+
+Tensor vec_norm_bwd(const Tensor& v, const Tensor& gout) {
+  OpGuard g(v, "vec_norm_bwd");
+  f32(v, "v");
+  f32(gout, "grad_out");
+  TORCH_CHECK(v.dim() == 3 && v.size(2) == 3, "vec_norm_bwd: v must be (rows, channels, 3)");
+  shape(gout, v.sizes(), "grad_out");
+  Tensor gv = at::empty_like(v);
+  check_rc(gmp_vec_norm_bwd_f32(v.size(0), v.size(1), fp(v), fp(gout), fp(gv), cur_stream()),
+           "gmp_vec_norm_bwd_f32");
+  return gv;
+}
+
 // ------------------------------------------------------------------ K1 featurisation
 int64_t edge_checks(const Tensor& pos, const Tensor& edge_index) {
   f32(pos, "pos");
@@ -1357,6 +1380,8 @@ std::tuple<Tensor, Tensor> ln_act_bwd(const Tensor&, const Tensor& xhat, const T
                                       const Tensor&, const Tensor&, int64_t) {
   return {at::empty_like(xhat), at::empty({2 * xhat.size(-1)}, xhat.options())};
 }
+Tensor vec_norm_fwd(const Tensor& v) { return at::empty_like(v); }
+Tensor vec_norm_bwd(const Tensor& v, const Tensor&) { return at::empty_like(v); }
 std::tuple<Tensor, Tensor> edge_featurize(const Tensor& pos, const Tensor& ei,
                                           at::ArrayRef<double> w, double, double, double,
                                           int64_t lmax) {
@@ -1539,6 +1564,8 @@ TORCH_LIBRARY(gmp, m) {
         "(Tensor y, Tensor xhat, Tensor rstd)");
   m.def("ln_act_bwd(Tensor grad_y, Tensor xhat, Tensor rstd, Tensor gamma, Tensor beta, "
         "int act) -> (Tensor grad_x, Tensor grad_gamma_beta)");
+  m.def("vec_norm_fwd(Tensor v) -> Tensor");
+  m.def("vec_norm_bwd(Tensor v, Tensor grad_out) -> Tensor");
   m.def("edge_featurize(Tensor pos, Tensor edge_index, float[] bessel_weights, float prefactor, "
         "float r_max, float p, int lmax=2) -> (Tensor sh, Tensor radial)");
   m.def("edge_featurize_bwd(Tensor pos, Tensor edge_index, float[] bessel_weights, "
@@ -1620,6 +1647,8 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("ssp_bwd", ns ssp_bwd);                                          \
   m.impl("ln_act_fwd", ns ln_act_fwd);                                    \
   m.impl("ln_act_bwd", ns ln_act_bwd);                                    \
+  m.impl("vec_norm_fwd", ns vec_norm_fwd);                                \
+  m.impl("vec_norm_bwd", ns vec_norm_bwd);                                \
   m.impl("edge_featurize", ns edge_featurize);                            \
   m.impl("edge_featurize_bwd", ns edge_featurize_bwd);                    \
   m.impl("edge_featurize_gvp", ns edge_featurize_gvp);                    \

@@ -130,6 +130,29 @@ class Dropout(nn.Module):
         return self.sdropout(s), self.vdropout(v)
 
 
+# GMP_GVP_VECNORM=0: the vector LayerNorm as the reference's torch chain (A/B)
+VEC_NORM_FUSED = os.environ.get("GMP_GVP_VECNORM", "1") != "0"
+
+
+class VecNormFn(torch.autograd.Function):
+    """v / sqrt(mean_c clamp(|v_c|^2, 1e-8)) over (rows, C, 3): the vector half of the GVP
+    LayerNorm (gvp_layer.py:232-243) in one HIP pass each way (gmp_vec_norm_{fwd,bwd}_f32) instead
+    of the square / sum / clamp / mean / sqrt / divide chain and its autograd graph."""
+
+    @staticmethod
+    def forward(ctx, v):
+        v = ops._f32c(v)
+        ops._need_cuda(v)
+        ctx.save_for_backward(v)
+        return _lib.torch_ops().vec_norm_fwd(v)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        (v,) = ctx.saved_tensors
+        return _lib.torch_ops().vec_norm_bwd(v, ops._f32c(g))
+
+
 class LayerNorm(nn.Module):
     """gvp_layer.py:221-243."""
 
@@ -142,6 +165,8 @@ class LayerNorm(nn.Module):
         if not self.v:
             return ops.ln_act(x, self.scalar_norm)  # K12 (act = identity)
         s, v = x
+        if VEC_NORM_FUSED and v.is_cuda and v.dtype == torch.float32 and 1 <= v.shape[-2] <= 64:
+            return ops.ln_act(s, self.scalar_norm), VecNormFn.apply(v)
         vn = _norm_no_nan(v, axis=-1, keepdims=True, sqrt=False)
         vn = torch.sqrt(torch.mean(vn, dim=-2, keepdim=True))
         return ops.ln_act(s, self.scalar_norm), v / vn

@@ -635,6 +635,17 @@ int gmp_sum_rows_f32(const float* partials, int64_t nrows, int64_t width, float*
                      void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * GVP vector LayerNorm (gvp_layer.py:232-243: v / sqrt(mean_c clamp(|v_c|^2, 1e-8)), the norm
+ * of _norm_no_nan, :66-73).  v (rows, channels, 3) contiguous, 1 <= channels <= 64.  Forward
+ * writes out = v / vn; backward recomputes vn from v and writes grad_v from grad_out (the clamp
+ * passes the gradient where |v_c|^2 >= 1e-8, as torch's clamp_min).  No workspace.
+ * ------------------------------------------------------------------------------------------ */
+int gmp_vec_norm_fwd_f32(int64_t rows, int64_t channels, const float* v, float* out,
+                         void* stream);
+int gmp_vec_norm_bwd_f32(int64_t rows, int64_t channels, const float* v, const float* grad_out,
+                         float* grad_v, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
  * element_dependent=False, called per output irrep at :176-185), all output irreps of C channels
  * at once.  x (N, C, D) = reshape_irreps of C x (0e+1o[+2e[+3o]]) (irreps_tools.py:63-79),
