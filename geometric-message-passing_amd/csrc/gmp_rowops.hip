@@ -480,6 +480,31 @@ int vec_norm_launch(int64_t rows, int64_t C, const float* v, const float* g, flo
   return launch_status();
 }
 
+// _norm_no_nan over the xyz axis of (rows, 3, h) rows (gvp_layer.py:66-73 as GVP.forward applies
+// it to vh, :101-170): out (rows, h) = sqrt(max(sum_x vh[x, c]^2, 1e-8)); backward
+// dvh[x, c] = g[c] vh[x, c] / out[c] where the sum reaches the bound (torch's clamp_min mask).
+// One thread per (row, c): the three strided loads coalesce across c.
+template <bool BWD>
+__global__ __launch_bounds__(kRowT) void xyz_norm_kernel(int64_t n, int h,
+                                                         const float* __restrict__ vh,
+                                                         const float* __restrict__ g,
+                                                         float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * kRowT + threadIdx.x;
+  if (t >= n) return;
+  const int64_t r = t / h, c = t - r * h, o = r * 3 * (int64_t)h + c;
+  const float x = vh[o], y = vh[o + h], z = vh[o + 2 * h];
+  const float q = x * x + y * y + z * z;
+  const float nv = sqrtf(fmaxf(q, 1e-8f));
+  if constexpr (!BWD) {
+    out[t] = nv;
+  } else {
+    const float k = q >= 1e-8f ? g[t] / nv : 0.f;
+    out[o] = k * x;
+    out[o + h] = k * y;
+    out[o + 2 * h] = k * z;
+  }
+}
+
 // GMP_LN_SMALL=0: narrow rows on the generic kernels (A/B)
 int g_ln_small = getenv("GMP_LN_SMALL") ? atoi(getenv("GMP_LN_SMALL")) : 1;
 bool small_form(int64_t d) { return g_ln_small && (d == 8 || d == 16 || d == 32); }
@@ -619,6 +644,27 @@ int gmp_vec_norm_bwd_f32(int64_t rows, int64_t channels, const float* v, const f
   if (rows == 0) return GMP_OK;
   GMP_CHECK_ARG(v && grad_out && grad_v);
   return vec_norm_launch<true>(rows, channels, v, grad_out, grad_v, as_stream(stream));
+}
+
+int gmp_xyz_norm_fwd_f32(int64_t rows, int64_t h, const float* vh, float* out, void* stream) {
+  GMP_CHECK_ARG(rows >= 0 && h >= 1);
+  if (rows == 0) return GMP_OK;
+  GMP_CHECK_ARG(vh && out);
+  const int64_t n = rows * h;
+  xyz_norm_kernel<false><<<(unsigned)ceil_div(n, (int64_t)kRowT), kRowT, 0, as_stream(stream)>>>(
+      n, (int)h, vh, nullptr, out);
+  return launch_status();
+}
+
+int gmp_xyz_norm_bwd_f32(int64_t rows, int64_t h, const float* vh, const float* grad_out,
+                         float* grad_vh, void* stream) {
+  GMP_CHECK_ARG(rows >= 0 && h >= 1);
+  if (rows == 0) return GMP_OK;
+  GMP_CHECK_ARG(vh && grad_out && grad_vh);
+  const int64_t n = rows * h;
+  xyz_norm_kernel<true><<<(unsigned)ceil_div(n, (int64_t)kRowT), kRowT, 0, as_stream(stream)>>>(
+      n, (int)h, vh, grad_out, grad_vh);
+  return launch_status();
 }
 
 int64_t gmp_ln_act_bwd_partial_rows(int64_t rows) { return bwd_blocks(rows); }

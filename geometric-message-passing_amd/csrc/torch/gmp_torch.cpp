@@ -412,6 +412,29 @@ Tensor vec_norm_bwd(const Tensor& v, const Tensor& gout) {
   return gv;
 }
 
+// GVP |vh| over the xyz axis of (rows, 3, h)
+Tensor xyz_norm_fwd(const Tensor& vh) {
+  OpGuard g(vh, "xyz_norm_fwd");
+  f32(vh, "vh");
+  TORCH_CHECK(vh.dim() == 3 && vh.size(1) == 3, "xyz_norm_fwd: vh must be (rows, 3, h)");
+  Tensor out = at::empty({vh.size(0), vh.size(2)}, vh.options());
+  check_rc(gmp_xyz_norm_fwd_f32(vh.size(0), vh.size(2), fp(vh), fp(out), cur_stream()),
+           "gmp_xyz_norm_fwd_f32");
+  return out;
+}
+
+Tensor xyz_norm_bwd(const Tensor& vh, const Tensor& gout) {
+  OpGuard g(vh, "xyz_norm_bwd");
+  f32(vh, "vh");
+  f32(gout, "grad_out");
+  TORCH_CHECK(vh.dim() == 3 && vh.size(1) == 3, "xyz_norm_bwd: vh must be (rows, 3, h)");
+  shape(gout, {vh.size(0), vh.size(2)}, "grad_out");
+  Tensor gv = at::empty_like(vh);
+  check_rc(gmp_xyz_norm_bwd_f32(vh.size(0), vh.size(2), fp(vh), fp(gout), fp(gv), cur_stream()),
+           "gmp_xyz_norm_bwd_f32");
+  return gv;
+}
+
 // ------------------------------------------------------------------ K1 featurisation
 int64_t edge_checks(const Tensor& pos, const Tensor& edge_index) {
   f32(pos, "pos");
@@ -1382,6 +1405,8 @@ std::tuple<Tensor, Tensor> ln_act_bwd(const Tensor&, const Tensor& xhat, const T
 }
 Tensor vec_norm_fwd(const Tensor& v) { return at::empty_like(v); }
 Tensor vec_norm_bwd(const Tensor& v, const Tensor&) { return at::empty_like(v); }
+Tensor xyz_norm_fwd(const Tensor& vh) { return at::empty({vh.size(0), vh.size(2)}, vh.options()); }
+Tensor xyz_norm_bwd(const Tensor& vh, const Tensor&) { return at::empty_like(vh); }
 std::tuple<Tensor, Tensor> edge_featurize(const Tensor& pos, const Tensor& ei,
                                           at::ArrayRef<double> w, double, double, double,
                                           int64_t lmax) {
@@ -1566,6 +1591,8 @@ TORCH_LIBRARY(gmp, m) {
         "int act) -> (Tensor grad_x, Tensor grad_gamma_beta)");
   m.def("vec_norm_fwd(Tensor v) -> Tensor");
   m.def("vec_norm_bwd(Tensor v, Tensor grad_out) -> Tensor");
+  m.def("xyz_norm_fwd(Tensor vh) -> Tensor");
+  m.def("xyz_norm_bwd(Tensor vh, Tensor grad_out) -> Tensor");
   m.def("edge_featurize(Tensor pos, Tensor edge_index, float[] bessel_weights, float prefactor, "
         "float r_max, float p, int lmax=2) -> (Tensor sh, Tensor radial)");
   m.def("edge_featurize_bwd(Tensor pos, Tensor edge_index, float[] bessel_weights, "
@@ -1649,6 +1676,8 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("ln_act_bwd", ns ln_act_bwd);                                    \
   m.impl("vec_norm_fwd", ns vec_norm_fwd);                                \
   m.impl("vec_norm_bwd", ns vec_norm_bwd);                                \
+  m.impl("xyz_norm_fwd", ns xyz_norm_fwd);                                \
+  m.impl("xyz_norm_bwd", ns xyz_norm_bwd);                                \
   m.impl("edge_featurize", ns edge_featurize);                            \
   m.impl("edge_featurize_bwd", ns edge_featurize_bwd);                    \
   m.impl("edge_featurize_gvp", ns edge_featurize_gvp);                    \

@@ -179,6 +179,8 @@ SIGNATURES = {
     "gmp_ln_act_bwd_partial_rows": (c_i64, [c_i64]),
     "gmp_vec_norm_fwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp]),
     "gmp_vec_norm_bwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_xyz_norm_fwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "gmp_xyz_norm_bwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "gmp_sum_rows_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "gmp_ln_act_bwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp,
                                    c_vp, c_size, c_vp]),

@@ -39,7 +39,8 @@ def _merge(s, v):
 
 
 def tuple_sum(*args):
-    return tuple(map(sum, zip(*args)))
+    # (the reference's map(sum, ...) starts from 0: one extra full-size add per component)
+    return tuple(functools.reduce(lambda a, b: a + b, xs) for xs in zip(*args))
 
 
 def tuple_cat(*args, dim=-1):
@@ -93,8 +94,7 @@ class GVP(nn.Module):
         if self.vi:
             s, v = x
             vh = ops.linear(v.transpose(-1, -2), self.wh.weight)
-            s = ops.linear(torch.cat([s, _norm_no_nan(vh, axis=-2)], -1), self.ws.weight,
-                           self.ws.bias)
+            s = ops.linear(torch.cat([s, _xyz_norm(vh)], -1), self.ws.weight, self.ws.bias)
             return self._tail(s, vh)
         s = self.ws(x)
         v = torch.zeros(s.shape[0], self.vo, 3, device=s.device, dtype=s.dtype) if self.vo \
@@ -151,6 +151,31 @@ class VecNormFn(torch.autograd.Function):
     def backward(ctx, g):
         (v,) = ctx.saved_tensors
         return _lib.torch_ops().vec_norm_bwd(v, ops._f32c(g))
+
+
+class XyzNormFn(torch.autograd.Function):
+    """_norm_no_nan(vh, axis=-2) of GVP.forward (gvp_layer.py:66-73, :101-170) for vh (rows, 3, h):
+    one HIP pass each way (gmp_xyz_norm_{fwd,bwd}_f32) instead of square / sum / clamp / sqrt."""
+
+    @staticmethod
+    def forward(ctx, vh):
+        vh = ops._f32c(vh)
+        ops._need_cuda(vh)
+        ctx.save_for_backward(vh)
+        return _lib.torch_ops().xyz_norm_fwd(vh)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        (vh,) = ctx.saved_tensors
+        return _lib.torch_ops().xyz_norm_bwd(vh, ops._f32c(g))
+
+
+def _xyz_norm(vh):
+    if VEC_NORM_FUSED and vh.is_cuda and vh.dtype == torch.float32 and vh.dim() == 3 \
+            and vh.shape[1] == 3:
+        return XyzNormFn.apply(vh)
+    return _norm_no_nan(vh, axis=-2)
 
 
 class LayerNorm(nn.Module):
@@ -456,7 +481,7 @@ class GVPConv(MessagePassing):
         es, ev = edge_attr
         evt = ev.transpose(-1, -2)                 # (E, 3, ve)
         vh = Qj + Qi + ops.linear(evt, Wh[:, vi:vi + ve])
-        vn = _norm_no_nan(vh, axis=-2)
+        vn = _xyz_norm(vh)
         # edge part of W_s on [e_s | |vh|] as one per-edge Linear (dW by the edge outer sum)
         We = torch.cat([Ws[:, si:si + se], Ws[:, 2 * si + se:]], 1)
         s1 = ops.linear(torch.cat([es, vn], -1), We, g0.ws.bias) + Pj + Pi

@@ -644,6 +644,12 @@ int gmp_vec_norm_fwd_f32(int64_t rows, int64_t channels, const float* v, float* 
                          void* stream);
 int gmp_vec_norm_bwd_f32(int64_t rows, int64_t channels, const float* v, const float* grad_out,
                          float* grad_v, void* stream);
+/* _norm_no_nan over the xyz axis of vh (rows, 3, h) contiguous (GVP.forward's |vh|,
+ * gvp_layer.py:66-73, :101-170): out (rows, h) = sqrt(max(sum_x vh^2, 1e-8)); backward
+ * grad_vh (rows, 3, h) from grad_out (rows, h). */
+int gmp_xyz_norm_fwd_f32(int64_t rows, int64_t h, const float* vh, float* out, void* stream);
+int gmp_xyz_norm_bwd_f32(int64_t rows, int64_t h, const float* vh, const float* grad_out,
+                         float* grad_vh, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with

@@ -275,3 +275,26 @@ def test_vec_norm_vs_torch(rows, C):
     scale = vb.grad.abs().amax(dim=(1, 2))
     err = (va.grad.double().cpu() - vb.grad).abs().amax(dim=(1, 2))
     assert bool((err <= 1e-5 * scale + 1e-6).all()), (err / (scale + 1e-12)).max().item()
+
+
+@pytest.mark.parametrize("rows,h", [(50_000, 32), (1_000_001, 1), (333, 33), (0, 16)])
+def test_xyz_norm_vs_torch(rows, h):
+    """GVP.forward's |vh| over the xyz axis (gmp_xyz_norm_{fwd,bwd}_f32) against the reference's
+    _norm_no_nan(vh, axis=-2) in fp64, zero columns exercising the clamp."""
+    from gmp_amd.gvp import XyzNormFn
+    g = torch.Generator().manual_seed(rows + h)
+    vh = torch.randn(rows, 3, h, generator=g)
+    if rows:
+        vh[::5, :, 0] = 0.0
+    gout = torch.randn(rows, h, generator=g)
+    va = vh.to(DEV).requires_grad_(True)
+    y = XyzNormFn.apply(va)
+    (y * gout.to(DEV)).sum().backward()
+    vb = vh.double().requires_grad_(True)
+    yr = torch.sqrt(torch.clamp(torch.sum(torch.square(vb), -2), min=1e-8))
+    (yr * gout.double()).sum().backward()
+    assert y.shape == (rows, h) and va.grad.shape == (rows, 3, h)
+    if rows == 0:
+        return
+    assert (y.double().cpu() - yr.detach()).abs().max().item() <= 1e-6 * yr.abs().max().item()
+    assert (va.grad.double().cpu() - vb.grad).abs().max().item() <= 1e-6 * vb.grad.abs().max().item() + 1e-7
