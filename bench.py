@@ -21,11 +21,15 @@ xGMI).  --graph replays the step from a HIP graph instead of launching it eagerl
 itself (torch.distributed.run, 127.0.0.1 rendezvous) before this process touches the GPU and exits
 with their status; under torchrun, WORLD_SIZE must equal N (else exit status 2).
 
-Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel of the value's workload
-(EGNN: egnn_edge_bwd, both bounds, the closer one primary), timed with HIP events on the stream
-it is launched on; the `mace` object's roofline is the whole TP contraction's algorithmic FLOP
-against the three-plane bf16 ceiling, with the step's PMC HBM bytes against SURVEY §8(d)'s
-algorithmic bytes as `traffic` / `waste_ratio` (mace_roofline).  `cpu_baseline` times the CPU
+Rank 0 prints ONE JSON line.  Every `roofline.frac` is ALGORITHMIC work over measured time over
+the peak, recomputable from SURVEY §8(d) and the committed profiles/r05_*:
+  EGNN  frac = 1,592 B/edge x E / t(egnn_bwd_kernel, HIP events on its stream) / 8 TB/s
+  GVP   frac = 2,268 B/edge x 3 (fwd + bwd) x layers x E / t(step) / 8 TB/s
+  MACE, TFN  frac = TP-contraction FLOP per step (tp_node_flops) / t(its kernels) / 419.5 TF
+                    (the bf16 dense peak / 6: three-plane split products)
+and `traffic` = PMC HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, separate passes) of the newest
+committed profile, `waste_ratio` = traffic / the algorithmic bytes.  The design's own byte counts
+and MFMA fractions are secondary fields.  `cpu_baseline` times the CPU
 oracle (oracle/*.py, plain PyTorch on the host cores: the reference's CPU path restated) on a
 bounded spatial sample of the same graph, median of the timed steps (CPU_SAMPLE).
 """
@@ -210,6 +214,8 @@ def egnn_bwd_bytes_per_edge(d, n_nodes, n_edges, planes=3):
 # SURVEY §8(d) algorithmic bytes per edge and layer of the EGNN forward (fused minimum: idx 16 +
 # pos 24 + h_i, h_j 1,024 + message scatter 512 + pos 12 + count 4)
 EGNN_SURVEY_BYTES_PER_EDGE = 1592
+# ... and of a GVP layer (2,268 B/edge)
+GVP_SURVEY_BYTES_PER_EDGE = 2268
 
 
 def tp_forward_flops(model, n_nodes, n_edges):
@@ -588,27 +594,23 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup, exact=False
             # (default) or the exact f32 MFMA
             peak = FP32_MFMA_PEAK_TFLOPS if f32_mode else HF2_PEAK_TFLOPS
             f_mfma, f_hbm = tflops / peak, gbs / HBM_PEAK_GBS
-            # both bounds are reported; the primary one is the closer of the two
-            if f_mfma >= f_hbm:
-                prim = {"bound": "mfma", "achieved": tflops, "peak": peak,
-                        "unit": "TFLOP/s (f32-equivalent)", "frac": f_mfma}
-            else:
-                prim = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": f_hbm}
-            # SURVEY §8(d)'s algorithmic bytes (1,592 B per edge and layer) instead of the bytes
-            # this design's backward moves (saved x_hat planes, dpre rows for the weight sums)
-            frac_survey = EGNN_SURVEY_BYTES_PER_EDGE * g.num_edges / (ms_bwd * 1e-3) / 1e9 \
-                / HBM_PEAK_GBS
-            roof = {"kernel": "egnn_edge_bwd", "kernel_prefix": "egnn_bwd_kernel", **prim,
-                    "frac_survey": frac_survey,
-                    "frac_survey_note": "SURVEY §8(d) 1,592 B/edge per layer over this kernel's "
-                                        "time at 8 TB/s",
+            # primary: SURVEY §8(d)'s algorithmic bytes, 1,592 B per edge and
+            # layer, over this kernel's time at 8 TB/s.  The bytes this design's backward moves
+            # (saved x_hat planes, the dpre rows of the weight sums) and its MFMA ceiling are
+            # secondary fields; waste_ratio = PMC bytes per launch / the algorithmic bytes.
+            algo = EGNN_SURVEY_BYTES_PER_EDGE * g.num_edges
+            frac_survey = algo / (ms_bwd * 1e-3) / 1e9 / HBM_PEAK_GBS
+            roof = {"kernel": "egnn_edge_bwd", "kernel_prefix": "egnn_bwd_kernel",
+                    "bound": "hbm", "achieved": algo / (ms_bwd * 1e-3) / 1e9,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": frac_survey,
+                    "algorithmic_bytes_per_launch": algo,
+                    "frac_note": "SURVEY §8(d) 1,592 B/edge per layer x E / kernel time / 8 TB/s",
                     "traffic": None, "ms_per_launch": ms_bwd,
-                    "flops_per_edge": fl["egnn_edge_bwd"], "mfma_frac": f_mfma,
-                    "mfma_peak": peak, "products": "f32 MFMA" if f32_mode else
-                    "f16 MFMA, 2-plane split operands (3 products per f32 product)",
-                    "bytes_per_edge_min": bpe, "xhat_planes_saved": planes,
-                    "hbm_gbs": gbs, "hbm_frac": f_hbm,
+                    "design_bytes_per_edge": bpe, "design_gbs": gbs, "design_frac": f_hbm,
+                    "flops_per_edge": fl["egnn_edge_bwd"], "mfma_achieved": tflops,
+                    "mfma_frac": f_mfma, "mfma_peak": peak, "products": "f32 MFMA" if f32_mode
+                    else "f16 MFMA, 2-plane split operands (3 products per f32 product)",
+                    "xhat_planes_saved": planes,
                     "fwd_kernel_ms": ms_fwd,
                     "fwd_kernel_tflops": fl["egnn_edge_fwd"] * g.num_edges
                     / (ms_fwd * 1e-3) / 1e12}
@@ -625,24 +627,35 @@ def run_workload(workload, args, g, rank, world, dev, steps, warmup, exact=False
                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                     "traffic": None, "flops_per_edge": fl}
             st = step_traffic(workload)
-            if st is not None:
-                # the step moves more bytes per second than it computes: HBM is the binding
-                # bound (DESIGN.md §3 "Round 4", GVP); the MFMA figures stay as secondary fields
-                gbs = st[0] / (elapsed / steps) / 1e9
+            if workload == "gvp":
+                # primary: SURVEY §8(d)'s algorithmic bytes (2,268 B per edge and
+                # layer, x 3 for forward + backward) over the step time at 8 TB/s; the committed
+                # PMC bytes per step are `traffic`, waste_ratio = traffic / algorithmic
+                algo = GVP_SURVEY_BYTES_PER_EDGE * 3 * layers * g.num_edges
+                gbs = algo / (elapsed / steps) / 1e9
                 roof = {"kernel": "whole step (fwd+bwd, all kernels)", "kernel_prefix": "-",
                         "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": gbs / HBM_PEAK_GBS, "traffic": st[0],
-                        "traffic_note": "PMC HBM bytes per training step (FETCH_SIZE x2 + "
-                                        "WRITE_SIZE) of the committed profile",
-                        "traffic_source": f"profiles/{st[1]}",
-                        "mfma_achieved": achieved, "mfma_peak": FP32_MFMA_PEAK_TFLOPS,
+                        "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_step": algo,
+                        "frac_note": "SURVEY §8(d) 2,268 B/edge per layer x 3 (fwd + bwd) x "
+                                     "layers x E / step time / 8 TB/s",
+                        "traffic": None, "mfma_achieved": achieved,
+                        "mfma_peak": FP32_MFMA_PEAK_TFLOPS,
                         "mfma_frac": achieved / FP32_MFMA_PEAK_TFLOPS, "flops_per_edge": fl}
+                if st is not None:
+                    roof.update({"traffic": st[0], "waste_ratio": st[0] / algo,
+                                 "traffic_note": "PMC HBM bytes per training step (FETCH_SIZE "
+                                                 "x2 + WRITE_SIZE) of the committed profile",
+                                 "traffic_source": f"profiles/{st[1]}",
+                                 "traffic_gbs": st[0] / (elapsed / steps) / 1e9})
         else:
             roof = mace_roofline(model, g.num_nodes, g.num_edges, totals, counts, n_timed,
                                  workload)
-        t = None if workload in ("mace", "tfn") else pmc_traffic(workload, roof["kernel_prefix"])
+        t = None if workload in ("mace", "tfn", "gvp") else pmc_traffic(workload,
+                                                                         roof["kernel_prefix"])
         if t is not None:
             roof["traffic"], roof["traffic_source"] = t[0], f"profiles/{t[1]}"
+            if "algorithmic_bytes_per_launch" in roof:
+                roof["waste_ratio"] = t[0] / roof["algorithmic_bytes_per_launch"]
         rec = {"value": total_edges * steps / elapsed, "unit": "edges/s", "steps": steps,
                "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
                "workload": f"{WORKLOADS[workload][0]} {layers}L/{emb} radius graph "

@@ -32,7 +32,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // backward: 8 waves (<= 256 VGPRs -> 2 per SIMD).
 constexpr int kFwdWaves = 12;
 #ifndef GMP_EGNN_HF_FWD_WAVES
-#define GMP_EGNN_HF_FWD_WAVES 8
+#define GMP_EGNN_HF_FWD_WAVES 12
 #endif
 // HF forward: 8 waves (<= 256 VGPRs -> 2 per SIMD): its products need fewer MFMA cycles but more
 // live registers (fp16 operand planes) than 168 allow without spills
@@ -50,7 +50,15 @@ struct Cfg {
 // feature held by lane group g in slot s = 4p + c
 __device__ __forceinline__ constexpr int featq(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
 
-enum VecId { V_W1D = 0, V_B1, V_LN1W, V_LN1B, V_B2, V_LN2W, V_LN2B, V_B3, V_LN3W, V_LN3B, V_W4, NV };
+// LDS vectors.  The first NVB are the parameters as given; the HF path adds pre-scaled copies
+// (DESIGN.md "K4 r05"): V_B2S / V_B3S = the centred biases times 2^(ex + sw) (the products'
+// accumulator scale), V_LN1WS / V_LN1BS = the first LayerNorm's affine times 2^ex2 (relu is
+// positively homogeneous, so act(x w 2^ex + b 2^ex) = 2^ex act(x w + b) exactly; y1 feeds only
+// the W2 product).  (The message m = act(LN2) is aggregated as well, so it stays unscaled.)
+enum VecId {
+  V_W1D = 0, V_B1, V_LN1W, V_LN1B, V_B2, V_LN2W, V_LN2B, V_B3, V_LN3W, V_LN3B, V_W4, NVB,
+  V_B2S = NVB, V_B3S, V_LN1WS, V_LN1BS, NV
+};
 
 template <int D>
 constexpr int carry_stride() { return D / 4 + 4; }
@@ -125,9 +133,9 @@ __device__ void load_params_to_lds(float* smem, const gmp_egnn_params& P) {
       *reinterpret_cast<float4*>(sW3 + o * LDW + k) = b;
     }
   }
-  const float* vsrc[NV] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
-                           P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
-  for (int i = threadIdx.x; i < NV * D; i += blockDim.x) sV[i] = vsrc[i / D][i % D];
+  const float* vsrc[NVB] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
+                            P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
+  for (int i = threadIdx.x; i < NVB * D; i += blockDim.x) sV[i] = vsrc[i / D][i % D];
 }
 
 // exponent s with max|v| 2^s < 2^15 (fp16 range with headroom), clamped to [-60, 60]
@@ -148,30 +156,61 @@ __device__ __forceinline__ int hf_pos(int k) {
   const int tt = k >> 4, gg = (k >> 2) & 3, q = k & 3;
   return 32 * (tt >> 1) + 8 * gg + 4 * (tt & 1) + q;
 }
-template <int D, bool TRANSPOSE>
-__device__ void load_params_hf(float* sV, _Float16* hW, const gmp_egnn_params& P) {
+// the effective static input exponent of a forward product: sx clamped so that sx + sw stays in
+// [-100, 100] (the accumulator scale 2^(sx + sw) and its inverse are normal floats)
+__device__ __forceinline__ int clamp_in_exp(int sx, int sw) {
+  return sx < -100 - sw ? -100 - sw : (sx > 100 - sw ? 100 - sw : sx);
+}
+
+// CMASK bit m: centre matrix m (0: W2, 1: W3) and its bias over the output dimension,
+// W_c[o][k] = W[o][k] - mean_o W[o][k], b_c = b - mean(b).  The centred product's outputs then
+// have zero mean, LN(W_c x + b_c) = LN(W x + b) exactly in real arithmetic, and the LayerNorm
+// after it needs no mean pass (ln_rms).  The backward needs no change: LayerNorm's input gradient
+// has zero mean, so W_c^T dpre = W^T dpre and dW = dpre x^T are the original ones.
+// `scratch` (2 d + 2 floats: the column and bias means) is the carry area, unused until the loop.
+template <int D, bool TRANSPOSE, int CMASK, int ACT>
+__device__ void load_params_hf(float* sV, _Float16* hW, float* scratch, const gmp_egnn_params& P) {
   using H = HCfg<D>;
-  // scalars after the vectors: [0] [1] exponents of W2 / W3, [2] [3] static input exponents of
-  // the forward products (below), [4..7] max scratch
+  // scalars after the vectors: [0] [1] exponents of W2 / W3, [2] [3] the static (clamped) input
+  // exponents ex2 / ex3 of the forward products (below), [4..9] max scratch
   unsigned* mxw = reinterpret_cast<unsigned*>(sV + NV * D + 4);
   if (threadIdx.x < 6) mxw[threadIdx.x] = 0u;
   __syncthreads();
-  unsigned m2 = 0u, m3 = 0u;  // |w| bit patterns order like the values
-  for (int i = threadIdx.x; i < D * D / 4; i += blockDim.x) {
-    const float4 a = reinterpret_cast<const float4*>(P.W2)[i];
-    const float4 b = reinterpret_cast<const float4*>(P.W3)[i];
-    m2 = max(m2, max(max(__float_as_uint(fabsf(a.x)), __float_as_uint(fabsf(a.y))),
-                     max(__float_as_uint(fabsf(a.z)), __float_as_uint(fabsf(a.w)))));
-    m3 = max(m3, max(max(__float_as_uint(fabsf(b.x)), __float_as_uint(fabsf(b.y))),
-                     max(__float_as_uint(fabsf(b.z)), __float_as_uint(fabsf(b.w)))));
+  if (threadIdx.x < 2 * D) {  // column (mat, k): mean over the output rows and max |W| (fixed order)
+    const int mat = threadIdx.x / D, k = threadIdx.x - mat * D;
+    const float* W = mat ? P.W3 : P.W2;
+    float s = 0.f, m = 0.f;
+#pragma unroll 8
+    for (int o = 0; o < D; ++o) {
+      const float w = W[o * D + k];
+      s += w;
+      m = fmaxf(m, fabsf(w));
+    }
+    const float mean = ((CMASK >> mat) & 1) ? s * (1.f / D) : 0.f;
+    scratch[threadIdx.x] = mean;
+    atomicMax(&mxw[mat], __float_as_uint(m + fabsf(mean)));  // >= max |W_c| (a bound suffices)
+  } else if (threadIdx.x < 2 * D + 64) {  // bias means (one wave, fixed-order butterfly)
+    const int l = threadIdx.x - 2 * D;
+    float a = 0.f, b = 0.f;
+    for (int k = l; k < D; k += 64) {
+      a += P.b2[k];
+      b += P.b3[k];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      a += __shfl_xor(a, off, 64);
+      b += __shfl_xor(b, off, 64);
+    }
+    if (l == 0) {
+      scratch[2 * D] = (CMASK & 1) ? a * (1.f / D) : 0.f;
+      scratch[2 * D + 1] = (CMASK & 2) ? b * (1.f / D) : 0.f;
+    }
   }
-  atomicMax(&mxw[0], m2);
-  atomicMax(&mxw[1], m3);
   // forward inputs of W2 / W3 are act(x_hat * w + b) of a LayerNorm over d features:
   // |x_hat| <= sqrt(d - 1), |act(z)| <= |z| (relu, silu) => |input| <= sqrt(d) max|w| + max|b|
-  if (threadIdx.x < 64) {  // (the backward's x_hat3 recompute uses sx3 too)
+  if (threadIdx.x >= 2 * D + 64 && threadIdx.x < 2 * D + 128) {
     unsigned a = 0u, b = 0u, c = 0u, e = 0u;
-    for (int k = threadIdx.x; k < D; k += 64) {
+    for (int k = threadIdx.x - 2 * D - 64; k < D; k += 64) {
       a = max(a, __float_as_uint(fabsf(P.ln1_w[k])));
       b = max(b, __float_as_uint(fabsf(P.ln1_b[k])));
       c = max(c, __float_as_uint(fabsf(P.ln2_w[k])));
@@ -185,27 +224,36 @@ __device__ void load_params_hf(float* sV, _Float16* hW, const gmp_egnn_params& P
   __syncthreads();
   const int s2 = scale_exp(__uint_as_float(mxw[0])), s3 = scale_exp(__uint_as_float(mxw[1]));
   const float rd = sqrtf((float)D);
-  const int sx2 = scale_exp(rd * __uint_as_float(mxw[2]) + __uint_as_float(mxw[3]));
-  const int sx3 = scale_exp(rd * __uint_as_float(mxw[4]) + __uint_as_float(mxw[5]));
+  const int ex2 = clamp_in_exp(scale_exp(rd * __uint_as_float(mxw[2]) + __uint_as_float(mxw[3])), s2);
+  const int ex3 = clamp_in_exp(scale_exp(rd * __uint_as_float(mxw[4]) + __uint_as_float(mxw[5])), s3);
   __syncthreads();  // (the scratch words are overwritten below)
   for (int i = threadIdx.x; i < 2 * D * D; i += blockDim.x) {
     const int mat = i / (D * D), e = i - mat * D * D;
     const int o = e / D, k = e - o * D;  // W[o][k]
-    const float w = ldexpf((mat ? P.W3 : P.W2)[e], mat ? s3 : s2);
+    const float w = ldexpf((mat ? P.W3 : P.W2)[e] - scratch[mat * D + k], mat ? s3 : s2);
     const int r = TRANSPOSE ? k : o, c = TRANSPOSE ? o : k;
     const _Float16 hi = (_Float16)w;
     _Float16* dst = hW + mat * H::MAT + r * H::LDH + hf_pos(c);
     dst[0] = hi;
     dst[H::PLANE] = (_Float16)(w - (float)hi);
   }
-  const float* vsrc[NV] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
-                           P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
-  for (int i = threadIdx.x; i < NV * D; i += blockDim.x) sV[i] = vsrc[i / D][i % D];
+  const float* vsrc[NVB] = {P.w1d, P.b1, P.ln1_w, P.ln1_b, P.b2, P.ln2_w,
+                            P.ln2_b, P.b3, P.ln3_w, P.ln3_b, P.w4};
+  for (int i = threadIdx.x; i < NVB * D; i += blockDim.x) sV[i] = vsrc[i / D][i % D];
+  // pre-scaled copies: accumulator biases at 2^(ex + sw); relu inputs at 2^ex (silu is not
+  // homogeneous: its inputs are scaled in the operand split instead)
+  for (int k = threadIdx.x; k < D; k += blockDim.x) {
+    sV[V_B2S * D + k] = ldexpf(P.b2[k] - scratch[2 * D], ex2 + s2);
+    sV[V_B3S * D + k] = ldexpf(P.b3[k] - scratch[2 * D + 1], ex3 + s3);
+    const int e1 = ACT == GMP_ACT_RELU ? ex2 : 0;
+    sV[V_LN1WS * D + k] = ldexpf(P.ln1_w[k], e1);
+    sV[V_LN1BS * D + k] = ldexpf(P.ln1_b[k], e1);
+  }
   if (threadIdx.x == 0) {
     sV[NV * D + 0] = (float)s2;
     sV[NV * D + 1] = (float)s3;
-    sV[NV * D + 2] = (float)sx2;
-    sV[NV * D + 3] = (float)sx3;
+    sV[NV * D + 2] = (float)ex2;
+    sV[NV * D + 3] = (float)ex3;
   }
 }
 
@@ -300,9 +348,53 @@ __device__ __forceinline__ void gemm_wx(const float* __restrict__ sW, const f32x
 }
 
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #ifndef HF_TILES_PER_FENCE
 #define HF_TILES_PER_FENCE 2
 #endif
+
+// 2-plane fp16 split of 8 (already scaled) floats a[0..3], b[0..3]: hi = RNE fp16 of v, lo = RNE
+// fp16 of v - hi (exact in f32, so one rounding: bitwise (_Float16)(v - (float)hi)).  hi by
+// v_cvt_pk_f16_f32 (two values per instruction); lo by v_fma_mix{lo,hi}_f16 v * 1.0 - hi, which
+// reads the fp16 hi straight from the packed pair — 3 instructions per pair where the compiler's
+// form (two cvt_f32_f16, a packed subtract, a second cvt_pk) takes 5.  The trailing s_nop 1 is the
+// VALU-write -> MFMA-operand wait the compiler does not insert after an asm statement
+// (cdna_hip_programming.md §5.7 item 2).
+__device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, h16x8& bh, h16x8& bl) {
+#ifdef K4_C_SPLIT
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = j < 4 ? a[j] : b[j - 4];
+    const _Float16 h = (_Float16)v;
+    bh[j] = h;
+    bl[j] = (_Float16)(v - (float)h);
+  }
+  return;
+#endif
+  const h16x2 p0 = {(_Float16)a[0], (_Float16)a[1]}, p1 = {(_Float16)a[2], (_Float16)a[3]};
+  const h16x2 p2 = {(_Float16)b[0], (_Float16)b[1]}, p3 = {(_Float16)b[2], (_Float16)b[3]};
+  const unsigned u0 = __builtin_bit_cast(unsigned, p0), u1 = __builtin_bit_cast(unsigned, p1);
+  const unsigned u2 = __builtin_bit_cast(unsigned, p2), u3 = __builtin_bit_cast(unsigned, p3);
+  unsigned l0, l1, l2, l3;
+  // (1.0 from a register: an inline constant's interpretation in a mixed-precision operand slot
+  // is not something to rely on)
+  const float one = 1.0f;
+  asm("v_fma_mixlo_f16 %0, %4, %16, -%12 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %5, %16, -%12 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %6, %16, -%13 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %7, %16, -%13 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %2, %8, %16, -%14 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %2, %9, %16, -%14 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %3, %10, %16, -%15 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %3, %11, %16, -%15 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "s_nop 1"
+      : "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]),
+        "v"(u0), "v"(u1), "v"(u2), "v"(u3), "s"(one));
+  bh = __builtin_bit_cast(h16x8, (u32x4){u0, u1, u2, u3});
+  bl = __builtin_bit_cast(h16x8, (u32x4){l0, l1, l2, l3});
+}
 
 __device__ __forceinline__ float max_groups(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
@@ -336,20 +428,14 @@ __device__ __forceinline__ void gemm_h2(const _Float16* __restrict__ hW, int sw,
       for (int c = 0; c < 4; ++c) mx = fmaxf(mx, fabsf(x[p][c]));
     sx = scale_exp(max_groups(mx));
   }
-  sx = sx < -100 - sw ? -100 - sw : (sx > 100 - sw ? 100 - sw : sx);
+  sx = clamp_in_exp(sx, sw);
   const float fx = ldexpf(1.f, sx), up = ldexpf(1.f, sx + sw), down = ldexpf(1.f, -(sx + sw));
 #pragma unroll
   for (int t = 0; t < T; ++t) y[t] *= up;
 #pragma unroll
   for (int p = 0; p < PB; ++p) {
     h16x8 bh, bl;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v = x[2 * p + (j >> 2)][j & 3] * fx;
-      const _Float16 h = (_Float16)v;
-      bh[j] = h;
-      bl[j] = (_Float16)(v - (float)h);
-    }
+    split8(x[2 * p] * fx, x[2 * p + 1] * fx, bh, bl);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       // compiler-level fence: keeps the A reads from being hoisted ahead of the operand split
@@ -368,6 +454,38 @@ __device__ __forceinline__ void gemm_h2(const _Float16* __restrict__ hW, int sw,
   for (int t = 0; t < T; ++t) y[t] *= down;
 }
 
+// HF forward product with static scales (r05): y (the accumulators, initialised with the bias
+// pre-scaled to 2^(ex + sw): V_B2S / V_B3S) += W_c x at scale 2^(ex + sw), and it STAYS at that
+// scale: the LayerNorm that follows folds 2^-(ex + sw) into its 1/std (ln_rms), so there is no
+// scale-up / scale-down pass over the accumulators.  XS: x already carries 2^ex (relu: the
+// affine's pre-scaled vectors); otherwise (silu) it is scaled here.  Planes, operands and MFMA
+// order are gemm_h2's: bitwise the r04 products.
+template <int D, bool XS>
+__device__ __forceinline__ void gemm_h2s(const _Float16* __restrict__ hW, int ex,
+                                         const f32x4 (&x)[D / 16], f32x4 (&y)[D / 16], int i,
+                                         int g) {
+  using H = HCfg<D>;
+  constexpr int T = D / 16, PB = D / 32;
+  const float fx = ldexpf(1.f, ex);
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    h16x8 bh, bl;
+    if constexpr (XS) split8(x[2 * p], x[2 * p + 1], bh, bl);
+    else split8(x[2 * p] * fx, x[2 * p + 1] * fx, bh, bl);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if (t % HF_TILES_PER_FENCE == 0) asm volatile("" ::: "memory");
+      const _Float16* row = hW + (16 * t + i) * H::LDH + 32 * p + 8 * g;
+      const h16x8 ah = *reinterpret_cast<const h16x8*>(row);
+      const h16x8 al = *reinterpret_cast<const h16x8*>(row + H::PLANE);
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, y[t], 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
+      y[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
+      if (t % HF_TILES_PER_FENCE == HF_TILES_PER_FENCE - 1) GMP_GEMM_FENCE();
+    }
+  }
+}
+
 // HF, the FORWARD product y[slot(o)] += sum_k W[o][k] x[slot(k)] read from the TRANSPOSED planes
 // (rows k, columns hf_pos(o): the backward's LDS image) with ds_read_b64_tr_b16.  Per 16-lane
 // group g and k block p, two transposed reads per plane (lane 4q + c of the group supplies row
@@ -383,27 +501,19 @@ __device__ __forceinline__ h16x4 lds_tr16(const _Float16* p) {
   return __builtin_bit_cast(h16x4, v);
 }
 
-template <int D>
-__device__ __forceinline__ void gemm_h2_tr(const _Float16* __restrict__ hWt, int sw, int sx,
-                                           const f32x4 (&x)[D / 16], f32x4 (&y)[D / 16],
-                                           int lane, int g) {
+template <int D, bool XS>
+__device__ __forceinline__ void gemm_h2s_tr(const _Float16* __restrict__ hWt, int ex,
+                                            const f32x4 (&x)[D / 16], f32x4 (&y)[D / 16],
+                                            int lane, int g) {
   using H = HCfg<D>;
   constexpr int T = D / 16, PB = D / 32;
-  sx = sx < -100 - sw ? -100 - sw : (sx > 100 - sw ? 100 - sw : sx);
-  const float fx = ldexpf(1.f, sx), up = ldexpf(1.f, sx + sw), down = ldexpf(1.f, -(sx + sw));
+  const float fx = ldexpf(1.f, ex);
   const int q = (lane & 15) >> 2, c = lane & 3;
-#pragma unroll
-  for (int t = 0; t < T; ++t) y[t] *= up;
 #pragma unroll
   for (int p = 0; p < PB; ++p) {
     h16x8 bh, bl;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v = x[2 * p + (j >> 2)][j & 3] * fx;
-      const _Float16 h = (_Float16)v;
-      bh[j] = h;
-      bl[j] = (_Float16)(v - (float)h);
-    }
+    if constexpr (XS) split8(x[2 * p], x[2 * p + 1], bh, bl);
+    else split8(x[2 * p] * fx, x[2 * p + 1] * fx, bh, bl);
     const _Float16* rowk = hWt + (32 * p + 4 * g + q) * H::LDH + 8 * c;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -420,8 +530,6 @@ __device__ __forceinline__ void gemm_h2_tr(const _Float16* __restrict__ hWt, int
       if (t % HF_TILES_PER_FENCE == HF_TILES_PER_FENCE - 1) GMP_GEMM_FENCE();
     }
   }
-#pragma unroll
-  for (int t = 0; t < T; ++t) y[t] *= down;
 }
 
 // y[slot(k)] += sum_o W[o][k] gin[slot(o)]   (transposed product for the backward)
@@ -476,7 +584,7 @@ __device__ __forceinline__ float sum_groups(float v) {
 // ---------------------------------------------------------------------------------- LayerNorm
 
 // in place: x <- (x - mean) * rstd  (x_hat); returns rstd.  Two-pass statistics.
-template <int D>
+template <int D, bool RSQ = false>
 __device__ __forceinline__ float ln_normalize(f32x4 (&x)[D / 16], float eps) {
   constexpr int T = D / 16;
   float s = 0.f;
@@ -489,7 +597,8 @@ __device__ __forceinline__ float ln_normalize(f32x4 (&x)[D / 16], float eps) {
     x[p] -= mean;
     v += x[p][0] * x[p][0] + x[p][1] * x[p][1] + x[p][2] * x[p][2] + x[p][3] * x[p][3];
   }
-  const float rstd = 1.f / sqrtf(sum_groups(v) * (1.f / D) + eps);
+  const float var = sum_groups(v) * (1.f / D) + eps;
+  const float rstd = RSQ ? __builtin_amdgcn_rsqf(var) : 1.f / sqrtf(var);  // (RSQ: the HF path)
 #pragma unroll
   for (int p = 0; p < T; ++p) x[p] *= rstd;
   return rstd;
@@ -509,6 +618,23 @@ __device__ __forceinline__ void ln_recenter(f32x4 (&x)[D / 16], float rstd) {
     x[p] -= mean;
     x[p] *= rstd;
   }
+}
+
+// HF path (r05): the LayerNorm of a centred product's output y_s = 2^k y (zero mean by
+// construction, load_params_hf): x_hat = y rstd, rstd = 1 / sqrt(mean(y^2) + eps), with the
+// scale 2^-k folded into the multiplier (x_hat = y_s (rstd 2^-k): the same rounding as y rstd).
+// No mean pass, no scale-down pass.  rstd by v_rsq_f32.  Returns rstd (saved for the backward).
+template <int D>
+__device__ __forceinline__ float ln_rms(f32x4 (&x)[D / 16], float eps, int k) {
+  constexpr int T = D / 16;
+  float v = 0.f;
+#pragma unroll
+  for (int p = 0; p < T; ++p) v += x[p][0] * x[p][0] + x[p][1] * x[p][1] + x[p][2] * x[p][2] + x[p][3] * x[p][3];
+  const float rstd = __builtin_amdgcn_rsqf(ldexpf(sum_groups(v), -2 * k) * (1.f / D) + eps);
+  const float r = ldexpf(rstd, -k);
+#pragma unroll
+  for (int p = 0; p < T; ++p) x[p] *= r;
+  return rstd;
 }
 
 // dpre = rstd * (gr - mean(gr) - xhat * mean(gr * xhat)), gr = dL/dxhat ; in place on gr
@@ -784,15 +910,17 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
   const _Float16* hW3 = hW + HCfg<D>::MAT;
   float* sVw = smem + smem_vec_off<D, fwd_waves<HF>(), HF>();
   const float* sV = sVw;
-  if constexpr (HF) load_params_hf<D, false>(sVw, hW, P);
+  float* carry0 = smem + smem_carry_off<D, fwd_waves<HF>(), HF>();
+  if constexpr (HF) load_params_hf<D, false, 3, ACT>(sVw, hW, carry0, P);
   else load_params_to_lds<D>(smem, P);
   __syncthreads();
   const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
-  const int sx2 = HF ? (int)sV[NV * D + 2] : 0, sx3 = HF ? (int)sV[NV * D + 3] : 0;
+  const int ex2 = HF ? (int)sV[NV * D + 2] : 0, ex3 = HF ? (int)sV[NV * D + 3] : 0;
+  constexpr bool XS = ACT == GMP_ACT_RELU;  // relu: y1 comes pre-scaled for the W2 product
 
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* cbuf = smem + smem_carry_off<D, fwd_waves<HF>(), HF>() + (wid * 4 + g) * carry_stride<D>();
+  float* cbuf = carry0 + (wid * 4 + g) * carry_stride<D>();
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, fwd_waves<HF>());
   const float b4 = P.b4[0];
   int carry_node = -1;
@@ -810,28 +938,40 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     const size_t ED = (size_t)n_edges * D;
     f32x4 x[T];  // y1 = act(LN1(pre1))
     load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);
-    const float r1 = ln_normalize<D>(x, eps);
+    const float r1 = ln_normalize<D, HF>(x, eps);
     // chunk windows: edges [base, base + ne) of the saved tensors, receivers [i0, i1]
     const int ne = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
     const int i0 = __builtin_amdgcn_readfirstlane(c.i);
     const int i1 = __builtin_amdgcn_readlane(c.i, 15);
     const unsigned eoff = c.valid ? (unsigned)(li * D * 4) : kOob;
     if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave, base, ne, D), eoff, x, g);
-    affine_act<D, ACT>(x, sV, V_LN1W, V_LN1B, g);
+    affine_act<D, ACT>(x, sV, HF ? V_LN1WS : V_LN1W, HF ? V_LN1BS : V_LN1B, g);
 
     f32x4 m[T];  // m = act(LN2(W2 y1 + b2))
-    load_vec<D>(m, sV, V_B2, g);
-    if constexpr (HF) gemm_h2<D, false>(hW2, sw2, sx2, x, m, li, g);
-    else gemm_wx<D>(sW2, x, m, li, g);
-    const float r2 = ln_normalize<D>(m, eps);
+    float r2;
+    if constexpr (HF) {
+      load_vec<D>(m, sV, V_B2S, g);
+      gemm_h2s<D, XS>(hW2, ex2, x, m, li, g);
+      r2 = ln_rms<D>(m, eps, ex2 + sw2);
+    } else {
+      load_vec<D>(m, sV, V_B2, g);
+      gemm_wx<D>(sW2, x, m, li, g);
+      r2 = ln_normalize<D, false>(m, eps);
+    }
     if (SAVE) store_row_w<D, kAuxNT>(rows_window(xsave + ED, base, ne, D), eoff, m, g);
-    affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);
+    affine_act<D, ACT>(m, sV, V_LN2W, V_LN2B, g);  // (unscaled: m is also the message)
 
     // y3 = act(LN3(W3 m + b3)); s = w4 . y3 + b4   (x reused)
-    load_vec<D>(x, sV, V_B3, g);
-    if constexpr (HF) gemm_h2<D, false>(hW3, sw3, sx3, m, x, li, g);
-    else gemm_wx<D>(sW3, m, x, li, g);
-    const float r3 = ln_normalize<D>(x, eps);
+    float r3;
+    if constexpr (HF) {
+      load_vec<D>(x, sV, V_B3S, g);
+      gemm_h2s<D, false>(hW3, ex3, m, x, li, g);
+      r3 = ln_rms<D>(x, eps, ex3 + sw3);
+    } else {
+      load_vec<D>(x, sV, V_B3, g);
+      gemm_wx<D>(sW3, m, x, li, g);
+      r3 = ln_normalize<D, false>(x, eps);
+    }
     if (SAVE) {
       if (save_planes == 3)
         store_row_w<D, kAuxNT>(rows_window(xsave + 2 * ED, base, ne, D), eoff, x, g);
@@ -933,11 +1073,13 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   const _Float16* hW3t = hW + HCfg<D>::MAT;
   float* sVw = smem + smem_vec_off<D, kBwdWaves, HF>();
   const float* sV = sVw;
-  if constexpr (HF) load_params_hf<D, true>(sVw, hW, P);
+  // (HF: W3^T centred as the forward's W3, so the x_hat3 recompute is bitwise the forward's; W2 as
+  // given)
+  if constexpr (HF) load_params_hf<D, true, 2, ACT>(sVw, hW, smem + smem_carry_off<D, kBwdWaves, HF>(), P);
   else load_params_to_lds<D, true>(smem, P);
   __syncthreads();
   const int sw2 = HF ? (int)sV[NV * D] : 0, sw3 = HF ? (int)sV[NV * D + 1] : 0;
-  const int sx3 = HF ? (int)sV[NV * D + 3] : 0;  // the forward's static W3 input exponent
+  const int ex3 = HF ? (int)sV[NV * D + 3] : 0;  // the forward's static W3 input exponent
   const float* xr1 = xsave;
   const float* xr2 = xsave + (size_t)n_edges * D;
   // AMAX: per-chunk wave maxima go to two LDS words (no loop-carried registers: the kernel sits
@@ -989,11 +1131,19 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     if constexpr (RC == 1) {
       // z = xhat3 = LN3(W3 act(LN2 affine(xhat2)) + b3) with the forward's 1/std: the forward's
       // products (same operands, planes, scales and MFMA order) -> bitwise its x_hat3
-      affine_act<D, ACT>(x, sV, V_LN2W, V_LN2B, g);
-      load_vec<D>(z, sV, V_B3, g);
-      if constexpr (HF) gemm_h2_tr<D>(hW3t, sw3, sx3, x, z, lane, g);
-      else gemm_wtx<D>(sW3t, x, z, li, g);
-      ln_recenter<D>(z, rs3);
+      if constexpr (HF) {
+        affine_act<D, ACT>(x, sV, V_LN2W, V_LN2B, g);
+        load_vec<D>(z, sV, V_B3S, g);
+        gemm_h2s_tr<D, false>(hW3t, ex3, x, z, lane, g);
+        const float r = ldexpf(rs3, -(ex3 + sw3));  // ln_rms's multiplier
+#pragma unroll
+        for (int p = 0; p < T; ++p) z[p] *= r;
+      } else {
+        affine_act<D, ACT>(x, sV, V_LN2W, V_LN2B, g);
+        load_vec<D>(z, sV, V_B3, g);
+        gemm_wtx<D>(sW3t, x, z, li, g);
+        ln_recenter<D>(z, rs3);
+      }
     }
 
   // ---------------- pos-branch backward

@@ -24,54 +24,6 @@ int device_cu_count() {
   return cus;
 }
 
-// Completion tickets of the kernels that end in a last-workgroup reduction: one zeroed word per
-// (device, stream), allocated on first use (kernels on one stream run in order, and the last
-// workgroup resets its ticket, so a word serves every later launch on that stream).
-unsigned* stream_ticket(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, unsigned*> slots;
-  static std::map<int, std::pair<unsigned*, int>> pools;  // device -> (64 words, next free)
-  constexpr int kSlots = 64;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = slots.find({dev, s});
-  if (it != slots.end()) return it->second;
-  auto& pool = pools[dev];
-  if (!pool.first) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-      return nullptr;  // no allocation inside a capture: the caller uses its two-kernel form
-    unsigned* p = nullptr;
-    if (hipMalloc(&p, kSlots * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, kSlots * sizeof(unsigned)) != hipSuccess) return nullptr;
-    pool = {p, 0};
-  }
-  if (pool.second >= kSlots) return nullptr;
-  unsigned* t = pool.first + pool.second++;
-  slots[{dev, s}] = t;
-  return t;
-}
-
-unsigned* stream_ticket_block(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, unsigned*> blocks;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = blocks.find({dev, s});
-  if (it != blocks.end()) return it->second;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-    return nullptr;
-  if (blocks.size() >= 64) return nullptr;
-  unsigned* p = nullptr;
-  if (hipMalloc(&p, kTicketWords * sizeof(unsigned)) != hipSuccess) return nullptr;
-  if (hipMemset(p, 0, kTicketWords * sizeof(unsigned)) != hipSuccess) return nullptr;
-  blocks[{dev, s}] = p;
-  return p;
-}
-
 namespace {
 
 constexpr size_t kAlign = 256;

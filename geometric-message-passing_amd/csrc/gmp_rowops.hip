@@ -124,10 +124,8 @@ template <int ACT>
 __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
     int64_t rows, int d, const float* __restrict__ gy, const float* __restrict__ xhat,
     const float* __restrict__ rstd_in, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials,
-    float* __restrict__ out_gb, unsigned* __restrict__ ticket) {
+    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials) {
   __shared__ float red[kRowT / 64][2 * 512];
-  __shared__ unsigned is_last;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float dg[kMaxF], db[kMaxF];
 #pragma unroll
@@ -195,45 +193,19 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_kernel(
     for (int w = 0; w < kRowT / 64; ++w) s += red[w][off];
     partials[(int64_t)blockIdx.x * 2 * d + f] = s;
   }
-  if (!out_gb) return;
-  // last-workgroup reduction (threadfence pattern): every workgroup publishes its partial row,
-  // takes a ticket; the last one adds the rows in workgroup order (deterministic) and resets
-  // the ticket for the next launch on this stream
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) is_last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (!is_last) return;
-  __threadfence();
-  const int G = (int)gridDim.x;
-  for (int f = threadIdx.x; f < 2 * d; f += kRowT) {
-    float s = 0.f;
-    for (int g0 = 0; g0 < G; g0 += 16) {
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = g0 + u < G ? partials[(int64_t)(g0 + u) * 2 * d + f] : 0.f;
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (g0 + u < G) s += v[u];
-    }
-    out_gb[f] = s;
-  }
-  if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
 // r04 form for d = 64 F (F = 1, 2, 4): lane l holds the F consecutive features F l .. F l + F - 1
 // of a row (one 4F-byte load per lane and tensor), each wave takes kRB4 rows per iteration (their
 // loads issued together) over a short grid-stride loop; the grid is sized to give every SIMD
 // several waves (r03's 256-workgroup grid ran one wave per SIMD through ~25 dependent rounds:
-// 70 us for 50k x 128).  [dgamma | dbeta] leaves through tree_finish (two-level last-workgroup
-// sums in fixed order) instead of a second kernel.
+// 70 us for 50k x 128).  [dgamma | dbeta]: one partial row per workgroup (sum_rows_kernel).
 constexpr int kRB4 = 4;
 template <int ACT, int F>
 __global__ __launch_bounds__(kRowT) void ln_act_bwd_vec_kernel(
     int64_t rows, const float* __restrict__ gy, const float* __restrict__ xhat,
     const float* __restrict__ rstd_in, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials,
-    float* __restrict__ grows, float* __restrict__ out_gb, unsigned* __restrict__ tickets) {
+    const float* __restrict__ beta, float* __restrict__ gx, float* __restrict__ partials) {
   constexpr int D = 64 * F;
   typedef float fv __attribute__((ext_vector_type(F)));
   __shared__ float red[kRowT / 64][2 * D];
@@ -287,7 +259,6 @@ __global__ __launch_bounds__(kRowT) void ln_act_bwd_vec_kernel(
     for (int w = 0; w < kRowT / 64; ++w) sacc += red[w][f];
     partials[(int64_t)blockIdx.x * 2 * D + f] = sacc;
   }
-  if (out_gb) tree_finish(partials, grows, (int)gridDim.x, 2 * D, out_gb, tickets);
 }
 
 // r04 form for narrow rows, D = 8, 16, 32 (GVP's edge-scalar LayerNorm: 1M rows of 32): a wave
@@ -389,19 +360,10 @@ __global__ __launch_bounds__(kSC * kSG) void sum_rows_kernel(const float* __rest
   }
 }
 
-// [dgamma | dbeta] inside the backward kernel (last workgroup) with GMP_LN_FUSED_SUM=1; off by
-// default: measured 99.1 vs 101.0-101.6 M EGNN edges/s (the last workgroup sums 256 rows alone)
-int g_ln_fused_sum = getenv("GMP_LN_FUSED_SUM") ? atoi(getenv("GMP_LN_FUSED_SUM")) : 0;
-// GMP_LN_TREE=1: the vectorised kernel finishes [dgamma | dbeta] itself (tree_finish); measured
-// slower on the EGNN step (96 vs 102 M edges/s: every workgroup's __threadfence writes back L2)
-int g_ln_tree = getenv("GMP_LN_TREE") ? atoi(getenv("GMP_LN_TREE")) : 0;
-// GMP_LN_R03=1: the r03 one-wave-per-SIMD kernel + separate column sum (A/B)
-int g_ln_r03 = getenv("GMP_LN_R03") ? atoi(getenv("GMP_LN_R03")) : 0;
-// backward grid cap (GMP_LN_BWD_BLOCKS; A/B)
-int g_ln_blocks = getenv("GMP_LN_BWD_BLOCKS") ? atoi(getenv("GMP_LN_BWD_BLOCKS")) : kRowBlocks;
+// generic backward grid: at most kRowBlocks workgroups (one partial row each)
 int bwd_blocks(int64_t rows) {
   const int64_t b = ceil_div(rows, kRowT / 64);
-  return (int)(b < g_ln_blocks ? (b < 1 ? 1 : b) : g_ln_blocks);
+  return (int)(b < kRowBlocks ? (b < 1 ? 1 : b) : kRowBlocks);
 }
 
 // GVP vector LayerNorm (gvp_layer.py:232-243 with the clamp of _norm_no_nan, :66-73): rows of C
@@ -505,9 +467,7 @@ __global__ __launch_bounds__(kRowT) void xyz_norm_kernel(int64_t n, int h,
   }
 }
 
-// GMP_LN_SMALL=0: narrow rows on the generic kernels (A/B)
-int g_ln_small = getenv("GMP_LN_SMALL") ? atoi(getenv("GMP_LN_SMALL")) : 1;
-bool small_form(int64_t d) { return g_ln_small && (d == 8 || d == 16 || d == 32); }
+bool small_form(int64_t d) { return d == 8 || d == 16 || d == 32; }
 
 }  // namespace
 }  // namespace gmp
@@ -549,11 +509,13 @@ int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gam
 
 bool vec_form(int64_t d) { return d == 64 || d == 128 || d == 256; }
 
+// The backward's partial rows: the narrow / vectorised kernels (with grad_gamma_beta) write
+// vec_blocks(rows) rows, the generic kernel (every other case, and grad_gamma_beta == NULL: the
+// caller-reduces form) bwd_blocks(rows).  The workspace covers whichever runs (the
+// r04 size was the vectorised count alone, which the generic fallback overran below ~16k rows).
 size_t gmp_ln_act_bwd_workspace_size(int64_t rows, int64_t d) {
-  if (small_form(d)) return (size_t)vec_blocks(rows) * 2 * (size_t)d * sizeof(float);
-  if (vec_form(d))  // partial rows + the tree_finish group rows
-    return (size_t)(vec_blocks(rows) + kTicketWords) * 2 * (size_t)d * sizeof(float);
-  return (size_t)bwd_blocks(rows) * 2 * (size_t)d * sizeof(float);
+  const int64_t v = vec_blocks(rows), b = bwd_blocks(rows);
+  return (size_t)(v > b ? v : b) * 2 * (size_t)d * sizeof(float);
 }
 
 int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float* xhat,
@@ -575,57 +537,41 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
   const uintptr_t al = reinterpret_cast<uintptr_t>(grad_y) | reinterpret_cast<uintptr_t>(xhat) |
                        reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
                        reinterpret_cast<uintptr_t>(grad_x);
-  if (small_form(d) && grad_gamma_beta && !g_ln_r03) {
-    const int GV = vec_blocks(rows);
-#define GMP_LNS(A, D) \
-  ln_act_bwd_small_kernel<A, D><<<GV, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, beta, grad_x, part)
+  int rows_written = G;  // partial rows for sum_rows_kernel
+  if (small_form(d) && grad_gamma_beta) {
+    rows_written = vec_blocks(rows);
+#define GMP_LNS(A, D)                                                                 \
+  ln_act_bwd_small_kernel<A, D><<<rows_written, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, \
+                                                               beta, grad_x, part)
 #define GMP_LNS_D(A) \
   if (d == 8) GMP_LNS(A, 8); else if (d == 16) GMP_LNS(A, 16); else GMP_LNS(A, 32)
     if (act == 0) { GMP_LNS_D(0); } else if (act == 1) { GMP_LNS_D(1); } else { GMP_LNS_D(2); }
 #undef GMP_LNS_D
 #undef GMP_LNS
-    int rc = launch_status();
-    if (rc) return rc;
-    sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, GV, (int)(2 * d),
-                                                                         grad_gamma_beta);
-    return launch_status();
-  }
-  if (vec_form(d) && grad_gamma_beta && !g_ln_r03 && al % (d / 16) == 0) {
-    // [dgamma | dbeta]: the two-level in-kernel finish (GMP_LN_TREE=1) or the column-sum kernel
-    unsigned* tk = g_ln_tree ? stream_ticket_block(s) : nullptr;
-    const int GV = vec_blocks(rows);
-    float* grows = part + (size_t)GV * 2 * d;
-    float* ogb = tk ? grad_gamma_beta : nullptr;
-#define GMP_LNV(A, F)                                                                        \
-  ln_act_bwd_vec_kernel<A, F><<<GV, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, beta,    \
-                                                   grad_x, part, grows, ogb, tk)
+  } else if (vec_form(d) && grad_gamma_beta && al % (d / 16) == 0) {
+    rows_written = vec_blocks(rows);
+#define GMP_LNV(A, F)                                                                \
+  ln_act_bwd_vec_kernel<A, F><<<rows_written, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, \
+                                                             beta, grad_x, part)
 #define GMP_LNV_F(A) \
   if (d == 64) GMP_LNV(A, 1); else if (d == 128) GMP_LNV(A, 2); else GMP_LNV(A, 4)
     if (act == 0) { GMP_LNV_F(0); } else if (act == 1) { GMP_LNV_F(1); } else { GMP_LNV_F(2); }
 #undef GMP_LNV_F
 #undef GMP_LNV
-    int rc = launch_status();
-    if (rc || tk) return rc;
-    sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, GV, (int)(2 * d),
-                                                                         grad_gamma_beta);
-    return launch_status();
-  }
-  // [dgamma | dbeta] by the kernel's last workgroup when a ticket is available (one launch);
-  // otherwise (or GMP_LN_FUSED_SUM=0) the partial rows go through sum_rows_kernel
-  unsigned* ticket = (grad_gamma_beta && g_ln_fused_sum) ? stream_ticket(s) : nullptr;
-  float* ogb = ticket ? grad_gamma_beta : nullptr;
-  if (act == 0)
+  } else if (act == 0) {
     ln_act_bwd_kernel<0><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
-                                             grad_x, part, ogb, ticket);
-  else if (act == 1)
+                                             grad_x, part);
+  } else if (act == 1) {
     ln_act_bwd_kernel<1><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
-                                             grad_x, part, ogb, ticket);
-  else
+                                             grad_x, part);
+  } else {
     ln_act_bwd_kernel<2><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
-                                             grad_x, part, ogb, ticket);
-  int rc = launch_status();
-  if (rc || !grad_gamma_beta || ticket) return rc;  // NULL: the caller reduces the partials
-  sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, G, (int)(2 * d),
+                                             grad_x, part);
+  }
+  const int rc = launch_status();
+  if (rc || !grad_gamma_beta) return rc;  // NULL: the caller reduces the G partial rows
+  sum_rows_kernel<<<(unsigned)ceil_div(2 * d, kSC), kSC * kSG, 0, s>>>(part, rows_written,
+                                                                       (int)(2 * d),
                                                                        grad_gamma_beta);
   return launch_status();
 }

@@ -190,8 +190,12 @@ class LayerNorm(nn.Module):
         if not self.v:
             return ops.ln_act(x, self.scalar_norm)  # K12 (act = identity)
         s, v = x
-        if VEC_NORM_FUSED and v.is_cuda and v.dtype == torch.float32 and 1 <= v.shape[-2] <= 64:
-            return ops.ln_act(s, self.scalar_norm), VecNormFn.apply(v)
+        if (VEC_NORM_FUSED and v.is_cuda and v.dtype == torch.float32 and v.dim() >= 2
+                and v.shape[-1] == 3 and 1 <= v.shape[-2] <= 64):
+            # (..., C, 3) inputs as (rows, C, 3) for the kernel (a batched input
+            # used to reach the op's 3-D check and raise)
+            vv = VecNormFn.apply(v.reshape(-1, v.shape[-2], 3)).view(v.shape)
+            return ops.ln_act(s, self.scalar_norm), vv
         vn = _norm_no_nan(v, axis=-1, keepdims=True, sqrt=False)
         vn = torch.sqrt(torch.mean(vn, dim=-2, keepdim=True))
         return ops.ln_act(s, self.scalar_norm), v / vn

@@ -8,16 +8,16 @@ device tensor), each owning one graph, through
 * DDP (gmp_amd/dist.wrap_ddp: deferral switched off so the reducer's per-parameter hooks see
   every gradient through autograd, find_unused_parameters for the readout slices).
 
-The first step's averaged gradients must equal those of a single process that averages the
-gradients of the same two graphs (rank 0 computes that reference in its own process after the
-collective part), within 1e-5 of each gradient's scale (measured: bitwise equal — the
-all-reduce sums two per-rank gradients exactly as the single process accumulates them; scaling
-by 1/2 is exact).  Parameters after two Adam steps: bitwise equal for the executor; under DDP
-the second step's gradients were measured to differ in the last bits (max 3e-7 on the
-parameters), which Adam's per-coordinate normalisation amplifies where a gradient coordinate
-is near zero (one of 32,896 entries: 1.4e-5 after two lr = 1e-2 steps; at C5's widths 1.1e-4) —
-the DDP parameter check therefore allows 5e-4 absolute (5 % of one Adam step) and requires all
-but 0.1 % of the coordinates to agree to 1e-5.
+The averaged gradients of BOTH steps (what the collective delivered to the optimizer, read
+before Adam uses them) must equal those of a single process that averages the gradients of the
+same two graphs (rank 0 computes that reference in its own process after the collective part),
+within 1e-5 of each gradient's scale (step 1 measured bitwise equal — the all-reduce sums two
+per-rank gradients exactly as the single process accumulates them; scaling by 1/2 is exact;
+step 2 starts from parameters equal to 1e-6).  Parameters after one Adam step: 1e-6; after two:
+1e-5 for the executor.  (the r04 DDP check compared post-Adam parameters, where
+Adam's per-coordinate normalisation amplifies last-bit gradient differences at near-zero
+coordinates, with a near-vacuous bound; the gradients are the quantity the data-parallel path
+must get right.)
 Multi-GPU scaling itself is unmeasured on hardware here (the driver owns 8-GPU runs)."""
 import os
 import socket
@@ -90,9 +90,12 @@ def _rank_worker(rank, world, port, out_dir, kind, mode):
         for it in range(2):
             opt.zero_grad(set_to_none=True)
             _loss(model, b, y).backward()
+            gr = {k: p.grad.detach().cpu() for k, p in model.module.named_parameters()
+                  if p.grad is not None}
             if it == 0:
-                grads = {k: p.grad.detach().cpu() for k, p in model.module.named_parameters()
-                         if p.grad is not None}
+                grads = gr
+            else:
+                grads2 = gr
             opt.step()
             if it == 0:
                 params1 = {k: p.detach().cpu() for k, p in model.module.named_parameters()}
@@ -109,14 +112,18 @@ def _rank_worker(rank, world, port, out_dir, kind, mode):
         step = GraphedStep(model, lambda: _loss(model, b, y), opt, warmup=0, use_graph=False)
         for it in range(2):
             step()
+            torch.cuda.synchronize()
+            # p.grad after the step holds the all-reduced gradient Adam consumed
+            gr = {k: p.grad.detach().cpu() for k, p in model.named_parameters()
+                  if p.grad is not None}
             if it == 0:
-                torch.cuda.synchronize()
-                grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()
-                         if p.grad is not None}
+                grads = gr
                 params1 = {k: p.detach().cpu() for k, p in model.named_parameters()}
+            else:
+                grads2 = gr
         torch.cuda.synchronize()
         params = {k: p.detach().cpu() for k, p in model.named_parameters()}
-    torch.save({"params": params, "params1": params1, "grads": grads},
+    torch.save({"params": params, "params1": params1, "grads": grads, "grads2": grads2},
                os.path.join(out_dir, f"{mode}{rank}.pt"))
     torch.distributed.destroy_process_group()
     if rank == 0:
@@ -132,16 +139,20 @@ def _rank_worker(rank, world, port, out_dir, kind, mode):
             for p in ref.parameters():  # the executor all-reduces zeros for unused parameters
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
+            torch.cuda.synchronize()
+            gr = {k: p.grad.detach().cpu() for k, p in ref.named_parameters()}
             if it == 0:
-                torch.cuda.synchronize()
-                grads = {k: p.grad.detach().cpu() for k, p in ref.named_parameters()}
+                grads = gr
+            else:
+                grads2 = gr
             opt.step()
             if it == 0:
                 torch.cuda.synchronize()
                 params1 = {k: p.detach().cpu() for k, p in ref.named_parameters()}
         torch.cuda.synchronize()
         torch.save({"params": {k: p.detach().cpu() for k, p in ref.named_parameters()},
-                    "params1": params1, "grads": grads}, os.path.join(out_dir, f"{mode}_ref.pt"))
+                    "params1": params1, "grads": grads, "grads2": grads2},
+                   os.path.join(out_dir, f"{mode}_ref.pt"))
 
 
 @pytest.mark.timeout(240)
@@ -155,50 +166,28 @@ def test_product_world2_gloo_on_gpu_matches_single_process(kind, mode):
         res = [torch.load(os.path.join(d, f"{mode}{r}.pt"), weights_only=True)
                for r in range(world)]
         ref = torch.load(os.path.join(d, f"{mode}_ref.pt"), weights_only=True)
-    # the first step's averaged gradients (what the collective delivered to the optimizer)
+    # both steps' averaged gradients (what the collective delivered to the optimizer)
     bad = []
-    for k, g in ref["grads"].items():
-        for r in range(world):
-            got = res[r]["grads"].get(k, torch.zeros_like(g))
-            err, scale = (got - g).abs().max().item(), g.abs().max().item()
-            print(f"grad {k} rank {r}: max|d| {err:.3e} scale {scale:.3e}")
-            if err > 1e-5 * scale + 1e-7:
-                bad.append((k, r, err, scale))
+    for step_key in ("grads", "grads2"):
+        for k, g in ref[step_key].items():
+            for r in range(world):
+                got = res[r][step_key].get(k, torch.zeros_like(g))
+                err, scale = (got - g).abs().max().item(), g.abs().max().item()
+                print(f"{step_key} {k} rank {r}: max|d| {err:.3e} scale {scale:.3e}")
+                if err > 1e-5 * scale + 1e-7:
+                    bad.append((step_key, k, r, err, scale))
     assert not bad, bad
-    # parameters after ONE optimizer step: the first step's averaged gradients are equal (above),
-    # so the executor and DDP must both reproduce the single-process parameters to 1e-6 (the
-    # real bound of the data-parallel path; the two-step check below is only a fraction test
-    # for DDP)
+    # parameters after ONE optimizer step (equal first-step gradients): 1e-6
     for k, p in ref["params1"].items():
         for r in range(world):
             err = (res[r]["params1"][k] - p).abs().max().item()
             assert err <= 1e-6, ("after one step", k, r, err)
     moved = 0
-    n_off = [0] * world  # DDP: coordinates off by more than f32 closeness, over all parameters
-    n_all = 0
     for k, p in ref["params"].items():
-        n_all += p.numel()
-        for r in range(world):
-            got = res[r]["params"][k]
-            err = (got - p).abs().max().item()
-            print(f"param {k} rank {r}: max|d| {err:.3e}")
-            if mode == "ddp":
-                # DDP's bucketed all-reduce reorders the second step's sums (last-bit gradient
-                # differences); Adam's m / sqrt(v) is scale-free, so at a coordinate whose
-                # gradient is near zero those last bits can move the update by up to ~lr per
-                # step (C5 widths, r03: 2.7e-3 at one of 5.2M weights).  Bound: Adam's own
-                # update bound (2 steps x 2 lr) anywhere, and f32-close on all but a sliver of
-                # the coordinates (counted over the whole model: a per-tensor fraction fails on
-                # one coordinate of a 256-element bias, seen once in r04)
-                d = (got - p).abs()
-                assert err <= 4e-2, (k, r, err)
-                n_off[r] += int((d > 1e-5 + 1e-5 * p.abs()).sum().item())
-            else:
-                torch.testing.assert_close(got, p, atol=1e-5, rtol=1e-5)
+        if mode != "ddp":  # the executor sums in the single process's order: 1e-5 after two steps
+            for r in range(world):
+                torch.testing.assert_close(res[r]["params"][k], p, atol=1e-5, rtol=1e-5)
         moved += int(not torch.equal(p, _init_cpu(kind)[k]))
-    if mode == "ddp":
-        for r in range(world):
-            assert n_off[r] < 1e-3 * n_all, (r, n_off[r], n_all)
     assert moved > len(ref["params"]) // 2  # the steps really trained (not vacuous)
 
 

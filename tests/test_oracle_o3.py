@@ -83,6 +83,12 @@ def test_sh_l45_norm_equivariance_and_recursion(l):
     e = torch.zeros(2 * l + 1, dtype=torch.float64)
     e[l] = math.sqrt(2 * l + 1)  # e3nn: the m = 0 component along the polar (y) axis
     torch.testing.assert_close(yhat[l * l:].abs(), e, atol=1e-12, rtol=0)
+    # the SIGN too: e3nn's m = 0 component is proportional to the Legendre P_l(y),
+    # +sqrt(2l+1) along +y, at every l (its generated l <= 3 code: sh_1_1 = y, sh_2_2 =
+    # y^2 - (x^2 + z^2) / 2, sh_3_3 = 2/3 sqrt(3) sh_2_2 y - ...).  The l = 4, 5 blocks come from
+    # this oracle's wigner_3j recursion and stay parity-unpinned against e3nn's own output (no
+    # fixture covers l >= 4), but a flipped block sign would fail here.
+    torch.testing.assert_close(yhat[l * l:], e, atol=1e-12, rtol=0)
     torch.testing.assert_close(o3.spherical_harmonics(2.5 * v, l), Y)
     # the same recursion at l = 2, 3 gives the closed forms with a positive factor
     u = torch.nn.functional.normalize(v, dim=-1)
