@@ -771,17 +771,28 @@ __device__ __forceinline__ void carry_store(float* cbuf, const f32x4 (&x)[D / 16
   cbuf[D / 4 + 1] = p3[1];
   cbuf[D / 4 + 2] = p3[2];
 }
+// every lane reads its group's carry (one broadcast read) and adds take * carry: no select, no
+// divergent load.  The carry buffer is zeroed before the loop (carry_clear), so it always holds
+// finite values.  Lanes past the wave's range keep their (finite, clamped-edge) values: they
+// lie after every valid lane of the chunk, so no valid lane's scan reads them, and they never
+// store.
 template <int D>
 __device__ __forceinline__ void carry_apply(const float* cbuf, f32x4 (&x)[D / 16], float (&p3)[3],
-                                            bool valid, bool take) {
+                                            bool take) {
+  const float tf = take ? 1.f : 0.f;
 #pragma unroll
   for (int p = 0; p < D / 16; ++p) {
-    f32x4 c = {0.f, 0.f, 0.f, 0.f};
-    if (take) c = *reinterpret_cast<const f32x4*>(cbuf + 4 * p);
-    x[p] = valid ? x[p] + c : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 c = *reinterpret_cast<const f32x4*>(cbuf + 4 * p);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[p][q] = __builtin_fmaf(c[q], tf, x[p][q]);
   }
 #pragma unroll
-  for (int c = 0; c < 3; ++c) p3[c] = valid ? p3[c] + (take ? cbuf[D / 4 + c] : 0.f) : 0.f;
+  for (int c = 0; c < 3; ++c) p3[c] = __builtin_fmaf(cbuf[D / 4 + c], tf, p3[c]);
+}
+// zero this wave's four group carries (before the loop)
+template <int D>
+__device__ __forceinline__ void carry_clear(float* wave_cbuf, int lane) {
+  for (int k = lane; k < 4 * carry_stride<D>(); k += 64) wave_cbuf[k] = 0.f;
 }
 
 struct EdgeCtx {
@@ -836,18 +847,22 @@ __device__ __forceinline__ EdgeCtx edge_ctx(EdgeIJ ij, int base, int lane_e, int
   c.pjz = pos[3 * c.j + 2];
   return c;
 }
-// rel = pos_i - pos_j (egnn_layer.py:64), dist = |rel|: called once the chunk's loads are issued
+// rel = pos_i - pos_j (egnn_layer.py:64), dist = |rel|: called once the chunk's loads are issued.
+// FAST (the HF path, forward and backward alike): v_sqrt_f32 (~1 ulp) instead of the correctly
+// rounded sequence.
+template <bool FAST = false>
 __device__ __forceinline__ void edge_geom(EdgeCtx& c) {
   c.rx -= c.pjx;
   c.ry -= c.pjy;
   c.rz -= c.pjz;
-  c.dist = sqrtf(c.rx * c.rx + c.ry * c.ry + c.rz * c.rz);
+  const float q = c.rx * c.rx + c.ry * c.ry + c.rz * c.rz;
+  c.dist = FAST ? __builtin_amdgcn_sqrtf(q) : sqrtf(q);
 }
 
 // first pre-activation AB[i,:d] + AB[j,d:] + w1d*dist + b1.  All 2*d/4 row loads are issued
 // back to back (one round trip) before any is consumed; the scheduler would otherwise batch
 // them four at a time with a full wait between batches.
-template <int D, class Ctx>
+template <int D, bool FAST, class Ctx>
 __device__ __forceinline__ void load_pre1(f32x4 (&x)[D / 16], const float* arow, const float* brow,
                                           const float* sV, Ctx& c, int g) {
   f32x4 b[D / 16];
@@ -857,7 +872,7 @@ __device__ __forceinline__ void load_pre1(f32x4 (&x)[D / 16], const float* arow,
     b[p] = *reinterpret_cast<const f32x4*>(brow + 16 * p + 4 * g);
   }
   __builtin_amdgcn_sched_barrier(0);
-  edge_geom(c);
+  edge_geom<FAST>(c);
   const float dist = c.dist;
 #pragma unroll
   for (int p = 0; p < D / 16; ++p)
@@ -921,6 +936,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* cbuf = carry0 + (wid * 4 + g) * carry_stride<D>();
+  carry_clear<D>(carry0 + wid * 4 * carry_stride<D>(), lane);
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, fwd_waves<HF>());
   const float b4 = P.b4[0];
   int carry_node = -1;
@@ -937,7 +953,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
 
     const size_t ED = (size_t)n_edges * D;
     f32x4 x[T];  // y1 = act(LN1(pre1))
-    load_pre1<D>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);
+    load_pre1<D, HF>(x, rowp(AB, c.i, 2 * D), rowp(AB, c.j, 2 * D) + D, sV, c, g);
     const float r1 = ln_normalize<D, HF>(x, eps);
     // chunk windows: edges [base, base + ne) of the saved tensors, receivers [i0, i1]
     const int ne = __builtin_amdgcn_readfirstlane(min(16, wr.e_hi - base));
@@ -992,7 +1008,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     const bool is_end = c.valid && (c.e == c.seg1 - 1);
     const bool take = (li == 0) && c.valid && (c.i == carry_node);
     float pv[3] = {c.rx * s_e, c.ry * s_e, c.rz * s_e};
-    carry_apply<D>(cbuf, m, pv, c.valid, take);
+    carry_apply<D>(cbuf, m, pv, take);
     seg_scan<T>(m, li, head);
     {
       f32x4 pw[1] = {{pv[0], pv[1], pv[2], 0.f}};
@@ -1001,8 +1017,10 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
     }
     {  // receiver rows, stored by the last edge of each segment
       const float deg = (float)(c.seg1 - c.seg0);
+      // 1/deg: v_rcp_f32 (~1 ulp) on the HF path, the correctly rounded quotient on the f32 one
+      const float rdeg = HF ? __builtin_amdgcn_rcpf(deg) : 1.f / deg;
       if (MSG_MEAN) {  // only segment ends (an open segment's m is the next chunk's carry)
-        const float sc = is_end ? 1.f / deg : 1.f;
+        const float sc = is_end ? rdeg : 1.f;
 #pragma unroll
         for (int p = 0; p < T; ++p) m[p] *= sc;
       }
@@ -1010,8 +1028,9 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
       store_row_w<D, 0>(rows_window(m_aggr, i0, nn, D), is_end ? (unsigned)((c.i - i0) * D * 4) : kOob,
                         m, g);
       store3_w<0>(rows_window(pos_aggr, i0, nn, 3),
-                  (is_end && g == 0) ? (unsigned)((c.i - i0) * 12) : kOob, pv[0] / deg, pv[1] / deg,
-                  pv[2] / deg);
+                  (is_end && g == 0) ? (unsigned)((c.i - i0) * 12) : kOob,
+                  HF ? pv[0] * rdeg : pv[0] / deg, HF ? pv[1] * rdeg : pv[1] / deg,
+                  HF ? pv[2] * rdeg : pv[2] / deg);
     }
     if (li == 15) carry_store<D>(cbuf, m, pv);
     carry_node = __builtin_amdgcn_readlane(c.i, 15);
@@ -1093,6 +1112,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* cbuf = smem + smem_carry_off<D, kBwdWaves, HF>() + (wid * 4 + g) * carry_stride<D>();
+  carry_clear<D>(smem + smem_carry_off<D, kBwdWaves, HF>() + wid * 4 * carry_stride<D>(), lane);
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, kBwdWaves);
   const float b4 = P.b4[0];
   const size_t ED = (size_t)n_edges * D;
@@ -1124,7 +1144,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     if constexpr (RC == 1) load_row<D>(x, rowp(xsave + ED, c.ec, D), g);  // x = xhat2
     else load_row<D>(z, rowp(xsave + 2 * ED, c.ec, D), g);               // z = xhat3
     __builtin_amdgcn_sched_barrier(0);
-    edge_geom(c);
+    edge_geom<HF>(c);
     const float rstd1 = c.valid ? rs1 : 0.f;
     const float rstd2 = c.valid ? rs2 : 0.f;
     const float rstd3 = c.valid ? rs3 : 0.f;
@@ -1244,7 +1264,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
     const int head = c.valid ? (int)((c.seg0 > base) ? (c.seg0 - base) : 0) : li;
     const bool is_end = c.valid && (c.e == c.seg1 - 1);
     const bool take = (li == 0) && c.valid && (c.i == carry_node);
-    carry_apply<D>(cbuf, x, gd, c.valid, take);
+    carry_apply<D>(cbuf, x, gd, take);
     seg_scan<T>(x, li, head);
     {
       f32x4 pw[1] = {{gd[0], gd[1], gd[2], 0.f}};

@@ -74,7 +74,7 @@ class EGNNLayer(MessagePassing):
         m_aggr, p_aggr = ops.EgnnMessageFn.apply(
             h, pos, graph, self.activation_name, self.aggr == "mean", ln1.eps,
             m0.weight, m0.bias, ln1.weight, ln1.bias, m3.weight, m3.bias, ln2.weight, ln2.bias,
-            p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias)
+            p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias, torch.is_grad_enabled())
         return self._mlp_upd(h, m_aggr), pos + p_aggr
 
     def _mlp_upd(self, h, m_aggr):

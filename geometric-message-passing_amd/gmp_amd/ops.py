@@ -872,7 +872,7 @@ class EgnnMessageFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, pos, graph, act, msg_mean, eps, W1, b1, ln1w, ln1b, W2, b2, ln2w, ln2b,
-                W3, b3, ln3w, ln3b, w4, b4):
+                W3, b3, ln3w, ln3b, w4, b4, grad_mode=True):
         h, pos = _f32c(h), _f32c(pos)
         _need_cuda(h, pos, W1)
         N, d = h.shape
@@ -882,7 +882,11 @@ class EgnnMessageFn(torch.autograd.Function):
         AB = linear_x3(h, None, Wcat) if _x3_fits(2 * d, d) else h.mm(Wcat.t())
         params = tuple(_f32c(t) for t in (W1[:, 2 * d], b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3,
                                           b3, ln3w, ln3b, w4, b4))
-        train = any(ctx.needs_input_grad)
+        # save the LayerNorm outputs only for a backward: grad_mode is the CALLER's
+        # torch.is_grad_enabled() (forward() itself always runs with grad disabled, and
+        # needs_input_grad follows requires_grad alone: r04's inference forward saved 1 GB of
+        # x_hat planes per layer under torch.no_grad)
+        train = bool(grad_mode) and any(ctx.needs_input_grad)
         with _timed("egnn_edge_fwd"):
             m_aggr, pos_aggr, xhat, rstd = _lib.torch_ops().egnn_edge_fwd(
                 AB, pos, graph.rowptr, graph.recv, graph.send, list(params), _lib.ACT[act],
@@ -947,4 +951,4 @@ class EgnnMessageFn(torch.autograd.Function):
         # then b1 ... b4 (params[0] is the contiguous copy of W1's distance column)
         targets = (W1,) + tuple(params[1:])
         return (dh, dpos, None, None, None, None) + sw.deliver(ctx.needs_input_grad, 6, targets,
-                                                               grads, extra=(sw2,))
+                                                               grads, extra=(sw2,)) + (None,)
