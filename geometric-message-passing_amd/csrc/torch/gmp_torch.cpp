@@ -212,6 +212,77 @@ gmp_egnn_params egnn_params(const std::vector<Tensor>& p, int64_t d) {
   return P;
 }
 
+// K15 weight images (gmp_egnn_node_image_f32) of L layers: W0s[l] (d, 2d), W3s[l] (d, d), W1ns[l] the
+// next layer's mlp_msg.0.weight (d, >= 2d, unit column stride) or None.  -> uint8 (L, bytes).
+Tensor egnn_node_image(const std::vector<Tensor>& W0s, const std::vector<Tensor>& W3s,
+                       const std::vector<optional<Tensor>>& W1ns) {
+  TORCH_CHECK(!W0s.empty() && W3s.size() == W0s.size() && W1ns.size() == W0s.size(),
+              "gmp.egnn_node_image: one W0, W3 and W1n entry per layer");
+  OpGuard g(W0s[0], "egnn_node_image");
+  const int64_t L = (int64_t)W0s.size(), d = W0s[0].size(0);
+  std::vector<gmp_egnn_node_params> P(L);
+  for (int64_t l = 0; l < L; ++l) {
+    f32(W0s[l], "W0");
+    f32(W3s[l], "W3");
+    TORCH_CHECK(W0s[l].dim() == 2 && W0s[l].size(0) == d && W0s[l].size(1) == 2 * d &&
+                    W3s[l].dim() == 2 && W3s[l].size(0) == d && W3s[l].size(1) == d,
+                "gmp.egnn_node_image: W0 (d, 2d), W3 (d, d)");
+    P[l] = gmp_egnn_node_params{};
+    P[l].W0 = fp(W0s[l]);
+    P[l].W3 = fp(W3s[l]);
+    const optional<Tensor>& w1 = W1ns[l];
+    if (w1.has_value() && w1->defined()) {
+      TORCH_CHECK(w1->scalar_type() == at::kFloat && w1->dim() == 2 && w1->size(0) == d &&
+                      w1->size(1) >= 2 * d && w1->stride(1) == 1 && w1->stride(0) >= 2 * d &&
+                      w1->device() == W0s[0].device(),
+                  "gmp.egnn_node_image: W1n must be a (d, >= 2d) float32 matrix, unit column stride");
+      P[l].W1n = w1->data_ptr<float>();
+      P[l].ld1 = w1->stride(0);
+    }
+  }
+  const size_t bytes = gmp_egnn_node_image_bytes(d);
+  TORCH_CHECK(bytes > 0, "gmp.egnn_node_image: d must be 32, 64 or 128");
+  Tensor img = at::empty({L, (int64_t)bytes}, W0s[0].options().dtype(at::kByte));
+  check_rc(gmp_egnn_node_image_f32(d, L, P.data(), img.data_ptr(), cur_stream()),
+           "gmp_egnn_node_image_f32");
+  return img;
+}
+
+// K15 node update (gmp_egnn_node_fwd_f32): vecs = [b0, ln1_w, ln1_b, b3, ln2_w, ln2_b]; image =
+// this layer's row of egnn_node_image; with_ab: the image holds the next layer's W1n.
+// Returns (h_out (N, d), ab (N, 2d) or (0, 2d), xhat (2, N, d) or (0, N, d), rstd (2, N) or (0, N)).
+std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_node_fwd(
+    const Tensor& h, const Tensor& m_aggr, const std::vector<Tensor>& vecs, const Tensor& image,
+    bool with_ab, int64_t act, bool residual, double eps, bool train) {
+  OpGuard g(h, "egnn_node_fwd");
+  f32(h, "h");
+  f32(m_aggr, "m_aggr");
+  TORCH_CHECK(h.dim() == 2 && m_aggr.sizes() == h.sizes(), "gmp.egnn_node_fwd: h, m_aggr (N, d)");
+  const int64_t N = h.size(0), d = h.size(1);
+  TORCH_CHECK(vecs.size() == 6, "gmp.egnn_node_fwd: 6 parameter vectors expected");
+  for (int k = 0; k < 6; ++k) {
+    f32(vecs[k], "egnn_node parameter");
+    numel(vecs[k], d, "egnn_node parameter");
+  }
+  TORCH_CHECK(image.scalar_type() == at::kByte && image.is_contiguous() &&
+                  image.numel() == (int64_t)gmp_egnn_node_image_bytes(d) &&
+                  image.device() == h.device(),
+              "gmp.egnn_node_fwd: image must be one layer's row of egnn_node_image");
+  gmp_egnn_node_params P{};
+  P.b0 = fp(vecs[0]); P.ln1_w = fp(vecs[1]); P.ln1_b = fp(vecs[2]);
+  P.b3 = fp(vecs[3]); P.ln2_w = fp(vecs[4]); P.ln2_b = fp(vecs[5]);
+  Tensor ho = at::empty({N, d}, h.options());
+  Tensor abo = at::empty({with_ab ? N : 0, 2 * d}, h.options());
+  Tensor xh = at::empty({train ? 2 : 0, N, d}, h.options());
+  Tensor rs = at::empty({train ? 2 : 0, N}, h.options());
+  check_rc(gmp_egnn_node_fwd_f32(N, d, fp(h), fp(m_aggr), &P, image.data_ptr(), (int)act,
+                                 residual ? 1 : 0, (float)eps, fp(ho),
+                                 with_ab ? fp(abo) : nullptr, train ? fp(xh) : nullptr,
+                                 train ? fp(rs) : nullptr, cur_stream()),
+           "gmp_egnn_node_fwd_f32");
+  return {ho, abo, xh, rs};
+}
+
 void egnn_graph_checks(const Tensor& pos, const Tensor& rowptr, const Tensor& recv,
                        const Tensor& send) {
   f32(pos, "pos");
@@ -1375,6 +1446,21 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_edge_fwd(const Tensor& AB, const
   return {at::empty({N, d}, o), at::empty({N, 3}, o),
           at::empty({train ? xhat_planes : 0, E, d}, o), at::empty({train ? E : 0, 3}, o)};
 }
+Tensor egnn_node_image(const std::vector<Tensor>& W0s, const std::vector<Tensor>&,
+                       const std::vector<optional<Tensor>>&) {
+  const int64_t d = W0s[0].size(0);
+  return at::empty({(int64_t)W0s.size(), (int64_t)gmp_egnn_node_image_bytes(d)},
+                   W0s[0].options().dtype(at::kByte));
+}
+std::tuple<Tensor, Tensor, Tensor, Tensor> egnn_node_fwd(const Tensor& h, const Tensor&,
+                                                         const std::vector<Tensor>&, const Tensor&,
+                                                         bool with_ab, int64_t, bool, double,
+                                                         bool train) {
+  const int64_t N = h.size(0), d = h.size(1);
+  auto o = h.options();
+  return {at::empty({N, d}, o), at::empty({with_ab ? N : 0, 2 * d}, o),
+          at::empty({train ? 2 : 0, N, d}, o), at::empty({train ? 2 : 0, N}, o)};
+}
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> egnn_edge_bwd(
     const Tensor& pos, const Tensor&, const Tensor& recv, const Tensor&,
     const std::vector<Tensor>&, int64_t, bool, const Tensor& xhat, const Tensor&, const Tensor&,
@@ -1575,6 +1661,10 @@ TORCH_LIBRARY(gmp, m) {
   m.def("egnn_edge_fwd(Tensor AB, Tensor pos, Tensor rowptr, Tensor recv, Tensor send, "
         "Tensor[] params, int act, bool msg_mean, float eps, bool train, int xhat_planes=2) -> "
         "(Tensor m_aggr, Tensor pos_aggr, Tensor xhat, Tensor rstd)");
+  m.def("egnn_node_image(Tensor[] W0s, Tensor[] W3s, Tensor?[] W1ns) -> Tensor");
+  m.def("egnn_node_fwd(Tensor h, Tensor m_aggr, Tensor[] vecs, Tensor image, bool with_ab, "
+        "int act, bool residual, float eps, bool train) -> (Tensor h_out, Tensor ab, "
+        "Tensor xhat, Tensor rstd)");
   m.def("egnn_edge_bwd(Tensor pos, Tensor rowptr, Tensor recv, Tensor send, Tensor[] params, "
         "int act, bool msg_mean, Tensor xhat, Tensor rstd, Tensor g_m_aggr, Tensor g_pos_aggr, "
         "Tensor(a!)? amax=None) -> (Tensor dA, Tensor dpos_recv, "
@@ -1667,6 +1757,8 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("segment_reduce", ns segment_reduce);                            \
   m.impl("segment_reduce_bwd", ns segment_reduce_bwd);                    \
   m.impl("egnn_edge_fwd", ns egnn_edge_fwd);                              \
+  m.impl("egnn_node_fwd", ns egnn_node_fwd);                              \
+  m.impl("egnn_node_image", ns egnn_node_image);                          \
   m.impl("egnn_edge_bwd", ns egnn_edge_bwd);                              \
   m.impl("cfconv_aggregate", ns cfconv_aggregate);                        \
   m.impl("cfconv_wgrad", ns cfconv_wgrad);                                \

@@ -31,6 +31,11 @@ class GmpEgnnParams(ctypes.Structure):
         "w4", "b4")]
 
 
+class GmpEgnnNodeParams(ctypes.Structure):
+    _fields_ = [(n, c_vp) for n in ("W0", "b0", "ln1_w", "ln1_b", "W3", "b3", "ln2_w", "ln2_b",
+                                     "W1n")] + [("ld1", ctypes.c_longlong)]
+
+
 class TpPath(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("l1", "l2", "lo", "mul1", "mul_out", "x_off", "y_off", "io",
                                        "out_off", "z_off", "cg_off", "pad")] + [
@@ -190,14 +195,20 @@ SIGNATURES = {
                                                   c_vp, c_vp, c_vp, c_vp]),
     "gmp_symmetric_contraction_bwd_f32": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_egnn_node_image_bytes": (c_size, [c_i64]),
+    "gmp_egnn_node_image_f32": (c_int, [c_i64, c_i64, ctypes.POINTER(GmpEgnnNodeParams), c_vp,
+                                        c_vp]),
+    "gmp_egnn_node_fwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, ctypes.POINTER(GmpEgnnNodeParams),
+                                      c_vp, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
                                       ctypes.POINTER(GmpEgnnParams), c_int, c_int, c_vp, c_int]
                               + [c_vp] * 11),
 }
 
-# include/gmp.h GMP_ABI_VERSION (3: r04 — K8 dim / A4 arguments; 2: r04 — EGNN save_planes
+# include/gmp.h GMP_ABI_VERSION (4: r05 — gmp_egnn_node_fwd_f32;
+# 3: r04 — K8 dim / A4 arguments; 2: r04 — EGNN save_planes
 # arguments, the x_hat mode global and gmp_egnn_edge_bwd_ab_f32 removed)
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lib = None
 TORCH_LIB_PATH = os.environ.get("GMP_TORCH_LIB", os.path.join(_HERE, "libgmp_torch.so"))
 _torch_ops = None

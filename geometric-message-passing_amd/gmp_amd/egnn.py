@@ -67,15 +67,40 @@ class EGNNLayer(MessagePassing):
                 and h.dtype == torch.float32 and pos.dtype == torch.float32
                 and all(ln.elementwise_affine and ln.eps == lns[0].eps for ln in lns))
 
-    def fused_propagate(self, edge_index, h, pos):
+    def fused_message(self, edge_index, h, pos, AB=None):
+        """(m_aggr, pos_aggr) of the fused message block (K4); AB: the node projections when the
+        previous layer's K15 update produced them."""
         graph = ops.egnn_graph(edge_index, h.shape[0])
         m0, ln1, m3, ln2 = self.mlp_msg[0], self.mlp_msg[1], self.mlp_msg[3], self.mlp_msg[4]
         p0, ln3, p3 = self.mlp_pos[0], self.mlp_pos[1], self.mlp_pos[3]
-        m_aggr, p_aggr = ops.EgnnMessageFn.apply(
+        return ops.EgnnMessageFn.apply(
             h, pos, graph, self.activation_name, self.aggr == "mean", ln1.eps,
             m0.weight, m0.bias, ln1.weight, ln1.bias, m3.weight, m3.bias, ln2.weight, ln2.bias,
-            p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias, torch.is_grad_enabled())
+            p0.weight, p0.bias, ln3.weight, ln3.bias, p3.weight, p3.bias, torch.is_grad_enabled(),
+            AB)
+
+    def fused_propagate(self, edge_index, h, pos):
+        m_aggr, p_aggr = self.fused_message(edge_index, h, pos)
         return self._mlp_upd(h, m_aggr), pos + p_aggr
+
+    def node_fusable(self):
+        """K15 applies: LayerNorm update MLP with affine norms (the fused message already
+        requires LayerNorm and emb_dim in {32, 64, 128})."""
+        n1, n4 = self.mlp_upd[1], self.mlp_upd[4]
+        return (self.norm_name == "layer" and n1.elementwise_affine and n4.elementwise_affine
+                and n1.eps == n4.eps)
+
+    def fused_update(self, h, m_aggr, next_layer=None, residual=True, image=None):
+        """(h', AB') = K15: h' = h + mlp_upd([h | m_aggr]) (or the update alone without residual)
+        and the next layer's node projections (None when next_layer is None).  image: this
+        layer's row of ops.egnn_node_images (built here when not given)."""
+        l0, n1, l3, n4 = self.mlp_upd[0], self.mlp_upd[1], self.mlp_upd[3], self.mlp_upd[4]
+        if image is None:
+            image = ops.egnn_node_images([self], [next_layer])[0]
+        return ops.EgnnNodeFn.apply(h, m_aggr, l0.weight, l0.bias, n1.weight, n1.bias, l3.weight,
+                                    l3.bias, n4.weight, n4.bias, image, next_layer is not None,
+                                    self.activation_name, residual, n1.eps,
+                                    torch.is_grad_enabled())
 
     def _mlp_upd(self, h, m_aggr):
         """mlp_upd(cat([h, m_aggr])) (egnn_layer.py:37-39, :84) with the first Linear split over
@@ -112,12 +137,27 @@ class EGNNModel(nn.Module):
             self.pred = nn.Sequential(nn.Linear(emb_dim, emb_dim), nn.ReLU(),
                                       nn.Linear(emb_dim, out_dim))
 
+    def _layers_fused(self, h, pos):
+        return (len(self.convs) > 0 and all(c.fused_supported(h, pos) and c.node_fusable()
+                                            for c in self.convs)
+                and not ops.compiling() and not ops.egnn_exact_mode())
+
     def forward(self, batch):
         h = ops.gather(self.emb_in.weight, batch.atoms)  # == emb_in(atoms); bwd = segmented sum
         pos = batch.pos
-        for conv in self.convs:
-            h_update, pos = conv(h, pos, batch.edge_index)
-            h = h + h_update if self.residual else h_update
+        if self._layers_fused(h, pos):
+            # per layer: K4 message block, then K15 (update + residual + the next layer's AB)
+            convs, AB = list(self.convs), None
+            nexts = convs[1:] + [None]
+            images = ops.egnn_node_images(convs, nexts)  # one launch for every layer
+            for k, conv in enumerate(convs):
+                m_aggr, p_aggr = conv.fused_message(batch.edge_index, h, pos, AB)
+                h, AB = conv.fused_update(h, m_aggr, nexts[k], self.residual, images[k])
+                pos = pos + p_aggr
+        else:
+            for conv in self.convs:
+                h_update, pos = conv(h, pos, batch.edge_index)
+                h = h + h_update if self.residual else h_update
         feats = torch.cat([h, pos], dim=-1) if self.equivariant_pred else h
         out = self.pool(feats, batch.batch, getattr(batch, "num_graphs", None))
         return self.pred(out)

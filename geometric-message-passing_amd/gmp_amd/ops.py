@@ -867,19 +867,21 @@ class EgnnMessageFn(torch.autograd.Function):
     Parameters in module order: mlp_msg.0.{weight (d, 2d+1), bias}, mlp_msg.1.{weight, bias},
     mlp_msg.3.{weight, bias}, mlp_msg.4.{weight, bias}, mlp_pos.0.{weight, bias},
     mlp_pos.1.{weight, bias}, mlp_pos.3.{weight (1, d), bias}.
-    Returns (m_aggr (N, d), pos_aggr (N, 3)).
+    Returns (m_aggr (N, d), pos_aggr (N, 3)).  AB: the node projections precomputed by the
+    previous layer's K15 node update (EgnnNodeFn), a constant here: the gradient w.r.t. h still
+    comes from this Function's backward (dh = [dA | dB] [W1a ; W1b]).
     """
 
     @staticmethod
     def forward(ctx, h, pos, graph, act, msg_mean, eps, W1, b1, ln1w, ln1b, W2, b2, ln2w, ln2b,
-                W3, b3, ln3w, ln3b, w4, b4, grad_mode=True):
+                W3, b3, ln3w, ln3b, w4, b4, grad_mode=True, AB=None):
         h, pos = _f32c(h), _f32c(pos)
         _need_cuda(h, pos, W1)
         N, d = h.shape
         E = graph.num_edges
-        Wcat = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)
-        # [h W1a^T | h W1b^T]
-        AB = linear_x3(h, None, Wcat) if _x3_fits(2 * d, d) else h.mm(Wcat.t())
+        if AB is None:  # [h W1a^T | h W1b^T] (else: K15 produced it with the previous update)
+            Wcat = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)
+            AB = linear_x3(h, None, Wcat) if _x3_fits(2 * d, d) else h.mm(Wcat.t())
         params = tuple(_f32c(t) for t in (W1[:, 2 * d], b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3,
                                           b3, ln3w, ln3b, w4, b4))
         # save the LayerNorm outputs only for a backward: grad_mode is the CALLER's
@@ -951,4 +953,79 @@ class EgnnMessageFn(torch.autograd.Function):
         # then b1 ... b4 (params[0] is the contiguous copy of W1's distance column)
         targets = (W1,) + tuple(params[1:])
         return (dh, dpos, None, None, None, None) + sw.deliver(ctx.needs_input_grad, 6, targets,
-                                                               grads, extra=(sw2,)) + (None,)
+                                                               grads, extra=(sw2,)) + (None, None)
+
+
+def egnn_exact_mode():
+    """True while the EGNN kernels run their exact-f32 A/B mode (gmp_egnn_set_f32_mfma(1))."""
+    lib = _lib.load()
+    prev = lib.gmp_egnn_set_f32_mfma(0)
+    lib.gmp_egnn_set_f32_mfma(prev)
+    return bool(prev)
+
+
+def egnn_node_images(layers, next_layers):
+    """uint8 (L, bytes) K15 weight images (gmp_egnn_node_image_f32, one launch): per EGNN layer
+    its mlp_upd.0 / mlp_upd.3 weights and the next layer's mlp_msg.0 weight (None: last layer).
+    A constant for autograd (built from the current weights; rebuilt every forward)."""
+    with torch.no_grad():
+        return _lib.torch_ops().egnn_node_image(
+            [_f32c(l.mlp_upd[0].weight) for l in layers], [_f32c(l.mlp_upd[3].weight) for l in layers],
+            [None if n is None else n.mlp_msg[0].weight for n in next_layers])
+
+
+class EgnnNodeFn(torch.autograd.Function):
+    """K15 (gmp_egnn_node_fwd_f32): the EGNN node update of one layer (egnn_layer.py:82-86,
+    mlp_upd over [h | m_aggr]), the model's residual (egnn.py:75-76) and the next layer's node
+    projections AB' = [h' W1a'^T | h' W1b'^T] in one launch, from the layer's weight image
+    (egnn_node_images).  Returns (h', AB' or None) — AB' is a constant for autograd (the next
+    EgnnMessageFn differentiates through h').  Backward: the LayerNorm + act backwards (K12) from
+    the saved x_hat / 1/std, the dx GEMMs on the critical path, the weight gradients by the
+    deterministic outer sums on the side stream (deferred), as the unfused SplitLinearFn /
+    LnActFn / EdgeLinearFn chain does."""
+
+    @staticmethod
+    def forward(ctx, h, m, W0, b0, ln1w, ln1b, W3, b3, ln2w, ln2b, image, with_ab, act, residual,
+                eps, grad_mode):
+        h, m = _f32c(h), _f32c(m)
+        _need_cuda(h, m, W0)
+        vecs = [_f32c(t) for t in (b0, ln1w, ln1b, b3, ln2w, ln2b)]
+        train = bool(grad_mode) and any(ctx.needs_input_grad)
+        with _timed("egnn_node_fwd"):
+            ho, ab, xhat, rstd = _lib.torch_ops().egnn_node_fwd(
+                h, m, vecs, image, bool(with_ab), _lib.ACT[act], bool(residual), float(eps), train)
+        ctx.act, ctx.residual = act, bool(residual)
+        if train:
+            ctx.save_for_backward(h, m, xhat, rstd, _f32c(W0), vecs[0], vecs[1], vecs[2],
+                                  _f32c(W3), vecs[3], vecs[4], vecs[5])
+        ctx.mark_non_differentiable(ab)
+        return ho, (ab if with_ab else None)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g, _g_ab):
+        h, m, xhat, rstd, W0, b0, ln1w, ln1b, W3, b3, ln2w, ln2b = ctx.saved_tensors
+        d = h.shape[1]
+        g = _f32c(g)
+        tops = _lib.torch_ops()
+        a = _LN_ACT[ctx.act]
+        dpre2, gb2 = tops.ln_act_bwd(g, xhat[1], rstd[1], ln2w, ln2b, a)
+        dx1 = _dx(dpre2, W3)
+        dpre1, gb1 = tops.ln_act_bwd(dx1, xhat[0], rstd[0], ln1w, ln1b, a)
+        dh = _dx(dpre1, W0[:, :d]) if ctx.needs_input_grad[0] else None
+        if dh is not None and ctx.residual:
+            dh += g
+        dm = _dx(dpre1, W0[:, d:]) if ctx.needs_input_grad[1] else None
+        with side_work(dpre1, dpre2, h, m, xhat) as sw:
+            dW0 = torch.empty_like(W0)
+            db0 = torch.empty_like(b0)
+            outer_sum_into(dpre1, h, dW0[:, :d], db0)
+            outer_sum_into(dpre1, m, dW0[:, d:], None)
+            dW3 = torch.empty_like(W3)
+            db3 = torch.empty_like(b3)
+            # x1 = act(x_hat1 ln1w + ln1b), rebuilt at load time
+            outer_sum_into(dpre2, xhat[0], dW3, db3, ctx.act, ln1w, ln1b)
+        grads = (dW0, db0, gb1[:d], gb1[d:], dW3, db3, gb2[:d], gb2[d:])
+        return ((dh, dm) + sw.deliver(ctx.needs_input_grad, 2,
+                                      (W0, b0, ln1w, ln1b, W3, b3, ln2w, ln2b), grads)
+                + (None, None, None, None, None, None))

@@ -29,8 +29,9 @@ extern "C" {
 /* 3 (r04): K8 symmetric contraction takes the per-channel dim and A4 (gmp_sc_monomials added);
  * the TP descriptor holds 8 output blocks (128 bytes), <= 48 paths.
  * 2 (r04): EGNN forward / backward take save_planes; gmp_egnn_set_xhat_mode and
- * gmp_egnn_edge_bwd_ab_f32 removed.  (r03 changed gmp_triplet_fill_f32 under version 1.) */
-#define GMP_ABI_VERSION 3
+ * gmp_egnn_edge_bwd_ab_f32 removed.  (r03 changed gmp_triplet_fill_f32 under version 1.)
+ * Version 4 (r05): gmp_egnn_node_fwd_f32 / gmp_egnn_node_params added. */
+#define GMP_ABI_VERSION 4
 
 enum {
   GMP_OK = 0,
@@ -139,6 +140,44 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
                           const int64_t* send, const gmp_egnn_params* params, int act,
                           int msg_mean, float ln_eps, float* m_aggr, float* pos_aggr,
                           float* save_xhat, int save_planes, float* save_rstd, void* stream);
+
+/* K15 (r05): the EGNN node update of one layer and the next layer's node projections in one
+ * launch — replaces egnn_layer.py:82-86 (update: mlp_upd(cat([h, m_aggr]))), egnn.py:75-76 (the
+ * residual h + h_update) and the AB = [h W1a^T | h W1b^T] projection of the next layer's
+ * mlp_msg.0 (egnn_layer.py:28-29; the node half of gmp_egnn_edge_fwd_f32's split Linear):
+ *   x1 = act(LN1(W0 [h | m_aggr] + b0)); x2 = act(LN2(W3 x1 + b3));
+ *   h_out = (residual ? h + x2 : x2);  ab_out = [h_out W1n[:, :d]^T | h_out W1n[:, d:2d]^T]
+ * W0 = mlp_upd.0.weight (d, 2d) row-major; W3 = mlp_upd.3.weight (d, d); W1n = the next layer's
+ * mlp_msg.0.weight (d, 2d + 1) with row stride ld1 (>= 2d), or NULL (that layer has no ab_out).
+ * The three matrices enter as a weight IMAGE (2-plane fp16 tiles with per-16-row power-of-two
+ * scales, the layout the kernel copies into LDS): gmp_egnn_node_image_f32 builds the images of
+ * n_layers layers (params: a host array of n_layers structs) into `images`
+ * (n_layers x gmp_egnn_node_image_bytes(d) bytes, 16-byte aligned) in one launch; rebuild after
+ * every weight change.  gmp_egnn_node_fwd_f32 reads this layer's image and, from params, the
+ * vectors b0, ln1_w, ln1_b, b3, ln2_w, ln2_b; ab_out non-NULL only if the image holds W1n.
+ * save_xhat ((2, N, d): the two LayerNorm outputs) and save_rstd ((2, N): their 1/std) both NULL
+ * (inference) or both set (training; the LayerNorm backwards read them).  Products as
+ * gmp_egnn_edge_fwd_f32's HF path (2-plane fp16 splits, f32 accumulation); GMP_ERR_UNSUPPORTED
+ * under gmp_egnn_set_f32_mfma(1) and for d outside {32, 64, 128}. */
+typedef struct gmp_egnn_node_params {
+  const float* W0;   /* (d, 2d) mlp_upd.0.weight */
+  const float* b0;   /* (d) */
+  const float* ln1_w;
+  const float* ln1_b;
+  const float* W3;   /* (d, d) mlp_upd.3.weight */
+  const float* b3;
+  const float* ln2_w;
+  const float* ln2_b;
+  const float* W1n;  /* next layer's mlp_msg.0.weight (d, 2d + 1), row stride ld1; or NULL */
+  int64_t ld1;
+} gmp_egnn_node_params;
+size_t gmp_egnn_node_image_bytes(int64_t d);
+int gmp_egnn_node_image_f32(int64_t d, int64_t n_layers, const gmp_egnn_node_params* params,
+                            void* images, void* stream);
+int gmp_egnn_node_fwd_f32(int64_t n_nodes, int64_t d, const float* h, const float* m_aggr,
+                          const gmp_egnn_node_params* params, const void* image, int act,
+                          int residual, float ln_eps, float* h_out, float* ab_out,
+                          float* save_xhat, float* save_rstd, void* stream);
 
 /* Backward of gmp_egnn_edge_fwd_f32 from its saved x_hat / rstd (no forward recompute).
  * Inputs g_m_aggr (N,d), g_pos_aggr (N,3), the forward's save_xhat (save_planes, E, d) and

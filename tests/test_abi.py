@@ -33,7 +33,7 @@ def test_library_exports_all_symbols():
     # every declared entry point has a ctypes signature (and vice versa)
     assert set(_declared()) == set(_lib.SIGNATURES), set(_declared()) ^ set(_lib.SIGNATURES)
     lib2 = _lib.load()
-    assert lib2.gmp_abi_version() == _lib.ABI_VERSION == 3
+    assert lib2.gmp_abi_version() == _lib.ABI_VERSION == 4
     assert lib2.gmp_error_string(-1) == b"invalid argument"
 
 
@@ -55,6 +55,7 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
         pytest.skip("libgmp_torch.so not built")
     tops = _lib.torch_ops()
     for name in ("csr_build", "gather_rows", "segment_reduce", "egnn_edge_fwd", "egnn_edge_bwd",
+                 "egnn_node_fwd", "egnn_node_image",
                  "tp_edge_z", "tp_edge_z_bwd", "tp_node_outer", "tp_node_apply", "tp_gemm_x3",
                  "tp_gemm_x3_widen", "outer_sum_cols", "edge_outer_sum_ex",
                  "edge_outer_sum_ex2", "edge_outer_sum_act", "gvp_layer_fwd", "gvp_layer_bwd",

@@ -437,3 +437,87 @@ def test_egnn_c2_full_size_properties_hf():
     a, b = run(pos, ei), run(pos, ei)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     assert a[1].abs().max().item() > 0
+
+
+@pytest.mark.parametrize("d,act,residual,n", [(128, "relu", True, 3001), (128, "swish", True, 700),
+                                              (64, "relu", False, 513), (32, "swish", True, 17),
+                                              (128, "relu", True, 50_000)])
+def test_egnn_node_update_vs_fp64(d, act, residual, n):
+    """K15 (gmp_egnn_node_fwd_f32 via ops.EgnnNodeFn): h' = h + mlp_upd([h | m]) and the next
+    layer's AB' against an fp64 torch evaluation of egnn_layer.py:37-39 / :82-86 + egnn.py:75-76;
+    the backward (K12 LayerNorm backwards, dx GEMMs, outer-sum weight gradients) against fp64
+    autograd.  Bounds: h' and AB' 1e-5 of scale (HF products, as K4), gradients 1e-4 of their
+    scale; row counts not multiples of the 256-row workgroup tile included."""
+    import gmp_amd
+    torch.manual_seed(n + d)
+    lay, nxt = gmp_amd.EGNNLayer(d, act), gmp_amd.EGNNLayer(d, act)
+    with torch.no_grad():
+        for p in list(lay.parameters()) + list(nxt.parameters()):
+            if p.dim() == 1:
+                p.add_(0.2 * torch.randn_like(p))
+    lay, nxt = lay.to(DEV), nxt.to(DEV)
+    h = (torch.randn(n, d) * 2).to(DEV).requires_grad_(True)
+    m = (torch.randn(n, d) * 5 + 1).to(DEV).requires_grad_(True)
+    ho, ab = lay.fused_update(h, m, nxt, residual)
+    gh = torch.randn(n, d, device=DEV)
+    (ho * gh).sum().backward()
+    # fp64 reference (CPU) of the same module tree
+    ref = {k: v.detach().double().cpu() for k, v in lay.state_dict().items()}
+    P = {k: v.clone().requires_grad_(True) for k, v in ref.items()}
+    hr = h.detach().double().cpu().requires_grad_(True)
+    mr = m.detach().double().cpu().requires_grad_(True)
+    fn = {"relu": torch.relu, "swish": torch.nn.functional.silu}[act]
+    ln = lambda x, w, b: torch.nn.functional.layer_norm(x, (d,), w, b, 1e-5)
+    x1 = fn(ln(torch.cat([hr, mr], -1) @ P["mlp_upd.0.weight"].T + P["mlp_upd.0.bias"],
+               P["mlp_upd.1.weight"], P["mlp_upd.1.bias"]))
+    x2 = fn(ln(x1 @ P["mlp_upd.3.weight"].T + P["mlp_upd.3.bias"], P["mlp_upd.4.weight"],
+               P["mlp_upd.4.bias"]))
+    hor = hr + x2 if residual else x2
+    W1 = nxt.mlp_msg[0].weight.detach().double().cpu()
+    abr = torch.cat([hor @ W1[:, :d].T, hor @ W1[:, d:2 * d].T], 1)
+    (hor * gh.double().cpu()).sum().backward()
+
+    def close(a, b, tol, what):
+        a = a.detach().double().cpu()
+        scale = b.abs().max().item() + 1e-12
+        err = (a - b).abs().max().item()
+        assert err <= tol * scale, f"{what}: max|d| {err:.3e} scale {scale:.3e}"
+
+    close(ho, hor.detach(), 1e-5, "h'")
+    close(ab, abr.detach(), 1e-5, "AB'")
+    close(h.grad, hr.grad, 1e-4, "dh")
+    close(m.grad, mr.grad, 1e-4, "dm")
+    for name, p in lay.named_parameters():
+        if name.startswith("mlp_upd"):
+            close(p.grad, P[name].grad, 1e-4, "d" + name)
+
+
+def test_egnn_model_uses_node_update_and_matches_unfused():
+    """The model's fused loop (K4 + K15 per layer) against the same model with K15 bypassed
+    (per-layer EGNNLayer path: split Linear, K12, Linear, K12, residual): prediction and every
+    parameter gradient within 1e-5 / 1e-4 of scale."""
+    import gmp_amd
+    from gmp_amd import ops
+    g = _graph(3000, 60_000, seed=5)
+    torch.manual_seed(0)
+    model = gmp_amd.EGNNModel(num_layers=3, emb_dim=128, in_dim=1, out_dim=1).to(DEV)
+    b = g.to(DEV)
+    calls = []
+    orig = ops.EgnnNodeFn.apply
+    ops.EgnnNodeFn.apply = lambda *a: calls.append(1) or orig(*a)
+    try:
+        out = model(b)
+        out.sum().backward()
+    finally:
+        ops.EgnnNodeFn.apply = orig
+    assert len(calls) == 3
+    grads = {k: p.grad.clone() for k, p in model.named_parameters()}
+    model.zero_grad(set_to_none=True)
+    model._layers_fused = lambda h, pos: False
+    out2 = model(b)
+    out2.sum().backward()
+    scale = out2.abs().max().item()
+    assert (out - out2).abs().max().item() <= 1e-5 * scale + 1e-6
+    for k, p in model.named_parameters():
+        sc = p.grad.abs().max().item() + 1e-8
+        assert (grads[k] - p.grad).abs().max().item() <= 1e-4 * sc, k
