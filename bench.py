@@ -233,18 +233,23 @@ def tp_forward_flops(model, n_nodes, n_edges):
 
 def time_forward(model, batch, reps):
     """Inference forward (no autograd; the kernels save nothing for a backward): average wall
-    seconds per pass over `reps` passes after one warm-up pass, synchronised on both sides, and
-    the per-region kernel times recorded meanwhile (ops timers)."""
+    seconds per pass over `reps` passes after one warm-up pass, synchronised on both sides, with
+    the per-kernel timers OFF (their event records sit between the kernels); then `reps` more
+    passes with the timers on for the per-region kernel times (ops timers)."""
     from gmp_amd import ops
     with torch.no_grad():
         model(batch)
         torch.cuda.synchronize()
-        ops.KERNEL_TIMERS = {}
+        ops.KERNEL_TIMERS = None
         t0 = time.perf_counter()
         for _ in range(reps):
             model(batch)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
+        ops.KERNEL_TIMERS = {}
+        for _ in range(reps):
+            model(batch)
+        torch.cuda.synchronize()
     timers = {k: ops.kernel_time_ms(k) * len(v) / reps for k, v in ops.KERNEL_TIMERS.items()}
     ops.KERNEL_TIMERS = None
     return dt, timers

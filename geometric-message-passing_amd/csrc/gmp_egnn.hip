@@ -19,6 +19,10 @@
 //    accumulation) with power-of-two scaling (W per matrix, x per edge) that keeps the planes
 //    in fp16 range; the planes of W take the LDS of the f32 W (gemm_h2 below).  The f32 path
 //    (exact fmaf chains on the f32 MFMA) stays selectable: gmp_egnn_set_f32_mfma(1).
+#include <mutex>
+#include <set>
+#include <tuple>
+
 #include "gmp_egnn_common.h"
 
 namespace gmp {
@@ -57,6 +61,7 @@ __global__ __launch_bounds__(fwd_waves<HF>() * 64, fwd_waves<HF>() / 4) void egn
   float* cbuf = carry0 + (wid * 4 + g) * carry_stride<D>();
   carry_clear<D>(carry0 + wid * 4 * carry_stride<D>(), lane);
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, fwd_waves<HF>());
+  zero_isolated<D>(wr, rowptr, m_aggr, pos_aggr, lane);
   const float b4 = P.b4[0];
   int carry_node = -1;
   EdgeIJ nxt = load_ij(wr.e_lo, li, wr.e_hi, recv, send);
@@ -233,6 +238,7 @@ __global__ __launch_bounds__(kBwdWaves * 64, 2) void egnn_bwd_kernel(
   float* cbuf = smem + smem_carry_off<D, kBwdWaves, HF>() + (wid * 4 + g) * carry_stride<D>();
   carry_clear<D>(smem + smem_carry_off<D, kBwdWaves, HF>() + wid * 4 * carry_stride<D>(), lane);
   const WaveRange wr = wave_range(rowptr, n_nodes, n_edges, n_waves, wid, kBwdWaves);
+  zero_isolated<D>(wr, rowptr, dA, dpos_recv, lane);
   const float b4 = P.b4[0];
   const size_t ED = (size_t)n_edges * D;
 
@@ -492,6 +498,19 @@ bool params_ok(const gmp_egnn_params* P) {
 
 }  // namespace
 
+int prep_kernel_once(const void* k, size_t smem) {
+  static std::mutex mu;
+  static std::set<std::tuple<int, const void*, size_t>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return GMP_ERR_HIP;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({dev, k, smem})) return GMP_OK;
+  const int rc = hip_check(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)smem));
+  if (!rc) done.insert({dev, k, smem});
+  return rc;
+}
+
 // 1: the f32-MFMA (exact fmaf chain) products instead of the HF path; initial value from
 // GMP_EGNN_F32_MFMA, changed by gmp_egnn_set_f32_mfma
 int g_egnn_f32 = -1;
@@ -544,9 +563,12 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
   GMP_CHECK_ARG(save_xhat == nullptr || save_planes == 2 || save_planes == 3);
   hipStream_t s = as_stream(stream);
   if (n_nodes == 0) return GMP_OK;
-  int rc = hip_check(hipMemsetAsync(m_aggr, 0, n_nodes * d * sizeof(float), s));
-  if (!rc) rc = hip_check(hipMemsetAsync(pos_aggr, 0, n_nodes * 3 * sizeof(float), s));
-  if (rc || n_edges == 0) return rc;
+  int rc = GMP_OK;
+  if (n_edges == 0) {  // (otherwise the kernel writes every row: zero_isolated)
+    rc = hip_check(hipMemsetAsync(m_aggr, 0, n_nodes * d * sizeof(float), s));
+    if (!rc) rc = hip_check(hipMemsetAsync(pos_aggr, 0, n_nodes * 3 * sizeof(float), s));
+    return rc;
+  }
   GMP_CHECK_ARG(AB && pos && recv && send && aligned16(AB) && aligned16(m_aggr));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
   GMP_CHECK_ARG(save_xhat == nullptr || aligned16(save_xhat));
@@ -577,7 +599,7 @@ int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, cons
   GMP_CHECK_ARG(save_planes == 2 || save_planes == 3);
   hipStream_t s = as_stream(stream);
   int rc = GMP_OK;
-  if (n_nodes > 0) {
+  if (n_nodes > 0 && n_edges == 0) {  // (otherwise the kernel writes every row: zero_isolated)
     rc = hip_check(hipMemsetAsync(dA, 0, n_nodes * d * sizeof(float), s));
     if (!rc) rc = hip_check(hipMemsetAsync(dpos_recv, 0, n_nodes * 3 * sizeof(float), s));
   }

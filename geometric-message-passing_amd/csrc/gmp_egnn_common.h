@@ -443,29 +443,44 @@ __device__ __forceinline__ void gemm_h2(const _Float16* __restrict__ hW, int sw,
 // scale-up / scale-down pass over the accumulators.  XS: x already carries 2^ex (relu: the
 // affine's pre-scaled vectors); otherwise (silu) it is scaled here.  Planes, operands and MFMA
 // order are gemm_h2's: bitwise the r04 products.
+#ifndef K4_PD
+#define K4_PD 1
+#endif
 template <int D, bool XS>
 __device__ __forceinline__ void gemm_h2s(const _Float16* __restrict__ hW, int ex,
                                          const f32x4 (&x)[D / 16], f32x4 (&y)[D / 16], int i,
                                          int g) {
   using H = HCfg<D>;
-  constexpr int T = D / 16, PB = D / 32;
+  constexpr int T = D / 16, PB = D / 32, NQ = PB * T, PD = K4_PD;
   const float fx = ldexpf(1.f, ex);
+  // the A operand (W planes) of step q + PD is read from LDS while step q's MFMAs run
+  const _Float16* base = hW + i * H::LDH + 8 * g;
+  h16x8 ah[PD + 1], al[PD + 1];
 #pragma unroll
-  for (int p = 0; p < PB; ++p) {
-    h16x8 bh, bl;
-    if constexpr (XS) split8(x[2 * p], x[2 * p + 1], bh, bl);
-    else split8(x[2 * p] * fx, x[2 * p + 1] * fx, bh, bl);
+  for (int q = 0; q < PD; ++q) {
+    const _Float16* row = base + 16 * (q % T) * H::LDH + 32 * (q / T);
+    ah[q] = *reinterpret_cast<const h16x8*>(row);
+    al[q] = *reinterpret_cast<const h16x8*>(row + H::PLANE);
+  }
+  h16x8 bh, bl;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      if (t % HF_TILES_PER_FENCE == 0) asm volatile("" ::: "memory");
-      const _Float16* row = hW + (16 * t + i) * H::LDH + 32 * p + 8 * g;
-      const h16x8 ah = *reinterpret_cast<const h16x8*>(row);
-      const h16x8 al = *reinterpret_cast<const h16x8*>(row + H::PLANE);
-      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, y[t], 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
-      y[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
-      if (t % HF_TILES_PER_FENCE == HF_TILES_PER_FENCE - 1) GMP_GEMM_FENCE();
+  for (int q = 0; q < NQ; ++q) {
+    const int p = q / T, t = q % T;
+    if (t == 0) {
+      if constexpr (XS) split8(x[2 * p], x[2 * p + 1], bh, bl);
+      else split8(x[2 * p] * fx, x[2 * p + 1] * fx, bh, bl);
     }
+    if (q + PD < NQ) {
+      const int qn = q + PD;
+      const _Float16* row = base + 16 * (qn % T) * H::LDH + 32 * (qn / T);
+      ah[qn % (PD + 1)] = *reinterpret_cast<const h16x8*>(row);
+      al[qn % (PD + 1)] = *reinterpret_cast<const h16x8*>(row + H::PLANE);
+    }
+    const int b = q % (PD + 1);
+    f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], bh, y[t], 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], bl, acc, 0, 0, 0);
+    y[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], bh, acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -872,7 +887,7 @@ __device__ __forceinline__ float* rowp(float* base, int r, int ld) {
 
 // wave-uniform range of this wave (scalar registers)
 struct WaveRange {
-  int e_lo, e_hi;
+  int e_lo, e_hi, n_lo, n_hi;  // edges [e_lo, e_hi) = the in-edges of receivers [n_lo, n_hi)
 };
 __device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowptr, int64_t n_nodes,
                                                 int64_t n_edges, int64_t n_waves, int wid,
@@ -885,17 +900,42 @@ __device__ __forceinline__ WaveRange wave_range(const int64_t* __restrict__ rowp
   r.e_hi = (nb < ne) ? (int)rowptr[ne] : 0;
   r.e_lo = __builtin_amdgcn_readfirstlane(r.e_lo);
   r.e_hi = __builtin_amdgcn_readfirstlane(r.e_hi);
+  r.n_lo = __builtin_amdgcn_readfirstlane((int)nb);
+  r.n_hi = __builtin_amdgcn_readfirstlane((int)ne);
   return r;
+}
+
+// The receiver rows of the wave's zero in-degree nodes: zeros.  The edge loop writes a row at
+// each segment end only, so these are the rows it never writes; covering them here replaces
+// two full memsets of the outputs per launch (r04: ~11 us of fill kernels + their boundaries
+// per layer).  The waves' node ranges partition [0, n_nodes).
+template <int D>
+__device__ __forceinline__ void zero_isolated(const WaveRange& wr, const int64_t* __restrict__ rowptr,
+                                              float* __restrict__ rows, float* __restrict__ rows3,
+                                              int lane) {
+  const int* rp = reinterpret_cast<const int*>(rowptr);  // low dwords (values < 2^31)
+  for (int n = wr.n_lo + lane; n < wr.n_hi; n += 64) {
+    if (rp[2 * n] == rp[2 * n + 2]) {
+      float4* r = reinterpret_cast<float4*>(rows + (size_t)n * D);
+#pragma unroll
+      for (int k = 0; k < D / 4; ++k) r[k] = float4{0.f, 0.f, 0.f, 0.f};
+      rows3[3 * (size_t)n] = 0.f;
+      rows3[3 * (size_t)n + 1] = 0.f;
+      rows3[3 * (size_t)n + 2] = 0.f;
+    }
+  }
 }
 
 
 // 1: the f32-MFMA (exact fmaf chain) products instead of the HF path (gmp_egnn_set_f32_mfma)
 bool egnn_f32();
 
+// the dynamic-LDS attribute, set once per (device, kernel): a hipFuncSetAttribute before every
+// launch showed as ~10 us gaps in front of the K4 / K15 launches (r05 trace)
+int prep_kernel_once(const void* k, size_t smem);
 template <class K>
 inline int prep_kernel(K k, size_t smem) {
-  return hip_check(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)smem));
+  return prep_kernel_once((const void*)k, smem);
 }
 
 inline bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }

@@ -147,9 +147,16 @@ class EGNNModel(nn.Module):
         pos = batch.pos
         if self._layers_fused(h, pos):
             # per layer: K4 message block, then K15 (update + residual + the next layer's AB)
-            convs, AB = list(self.convs), None
+            convs = list(self.convs)
             nexts = convs[1:] + [None]
             images = ops.egnn_node_images(convs, nexts)  # one launch for every layer
+            # the first layer's node projections: the embedding table projected once (in_dim
+            # rows), then gathered — AB0 = emb[atoms] [W1a | W1b]^T without an (N, d) GEMM
+            with torch.no_grad():
+                W1 = convs[0].mlp_msg[0].weight
+                d = h.shape[1]
+                table = self.emb_in.weight.mm(torch.cat([W1[:, :d], W1[:, d:2 * d]], 0).t())
+                AB = ops.gather_rows(table, batch.atoms)
             for k, conv in enumerate(convs):
                 m_aggr, p_aggr = conv.fused_message(batch.edge_index, h, pos, AB)
                 h, AB = conv.fused_update(h, m_aggr, nexts[k], self.residual, images[k])
