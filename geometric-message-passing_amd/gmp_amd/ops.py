@@ -314,14 +314,6 @@ def _engine_accumulates(p):
 # fewer workgroups the weight gradients leave CUs to the critical path's node-level kernels.
 SIDE_GRID_CAP = int(os.environ.get("GMP_SIDE_GRID_CAP", "0") or 0)
 
-# side-stream lane of the EGNN edge-level weight sums (dW2, dW3); 0 = the node-level sums' stream.
-# A second lane removes the first layer's tail (the sums start when their inputs are ready
-# instead of behind the node-level sums) but measured slower on the whole step (C2, one box:
-# 103.5 / 102.2 vs 104.4 / 103.8 M edges/s): the concurrent sums crowd the critical path's
-# node kernels for CUs.  Default 0.
-EDGE_SUM_LANE = int(os.environ.get("GMP_EDGE_SUM_LANE", "0") or 0)
-
-
 def compiling():
     """True while torch.compile (dynamo) traces: the ops then run inline on the current stream,
     without the per-graph caches, side streams or end-of-backward callbacks of eager mode."""
@@ -338,10 +330,10 @@ class side_work:
     EGNN edge-level sums behind the node-level ones) runs concurrently with it; deliver(...,
     extra=(other side_work, ..)) joins those streams too."""
 
-    def __init__(self, *used, tail=False, lane=0):
+    def __init__(self, *used, tail=False, lane=0, inline=False):
         self.used = [t for t in used if t is not None]
         self.cap = 0 if tail else SIDE_GRID_CAP
-        self.inline = compiling()
+        self.inline = compiling() or inline
         self.lane = lane
         self.extra = ()
 
@@ -932,9 +924,11 @@ class EgnnMessageFn(torch.autograd.Function):
 
         # weight gradients: side stream, accumulated at the end of the backward pass
         (_, b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3, b3, ln3w, ln3b, w4, b4) = params
-        # the edge-level sums (dW2, dW3: ~0.2 ms each), on a side-stream lane of their own when
-        # EDGE_SUM_LANE > 0
-        with side_work(dpre2, dpre3, xhat, amax, lane=EDGE_SUM_LANE) as sw2:
+        # the edge-level sums (dW2, dW3: ~0.2 ms each) inline on the main stream (r05): on the
+        # side stream they took the CUs from the critical path's node-level backward kernels
+        # (LayerNorm backward + its column sums 0.33 ms instead of ~0.04 ms per layer, trace);
+        # A/B on one box, 20-step runs: 114.4 (113.7-115.0) vs 113.2 (112.9-113.4) M edges/s
+        with side_work(dpre2, dpre3, xhat, amax, inline=True) as sw2:
             dW2, db2 = edge_outer_sum_act(dpre2, xh1, ln1w, ln1b, ctx.act,
                                           amax[0:1] if amax is not None else None)
             dW3, db3 = edge_outer_sum_act(dpre3, xh2, ln2w, ln2b, ctx.act,
