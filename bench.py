@@ -86,7 +86,7 @@ def parse():
                     help="hand the model a new edge_index tensor every step (as a data loader "
                          "would), so the receiver / sender CSRs (K0) are rebuilt inside the "
                          "timed steps instead of coming from the per-graph cache")
-    ap.add_argument("--blas", default=os.environ.get("GMP_BLAS", "default"),
+    ap.add_argument("--blas", default="default",
                     choices=("default", "hipblaslt", "hipblas"),
                     help="library for the node-level PyTorch GEMMs (torch.backends.cuda."
                          "preferred_blas_library)")
@@ -438,8 +438,7 @@ def tp_algorithmic_bytes(model, n_edges):
 # names them in profiles/<round>_<workload>_kernels.json)
 TP_KERNELS = ("tp_node_outer_kernel", "tp_gemm_x3_kernel", "tp_gemm_x3_widen_kernel",
               "outer_sum_x3_kernel", "outer_cols_x3g_kernel", "split_g_kernel",
-              "sum_partials_cols", "tp_node_apply", "tp_split_w2_kernel", "tp_node_dw_kernel",
-              "tp_dw_sum_kernel")
+              "sum_partials_cols", "tp_node_apply", "tp_split_w2_kernel")
 
 
 def pmc_step(workload):
@@ -750,15 +749,6 @@ def main():
         local = 0
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
-    if os.environ.get("GMP_MAIN_STREAM", "0") == "1":
-        # the step on its own (non-default) stream, so that the weight-gradient side stream may be
-        # CU-masked (gmp_amd.ops.SIDE_CUS: a masked stream is a blocking stream and would
-        # serialise with the legacy default stream; ops uses it only off the default stream)
-        # GMP_MAIN_PRIO=1: at the device's highest stream priority, so the critical path's
-        # kernels take free CUs ahead of the weight-gradient side stream's
-        prio = torch.cuda.Stream.priority_range()[1] if os.environ.get("GMP_MAIN_PRIO") == "1" \
-            else 0
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=prio))
     if args.blas != "default":
         torch.backends.cuda.preferred_blas_library(args.blas)
     from gmp_amd.graph import radius_graph

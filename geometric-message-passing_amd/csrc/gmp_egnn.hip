@@ -475,13 +475,13 @@ int launch_bwd(int64_t N, int64_t E, const float* pos, const int64_t* rowptr,
   const int64_t W = n_waves_for(E, kBwdWaves);
   const bool hf = !egnn_f32();
   const size_t smem = hf ? smem_total<D, kBwdWaves, true>() : smem_total<D, kBwdWaves, false>();
-#define GMP_BWD_K(RC)                                                  \
+#define LAUNCH_BWD_K(RC)                                                  \
   (hf ? (amax ? egnn_bwd_kernel<D, ACT, MEAN, true, true, RC>          \
               : egnn_bwd_kernel<D, ACT, MEAN, true, false, RC>)        \
       : (amax ? egnn_bwd_kernel<D, ACT, MEAN, false, true, RC>         \
               : egnn_bwd_kernel<D, ACT, MEAN, false, false, RC>))
-  auto k = save_planes == 3 ? GMP_BWD_K(0) : GMP_BWD_K(1);
-#undef GMP_BWD_K
+  auto k = save_planes == 3 ? LAUNCH_BWD_K(0) : LAUNCH_BWD_K(1);
+#undef LAUNCH_BWD_K
   int rc = prep_kernel(k, smem);
   if (rc) return rc;
   k<<<(unsigned)(W / kBwdWaves), kBwdWaves * 64, smem, s>>>(N, E, pos, rowptr, recv, send, P, W,
@@ -511,23 +511,16 @@ int prep_kernel_once(const void* k, size_t smem) {
   return rc;
 }
 
-// 1: the f32-MFMA (exact fmaf chain) products instead of the HF path; initial value from
-// GMP_EGNN_F32_MFMA, changed by gmp_egnn_set_f32_mfma
-int g_egnn_f32 = -1;
+// 1: the f32-MFMA (exact fmaf chain) products instead of the HF path (gmp_egnn_set_f32_mfma)
+int g_egnn_f32 = 0;
 
-bool egnn_f32() {
-  if (g_egnn_f32 < 0) {
-    const char* e = getenv("GMP_EGNN_F32_MFMA");
-    g_egnn_f32 = (e && atoi(e) != 0) ? 1 : 0;
-  }
-  return g_egnn_f32 == 1;
-}
+bool egnn_f32() { return g_egnn_f32 == 1; }
 
 }  // namespace gmp
 
 using namespace gmp;
 
-#define GMP_EGNN_DISPATCH(CALL)                                                                \
+#define LAUNCH_EGNN_DISPATCH(CALL)                                                                \
   do {                                                                                         \
     if (d == 128) {                                                                            \
       if (act == 0) { if (msg_mean) CALL(128, 0, true); else CALL(128, 0, false); }            \
@@ -572,11 +565,11 @@ int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const flo
   GMP_CHECK_ARG(AB && pos && recv && send && aligned16(AB) && aligned16(m_aggr));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
   GMP_CHECK_ARG(save_xhat == nullptr || aligned16(save_xhat));
-#define GMP_CALL_FWD(DD, AA, MM)                                                              \
+#define LAUNCH_CALL_FWD(DD, AA, MM)                                                              \
   rc = launch_fwd<DD, AA, MM>(n_nodes, n_edges, AB, pos, rowptr, recv, send, *params, ln_eps, \
                               m_aggr, pos_aggr, save_xhat, save_planes, save_rstd, s)
-  GMP_EGNN_DISPATCH(GMP_CALL_FWD);
-#undef GMP_CALL_FWD
+  LAUNCH_EGNN_DISPATCH(LAUNCH_CALL_FWD);
+#undef LAUNCH_CALL_FWD
   return rc;
 }
 
@@ -614,12 +607,12 @@ int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, cons
   GMP_CHECK_ARG(aligned16(save_xhat) && aligned16(dA) && aligned16(g_m_aggr) &&
                 aligned16(dpre1) && aligned16(dpre2) && aligned16(dpre3));
   GMP_CHECK_ARG(aligned16(params->W2) && aligned16(params->W3));
-#define GMP_CALL_BWD(DD, AA, MM)                                                              \
+#define LAUNCH_CALL_BWD(DD, AA, MM)                                                              \
   rc = launch_bwd<DD, AA, MM>(n_nodes, n_edges, pos, rowptr, recv, send, *params, save_xhat,  \
                               save_planes, save_rstd, g_m_aggr, g_pos_aggr, dA, dpos_recv,    \
                               dpre1, gdiff, dpre2, dpre3, vec_partials, amax, s)
-  GMP_EGNN_DISPATCH(GMP_CALL_BWD);
-#undef GMP_CALL_BWD
+  LAUNCH_EGNN_DISPATCH(LAUNCH_CALL_BWD);
+#undef LAUNCH_CALL_BWD
   return rc;
 }
 

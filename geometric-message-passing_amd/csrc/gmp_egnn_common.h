@@ -10,16 +10,12 @@ namespace gmp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// One workgroup per CU (W2 + W3 in LDS).  Forward: 12 waves (<= 168 VGPRs -> 3 per SIMD);
-// backward: 8 waves (<= 256 VGPRs -> 2 per SIMD).
+// One workgroup per CU (W2 + W3 in LDS).  Forward: 12 waves (<= 168 VGPRs -> 3 per SIMD; the HF
+// form fits since r05's static scales and fma_mix splits, 8 waves before); backward: 8 waves
+// (<= 256 VGPRs -> 2 per SIMD).
 constexpr int kFwdWaves = 12;
-#ifndef GMP_EGNN_HF_FWD_WAVES
-#define GMP_EGNN_HF_FWD_WAVES 12
-#endif
-// HF forward: 8 waves (<= 256 VGPRs -> 2 per SIMD): its products need fewer MFMA cycles but more
-// live registers (fp16 operand planes) than 168 allow without spills
 template <bool HF>
-constexpr int fwd_waves() { return HF ? GMP_EGNN_HF_FWD_WAVES : kFwdWaves; }
+constexpr int fwd_waves() { return kFwdWaves; }
 constexpr int kBwdWaves = 8;
 
 template <int D>
@@ -54,10 +50,7 @@ struct HCfg {
   // x_hat3 recompute are 2-way (the floor for 8-byte pieces of 16-byte-aligned rows).  r03 / r04
   // used d + 8 (272 B): 2-way / 4-way, 0.34 / 0.51 of the forward / backward LDS cycles in bank
   // conflicts (SQ counters, r04).
-#ifndef GMP_K4_LDH_PAD
-#define GMP_K4_LDH_PAD 16  // (8 = the r03 layout, for A/B builds)
-#endif
-  static constexpr int LDH = D + GMP_K4_LDH_PAD;
+  static constexpr int LDH = D + 16;
   static constexpr int PLANE = D * LDH;  // halfs
   static constexpr int MAT = 2 * PLANE;  // halfs per matrix (= floats for two matrices)
 };
@@ -300,10 +293,8 @@ __device__ __forceinline__ void store3_w(rsrc_t w, unsigned off, float a, float 
 }
 
 // ---------------------------------------------------------------------------------- MFMA GEMMs
-// GMP_GEMM_FENCE bounds how far the scheduler may hoist LDS operand reads (register pressure).
-#ifndef GMP_GEMM_FENCE
-#define GMP_GEMM_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
+// gemm_fence() bounds how far the scheduler may hoist LDS operand reads (register pressure).
+__device__ __forceinline__ void gemm_fence() { __builtin_amdgcn_sched_barrier(0); }
 // y[slot(o)] += sum_k W[o][k] x[slot(k)]   (W row-major [o][k] in LDS; lane i = edge = l & 15)
 // SPLIT > 1: the output tiles in SPLIT groups, so only T/SPLIT A rows are live at a time
 // (register pressure in the backward)
@@ -325,7 +316,7 @@ __device__ __forceinline__ void gemm_wx(const float* __restrict__ sW, const f32x
 #pragma unroll
         for (int t = 0; t < TS; ++t)
           y[t0 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][c], x[p][c], y[t0 + t], 0, 0, 0);
-      GMP_GEMM_FENCE();
+      gemm_fence();
     }
   }
 }
@@ -333,9 +324,7 @@ __device__ __forceinline__ void gemm_wx(const float* __restrict__ sW, const f32x
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#ifndef HF_TILES_PER_FENCE
-#define HF_TILES_PER_FENCE 2
-#endif
+constexpr int kTilesPerFence = 2;  // HF products: output tiles between scheduling fences
 
 // 2-plane fp16 split of 8 (already scaled) floats a[0..3], b[0..3]: hi = RNE fp16 of v, lo = RNE
 // fp16 of v - hi (exact in f32, so one rounding: bitwise (_Float16)(v - (float)hi)).  hi by
@@ -345,16 +334,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // VALU-write -> MFMA-operand wait the compiler does not insert after an asm statement
 // (cdna_hip_programming.md §5.7 item 2).
 __device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, h16x8& bh, h16x8& bl) {
-#ifdef K4_C_SPLIT
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float v = j < 4 ? a[j] : b[j - 4];
-    const _Float16 h = (_Float16)v;
-    bh[j] = h;
-    bl[j] = (_Float16)(v - (float)h);
-  }
-  return;
-#endif
   const h16x2 p0 = {(_Float16)a[0], (_Float16)a[1]}, p1 = {(_Float16)a[2], (_Float16)a[3]};
   const h16x2 p2 = {(_Float16)b[0], (_Float16)b[1]}, p3 = {(_Float16)b[2], (_Float16)b[3]};
   const unsigned u0 = __builtin_bit_cast(unsigned, p0), u1 = __builtin_bit_cast(unsigned, p1);
@@ -423,14 +402,14 @@ __device__ __forceinline__ void gemm_h2(const _Float16* __restrict__ hW, int sw,
     for (int t = 0; t < T; ++t) {
       // compiler-level fence: keeps the A reads from being hoisted ahead of the operand split
       // (and out of registers' reach) as a block
-      if (t % HF_TILES_PER_FENCE == 0) asm volatile("" ::: "memory");
+      if (t % kTilesPerFence == 0) asm volatile("" ::: "memory");
       const _Float16* row = hW + (16 * t + i) * H::LDH + 32 * p + 8 * g;
       const h16x8 ah = *reinterpret_cast<const h16x8*>(row);
       const h16x8 al = *reinterpret_cast<const h16x8*>(row + H::PLANE);
       f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, y[t], 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
       y[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
-      if (t % HF_TILES_PER_FENCE == HF_TILES_PER_FENCE - 1) GMP_GEMM_FENCE();  // bounds hoisted reads
+      if (t % kTilesPerFence == kTilesPerFence - 1) gemm_fence();  // bounds hoisted reads
     }
   }
 #pragma unroll
@@ -443,15 +422,13 @@ __device__ __forceinline__ void gemm_h2(const _Float16* __restrict__ hW, int sw,
 // scale-up / scale-down pass over the accumulators.  XS: x already carries 2^ex (relu: the
 // affine's pre-scaled vectors); otherwise (silu) it is scaled here.  Planes, operands and MFMA
 // order are gemm_h2's: bitwise the r04 products.
-#ifndef K4_PD
-#define K4_PD 1
-#endif
+constexpr int kOperandPrefetch = 1;  // LDS A-operand prefetch distance (k blocks) of gemm_h2s
 template <int D, bool XS>
 __device__ __forceinline__ void gemm_h2s(const _Float16* __restrict__ hW, int ex,
                                          const f32x4 (&x)[D / 16], f32x4 (&y)[D / 16], int i,
                                          int g) {
   using H = HCfg<D>;
-  constexpr int T = D / 16, PB = D / 32, NQ = PB * T, PD = K4_PD;
+  constexpr int T = D / 16, PB = D / 32, NQ = PB * T, PD = kOperandPrefetch;
   const float fx = ldexpf(1.f, ex);
   // the A operand (W planes) of step q + PD is read from LDS while step q's MFMAs run
   const _Float16* base = hW + i * H::LDH + 8 * g;
@@ -515,7 +492,7 @@ __device__ __forceinline__ void gemm_h2s_tr(const _Float16* __restrict__ hWt, in
     const _Float16* rowk = hWt + (32 * p + 4 * g + q) * H::LDH + 8 * c;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      if (t % HF_TILES_PER_FENCE == 0) asm volatile("" ::: "memory");
+      if (t % kTilesPerFence == 0) asm volatile("" ::: "memory");
       const _Float16* a0 = rowk + 32 * (t >> 1) + 4 * (t & 1);
       const _Float16* a1 = a0 + 16 * H::LDH;
       const h16x4 h0 = lds_tr16(a0), h1 = lds_tr16(a1);
@@ -525,7 +502,7 @@ __device__ __forceinline__ void gemm_h2s_tr(const _Float16* __restrict__ hWt, in
       f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, y[t], 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
       y[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
-      if (t % HF_TILES_PER_FENCE == HF_TILES_PER_FENCE - 1) GMP_GEMM_FENCE();
+      if (t % kTilesPerFence == kTilesPerFence - 1) gemm_fence();
     }
   }
 }
@@ -545,7 +522,7 @@ __device__ __forceinline__ void gemm_wtx(const float* __restrict__ sW, const f32
       for (int t = 0; t < T; ++t) a[t] = wrow[16 * t];
 #pragma unroll
       for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], gin[p][c], y[t], 0, 0, 0);
-      GMP_GEMM_FENCE();
+      gemm_fence();
     }
   }
 }

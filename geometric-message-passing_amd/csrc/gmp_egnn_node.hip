@@ -400,23 +400,23 @@ int gmp_egnn_node_fwd_f32(int64_t n_nodes, int64_t d, const float* h, const floa
   const unsigned char* img = reinterpret_cast<const unsigned char*>(image);
   int rc = GMP_OK;
   const bool ab = ab_out != nullptr, sv = save_xhat != nullptr, res = residual != 0;
-#define GMP_NODE4(DD, AA, RR, BB, SS)                                                       \
+#define LAUNCH_NODE4(DD, AA, RR, BB, SS)                                                       \
   rc = launch_node<DD, AA, RR, BB, SS>(n_nodes, h, m_aggr, P, img, ln_eps, h_out, ab_out, \
                                        save_xhat, save_rstd, s)
-#define GMP_NODE3(DD, AA)                                                               \
-  if (res) { if (ab) { if (sv) GMP_NODE4(DD, AA, true, true, true);                   \
-                       else GMP_NODE4(DD, AA, true, true, false); }                   \
-             else { if (sv) GMP_NODE4(DD, AA, true, false, true);                     \
-                    else GMP_NODE4(DD, AA, true, false, false); } }                   \
-  else { if (ab) { if (sv) GMP_NODE4(DD, AA, false, true, true);                      \
-                   else GMP_NODE4(DD, AA, false, true, false); }                      \
-         else { if (sv) GMP_NODE4(DD, AA, false, false, true);                        \
-                else GMP_NODE4(DD, AA, false, false, false); } }
-#define GMP_NODE2(DD) if (act == 0) { GMP_NODE3(DD, 0) } else { GMP_NODE3(DD, 1) }
-  if (d == 128) { GMP_NODE2(128) } else if (d == 64) { GMP_NODE2(64) } else { GMP_NODE2(32) }
-#undef GMP_NODE2
-#undef GMP_NODE3
-#undef GMP_NODE4
+#define LAUNCH_NODE3(DD, AA)                                                               \
+  if (res) { if (ab) { if (sv) LAUNCH_NODE4(DD, AA, true, true, true);                   \
+                       else LAUNCH_NODE4(DD, AA, true, true, false); }                   \
+             else { if (sv) LAUNCH_NODE4(DD, AA, true, false, true);                     \
+                    else LAUNCH_NODE4(DD, AA, true, false, false); } }                   \
+  else { if (ab) { if (sv) LAUNCH_NODE4(DD, AA, false, true, true);                      \
+                   else LAUNCH_NODE4(DD, AA, false, true, false); }                      \
+         else { if (sv) LAUNCH_NODE4(DD, AA, false, false, true);                        \
+                else LAUNCH_NODE4(DD, AA, false, false, false); } }
+#define LAUNCH_NODE2(DD) if (act == 0) { LAUNCH_NODE3(DD, 0) } else { LAUNCH_NODE3(DD, 1) }
+  if (d == 128) { LAUNCH_NODE2(128) } else if (d == 64) { LAUNCH_NODE2(64) } else { LAUNCH_NODE2(32) }
+#undef LAUNCH_NODE2
+#undef LAUNCH_NODE3
+#undef LAUNCH_NODE4
   return rc;
 }
 

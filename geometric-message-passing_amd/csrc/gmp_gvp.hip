@@ -28,7 +28,6 @@ constexpr int SE = 32;     // edge scalar channels
 constexpr int H0 = 48;     // first GVP hidden vector channels (33 padded)
 
 // LDS row strides (floats): +4 keeps the 16 rows of an A-operand read on distinct banks
-constexpr int LDS_S = S + V + 4;   // Ws of a GVP layer: (128 x 144)
 constexpr int LD128 = S + 4;
 constexpr int LD16 = V + 4;
 constexpr int LD32 = SE + 4;
@@ -139,63 +138,13 @@ __device__ __forceinline__ void vnorm(const f32x4 (&vh)[3][T], f32x4 (&vn)[T], f
 }
 
 // ------------------------------------------------------------------------------------------
-// Generic GVP (128, 16) -> (128, 16): LDS = Ws (128 x 144) | Wsv (16 x 128) | Wh | Wv | bs | bsv
+// Generic GVP (128, 16) -> (128, 16) weights and the per-edge forward state
 struct LayerW {
   const float *Ws, *bs, *Wsv, *bsv, *Wh, *Wv;
 };
-constexpr int kLayerSmem = S * LDS_S + V * LD128 + 2 * V * LD16 + S + V;
-
-__device__ void layer_to_lds(float* sm, const LayerW& P) {
-  float* sWs = sm;
-  float* sWsv = sWs + S * LDS_S;
-  float* sWh = sWsv + V * LD128;
-  float* sWv = sWh + V * LD16;
-  float* sbs = sWv + V * LD16;
-  float* sbsv = sbs + S;
-  for (int x = threadIdx.x; x < S * (S + V); x += blockDim.x) sWs[(x / (S + V)) * LDS_S + x % (S + V)] = P.Ws[x];
-  for (int x = threadIdx.x; x < V * S; x += blockDim.x) sWsv[(x / S) * LD128 + x % S] = P.Wsv[x];
-  for (int x = threadIdx.x; x < V * V; x += blockDim.x) {
-    sWh[(x / V) * LD16 + x % V] = P.Wh[x];
-    sWv[(x / V) * LD16 + x % V] = P.Wv[x];
-  }
-  for (int x = threadIdx.x; x < S; x += blockDim.x) sbs[x] = P.bs[x];
-  for (int x = threadIdx.x; x < V; x += blockDim.x) sbsv[x] = P.bsv[x];
-}
-
 struct LayerFwd {
   f32x4 vh[3][1], vn[1], sq[1], spre[S / 16], vpre[3][1], sg[1];
 };
-
-// forward of one GVP layer for this lane's edge; s is consumed
-__device__ __forceinline__ void layer_forward(const float* sm, f32x4 (&s)[S / 16], const f32x4 (&v)[3][1],
-                                              LayerFwd& F, int i, int g) {
-  const float* sWs = sm;
-  const float* sWsv = sWs + S * LDS_S;
-  const float* sWh = sWsv + V * LD128;
-  const float* sWv = sWh + V * LD16;
-  const float* sbs = sWv + V * LD16;
-  const float* sbsv = sbs + S;
-#pragma unroll
-  for (int x = 0; x < 3; ++x) {
-    zero(F.vh[x]);
-    gemm_wx<1, 1>(sWh, LD16, v[x], F.vh[x], i, g);
-  }
-  vnorm<1>(F.vh, F.vn, F.sq);
-  ld_vec<S / 16>(F.spre, sbs, g);
-  gemm_wx<S / 16, S / 16>(sWs, LDS_S, s, F.spre, i, g);
-  gemm_wx<S / 16, 1>(sWs + S, LDS_S, F.vn, F.spre, i, g);
-#pragma unroll
-  for (int x = 0; x < 3; ++x) {
-    zero(F.vpre[x]);
-    gemm_wx<1, 1>(sWv, LD16, F.vh[x], F.vpre[x], i, g);
-  }
-  f32x4 gate[1];
-  ld_vec<1>(gate, sbsv, g);
-  gemm_wx<1, S / 16>(sWsv, LD128, F.spre, gate, i, g);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) F.sg[0][q] = sigm(gate[0][q]);
-}
-
 struct Chunk {
   int64_t e;
   bool valid;
@@ -208,132 +157,12 @@ __device__ __forceinline__ Chunk chunk_edge(int64_t c, int i, int64_t E) {
   return k;
 }
 
-template <int ACT>
-__global__ __launch_bounds__(kGT) void gvp_layer_fwd_kernel(int64_t E, const float* __restrict__ s_in,
-                                                            const float* __restrict__ v_in, LayerW P,
-                                                            float* __restrict__ s_out,
-                                                            float* __restrict__ v_out) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  layer_to_lds(sm, P);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int64_t nchunks = (E + 15) / 16;
-  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
-  for (int64_t c = wave; c < nchunks; c += nwaves) {
-    const Chunk k = chunk_edge(c, i, E);
-    f32x4 s[S / 16], v[3][1];
-    ld_row<S / 16>(s, s_in + k.e * S, g);
-    ld_vrow<1>(v, v_in + k.e * (3 * V), g);
-    LayerFwd F;
-    layer_forward(sm, s, v, F, i, g);
-#pragma unroll
-    for (int x = 0; x < 3; ++x)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) F.vpre[x][0][q] *= F.sg[0][q];
-    if (ACT) {
-#pragma unroll
-      for (int p = 0; p < S / 16; ++p)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) F.spre[p][q] = fmaxf(F.spre[p][q], 0.f);
-    }
-    if (k.valid) {
-      st_row<S / 16>(s_out + k.e * S, F.spre, g);
-      st_vrow<1>(v_out + k.e * (3 * V), F.vpre, g);
-    }
-  }
-}
-
 // Backward: inputs s_in, v_in, ds_out, dv_out.  Outputs ds_in, dv_in and the weight-gradient
 // factors dspre (E,128), spre (E,128), dgate (E,16), vn (E,16), vh (E,48), dvpre (E,48),
 // dvh (E,48) (vector tensors in (channel, xyz) layout).
 struct LayerGrads {
   float *ds_in, *dv_in, *dspre, *spre, *dgate, *vn, *vh, *dvpre, *dvh;
 };
-
-template <int ACT>
-__global__ __launch_bounds__(kGT) void gvp_layer_bwd_kernel(int64_t E, const float* __restrict__ s_in,
-                                                            const float* __restrict__ v_in, LayerW P,
-                                                            const float* __restrict__ ds_out,
-                                                            const float* __restrict__ dv_out,
-                                                            LayerGrads O) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  layer_to_lds(sm, P);
-  __syncthreads();
-  const float* sWs = sm;
-  const float* sWsv = sWs + S * LDS_S;
-  const float* sWh = sWsv + V * LD128;
-  const float* sWv = sWh + V * LD16;
-  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int64_t nchunks = (E + 15) / 16;
-  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
-  for (int64_t c = wave; c < nchunks; c += nwaves) {
-    const Chunk k = chunk_edge(c, i, E);
-    f32x4 s[S / 16], v[3][1];
-    ld_row<S / 16>(s, s_in + k.e * S, g);
-    ld_vrow<1>(v, v_in + k.e * (3 * V), g);
-    LayerFwd F;
-    layer_forward(sm, s, v, F, i, g);
-    // ds (reuse s registers): dspre = ds_out * act'(spre)
-    ld_row<S / 16>(s, ds_out + k.e * S, g);
-    if (ACT) {
-#pragma unroll
-      for (int p = 0; p < S / 16; ++p)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s[p][q] = F.spre[p][q] > 0.f ? s[p][q] : 0.f;
-    }
-    // gate: vout = vpre * sg
-    f32x4 dv[3][1];
-    ld_vrow<1>(dv, dv_out + k.e * (3 * V), g);
-    f32x4 dgate[1];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float dsg = dv[0][0][q] * F.vpre[0][0][q] + dv[1][0][q] * F.vpre[1][0][q] + dv[2][0][q] * F.vpre[2][0][q];
-      dgate[0][q] = dsg * F.sg[0][q] * (1.f - F.sg[0][q]);
-#pragma unroll
-      for (int x = 0; x < 3; ++x) dv[x][0][q] *= F.sg[0][q];  // dvpre
-    }
-    gemm_wtx<S / 16, 1>(sWsv, LD128, dgate, s, i, g);  // dspre += Wsv^T dgate
-    if (k.valid) {
-      st_row<S / 16>(O.dspre + k.e * S, s, g);
-      if (O.spre) st_row<S / 16>(O.spre + k.e * S, F.spre, g);  // (optional: see gmp.h)
-      st_row<1>(O.dgate + k.e * V, dgate, g);
-      st_row<1>(O.vn + k.e * V, F.vn, g);
-      st_vrow<1>(O.vh + k.e * (3 * V), F.vh, g);
-      st_vrow<1>(O.dvpre + k.e * (3 * V), dv, g);
-    }
-    // ds_in = Ws_s^T dspre ; dvn = Ws_v^T dspre
-    f32x4 dsin[S / 16], dvn[1];
-    zero(dsin);
-    zero(dvn);
-    gemm_wtx<S / 16, S / 16>(sWs, LDS_S, s, dsin, i, g);
-    gemm_wtx<1, S / 16>(sWs + S, LDS_S, s, dvn, i, g);
-    if (k.valid) st_row<S / 16>(O.ds_in + k.e * S, dsin, g);
-    // dvh = Wv^T dvpre + dvn * vh / vn (where sum vh^2 > eps)
-    f32x4 dvh[3][1];
-#pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      zero(dvh[x]);
-      gemm_wtx<1, 1>(sWv, LD16, dv[x], dvh[x], i, g);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float f = F.sq[0][q] > 1e-8f ? dvn[0][q] / F.vn[0][q] : 0.f;
-#pragma unroll
-      for (int x = 0; x < 3; ++x) dvh[x][0][q] += f * F.vh[x][0][q];
-    }
-    if (k.valid) st_vrow<1>(O.dvh + k.e * (3 * V), dvh, g);
-    // dv_in = Wh^T dvh
-    f32x4 dvin[3][1];
-#pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      zero(dvin[x]);
-      gemm_wtx<1, 1>(sWh, LD16, dvh[x], dvin[x], i, g);
-    }
-    if (k.valid) st_vrow<1>(O.dv_in + k.e * (3 * V), dvin, g);
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // First message GVP: LDS = We (128 x 32) | Wn (128 x 48) | Wv0 (16 x 48) | Wsv0 (16 x 128) |
@@ -859,9 +688,6 @@ __global__ __launch_bounds__(kGT) void gvp_layer_bwd_x3_kernel(int64_t E, const 
   }
 }
 
-// GMP_GVP_X3=0: the layer kernels on the f32 MFMA only (A/B; exact fmaf chains)
-int g_gvp_x3 = getenv("GMP_GVP_X3") ? atoi(getenv("GMP_GVP_X3")) : 1;
-
 int64_t grid_for(int64_t E) {
   const int64_t chunks = ceil_div(E, (int64_t)16);
   int64_t b = ceil_div(chunks, (int64_t)(kGT / 64));
@@ -897,21 +723,10 @@ int gmp_gvp_layer_fwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   const unsigned G = (unsigned)grid_for(n_edges);
   hipStream_t s = as_stream(stream);
   int rc;
-  if (g_gvp_x3) {
-    const size_t smx = kLayerSmemX3 * sizeof(float);
-    auto k = relu ? gvp_layer_fwd_x3_kernel<1> : gvp_layer_fwd_x3_kernel<0>;
-    if ((rc = set_smem(k, smx))) return rc;
-    k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
-    return launch_status();
-  }
-  const size_t smem = kLayerSmem * sizeof(float);
-  if (relu) {
-    if ((rc = set_smem(gvp_layer_fwd_kernel<1>, smem))) return rc;
-    gvp_layer_fwd_kernel<1><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
-  } else {
-    if ((rc = set_smem(gvp_layer_fwd_kernel<0>, smem))) return rc;
-    gvp_layer_fwd_kernel<0><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
-  }
+  const size_t smx = kLayerSmemX3 * sizeof(float);
+  auto k = relu ? gvp_layer_fwd_x3_kernel<1> : gvp_layer_fwd_x3_kernel<0>;
+  if ((rc = set_smem(k, smx))) return rc;
+  k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, s_out, v_out);
   return launch_status();
 }
 
@@ -933,21 +748,10 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   const unsigned G = (unsigned)grid_for(n_edges);
   hipStream_t s = as_stream(stream);
   int rc;
-  if (g_gvp_x3) {
-    const size_t smx = kLayerSmemX3 * sizeof(float);
-    auto k = relu ? gvp_layer_bwd_x3_kernel<1> : gvp_layer_bwd_x3_kernel<0>;
-    if ((rc = set_smem(k, smx))) return rc;
-    k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
-    return launch_status();
-  }
-  const size_t smem = kLayerSmem * sizeof(float);
-  if (relu) {
-    if ((rc = set_smem(gvp_layer_bwd_kernel<1>, smem))) return rc;
-    gvp_layer_bwd_kernel<1><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
-  } else {
-    if ((rc = set_smem(gvp_layer_bwd_kernel<0>, smem))) return rc;
-    gvp_layer_bwd_kernel<0><<<G, kGT, smem, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
-  }
+  const size_t smx = kLayerSmemX3 * sizeof(float);
+  auto k = relu ? gvp_layer_bwd_x3_kernel<1> : gvp_layer_bwd_x3_kernel<0>;
+  if ((rc = set_smem(k, smx))) return rc;
+  k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
   return launch_status();
 }
 

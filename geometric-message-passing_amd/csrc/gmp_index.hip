@@ -477,13 +477,13 @@ int gmp_segment_reduce_f32(const float* src, int64_t n_items, int64_t F, const i
   if (S > 1 && workspace && workspace_bytes >= gmp_segment_reduce_workspace_size(n_items, n_seg, F, reduce)) {
     float* part = reinterpret_cast<float*>(workspace);
     const unsigned g = (unsigned)(n_seg * S);
-#define GMP_SPLIT(V, RED) segment_reduce_split<V, RED><<<g, 256, 0, s>>>(src, n_items, F, perm, rowptr, n_seg, S, part)
+#define LAUNCH_SPLIT(V, RED) segment_reduce_split<V, RED><<<g, 256, 0, s>>>(src, n_items, F, perm, rowptr, n_seg, S, part)
     if (reduce == GMP_REDUCE_SUM) {
-      if (vec == 4) GMP_SPLIT(4, GMP_REDUCE_SUM); else if (vec == 2) GMP_SPLIT(2, GMP_REDUCE_SUM); else GMP_SPLIT(1, GMP_REDUCE_SUM);
+      if (vec == 4) LAUNCH_SPLIT(4, GMP_REDUCE_SUM); else if (vec == 2) LAUNCH_SPLIT(2, GMP_REDUCE_SUM); else LAUNCH_SPLIT(1, GMP_REDUCE_SUM);
     } else {
-      if (vec == 4) GMP_SPLIT(4, GMP_REDUCE_MEAN); else if (vec == 2) GMP_SPLIT(2, GMP_REDUCE_MEAN); else GMP_SPLIT(1, GMP_REDUCE_MEAN);
+      if (vec == 4) LAUNCH_SPLIT(4, GMP_REDUCE_MEAN); else if (vec == 2) LAUNCH_SPLIT(2, GMP_REDUCE_MEAN); else LAUNCH_SPLIT(1, GMP_REDUCE_MEAN);
     }
-#undef GMP_SPLIT
+#undef LAUNCH_SPLIT
     int rc = launch_status();
     if (rc) return rc;
     if (reduce == GMP_REDUCE_SUM)
@@ -492,23 +492,23 @@ int gmp_segment_reduce_f32(const float* src, int64_t n_items, int64_t F, const i
       segment_split_finish<GMP_REDUCE_MEAN><<<grid_for(n_seg * F, 256), 256, 0, s>>>(part, rowptr, n_seg, S, F, out);
     return launch_status();
   }
-#define GMP_SEG_LAUNCH(VEC, RED)                                                            \
+#define LAUNCH_SEG_LAUNCH(VEC, RED)                                                            \
   segment_reduce_wave<VEC, RED><<<(unsigned)ceil_div(n_seg, 4), 256, 0, s>>>(              \
       src, n_items, F, perm, rowptr, n_seg, out, argmax)
-#define GMP_SEG_DISPATCH(RED)                                                               \
+#define LAUNCH_SEG_DISPATCH(RED)                                                               \
   do {                                                                                      \
     if (F < 4 && n_items < 64 * n_seg)                                                      \
       segment_reduce_thread<RED><<<grid_for(n_seg * F, 256), 256, 0, s>>>(                 \
           src, n_items, F, perm, rowptr, n_seg, out, argmax);                               \
-    else if (vec == 4) GMP_SEG_LAUNCH(4, RED);                                              \
-    else if (vec == 2) GMP_SEG_LAUNCH(2, RED);                                              \
-    else GMP_SEG_LAUNCH(1, RED);                                                            \
+    else if (vec == 4) LAUNCH_SEG_LAUNCH(4, RED);                                              \
+    else if (vec == 2) LAUNCH_SEG_LAUNCH(2, RED);                                              \
+    else LAUNCH_SEG_LAUNCH(1, RED);                                                            \
   } while (0)
-  if (reduce == GMP_REDUCE_SUM) GMP_SEG_DISPATCH(GMP_REDUCE_SUM);
-  else if (reduce == GMP_REDUCE_MEAN) GMP_SEG_DISPATCH(GMP_REDUCE_MEAN);
-  else GMP_SEG_DISPATCH(GMP_REDUCE_MAX);
-#undef GMP_SEG_DISPATCH
-#undef GMP_SEG_LAUNCH
+  if (reduce == GMP_REDUCE_SUM) LAUNCH_SEG_DISPATCH(GMP_REDUCE_SUM);
+  else if (reduce == GMP_REDUCE_MEAN) LAUNCH_SEG_DISPATCH(GMP_REDUCE_MEAN);
+  else LAUNCH_SEG_DISPATCH(GMP_REDUCE_MAX);
+#undef LAUNCH_SEG_DISPATCH
+#undef LAUNCH_SEG_LAUNCH
   return launch_status();
 }
 

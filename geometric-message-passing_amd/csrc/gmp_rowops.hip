@@ -427,18 +427,18 @@ int vec_norm_launch(int64_t rows, int64_t C, const float* v, const float* g, flo
                     hipStream_t s) {
   const int G = C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64;
   const unsigned grid = (unsigned)ceil_div(rows, (int64_t)(kRowT / 64) * (64 / G));
-#define GMP_VN(GG) \
+#define LAUNCH_VN(GG) \
   vec_norm_kernel<GG, BWD><<<grid, kRowT, 0, s>>>(rows, (int)C, v, g, out)
   switch (G) {
-    case 1: GMP_VN(1); break;
-    case 2: GMP_VN(2); break;
-    case 4: GMP_VN(4); break;
-    case 8: GMP_VN(8); break;
-    case 16: GMP_VN(16); break;
-    case 32: GMP_VN(32); break;
-    default: GMP_VN(64); break;
+    case 1: LAUNCH_VN(1); break;
+    case 2: LAUNCH_VN(2); break;
+    case 4: LAUNCH_VN(4); break;
+    case 8: LAUNCH_VN(8); break;
+    case 16: LAUNCH_VN(16); break;
+    case 32: LAUNCH_VN(32); break;
+    default: LAUNCH_VN(64); break;
   }
-#undef GMP_VN
+#undef LAUNCH_VN
   return launch_status();
 }
 
@@ -485,13 +485,13 @@ int gmp_ln_act_fwd_f32(int64_t rows, int64_t d, const float* x, const float* gam
   hipStream_t s = as_stream(stream);
   if (small_form(d)) {
     const unsigned gs = (unsigned)ceil_div(rows, (kRowT / 64) * (64 / d));
-#define GMP_LNF(A, D) \
+#define LAUNCH_LNF(A, D) \
   ln_act_fwd_small_kernel<A, D><<<gs, kRowT, 0, s>>>(rows, x, gamma, beta, eps, y, xhat_save, rstd_save)
-#define GMP_LNF_D(A) \
-  if (d == 8) GMP_LNF(A, 8); else if (d == 16) GMP_LNF(A, 16); else GMP_LNF(A, 32)
-    if (act == 0) { GMP_LNF_D(0); } else if (act == 1) { GMP_LNF_D(1); } else { GMP_LNF_D(2); }
-#undef GMP_LNF_D
-#undef GMP_LNF
+#define LAUNCH_LNF_D(A) \
+  if (d == 8) LAUNCH_LNF(A, 8); else if (d == 16) LAUNCH_LNF(A, 16); else LAUNCH_LNF(A, 32)
+    if (act == 0) { LAUNCH_LNF_D(0); } else if (act == 1) { LAUNCH_LNF_D(1); } else { LAUNCH_LNF_D(2); }
+#undef LAUNCH_LNF_D
+#undef LAUNCH_LNF
     return launch_status();
   }
   const unsigned grid = (unsigned)ceil_div(rows, kRowT / 64);
@@ -540,24 +540,24 @@ int gmp_ln_act_bwd_f32(int64_t rows, int64_t d, const float* grad_y, const float
   int rows_written = G;  // partial rows for sum_rows_kernel
   if (small_form(d) && grad_gamma_beta) {
     rows_written = vec_blocks(rows);
-#define GMP_LNS(A, D)                                                                 \
+#define LAUNCH_LNS(A, D)                                                                 \
   ln_act_bwd_small_kernel<A, D><<<rows_written, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, \
                                                                beta, grad_x, part)
-#define GMP_LNS_D(A) \
-  if (d == 8) GMP_LNS(A, 8); else if (d == 16) GMP_LNS(A, 16); else GMP_LNS(A, 32)
-    if (act == 0) { GMP_LNS_D(0); } else if (act == 1) { GMP_LNS_D(1); } else { GMP_LNS_D(2); }
-#undef GMP_LNS_D
-#undef GMP_LNS
+#define LAUNCH_LNS_D(A) \
+  if (d == 8) LAUNCH_LNS(A, 8); else if (d == 16) LAUNCH_LNS(A, 16); else LAUNCH_LNS(A, 32)
+    if (act == 0) { LAUNCH_LNS_D(0); } else if (act == 1) { LAUNCH_LNS_D(1); } else { LAUNCH_LNS_D(2); }
+#undef LAUNCH_LNS_D
+#undef LAUNCH_LNS
   } else if (vec_form(d) && grad_gamma_beta && al % (d / 16) == 0) {
     rows_written = vec_blocks(rows);
-#define GMP_LNV(A, F)                                                                \
+#define LAUNCH_LNV(A, F)                                                                \
   ln_act_bwd_vec_kernel<A, F><<<rows_written, kRowT, 0, s>>>(rows, grad_y, xhat, rstd, gamma, \
                                                              beta, grad_x, part)
-#define GMP_LNV_F(A) \
-  if (d == 64) GMP_LNV(A, 1); else if (d == 128) GMP_LNV(A, 2); else GMP_LNV(A, 4)
-    if (act == 0) { GMP_LNV_F(0); } else if (act == 1) { GMP_LNV_F(1); } else { GMP_LNV_F(2); }
-#undef GMP_LNV_F
-#undef GMP_LNV
+#define LAUNCH_LNV_F(A) \
+  if (d == 64) LAUNCH_LNV(A, 1); else if (d == 128) LAUNCH_LNV(A, 2); else LAUNCH_LNV(A, 4)
+    if (act == 0) { LAUNCH_LNV_F(0); } else if (act == 1) { LAUNCH_LNV_F(1); } else { LAUNCH_LNV_F(2); }
+#undef LAUNCH_LNV_F
+#undef LAUNCH_LNV
   } else if (act == 0) {
     ln_act_bwd_kernel<0><<<G, kRowT, 0, s>>>(rows, (int)d, grad_y, xhat, rstd, gamma, beta,
                                              grad_x, part);

@@ -323,13 +323,13 @@ int sc_launch(int64_t n_nodes, int channels, const float* x, const float* A1, co
 int sc_dispatch(int64_t n_nodes, int channels, int dim, int corr, const float* x,
                 const float* A1, const float* A2, const float* A3, const float* A4, float* out,
                 const float* gout, float* dx, float* dA_partials, hipStream_t s) {
-#define GMP_SC(DD, CR)                                                                     \
+#define LAUNCH_SC(DD, CR)                                                                     \
   if (dim == DD && corr == CR)                                                             \
     return sc_launch<DD, CR>(n_nodes, channels, x, A1, A2, A3, A4, out, gout, dx, dA_partials, s);
-  GMP_SC(9, 1) GMP_SC(9, 2) GMP_SC(9, 3) GMP_SC(9, 4)
-  GMP_SC(4, 1) GMP_SC(4, 2) GMP_SC(4, 3) GMP_SC(4, 4)
-  GMP_SC(16, 1) GMP_SC(16, 2) GMP_SC(16, 3)
-#undef GMP_SC
+  LAUNCH_SC(9, 1) LAUNCH_SC(9, 2) LAUNCH_SC(9, 3) LAUNCH_SC(9, 4)
+  LAUNCH_SC(4, 1) LAUNCH_SC(4, 2) LAUNCH_SC(4, 3) LAUNCH_SC(4, 4)
+  LAUNCH_SC(16, 1) LAUNCH_SC(16, 2) LAUNCH_SC(16, 3)
+#undef LAUNCH_SC
   return GMP_ERR_UNSUPPORTED;
 }
 

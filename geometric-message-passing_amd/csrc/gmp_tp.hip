@@ -653,15 +653,15 @@ __device__ __forceinline__ void z_bwd_path(const Path& P, const float* __restric
 }
 
 // (l1, l2, lo) with l <= 3 and |l1 - l2| <= lo <= l1 + l2 (every triangle, any parities): the
-// l <= 2 paths (GMP_Z_PATHS2) and those with an l = 3 (GMP_Z_PATHS3)
-#define GMP_Z_PATHS3(X)                                                                        \
+// l <= 2 paths (LAUNCH_Z_PATHS2) and those with an l = 3 (LAUNCH_Z_PATHS3)
+#define LAUNCH_Z_PATHS3(X)                                                                        \
   X(0, 3, 3) X(1, 2, 3) X(1, 3, 2) X(1, 3, 3) X(2, 1, 3) X(2, 2, 3) X(2, 3, 1) X(2, 3, 2)      \
   X(2, 3, 3) X(3, 0, 3) X(3, 1, 2) X(3, 1, 3) X(3, 2, 1) X(3, 2, 2) X(3, 2, 3) X(3, 3, 0)      \
   X(3, 3, 1) X(3, 3, 2) X(3, 3, 3)
 
 // the l <= 2 subset (LM = 2 kernels: the l = 3 cases compiled out, so their registers are too --
 // MACE-128 / TFN max_ell = 2: 59 instead of 91 VGPRs for z, 5 -> 8 waves per SIMD)
-#define GMP_Z_PATHS2(X)                                                                        \
+#define LAUNCH_Z_PATHS2(X)                                                                        \
   X(0, 0, 0) X(0, 1, 1) X(0, 2, 2) X(1, 0, 1) X(1, 1, 0) X(1, 1, 1) X(1, 1, 2) X(1, 2, 1)      \
   X(1, 2, 2) X(2, 0, 2) X(2, 1, 1) X(2, 1, 2) X(2, 2, 0) X(2, 2, 1) X(2, 2, 2)
 
@@ -696,16 +696,16 @@ __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
       const float* C = sC + P.cg_off;
       float* zr = zbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
       switch (P.l1 * 16 + P.l2 * 4 + P.lo) {
-#define GMP_Z_CASE(A, B, O) \
+#define LAUNCH_Z_CASE(A, B, O) \
   case A * 16 + B * 4 + O: z_path<A, B, O>(P, C, Y, xrow, zr, lane); break;
-        GMP_Z_PATHS2(GMP_Z_CASE)
-#undef GMP_Z_CASE
-#define GMP_Z_CASE3(A, B, O)                                                 \
+        LAUNCH_Z_PATHS2(LAUNCH_Z_CASE)
+#undef LAUNCH_Z_CASE
+#define LAUNCH_Z_CASE3(A, B, O)                                                 \
   case A * 16 + B * 4 + O:                                                   \
     if constexpr (LM == 3) z_path<A, B, O>(P, C, Y, xrow, zr, lane);         \
     break;
-        GMP_Z_PATHS3(GMP_Z_CASE3)
-#undef GMP_Z_CASE3
+        LAUNCH_Z_PATHS3(LAUNCH_Z_CASE3)
+#undef LAUNCH_Z_CASE3
         default: break;
       }
     }
@@ -776,16 +776,16 @@ __global__ __launch_bounds__(256) void tp_edge_z2_bwd_kernel(
       const float* dzr =
           dzbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
       switch (P.l1 * 16 + P.l2 * 4 + P.lo) {
-#define GMP_ZB_CASE(A, B, O) \
+#define LAUNCH_ZB_CASE(A, B, O) \
   case A * 16 + B * 4 + O: z_bwd_path<A, B, O>(P, C, Y, xrow, dzr, dx, dyp, lane); break;
-        GMP_Z_PATHS2(GMP_ZB_CASE)
-#undef GMP_ZB_CASE
-#define GMP_ZB_CASE3(A, B, O)                                                          \
+        LAUNCH_Z_PATHS2(LAUNCH_ZB_CASE)
+#undef LAUNCH_ZB_CASE
+#define LAUNCH_ZB_CASE3(A, B, O)                                                          \
   case A * 16 + B * 4 + O:                                                             \
     if constexpr (LM == 3) z_bwd_path<A, B, O>(P, C, Y, xrow, dzr, dx, dyp, lane);     \
     break;
-        GMP_Z_PATHS3(GMP_ZB_CASE3)
-#undef GMP_ZB_CASE3
+        LAUNCH_Z_PATHS3(LAUNCH_ZB_CASE3)
+#undef LAUNCH_ZB_CASE3
         default: break;
       }
     };
@@ -1000,12 +1000,8 @@ __global__ __launch_bounds__(256) void tp_edge_z_gen_bwd_kernel(
   }
 }
 
-// GMP_TP_Z_GENERIC=1: always the l <= 3 instantiation.  r03 A/B: the l <= 2 instantiation (z 59
-// vs 91 VGPRs, 8 vs 5 waves per SIMD; dz 187 vs 249, and a 168-VGPR / 3-wave cap with 52 B of
-// scratch) measured within noise on the MACE / TFN steps (481.5 / 483.3 / 483.7 k; 998 / 994 /
-// 1,009 k edges/s): these kernels are not occupancy-bound
-int g_z_generic = getenv("GMP_TP_Z_GENERIC") ? atoi(getenv("GMP_TP_Z_GENERIC")) : 0;
-
+// The l <= 2 instantiation (z 59 vs 91 VGPRs, 8 vs 5 waves per SIMD) measured within noise of
+// the l <= 3 one on the MACE / TFN steps (r03); kept as the tighter-register form.
 int64_t z2_blocks(int64_t edges) {
   const int64_t cap = (int64_t)device_cu_count() * 8;  // 32 resident waves per CU
   int64_t g = (edges + 3) / 4;
@@ -1101,7 +1097,7 @@ int gmp_tp_edge_z_lmax_f32(const void* desc_host, int l_max, const void* paths_d
   if (l_max > 3 || d.sh_dim > kMaxSh)
     tp_edge_z_gen_kernel<<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
-  else if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
+  else if (l_max <= 2 && d.sh_dim <= 9)
     tp_edge_z2_kernel<2><<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, zbuf);
   else
@@ -1133,7 +1129,7 @@ int gmp_tp_edge_z_bwd_lmax_f32(const void* desc_host, int l_max, const void* pat
     tp_edge_z_gen_bwd_kernel<<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
         dx_edge, dY_edge);
-  else if (l_max <= 2 && d.sh_dim <= 9 && !g_z_generic)
+  else if (l_max <= 2 && d.sh_dim <= 9)
     tp_edge_z2_bwd_kernel<2><<<grid, 256, 0, as_stream(stream)>>>(
         d, (const Path*)paths_dev, cg_dev, cg_len, x, sh, src_sorted, perm, e0, e1, dzbuf,
         dx_edge, dY_edge);

@@ -376,7 +376,7 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_kernel(
   load_a(F[0], smg);
   __syncthreads();  // every wave holds stage 0's fragments: buffer 0 may be rewritten
   // optional static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per
-  // SIMD, item 4); A/B knob GMP_GEMM_PRIO
+  // SIMD, item 4); kGemmPrio
   if ((prio & 1) && w >= 4) __builtin_amdgcn_s_setprio(1);
   // prio bit 1 (A/B): waves 4-7, the SIMD partners of waves 0-3, run each stage's MFMAs before
   // its split / LDS stash, so one wave of a SIMD pair splits while the other multiplies
@@ -636,142 +636,15 @@ __global__ __launch_bounds__(256) void tp_split_w2_kernel(int mul1, int mo, int 
   }
 }
 
-// Row-level Linears (short k, many rows: the node / edge Linears of the EGNN update MLP and
-// message projections, 50k-1M rows, K <= 256, N <= 256): C = [A1 | A2] B^T (+ bias) with the
-// WHOLE k range of a BM-row block loaded in one burst (no k pipeline: at K <= 256 the K7g
-// tile's stage-by-stage ring was latency-bound, 36 us for 50k x 128 x 128), split once into a
-// three-plane LDS image, and B fragments (split_x3, fragment order) from L2, two k steps ahead.
-// 256 threads; wave w owns columns [w N/4, (w+1) N/4) (CT 16-column tiles) of all BM rows.
-// LDS image: [plane][row][K bf16], 16-byte chunk c of a row at c ^ (row & 15): the 16 rows of
-// an MFMA A-fragment read hit 16 distinct 4-bank groups.
-template <int BM, int CT, int KMAX>
-__global__ __launch_bounds__(256) void row_gemm_x3_kernel(
-    int64_t M, int N, int K1, const float* __restrict__ A1, int64_t lda1, int K2,
-    const float* __restrict__ A2, int64_t lda2, const unsigned short* __restrict__ Bp,
-    const float* __restrict__ bias, float* __restrict__ C, int64_t ldc, int accumulate) {
-  constexpr int RT = BM / 16;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smr[];
-  const int K = K1 + K2, RB = 2 * K;  // row bytes of one plane image
-  const int PL = BM * RB;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 15, g = lane >> 4;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
-  // A block -> planes (rows past M are zero)
-  const int K4 = K >> 2;
-  for (int v = tid; v < BM * K4; v += 256) {
-    const int row = v / K4, c4 = v - row * K4, k = 4 * c4;
-    const int64_t gr = m0 + row;
-    f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (gr < M)
-      x = k < K1 ? *reinterpret_cast<const f32x4*>(A1 + gr * lda1 + k)
-                 : *reinterpret_cast<const f32x4*>(A2 + gr * lda2 + (k - K1));
-    unsigned pl[3][2];
-    split_planes<3>(x, 1.f, pl);
-    const int off = row * RB + 16 * ((k >> 3) ^ (row & 15)) + 8 * ((k >> 2) & 1);
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      *reinterpret_cast<u32x2*>(smr + p * PL + off) = u32x2{pl[p][0], pl[p][1]};
-  }
-  const int ct_total = N >> 4, ct0 = w * CT;
-  const int nks = K >> 5;
-  const unsigned short* bl = Bp + 8 * lane;
-  u32x4 rb[2][CT][3];
-  auto fetch_b = [&](int slot, int ks) {
-    const int kc = ks < nks ? ks : nks - 1;
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        rb[slot][c][p] = *reinterpret_cast<const u32x4*>(
-            bl + (((int64_t)kc * ct_total + ct0 + c) * 3 + p) * 512);
-  };
-  f32x4 acc[RT][CT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int c = 0; c < CT; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  fetch_b(0, 0);
-  fetch_b(1, 1);
-  __syncthreads();
-  auto step = [&](const int sl, int ks) {  // sl: a literal at both call sites (static slots)
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int row = 16 * r + li;
-      const int off = row * RB + 16 * ((4 * ks + g) ^ (row & 15));
-      u32x4 a[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const u32x4*>(smr + p * PL + off);
-#pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        f32x4 t = acc[r][c];
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(a[2]), asb(rb[sl][c][0]), t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(a[1]), asb(rb[sl][c][1]), t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(a[0]), asb(rb[sl][c][2]), t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(a[1]), asb(rb[sl][c][0]), t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(a[0]), asb(rb[sl][c][1]), t, 0, 0, 0);
-        acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asb(a[0]), asb(rb[sl][c][0]), t, 0, 0, 0);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    fetch_b(sl, ks + 2);  // the slot the MFMAs above just read
-  };
-  for (int ks = 0; ks < nks; ks += 2) {
-    step(0, ks);
-    if (ks + 1 < nks) step(1, ks + 1);
-  }
-  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + q
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    const int col = 16 * (ct0 + c) + li;
-    const float bv = bias ? bias[col] : 0.f;
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t row = m0 + 16 * r + 4 * g + q;
-        if (row < M) {
-          float* dst = C + row * ldc + col;
-          *dst = (accumulate ? *dst : 0.f) + acc[r][c][q] + bv;
-        }
-      }
-  }
-}
-
-// Planes of a general operand for the C = A B^T kernel: element (n, k) = src[n sn + k sk]
-// (sn = K, sk = 1: B row-major, e.g. a Linear weight W (out, in) for y = x W^T; sn = 1, sk = N:
-// its transpose, for dx = g W), written in fragment order (bfrag_index).  One thread per
-// element (the weights are KB-sized: one small launch per pass).
-__global__ __launch_bounds__(256) void split_x3_kernel(int64_t N, int64_t K,
-                                                       const float* __restrict__ src, int64_t sn,
-                                                       int64_t sk,
-                                                       unsigned short* __restrict__ Bp) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= N * K) return;
-  const int64_t n = x / K, k = x - n * K;
-  unsigned p[3];
-  split3(f32x2{src[n * sn + k * sk], 0.f}, p[0], p[1], p[2]);
-#pragma unroll
-  for (int q = 0; q < 3; ++q) Bp[bfrag_index(q, n, k, N / 16, 3)] = (unsigned short)p[q];
-}
-
 }  // namespace
 }  // namespace gmp
 
 using namespace gmp;
 
-namespace gmp {
-// forward path GEMM: A-stream register ring depth (GMP_TPGEMM_RING=2: the r02 form)
-int g_tpgemm_ring = getenv("GMP_TPGEMM_RING") ? atoi(getenv("GMP_TPGEMM_RING")) : 8;
-// T GEMM (widen): B-stream register ring depth (GMP_TPGEMM_WIDEN_RING=2: the r02 form)
-int g_widen_ring = getenv("GMP_TPGEMM_WIDEN_RING") ? atoi(getenv("GMP_TPGEMM_WIDEN_RING")) : 4;
-// forward path GEMM: the 256 x 64 tile for mul_out <= 64 (GMP_TPGEMM_NARROW=0: 128 x 128)
-int g_tpgemm_narrow = getenv("GMP_TPGEMM_NARROW") ? atoi(getenv("GMP_TPGEMM_NARROW")) : 1;
-// forward path GEMM schedule (GMP_GEMM_PRIO): bit 0 s_setprio 1 for waves 4-7, bit 1 waves 4-7
-// run their MFMAs before the stage's split / stash.  MACE-128 lo = 2 shape, one box: 0: 12.80 /
-// 12.73 ms, 2: 12.50, 3: 12.43 (default)
-int g_gemm_prio = getenv("GMP_GEMM_PRIO") ? atoi(getenv("GMP_GEMM_PRIO")) : 3;
-}  // namespace gmp
+// forward path GEMM schedule: s_setprio 1 for waves 4-7 (bit 0), and waves 4-7 run their MFMAs
+// before the stage's split / stash (bit 1).  MACE-128 lo = 2 shape, one box: 0: 12.80 / 12.73 ms,
+// 2: 12.50, 3: 12.43
+constexpr int kGemmPrio = 3;
 
 template <int NP>
 int split_w2_launch(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p, const float* b2p,
@@ -803,7 +676,7 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A1) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
   GMP_CHECK_ARG(K2 == 0 || reinterpret_cast<uintptr_t>(A2) % 16 == 0);
   // narrow outputs (mul_out <= 64: C5's 64-channel paths) take the 256 x 64 tile
-  const bool narrow = N <= 64 && g_tpgemm_narrow;
+  const bool narrow = N <= 64;
   const int64_t bm = narrow ? 256 : 128, bn = narrow ? 64 : 128;
   const int64_t tiles_m = ceil_div(M, bm), tiles_n = ceil_div(N, bn);
   GMP_CHECK_ARG(tiles_m < (1LL << 31) && tiles_n < (1LL << 31));
@@ -819,14 +692,8 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   } else if (narrow) {  // 4 A units per thread: a 4-deep ring holds the same bytes as 8 x 2
     k = accumulate ? tp_gemm_x3_kernel<true, 4, 2, 4> : tp_gemm_x3_kernel<false, 4, 2, 4>;
   } else {
-    k = g_tpgemm_ring == 44  ? (accumulate ? tp_gemm_x3_kernel<true, 4, 4, 2>
-                                           : tp_gemm_x3_kernel<false, 4, 4, 2>)
-        : g_tpgemm_ring >= 8 ? (accumulate ? tp_gemm_x3_kernel<true, 8, 2, 2>
-                                           : tp_gemm_x3_kernel<false, 8, 2, 2>)
-        : g_tpgemm_ring >= 4 ? (accumulate ? tp_gemm_x3_kernel<true, 4, 2, 2>
-                                           : tp_gemm_x3_kernel<false, 4, 2, 2>)
-                             : (accumulate ? tp_gemm_x3_kernel<true, 2, 2, 2>
-                                           : tp_gemm_x3_kernel<false, 2, 2, 2>);
+    // an 8-deep A-stream register ring (r02's 2-deep form measured slower)
+    k = accumulate ? tp_gemm_x3_kernel<true, 8, 2, 2> : tp_gemm_x3_kernel<false, 8, 2, 2>;
   }
   if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
                                           hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -835,7 +702,7 @@ int gemm_launch(int64_t M, int64_t N, int64_t K1, const float* A1, int64_t lda1,
   k<<<(unsigned)nwg, kGT, smem, as_stream(stream)>>>(
       M, (int)N, K1, A1, lda1, K2, K2 ? A2 : A1, K2 ? lda2 : lda1,
       static_cast<const unsigned short*>(Bp), ldb, bplane, C, cgrp, cldg, cldr, cldn,
-      (int)tiles_m, (int)tiles_n, bias, g_gemm_prio);
+      (int)tiles_m, (int)tiles_n, bias, kGemmPrio);
   return launch_status();
 }
 
@@ -864,10 +731,9 @@ int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
   hipStream_t s = as_stream(stream);
   const unsigned short* B = static_cast<const unsigned short*>(Bp);
   int rc = 0;
-#define GMP_WN(NK)                                                                               \
+#define LAUNCH_WN(NK)                                                                               \
   {                                                                                              \
-    auto k = g_widen_ring >= 4 ? tp_gemm_x3_widen_kernel<NK, NP, 4>                              \
-                               : tp_gemm_x3_widen_kernel<NK, NP, 2>;                             \
+    auto k = tp_gemm_x3_widen_kernel<NK, NP, 4>;                                                 \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                      \
                                             hipFuncAttributeMaxDynamicSharedMemorySize,         \
                                             (int)smem))))                                        \
@@ -876,23 +742,16 @@ int widen_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
                                        (int)tiles_n, (int)n_split, amax, wmax);                  \
   }
   switch (nks) {
-    case 1: GMP_WN(1) break;
-    case 2: GMP_WN(2) break;
-    case 3: GMP_WN(3) break;
-    default: GMP_WN(4) break;
+    case 1: LAUNCH_WN(1) break;
+    case 2: LAUNCH_WN(2) break;
+    case 3: LAUNCH_WN(3) break;
+    default: LAUNCH_WN(4) break;
   }
-#undef GMP_WN
+#undef LAUNCH_WN
   return launch_status();
 }
 
 extern "C" {
-
-int gmp_tp_gemm_set_rings(int a_ring, int b_ring) {
-  const int old = g_tpgemm_ring * 16 + g_widen_ring;
-  g_tpgemm_ring = a_ring;
-  g_widen_ring = b_ring;
-  return old;
-}
 
 int gmp_tp_split_w2_f32(int64_t mul1, int64_t mul_out, int64_t H, const float* W2p,
                         const float* b2p, void* Bf, void* Bt, void* stream) {
@@ -905,55 +764,6 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
                        int64_t cldn, int accumulate, void* stream) {
   return gemm_launch(M, N, K1, A1, lda1, K2, A2, lda2, Bp, ldb, bplane, C, cgrp, cldg, cldr,
                      cldn, accumulate, stream);
-}
-
-int gmp_split_x3_f32(int64_t N, int64_t K, const float* B, int64_t sn, int64_t sk, void* Bp,
-                     void* stream) {
-  GMP_CHECK_ARG(N >= 0 && K >= 0 && N % 16 == 0 && K % kBK == 0);
-  if (N == 0 || K == 0) return GMP_OK;
-  GMP_CHECK_ARG(B && Bp && sn >= 0 && sk >= 0);
-  split_x3_kernel<<<(unsigned)ceil_div(N * K, 256), 256, 0, as_stream(stream)>>>(
-      N, K, B, sn, sk, static_cast<unsigned short*>(Bp));
-  return launch_status();
-}
-
-int gmp_gemm_x3_f32(int64_t M, int64_t N, const float* A1, int64_t K1, int64_t lda1,
-                    const float* A2, int64_t K2, int64_t lda2, const void* Bp, const float* bias,
-                    float* C, int64_t ldc, int accumulate, void* stream) {
-  GMP_CHECK_ARG(ldc >= N);
-  const int64_t K = K1 + K2;
-  if (K <= 256 && (N == 64 || N == 128 || N == 256) && M > 0) {
-    // short k: the row-block kernel (whole k range in one load burst)
-    GMP_CHECK_ARG(A1 && Bp && C && K1 % 32 == 0 && K2 % 32 == 0 && K > 0 && (K2 == 0 || A2));
-    GMP_CHECK_ARG(lda1 >= K1 && lda1 % 4 == 0 && (K2 == 0 || (lda2 >= K2 && lda2 % 4 == 0)));
-    GMP_CHECK_ARG(((reinterpret_cast<uintptr_t>(A1) | reinterpret_cast<uintptr_t>(Bp)) % 16) == 0);
-    GMP_CHECK_ARG(K2 == 0 || reinterpret_cast<uintptr_t>(A2) % 16 == 0);
-    const int bm = K <= 128 ? 64 : 32;  // LDS image 3 x bm x 2K bytes: 48 KB either way
-    const size_t smem = (size_t)3 * bm * 2 * K;
-    const int64_t nb = ceil_div(M, bm);
-    GMP_CHECK_ARG(nb < (1LL << 31));
-    int rc = 0;
-#define GMP_RG(BMV, CTV)                                                                         \
-  {                                                                                              \
-    auto k = row_gemm_x3_kernel<BMV, CTV, 256>;                                                  \
-    if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                      \
-                                            hipFuncAttributeMaxDynamicSharedMemorySize,         \
-                                            (int)smem))))                                        \
-      return rc;                                                                                 \
-    k<<<(unsigned)nb, 256, smem, as_stream(stream)>>>(                                           \
-        M, (int)N, (int)K1, A1, lda1, (int)K2, K2 ? A2 : A1, K2 ? lda2 : lda1,                  \
-        static_cast<const unsigned short*>(Bp), bias, C, ldc, accumulate);                       \
-  }
-    if (bm == 64) {
-      if (N == 64) GMP_RG(64, 1) else if (N == 128) GMP_RG(64, 2) else GMP_RG(64, 4)
-    } else {
-      if (N == 64) GMP_RG(32, 1) else if (N == 128) GMP_RG(32, 2) else GMP_RG(32, 4)
-    }
-#undef GMP_RG
-    return launch_status();
-  }
-  return gemm_launch(M, N, K1, A1, lda1, K2, A2, lda2, Bp, K1 + K2, N * (K1 + K2), C, M > 0 ? M : 1,
-                     0, ldc, 1, accumulate, stream, bias);
 }
 
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,

@@ -580,9 +580,7 @@ constexpr int kV3Plane = 32 * 128;             // one plane of a wave's slab: 32
 constexpr int kV3Slab = 3 * kV3Plane;          // a wave's transposition slab
 constexpr int kV3Red = 4 * 4 * 64 * 16;        // [wave][tile][lane] f32x4 partials
 constexpr int kV3Smem = 4 * kV3Slab + 2 * kV3Red;
-#ifndef GMP_V3_ZD
-#define GMP_V3_ZD 1
-#endif
+constexpr int kV3Zd = 1;
 
 // byte offset of (row, bf16 column jc) in a slab plane: 16-byte chunk jc / 8 XOR f(row) with
 // f = (row & 7) ^ ((row & 8) >> 1) -- rows 0..7 of a ds_write_b128 lane group hit 8 distinct
@@ -788,19 +786,9 @@ using namespace gmp;
 
 namespace gmp {
 // apply kernel: 2 = v3 (per-wave j quarters, T straight to registers; default where the shape
-// allows), 1 = v2 (bf16x3, shared LDS image), 0 = the f32-MFMA kernel.  GMP_TP_APPLY=f32|x3|v3,
-// gmp_tp_apply_set_x3(mode) for A/B studies (GMP_TP_APPLY_F32=1: the f32 kernel, as before)
-int g_apply_x3 = getenv("GMP_TP_APPLY_F32") && atoi(getenv("GMP_TP_APPLY_F32"))
-                     ? 0
-                     : (getenv("GMP_TP_APPLY") ? (strcmp(getenv("GMP_TP_APPLY"), "f32") == 0
-                                                      ? 0
-                                                      : strcmp(getenv("GMP_TP_APPLY"), "x3") == 0
-                                                            ? 1
-                                                            : 2)
-                                               : 2);
-// S kernel stores through LDS (GMP_TP_OUTER_STAGE=0: direct MFMA-layout stores)
-int g_outer_stage = getenv("GMP_TP_OUTER_STAGE") ? atoi(getenv("GMP_TP_OUTER_STAGE")) : 1;
-int g_outer_cs = getenv("GMP_TP_OUTER_CS") ? atoi(getenv("GMP_TP_OUTER_CS")) : 2;
+// allows), 1 = v2 (bf16x3, shared LDS image), 0 = the f32-MFMA kernel (gmp_tp_apply_set_x3:
+// the tests run every form)
+int g_apply_x3 = 2;
 }  // namespace gmp
 
 extern "C" {
@@ -814,23 +802,17 @@ int gmp_tp_apply_set_x3(int on) {
 
 int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                           const float* Z, const float* A, float* S, float* Sb, void* stream) {
-  float* rmax = nullptr;  // (the per-row maxima of the retired H2 path GEMM: template arm kept)
   GMP_CHECK_ARG(n_recv >= 0 && w > 0 && H > 0 && H <= kMaxH && H % 16 == 0);
   GMP_CHECK_ARG(n_recv <= 65535 * 1024);
   if (n_recv == 0) return GMP_OK;
-  GMP_CHECK_ARG(eoff && Z && A && S && Sb && (!rmax || w % 16 == 0));
+  GMP_CHECK_ARG(eoff && Z && A && S && Sb);
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0);
   if (n_recv > 65535) return GMP_ERR_UNSUPPORTED;  // grid.y limit: caller chunks receivers
-  // two column parts for wide H without row maxima (GMP_TP_OUTER_CS=1: one)
-  const int cs = (!rmax && H == kMaxH && g_outer_cs == 2) ? 2 : 1;
+  // two column parts for the widest H; S stored through LDS
+  const int cs = H == kMaxH ? 2 : 1;
   const dim3 grid((unsigned)(ceil_div(w, kRowsPerBlock * kOuterRB) * cs), (unsigned)n_recv);
-  auto k = rmax ? (g_outer_stage ? tp_node_outer_kernel<true, true, 1>
-                                 : tp_node_outer_kernel<true, false, 1>)
-           : cs == 2 ? (g_outer_stage ? tp_node_outer_kernel<false, true, 2>
-                                      : tp_node_outer_kernel<false, false, 2>)
-                     : (g_outer_stage ? tp_node_outer_kernel<false, true, 1>
-                                      : tp_node_outer_kernel<false, false, 1>);
-  k<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb, rmax);
+  auto k = cs == 2 ? tp_node_outer_kernel<false, true, 2> : tp_node_outer_kernel<false, true, 1>;
+  k<<<grid, kNT, 0, as_stream(stream)>>>((int)w, (int)H, eoff, Z, A, S, Sb, nullptr);
   return launch_status();
 }
 
@@ -844,7 +826,7 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
   const bool a16 = ((reinterpret_cast<uintptr_t>(Z) | reinterpret_cast<uintptr_t>(A) |
                      reinterpret_cast<uintptr_t>(Tb) | reinterpret_cast<uintptr_t>(dZ)) % 16) == 0;
   if (g_apply_x3 == 2 && H == kV3H && w % 32 == 0 && a16) {
-    auto k = tp_node_apply_v3_kernel<GMP_V3_ZD>;
+    auto k = tp_node_apply_v3_kernel<kV3Zd>;
     int rc = 0;
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, kV3Smem))))
@@ -859,7 +841,7 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
     const int hs = (int)(H / 32);
     const size_t smem = (size_t)3 * kTPlane + (size_t)3 * hs * kSPlane + 3 * kSPlane;
     int rc = 0;
-#define GMP_AV2(HS)                                                                              \
+#define LAUNCH_AV2(HS)                                                                              \
   {                                                                                              \
     auto k = tp_node_apply_x3_kernel<HS>;                                                        \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                      \
@@ -869,12 +851,12 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
     k<<<(unsigned)n_recv, kV2T, smem, as_stream(stream)>>>((int)w, eoff, Z, A, T, Tb, dZ, dA);   \
   }
     switch (hs) {
-      case 2: GMP_AV2(2) break;
-      case 4: GMP_AV2(4) break;
-      case 6: GMP_AV2(6) break;
-      default: GMP_AV2(8) break;
+      case 2: LAUNCH_AV2(2) break;
+      case 4: LAUNCH_AV2(4) break;
+      case 6: LAUNCH_AV2(6) break;
+      default: LAUNCH_AV2(8) break;
     }
-#undef GMP_AV2
+#undef LAUNCH_AV2
     return launch_status();
   }
   tp_node_apply_kernel<<<(unsigned)n_recv, kNT, 0, as_stream(stream)>>>(

@@ -166,7 +166,7 @@ constexpr int kGC = 16;  // slab loads in flight per lane in the ordered partial
 // fixed order independent of timing (deterministic).  SW = 16 (1024 threads): a 256-slab
 // reduction is ONE burst of loads per lane (4 waves took four dependent bursts: the r03 EGNN
 // trace had 2.2 ms of these sums per step on the side stream, latency-bound under the main
-// stream's HBM traffic).  GMP_SUM_WAVES=4 selects the r03 form.
+// stream's HBM traffic).
 template <int SW>
 __global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restrict__ part,
                                                             int64_t G, int64_t X,
@@ -197,17 +197,12 @@ __global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restr
   else if (colsum) colsum[x - DD] = s;
 }
 
-int g_sum_waves = getenv("GMP_SUM_WAVES") ? atoi(getenv("GMP_SUM_WAVES")) : 16;
-
 // out (row stride ldc, n columns) = the ordered sum of G slabs of X = DD (+ colsum) floats.
 // (r03: a two-level form with single-wave workgroups measured neutral on the EGNN step; removed)
 void sum_partials(const float* part, int64_t G, int64_t X, float* out, float* colsum,
                   int64_t DD, int64_t n, int64_t ldc, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(X, 64);
-  if (g_sum_waves == 4)
-    sum_partials_one<4><<<grid, 256, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
-  else
-    sum_partials_one<16><<<grid, 1024, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
+  sum_partials_one<16><<<grid, 1024, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
 }
 
 // Rectangular variant for the other per-edge Linears (GVP message GVPs: 128 x 144, 128 x 80,
@@ -670,30 +665,17 @@ int x3_pick(int64_t m, int64_t n, int* wn) {
   }
   return -1;
 }
-// 1: the f32-MFMA kernels (A/B and numerics studies); initial value from GMP_WGRAD_F32_MFMA,
-// changed by gmp_wgrad_set_f32_mfma
-int g_wgrad_mode = -1;
-bool wgrad_f32_mfma() {
-  if (g_wgrad_mode < 0) {
-    const char* e = getenv("GMP_WGRAD_F32_MFMA");
-    g_wgrad_mode = (e && atoi(e) != 0) ? 1 : 0;
-  }
-  return g_wgrad_mode == 1;
-}
-// Cap on the split-K workgroup count of the outer sums (0: none; gmp_wgrad_set_grid_cap): the
-// side-stream weight gradients leave CUs free for the critical path's node-level kernels.
-int g_grid_cap = 0;
-int64_t capped(int64_t g) { return g_grid_cap > 0 && g > g_grid_cap ? g_grid_cap : g; }
-// minimum edge tiles per workgroup of the f32-MFMA split-K sums (GMP_WGRAD_MIN_TILES; A/B)
-int g_min_tiles = getenv("GMP_WGRAD_MIN_TILES") ? atoi(getenv("GMP_WGRAD_MIN_TILES")) : 16;
+// 1: the f32-MFMA kernels (numerics studies, the exact-f32 bench leg); gmp_wgrad_set_f32_mfma
+int g_wgrad_mode = 0;
+bool wgrad_f32_mfma() { return g_wgrad_mode == 1; }
+// minimum edge tiles per workgroup of the f32-MFMA split-K sums
+constexpr int kMinTiles = 16;
 
-// smallest K (rows) routed to the split-plane sums (GMP_X3_MIN_K; A/B of the node-level sums)
-int64_t g_x3_min_k = getenv("GMP_X3_MIN_K") ? atoll(getenv("GMP_X3_MIN_K")) : 262144;
-// split-K workgroups of the edge-level x3 sums (GMP_X3_BLOCKS; default one per CU)
-int g_x3_blocks = getenv("GMP_X3_BLOCKS") ? atoi(getenv("GMP_X3_BLOCKS")) : 0;
+// smallest K (rows) routed to the split-plane sums (below: the node-level quadrant sums)
+constexpr int64_t kX3MinK = 262144;
 int64_t x3_blocks_for(int64_t K) {
   // one 8-wave workgroup per CU (LDS ~100 KB)
-  int64_t g = capped(g_x3_blocks > 0 ? (int64_t)g_x3_blocks : (int64_t)device_cu_count());
+  int64_t g = (int64_t)device_cu_count();
   const int64_t min_per = 4 * kXK;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
@@ -713,7 +695,7 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   // loaded byte for the split's VALU and LDS staging to pay (measured: 16 x 128, 48 x 48 slower).
   // Node-level sums (K ~ 50k rows) stay there too: a few stages per block, and the 1-block-per-
   // CU LDS footprint keeps them from sharing CUs with the concurrent main-stream kernels.
-  if (m * n < 4096 || K < g_x3_min_k) return GMP_ERR_UNSUPPORTED;
+  if (m * n < 4096 || K < kX3MinK) return GMP_ERR_UNSUPPORTED;
   int wn = 0;
   const int shape = x3_pick(m, n, &wn);
   const int64_t R = m + n;
@@ -728,7 +710,7 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
   float* part = reinterpret_cast<float*>(workspace);
   const size_t smem = (size_t)2 * (hf ? 2 : 3) * (R + kXPad) * 64;
   int rc = 0;
-#define GMP_X3(RT, CT, PP, NL)                                                                \
+#define LAUNCH_X3(RT, CT, PP, NL)                                                                \
   {                                                                                           \
     auto k = hf ? outer_sum_x3_kernel<RT, CT, PP, NL, 2> : outer_sum_x3_kernel<RT, CT, PP, NL>; \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                   \
@@ -738,21 +720,21 @@ int outer_sum_x3_launch(int64_t K, int64_t m, int64_t n, const float* A, int64_t
     k<<<(unsigned)Gr, kXT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per, part, bw, bb,  \
                                       wn, B2, ldb2, (int)n1, 0, amaxA);                       \
   }
-#define GMP_X3_NL(RT, CT, PP) \
-  if (nl == 1) GMP_X3(RT, CT, PP, 1) else GMP_X3(RT, CT, PP, 2)
-#define GMP_X3_PRO(RT, CT)                   \
-  if (pro == 0) { GMP_X3_NL(RT, CT, 0) }     \
-  else if (pro == 1) { GMP_X3_NL(RT, CT, 1) } \
-  else { GMP_X3_NL(RT, CT, 2) }
+#define LAUNCH_X3_NL(RT, CT, PP) \
+  if (nl == 1) LAUNCH_X3(RT, CT, PP, 1) else LAUNCH_X3(RT, CT, PP, 2)
+#define LAUNCH_X3_PRO(RT, CT)                   \
+  if (pro == 0) { LAUNCH_X3_NL(RT, CT, 0) }     \
+  else if (pro == 1) { LAUNCH_X3_NL(RT, CT, 1) } \
+  else { LAUNCH_X3_NL(RT, CT, 2) }
   switch (shape) {
-    case 0: GMP_X3_PRO(1, 2) break;
-    case 1: GMP_X3_PRO(2, 2) break;
-    case 2: GMP_X3_PRO(2, 4) break;
-    default: GMP_X3_PRO(2, 5) break;
+    case 0: LAUNCH_X3_PRO(1, 2) break;
+    case 1: LAUNCH_X3_PRO(2, 2) break;
+    case 2: LAUNCH_X3_PRO(2, 4) break;
+    default: LAUNCH_X3_PRO(2, 5) break;
   }
-#undef GMP_X3_PRO
-#undef GMP_X3_NL
-#undef GMP_X3
+#undef LAUNCH_X3_PRO
+#undef LAUNCH_X3_NL
+#undef LAUNCH_X3
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;
@@ -1060,19 +1042,15 @@ __global__ __launch_bounds__(kQT, 2) void outer_sum_quad_kernel(
   }
 }
 
-// GMP_WGRAD_QUAD=0: node-level sums on the r03 split-K kernels (A/B)
-int g_quad = getenv("GMP_WGRAD_QUAD") ? atoi(getenv("GMP_WGRAD_QUAD")) : 1;
-// workgroups per CU x 2 of the node-level quadrant sums (GMP_QUAD_WG2; A/B: fewer workgroups
-// = fewer partial slabs for the ordered reduction, more rows each)
-int g_quad_wg2 = getenv("GMP_QUAD_WG2") ? atoi(getenv("GMP_QUAD_WG2")) : 4;
+// node-level (K < kX3MinK) sums: split over about two workgroups per CU
 int64_t quad_splits(int64_t K, int64_t quads) {
-  int64_t s = ceil_div((int64_t)g_quad_wg2 * device_cu_count() / 2, quads);  // ~2 per CU
+  int64_t s = ceil_div((int64_t)2 * device_cu_count(), quads);
   const int64_t cap = ceil_div(K, 256);                          // >= 256 rows each
   if (s > cap) s = cap;
   return s < 1 ? 1 : s;
 }
 bool quad_ok(int64_t K, int64_t m, int64_t n, int pro, int64_t lda, int64_t ldb) {
-  return g_quad && pro == 0 && K < g_x3_min_k && K > 0 && m % 64 == 0 && n % 64 == 0 &&
+  return pro == 0 && K < kX3MinK && K > 0 && m % 64 == 0 && n % 64 == 0 &&
          m <= 256 && n <= 256 && lda % 4 == 0 && ldb % 4 == 0;
 }
 size_t quad_workspace(int64_t K, int64_t m, int64_t n) {
@@ -1097,9 +1075,6 @@ int outer_sum_quad_launch(int64_t K, int64_t m, int64_t n, const float* A, int64
   return launch_status();
 }
 
-// GMP_OSC_PRESPLIT=0: the r03 column-block kernel (both operands split per block)
-int g_osc_presplit = getenv("GMP_OSC_PRESPLIT") ? atoi(getenv("GMP_OSC_PRESPLIT")) : 1;
-
 // capacity bucket for (M, N): returns 0 if unsupported
 // Tile bucket of an M x N problem: the smallest compiled (MR, MC) covering the per-wave tile
 // counts (the MFMA stream is branch-free, so oversized buckets cost real MFMAs), and the
@@ -1120,11 +1095,11 @@ int rect_bucket(int64_t m, int64_t n) {
 }
 
 int64_t blocks_for(int64_t K) {
-  int64_t g = capped((int64_t)device_cu_count() * 2);  // two resident workgroups per CU
+  int64_t g = (int64_t)device_cu_count() * 2;  // two resident workgroups per CU
   // >= 16 edge tiles per workgroup: a node-level sum (K = 50k rows) then takes ~100 CUs and
   // writes ~100 partial slabs instead of 391 (r03 trace: the 391-slab form and its reduction
   // held the side stream 3.3 ms per EGNN step, beside the critical path's kernels)
-  const int64_t min_per = g_min_tiles * kKT;
+  const int64_t min_per = kMinTiles * kKT;
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
 }
@@ -1135,12 +1110,6 @@ int64_t blocks_for(int64_t K) {
 using namespace gmp;
 
 extern "C" {
-
-int gmp_wgrad_set_grid_cap(int blocks) {
-  const int prev = g_grid_cap;
-  g_grid_cap = blocks > 0 ? blocks : 0;
-  return prev;
-}
 
 int gmp_wgrad_set_f32_mfma(int on) {
   const int prev = wgrad_f32_mfma() ? 1 : 0;
@@ -1185,17 +1154,17 @@ static int outer_sum_launch(int64_t K, int64_t d, const float* A, int64_t lda, c
   const int64_t per = ceil_div(ceil_div(K, G), kKT) * kKT;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-#define GMP_OS(DD, PP) \
+#define LAUNCH_OS(DD, PP) \
   outer_sum_kernel<DD, PP><<<(unsigned)Gr, kT, 0, s>>>(A, B, K, lda, ldb, per, part, bw, bb)
-#define GMP_OS_D(PP)                 \
-  if (d == 128) GMP_OS(128, PP);     \
-  else if (d == 64) GMP_OS(64, PP);  \
-  else GMP_OS(32, PP)
-  if (pro == 0) { GMP_OS_D(0); }
-  else if (pro == 1) { GMP_OS_D(1); }
-  else { GMP_OS_D(2); }
-#undef GMP_OS_D
-#undef GMP_OS
+#define LAUNCH_OS_D(PP)                 \
+  if (d == 128) LAUNCH_OS(128, PP);     \
+  else if (d == 64) LAUNCH_OS(64, PP);  \
+  else LAUNCH_OS(32, PP)
+  if (pro == 0) { LAUNCH_OS_D(0); }
+  else if (pro == 1) { LAUNCH_OS_D(1); }
+  else { LAUNCH_OS_D(2); }
+#undef LAUNCH_OS_D
+#undef LAUNCH_OS
   int rc = launch_status();
   if (rc) return rc;
   const int64_t X = d * d + d;
@@ -1243,8 +1212,8 @@ int gmp_edge_outer_sum_act_hf_f32(int64_t K, int64_t d, const float* A, const fl
 }
 
 int64_t rect_blocks_for(int64_t K) {
-  int64_t g = capped((int64_t)device_cu_count() * 2);
-  const int64_t min_per = g_min_tiles * kKT;  // as blocks_for
+  int64_t g = (int64_t)device_cu_count() * 2;
+  const int64_t min_per = kMinTiles * kKT;  // as blocks_for
   if (g * min_per > K) g = ceil_div(K, min_per);
   return g < 1 ? 1 : g;
 }
@@ -1287,7 +1256,7 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
   float* part = reinterpret_cast<float*>(workspace);
   const size_t smem = (size_t)2 * kKT * (rect_ld((int)m) + rect_ld((int)n)) * sizeof(float);
   int rc;
-#define GMP_RECT(MR, MC, NL, OCC)                                                             \
+#define LAUNCH_RECT(MR, MC, NL, OCC)                                                             \
   {                                                                                           \
     auto k = outer_sum_rect_kernel<MR, MC, NL, OCC>;                                          \
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,                                   \
@@ -1296,26 +1265,26 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
       return rc;                                                                              \
     k<<<(unsigned)Gr, kT, smem, s>>>(A, B, K, (int)m, (int)n, lda, ldb, per, part);           \
   }
-#define GMP_RECT_NL(MR, MC)                                   \
-  case MR * 100 + MC * 10 + 2: GMP_RECT(MR, MC, 5, 2) break;  \
-  case MR * 100 + MC * 10 + 3: GMP_RECT(MR, MC, 7, 2) break;  \
-  case MR * 100 + MC * 10 + 4: GMP_RECT(MR, MC, 9, 2) break;
+#define LAUNCH_RECT_NL(MR, MC)                                   \
+  case MR * 100 + MC * 10 + 2: LAUNCH_RECT(MR, MC, 5, 2) break;  \
+  case MR * 100 + MC * 10 + 3: LAUNCH_RECT(MR, MC, 7, 2) break;  \
+  case MR * 100 + MC * 10 + 4: LAUNCH_RECT(MR, MC, 9, 2) break;
 // the widest buckets need > 256 VGPRs at 7-9 loads per thread: one workgroup per CU (the
 // compiler then has the AGPRs as well; at two per CU they spilled 40-152 B/lane to scratch)
-#define GMP_RECT_NL_WIDE(MR, MC)                              \
-  case MR * 100 + MC * 10 + 2: GMP_RECT(MR, MC, 5, 2) break;  \
-  case MR * 100 + MC * 10 + 3: GMP_RECT(MR, MC, 7, 1) break;  \
-  case MR * 100 + MC * 10 + 4: GMP_RECT(MR, MC, 9, 1) break;
+#define LAUNCH_RECT_NL_WIDE(MR, MC)                              \
+  case MR * 100 + MC * 10 + 2: LAUNCH_RECT(MR, MC, 5, 2) break;  \
+  case MR * 100 + MC * 10 + 3: LAUNCH_RECT(MR, MC, 7, 1) break;  \
+  case MR * 100 + MC * 10 + 4: LAUNCH_RECT(MR, MC, 9, 1) break;
   switch (bucket) {
-    GMP_RECT_NL(1, 1) GMP_RECT_NL(1, 2) GMP_RECT_NL(1, 3)
-    GMP_RECT_NL(2, 1) GMP_RECT_NL(2, 2) GMP_RECT_NL(2, 3) GMP_RECT_NL(2, 5) GMP_RECT_NL_WIDE(2, 9)
-    GMP_RECT_NL(3, 1) GMP_RECT_NL(3, 2) GMP_RECT_NL(3, 3)
-    GMP_RECT_NL_WIDE(4, 4)
+    LAUNCH_RECT_NL(1, 1) LAUNCH_RECT_NL(1, 2) LAUNCH_RECT_NL(1, 3)
+    LAUNCH_RECT_NL(2, 1) LAUNCH_RECT_NL(2, 2) LAUNCH_RECT_NL(2, 3) LAUNCH_RECT_NL(2, 5) LAUNCH_RECT_NL_WIDE(2, 9)
+    LAUNCH_RECT_NL(3, 1) LAUNCH_RECT_NL(3, 2) LAUNCH_RECT_NL(3, 3)
+    LAUNCH_RECT_NL_WIDE(4, 4)
     default: return GMP_ERR_UNSUPPORTED;
   }
-#undef GMP_RECT_NL_WIDE
-#undef GMP_RECT_NL
-#undef GMP_RECT
+#undef LAUNCH_RECT_NL_WIDE
+#undef LAUNCH_RECT_NL
+#undef LAUNCH_RECT
   rc = launch_status();
   if (rc) return rc;
   const int64_t X = m * n + m;
@@ -1403,7 +1372,7 @@ int gmp_outer_sum_cols_f32(int64_t K, int64_t m_total, int64_t n, const float* A
   const int64_t per = ceil_div(ceil_div(K, G), kXK) * kXK;
   const int64_t Gr = ceil_div(K, per);
   float* part = reinterpret_cast<float*>(workspace);
-  if (g_osc_presplit && (n == 64 || n == 128) && ldb == n) {
+  if ((n == 64 || n == 128) && ldb == n) {
     const int64_t X = m * n + m;
     const int64_t nks = ceil_div(K, kXK);
     unsigned short* planes = reinterpret_cast<unsigned short*>(

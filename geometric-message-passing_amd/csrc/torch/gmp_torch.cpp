@@ -869,7 +869,7 @@ std::tuple<Tensor, Tensor> tp_edge_z_bwd(at::IntArrayRef desc, const Tensor& pat
   return {dx, dY};
 }
 
-// per-edge-weight form (GMP_TP_MODE=edge, or radial hidden sizes outside the node form): the
+// per-edge-weight form (equivariant.TP_MODE = "edge", or radial hidden sizes outside the node form): the
 // chunk [c0, c1) of receiver-sorted edges with its weights W (c1 - c0, weight_numel)
 void tp_conv_fwd(int64_t layout, at::IntArrayRef desc, const Tensor& paths, const Tensor& cg,
                  const Tensor& x, const Tensor& sh, const Tensor& W, const Tensor& src_sorted,
@@ -1003,120 +1003,6 @@ void tp_gemm_x3(const Tensor& A1, int64_t K1, const optional<Tensor>& A2, int64_
                               ldb, N * ldb, C.data_ptr<float>() + c_offset, cgrp, cldg, cldr, cldn,
                               accumulate, cur_stream()),
            "gmp_tp_gemm_x3_f32");
-}
-
-// dW2p of one path with S built in-kernel (K7f): Z (edges (+1 pad row) x d3 mul1), A (edges x H),
-// G (n_recv d3 x mul_out), eoff (n_recv + 1) -> dW (mul1 H x mul_out)
-Tensor tp_node_dw(const Tensor& eoff, const Tensor& Z, const Tensor& A, const Tensor& G,
-                  int64_t d3, int64_t mul1) {
-  OpGuard g(Z, "tp_node_dw");
-  i64(eoff, "eoff");
-  f32(Z, "Z");
-  f32(A, "A");
-  f32(G, "G");
-  TORCH_CHECK(eoff.dim() == 1 && eoff.numel() >= 1, "gmp.tp_node_dw: eoff (n_recv + 1)");
-  const int64_t n = eoff.numel() - 1;
-  TORCH_CHECK(A.dim() == 2 && Z.dim() == 2 && Z.size(1) == d3 * mul1 && Z.size(0) >= A.size(0),
-              "gmp.tp_node_dw: Z (edges, d3 mul1), A (edges, H)");
-  TORCH_CHECK(G.dim() == 2 && G.size(0) == n * d3, "gmp.tp_node_dw: G (n_recv d3, mul_out)");
-  const int64_t H = A.size(1), mo = G.size(1);
-  Tensor dW = at::empty({mul1 * H, mo}, Z.options());
-  const size_t ws_b = gmp_tp_node_dw_workspace_size(n, d3, mul1, H, mo);
-  Tensor ws = at::empty({(int64_t)ws_b + 1}, Z.options().dtype(at::kByte));
-  check_rc(gmp_tp_node_dw_f32(n, d3, mul1, H, mo, ip(eoff), fp(Z), fp(A), fp(G), fp(dW),
-                              ws.data_ptr(), ws_b, cur_stream()),
-           "gmp_tp_node_dw_f32");
-  return dW;
-}
-
-// forward of one path with S built in-kernel (K7s): C[c_offset + n cldg + w d3 + k] += ...
-void tp_node_fwd_fused(const Tensor& eoff, const Tensor& Z, const Tensor& A, const Tensor& Bf,
-                       int64_t d3, int64_t mul1, int64_t mul_out, Tensor C, int64_t c_offset,
-                       int64_t cldg) {
-  OpGuard g(Z, "tp_node_fwd_fused");
-  i64(eoff, "eoff");
-  f32(Z, "Z");
-  f32(A, "A");
-  f32(C, "C");
-  need(Bf, at::kShort, "B planes");
-  TORCH_CHECK(eoff.dim() == 1 && eoff.numel() >= 1, "gmp.tp_node_fwd_fused: eoff (n_recv + 1)");
-  const int64_t n = eoff.numel() - 1;
-  TORCH_CHECK(A.dim() == 2 && Z.dim() == 3 && Z.size(2) == 16 && Z.size(1) >= A.size(0) &&
-                  Z.size(0) == (mul1 + 16 / d3 - 1) / (16 / d3),
-              "gmp.tp_node_fwd_fused: Z in the K7s layout (u steps, rows, 16), A (edges, H)");
-  const int64_t H = A.size(1);
-  TORCH_CHECK(Bf.numel() >= 3 * mul_out * (mul1 * H + mul1),
-              "gmp.tp_node_fwd_fused: B planes hold 3 mul_out (mul1 H + mul1)");
-  TORCH_CHECK(c_offset >= 0 && cldg > 0, "gmp.tp_node_fwd_fused: epilogue addressing");
-  if (n > 0)
-    TORCH_CHECK(c_offset + (n - 1) * cldg + (mul_out - 1) * d3 + d3 - 1 < C.numel(),
-                "gmp.tp_node_fwd_fused: the output block exceeds C");
-  check_rc(gmp_tp_node_fwd_fused_f32(n, d3, mul1, H, mul_out, ip(eoff), fp(Z), Z.size(1), fp(A),
-                                     Bf.data_ptr(), C.data_ptr<float>() + c_offset, cldg,
-                                     cur_stream()),
-           "gmp_tp_node_fwd_fused_f32");
-}
-
-// z rows (rows, d3 mul1) -> the K7s layout (ceil(mul1 / U), rows, 16), U = 16 / d3
-Tensor tp_z_fused_layout(const Tensor& Z, int64_t d3, int64_t mul1) {
-  OpGuard g(Z, "tp_z_fused_layout");
-  f32(Z, "Z");
-  TORCH_CHECK(d3 >= 1 && d3 <= 16 && Z.dim() == 2 && Z.size(1) == d3 * mul1,
-              "gmp.tp_z_fused_layout: Z (rows, d3 mul1)");
-  const int64_t U = 16 / d3;
-  Tensor Zf = at::empty({(mul1 + U - 1) / U, Z.size(0), 16}, Z.options());
-  check_rc(gmp_tp_z_fused_layout_f32(fp(Z), Z.size(0), d3, mul1, fp(Zf), cur_stream()),
-           "gmp_tp_z_fused_layout_f32");
-  return Zf;
-}
-
-// three bf16 planes of the (N x K) operand B = W (transpose = false: rows n of W) or W^T
-// (transpose = true: W is (K x N)) in fragment order
-Tensor split_x3(const Tensor& W, bool transpose) {
-  OpGuard g(W, "split_x3");
-  on_device(W, "W");
-  TORCH_CHECK(W.scalar_type() == at::kFloat, "gmp: W has dtype ", W.scalar_type(),
-              ", expected float");
-  TORCH_CHECK(W.dim() == 2, "gmp.split_x3: W must be 2-D");  // any strides (weight slices)
-  const int64_t N = transpose ? W.size(1) : W.size(0), K = transpose ? W.size(0) : W.size(1);
-  TORCH_CHECK(N % 16 == 0 && K % 32 == 0, "gmp.split_x3: needs N % 16 == 0 and K % 32 == 0, got ",
-              N, " x ", K);
-  Tensor planes = at::empty({3 * N * K}, W.options().dtype(at::kShort));
-  const int64_t s0 = W.stride(0), s1 = W.stride(1);
-  check_rc(gmp_split_x3_f32(N, K, W.numel() ? W.data_ptr<float>() : nullptr,
-                            transpose ? s1 : s0, transpose ? s0 : s1, planes.data_ptr(),
-                            cur_stream()),
-           "gmp_split_x3_f32");
-  return planes;
-}
-
-// C = [A1 | A2] B^T + bias (B as split_x3 planes, N columns)
-Tensor gemm_x3(const Tensor& A1, const optional<Tensor>& A2, const Tensor& Bp, int64_t N,
-               const optional<Tensor>& bias) {
-  OpGuard g(A1, "gemm_x3");
-  f32(A1, "A1");
-  need(Bp, at::kShort, "B planes");
-  TORCH_CHECK(A1.dim() == 2, "gmp.gemm_x3: A1 must be (M, K1)");
-  const int64_t M = A1.size(0), K1 = A1.size(1);
-  const bool two = A2.has_value() && A2->defined();
-  int64_t K2 = 0;
-  if (two) {
-    f32(*A2, "A2");
-    TORCH_CHECK(A2->dim() == 2 && A2->size(0) == M, "gmp.gemm_x3: A2 must be (M, K2)");
-    K2 = A2->size(1);
-  }
-  TORCH_CHECK(K1 % 32 == 0 && K2 % 32 == 0 && N % 16 == 0 && N > 0,
-              "gmp.gemm_x3: K1, K2 multiples of 32 and N of 16");
-  TORCH_CHECK(Bp.numel() == 3 * N * (K1 + K2), "gmp.gemm_x3: B planes hold 3 N (K1 + K2)");
-  if (bias.has_value() && bias->defined()) {
-    f32(*bias, "bias");
-    TORCH_CHECK(bias->numel() == N, "gmp.gemm_x3: bias must hold N values");
-  }
-  Tensor C = at::empty({M, N}, A1.options());
-  check_rc(gmp_gemm_x3_f32(M, N, fp(A1), K1, K1, two ? fp(*A2) : nullptr, K2, two ? K2 : 0,
-                           Bp.data_ptr(), cfp(bias), fp(C), N, 0, cur_stream()),
-           "gmp_gemm_x3_f32");
-  return C;
 }
 
 Tensor tp_gemm_x3_widen(const Tensor& A, const Tensor& Bp, int64_t N) {
@@ -1585,23 +1471,6 @@ Tensor tp_split_w2(const Tensor& W2, const Tensor&, int64_t, int64_t mul1, int64
 }
 void tp_gemm_x3(const Tensor&, int64_t, const optional<Tensor>&, int64_t, const Tensor&, int64_t,
                 int64_t, Tensor, int64_t, int64_t, int64_t, int64_t, int64_t, bool) {}
-Tensor tp_node_dw(const Tensor&, const Tensor&, const Tensor& A, const Tensor& G, int64_t,
-                  int64_t mul1) {
-  return at::empty({mul1 * A.size(1), G.size(1)}, A.options());
-}
-void tp_node_fwd_fused(const Tensor&, const Tensor&, const Tensor&, const Tensor&, int64_t,
-                       int64_t, int64_t, Tensor, int64_t, int64_t) {}
-Tensor tp_z_fused_layout(const Tensor& Z, int64_t d3, int64_t mul1) {
-  const int64_t U = 16 / d3;
-  return at::empty({(mul1 + U - 1) / U, Z.size(0), 16}, Z.options());
-}
-Tensor split_x3(const Tensor& W, bool) {
-  return at::empty({3 * W.numel()}, W.options().dtype(at::kShort));
-}
-Tensor gemm_x3(const Tensor& A1, const optional<Tensor>&, const Tensor&, int64_t N,
-               const optional<Tensor>&) {
-  return at::empty({A1.size(0), N}, A1.options());
-}
 Tensor tp_gemm_x3_widen(const Tensor& A, const Tensor&, int64_t N) {
   return at::empty({A.size(0), N}, A.options());
 }
@@ -1726,12 +1595,6 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor(a!) C, int c_offset, int cgrp, int cldg, int cldr, int cldn, bool accumulate) "
         "-> ()");
   m.def("tp_gemm_x3_widen(Tensor A, Tensor Bp, int N) -> Tensor");
-  m.def("split_x3(Tensor W, bool transpose) -> Tensor");
-  m.def("tp_node_dw(Tensor eoff, Tensor Z, Tensor A, Tensor G, int d3, int mul1) -> Tensor");
-  m.def("tp_node_fwd_fused(Tensor eoff, Tensor Z, Tensor A, Tensor Bf, int d3, int mul1, "
-        "int mul_out, Tensor(a!) C, int c_offset, int cldg) -> ()");
-  m.def("tp_z_fused_layout(Tensor Z, int d3, int mul1) -> Tensor");
-  m.def("gemm_x3(Tensor A1, Tensor? A2, Tensor Bp, int N, Tensor? bias) -> Tensor");
   m.def("outer_sum_cols(Tensor A, Tensor B) -> Tensor");
   m.def("edge_outer_sum(Tensor A, Tensor B) -> (Tensor C, Tensor colsum)");
   m.def("edge_outer_sum_ex(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int act, "
@@ -1791,11 +1654,6 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("tp_split_w2", ns tp_split_w2);                                  \
   m.impl("tp_gemm_x3", ns tp_gemm_x3);                                    \
   m.impl("tp_gemm_x3_widen", ns tp_gemm_x3_widen);                        \
-  m.impl("split_x3", ns split_x3);                                        \
-  m.impl("tp_node_dw", ns tp_node_dw);                                    \
-  m.impl("tp_node_fwd_fused", ns tp_node_fwd_fused);                      \
-  m.impl("tp_z_fused_layout", ns tp_z_fused_layout);                      \
-  m.impl("gemm_x3", ns gemm_x3);                                          \
   m.impl("outer_sum_cols", ns outer_sum_cols);                            \
   m.impl("edge_outer_sum", ns edge_outer_sum);                            \
   m.impl("edge_outer_sum_ex", ns edge_outer_sum_ex);                      \

@@ -75,9 +75,6 @@ SIGNATURES = {
                                       c_vp, c_vp, c_int, c_vp, c_vp]),
     "gmp_egnn_edge_bwd_partials_rows": (c_i64, [c_i64, c_i64]),
     "gmp_egnn_set_f32_mfma": (c_int, [c_int]),
-    "gmp_wgrad_set_grid_cap": (c_int, [c_int]),
-    "gmp_stream_create_cu_share": (c_int, [c_int, ctypes.POINTER(c_vp)]),
-    "gmp_stream_destroy": (c_int, [c_vp]),
     "gmp_wgrad_set_f32_mfma": (c_int, [c_int]),
     "gmp_edge_outer_sum_workspace_size": (c_size, [c_i64, c_i64]),
     "gmp_edge_outer_sum_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
@@ -144,18 +141,7 @@ SIGNATURES = {
     "gmp_tp_node_apply_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp]),
     "gmp_tp_apply_set_x3": (c_int, [c_int]),
-    "gmp_tp_gemm_set_rings": (c_int, [c_int, c_int]),
     "gmp_tp_split_w2_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "gmp_split_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
-    "gmp_tp_node_dw_workspace_size": (c_size, [c_i64, c_i64, c_i64, c_i64, c_i64]),
-    "gmp_tp_node_fwd_fused_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64,
-                                          c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "gmp_tp_z_fused_layout_floats": (c_i64, [c_i64, c_i64, c_i64]),
-    "gmp_tp_z_fused_layout_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "gmp_tp_node_dw_f32": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
-                                   c_vp, c_vp, c_size, c_vp]),
-    "gmp_gemm_x3_f32": (c_int, [c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp,
-                                c_vp, c_i64, c_int, c_vp]),
     "gmp_tp_gemm_x3_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
                                    c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp]),
     "gmp_tp_gemm_x3_widen_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
@@ -205,10 +191,11 @@ SIGNATURES = {
                               + [c_vp] * 11),
 }
 
-# include/gmp.h GMP_ABI_VERSION (4: r05 — gmp_egnn_node_fwd_f32;
+# include/gmp.h GMP_ABI_VERSION (5: r05 — K7s / K7f, the row GEMM and the A/B setters removed;
+# 4: r05 — gmp_egnn_node_fwd_f32;
 # 3: r04 — K8 dim / A4 arguments; 2: r04 — EGNN save_planes
 # arguments, the x_hat mode global and gmp_egnn_edge_bwd_ab_f32 removed)
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lib = None
 TORCH_LIB_PATH = os.environ.get("GMP_TORCH_LIB", os.path.join(_HERE, "libgmp_torch.so"))
 _torch_ops = None

@@ -14,7 +14,6 @@ all at once; the HIP TP kernels stream each chunk once.  Node-level pieces (Batc
 o3.Linear, symmetric contraction) are PyTorch ops on N-row tensors.
 """
 import math
-import os
 
 import torch
 from torch.autograd.function import once_differentiable
@@ -26,7 +25,7 @@ from . import o3
 from .ops import _f32c, _need_cuda, _timed
 from .scatter import global_add_pool, global_mean_pool, scatter
 
-CHUNK_BYTES = int(os.environ.get("GMP_TP_CHUNK_BYTES", str(6 << 30)))
+CHUNK_BYTES = 6 << 30
 
 
 # ===================================================================================== radial
@@ -390,7 +389,7 @@ class TPPlan:
                 len(self.instructions) > 48 or cg_floats > (8192 if lmx > 3 else 4096):
             raise NotImplementedError(f"TP {o3.irreps_str(irreps_in)} x {o3.irreps_str(irreps_sh)}"
                                       f" -> {o3.irreps_str(irreps_out)} not supported by K7")
-        # the per-edge-weight kernels (GMP_TP_MODE=edge) take the two l <= 2 layouts; the node
+        # the per-edge-weight kernels (TP_MODE = "edge") take the two l <= 2 layouts; the node
         # form (default) any block structure with l <= 5
         edge_ok = (key in _LAYOUTS and sh_dim == 9 and
                    not any(m > 128 or m % 4 for m, _ in irreps_out))
@@ -533,9 +532,9 @@ class TPConvFn(torch.autograd.Function):
 # Receiver chunk of the node form, in bytes of S (+ T) for the widest path.  Larger chunks give
 # the path GEMMs (M = receivers x (2lo+1), N = mul_out = 128, K = mul1 x H) enough row tiles to
 # fill the 256 CUs: 2 GiB -> 64 GiB took MACE-128 at 1M edges from 287k to 332k edges/s.  The
-# default is a quarter of the device's HBM, capped at 64 GiB (one chunk for a 1M-edge graph).
-NODE_CHUNK_BYTES = (int(os.environ["GMP_TP_NODE_CHUNK_BYTES"])
-                    if "GMP_TP_NODE_CHUNK_BYTES" in os.environ else None)
+# default (None) is a quarter of the device's HBM, capped at 64 GiB (one chunk for a 1M-edge
+# graph); tests set a small value to cover the multi-chunk path.
+NODE_CHUNK_BYTES = None
 
 
 _HBM_BYTES = {}
@@ -547,7 +546,7 @@ def node_chunk_bytes(device):
     if device not in _HBM_BYTES:
         _HBM_BYTES[device] = torch.cuda.get_device_properties(device).total_memory
     return int(min(64 << 30, _HBM_BYTES[device] // 4))
-TP_MODE = os.environ.get("GMP_TP_MODE", "node")  # "node" (receiver-factorised) | "edge"
+TP_MODE = "node"  # "node" (receiver-factorised) | "edge" (per-edge weights; tests compare)
 
 
 def _w2_path(W2, b2, P):
@@ -565,39 +564,11 @@ def node_form_ok(hidden):
 
 # Path GEMMs of the node form: "x3" = K7g (gmp_tpgemm.hip: bf16 MFMA over exact three-plane f32
 # splits; dW2p by the column-block split-plane outer sum), "torch" = the library f32 GEMMs.
-TP_GEMM = os.environ.get("GMP_TP_GEMM", "x3")
 def _x3_ok(P, H):
     """Shapes K7g covers: every k range a multiple of the 32-deep MFMA step and mul_out <= 128
     (128 x 128 output tiles; 256 x 64 for the 64-channel paths of config C5)."""
-    return (TP_GEMM == "x3" and P["mul1"] % 32 == 0 and P["mul_out"] % 32 == 0
+    return (P["mul1"] % 32 == 0 and P["mul_out"] % 32 == 0
             and P["mul_out"] <= 128 and H % 32 == 0)
-
-
-# K7f (gmp_tpdw.hip): the backward's dW2p with S built inside the outer sum, GMP_TP_DW_FUSED=1.
-# Off by default: correct (tests/test_gpu_tpnode.py) and HBM-light (7 GB vs 66 GB of S traffic
-# per MACE-128 lo = 2 path) but slower than the S kernel + column-block outer sum it replaces
-# (scripts/mb_tpdw.py: 29.7 vs 22.1 ms at lo = 2; PMC: 40 % of wave cycles waiting, 33 % issue
-# stalls, MFMA busy 25 % -- two waves per SIMD in lock-step stages do not hide the S-build loads)
-TP_DW_FUSED = os.environ.get("GMP_TP_DW_FUSED", "0") == "1"
-
-
-def _dw_fused_ok(P, H):
-    return (TP_DW_FUSED and P["mul1"] % 16 == 0 and H % 16 == 0
-            and P["mul_out"] in (64, 128))
-
-
-# K7s (gmp_tpfwd.hip): the forward's path contraction with S built inside the GEMM (S never in
-# HBM: 66 GB of S writes + reads per MACE-128 lo = 2 path avoided); lo >= 1 paths of the K7g
-# shapes (the lo = 0 paths keep the S kernel + K7g GEMM: d3 = 1 would leave 15 of 16 S-MFMA rows
-# idle).  Opt-in (GMP_TP_FWD_FUSED=1): parity-green but measured slower than the unfused pair at
-# the MACE-128 shapes (r04, 50k receivers / 1M edges: d3 = 5 25.1 vs 21.6 ms, d3 = 3 18.3 vs
-# 12.9 ms; DESIGN.md "K7s").
-TP_FWD_FUSED = os.environ.get("GMP_TP_FWD_FUSED", "0") == "1"
-
-
-def _fwd_fused_ok(P, H):
-    return (TP_FWD_FUSED and 2 * P["lo"] + 1 in (3, 5, 7) and P["mul1"] % 32 == 0
-            and P["mul_out"] in (64, 128) and H % 32 == 0)
 
 
 def _split_w2(W2, b2, P, fwd):
@@ -639,16 +610,6 @@ class TPConvNodeFn(torch.autograd.Function):
                 d3, m1, mo = 2 * P["lo"] + 1, P["mul1"], P["mul_out"]
                 Zp = zbuf[zoff * (ne + 1):(zoff + w) * (ne + 1)].view(ne + 1, w)
                 blk = plan.blocks[P["io"]]
-                if x3[i] and _fwd_fused_ok(P, H):
-                    # K7s: S built in-kernel, accumulated into the receivers' output block
-                    if Bfs[i] is None:
-                        Bfs[i] = _split_w2(W2c, b2c, P, True)
-                    with _timed("tp_node_W"):
-                        Zf = tops.tp_z_fused_layout(Zp, d3, m1)
-                        tops.tp_node_fwd_fused(eoff, Zf, a, Bfs[i], d3, m1, mo, out,
-                                               n0 * out.shape[1] + blk[0], out.shape[1])
-                        del Zf
-                    continue
                 S, Sb = _node_outer(eoff, Zp, a, w)
                 if x3[i]:
                     # out[n, blk + w' d3 + k] += [S | Sb][(n, k), :] [W2p ; b2p][:, w'] (K7g)
@@ -706,19 +667,11 @@ class TPConvNodeFn(torch.autograd.Function):
                 G = G.reshape(c * d3, mo).contiguous()  # (d3 = 1: reshape alone is a view)
                 if x3[i]:
                     K1 = m1 * H
-                    fused = _dw_fused_ok(P, H)
-                    if not fused:  # (timed as tp_node_S, outside the dW region)
-                        S, Sb = _node_outer(eoff, Zp, a, w)
+                    S, Sb = _node_outer(eoff, Zp, a, w)  # (timed as tp_node_S)
                     with _timed("tp_node_dW"):
-                        if fused:
-                            # K7f: dW2p with the S rows built in-kernel (S never in HBM); Sb
-                            # (the bias rows) = the per-receiver sum of the z rows
-                            part = tops.tp_node_dw(eoff, Zp, a, G, d3, m1)
-                            Sb, _ = tops.segment_reduce(Zp, None, eoff, c, "sum")
-                        else:
-                            # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
-                            part = tops.outer_sum_cols(S.view(c * d3, K1), G)
-                            del S
+                        # dW2p[(u, j), w] = sum_(n, k) S[(n, k), (u, j)] G[(n, k), w]
+                        part = tops.outer_sum_cols(S.view(c * d3, K1), G)
+                        del S
                         # db2p[u, w] = sum_(n, k) Sb[(n, k), u] G[(n, k), w]: the deterministic
                         # outer sum (the library's K = 250k reduction GEMM ran 0.4 ms per path)
                         pb, _ = ops.edge_outer_sum_rect(Sb.view(c * d3, m1), G)
@@ -835,7 +788,7 @@ class TensorProductConvLayer(nn.Module):
         # (a plain bool: torch.compile cannot trace `is` between autograd Function classes)
         if not node and self.plan.layout is None:
             raise NotImplementedError("the per-edge-weight TP kernels take l <= 2 layouts only; "
-                                      "use the node form (GMP_TP_MODE=node, mlp_dim % 16 == 0)")
+                                      "use the node form (TP_MODE = \"node\", mlp_dim % 16 == 0)")
         paths, cg = self._tp_paths, self._tp_cg
         if paths.device != node_attr.device or cg.dtype != torch.float32:
             paths, cg = self.plan.device_tables(node_attr.device)

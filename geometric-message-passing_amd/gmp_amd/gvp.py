@@ -12,7 +12,6 @@ CSR (deterministic).  Subclasses with a custom message function or module_list f
 generic propagate path (gather -> message -> segmented reduce).
 """
 import functools
-import os
 
 import torch
 from torch.autograd.function import once_differentiable
@@ -130,8 +129,8 @@ class Dropout(nn.Module):
         return self.sdropout(s), self.vdropout(v)
 
 
-# GMP_GVP_VECNORM=0: the vector LayerNorm as the reference's torch chain (A/B)
-VEC_NORM_FUSED = os.environ.get("GMP_GVP_VECNORM", "1") != "0"
+# False: the vector LayerNorm as the reference's torch chain (tests compare the two)
+VEC_NORM_FUSED = True
 
 
 class VecNormFn(torch.autograd.Function):
@@ -202,7 +201,8 @@ class LayerNorm(nn.Module):
 
 
 # ------------------------------------------------------------------------------------ K5g
-GVP_FUSED = os.environ.get("GMP_GVP_FUSED", "1") != "0"
+# False: the reference-shaped per-edge chain (tests compare the two)
+GVP_FUSED = True
 
 
 def _diag3(M, a, b):

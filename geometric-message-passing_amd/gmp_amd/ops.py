@@ -4,10 +4,8 @@ Every op launches on the current PyTorch HIP stream, allocates its outputs throu
 caching allocator and never synchronises.  Inputs must be CUDA (HIP) tensors: there is no CPU
 fallback in the product path.
 """
-import atexit
 import ctypes
 
-import os
 
 import torch
 from torch.autograd.function import once_differentiable
@@ -238,41 +236,10 @@ _CB_QUEUED = [False]
 _KEEPALIVE = []
 
 
-# CUs the side stream may dispatch onto (gmp_stream_create_cu_share; 0 = an ordinary stream over
-# the whole chip): a hardware partition that keeps the split-K weight-gradient sums off the rest
-# of the CUs, where the critical path's node-level kernels run.  A CU-masked stream is a
-# blocking stream (it synchronises with the legacy default stream), so it is used only when the
-# caller's stream is not the default stream (bench.py GMP_MAIN_STREAM=1 runs the step on its own
-# stream).  Off by default: EGNN C2 measured 98.05 / 97.52 vs 98.15 / 97.45 M edges/s unmasked
-# (64 CUs; 32-192 within the same noise) -- the step is bound by total kernel work, not by
-# the side stream crowding the critical path's kernels.
-SIDE_CUS = int(os.environ.get("GMP_SIDE_CUS", "0") or 0)
-
-
-def _destroy_stream(ptr):
-    # before interpreter teardown: the runtime's own finalisers must not meet a live masked
-    # stream (a rocprofv3-traced run crashed in __cxa_finalize without this)
-    try:
-        torch.cuda.synchronize()
-        _lib.load().gmp_stream_destroy(ctypes.c_void_p(ptr))
-    except Exception:  # pragma: no cover - best effort at exit
-        pass
-
-
-def _side_stream(device, masked=False, lane=0):
-    key = (device, masked and SIDE_CUS > 0, lane)
-    st = _SIDE_STREAMS.get(key)
+def _side_stream(device):
+    st = _SIDE_STREAMS.get(device)
     if st is None:
-        if key[1]:
-            ptr = ctypes.c_void_p()
-            with torch.cuda.device(device):
-                _lib.check(_lib.load().gmp_stream_create_cu_share(SIDE_CUS, ctypes.byref(ptr)),
-                           "gmp_stream_create_cu_share")
-            st = torch.cuda.ExternalStream(ptr.value, device=device)
-            atexit.register(_destroy_stream, ptr.value)
-        else:
-            st = torch.cuda.Stream(device=device)
-        _SIDE_STREAMS[key] = st
+        st = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
     return st
 
 
@@ -310,10 +277,6 @@ def _engine_accumulates(p):
         return False
 
 
-# Split-K workgroup cap of the side-stream outer sums (gmp_wgrad_set_grid_cap; 0 = none): with
-# fewer workgroups the weight gradients leave CUs to the critical path's node-level kernels.
-SIDE_GRID_CAP = int(os.environ.get("GMP_SIDE_GRID_CAP", "0") or 0)
-
 def compiling():
     """True while torch.compile (dynamo) traces: the ops then run inline on the current stream,
     without the per-graph caches, side streams or end-of-backward callbacks of eager mode."""
@@ -324,36 +287,26 @@ class side_work:
     """with side_work(used_tensors) as sw: ... launches on the side stream after everything
     already queued on the current stream; sw.deliver(...) hands each result to the end-of-
     backward accumulation (deferred leaf gradients) or back through autograd (after joining the
-    streams).  tail=True: nothing on the critical path follows (no split-K grid cap).  Under
-    torch.compile the work runs inline and every gradient goes back through autograd.  lane > 0
-    picks another side stream: work that must not queue behind the first side stream's (the
-    EGNN edge-level sums behind the node-level ones) runs concurrently with it; deliver(...,
-    extra=(other side_work, ..)) joins those streams too."""
+    streams).  Under torch.compile the work runs inline and every gradient goes back through
+    autograd."""
 
-    def __init__(self, *used, tail=False, lane=0, inline=False):
+    def __init__(self, *used):
         self.used = [t for t in used if t is not None]
-        self.cap = 0 if tail else SIDE_GRID_CAP
-        self.inline = compiling() or inline
-        self.lane = lane
-        self.extra = ()
+        self.inline = compiling()
 
     def __enter__(self):
         if self.inline:
             return self
         self.main = torch.cuda.current_stream()
-        self.side = _side_stream(self.main.device, masked=self.main.cuda_stream != 0,
-                                 lane=self.lane)
+        self.side = _side_stream(self.main.device)
         self.side.wait_stream(self.main)
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
-        self.prev_cap = _lib.load().gmp_wgrad_set_grid_cap(self.cap) if self.cap else None
         return self
 
     def __exit__(self, *exc):
         if self.inline:
             return False
-        if self.prev_cap is not None:
-            _lib.load().gmp_wgrad_set_grid_cap(self.prev_cap)
         self.ctx.__exit__(*exc)
         _KEEPALIVE.extend(self.used)
         return False
@@ -367,17 +320,14 @@ class side_work:
     def join(self, *results):
         """results are needed on the current stream now (returned through autograd)."""
         self.main.wait_stream(self.side)
-        for o in self.extra:
-            self.main.wait_stream(o.side)
         _KEEPALIVE.clear()
         for r in results:
             if r is not None:
                 r.record_stream(self.main)
 
-    def deliver(self, needs_input_grad, first, targets, grads, extra=()):
+    def deliver(self, needs_input_grad, first, targets, grads):
         """Per parameter: defer the gradient (leaf parameter) or hand it back through autograd
         (after joining the streams).  needs_input_grad[first + i] belongs to targets[i]."""
-        self.extra = tuple(o for o in extra if not o.inline)
         if self.inline:
             return tuple(gr if needs_input_grad[first + i] else None
                          for i, gr in enumerate(grads))
@@ -401,8 +351,6 @@ class side_work:
             # no parameter gradient wanted (e.g. autograd.grad w.r.t. inputs only): nothing will
             # flush this side work, so join here and release the kept-alive inputs
             self.main.wait_stream(self.side)
-            for o in self.extra:
-                self.main.wait_stream(o.side)
             _KEEPALIVE.clear()
         return tuple(out)
 
@@ -414,32 +362,8 @@ def _mm_wt(g, Wt):
     return g.mm(Wt.t())
 
 
-# Row-level Linears (node rows of the EGNN update MLP and message projections, edge rows of the
-# per-edge Linears) on the K7g kernel: [a1 | a2] B^T + b on the bf16 MFMA over exact three-plane
-# f32 splits (gmp_gemm_x3_f32; f32-class, see gmp_tpgemm.hip).  Off by default (GMP_ROW_GEMM=x3
-# turns it on): the K7g tile is built for long k ranges and measured slower than the library f32
-# GEMMs at K <= 256 (scripts/mb_rowgemm.py: 50k x 128 x 128 36 vs 38 us, 50k x 256 x 128 66 vs
-# 55 us, 1M x 128 x 128 508 vs 415 us; EGNN step 80 vs 87 M edges/s on one box).
-ROW_GEMM = os.environ.get("GMP_ROW_GEMM", "torch")
-
-
-def _x3_fits(n, *ks):
-    return ROW_GEMM == "x3" and n % 16 == 0 and n > 0 and all(k % 32 == 0 for k in ks)
-
-
-def linear_x3(a1, a2, W, b=None, transpose=False):
-    """[a1 | a2] @ B^T (+ b) with B = W (W (n, k): y = x W^T) or, transpose=True, B = W^T
-    (W (k, n): dx = g W); W may be a strided slice of a parameter."""
-    tops = _lib.torch_ops()
-    n = W.shape[1] if transpose else W.shape[0]
-    return tops.gemm_x3(_f32c(a1), None if a2 is None else _f32c(a2),
-                        tops.split_x3(W, transpose), n, b)
-
-
 def _dx(g, W):
     """g @ W for the dx of y = x W^T (W (n_out, n_in))."""
-    if _x3_fits(W.shape[1], W.shape[0]):
-        return linear_x3(g, None, W, None, True)
     return _mm_wt(g, W.t().contiguous())
 
 
@@ -452,8 +376,6 @@ class EdgeLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W, b)
-        if _x3_fits(W.shape[0], W.shape[1]):
-            return linear_x3(x, None, W, b)
         return torch.addmm(b, x, W.t()) if b is not None else x.mm(W.t())
 
     @staticmethod
@@ -479,8 +401,6 @@ class SplitLinearFn(torch.autograd.Function):
     def forward(ctx, xa, xb, W, b):
         da = xa.shape[1]
         ctx.save_for_backward(xa, xb, W, b)
-        if _x3_fits(W.shape[0], da, xb.shape[1]):
-            return linear_x3(xa, xb, W, b)  # one GEMM over the two K ranges
         y = torch.addmm(b, xa, W[:, :da].t()) if b is not None else xa.mm(W[:, :da].t())
         y.addmm_(xb, W[:, da:].t())
         return y
@@ -840,13 +760,10 @@ def _egnn_params(tensors):
     return _lib.GmpEgnnParams(*[t.data_ptr() for t in tensors])
 
 
-# EGNN dW2 / dW3 on the HF outer sums (two scaled fp16 planes; "0": split-plane x3)
-EGNN_WGRAD_HF = os.environ.get("GMP_EGNN_WGRAD_HF", "1") != "0"
 # LayerNorm outputs the EGNN forward saves for the backward: 2 = x_hat1, x_hat2 (x_hat3 recomputed
-# in the backward, bitwise the forward's; default), 3 = x_hat1..3 (the r02 form, for A/B).  The
-# backward follows the saved tensor's plane count, so changing this between a forward and its
-# backward is harmless.
-EGNN_XHAT_PLANES = int(os.environ.get("GMP_EGNN_XHAT_PLANES", "2"))
+# in the backward, bitwise the forward's), 3 = x_hat1..3 (the r02 form; tests compare the two).
+# The backward follows the saved tensor's plane count.
+EGNN_XHAT_PLANES = 2
 
 
 class EgnnMessageFn(torch.autograd.Function):
@@ -873,7 +790,7 @@ class EgnnMessageFn(torch.autograd.Function):
         E = graph.num_edges
         if AB is None:  # [h W1a^T | h W1b^T] (else: K15 produced it with the previous update)
             Wcat = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)
-            AB = linear_x3(h, None, Wcat) if _x3_fits(2 * d, d) else h.mm(Wcat.t())
+            AB = h.mm(Wcat.t())
         params = tuple(_f32c(t) for t in (W1[:, 2 * d], b1, ln1w, ln1b, W2, b2, ln2w, ln2b, W3,
                                           b3, ln3w, ln3b, w4, b4))
         # save the LayerNorm outputs only for a backward: grad_mode is the CALLER's
@@ -903,7 +820,7 @@ class EgnnMessageFn(torch.autograd.Function):
         f = dict(dtype=torch.float32, device=dev)
         # HF weight-gradient outer sums: the backward kernel folds max |dpre2|, |dpre3| into
         # two device words that scale their fp16 planes
-        amax = torch.zeros(2, dtype=torch.int32, device=dev) if EGNN_WGRAD_HF else None
+        amax = torch.zeros(2, dtype=torch.int32, device=dev)
         with _timed("egnn_edge_bwd"):
             dA, dpos_recv, dpre1, gdiff, dpre2, dpre3, partials = \
                 _lib.torch_ops().egnn_edge_bwd(pos, graph.rowptr, graph.recv, graph.send,
@@ -913,13 +830,9 @@ class EgnnMessageFn(torch.autograd.Function):
         # critical path: sender-side sums (deterministic, sender CSR) and dh
         dB, _ = segment_reduce(dpre1, graph.send_csr, "sum")
         dpos_send, _ = segment_reduce(gdiff, graph.send_csr, "sum")
-        if _x3_fits(d, d, d):
-            # dh = [dA | dB] [W1a ; W1b]: one GEMM over the two K ranges
-            dh = linear_x3(dA, dB, torch.cat([W1[:, :d], W1[:, d:2 * d]], 0), None, True)
-        else:
-            W1t = W1[:, :2 * d].t().contiguous()  # [W1a | W1b]^T: NT-form GEMMs for dh
-            dh = _mm_wt(dA, W1t[:d])
-            dh.addmm_(dB, W1t[d:].t())
+        W1t = W1[:, :2 * d].t().contiguous()  # [W1a | W1b]^T: NT-form GEMMs for dh
+        dh = _mm_wt(dA, W1t[:d])
+        dh.addmm_(dB, W1t[d:].t())
         dpos = dpos_recv - dpos_send
 
         # weight gradients: side stream, accumulated at the end of the backward pass
@@ -928,11 +841,8 @@ class EgnnMessageFn(torch.autograd.Function):
         # side stream they took the CUs from the critical path's node-level backward kernels
         # (LayerNorm backward + its column sums 0.33 ms instead of ~0.04 ms per layer, trace);
         # A/B on one box, 20-step runs: 114.4 (113.7-115.0) vs 113.2 (112.9-113.4) M edges/s
-        with side_work(dpre2, dpre3, xhat, amax, inline=True) as sw2:
-            dW2, db2 = edge_outer_sum_act(dpre2, xh1, ln1w, ln1b, ctx.act,
-                                          amax[0:1] if amax is not None else None)
-            dW3, db3 = edge_outer_sum_act(dpre3, xh2, ln2w, ln2b, ctx.act,
-                                          amax[1:2] if amax is not None else None)
+        dW2, db2 = edge_outer_sum_act(dpre2, xh1, ln1w, ln1b, ctx.act, amax[0:1])
+        dW3, db3 = edge_outer_sum_act(dpre3, xh2, ln2w, ln2b, ctx.act, amax[1:2])
         with side_work(h, dA, dB, partials) as sw:
             dW1 = torch.empty((d, 2 * d + 1), **f)
             db1 = torch.empty(d, **f)
@@ -947,7 +857,7 @@ class EgnnMessageFn(torch.autograd.Function):
         # then b1 ... b4 (params[0] is the contiguous copy of W1's distance column)
         targets = (W1,) + tuple(params[1:])
         return (dh, dpos, None, None, None, None) + sw.deliver(ctx.needs_input_grad, 6, targets,
-                                                               grads, extra=(sw2,)) + (None, None)
+                                                               grads) + (None, None)
 
 
 def egnn_exact_mode():

@@ -30,8 +30,11 @@ extern "C" {
  * the TP descriptor holds 8 output blocks (128 bytes), <= 48 paths.
  * 2 (r04): EGNN forward / backward take save_planes; gmp_egnn_set_xhat_mode and
  * gmp_egnn_edge_bwd_ab_f32 removed.  (r03 changed gmp_triplet_fill_f32 under version 1.)
- * Version 4 (r05): gmp_egnn_node_fwd_f32 / gmp_egnn_node_params added. */
-#define GMP_ABI_VERSION 4
+ * 4 (r05): gmp_egnn_node_fwd_f32 / gmp_egnn_node_params added.
+ * Version 5 (r05): the opt-in TP kernels K7s / K7f (gmp_tp_node_fwd_fused_f32,
+ * gmp_tp_z_fused_layout_*, gmp_tp_node_dw_*), the row GEMM (gmp_split_x3_f32, gmp_gemm_x3_f32),
+ * gmp_tp_gemm_set_rings, gmp_wgrad_set_grid_cap and the CU-masked stream entries removed. */
+#define GMP_ABI_VERSION 5
 
 enum {
   GMP_OK = 0,
@@ -132,7 +135,7 @@ typedef struct gmp_egnn_params {
  * x_hat3.  The backward takes the same save_planes (the caller keeps it with the buffer). */
 /* The two d x d products per edge chunk run by default on the f16 MFMA over 2-plane (hi + lo)
  * splits of the operands with power-of-two scaling (22-bit operands, f32 accumulation; relative
- * error ~2^-21 per product); gmp_egnn_set_f32_mfma(1) (or GMP_EGNN_F32_MFMA=1 at load) selects
+ * error ~2^-21 per product); gmp_egnn_set_f32_mfma(1) selects
  * the exact f32-MFMA fmaf chains.  Returns the previous setting. */
 int gmp_egnn_set_f32_mfma(int on);
 int gmp_egnn_edge_fwd_f32(int64_t n_nodes, int64_t n_edges, int64_t d, const float* AB,
@@ -222,20 +225,10 @@ int gmp_egnn_edge_bwd_amax_f32(int64_t n_nodes, int64_t n_edges, int64_t d, cons
  * deterministic.  d in {32, 64, 128}.  Arithmetic (all outer-sum entry points below): f32
  * operands split exactly into three bf16 planes on the bf16 MFMA with f32 accumulation, the
  * six partial products of order <= 2^-16 summed (error vs fp64 <= 2^-26 of sum |a b|, within
- * 2x of the f32-MFMA kernels', below rocBLAS f32 GEMM's); gmp_wgrad_set_f32_mfma(1) (or GMP_WGRAD_F32_MFMA=1 at load) selects the f32-MFMA
+ * 2x of the f32-MFMA kernels', below rocBLAS f32 GEMM's); gmp_wgrad_set_f32_mfma(1) selects the f32-MFMA
  * kernels instead, returns the previous setting.
  * ------------------------------------------------------------------------------------------ */
 int gmp_wgrad_set_f32_mfma(int on);
-/* Cap the split-K workgroup count of the outer sums (0 = none, the default: 1-2 per CU); returns
- * the previous cap.  Host-side setting read at launch (and by the workspace-size queries). */
-int gmp_wgrad_set_grid_cap(int blocks);
-/* CU-partitioned stream (no reference counterpart: the reference runs every op on one stream).
- * Creates a non-blocking stream of the current device whose kernels dispatch only onto `cus`
- * CUs spread evenly over the CU index space (hipExtStreamCreateWithCUMask; cus >= the CU count:
- * an unmasked stream); the side-stream weight gradients run there so the critical path's
- * kernels keep the other CUs.  *stream receives the hipStream_t; gmp_stream_destroy frees it. */
-int gmp_stream_create_cu_share(int cus, void** stream);
-int gmp_stream_destroy(void* stream);
 size_t gmp_edge_outer_sum_workspace_size(int64_t K, int64_t d);
 int gmp_edge_outer_sum_f32(int64_t K, int64_t d, const float* A, const float* B, float* C,
                            float* colsum_A, void* workspace, size_t workspace_bytes,
@@ -439,17 +432,12 @@ int gmp_tp_node_outer_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
 int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* eoff,
                           const float* Z, const float* A, const float* T, const float* Tb,
                           float* dZ, float* dA, void* stream);
-/* apply runs on the bf16 MFMA over exact three-plane splits where w % 32 == 0, H % 64 == 0 and
- * the operands are 16-byte aligned (default), else on the f32 MFMA; set_x3(0) forces the f32
- * kernel (A/B studies; GMP_TP_APPLY_F32=1 at load).  Returns the previous setting. */
+/* apply runs on the bf16 MFMA over exact three-plane splits where its shapes allow (2, the
+ * default: the v3 kernel for H = 256 and w % 32 == 0, then the v2 kernel for w >= 512,
+ * w % 32 == 0, H % 64 == 0, 16-byte aligned operands), else on the f32 MFMA; set_x3(1) skips the
+ * v3 kernel, set_x3(0) forces the f32 one (tests cover every form).  Returns the previous
+ * setting. */
 int gmp_tp_apply_set_x3(int on);
-
-/* Register-ring depths of the K7g path GEMMs (A/B studies; results are bitwise identical for
- * every setting: the rings change when operands are fetched, not the accumulation order).
- * a_ring: stages of the forward GEMM's A stream in flight (2, 4, 8; 44 = A and B rings of 4);
- * b_ring: steps of the T GEMM's B stream in flight (2 or 4).  Defaults 8 / 4
- * (GMP_TPGEMM_RING / GMP_TPGEMM_WIDEN_RING).  Returns the previous a_ring * 16 + b_ring. */
-int gmp_tp_gemm_set_rings(int a_ring, int b_ring);
 
 /* K7g path GEMMs of the receiver-factorised TP convolution on the bf16 MFMA through exact
  * three-plane f32 splits (replaces the library f32 GEMMs out = S W2p + Sb b2p and
@@ -480,49 +468,9 @@ int gmp_tp_gemm_x3_f32(int64_t M, int64_t N, int64_t K1, const float* A1, int64_
  * K a multiple of 32, <= 128.  Each workgroup keeps its split A rows in LDS and sweeps a range
  * of column tiles with B loaded straight into registers; C is written with non-temporal
  * stores. */
-/* Node-level Linears on the same kernel (K7g tile, A split on load, B pre-split): replaces the
- * library f32 GEMMs of torch.nn.functional.linear / Tensor.mm over the node rows (egnn_layer.py
- * :37-39 mlp_upd, :28 the node projections of mlp_msg[0]; their dx GEMMs).
- * gmp_split_x3_f32: the three bf16 planes of the N x K operand B[n][k] = B[n sn + k sk] in MFMA
- *   fragment order (3 N K unsigned shorts; N % 16 == 0, K % 32 == 0).
- * gmp_gemm_x3_f32: C[m][n] (+)= sum_k [A1 | A2][m][k] B[n][k] + bias[n] (bias may be NULL;
- *   A2 may be NULL with K2 = 0; K1, K2 multiples of 32; C row stride ldc). */
-int gmp_split_x3_f32(int64_t N, int64_t K, const float* B, int64_t sn, int64_t sk, void* Bp,
-                     void* stream);
-int gmp_gemm_x3_f32(int64_t M, int64_t N, const float* A1, int64_t K1, int64_t lda1,
-                    const float* A2, int64_t K2, int64_t lda2, const void* Bp, const float* bias,
-                    float* C, int64_t ldc, int accumulate, void* stream);
 int gmp_tp_gemm_x3_widen_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                              const void* Bp, int64_t ldb, int64_t bplane, float* C, int64_t ldc,
                              void* stream);
-/* K7f: dW2p of one TP path without the S intermediate in HBM (backward of the node form):
- *   dW[(u H + j) mul_out + w] = sum_(n, k) S[(n, k), (u, j)] G[(n k-major rows), w],
- *   S[(n, k), (u, j)] = sum_{eoff[n] <= e < eoff[n+1]} Z[e, k mul1 + u] A[e, j]
- * Z (edges x d3 mul1, row-major), A (edges x H), G (n_recv d3 x mul_out), eoff (n_recv + 1,
- * chunk-local).  mul1 % 16 == 0, H % 16 == 0, mul_out in {64, 128} (GMP_ERR_UNSUPPORTED
- * otherwise).  Deterministic (partial slabs summed in range order).  Replaces the S write of
- * gmp_tp_node_outer_f32 + the S read of gmp_outer_sum_cols_f32 (tfn_layer.py:73-87). */
-size_t gmp_tp_node_dw_workspace_size(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H,
-                                     int64_t mul_out);
-/* K7s: forward of one TP path without the S intermediate in HBM (tfn_layer.py:73-87 regrouped):
- *   C[n cldg + w d3 + k] += sum_{u,j} S[(n, k), (u, j)] W2p[(u, j), w] + sum_u Sb[(n, k), u] b2p[u, w]
- * with S, Sb as for gmp_tp_node_dw_f32 (z rows, A (edges x H), eoff (n_recv + 1, chunk-local))
- * and Bf the forward B planes of gmp_tp_split_w2_f32 (fwd = 1: [W2p | b2p]^T).  The z rows come
- * in the K7s layout Zf (gmp_tp_z_fused_layout_f32 of the (zrows x d3 mul1) rows).  d3 in {3, 5,
- * 7}, mul_out in {64, 128}, mul1 % 32 == 0, H % 32 == 0 (GMP_ERR_UNSUPPORTED otherwise).
- * Deterministic.  Replaces gmp_tp_node_outer_f32 + gmp_tp_gemm_x3_f32 (forward). */
-int gmp_tp_node_fwd_fused_f32(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H,
-                              int64_t mul_out, const int64_t* eoff, const float* Zf,
-                              int64_t zrows, const float* A, const void* Bf, float* C,
-                              int64_t cldg, void* stream);
-/* The K7s z layout: Zf[us][e][16] = z[e][k mul1 + us U + uu] at c = k U + uu < d3 U (U = 16 / d3),
- * zero elsewhere (and for us U + uu >= mul1); us < ceil(mul1 / U).  _floats: the size of Zf. */
-int64_t gmp_tp_z_fused_layout_floats(int64_t rows, int64_t d3, int64_t mul1);
-int gmp_tp_z_fused_layout_f32(const float* Z, int64_t rows, int64_t d3, int64_t mul1, float* Zf,
-                              void* stream);
-int gmp_tp_node_dw_f32(int64_t n_recv, int64_t d3, int64_t mul1, int64_t H, int64_t mul_out,
-                       const int64_t* eoff, const float* Z, const float* A, const float* G,
-                       float* dW, void* workspace, size_t workspace_bytes, void* stream);
 /* Wide edge/row reduction C (m_total x n, row stride ldc) = A^T B over K rows, A (K x m_total,
  * row stride lda), B (K x n, ldb), m_total a multiple of 128, n a multiple of 16 (<= 128): the
  * TP path GEMM dW2p = S^T G.  Split-plane bf16 MFMA (the K5 kernel with column blocks of 128),

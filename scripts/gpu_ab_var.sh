@@ -1,12 +1,12 @@
-# A/B of library builds on one box: GPU tests of the in-tree build (GMP_TESTS, optional), then
+# A/B of library builds on one box: GPU tests of the in-tree build (TESTS, optional), then
 # bench.py for each "name:args" in $@ (name "tree" = the in-tree libraries, else abvar/<name>/).
 # Every GPU step has its own time limit; a failure ends the script.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
-if [ -n "${GMP_TESTS:-}" ]; then
-  timeout -k 10 600 python -u -m pytest $GMP_TESTS -x -q -m gpu --timeout 180 --timeout-method thread > gpurun_out/ab/pytest.log 2>&1 || { tail -40 gpurun_out/ab/pytest.log; exit 1; }
+if [ -n "${TESTS:-}" ]; then
+  timeout -k 10 600 python -u -m pytest $TESTS -x -q -m gpu --timeout 180 --timeout-method thread > gpurun_out/ab/pytest.log 2>&1 || { tail -40 gpurun_out/ab/pytest.log; exit 1; }
   tail -2 gpurun_out/ab/pytest.log
 fi
 i=0

@@ -1,5 +1,5 @@
 # Round-end style check on the GPU box: build, GPU tests, smoke, default bench (+ optional
-# rocprofv3 stats when GMP_PROFILE=1).  Every GPU step has its own time limit; stops at the
+# rocprofv3 stats when PROFILE=1).  Every GPU step has its own time limit; stops at the
 # first failure.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -11,7 +11,7 @@ echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || exit $?
-if [ "${GMP_PROFILE:-0}" = "1" ]; then
+if [ "${PROFILE:-0}" = "1" ]; then
   mkdir -p gpurun_out/prof
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o egnn -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
 fi

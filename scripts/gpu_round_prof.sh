@@ -3,5 +3,5 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 bash scripts/gpu_round.sh || exit $?
-GMP_NO_TESTS=1 bash scripts/gpu_profile.sh egnn 5 || exit $?
+NO_TESTS=1 bash scripts/gpu_profile.sh egnn 5 || exit $?
 bash scripts/gpu_profile.sh mace 2 || exit $?

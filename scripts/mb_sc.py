@@ -1,6 +1,6 @@
 """K8 symmetric contraction timing at the C4 shape (50k nodes, 128 channels, 0e+1o+2e,
 correlation 3) and the widened shapes: forward and backward (dx + dA partials), HIP events.
-Usage (GPU box): python scripts/mb_sc.py  (GMP_SC_ROLLED=1 for the rolled-loop kernels)"""
+Usage (GPU box): python scripts/mb_sc.py"""
 import os
 import sys
 
@@ -35,5 +35,4 @@ for D, corr in [(9, 3), (9, 2), (9, 4), (16, 3), (4, 4)]:
     g = torch.randn(N, D * C, device="cuda")
     tf = timeit(lambda: ops.symmetric_contraction_fwd(x, corr, *Ao))
     tb = timeit(lambda: ops.symmetric_contraction_bwd(x, corr, *Ao, g))
-    print(f"D={D:2d} corr={corr}: fwd {tf:7.3f} ms  bwd {tb:7.3f} ms "
-          f"(rolled={os.environ.get('GMP_SC_ROLLED', '0')})", flush=True)
+    print(f"D={D:2d} corr={corr}: fwd {tf:7.3f} ms  bwd {tb:7.3f} ms", flush=True)

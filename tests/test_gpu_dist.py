@@ -166,15 +166,20 @@ def test_product_world2_gloo_on_gpu_matches_single_process(kind, mode):
         res = [torch.load(os.path.join(d, f"{mode}{r}.pt"), weights_only=True)
                for r in range(world)]
         ref = torch.load(os.path.join(d, f"{mode}_ref.pt"), weights_only=True)
-    # both steps' averaged gradients (what the collective delivered to the optimizer)
+    # both steps' averaged gradients (what the collective delivered to the optimizer).  Step 1:
+    # 1e-5 of the gradient's scale.  Step 2 is evaluated at parameters that agree to 1e-6 (checked
+    # below): under DDP (all-reduce of the per-rank means, not the reference's summation order,
+    # then a non-fused Adam) the second gradients are sensitivity-limited to ~3e-5 of scale on
+    # the EGNN / TFN heads, so 1e-4 there -- a missing or wrong collective is off by O(1).
     bad = []
     for step_key in ("grads", "grads2"):
+        tol = 1e-4 if (step_key == "grads2" and mode == "ddp") else 1e-5
         for k, g in ref[step_key].items():
             for r in range(world):
                 got = res[r][step_key].get(k, torch.zeros_like(g))
                 err, scale = (got - g).abs().max().item(), g.abs().max().item()
                 print(f"{step_key} {k} rank {r}: max|d| {err:.3e} scale {scale:.3e}")
-                if err > 1e-5 * scale + 1e-7:
+                if err > tol * scale + 1e-7:
                     bad.append((step_key, k, r, err, scale))
     assert not bad, bad
     # parameters after ONE optimizer step (equal first-step gradients): 1e-6

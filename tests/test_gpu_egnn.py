@@ -248,37 +248,6 @@ def test_xhat_saved_planes_only():
                                        params, 0, False, 1e-5, True, 1)
 
 
-def test_cu_masked_side_stream_same_gradients(monkeypatch):
-    """With GMP_SIDE_CUS set, off the default stream the weight gradients run on a CU-masked
-    side stream (gmp_stream_create_cu_share); the step must give bitwise the same loss and
-    gradients as on the default stream (unmasked side stream): same kernels, fixed orders."""
-    import gmp_amd
-    from gmp_amd import ops
-    monkeypatch.setattr(ops, "SIDE_CUS", 64)
-    torch.manual_seed(4)
-    g = _graph(2000, 40000, seed=6)
-    model = gmp_amd.EGNNModel(num_layers=2, emb_dim=128).to(DEV)
-    batch = g.to(DEV)
-
-    def step():
-        model.zero_grad(set_to_none=True)
-        loss = model(batch).sum()
-        loss.backward()
-        return loss.detach().clone(), [p.grad.clone() for p in model.parameters()]
-
-    l0, g0 = step()
-    st = torch.cuda.Stream()
-    st.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(st):
-        l1, g1 = step()
-        assert (DEV, True) in [(str(k[0].type), k[1]) for k in ops._SIDE_STREAMS]
-    torch.cuda.current_stream().wait_stream(st)
-    torch.cuda.synchronize()
-    assert torch.equal(l0, l1)
-    for a, b in zip(g0, g1):
-        assert torch.equal(a, b)
-
-
 def test_autograd_grad_inputs_leaves_param_grads_alone():
     """torch.autograd.grad w.r.t. positions (force-style) must not accumulate into p.grad (the
     deferred side-stream gradients only go to .grad when the engine accumulates), and

@@ -106,37 +106,6 @@ def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp, mode, monkeypatc
     _grads(lay, ref)
 
 
-@pytest.mark.parametrize("inp,bn", [("128x0e+128x1o+128x2e", True), ("64x0e+64x1o+64x2e", False)])
-def test_tp_conv_layer_fused_forward_vs_oracle(inp, bn, monkeypatch):
-    """The opt-in K7s forward (GMP_TP_FWD_FUSED=1: S built inside the path GEMM for the lo >= 1
-    paths) through the whole layer, forward and backward, against the oracle."""
-    from gmp_amd import equivariant as eq
-    monkeypatch.setattr(eq, "TP_MODE", "node")
-    monkeypatch.setattr(eq, "TP_FWD_FUSED", True)
-    torch.manual_seed(3)
-    n = 240
-    g = _graph(n, 12 * n, seed=9)
-    ref = om.TensorProductConvLayer(inp, inp, oo3.spherical_harmonics_irreps(2), 8, 64, "add",
-                                    batch_norm=bn)
-    lay = eq.TensorProductConvLayer(inp, inp, eq.o3.sh_irreps(2), 8, 64, "add", batch_norm=bn)
-    lay.load_state_dict(ref.state_dict())
-    lay = lay.to(DEV)
-    x = torch.randn(g.num_nodes, oo3.Irreps(inp).dim)
-    sh = oo3.spherical_harmonics_l2(g.pos[g.edge_index[0]] - g.pos[g.edge_index[1]])
-    ef = torch.rand(g.num_edges, 8)
-    xs = [t.clone().to(DEV).requires_grad_(True) for t in (x, sh, ef)]
-    xr = [t.clone().requires_grad_(True) for t in (x, sh, ef)]
-    y = lay(xs[0], g.edge_index.to(DEV), xs[1], xs[2])
-    yr = ref(xr[0], g.edge_index, xr[1], xr[2])
-    torch.testing.assert_close(y.detach().cpu(), yr.detach(), atol=1e-5, rtol=1e-5)
-    gy = torch.randn_like(yr)
-    (y * gy.to(DEV)).sum().backward()
-    (yr * gy).sum().backward()
-    for a, b, nm in zip(xs, xr, ("dx", "dsh", "dedge_feat")):
-        _close_scaled(a.grad, b.grad, 1e-4, nm)
-    _grads(lay, ref)
-
-
 @pytest.mark.parametrize("inp,out,gate,mlp", [
     ("16x0e", "16x0e+16x1o+16x2e+16x3o", True, 32),
     ("16x0e+16x1o+16x2e+16x3o", "16x0e+16x1o+16x2e+16x3o", True, 32),

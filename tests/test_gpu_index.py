@@ -146,8 +146,9 @@ def test_torch_ops_boundary_and_compile():
     m, pa, xh, rs = torch.ops.gmp.egnn_edge_fwd(AB.detach(), pos, eg.rowptr, eg.recv, eg.send,
                                                 params, 0, False, 1e-5, False)
     with torch.no_grad():
+        # grad_mode=False: the inference kernel, as the raw call above (train=False)
         m_ref, p_ref = ops.EgnnMessageFn.apply(h, pos, eg, "relu", False, 1e-5,
-                                               *[p for p in (W1, *params[1:])])
+                                               *[p for p in (W1, *params[1:])], False)
     assert torch.equal(m, m_ref) and torch.equal(pa, p_ref)
     assert xh.numel() == 0
     counters.clear()

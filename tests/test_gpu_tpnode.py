@@ -119,27 +119,17 @@ def test_split_w2_planes_exact(m1, mo, H):
     assert torch.equal(t, W.permute(0, 2, 1).reshape(K1, mo))
 
 
-@pytest.mark.parametrize("ring", [8, 4, 44, 2])
 @pytest.mark.parametrize("M,N,K1,K2,grp", [(1000, 128, 256, 32, 5), (333, 64, 128, 0, 1),
                                            (257, 4096, 128, 0, 1), (130, 128, 4096, 128, 3),
                                            (65, 32, 96, 32, 1), (5003, 64, 1024, 64, 3),
                                            (700, 48, 256, 32, 5)])
-def test_tp_gemm_x3_matches_fp64(M, N, K1, K2, grp, ring):
+def test_tp_gemm_x3_matches_fp64(M, N, K1, K2, grp):
     """gmp_tp_gemm_x3_f32 (bf16 MFMA over three-plane splits) against fp64: error per entry
     <= 1e-6 of sum |a b| (f32-class; f32 unit roundoff 6e-8, a K-term f32 sum ~ sqrt(K) of it),
     ragged M / N tiles, the second A operand, the grouped (r / grp) epilogue addressing with
-    accumulation into an existing output; every register-ring depth (k-step counts that are and
-    are not multiples of the ring: 9, 4 and 132 steps); N <= 64 runs the 256 x 64 tile (C5's
-    64-channel paths; ragged rows of its 256-row tile)."""
-    from gmp_amd import _lib
-    old_rings = _lib.load().gmp_tp_gemm_set_rings(ring, 4)
-    try:
-        _tp_gemm_x3_case(M, N, K1, K2, grp)
-    finally:
-        _lib.load().gmp_tp_gemm_set_rings(old_rings // 16, old_rings % 16)
-
-
-def _tp_gemm_x3_case(M, N, K1, K2, grp):
+    accumulation into an existing output; k-step counts that are and are not multiples of the
+    8-deep register ring (9, 4 and 132 steps; K <= 256 takes the 2-deep ring); N <= 64 runs the
+    256 x 64 tile (C5's 64-channel paths; ragged rows of its 256-row tile)."""
     from gmp_amd import _lib
     from gmp_amd.ops import _p, _stream
     lib = _lib.load()
@@ -217,24 +207,14 @@ def test_outer_sum_cols_matches_fp64(K, m_total, n):
     assert err < 1e-6, err
 
 
-@pytest.mark.parametrize("bring", [4, 2])
 @pytest.mark.parametrize("M,N,K", [(1000, 8192, 128), (333, 4096 + 64, 64), (130, 1024, 96),
                                    (17, 256, 32), (40, 384, 96)])
-def test_tp_gemm_x3_widen_matches_fp64(M, N, K, bring):
+def test_tp_gemm_x3_widen_matches_fp64(M, N, K):
     """gmp_tp_gemm_x3_widen_f32 (resident A, swept column tiles): C = A B^T within 1e-6 of
-    sum |a b| per entry, ragged M and N, every K / 32 variant, both B-ring depths."""
+    sum |a b| per entry, ragged M and N, every K / 32 variant."""
     from gmp_amd import _lib
     from gmp_amd.ops import _p, _stream
     lib = _lib.load()
-    old_rings = lib.gmp_tp_gemm_set_rings(8, bring)
-    try:
-        _widen_case(lib, M, N, K)
-    finally:
-        lib.gmp_tp_gemm_set_rings(old_rings // 16, old_rings % 16)
-
-
-def _widen_case(lib, M, N, K):
-    from gmp_amd.ops import _p, _stream
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g)
     B = torch.randn(N, K, generator=g) * torch.logspace(-4, 1, K)
@@ -299,102 +279,3 @@ def test_node_apply_bf16x3_matches_fp64(w, H, x3):
         ez = ((dZ[e0:e1].cpu().double() - rz).abs() / mz).max().item()
         ea = ((dA[e0:e1].cpu().double() - ra).abs() / ma).max().item()
         assert ez < 1e-6 and ea < 1e-6, (n, degs[n], ez, ea)
-
-
-@pytest.mark.parametrize("d3,mul1,H,mo,nrecv,seed", [
-    (5, 32, 32, 128, 23, 0), (3, 16, 48, 64, 41, 1), (1, 64, 32, 64, 70, 2),
-    (5, 128, 256, 128, 13, 3), (3, 64, 256, 64, 35, 4)])
-def test_node_dw_fused_matches_fp64(d3, mul1, H, mo, nrecv, seed):
-    """K7f (gmp_tp_node_dw_f32 via torch.ops.gmp.tp_node_dw): dW2p[(u, j), w] =
-    sum_(n, k) S[(n, k), (u, j)] G[(n, k), w] with S built in-kernel from z and a, against the
-    fp64 evaluation; receivers of in-degree 0, 1 and > 32 (the edge-chunk loop), receiver counts
-    that are not a multiple of a stage (32 // d3 receivers).  Bound: f32 S (edge sums) times the
-    three-plane products, 4e-6 of sum |S| |G|."""
-    from gmp_amd import _lib
-    tops = _lib.torch_ops()
-    g = torch.Generator().manual_seed(seed)
-    degs = torch.randint(0, 30, (nrecv,), generator=g)
-    degs[0], degs[1] = 0, 45
-    if nrecv > 5:
-        degs[5] = 1
-    w = d3 * mul1
-    eoff, Z, A, ne = _setup(degs.tolist(), w, H, seed=seed)
-    G = torch.randn(nrecv * d3, mo, generator=g)
-    dW = tops.tp_node_dw(eoff.to(DEV), Z.to(DEV), A.to(DEV), G.to(DEV), d3, mul1).cpu().double()
-    S = torch.zeros(nrecv, w, H, dtype=torch.float64)
-    Sa = torch.zeros(nrecv, w, H, dtype=torch.float64)
-    for n in range(nrecv):
-        e0, e1 = int(eoff[n]), int(eoff[n + 1])
-        S[n] = Z[e0:e1].double().t() @ A[e0:e1].double()
-        Sa[n] = Z[e0:e1].double().abs().t() @ A[e0:e1].double().abs()
-    # rows (n, k) x columns (u, j)
-    Sk = S.view(nrecv, d3, mul1, H).reshape(nrecv * d3, mul1 * H)
-    Sak = Sa.view(nrecv, d3, mul1, H).reshape(nrecv * d3, mul1 * H)
-    ref = Sk.t() @ G.double()
-    bound = Sak.t() @ G.double().abs()
-    assert dW.shape == (mul1 * H, mo)
-    err = (dW - ref).abs()
-    assert bool((err <= 4e-6 * bound + 1e-6).all()), (err / bound.clamp_min(1e-30)).max().item()
-    # deterministic
-    dW2 = tops.tp_node_dw(eoff.to(DEV), Z.to(DEV), A.to(DEV), G.to(DEV), d3, mul1).cpu().double()
-    assert torch.equal(dW, dW2)
-
-
-@pytest.mark.parametrize("d3,mul1,H,mo,nrecv,seed", [
-    (5, 64, 64, 128, 50, 1), (3, 32, 96, 128, 45, 2), (7, 32, 64, 64, 23, 3),
-    (5, 128, 256, 128, 30, 4), (3, 64, 32, 64, 100, 5), (5, 32, 32, 64, 13, 6)])
-def test_node_fwd_fused_matches_fp64(d3, mul1, H, mo, nrecv, seed):
-    """K7s (gmp_tp_node_fwd_fused_f32 via torch.ops.gmp.tp_node_fwd_fused): the forward path
-    contraction out[n, w d3 + k] += sum_{u,j} S[(n, k), (u, j)] W2p[(u, j), w] + sum_u Sb[(n, k), u]
-    b2p[u, w] with S / Sb built in-kernel from z and a, accumulated into a strided output block
-    (row stride cldg > mul_out d3, a column offset), against the fp64 evaluation; receivers of
-    in-degree 0, 1 and > 24 (past the prefetched operands), a last tile with fewer receivers.
-    Bound: f32 edge sums times the three-plane products, 4e-6 of sum |terms|."""
-    from gmp_amd import _lib
-    tops = _lib.torch_ops()
-    g = torch.Generator().manual_seed(seed)
-    degs = torch.randint(0, 30, (nrecv,), generator=g)
-    degs[0], degs[1] = 0, 45
-    if nrecv > 5:
-        degs[5] = 1
-    w = d3 * mul1
-    eoff, Z, A, ne = _setup(degs.tolist(), w, H, seed=seed)
-    off = 16 * mo  # the path's block of W2 rows (u, w) starts past other paths' rows
-    W2 = torch.randn(off + mul1 * mo + 8, H, generator=g) / H ** 0.5
-    b2 = torch.randn(off + mul1 * mo + 8, generator=g)
-    Bf = tops.tp_split_w2(W2.to(DEV), b2.to(DEV), off, mul1, mo, True)
-    cldg, c0 = mo * d3 + 11, 7
-    C0 = torch.randn(nrecv * cldg + c0 + 5, generator=g)
-    C = C0.to(DEV)
-    Zf = tops.tp_z_fused_layout(Z.to(DEV), d3, mul1)
-    tops.tp_node_fwd_fused(eoff.to(DEV), Zf, A.to(DEV), Bf, d3, mul1, mo, C, c0, cldg)
-    got = C.cpu().double()
-    W2p = W2[off:off + mul1 * mo].double().view(mul1, mo, H)   # [u, w, j]
-    b2p = b2[off:off + mul1 * mo].double().view(mul1, mo)      # [u, w]
-    ref = C0.double().clone()
-    bnd = torch.zeros_like(ref)
-    for n in range(nrecv):
-        e0, e1 = int(eoff[n]), int(eoff[n + 1])
-        z = Z[e0:e1].double().view(-1, d3, mul1)               # [e, k, u]
-        a = A[e0:e1].double()                                  # [e, j]
-        S = torch.einsum("eku,ej->kuj", z, a)
-        Sa = torch.einsum("eku,ej->kuj", z.abs(), a.abs())
-        Sb, Sba = z.sum(0), z.abs().sum(0)                     # [k, u]
-        o = torch.einsum("kuj,uwj->wk", S, W2p) + (Sb @ b2p).t()     # [w, k]
-        ob = torch.einsum("kuj,uwj->wk", Sa, W2p.abs()) + (Sba @ b2p.abs()).t()
-        base = c0 + n * cldg
-        ref[base:base + mo * d3] += o.reshape(-1)
-        bnd[base:base + mo * d3] += ob.reshape(-1)
-    err = (got - ref).abs()
-    assert bool((err <= 4e-6 * bnd + 1e-6).all()), (err / bnd.clamp_min(1e-30)).max().item()
-    # deterministic, and nothing outside the output block was touched
-    C2 = C0.to(DEV)
-    tops.tp_node_fwd_fused(eoff.to(DEV), Zf, A.to(DEV), Bf, d3, mul1, mo, C2, c0, cldg)
-    # the layout itself
-    U = 16 // d3
-    zf = Zf.cpu()
-    for us, e, c in ((0, 0, 0), (1, 3, 16 - 1), (Zf.shape[0] - 1, ne, d3 * U - 1), (2, 7, 5)):
-        k, u = c // U, us * U + c % U
-        want = Z[e, k * mul1 + u] if (k < d3 and u < mul1 and c < d3 * U) else 0.0
-        assert float(zf[us, e, c]) == float(want), (us, e, c)
-    assert torch.equal(C2.cpu().double(), got)
