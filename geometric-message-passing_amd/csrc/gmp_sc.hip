@@ -1,336 +1,223 @@
-// K8: MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188,
-// element_dependent=False) for node features x (B, C, D) = C channels of 0e+1o(+2e(+3o)) --
-// D = (L+1)^2 for max_ell L = 1, 2, 3 (reshape_irreps, irreps_tools.py:63-79) -- all L+1 output
-// irreps (M = D rows) at once.
+// K8: MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:20-188,
+// element_dependent=False) for node features x (B, C, D) = C channels of ANY irreps list
+// (reshape_irreps, irreps_tools.py:63-79: 0e+1o+2e, both parities, repeated l, max_ell up to 5 or
+// more; D <= 63 components per channel) and any output irreps list of C channels each (M <= 255
+// rows), correlation 1..4.
 //
-// With the per-channel coefficient tensors A_nu[c] = sum_k U_nu[..., k] W_nu[k, c] (prepared by
-// the host), the reference's nested contraction (((A4 x + A3) x + A2) x + A1) x is the polynomial
-//   out[b, c, m] = sum_{nu <= corr} sum_{i1..inu} A_nu[c, m, i1..inu] x_i1 ... x_inu
-// (x = x[b, c, :]) written directly in the mul_ir output layout [0e: c | 1o: C + 3c + m' |
-// 2e: 4C + 5c + m'' | 3o: 9C + 7c + m'''], evaluated over the symmetric monomial basis below
-// (the caller passes the folded coefficients).  One thread per (node, channel), grid-stride over
-// nodes, with the channel's coefficients (NQ x D floats, monomial-major) in LDS.  Backward: dx by
-// the product rule (same loop), dA~ = sum_b g[b,c,m] (monomial of x[b,c]) reduced over node groups
-// into per-group partials (summed in fixed order by the caller).
+// With the per-channel coefficient tensors A_nu[c] = sum_k U_nu[..., k] W_nu[k, c] (built by the
+// host, differentiably), the reference's nested contraction (((A4 x + A3) x + A2) x + A1) x is the
+// polynomial
+//   out[b, c, m] = sum_{nu <= corr} sum_{i1..inu} A_nu[c, m, i1..inu] x_i1 ... x_inu,
+// x = x[b, c, :].  The monomials are symmetric in their indices, so the host folds every
+// permutation's coefficient into the sorted index tuple, and the couplings that reach row m are
+// sparse: real Clebsch-Gordan selection rules (parity, |l1 - l2| <= l <= l1 + l2, the m-selection
+// of the real basis) and the antisymmetric couplings that vanish on symmetric monomials leave ~10 %
+// of the (row, monomial) pairs non-zero (C4's 0e+1o+2e at correlation 3: 247 of 1,971;
+// 0e+1o+2e+3o at correlation 4: 8,652 of 77,504).  The host keeps that pattern -- the TERM LIST,
+// identical for every channel because the weights are dense -- and the kernels walk it:
+//   term t = (row m_t, factors f0..f3 of its monomial; a factor index D addresses a constant 1.0
+//   slot, so degree < 4 monomials need no branch), coefficient coef[c, t].
+// Plan (int32, built once per module): [row_ptr (M + 1) | out_base (M) | out_stride (M) |
+// terms (T)], terms of row m at row_ptr[m] .. row_ptr[m+1] - 1, sorted by monomial; term word =
+// f0 | f1 << 6 | f2 << 12 | f3 << 18 | m << 24.  Output column of (row m, channel c):
+// out_base[m] + out_stride[m] c (the mul_ir layout of the output irreps: block offset + (2l+1) c +
+// component).
+//
+// Mapping: a workgroup owns a tile of CT channels (lane = channel fastest, 256 / CT nodes per
+// pass, grid-stride over nodes); the coefficients are term-major (coef (T, C): a tile reads CT
+// consecutive floats per term, from L1 / L2), term words are wave-uniform (scalar loads), each
+// thread's x row (and dx row) sits in a private LDS row with an odd stride.  Lanes of one node
+// read / write its CT channels' x, g and out entries -- runs of CT * (2l+1) floats per output
+// block instead of one scattered float per lane.  dcoef[t, c] = sum_b g[b, c, m_t] mono_t(x[b, c])
+// runs over (term, channel) pairs of a channel tile with the node group's x / g rows staged
+// through LDS, reduced over node groups into per-group partials (summed in fixed order by the
+// caller).  Deterministic: fixed orders throughout, no atomics.
 #include "gmp_common.h"
 
 namespace gmp {
 namespace {
 
-// Symmetric monomial basis: x_i x_j x_k is symmetric in its indices, so the host folds every
-// permutation's coefficient into the sorted one (A~_nu[c, m, q] = sum over the distinct
-// permutations of q of A_nu[c, m, .]; exact algebra, fp32 re-association only) and the
-// contraction runs over C(D + nu - 1, nu) monomials of degree nu instead of D^nu (D = 9, nu = 3:
-// 165 instead of 729).  Order: deg1 i | deg2 i <= j | deg3 i <= j <= k | deg4 i <= j <= k <= l,
-// lexicographic within a degree.
-__host__ __device__ constexpr int nq_deg(int D, int deg) {
-  return deg == 1 ? D
-       : deg == 2 ? D * (D + 1) / 2
-       : deg == 3 ? D * (D + 1) * (D + 2) / 6
-                  : D * (D + 1) * (D + 2) * (D + 3) / 24;
-}
-__host__ __device__ constexpr int nq_total(int D, int corr) {
-  return (corr >= 1 ? nq_deg(D, 1) : 0) + (corr >= 2 ? nq_deg(D, 2) : 0) +
-         (corr >= 3 ? nq_deg(D, 3) : 0) + (corr >= 4 ? nq_deg(D, 4) : 0);
-}
 constexpr int kSC = 256;
-constexpr int kNodeBlocks = 16;  // node blocks per channel (grid-stride: coefficients load once)
+constexpr int kMaxDim = 63;     // factor fields are 6 bits; index D is the 1.0 slot
+constexpr int kMaxRows = 255;   // row field is 8 bits
+constexpr int kMaxCT = 16;      // channels per workgroup tile of the forward / dx kernels
+constexpr int kQPT = 16;        // dcoef kernel: (term, channel) pairs per thread
+constexpr int kPairs = kSC * kQPT;
+constexpr int kStageLds = 16384; // floats of staged node rows in the dcoef kernel
 
-// compiled (D, corr): D in {4, 9, 16}; corr <= 4 for D <= 9, <= 3 for D = 16 (the D = 16, nu = 4
-// table, 4844 x 16 floats, exceeds LDS)
-__host__ __device__ constexpr bool sc_supported(int D, int corr) {
-  return corr >= 1 && ((D == 4 || D == 9) ? corr <= 4 : (D == 16 ? corr <= 3 : false));
+struct Plan {
+  const int* row_ptr;
+  const int* out_base;
+  const int* out_stride;
+  const unsigned* terms;
+};
+__device__ __forceinline__ Plan plan_of(const int* p, int M) {
+  return Plan{p, p + M + 1, p + 2 * M + 1, reinterpret_cast<const unsigned*>(p + 3 * M + 1)};
 }
 
-// LDS coefficient layout: a[q * D + m] (monomial-major: one q's D rows are contiguous and every
-// lane of the block reads the same address -> broadcast reads)
-template <int D, int CORR>
-__device__ __forceinline__ void load_coeffs(int c, const float* __restrict__ A1,
-                                            const float* __restrict__ A2,
-                                            const float* __restrict__ A3,
-                                            const float* __restrict__ A4, float* a) {
-  const float* As[4] = {A1, A2, A3, A4};
-  int q0 = 0;
-#pragma unroll
-  for (int nu = 1; nu <= CORR; ++nu) {
-    const int nqd = nq_deg(D, nu);
-    const float* An = As[nu - 1];
-    for (int e = threadIdx.x; e < D * nqd; e += blockDim.x) {
-      const int m = e / nqd, q = e - m * nqd;
-      a[(q0 + q) * D + m] = An[((int64_t)c * D + m) * nqd + q];
-    }
-    q0 += nqd;
-  }
+__host__ __device__ constexpr int row_stride(int D) { return (D + 1) | 1; }
+
+__device__ __forceinline__ float mono(const float* xt, unsigned f) {
+  return (xt[f & 63u] * xt[(f >> 6) & 63u]) * (xt[(f >> 12) & 63u] * xt[(f >> 18) & 63u]);
 }
 
-// output column of row m (irrep block l = floor(sqrt(m)), component m - l^2) of channel c
-__device__ __forceinline__ int out_col(int C, int c, int m) {
-  const int l = m >= 9 ? 3 : (m >= 4 ? 2 : (m >= 1 ? 1 : 0));
-  return l * l * C + (2 * l + 1) * c + (m - l * l);
+__device__ __forceinline__ void load_row(float* xt, const float* __restrict__ xr, int D) {
+  for (int i = 0; i < D; ++i) xt[i] = xr[i];
+  xt[D] = 1.f;
 }
 
-// The monomial walk: rolled loops over the basis in order, this thread's x (and dx) in a private
-// LDS row.  (r04: a fully unrolled walk with x and dx in registers measured slower at the C4
-// shape -- 1.75 / 3.80 ms against 1.05 / 3.03 ms forward / backward at 50k nodes x 128
-// channels, scripts/mb_sc.py: 256 VGPRs and 404 B of scratch per lane in its backward -- and
-// compiled for minutes at D = 16.)
-template <int D, int CORR, class F>
-__device__ __forceinline__ void for_monomials(const float* xv, F&& f) {
-  int q = 0;
-#pragma unroll 1
-  for (int i = 0; i < D; ++i) f(q++, xv[i], i, 0, 0, 0, 1);
-  if constexpr (CORR >= 2) {
-#pragma unroll 1
-    for (int i = 0; i < D; ++i)
-#pragma unroll 1
-      for (int j = i; j < D; ++j) f(q++, xv[i] * xv[j], i, j, 0, 0, 2);
-  }
-  if constexpr (CORR >= 3) {
-#pragma unroll 1
-    for (int i = 0; i < D; ++i)
-#pragma unroll 1
-      for (int j = i; j < D; ++j) {
-        const float xij = xv[i] * xv[j];
-#pragma unroll 1
-        for (int k = j; k < D; ++k) f(q++, xij * xv[k], i, j, k, 0, 3);
-      }
-  }
-  if constexpr (CORR >= 4) {
-#pragma unroll 1
-    for (int i = 0; i < D; ++i)
-#pragma unroll 1
-      for (int j = i; j < D; ++j) {
-        const float xij = xv[i] * xv[j];
-#pragma unroll 1
-        for (int k = j; k < D; ++k) {
-          const float xijk = xij * xv[k];
-#pragma unroll 1
-          for (int l = k; l < D; ++l) f(q++, xijk * xv[l], i, j, k, l, 4);
-        }
-      }
-  }
-}
-
-template <int D, int CORR>
-__global__ __launch_bounds__(kSC) void sc_fwd_kernel(int64_t B, int C,
+__global__ __launch_bounds__(kSC) void sc_fwd_kernel(int64_t B, int C, int D, int M, int T, int CT,
+                                                        const int* __restrict__ plan,
+                                                        const float* __restrict__ coef,
                                                         const float* __restrict__ x,
-                                                        const float* __restrict__ A1,
-                                                        const float* __restrict__ A2,
-                                                        const float* __restrict__ A3,
-                                                        const float* __restrict__ A4,
                                                         float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float a[];
-  float* xt = a + nq_total(D, CORR) * D + threadIdx.x * (D + 1);  // this thread's x row
-  const int c = blockIdx.y;
-  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
-  __syncthreads();
-  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
-    const float* xr = x + (b * C + c) * D;
-    for (int i = 0; i < D; ++i) xt[i] = xr[i];
-    float acc[D];
-#pragma unroll
-    for (int m = 0; m < D; ++m) acc[m] = 0.f;
-    for_monomials<D, CORR>(xt, [&](int q, float z, int, int, int, int, int) {
-      const float* ar = a + q * D;
-#pragma unroll
-      for (int m = 0; m < D; ++m) acc[m] += ar[m] * z;
-    });
-    float* orow = out + b * (int64_t)(D * C);
-#pragma unroll
-    for (int m = 0; m < D; ++m) orow[out_col(C, c, m)] = acc[m];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xt = sm + threadIdx.x * row_stride(D);
+  const int cl = threadIdx.x % CT, npb = kSC / CT, c = blockIdx.y * CT + cl;
+  if (threadIdx.x >= npb * CT || c >= C) return;  // (no barrier in this kernel)
+  const Plan P = plan_of(plan, M);
+  const float* cf = coef + c;  // coef[t, c] at cf[t C]: CT consecutive floats per term
+  for (int64_t b = (int64_t)blockIdx.x * npb + threadIdx.x / CT; b < B;
+       b += (int64_t)gridDim.x * npb) {
+    load_row(xt, x + (b * C + c) * D, D);
+    float* orow = out + b * (int64_t)M * C;
+    int t = P.row_ptr[0];
+    for (int m = 0; m < M; ++m) {
+      const int t1 = P.row_ptr[m + 1];
+      float acc = 0.f;
+      for (; t < t1; ++t) acc = fmaf(cf[(int64_t)t * C], mono(xt, P.terms[t]), acc);
+      orow[P.out_base[m] + P.out_stride[m] * c] = acc;
+    }
   }
 }
 
-template <int D, int CORR>
-__global__ __launch_bounds__(kSC) void sc_bwd_x_kernel(int64_t B, int C,
+__global__ __launch_bounds__(kSC) void sc_bwd_x_kernel(int64_t B, int C, int D, int M, int T,
+                                                          int CT, const int* __restrict__ plan,
+                                                          const float* __restrict__ coef,
                                                           const float* __restrict__ x,
-                                                          const float* __restrict__ A1,
-                                                          const float* __restrict__ A2,
-                                                          const float* __restrict__ A3,
-                                                          const float* __restrict__ A4,
                                                           const float* __restrict__ gout,
                                                           float* __restrict__ dx) {
-  extern __shared__ __attribute__((aligned(16))) float a[];
-  float* xt = a + nq_total(D, CORR) * D + threadIdx.x * (2 * D + 1);  // x row | dx row
-  float* dt = xt + D;
-  const int c = blockIdx.y;
-  load_coeffs<D, CORR>(c, A1, A2, A3, A4, a);
-  __syncthreads();
-  for (int64_t b = (int64_t)blockIdx.x * kSC + threadIdx.x; b < B; b += (int64_t)gridDim.x * kSC) {
-    float g[D];
-    const float* xr = x + (b * C + c) * D;
-    const float* gr = gout + b * (int64_t)(D * C);
-    for (int i = 0; i < D; ++i) {
-      xt[i] = xr[i];
-      dt[i] = 0.f;
-    }
-#pragma unroll
-    for (int m = 0; m < D; ++m) g[m] = gr[out_col(C, c, m)];
-    for_monomials<D, CORR>(xt, [&](int q, float, int i, int j, int k, int l, int deg) {
-      const float* ar = a + q * D;
-      float gA = 0.f;
-#pragma unroll
-      for (int m = 0; m < D; ++m) gA += ar[m] * g[m];
-      if (deg == 1) {
-        dt[i] += gA;
-      } else if (deg == 2) {
-        dt[i] += gA * xt[j];
-        dt[j] += gA * xt[i];
-      } else if (deg == 3) {
-        dt[i] += gA * (xt[j] * xt[k]);
-        dt[j] += gA * (xt[i] * xt[k]);
-        dt[k] += gA * (xt[i] * xt[j]);
-      } else {
-        const float xij = xt[i] * xt[j], xkl = xt[k] * xt[l];
-        dt[i] += gA * (xt[j] * xkl);
-        dt[j] += gA * (xt[i] * xkl);
-        dt[k] += gA * (xij * xt[l]);
-        dt[l] += gA * (xij * xt[k]);
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int RS = row_stride(D);
+  float* xt = sm + threadIdx.x * RS;
+  float* dt = sm + kSC * RS + threadIdx.x * RS;
+  const int cl = threadIdx.x % CT, npb = kSC / CT, c = blockIdx.y * CT + cl;
+  if (threadIdx.x >= npb * CT || c >= C) return;  // (no barrier in this kernel)
+  const Plan P = plan_of(plan, M);
+  const float* cf = coef + c;
+  for (int64_t b = (int64_t)blockIdx.x * npb + threadIdx.x / CT; b < B;
+       b += (int64_t)gridDim.x * npb) {
+    load_row(xt, x + (b * C + c) * D, D);
+    for (int i = 0; i <= D; ++i) dt[i] = 0.f;
+    const float* grow = gout + b * (int64_t)M * C;
+    int t = P.row_ptr[0];
+    for (int m = 0; m < M; ++m) {
+      const int t1 = P.row_ptr[m + 1];
+      const float gm = grow[P.out_base[m] + P.out_stride[m] * c];
+      for (; t < t1; ++t) {
+        // d/dx of x_f0 x_f1 x_f2 x_f3: one product-rule term per factor (a repeated factor gets
+        // each of its terms; the 1.0 slot D collects the padding factors' terms, unused)
+        const unsigned f = P.terms[t];
+        const unsigned i0 = f & 63u, i1 = (f >> 6) & 63u, i2 = (f >> 12) & 63u, i3 = (f >> 18) & 63u;
+        const float a = xt[i0], bb = xt[i1], cc = xt[i2], d = xt[i3];
+        const float w = gm * cf[(int64_t)t * C], ab = a * bb, cd = cc * d;
+        dt[i0] = fmaf(w, bb * cd, dt[i0]);
+        dt[i1] = fmaf(w, a * cd, dt[i1]);
+        dt[i2] = fmaf(w, ab * d, dt[i2]);
+        dt[i3] = fmaf(w, ab * cc, dt[i3]);
       }
-    });
+    }
     float* dr = dx + (b * C + c) * D;
     for (int i = 0; i < D; ++i) dr[i] = dt[i];
   }
 }
 
-// factor indices of monomial q of degree deg (q counted within its degree, lexicographic)
-__device__ __forceinline__ void decode_monomial(int D, int deg, int r, int (&f)[4]) {
-  int lo = 0;
-  for (int t = 0; t < deg; ++t) {
-    // number of sorted (deg - t - 1)-tuples over [v, D) for each candidate first index v
-    const int rest = deg - t - 1;
-    int v = lo;
-    while (true) {
-      const int n = D - v;  // values available from v on
-      int cnt = 1;          // C(n - 1 + rest, rest): sorted tuples starting with v
-      for (int s = 1; s <= rest; ++s) cnt = cnt * (n - 1 + s) / s;
-      if (r < cnt) break;
-      r -= cnt;
-      ++v;
-    }
-    f[t] = v;
-    lo = v;
-  }
-}
-
-// dA~ partials: part[grp, c, m, q] = sum_{b in group grp} g[b, c, m] * mono_q(x[b, c]).
-// Thread t owns monomials t, t + kSC, ... (QPT of them) and all D rows m; nodes staged through
-// LDS in batches, their x and g rows read as broadcasts.
-constexpr int kNodeBatch = 32;
-
-template <int D, int CORR>
-__global__ __launch_bounds__(kSC) void sc_bwd_a_kernel(int64_t B, int C, int64_t nodes_per_group,
-                                                       const float* __restrict__ x,
-                                                       const float* __restrict__ gout,
-                                                       float* __restrict__ part) {
-  constexpr int NQ = nq_total(D, CORR);
-  constexpr int QPT = (NQ + kSC - 1) / kSC;
-  __shared__ float xs[kNodeBatch][D];
-  __shared__ float gs[kNodeBatch][D];
-  const int c = blockIdx.y;
+// dcoef partials: part[grp, t, c] = sum_{b in group grp} g[b, c, m_t] mono_t(x[b, c]).  A
+// workgroup owns a node group (blockIdx.x), a channel tile of CT channels (blockIdx.y) and a
+// range of <= kPairs / CT terms (blockIdx.z); thread pair p = tid + 256 u is (term t0 + p / CT,
+// channel p % CT).  The group's nodes are staged through LDS NB at a time: x rows (+ the 1.0
+// slot) and g rows of the tile's channels.
+__global__ __launch_bounds__(kSC) void sc_bwd_coef_kernel(int64_t B, int C, int D, int M, int T,
+                                                             int CT, int NB,
+                                                             int64_t nodes_per_group,
+                                                             const int* __restrict__ plan,
+                                                             const float* __restrict__ x,
+                                                             const float* __restrict__ gout,
+                                                             float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xsb = sm;                          // [NB][CT][D + 1]
+  float* gsb = sm + NB * CT * (D + 1);      // [NB][CT][M]
+  const int c0 = blockIdx.y * CT;
   const int64_t grp = blockIdx.x;
+  const int tpb = kPairs / CT;              // terms per workgroup
+  const int t0 = blockIdx.z * tpb;
+  const int nt = min(tpb, T - t0);
+  const Plan P = plan_of(plan, M);
   const int64_t b0 = grp * nodes_per_group;
   const int64_t b1 = (b0 + nodes_per_group < B) ? b0 + nodes_per_group : B;
-  int fac[QPT][4], deg[QPT];
+  const int rounds = (nt * CT + kSC - 1) / kSC;  // uniform, <= kQPT
+  unsigned f[kQPT];
+  int xo[kQPT], go[kQPT];
+  float acc[kQPT];
 #pragma unroll
-  for (int u = 0; u < QPT; ++u) {
-    const int q = threadIdx.x + u * kSC;
-    fac[u][0] = fac[u][1] = fac[u][2] = fac[u][3] = 0;
-    deg[u] = 0;
-    int r = q;
-    for (int dg = 1; dg <= CORR && q < NQ; ++dg) {
-      if (r < nq_deg(D, dg)) {
-        deg[u] = dg;
-        decode_monomial(D, dg, r, fac[u]);
-        break;
-      }
-      r -= nq_deg(D, dg);
-    }
+  for (int u = 0; u < kQPT; ++u) {
+    const int p = threadIdx.x + u * kSC, tl = p / CT, j = p - tl * CT;
+    const bool ok = u < rounds && tl < nt && c0 + j < C;
+    f[u] = ok ? P.terms[t0 + tl] : 0xffffffffu;
+    xo[u] = j * (D + 1);
+    go[u] = ok ? j * M + (int)(f[u] >> 24) : 0;
+    acc[u] = 0.f;
   }
-  float acc[QPT][D];
-#pragma unroll
-  for (int u = 0; u < QPT; ++u)
-#pragma unroll
-    for (int m = 0; m < D; ++m) acc[u][m] = 0.f;
-  for (int64_t bb = b0; bb < b1; bb += kNodeBatch) {
-    const int nb = (int)((b1 - bb) < kNodeBatch ? (b1 - bb) : kNodeBatch);
+  for (int64_t bb = b0; bb < b1; bb += NB) {
+    const int nb = (int)((b1 - bb) < NB ? (b1 - bb) : NB);
     __syncthreads();
-    for (int e = threadIdx.x; e < kNodeBatch * D; e += kSC) {
-      const int n = e / D, t = e - n * D;
-      xs[n][t] = (n < nb) ? x[((bb + n) * C + c) * D + t] : 0.f;
-      gs[n][t] = (n < nb) ? gout[(bb + n) * (int64_t)(D * C) + out_col(C, c, t)] : 0.f;
+    for (int e = threadIdx.x; e < NB * CT * (D + 1); e += kSC) {
+      const int i = e % (D + 1), r = e / (D + 1), j = r % CT, n = r / CT;
+      xsb[e] = (n < nb && i < D && c0 + j < C) ? x[((bb + n) * C + c0 + j) * D + i] : 1.f;
+    }
+    for (int e = threadIdx.x; e < NB * CT * M; e += kSC) {
+      const int j = e % CT, r = e / CT, m = r % M, n = r / M;
+      gsb[(n * CT + j) * M + m] =
+          (n < nb && c0 + j < C)
+              ? gout[(bb + n) * (int64_t)M * C + P.out_base[m] + P.out_stride[m] * (c0 + j)]
+              : 0.f;
     }
     __syncthreads();
     for (int n = 0; n < nb; ++n) {
+      const float* xr = xsb + n * CT * (D + 1);
+      const float* gr = gsb + n * CT * M;
 #pragma unroll
-      for (int u = 0; u < QPT; ++u) {
-        if (deg[u] == 0) continue;
-        float z = xs[n][fac[u][0]];
-        if (deg[u] >= 2) z *= xs[n][fac[u][1]];
-        if (deg[u] >= 3) z *= xs[n][fac[u][2]];
-        if (deg[u] >= 4) z *= xs[n][fac[u][3]];
-#pragma unroll
-        for (int m = 0; m < D; ++m) acc[u][m] += gs[n][m] * z;
+      for (int u = 0; u < kQPT; ++u) {
+        if (u < rounds && f[u] != 0xffffffffu)
+          acc[u] = fmaf(gr[go[u]], mono(xr + xo[u], f[u]), acc[u]);
       }
     }
   }
-  float* pr = part + (grp * C + c) * (int64_t)(D * NQ);
 #pragma unroll
-  for (int u = 0; u < QPT; ++u) {
-    const int q = threadIdx.x + u * kSC;
-    if (q >= NQ) continue;
-#pragma unroll
-    for (int m = 0; m < D; ++m) pr[m * NQ + q] = acc[u][m];
+  for (int u = 0; u < kQPT; ++u) {
+    const int p = threadIdx.x + u * kSC, tl = p / CT, j = p - tl * CT;
+    if (u < rounds && tl < nt && c0 + j < C) part[(grp * T + t0 + tl) * C + c0 + j] = acc[u];
   }
 }
 
-template <int D, int CORR>
-int sc_launch(int64_t n_nodes, int channels, const float* x, const float* A1, const float* A2,
-              const float* A3, const float* A4, float* out, const float* gout, float* dx,
-              float* dA_partials, hipStream_t s) {
-  constexpr int NQ = nq_total(D, CORR);
-  const int smem_f = (NQ * D + kSC * (D + 1)) * 4;
-  const int smem_b = (NQ * D + kSC * (2 * D + 1)) * 4;
-  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(n_nodes, kSC), kNodeBlocks),
-                  (unsigned)channels);
-  int rc;
-  auto fwd_k = sc_fwd_kernel<D, CORR>;
-  auto bwd_k = sc_bwd_x_kernel<D, CORR>;
-  if (out) {
-    if ((rc = hip_check(hipFuncSetAttribute((const void*)fwd_k,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem_f))))
-      return rc;
-    fwd_k<<<grid, kSC, smem_f, s>>>(n_nodes, channels, x, A1, A2, A3, A4, out);
-    if ((rc = launch_status())) return rc;
-  }
-  if (dx) {
-    if ((rc = hip_check(hipFuncSetAttribute((const void*)bwd_k,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem_b))))
-      return rc;
-    bwd_k<<<grid, kSC, smem_b, s>>>(n_nodes, channels, x, A1, A2, A3, A4, gout, dx);
-    if ((rc = launch_status())) return rc;
-  }
-  if (dA_partials) {
-    const int G = gmp_sc_groups(n_nodes);
-    const int64_t per = ceil_div(n_nodes, (int64_t)G);
-    sc_bwd_a_kernel<D, CORR><<<dim3((unsigned)G, (unsigned)channels), kSC, 0, s>>>(
-        n_nodes, channels, per, x, gout, dA_partials);
-    if ((rc = launch_status())) return rc;
-  }
-  return GMP_OK;
+unsigned node_blocks(int64_t B, int C, int CT) {
+  // enough workgroups for the chip (~8 per CU over the channel tiles), each sweeping nodes
+  const int64_t tiles = ceil_div((int64_t)C, (int64_t)CT);
+  int64_t want = ceil_div((int64_t)8 * device_cu_count(), tiles);
+  if (want < 1) want = 1;
+  const int64_t most = ceil_div(B, (int64_t)(kSC / CT));
+  return (unsigned)(want < most ? want : most);
 }
 
-int sc_dispatch(int64_t n_nodes, int channels, int dim, int corr, const float* x,
-                const float* A1, const float* A2, const float* A3, const float* A4, float* out,
-                const float* gout, float* dx, float* dA_partials, hipStream_t s) {
-#define LAUNCH_SC(DD, CR)                                                                     \
-  if (dim == DD && corr == CR)                                                             \
-    return sc_launch<DD, CR>(n_nodes, channels, x, A1, A2, A3, A4, out, gout, dx, dA_partials, s);
-  LAUNCH_SC(9, 1) LAUNCH_SC(9, 2) LAUNCH_SC(9, 3) LAUNCH_SC(9, 4)
-  LAUNCH_SC(4, 1) LAUNCH_SC(4, 2) LAUNCH_SC(4, 3) LAUNCH_SC(4, 4)
-  LAUNCH_SC(16, 1) LAUNCH_SC(16, 2) LAUNCH_SC(16, 3)
-#undef LAUNCH_SC
-  return GMP_ERR_UNSUPPORTED;
+template <class K>
+int allow_smem(K k, size_t bytes) {
+  return hip_check(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)bytes));
+}
+
+bool shape_ok(int channels, int dim, int rows, int n_terms) {
+  return channels > 0 && channels <= 65535 && dim >= 1 && dim <= kMaxDim && rows >= 1 &&
+         rows <= kMaxRows && n_terms >= 0;
 }
 
 }  // namespace
@@ -341,40 +228,66 @@ using namespace gmp;
 extern "C" {
 
 int gmp_sc_groups(int64_t n_nodes) {
-  // node groups of the dA reduction: enough workgroups (x C channels) to fill the device
-  int64_t g = ceil_div(n_nodes, 512);
-  if (g > 64) g = 64;
+  // node groups of the dcoef reduction: ~256 nodes each, at most 128
+  int64_t g = ceil_div(n_nodes, 256);
+  if (g > 128) g = 128;
   return (int)(g < 1 ? 1 : g);
 }
 
-int gmp_sc_monomials(int dim, int correlation) {
-  return sc_supported(dim, correlation) ? nq_total(dim, correlation) : -1;
+int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int dim, int rows,
+                                      int n_terms, const int32_t* plan, const float* coef,
+                                      const float* x, float* out, void* stream) {
+  GMP_CHECK_ARG(n_nodes >= 0 && shape_ok(channels, dim, rows, n_terms));
+  GMP_CHECK_ARG(plan && x && out && (n_terms == 0 || coef));
+  if (n_nodes == 0) return GMP_OK;
+  const int CT = channels < kMaxCT ? channels : kMaxCT;
+  const size_t smem = (size_t)kSC * row_stride(dim) * sizeof(float);
+  int rc;
+  if ((rc = allow_smem(sc_fwd_kernel, smem))) return rc;
+  sc_fwd_kernel<<<dim3(node_blocks(n_nodes, channels, CT), (unsigned)ceil_div(channels, CT)), kSC,
+                  smem, as_stream(stream)>>>(n_nodes, channels, dim, rows, n_terms, CT, plan, coef,
+                                             x, out);
+  return launch_status();
 }
 
-int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
-                                      const float* x, const float* A1, const float* A2,
-                                      const float* A3, const float* A4, float* out,
-                                      void* stream) {
-  GMP_CHECK_ARG(n_nodes >= 0 && channels > 0 && channels <= 65535);
-  if (!sc_supported(dim, correlation)) return GMP_ERR_UNSUPPORTED;
-  GMP_CHECK_ARG(x && A1 && out && (correlation < 2 || A2) && (correlation < 3 || A3) &&
-                (correlation < 4 || A4));
+int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int dim, int rows,
+                                      int n_terms, const int32_t* plan, const float* coef,
+                                      const float* x, const float* gout, float* dx,
+                                      float* dcoef_partials, void* stream) {
+  GMP_CHECK_ARG(n_nodes >= 0 && shape_ok(channels, dim, rows, n_terms));
+  GMP_CHECK_ARG(plan && x && gout && (n_terms == 0 || coef || !dx));
   if (n_nodes == 0) return GMP_OK;
-  return sc_dispatch(n_nodes, channels, dim, correlation, x, A1, A2, A3, A4, out, nullptr,
-                     nullptr, nullptr, as_stream(stream));
-}
-
-int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
-                                      const float* x, const float* A1, const float* A2,
-                                      const float* A3, const float* A4, const float* gout,
-                                      float* dx, float* dA_partials, void* stream) {
-  GMP_CHECK_ARG(n_nodes >= 0 && channels > 0 && channels <= 65535);
-  if (!sc_supported(dim, correlation)) return GMP_ERR_UNSUPPORTED;
-  GMP_CHECK_ARG(x && A1 && gout && (correlation < 2 || A2) && (correlation < 3 || A3) &&
-                (correlation < 4 || A4));
-  if (n_nodes == 0) return GMP_OK;
-  return sc_dispatch(n_nodes, channels, dim, correlation, x, A1, A2, A3, A4, nullptr, gout, dx,
-                     dA_partials, as_stream(stream));
+  hipStream_t s = as_stream(stream);
+  int rc;
+  if (dx) {
+    const int CT = channels < kMaxCT ? channels : kMaxCT;
+    const size_t smem = (size_t)2 * kSC * row_stride(dim) * sizeof(float);
+    if ((rc = allow_smem(sc_bwd_x_kernel, smem))) return rc;
+    sc_bwd_x_kernel<<<dim3(node_blocks(n_nodes, channels, CT), (unsigned)ceil_div(channels, CT)),
+                      kSC, smem, s>>>(n_nodes, channels, dim, rows, n_terms, CT, plan, coef, x,
+                                      gout, dx);
+    if ((rc = launch_status())) return rc;
+  }
+  if (dcoef_partials && n_terms > 0) {
+    const int G = gmp_sc_groups(n_nodes);
+    const int64_t per = ceil_div(n_nodes, (int64_t)G);
+    int CT = kPairs / n_terms;  // channels per tile: all of a tile's pairs in one workgroup
+    if (CT > kMaxCT) CT = kMaxCT;
+    if (CT > channels) CT = channels;
+    if (CT < 1) CT = 1;
+    const int tpb = kPairs / CT;
+    int NB = kStageLds / (CT * (dim + 1 + rows));
+    if (NB > 32) NB = 32;
+    if (NB < 1) NB = 1;
+    const size_t smem = (size_t)NB * CT * (dim + 1 + rows) * sizeof(float);
+    if ((rc = allow_smem(sc_bwd_coef_kernel, smem))) return rc;
+    sc_bwd_coef_kernel<<<dim3((unsigned)G, (unsigned)ceil_div(channels, CT),
+                              (unsigned)ceil_div(n_terms, tpb)),
+                         kSC, smem, s>>>(n_nodes, channels, dim, rows, n_terms, CT, NB, per, plan,
+                                         x, gout, dcoef_partials);
+    if ((rc = launch_status())) return rc;
+  }
+  return GMP_OK;
 }
 
 }  // extern "C"

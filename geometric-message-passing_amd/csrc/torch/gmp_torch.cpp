@@ -718,62 +718,48 @@ std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor& 
 }
 
 // ------------------------------------------------------------------ K8 symmetric contraction
-int64_t sc_nq(int64_t D, int64_t corr) {
-  const int nq = gmp_sc_monomials((int)D, (int)corr);
-  TORCH_CHECK(nq > 0, "gmp.symmetric_contraction: unsupported (dim ", D, ", correlation ", corr,
-              "): dim 4 / 9 with correlation 1..4, dim 16 with 1..3");
-  return nq;
-}
-int64_t sc_nq_deg(int64_t D, int64_t nu) {
-  int64_t c = 1;
-  for (int64_t s = 1; s <= nu; ++s) c = c * (D - 1 + s) / s;
-  return c;
-}
-
-void sc_checks(const Tensor& x, int64_t corr, const Tensor& A1, const optional<Tensor>& A2,
-               const optional<Tensor>& A3, const optional<Tensor>& A4) {
+// plan: the int32 term plan of gmp_symmetric_contraction_fwd_f32 ([row_ptr | out_base |
+// out_stride | terms], built and validated on the host by gmp_amd.equivariant); rows = M
+int64_t sc_terms(const Tensor& x, const Tensor& plan, int64_t rows, const Tensor& coef) {
   f32(x, "x");
   TORCH_CHECK(x.dim() == 3, "gmp.symmetric_contraction: x must be (N, C, D)");
-  const int64_t C = x.size(1), D = x.size(2);
-  sc_nq(D, corr);
-  f32(A1, "A1");
-  shape(A1, {C, D, D}, "A1");
-  const optional<Tensor>* As[3] = {&A2, &A3, &A4};
-  const char* names[3] = {"A2", "A3", "A4"};
-  for (int64_t nu = 2; nu <= corr; ++nu) {
-    TORCH_CHECK(As[nu - 2]->has_value(), "gmp.symmetric_contraction: ", names[nu - 2], " needed");
-    opt_f32(*As[nu - 2], {C, D, sc_nq_deg(D, nu)}, names[nu - 2]);
-  }
+  TORCH_CHECK(x.size(2) >= 1 && x.size(2) <= 63, "gmp.symmetric_contraction: D must be 1..63");
+  TORCH_CHECK(rows >= 1 && rows <= 255, "gmp.symmetric_contraction: rows must be 1..255");
+  need(plan, at::kInt, "plan");
+  TORCH_CHECK(plan.dim() == 1 && plan.numel() >= 3 * rows + 1,
+              "gmp.symmetric_contraction: plan must hold 3 rows + 1 + n_terms int32");
+  const int64_t T = plan.numel() - (3 * rows + 1);
+  f32(coef, "coef");
+  shape(coef, {T, x.size(1)}, "coef");
+  return T;
 }
 
-Tensor symmetric_contraction_fwd(const Tensor& x, int64_t corr, const Tensor& A1,
-                                 const optional<Tensor>& A2, const optional<Tensor>& A3,
-                                 const optional<Tensor>& A4) {
+Tensor symmetric_contraction_fwd(const Tensor& x, const Tensor& plan, int64_t rows,
+                                 const Tensor& coef) {
   OpGuard g(x, "symmetric_contraction_fwd");
-  sc_checks(x, corr, A1, A2, A3, A4);
+  const int64_t T = sc_terms(x, plan, rows, coef);
   const int64_t N = x.size(0), C = x.size(1), D = x.size(2);
-  Tensor out = at::empty({N, D * C}, x.options());
-  check_rc(gmp_symmetric_contraction_fwd_f32(N, (int)C, (int)D, (int)corr, fp(x), fp(A1),
-                                             cfp(A2), cfp(A3), cfp(A4), fp(out), cur_stream()),
+  Tensor out = at::empty({N, rows * C}, x.options());
+  check_rc(gmp_symmetric_contraction_fwd_f32(N, (int)C, (int)D, (int)rows, (int)T,
+                                             plan.data_ptr<int32_t>(), fp(coef), fp(x), fp(out),
+                                             cur_stream()),
            "gmp_symmetric_contraction_fwd_f32");
   return out;
 }
 
-std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t corr,
-                                                     const Tensor& A1, const optional<Tensor>& A2,
-                                                     const optional<Tensor>& A3,
-                                                     const optional<Tensor>& A4,
+std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, const Tensor& plan,
+                                                     int64_t rows, const Tensor& coef,
                                                      const Tensor& gout) {
   OpGuard g(x, "symmetric_contraction_bwd");
-  sc_checks(x, corr, A1, A2, A3, A4);
+  const int64_t T = sc_terms(x, plan, rows, coef);
   f32(gout, "gout");
   const int64_t N = x.size(0), C = x.size(1), D = x.size(2);
-  shape(gout, {N, D * C}, "gout");
+  shape(gout, {N, rows * C}, "gout");
   Tensor dx = at::empty_like(x);
-  Tensor part = at::empty({gmp_sc_groups(N), C, D, sc_nq(D, corr)}, x.options());
-  check_rc(gmp_symmetric_contraction_bwd_f32(N, (int)C, (int)D, (int)corr, fp(x), fp(A1),
-                                             cfp(A2), cfp(A3), cfp(A4), fp(gout), fp(dx),
-                                             fp(part), cur_stream()),
+  Tensor part = at::empty({gmp_sc_groups(N), T, C}, x.options());
+  check_rc(gmp_symmetric_contraction_bwd_f32(N, (int)C, (int)D, (int)rows, (int)T,
+                                             plan.data_ptr<int32_t>(), fp(coef), fp(x), fp(gout),
+                                             fp(dx), fp(part), cur_stream()),
            "gmp_symmetric_contraction_bwd_f32");
   return {dx, part};
 }
@@ -1430,16 +1416,13 @@ std::tuple<Tensor, Tensor, Tensor> irreps_bn_bwd(const Tensor& x, const Tensor&,
   return {at::empty_like(x), at::empty({chan_col.size(0)}, x.options()),
           at::empty({n_scalar}, x.options())};
 }
-Tensor symmetric_contraction_fwd(const Tensor& x, int64_t, const Tensor&, const optional<Tensor>&,
-                                 const optional<Tensor>&, const optional<Tensor>&) {
-  return at::empty({x.size(0), x.size(2) * x.size(1)}, x.options());
+Tensor symmetric_contraction_fwd(const Tensor& x, const Tensor&, int64_t rows, const Tensor&) {
+  return at::empty({x.size(0), rows * x.size(1)}, x.options());
 }
-std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, int64_t corr,
-                                                     const Tensor&, const optional<Tensor>&,
-                                                     const optional<Tensor>&,
-                                                     const optional<Tensor>&, const Tensor&) {
-  return {at::empty_like(x), at::empty({gmp_sc_groups(x.size(0)), x.size(1), x.size(2),
-                                        sc_nq(x.size(2), corr)}, x.options())};
+std::tuple<Tensor, Tensor> symmetric_contraction_bwd(const Tensor& x, const Tensor&, int64_t,
+                                                     const Tensor& coef, const Tensor&) {
+  return {at::empty_like(x), at::empty({gmp_sc_groups(x.size(0)), coef.size(0), x.size(1)},
+                                       x.options())};
 }
 Tensor tp_edge_z(at::IntArrayRef desc, const Tensor&, const Tensor&, const Tensor& x,
                  const Tensor&, const Tensor&, const Tensor&, int64_t e0, int64_t e1) {
@@ -1573,10 +1556,9 @@ TORCH_LIBRARY(gmp, m) {
   m.def("irreps_bn_bwd(Tensor x, Tensor grad_y, Tensor col_chan, Tensor chan_col, "
         "Tensor chan_info, Tensor weight, Tensor shift, Tensor invstd, bool training, "
         "int n_scalar) -> (Tensor grad_x, Tensor grad_weight, Tensor grad_bias)");
-  m.def("symmetric_contraction_fwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
-        "Tensor? A3, Tensor? A4=None) -> Tensor");
-  m.def("symmetric_contraction_bwd(Tensor x, int correlation, Tensor A1, Tensor? A2, "
-        "Tensor? A3, Tensor? A4, Tensor gout) -> (Tensor dx, Tensor dA_partials)");
+  m.def("symmetric_contraction_fwd(Tensor x, Tensor plan, int rows, Tensor coef) -> Tensor");
+  m.def("symmetric_contraction_bwd(Tensor x, Tensor plan, int rows, Tensor coef, Tensor gout) "
+        "-> (Tensor dx, Tensor dcoef_partials)");
   m.def("tp_edge_z(int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, Tensor src_sorted, "
         "Tensor perm, int e0, int e1) -> Tensor");
   m.def("tp_edge_z_bwd(int[] desc, Tensor paths, Tensor cg, Tensor x, Tensor sh, "

@@ -176,11 +176,10 @@ SIGNATURES = {
     "gmp_ln_act_bwd_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp,
                                    c_vp, c_size, c_vp]),
     "gmp_sc_groups": (c_int, [c_i64]),
-    "gmp_sc_monomials": (c_int, [c_int, c_int]),
-    "gmp_symmetric_contraction_fwd_f32": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp,
-                                                  c_vp, c_vp, c_vp, c_vp]),
-    "gmp_symmetric_contraction_bwd_f32": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp,
-                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gmp_symmetric_contraction_fwd_f32": (c_int, [c_i64, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                                  c_vp, c_vp, c_vp]),
+    "gmp_symmetric_contraction_bwd_f32": (c_int, [c_i64, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                                  c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gmp_egnn_node_image_bytes": (c_size, [c_i64]),
     "gmp_egnn_node_image_f32": (c_int, [c_i64, c_i64, ctypes.POINTER(GmpEgnnNodeParams), c_vp,
                                         c_vp]),

@@ -853,6 +853,7 @@ class Contraction(nn.Module):
     def __init__(self, irreps_in, irrep_out, correlation):
         super().__init__()
         irreps_in = o3.parse_irreps(irreps_in)
+        self.irrep_out = tuple(irrep_out)
         self.num_features = sum(m for m, ir in irreps_in if ir == (0, 1))
         coupling = tuple((1, ir) for _, ir in irreps_in)
         self.correlation = correlation
@@ -886,43 +887,29 @@ class Contraction(nn.Module):
         return torch.cat(outs, dim=0)
 
 
-def _nq_deg(D, nu):
-    return math.comb(D + nu - 1, nu)
-
-
 class SymmetricContractionFn(torch.autograd.Function):
-    """K8 (torch.ops.gmp.symmetric_contraction_{fwd,bwd}): out (N, D C) from x (N, C, D) and the
-    per-channel coefficients over the symmetric monomial basis A~_nu (C, D, C(D+nu-1, nu))."""
+    """K8 (torch.ops.gmp.symmetric_contraction_{fwd,bwd}): out (N, M C) from x (N, C, D) and the
+    coefficients coef (T, C) of the module's sparse term plan (gmp_sc.hip)."""
 
     @staticmethod
-    def forward(ctx, x, corr, *A):
-        x = _f32c(x)
-        A = [_f32c(a) for a in A]
-        _need_cuda(x, *A)
-        Ao = list(A) + [None] * (4 - len(A))
+    def forward(ctx, x, coef, plan, rows):
+        x, coef = _f32c(x), _f32c(coef)
+        _need_cuda(x, coef, plan)
         with _timed("symmetric_contraction_fwd"):
-            out = _lib.torch_ops().symmetric_contraction_fwd(x, corr, *Ao)
-        ctx.corr = corr
-        ctx.save_for_backward(x, *A)
+            out = _lib.torch_ops().symmetric_contraction_fwd(x, plan, rows, coef)
+        ctx.rows = rows
+        ctx.save_for_backward(x, coef, plan)
         return out
 
     @staticmethod
     @once_differentiable
     def backward(ctx, g):
-        x, *A = ctx.saved_tensors
-        g = _f32c(g)
-        Ao = list(A) + [None] * (4 - len(A))
+        x, coef, plan = ctx.saved_tensors
         with _timed("symmetric_contraction_bwd"):
-            dx, part = _lib.torch_ops().symmetric_contraction_bwd(x, ctx.corr, *Ao, g)
-        if not ctx.needs_input_grad[0]:
-            dx = None
-        dA = part.sum(0)  # fixed-order sum over node groups
-        D, grads, q0 = x.shape[2], [], 0
-        for nu in range(1, len(A) + 1):
-            n = _nq_deg(D, nu)
-            grads.append(dA[..., q0:q0 + n].contiguous())
-            q0 += n
-        return (dx, None, *grads)
+            dx, part = _lib.torch_ops().symmetric_contraction_bwd(x, plan, ctx.rows, coef,
+                                                                  _f32c(g))
+        dcoef = part.sum(0) if ctx.needs_input_grad[1] else None  # fixed-order group sum
+        return (dx if ctx.needs_input_grad[0] else None, dcoef, None, None)
 
 
 _SYM_IDX = {}
@@ -945,7 +932,7 @@ def _sym_index(nu, device, D=9):
 
 
 def fold_symmetric(A, nu):
-    """A (C, M, D^nu) -> A~ (C, M, C(D - 1 + nu, nu)): every permutation's coefficient summed
+    """A (..., D^nu) -> A~ (..., C(D - 1 + nu, nu)): every permutation's coefficient summed
     into the sorted monomial (differentiable; the adjoint spreads dA~ back to each permutation)."""
     if nu == 1:
         return A
@@ -955,10 +942,53 @@ def fold_symmetric(A, nu):
     return Ap[..., idx].sum(-1)
 
 
-# K8's compiled (per-channel dim, correlation) pairs: C x (0e+1o[+2e[+3o]]) -> the same irreps
-_K8_IRREPS = {4: ((0, 1), (1, -1)), 9: ((0, 1), (1, -1), (2, 1)),
-              16: ((0, 1), (1, -1), (2, 1), (3, -1))}
-_K8_MAX_CORR = {4: 4, 9: 4, 16: 3}
+_K8_MAX_DIM, _K8_MAX_ROWS = 63, 255
+
+
+def k8_plan(contractions, D, C, correlation):
+    """The K8 term plan of a SymmetricContraction (gmp.h gmp_symmetric_contraction_fwd_f32):
+    the (row m, monomial) pairs whose folded coefficient can be non-zero for some weights --
+    the fold of some U_nu[m, ..., k] over the monomial's permutations is (structurally) non-zero
+    -- in row order, monomials ascending within a row.  Returns (plan int32, gather int64): coef
+    (T, C) = the rows `gather` of cat_nu(A~_nu) (C, M, NQ) flattened over (m, q) and transposed."""
+    import itertools
+    masks, nq = [], []
+    for nu in range(1, correlation + 1):
+        rows = []
+        for con in contractions:
+            U = con.U(nu).double()
+            if U.dim() == nu + 1:  # scalar output: the m axis was squeezed
+                U = U.unsqueeze(0)
+            K = U.shape[-1]
+            F = fold_symmetric(U.reshape(U.shape[0], -1, K).permute(2, 0, 1), nu)  # (K, Mk, NQ)
+            tol = 1e-6 * float(U.abs().max())
+            rows.append((F.abs() > tol).any(0))
+        masks.append(torch.cat(rows, 0))
+        nq.append(masks[-1].shape[1])
+    M = masks[0].shape[0]
+    factors = [list(itertools.combinations_with_replacement(range(D), nu))
+               for nu in range(1, correlation + 1)]
+    row_ptr, terms, gather = [0], [], []
+    nq_total, q_off = sum(nq), [sum(nq[:i]) for i in range(len(nq))]
+    for m in range(M):
+        for nu in range(1, correlation + 1):
+            for q in torch.nonzero(masks[nu - 1][m]).view(-1).tolist():
+                f = list(factors[nu - 1][q]) + [D] * (4 - nu)
+                terms.append(f[0] | f[1] << 6 | f[2] << 12 | f[3] << 18 | m << 24)
+                gather.append(m * nq_total + q_off[nu - 1] + q)
+        row_ptr.append(len(terms))
+    base, stride, m0 = [], [], 0
+    for con in contractions:
+        d = 2 * con.irrep_out[0] + 1
+        for mm in range(d):
+            base.append(C * m0 + mm)
+            stride.append(d)
+        m0 += d
+    assert m0 == M
+    words = torch.tensor(terms, dtype=torch.int64)
+    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words)  # int32 bit patterns
+    plan = torch.cat([torch.tensor(row_ptr + base + stride, dtype=torch.int64), words])
+    return plan.to(torch.int32), torch.tensor(gather, dtype=torch.int64)
 
 
 class SymmetricContraction(nn.Module):
@@ -968,20 +998,24 @@ class SymmetricContraction(nn.Module):
         self.correlation = correlation
         irreps_in = o3.parse_irreps(irreps_in)
         C = irreps_in[0][0]
-        irs = tuple(ir for _, ir in irreps_in)
-        D = sum(2 * l + 1 for l, _ in irs)
-        # K8 applies to C x (0e + 1o [+ 2e [+ 3o]]) -> the same irreps (max_ell 1..3), correlation
-        # <= 4 (<= 3 at max_ell 3); other irreps (both parities, repeated l) run the per-irrep
-        # contraction below (torch on the GPU)
-        self._k8 = (_K8_IRREPS.get(D) == irs and all(m == C for m, _ in irreps_in) and
-                    tuple(self.irreps_out) == tuple(irreps_in) and
-                    1 <= correlation <= _K8_MAX_CORR[D])
+        D = sum(2 * l + 1 for _, (l, _) in irreps_in)
         self.contractions = nn.ModuleDict({
             f"{m}x{l}{'e' if p == 1 else 'o'}": Contraction(irreps_in, (l, p), correlation)
             for m, (l, p) in self.irreps_out})
+        o3.clear_cg_cache()
+        M = sum(2 * l + 1 for _, (l, _) in self.irreps_out)
+        # K8 takes any irreps with C channels each (x (N, C, D) is reshape_irreps' layout; the
+        # reference's Contraction needs the same, symmetric_contraction.py:102), D <= 63, M <= 255
+        self._k8 = (all(m == C for m, _ in irreps_in) and all(m == C for m, _ in self.irreps_out)
+                    and D <= _K8_MAX_DIM and M <= _K8_MAX_ROWS and correlation >= 1)
+        if self._k8:
+            plan, gather = k8_plan(list(self.contractions.values()), D, C, correlation)
+            self.register_buffer("_k8_plan", plan, persistent=False)
+            self.register_buffer("_k8_gather", gather, persistent=False)
+            self._k8_rows = M
 
     def coefficients(self):
-        """A_nu (C, D, D^nu): per-channel coefficient tensors, output rows [0e | 1o | 2e ..]."""
+        """A_nu (C, M, D^nu): per-channel coefficient tensors, output rows in irreps_out order."""
         out = []
         for nu in range(1, self.correlation + 1):
             rows = []
@@ -994,10 +1028,17 @@ class SymmetricContraction(nn.Module):
             out.append(torch.cat(rows, dim=1))
         return out
 
+    def k8_coefficients(self):
+        """coef (T, C): the folded coefficients at the plan's terms, term-major
+        (differentiable)."""
+        A = torch.cat([fold_symmetric(a, nu + 1) for nu, a in enumerate(self.coefficients())],
+                      dim=-1)
+        return A.reshape(A.shape[0], -1).t().index_select(0, self._k8_gather)
+
     def forward(self, x, y=None):
         if self._k8 and x.is_cuda:
-            A = [fold_symmetric(a, nu + 1) for nu, a in enumerate(self.coefficients())]
-            return SymmetricContractionFn.apply(x, self.correlation, *A)
+            return SymmetricContractionFn.apply(x, self.k8_coefficients(), self._k8_plan,
+                                                self._k8_rows)
         return torch.cat([c(x) for c in self.contractions.values()], dim=-1)
 
 

@@ -145,10 +145,11 @@ def fctp_instructions(irreps_in1, irreps_in2, irreps_out):
 
 
 # ----------------------------------------------------------------------------------- MACE U
-def _cg_chain(irreps_list, filter_ir=None):
+def _cg_chain(irreps_list, filter_ir=None, only=None):
     """Generalised CG of a product of irreps (cg.py:_wigner_nj, component normalisation):
     list of (irrep_out, tensor (2lo+1, d, ..., d)) sorted (stably) by irrep.  filter_ir: the
-    irreps allowed at every coupling step (cg.py:_wigner_nj filter_ir_mid)."""
+    irreps allowed at every coupling step (cg.py:_wigner_nj filter_ir_mid).  only: keep just
+    this output irrep at the last step (the chain of the left factors is shared, _chain_left)."""
     if len(irreps_list) == 1:
         irreps = irreps_list[0]
         dim = irreps_dim(irreps)
@@ -164,17 +165,21 @@ def _cg_chain(irreps_list, filter_ir=None):
     dims_left = [irreps_dim(x) for x in left]
     dr = irreps_dim(right)
     out = []
-    for ir_left, C_left in _cg_chain(left, filter_ir):
+    for ir_left, C_left in _chain_left(tuple(left), _fkey(filter_ir)):
         i = 0
         for m, ir in right:
             d = 2 * ir[0] + 1
             for ir_out in product_irreps(ir_left, ir):
                 if filter_ir is not None and tuple(ir_out) not in filter_ir:
                     continue
+                if only is not None and tuple(ir_out) != tuple(only):
+                    continue
                 lo = ir_out[0]
                 C = wigner_3j(lo, ir_left[0], ir[0]) * math.sqrt(2 * lo + 1)
-                C = np.einsum("jk,ijl->ikl", C_left.reshape(C_left.shape[0], -1), C)
-                C = C.reshape((2 * lo + 1, *dims_left, d))
+                # C[i, k, l] = sum_j C_left[j, k] w3j[i, j, l] (BLAS: the einsum's loop form ran
+                # ~30 s per output irrep at max_ell 3, correlation 4)
+                C = np.tensordot(C, C_left.reshape(C_left.shape[0], -1), axes=([1], [0]))
+                C = C.transpose(0, 2, 1).reshape((2 * lo + 1, *dims_left, d))
                 for u in range(m):
                     E = np.zeros((2 * lo + 1, *dims_left, dr))
                     E[..., i + u * d:i + (u + 1) * d] = C
@@ -184,13 +189,33 @@ def _cg_chain(irreps_list, filter_ir=None):
     return out
 
 
+def _fkey(filter_ir):
+    return None if filter_ir is None else frozenset(filter_ir)
+
+
+@lru_cache(maxsize=4)
+def _chain_left(irreps_list, filter_key):
+    """The chain of the left factors, shared by every output irrep of one SymmetricContraction
+    (cleared by clear_cg_cache() once the module is built)."""
+    return _cg_chain(list(irreps_list), None if filter_key is None else set(filter_key))
+
+
+def clear_cg_cache():
+    _chain_left.cache_clear()
+
+
 def u_matrix(coupling_irreps, ir_out, nu):
     """cg.py U_matrix_real(coupling, ir_out, nu)[-1]: (2lo+1 [squeezed if 1], d^nu..., K).
-    correlation 4 couples through the natural-parity irreps l < 12 only (cg.py:101-115)."""
+    correlation 4 couples through the natural-parity irreps l < 12 only (cg.py:101-115).  An
+    output irrep no coupling path reaches raises, as the reference does (cg.py:116-133 leaves
+    last_ir unbound: e.g. 0o at correlation 4, where the filter admits natural parity only)."""
     filt = {(l, (-1) ** l) for l in range(12)} if nu == 4 else None
-    blocks = [C for ir, C in _cg_chain([coupling_irreps] * nu, filt) if ir == tuple(ir_out)]
-    stacked = np.stack([np.squeeze(C) for C in blocks], axis=-1)
-    return stacked
+    blocks = [C for ir, C in _cg_chain([tuple(coupling_irreps)] * nu, filt, only=ir_out)
+              if ir == tuple(ir_out)]
+    if not blocks:
+        raise ValueError(f"no coupling path reaches {ir_out} at correlation {nu} (the "
+                         "reference's cg.U_matrix_real fails here too)")
+    return np.stack([np.squeeze(C) for C in blocks], axis=-1)
 
 
 # ----------------------------------------------------------------------------------- gates

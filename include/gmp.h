@@ -33,7 +33,8 @@ extern "C" {
  * 4 (r05): gmp_egnn_node_fwd_f32 / gmp_egnn_node_params added.
  * Version 5 (r05): the opt-in TP kernels K7s / K7f (gmp_tp_node_fwd_fused_f32,
  * gmp_tp_z_fused_layout_*, gmp_tp_node_dw_*), the row GEMM (gmp_split_x3_f32, gmp_gemm_x3_f32),
- * gmp_tp_gemm_set_rings, gmp_wgrad_set_grid_cap and the CU-masked stream entries removed. */
+ * gmp_tp_gemm_set_rings, gmp_wgrad_set_grid_cap and the CU-masked stream entries removed; K8 takes
+ * the sparse term plan (any irreps), gmp_sc_monomials removed. */
 #define GMP_ABI_VERSION 5
 
 enum {
@@ -639,30 +640,33 @@ int gmp_xyz_norm_bwd_f32(int64_t rows, int64_t h, const float* vh, const float* 
                          float* grad_vh, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:88-188 with
- * element_dependent=False, called per output irrep at :176-185), all output irreps of C channels
- * at once.  x (N, C, D) = reshape_irreps of C x (0e+1o[+2e[+3o]]) (irreps_tools.py:63-79),
- * D = (L+1)^2 for max_ell L = 1, 2, 3 (D = 4, 9, 16).  Coefficients over the SYMMETRIC monomial
- * basis (x_i x_j x_k is symmetric, so every permutation's coefficient folds into the sorted index
- * tuple): A_nu (C, D, C(D+nu-1, nu)) over i1 <= .. <= inu (lexicographic),
- *   A_nu[c, m, q] = sum over the distinct permutations p of q of sum_k U_nu[m, p, k] W_nu[k, c]
- * (the host builds them from the module's U_matrix_nu buffers and weights, differentiably).
- * correlation 1..4 for D = 4, 9; 1..3 for D = 16 (else GMP_ERR_UNSUPPORTED); A_nu for nu >
- * correlation may be NULL.  out (N, D C) in mul_ir order [0e: C | 1o: 3C | 2e: 5C | 3o: 7C].
- * Backward: dx (N, C, D) (may be NULL) and dA partials (gmp_sc_groups(N), C, D, nq) with
- * nq = gmp_sc_monomials(D, correlation) (monomials [deg1 | deg2 | ..] as above; may be NULL);
- * the caller sums the groups.  (ABI 3: the dim argument and A4 are new.)
+ * K8 MACE symmetric contraction (models/mace_modules/symmetric_contraction.py:20-188 with
+ * element_dependent=False; SymmetricContraction.forward :81-85 concatenates the per-output-irrep
+ * Contraction.forward :150-185), all output irreps of C channels at once, any irreps: x (N, C, D)
+ * = reshape_irreps of C x (irreps) (irreps_tools.py:63-79; D <= 63 components per channel, any
+ * parities, repeated l), correlation 1..4 folded into one polynomial over symmetric monomials
+ * and evaluated over the sparse TERM LIST of the module's coupling pattern:
+ *   out[b, out_base[m] + out_stride[m] c] = sum_{t in row m} coef[t, c] prod_{r < 4} xx[f_r(t)]
+ * with xx = [x[b, c, 0..D-1], 1.0] (factor index D = the constant 1: degree < 4 monomials).
+ * plan (int32): [row_ptr (rows + 1) | out_base (rows) | out_stride (rows) | terms (n_terms)],
+ *   term word f0 | f1 << 6 | f2 << 12 | f3 << 18 | m << 24 (m < rows <= 255), terms of row m at
+ *   row_ptr[m] .. row_ptr[m+1] - 1 (summed in that order);
+ * coef (n_terms, C), term-major: coef[t, c] = A~_nu[c, m_t, q_t], the folded coefficient
+ *   A~_nu[c, m, q] = sum over the distinct permutations p of monomial q of
+ *   sum_k U_nu[m, p, k] W_nu[k, c] (the host builds the plan once and coef per call,
+ *   differentiably).  out (N, rows C).
+ * Backward: dx (N, C, D) (may be NULL) and dcoef partials (gmp_sc_groups(N), n_terms, C) (may
+ * be NULL; the caller sums the groups in order).  Deterministic.  (ABI 5: the plan form replaces
+ * the dense per-degree A_nu arguments and gmp_sc_monomials.)
  * ------------------------------------------------------------------------------------------ */
 int gmp_sc_groups(int64_t n_nodes);
-int gmp_sc_monomials(int dim, int correlation);
-int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
-                                      const float* x, const float* A1, const float* A2,
-                                      const float* A3, const float* A4, float* out,
-                                      void* stream);
-int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int dim, int correlation,
-                                      const float* x, const float* A1, const float* A2,
-                                      const float* A3, const float* A4, const float* gout,
-                                      float* dx, float* dA_partials, void* stream);
+int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int dim, int rows,
+                                      int n_terms, const int32_t* plan, const float* coef,
+                                      const float* x, float* out, void* stream);
+int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int dim, int rows,
+                                      int n_terms, const int32_t* plan, const float* coef,
+                                      const float* x, const float* gout, float* dx,
+                                      float* dcoef_partials, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * K13 SchNet CFConv fused message + aggregation (PyG 2.3.1 CFConv.message `x_j * W` and

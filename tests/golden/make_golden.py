@@ -139,16 +139,26 @@ def make_mace_widening():
     mm = _ref_stubs.load_mace_contraction(REF)
     o3l = sys.modules["e3nn.o3"]
     out = []
-    for name, irr, corr, seed in [("mace_symmetric_contraction_c4.pt", "4x0e+4x1o+4x2e", 4, 21),
-                                  ("mace_symmetric_contraction_l3.pt", "4x0e+4x1o+4x2e+4x3o", 3,
-                                   22)]:
+    cases = [("mace_symmetric_contraction_c4.pt", "4x0e+4x1o+4x2e", 4, 21),
+             ("mace_symmetric_contraction_l3.pt", "4x0e+4x1o+4x2e+4x3o", 3, 22),
+             # r05: both parities (incompleteness.ipynb:530-538's irreps; correlation 3 -- at 4
+             # the reference raises, recorded below), max_ell 5 at correlation 2
+             # (rotsym.ipynb:247-257), correlation 4 at max_ell 3
+             ("mace_symmetric_contraction_bp3.pt", "4x0e+4x0o+4x1e+4x1o+4x2e+4x2o", 3, 23),
+             ("mace_symmetric_contraction_l5.pt", "4x0e+4x1o+4x2e+4x3o+4x4e+4x5o", 2, 24),
+             ("mace_symmetric_contraction_l3c4.pt", "2x0e+2x1o+2x2e+2x3o", 4, 25)]
+    if os.environ.get("GOLDEN_CASES"):
+        keep = set(os.environ["GOLDEN_CASES"].split(","))
+        cases = [c for c in cases if c[0] in keep]
+    for name, irr, corr, seed in cases:
         torch.manual_seed(seed)
         irreps = o3l.Irreps(irr)
         SC = mm["models.mace_modules.symmetric_contraction"].SymmetricContraction(
             irreps_in=irreps, irreps_out=irreps, correlation=corr, element_dependent=False,
             num_elements=1)
         D = sum(2 * ir.l + 1 for _, ir in irreps)
-        x = torch.randn(23, 4, D, requires_grad=True)
+        C = int(irr.split("x")[0])
+        x = torch.randn(23, C, D, requires_grad=True)
         y = SC(x, None)
         gy = torch.randn_like(y)
         (y * gy).sum().backward()
@@ -160,6 +170,21 @@ def make_mace_widening():
         d.update(grads_dict(SC))
         torch.save(d, os.path.join(HERE, name))
         out.append(name)
+    # the incompleteness notebook's MACE line (correlation 4 on both parities): the reference's
+    # U_matrix_real has no coupling path to 0o under its natural-parity filter and raises
+    irreps = o3l.Irreps("4x0e+4x0o+4x1e+4x1o+4x2e+4x2o")
+    try:
+        mm["models.mace_modules.symmetric_contraction"].SymmetricContraction(
+            irreps_in=irreps, irreps_out=irreps, correlation=4, element_dependent=False,
+            num_elements=1)
+        rec = {"raised": None}
+    except Exception as e:  # noqa: BLE001 - the reference's own failure is the fixture
+        rec = {"raised": type(e).__name__, "message": str(e)}
+    rec.update(irreps=str(irreps), correlation=4)
+    import json
+    with open(os.path.join(HERE, "mace_symmetric_contraction_bp4_error.json"), "w") as fh:
+        json.dump(rec, fh, indent=1)
+    out.append("mace_symmetric_contraction_bp4_error.json")
     return out
 
 

@@ -2,6 +2,8 @@
 match the oracle (hence the reference's), the node-level e3nn pieces (o3.Linear, BatchNorm,
 Gate, SymmetricContraction, which run as PyTorch ops on N-row tensors) agree with the oracle,
 and the K7 path tables are well formed."""
+import os
+
 import pytest
 import torch
 
@@ -165,7 +167,9 @@ def test_schnet_oracle_known_answers():
 
 
 _WIDENING = [("mace_symmetric_contraction_c4.pt", "4x0e+4x1o+4x2e", 4),
-             ("mace_symmetric_contraction_l3.pt", "4x0e+4x1o+4x2e+4x3o", 3)]
+             ("mace_symmetric_contraction_l3.pt", "4x0e+4x1o+4x2e+4x3o", 3),
+             ("mace_symmetric_contraction_bp3.pt", "4x0e+4x0o+4x1e+4x1o+4x2e+4x2o", 3),
+             ("mace_symmetric_contraction_l5.pt", "4x0e+4x1o+4x2e+4x3o+4x4e+4x5o", 2)]
 
 
 @pytest.mark.parametrize("name,irr,corr", _WIDENING)
@@ -186,3 +190,61 @@ def test_symmetric_contraction_widening_golden(golden, name, irr, corr):
         torch.testing.assert_close(x.grad, d["grad_x"], atol=1e-5, rtol=1e-5)
         for k, p in mod.named_parameters():
             torch.testing.assert_close(p.grad, d["grad." + k], atol=1e-5, rtol=1e-5, msg=k)
+
+
+def _eval_plan(sc, x):
+    """The K8 term plan evaluated in torch exactly as gmp_sc.hip's forward walks it."""
+    plan, M = sc._k8_plan.long(), sc._k8_rows
+    C, D = x.shape[1], x.shape[2]
+    row_ptr, base, stride = plan[:M + 1], plan[M + 1:2 * M + 1], plan[2 * M + 1:3 * M + 1]
+    words = plan[3 * M + 1:] & 0xFFFFFFFF
+    coef = sc.k8_coefficients()
+    xx = torch.cat([x, torch.ones(x.shape[0], C, 1)], -1)
+    out = torch.zeros(x.shape[0], M * C)
+    cols = torch.arange(C)
+    for m in range(M):
+        acc = torch.zeros(x.shape[0], C)
+        for t in range(int(row_ptr[m]), int(row_ptr[m + 1])):
+            w = int(words[t])
+            assert w >> 24 == m
+            z = torch.ones(x.shape[0], C)
+            for r in range(4):
+                z = z * xx[:, :, (w >> (6 * r)) & 63]
+            acc = acc + coef[t] * z
+        out[:, int(base[m]) + int(stride[m]) * cols] = acc
+    return out
+
+
+@pytest.mark.parametrize("irr,corr", [("3x0e+3x1o+3x2e", 3), ("2x0e+2x0o+2x1e+2x1o+2x2e+2x2o", 3),
+                                      ("2x0e+2x1o+2x2e+2x3o+2x4e+2x5o", 2), ("2x0e+2x1o", 4),
+                                      ("2x1o+2x0e+2x1e", 2)])
+def test_k8_term_plan_matches_contraction(irr, corr):
+    """The K8 host logic (k8_plan: the structurally non-zero (row, monomial) pairs, the factor
+    words with the 1.0 slot, the output columns; k8_coefficients: fold + gather) evaluated as the
+    kernel walks it equals the module's per-irrep contraction (CPU)."""
+    eq = _eq()
+    torch.manual_seed(corr)
+    sc = eq.SymmetricContraction(irr, irr, corr)
+    assert sc._k8
+    C = int(irr.split("x")[0])
+    D = sum(2 * int(t.split("x")[1][:-1]) + 1 for t in irr.split("+"))
+    x = torch.randn(6, C, D)
+    with torch.no_grad():
+        ref = torch.cat([c(x) for c in sc.contractions.values()], dim=-1)
+        got = _eval_plan(sc, x)
+    torch.testing.assert_close(got, ref, atol=2e-5, rtol=1e-5)
+
+
+def test_k8_both_parity_correlation4_raises_like_reference():
+    """incompleteness.ipynb:530-538's MACE line (correlation 4 on 0e+0o+1e+1o+2e+2o): the
+    reference's own SymmetricContraction raises (no path reaches 0o under cg.py's natural-parity
+    filter; fixture written by make_golden.py mace_widening); the product module raises too."""
+    import json
+    from conftest import GOLDEN
+    eq = _eq()
+    with open(os.path.join(GOLDEN, "mace_symmetric_contraction_bp4_error.json")) as fh:
+        rec = json.load(fh)
+    assert rec["raised"] == "UnboundLocalError" and rec["correlation"] == 4
+    irr = "2x0e+2x0o+2x1e+2x1o+2x2e+2x2o"
+    with pytest.raises(ValueError, match="no coupling path"):
+        eq.SymmetricContraction(irr, irr, 4)

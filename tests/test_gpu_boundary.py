@@ -132,16 +132,15 @@ def test_shape_checks_irreps_sc_gate():
          torch.zeros(12, 2, **i32), torch.ones(12, **f), None, torch.zeros(4, **f),
          torch.ones(12, **f), True, 0.1, 1e-5, match="col_chan")
     xs = torch.randn(7, 4, 9, **f)
-    _bad(ops_.symmetric_contraction_fwd, xs, 3, torch.randn(4, 9, 9, **f),
-         torch.randn(4, 9, 45, **f), torch.randn(4, 9, 160, **f), match="A3")
-    _bad(ops_.symmetric_contraction_bwd, xs, 1, torch.randn(4, 9, 9, **f), None, None, None,
+    plan = torch.zeros(3 * 9 + 1 + 5, **i32)  # 9 rows, 5 terms
+    _bad(ops_.symmetric_contraction_fwd, xs, plan, 9, torch.randn(6, 4, **f), match="coef")
+    _bad(ops_.symmetric_contraction_fwd, xs, plan.long(), 9, torch.randn(5, 4, **f),
+         match="plan")
+    _bad(ops_.symmetric_contraction_fwd, xs, plan[:20], 9, torch.randn(5, 4, **f), match="plan")
+    _bad(ops_.symmetric_contraction_fwd, torch.randn(7, 4, 64, **f), plan, 9,
+         torch.randn(5, 4, **f), match="D must")
+    _bad(ops_.symmetric_contraction_bwd, xs, plan, 9, torch.randn(5, 4, **f),
          torch.randn(7, 35, **f), match="gout")
-    _bad(ops_.symmetric_contraction_fwd, torch.randn(7, 4, 16, **f), 4,
-         torch.randn(4, 16, 16, **f), torch.randn(4, 16, 136, **f), torch.randn(4, 16, 816, **f),
-         torch.randn(4, 16, 3876, **f), match="unsupported")
-    _bad(ops_.symmetric_contraction_fwd, torch.randn(7, 4, 9, **f), 4,
-         torch.randn(4, 9, 9, **f), torch.randn(4, 9, 45, **f), torch.randn(4, 9, 165, **f),
-         None, match="A4")
 
 
 def test_shape_checks_tp_and_outer_sums():
