@@ -331,10 +331,10 @@ __global__ __launch_bounds__(kGT) void gvp_msg0_bwd_kernel(int64_t E, const int6
     gemm_wtx<S / 16, 1>(sWsv, LD128, dgate, ds, i, g);  // dspre total
     if (k.valid) {
       st_row<S / 16>(O.dspre + k.e * S, ds, g);
-      st_row<S / 16>(O.spre + k.e * S, F.spre, g);
+      if (O.spre) st_row<S / 16>(O.spre + k.e * S, F.spre, g);
       st_row<1>(O.dgate + k.e * V, dgate, g);
       st_row<3>(O.vn + k.e * H0, F.vn, g);
-      st_vrow<3>(O.vh + k.e * (3 * H0), F.vh, g);
+      if (O.vh) st_vrow<3>(O.vh + k.e * (3 * H0), F.vh, g);
       st_vrow<1>(O.dvpre + k.e * (3 * V), dv, g);
     }
     // des = We^T dspre ; dvn = Wn^T dspre
@@ -607,12 +607,53 @@ __global__ __launch_bounds__(kGT) void gvp_layer_fwd_x3_kernel(int64_t E, const 
   }
 }
 
-template <int ACT>
+// Upstream gradient of the layer's per-edge outputs.  AGG = 0: per-edge rows ds_out (E, S),
+// dv_out (E, 3V).  AGG = 1 / 2: the layer feeds a sum / mean aggregation at the receivers
+// (GVPConv, gvp_layer.py:319-324 with aggr "add" / "mean"): the rows are the aggregation's node
+// gradient gathered at index[e] (x 1 / max(count, 1) for the mean, count from rowptr; an index
+// outside [0, n_nodes) gets zeros) -- K3's sum / mean backward in the load, so the (E, S + 3V)
+// per-edge gradient is never written.
+struct AggGrad {
+  const int64_t* index;
+  const int64_t* rowptr;
+  int64_t n_nodes;
+};
+template <int AGG>
+__device__ __forceinline__ void ld_grad_rows(const float* __restrict__ ds_out,
+                                             const float* __restrict__ dv_out, const AggGrad& A,
+                                             int64_t e, int g, f32x4 (&ds)[S / 16],
+                                             f32x4 (&dv)[3][1]) {
+  if (AGG == 0) {
+    ld_row<S / 16>(ds, ds_out + e * S, g);
+    ld_vrow<1>(dv, dv_out + e * (3 * V), g);
+    return;
+  }
+  const int64_t n = A.index[e];
+  const bool ok = n >= 0 && n < A.n_nodes;
+  const int64_t r = ok ? n : 0;
+  ld_row<S / 16>(ds, ds_out + r * S, g);
+  ld_vrow<1>(dv, dv_out + r * (3 * V), g);
+  float sc = ok ? 1.f : 0.f;
+  if (AGG == 2 && ok) {
+    const int64_t cnt = A.rowptr[r + 1] - A.rowptr[r];
+    sc = 1.f / (float)(cnt > 0 ? cnt : 1);
+  }
+#pragma unroll
+  for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ds[p][q] *= sc;
+#pragma unroll
+  for (int x = 0; x < 3; ++x)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dv[x][0][q] *= sc;
+}
+
+template <int ACT, int AGG>
 __global__ __launch_bounds__(kGT) void gvp_layer_bwd_x3_kernel(int64_t E, const float* __restrict__ s_in,
                                                                const float* __restrict__ v_in, LayerW P,
                                                                const float* __restrict__ ds_out,
                                                                const float* __restrict__ dv_out,
-                                                               LayerGrads O) {
+                                                               AggGrad A, LayerGrads O) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   layer_to_lds_x3<true>(sm, P);
   __syncthreads();
@@ -632,15 +673,14 @@ __global__ __launch_bounds__(kGT) void gvp_layer_bwd_x3_kernel(int64_t E, const 
     ld_vrow<1>(v, v_in + k.e * (3 * V), g);
     LayerFwd F;
     layer_forward_x3<true>(sm, s, v, F, lane, i, g);
-    ld_row<S / 16>(s, ds_out + k.e * S, g);
+    f32x4 dv[3][1];
+    ld_grad_rows<AGG>(ds_out, dv_out, A, k.e, g, s, dv);
     if (ACT) {
 #pragma unroll
       for (int p = 0; p < S / 16; ++p)
 #pragma unroll
         for (int q = 0; q < 4; ++q) s[p][q] = F.spre[p][q] > 0.f ? s[p][q] : 0.f;
     }
-    f32x4 dv[3][1];
-    ld_vrow<1>(dv, dv_out + k.e * (3 * V), g);
     f32x4 dgate[1];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -730,12 +770,14 @@ int gmp_gvp_layer_fwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   return launch_status();
 }
 
-int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
-                          const float* Ws, const float* bs, const float* Wsv, const float* bsv,
-                          const float* Wh, const float* Wv, const float* ds_out,
-                          const float* dv_out, float* ds_in, float* dv_in, float* dspre,
-                          float* spre, float* dgate, float* vn, float* vh, float* dvpre,
-                          float* dvh, void* stream) {
+}  // extern "C"
+
+namespace {
+int layer_bwd(int64_t n_edges, int relu, int agg, const AggGrad& A, const float* s_in,
+              const float* v_in, const float* Ws, const float* bs, const float* Wsv,
+              const float* bsv, const float* Wh, const float* Wv, const float* ds_out,
+              const float* dv_out, float* ds_in, float* dv_in, float* dspre, float* spre,
+              float* dgate, float* vn, float* vh, float* dvpre, float* dvh, void* stream) {
   GMP_CHECK_ARG(n_edges >= 0);
   if (n_edges == 0) return GMP_OK;
   GMP_CHECK_ARG(s_in && v_in && Ws && bs && Wsv && bsv && Wh && Wv && ds_out && dv_out);
@@ -749,10 +791,45 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   hipStream_t s = as_stream(stream);
   int rc;
   const size_t smx = kLayerSmemX3 * sizeof(float);
-  auto k = relu ? gvp_layer_bwd_x3_kernel<1> : gvp_layer_bwd_x3_kernel<0>;
+  auto k = relu ? (agg == 0 ? gvp_layer_bwd_x3_kernel<1, 0>
+                            : (agg == 1 ? gvp_layer_bwd_x3_kernel<1, 1>
+                                        : gvp_layer_bwd_x3_kernel<1, 2>))
+                : (agg == 0 ? gvp_layer_bwd_x3_kernel<0, 0>
+                            : (agg == 1 ? gvp_layer_bwd_x3_kernel<0, 1>
+                                        : gvp_layer_bwd_x3_kernel<0, 2>));
   if ((rc = set_smem(k, smx))) return rc;
-  k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, O);
+  k<<<G, kGT, smx, s>>>(n_edges, s_in, v_in, P, ds_out, dv_out, A, O);
   return launch_status();
+}
+}  // namespace
+
+extern "C" {
+
+int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
+                          const float* Ws, const float* bs, const float* Wsv, const float* bsv,
+                          const float* Wh, const float* Wv, const float* ds_out,
+                          const float* dv_out, float* ds_in, float* dv_in, float* dspre,
+                          float* spre, float* dgate, float* vn, float* vh, float* dvpre,
+                          float* dvh, void* stream) {
+  return layer_bwd(n_edges, relu, 0, AggGrad{nullptr, nullptr, 0}, s_in, v_in, Ws, bs, Wsv, bsv,
+                   Wh, Wv, ds_out, dv_out, ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh,
+                   stream);
+}
+
+int gmp_gvp_layer_bwd_agg_f32(int64_t n_edges, int64_t n_nodes, int reduce, const int64_t* index,
+                              const int64_t* rowptr, int relu, const float* s_in,
+                              const float* v_in, const float* Ws, const float* bs,
+                              const float* Wsv, const float* bsv, const float* Wh,
+                              const float* Wv, const float* ds_node, const float* dv_node,
+                              float* ds_in, float* dv_in, float* dspre, float* spre,
+                              float* dgate, float* vn, float* vh, float* dvpre, float* dvh,
+                              void* stream) {
+  GMP_CHECK_ARG(n_nodes >= 0 && index && (reduce == GMP_REDUCE_SUM ||
+                                          (reduce == GMP_REDUCE_MEAN && rowptr)));
+  if (n_edges > 0) GMP_CHECK_ARG(n_nodes > 0);
+  return layer_bwd(n_edges, relu, reduce == GMP_REDUCE_MEAN ? 2 : 1,
+                   AggGrad{index, rowptr, n_nodes}, s_in, v_in, Ws, bs, Wsv, bsv, Wh, Wv, ds_node,
+                   dv_node, ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh, stream);
 }
 
 int gmp_gvp_msg0_fwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
@@ -785,7 +862,7 @@ int gmp_gvp_msg0_bwd_f32(int64_t n_edges, const int64_t* send, const int64_t* re
   if (n_edges == 0) return GMP_OK;
   GMP_CHECK_ARG(send && recv && P && Q && es && ev && We && Wn && b && Wv && Wsv && bsv && wev &&
                 ds_out && dv_out);
-  GMP_CHECK_ARG(dspre && spre && dgate && vn && vh && dvpre && dvh && des && dev);
+  GMP_CHECK_ARG(dspre && dgate && vn && dvpre && dvh && des && dev);  // spre, vh: optional
   GMP_CHECK_ARG(al16(P) && al16(Q) && al16(es) && al16(ds_out) && al16(dv_out) && al16(dspre) &&
                 al16(spre) && al16(dgate) && al16(vn) && al16(vh) && al16(dvpre) && al16(dvh) &&
                 al16(des));

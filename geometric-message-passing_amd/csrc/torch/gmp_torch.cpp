@@ -1230,6 +1230,44 @@ std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::v
   return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
 }
 
+// the last message GVP's backward with the receivers' sum / mean backward in its loads: ds, dv
+// are the aggregation's node gradients (N, 128), (N, 16, 3); index the receiver per edge,
+// rowptr its CSR row pointer (counts for the mean)
+std::vector<Tensor> gvp_layer_bwd_agg(const Tensor& s, const Tensor& v,
+                                      const std::vector<Tensor>& W, const Tensor& ds,
+                                      const Tensor& dv, const Tensor& index,
+                                      const Tensor& rowptr, const std::string& reduce, bool relu,
+                                      bool want_spre) {
+  OpGuard g(s, "gvp_layer_bwd_agg");
+  const int64_t E = gvp_rows(s, v);
+  gvp_w_checks(W, kGvpLayerW);
+  f32(ds, "ds");
+  f32(dv, "dv");
+  const int64_t N = ds.size(0);
+  shape(ds, {N, 128}, "ds");
+  shape(dv, {N, 16, 3}, "dv");
+  i64(index, "index");
+  i64(rowptr, "rowptr");
+  shape(index, {E}, "index");
+  shape(rowptr, {N + 1}, "rowptr");
+  const int red = reduce_code(reduce);
+  TORCH_CHECK(red == GMP_REDUCE_SUM || red == GMP_REDUCE_MEAN,
+              "gmp.gvp_layer_bwd_agg: reduce must be sum or mean");
+  auto o = fopt(s);
+  Tensor ds_in = at::empty_like(s), dv_in = at::empty_like(v);
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({want_spre ? E : 0, 128}, o);
+  Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 16}, o);
+  Tensor vh = at::empty({E, 48}, o), dvpre = at::empty({E, 48}, o), dvh = at::empty({E, 48}, o);
+  check_rc(gmp_gvp_layer_bwd_agg_f32(E, N, red, index.data_ptr<int64_t>(),
+                                     rowptr.data_ptr<int64_t>(), relu ? 1 : 0, fp(s), fp(v),
+                                     fp(W[0]), fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]),
+                                     fp(ds), fp(dv), fp(ds_in), fp(dv_in), fp(dspre),
+                                     want_spre ? fp(spre) : nullptr, fp(dgate), fp(vn), fp(vh),
+                                     fp(dvpre), fp(dvh), cur_stream()),
+           "gmp_gvp_layer_bwd_agg_f32");
+  return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
+}
+
 int64_t gvp_msg0_checks(const Tensor& send, const Tensor& recv, const Tensor& P, const Tensor& Q,
                         const Tensor& es, const Tensor& ev, const std::vector<Tensor>& W) {
   i64(send, "send");
@@ -1265,7 +1303,7 @@ std::tuple<Tensor, Tensor> gvp_msg0_fwd(const Tensor& send, const Tensor& recv, 
 std::vector<Tensor> gvp_msg0_bwd(const Tensor& send, const Tensor& recv, const Tensor& P,
                                  const Tensor& Q, const Tensor& es, const Tensor& ev,
                                  const std::vector<Tensor>& W, const Tensor& ds,
-                                 const Tensor& dv) {
+                                 const Tensor& dv, bool want_factors) {
   OpGuard g(P, "gvp_msg0_bwd");
   const int64_t E = gvp_msg0_checks(send, recv, P, Q, es, ev, W);
   f32(ds, "ds");
@@ -1273,14 +1311,16 @@ std::vector<Tensor> gvp_msg0_bwd(const Tensor& send, const Tensor& recv, const T
   shape(ds, {E, 128}, "ds");
   numel(dv, E * 48, "dv");
   auto o = fopt(P);
-  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({E, 128}, o);
+  const int64_t Ef = want_factors ? E : 0;  // spre / vh rows (optional, see gmp.h)
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({Ef, 128}, o);
   Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 48}, o);
-  Tensor vh = at::empty({E, 144}, o), dvh = at::empty({E, 144}, o);
+  Tensor vh = at::empty({Ef, 144}, o), dvh = at::empty({E, 144}, o);
   Tensor dvpre = at::empty({E, 48}, o), des = at::empty({E, 32}, o), dev = at::empty({E, 3}, o);
   check_rc(gmp_gvp_msg0_bwd_f32(E, ip(send), ip(recv), fp(P), fp(Q), fp(es), fp(ev), fp(W[0]),
                                 fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]), fp(W[6]),
-                                fp(ds), fp(dv), fp(dspre), fp(spre), fp(dgate), fp(vn), fp(vh),
-                                fp(dvpre), fp(dvh), fp(des), fp(dev), cur_stream()),
+                                fp(ds), fp(dv), fp(dspre), want_factors ? fp(spre) : nullptr,
+                                fp(dgate), fp(vn), want_factors ? fp(vh) : nullptr, fp(dvpre),
+                                fp(dvh), fp(des), fp(dev), cur_stream()),
            "gmp_gvp_msg0_bwd_f32");
   return {dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev};
 }
@@ -1475,6 +1515,12 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
                                          const std::vector<Tensor>&, bool) {
   return {at::empty_like(s), at::empty_like(v)};
 }
+std::vector<Tensor> gvp_layer_bwd_agg(const Tensor& s, const Tensor& v,
+                                      const std::vector<Tensor>& W, const Tensor& ds,
+                                      const Tensor& dv, const Tensor&, const Tensor&,
+                                      const std::string&, bool relu, bool want_spre) {
+  return gvp_layer_bwd(s, v, W, ds, dv, relu, want_spre);
+}
 std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&,
                                   const Tensor&, const Tensor&, bool, bool want_spre) {
   const int64_t E = s.size(0);
@@ -1491,11 +1537,12 @@ std::tuple<Tensor, Tensor> gvp_msg0_fwd(const Tensor& send, const Tensor&, const
 }
 std::vector<Tensor> gvp_msg0_bwd(const Tensor& send, const Tensor&, const Tensor& P,
                                  const Tensor&, const Tensor&, const Tensor&,
-                                 const std::vector<Tensor>&, const Tensor&, const Tensor&) {
-  const int64_t E = send.numel();
+                                 const std::vector<Tensor>&, const Tensor&, const Tensor&,
+                                 bool want_factors) {
+  const int64_t E = send.numel(), Ef = want_factors ? E : 0;
   auto o = P.options();
-  return {at::empty({E, 128}, o), at::empty({E, 128}, o), at::empty({E, 16}, o),
-          at::empty({E, 48}, o),  at::empty({E, 144}, o), at::empty({E, 48}, o),
+  return {at::empty({E, 128}, o), at::empty({Ef, 128}, o), at::empty({E, 16}, o),
+          at::empty({E, 48}, o),  at::empty({Ef, 144}, o), at::empty({E, 48}, o),
           at::empty({E, 144}, o), at::empty({E, 32}, o),  at::empty({E, 3}, o)};
 }
 }  // namespace meta
@@ -1590,10 +1637,12 @@ TORCH_LIBRARY(gmp, m) {
   m.def("gvp_layer_bwd(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, bool relu, "
         "bool want_spre=True) -> "
         "Tensor[]");
+  m.def("gvp_layer_bwd_agg(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, Tensor index, "
+        "Tensor rowptr, str reduce, bool relu, bool want_spre=True) -> Tensor[]");
   m.def("gvp_msg0_fwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
         "Tensor[] W) -> (Tensor s_out, Tensor v_out)");
   m.def("gvp_msg0_bwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
-        "Tensor[] W, Tensor ds, Tensor dv) -> Tensor[]");
+        "Tensor[] W, Tensor ds, Tensor dv, bool want_factors=True) -> Tensor[]");
 }
 
 #define GMP_IMPL(m, ns)                                                    \
@@ -1643,6 +1692,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("edge_outer_sum_act", ns edge_outer_sum_act);                    \
   m.impl("gvp_layer_fwd", ns gvp_layer_fwd);                              \
   m.impl("gvp_layer_bwd", ns gvp_layer_bwd);                              \
+  m.impl("gvp_layer_bwd_agg", ns gvp_layer_bwd_agg);                      \
   m.impl("gvp_msg0_fwd", ns gvp_msg0_fwd);                                \
   m.impl("gvp_msg0_bwd", ns gvp_msg0_bwd);
 

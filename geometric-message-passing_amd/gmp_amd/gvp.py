@@ -233,27 +233,69 @@ class GvpLayerFn(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, ds, dv):
         s, v, *W = ctx.saved_tensors
-        E = s.shape[0]
         ds = ops._f32c(ds) if ds is not None else torch.zeros_like(s)
         dv = ops._f32c(dv) if dv is not None else torch.zeros_like(v)
-        f = dict(dtype=torch.float32, device=s.device)
         with ops._timed("gvp_layer_bwd"):
             ds_in, dv_in, dspre, _, dgate, vn, vh, dvpre, dvh = _lib.torch_ops().gvp_layer_bwd(
                 s, v, W, ds, dv, bool(ctx.relu), False)
-        # weight gradients (edge outer sums) on the side stream, deferred to the end of backward
-        with ops.side_work(dspre, s, vn, dgate, dvh, v, dvpre, vh) as sw:
-            # dWs = dspre^T [s | vn]: one pass over dspre where the split-plane kernel applies
-            dWs, dbs = torch.empty((128, 144), **f), torch.empty(128, **f)
-            ops.outer_sum_into2(dspre, s.view(E, 128), vn, dWs, dbs)
-            # dWsv = sum_e dgate (x) spre with spre = Ws [s | vn] + bs, without the (E, 128) spre
-            # rows: (sum_e dgate (x) [s | vn]) Ws^T + (sum_e dgate) (x) bs
-            Gx, dbsv = torch.empty((16, 144), **f), torch.empty(16, **f)
-            ops.outer_sum_into2(dgate, s.view(E, 128), vn, Gx, dbsv)
-            dWsv = torch.addmm(torch.outer(dbsv, W[1]), Gx, W[0].t())
-            dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
-            dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
-        grads = (dWs, dbs, dWsv, dbsv, dWh, dWv)
-        return (ds_in, dv_in) + sw.deliver(ctx.needs_input_grad, 2, W, grads) + (None,)
+        return (ds_in, dv_in) + _layer_wgrads(ctx.needs_input_grad, 2, s, v, W, dspre, dgate, vn,
+                                              vh, dvpre, dvh) + (None,)
+
+
+def _layer_wgrads(needs_input_grad, first, s, v, W, dspre, dgate, vn, vh, dvpre, dvh):
+    """Weight gradients of one GVP layer (edge outer sums) on the side stream, deferred to the
+    end of the backward pass; needs_input_grad[first + i] belongs to W[i]."""
+    E = s.shape[0]
+    f = dict(dtype=torch.float32, device=s.device)
+    with ops.side_work(dspre, s, vn, dgate, dvh, v, dvpre, vh) as sw:
+        # dWs = dspre^T [s | vn]: one pass over dspre where the split-plane kernel applies
+        dWs, dbs = torch.empty((128, 144), **f), torch.empty(128, **f)
+        ops.outer_sum_into2(dspre, s.view(E, 128), vn, dWs, dbs)
+        # dWsv = sum_e dgate (x) spre with spre = Ws [s | vn] + bs, without the (E, 128) spre
+        # rows: (sum_e dgate (x) [s | vn]) Ws^T + (sum_e dgate) (x) bs
+        Gx, dbsv = torch.empty((16, 144), **f), torch.empty(16, **f)
+        ops.outer_sum_into2(dgate, s.view(E, 128), vn, Gx, dbsv)
+        dWsv = torch.addmm(torch.outer(dbsv, W[1]), Gx, W[0].t())
+        dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
+        dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
+    grads = (dWs, dbs, dWsv, dbsv, dWh, dWv)
+    return sw.deliver(needs_input_grad, first, W, grads)
+
+
+class GvpLayerAggFn(torch.autograd.Function):
+    """The last message GVP (no scalar activation) followed by the receivers' sum / mean
+    aggregation (GVPConv.forward, gvp_layer.py:319-324): forward = gmp_gvp_layer_fwd_f32 + K3
+    (scalar and vector channels aggregated separately); backward = gmp_gvp_layer_bwd_agg_f32,
+    which gathers the aggregation's node gradient per edge in its loads instead of reading the
+    (E, 176) per-edge gradient rows K3's backward would write."""
+
+    @staticmethod
+    def forward(ctx, s, v, Ws, bs, Wsv, bsv, Wh, Wv, csr, reduce):
+        s, v = ops._f32c(s), ops._f32c(v)
+        ops._need_cuda(s, v)
+        W = [ops._f32c(t) for t in (Ws, bs, Wsv, bsv, Wh, Wv)]
+        with ops._timed("gvp_layer_fwd"):
+            s3, v3 = _lib.torch_ops().gvp_layer_fwd(s, v, W, False)
+        agg_s, _ = ops.segment_reduce(s3, csr, reduce)
+        agg_v, _ = ops.segment_reduce(v3.view(v3.shape[0], -1), csr, reduce)
+        ctx.csr, ctx.reduce = csr, reduce
+        ctx.save_for_backward(s, v, *W)
+        return agg_s, agg_v.view(-1, v3.shape[1], 3)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gs, gv):
+        s, v, *W = ctx.saved_tensors
+        csr = ctx.csr
+        n = csr.n_seg
+        gs = ops._f32c(gs) if gs is not None else torch.zeros((n, 128), device=s.device)
+        gv = ops._f32c(gv) if gv is not None else torch.zeros((n, 16, 3), device=s.device)
+        with ops._timed("gvp_layer_bwd"):
+            ds_in, dv_in, dspre, _, dgate, vn, vh, dvpre, dvh = \
+                _lib.torch_ops().gvp_layer_bwd_agg(s, v, W, gs, gv, csr.index, csr.rowptr,
+                                                   ctx.reduce, False, False)
+        return (ds_in, dv_in) + _layer_wgrads(ctx.needs_input_grad, 2, s, v, W, dspre, dgate, vn,
+                                              vh, dvpre, dvh) + (None, None)
 
 
 class GvpMsg0Fn(torch.autograd.Function):
@@ -289,18 +331,38 @@ class GvpMsg0Fn(torch.autograd.Function):
         dv = ops._f32c(dv) if dv is not None else torch.zeros((E, 16, 3), device=P.device)
         f = dict(dtype=torch.float32, device=P.device)
         with ops._timed("gvp_msg0_bwd"):
-            dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev = _lib.torch_ops().gvp_msg0_bwd(
-                send, recv, P, Q, es, ev, W, ds, dv)
-        # weight gradients (edge outer sums) on the side stream, as full-size leaf gradients
-        with ops.side_work(dspre, es, vn, dgate, spre, dvpre, vh, ev, dvh) as sw:
+            dspre, _, dgate, vn, _, dvpre, dvh, des, dev = _lib.torch_ops().gvp_msg0_bwd(
+                send, recv, P, Q, es, ev, W, ds, dv, False)
+        # weight gradients (edge outer sums) on the side stream, as full-size leaf gradients.
+        # The pre-activation rows spre and the mixed vectors vh are not written by the kernel
+        # (gmp.h gmp_gvp_msg0_bwd_f32): both are sums of per-edge terms and the gathered node
+        # projections, so their sums split into edge sums and node-level products of the
+        # sender / receiver segment sums of dgate / dvpre.
+        with ops.side_work(dspre, es, vn, dgate, dvpre, ev, dvh, P, Q) as sw:
             vi = Wv.shape[1]
+            n = P.shape[0]
             # [dWe | dWn] = dspre^T [es | vn]: one pass over dspre when the split path applies
             Cen, db = torch.empty((128, 80), **f), torch.empty(128, **f)
             ops.outer_sum_into2(dspre, es, vn, Cen, db)
             dWe, dWn = Cen[:, :32], Cen[:, 32:]
-            dWsv, dbsv = _osum(dgate, spre)
-            dWv = _diag3(_osum(dvpre, vh)[0], 16, 48)
-            M, _ = _osum(torch.nn.functional.pad(ev, (0, 13)), dvh)  # (16, 144): rows x = 0..2
+            # dWsv = dgate^T spre, spre = [es | vn] [We | Wn]^T + Pa[j] + Pb[i] + b
+            Gx, dbsv = torch.empty((16, 80), **f), torch.empty(16, **f)
+            ops.outer_sum_into2(dgate, es, vn, Gx, dbsv)
+            Sg = torch.cat([ops.segment_reduce(dgate, send_csr, "sum")[0],
+                            ops.segment_reduce(dgate, recv_csr, "sum")[0]], 0)   # (2N, 16)
+            Pab = P.view(n, 2, 128).transpose(0, 1).reshape(2 * n, 128)      # [Pa ; Pb]
+            dWsv = _osum(Sg, Pab)[0].addmm_(Gx[:, :32], W[0].t()).addmm_(Gx[:, 32:], W[1].t())
+            dWsv.add_(torch.outer(dbsv, W[2]))
+            # dWv = sum_(e,x) dvpre[e, o, x] vh[e, h, x], vh = Qa[j] + Qb[i] + wev (x) ev
+            Sv = torch.cat([ops.segment_reduce(dvpre, send_csr, "sum")[0],
+                            ops.segment_reduce(dvpre, recv_csr, "sum")[0]], 0)   # (2N, 48)
+            Qab = Q.view(n, 2, 144).transpose(0, 1).reshape(2 * n, 144)      # [Qa ; Qb]
+            dWv = _diag3(_osum(Sv, Qab)[0], 16, 48)
+            ev16 = torch.nn.functional.pad(ev, (0, 13))
+            Mu, _ = _osum(ev16, dvpre)                                       # (16, 48)
+            u = Mu[:3].reshape(3, 16, 3).diagonal(dim1=0, dim2=2).sum(-1)    # (16,)
+            dWv.add_(torch.outer(u, W[6]))
+            M, _ = _osum(ev16, dvh)  # (16, 144): rows x = 0..2
             dwev = M[:3].reshape(3, 48, 3).diagonal(dim1=0, dim2=2).sum(-1)
             gWs0 = torch.zeros_like(Ws0)
             gWs0[:, 128:160] = dWe
@@ -443,14 +505,12 @@ class GVPConv(MessagePassing):
                                  g0.wsv.weight, g0.wsv.bias, Wh0, send_csr, recv_csr, ei)
         s2, v2 = GvpLayerFn.apply(s1, v1, g1.ws.weight, g1.ws.bias, g1.wsv.weight, g1.wsv.bias,
                                   g1.wh.weight, g1.wv.weight, True)
-        s3, v3 = GvpLayerFn.apply(s2, v2, g2.ws.weight, g2.ws.bias, g2.wsv.weight, g2.wsv.bias,
-                                  g2.wh.weight, g2.wv.weight, False)
-        # aggregate the scalar and vector channels separately (no concatenated (E, 176) copy
-        # forward, no split copies of its gradient backward)
+        # the last GVP with the receivers' aggregation: scalar and vector channels aggregated
+        # separately (no concatenated (E, 176) copy), and its backward gathers the node gradient
+        # in the layer kernel's loads (no (E, 176) per-edge gradient rows)
         reduce = "sum" if self.aggr == "add" else self.aggr
-        agg_s = ops.SegmentReduceFn.apply(s3, recv_csr, reduce)
-        agg_v = ops.SegmentReduceFn.apply(v3.reshape(-1, 3 * self.vo), recv_csr, reduce)
-        return agg_s, agg_v.view(-1, self.vo, 3)
+        return GvpLayerAggFn.apply(s2, v2, g2.ws.weight, g2.ws.bias, g2.wsv.weight, g2.wsv.bias,
+                                   g2.wh.weight, g2.wv.weight, recv_csr, reduce)
 
     def forward(self, x, edge_index, edge_attr):
         x_s, x_v = x

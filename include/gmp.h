@@ -509,11 +509,32 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
                           const float* dv_out, float* ds_in, float* dv_in, float* dspre,
                           float* spre, float* dgate, float* vn, float* vh, float* dvpre,
                           float* dvh, void* stream);
+/* gmp_gvp_layer_bwd_agg_f32: the same backward for the last message GVP of GVPConv, whose
+ * per-edge outputs feed the receivers' aggregation (gvp_layer.py:319-324, aggr "add" / "mean"
+ * = reduce GMP_REDUCE_SUM / GMP_REDUCE_MEAN): ds_node (n_nodes, 128), dv_node (n_nodes, 16, 3)
+ * are the aggregation's node gradients, gathered per edge at index[e] (the receiver; x 1 /
+ * max(count, 1) for the mean with count = rowptr[n + 1] - rowptr[n] of the receiver CSR,
+ * exactly K3's mean backward; an index outside [0, n_nodes) contributes zeros) -- the (E, 176)
+ * per-edge gradient of gmp_segment_reduce_bwd_f32 is never materialised. */
+int gmp_gvp_layer_bwd_agg_f32(int64_t n_edges, int64_t n_nodes, int reduce, const int64_t* index,
+                              const int64_t* rowptr, int relu, const float* s_in,
+                              const float* v_in, const float* Ws, const float* bs,
+                              const float* Wsv, const float* bsv, const float* Wh,
+                              const float* Wv, const float* ds_node, const float* dv_node,
+                              float* ds_in, float* dv_in, float* dspre, float* spre,
+                              float* dgate, float* vn, float* vh, float* dvpre, float* dvh,
+                              void* stream);
 int gmp_gvp_msg0_fwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
                          const float* P, const float* Q, const float* es, const float* ev,
                          const float* We, const float* Wn, const float* b, const float* Wv,
                          const float* Wsv, const float* bsv, const float* wev, float* s_out,
                          float* v_out, void* stream);
+/* gmp_gvp_msg0_bwd_f32: spre (E, 128) and vh (E, 144), read only by the dWsv / dWv weight sums,
+ * may be NULL (r05): the caller then forms those sums from the node projections,
+ *   dWsv = (dgate^T [es | vn]) [We | Wn]^T + (S_j dgate)^T Pa + (S_i dgate)^T Pb + (1^T dgate) b,
+ *   dWv[o, h] = sum_(n,x) (S_j dvpre)[n, o, x] Qa[n, h, x] + (S_i dvpre) .. Qb + wev[h] u[o]
+ * (S_j, S_i the sender / receiver segment sums, u[o] = sum_(e,x) dvpre[e, o, x] ev[e, x]):
+ * 2.2 KB per edge of HBM traffic less per layer. */
 int gmp_gvp_msg0_bwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
                          const float* P, const float* Q, const float* es, const float* ev,
                          const float* We, const float* Wn, const float* b, const float* Wv,

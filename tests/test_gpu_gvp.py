@@ -298,3 +298,42 @@ def test_xyz_norm_vs_torch(rows, h):
         return
     assert (y.double().cpu() - yr.detach()).abs().max().item() <= 1e-6 * yr.abs().max().item()
     assert (va.grad.double().cpu() - vb.grad).abs().max().item() <= 1e-6 * vb.grad.abs().max().item() + 1e-7
+
+
+@pytest.mark.parametrize("reduce", ["mean", "sum"])
+def test_gvp_layer_agg_backward_bitwise(reduce):
+    """GvpLayerAggFn (the last message GVP with the receivers' aggregation; backward through
+    gmp_gvp_layer_bwd_agg_f32, the node gradient gathered in the layer kernel's loads) against
+    the unfused pair GvpLayerFn + K3 segment_reduce (its backward writes the (E, 176) per-edge
+    gradient rows): forward, input and weight gradients bitwise equal -- the same products in
+    the same order.  Receivers with in-degree 0 and a shuffled edge order."""
+    import gmp_amd.gvp as g
+    from gmp_amd import ops
+    from gmp_amd.graph import radius_graph
+    torch.manual_seed(7)
+    gr = radius_graph(num_nodes=600, target_edges=9000, r=2.0, seed=4, tol=0.2, shuffle=True)
+    n, E = gr.num_nodes + 5, gr.edge_index.shape[1]  # 5 receivers without edges
+    recv = gr.edge_index[1].to(DEV)
+    csr = ops.get_csr(recv, n)
+    lay = g.GVP((128, 16), (128, 16), activations=(None, None)).to(DEV)
+    W = (lay.ws.weight, lay.ws.bias, lay.wsv.weight, lay.wsv.bias, lay.wh.weight, lay.wv.weight)
+    s = torch.randn(E, 128, device=DEV)
+    v = torch.randn(E, 16, 3, device=DEV)
+    gs = torch.randn(n, 128, device=DEV)
+    gv = torch.randn(n, 16, 3, device=DEV)
+    outs = []
+    for fused in (True, False):
+        for p in W:
+            p.grad = None
+        sd, vd = s.clone().requires_grad_(True), v.clone().requires_grad_(True)
+        if fused:
+            a_s, a_v = g.GvpLayerAggFn.apply(sd, vd, *W, csr, reduce)
+        else:
+            s3, v3 = g.GvpLayerFn.apply(sd, vd, *W, False)
+            a_s = ops.SegmentReduceFn.apply(s3, csr, reduce)
+            a_v = ops.SegmentReduceFn.apply(v3.reshape(E, 48), csr, reduce).view(n, 16, 3)
+        ((a_s * gs).sum() + (a_v * gv).sum()).backward()
+        torch.cuda.synchronize()
+        outs.append([a_s.detach(), a_v.detach(), sd.grad, vd.grad] + [p.grad.clone() for p in W])
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), i
