@@ -26,7 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import _ref_stubs  # noqa: E402
 
-REF = os.environ.get("GMP_REFERENCE", "/root/reference")
+REF = os.environ.get("REFERENCE_ROOT", "/root/reference")
 
 
 def radius_graph_np(pos, r):
