@@ -607,6 +607,142 @@ __global__ __launch_bounds__(kGT) void gvp_layer_fwd_x3_kernel(int64_t E, const 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// r05: the last message GVP fused with the receivers' sum / mean (GVPConv, gvp_layer.py:319-324):
+// no (E, S + 3V) per-edge output rows.  Edges are walked in receiver-sorted order (the CSR of
+// the receivers: perm = original edge of sorted position k, skey = its receiver, rowptr); each
+// wave owns the in-edges of a contiguous receiver range (edge-balanced, as K4), reads its rows
+// through perm, runs the layer in registers and sums each receiver's rows by an in-wave
+// segmented scan over the chunk's 16 edge lanes (DPP row_shr) with the open segment carried to
+// the next chunk through LDS; the last edge of a segment stores the receiver's row (x 1 / count
+// for the mean).  Deterministic (fixed order; a tree order inside a chunk, so not bitwise K3's
+// sequential sum).  Receivers without in-edges get zero rows.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int OFF, int T>
+__device__ __forceinline__ void seg_scan_level(f32x4 (&x)[T], int i, int head) {
+  const bool take = (i - OFF) >= head;
+#pragma unroll
+  for (int p = 0; p < T; ++p)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float u = dpp_mov<0x110 + OFF>(x[p][c]);  // row_shr:OFF = lane i - OFF
+      if (take) x[p][c] += u;
+    }
+}
+template <int T>
+__device__ __forceinline__ void seg_scan(f32x4 (&x)[T], int i, int head) {
+  seg_scan_level<1>(x, i, head);
+  seg_scan_level<2>(x, i, head);
+  seg_scan_level<4>(x, i, head);
+  seg_scan_level<8>(x, i, head);
+}
+constexpr int kAggCarry = S / 4 + 3 * 4;  // floats per (wave, lane group): scalar + 3 xyz slots
+constexpr int kAggSmem = kLayerSmemX3 + (kGT / 64) * 4 * kAggCarry;
+
+// first receiver of wave w under an edge-balanced, receiver-aligned split (K4's node_begin)
+__device__ __forceinline__ int64_t agg_node_begin(const int64_t* __restrict__ rowptr,
+                                                  int64_t n_nodes, int64_t n_edges, int64_t w,
+                                                  int64_t n_waves) {
+  if (w >= n_waves) return n_nodes;
+  if (w <= 0) return 0;
+  const int64_t target = (n_edges * w) / n_waves;
+  int64_t lo = 0, hi = n_nodes;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <bool MEAN>
+__global__ __launch_bounds__(kGT) void gvp_layer_fwd_agg_kernel(
+    int64_t E, int64_t N, const float* __restrict__ s_in, const float* __restrict__ v_in,
+    LayerW P, const int64_t* __restrict__ perm, const int64_t* __restrict__ skey,
+    const int64_t* __restrict__ rowptr, float* __restrict__ s_agg, float* __restrict__ v_agg) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  layer_to_lds_x3<false>(sm, P);
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* wcarry = sm + kLayerSmemX3 + wid * 4 * kAggCarry;
+  for (int k = lane; k < 4 * kAggCarry; k += 64) wcarry[k] = 0.f;
+  float* cbuf = wcarry + g * kAggCarry;
+  __syncthreads();
+  const int64_t n_waves = (int64_t)gridDim.x * (kGT / 64);
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + wid;
+  const int64_t nb = agg_node_begin(rowptr, N, E, wave, n_waves);
+  const int64_t ne = agg_node_begin(rowptr, N, E, wave + 1, n_waves);
+  const int64_t e_lo = (nb < ne) ? rowptr[nb] : 0, e_hi = (nb < ne) ? rowptr[ne] : 0;
+  // receivers of this wave's range without in-edges: zero rows (no other writer)
+  for (int64_t n = nb + lane; n < ne; n += 64) {
+    if (rowptr[n] == rowptr[n + 1]) {
+      for (int c = 0; c < S; c += 4)
+        *reinterpret_cast<f32x4*>(s_agg + n * S + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < 3 * V; c += 4)
+        *reinterpret_cast<f32x4*>(v_agg + n * (3 * V) + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  int64_t carry_node = -1;
+  for (int64_t base = e_lo; base < e_hi; base += 16) {
+    const int64_t k = base + i;
+    const bool valid = k < e_hi;
+    const int64_t kc = valid ? k : e_hi - 1;  // clamp loads; stores are masked
+    const int64_t e = perm ? perm[kc] : kc;
+    int64_t n = skey[kc];
+    n = (n >= 0 && n < N) ? n : 0;
+    const int64_t seg0 = rowptr[n], seg1 = rowptr[n + 1];
+    f32x4 s[S / 16], v[3][1];
+    ld_row<S / 16>(s, s_in + e * S, g);
+    ld_vrow<1>(v, v_in + e * (3 * V), g);
+    LayerFwd F;
+    layer_forward_x3<false>(sm, s, v, F, lane, i, g);
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F.vpre[x][0][q] *= F.sg[0][q];
+    // open segment carried from the previous chunk (lane 0 of the group only)
+    const float tf = (i == 0 && valid && n == carry_node) ? 1.f : 0.f;
+#pragma unroll
+    for (int p = 0; p < S / 16; ++p) {
+      const f32x4 c = *reinterpret_cast<const f32x4*>(cbuf + 4 * p);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F.spre[p][q] = __builtin_fmaf(c[q], tf, F.spre[p][q]);
+    }
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      const f32x4 c = *reinterpret_cast<const f32x4*>(cbuf + S / 4 + 4 * x);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F.vpre[x][0][q] = __builtin_fmaf(c[q], tf, F.vpre[x][0][q]);
+    }
+    const int head = valid ? (int)((seg0 > base) ? (seg0 - base) : 0) : i;
+    seg_scan<S / 16>(F.spre, i, head);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) seg_scan<1>(F.vpre[x], i, head);
+    const bool is_end = valid && (k == seg1 - 1);
+    if (i == 15) {  // the (possibly open) segment of lane 15: the next chunk's carry
+#pragma unroll
+      for (int p = 0; p < S / 16; ++p) *reinterpret_cast<f32x4*>(cbuf + 4 * p) = F.spre[p];
+#pragma unroll
+      for (int x = 0; x < 3; ++x) *reinterpret_cast<f32x4*>(cbuf + S / 4 + 4 * x) = F.vpre[x][0];
+    }
+    if (is_end) {
+      if (MEAN) {
+        const float sc = 1.f / (float)(seg1 - seg0);
+#pragma unroll
+        for (int p = 0; p < S / 16; ++p) F.spre[p] *= sc;
+#pragma unroll
+        for (int x = 0; x < 3; ++x) F.vpre[x][0] *= sc;
+      }
+      st_row<S / 16>(s_agg + n * S, F.spre, g);
+      st_vrow<1>(v_agg + n * (3 * V), F.vpre, g);
+    }
+    carry_node = __builtin_amdgcn_readlane((int)n, 15);
+  }
+}
+
 // Upstream gradient of the layer's per-edge outputs.  AGG = 0: per-edge rows ds_out (E, S),
 // dv_out (E, 3V).  AGG = 1 / 2: the layer feeds a sum / mean aggregation at the receivers
 // (GVPConv, gvp_layer.py:319-324 with aggr "add" / "mean"): the rows are the aggregation's node
@@ -695,7 +831,7 @@ __global__ __launch_bounds__(kGT) void gvp_layer_bwd_x3_kernel(int64_t E, const 
       if (O.spre) st_row<S / 16>(O.spre + k.e * S, F.spre, g);
       st_row<1>(O.dgate + k.e * V, dgate, g);
       st_row<1>(O.vn + k.e * V, F.vn, g);
-      st_vrow<1>(O.vh + k.e * (3 * V), F.vh, g);
+      if (O.vh) st_vrow<1>(O.vh + k.e * (3 * V), F.vh, g);
       st_vrow<1>(O.dvpre + k.e * (3 * V), dv, g);
     }
     // ds_in = Ws_s^T dspre (image rows k) ; dvn = Ws_v^T dspre (f32)
@@ -781,7 +917,7 @@ int layer_bwd(int64_t n_edges, int relu, int agg, const AggGrad& A, const float*
   GMP_CHECK_ARG(n_edges >= 0);
   if (n_edges == 0) return GMP_OK;
   GMP_CHECK_ARG(s_in && v_in && Ws && bs && Wsv && bsv && Wh && Wv && ds_out && dv_out);
-  GMP_CHECK_ARG(ds_in && dv_in && dspre && dgate && vn && vh && dvpre && dvh);
+  GMP_CHECK_ARG(ds_in && dv_in && dspre && dgate && vn && dvpre && dvh);  // spre, vh: optional
   GMP_CHECK_ARG(al16(s_in) && al16(v_in) && al16(ds_out) && al16(dv_out) && al16(ds_in) &&
                 al16(dv_in) && al16(dspre) && al16(spre) && al16(dgate) && al16(vn) &&
                 al16(vh) && al16(dvpre) && al16(dvh));
@@ -814,6 +950,33 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   return layer_bwd(n_edges, relu, 0, AggGrad{nullptr, nullptr, 0}, s_in, v_in, Ws, bs, Wsv, bsv,
                    Wh, Wv, ds_out, dv_out, ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh,
                    stream);
+}
+
+int gmp_gvp_layer_fwd_agg_f32(int64_t n_edges, int64_t n_nodes, int reduce, const int64_t* perm,
+                              const int64_t* skey, const int64_t* rowptr, const float* s_in,
+                              const float* v_in, const float* Ws, const float* bs,
+                              const float* Wsv, const float* bsv, const float* Wh,
+                              const float* Wv, float* s_agg, float* v_agg, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && n_edges < (1LL << 31) && n_nodes < (1LL << 31));
+  GMP_CHECK_ARG(reduce == GMP_REDUCE_SUM || reduce == GMP_REDUCE_MEAN);
+  if (n_nodes == 0) return GMP_OK;
+  GMP_CHECK_ARG(rowptr && s_agg && v_agg && al16(s_agg) && al16(v_agg));
+  GMP_CHECK_ARG(n_edges == 0 || (skey && s_in && v_in && al16(s_in) && al16(v_in) && Ws && bs &&
+                                 Wsv && bsv && Wh && Wv));
+  const LayerW P{Ws, bs, Wsv, bsv, Wh, Wv};
+  // enough waves for the chip, but whole receiver ranges of >= ~4 chunks each
+  int64_t G = (int64_t)device_cu_count();
+  const int64_t cap = ceil_div(n_edges, (int64_t)(kGT / 64) * 64);
+  if (G > cap) G = cap;
+  if (G < 1) G = 1;
+  hipStream_t s = as_stream(stream);
+  const size_t smem = kAggSmem * sizeof(float);
+  auto k = reduce == GMP_REDUCE_MEAN ? gvp_layer_fwd_agg_kernel<true> : gvp_layer_fwd_agg_kernel<false>;
+  int rc;
+  if ((rc = set_smem(k, smem))) return rc;
+  k<<<(unsigned)G, kGT, smem, s>>>(n_edges, n_nodes, s_in, v_in, P, perm, skey, rowptr, s_agg,
+                                    v_agg);
+  return launch_status();
 }
 
 int gmp_gvp_layer_bwd_agg_f32(int64_t n_edges, int64_t n_nodes, int reduce, const int64_t* index,

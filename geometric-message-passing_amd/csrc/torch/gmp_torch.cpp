@@ -1209,7 +1209,7 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
 }
 
 std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>& W,
-                                  const Tensor& ds, const Tensor& dv, bool relu, bool want_spre) {
+                                  const Tensor& ds, const Tensor& dv, bool relu, bool want_factors) {
   OpGuard g(s, "gvp_layer_bwd");
   const int64_t E = gvp_rows(s, v);
   gvp_w_checks(W, kGvpLayerW);
@@ -1219,15 +1219,48 @@ std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::v
   shape(dv, v.sizes(), "dv");
   auto o = fopt(s);
   Tensor ds_in = at::empty_like(s), dv_in = at::empty_like(v);
-  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({want_spre ? E : 0, 128}, o);
+  // spre, vh: only when the caller forms dWsv / dWv from them (want_factors; see gmp.h)
+  const int64_t Ef = want_factors ? E : 0;
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({Ef, 128}, o);
   Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 16}, o);
-  Tensor vh = at::empty({E, 48}, o), dvpre = at::empty({E, 48}, o), dvh = at::empty({E, 48}, o);
+  Tensor vh = at::empty({Ef, 48}, o), dvpre = at::empty({E, 48}, o), dvh = at::empty({E, 48}, o);
   check_rc(gmp_gvp_layer_bwd_f32(E, relu ? 1 : 0, fp(s), fp(v), fp(W[0]), fp(W[1]), fp(W[2]),
                                  fp(W[3]), fp(W[4]), fp(W[5]), fp(ds), fp(dv), fp(ds_in),
-                                 fp(dv_in), fp(dspre), want_spre ? fp(spre) : nullptr, fp(dgate),
-                                 fp(vn), fp(vh), fp(dvpre), fp(dvh), cur_stream()),
+                                 fp(dv_in), fp(dspre), want_factors ? fp(spre) : nullptr, fp(dgate),
+                                 fp(vn), want_factors ? fp(vh) : nullptr, fp(dvpre), fp(dvh), cur_stream()),
            "gmp_gvp_layer_bwd_f32");
   return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
+}
+
+// the last message GVP fused with the receivers' sum / mean: (N, 128), (N, 16, 3) node rows
+std::tuple<Tensor, Tensor> gvp_layer_fwd_agg(const Tensor& s, const Tensor& v,
+                                             const std::vector<Tensor>& W,
+                                             const optional<Tensor>& perm, const Tensor& skey,
+                                             const Tensor& rowptr, int64_t n_nodes,
+                                             const std::string& reduce) {
+  OpGuard g(s, "gvp_layer_fwd_agg");
+  const int64_t E = gvp_rows(s, v);
+  gvp_w_checks(W, kGvpLayerW);
+  i64(skey, "skey");
+  i64(rowptr, "rowptr");
+  shape(skey, {E}, "skey");
+  shape(rowptr, {n_nodes + 1}, "rowptr");
+  if (perm.has_value() && perm->defined()) {
+    i64(*perm, "perm");
+    shape(*perm, {E}, "perm");
+  }
+  const int red = reduce_code(reduce);
+  TORCH_CHECK(red == GMP_REDUCE_SUM || red == GMP_REDUCE_MEAN,
+              "gmp.gvp_layer_fwd_agg: reduce must be sum or mean");
+  auto o = fopt(s);
+  Tensor sa = at::empty({n_nodes, 128}, o), va = at::empty({n_nodes, 16, 3}, o);
+  const bool hp = perm.has_value() && perm->defined();
+  check_rc(gmp_gvp_layer_fwd_agg_f32(E, n_nodes, red, hp ? perm->data_ptr<int64_t>() : nullptr,
+                                     skey.data_ptr<int64_t>(), rowptr.data_ptr<int64_t>(), fp(s),
+                                     fp(v), fp(W[0]), fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]),
+                                     fp(W[5]), fp(sa), fp(va), cur_stream()),
+           "gmp_gvp_layer_fwd_agg_f32");
+  return {sa, va};
 }
 
 // the last message GVP's backward with the receivers' sum / mean backward in its loads: ds, dv
@@ -1237,7 +1270,7 @@ std::vector<Tensor> gvp_layer_bwd_agg(const Tensor& s, const Tensor& v,
                                       const std::vector<Tensor>& W, const Tensor& ds,
                                       const Tensor& dv, const Tensor& index,
                                       const Tensor& rowptr, const std::string& reduce, bool relu,
-                                      bool want_spre) {
+                                      bool want_factors) {
   OpGuard g(s, "gvp_layer_bwd_agg");
   const int64_t E = gvp_rows(s, v);
   gvp_w_checks(W, kGvpLayerW);
@@ -1255,14 +1288,17 @@ std::vector<Tensor> gvp_layer_bwd_agg(const Tensor& s, const Tensor& v,
               "gmp.gvp_layer_bwd_agg: reduce must be sum or mean");
   auto o = fopt(s);
   Tensor ds_in = at::empty_like(s), dv_in = at::empty_like(v);
-  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({want_spre ? E : 0, 128}, o);
+  // spre, vh: only when the caller forms dWsv / dWv from them (want_factors; see gmp.h)
+  const int64_t Ef = want_factors ? E : 0;
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({Ef, 128}, o);
   Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 16}, o);
-  Tensor vh = at::empty({E, 48}, o), dvpre = at::empty({E, 48}, o), dvh = at::empty({E, 48}, o);
+  Tensor vh = at::empty({Ef, 48}, o), dvpre = at::empty({E, 48}, o), dvh = at::empty({E, 48}, o);
   check_rc(gmp_gvp_layer_bwd_agg_f32(E, N, red, index.data_ptr<int64_t>(),
                                      rowptr.data_ptr<int64_t>(), relu ? 1 : 0, fp(s), fp(v),
                                      fp(W[0]), fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]),
                                      fp(ds), fp(dv), fp(ds_in), fp(dv_in), fp(dspre),
-                                     want_spre ? fp(spre) : nullptr, fp(dgate), fp(vn), fp(vh),
+                                     want_factors ? fp(spre) : nullptr, fp(dgate), fp(vn),
+                                     want_factors ? fp(vh) : nullptr,
                                      fp(dvpre), fp(dvh), cur_stream()),
            "gmp_gvp_layer_bwd_agg_f32");
   return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
@@ -1515,19 +1551,26 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
                                          const std::vector<Tensor>&, bool) {
   return {at::empty_like(s), at::empty_like(v)};
 }
+std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&,
+                                  const Tensor&, const Tensor&, bool, bool want_factors) {
+  const int64_t E = s.size(0);
+  auto o = s.options();
+  const int64_t Ef = want_factors ? E : 0;
+  return {at::empty_like(s),      at::empty_like(v),     at::empty({E, 128}, o),
+          at::empty({Ef, 128}, o), at::empty({E, 16}, o), at::empty({E, 16}, o),
+          at::empty({Ef, 48}, o),  at::empty({E, 48}, o), at::empty({E, 48}, o)};
+}
 std::vector<Tensor> gvp_layer_bwd_agg(const Tensor& s, const Tensor& v,
                                       const std::vector<Tensor>& W, const Tensor& ds,
                                       const Tensor& dv, const Tensor&, const Tensor&,
-                                      const std::string&, bool relu, bool want_spre) {
-  return gvp_layer_bwd(s, v, W, ds, dv, relu, want_spre);
+                                      const std::string&, bool relu, bool want_factors) {
+  return meta::gvp_layer_bwd(s, v, W, ds, dv, relu, want_factors);
 }
-std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&,
-                                  const Tensor&, const Tensor&, bool, bool want_spre) {
-  const int64_t E = s.size(0);
-  auto o = s.options();
-  return {at::empty_like(s),      at::empty_like(v),     at::empty({E, 128}, o),
-          at::empty({want_spre ? E : 0, 128}, o), at::empty({E, 16}, o), at::empty({E, 16}, o),
-          at::empty({E, 48}, o),  at::empty({E, 48}, o), at::empty({E, 48}, o)};
+std::tuple<Tensor, Tensor> gvp_layer_fwd_agg(const Tensor& s, const Tensor&,
+                                             const std::vector<Tensor>&, const optional<Tensor>&,
+                                             const Tensor&, const Tensor&, int64_t n_nodes,
+                                             const std::string&) {
+  return {at::empty({n_nodes, 128}, s.options()), at::empty({n_nodes, 16, 3}, s.options())};
 }
 std::tuple<Tensor, Tensor> gvp_msg0_fwd(const Tensor& send, const Tensor&, const Tensor& P,
                                         const Tensor&, const Tensor&, const Tensor&,
@@ -1635,10 +1678,12 @@ TORCH_LIBRARY(gmp, m) {
   m.def("gvp_layer_fwd(Tensor s, Tensor v, Tensor[] W, bool relu) -> (Tensor s_out, "
         "Tensor v_out)");
   m.def("gvp_layer_bwd(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, bool relu, "
-        "bool want_spre=True) -> "
+        "bool want_factors=True) -> "
         "Tensor[]");
+  m.def("gvp_layer_fwd_agg(Tensor s, Tensor v, Tensor[] W, Tensor? perm, Tensor skey, "
+        "Tensor rowptr, int n_nodes, str reduce) -> (Tensor s_agg, Tensor v_agg)");
   m.def("gvp_layer_bwd_agg(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, Tensor index, "
-        "Tensor rowptr, str reduce, bool relu, bool want_spre=True) -> Tensor[]");
+        "Tensor rowptr, str reduce, bool relu, bool want_factors=True) -> Tensor[]");
   m.def("gvp_msg0_fwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
         "Tensor[] W) -> (Tensor s_out, Tensor v_out)");
   m.def("gvp_msg0_bwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
@@ -1693,6 +1738,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("gvp_layer_fwd", ns gvp_layer_fwd);                              \
   m.impl("gvp_layer_bwd", ns gvp_layer_bwd);                              \
   m.impl("gvp_layer_bwd_agg", ns gvp_layer_bwd_agg);                      \
+  m.impl("gvp_layer_fwd_agg", ns gvp_layer_fwd_agg);                      \
   m.impl("gvp_msg0_fwd", ns gvp_msg0_fwd);                                \
   m.impl("gvp_msg0_bwd", ns gvp_msg0_bwd);
 

@@ -247,7 +247,7 @@ def _layer_wgrads(needs_input_grad, first, s, v, W, dspre, dgate, vn, vh, dvpre,
     end of the backward pass; needs_input_grad[first + i] belongs to W[i]."""
     E = s.shape[0]
     f = dict(dtype=torch.float32, device=s.device)
-    with ops.side_work(dspre, s, vn, dgate, dvh, v, dvpre, vh) as sw:
+    with ops.side_work(dspre, s, vn, dgate, dvh, v, dvpre) as sw:
         # dWs = dspre^T [s | vn]: one pass over dspre where the split-plane kernel applies
         dWs, dbs = torch.empty((128, 144), **f), torch.empty(128, **f)
         ops.outer_sum_into2(dspre, s.view(E, 128), vn, dWs, dbs)
@@ -257,17 +257,20 @@ def _layer_wgrads(needs_input_grad, first, s, v, W, dspre, dgate, vn, vh, dvpre,
         ops.outer_sum_into2(dgate, s.view(E, 128), vn, Gx, dbsv)
         dWsv = torch.addmm(torch.outer(dbsv, W[1]), Gx, W[0].t())
         dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
-        dWv = _diag3(_osum(dvpre, vh)[0], 16, 16)
+        # dWv = sum_(e,x) dvpre[e, o, x] vh[e, h, x] with vh = Wh v: (sum dvpre (x) v) Wh^T, so
+        # the kernel does not write the (E, 48) vh rows (gmp.h gmp_gvp_layer_bwd_f32)
+        dWv = _diag3(_osum(dvpre, v.reshape(E, 48))[0], 16, 16).mm(W[4].t())
     grads = (dWs, dbs, dWsv, dbsv, dWh, dWv)
     return sw.deliver(needs_input_grad, first, W, grads)
 
 
 class GvpLayerAggFn(torch.autograd.Function):
     """The last message GVP (no scalar activation) followed by the receivers' sum / mean
-    aggregation (GVPConv.forward, gvp_layer.py:319-324): forward = gmp_gvp_layer_fwd_f32 + K3
-    (scalar and vector channels aggregated separately); backward = gmp_gvp_layer_bwd_agg_f32,
-    which gathers the aggregation's node gradient per edge in its loads instead of reading the
-    (E, 176) per-edge gradient rows K3's backward would write."""
+    aggregation (GVPConv.forward, gvp_layer.py:319-324), neither direction materialising the
+    (E, 176) per-edge rows: forward = gmp_gvp_layer_fwd_agg_f32 (the layer over the
+    receiver-sorted edges with an in-wave segmented sum per receiver), backward =
+    gmp_gvp_layer_bwd_agg_f32 (the aggregation's node gradient gathered per edge in the layer
+    kernel's loads)."""
 
     @staticmethod
     def forward(ctx, s, v, Ws, bs, Wsv, bsv, Wh, Wv, csr, reduce):
@@ -275,12 +278,11 @@ class GvpLayerAggFn(torch.autograd.Function):
         ops._need_cuda(s, v)
         W = [ops._f32c(t) for t in (Ws, bs, Wsv, bsv, Wh, Wv)]
         with ops._timed("gvp_layer_fwd"):
-            s3, v3 = _lib.torch_ops().gvp_layer_fwd(s, v, W, False)
-        agg_s, _ = ops.segment_reduce(s3, csr, reduce)
-        agg_v, _ = ops.segment_reduce(v3.view(v3.shape[0], -1), csr, reduce)
+            agg_s, agg_v = _lib.torch_ops().gvp_layer_fwd_agg(s, v, W, csr.perm, csr.sorted,
+                                                               csr.rowptr, csr.n_seg, reduce)
         ctx.csr, ctx.reduce = csr, reduce
         ctx.save_for_backward(s, v, *W)
-        return agg_s, agg_v.view(-1, v3.shape[1], 3)
+        return agg_s, agg_v
 
     @staticmethod
     @once_differentiable

@@ -502,13 +502,26 @@ int gmp_gvp_layer_fwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
                           void* stream);
 /* gmp_gvp_layer_bwd_f32: spre (the pre-activation scalar rows, only the dWsv weight sum reads
  * them) may be NULL -- the caller then forms dWsv = (sum_e dgate_e (x) [s_e | vn_e]) Ws^T +
- * (sum_e dgate_e) (x) bs without them (r04: 1 KB per edge of HBM traffic less). */
+ * (sum_e dgate_e) (x) bs without them (r04: 1 KB per edge of HBM traffic less); vh (read only
+ * by dWv) may be NULL too -- dWv = (sum_(e,x) dvpre (x) v_in) Wh^T (r05: 0.4 KB per edge). */
 int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const float* v_in,
                           const float* Ws, const float* bs, const float* Wsv, const float* bsv,
                           const float* Wh, const float* Wv, const float* ds_out,
                           const float* dv_out, float* ds_in, float* dv_in, float* dspre,
                           float* spre, float* dgate, float* vn, float* vh, float* dvpre,
                           float* dvh, void* stream);
+/* gmp_gvp_layer_fwd_agg_f32: the last message GVP of GVPConv fused with the receivers' sum /
+ * mean (gvp_layer.py:319-324, aggr "add" / "mean" = reduce GMP_REDUCE_SUM / GMP_REDUCE_MEAN):
+ * s_agg (n_nodes, 128), v_agg (n_nodes, 16, 3) directly, no per-edge output rows.  The receiver
+ * CSR: rowptr (n_nodes + 1), skey (E) the receiver of sorted position k, perm (E) its original
+ * edge (NULL: the edges are already receiver-sorted); s_in / v_in in original edge order.  Each
+ * receiver's rows are summed in sorted order by an in-wave segmented scan (deterministic;
+ * within fp32 rounding of K3's sequential sum); receivers without in-edges get zeros. */
+int gmp_gvp_layer_fwd_agg_f32(int64_t n_edges, int64_t n_nodes, int reduce, const int64_t* perm,
+                              const int64_t* skey, const int64_t* rowptr, const float* s_in,
+                              const float* v_in, const float* Ws, const float* bs,
+                              const float* Wsv, const float* bsv, const float* Wh,
+                              const float* Wv, float* s_agg, float* v_agg, void* stream);
 /* gmp_gvp_layer_bwd_agg_f32: the same backward for the last message GVP of GVPConv, whose
  * per-edge outputs feed the receivers' aggregation (gvp_layer.py:319-324, aggr "add" / "mean"
  * = reduce GMP_REDUCE_SUM / GMP_REDUCE_MEAN): ds_node (n_nodes, 128), dv_node (n_nodes, 16, 3)
