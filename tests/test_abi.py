@@ -59,7 +59,9 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
                  "tp_edge_z", "tp_edge_z_bwd", "tp_node_outer", "tp_node_apply", "tp_gemm_x3",
                  "tp_gemm_x3_widen", "outer_sum_cols", "edge_outer_sum_ex",
                  "edge_outer_sum_ex2", "edge_outer_sum_act", "gvp_layer_fwd", "gvp_layer_bwd",
-                 "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd"):
+                 "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd",
+                 "gvp_layer_fwd_agg", "gvp_layer_bwd_agg", "symmetric_contraction_fwd",
+                 "symmetric_contraction_bwd"):
         assert hasattr(tops, name), name
     with pytest.raises(RuntimeError, match="HIP device"):
         tops.gather_rows(torch.zeros(4, 4), torch.zeros(2, dtype=torch.long))
@@ -72,6 +74,20 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
     assert [tuple(t.shape) for t in out] == [(1000, 128), (1000, 16, 3), (1000, 128),
                                             (1000, 128), (1000, 16), (1000, 16), (1000, 48),
                                             (1000, 48), (1000, 48)]
+    # without the optional factor rows (spre, vh), and the aggregation-fused forms (r05)
+    out = tops.gvp_layer_bwd(s, v, W, s, v, True, False)
+    assert tuple(out[3].shape) == (0, 128) and tuple(out[6].shape) == (0, 48)
+    i64 = dict(dtype=torch.long, device="meta")
+    sa, va = tops.gvp_layer_fwd_agg(s, v, W, torch.empty(1000, **i64), torch.empty(1000, **i64),
+                                    torch.empty(301, **i64), 300, "mean")
+    assert tuple(sa.shape) == (300, 128) and tuple(va.shape) == (300, 16, 3)
+    # K8 on a term plan: out (N, rows C), partials (groups, T, C)
+    x = torch.empty(50, 8, 9, device="meta")
+    plan = torch.empty(3 * 9 + 1 + 40, dtype=torch.int32, device="meta")
+    coef = torch.empty(40, 8, device="meta")
+    assert tuple(tops.symmetric_contraction_fwd(x, plan, 9, coef).shape) == (50, 72)
+    dx, part = tops.symmetric_contraction_bwd(x, plan, 9, coef, torch.empty(50, 72, device="meta"))
+    assert tuple(dx.shape) == (50, 8, 9) and tuple(part.shape)[1:] == (40, 8)
     z = tops.tp_edge_z([11, 1152, 1152, 9, 180224, 4480, 3] + [0] * 18,
                        torch.empty(11 * 64, dtype=torch.uint8, device="meta"),
                        torch.empty(10, device="meta"), torch.empty(50, 1152, device="meta"),
