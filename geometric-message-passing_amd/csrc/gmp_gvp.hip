@@ -285,6 +285,95 @@ struct Msg0Grads {
   float *dspre, *spre, *dgate, *vn, *vh, *dvpre, *dvh, *des, *dev;
 };
 
+// Backward of the first message GVP for this lane's edge e (gathers at j = send[e], r = recv[e]):
+// the per-edge outputs (stored here, at row e) and, returned for callers that reduce them over
+// the receivers, the rows dspre (ds), dgate, dvpre (dv) and dvh.
+struct Msg0Bwd {
+  f32x4 ds[S / 16], dgate[1], dv[3][1], dvh[3][3];
+};
+__device__ __forceinline__ void msg0_bwd_edge(const float* sm, int64_t e, bool valid, int64_t j,
+                                              int64_t r, const float* __restrict__ Pn,
+                                              const float* __restrict__ Qn,
+                                              const float* __restrict__ es,
+                                              const float* __restrict__ ev,
+                                              const float* __restrict__ ds_out,
+                                              const float* __restrict__ dv_out,
+                                              const Msg0Grads& O, Msg0Bwd& B, int i, int g) {
+  const float* sWe = sm;
+  const float* sWn = sWe + S * LD32;
+  const float* sWv = sWn + S * LD48;
+  const float* sWsv = sWv + V * LD48;
+  const float* swev = sWsv + V * LD128 + S + V;
+  Msg0Fwd F;
+  msg0_forward(sm, Pn + j * 2 * S, Pn + r * 2 * S, Qn + j * 6 * H0, Qn + r * 6 * H0,
+               es + e * SE, ev + e * 3, F, i, g);
+  ld_row<S / 16>(B.ds, ds_out + e * S, g);
+#pragma unroll
+  for (int p = 0; p < S / 16; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) B.ds[p][q] = F.spre[p][q] > 0.f ? B.ds[p][q] : 0.f;
+  ld_vrow<1>(B.dv, dv_out + e * (3 * V), g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float dsg = B.dv[0][0][q] * F.vpre[0][0][q] + B.dv[1][0][q] * F.vpre[1][0][q] + B.dv[2][0][q] * F.vpre[2][0][q];
+    B.dgate[0][q] = dsg * F.sg[0][q] * (1.f - F.sg[0][q]);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) B.dv[x][0][q] *= F.sg[0][q];
+  }
+  gemm_wtx<S / 16, 1>(sWsv, LD128, B.dgate, B.ds, i, g);  // dspre total
+  if (valid) {
+    st_row<S / 16>(O.dspre + e * S, B.ds, g);
+    if (O.spre) st_row<S / 16>(O.spre + e * S, F.spre, g);
+    st_row<1>(O.dgate + e * V, B.dgate, g);
+    st_row<3>(O.vn + e * H0, F.vn, g);
+    if (O.vh) st_vrow<3>(O.vh + e * (3 * H0), F.vh, g);
+    st_vrow<1>(O.dvpre + e * (3 * V), B.dv, g);
+  }
+  // des = We^T dspre ; dvn = Wn^T dspre
+  f32x4 des[2], dvn[3];
+  zero(des);
+  zero(dvn);
+  gemm_wtx<2, S / 16>(sWe, LD32, B.ds, des, i, g);
+  gemm_wtx<3, S / 16>(sWn, LD48, B.ds, dvn, i, g);
+  if (valid) st_row<2>(O.des + e * SE, des, g);
+  // dvh = Wv^T dvpre + dvn * vh / vn
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    zero(B.dvh[x]);
+    gemm_wtx<3, 1>(sWv, LD48, B.dv[x], B.dvh[x], i, g);
+  }
+  float dev0 = 0.f, dev1 = 0.f, dev2 = 0.f;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const f32x4 w = *reinterpret_cast<const f32x4*>(swev + 16 * p + 4 * g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float f = F.sq[p][q] > 1e-8f ? dvn[p][q] / F.vn[p][q] : 0.f;
+      B.dvh[0][p][q] += f * F.vh[0][p][q];
+      B.dvh[1][p][q] += f * F.vh[1][p][q];
+      B.dvh[2][p][q] += f * F.vh[2][p][q];
+      dev0 += w[q] * B.dvh[0][p][q];
+      dev1 += w[q] * B.dvh[1][p][q];
+      dev2 += w[q] * B.dvh[2][p][q];
+    }
+  }
+  // dev = sum over the 48 channels: reduce the 4 lane groups of this edge (fixed order)
+  dev0 += __shfl_xor(dev0, 16);
+  dev0 += __shfl_xor(dev0, 32);
+  dev1 += __shfl_xor(dev1, 16);
+  dev1 += __shfl_xor(dev1, 32);
+  dev2 += __shfl_xor(dev2, 16);
+  dev2 += __shfl_xor(dev2, 32);
+  if (valid) {
+    st_vrow<3>(O.dvh + e * (3 * H0), B.dvh, g);
+    if (g == 0) {
+      O.dev[e * 3 + 0] = dev0;
+      O.dev[e * 3 + 1] = dev1;
+      O.dev[e * 3 + 2] = dev2;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kGT) void gvp_msg0_bwd_kernel(int64_t E, const int64_t* __restrict__ send,
                                                            const int64_t* __restrict__ recv,
                                                            const float* __restrict__ Pn,
@@ -297,90 +386,15 @@ __global__ __launch_bounds__(kGT) void gvp_msg0_bwd_kernel(int64_t E, const int6
   extern __shared__ __attribute__((aligned(16))) float sm[];
   msg0_to_lds(sm, W);
   __syncthreads();
-  const float* sWe = sm;
-  const float* sWn = sWe + S * LD32;
-  const float* sWv = sWn + S * LD48;
-  const float* sWsv = sWv + V * LD48;
-  const float* swev = sWsv + V * LD128 + S + V;
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int64_t nchunks = (E + 15) / 16;
   const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (kGT / 64);
   for (int64_t c = wave; c < nchunks; c += nwaves) {
     const Chunk k = chunk_edge(c, i, E);
-    const int64_t j = send[k.e], r = recv[k.e];
-    Msg0Fwd F;
-    msg0_forward(sm, Pn + j * 2 * S, Pn + r * 2 * S, Qn + j * 6 * H0, Qn + r * 6 * H0,
-                 es + k.e * SE, ev + k.e * 3, F, i, g);
-    f32x4 ds[S / 16];
-    ld_row<S / 16>(ds, ds_out + k.e * S, g);
-#pragma unroll
-    for (int p = 0; p < S / 16; ++p)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) ds[p][q] = F.spre[p][q] > 0.f ? ds[p][q] : 0.f;
-    f32x4 dv[3][1];
-    ld_vrow<1>(dv, dv_out + k.e * (3 * V), g);
-    f32x4 dgate[1];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float dsg = dv[0][0][q] * F.vpre[0][0][q] + dv[1][0][q] * F.vpre[1][0][q] + dv[2][0][q] * F.vpre[2][0][q];
-      dgate[0][q] = dsg * F.sg[0][q] * (1.f - F.sg[0][q]);
-#pragma unroll
-      for (int x = 0; x < 3; ++x) dv[x][0][q] *= F.sg[0][q];
-    }
-    gemm_wtx<S / 16, 1>(sWsv, LD128, dgate, ds, i, g);  // dspre total
-    if (k.valid) {
-      st_row<S / 16>(O.dspre + k.e * S, ds, g);
-      if (O.spre) st_row<S / 16>(O.spre + k.e * S, F.spre, g);
-      st_row<1>(O.dgate + k.e * V, dgate, g);
-      st_row<3>(O.vn + k.e * H0, F.vn, g);
-      if (O.vh) st_vrow<3>(O.vh + k.e * (3 * H0), F.vh, g);
-      st_vrow<1>(O.dvpre + k.e * (3 * V), dv, g);
-    }
-    // des = We^T dspre ; dvn = Wn^T dspre
-    f32x4 des[2], dvn[3];
-    zero(des);
-    zero(dvn);
-    gemm_wtx<2, S / 16>(sWe, LD32, ds, des, i, g);
-    gemm_wtx<3, S / 16>(sWn, LD48, ds, dvn, i, g);
-    if (k.valid) st_row<2>(O.des + k.e * SE, des, g);
-    // dvh = Wv^T dvpre + dvn * vh / vn
-    f32x4 dvh[3][3];
-#pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      zero(dvh[x]);
-      gemm_wtx<3, 1>(sWv, LD48, dv[x], dvh[x], i, g);
-    }
-    float dev0 = 0.f, dev1 = 0.f, dev2 = 0.f;
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(swev + 16 * p + 4 * g);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float f = F.sq[p][q] > 1e-8f ? dvn[p][q] / F.vn[p][q] : 0.f;
-        dvh[0][p][q] += f * F.vh[0][p][q];
-        dvh[1][p][q] += f * F.vh[1][p][q];
-        dvh[2][p][q] += f * F.vh[2][p][q];
-        dev0 += w[q] * dvh[0][p][q];
-        dev1 += w[q] * dvh[1][p][q];
-        dev2 += w[q] * dvh[2][p][q];
-      }
-    }
-    // dev = sum over the 48 channels: reduce the 4 lane groups of this edge (fixed order)
-    dev0 += __shfl_xor(dev0, 16);
-    dev0 += __shfl_xor(dev0, 32);
-    dev1 += __shfl_xor(dev1, 16);
-    dev1 += __shfl_xor(dev1, 32);
-    dev2 += __shfl_xor(dev2, 16);
-    dev2 += __shfl_xor(dev2, 32);
-    if (k.valid) {
-      st_vrow<3>(O.dvh + k.e * (3 * H0), dvh, g);
-      if (g == 0) {
-        O.dev[k.e * 3 + 0] = dev0;
-        O.dev[k.e * 3 + 1] = dev1;
-        O.dev[k.e * 3 + 2] = dev2;
-      }
-    }
+    Msg0Bwd B;
+    msg0_bwd_edge(sm, k.e, k.valid, send[k.e], recv[k.e], Pn, Qn, es, ev, ds_out, dv_out, O, B,
+                  i, g);
   }
 }
 
@@ -743,6 +757,97 @@ __global__ __launch_bounds__(kGT) void gvp_layer_fwd_agg_kernel(
   }
 }
 
+// r05: the first message GVP's backward over the receiver-sorted edges, additionally reducing
+// dspre, dgate, dvpre and dvh over each receiver in registers (segmented scan, LDS carries; as
+// gvp_layer_fwd_agg_kernel): the receiver-side sums dPb = S_i dspre, dQb = S_i dvh and the
+// weight sums' S_i dgate, S_i dvpre without re-reading those per-edge rows.  Per-edge outputs
+// are stored at the original edge rows (perm), bitwise those of gvp_msg0_bwd_kernel.
+constexpr int kM0Carry = S / 4 + 4 + 12 + 36;  // ds | dgate | dvpre (3 x 4) | dvh (3 x 12)
+constexpr int kM0AggSmem = kMsg0Smem + (kGT / 64) * 4 * kM0Carry;
+
+__device__ __forceinline__ void carry_in(const float* c, f32x4* x, int n4, float tf) {
+  for (int t = 0; t < n4; ++t) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(c + 4 * t);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[t][q] = __builtin_fmaf(v[q], tf, x[t][q]);
+  }
+}
+__device__ __forceinline__ void carry_out(float* c, const f32x4* x, int n4) {
+  for (int t = 0; t < n4; ++t) *reinterpret_cast<f32x4*>(c + 4 * t) = x[t];
+}
+
+__global__ __launch_bounds__(kGT) void gvp_msg0_bwd_agg_kernel(
+    int64_t E, int64_t N, const int64_t* __restrict__ send, const int64_t* __restrict__ recv,
+    const int64_t* __restrict__ perm, const int64_t* __restrict__ rowptr,
+    const float* __restrict__ Pn, const float* __restrict__ Qn, const float* __restrict__ es,
+    const float* __restrict__ ev, Msg0W W, const float* __restrict__ ds_out,
+    const float* __restrict__ dv_out, Msg0Grads O, float* __restrict__ dPb,
+    float* __restrict__ dQb, float* __restrict__ sgr, float* __restrict__ svr) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  msg0_to_lds(sm, W);
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* wcarry = sm + kMsg0Smem + wid * 4 * kM0Carry;
+  for (int k = lane; k < 4 * kM0Carry; k += 64) wcarry[k] = 0.f;
+  float* cbuf = wcarry + g * kM0Carry;
+  __syncthreads();
+  const int64_t n_waves = (int64_t)gridDim.x * (kGT / 64);
+  const int64_t wave = (int64_t)blockIdx.x * (kGT / 64) + wid;
+  const int64_t nb = agg_node_begin(rowptr, N, E, wave, n_waves);
+  const int64_t ne = agg_node_begin(rowptr, N, E, wave + 1, n_waves);
+  const int64_t e_lo = (nb < ne) ? rowptr[nb] : 0, e_hi = (nb < ne) ? rowptr[ne] : 0;
+  for (int64_t n = nb + lane; n < ne; n += 64) {
+    if (rowptr[n] == rowptr[n + 1]) {
+      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < S; c += 4) *reinterpret_cast<f32x4*>(dPb + n * S + c) = z;
+      for (int c = 0; c < 3 * H0; c += 4) *reinterpret_cast<f32x4*>(dQb + n * (3 * H0) + c) = z;
+      for (int c = 0; c < V; c += 4) *reinterpret_cast<f32x4*>(sgr + n * V + c) = z;
+      for (int c = 0; c < 3 * V; c += 4) *reinterpret_cast<f32x4*>(svr + n * (3 * V) + c) = z;
+    }
+  }
+  int64_t carry_node = -1;
+  for (int64_t base = e_lo; base < e_hi; base += 16) {
+    const int64_t k = base + i;
+    const bool valid = k < e_hi;
+    const int64_t kc = valid ? k : e_hi - 1;
+    const int64_t e = perm ? perm[kc] : kc;
+    const int64_t r = recv[e];
+    const int64_t n = (r >= 0 && r < N) ? r : 0;
+    const int64_t seg0 = rowptr[n], seg1 = rowptr[n + 1];
+    Msg0Bwd B;
+    msg0_bwd_edge(sm, e, valid, send[e], r, Pn, Qn, es, ev, ds_out, dv_out, O, B, i, g);
+    const float tf = (i == 0 && valid && n == carry_node) ? 1.f : 0.f;
+    carry_in(cbuf, B.ds, S / 16, tf);
+    carry_in(cbuf + S / 4, B.dgate, 1, tf);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) carry_in(cbuf + S / 4 + 4 + 4 * x, B.dv[x], 1, tf);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) carry_in(cbuf + S / 4 + 16 + 12 * x, B.dvh[x], 3, tf);
+    const int head = valid ? (int)((seg0 > base) ? (seg0 - base) : 0) : i;
+    seg_scan<S / 16>(B.ds, i, head);
+    seg_scan<1>(B.dgate, i, head);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) seg_scan<1>(B.dv[x], i, head);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) seg_scan<3>(B.dvh[x], i, head);
+    if (i == 15) {
+      carry_out(cbuf, B.ds, S / 16);
+      carry_out(cbuf + S / 4, B.dgate, 1);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) carry_out(cbuf + S / 4 + 4 + 4 * x, B.dv[x], 1);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) carry_out(cbuf + S / 4 + 16 + 12 * x, B.dvh[x], 3);
+    }
+    if (valid && k == seg1 - 1) {
+      st_row<S / 16>(dPb + n * S, B.ds, g);
+      st_row<1>(sgr + n * V, B.dgate, g);
+      st_vrow<1>(svr + n * (3 * V), B.dv, g);
+      st_vrow<3>(dQb + n * (3 * H0), B.dvh, g);
+    }
+    carry_node = __builtin_amdgcn_readlane((int)n, 15);
+  }
+}
+
 // Upstream gradient of the layer's per-edge outputs.  AGG = 0: per-edge rows ds_out (E, S),
 // dv_out (E, 3V).  AGG = 1 / 2: the layer feeds a sum / mean aggregation at the receivers
 // (GVPConv, gvp_layer.py:319-324 with aggr "add" / "mean"): the rows are the aggregation's node
@@ -950,6 +1055,42 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
   return layer_bwd(n_edges, relu, 0, AggGrad{nullptr, nullptr, 0}, s_in, v_in, Ws, bs, Wsv, bsv,
                    Wh, Wv, ds_out, dv_out, ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh,
                    stream);
+}
+
+int gmp_gvp_msg0_bwd_agg_f32(int64_t n_edges, int64_t n_nodes, const int64_t* send,
+                             const int64_t* recv, const int64_t* perm, const int64_t* rowptr,
+                             const float* P, const float* Q, const float* es, const float* ev,
+                             const float* We, const float* Wn, const float* b, const float* Wv,
+                             const float* Wsv, const float* bsv, const float* wev,
+                             const float* ds_out, const float* dv_out, float* dspre, float* spre,
+                             float* dgate, float* vn, float* vh, float* dvpre, float* dvh,
+                             float* des, float* dev, float* dPb, float* dQb, float* sgate_recv,
+                             float* svpre_recv, void* stream) {
+  GMP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && n_edges < (1LL << 31) && n_nodes < (1LL << 31));
+  if (n_nodes == 0) return GMP_OK;
+  GMP_CHECK_ARG(rowptr && dPb && dQb && sgate_recv && svpre_recv && al16(dPb) && al16(dQb) &&
+                al16(sgate_recv) && al16(svpre_recv));
+  if (n_edges > 0) {
+    GMP_CHECK_ARG(send && recv && P && Q && es && ev && We && Wn && b && Wv && Wsv && bsv &&
+                  wev && ds_out && dv_out);
+    GMP_CHECK_ARG(dspre && dgate && vn && dvpre && dvh && des && dev);  // spre, vh: optional
+    GMP_CHECK_ARG(al16(P) && al16(Q) && al16(es) && al16(ds_out) && al16(dv_out) &&
+                  al16(dspre) && al16(spre) && al16(dgate) && al16(vn) && al16(vh) &&
+                  al16(dvpre) && al16(dvh) && al16(des));
+  }
+  const Msg0W W{We, Wn, b, Wv, Wsv, bsv, wev};
+  const Msg0Grads O{dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev};
+  int64_t G = (int64_t)device_cu_count();
+  const int64_t cap = ceil_div(n_edges, (int64_t)(kGT / 64) * 64);
+  if (G > cap) G = cap;
+  if (G < 1) G = 1;
+  const size_t smem = kM0AggSmem * sizeof(float);
+  int rc;
+  if ((rc = set_smem(gvp_msg0_bwd_agg_kernel, smem))) return rc;
+  gvp_msg0_bwd_agg_kernel<<<(unsigned)G, kGT, smem, as_stream(stream)>>>(
+      n_edges, n_nodes, send, recv, perm, rowptr, P, Q, es, ev, W, ds_out, dv_out, O, dPb, dQb,
+      sgate_recv, svpre_recv);
+  return launch_status();
 }
 
 int gmp_gvp_layer_fwd_agg_f32(int64_t n_edges, int64_t n_nodes, int reduce, const int64_t* perm,

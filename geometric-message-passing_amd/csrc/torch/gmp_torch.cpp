@@ -1361,6 +1361,46 @@ std::vector<Tensor> gvp_msg0_bwd(const Tensor& send, const Tensor& recv, const T
   return {dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev};
 }
 
+// gvp_msg0_bwd walking the receiver-sorted edges, with the receiver-side sums S_i dspre,
+// S_i dvh, S_i dgate, S_i dvpre reduced in the kernel (appended to the outputs)
+std::vector<Tensor> gvp_msg0_bwd_agg(const Tensor& send, const Tensor& recv, const Tensor& P,
+                                     const Tensor& Q, const Tensor& es, const Tensor& ev,
+                                     const std::vector<Tensor>& W, const Tensor& ds,
+                                     const Tensor& dv, const optional<Tensor>& perm,
+                                     const Tensor& rowptr, int64_t n_nodes, bool want_factors) {
+  OpGuard g(P, "gvp_msg0_bwd_agg");
+  const int64_t E = gvp_msg0_checks(send, recv, P, Q, es, ev, W);
+  f32(ds, "ds");
+  f32(dv, "dv");
+  shape(ds, {E, 128}, "ds");
+  numel(dv, E * 48, "dv");
+  i64(rowptr, "rowptr");
+  shape(rowptr, {n_nodes + 1}, "rowptr");
+  const bool hp = perm.has_value() && perm->defined();
+  if (hp) {
+    i64(*perm, "perm");
+    shape(*perm, {E}, "perm");
+  }
+  auto o = fopt(P);
+  const int64_t Ef = want_factors ? E : 0;
+  Tensor dspre = at::empty({E, 128}, o), spre = at::empty({Ef, 128}, o);
+  Tensor dgate = at::empty({E, 16}, o), vn = at::empty({E, 48}, o);
+  Tensor vh = at::empty({Ef, 144}, o), dvh = at::empty({E, 144}, o);
+  Tensor dvpre = at::empty({E, 48}, o), des = at::empty({E, 32}, o), dev = at::empty({E, 3}, o);
+  Tensor dPb = at::empty({n_nodes, 128}, o), dQb = at::empty({n_nodes, 144}, o);
+  Tensor sgr = at::empty({n_nodes, 16}, o), svr = at::empty({n_nodes, 48}, o);
+  check_rc(gmp_gvp_msg0_bwd_agg_f32(E, n_nodes, ip(send), ip(recv),
+                                    hp ? perm->data_ptr<int64_t>() : nullptr,
+                                    rowptr.data_ptr<int64_t>(), fp(P), fp(Q), fp(es), fp(ev),
+                                    fp(W[0]), fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]),
+                                    fp(W[6]), fp(ds), fp(dv), fp(dspre),
+                                    want_factors ? fp(spre) : nullptr, fp(dgate), fp(vn),
+                                    want_factors ? fp(vh) : nullptr, fp(dvpre), fp(dvh), fp(des),
+                                    fp(dev), fp(dPb), fp(dQb), fp(sgr), fp(svr), cur_stream()),
+           "gmp_gvp_msg0_bwd_agg_f32");
+  return {dspre, spre, dgate, vn, vh, dvpre, dvh, des, dev, dPb, dQb, sgr, svr};
+}
+
 // ------------------------------------------------------------------ Meta (shape) kernels
 namespace meta {
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> csr_build(const Tensor& index, int64_t n_seg,
@@ -1588,6 +1628,19 @@ std::vector<Tensor> gvp_msg0_bwd(const Tensor& send, const Tensor&, const Tensor
           at::empty({E, 48}, o),  at::empty({Ef, 144}, o), at::empty({E, 48}, o),
           at::empty({E, 144}, o), at::empty({E, 32}, o),  at::empty({E, 3}, o)};
 }
+std::vector<Tensor> gvp_msg0_bwd_agg(const Tensor& send, const Tensor& recv, const Tensor& P,
+                                     const Tensor& Q, const Tensor& es, const Tensor& ev,
+                                     const std::vector<Tensor>& W, const Tensor& ds,
+                                     const Tensor& dv, const optional<Tensor>&, const Tensor&,
+                                     int64_t n_nodes, bool want_factors) {
+  auto out = meta::gvp_msg0_bwd(send, recv, P, Q, es, ev, W, ds, dv, want_factors);
+  auto o = P.options();
+  out.push_back(at::empty({n_nodes, 128}, o));
+  out.push_back(at::empty({n_nodes, 144}, o));
+  out.push_back(at::empty({n_nodes, 16}, o));
+  out.push_back(at::empty({n_nodes, 48}, o));
+  return out;
+}
 }  // namespace meta
 
 }  // namespace
@@ -1688,6 +1741,9 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor[] W) -> (Tensor s_out, Tensor v_out)");
   m.def("gvp_msg0_bwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
         "Tensor[] W, Tensor ds, Tensor dv, bool want_factors=True) -> Tensor[]");
+  m.def("gvp_msg0_bwd_agg(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
+        "Tensor[] W, Tensor ds, Tensor dv, Tensor? perm, Tensor rowptr, int n_nodes, "
+        "bool want_factors=True) -> Tensor[]");
 }
 
 #define GMP_IMPL(m, ns)                                                    \
@@ -1739,6 +1795,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("gvp_layer_bwd", ns gvp_layer_bwd);                              \
   m.impl("gvp_layer_bwd_agg", ns gvp_layer_bwd_agg);                      \
   m.impl("gvp_layer_fwd_agg", ns gvp_layer_fwd_agg);                      \
+  m.impl("gvp_msg0_bwd_agg", ns gvp_msg0_bwd_agg);                        \
   m.impl("gvp_msg0_fwd", ns gvp_msg0_fwd);                                \
   m.impl("gvp_msg0_bwd", ns gvp_msg0_bwd);
 

@@ -332,17 +332,20 @@ class GvpMsg0Fn(torch.autograd.Function):
         ds = ops._f32c(ds) if ds is not None else torch.zeros((E, 128), device=P.device)
         dv = ops._f32c(dv) if dv is not None else torch.zeros((E, 16, 3), device=P.device)
         f = dict(dtype=torch.float32, device=P.device)
+        n = P.shape[0]
         with ops._timed("gvp_msg0_bwd"):
-            dspre, _, dgate, vn, _, dvpre, dvh, des, dev = _lib.torch_ops().gvp_msg0_bwd(
-                send, recv, P, Q, es, ev, W, ds, dv, False)
+            # receiver-sorted walk; the receiver-side sums (dPb, dQb and the weight sums' S_i
+            # dgate, S_i dvpre) come out of the kernel's segmented scan
+            (dspre, _, dgate, vn, _, dvpre, dvh, des, dev, dPb, dQb, sg_i,
+             sv_i) = _lib.torch_ops().gvp_msg0_bwd_agg(send, recv, P, Q, es, ev, W, ds, dv,
+                                                       recv_csr.perm, recv_csr.rowptr, n, False)
         # weight gradients (edge outer sums) on the side stream, as full-size leaf gradients.
         # The pre-activation rows spre and the mixed vectors vh are not written by the kernel
         # (gmp.h gmp_gvp_msg0_bwd_f32): both are sums of per-edge terms and the gathered node
         # projections, so their sums split into edge sums and node-level products of the
         # sender / receiver segment sums of dgate / dvpre.
-        with ops.side_work(dspre, es, vn, dgate, dvpre, ev, dvh, P, Q) as sw:
+        with ops.side_work(dspre, es, vn, dgate, dvpre, ev, dvh, P, Q, sg_i, sv_i) as sw:
             vi = Wv.shape[1]
-            n = P.shape[0]
             # [dWe | dWn] = dspre^T [es | vn]: one pass over dspre when the split path applies
             Cen, db = torch.empty((128, 80), **f), torch.empty(128, **f)
             ops.outer_sum_into2(dspre, es, vn, Cen, db)
@@ -350,14 +353,12 @@ class GvpMsg0Fn(torch.autograd.Function):
             # dWsv = dgate^T spre, spre = [es | vn] [We | Wn]^T + Pa[j] + Pb[i] + b
             Gx, dbsv = torch.empty((16, 80), **f), torch.empty(16, **f)
             ops.outer_sum_into2(dgate, es, vn, Gx, dbsv)
-            Sg = torch.cat([ops.segment_reduce(dgate, send_csr, "sum")[0],
-                            ops.segment_reduce(dgate, recv_csr, "sum")[0]], 0)   # (2N, 16)
+            Sg = torch.cat([ops.segment_reduce(dgate, send_csr, "sum")[0], sg_i], 0)  # (2N, 16)
             Pab = P.view(n, 2, 128).transpose(0, 1).reshape(2 * n, 128)      # [Pa ; Pb]
             dWsv = _osum(Sg, Pab)[0].addmm_(Gx[:, :32], W[0].t()).addmm_(Gx[:, 32:], W[1].t())
             dWsv.add_(torch.outer(dbsv, W[2]))
             # dWv = sum_(e,x) dvpre[e, o, x] vh[e, h, x], vh = Qa[j] + Qb[i] + wev (x) ev
-            Sv = torch.cat([ops.segment_reduce(dvpre, send_csr, "sum")[0],
-                            ops.segment_reduce(dvpre, recv_csr, "sum")[0]], 0)   # (2N, 48)
+            Sv = torch.cat([ops.segment_reduce(dvpre, send_csr, "sum")[0], sv_i], 0)  # (2N, 48)
             Qab = Q.view(n, 2, 144).transpose(0, 1).reshape(2 * n, 144)      # [Qa ; Qb]
             dWv = _diag3(_osum(Sv, Qab)[0], 16, 48)
             ev16 = torch.nn.functional.pad(ev, (0, 13))
@@ -372,11 +373,10 @@ class GvpMsg0Fn(torch.autograd.Function):
             gWh0 = torch.zeros_like(Wh0)
             gWh0[:, 16] = dwev[:Wh0.shape[0]]
             grads = (gWs0, db, dWv[:, :vi].contiguous(), dWsv, dbsv, gWh0)
-        # node-projection gradients: deterministic segmented sums at the senders / receivers
+        # node-projection gradients: deterministic segmented sums at the senders (the receivers'
+        # came out of the kernel)
         dPa, _ = ops.segment_reduce(dspre, send_csr, "sum")
-        dPb, _ = ops.segment_reduce(dspre, recv_csr, "sum")
         dQa, _ = ops.segment_reduce(dvh, send_csr, "sum")
-        dQb, _ = ops.segment_reduce(dvh, recv_csr, "sum")
         return ((torch.cat([dPa, dPb], 1), torch.cat([dQa, dQb], 1).view(-1, 288), des, dev)
                 + sw.deliver(ctx.needs_input_grad, 4, ctx.leaves, grads) + (None, None, None))
 

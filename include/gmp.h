@@ -510,6 +510,21 @@ int gmp_gvp_layer_bwd_f32(int64_t n_edges, int relu, const float* s_in, const fl
                           const float* dv_out, float* ds_in, float* dv_in, float* dspre,
                           float* spre, float* dgate, float* vn, float* vh, float* dvpre,
                           float* dvh, void* stream);
+/* gmp_gvp_msg0_bwd_agg_f32: gmp_gvp_msg0_bwd_f32 walking the receiver-sorted edges (perm: original
+ * edge of sorted position k, NULL if the edges are receiver-sorted; rowptr: the receiver CSR)
+ * and also reducing over each receiver, in registers, the rows the receiver-side sums need:
+ * dPb (n_nodes, 128) = S_i dspre, dQb (n_nodes, 144) = S_i dvh, sgate_recv (n_nodes, 16) =
+ * S_i dgate, svpre_recv (n_nodes, 48) = S_i dvpre (receivers without edges: zero rows; tree
+ * order inside a 16-edge chunk).  The per-edge outputs are bitwise gmp_gvp_msg0_bwd_f32's. */
+int gmp_gvp_msg0_bwd_agg_f32(int64_t n_edges, int64_t n_nodes, const int64_t* send,
+                             const int64_t* recv, const int64_t* perm, const int64_t* rowptr,
+                             const float* P, const float* Q, const float* es, const float* ev,
+                             const float* We, const float* Wn, const float* b, const float* Wv,
+                             const float* Wsv, const float* bsv, const float* wev,
+                             const float* ds_out, const float* dv_out, float* dspre, float* spre,
+                             float* dgate, float* vn, float* vh, float* dvpre, float* dvh,
+                             float* des, float* dev, float* dPb, float* dQb, float* sgate_recv,
+                             float* svpre_recv, void* stream);
 /* gmp_gvp_layer_fwd_agg_f32: the last message GVP of GVPConv fused with the receivers' sum /
  * mean (gvp_layer.py:319-324, aggr "add" / "mean" = reduce GMP_REDUCE_SUM / GMP_REDUCE_MEAN):
  * s_agg (n_nodes, 128), v_agg (n_nodes, 16, 3) directly, no per-edge output rows.  The receiver

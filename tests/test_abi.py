@@ -60,7 +60,8 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
                  "tp_gemm_x3_widen", "outer_sum_cols", "edge_outer_sum_ex",
                  "edge_outer_sum_ex2", "edge_outer_sum_act", "gvp_layer_fwd", "gvp_layer_bwd",
                  "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd",
-                 "gvp_layer_fwd_agg", "gvp_layer_bwd_agg", "symmetric_contraction_fwd",
+                 "gvp_layer_fwd_agg", "gvp_layer_bwd_agg", "gvp_msg0_bwd_agg",
+                 "symmetric_contraction_fwd",
                  "symmetric_contraction_bwd"):
         assert hasattr(tops, name), name
     with pytest.raises(RuntimeError, match="HIP device"):

@@ -360,3 +360,35 @@ def test_gvp_layer_agg_no_edges():
                                          torch.zeros(0, 16, 3, device=DEV), *W, csr, reduce)
         assert a_s.shape == (7, 128) and a_v.shape == (7, 16, 3)
         assert not bool(a_s.abs().sum()) and not bool(a_v.abs().sum())
+
+
+def test_gvp_msg0_bwd_agg_matches_unfused():
+    """gmp_gvp_msg0_bwd_agg_f32 (receiver-sorted walk with the receiver-side sums reduced in the
+    kernel) against gmp_gvp_msg0_bwd_f32 + K3: per-edge outputs bitwise equal, the receiver sums
+    S_i dspre, S_i dvh, S_i dgate, S_i dvpre within 1e-6 of their scale (tree order inside a
+    16-edge chunk); shuffled edges, receivers without edges."""
+    from gmp_amd import _lib, ops
+    from gmp_amd.graph import radius_graph
+    tops = _lib.torch_ops()
+    torch.manual_seed(5)
+    gr = radius_graph(num_nodes=500, target_edges=8000, r=2.0, seed=6, tol=0.2, shuffle=True)
+    n, E = gr.num_nodes + 3, gr.edge_index.shape[1]
+    send, recv = (gr.edge_index[k].to(DEV).contiguous() for k in (0, 1))
+    rcsr, scsr = ops.get_csr(recv, n), ops.get_csr(send, n)
+    f = dict(device=DEV)
+    P, Q = torch.randn(n, 256, **f), torch.randn(n, 288, **f)
+    es, ev = torch.randn(E, 32, **f), torch.randn(E, 3, **f)
+    W = [torch.randn(128, 32, **f) * 0.2, torch.randn(128, 48, **f) * 0.2, torch.randn(128, **f),
+         torch.randn(16, 48, **f) * 0.2, torch.randn(16, 128, **f) * 0.1, torch.randn(16, **f),
+         torch.randn(48, **f) * 0.3]
+    ds, dv = torch.randn(E, 128, **f), torch.randn(E, 48, **f)
+    ref = tops.gvp_msg0_bwd(send, recv, P, Q, es, ev, W, ds, dv, False)
+    got = tops.gvp_msg0_bwd_agg(send, recv, P, Q, es, ev, W, ds, dv, rcsr.perm, rcsr.rowptr, n,
+                                False)
+    torch.cuda.synchronize()
+    for k in (0, 2, 3, 5, 6, 7, 8):
+        assert torch.equal(got[k], ref[k]), k
+    for k, src in ((9, ref[0]), (10, ref[6]), (11, ref[2]), (12, ref[5])):
+        want, _ = ops.segment_reduce(src, rcsr, "sum")
+        _scaled(got[k], want, 1e-6, f"receiver sum {k}")
+    assert bool((got[9][rcsr.counts() == 0] == 0).all())
