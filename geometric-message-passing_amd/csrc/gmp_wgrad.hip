@@ -158,16 +158,18 @@ __global__ __launch_bounds__(kT, 2) void outer_sum_kernel(const float* __restric
   }
 }
 
-constexpr int kGC = 16;  // slab loads in flight per lane in the ordered partial sums
+constexpr int kGC = 16;  // slab loads in flight per lane in the ordered partial sums (default)
 
 // One-pass ordered sum of the G partial slabs (replaces l1 + l2 on the split-K paths): a
 // workgroup owns 64 columns x; its SW waves each add a contiguous 1/SW of the slabs (slab
-// order, 16 loads in flight per lane), then wave 0 adds the SW partial sums in wave order -- a
-// fixed order independent of timing (deterministic).  SW = 16 (1024 threads): a 256-slab
-// reduction is ONE burst of loads per lane (4 waves took four dependent bursts: the r03 EGNN
-// trace had 2.2 ms of these sums per step on the side stream, latency-bound under the main
-// stream's HBM traffic).
-template <int SW>
+// order, GC loads in flight per lane), then wave 0 adds the SW partial sums in wave order -- a
+// fixed order independent of timing (deterministic).  The split-K sums use SW = 4, GC = 32
+// (256 threads, a 256-slab reduction in two bursts of loads per lane): these sums run on the
+// side stream beside the main stream's edge kernels, and a 256-thread workgroup fits beside
+// those kernels' waves on a CU where the r03-r05 1024-thread form (SW = 16, one burst) had to
+// wait for a whole CU to drain -- up to 0.9 ms per sum behind the GVP message backward in the
+// r05 trace.
+template <int SW, int GC = kGC>
 __global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restrict__ part,
                                                             int64_t G, int64_t X,
                                                             float* __restrict__ out,
@@ -179,12 +181,12 @@ __global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restr
   const int64_t q = (G + SW - 1) / SW, g0 = wv * q, g1 = (g0 + q < G) ? g0 + q : G;
   float s = 0.f;
   if (x < X) {
-    for (int64_t c0 = g0; c0 < g1; c0 += kGC) {
-      float v[kGC];
+    for (int64_t c0 = g0; c0 < g1; c0 += GC) {
+      float v[GC];
 #pragma unroll
-      for (int u = 0; u < kGC; ++u) v[u] = (c0 + u < g1) ? part[(c0 + u) * X + x] : 0.f;
+      for (int u = 0; u < GC; ++u) v[u] = (c0 + u < g1) ? part[(c0 + u) * X + x] : 0.f;
 #pragma unroll
-      for (int u = 0; u < kGC; ++u)
+      for (int u = 0; u < GC; ++u)
         if (c0 + u < g1) s += v[u];
     }
   }
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restr
 void sum_partials(const float* part, int64_t G, int64_t X, float* out, float* colsum,
                   int64_t DD, int64_t n, int64_t ldc, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(X, 64);
-  sum_partials_one<16><<<grid, 1024, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
+  sum_partials_one<4, 32><<<grid, 256, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
 }
 
 // Rectangular variant for the other per-edge Linears (GVP message GVPs: 128 x 144, 128 x 80,

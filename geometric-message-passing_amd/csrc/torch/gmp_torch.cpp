@@ -1304,6 +1304,63 @@ std::vector<Tensor> gvp_layer_bwd_agg(const Tensor& s, const Tensor& v,
   return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
 }
 
+// K1e: the GVP-GNN edge embedding (LayerNorm((R, 1)) + GVP((R, 1), (so, 1))) over edge rows.
+// W = [ln_w (R), ln_b (R), wh (1, 1), Ws (so, R + 1), bs (so), wv (1, 1), wsv (1, so), bsv (1)]
+int64_t gvp_embed_checks(const Tensor& radial, const Tensor& unit, const std::vector<Tensor>& W) {
+  f32(radial, "radial");
+  f32(unit, "unit");
+  TORCH_CHECK(radial.dim() == 2, "gmp.gvp_edge_embed: radial must be (E, R)");
+  const int64_t E = radial.size(0), R = radial.size(1);
+  numel(unit, E * 3, "unit");
+  TORCH_CHECK(W.size() == 8, "gmp.gvp_edge_embed: 8 parameter tensors");
+  for (const auto& w : W) f32(w, "W");
+  const int64_t so = W[3].size(0);
+  TORCH_CHECK(W[3].dim() == 2 && W[3].size(1) == R + 1, "gmp.gvp_edge_embed: Ws (so, R + 1)");
+  numel(W[0], R, "ln_w");
+  numel(W[1], R, "ln_b");
+  numel(W[2], 1, "wh");
+  numel(W[4], so, "bs");
+  numel(W[5], 1, "wv");
+  numel(W[6], so, "wsv");
+  numel(W[7], 1, "bsv");
+  return E;
+}
+
+std::tuple<Tensor, Tensor> gvp_edge_embed_fwd(const Tensor& radial, const Tensor& unit,
+                                              const std::vector<Tensor>& W, double eps) {
+  OpGuard g(radial, "gvp_edge_embed_fwd");
+  const int64_t E = gvp_embed_checks(radial, unit, W);
+  const int64_t so = W[3].size(0);
+  auto o = fopt(radial);
+  Tensor es = at::empty({E, so}, o), ev = at::empty({E, 1, 3}, o);
+  check_rc(gmp_gvp_edge_embed_fwd_f32(E, radial.size(1), so, fp(radial), fp(unit), fp(W[0]),
+                                      fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]), fp(W[6]),
+                                      fp(W[7]), (float)eps, fp(es), fp(ev), cur_stream()),
+           "gmp_gvp_edge_embed_fwd_f32");
+  return {es, ev};
+}
+
+Tensor gvp_edge_embed_bwd(const Tensor& radial, const Tensor& unit, const std::vector<Tensor>& W,
+                          double eps, const Tensor& des, const Tensor& dev) {
+  OpGuard g(radial, "gvp_edge_embed_bwd");
+  const int64_t E = gvp_embed_checks(radial, unit, W);
+  const int64_t R = radial.size(1), so = W[3].size(0);
+  f32(des, "grad_es");
+  f32(dev, "grad_ev");
+  shape(des, {E, so}, "grad_es");
+  numel(dev, E * 3, "grad_ev");
+  auto o = fopt(radial);
+  Tensor grad = at::empty({2 * R + 3 + so * (R + 3)}, o);
+  const size_t ws_b = gmp_gvp_edge_embed_bwd_workspace_size(E);
+  Tensor ws = at::empty({(int64_t)ws_b + 1}, o.dtype(at::kByte));
+  check_rc(gmp_gvp_edge_embed_bwd_f32(E, R, so, fp(radial), fp(unit), fp(W[0]), fp(W[1]),
+                                      fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]), fp(W[6]), fp(W[7]),
+                                      (float)eps, fp(des), fp(dev), fp(grad), ws.data_ptr(), ws_b,
+                                      cur_stream()),
+           "gmp_gvp_edge_embed_bwd_f32");
+  return grad;
+}
+
 int64_t gvp_msg0_checks(const Tensor& send, const Tensor& recv, const Tensor& P, const Tensor& Q,
                         const Tensor& es, const Tensor& ev, const std::vector<Tensor>& W) {
   i64(send, "send");
@@ -1612,6 +1669,16 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd_agg(const Tensor& s, const Tensor&,
                                              const std::string&) {
   return {at::empty({n_nodes, 128}, s.options()), at::empty({n_nodes, 16, 3}, s.options())};
 }
+std::tuple<Tensor, Tensor> gvp_edge_embed_fwd(const Tensor& radial, const Tensor&,
+                                              const std::vector<Tensor>& W, double) {
+  const int64_t E = radial.size(0);
+  return {at::empty({E, W[3].size(0)}, radial.options()), at::empty({E, 1, 3}, radial.options())};
+}
+Tensor gvp_edge_embed_bwd(const Tensor& radial, const Tensor&, const std::vector<Tensor>& W,
+                          double, const Tensor&, const Tensor&) {
+  const int64_t R = radial.size(1), so = W[3].size(0);
+  return at::empty({2 * R + 3 + so * (R + 3)}, radial.options());
+}
 std::tuple<Tensor, Tensor> gvp_msg0_fwd(const Tensor& send, const Tensor&, const Tensor& P,
                                         const Tensor&, const Tensor&, const Tensor&,
                                         const std::vector<Tensor>&) {
@@ -1737,6 +1804,10 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor rowptr, int n_nodes, str reduce) -> (Tensor s_agg, Tensor v_agg)");
   m.def("gvp_layer_bwd_agg(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, Tensor index, "
         "Tensor rowptr, str reduce, bool relu, bool want_factors=True) -> Tensor[]");
+  m.def("gvp_edge_embed_fwd(Tensor radial, Tensor unit, Tensor[] W, float eps) "
+        "-> (Tensor es, Tensor ev)");
+  m.def("gvp_edge_embed_bwd(Tensor radial, Tensor unit, Tensor[] W, float eps, Tensor grad_es, "
+        "Tensor grad_ev) -> Tensor");
   m.def("gvp_msg0_fwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
         "Tensor[] W) -> (Tensor s_out, Tensor v_out)");
   m.def("gvp_msg0_bwd(Tensor send, Tensor recv, Tensor P, Tensor Q, Tensor es, Tensor ev, "
@@ -1761,6 +1832,8 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("ssp_bwd", ns ssp_bwd);                                          \
   m.impl("ln_act_fwd", ns ln_act_fwd);                                    \
   m.impl("ln_act_bwd", ns ln_act_bwd);                                    \
+  m.impl("gvp_edge_embed_fwd", ns gvp_edge_embed_fwd);                    \
+  m.impl("gvp_edge_embed_bwd", ns gvp_edge_embed_bwd);                    \
   m.impl("vec_norm_fwd", ns vec_norm_fwd);                                \
   m.impl("vec_norm_bwd", ns vec_norm_bwd);                                \
   m.impl("xyz_norm_fwd", ns xyz_norm_fwd);                                \

@@ -381,6 +381,69 @@ class GvpMsg0Fn(torch.autograd.Function):
                 + sw.deliver(ctx.needs_input_grad, 4, ctx.leaves, grads) + (None, None, None))
 
 
+# False: the edge embedding W_e as the module chain (tests compare the two)
+EDGE_EMBED_FUSED = True
+
+
+class GvpEdgeEmbedFn(torch.autograd.Function):
+    """K1e: the edge embedding W_e = LayerNorm((R, 1)) + GVP((R, 1), (so, 1)) (gvpgnn.py:73-77,
+    applied at :116) over the edge rows in one HIP pass each way (gmp_gvp_edge_embed_{fwd,bwd}_f32):
+    the module chain's 1M-row library GEMMs with K or N = 1 and its elementwise passes (~0.6 ms
+    forward, ~1.5 ms of the backward's tail per C3 step) become two kernels.  The backward
+    returns only the parameters' gradients (radial / unit come from positions without
+    requires_grad; the caller checks)."""
+
+    @staticmethod
+    def forward(ctx, radial, unit, eps, ln_w, ln_b, wh, ws, bs, wv, wsv, bsv):
+        radial, unit = ops._f32c(radial), ops._f32c(unit)
+        ops._need_cuda(radial, unit)
+        W = [ops._f32c(t) for t in (ln_w, ln_b, wh, ws, bs, wv, wsv, bsv)]
+        es, ev = _lib.torch_ops().gvp_edge_embed_fwd(radial, unit, W, float(eps))
+        ctx.eps = float(eps)
+        ctx.shapes = [t.shape for t in (ln_w, ln_b, wh, ws, bs, wv, wsv, bsv)]
+        ctx.save_for_backward(radial, unit, *W)
+        return es, ev
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, des, dev):
+        radial, unit, *W = ctx.saved_tensors
+        E, so = radial.shape[0], W[3].shape[0]
+        des = ops._f32c(des) if des is not None else radial.new_zeros((E, so))
+        dev = ops._f32c(dev) if dev is not None else radial.new_zeros((E, 1, 3))
+        g = _lib.torch_ops().gvp_edge_embed_bwd(radial, unit, W, ctx.eps, des, dev)
+        grads, o = [], 0
+        for shp in ctx.shapes:
+            n = int(torch.Size(shp).numel())
+            grads.append(g[o:o + n].view(shp))
+            o += n
+        return (None, None, None) + tuple(grads)
+
+
+def _edge_embed_ok(W_e, rad, unit):
+    if not (EDGE_EMBED_FUSED and len(W_e) == 2 and rad.is_cuda and rad.dtype == torch.float32
+            and unit.dtype == torch.float32 and rad.dim() == 2 and rad.shape[1] == 8):
+        return False
+    ln, g = W_e
+    if torch.is_grad_enabled() and (rad.requires_grad or unit.requires_grad):
+        return False  # the fused backward gives the edge rows no gradient
+    return (type(ln) is LayerNorm and type(g) is GVP and (ln.s, ln.v) == (8, 1)
+            and ln.scalar_norm.elementwise_affine and ln.scalar_norm.bias is not None
+            and (g.si, g.vi, g.vo) == (8, 1, 1) and 1 <= g.so <= 32 and g.h_dim == 1
+            and g.vector_gate and g.scalar_act is None and g.vector_act is None)
+
+
+def edge_embed(W_e, rad, unit):
+    """W_e((rad, unit[:, None])) -> (es (E, so), ev (E, 1, 3)): K1e when the module is the
+    reference's shape, else the module chain."""
+    if _edge_embed_ok(W_e, rad, unit):
+        ln, g = W_e
+        return GvpEdgeEmbedFn.apply(rad, unit, ln.scalar_norm.eps, ln.scalar_norm.weight,
+                                    ln.scalar_norm.bias, g.wh.weight, g.ws.weight, g.ws.bias,
+                                    g.wv.weight, g.wsv.weight, g.wsv.bias)
+    return W_e((rad, unit.unsqueeze(-2)))
+
+
 class NodeProjFn(torch.autograd.Function):
     """P = s [Ws0[:, :si] ; Ws0[:, si + se : 2 si + se]]^T (N, 2 so): the sender / receiver
     scalar blocks of the first message GVP's Linear applied once per node.  dWs0 (a K = N
@@ -640,9 +703,8 @@ class GVPGNNModel(nn.Module):
         # K1: radial embedding of |vec| and nan_to_num(vec / |vec|) in one pass (gvpgnn.py:106-112)
         rad, unit = ops.GvpEdgeFeaturizeFn.apply(batch.pos, ei, self.radial_embedding._host)
         h_V = ops.gather(self.emb_in.weight, batch.atoms, 0)
-        h_E = (rad, unit.unsqueeze(-2))
         h_V = self.W_v(h_V)
-        h_E = self.W_e(h_E)
+        h_E = edge_embed(self.W_e, rad, unit)   # K1e (gvpgnn.py:116)
         for layer in self.layers:
             h_V = layer(h_V, ei, h_E)
         out = self.pool(_merge(*h_V), batch.batch, getattr(batch, "num_graphs", None))

@@ -552,6 +552,30 @@ int gmp_gvp_layer_bwd_agg_f32(int64_t n_edges, int64_t n_nodes, int reduce, cons
                               float* ds_in, float* dv_in, float* dspre, float* spre,
                               float* dgate, float* vn, float* vh, float* dvpre, float* dvh,
                               void* stream);
+/* gmp_gvp_edge_embed_{fwd,bwd}_f32 (K1e): the GVP-GNN edge embedding W_e (models/gvpgnn.py:73-77,
+ * :116) = LayerNorm((R, 1)) then GVP((R, 1), (so, 1), activations (None, None), vector_gate,
+ * h_dim 1) (gvp_layer.py:101-170, :221-243) over E edge rows: radial (E, R) row-major 16-byte
+ * aligned, unit (E, 3); parameters ln_w, ln_b (R) [the LayerNorm's weight / bias, eps], wh (1)
+ * [wh.weight], Ws (so, R + 1) [ws.weight], bs (so), wv (1) [wv.weight], wsv (so) [wsv.weight],
+ * bsv (1).  Forward: es (E, so), ev (E, 3) [= (E, 1, 3)].  Backward: the parameters' gradients
+ * from grad_es (E, so), grad_ev (E, 3) (radial / unit get none: positions without
+ * requires_grad), packed in grad_params as [ln_w R | ln_b R | wh 1 | Ws so (R + 1) | bs so |
+ * wv 1 | wsv so | bsv 1] (2R + 3 + so (R + 3) floats); per-workgroup partial rows in the
+ * workspace, added in a fixed order (deterministic).  R = 8 and 1 <= so <= 32 are compiled
+ * (GMP_ERR_UNSUPPORTED otherwise: the caller runs the module chain). */
+int gmp_gvp_edge_embed_fwd_f32(int64_t n_edges, int64_t radial_dim, int64_t so,
+                               const float* radial, const float* unit, const float* ln_w,
+                               const float* ln_b, const float* wh, const float* Ws,
+                               const float* bs, const float* wv, const float* wsv,
+                               const float* bsv, float eps, float* es, float* ev, void* stream);
+size_t gmp_gvp_edge_embed_bwd_workspace_size(int64_t n_edges);
+int gmp_gvp_edge_embed_bwd_f32(int64_t n_edges, int64_t radial_dim, int64_t so,
+                               const float* radial, const float* unit, const float* ln_w,
+                               const float* ln_b, const float* wh, const float* Ws,
+                               const float* bs, const float* wv, const float* wsv,
+                               const float* bsv, float eps, const float* grad_es,
+                               const float* grad_ev, float* grad_params, void* workspace,
+                               size_t workspace_bytes, void* stream);
 int gmp_gvp_msg0_fwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
                          const float* P, const float* Q, const float* es, const float* ev,
                          const float* We, const float* Wn, const float* b, const float* Wv,

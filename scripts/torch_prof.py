@@ -46,3 +46,8 @@ rows.sort(key=lambda e: -e.count)
 for e in rows[:45]:
     dt = getattr(e, "device_time_total", 0.0) or getattr(e, "cuda_time_total", 0.0)
     print(f"{e.count:4d} {dt:9.1f}us {e.key:18s} {str(e.input_shapes)[:100]}")
+print("--- top ops by self device time (all ops, grouped by input shape)")
+allr = [e for e in tab if (getattr(e, "self_device_time_total", 0.0) or 0.0) > 0]
+allr.sort(key=lambda e: -e.self_device_time_total)
+for e in allr[:50]:
+    print(f"{e.count:4d} {e.self_device_time_total:9.1f}us {e.key[:40]:40s} {str(e.input_shapes)[:90]}")

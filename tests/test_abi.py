@@ -61,7 +61,7 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
                  "edge_outer_sum_ex2", "edge_outer_sum_act", "gvp_layer_fwd", "gvp_layer_bwd",
                  "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd",
                  "gvp_layer_fwd_agg", "gvp_layer_bwd_agg", "gvp_msg0_bwd_agg",
-                 "symmetric_contraction_fwd",
+                 "gvp_edge_embed_fwd", "gvp_edge_embed_bwd", "symmetric_contraction_fwd",
                  "symmetric_contraction_bwd"):
         assert hasattr(tops, name), name
     with pytest.raises(RuntimeError, match="HIP device"):
@@ -82,6 +82,13 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
     sa, va = tops.gvp_layer_fwd_agg(s, v, W, torch.empty(1000, **i64), torch.empty(1000, **i64),
                                     torch.empty(301, **i64), 300, "mean")
     assert tuple(sa.shape) == (300, 128) and tuple(va.shape) == (300, 16, 3)
+    # K1e edge embedding: es (E, so), ev (E, 1, 3); packed parameter gradients (2R + 3 + so (R + 3))
+    We = [torch.empty(*sh, device="meta") for sh in ((8,), (8,), (1, 1), (32, 9), (32,), (1, 1),
+                                                    (1, 32), (1,))]
+    rad, unit = torch.empty(700, 8, device="meta"), torch.empty(700, 3, device="meta")
+    es, ev = tops.gvp_edge_embed_fwd(rad, unit, We, 1e-5)
+    assert tuple(es.shape) == (700, 32) and tuple(ev.shape) == (700, 1, 3)
+    assert tuple(tops.gvp_edge_embed_bwd(rad, unit, We, 1e-5, es, ev).shape) == (371,)
     # K8 on a term plan: out (N, rows C), partials (groups, T, C)
     x = torch.empty(50, 8, 9, device="meta")
     plan = torch.empty(3 * 9 + 1 + 40, dtype=torch.int32, device="meta")

@@ -392,3 +392,80 @@ def test_gvp_msg0_bwd_agg_matches_unfused():
         want, _ = ops.segment_reduce(src, rcsr, "sum")
         _scaled(got[k], want, 1e-6, f"receiver sum {k}")
     assert bool((got[9][rcsr.counts() == 0] == 0).all())
+
+
+@pytest.mark.parametrize("E,so", [(200_000, 32), (1000, 16), (5, 32), (0, 32)])
+def test_gvp_edge_embed_vs_oracle(E, so):
+    """K1e (gmp_gvp_edge_embed_{fwd,bwd}_f32): W_e = LayerNorm((8, 1)) + GVP((8, 1), (so, 1))
+    (gvpgnn.py:73-77) against the oracle modules in fp64 on the same parameters (random LayerNorm
+    affine, a negative wh, some zero-length unit rows): es / ev within 1e-5, every parameter
+    gradient within 1e-5 of its scale (E-row sums); bitwise repeatable."""
+    import gmp_amd.gvp as g
+    torch.manual_seed(E + so)
+    ref = torch.nn.Sequential(ogvp.LayerNorm((8, 1)),
+                              ogvp.GVP((8, 1), (so, 1), activations=(None, None),
+                                       vector_gate=True))
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(torch.randn_like(p) * 0.5)
+        ref[1].wh.weight.fill_(-0.8)
+    mod = torch.nn.Sequential(g.LayerNorm((8, 1)),
+                              g.GVP((8, 1), (so, 1), activations=(None, None), vector_gate=True))
+    mod.load_state_dict(ref.state_dict(), strict=True)
+    mod = mod.to(DEV)
+    rad = torch.rand(E, 8) * 2
+    unit = torch.nn.functional.normalize(torch.randn(E, 3), dim=-1)
+    unit[::97] = 0.0                                      # zero-length edges
+    des, dev = torch.randn(E, so), torch.randn(E, 1, 3)
+    assert g._edge_embed_ok(mod, rad.to(DEV), unit.to(DEV))
+
+    def fused():
+        mod.zero_grad(set_to_none=True)
+        es, ev = g.edge_embed(mod, rad.to(DEV), unit.to(DEV))
+        ((es * des.to(DEV)).sum() + (ev * dev.to(DEV)).sum()).backward()
+        return es, ev, {k: p.grad.clone() for k, p in mod.named_parameters() if p.numel()}
+
+    es, ev, gr = fused()
+    ref64 = copy.deepcopy(ref).double()
+    es_r, ev_r = ref64((rad.double(), unit.double().unsqueeze(-2)))
+    ((es_r * des.double()).sum() + (ev_r * dev.double()).sum()).backward()
+    assert es.shape == (E, so) and ev.shape == (E, 1, 3)
+    if E:
+        torch.testing.assert_close(es.cpu().double(), es_r.detach(), atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(ev.cpu().double(), ev_r.detach(), atol=1e-5, rtol=1e-5)
+    for k, p in ref64.named_parameters():
+        if p.numel():
+            _scaled(gr[k].double(), p.grad, 1e-5, k)
+    es2, ev2, gr2 = fused()
+    assert torch.equal(es, es2) and torch.equal(ev, ev2)
+    assert all(torch.equal(gr[k], gr2[k]) for k in gr)
+
+
+def test_gvp_model_c3_edge_embed_fused_vs_chain():
+    """The C3 model with positions without requires_grad (the bench step) takes K1e; its loss and
+    every parameter gradient match the module chain (EDGE_EMBED_FUSED = False) within 1e-5 of
+    scale."""
+    import gmp_amd.gvp as g
+    from gmp_amd.graph import Batch, radius_graph
+    torch.manual_seed(12)
+    gr = radius_graph(num_nodes=600, target_edges=9000, r=2.0, seed=5, tol=0.2, shuffle=True)
+    model = g.GVPGNNModel(r_max=2.0, in_dim=1, out_dim=1, **C3).to(DEV).eval()
+    b = Batch(gr.atoms.to(DEV), gr.pos.to(DEV), gr.edge_index.to(DEV))
+
+    def run(fused):
+        g.EDGE_EMBED_FUSED = fused
+        try:
+            model.zero_grad(set_to_none=True)
+            y = model(b)
+            y.sum().backward()
+        finally:
+            g.EDGE_EMBED_FUSED = True
+        return y.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()
+                                    if p.grad is not None}
+
+    y1, g1 = run(True)
+    y0, g0 = run(False)
+    torch.testing.assert_close(y1, y0, atol=1e-5, rtol=1e-5)
+    assert set(g1) == set(g0)
+    for k in g0:
+        _scaled(g1[k], g0[k], 1e-5, k)
