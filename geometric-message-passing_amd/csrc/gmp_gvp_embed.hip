@@ -37,7 +37,6 @@ constexpr int kEmbAcc = kEmbR + 4;         // per-channel accumulators A[R], dbs
 constexpr int kEmbPart = kEmbSO * kEmbAcc + 3;  // + dbsv, dwv, T1
 constexpr int kEmbStepsPerBlock = 16;      // forward: edge steps (8 edges each) per workgroup
 constexpr int kEmbFinT = 1024;             // finishing kernel threads
-constexpr int kEmbFinSlices = 8;           // partial rows split in 8 ordered slices
 
 struct EmbedW {
   const float *ln_w, *ln_b, *wh, *Ws, *bs, *wv, *wsv, *bsv;
@@ -207,25 +206,42 @@ __global__ __launch_bounds__(kEmbT) void gvp_embed_bwd_kernel(int64_t E, int so,
 }
 
 // packed gradient layout (gmp.h): [ln_w R | ln_b R | wh 1 | Ws SO x (R+1) | bs SO | wv 1 |
-// wsv SO | bsv 1]
+// wsv SO | bsv 1].  16 waves, wave w adding rows w, w + 16, .. (4 rows of loads in flight per
+// lane, lane owning columns lane + 64 k), the waves' sums added in wave order: deterministic.
+constexpr int kEmbFinW = kEmbFinT / 64;
+constexpr int kEmbFinC = (kEmbPart + 63) / 64;  // columns per lane
 __global__ __launch_bounds__(kEmbFinT) void gvp_embed_finish_kernel(int64_t G, int so, EmbedW W,
                                                                     const float* __restrict__ part,
                                                                     float* __restrict__ grad) {
-  __shared__ float sl[kEmbFinSlices][kEmbPart];
-  __shared__ float tot[kEmbPart];
-  const int64_t q = (G + kEmbFinSlices - 1) / kEmbFinSlices;
-  for (int j = threadIdx.x; j < kEmbFinSlices * kEmbPart; j += kEmbFinT) {
-    const int sli = j / kEmbPart, col = j - sli * kEmbPart;
-    const int64_t g0 = sli * q, g1 = (g0 + q < G) ? g0 + q : G;
-    float s = 0.f;
-    for (int64_t g = g0; g < g1; ++g) s += part[g * kEmbPart + col];
-    sl[sli][col] = s;
+  __shared__ float sl[kEmbFinW][kEmbFinC * 64];
+  __shared__ float tot[kEmbFinC * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float acc[kEmbFinC];
+#pragma unroll
+  for (int k = 0; k < kEmbFinC; ++k) acc[k] = 0.f;
+  for (int64_t g0 = w; g0 < G; g0 += 4 * kEmbFinW) {
+    float v[4][kEmbFinC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t g = g0 + (int64_t)u * kEmbFinW;
+#pragma unroll
+      for (int k = 0; k < kEmbFinC; ++k) {
+        const int col = lane + 64 * k;
+        v[u][k] = (g < G && col < kEmbPart) ? part[g * kEmbPart + col] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < kEmbFinC; ++k) acc[k] += v[u][k];
   }
+#pragma unroll
+  for (int k = 0; k < kEmbFinC; ++k) sl[w][lane + 64 * k] = acc[k];
   __syncthreads();
   for (int t = threadIdx.x; t < kEmbPart; t += kEmbFinT) {
     float s = sl[0][t];
 #pragma unroll
-    for (int k = 1; k < kEmbFinSlices; ++k) s += sl[k][t];
+    for (int k = 1; k < kEmbFinW; ++k) s += sl[k][t];
     tot[t] = s;
   }
   __syncthreads();
@@ -269,8 +285,8 @@ __global__ __launch_bounds__(kEmbFinT) void gvp_embed_finish_kernel(int64_t G, i
 }
 
 int64_t embed_bwd_blocks(int64_t E) {
-  // four 4-wave workgroups per CU; >= 64 edges per workgroup
-  int64_t g = 4 * (int64_t)device_cu_count();
+  // two 4-wave workgroups per CU (fewer partial rows for the finishing kernel); >= 64 edges each
+  int64_t g = 2 * (int64_t)device_cu_count();
   if (g * 64 > E) g = ceil_div(E, 64);
   return g < 1 ? 1 : g;
 }

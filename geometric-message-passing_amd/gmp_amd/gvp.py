@@ -256,13 +256,11 @@ def _layer_wgrads(needs_input_grad, first, s, v, W, dspre, dgate, vn, vh, dvpre,
         Gx, dbsv = torch.empty((16, 144), **f), torch.empty(16, **f)
         ops.outer_sum_into2(dgate, s.view(E, 128), vn, Gx, dbsv)
         dWsv = torch.addmm(torch.outer(dbsv, W[1]), Gx, W[0].t())
-        # dWh from dvh^T v; dWv = sum_(e,x) dvpre[e, o, x] vh[e, h, x] with vh = Wh v:
-        # (dvpre^T v) Wh^T, so the kernel does not write the (E, 48) vh rows (gmp.h
-        # gmp_gvp_layer_bwd_f32).  Both products in one pass over v: v^T [dvh | dvpre]
-        Cv = torch.empty((48, 96), **f)
-        ops.outer_sum_into2(v.reshape(E, 48), dvh, dvpre, Cv)
-        dWh = _diag3(Cv[:, :48].t(), 16, 16)
-        dWv = _diag3(Cv[:, 48:].t(), 16, 16).mm(W[4].t())
+        dWh = _diag3(_osum(dvh, v.reshape(E, 48))[0], 16, 16)
+        # dWv = sum_(e,x) dvpre[e, o, x] vh[e, h, x] with vh = Wh v: (sum dvpre (x) v) Wh^T, so
+        # the kernel does not write the (E, 48) vh rows (gmp.h gmp_gvp_layer_bwd_f32).  (r05: the
+        # two products as one x3 pass v^T [dvh | dvpre] measured 331 us against 2 x ~130 us)
+        dWv = _diag3(_osum(dvpre, v.reshape(E, 48))[0], 16, 16).mm(W[4].t())
     grads = (dWs, dbs, dWsv, dbsv, dWh, dWv)
     return sw.deliver(needs_input_grad, first, W, grads)
 
