@@ -1097,6 +1097,65 @@ int rect_bucket(int64_t m, int64_t n) {
   return 0;
 }
 
+// out[c] = sum_e sum_x A[e, 3c + x] v[e, x] for A (E, 3C) contiguous, v (E, 3): the xyz
+// contractions of per-edge vector gradients with the edge vectors in the GVP first-message
+// weight sums (u = sum dvpre . ev, dwev = sum dvh . ev).  A workgroup streams tiles of kXdRows
+// whole rows as float4s (kXdRows x W3 / 4 / kXdT float4 per thread): the (thread, slot) ->
+// column map is the same in every tile, so each thread accumulates fixed columns in registers;
+// the tile rows are then added per column in row order through LDS, the three x of a column
+// group in order: one partial row of C floats per workgroup (deterministic), summed by
+// sum_partials.
+constexpr int kXdT = 256, kXdRows = 64;
+template <int W3>
+__global__ __launch_bounds__(kXdT) void xyz_dot_kernel(const float* __restrict__ A,
+                                                       const float* __restrict__ v, int64_t E,
+                                                       int64_t per, float* __restrict__ part) {
+  constexpr int U = kXdRows * W3 / 4 / kXdT;  // float4 per thread per tile
+  static_assert(kXdRows * W3 % (4 * kXdT) == 0, "tile must split into whole float4 per thread");
+  __shared__ float sT[kXdRows][W3];
+  const int t = threadIdx.x;
+  f32x4 acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t k0 = (int64_t)blockIdx.x * per;
+  const int64_t k1 = (k0 + per < E) ? k0 + per : E;
+  for (int64_t r0 = k0; r0 < k1; r0 += kXdRows) {
+    f32x4 a[U];
+    float w[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = t + kXdT * u, row = 4 * f / W3, col = 4 * f - row * W3;
+      const int64_t e = r0 + row;
+      const bool ok = e < k1;
+      a[u] = ok ? *reinterpret_cast<const f32x4*>(A + e * W3 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int64_t ec = ok ? e : k0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[u][i] = v[3 * ec + (col + i) % 3];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[u][i] += a[u][i] * w[u][i];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int f = t + kXdT * u, row = 4 * f / W3, col = 4 * f - row * W3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sT[row][col + i] = acc[u][i];
+  }
+  __syncthreads();
+  if (t < W3 / 3) {
+    float s = 0.f;
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      float c = 0.f;
+      for (int r = 0; r < kXdRows; ++r) c += sT[r][3 * t + x];
+      s += c;
+    }
+    part[(int64_t)blockIdx.x * (W3 / 3) + t] = s;
+  }
+}
+
 int64_t blocks_for(int64_t K) {
   int64_t g = (int64_t)device_cu_count() * 2;  // two resident workgroups per CU
   // >= 16 edge tiles per workgroup: a node-level sum (K = 50k rows) then takes ~100 CUs and
@@ -1412,6 +1471,33 @@ int gmp_outer_sum_cols_f32(int64_t K, int64_t m_total, int64_t n, const float* A
   const int64_t X = m * n + m;
   sum_partials_cols<<<dim3((unsigned)ceil_div(m * n, 256), (unsigned)Y), 256, 0, s>>>(
       part, Gr, X, (int)m, (int)n, C, ldc);
+  return launch_status();
+}
+
+size_t gmp_edge_xyz_dot_workspace_size(int64_t K) {
+  return (size_t)(2 * device_cu_count()) * 48 * sizeof(float);
+}
+
+int gmp_edge_xyz_dot_f32(int64_t K, int64_t C, const float* A, const float* v, float* out,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  GMP_CHECK_ARG(K >= 0 && out);
+  if (!(C == 16 || C == 48)) return GMP_ERR_UNSUPPORTED;
+  hipStream_t s = as_stream(stream);
+  if (K == 0) return hip_check(hipMemsetAsync(out, 0, C * sizeof(float), s));
+  GMP_CHECK_ARG(A && v && workspace);
+  GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(A) % 16 == 0);
+  if (workspace_bytes < gmp_edge_xyz_dot_workspace_size(K)) return GMP_ERR_WORKSPACE;
+  int64_t G = 2 * (int64_t)device_cu_count();
+  const int64_t per = ceil_div(ceil_div(K, G), (int64_t)kXdRows) * kXdRows;
+  G = ceil_div(K, per);
+  float* part = reinterpret_cast<float*>(workspace);
+  if (C == 48)
+    xyz_dot_kernel<144><<<(unsigned)G, kXdT, 0, s>>>(A, v, K, per, part);
+  else
+    xyz_dot_kernel<48><<<(unsigned)G, kXdT, 0, s>>>(A, v, K, per, part);
+  int rc = launch_status();
+  if (rc) return rc;
+  sum_partials(part, G, C, out, nullptr, C, C, C, s);
   return launch_status();
 }
 

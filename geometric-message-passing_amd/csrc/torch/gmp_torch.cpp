@@ -1022,6 +1022,26 @@ Tensor outer_sum_cols(const Tensor& A, const Tensor& B) {
 }
 
 // ------------------------------------------------------------------ edge outer sums (K5)
+// out[c] = sum_(e,x) A[e, 3c + x] v[e, x]  (A (K, 3C), v (K, 3); C = 16 or 48)
+Tensor edge_xyz_dot(const Tensor& A_, const Tensor& v_) {
+  OpGuard g(A_, "edge_xyz_dot");
+  f32(A_, "A");
+  f32(v_, "v");
+  TORCH_CHECK(A_.dim() == 2 && A_.size(1) % 3 == 0, "gmp.edge_xyz_dot: A must be (K, 3C)");
+  const int64_t K = A_.size(0), C = A_.size(1) / 3;
+  numel(v_, K * 3, "v");
+  Tensor A = A_.contiguous(), v = v_.contiguous();
+  Tensor out = at::empty({C}, A.options());
+  const size_t ws_b = gmp_edge_xyz_dot_workspace_size(K);
+  Tensor ws = at::empty({(int64_t)ws_b + 1}, A.options().dtype(at::kByte));
+  const int rc = gmp_edge_xyz_dot_f32(K, C, fp(A), fp(v), fp(out), ws.data_ptr(), ws_b,
+                                      cur_stream());
+  if (rc == GMP_ERR_UNSUPPORTED)
+    return (A.view({K, C, 3}) * v.view({K, 1, 3})).sum(at::IntArrayRef{0, 2});
+  check_rc(rc, "gmp_edge_xyz_dot_f32");
+  return out;
+}
+
 std::tuple<Tensor, Tensor> edge_outer_sum(const Tensor& A, const Tensor& B) {
   OpGuard g(A, "edge_outer_sum");
   f32(A, "A");
@@ -1534,6 +1554,9 @@ std::tuple<Tensor, Tensor> ln_act_bwd(const Tensor&, const Tensor& xhat, const T
                                       const Tensor&, const Tensor&, int64_t) {
   return {at::empty_like(xhat), at::empty({2 * xhat.size(-1)}, xhat.options())};
 }
+Tensor edge_xyz_dot(const Tensor& A, const Tensor&) {
+  return at::empty({A.size(1) / 3}, A.options());
+}
 Tensor vec_norm_fwd(const Tensor& v) { return at::empty_like(v); }
 Tensor vec_norm_bwd(const Tensor& v, const Tensor&) { return at::empty_like(v); }
 Tensor xyz_norm_fwd(const Tensor& vh) { return at::empty({vh.size(0), vh.size(2)}, vh.options()); }
@@ -1804,6 +1827,7 @@ TORCH_LIBRARY(gmp, m) {
         "Tensor rowptr, int n_nodes, str reduce) -> (Tensor s_agg, Tensor v_agg)");
   m.def("gvp_layer_bwd_agg(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, Tensor index, "
         "Tensor rowptr, str reduce, bool relu, bool want_factors=True) -> Tensor[]");
+  m.def("edge_xyz_dot(Tensor A, Tensor v) -> Tensor");
   m.def("gvp_edge_embed_fwd(Tensor radial, Tensor unit, Tensor[] W, float eps) "
         "-> (Tensor es, Tensor ev)");
   m.def("gvp_edge_embed_bwd(Tensor radial, Tensor unit, Tensor[] W, float eps, Tensor grad_es, "
@@ -1832,6 +1856,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("ssp_bwd", ns ssp_bwd);                                          \
   m.impl("ln_act_fwd", ns ln_act_fwd);                                    \
   m.impl("ln_act_bwd", ns ln_act_bwd);                                    \
+  m.impl("edge_xyz_dot", ns edge_xyz_dot);                                \
   m.impl("gvp_edge_embed_fwd", ns gvp_edge_embed_fwd);                    \
   m.impl("gvp_edge_embed_bwd", ns gvp_edge_embed_bwd);                    \
   m.impl("vec_norm_fwd", ns vec_norm_fwd);                                \

@@ -135,6 +135,8 @@ SIGNATURES = {
     "gmp_edge_outer_sum_ex_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_int,
                                           c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
     "gmp_edge_outer_sum_rect_workspace_size": (c_size, [c_i64, c_i64, c_i64]),
+    "gmp_edge_xyz_dot_workspace_size": (c_size, [c_i64]),
+    "gmp_edge_xyz_dot_f32": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "gmp_edge_outer_sum_rect_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_size, c_vp]),
     "gmp_tp_node_outer_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

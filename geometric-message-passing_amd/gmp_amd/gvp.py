@@ -362,12 +362,12 @@ class GvpMsg0Fn(torch.autograd.Function):
             Sv = torch.cat([ops.segment_reduce(dvpre, send_csr, "sum")[0], sv_i], 0)  # (2N, 48)
             Qab = Q.view(n, 2, 144).transpose(0, 1).reshape(2 * n, 144)      # [Qa ; Qb]
             dWv = _diag3(_osum(Sv, Qab)[0], 16, 48)
-            ev16 = torch.nn.functional.pad(ev, (0, 13))
-            Mu, _ = _osum(ev16, dvpre)                                       # (16, 48)
-            u = Mu[:3].reshape(3, 16, 3).diagonal(dim1=0, dim2=2).sum(-1)    # (16,)
+            # u[o] = sum_(e,x) dvpre[e, o, x] ev[e, x], dwev[h] = sum_(e,x) dvh[e, h, x] ev[e, x]:
+            # one pass over each (gmp_edge_xyz_dot_f32)
+            xdot = _lib.torch_ops().edge_xyz_dot
+            u = xdot(dvpre, ev)                                              # (16,)
             dWv.add_(torch.outer(u, W[6]))
-            M, _ = _osum(ev16, dvh)  # (16, 144): rows x = 0..2
-            dwev = M[:3].reshape(3, 48, 3).diagonal(dim1=0, dim2=2).sum(-1)
+            dwev = xdot(dvh, ev)                                             # (48,)
             gWs0 = torch.zeros_like(Ws0)
             gWs0[:, 128:160] = dWe
             gWs0[:, 288:288 + vi] = dWn[:, :vi]

@@ -256,6 +256,14 @@ int gmp_edge_outer_sum_act_hf_f32(int64_t K, int64_t d, const float* A, const fl
  * C (m x n) = A^T B, A (K, m), B (K, n) row-major, m, n multiples of 16, m <= 256,
  * (m/16)(n/16) <= 72; colsum_A (m) optional.  Same deterministic split-K reduction. */
 size_t gmp_edge_outer_sum_rect_workspace_size(int64_t K, int64_t m, int64_t n);
+/* gmp_edge_xyz_dot_f32 (r05): out[c] = sum_e sum_x A[e, 3c + x] v[e, x] for A (K, 3C) contiguous
+ * 16-byte aligned, v (K, 3), C in {16, 48} (GMP_ERR_UNSUPPORTED otherwise): the xyz
+ * contractions of the GVP first message's weight sums (sum dvpre . ev, sum dvh . ev,
+ * gvp_layer.py:101-170 through the e_v column of W_h) in one pass over A; per-workgroup partial
+ * rows in the workspace, added in a fixed order (deterministic). */
+size_t gmp_edge_xyz_dot_workspace_size(int64_t K);
+int gmp_edge_xyz_dot_f32(int64_t K, int64_t C, const float* A, const float* v, float* out,
+                         void* workspace, size_t workspace_bytes, void* stream);
 int gmp_edge_outer_sum_rect_f32(int64_t K, int64_t m, int64_t n, const float* A, const float* B,
                                 float* C, float* colsum_A, void* workspace,
                                 size_t workspace_bytes, void* stream);

@@ -61,7 +61,8 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
                  "edge_outer_sum_ex2", "edge_outer_sum_act", "gvp_layer_fwd", "gvp_layer_bwd",
                  "gvp_msg0_fwd", "gvp_msg0_bwd", "tp_conv_fwd", "tp_conv_bwd",
                  "gvp_layer_fwd_agg", "gvp_layer_bwd_agg", "gvp_msg0_bwd_agg",
-                 "gvp_edge_embed_fwd", "gvp_edge_embed_bwd", "symmetric_contraction_fwd",
+                 "gvp_edge_embed_fwd", "gvp_edge_embed_bwd", "edge_xyz_dot",
+                 "symmetric_contraction_fwd",
                  "symmetric_contraction_bwd"):
         assert hasattr(tops, name), name
     with pytest.raises(RuntimeError, match="HIP device"):
@@ -89,6 +90,7 @@ def test_torch_ops_registered_and_reject_cpu_tensors():
     es, ev = tops.gvp_edge_embed_fwd(rad, unit, We, 1e-5)
     assert tuple(es.shape) == (700, 32) and tuple(ev.shape) == (700, 1, 3)
     assert tuple(tops.gvp_edge_embed_bwd(rad, unit, We, 1e-5, es, ev).shape) == (371,)
+    assert tuple(tops.edge_xyz_dot(torch.empty(700, 144, device="meta"), unit).shape) == (48,)
     # K8 on a term plan: out (N, rows C), partials (groups, T, C)
     x = torch.empty(50, 8, 9, device="meta")
     plan = torch.empty(3 * 9 + 1 + 40, dtype=torch.int32, device="meta")

@@ -472,3 +472,19 @@ def test_gvp_model_c3_edge_embed_fused_vs_chain():
     assert set(g1) == set(g0)
     for k in g0:
         _scaled(g1[k], g0[k], 1e-4, k)
+
+
+@pytest.mark.parametrize("K,C", [(999_722, 48), (999_722, 16), (1000, 48), (77, 16), (0, 48)])
+def test_edge_xyz_dot(K, C):
+    """gmp_edge_xyz_dot_f32: out[c] = sum_(e,x) A[e, 3c + x] v[e, x] against fp64 torch, within
+    1e-5 of scale; bitwise repeatable (fixed-order partial rows)."""
+    from gmp_amd import _lib
+    torch.manual_seed(K + C)
+    A = torch.randn(K, 3 * C)
+    v = torch.randn(K, 3)
+    xdot = _lib.torch_ops().edge_xyz_dot
+    out = xdot(A.to(DEV), v.to(DEV))
+    ref = (A.double().view(K, C, 3) * v.double().view(K, 1, 3)).sum((0, 2))
+    assert out.shape == (C,)
+    _scaled(out.double(), ref, 1e-5, "xyz_dot")
+    assert torch.equal(out, xdot(A.to(DEV), v.to(DEV)))
