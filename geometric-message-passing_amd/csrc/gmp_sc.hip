@@ -238,8 +238,8 @@ int gmp_symmetric_contraction_fwd_f32(int64_t n_nodes, int channels, int dim, in
                                       int n_terms, const int32_t* plan, const float* coef,
                                       const float* x, float* out, void* stream) {
   GMP_CHECK_ARG(n_nodes >= 0 && shape_ok(channels, dim, rows, n_terms));
+  if (n_nodes == 0) return GMP_OK;  // (an empty batch's x / out may be NULL)
   GMP_CHECK_ARG(plan && x && out && (n_terms == 0 || coef));
-  if (n_nodes == 0) return GMP_OK;
   const int CT = channels < kMaxCT ? channels : kMaxCT;
   const size_t smem = (size_t)kSC * row_stride(dim) * sizeof(float);
   int rc;
@@ -255,9 +255,15 @@ int gmp_symmetric_contraction_bwd_f32(int64_t n_nodes, int channels, int dim, in
                                       const float* x, const float* gout, float* dx,
                                       float* dcoef_partials, void* stream) {
   GMP_CHECK_ARG(n_nodes >= 0 && shape_ok(channels, dim, rows, n_terms));
-  GMP_CHECK_ARG(plan && x && gout && (n_terms == 0 || coef || !dx));
-  if (n_nodes == 0) return GMP_OK;
   hipStream_t s = as_stream(stream);
+  if (n_nodes == 0) {
+    // an empty node batch (x / gout / dx may be NULL): the single partial group is all zeros
+    if (dcoef_partials && n_terms > 0)
+      return hip_check(
+          hipMemsetAsync(dcoef_partials, 0, (size_t)n_terms * channels * sizeof(float), s));
+    return GMP_OK;
+  }
+  GMP_CHECK_ARG(plan && x && gout && (n_terms == 0 || coef || !dx));
   int rc;
   if (dx) {
     const int CT = channels < kMaxCT ? channels : kMaxCT;

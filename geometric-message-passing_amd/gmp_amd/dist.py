@@ -12,10 +12,11 @@ def env_world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend="nccl"):
-    """Initialise the default process group from torchrun's env (MASTER_ADDR 127.0.0.1)."""
+def init(backend="nccl", force=False):
+    """Initialise the default process group from torchrun's env (MASTER_ADDR 127.0.0.1); at
+    WORLD_SIZE 1 only when `force` (a one-rank group: the collectives' code path on one GPU)."""
     rank, world, local = env_world()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

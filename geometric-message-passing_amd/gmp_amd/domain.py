@@ -104,6 +104,8 @@ def _exchange(x, send_counts, recv_counts):
     out = x.new_empty((sum(recv_counts),) + tuple(x.shape[1:]))
     if dist.get_backend() == "gloo":  # gloo has no all_to_all: pairwise send / recv
         rank, W = dist.get_rank(), dist.get_world_size()
+        if x.is_cuda:  # the gloo rehearsal of device tensors: pairwise transfers through host
+            return _exchange(x.cpu(), send_counts, recv_counts).to(x.device)
         sends = torch.split(x, send_counts)
         recvs = torch.split(out, recv_counts)
         ops = []

@@ -559,7 +559,21 @@ def _w2_path(W2, b2, P):
 
 
 def node_form_ok(hidden):
-    return hidden % 16 == 0 and hidden <= 256
+    """The node-form kernels take any radial hidden width H <= 256: a width that is not a
+    multiple of 32 runs zero-padded (`_node_radial`)."""
+    return 0 < hidden <= 256
+
+
+def _node_radial(fc):
+    """fc's W1, b1, W2, b2 for the node form, the hidden width zero-padded to a multiple of 32
+    (the kernels' 16-wide MFMA k steps, and K7g's 32-deep ones): padded units have zero W1 rows
+    and bias, so relu(0) = 0 contributes nothing to S, T or the weight sums, and F.pad's
+    backward drops their gradient rows (tfn_layer.py:73-77 takes any mlp_dim)."""
+    W1, b1, W2, b2 = fc[0].weight, fc[0].bias, fc[2].weight, fc[2].bias
+    pad = -W1.shape[0] % 32
+    if pad:
+        W1, b1, W2 = F.pad(W1, (0, 0, 0, pad)), F.pad(b1, (0, pad)), F.pad(W2, (0, pad))
+    return W1, b1, W2, b2
 
 
 # Path GEMMs of the node form: "x3" = K7g (gmp_tpgemm.hip: bf16 MFMA over exact three-plane f32
@@ -788,12 +802,13 @@ class TensorProductConvLayer(nn.Module):
         # (a plain bool: torch.compile cannot trace `is` between autograd Function classes)
         if not node and self.plan.layout is None:
             raise NotImplementedError("the per-edge-weight TP kernels take l <= 2 layouts only; "
-                                      "use the node form (TP_MODE = \"node\", mlp_dim % 16 == 0)")
+                                      "use the node form (TP_MODE = \"node\", mlp_dim <= 256)")
         paths, cg = self._tp_paths, self._tp_cg
         if paths.device != node_attr.device or cg.dtype != torch.float32:
             paths, cg = self.plan.device_tables(node_attr.device)
-        out = fn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight, self.fc[0].bias,
-                       self.fc[2].weight, self.fc[2].bias, self.plan, graph, paths, cg)
+        fcw = (_node_radial(self.fc) if node else
+               (self.fc[0].weight, self.fc[0].bias, self.fc[2].weight, self.fc[2].bias))
+        out = fn.apply(node_attr, edge_sh, edge_feat, *fcw, self.plan, graph, paths, cg)
         if self.aggr == "mean":
             out = out / graph.recv_csr.counts().clamp(min=1).unsqueeze(1).to(out.dtype)
         elif self.aggr not in ("add", "sum"):
@@ -816,7 +831,7 @@ class TensorProductConvLayer(nn.Module):
         in-degree times more (not a benchmark path)."""
         if not node_form_ok(self.fc[0].out_features):
             raise NotImplementedError(f"aggr={self.aggr}: the node-form kernels need "
-                                      "mlp_dim % 16 == 0 and <= 256")
+                                      "mlp_dim <= 256")
         E = edge_index.shape[1]
         ar = torch.arange(E, device=edge_index.device, dtype=edge_index.dtype)
         ei_e = torch.stack([ar, edge_index[1]])
@@ -824,9 +839,8 @@ class TensorProductConvLayer(nn.Module):
         paths, cg = self._tp_paths, self._tp_cg
         if paths.device != node_attr.device or cg.dtype != torch.float32:
             paths, cg = self.plan.device_tables(node_attr.device)
-        msg = TPConvNodeFn.apply(node_attr, edge_sh, edge_feat, self.fc[0].weight,
-                                 self.fc[0].bias, self.fc[2].weight, self.fc[2].bias, self.plan,
-                                 graph, paths, cg)
+        msg = TPConvNodeFn.apply(node_attr, edge_sh, edge_feat, *_node_radial(self.fc),
+                                 self.plan, graph, paths, cg)
         out = scatter(msg, edge_index[0], dim=0, dim_size=node_attr.shape[0], reduce=self.aggr)
         return self._epilogue(out)
 
@@ -942,7 +956,7 @@ def fold_symmetric(A, nu):
     return Ap[..., idx].sum(-1)
 
 
-_K8_MAX_DIM, _K8_MAX_ROWS = 63, 255
+_K8_MAX_DIM, _K8_MAX_ROWS, _K8_MAX_CORR = 63, 255, 4
 
 
 def k8_plan(contractions, D, C, correlation):
@@ -952,6 +966,8 @@ def k8_plan(contractions, D, C, correlation):
     -- in row order, monomials ascending within a row.  Returns (plan int32, gather int64): coef
     (T, C) = the rows `gather` of cat_nu(A~_nu) (C, M, NQ) flattened over (m, q) and transposed."""
     import itertools
+    # the term word holds four 6-bit factor fields (gmp_sc.hip): degree <= 4
+    assert 1 <= correlation <= _K8_MAX_CORR, "K8 term words hold at most 4 factors"
     masks, nq = [], []
     for nu in range(1, correlation + 1):
         rows = []
@@ -1005,9 +1021,12 @@ class SymmetricContraction(nn.Module):
         o3.clear_cg_cache()
         M = sum(2 * l + 1 for _, (l, _) in self.irreps_out)
         # K8 takes any irreps with C channels each (x (N, C, D) is reshape_irreps' layout; the
-        # reference's Contraction needs the same, symmetric_contraction.py:102), D <= 63, M <= 255
+        # reference's Contraction needs the same, symmetric_contraction.py:102), D <= 63, M <= 255,
+        # correlation 1..4 (four factor fields per term word); higher correlations run the
+        # per-irrep torch contraction
         self._k8 = (all(m == C for m, _ in irreps_in) and all(m == C for m, _ in self.irreps_out)
-                    and D <= _K8_MAX_DIM and M <= _K8_MAX_ROWS and correlation >= 1)
+                    and D <= _K8_MAX_DIM and M <= _K8_MAX_ROWS
+                    and 1 <= correlation <= _K8_MAX_CORR)
         if self._k8:
             plan, gather = k8_plan(list(self.contractions.values()), D, C, correlation)
             self.register_buffer("_k8_plan", plan, persistent=False)

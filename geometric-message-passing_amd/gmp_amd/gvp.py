@@ -566,7 +566,10 @@ class GVPConv(MessagePassing):
         Q = NodeVecProjFn.apply(v, Wh0, 16)                                  # (N, 288)
         es, ev = edge_attr
         ei = edge_index
-        send_csr, recv_csr = ops.get_csr(ei[0], n), ops.get_csr(ei[1], n)
+        # range-checked once per graph (one host sync, as index_select / torch_scatter raise):
+        # the receiver-sorted kernels visit only in-range edges, so an out-of-range index would
+        # leave rows of the per-edge outputs unwritten
+        send_csr, recv_csr = ops.checked_csr(ei[0], n), ops.checked_csr(ei[1], n)
         s1, v1 = GvpMsg0Fn.apply(P, Q, es, ev.reshape(-1, 3), Ws0, g0.ws.bias, g0.wv.weight,
                                  g0.wsv.weight, g0.wsv.bias, Wh0, send_csr, recv_csr, ei)
         s2, v2 = GvpLayerFn.apply(s1, v1, g1.ws.weight, g1.ws.bias, g1.wsv.weight, g1.wsv.bias,

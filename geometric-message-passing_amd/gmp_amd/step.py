@@ -24,9 +24,11 @@ import torch.distributed as dist
 
 
 def _dist_world():
+    """World size of the initialised process group, or 0 when there is none (a one-rank group
+    still runs the collectives: RCCL's one-rank all-reduce is the same code path)."""
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size()
-    return 1
+    return 0
 
 
 class GraphedStep:
@@ -42,7 +44,7 @@ class GraphedStep:
         self.world = _dist_world()
         self.use_graph = use_graph
         self.params = [p for p in model.parameters() if p.requires_grad]
-        if self.world > 1:
+        if self.world:
             with torch.no_grad():
                 for p in model.parameters():
                     dist.broadcast(p, 0)
@@ -62,7 +64,7 @@ class GraphedStep:
         return loss
 
     def _allreduce(self):
-        if self.world == 1:
+        if not self.world:
             return
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
         for p, g in zip(self.params, grads):
@@ -92,9 +94,9 @@ class GraphedStep:
         with torch.cuda.graph(self.graph):
             self.loss = self.loss_fn()
             self.loss.backward()
-            if self.world == 1:
+            if not self.world:
                 self.opt.step()
-        if self.world > 1:
+        if self.world:
             # grads are static tensors now; the all-reduce runs eagerly between the graphs
             for p in self.params:
                 if p.grad is None:
@@ -108,7 +110,7 @@ class GraphedStep:
             self._eager()
             return self.loss
         self.graph.replay()
-        if self.world > 1:
+        if self.world:
             self._allreduce()
             self.graph_opt.replay()
         return self.loss

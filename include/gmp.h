@@ -737,7 +737,8 @@ int gmp_xyz_norm_bwd_f32(int64_t rows, int64_t h, const float* vh, const float* 
  *   sum_k U_nu[m, p, k] W_nu[k, c] (the host builds the plan once and coef per call,
  *   differentiably).  out (N, rows C).
  * Backward: dx (N, C, D) (may be NULL) and dcoef partials (gmp_sc_groups(N), n_terms, C) (may
- * be NULL; the caller sums the groups in order).  Deterministic.  (ABI 5: the plan form replaces
+ * be NULL; the caller sums the groups in order; N = 0 writes one all-zero group).
+ * Deterministic.  (ABI 5: the plan form replaces
  * the dense per-degree A_nu arguments and gmp_sc_monomials.)
  * ------------------------------------------------------------------------------------------ */
 int gmp_sc_groups(int64_t n_nodes);

@@ -29,8 +29,8 @@ def scatter(src, index, dim=0, dim_size=None, reduce="sum", out=None):
         if reduce in ("sum", "add", "mean"):
             r = o + scatter(src, index, dim, n, "sum").movedim(dim, 0)
             if reduce == "mean":
-                cnt = torch.zeros(n, dtype=src.dtype)
-                cnt.index_add_(0, index, torch.ones(index.shape[0], dtype=src.dtype))
+                cnt = torch.zeros(n, dtype=src.dtype, device=src.device)
+                cnt.index_add_(0, index, torch.ones(index.shape[0], dtype=src.dtype, device=src.device))
                 r = r / cnt.clamp(min=1).view((n,) + (1,) * (r.dim() - 1))
         else:
             idx = index.view((-1,) + (1,) * (x.dim() - 1)).expand_as(x)
@@ -41,19 +41,19 @@ def scatter(src, index, dim=0, dim_size=None, reduce="sum", out=None):
     x = src.movedim(dim, 0)
     shape = (n,) + tuple(x.shape[1:])
     if reduce in ("sum", "add", "mean"):
-        out = torch.zeros(shape, dtype=src.dtype)
+        out = torch.zeros(shape, dtype=src.dtype, device=src.device)
         out.index_add_(0, index, x)
         if reduce == "mean":
-            cnt = torch.zeros(n, dtype=src.dtype)
-            cnt.index_add_(0, index, torch.ones(index.shape[0], dtype=src.dtype))
+            cnt = torch.zeros(n, dtype=src.dtype, device=src.device)
+            cnt.index_add_(0, index, torch.ones(index.shape[0], dtype=src.dtype, device=src.device))
             out = out / cnt.clamp(min=1).view((n,) + (1,) * (out.dim() - 1))
     elif reduce == "max":
-        out = torch.full(shape, float("-inf"), dtype=src.dtype)
+        out = torch.full(shape, float("-inf"), dtype=src.dtype, device=src.device)
         idx = index.view((-1,) + (1,) * (x.dim() - 1)).expand_as(x)
         out = out.scatter_reduce(0, idx, x, reduce="amax", include_self=True)
         out = torch.where(torch.isinf(out) & (out < 0), torch.zeros_like(out), out)
     elif reduce == "min":
-        out = torch.full(shape, float("inf"), dtype=src.dtype)
+        out = torch.full(shape, float("inf"), dtype=src.dtype, device=src.device)
         idx = index.view((-1,) + (1,) * (x.dim() - 1)).expand_as(x)
         out = out.scatter_reduce(0, idx, x, reduce="amin", include_self=True)
         out = torch.where(torch.isinf(out) & (out > 0), torch.zeros_like(out), out)

@@ -248,3 +248,15 @@ def test_k8_both_parity_correlation4_raises_like_reference():
     irr = "2x0e+2x0o+2x1e+2x1o+2x2e+2x2o"
     with pytest.raises(ValueError, match="no coupling path"):
         eq.SymmetricContraction(irr, irr, 4)
+
+
+def test_k8_refuses_correlation_above_four():
+    """The K8 term word has four 6-bit factor fields (gmp_sc.hip): correlation >= 5 must not
+    select K8 (its fifth factor would be dropped), and k8_plan itself refuses it."""
+    from gmp_amd import equivariant as eq
+    irr = "2x0e+2x1o"
+    sc = eq.SymmetricContraction(irr, irr, 5)
+    assert not sc._k8
+    with pytest.raises(AssertionError):
+        eq.k8_plan(list(sc.contractions.values()), 4, 2, 5)
+    assert eq.SymmetricContraction(irr, irr, 4)._k8

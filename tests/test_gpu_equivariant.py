@@ -74,6 +74,9 @@ def test_featurize_vs_oracle(lmax):
     # aggr max / min (tfn_layer.py:87 passes aggr to scatter): per-edge messages + K3 max / min
     ("16x0e+16x1o+16x2e", "16x0e+16x1o+16x2e", False, True, "max", 32),
     ("16x0e", "16x0e+16x1o+16x2e", True, False, "min", 32),
+    # radial hidden widths that are not multiples of 32: zero-padded in the node form
+    ("16x0e+16x1o+16x2e", "16x0e+16x1o+16x2e", False, True, "add", 37),
+    ("32x0e+32x1o+32x2e", "32x0e+32x1o+32x2e", True, False, "mean", 100),
 ])
 @pytest.mark.parametrize("mode", ["node", "edge"])
 def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp, mode, monkeypatch):
@@ -111,6 +114,9 @@ def test_tp_conv_layer_vs_oracle(inp, out, gate, bn, aggr, mlp, mode, monkeypatc
     ("16x0e+16x1o+16x2e+16x3o", "16x0e+16x1o+16x2e+16x3o", True, 32),
     ("32x0e+32x1o+32x2e+32x3o", "32x0e+32x1o+32x2e+32x3o", False, 64),
     ("32x0e+32x1o+32x2e+32x3o", "32x0e+32x1o+32x2e+32x3o", True, 64),
+    # any mlp_dim (tfn_layer.py:73-77): 100 and 250 run zero-padded to 128 / 256
+    ("16x0e+16x1o+16x2e+16x3o", "16x0e+16x1o+16x2e+16x3o", True, 100),
+    ("32x0e+32x1o+32x2e+32x3o", "32x0e+32x1o+32x2e+32x3o", False, 250),
 ])
 def test_tp_conv_layer_l3_vs_oracle(inp, out, gate, mlp):
     """max_ell = 3 (TFN's max_ell kwarg, tfn.py:47): 16-dim SH, l = 3 hidden blocks, up to 27
@@ -214,6 +220,10 @@ def test_tp_conv_chunking_and_determinism(monkeypatch, mode):
                       out_dim=2)),
     ("MACEModel", dict(num_layers=1, emb_dim=32, max_ell=5, correlation=2, r_max=2.0,
                        equivariant_pred=True, out_dim=2)),
+    # radial hidden width 100 at max_ell 3 (node form, zero-padded to 128)
+    ("MACEModel", dict(num_layers=2, emb_dim=16, correlation=3, max_ell=3, r_max=2.0,
+                       mlp_dim=100)),
+    ("TFNModel", dict(num_layers=2, emb_dim=16, max_ell=4, r_max=2.0, mlp_dim=70)),
 ])
 def test_model_vs_oracle(kind, kw):
     from gmp_amd import equivariant as eq
@@ -301,6 +311,50 @@ def test_symmetric_contraction_k8_vs_oracle(C, corr, lmax, both):
     _close_scaled(xd.grad, xr.grad, 1e-5, "dx")
     for (k, p), q in zip(sc.named_parameters(), ref.parameters()):
         _close_scaled(p.grad, q.grad, 1e-5, k)
+
+
+def test_symmetric_contraction_correlation5_torch_path():
+    """Correlation 5 (the reference's U_matrix_real takes any correlation, cg.py:91-133): K8's
+    term words hold four factors, so the module must run the per-irrep contraction on the
+    device, forward and both gradients, against the oracle."""
+    from gmp_amd import equivariant as eq
+    torch.manual_seed(55)
+    irr = _sc_irreps(4, 1)
+    ref = om.SymmetricContraction(irr, irr, 5)
+    sc = eq.SymmetricContraction(irr, irr, 5)
+    sc.load_state_dict(ref.state_dict())
+    sc = sc.to(DEV)
+    assert not sc._k8
+    x = torch.randn(300, 4, 4)
+    xd = x.to(DEV).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y, yr = sc(xd), ref(xr)
+    _close_scaled(y, yr, 1e-5, "out")
+    g = torch.randn_like(yr)
+    (y * g.to(DEV)).sum().backward()
+    (yr * g).sum().backward()
+    _close_scaled(xd.grad, xr.grad, 1e-5, "dx")
+    for (k, p), q in zip(sc.named_parameters(), ref.parameters()):
+        _close_scaled(p.grad, q.grad, 1e-5, k)
+
+
+def test_symmetric_contraction_k8_empty_batch():
+    """N = 0 nodes: an empty output and exactly zero weight gradients (the dcoef partials of an
+    empty batch are written as one zero group, not left uninitialised)."""
+    from gmp_amd import equivariant as eq
+    irr = _sc_irreps(16, 2)
+    sc = eq.SymmetricContraction(irr, irr, 3).to(DEV)
+    assert sc._k8
+    for _ in range(2):  # the second call reuses the caching allocator's (dirty) blocks
+        big = torch.full((1 << 20,), float("nan"), device=DEV)
+        del big
+        sc.zero_grad(set_to_none=True)
+        x = torch.randn(0, 16, 9, device=DEV, requires_grad=True)
+        y = sc(x)
+        assert y.shape == (0, 9 * 16)
+        y.sum().backward()
+        for k, p in sc.named_parameters():
+            assert p.grad is not None and torch.equal(p.grad, torch.zeros_like(p.grad)), k
 
 
 def test_symmetric_contraction_k8_deterministic_and_large():

@@ -106,6 +106,29 @@ def test_gvp_conv_layer_c3_widths_vs_oracle(fast, edge_linear, fused, defer, mon
             _scaled(p.grad, q.grad, 1e-4, k)
 
 
+@pytest.mark.parametrize("row", [0, 1])
+def test_gvp_fused_out_of_range_index_raises(row):
+    """An edge_index entry >= N on the fused GVPConv path raises IndexError, as the reference's
+    index_select / torch_scatter do, before any receiver-sorted kernel runs (those visit only the
+    in-range edges, so their per-edge outputs would hold unwritten rows)."""
+    import gmp_amd.gvp as g
+    from gmp_amd.graph import radius_graph
+    torch.manual_seed(2)
+    gr = radius_graph(num_nodes=200, target_edges=2000, r=2.0, seed=6, tol=0.2, shuffle=True)
+    lay = g.GVPConvLayer((128, 16), (32, 1), activations=(RELU, None), vector_gate=True)
+    lay = lay.to(DEV).eval()
+    n, e = gr.num_nodes, gr.num_edges
+    ei = gr.edge_index.clone()
+    ei[row, e // 2] = n + 3
+    x = (torch.randn(n, 128, device=DEV), torch.randn(n, 16, 3, device=DEV))
+    ea = (torch.randn(e, 32, device=DEV), torch.randn(e, 1, 3, device=DEV))
+    assert lay.conv._fused_ok(x, ea)
+    with pytest.raises(IndexError):
+        lay(x, ei.to(DEV), ea)
+    so, vo = lay(x, gr.edge_index.to(DEV), ea)  # the valid graph still runs afterwards
+    assert bool(torch.isfinite(so).all()) and bool(torch.isfinite(vo).all())
+
+
 C3 = dict(num_layers=4, s_dim=128, v_dim=16, s_dim_edge=32, v_dim_edge=1)  # gvpgnn.py:13-27
 
 
