@@ -200,10 +200,51 @@ __global__ __launch_bounds__(64 * SW) void sum_partials_one(const float* __restr
   else if (colsum) colsum[x - DD] = s;
 }
 
+// Narrow outputs (X of a few thousand floats: the GVP message-GVP products 16 x 128, 16 x 48,
+// 48 x 48, ...): sum_partials_one's 64 columns per workgroup leave X / 64 ~ 30 workgroups, each
+// lane walking G / 4 ~ 128 slabs in dependent bursts (34 us per finish in the r05 GVP step, 128
+// finishes per step).  Here a workgroup owns 16 columns and its 16 lane groups (4 per wave) each
+// add a contiguous 1/16 of the slabs in one burst of loads (64-byte row pieces), then one lane
+// group adds the 16 group sums in group order: X / 16 workgroups, a fixed order (deterministic).
+template <int GC>
+__global__ __launch_bounds__(256) void sum_partials_narrow(const float* __restrict__ part,
+                                                           int64_t G, int64_t X,
+                                                           float* __restrict__ out,
+                                                           float* __restrict__ colsum,
+                                                           int64_t DD, int64_t n, int64_t ldc) {
+  __shared__ float red[16][16];
+  const int q = threadIdx.x >> 4, c = threadIdx.x & 15;
+  const int64_t x = blockIdx.x * (int64_t)16 + c;
+  const int64_t per = (G + 15) / 16, g0 = q * per, g1 = (g0 + per < G) ? g0 + per : G;
+  float s = 0.f;
+  if (x < X) {
+    for (int64_t c0 = g0; c0 < g1; c0 += GC) {
+      float v[GC];
+#pragma unroll
+      for (int u = 0; u < GC; ++u) v[u] = (c0 + u < g1) ? part[(c0 + u) * X + x] : 0.f;
+#pragma unroll
+      for (int u = 0; u < GC; ++u)
+        if (c0 + u < g1) s += v[u];
+    }
+  }
+  red[q][c] = s;
+  __syncthreads();
+  if (q != 0 || x >= X) return;
+#pragma unroll
+  for (int w = 1; w < 16; ++w) s += red[w][c];
+  if (x < DD) out[(x / n) * ldc + x % n] = s;
+  else if (colsum) colsum[x - DD] = s;
+}
+
 // out (row stride ldc, n columns) = the ordered sum of G slabs of X = DD (+ colsum) floats.
 // (r03: a two-level form with single-wave workgroups measured neutral on the EGNN step; removed)
 void sum_partials(const float* part, int64_t G, int64_t X, float* out, float* colsum,
                   int64_t DD, int64_t n, int64_t ldc, hipStream_t s) {
+  if (X < 8192 && G >= 64) {  // narrow: < 128 workgroups of 64 columns
+    sum_partials_narrow<32><<<(unsigned)ceil_div(X, 16), 256, 0, s>>>(part, G, X, out, colsum,
+                                                                      DD, n, ldc);
+    return;
+  }
   const unsigned grid = (unsigned)ceil_div(X, 64);
   sum_partials_one<4, 32><<<grid, 256, 0, s>>>(part, G, X, out, colsum, DD, n, ldc);
 }
@@ -1073,8 +1114,7 @@ int outer_sum_quad_launch(int64_t K, int64_t m, int64_t n, const float* A, int64
                                                                            part, X);
   int rc = launch_status();
   if (rc) return rc;
-  sum_partials_one<4><<<(unsigned)ceil_div(X, 64), 256, 0, s>>>(part, Sr, X, C, colsum_A, m * n,
-                                                                n, ldc);
+  sum_partials(part, Sr, X, C, colsum_A, m * n, n, ldc, s);
   return launch_status();
 }
 

@@ -627,6 +627,92 @@ class GVPConv(MessagePassing):
         return _split(agg, self.vo)
 
 
+# False: the node feed-forward as the reference's module chain (tests compare the two)
+GVP_FF_FUSED = True
+
+
+def _ff_fusable(ff, x):
+    """K17 takes GVPConvLayer's default feed-forward at the GVP-GNN widths (gvp_layer.py:361-366
+    with node_dims (128, 16), n_feedforward 2, vector_gate, activations (relu, None))."""
+    if not (GVP_FF_FUSED and len(ff) == 2):
+        return False
+    g1, g2 = ff
+    s, v = x
+    return ((g1.si, g1.vi, g1.so, g1.vo, g2.si, g2.vi, g2.so, g2.vo) ==
+            (128, 16, 512, 32, 512, 32, 128, 16) and g1.h_dim == 32 and g2.h_dim == 32 and
+            g1.vector_gate and g2.vector_gate and g1.vector_act is None and
+            g2.vector_act is None and g1.scalar_act is F.relu and g2.scalar_act is None and
+            s.is_cuda and s.dtype == torch.float32 and v.dtype == torch.float32 and
+            s.dim() == 2 and v.dim() == 3 and v.shape[1:] == (16, 3))
+
+
+class GvpFFFn(torch.autograd.Function):
+    """K17 (gmp_gvp_ff_{fwd,bwd}_f32): GVPConvLayer's node feed-forward GVP((128, 16), (512, 32))
+    -> GVP((512, 32), (128, 16)) (gvp_layer.py:361-366, :433-434; GVP.forward :140-170) as one
+    kernel per direction; the weight gradients are node outer sums of the backward's factors on
+    the side stream (deferred to the end of the backward pass)."""
+
+    @staticmethod
+    def forward(ctx, s, v, *W):
+        s, v = ops._f32c(s), ops._f32c(v)
+        ops._need_cuda(s, v)
+        Wc = [ops._f32c(w) for w in W]
+        with ops._timed("gvp_ff_fwd"):
+            s2, v2, s1, gate1 = _lib.torch_ops().gvp_ff_fwd(s, v, Wc)
+        ctx.save_for_backward(s, v, s1, gate1, s2, *Wc)
+        return s2, v2
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, ds, dv):
+        s, v, s1, gate1, s2, *W = ctx.saved_tensors
+        ds = ops._f32c(ds) if ds is not None else torch.zeros_like(s2)
+        dv = ops._f32c(dv) if dv is not None else torch.zeros_like(v)
+        with ops._timed("gvp_ff_bwd"):
+            (ds_in, dv_in, dp1, dp2, dg1, dg2, vn1, vn2, du1, dvh1, dvh2, v1,
+             du2) = _lib.torch_ops().gvp_ff_bwd(s, v, W, s1, gate1, s2, ds, dv)
+        return (ds_in, dv_in) + _ff_wgrads(ctx.needs_input_grad, s, v, s1, s2, W, dp1, dp2, dg1,
+                                           dg2, vn1, vn2, du1, dvh1, dvh2, v1, du2)
+
+
+def _ff_wgrads(needs_input_grad, s, v, s1, s2, W, dp1, dp2, dg1, dg2, vn1, vn2, du1, dvh1, dvh2,
+               v1, du2):
+    """K17's weight gradients from its per-node factors (gmp.h gmp_gvp_ff_bwd_f32): deterministic
+    node outer sums on the side stream; dWsv1 through Ws1 (p1 = Ws1 [s | vn1] + b1 is not
+    stored), dWv1 / dWv2 through Wh1 / Wh2 (vh = Wh v is not stored)."""
+    N = s.shape[0]
+    Wh1, Ws1, b1, _, _, _, Wh2, _, _, _, _, _ = W
+    v48, v196 = v.reshape(N, 48), v1.reshape(N, 96)
+    with ops.side_work(dp1, s, vn1, dg1, du1, dvh1, v, dp2, s1, vn2, dg2, s2, du2, dvh2,
+                       v1) as sw:
+        A, db1 = _osum(dp1, s)                                   # (512, 128)
+        B, _ = _osum(dp1, vn1)                                   # (512, 32)
+        dWs1 = torch.cat([A, B], 1)
+        Gs, dbsv1 = _osum(dg1, s)
+        Gv, _ = _osum(dg1, vn1)
+        dWsv1 = torch.addmm(torch.outer(dbsv1, b1), torch.cat([Gs, Gv], 1), Ws1.t())
+        dWh1 = _diag3(_osum(dvh1.reshape(N, 96), v48)[0], 32, 16)
+        dWv1 = _diag3(_osum(du1.reshape(N, 96), v48)[0], 32, 16).mm(Wh1.t())
+        A2, db2 = _osum(dp2, s1)                                 # (128, 512)
+        B2, _ = _osum(dp2, vn2)                                  # (128, 32)
+        dWs2 = torch.cat([A2, B2], 1)
+        dWsv2, dbsv2 = _osum(dg2, s2)                            # (16, 128)
+        dWh2 = _diag3(_osum(dvh2.reshape(N, 96), v196)[0], 32, 32)
+        dWv2 = _diag3(_osum(du2.reshape(N, 48), v196)[0], 16, 32).mm(Wh2.t())
+    grads = (dWh1, dWs1, db1, dWv1, dWsv1, dbsv1, dWh2, dWs2, db2, dWv2, dWsv2, dbsv2)
+    return sw.deliver(needs_input_grad, 2, W, grads)
+
+
+def gvp_ff(ff, x):
+    """ff_func(x) (gvp_layer.py:433) on K17 where it applies, else the module chain."""
+    if _ff_fusable(ff, x):
+        g1, g2 = ff
+        return GvpFFFn.apply(x[0], x[1], g1.wh.weight, g1.ws.weight, g1.ws.bias, g1.wv.weight,
+                             g1.wsv.weight, g1.wsv.bias, g2.wh.weight, g2.ws.weight,
+                             g2.ws.bias, g2.wv.weight, g2.wsv.weight, g2.wsv.bias)
+    return ff(x)
+
+
 class GVPConvLayer(nn.Module):
     """gvp_layer.py:327-438."""
 
@@ -665,7 +751,7 @@ class GVPConvLayer(nn.Module):
             x_ = x
             x, dh = tuple_index(x, node_mask), tuple_index(dh, node_mask)
         x = self.norm[0](tuple_sum(x, self.dropout[0](dh))) if self.residual else dh
-        dh = self.ff_func(x)
+        dh = gvp_ff(self.ff_func, x)
         x = self.norm[1](tuple_sum(x, self.dropout[1](dh))) if self.residual else dh
         if node_mask is not None:
             x_[0][node_mask], x_[1][node_mask] = x[0], x[1]

@@ -33,7 +33,7 @@ def test_library_exports_all_symbols():
     # every declared entry point has a ctypes signature (and vice versa)
     assert set(_declared()) == set(_lib.SIGNATURES), set(_declared()) ^ set(_lib.SIGNATURES)
     lib2 = _lib.load()
-    assert lib2.gmp_abi_version() == _lib.ABI_VERSION == 5
+    assert lib2.gmp_abi_version() == _lib.ABI_VERSION == 6
     assert lib2.gmp_error_string(-1) == b"invalid argument"
 
 
