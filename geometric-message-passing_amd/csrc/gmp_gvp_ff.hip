@@ -14,13 +14,18 @@
 // Ws1[chunk, :] (64 x 160), Wsv1[:, chunk] (32 x 64) and Ws2[:, chunk] (128 x 64) in LDS
 // (86 KB), next to the resident small weights (44 KB).
 //
-// Forward saves s1 = relu(p1) (N x 512) and gate1 (N x 32) for the backward.  The backward
-// recomputes the vector path from v, takes p2 = s2 (the second GVP has no scalar activation) and
-// writes the input gradients plus the per-node factors of every weight gradient, which the host
-// reduces with the deterministic node outer sums:
-//   dp1 (N, 512), dp2 (N, 128), dgate1 (N, 32), dgate2 (N, 16), vn1 (N, 32), vn2 (N, 32),
-//   du1, dvh1, dvh2, v1 (N, 32, 3) and du2 (N, 16, 3)   [(channel, xyz) layout]
-// with du = dv * sigmoid(gate) (the gradient at W_v vh) and dvh the gradient at vh.
+// The weight gradients are four node outer sums C = A^T B over the N rows (the host's
+// deterministic quadrant sums, one launch each), whose operands the kernels write side by side,
+// zero-padded to 64-column multiples:
+//   forward : B1 = [s | vn1 | 0] (N, 192), B2 = [s1 | vn2 | 0] (N, 576) with s1 = relu(p1),
+//             B3 = [v | 0] (N, 64), B4 = [v1 | 0] (N, 128), and gate1 (N, 32);
+//   backward: A1 = [dp1 | dgate1 | 0] (N, 576), A2 = [dp2 | dgate2 | 0] (N, 192),
+//             A3 = [dvh1 | du1] (N, 192), A4 = [dvh2 | du2 | 0] (N, 192)
+// (vectors in the (channel, xyz) layout; dp the gradient at a scalar Linear's output, du =
+// grad_v * sigmoid(gate) the gradient at W_v vh, dvh the gradient at vh).  A1^T B1 holds dWs1 and
+// dgate1^T [s | vn1] (-> dWsv1 through Ws1), A2^T B2 dWs2 and dgate2^T [s1 | vn2] (-> dWsv2
+// through Ws2), A3^T B3 and A4^T B4 the xyz-diagonal blocks of dWh / dWv (gmp.h).  The backward
+// reads s1 from B2 and takes p2 = s2 (the second GVP has no scalar activation).
 #include "gmp_gvp_common.h"
 
 namespace gmp {
@@ -56,6 +61,9 @@ constexpr int oWs1c = oChunk;                // Ws1[chunk rows, 0:160] (64 x 160
 constexpr int oWsv1c = oWs1c + CH * L160;    // Wsv1[:, chunk cols] (32 x 64)
 constexpr int oWs2c = oWsv1c + HV * L64;     // Ws2[:, chunk cols] (128 x 64)
 constexpr int kFFSmem = oWs2c + FS * L64;    // floats
+// row strides of the weight-sum operands
+constexpr int kB1 = 192, kB2 = 576, kB3 = 64, kB4 = 128, kA1 = 576, kA2 = 192, kA3 = 192,
+              kA4 = 192;
 
 struct FFW {
   const float *Wh1, *Ws1, *b1, *Wv1, *Wsv1, *bsv1;  // GVP 1: (32,16) (512,160) (512) (32,32) (32,512) (32)
@@ -83,10 +91,41 @@ __device__ void ff_resident_to_lds(float* sm, const FFW& P) {
   for (int x = threadIdx.x; x < FV; x += blockDim.x) sm[obsv2 + x] = P.bsv2[x];
 }
 
-__device__ void ff_chunk_to_lds(float* sm, const FFW& P, int c) {
-  copy_mat(sm + oWs1c, L160, P.Ws1 + (int64_t)c * CH * (FS + HV), CH, FS + HV, FS + HV, 0);
-  copy_mat(sm + oWsv1c, L64, P.Wsv1, HV, CH, HS, c * CH);
-  copy_mat(sm + oWs2c, L64, P.Ws2, FS, CH, HS + HV, c * CH);
+// float4 tile copy global -> LDS: ROWS x COLS floats (COLS % 4 == 0) of a row-major source with
+// row stride SLD starting at column col0; the loads of a thread are issued together (one L2 round
+// trip per chunk instead of one per element)
+template <int ROWS, int COLS, int SLD, int LD>
+struct Tile4 {
+  static constexpr int N4 = ROWS * COLS / 4, PER = (N4 + kFT - 1) / kFT;
+  f32x4 r[PER];
+  __device__ __forceinline__ void load(const float* __restrict__ src, int col0) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int x = threadIdx.x + k * kFT;
+      const int row = x / (COLS / 4), c4 = x - row * (COLS / 4);
+      if (x < N4) r[k] = *reinterpret_cast<const f32x4*>(src + row * SLD + col0 + 4 * c4);
+    }
+  }
+  __device__ __forceinline__ void store(float* dst) const {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int x = threadIdx.x + k * kFT;
+      const int row = x / (COLS / 4), c4 = x - row * (COLS / 4);
+      if (x < N4) *reinterpret_cast<f32x4*>(dst + row * LD + 4 * c4) = r[k];
+    }
+  }
+};
+
+__device__ __forceinline__ void ff_chunk_to_lds(float* sm, const FFW& P, int c) {
+  Tile4<CH, FS + HV, FS + HV, L160> a;
+  Tile4<HV, CH, HS, L64> b;
+  Tile4<FS, CH, HS + HV, L64> d;
+  a.load(P.Ws1 + (int64_t)c * CH * (FS + HV), 0);
+  a.store(sm + oWs1c);  // (two bursts: the backward kernel has no registers for all ten)
+  b.load(P.Wsv1, c * CH);
+  d.load(P.Ws2, c * CH);
+  b.store(sm + oWsv1c);
+  d.store(sm + oWs2c);
 }
 
 // node n of a 16-row chunk, clamped for the loads (stores are masked by `valid`)
@@ -144,8 +183,11 @@ __global__ __launch_bounds__(kFT) void gvp_ff_fwd_kernel(int64_t N, const float*
                                                          const float* __restrict__ v_in, FFW P,
                                                          float* __restrict__ s_out,
                                                          float* __restrict__ v_out,
-                                                         float* __restrict__ s1_out,
-                                                         float* __restrict__ gate1_out) {
+                                                         float* __restrict__ gate1_out,
+                                                         float* __restrict__ B1,
+                                                         float* __restrict__ B2,
+                                                         float* __restrict__ B3,
+                                                         float* __restrict__ B4) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   ff_resident_to_lds(sm, P);
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
@@ -163,6 +205,16 @@ __global__ __launch_bounds__(kFT) void gvp_ff_fwd_kernel(int64_t N, const float*
     __syncthreads();  // resident weights (first pass) / previous pass done with the chunk LDS
     VecPath F;
     vec_path_1(sm, v, F, i, g);
+    if (valid) {  // B1 = [s | vn1 | 0], B3 = [v | 0]: stored now, their registers freed early
+      f32x4 z2[2], z1[1];
+      zero(z2);
+      zero(z1);
+      st_row<FS / 16>(B1 + k.n * kB1, s, g);
+      st_row<2>(B1 + k.n * kB1 + FS, F.vn1, g);
+      st_row<2>(B1 + k.n * kB1 + FS + HV, z2, g);
+      st_vrow<1>(B3 + k.n * kB3, v, g);
+      st_row<1>(B3 + k.n * kB3 + 3 * FV, z1, g);
+    }
     f32x4 gate1[2], p2[FS / 16];
     ld_vec<2>(gate1, sm + obsv1, g);
     ld_vec<FS / 16>(p2, sm + ob2, g);
@@ -179,7 +231,7 @@ __global__ __launch_bounds__(kFT) void gvp_ff_fwd_kernel(int64_t N, const float*
       for (int p = 0; p < CH / 16; ++p)
 #pragma unroll
         for (int q = 0; q < 4; ++q) p1[p][q] = fmaxf(p1[p][q], 0.f);
-      if (valid) st_row<CH / 16>(s1_out + k.n * HS + c * CH, p1, g);
+      if (valid) st_row<CH / 16>(B2 + k.n * kB2 + c * CH, p1, g);
       gemm_wx<FS / 16, CH / 16>(sm + oWs2c, L64, p1, p2, i, g);
     }
 #pragma unroll
@@ -200,12 +252,18 @@ __global__ __launch_bounds__(kFT) void gvp_ff_fwd_kernel(int64_t N, const float*
       st_row<FS / 16>(s_out + k.n * FS, p2, g);
       st_vrow<1>(v_out + k.n * (3 * FV), v2, g);
       st_row<2>(gate1_out + k.n * HV, gate1, g);
+      f32x4 z2[2];
+      zero(z2);
+      st_row<2>(B2 + k.n * kB2 + HS, F.vn2, g);
+      st_row<2>(B2 + k.n * kB2 + HS + HV, z2, g);
+      st_vrow<2>(B4 + k.n * kB4, F.v1, g);
+      st_row<2>(B4 + k.n * kB4 + 3 * HV, z2, g);
     }
   }
 }
 
 struct FFGrads {
-  float *ds, *dv, *dp1, *dp2, *dgate1, *dgate2, *vn1, *vn2, *du1, *dvh1, *dvh2, *v1, *du2;
+  float *ds, *dv, *A1, *A2, *A3, *A4;
 };
 
 // d|vh| -> dvh with the reference's clamp: zero gradient where sum x^2 < 1e-8
@@ -226,7 +284,7 @@ __device__ __forceinline__ void norm_bwd(f32x4 (&dvh)[3][T], const f32x4 (&vh)[3
 // Factors are stored as soon as they are final and the first GVP's vector state (vh1, |vh1|) is
 // recomputed after the scalar chunks instead of being held across them (register budget).
 __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
-    int64_t N, const float* __restrict__ s1, const float* __restrict__ gate1_in,
+    int64_t N, const float* __restrict__ B2, const float* __restrict__ gate1_in,
     const float* __restrict__ s2, const float* __restrict__ ds_out,
     const float* __restrict__ v_in, const float* __restrict__ dv_out, FFW P, FFGrads O) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -252,7 +310,6 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
         gemm_wx<2, 1>(sm + oWh1, L16, v[x], vh1[x], i, g);
       }
       vnorm<2>(vh1, vn1, sq1);
-      if (valid) st_row<2>(O.vn1 + k.n * HV, vn1, g);
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -265,7 +322,6 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
 #pragma unroll
         for (int p = 0; p < 2; ++p) v1[x][p] = u1[x][p] * sg1[p];
       }
-      if (valid) st_vrow<2>(O.v1 + k.n * (3 * HV), v1, g);
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
         zero(vh2[x]);
@@ -273,7 +329,6 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
       }
     }
     vnorm<2>(vh2, vn2, sq2);
-    if (valid) st_row<2>(O.vn2 + k.n * HV, vn2, g);
     // ---- GVP 2 backward: du2 = dv2 sg2, dgate2 = sum_x dv2 u2 sg2 (1 - sg2), dvh2 = Wv2^T du2,
     // dp2 = ds2 + Wsv2^T dgate2, dvn2 = Ws2[:, 512:]^T dp2
     f32x4 dp2[FS / 16], dvh2[3][2];
@@ -303,8 +358,12 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
         dg2[0][q] = acc * sg * (1.f - sg);
       }
       if (valid) {
-        st_vrow<1>(O.du2 + k.n * (3 * FV), du2, g);
-        st_row<1>(O.dgate2 + k.n * FV, dg2, g);
+        f32x4 z[3];
+        zero(z);
+        st_vrow<1>(O.A4 + k.n * kA4 + 3 * HV, du2, g);
+        st_row<3>(O.A4 + k.n * kA4 + 3 * HV + 3 * FV, z, g);
+        st_row<1>(O.A2 + k.n * kA2 + FS, dg2, g);
+        st_row<3>(O.A2 + k.n * kA2 + FS + FV, z, g);
       }
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
@@ -321,8 +380,8 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
       norm_bwd<2>(dvh2, vh2, vn2, sq2, dvn2);
     }
     if (valid) {
-      st_vrow<2>(O.dvh2 + k.n * (3 * HV), dvh2, g);
-      st_row<FS / 16>(O.dp2 + k.n * FS, dp2, g);
+      st_vrow<2>(O.A4 + k.n * kA4, dvh2, g);
+      st_row<FS / 16>(O.A2 + k.n * kA2, dp2, g);
     }
     // ---- GVP 1 vector backward: dv1 = Wh2^T dvh2, du1 = dv1 sg1, dgate1, dvh1 = Wv1^T du1
     f32x4 dg1[2], dvh1[3][2];
@@ -347,8 +406,11 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
           dg1[p][q] = acc * sg * (1.f - sg);
         }
       if (valid) {
-        st_vrow<2>(O.du1 + k.n * (3 * HV), du1, g);
-        st_row<2>(O.dgate1 + k.n * HV, dg1, g);
+        f32x4 z[2];
+        zero(z);
+        st_vrow<2>(O.A3 + k.n * kA3 + 3 * HV, du1, g);
+        st_row<2>(O.A1 + k.n * kA1 + HS, dg1, g);
+        st_row<2>(O.A1 + k.n * kA1 + HS + HV, z, g);
       }
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
@@ -366,7 +428,7 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
       ff_chunk_to_lds(sm, P, c);
       __syncthreads();
       f32x4 a1[CH / 16], dp1[CH / 16];
-      ld_row<CH / 16>(a1, s1 + k.n * HS + c * CH, g);
+      ld_row<CH / 16>(a1, B2 + k.n * kB2 + c * CH, g);
       zero(dp1);
       gemm_wtx<CH / 16, FS / 16>(sm + oWs2c, L64, dp2, dp1, i, g);
 #pragma unroll
@@ -374,7 +436,7 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) dp1[p][q] = a1[p][q] > 0.f ? dp1[p][q] : 0.f;
       gemm_wtx<CH / 16, 2>(sm + oWsv1c, L64, dg1, dp1, i, g);
-      if (valid) st_row<CH / 16>(O.dp1 + k.n * HS + c * CH, dp1, g);
+      if (valid) st_row<CH / 16>(O.A1 + k.n * kA1 + c * CH, dp1, g);
       gemm_wtx<FS / 16, CH / 16>(sm + oWs1c, L160, dp1, ds, i, g);
       gemm_wtx<2, CH / 16>(sm + oWs1c + FS, L160, dp1, dvn1, i, g);
     }
@@ -398,7 +460,7 @@ __global__ __launch_bounds__(kFT) void gvp_ff_bwd_kernel(
     if (valid) {
       st_row<FS / 16>(O.ds + k.n * FS, ds, g);
       st_vrow<1>(O.dv + k.n * (3 * FV), dv, g);
-      st_vrow<2>(O.dvh1 + k.n * (3 * HV), dvh1, g);
+      st_vrow<2>(O.A3 + k.n * kA3, dvh1, g);
     }
   }
 }
@@ -427,47 +489,46 @@ int gmp_gvp_ff_fwd_f32(int64_t n_nodes, const float* s_in, const float* v_in, co
                        const float* Ws1, const float* b1, const float* Wv1, const float* Wsv1,
                        const float* bsv1, const float* Wh2, const float* Ws2, const float* b2,
                        const float* Wv2, const float* Wsv2, const float* bsv2, float* s_out,
-                       float* v_out, float* s1_out, float* gate1_out, void* stream) {
+                       float* v_out, float* gate1_out, float* B1, float* B2, float* B3, float* B4,
+                       void* stream) {
   GMP_CHECK_ARG(n_nodes >= 0);
   if (n_nodes == 0) return GMP_OK;
   const FFW P{Wh1, Ws1, b1, Wv1, Wsv1, bsv1, Wh2, Ws2, b2, Wv2, Wsv2, bsv2};
-  GMP_CHECK_ARG(ffw_ok(P) && s_in && v_in && s_out && v_out && s1_out && gate1_out);
-  GMP_CHECK_ARG(a16(s_in) && a16(v_in) && a16(s_out) && a16(v_out) && a16(s1_out) &&
-                a16(gate1_out));
+  GMP_CHECK_ARG(ffw_ok(P) && s_in && v_in && s_out && v_out && gate1_out && B1 && B2 && B3 && B4);
+  GMP_CHECK_ARG(a16(Ws1) && a16(Wsv1) && a16(Ws2));  // float4 chunk staging
+  GMP_CHECK_ARG(a16(s_in) && a16(v_in) && a16(s_out) && a16(v_out) && a16(gate1_out) &&
+                a16(B1) && a16(B2) && a16(B3) && a16(B4));
   const size_t smem = (size_t)kFFSmem * sizeof(float);
   int rc = hip_check(hipFuncSetAttribute((const void*)gvp_ff_fwd_kernel,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
   if (rc) return rc;
   gvp_ff_fwd_kernel<<<ff_grid(n_nodes), kFT, smem, as_stream(stream)>>>(
-      n_nodes, s_in, v_in, P, s_out, v_out, s1_out, gate1_out);
+      n_nodes, s_in, v_in, P, s_out, v_out, gate1_out, B1, B2, B3, B4);
   return launch_status();
 }
 
-int gmp_gvp_ff_bwd_f32(int64_t n_nodes, const float* s_in, const float* v_in, const float* s1,
-                       const float* gate1, const float* s2, const float* ds_out,
-                       const float* dv_out, const float* Wh1, const float* Ws1, const float* b1,
-                       const float* Wv1, const float* Wsv1, const float* bsv1, const float* Wh2,
-                       const float* Ws2, const float* b2, const float* Wv2, const float* Wsv2,
-                       const float* bsv2, float* ds_in, float* dv_in, float* dp1, float* dp2,
-                       float* dgate1, float* dgate2, float* vn1, float* vn2, float* du1,
-                       float* dvh1, float* dvh2, float* v1, float* du2, void* stream) {
+int gmp_gvp_ff_bwd_f32(int64_t n_nodes, const float* v_in, const float* gate1, const float* B2,
+                       const float* s2, const float* ds_out, const float* dv_out,
+                       const float* Wh1, const float* Ws1, const float* b1, const float* Wv1,
+                       const float* Wsv1, const float* bsv1, const float* Wh2, const float* Ws2,
+                       const float* b2, const float* Wv2, const float* Wsv2, const float* bsv2,
+                       float* ds_in, float* dv_in, float* A1, float* A2, float* A3, float* A4,
+                       void* stream) {
   GMP_CHECK_ARG(n_nodes >= 0);
   if (n_nodes == 0) return GMP_OK;
   const FFW P{Wh1, Ws1, b1, Wv1, Wsv1, bsv1, Wh2, Ws2, b2, Wv2, Wsv2, bsv2};
-  const FFGrads O{ds_in, dv_in, dp1, dp2, dgate1, dgate2, vn1, vn2, du1, dvh1, dvh2, v1, du2};
-  GMP_CHECK_ARG(ffw_ok(P) && s_in && v_in && s1 && gate1 && s2 && ds_out && dv_out);
-  GMP_CHECK_ARG(ds_in && dv_in && dp1 && dp2 && dgate1 && dgate2 && vn1 && vn2 && du1 && dvh1 &&
-                dvh2 && v1 && du2);
-  GMP_CHECK_ARG(a16(s_in) && a16(v_in) && a16(s1) && a16(gate1) && a16(s2) && a16(ds_out) &&
-                a16(dv_out) && a16(ds_in) && a16(dv_in) && a16(dp1) && a16(dp2) &&
-                a16(dgate1) && a16(dgate2) && a16(vn1) && a16(vn2) && a16(du1) && a16(dvh1) &&
-                a16(dvh2) && a16(v1) && a16(du2));
+  const FFGrads O{ds_in, dv_in, A1, A2, A3, A4};
+  GMP_CHECK_ARG(ffw_ok(P) && v_in && gate1 && B2 && s2 && ds_out && dv_out);
+  GMP_CHECK_ARG(ds_in && dv_in && A1 && A2 && A3 && A4);
+  GMP_CHECK_ARG(a16(Ws1) && a16(Wsv1) && a16(Ws2));
+  GMP_CHECK_ARG(a16(v_in) && a16(gate1) && a16(B2) && a16(s2) && a16(ds_out) && a16(dv_out) &&
+                a16(ds_in) && a16(dv_in) && a16(A1) && a16(A2) && a16(A3) && a16(A4));
   const size_t smem = (size_t)kFFSmem * sizeof(float);
   int rc = hip_check(hipFuncSetAttribute((const void*)gvp_ff_bwd_kernel,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
   if (rc) return rc;
   gvp_ff_bwd_kernel<<<ff_grid(n_nodes), kFT, smem, as_stream(stream)>>>(
-      n_nodes, s1, gate1, s2, ds_out, v_in, dv_out, P, O);
+      n_nodes, B2, gate1, s2, ds_out, v_in, dv_out, P, O);
   return launch_status();
 }
 

@@ -1093,9 +1093,11 @@ int64_t quad_splits(int64_t K, int64_t quads) {
   if (s > cap) s = cap;
   return s < 1 ? 1 : s;
 }
+// (r06: up to 1024 x 1024 -- the quadrants are grid blocks, nothing in LDS scales with m, n --
+// so K17's combined weight-sum operands, e.g. 576 x 192, are one launch)
 bool quad_ok(int64_t K, int64_t m, int64_t n, int pro, int64_t lda, int64_t ldb) {
   return pro == 0 && K < kX3MinK && K > 0 && m % 64 == 0 && n % 64 == 0 &&
-         m <= 256 && n <= 256 && lda % 4 == 0 && ldb % 4 == 0;
+         m <= 1024 && n <= 1024 && lda % 4 == 0 && ldb % 4 == 0;
 }
 size_t quad_workspace(int64_t K, int64_t m, int64_t n) {
   return (size_t)quad_splits(K, (m / 64) * (n / 64)) * (size_t)(m * n + m) * sizeof(float);
@@ -1331,9 +1333,10 @@ static int outer_sum_rect_launch(int64_t K, int64_t m, int64_t n, const float* A
                                  const float* B, int64_t ldb, float* C, int64_t ldc,
                                  float* colsum_A, void* workspace, size_t workspace_bytes,
                                  void* stream) {
-  GMP_CHECK_ARG(K >= 0 && C && m > 0 && n > 0 && m % 16 == 0 && n % 16 == 0 && m <= kT);
+  GMP_CHECK_ARG(K >= 0 && C && m > 0 && n > 0 && m % 16 == 0 && n % 16 == 0);
   GMP_CHECK_ARG(lda >= m && ldb >= n && ldc >= n && lda % 4 == 0 && ldb % 4 == 0);
-  const int bucket = rect_bucket(m, n);
+  GMP_CHECK_ARG(m <= kT || quad_ok(K, m, n, 0, lda, ldb));
+  const int bucket = m <= kT ? rect_bucket(m, n) : 0;
   if (!bucket && !quad_ok(K, m, n, 0, lda, ldb)) return GMP_ERR_UNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if (K == 0) {

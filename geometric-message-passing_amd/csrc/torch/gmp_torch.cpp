@@ -1257,48 +1257,45 @@ const std::vector<std::vector<int64_t>> kGvpFFW = {{32, 16}, {512, 160}, {512}, 
                                                    {32, 512}, {32}, {32, 32}, {128, 544},
                                                    {128}, {16, 32}, {16, 128}, {16}};
 
+// returns s2, v2, gate1, B1 (N, 192), B2 (N, 576), B3 (N, 64), B4 (N, 128) (gmp.h)
 std::vector<Tensor> gvp_ff_fwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>& W) {
   OpGuard g(s, "gvp_ff_fwd");
   const int64_t N = gvp_rows(s, v);
   gvp_w_checks(W, kGvpFFW);
   auto o = fopt(s);
-  Tensor so = at::empty_like(s), vo = at::empty_like(v);
-  Tensor s1 = at::empty({N, 512}, o), gate1 = at::empty({N, 32}, o);
+  Tensor so = at::empty_like(s), vo = at::empty_like(v), gate1 = at::empty({N, 32}, o);
+  Tensor B1 = at::empty({N, 192}, o), B2 = at::empty({N, 576}, o);
+  Tensor B3 = at::empty({N, 64}, o), B4 = at::empty({N, 128}, o);
   check_rc(gmp_gvp_ff_fwd_f32(N, fp(s), fp(v), fp(W[0]), fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]),
                               fp(W[5]), fp(W[6]), fp(W[7]), fp(W[8]), fp(W[9]), fp(W[10]),
-                              fp(W[11]), fp(so), fp(vo), fp(s1), fp(gate1), cur_stream()),
+                              fp(W[11]), fp(so), fp(vo), fp(gate1), fp(B1), fp(B2), fp(B3), fp(B4),
+                              cur_stream()),
            "gmp_gvp_ff_fwd_f32");
-  return {so, vo, s1, gate1};
+  return {so, vo, gate1, B1, B2, B3, B4};
 }
 
-// returns ds, dv, dp1, dp2, dgate1, dgate2, vn1, vn2, du1, dvh1, dvh2, v1, du2
-std::vector<Tensor> gvp_ff_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>& W,
-                               const Tensor& s1, const Tensor& gate1, const Tensor& s2,
-                               const Tensor& ds, const Tensor& dv) {
-  OpGuard g(s, "gvp_ff_bwd");
-  const int64_t N = gvp_rows(s, v);
+// returns ds, dv, A1 (N, 576), A2 (N, 192), A3 (N, 192), A4 (N, 192) (gmp.h)
+std::vector<Tensor> gvp_ff_bwd(const Tensor& v, const std::vector<Tensor>& W, const Tensor& gate1,
+                               const Tensor& B2, const Tensor& s2, const Tensor& ds,
+                               const Tensor& dv) {
+  OpGuard g(v, "gvp_ff_bwd");
+  const int64_t N = gvp_rows(s2, v);
   gvp_w_checks(W, kGvpFFW);
-  for (const Tensor* t : {&s1, &gate1, &s2, &ds, &dv}) f32(*t, "gvp_ff saved / grad");
-  shape(s1, {N, 512}, "s1");
+  for (const Tensor* t : {&gate1, &B2, &ds, &dv}) f32(*t, "gvp_ff saved / grad");
   shape(gate1, {N, 32}, "gate1");
-  shape(s2, s.sizes(), "s2");
-  shape(ds, s.sizes(), "ds");
+  shape(B2, {N, 576}, "B2");
+  shape(ds, s2.sizes(), "ds");
   shape(dv, v.sizes(), "dv");
-  auto o = fopt(s);
-  Tensor ds_in = at::empty_like(s), dv_in = at::empty_like(v);
-  Tensor dp1 = at::empty({N, 512}, o), dp2 = at::empty({N, 128}, o);
-  Tensor dg1 = at::empty({N, 32}, o), dg2 = at::empty({N, 16}, o);
-  Tensor vn1 = at::empty({N, 32}, o), vn2 = at::empty({N, 32}, o);
-  Tensor du1 = at::empty({N, 32, 3}, o), dvh1 = at::empty({N, 32, 3}, o);
-  Tensor dvh2 = at::empty({N, 32, 3}, o), v1 = at::empty({N, 32, 3}, o);
-  Tensor du2 = at::empty({N, 16, 3}, o);
-  check_rc(gmp_gvp_ff_bwd_f32(N, fp(s), fp(v), fp(s1), fp(gate1), fp(s2), fp(ds), fp(dv),
-                              fp(W[0]), fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]),
-                              fp(W[6]), fp(W[7]), fp(W[8]), fp(W[9]), fp(W[10]), fp(W[11]),
-                              fp(ds_in), fp(dv_in), fp(dp1), fp(dp2), fp(dg1), fp(dg2), fp(vn1),
-                              fp(vn2), fp(du1), fp(dvh1), fp(dvh2), fp(v1), fp(du2), cur_stream()),
+  auto o = fopt(v);
+  Tensor ds_in = at::empty_like(s2), dv_in = at::empty_like(v);
+  Tensor A1 = at::empty({N, 576}, o), A2 = at::empty({N, 192}, o);
+  Tensor A3 = at::empty({N, 192}, o), A4 = at::empty({N, 192}, o);
+  check_rc(gmp_gvp_ff_bwd_f32(N, fp(v), fp(gate1), fp(B2), fp(s2), fp(ds), fp(dv), fp(W[0]),
+                              fp(W[1]), fp(W[2]), fp(W[3]), fp(W[4]), fp(W[5]), fp(W[6]),
+                              fp(W[7]), fp(W[8]), fp(W[9]), fp(W[10]), fp(W[11]), fp(ds_in),
+                              fp(dv_in), fp(A1), fp(A2), fp(A3), fp(A4), cur_stream()),
            "gmp_gvp_ff_bwd_f32");
-  return {ds_in, dv_in, dp1, dp2, dg1, dg2, vn1, vn2, du1, dvh1, dvh2, v1, du2};
+  return {ds_in, dv_in, A1, A2, A3, A4};
 }
 
 // the last message GVP fused with the receivers' sum / mean: (N, 128), (N, 16, 3) node rows
@@ -1721,20 +1718,18 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
   return {at::empty_like(s), at::empty_like(v)};
 }
 std::vector<Tensor> gvp_ff_fwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&) {
-  auto o = s.options();
-  return {at::empty_like(s), at::empty_like(v), at::empty({s.size(0), 512}, o),
-          at::empty({s.size(0), 32}, o)};
-}
-std::vector<Tensor> gvp_ff_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&,
-                               const Tensor&, const Tensor&, const Tensor&, const Tensor&,
-                               const Tensor&) {
   const int64_t N = s.size(0);
   auto o = s.options();
-  return {at::empty_like(s),        at::empty_like(v),         at::empty({N, 512}, o),
-          at::empty({N, 128}, o),   at::empty({N, 32}, o),     at::empty({N, 16}, o),
-          at::empty({N, 32}, o),    at::empty({N, 32}, o),     at::empty({N, 32, 3}, o),
-          at::empty({N, 32, 3}, o), at::empty({N, 32, 3}, o),  at::empty({N, 32, 3}, o),
-          at::empty({N, 16, 3}, o)};
+  return {at::empty_like(s),       at::empty_like(v),      at::empty({N, 32}, o),
+          at::empty({N, 192}, o),  at::empty({N, 576}, o), at::empty({N, 64}, o),
+          at::empty({N, 128}, o)};
+}
+std::vector<Tensor> gvp_ff_bwd(const Tensor& v, const std::vector<Tensor>&, const Tensor&,
+                               const Tensor&, const Tensor& s2, const Tensor&, const Tensor&) {
+  const int64_t N = s2.size(0);
+  auto o = s2.options();
+  return {at::empty_like(s2),     at::empty_like(v),      at::empty({N, 576}, o),
+          at::empty({N, 192}, o), at::empty({N, 192}, o), at::empty({N, 192}, o)};
 }
 
 std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&,
@@ -1885,8 +1880,8 @@ TORCH_LIBRARY(gmp, m) {
   m.def("edge_outer_sum_act(Tensor A, Tensor X, Tensor w, Tensor b, int act, Tensor? amax=None) "
         "-> (Tensor C, Tensor colsum)");
   m.def("gvp_ff_fwd(Tensor s, Tensor v, Tensor[] W) -> Tensor[]");
-  m.def("gvp_ff_bwd(Tensor s, Tensor v, Tensor[] W, Tensor s1, Tensor gate1, Tensor s2, "
-        "Tensor ds, Tensor dv) -> Tensor[]");
+  m.def("gvp_ff_bwd(Tensor v, Tensor[] W, Tensor gate1, Tensor B2, Tensor s2, Tensor ds, "
+        "Tensor dv) -> Tensor[]");
   m.def("gvp_layer_fwd(Tensor s, Tensor v, Tensor[] W, bool relu) -> (Tensor s_out, "
         "Tensor v_out)");
   m.def("gvp_layer_bwd(Tensor s, Tensor v, Tensor[] W, Tensor ds, Tensor dv, bool relu, "

@@ -158,8 +158,8 @@ SIGNATURES = {
     "gmp_gvp_layer_fwd_agg_f32": (c_int, [c_i64, c_i64, c_int] + [c_vp] * 13 + [c_vp]),
     "gmp_gvp_msg0_bwd_agg_f32": (c_int, [c_i64, c_i64] + [c_vp] * 30 + [c_vp]),
     "gmp_gvp_msg0_fwd_f32": (c_int, [c_i64] + [c_vp] * 15 + [c_vp]),
-    "gmp_gvp_ff_fwd_f32": (c_int, [c_i64] + [c_vp] * 18 + [c_vp]),
-    "gmp_gvp_ff_bwd_f32": (c_int, [c_i64] + [c_vp] * 32 + [c_vp]),
+    "gmp_gvp_ff_fwd_f32": (c_int, [c_i64] + [c_vp] * 21 + [c_vp]),
+    "gmp_gvp_ff_bwd_f32": (c_int, [c_i64] + [c_vp] * 25 + [c_vp]),
     "gmp_gvp_edge_embed_fwd_f32": (c_int, [c_i64, c_i64, c_i64] + [c_vp] * 10 + [c_f32, c_vp,
                                                                                  c_vp, c_vp]),
     "gmp_gvp_edge_embed_bwd_workspace_size": (c_size, [c_i64]),

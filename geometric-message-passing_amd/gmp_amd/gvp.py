@@ -643,14 +643,15 @@ def _ff_fusable(ff, x):
             g1.vector_gate and g2.vector_gate and g1.vector_act is None and
             g2.vector_act is None and g1.scalar_act is F.relu and g2.scalar_act is None and
             s.is_cuda and s.dtype == torch.float32 and v.dtype == torch.float32 and
-            s.dim() == 2 and v.dim() == 3 and v.shape[1:] == (16, 3))
+            s.dim() == 2 and v.dim() == 3 and v.shape[1:] == (16, 3) and
+            all(w.data_ptr() % 16 == 0 for w in (g1.ws.weight, g1.wsv.weight, g2.ws.weight)))
 
 
 class GvpFFFn(torch.autograd.Function):
     """K17 (gmp_gvp_ff_{fwd,bwd}_f32): GVPConvLayer's node feed-forward GVP((128, 16), (512, 32))
     -> GVP((512, 32), (128, 16)) (gvp_layer.py:361-366, :433-434; GVP.forward :140-170) as one
-    kernel per direction; the weight gradients are node outer sums of the backward's factors on
-    the side stream (deferred to the end of the backward pass)."""
+    kernel per direction; the weight gradients are four node outer sums of operands the kernels
+    write side by side (gmp.h), on the side stream and deferred to the end of the backward."""
 
     @staticmethod
     def forward(ctx, s, v, *W):
@@ -658,49 +659,45 @@ class GvpFFFn(torch.autograd.Function):
         ops._need_cuda(s, v)
         Wc = [ops._f32c(w) for w in W]
         with ops._timed("gvp_ff_fwd"):
-            s2, v2, s1, gate1 = _lib.torch_ops().gvp_ff_fwd(s, v, Wc)
-        ctx.save_for_backward(s, v, s1, gate1, s2, *Wc)
+            s2, v2, gate1, B1, B2, B3, B4 = _lib.torch_ops().gvp_ff_fwd(s, v, Wc)
+        ctx.save_for_backward(v, gate1, B1, B2, B3, B4, s2, *Wc)
         return s2, v2
 
     @staticmethod
     @once_differentiable
     def backward(ctx, ds, dv):
-        s, v, s1, gate1, s2, *W = ctx.saved_tensors
+        v, gate1, B1, B2, B3, B4, s2, *W = ctx.saved_tensors
         ds = ops._f32c(ds) if ds is not None else torch.zeros_like(s2)
         dv = ops._f32c(dv) if dv is not None else torch.zeros_like(v)
         with ops._timed("gvp_ff_bwd"):
-            (ds_in, dv_in, dp1, dp2, dg1, dg2, vn1, vn2, du1, dvh1, dvh2, v1,
-             du2) = _lib.torch_ops().gvp_ff_bwd(s, v, W, s1, gate1, s2, ds, dv)
-        return (ds_in, dv_in) + _ff_wgrads(ctx.needs_input_grad, s, v, s1, s2, W, dp1, dp2, dg1,
-                                           dg2, vn1, vn2, du1, dvh1, dvh2, v1, du2)
+            ds_in, dv_in, A1, A2, A3, A4 = _lib.torch_ops().gvp_ff_bwd(v, W, gate1, B2, s2, ds, dv)
+        return (ds_in, dv_in) + _ff_wgrads(ctx.needs_input_grad, W, (A1, A2, A3, A4),
+                                           (B1, B2, B3, B4))
 
 
-def _ff_wgrads(needs_input_grad, s, v, s1, s2, W, dp1, dp2, dg1, dg2, vn1, vn2, du1, dvh1, dvh2,
-               v1, du2):
-    """K17's weight gradients from its per-node factors (gmp.h gmp_gvp_ff_bwd_f32): deterministic
-    node outer sums on the side stream; dWsv1 through Ws1 (p1 = Ws1 [s | vn1] + b1 is not
-    stored), dWv1 / dWv2 through Wh1 / Wh2 (vh = Wh v is not stored)."""
-    N = s.shape[0]
-    Wh1, Ws1, b1, _, _, _, Wh2, _, _, _, _, _ = W
-    v48, v196 = v.reshape(N, 48), v1.reshape(N, 96)
-    with ops.side_work(dp1, s, vn1, dg1, du1, dvh1, v, dp2, s1, vn2, dg2, s2, du2, dvh2,
-                       v1) as sw:
-        A, db1 = _osum(dp1, s)                                   # (512, 128)
-        B, _ = _osum(dp1, vn1)                                   # (512, 32)
-        dWs1 = torch.cat([A, B], 1)
-        Gs, dbsv1 = _osum(dg1, s)
-        Gv, _ = _osum(dg1, vn1)
-        dWsv1 = torch.addmm(torch.outer(dbsv1, b1), torch.cat([Gs, Gv], 1), Ws1.t())
-        dWh1 = _diag3(_osum(dvh1.reshape(N, 96), v48)[0], 32, 16)
-        dWv1 = _diag3(_osum(du1.reshape(N, 96), v48)[0], 32, 16).mm(Wh1.t())
-        A2, db2 = _osum(dp2, s1)                                 # (128, 512)
-        B2, _ = _osum(dp2, vn2)                                  # (128, 32)
-        dWs2 = torch.cat([A2, B2], 1)
-        dWsv2, dbsv2 = _osum(dg2, s2)                            # (16, 128)
-        dWh2 = _diag3(_osum(dvh2.reshape(N, 96), v196)[0], 32, 32)
-        dWv2 = _diag3(_osum(du2.reshape(N, 48), v196)[0], 16, 32).mm(Wh2.t())
-    grads = (dWh1, dWs1, db1, dWv1, dWsv1, dbsv1, dWh2, dWs2, db2, dWv2, dWsv2, dbsv2)
-    return sw.deliver(needs_input_grad, 2, W, grads)
+def _ff_wgrads(needs_input_grad, W, As, Bs):
+    """K17's weight gradients: C_k = A_k^T B_k (one node outer sum each, the quadrant kernel) and
+    their blocks (gmp.h gmp_gvp_ff_bwd_f32), on the side stream, deferred."""
+    Wh1, Ws1, b1, _, _, _, Wh2, Ws2, b2, _, _, _ = W
+    f = dict(dtype=torch.float32, device=Ws1.device)
+    with ops.side_work(*As, *Bs) as sw:
+        C, cs = [], []
+        for A, B in zip(As, Bs):
+            c, k = torch.empty((A.shape[1], B.shape[1]), **f), torch.empty(A.shape[1], **f)
+            ops.outer_sum_into(A, B, c, k)
+            C.append(c)
+            cs.append(k)
+        dWs1, db1, dbsv1 = C[0][:512, :160], cs[0][:512], cs[0][512:544]
+        dWsv1 = torch.addmm(torch.outer(dbsv1, b1), C[0][512:544, :160], Ws1.t())
+        dWs2, db2, dbsv2 = C[1][:128, :544], cs[1][:128], cs[1][128:144]
+        dWsv2 = torch.addmm(torch.outer(dbsv2, b2), C[1][128:144, :544], Ws2.t())
+        dWh1 = _diag3(C[2][:96, :48], 32, 16)
+        dWv1 = _diag3(C[2][96:, :48], 32, 16).mm(Wh1.t())
+        dWh2 = _diag3(C[3][:96, :96], 32, 32)
+        dWv2 = _diag3(C[3][96:144, :96], 16, 32).mm(Wh2.t())
+        grads = [dWh1, dWs1, db1, dWv1, dWsv1, dbsv1, dWh2, dWs2, db2, dWv2, dWsv2, dbsv2]
+        grads = [g.contiguous() for g in grads]
+    return sw.deliver(needs_input_grad, 2, W, tuple(grads))
 
 
 def gvp_ff(ff, x):

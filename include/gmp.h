@@ -589,32 +589,36 @@ int gmp_gvp_edge_embed_bwd_f32(int64_t n_edges, int64_t radial_dim, int64_t so,
  * (models/layers/gvp_layer.py:361-366, :433-434 -- ff_func = GVP((128, 16), (512, 32)) with
  * activations (relu, None) then GVP((512, 32), (128, 16)) with (None, None), vector_gate, h_dim 32;
  * GVP.forward gvp_layer.py:140-170) over N node rows in one kernel per direction.  s (N, 128),
- * v (N, 16, 3) row-major 16-byte aligned; weights in the reference's nn.Linear layout: Wh1
- * (32, 16), Ws1 (512, 160) [columns s | |vh1|], b1 (512), Wv1 (32, 32), Wsv1 (32, 512), bsv1 (32),
- * Wh2 (32, 32), Ws2 (128, 544) [columns s1 | |vh2|], b2 (128), Wv2 (16, 32), Wsv2 (16, 128),
- * bsv2 (16).  Forward: s2 (N, 128), v2 (N, 16, 3) and, for the backward, s1 = relu(p1) (N, 512)
- * and gate1 (N, 32) (the first GVP's gate pre-activation).  Backward: from grad_s2, grad_v2 (and
- * s2 itself, the second GVP's pre-activation) the input gradients ds (N, 128), dv (N, 16, 3) and
- * the per-node factors of the weight gradients: dp1 (N, 512), dp2 (N, 128) [gradients at the
- * scalar Linears' outputs], dgate1 (N, 32), dgate2 (N, 16), vn1, vn2 (N, 32) [|vh|], du1, dvh1,
- * dvh2, v1 (N, 32, 3) and du2 (N, 16, 3) [du = grad_v * sigmoid(gate), dvh the gradient at vh,
- * v1 the first GVP's vector output], so that dWs1 = dp1^T [s | vn1], dWsv1 = (dgate1^T [s | vn1])
- * Ws1^T + (1^T dgate1) b1^T, dWv1[o, h] = sum_(n,x) du1[n,o,x] (Wh1 v)[n,h,x], dWh1 =
- * sum dvh1 (x) v, dWs2 = dp2^T [s1 | vn2], dWsv2 = dgate2^T s2, dWv2 = sum du2 (x) (Wh2 v1),
- * dWh2 = sum dvh2 (x) v1 (the caller's deterministic outer sums).  Exact f32 products. */
+ * v (N, 16, 3) row-major, all row tensors 16-byte aligned; weights in the reference's nn.Linear
+ * layout: Wh1 (32, 16), Ws1 (512, 160) [columns s | |vh1|], b1 (512), Wv1 (32, 32), Wsv1
+ * (32, 512), bsv1 (32), Wh2 (32, 32), Ws2 (128, 544) [columns s1 | |vh2|], b2 (128), Wv2 (16, 32),
+ * Wsv2 (16, 128), bsv2 (16); Ws1, Wsv1, Ws2 16-byte aligned.
+ * Forward: s2 (N, 128), v2 (N, 16, 3), gate1 (N, 32) [the first GVP's gate pre-activation] and
+ * the right operands of the weight sums, zero-padded: B1 = [s | vn1 | 0] (N, 192),
+ * B2 = [s1 | vn2 | 0] (N, 576) [s1 = relu(p1), vn = |vh| clamped], B3 = [v | 0] (N, 64),
+ * B4 = [v1 | 0] (N, 128) [v1 the first GVP's vector output, (channel, xyz)].
+ * Backward (from gate1, B2, s2 = the second GVP's pre-activation, grad_s2, grad_v2): ds (N, 128),
+ * dv (N, 16, 3) and the left operands A1 = [dp1 | dgate1 | 0] (N, 576), A2 = [dp2 | dgate2 | 0]
+ * (N, 192), A3 = [dvh1 | du1] (N, 192), A4 = [dvh2 | du2 | 0] (N, 192) [dp the gradient at a
+ * scalar Linear's output, du = grad_v * sigmoid(gate) at W_v vh, dvh at vh; (channel, xyz)].
+ * With C_k = A_k^T B_k (sums over the N rows) and x~ the xyz diagonal of a (3a, 3b) block:
+ *   dWs1 = C1[:512, :160], db1 = colsum(dp1), dWsv1 = C1[512:544, :160] Ws1^T + dbsv1 b1^T;
+ *   dWs2 = C2[:128, :544], db2 = colsum(dp2), dWsv2 = C2[128:144, :544] Ws2^T + dbsv2 b2^T;
+ *   dWh1 = C3[:96, :48]~, dWv1 = C3[96:, :48]~ Wh1^T; dWh2 = C4[:96, :96]~,
+ *   dWv2 = C4[96:144, :96]~ Wh2^T.  Exact f32 products. */
 int gmp_gvp_ff_fwd_f32(int64_t n_nodes, const float* s_in, const float* v_in, const float* Wh1,
                        const float* Ws1, const float* b1, const float* Wv1, const float* Wsv1,
                        const float* bsv1, const float* Wh2, const float* Ws2, const float* b2,
                        const float* Wv2, const float* Wsv2, const float* bsv2, float* s_out,
-                       float* v_out, float* s1_out, float* gate1_out, void* stream);
-int gmp_gvp_ff_bwd_f32(int64_t n_nodes, const float* s_in, const float* v_in, const float* s1,
-                       const float* gate1, const float* s2, const float* ds_out,
-                       const float* dv_out, const float* Wh1, const float* Ws1, const float* b1,
-                       const float* Wv1, const float* Wsv1, const float* bsv1, const float* Wh2,
-                       const float* Ws2, const float* b2, const float* Wv2, const float* Wsv2,
-                       const float* bsv2, float* ds_in, float* dv_in, float* dp1, float* dp2,
-                       float* dgate1, float* dgate2, float* vn1, float* vn2, float* du1,
-                       float* dvh1, float* dvh2, float* v1, float* du2, void* stream);
+                       float* v_out, float* gate1_out, float* B1, float* B2, float* B3, float* B4,
+                       void* stream);
+int gmp_gvp_ff_bwd_f32(int64_t n_nodes, const float* v_in, const float* gate1, const float* B2,
+                       const float* s2, const float* ds_out, const float* dv_out,
+                       const float* Wh1, const float* Ws1, const float* b1, const float* Wv1,
+                       const float* Wsv1, const float* bsv1, const float* Wh2, const float* Ws2,
+                       const float* b2, const float* Wv2, const float* Wsv2, const float* bsv2,
+                       float* ds_in, float* dv_in, float* A1, float* A2, float* A3, float* A4,
+                       void* stream);
 int gmp_gvp_msg0_fwd_f32(int64_t n_edges, const int64_t* send, const int64_t* recv,
                          const float* P, const float* Q, const float* es, const float* ev,
                          const float* We, const float* Wn, const float* b, const float* Wv,

@@ -580,8 +580,12 @@ def test_gvp_ff_fused_vs_oracle(n):
 
 
 def test_gvp_ff_fused_matches_chain_and_is_deterministic():
-    """At the C3 node count (50k) the fused feed-forward equals the module chain on the device
-    (outputs 1e-5, gradients 1e-4 of scale) and two runs are bitwise equal."""
+    """At the C3 node count (50k): two runs of K17 bitwise equal, and K17 against the fp64 oracle
+    no worse than 1e-5 (outputs) / 1e-4 (gradients) of scale + 2x the module chain's own error
+    on the device.  (At 50k rows some first-GVP pre-activations sit within fp32 rounding of the
+    ReLU kink -- row 16341 here at 3.6e-8 -- and a correct fp32 evaluation may take the other
+    branch there: the reference's torch ops on the device do, scripts/dbg_gvp_chain.py; that row
+    moves the weight sums by ~1e-4 of scale, so fp64 is the yardstick, as elsewhere.)"""
     import gmp_amd.gvp as g
     ref = _ff_pair(5)
     lay = torch.nn.Sequential(g.GVP((128, 16), (512, 32), activations=(RELU, None),
@@ -590,8 +594,10 @@ def test_gvp_ff_fused_matches_chain_and_is_deterministic():
                                     vector_gate=True))
     lay.load_state_dict(ref.state_dict())
     lay = lay.to(DEV)
-    s, v = _ff_inputs(50_000, 3)
-    gs, gv = torch.randn(50_000, 128, device=DEV), torch.randn(50_000, 16, 3, device=DEV)
+    n = 50_000
+    s, v = _ff_inputs(n, 3)
+    torch.manual_seed(9)
+    gs, gv = torch.randn(n, 128), torch.randn(n, 16, 3)
 
     def run(fused):
         g.GVP_FF_FUSED = fused
@@ -599,7 +605,7 @@ def test_gvp_ff_fused_matches_chain_and_is_deterministic():
             lay.zero_grad(set_to_none=True)
             sd, vd = s.to(DEV).requires_grad_(True), v.to(DEV).requires_grad_(True)
             so, vo = g.gvp_ff(lay, (sd, vd))
-            ((so * gs).sum() + (vo * gv).sum()).backward()
+            ((so * gs.to(DEV)).sum() + (vo * gv.to(DEV)).sum()).backward()
             return [so.detach(), vo.detach(), sd.grad, vd.grad] + \
                 [p.grad.clone() for p in lay.parameters() if p.numel()]
         finally:
@@ -607,23 +613,18 @@ def test_gvp_ff_fused_matches_chain_and_is_deterministic():
 
     a, b, c = run(True), run(True), run(False)
     assert all(torch.equal(x, y) for x, y in zip(a, b))
-    # rows whose first-GVP pre-activation has an entry at the ReLU kink (|p1| within fp32
-    # rounding of 0: row 16341 here, 3.6e-8) may take the other branch in one of two correct fp32
-    # evaluations (measured: the reference's torch ops on the device flip it, K17 does not), so
-    # the input gradients are compared on the other rows (scripts/dbg_gvp_chain.py)
-    with torch.no_grad():
-        g1 = copy.deepcopy(ref[0]).double()
-        vh = g1.wh(v.double().transpose(-1, -2))
-        vn = torch.sqrt(torch.clamp((vh ** 2).sum(-2), min=1e-8))
-        p1 = g1.ws(torch.cat([s.double(), vn], -1)).abs()
-        ok = (p1.amin(1) > 1e-5 * p1.max()).to(DEV)
-    assert int((~ok).sum()) < 5
-    for i, (x, y) in enumerate(zip(a, c)):
-        if i in (2, 3):
-            x, y = x[ok], y[ok]
-        sc = y.abs().max().item()
-        tol = 1e-5 if i < 2 else 1e-4
-        assert (x - y).abs().max().item() <= tol * max(sc, 1.0 if i < 2 else sc) + 1e-7, i
+    ref64 = copy.deepcopy(ref).double()
+    s64, v64 = s.double().requires_grad_(True), v.double().requires_grad_(True)
+    so, vo = ref64((s64, v64))
+    ((so * gs.double()).sum() + (vo * gv.double()).sum()).backward()
+    r = [so.detach(), vo.detach(), s64.grad, v64.grad] + \
+        [p.grad for p in ref64.parameters() if p.numel()]
+    for i, (x, y, t) in enumerate(zip(a, c, r)):
+        ef = (x.cpu().double() - t).abs().max().item()
+        ec = (y.cpu().double() - t).abs().max().item()
+        sc = t.abs().max().item()
+        tol = (1e-5 * max(sc, 1.0)) if i < 2 else 1e-4 * sc
+        assert ef <= tol + 2 * ec + 1e-7, (i, ef, ec, sc)
 
 
 def test_gvp_model_c3_uses_fused_ff():
