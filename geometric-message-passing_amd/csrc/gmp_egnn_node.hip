@@ -342,6 +342,184 @@ int launch_node(int64_t N, const float* h, const float* m, const gmp_egnn_node_p
   return launch_status();
 }
 
+// ================================================================================== K15b backward
+// The node update's backward in one launch (r06): from the upstream gradient g of h_out and the
+// forward's saved x_hat1, x_hat2 / 1/std,
+//   dz2 = g act'(x_hat2 w2 + b2), dpre2 = LN2'(dz2 w2);  dx1 = W3^T dpre2;
+//   dz1 = dx1 act'(x_hat1 w1 + b1), dpre1 = LN1'(dz1 w1);
+//   dh = W0[:, :d]^T dpre1 (+ g: residual), dm = W0[:, d:]^T dpre1,
+// and the LayerNorm affine gradients [dw1 | db1 | dw2 | db2] = sum_rows [dz1 x1 | dz1 | dz2 x2 |
+// dz2] as one partial row per workgroup (fixed order).  dpre1, dpre2 are written for the
+// caller's weight sums (dW0 = dpre1^T [h | m], dW3 = dpre2^T act(LN1)).  Exact f32 MFMA; one
+// 16-row tile per wave, 8 waves per workgroup; W3 then W0 pass through the same LDS region (two
+// phases, the row tile's dpre1 and g carried in registers between them).  Replaces two
+// LayerNorm-backward kernels with their partial-sum finishes, three library GEMMs and the
+// residual add per layer (r05 trace: ~190 us of the ~9 ms EGNN step per layer).
+constexpr int kNbWaves = 8;
+template <int D>
+__device__ __forceinline__ float slot(const f32x4 (&x)[D / 16], int s) { return x[s >> 2][s & 3]; }
+template <int D>
+struct NbCfg {
+  static constexpr int LD3 = D + 4, LD0 = 2 * D + 4;
+  static constexpr int W_FLOATS = D * LD0;                // the larger of W3 / W0 in LDS
+  static constexpr int VEC = W_FLOATS;                    // ln1w, ln1b, ln2w, ln2b (4 D)
+  static constexpr size_t smem_bytes() { return (size_t)(W_FLOATS + 4 * D) * sizeof(float); }
+};
+
+// y[slot(k)] += sum_o W[o][k0 + k] gin[slot(o)] with W row stride ldw
+template <int D>
+__device__ __forceinline__ void gemm_wtx_ld(const float* __restrict__ sW, int ldw,
+                                            const f32x4 (&gin)[D / 16], f32x4 (&y)[D / 16], int i,
+                                            int g) {
+  constexpr int T = D / 16;
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float* wrow = sW + (16 * p + 4 * g + c) * ldw + i;
+      float a[T];
+#pragma unroll
+      for (int t = 0; t < T; ++t) a[t] = wrow[16 * t];
+#pragma unroll
+      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], gin[p][c], y[t], 0, 0, 0);
+      gemm_fence();
+    }
+  }
+}
+
+// rows x cols floats of a row-major global matrix (row stride sld) into LDS (row stride ld),
+// float4 loads issued together per thread
+template <int ROWS, int COLS>
+__device__ __forceinline__ void nb_copy(float* dst, int ld, const float* __restrict__ src,
+                                        int64_t sld) {
+  constexpr int N4 = ROWS * COLS / 4, PER = (N4 + kNbWaves * 64 - 1) / (kNbWaves * 64);
+  f32x4 r[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int x = threadIdx.x + k * kNbWaves * 64;
+    const int row = x / (COLS / 4), c4 = x - row * (COLS / 4);
+    if (x < N4) r[k] = *reinterpret_cast<const f32x4*>(src + row * sld + 4 * c4);
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int x = threadIdx.x + k * kNbWaves * 64;
+    const int row = x / (COLS / 4), c4 = x - row * (COLS / 4);
+    if (x < N4) *reinterpret_cast<f32x4*>(dst + row * ld + 4 * c4) = r[k];
+  }
+}
+
+template <int D, int ACT, bool RES>
+__global__ __launch_bounds__(kNbWaves * 64) void egnn_node_bwd_kernel(
+    int64_t N, const float* __restrict__ gout, const float* __restrict__ xsave,
+    const float* __restrict__ rsave, const float* __restrict__ W0, const float* __restrict__ W3,
+    const float* __restrict__ ln1w, const float* __restrict__ ln1b,
+    const float* __restrict__ ln2w, const float* __restrict__ ln2b, float* __restrict__ dh,
+    float* __restrict__ dm, float* __restrict__ dpre1_out, float* __restrict__ dpre2_out,
+    float* __restrict__ partials) {
+  using C = NbCfg<D>;
+  constexpr int T = D / 16, K = VecAcc<D>::K;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sV = smem + C::VEC;  // [ln1w | ln1b | ln2w | ln2b]
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int wid = threadIdx.x >> 6;
+  nb_copy<D, D>(smem, C::LD3, W3, D);
+  for (int x = threadIdx.x; x < D; x += blockDim.x) {
+    sV[x] = ln1w[x];
+    sV[D + x] = ln1b[x];
+    sV[2 * D + x] = ln2w[x];
+    sV[3 * D + x] = ln2b[x];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * (kNbWaves * 16) + wid * 16;
+  const bool valid = r0 + i < N;
+  const int64_t n = valid ? r0 + i : N - 1;
+  const float vf = valid ? 1.f : 0.f;
+  const size_t ND = (size_t)N * D;
+  f32x4 gr[T], xh[T], a[T];
+  load_row<D>(gr, gout + n * D, g);
+  load_row<D>(xh, xsave + ND + n * D, g);  // x_hat2
+  const float rs2 = rsave[N + n], rs1 = rsave[n];
+  float vacc[4][K];
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+#pragma unroll
+    for (int k = 0; k < K; ++k) vacc[v][k] = 0.f;
+  __syncthreads();
+  // ---- LN2 + act backward: dz2 -> dpre2 (a)
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+    const f32x4 w = vec4<D>(sV, 2, p, g), b = vec4<D>(sV, 3, p, g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[p][q] = vf * gr[p][q] * act_df<ACT>(xh[p][q] * w[q] + b[q]);
+  }
+  accumulate_vec<D>([&](int s) { return slot<D>(a, s) * slot<D>(xh, s); }, vacc[2], i);
+  accumulate_vec<D>([&](int s) { return slot<D>(a, s); }, vacc[3], i);
+#pragma unroll
+  for (int p = 0; p < T; ++p) a[p] *= vec4<D>(sV, 2, p, g);
+  ln_backward<D>(a, xh, rs2);
+  if (valid) store_row<D>(dpre2_out + n * D, a, g);
+  // ---- dx1 = W3^T dpre2 (xh <- dx1), then LN1 + act backward: dpre1 (a)
+  load_row<D>(xh, xsave + n * D, g);  // x_hat1 (in flight during the product)
+  f32x4 dx[T];
+#pragma unroll
+  for (int p = 0; p < T; ++p) dx[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gemm_wtx_ld<D>(smem, C::LD3, a, dx, i, g);
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+    const f32x4 w = vec4<D>(sV, 0, p, g), b = vec4<D>(sV, 1, p, g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[p][q] = vf * dx[p][q] * act_df<ACT>(xh[p][q] * w[q] + b[q]);
+  }
+  accumulate_vec<D>([&](int s) { return slot<D>(a, s) * slot<D>(xh, s); }, vacc[0], i);
+  accumulate_vec<D>([&](int s) { return slot<D>(a, s); }, vacc[1], i);
+#pragma unroll
+  for (int p = 0; p < T; ++p) a[p] *= vec4<D>(sV, 0, p, g);
+  ln_backward<D>(a, xh, rs1);
+  if (valid) store_row<D>(dpre1_out + n * D, a, g);
+  // ---- phase B: W0 replaces W3 in LDS; dh = W0[:, :d]^T dpre1 (+ g), dm = W0[:, d:]^T dpre1
+  __syncthreads();
+  nb_copy<D, 2 * D>(smem, C::LD0, W0, 2 * D);
+  __syncthreads();
+  if (!RES) {
+#pragma unroll
+    for (int p = 0; p < T; ++p) gr[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  gemm_wtx_ld<D>(smem, C::LD0, a, gr, i, g);
+  if (valid) store_row<D>(dh + n * D, gr, g);
+#pragma unroll
+  for (int p = 0; p < T; ++p) gr[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gemm_wtx_ld<D>(smem + D, C::LD0, a, gr, i, g);
+  if (valid) store_row<D>(dm + n * D, gr, g);
+  // ---- workgroup partial row of [dw1 | db1 | dw2 | db2] (waves in order: deterministic)
+  __syncthreads();  // every wave is done with W0: reuse that LDS
+  float* red = smem;  // [wave][4 D]
+  if (acc_owner<D>(i)) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int k = 0; k < K; ++k) red[wid * 4 * D + v * D + featq(acc_slot<D>(i, k), g)] = vacc[v][k];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 4 * D; t += blockDim.x) {
+    float sacc = 0.f;
+    for (int w = 0; w < kNbWaves; ++w) sacc += red[w * 4 * D + t];
+    partials[(int64_t)blockIdx.x * 4 * D + t] = sacc;
+  }
+}
+
+template <int D, int ACT, bool RES>
+int launch_node_bwd(int64_t N, const float* g, const float* xs, const float* rs, const float* W0,
+                    const float* W3, const float* l1w, const float* l1b, const float* l2w,
+                    const float* l2b, float* dh, float* dm, float* dp1, float* dp2, float* part,
+                    hipStream_t s) {
+  auto k = egnn_node_bwd_kernel<D, ACT, RES>;
+  const size_t smem = NbCfg<D>::smem_bytes();
+  int rc = prep_kernel_once((const void*)k, smem);
+  if (rc) return rc;
+  k<<<(unsigned)ceil_div(N, kNbWaves * 16), kNbWaves * 64, smem, s>>>(
+      N, g, xs, rs, W0, W3, l1w, l1b, l2w, l2b, dh, dm, dp1, dp2, part);
+  return launch_status();
+}
+
 size_t image_bytes(int64_t d) {
   return d == 128 ? NImg<128>::bytes : d == 64 ? NImg<64>::bytes : d == 32 ? NImg<32>::bytes : 0;
 }
@@ -417,6 +595,36 @@ int gmp_egnn_node_fwd_f32(int64_t n_nodes, int64_t d, const float* h, const floa
 #undef LAUNCH_NODE2
 #undef LAUNCH_NODE3
 #undef LAUNCH_NODE4
+  return rc;
+}
+
+int64_t gmp_egnn_node_bwd_partial_rows(int64_t n_nodes) {
+  return n_nodes > 0 ? ceil_div(n_nodes, kNbWaves * 16) : 0;
+}
+
+int gmp_egnn_node_bwd_f32(int64_t n_nodes, int64_t d, int act, int residual, const float* grad_h,
+                          const float* save_xhat, const float* save_rstd, const float* W0,
+                          const float* W3, const float* ln1_w, const float* ln1_b,
+                          const float* ln2_w, const float* ln2_b, float* dh, float* dm,
+                          float* dpre1, float* dpre2, float* partials, void* stream) {
+  if (!(d == 32 || d == 64 || d == 128)) return GMP_ERR_UNSUPPORTED;
+  GMP_CHECK_ARG(n_nodes >= 0 && (act == 0 || act == 1));
+  if (n_nodes == 0) return GMP_OK;
+  GMP_CHECK_ARG(grad_h && save_xhat && save_rstd && W0 && W3 && ln1_w && ln1_b && ln2_w &&
+                ln2_b && dh && dm && dpre1 && dpre2 && partials);
+  GMP_CHECK_ARG(aligned16(grad_h) && aligned16(save_xhat) && aligned16(W0) && aligned16(W3) &&
+                aligned16(dh) && aligned16(dm) && aligned16(dpre1) && aligned16(dpre2));
+  hipStream_t s = as_stream(stream);
+  int rc;
+#define LNB(DD, AA, RR)                                                                        \
+  rc = launch_node_bwd<DD, AA, RR>(n_nodes, grad_h, save_xhat, save_rstd, W0, W3, ln1_w, ln1_b, \
+                                   ln2_w, ln2_b, dh, dm, dpre1, dpre2, partials, s)
+#define LNB2(DD)                                                             \
+  if (act == 0) { if (residual) LNB(DD, 0, true); else LNB(DD, 0, false); } \
+  else { if (residual) LNB(DD, 1, true); else LNB(DD, 1, false); }
+  if (d == 128) { LNB2(128) } else if (d == 64) { LNB2(64) } else { LNB2(32) }
+#undef LNB2
+#undef LNB
   return rc;
 }
 

@@ -1252,6 +1252,41 @@ std::vector<Tensor> gvp_layer_bwd(const Tensor& s, const Tensor& v, const std::v
   return {ds_in, dv_in, dspre, spre, dgate, vn, vh, dvpre, dvh};
 }
 
+// K15b: the EGNN node update's backward; vecs = [ln1_w, ln1_b, ln2_w, ln2_b]; returns dh, dm,
+// dpre1, dpre2 and gb = [d ln1_w | d ln1_b | d ln2_w | d ln2_b] (4 d; partial rows summed in order)
+std::vector<Tensor> egnn_node_bwd(const Tensor& g, const Tensor& xhat, const Tensor& rstd,
+                                  const Tensor& W0, const Tensor& W3,
+                                  const std::vector<Tensor>& vecs, int64_t act, bool residual) {
+  OpGuard og(g, "egnn_node_bwd");
+  f32(g, "grad_h");
+  TORCH_CHECK(g.dim() == 2, "gmp.egnn_node_bwd: grad_h (N, d)");
+  const int64_t N = g.size(0), d = g.size(1);
+  f32(xhat, "xhat");
+  f32(rstd, "rstd");
+  shape(xhat, {2, N, d}, "xhat");
+  shape(rstd, {2, N}, "rstd");
+  f32(W0, "W0");
+  f32(W3, "W3");
+  shape(W0, {d, 2 * d}, "W0");
+  shape(W3, {d, d}, "W3");
+  TORCH_CHECK(vecs.size() == 4, "gmp.egnn_node_bwd: 4 LayerNorm vectors expected");
+  for (const auto& v : vecs) {
+    f32(v, "LayerNorm vector");
+    numel(v, d, "LayerNorm vector");
+  }
+  auto o = g.options();
+  Tensor dh = at::empty({N, d}, o), dm = at::empty({N, d}, o);
+  Tensor dp1 = at::empty({N, d}, o), dp2 = at::empty({N, d}, o);
+  Tensor part = at::empty({gmp_egnn_node_bwd_partial_rows(N), 4 * d}, o);
+  check_rc(gmp_egnn_node_bwd_f32(N, d, (int)act, residual ? 1 : 0, fp(g), fp(xhat), fp(rstd),
+                                 fp(W0), fp(W3), fp(vecs[0]), fp(vecs[1]), fp(vecs[2]),
+                                 fp(vecs[3]), fp(dh), fp(dm), fp(dp1), fp(dp2), fp(part),
+                                 cur_stream()),
+           "gmp_egnn_node_bwd_f32");
+  Tensor gb = N > 0 ? part.sum(0) : at::zeros({4 * d}, o);
+  return {dh, dm, dp1, dp2, gb};
+}
+
 // K17 node feed-forward: W = [Wh1, Ws1, b1, Wv1, Wsv1, bsv1, Wh2, Ws2, b2, Wv2, Wsv2, bsv2]
 const std::vector<std::vector<int64_t>> kGvpFFW = {{32, 16}, {512, 160}, {512}, {32, 32},
                                                    {32, 512}, {32}, {32, 32}, {128, 544},
@@ -1717,6 +1752,13 @@ std::tuple<Tensor, Tensor> gvp_layer_fwd(const Tensor& s, const Tensor& v,
                                          const std::vector<Tensor>&, bool) {
   return {at::empty_like(s), at::empty_like(v)};
 }
+std::vector<Tensor> egnn_node_bwd(const Tensor& g, const Tensor&, const Tensor&, const Tensor&,
+                                  const Tensor&, const std::vector<Tensor>&, int64_t, bool) {
+  const int64_t N = g.size(0), d = g.size(1);
+  auto o = g.options();
+  return {at::empty({N, d}, o), at::empty({N, d}, o), at::empty({N, d}, o),
+          at::empty({N, d}, o), at::empty({4 * d}, o)};
+}
 std::vector<Tensor> gvp_ff_fwd(const Tensor& s, const Tensor& v, const std::vector<Tensor>&) {
   const int64_t N = s.size(0);
   auto o = s.options();
@@ -1879,6 +1921,8 @@ TORCH_LIBRARY(gmp, m) {
         "-> ()");
   m.def("edge_outer_sum_act(Tensor A, Tensor X, Tensor w, Tensor b, int act, Tensor? amax=None) "
         "-> (Tensor C, Tensor colsum)");
+  m.def("egnn_node_bwd(Tensor g, Tensor xhat, Tensor rstd, Tensor W0, Tensor W3, Tensor[] vecs, "
+        "int act, bool residual) -> Tensor[]");
   m.def("gvp_ff_fwd(Tensor s, Tensor v, Tensor[] W) -> Tensor[]");
   m.def("gvp_ff_bwd(Tensor v, Tensor[] W, Tensor gate1, Tensor B2, Tensor s2, Tensor ds, "
         "Tensor dv) -> Tensor[]");
@@ -1953,6 +1997,7 @@ TORCH_LIBRARY(gmp, m) {
   m.impl("edge_outer_sum_ex", ns edge_outer_sum_ex);                      \
   m.impl("edge_outer_sum_ex2", ns edge_outer_sum_ex2);                    \
   m.impl("edge_outer_sum_act", ns edge_outer_sum_act);                    \
+  m.impl("egnn_node_bwd", ns egnn_node_bwd);                              \
   m.impl("gvp_ff_fwd", ns gvp_ff_fwd);                                    \
   m.impl("gvp_ff_bwd", ns gvp_ff_bwd);                                    \
   m.impl("gvp_layer_fwd", ns gvp_layer_fwd);                              \

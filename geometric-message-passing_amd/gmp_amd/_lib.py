@@ -159,6 +159,8 @@ SIGNATURES = {
     "gmp_gvp_msg0_bwd_agg_f32": (c_int, [c_i64, c_i64] + [c_vp] * 30 + [c_vp]),
     "gmp_gvp_msg0_fwd_f32": (c_int, [c_i64] + [c_vp] * 15 + [c_vp]),
     "gmp_gvp_ff_fwd_f32": (c_int, [c_i64] + [c_vp] * 21 + [c_vp]),
+    "gmp_egnn_node_bwd_partial_rows": (c_i64, [c_i64]),
+    "gmp_egnn_node_bwd_f32": (c_int, [c_i64, c_i64, c_int, c_int] + [c_vp] * 13 + [c_vp]),
     "gmp_gvp_ff_bwd_f32": (c_int, [c_i64] + [c_vp] * 25 + [c_vp]),
     "gmp_gvp_edge_embed_fwd_f32": (c_int, [c_i64, c_i64, c_i64] + [c_vp] * 10 + [c_f32, c_vp,
                                                                                  c_vp, c_vp]),
@@ -204,7 +206,7 @@ SIGNATURES = {
                               + [c_vp] * 11),
 }
 
-# include/gmp.h GMP_ABI_VERSION (6: r06 — K17 gmp_gvp_ff_{fwd,bwd}_f32;
+# include/gmp.h GMP_ABI_VERSION (6: r06 — K17 gmp_gvp_ff_{fwd,bwd}_f32, K15b gmp_egnn_node_bwd_f32;
 # 5: r05 — K7s / K7f, the row GEMM and the A/B setters removed;
 # 4: r05 — gmp_egnn_node_fwd_f32;
 # 3: r04 — K8 dim / A4 arguments; 2: r04 — EGNN save_planes

@@ -878,6 +878,11 @@ def egnn_node_images(layers, next_layers):
             [None if n is None else n.mlp_msg[0].weight for n in next_layers])
 
 
+# False: the node update's backward as the composed kernels (K12 LayerNorm backwards + library
+# GEMMs; tests compare the two)
+EGNN_NODE_BWD_FUSED = True
+
+
 class EgnnNodeFn(torch.autograd.Function):
     """K15 (gmp_egnn_node_fwd_f32): the EGNN node update of one layer (egnn_layer.py:82-86,
     mlp_upd over [h | m_aggr]), the model's residual (egnn.py:75-76) and the next layer's node
@@ -913,13 +918,24 @@ class EgnnNodeFn(torch.autograd.Function):
         g = _f32c(g)
         tops = _lib.torch_ops()
         a = _LN_ACT[ctx.act]
-        dpre2, gb2 = tops.ln_act_bwd(g, xhat[1], rstd[1], ln2w, ln2b, a)
-        dx1 = _dx(dpre2, W3)
-        dpre1, gb1 = tops.ln_act_bwd(dx1, xhat[0], rstd[0], ln1w, ln1b, a)
-        dh = _dx(dpre1, W0[:, :d]) if ctx.needs_input_grad[0] else None
-        if dh is not None and ctx.residual:
-            dh += g
-        dm = _dx(dpre1, W0[:, d:]) if ctx.needs_input_grad[1] else None
+        if EGNN_NODE_BWD_FUSED and a in (0, 1) and d in (32, 64, 128):
+            # K15b: both LayerNorm + act backwards, the three dx products and the residual in
+            # one launch (gmp_egnn_node_bwd_f32)
+            with _timed("egnn_node_bwd"):
+                dh, dm, dpre1, dpre2, gb = tops.egnn_node_bwd(g, xhat, rstd, W0, W3,
+                                                              [ln1w, ln1b, ln2w, ln2b], a,
+                                                              ctx.residual)
+            gb1, gb2 = gb[:2 * d], gb[2 * d:]
+            dh = dh if ctx.needs_input_grad[0] else None
+            dm = dm if ctx.needs_input_grad[1] else None
+        else:
+            dpre2, gb2 = tops.ln_act_bwd(g, xhat[1], rstd[1], ln2w, ln2b, a)
+            dx1 = _dx(dpre2, W3)
+            dpre1, gb1 = tops.ln_act_bwd(dx1, xhat[0], rstd[0], ln1w, ln1b, a)
+            dh = _dx(dpre1, W0[:, :d]) if ctx.needs_input_grad[0] else None
+            if dh is not None and ctx.residual:
+                dh += g
+            dm = _dx(dpre1, W0[:, d:]) if ctx.needs_input_grad[1] else None
         with side_work(dpre1, dpre2, h, m, xhat) as sw:
             dW0 = torch.empty_like(W0)
             db0 = torch.empty_like(b0)

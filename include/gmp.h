@@ -35,7 +35,8 @@ extern "C" {
  * gmp_tp_z_fused_layout_*, gmp_tp_node_dw_*), the row GEMM (gmp_split_x3_f32, gmp_gemm_x3_f32),
  * gmp_tp_gemm_set_rings, gmp_wgrad_set_grid_cap and the CU-masked stream entries removed; K8 takes
  * the sparse term plan (any irreps), gmp_sc_monomials removed.
- * Version 6 (r06): gmp_gvp_ff_{fwd,bwd}_f32 (K17, the GVPConvLayer node feed-forward) added. */
+ * Version 6 (r06): gmp_gvp_ff_{fwd,bwd}_f32 (K17, the GVPConvLayer node feed-forward) and
+ * gmp_egnn_node_bwd_f32 / gmp_egnn_node_bwd_partial_rows (K15b) added. */
 #define GMP_ABI_VERSION 6
 
 enum {
@@ -184,6 +185,22 @@ int gmp_egnn_node_fwd_f32(int64_t n_nodes, int64_t d, const float* h, const floa
                           int residual, float ln_eps, float* h_out, float* ab_out,
                           float* save_xhat, float* save_rstd, void* stream);
 
+/* K15b (r06): backward of gmp_egnn_node_fwd_f32 (egnn_layer.py:82-86 update, egnn.py:75-76
+ * residual) in one launch, from grad_h (N, d) of h_out and the forward's save_xhat (2, N, d),
+ * save_rstd (2, N):  dz2 = grad_h act'(x_hat2 ln2_w + ln2_b), dpre2 = LN2'(dz2 ln2_w);
+ * dz1 = (W3^T dpre2) act'(x_hat1 ln1_w + ln1_b), dpre1 = LN1'(dz1 ln1_w);
+ * dh = W0[:, :d]^T dpre1 (+ grad_h when residual), dm = W0[:, d:]^T dpre1 (the m_aggr gradient);
+ * dpre1, dpre2 (N, d) out for the weight sums (dW0 = dpre1^T [h | m], dW3 = dpre2^T
+ * act(x_hat1 ln1_w + ln1_b)); partials (gmp_egnn_node_bwd_partial_rows(N), 4 d) per-workgroup rows
+ * of [d ln1_w | d ln1_b | d ln2_w | d ln2_b], the caller sums them in row order.  W0 (d, 2d),
+ * W3 (d, d) f32 row-major (not the forward's image); exact f32 products; d in {32, 64, 128}
+ * (GMP_ERR_UNSUPPORTED otherwise), act 0 relu / 1 swish. */
+int64_t gmp_egnn_node_bwd_partial_rows(int64_t n_nodes);
+int gmp_egnn_node_bwd_f32(int64_t n_nodes, int64_t d, int act, int residual, const float* grad_h,
+                          const float* save_xhat, const float* save_rstd, const float* W0,
+                          const float* W3, const float* ln1_w, const float* ln1_b,
+                          const float* ln2_w, const float* ln2_b, float* dh, float* dm,
+                          float* dpre1, float* dpre2, float* partials, void* stream);
 /* Backward of gmp_egnn_edge_fwd_f32 from its saved x_hat / rstd (no forward recompute).
  * Inputs g_m_aggr (N,d), g_pos_aggr (N,3), the forward's save_xhat (save_planes, E, d) and
  * save_rstd (E, 3).  Outputs:

@@ -591,6 +591,42 @@ def test_egnn_node_update_vs_fp64(d, act, residual, n):
             close(p.grad, P[name].grad, 1e-4, "d" + name)
 
 
+@pytest.mark.parametrize("d,act,residual,n", [(128, "relu", True, 50_000), (64, "swish", False, 777),
+                                              (32, "relu", True, 129)])
+def test_egnn_node_bwd_fused_matches_composed(d, act, residual, n, monkeypatch):
+    """K15b (gmp_egnn_node_bwd_f32, the node update's backward in one launch) against the
+    composed backward it replaces (K12 LayerNorm backwards + library dx GEMMs): input and weight
+    gradients within 1e-5 of scale (both exact-f32 products, different summation orders), and
+    two K15b runs bitwise equal.  (test_egnn_node_update_vs_fp64 holds both to fp64.)"""
+    import gmp_amd
+    from gmp_amd import ops
+    torch.manual_seed(d + n)
+    lay, nxt = gmp_amd.EGNNLayer(d, act), gmp_amd.EGNNLayer(d, act)
+    with torch.no_grad():
+        for p in list(lay.parameters()) + list(nxt.parameters()):
+            if p.dim() == 1:
+                p.add_(0.2 * torch.randn_like(p))
+    lay, nxt = lay.to(DEV), nxt.to(DEV)
+    h0 = torch.randn(n, d, device=DEV) * 2
+    m0 = torch.randn(n, d, device=DEV) * 5 + 1
+    gh = torch.randn(n, d, device=DEV)
+
+    def run(fused):
+        monkeypatch.setattr(ops, "EGNN_NODE_BWD_FUSED", fused)
+        lay.zero_grad(set_to_none=True)
+        h, m = h0.clone().requires_grad_(True), m0.clone().requires_grad_(True)
+        ho, _ = lay.fused_update(h, m, nxt, residual)
+        (ho * gh).sum().backward()
+        return [h.grad, m.grad] + [p.grad.clone() for k, p in lay.named_parameters()
+                                   if k.startswith("mlp_upd")]
+
+    a, b, c = run(True), run(True), run(False)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    for x, y in zip(a, c):
+        sc = y.abs().max().item()
+        assert (x - y).abs().max().item() <= 1e-5 * sc + 1e-7
+
+
 def test_egnn_model_uses_node_update_and_matches_unfused():
     """The model's fused loop (K4 + K15 per layer) against the same model with K15 bypassed
     (per-layer EGNNLayer path: split Linear, K12, Linear, K12, residual): prediction and every
