@@ -492,20 +492,22 @@ __global__ __launch_bounds__(kGT, 1) void tp_gemm_x3_widen_kernel(
   // shape: RB = 2 11.70 ms, RB = 4 11.41 ms (238 VGPRs, no scratch); MACE 2314 -> 2278 ms/step
   u32x4 ringB[RB][2][NP];
   // B fragments of global step gs (tile t0 + gs / NKS, k step gs % NKS) for this wave's two
-  // column tiles; steps past the range and tiles past N read a clamped block and are zeroed
+  // column tiles.  Steps past the range and tiles past N read a clamped (valid, finite) block
+  // WITHOUT masking: their products land in accumulators that are never stored (columns >= N,
+  // or the padded steps after the last tile's store, whose accumulators are discarded).  r05
+  // zeroed them with a select after each load; the compiler placed those selects at the
+  // unrolled loop's latch, so every RB steps the wave waited for all its B loads (vmcnt(0)) and
+  // the ring prefetched almost nothing: MACE-128 lo = 2 shape 11.60 -> 10.68 ms without them.
   auto fetch_b = [&](int slot, int gs) {
     const int gsc = gs < nst ? gs : nst - 1;
     const int64_t ks = gsc % NKS;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int64_t ct = (t0 + gsc / NKS) * (kBN / 16) + 2 * wn + c;
-      const bool ok = gs < nst && ct < ct_total;
       const int64_t ctc = ct < ct_total ? ct : ct_total - 1;
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(bl + ((ks * ct_total + ctc) * NP + p) * 512);
-        ringB[slot][c][p] = ok ? v : u32x4{0u, 0u, 0u, 0u};
-      }
+      for (int p = 0; p < NP; ++p)
+        ringB[slot][c][p] = *reinterpret_cast<const u32x4*>(bl + ((ks * ct_total + ctc) * NP + p) * 512);
     }
   };
   f32x4 acc[4][2];

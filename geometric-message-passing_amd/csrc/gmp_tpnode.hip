@@ -571,8 +571,9 @@ __global__ __launch_bounds__(kV2T, 1) void tp_node_apply_x3_kernel(
 // v2 staged the whole block for all 8 waves behind two barriers and re-read A_n from LDS for
 // every block (~300 KB of LDS reads per 32-row block); here ~24 KB per wave, the T stream
 // overlaps the MFMAs of the previous block, and 80 KB of LDS lets two workgroups share a CU.
-// Edge groups with <= 16 edges run half the MFMAs.  Requires H == 256, w % 32 == 0, 16-byte
-// aligned Z, A, T, Tb, dZ.
+// Edge groups with <= 16 edges run half the MFMAs.  Requires H == 256, w % 64 == 0 (an even
+// number of 32-row blocks: the block loop is unrolled by two without a guard), 16-byte aligned
+// Z, A, T, Tb, dZ.
 constexpr int kV3T = 256;
 constexpr int kV3H = 256;
 constexpr int kV3Q = kV3H / 4;                 // j per wave
@@ -681,21 +682,25 @@ __global__ __launch_bounds__(kV3T, 2) void tp_node_apply_v3_kernel(
     for (int et = 0; et < 2; ++et)
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt) accA[et][jt] = zero4;
+    // The ring loads are unconditional: past the receiver's rows (the last two blocks' look-ahead)
+    // the buffer range check returns zeros and no memory is touched.  r05 guarded them with
+    // `if (b + 2 < nblk)`: the guarded registers then met the unguarded ones in PHI copies at
+    // the unrolled loop's back edge, each behind a full vmcnt(0) wait, so the T ring prefetched
+    // nothing across iterations.
     auto body = [&](auto slot, int b) {
-      const bool more = b + 2 < nblk;
       constexpr int zs = ZD == 2 ? decltype(slot)::value : 0;
       bf16x8_t pz[2][3];
 #pragma unroll
       for (int et = 0; et < 2; ++et) split8(rZ[zs][et][0], rZ[zs][et][1], pz[et]);
       const f32x4 tb = rTb[zs];
-      if (b + ZD < nblk) fetch_z(ic_t<zs>{}, b + ZD);
+      fetch_z(ic_t<zs>{}, b + ZD);
       unsigned char* rb = red + parity * kV3Red;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         bf16x8_t pt[2][3];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) split8(rT[slot][rt][ks][0], rT[slot][rt][ks][1], pt[ks]);
-        if (more) fetch_t(slot, b + 2, rt);
+        fetch_t(slot, b + 2, rt);
         // planes into the wave's slab ([plane][row][64 j]); read back transposed below (one
         // wave's LDS operations complete in order: no barrier, no wait)
 #pragma unroll
@@ -755,26 +760,37 @@ __global__ __launch_bounds__(kV3T, 2) void tp_node_apply_v3_kernel(
     fetch_t(ic_t<0>{}, 0, 0);
     fetch_t(ic_t<0>{}, 0, 1);
     fetch_z(ic_t<0>{}, 0);
-    if (nblk > 1) {
-      fetch_t(ic_t<1>{}, 1, 0);
-      fetch_t(ic_t<1>{}, 1, 1);
-      if constexpr (ZD == 2) fetch_z(ic_t<ZD - 1>{}, 1);
-    }
-    for (int b = 0; b < nblk; b += 2) {
+    fetch_t(ic_t<1>{}, 1, 0);
+    fetch_t(ic_t<1>{}, 1, 1);
+    if constexpr (ZD == 2) fetch_z(ic_t<ZD - 1>{}, 1);
+    for (int b = 0; b < nblk; b += 2) {  // nblk even (w % 64 == 0, checked at the launch)
       body(ic_t<0>{}, b);
-      if (b + 1 < nblk) body(ic_t<1>{}, b + 1);
+      body(ic_t<1>{}, b + 1);
     }
-    // dA[e][j] += (per-path launches on one stream: ordered RMW, deterministic)
+    // dA[e][j] += (per-path launches on one stream: ordered RMW, deterministic), through a
+    // buffer descriptor over the group's ng rows: rows past ng load zeros and drop their stores,
+    // so the 32 loads issue back to back and meet one wait (r05's per-element `if (e < ng)`
+    // RMW was 32 dependent round trips per group and wave, each behind a vmcnt(0))
+    {
+      const rsrc_t dar = __builtin_amdgcn_make_buffer_rsrc(dA + eb * H, 0, ng * H * 4, 0x00020000);
+      float old[2][4][4];
 #pragma unroll
-    for (int et = 0; et < 2; ++et) {
+      for (int et = 0; et < 2; ++et)
 #pragma unroll
-      for (int jt = 0; jt < 4; ++jt) {
+        for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = 16 * et + 4 * g + q;
-          if (e < ng) dA[(eb + e) * H + jq + 16 * jt + li] += accA[et][jt][q];
-        }
-      }
+          for (int q = 0; q < 4; ++q)
+            old[et][jt][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                dar, ((16 * et + 4 * g + q) * H + jq + 16 * jt + li) * 4, 0, 0));
+#pragma unroll
+      for (int et = 0; et < 2; ++et)
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(
+                __float_as_uint(old[et][jt][q] + accA[et][jt][q]), dar,
+                ((16 * et + 4 * g + q) * H + jq + 16 * jt + li) * 4, 0, 0);
     }
   }
 }
@@ -825,7 +841,7 @@ int gmp_tp_node_apply_f32(int64_t n_recv, int64_t w, int64_t H, const int64_t* e
   GMP_CHECK_ARG(reinterpret_cast<uintptr_t>(T) % 16 == 0);
   const bool a16 = ((reinterpret_cast<uintptr_t>(Z) | reinterpret_cast<uintptr_t>(A) |
                      reinterpret_cast<uintptr_t>(Tb) | reinterpret_cast<uintptr_t>(dZ)) % 16) == 0;
-  if (g_apply_x3 == 2 && H == kV3H && w % 32 == 0 && a16) {
+  if (g_apply_x3 == 2 && H == kV3H && w % 64 == 0 && a16) {
     auto k = tp_node_apply_v3_kernel<kV3Zd>;
     int rc = 0;
     if ((rc = hip_check(hipFuncSetAttribute((const void*)k,
