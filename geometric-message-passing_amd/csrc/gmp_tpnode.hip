@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kNT, CS == 2 ? 5 : 1) void tp_node_outer_kernel(int
     // rows are staged once; no dependent global load inside the MFMA loop
     const int ns = (int)deg, nst = (ns + 3) >> 2;
     float zr[2][kEdgeStage / 4];
-    auto zload = [&](int buf, int rb) {
+    auto zload = [&](int buf, int rb) {  // (the guarded loads issue back to back: one wait)
       const int r = rb * kRowsPerBlock + wv * 16 + i;
 #pragma unroll
       for (int s = 0; s < kEdgeStage / 4; ++s) {
@@ -86,11 +86,27 @@ __global__ __launch_bounds__(kNT, CS == 2 ? 5 : 1) void tp_node_outer_kernel(int
       }
     };
     zload(0, rb0);
-    for (int x = tid; x < 4 * nst * (hc >> 2); x += kNT) {  // padding rows zeroed
-      const int e = x / (hc >> 2), q = x - e * (hc >> 2);
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (e < ns) v = *reinterpret_cast<const f32x4*>(Ac + (e0 + e) * H + 4 * q);
-      *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) = v;
+    // The a rows are staged with every load issued (at a clamped, valid row) before any is
+    // used, then masked: one memory round trip.  r05's staging loop (`if (e < ns) v = ..; sA =
+    // v` per iteration) waited vmcnt(0) in every iteration: up to 4 dependent round trips per
+    // workgroup.  (A has no pad row: a receiver without edges skips the loads.)
+    constexpr int kSI = (kEdgeStage * (kMaxH / CS) / 4 + kNT - 1) / kNT;  // float4s per thread
+    const int q4 = hc >> 2, cnt = 4 * nst * q4;                            // (padding rows zeroed)
+    if (ns > 0) {
+      f32x4 av[kSI];
+#pragma unroll
+      for (int it = 0; it < kSI; ++it) {
+        const int x = tid + it * kNT, e = x / q4, q = x - e * q4;
+        const int ec = e < ns ? e : ns - 1;
+        av[it] = *reinterpret_cast<const f32x4*>(Ac + (e0 + ec) * H + 4 * q);
+      }
+#pragma unroll
+      for (int it = 0; it < kSI; ++it) {
+        const int x = tid + it * kNT, e = x / q4, q = x - e * q4;
+        if (x < cnt)
+          *reinterpret_cast<f32x4*>(&sA[e * LDA + 4 * q]) =
+              e < ns ? av[it] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     __syncthreads();
     for (int rb = rb0; rb < rb1; ++rb) {
