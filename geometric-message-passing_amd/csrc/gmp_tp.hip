@@ -596,6 +596,41 @@ __device__ __forceinline__ void z_path(const Path& P, const float* __restrict__ 
   }
 }
 
+// The sender row's entries for the lane's channels (u = lane, lane + 64) of the l = 0, 1, 2 input
+// blocks, loaded once per edge before any z store (r06): with the loads inside z_path, every
+// path's loads queued behind the previous path's z stores (vmcnt retires in issue order), one
+// exposed round trip per path and edge.
+struct XPre {
+  float x0[2], x1[2][3], x2[2][5];
+};
+template <int L1>
+__device__ __forceinline__ float xpre(const XPre& x, int uu, int i) {
+  if constexpr (L1 == 0) return x.x0[uu];
+  else if constexpr (L1 == 1) return x.x1[uu][i];
+  else return x.x2[uu][i];
+}
+template <int L1, int L2, int LO>
+__device__ __forceinline__ void z_path_pre(const Path& P, const float* __restrict__ C,
+                                           const float (&Y)[kMaxSh], const XPre& xp,
+                                           float* __restrict__ zr, int lane) {
+  constexpr int D1 = 2 * L1 + 1, D3 = 2 * LO + 1;
+  float T[D1][D3];
+  t_table<L1, L2, LO>(C, Y, T);
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) {
+    const int u = lane + 64 * uu;
+    if (u < P.mul1) {
+#pragma unroll
+      for (int k = 0; k < D3; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < D1; ++i) a += xpre<L1>(xp, uu, i) * T[i][k];
+        zr[k * P.mul1 + u] = P.alpha * a;
+      }
+    }
+  }
+}
+
 struct DxAcc {
   float d0[2], d1[2][3], d2[2][5], d3[2][7];
 };
@@ -685,6 +720,50 @@ __global__ __launch_bounds__(256) void tp_edge_z2_kernel(
   const int lane = threadIdx.x & 63;
   const int64_t ne = e1 - e0;
   const int64_t nw = (int64_t)gridDim.x * 4;
+  // one input block per l1 <= 2 (wave-uniform, from the path table): the sender row is
+  // preloaded per edge (XPre); otherwise (l = 3, or a repeated l) each path loads its own
+  int xo[3] = {-1, -1, -1}, xm[3] = {0, 0, 0};
+  bool pre = LM == 2;
+  for (int p = 0; p < d.n_paths; ++p) {
+    const Path P = paths[p];
+    if (P.l1 > 2 || (xo[P.l1] >= 0 && xo[P.l1] != P.x_off)) pre = false;
+    else {
+      xo[P.l1] = P.x_off;
+      xm[P.l1] = P.mul1;
+    }
+  }
+  if (pre) {
+    for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
+      const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
+      const int64_t src = src_sorted[e], eo = perm[e];
+      float Y[kMaxSh];
+      load_y(sh, eo, d.sh_dim, Y);
+      const float* xrow = x + src * d.in_dim;
+      XPre xp;
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+        const int u = lane + 64 * uu;
+        xp.x0[uu] = u < xm[0] ? xrow[xo[0] + u] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xp.x1[uu][i] = u < xm[1] ? xrow[xo[1] + 3 * u + i] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) xp.x2[uu][i] = u < xm[2] ? xrow[xo[2] + 5 * u + i] : 0.f;
+      }
+      for (int p = 0; p < d.n_paths; ++p) {
+        const Path P = paths[p];
+        const float* C = sC + P.cg_off;
+        float* zr = zbuf + (int64_t)P.z_off * (ne + 1) + k * (int64_t)((2 * P.lo + 1) * P.mul1);
+        switch (P.l1 * 16 + P.l2 * 4 + P.lo) {
+#define LAUNCH_ZP_CASE(A, B, O) \
+  case A * 16 + B * 4 + O: z_path_pre<A, B, O>(P, C, Y, xp, zr, lane); break;
+          LAUNCH_Z_PATHS2(LAUNCH_ZP_CASE)
+#undef LAUNCH_ZP_CASE
+          default: break;
+        }
+      }
+    }
+    return;
+  }
   for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < ne; k += nw) {
     const int64_t e = e0 + __builtin_amdgcn_readfirstlane((int)k);
     const int64_t src = src_sorted[e], eo = perm[e];
